@@ -1,0 +1,197 @@
+"""oracle -- TEST INFRASTRUCTURE ONLY (the checker, never the product).
+
+ctypes loader for the plain-C restatement in ``oracle/fec_oracle.c`` of the reference's GF(2^8)
+streaming-erasure hot path (domanovi/FEC_Erasure_Code_Unit_Test_Relay: src/basicOperations.cpp,
+src/codingOperations.cpp, src/Encoder*.cpp, src/Decoder*.cpp, src/FEC_Encoder.cpp,
+src/FEC_Decoder.cpp).  Only ``tests/``, ``__graft_entry__.smoke()`` and ``bench.py``'s
+``cpu_baseline`` leg may import this module.  The reference itself is unbuildable here (it needs
+Intel ISA-L, which is absent); the restatement is pinned by the reference's published fixed-rate
+loss counts (tests/golden/published_fixed_logs.json).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB_PATH = os.path.join(_HERE, "build", "liboracle.so")
+_lib = None
+
+
+def build() -> str:
+    """Compile the restatement with gcc (oracle/Makefile) and return the .so path."""
+    subprocess.run(["make", "-s", "-C", _HERE], check=True)
+    return _LIB_PATH
+
+
+def lib() -> ctypes.CDLL:
+    global _lib
+    if _lib is None:
+        src = os.path.join(_HERE, "fec_oracle.c")
+        if not os.path.exists(_LIB_PATH) or os.path.getmtime(_LIB_PATH) < os.path.getmtime(src):
+            build()
+        L = ctypes.CDLL(_LIB_PATH)
+        u8p = ctypes.POINTER(ctypes.c_uint8)
+        ip = ctypes.POINTER(ctypes.c_int)
+        L.or_gf_mul.restype = ctypes.c_uint8
+        L.or_gf_mul.argtypes = [ctypes.c_uint8, ctypes.c_uint8]
+        L.or_gf_inv.restype = ctypes.c_uint8
+        L.or_gf_inv.argtypes = [ctypes.c_uint8]
+        L.or_gen_G.argtypes = [u8p] + [ctypes.c_int] * 5
+        L.or_rref_matrix.argtypes = [u8p, u8p, u8p, ctypes.c_int, ctypes.c_int]
+        L.or_decode_block.argtypes = [u8p, u8p, u8p, u8p] + [ctypes.c_int] * 4
+        L.or_geometry.argtypes = [ctypes.c_int] * 4 + [ip] * 4
+        L.or_encoder_new.restype = ctypes.c_void_p
+        L.or_encoder_new.argtypes = [ctypes.c_int] * 4
+        L.or_encoder_free.argtypes = [ctypes.c_void_p]
+        L.or_encoder_transmit.restype = ctypes.c_int
+        L.or_encoder_transmit.argtypes = [ctypes.c_void_p, u8p, ctypes.c_int, ctypes.c_int, u8p]
+        L.or_decoder_new.restype = ctypes.c_void_p
+        L.or_decoder_new.argtypes = [ctypes.c_int] * 5
+        L.or_decoder_free.argtypes = [ctypes.c_void_p]
+        L.or_decoder_receive.restype = ctypes.c_int
+        L.or_decoder_receive.argtypes = [ctypes.c_void_p, u8p, ctypes.c_int, ctypes.c_int,
+                                         ctypes.c_int, u8p]
+        L.or_fill_payload.argtypes = [u8p, ctypes.c_int64, ctypes.c_int64, ctypes.c_int,
+                                      ctypes.c_uint64]
+        L.or_run_stream.restype = ctypes.c_int64
+        L.or_run_stream.argtypes = [ctypes.c_int] * 4 + [ctypes.c_int64, u8p, ctypes.c_int64,
+                                    ctypes.c_uint64, ctypes.c_int, ip, u8p, u8p, ip]
+        L.or_encode_stream.restype = ctypes.c_int64
+        L.or_encode_stream.argtypes = [ctypes.c_int] * 4 + [ctypes.c_int64, ctypes.c_int64,
+                                       ctypes.c_uint64, u8p, ip]
+        _lib = L
+    return _lib
+
+
+def _u8(a: np.ndarray):
+    return a.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8))
+
+
+def _i32(a: np.ndarray):
+    return a.ctypes.data_as(ctypes.POINTER(ctypes.c_int))
+
+
+def geometry(max_payload: int, T: int, B: int, N: int):
+    """(k, n, S, CW) exactly as Encoder.cpp:31-39 derives them."""
+    v = [ctypes.c_int() for _ in range(4)]
+    lib().or_geometry(max_payload, T, B, N, *[ctypes.byref(x) for x in v])
+    return tuple(x.value for x in v)
+
+
+def gf_mul(a: int, b: int) -> int:
+    return int(lib().or_gf_mul(a, b))
+
+
+def gf_inv(a: int) -> int:
+    return int(lib().or_gf_inv(a))
+
+
+def gen_G(T: int, B: int, N: int) -> np.ndarray:
+    """k x n generator matrix (gen_G_cauchy, codingOperations.cpp:48-95)."""
+    k, n = T - N + 1, T - N + 1 + B
+    G = np.zeros(k * n, dtype=np.uint8)
+    lib().or_gen_G(_u8(G), T, B, N, k, n)
+    return G.reshape(k, n)
+
+
+def rref(mat: np.ndarray):
+    """gf256_rref_matrix (basicOperations.cpp:43-122) -> (out, action)."""
+    m, n = mat.shape
+    inp = np.ascontiguousarray(mat, dtype=np.uint8)
+    out = np.zeros_like(inp)
+    act = np.zeros((n, n), dtype=np.uint8)
+    lib().or_rref_matrix(_u8(inp), _u8(out), _u8(act), m, n)
+    return out, act
+
+
+def fill_payload(t0: int, count: int, L: int, seed: int) -> np.ndarray:
+    """Synthetic payloads: byte b of packet t = splitmix64(seed ^ (t*L + b)) & 0xff."""
+    buf = np.zeros(count * L, dtype=np.uint8)
+    lib().or_fill_payload(_u8(buf), t0, count, L, seed)
+    return buf.reshape(count, L)
+
+
+class Encoder:
+    """FEC_Encoder (src/FEC_Encoder.cpp:22-68) as restated by the oracle."""
+
+    def __init__(self, max_payload: int, T: int, B: int, N: int):
+        self.L = max_payload
+        self.k, self.n, self.S, self.CW = geometry(max_payload, T, B, N)
+        self._h = lib().or_encoder_new(max_payload, T, B, N)
+        if not self._h:
+            raise ValueError("unsupported (T,B,N)")
+
+    def __del__(self):
+        if getattr(self, "_h", None):
+            lib().or_encoder_free(self._h)
+            self._h = None
+
+    def onTransmit(self, data: np.ndarray, payload: int, seq: int):
+        """Returns (untrimmed CW-byte codeword, trimmed wire size)."""
+        d = np.ascontiguousarray(data, dtype=np.uint8)
+        cw = np.zeros(self.CW, dtype=np.uint8)
+        size = lib().or_encoder_transmit(self._h, _u8(d), payload, seq, _u8(cw))
+        return cw, size
+
+
+class Decoder:
+    """FEC_Decoder (src/FEC_Decoder.cpp:26-72) as restated by the oracle."""
+
+    def __init__(self, max_payload: int, T: int, B: int, N: int, loss_only: bool = False):
+        self.L = max_payload
+        self.k, self.n, self.S, self.CW = geometry(max_payload, T, B, N)
+        self._h = lib().or_decoder_new(max_payload, T, B, N, int(loss_only))
+        if not self._h:
+            raise ValueError("unsupported (T,B,N)")
+
+    def __del__(self):
+        if getattr(self, "_h", None):
+            lib().or_decoder_free(self._h)
+            self._h = None
+
+    def onReceive(self, codeword, size: int, seq: int, erasure: bool):
+        """Returns (payload length of packet seq-T, max_payload bytes zero-filled past it)."""
+        out = np.zeros(self.L, dtype=np.uint8)
+        if erasure or codeword is None:
+            p = lib().or_decoder_receive(self._h, None, 0, seq, 1, _u8(out))
+        else:
+            c = np.ascontiguousarray(codeword, dtype=np.uint8)
+            p = lib().or_decoder_receive(self._h, _u8(c), size, seq, 0, _u8(out))
+        return p, out
+
+
+def run_stream(max_payload: int, T: int, B: int, N: int, P: int, pattern: np.ndarray,
+               seed: int = 0x5EED, loss_only: bool = False, want_data: bool = False,
+               want_codewords: bool = False):
+    """Feed seq 0..P+T-1 through FEC_Encoder -> erasure channel -> FEC_Decoder.
+
+    Returns dict(lost, out_len[P], out_data[P,L]?, cw[P+T,CW]?, cw_len[P+T]?).
+    """
+    k, n, S, CW = geometry(max_payload, T, B, N)
+    pat = np.ascontiguousarray(pattern, dtype=np.uint8)
+    out_len = np.zeros(P, dtype=np.int32)
+    out_data = np.zeros((P, max_payload), dtype=np.uint8) if want_data else None
+    cw = np.zeros((P + T, CW), dtype=np.uint8) if want_codewords else None
+    cw_len = np.zeros(P + T, dtype=np.int32) if want_codewords else None
+    lost = lib().or_run_stream(max_payload, T, B, N, P, _u8(pat), pat.size, seed, int(loss_only),
+                               _i32(out_len), _u8(out_data) if want_data else None,
+                               _u8(cw) if want_codewords else None,
+                               _i32(cw_len) if want_codewords else None)
+    if lost < 0:
+        raise ValueError("unsupported (T,B,N)")
+    return dict(lost=int(lost), out_len=out_len, out_data=out_data, cw=cw, cw_len=cw_len)
+
+
+def encode_stream(max_payload: int, T: int, B: int, N: int, seq0: int, P: int, seed: int = 0x5EED,
+                  want_codewords: bool = True):
+    k, n, S, CW = geometry(max_payload, T, B, N)
+    cw = np.zeros((P, CW), dtype=np.uint8) if want_codewords else None
+    cw_len = np.zeros(P, dtype=np.int32) if want_codewords else None
+    total = lib().or_encode_stream(max_payload, T, B, N, seq0, P, seed,
+                                   _u8(cw) if want_codewords else None,
+                                   _i32(cw_len) if want_codewords else None)
+    return dict(total=int(total), cw=cw, cw_len=cw_len)

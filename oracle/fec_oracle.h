@@ -1,0 +1,73 @@
+/*
+ * oracle/fec_oracle.h -- TEST INFRASTRUCTURE ONLY (the checker, never the product).
+ *
+ * CPU restatement of the reference's GF(2^8) streaming-erasure hot path
+ * (domanovi/FEC_Erasure_Code_Unit_Test_Relay, src/basicOperations.cpp,
+ * src/codingOperations.cpp, src/Encoder*.cpp, src/Decoder*.cpp, src/FEC_Encoder.cpp,
+ * src/FEC_Decoder.cpp) plus the five ISA-L 2.23 functions it links.  Only tests/,
+ * __graft_entry__.smoke() and bench.py's cpu_baseline leg may load this library.
+ * See fec_oracle.c for the pinning status.
+ */
+#ifndef FEC_ORACLE_H
+#define FEC_ORACLE_H
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ISA-L restatement (erasure_code/ec_base.c, ISA-L 2.23.0; include/isal.h:10-12). */
+uint8_t or_gf_mul(uint8_t a, uint8_t b);
+uint8_t or_gf_inv(uint8_t a);
+void or_gf_gen_cauchy1_matrix(uint8_t *a, int m, int k);
+void or_gf_gen_rs_matrix(uint8_t *a, int m, int k);
+
+/* codingOperations.cpp / basicOperations.cpp restatements. */
+void or_gen_G(uint8_t *G, int T, int B, int N, int k, int n);
+void or_encode_block(const uint8_t *data, const uint8_t *G, uint8_t *cw, int k, int n, int t);
+void or_rref_matrix(const uint8_t *in, uint8_t *out, uint8_t *action, int m, int n);
+void or_decode_block(uint8_t *data, const uint8_t *G, uint8_t *cw, uint8_t *erasure, int k, int n,
+                     int T, int t);
+
+/* Geometry helper: fills k, n, S (= number of sub-streams), CW (= untrimmed codeword bytes). */
+void or_geometry(int max_payload, int T, int B, int N, int *k, int *n, int *S, int *CW);
+
+/* FEC_Encoder (src/FEC_Encoder.cpp:22-68) over a reference-structured encoder. */
+typedef struct or_encoder or_encoder;
+or_encoder *or_encoder_new(int max_payload, int T, int B, int N);
+void or_encoder_free(or_encoder *e);
+/* Writes the untrimmed CW-byte codeword to cw_out; returns the trimmed wire size. */
+int or_encoder_transmit(or_encoder *e, const uint8_t *data, int payload, int seq, uint8_t *cw_out);
+
+/* FEC_Decoder (src/FEC_Decoder.cpp:26-72) over a reference-structured decoder.
+ * loss_only != 0 runs only the sub-streams that decide the packet's fate (sub-stream 0, and 1 when
+ * k == 1); the returned payload is then only meaningful as zero/non-zero. */
+typedef struct or_decoder or_decoder;
+or_decoder *or_decoder_new(int max_payload, int T, int B, int N, int loss_only);
+void or_decoder_free(or_decoder *d);
+/* Returns the payload length of packet seq-T (0 = lost / not yet available); copies the
+ * payload bytes (max_payload bytes, zero beyond the payload) to out when out != NULL. */
+int or_decoder_receive(or_decoder *d, const uint8_t *cw, int cw_size, int seq, int erasure,
+                       uint8_t *out);
+
+/* Synthetic payload generator shared by the oracle harness, the tests and bench.py:
+ * byte b of packet t = low 8 bits of splitmix64(seed ^ (t * L + b)). */
+void or_fill_payload(uint8_t *buf, int64_t t0, int64_t count, int L, uint64_t seed);
+
+/* Whole-stream harness.  Feeds seq 0 .. P+T-1 (erasure of seq t = pattern[t] for t < pattern_len,
+ * else 0) through FEC_Encoder -> FEC_Decoder, and returns the payload length recovered for packets
+ * 0 .. P-1 in out_len (P ints).  When out_data != NULL (P*max_payload bytes) the recovered payload
+ * bytes are stored too; cw_out (optional, (P+T)*CW bytes) receives the untrimmed codewords and
+ * cw_len (optional, P+T ints) the trimmed wire sizes. Returns the number of lost packets. */
+int64_t or_run_stream(int max_payload, int T, int B, int N, int64_t P, const uint8_t *pattern,
+                      int64_t pattern_len, uint64_t seed, int loss_only, int *out_len,
+                      uint8_t *out_data, uint8_t *cw_out, int *cw_len);
+
+/* Encode-only harness (timed as the CPU baseline): P packets from seq0, returns total wire bytes. */
+int64_t or_encode_stream(int max_payload, int T, int B, int N, int64_t seq0, int64_t P,
+                         uint64_t seed, uint8_t *cw_out, int *cw_len);
+
+#ifdef __cplusplus
+}
+#endif
+#endif
