@@ -1,0 +1,223 @@
+"""bench.py -- device-resident GF(2^8) streaming-erasure encode+decode throughput on MI355X.
+
+Metric (BASELINE.json): GiB/s of device-resident erasure encode+decode, 300-byte packets, T=10,
+and its fraction of the HBM roofline.  One step = one pass of the hot path over one batch: encode
+P+T packets of a fresh stream ((T,B,N) = (10,3,3), 300-byte synthetic payloads), erase with the
+reference's recorded pattern bin/erasure.bin (replayed, ERASURE_TYPE=5 semantics), decode with a
+fresh decoder -> the reference's output for P packets.  Inputs are resident in HBM before timing.
+
+Multi-GPU (torchrun, one process per GPU): weak scaling, one independent stream per GPU (seed and
+pattern phase per rank); no collective in the data path -- RCCL only for the barrier, the
+max-over-ranks time and the final counter reduction.
+
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--packets P] [--tbn 10,3,3]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+L = 300
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak, /opt/skills/guides/MI355X_MICROARCH.md
+
+
+def load_pattern(name="bin_erasure"):
+    z = np.load(os.path.join(ROOT, "tests", "golden", "erasure_patterns.npz"))
+    return np.unpackbits(z[name])[: int(z[name + "_len"][0])].astype(np.uint8)
+
+
+def stream_pattern(P_fed, rank):
+    """bin/erasure.bin's first 360000 packets, replayed cyclically; each rank starts at its own
+    phase so that the streams differ."""
+    base = load_pattern("bin_erasure")[:360000]
+    return np.roll(np.resize(base, P_fed + 36000 * rank), -36000 * rank)[:P_fed].copy()
+
+
+def cpu_baseline(T, B, N, packets, rank_pattern):
+    """The oracle's reference-structured encoder+decoder (1 core) on a bounded sample."""
+    import oracle
+    pat = rank_pattern[: packets + T]
+    t0 = time.perf_counter()
+    r = oracle.run_stream(L, T, B, N, packets, pat, seed=0x5EED, want_data=False)
+    dt = time.perf_counter() - t0
+    return {"value": packets * L / dt / 2**30, "unit": "GiB/s", "cores": 1, "kind": "port",
+            "sample": f"oracle (reference-structured C restatement, oracle/fec_oracle.c) "
+                      f"encode+decode of {packets} packets, (T,B,N)=({T},{B},{N}), first "
+                      f"{packets} packets of the same replayed bin/erasure.bin stream "
+                      f"({int(pat[:packets].sum())} erased, {r['lost']} lost), {dt:.1f} s",
+            "seconds": dt}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--packets", type=int, default=1_000_000, help="decoded packets per GPU")
+    ap.add_argument("--tbn", default="10,3,3")
+    ap.add_argument("--cpu-packets", type=int, default=60000)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-host-inclusive", action="store_true")
+    args = ap.parse_args()
+    T, B, N = map(int, args.tbn.split(","))
+
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group(backend="nccl", device_id=torch.device("cuda", local))
+
+    from fec_erasure_code_unit_test_relay_amd import Codec, fill_payload
+
+    P = args.packets
+    Pf = P + T  # fed packets: the last T only complete the outputs of packets P-T..P-1
+    codec = Codec(L, T, B, N)
+    seed = 0x5EED + rank
+    pat = stream_pattern(Pf, rank)
+    payload = fill_payload(0, Pf, L, seed)
+    er = torch.from_numpy(pat).cuda()
+    cw = torch.empty((Pf, codec.CW), dtype=torch.uint8, device="cuda")
+    wl = torch.empty(Pf, dtype=torch.int32, device="cuda")
+    out = torch.empty((P, L), dtype=torch.uint8, device="cuda")
+    ol = torch.empty(P, dtype=torch.int32, device="cuda")
+    codec.workspace(Pf)
+
+    def step():
+        codec.encode(payload, out=cw, out_len=wl)
+        codec.decode(cw, er, out=out, out_len=ol)
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    # correctness of the timed work (outside the timed region): round trip + planner agreement
+    eps, rec, lost = codec.counters()
+    lost_mask = (ol == 0)
+    ok_rows = ~lost_mask
+    verified = bool(torch.equal(out[ok_rows], payload[:P][ok_rows])) and \
+        int((ol[ok_rows] != L).sum()) == 0 and int(lost_mask.sum()) == lost
+    stats = torch.tensor([rec, lost, int(pat[:P].sum()), int(verified)], dtype=torch.int64,
+                         device="cuda")
+    if world > 1:
+        dist.all_reduce(stats)  # trivial counter reduction over RCCL
+    rec_all, lost_all, erased_all, verified_all = (int(x) for x in stats.tolist())
+
+    # per-kernel durations: HIP events on the launch stream, separate pass
+    codec.timing(True)
+    for _ in range(max(3, min(args.steps, 10))):
+        step()
+    kt = codec.collect_timing()
+    codec.timing(False)
+    per_launch = {k: (ms / n if n else 0.0) for k, (ms, n) in kt.items()}
+    algo = {"fec_encode_kernel": (L + codec.CW) * Pf, "fec_copy_kernel": (codec.CW + 1 + L) * P}
+    dominant = max(algo, key=lambda k: per_launch[k])
+    achieved = algo[dominant] / (per_launch[dominant] * 1e-3) / 1e9
+
+    result = None
+    if rank == 0:
+        ms_per_step = elapsed / args.steps * 1e3
+        value = world * P * L / (elapsed / args.steps) / 2**30
+        result = {
+            "metric": "GiB/s device-resident erasure encode+decode, 300B pkts, T=10; %HBM roofline",
+            "value": round(value, 3),
+            "unit": "GiB/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms_per_step, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u8",
+            "data": "synthetic payloads (splitmix64, seed per GPU); erasures = bin/erasure.bin "
+                    "(reference recording) replayed, phase per GPU",
+            "config": {"workload": f"encode {Pf} + decode {P} x 300B packets per GPU, one stream "
+                                   f"per GPU, (T,B,N)=({T},{B},{N})",
+                       "T": T, "B": B, "N": N, "k": codec.k, "n": codec.n, "S": codec.S,
+                       "codeword_bytes": codec.CW, "packets_per_gpu": P,
+                       "parallelism": f"streams{world} (one independent stream per GPU)"},
+            "verified": bool(verified_all == world),
+            "decode": {"erased": erased_all, "recovered": rec_all, "lost": lost_all},
+            "algorithmic_bytes_per_packet": L + codec.CW + codec.CW + 1 + L,
+            "algorithmic_GBps": round(world * P * (2 * L + 2 * codec.CW + 1) / (elapsed / args.steps) / 1e9, 1),
+            "kernels_ms_per_launch": {k: round(v, 5) for k, v in per_launch.items()},
+            "roofline": {"bound": "hbm", "kernel": dominant, "achieved": round(achieved, 1),
+                         "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None},
+        }
+    if world == 1 and not args.no_host_inclusive:
+        # end-to-end from/to host memory (pinned): H2D payload, encode, D2H wire codewords,
+        # H2D codewords + erasures, decode, D2H payloads + lengths
+        h_payload = payload.cpu().pin_memory()
+        h_cw = torch.empty_like(cw, device="cpu").pin_memory()
+        h_wl = torch.empty_like(wl, device="cpu").pin_memory()
+        h_out = torch.empty_like(out, device="cpu").pin_memory()
+        h_ol = torch.empty_like(ol, device="cpu").pin_memory()
+        h_er = torch.from_numpy(pat).pin_memory()
+        d_in = torch.empty_like(payload)
+        d_cw2 = torch.empty_like(cw)
+        d_er2 = torch.empty_like(er)
+
+        def host_step():
+            d_in.copy_(h_payload, non_blocking=True)
+            codec.encode(d_in, out=cw, out_len=wl)
+            h_cw.copy_(cw, non_blocking=True)
+            h_wl.copy_(wl, non_blocking=True)
+            d_cw2.copy_(h_cw, non_blocking=True)
+            d_er2.copy_(h_er, non_blocking=True)
+            codec.decode(d_cw2, d_er2, out=out, out_len=ol)
+            h_out.copy_(out, non_blocking=True)
+            h_ol.copy_(ol, non_blocking=True)
+
+        host_step()
+        torch.cuda.synchronize()
+        hs = 3
+        t0 = time.perf_counter()
+        for _ in range(hs):
+            host_step()
+        torch.cuda.synchronize()
+        he = (time.perf_counter() - t0) / hs
+        result["host_inclusive"] = {"value": round(P * L / he / 2**30, 3), "unit": "GiB/s",
+                                    "ms_per_step": round(he * 1e3, 3),
+                                    "note": "pinned H2D payload+codewords+erasures, D2H codewords"
+                                            "+payloads, serialised on one stream"}
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        result["cpu_baseline"] = cpu_baseline(T, B, N, args.cpu_packets, pat)
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,85 @@
+"""ctypes binding of the in-tree HIP library ``libfec_amd.so`` (C ABI: include/fec_amd.h).
+
+The library is the product: there is no CPU fallback.  If it is missing the import of any op
+fails loudly with instructions to build it (``python -c "import __graft_entry__ as g; g.build()"``
+or ``make -C fec_erasure_code_unit_test_relay_amd/csrc``).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libfec_amd.so")
+HEADER_PATHS = [os.path.join(_HERE, "..", "include", "fec_amd.h")]
+
+FEC_OK = 0
+FEC_ERR_ARG = -1
+FEC_ERR_HIP = -2
+FEC_ERR_NOMEM = -3
+FEC_ERR_WORKSPACE = -4
+FEC_ERR_SEQUENCE = -5
+
+KERNEL_NAMES = ["fec_encode_kernel", "fec_scan_kernel", "fec_plan_kernel", "fec_copy_kernel",
+                "fec_recover_kernel"]
+
+
+class FecError(RuntimeError):
+    def __init__(self, status: int, what: str = ""):
+        msg = lib().fec_strerror(status).decode() if _lib is not None else str(status)
+        super().__init__(f"{what}: {msg} (status {status})")
+        self.status = status
+
+
+_lib = None
+
+
+def lib() -> ctypes.CDLL:
+    """Load libfec_amd.so (raises if it has not been built)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise RuntimeError(
+            f"{LIB_PATH} is missing: the HIP extension must be built first "
+            "(make -C fec_erasure_code_unit_test_relay_amd/csrc); there is no fallback")
+    L = ctypes.CDLL(LIB_PATH)
+    vp, i32, i64 = ctypes.c_void_p, ctypes.c_int, ctypes.c_int64
+    ip = ctypes.POINTER(ctypes.c_int)
+    i64p = ctypes.POINTER(ctypes.c_int64)
+    L.fec_strerror.restype = ctypes.c_char_p
+    L.fec_strerror.argtypes = [i32]
+    L.fec_version.restype = i32
+    L.fec_codec_create.argtypes = [i32, i32, i32, i32, ctypes.POINTER(vp)]
+    L.fec_codec_destroy.argtypes = [vp]
+    L.fec_codec_geometry.argtypes = [vp, ip, ip, ip, ip]
+    L.fec_codec_generator.argtypes = [vp, vp]
+    L.fec_encode_batch.argtypes = [vp, vp, vp, i64, i64, vp, vp, vp]
+    L.fec_decode_workspace_bytes.restype = ctypes.c_size_t
+    L.fec_decode_workspace_bytes.argtypes = [vp, i64]
+    L.fec_decode_batch.argtypes = [vp, vp, vp, i64, vp, vp, vp, ctypes.c_size_t, vp]
+    L.fec_decode_counters.argtypes = [vp, i64p, i64p, i64p]
+    L.fec_timing_enable.argtypes = [vp, i32]
+    L.fec_timing_collect.argtypes = [vp, ctypes.POINTER(ctypes.c_double), i64p]
+    L.fec_encoder_create.argtypes = [i32, i32, i32, i32, ctypes.POINTER(vp)]
+    L.fec_encoder_destroy.argtypes = [vp]
+    L.fec_encoder_transmit.argtypes = [vp, vp, i32, i32, vp, ip]
+    L.fec_decoder_create.argtypes = [i32, i32, i32, i32, ctypes.POINTER(vp)]
+    L.fec_decoder_destroy.argtypes = [vp]
+    L.fec_decoder_receive.argtypes = [vp, vp, i32, i32, i32, vp, ip]
+    L.fec_plan_host.argtypes = [i32, i32, i32, i32, vp, i64, vp]
+    L.fec_util_fill_payload.argtypes = [vp, i64, i64, i32, ctypes.c_uint64, vp]
+    for name in ["fec_codec_create", "fec_codec_destroy", "fec_codec_geometry",
+                 "fec_codec_generator", "fec_encode_batch", "fec_decode_batch",
+                 "fec_decode_counters", "fec_timing_enable", "fec_timing_collect",
+                 "fec_encoder_create", "fec_encoder_destroy", "fec_encoder_transmit",
+                 "fec_decoder_create", "fec_decoder_destroy", "fec_decoder_receive",
+                 "fec_plan_host", "fec_util_fill_payload"]:
+        getattr(L, name).restype = i32
+    _lib = L
+    return _lib
+
+
+def check(status: int, what: str) -> None:
+    if status != FEC_OK:
+        raise FecError(status, what)

@@ -1,0 +1,199 @@
+"""Host-side mirror of the reference's coding API over the MI355X C ABI.
+
+Two faces, both backed only by ``libfec_amd.so`` (no CPU fallback):
+
+* ``FEC_Encoder`` / ``FEC_Decoder`` -- the reference's per-packet interface
+  (src/FEC_Encoder.cpp:42-68 ``onTransmit``, src/FEC_Decoder.cpp:49-72 ``onReceive``): same
+  constructor arguments, one call per sequence number from 0, same return meaning.
+* ``Codec`` -- batched, device-resident encode/decode of a whole stream window held in HBM as
+  torch uint8 tensors; launches on the current torch stream (torch is plumbing here: device
+  memory and streams).
+"""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+
+from ._lib import KERNEL_NAMES, check, lib
+
+
+def _stream_handle(torch):
+    return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+def _ptr(t):
+    return ctypes.c_void_p(t.data_ptr()) if t is not None else None
+
+
+class Codec:
+    """One (max_payload, T, B, N) configuration on the current HIP device.
+
+    Geometry follows src/Encoder.cpp:31-39: k = T-N+1, n = k+B, S = ceil((max_payload+2)/k)
+    sub-streams, CW = S*n untrimmed codeword bytes.
+    """
+
+    def __init__(self, max_payload: int, T: int, B: int, N: int):
+        h = ctypes.c_void_p()
+        check(lib().fec_codec_create(max_payload, T, B, N, ctypes.byref(h)), "fec_codec_create")
+        self._h = h
+        v = [ctypes.c_int() for _ in range(4)]
+        check(lib().fec_codec_geometry(h, *[ctypes.byref(x) for x in v]), "fec_codec_geometry")
+        self.k, self.n, self.S, self.CW = (x.value for x in v)
+        self.L, self.T, self.B, self.N = max_payload, T, B, N
+        self._ws = None
+
+    def __del__(self):
+        if getattr(self, "_h", None) and lib is not None:
+            try:
+                lib().fec_codec_destroy(self._h)
+            except Exception:
+                pass
+            self._h = None
+
+    # -- configuration ------------------------------------------------------------------------
+    def generator(self) -> np.ndarray:
+        """Encoder::getG() -- the k x n systematic generator matrix."""
+        G = np.zeros(self.k * self.n, dtype=np.uint8)
+        check(lib().fec_codec_generator(self._h, G.ctypes.data_as(ctypes.c_void_p)), "generator")
+        return G.reshape(self.k, self.n)
+
+    # -- batched device-resident path -----------------------------------------------------------
+    def encode(self, payload, lengths=None, history: int = 0, out=None, out_len=None):
+        """Encode rows ``history..`` of ``payload`` ([rows, L] uint8 on the GPU).
+
+        Rows ``0..history-1`` are earlier packets of the same stream (context only).  Returns
+        (codewords [P, CW] uint8, trimmed wire sizes [P] int32).
+        """
+        import torch
+        assert payload.dtype == torch.uint8 and payload.is_cuda and payload.dim() == 2
+        assert payload.shape[1] == self.L and payload.is_contiguous()
+        P = payload.shape[0] - history
+        if lengths is not None:
+            assert lengths.dtype == torch.int32 and lengths.is_cuda and lengths.numel() == payload.shape[0]
+        if out is None:
+            out = torch.empty((P, self.CW), dtype=torch.uint8, device=payload.device)
+        if out_len is None:
+            out_len = torch.empty(P, dtype=torch.int32, device=payload.device)
+        row0 = payload[history:] if P > 0 else payload
+        len0 = lengths[history:] if lengths is not None else None
+        check(lib().fec_encode_batch(self._h, _ptr(row0), _ptr(len0), history, P, _ptr(out),
+                                     _ptr(out_len), _stream_handle(torch)), "fec_encode_batch")
+        return out, out_len
+
+    def workspace(self, P: int):
+        import torch
+        nbytes = int(lib().fec_decode_workspace_bytes(self._h, P))
+        if self._ws is None or self._ws.numel() < nbytes:
+            self._ws = torch.empty(nbytes, dtype=torch.uint8, device="cuda")
+        return self._ws
+
+    def decode(self, codewords, erasure, out=None, out_len=None):
+        """A fresh decoder fed packets 0..P-1: returns (payload [P-T, L], lengths [P-T])."""
+        import torch
+        assert codewords.dtype == torch.uint8 and codewords.is_cuda and codewords.is_contiguous()
+        assert codewords.shape[1] == self.CW
+        P = codewords.shape[0]
+        assert erasure.dtype == torch.uint8 and erasure.numel() == P and erasure.is_cuda
+        Pout = max(0, P - self.T)
+        if out is None:
+            out = torch.empty((Pout, self.L), dtype=torch.uint8, device=codewords.device)
+        if out_len is None:
+            out_len = torch.empty(Pout, dtype=torch.int32, device=codewords.device)
+        ws = self.workspace(P)
+        check(lib().fec_decode_batch(self._h, _ptr(codewords), _ptr(erasure), P, _ptr(out),
+                                     _ptr(out_len), _ptr(ws), ws.numel(), _stream_handle(torch)),
+              "fec_decode_batch")
+        return out, out_len
+
+    def counters(self):
+        """(episodes, recovered, lost) of the last decode (synchronises the device)."""
+        v = [ctypes.c_int64() for _ in range(3)]
+        check(lib().fec_decode_counters(_ptr(self._ws), *[ctypes.byref(x) for x in v]),
+              "fec_decode_counters")
+        return tuple(x.value for x in v)
+
+    # -- per-kernel HIP-event timing ----------------------------------------------------------
+    def timing(self, enable: bool = True):
+        check(lib().fec_timing_enable(self._h, int(enable)), "fec_timing_enable")
+
+    def collect_timing(self):
+        """{kernel name: (total ms, launches)} since the last collect (synchronises)."""
+        n = len(KERNEL_NAMES)
+        ms = (ctypes.c_double * n)()
+        cnt = (ctypes.c_int64 * n)()
+        check(lib().fec_timing_collect(self._h, ms, cnt), "fec_timing_collect")
+        return {KERNEL_NAMES[i]: (ms[i], cnt[i]) for i in range(n)}
+
+
+class FEC_Encoder:
+    """FEC_Encoder(max_payload, T, B, N) -- per-packet interface (src/FEC_Encoder.cpp:22-68)."""
+
+    def __init__(self, max_payload: int, T: int, B: int, N: int, memory=None):
+        h = ctypes.c_void_p()
+        check(lib().fec_encoder_create(max_payload, T, B, N, ctypes.byref(h)), "FEC_Encoder")
+        self._h = h
+        self.T, self.B, self.N, self.max_payload = T, B, N, max_payload
+        self.k = T - N + 1
+        self.n = self.k + B
+        self.max_blocklength = -(-(max_payload + 2) // self.k) * self.n
+        self._cw = np.zeros(self.max_blocklength, dtype=np.uint8)
+
+    def __del__(self):
+        if getattr(self, "_h", None):
+            try:
+                lib().fec_encoder_destroy(self._h)
+            except Exception:
+                pass
+            self._h = None
+
+    def onTransmit(self, data, payload: int, seq: int):
+        """Returns (wire codeword bytes (trimmed), codeword_size)."""
+        d = np.ascontiguousarray(np.frombuffer(bytes(data), dtype=np.uint8) if isinstance(data, (bytes, bytearray)) else data, dtype=np.uint8)
+        size = ctypes.c_int()
+        check(lib().fec_encoder_transmit(self._h, d.ctypes.data_as(ctypes.c_void_p), payload, seq,
+                                         self._cw.ctypes.data_as(ctypes.c_void_p), ctypes.byref(size)),
+              "onTransmit")
+        return self._cw[:size.value].copy(), size.value
+
+
+class FEC_Decoder:
+    """FEC_Decoder(max_payload, T, B, N) -- per-packet interface (src/FEC_Decoder.cpp:26-72)."""
+
+    def __init__(self, max_payload: int, T: int, B: int, N: int, memory=None):
+        h = ctypes.c_void_p()
+        check(lib().fec_decoder_create(max_payload, T, B, N, ctypes.byref(h)), "FEC_Decoder")
+        self._h = h
+        self.T, self.B, self.N, self.max_payload = T, B, N, max_payload
+        self._out = np.zeros(max_payload, dtype=np.uint8)
+
+    def __del__(self):
+        if getattr(self, "_h", None):
+            try:
+                lib().fec_decoder_destroy(self._h)
+            except Exception:
+                pass
+            self._h = None
+
+    def onReceive(self, codeword, codeword_size: int, seq: int, erasure: bool):
+        """Returns (payload bytes of packet seq-T (max_payload, zero past the payload), payload)."""
+        p = ctypes.c_int()
+        if erasure or codeword is None:
+            st = lib().fec_decoder_receive(self._h, None, 0, seq, 1,
+                                           self._out.ctypes.data_as(ctypes.c_void_p), ctypes.byref(p))
+        else:
+            c = np.ascontiguousarray(codeword, dtype=np.uint8)
+            st = lib().fec_decoder_receive(self._h, c.ctypes.data_as(ctypes.c_void_p), codeword_size,
+                                           seq, 0, self._out.ctypes.data_as(ctypes.c_void_p),
+                                           ctypes.byref(p))
+        check(st, "onReceive")
+        return self._out.copy(), p.value
+
+
+def plan_host(max_payload: int, T: int, B: int, N: int, erasure: np.ndarray) -> np.ndarray:
+    """Symbolic decoder on the host: fate of packets 0..P-T-1 (1 copy, 2 recovered, 3 lost)."""
+    e = np.ascontiguousarray(erasure, dtype=np.uint8)
+    fate = np.zeros(e.size, dtype=np.uint8)
+    check(lib().fec_plan_host(max_payload, T, B, N, e.ctypes.data_as(ctypes.c_void_p), e.size,
+                              fate.ctypes.data_as(ctypes.c_void_p)), "fec_plan_host")
+    return fate[: max(0, e.size - T)]

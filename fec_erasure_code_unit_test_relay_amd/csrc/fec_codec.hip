@@ -1,0 +1,599 @@
+// fec_codec.hip -- codec objects, launchers and the C ABI declared in include/fec_amd.h.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstring>
+#include <memory>
+#include <new>
+#include <vector>
+
+#include "fec_amd.h"
+#include "fec_host.h"
+#include "fec_kernels.h"
+
+using fec::Geometry;
+
+namespace {
+
+constexpr int kLdsBudget = 64 * 1024;
+constexpr int kMaxPayload = 1500;  // UDP MTU; bounds the LDS tiles
+
+inline int round16(int v) { return (v + 15) & ~15; }
+
+#define HIP_TRY(expr)                                  \
+    do {                                               \
+        if ((expr) != hipSuccess) return FEC_ERR_HIP;  \
+    } while (0)
+
+struct EventPair {
+    int kernel;
+    hipEvent_t a, b;
+};
+
+}  // namespace
+
+struct fec_codec {
+    Geometry g;
+    std::vector<uint8_t> G;
+    fec::DecodeRules rules;
+    uint32_t* d_ptab = nullptr;  // [k][n-k][8]
+    uint8_t* d_rules = nullptr;
+    int64_t* d_wbase = nullptr;  // [n+1]
+    uint8_t* d_gf = nullptr;     // exp[512], log[256]
+    int enc_tp = 0;              // encode tile (packets per workgroup)
+    int copy_tp = 0;             // decode-copy tile
+    bool timing = false;
+    std::vector<EventPair> events;
+
+    ~fec_codec() {
+        for (auto& e : events) {
+            (void)hipEventDestroy(e.a);
+            (void)hipEventDestroy(e.b);
+        }
+        if (d_ptab) (void)hipFree(d_ptab);
+        if (d_rules) (void)hipFree(d_rules);
+        if (d_wbase) (void)hipFree(d_wbase);
+        if (d_gf) (void)hipFree(d_gf);
+    }
+
+    int enc_lds(int tp) const {
+        const int SP = (g.S + 3) & ~3;
+        const int rows = tp + g.n - 1;
+        const int Sk = g.S * g.k;
+        return round16(g.k * rows * SP) + round16(tp * g.CW) + 2 * ((Sk + 7) & ~7) + 4 * rows;
+    }
+    int copy_lds(int tp) const { return round16(tp * g.CW) + 2 * ((g.L + 2 + 7) & ~7) + 4 * tp; }
+
+    int begin(int kernel, hipStream_t s, hipEvent_t* stop) {
+        *stop = nullptr;
+        if (!timing) return FEC_OK;
+        EventPair e{kernel, nullptr, nullptr};
+        HIP_TRY(hipEventCreate(&e.a));
+        HIP_TRY(hipEventCreate(&e.b));
+        HIP_TRY(hipEventRecord(e.a, s));
+        events.push_back(e);
+        *stop = e.b;
+        return FEC_OK;
+    }
+    int end(hipEvent_t stop, hipStream_t s) {
+        if (stop) HIP_TRY(hipEventRecord(stop, s));
+        return FEC_OK;
+    }
+};
+
+namespace {
+
+int codec_init(fec_codec* c, int max_payload, int T, int B, int N) {
+    c->g = Geometry::make(max_payload, T, B, N);
+    const Geometry& g = c->g;
+    if (g.L > kMaxPayload || g.B < g.N || g.n > fec::kMaxRuleN) return FEC_ERR_ARG;
+    c->G = fec::make_generator(T, B, N);
+    c->rules.build(c->G, g.k, g.n, g.T);
+    const fec::Field& F = fec::field();
+
+    // Per parity coefficient: the three register tables of gf_mul4 plus a non-zero flag.
+    const int np = g.n - g.k;
+    std::vector<uint32_t> ptab(static_cast<size_t>(std::max(1, g.k * np)) * 8, 0);
+    for (int i = 0; i < g.k; ++i)
+        for (int jj = 0; jj < np; ++jj) {
+            const uint8_t c0 = c->G[i * g.n + g.k + jj];
+            uint32_t* t = &ptab[(i * np + jj) * 8];
+            auto pack = [&](int shift, int base) {
+                uint32_t v = 0;
+                for (int e = 0; e < 4; ++e) v |= uint32_t(F.mul(c0, uint8_t((base + e) << shift))) << (8 * e);
+                return v;
+            };
+            t[0] = pack(0, 0);
+            t[1] = pack(0, 4);
+            t[2] = pack(3, 0);
+            t[3] = pack(3, 4);
+            t[4] = pack(6, 0);
+            t[5] = c0 ? 1u : 0u;
+        }
+    HIP_TRY(hipMalloc(&c->d_ptab, ptab.size() * 4));
+    HIP_TRY(hipMemcpy(c->d_ptab, ptab.data(), ptab.size() * 4, hipMemcpyHostToDevice));
+    HIP_TRY(hipMalloc(&c->d_rules, std::max<size_t>(16, c->rules.table.size())));
+    HIP_TRY(hipMemcpy(c->d_rules, c->rules.table.data(), c->rules.table.size(), hipMemcpyHostToDevice));
+    std::vector<int64_t> wb(c->rules.w_base.begin(), c->rules.w_base.end());
+    HIP_TRY(hipMalloc(&c->d_wbase, wb.size() * 8));
+    HIP_TRY(hipMemcpy(c->d_wbase, wb.data(), wb.size() * 8, hipMemcpyHostToDevice));
+    uint8_t gf[768];
+    std::memcpy(gf, F.exp, 512);
+    std::memcpy(gf + 512, F.log, 256);
+    HIP_TRY(hipMalloc(&c->d_gf, 768));
+    HIP_TRY(hipMemcpy(c->d_gf, gf, 768, hipMemcpyHostToDevice));
+
+    // Largest power-of-two tiles (<= 64 packets) that fit the LDS budget.
+    for (int tp = 64; tp >= 1; tp >>= 1)
+        if (c->enc_lds(tp) <= kLdsBudget) {
+            c->enc_tp = tp;
+            break;
+        }
+    for (int tp = 64; tp >= 1; tp >>= 1)
+        if (c->copy_lds(tp) <= kLdsBudget) {
+            c->copy_tp = tp;
+            break;
+        }
+    if (!c->enc_tp || !c->copy_tp) return FEC_ERR_ARG;
+    return FEC_OK;
+}
+
+struct WsLayout {
+    size_t counters, episodes, rec_list, coef, total;
+};
+
+WsLayout ws_layout(const Geometry& g, int64_t P) {
+    auto up = [](size_t v) { return (v + 255) & ~size_t(255); };
+    WsLayout w;
+    w.counters = 0;
+    w.episodes = up(64);
+    w.rec_list = w.episodes + up(static_cast<size_t>(P) * 4);
+    w.coef = w.rec_list + up(static_cast<size_t>(P) * 4);
+    w.total = w.coef + up(static_cast<size_t>(P) * g.k * g.n);
+    return w;
+}
+
+int launch_encode(fec_codec* c, const uint8_t* d_payload, const int32_t* d_len, int64_t history,
+                  int64_t P, uint8_t* d_cw, int32_t* d_cwlen, hipStream_t s) {
+    if (P <= 0) return FEC_OK;
+    const Geometry& g = c->g;
+    fec::EncArgs a;
+    a.payload = d_payload;
+    a.len = d_len;
+    a.history = std::max<int64_t>(0, history);
+    a.P = P;
+    a.cw = d_cw;
+    a.cw_len = d_cwlen;
+    a.ptab = c->d_ptab;
+    a.L = g.L;
+    a.k = g.k;
+    a.n = g.n;
+    a.S = g.S;
+    a.CW = g.CW;
+    a.SP = (g.S + 3) & ~3;
+    a.TP = c->enc_tp;
+    a.ROWS = a.TP + g.n - 1;
+    a.plane = a.ROWS * a.SP;
+    a.xin_bytes = round16(g.k * a.plane);
+    a.xout_bytes = round16(a.TP * g.CW);
+    const int64_t blocks = (P + a.TP - 1) / a.TP;
+    if (blocks > 0x7fffffff) return FEC_ERR_ARG;
+    hipEvent_t stop;
+    if (int st = c->begin(FEC_KERNEL_ENCODE, s, &stop)) return st;
+    hipLaunchKernelGGL(fec::fec_encode_kernel, dim3(static_cast<unsigned>(blocks)), dim3(256),
+                       c->enc_lds(a.TP), s, a);
+    HIP_TRY(hipGetLastError());
+    return c->end(stop, s);
+}
+
+int launch_decode(fec_codec* c, const uint8_t* d_cw, const uint8_t* d_er, int64_t P, uint8_t* d_out,
+                  int32_t* d_outlen, void* d_ws, size_t ws_bytes, hipStream_t s) {
+    const Geometry& g = c->g;
+    const int64_t Pout = P - g.T;
+    if (Pout <= 0) return FEC_OK;
+    if (P > 0x7fffffffLL) return FEC_ERR_ARG;
+    const WsLayout w = ws_layout(g, P);
+    if (!d_ws || ws_bytes < w.total) return FEC_ERR_WORKSPACE;
+    uint8_t* ws = static_cast<uint8_t*>(d_ws);
+    int32_t* counters = reinterpret_cast<int32_t*>(ws + w.counters);
+    int32_t* episodes = reinterpret_cast<int32_t*>(ws + w.episodes);
+    int32_t* rec_list = reinterpret_cast<int32_t*>(ws + w.rec_list);
+    uint8_t* coef = ws + w.coef;
+    HIP_TRY(hipMemsetAsync(counters, 0, 64, s));
+    hipEvent_t stop;
+
+    // 1. resync points
+    if (int st = c->begin(FEC_KERNEL_DEC_SCAN, s, &stop)) return st;
+    const int64_t sblocks = std::min<int64_t>((P + 255) / 256, 4096);
+    hipLaunchKernelGGL(fec::fec_scan_kernel, dim3(static_cast<unsigned>(sblocks)), dim3(256), 0, s,
+                       d_er, P, g.T, counters, episodes);
+    HIP_TRY(hipGetLastError());
+    if (int st = c->end(stop, s)) return st;
+
+    // 2. symbolic replay per episode (one wavefront each)
+    fec::PlanArgs pa;
+    pa.er = d_er;
+    pa.P = P;
+    pa.Pout = Pout;
+    pa.rules = c->d_rules;
+    pa.wbase = c->d_wbase;
+    pa.gf = c->d_gf;
+    pa.ES = c->rules.entry_bytes;
+    pa.k = g.k;
+    pa.n = g.n;
+    pa.T = g.T;
+    pa.counters = counters;
+    pa.episodes = episodes;
+    pa.rec_list = rec_list;
+    pa.coef = coef;
+    const int plan_lds = 768 + 128 + g.n * g.n * g.n + 2 * g.n * g.k * g.n;
+    if (int st = c->begin(FEC_KERNEL_DEC_PLAN, s, &stop)) return st;
+    hipLaunchKernelGGL(fec::fec_plan_kernel, dim3(4096), dim3(64), plan_lds, s, pa);
+    HIP_TRY(hipGetLastError());
+    if (int st = c->end(stop, s)) return st;
+
+    // 3. received packets
+    fec::CopyArgs ca;
+    ca.cw = d_cw;
+    ca.er = d_er;
+    ca.P = P;
+    ca.Pout = Pout;
+    ca.out = d_out;
+    ca.out_len = d_outlen;
+    ca.L = g.L;
+    ca.k = g.k;
+    ca.n = g.n;
+    ca.S = g.S;
+    ca.CW = g.CW;
+    ca.T = g.T;
+    ca.TP = c->copy_tp;
+    ca.cwt_bytes = round16(ca.TP * g.CW);
+    const int64_t cblocks = (Pout + ca.TP - 1) / ca.TP;
+    if (int st = c->begin(FEC_KERNEL_DEC_COPY, s, &stop)) return st;
+    hipLaunchKernelGGL(fec::fec_copy_kernel, dim3(static_cast<unsigned>(cblocks)), dim3(256),
+                       c->copy_lds(ca.TP), s, ca);
+    HIP_TRY(hipGetLastError());
+    if (int st = c->end(stop, s)) return st;
+
+    // 4. recovered packets
+    fec::RecArgs ra;
+    ra.cw = d_cw;
+    ra.P = P;
+    ra.counters = counters;
+    ra.rec_list = rec_list;
+    ra.coef = coef;
+    ra.gf = c->d_gf;
+    ra.out = d_out;
+    ra.out_len = d_outlen;
+    ra.L = g.L;
+    ra.k = g.k;
+    ra.n = g.n;
+    ra.S = g.S;
+    ra.CW = g.CW;
+    if (int st = c->begin(FEC_KERNEL_DEC_RECOVER, s, &stop)) return st;
+    hipLaunchKernelGGL(fec::fec_recover_kernel, dim3(2048), dim3(256), 0, s, ra);
+    HIP_TRY(hipGetLastError());
+    return c->end(stop, s);
+}
+
+template <class F>
+int guarded(F&& f) {
+    try {
+        return f();
+    } catch (const std::bad_alloc&) {
+        return FEC_ERR_NOMEM;
+    } catch (const std::invalid_argument&) {
+        return FEC_ERR_ARG;
+    } catch (...) {
+        return FEC_ERR_ARG;
+    }
+}
+
+}  // namespace
+
+// ------------------------------------------------------------------------------------------
+// Streaming objects
+// ------------------------------------------------------------------------------------------
+struct fec_encoder {
+    std::unique_ptr<fec_codec> codec;
+    int64_t next = 0;              // expected seq
+    std::vector<uint8_t> hist;     // last n-1 payload rows (oldest first) + current row
+    std::vector<int32_t> hlen;
+    uint8_t* d_in = nullptr;       // n rows x L
+    int32_t* d_len = nullptr;      // n
+    uint8_t* d_cw = nullptr;       // CW
+    int32_t* d_cwlen = nullptr;    // 1
+    ~fec_encoder() {
+        if (d_in) (void)hipFree(d_in);
+        if (d_len) (void)hipFree(d_len);
+        if (d_cw) (void)hipFree(d_cw);
+        if (d_cwlen) (void)hipFree(d_cwlen);
+    }
+};
+
+struct fec_decoder {
+    static constexpr int RR = 64;  // device ring rows (>= T + k)
+    std::unique_ptr<fec_codec> codec;
+    std::unique_ptr<fec::StreamPlanner> planner;
+    int64_t next = 0;
+    std::vector<uint8_t> pad;      // CW-byte staging row
+    uint8_t* d_ring = nullptr;     // RR x CW
+    uint8_t* d_coef = nullptr;     // k x n
+    uint8_t* d_out = nullptr;      // L
+    int32_t* d_outlen = nullptr;   // 1
+    ~fec_decoder() {
+        if (d_ring) (void)hipFree(d_ring);
+        if (d_coef) (void)hipFree(d_coef);
+        if (d_out) (void)hipFree(d_out);
+        if (d_outlen) (void)hipFree(d_outlen);
+    }
+};
+
+// ------------------------------------------------------------------------------------------
+// C ABI
+// ------------------------------------------------------------------------------------------
+extern "C" {
+
+const char* fec_strerror(int status) {
+    switch (status) {
+        case FEC_OK: return "ok";
+        case FEC_ERR_ARG: return "invalid argument or unsupported (max_payload,T,B,N)";
+        case FEC_ERR_HIP: return "HIP runtime error";
+        case FEC_ERR_NOMEM: return "out of memory";
+        case FEC_ERR_WORKSPACE: return "decode workspace too small";
+        case FEC_ERR_SEQUENCE: return "sequence numbers must be consecutive from 0";
+        default: return "unknown error";
+    }
+}
+
+int fec_version(void) { return 1; }
+
+int fec_codec_create(int max_payload, int T, int B, int N, fec_codec** out) {
+    if (!out) return FEC_ERR_ARG;
+    *out = nullptr;
+    return guarded([&] {
+        std::unique_ptr<fec_codec> c(new fec_codec());
+        if (int st = codec_init(c.get(), max_payload, T, B, N)) return st;
+        *out = c.release();
+        return FEC_OK;
+    });
+}
+
+int fec_codec_destroy(fec_codec* codec) {
+    delete codec;
+    return FEC_OK;
+}
+
+int fec_codec_geometry(const fec_codec* c, int* k, int* n, int* S, int* CW) {
+    if (!c) return FEC_ERR_ARG;
+    if (k) *k = c->g.k;
+    if (n) *n = c->g.n;
+    if (S) *S = c->g.S;
+    if (CW) *CW = c->g.CW;
+    return FEC_OK;
+}
+
+int fec_codec_generator(const fec_codec* c, uint8_t* G) {
+    if (!c || !G) return FEC_ERR_ARG;
+    std::memcpy(G, c->G.data(), c->G.size());
+    return FEC_OK;
+}
+
+int fec_encode_batch(fec_codec* c, const uint8_t* d_payload, const int32_t* d_len, int64_t history,
+                     int64_t P, uint8_t* d_cw, int32_t* d_cwlen, void* stream) {
+    if (!c || P < 0 || (P > 0 && (!d_payload || !d_cw || !d_cwlen))) return FEC_ERR_ARG;
+    return launch_encode(c, d_payload, d_len, history, P, d_cw, d_cwlen,
+                         static_cast<hipStream_t>(stream));
+}
+
+size_t fec_decode_workspace_bytes(const fec_codec* c, int64_t P) {
+    if (!c || P < 0) return 0;
+    return ws_layout(c->g, P).total;
+}
+
+int fec_decode_batch(fec_codec* c, const uint8_t* d_cw, const uint8_t* d_er, int64_t P,
+                     uint8_t* d_out, int32_t* d_outlen, void* d_ws, size_t ws_bytes, void* stream) {
+    if (!c || P < 0) return FEC_ERR_ARG;
+    if (P > c->g.T && (!d_cw || !d_er || !d_out || !d_outlen)) return FEC_ERR_ARG;
+    return launch_decode(c, d_cw, d_er, P, d_out, d_outlen, d_ws, ws_bytes,
+                         static_cast<hipStream_t>(stream));
+}
+
+int fec_decode_counters(const void* d_ws, int64_t* episodes, int64_t* recovered, int64_t* lost) {
+    if (!d_ws) return FEC_ERR_ARG;
+    int32_t h[4];
+    HIP_TRY(hipDeviceSynchronize());
+    HIP_TRY(hipMemcpy(h, d_ws, sizeof(h), hipMemcpyDeviceToHost));
+    if (episodes) *episodes = h[0];
+    if (recovered) *recovered = h[1];
+    if (lost) *lost = h[2];
+    return FEC_OK;
+}
+
+int fec_timing_enable(fec_codec* c, int enable) {
+    if (!c) return FEC_ERR_ARG;
+    c->timing = enable != 0;
+    return FEC_OK;
+}
+
+int fec_timing_collect(fec_codec* c, double* total_ms, int64_t* launches) {
+    if (!c || !total_ms || !launches) return FEC_ERR_ARG;
+    for (int i = 0; i < FEC_KERNEL_COUNT; ++i) {
+        total_ms[i] = 0.0;
+        launches[i] = 0;
+    }
+    for (auto& e : c->events) {
+        HIP_TRY(hipEventSynchronize(e.b));
+        float ms = 0.f;
+        HIP_TRY(hipEventElapsedTime(&ms, e.a, e.b));
+        total_ms[e.kernel] += ms;
+        launches[e.kernel] += 1;
+        (void)hipEventDestroy(e.a);
+        (void)hipEventDestroy(e.b);
+    }
+    c->events.clear();
+    return FEC_OK;
+}
+
+// ---- streaming encoder --------------------------------------------------------------------
+int fec_encoder_create(int max_payload, int T, int B, int N, fec_encoder** out) {
+    if (!out) return FEC_ERR_ARG;
+    *out = nullptr;
+    return guarded([&] {
+        std::unique_ptr<fec_encoder> e(new fec_encoder());
+        fec_codec* c = nullptr;
+        if (int st = fec_codec_create(max_payload, T, B, N, &c)) return st;
+        e->codec.reset(c);
+        const Geometry& g = c->g;
+        e->hist.assign(static_cast<size_t>(g.n) * g.L, 0);
+        e->hlen.assign(g.n, 0);
+        HIP_TRY(hipMalloc(&e->d_in, static_cast<size_t>(g.n) * g.L));
+        HIP_TRY(hipMalloc(&e->d_len, g.n * 4));
+        HIP_TRY(hipMalloc(&e->d_cw, g.CW));
+        HIP_TRY(hipMalloc(&e->d_cwlen, 4));
+        *out = e.release();
+        return FEC_OK;
+    });
+}
+
+int fec_encoder_destroy(fec_encoder* e) {
+    delete e;
+    return FEC_OK;
+}
+
+int fec_encoder_transmit(fec_encoder* e, const uint8_t* data, int payload, int seq, uint8_t* cw_out,
+                         int* cw_size) {
+    if (!e || !cw_out || !cw_size || payload < 0 || (payload > 0 && !data)) return FEC_ERR_ARG;
+    if (seq != e->next) return FEC_ERR_SEQUENCE;
+    const Geometry& g = e->codec->g;
+    if (payload > g.L) payload = g.L;
+    const int n = g.n;
+    // slide the (n-1)-packet history window and append packet seq as the last row
+    std::memmove(e->hist.data(), e->hist.data() + g.L, static_cast<size_t>(n - 1) * g.L);
+    std::memmove(e->hlen.data(), e->hlen.data() + 1, static_cast<size_t>(n - 1) * 4);
+    uint8_t* row = e->hist.data() + static_cast<size_t>(n - 1) * g.L;
+    std::memset(row, 0, g.L);
+    if (payload > 0) std::memcpy(row, data, payload);
+    e->hlen[n - 1] = payload;
+    HIP_TRY(hipMemcpy(e->d_in, e->hist.data(), e->hist.size(), hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpy(e->d_len, e->hlen.data(), n * 4, hipMemcpyHostToDevice));
+    const int64_t history = std::min<int64_t>(seq, n - 1);
+    if (int st = launch_encode(e->codec.get(), e->d_in + static_cast<size_t>(n - 1) * g.L,
+                               e->d_len + (n - 1), history, 1, e->d_cw, e->d_cwlen, nullptr))
+        return st;
+    HIP_TRY(hipMemcpy(cw_out, e->d_cw, g.CW, hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemcpy(cw_size, e->d_cwlen, 4, hipMemcpyDeviceToHost));
+    ++e->next;
+    return FEC_OK;
+}
+
+// ---- streaming decoder --------------------------------------------------------------------
+int fec_decoder_create(int max_payload, int T, int B, int N, fec_decoder** out) {
+    if (!out) return FEC_ERR_ARG;
+    *out = nullptr;
+    return guarded([&] {
+        std::unique_ptr<fec_decoder> d(new fec_decoder());
+        fec_codec* c = nullptr;
+        if (int st = fec_codec_create(max_payload, T, B, N, &c)) return st;
+        d->codec.reset(c);
+        const Geometry& g = c->g;
+        if (g.T + g.k > fec_decoder::RR) return FEC_ERR_ARG;
+        d->planner.reset(new fec::StreamPlanner(g, &c->rules));
+        d->pad.assign(g.CW, 0);
+        HIP_TRY(hipMalloc(&d->d_ring, static_cast<size_t>(fec_decoder::RR) * g.CW));
+        HIP_TRY(hipMemset(d->d_ring, 0, static_cast<size_t>(fec_decoder::RR) * g.CW));
+        HIP_TRY(hipMalloc(&d->d_coef, g.k * g.n));
+        HIP_TRY(hipMalloc(&d->d_out, g.L));
+        HIP_TRY(hipMalloc(&d->d_outlen, 4));
+        *out = d.release();
+        return FEC_OK;
+    });
+}
+
+int fec_decoder_destroy(fec_decoder* d) {
+    delete d;
+    return FEC_OK;
+}
+
+int fec_decoder_receive(fec_decoder* d, const uint8_t* cw, int cw_size, int seq, int erasure,
+                        uint8_t* payload_out, int* payload) {
+    if (!d || !payload_out || !payload) return FEC_ERR_ARG;
+    if (seq != d->next) return FEC_ERR_SEQUENCE;
+    const Geometry& g = d->codec->g;
+    const bool er = erasure != 0 || cw == nullptr;
+    if (!er) {  // FEC_Decoder.cpp:55-63: keep a zero-padded copy of the wire codeword
+        int sz = std::max(0, std::min(cw_size, g.CW));
+        std::memset(d->pad.data(), 0, g.CW);
+        if (sz) std::memcpy(d->pad.data(), cw, sz);
+        HIP_TRY(hipMemcpy(d->d_ring + static_cast<size_t>(seq % fec_decoder::RR) * g.CW,
+                          d->pad.data(), g.CW, hipMemcpyHostToDevice));
+    }
+    fec::StepResult r;
+    int st = guarded([&] {
+        r = d->planner->step(seq, er);
+        return FEC_OK;
+    });
+    if (st) return st;
+    ++d->next;
+    if (r.fate == fec::kNone || r.fate == fec::kLost) {
+        std::memset(payload_out, 0, g.L);
+        *payload = 0;
+        return FEC_OK;
+    }
+    uint8_t coef[fec::kMaxK * fec::kMaxN];
+    if (r.fate == fec::kCopy) {
+        std::memset(coef, 0, sizeof(coef));
+        for (int i = 0; i < g.k; ++i) coef[i * g.n + i] = 1;
+    } else {
+        std::memcpy(coef, r.coef, g.k * g.n);
+    }
+    HIP_TRY(hipMemcpy(d->d_coef, coef, g.k * g.n, hipMemcpyHostToDevice));
+    fec::StreamOutArgs a;
+    a.ring = d->d_ring;
+    a.RR = fec_decoder::RR;
+    a.x = r.x;
+    a.coef = d->d_coef;
+    a.gf = d->codec->d_gf;
+    a.out = d->d_out;
+    a.out_len = d->d_outlen;
+    a.L = g.L;
+    a.k = g.k;
+    a.n = g.n;
+    a.CW = g.CW;
+    a.clamp = r.slow ? 1 : 0;
+    hipLaunchKernelGGL(fec::fec_stream_out_kernel, dim3(1), dim3(256), 0, nullptr, a);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipMemcpy(payload_out, d->d_out, g.L, hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemcpy(payload, d->d_outlen, 4, hipMemcpyDeviceToHost));
+    return FEC_OK;
+}
+
+int fec_plan_host(int max_payload, int T, int B, int N, const uint8_t* erasure, int64_t P,
+                  uint8_t* fate) {
+    if (!erasure || !fate || P < 0) return FEC_ERR_ARG;
+    return guarded([&] {
+        const Geometry g = Geometry::make(max_payload, T, B, N);
+        if (g.B < g.N || g.n > fec::kMaxRuleN) return FEC_ERR_ARG;
+        fec::DecodeRules rules;
+        rules.build(fec::make_generator(T, B, N), g.k, g.n, g.T);
+        fec::StreamPlanner pl(g, &rules);
+        for (int64_t t = 0; t < P; ++t) {
+            const fec::StepResult r = pl.step(t, erasure[t] != 0);
+            if (r.x >= 0) fate[r.x] = static_cast<uint8_t>(r.fate);
+        }
+        return FEC_OK;
+    });
+}
+
+int fec_util_fill_payload(uint8_t* d_out, int64_t t0, int64_t count, int L, uint64_t seed,
+                          void* stream) {
+    if (!d_out || count < 0 || L <= 0) return FEC_ERR_ARG;
+    if (count == 0) return FEC_OK;
+    const int64_t blocks = std::min<int64_t>((count * L + 255) / 256, 8192);
+    hipLaunchKernelGGL(fec::fec_fill_kernel, dim3(static_cast<unsigned>(blocks)), dim3(256), 0,
+                       static_cast<hipStream_t>(stream), d_out, t0, count, L, seed);
+    HIP_TRY(hipGetLastError());
+    return FEC_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,276 @@
+// fec_host.cpp -- see fec_host.h.
+#include "fec_host.h"
+
+#include <algorithm>
+#include <atomic>
+#include <thread>
+
+namespace fec {
+
+const Field& field() {
+    static const Field f;
+    return f;
+}
+
+// gen_G_cauchy (src/codingOperations.cpp:48-95).  The ISA-L matrices it starts from
+// (gf_gen_cauchy1_matrix / gf_gen_rs_matrix, n x k, identity on top) are written directly in
+// transposed form: parity column j >= k of G holds row j of the ISA-L matrix.
+std::vector<uint8_t> make_generator(int T, int B, int N) {
+    const Field& F = field();
+    const int k = T - N + 1, n = k + B;
+    std::vector<uint8_t> G(static_cast<size_t>(k) * n, 0);
+    auto at = [&](int i, int j) -> uint8_t& { return G[static_cast<size_t>(i) * n + j]; };
+    for (int i = 0; i < k; ++i) at(i, i) = 1;
+    const bool rs = (T == 10 && B == 8 && N == 4) || (T == 11 && B == 5 && N == 4);
+    uint8_t gen = 1;  // RS: row j uses powers of 2^(j-k)
+    for (int j = k; j < n; ++j) {
+        uint8_t p = 1;
+        for (int i = 0; i < k; ++i) {
+            if (rs) {
+                at(i, j) = p;
+                p = F.mul(p, gen);
+            } else {
+                at(i, j) = F.inv(static_cast<uint8_t>(j ^ i));
+            }
+        }
+        gen = F.mul(gen, 2);
+    }
+    if (B == 0) return G;
+    const int d = B - N;  // width of the burst-only parity block
+    if (2 * k >= n) {      // high-rate regime
+        for (int i = 0; i < d; ++i) {
+            for (int j = k + N + i; j < n; ++j) at(i, j) = 0;
+            for (int j = k; j < k + i; ++j) at(i, j) = 0;
+        }
+        for (int i = d; i < B; ++i)
+            for (int j = k; j < k + d; ++j) at(i, j) = 0;
+    } else {  // low-rate regime
+        for (int i = 0; i < d; ++i) {
+            for (int j = k + N + i; j < n; ++j) at(i, j) = 0;
+            for (int j = B; j < B + i; ++j) at(i, j) = 0;
+        }
+        for (int i = d; i < k; ++i)
+            for (int j = B; j < B + d; ++j) at(i, j) = 0;
+    }
+    return G;
+}
+
+// One column of the k x w decoding matrix together with its column of the action matrix.
+struct Column {
+    uint8_t v[kMaxK];
+    uint8_t a[kMaxN];
+};
+
+// Column reduction with a sliding pivot row, exactly the semantics of gf256_rref_matrix
+// (src/basicOperations.cpp:43-122): for column position i the pivot sits in row i+offset; a zero
+// pivot is replaced by the first later column with a non-zero entry in that row (swap), and a row
+// without any such column bumps the offset.  The pivot column is normalised and eliminated from
+// every other column whose entry in the pivot row is non-zero.  Columns carry their action
+// column along, so decoded = codeword * action.
+static void column_reduce(const Field& F, int m, int w, Column* c) {
+    int row = 0;
+    for (int i = 0; i < w && row < m;) {
+        if (c[i].v[row] == 0) {
+            int j = i + 1;
+            while (j < w && c[j].v[row] == 0) ++j;
+            if (j == w) {  // no pivot available in this row
+                ++row;
+                continue;
+            }
+            std::swap(c[i], c[j]);
+        }
+        const uint8_t s = F.inv(c[i].v[row]);
+        for (int r = 0; r < m; ++r) c[i].v[r] = F.mul(c[i].v[r], s);
+        for (int r = 0; r < w; ++r) c[i].a[r] = F.mul(c[i].a[r], s);
+        for (int j = 0; j < w; ++j) {
+            if (j == i) continue;
+            const uint8_t f = c[j].v[row];
+            if (!f) continue;
+            for (int r = 0; r < m; ++r) c[j].v[r] ^= F.mul(f, c[i].v[r]);
+            for (int r = 0; r < w; ++r) c[j].a[r] ^= F.mul(f, c[i].a[r]);
+        }
+        ++i;
+        ++row;
+    }
+}
+
+void decode_rule(const uint8_t* G, int k, int n, int w, uint32_t mask, uint8_t* sel,
+                 uint8_t* col) {
+    const Field& F = field();
+    Column c[kMaxN];
+    for (int j = 0; j < w; ++j) {
+        const bool erased = (mask >> j) & 1u;
+        for (int r = 0; r < k; ++r) c[j].v[r] = erased ? 0 : G[r * n + j];
+        std::memset(c[j].a, 0, sizeof(c[j].a));
+        c[j].a[j] = 1;
+    }
+    column_reduce(F, k, w, c);
+    // A data symbol i is declared recovered when the first unit entry of row i among columns
+    // i..k-1 sits in a column that is zero below row i (codingOperations.cpp:204-230).
+    for (int i = 0; i < k; ++i) {
+        sel[i] = 0xFF;
+        std::memset(col + i * w, 0, w);
+        int j = i;
+        while (j < k && c[j].v[i] != 1) ++j;
+        if (j == k) continue;
+        bool unit = true;
+        for (int r = i + 1; r < k; ++r) unit = unit && c[j].v[r] == 0;
+        if (!unit) continue;
+        sel[i] = static_cast<uint8_t>(j);
+        for (int r = 0; r < w; ++r) col[i * w + r] = c[j].a[r];
+    }
+}
+
+void DecodeRules::build(const std::vector<uint8_t>& G, int k_, int n_, int T_) {
+    k = k_;
+    n = n_;
+    T = T_;
+    if (n > kMaxRuleN) throw std::invalid_argument("decode rules need n <= 17");
+    w_lo = std::min(T + 1, n);
+    entry_bytes = k * (1 + n);
+    w_base.assign(n + 1, -1);
+    int64_t total = 0;
+    for (int w = w_lo; w <= n; ++w) {
+        w_base[w] = total;
+        total += (int64_t(1) << w) * entry_bytes;
+    }
+    table.assign(static_cast<size_t>(total), 0);
+    struct Job { int w; uint32_t lo, hi; };
+    std::vector<Job> jobs;
+    for (int w = w_lo; w <= n; ++w) {
+        const uint32_t count = 1u << w, chunk = 512;
+        for (uint32_t m = 0; m < count; m += chunk) jobs.push_back({w, m, std::min(count, m + chunk)});
+    }
+    const unsigned nth = std::max(1u, std::min(8u, std::thread::hardware_concurrency()));
+    std::vector<std::thread> pool;
+    std::atomic<size_t> next{0};
+    auto worker = [&]() {
+        uint8_t col[kMaxK * kMaxN];
+        for (size_t q; (q = next.fetch_add(1)) < jobs.size();) {
+            const Job& jb = jobs[q];
+            for (uint32_t m = jb.lo; m < jb.hi; ++m) {
+                uint8_t* e = table.data() + w_base[jb.w] + int64_t(m) * entry_bytes;
+                decode_rule(G.data(), k, n, jb.w, m, e, col);
+                for (int i = 0; i < k; ++i) std::memcpy(e + k + i * n, col + i * jb.w, jb.w);
+            }
+        }
+    };
+    if (jobs.size() < 8) {
+        worker();
+    } else {
+        for (unsigned i = 0; i < nth; ++i) pool.emplace_back(worker);
+        for (auto& th : pool) th.join();
+    }
+}
+
+// ------------------------------------------------------------------------------------------
+// StreamPlanner
+// ------------------------------------------------------------------------------------------
+StreamPlanner::StreamPlanner(const Geometry& g, const DecodeRules* rules)
+    : k_(g.k), n_(g.n), T_(g.T), rules_(rules),
+      er_(g.n, 0u),
+      cwc_(static_cast<size_t>(g.n) * g.n * g.n, 0),
+      datc_(static_cast<size_t>(g.n) * g.k * g.n, 0),
+      hist_(g.T + 1, 0) {
+    if (g.B < g.N) throw std::invalid_argument("the streaming planner needs B >= N");
+}
+
+// Decode of data symbol t of block b with window min(t+T+1, n) (decodeBlock semantics).
+void StreamPlanner::decode_block(int b, int t) {
+    const Field& F = field();
+    if (t < k_ && !((er_[b] >> t) & 1u)) std::memcpy(dat(b, t), cw(b, t), n_);
+    const int w = std::min(t + T_ + 1, n_);
+    const uint32_t full = (w >= 32) ? 0xffffffffu : ((1u << w) - 1u);
+    const uint32_t m = er_[b] & full;
+    if (m == full) return;
+    const uint32_t kmask = (1u << k_) - 1u;
+    if (!(m & kmask)) return;  // no erased data symbol: nothing to recover
+    const uint8_t* e = rules_->entry(w, m);
+    uint8_t fresh[kMaxK][kMaxN];
+    uint32_t got = 0;
+    for (int i = 0; i < k_; ++i) {
+        if (!((m >> i) & 1u) || e[i] == 0xFF) continue;
+        const uint8_t* colv = e + k_ + i * n_;
+        std::memset(fresh[i], 0, n_);
+        for (int c = 0; c < w; ++c) {
+            const uint8_t f = colv[c];
+            if (!f || ((m >> c) & 1u)) continue;
+            const uint8_t* src = cw(b, c);
+            for (int q = 0; q < n_; ++q) fresh[i][q] ^= F.mul(f, src[q]);
+        }
+        got |= 1u << i;
+    }
+    for (int i = 0; i < k_; ++i) {
+        if (!((got >> i) & 1u)) continue;
+        er_[b] &= ~(1u << i);
+        std::memcpy(dat(b, i), fresh[i], n_);
+        std::memcpy(cw(b, i), fresh[i], n_);
+    }
+}
+
+// Decoder_Block_Code::decodeSymbol.
+void StreamPlanner::decode_symbol(int b, int p, bool erased) {
+    if (erased) {
+        er_[b] |= 1u << p;
+    } else {
+        er_[b] &= ~(1u << p);
+        uint8_t* v = cw(b, p);
+        std::memset(v, 0, n_);
+        v[p] = 1;
+    }
+    if (p < T_) return;
+    decode_block(b, p - T_);
+    if (p == n_ - 1)
+        for (int j = p - T_ + 1; j < k_; ++j) decode_block(b, j);
+}
+
+// Decoder_Basic::decodeStream input half: symbol p of a packet fed at `time` goes to block
+// (time - p) mod n.
+void StreamPlanner::feed(int64_t time, bool erased) {
+    const int r = static_cast<int>(((time % n_) + n_) % n_);
+    for (int p = 0; p < n_; ++p) decode_symbol((r - p + n_) % n_, p, erased);
+}
+
+StepResult StreamPlanner::step(int64_t t, bool erased) {
+    StepResult out;
+    out.x = t - T_;
+    hist_[t % (T_ + 1)] = erased ? 1 : 0;
+    if (!erased) {
+        if (t - latest_ > T_) latest_ = -1;
+        if (latest_ == -1) {  // fast path: the stored codeword t-T is output as is
+            out.fate = out.x >= 0 ? kCopy : kNone;
+            out.slow = false;
+            return out;
+        }
+    } else {
+        if (latest_ == -1) {  // resync (Decoder.cpp:111-133)
+            for (int i = 0; i < n_ - T_; ++i) feed(t + i, true);
+            for (int i = 0; i < T_; ++i)
+                if (t - T_ + i >= 0) feed(t - T_ + i, false);
+        }
+        latest_ = t;
+    }
+    feed(t, erased);
+    out.slow = true;
+    if (out.x < 0) {
+        out.fate = kNone;
+        return out;
+    }
+    const bool x_erased = hist_[out.x % (T_ + 1)] != 0;
+    if (!x_erased) {
+        out.fate = kCopy;
+        return out;
+    }
+    for (int i = 0; i < k_; ++i) {
+        const int b = static_cast<int>(((out.x - i) % n_ + n_) % n_);
+        if ((er_[b] >> i) & 1u) {
+            out.fate = kLost;
+            return out;
+        }
+        std::memcpy(out.coef + i * n_, dat(b, i), n_);
+    }
+    out.fate = kRecovered;
+    return out;
+}
+
+}  // namespace fec

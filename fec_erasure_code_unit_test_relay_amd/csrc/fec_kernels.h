@@ -1,0 +1,99 @@
+// fec_kernels.h -- device kernels of the MI355X streaming-erasure codec (gfx950 / CDNA4).
+//
+// Byte-wise GF(2^8) work, HBM-bound: no MFMA.  The kernels (launchers in fec_codec.hip):
+//   fec_encode_kernel      closed-form diagonal-interleaved encode of a tile of packets
+//                          (replaces Encoder::encodeStream -> Encoder_Basic -> encodeBlock,
+//                          src/Encoder.cpp:65-98, src/Encoder_Basic.cpp:48-74,
+//                          src/codingOperations.cpp:131-147);
+//   fec_scan_kernel        finds the packets where the reference decoder leaves its fast path
+//                          and resynchronises (src/Decoder.cpp:80-83, 109-133);
+//   fec_plan_kernel        one wavefront per erasure episode: symbolic replay of the reference's
+//                          per-symbol decode (decodeBlock / gf256_rref_matrix through the
+//                          precomputed decode rules), emitting per recovered packet k x n GF
+//                          coefficients over received codeword bytes;
+//   fec_copy_kernel        systematic gather + length parse for every received packet (the
+//                          decoder's fast path, src/Decoder.cpp:77-108, and the slow path's
+//                          received packets);
+//   fec_recover_kernel     applies the coefficients to the bytes of every recovered packet;
+//   fec_stream_out_kernel  single-packet output for the streaming (per-call) decoder.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace fec {
+
+struct EncArgs {
+    const uint8_t* payload;     // row 0 = first packet of the batch
+    const int32_t* len;         // may be null (all L)
+    int64_t history;            // valid rows before row 0
+    int64_t P;
+    uint8_t* cw;
+    int32_t* cw_len;
+    const uint32_t* ptab;       // [k][n-k][8] perm tables per parity coefficient
+    int L, k, n, S, CW;
+    int SP;                     // S rounded up to a multiple of 4
+    int TP;                     // packets per workgroup tile
+    int ROWS;                   // TP + n - 1
+    int plane;                  // ROWS * SP  (bytes of one position plane)
+    int xin_bytes, xout_bytes;  // 16-aligned LDS carve sizes
+};
+
+struct CopyArgs {
+    const uint8_t* cw;
+    const uint8_t* er;
+    int64_t P, Pout;
+    uint8_t* out;
+    int32_t* out_len;
+    int L, k, n, S, CW, T, TP;
+    int cwt_bytes;              // 16-aligned
+};
+
+struct PlanArgs {
+    const uint8_t* er;
+    int64_t P, Pout;
+    const uint8_t* rules;
+    const int64_t* wbase;
+    const uint8_t* gf;          // exp[512] then log[256]
+    int ES;                     // decode-rule entry bytes = k*(1+n)
+    int k, n, T;
+    int32_t* counters;          // [0] episodes, [1] recovered, [2] lost
+    const int32_t* episodes;
+    int32_t* rec_list;
+    uint8_t* coef;              // [recovered][k][n]
+};
+
+struct RecArgs {
+    const uint8_t* cw;
+    int64_t P;
+    const int32_t* counters;
+    const int32_t* rec_list;
+    const uint8_t* coef;
+    const uint8_t* gf;
+    uint8_t* out;
+    int32_t* out_len;
+    int L, k, n, S, CW;
+};
+
+struct StreamOutArgs {
+    const uint8_t* ring;        // RR rows of CW bytes, row = seq % RR
+    int RR;
+    int64_t x;                  // packet to output
+    const uint8_t* coef;        // k x n
+    const uint8_t* gf;
+    uint8_t* out;               // L bytes
+    int32_t* out_len;           // 1 int
+    int L, k, n, CW;
+    int clamp;                  // 1: slow path (payload clamped to L)
+};
+
+__global__ void fec_encode_kernel(EncArgs a);
+__global__ void fec_scan_kernel(const uint8_t* er, int64_t P, int T, int32_t* counters,
+                                int32_t* episodes);
+__global__ void fec_plan_kernel(PlanArgs a);
+__global__ void fec_copy_kernel(CopyArgs a);
+__global__ void fec_recover_kernel(RecArgs a);
+__global__ void fec_stream_out_kernel(StreamOutArgs a);
+__global__ void fec_fill_kernel(uint8_t* out, int64_t t0, int64_t count, int L, uint64_t seed);
+
+}  // namespace fec

@@ -1,0 +1,121 @@
+/*
+ * fec_amd.h -- C ABI of the MI355X-native GF(2^8) streaming-erasure codec.
+ *
+ * Drop-in boundary for the hot path of domanovi/FEC_Erasure_Code_Unit_Test_Relay.  Every entry
+ * point takes plain pointers and sizes (no torch, no C++ types) and returns an int status
+ * (FEC_OK = 0, negative = error, see fec_strerror); nothing throws across the ABI.
+ *
+ * Two layers:
+ *   1. Streaming per-packet API (host buffers), one call per sequence number in increasing order
+ *      starting at 0 -- exactly the reference's FEC_Encoder::onTransmit / FEC_Decoder::onReceive
+ *      contract.  The C++ classes in fec_amd_dropin.h wrap it with the reference's names.
+ *   2. Batched device-resident API: many packets of one stream per call, inputs and outputs in
+ *      HBM, asynchronous on a caller-supplied hipStream_t (passed as void*; NULL = null stream).
+ *
+ * Wire formats are the reference's: codeword = S sub-streams of n bytes (k systematic bytes of
+ * [len_hi, len_lo, payload, zero pad] then n-k parity bytes); the wire form is that codeword with
+ * trailing zero bytes trimmed; a received wire codeword is zero-padded back to CW bytes.
+ */
+#ifndef FEC_AMD_H
+#define FEC_AMD_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define FEC_OK 0
+#define FEC_ERR_ARG (-1)          /* bad argument / unsupported (T,B,N) */
+#define FEC_ERR_HIP (-2)          /* HIP runtime error (no device, launch failure, ...) */
+#define FEC_ERR_NOMEM (-3)        /* allocation failed */
+#define FEC_ERR_WORKSPACE (-4)    /* decode workspace too small */
+#define FEC_ERR_SEQUENCE (-5)     /* streaming call out of sequence order */
+
+typedef struct fec_codec fec_codec;        /* one (max_payload,T,B,N) configuration on a device */
+typedef struct fec_encoder fec_encoder;    /* one streaming encoder (per stream) */
+typedef struct fec_decoder fec_decoder;    /* one streaming decoder (per stream) */
+
+const char *fec_strerror(int status);
+int fec_version(void);
+
+/* ---- configuration -------------------------------------------------------------------------
+ * Replaces the constructors Encoder::Encoder / Decoder::Decoder (src/Encoder.cpp:26-50,
+ * src/Decoder.cpp:24-53) and init_at_sender/gen_G_cauchy (src/codingOperations.cpp:48-116):
+ * derives k=T-N+1, n=k+B, S=ceil((max_payload+2)/k), CW=S*n, builds G and the decode rules and
+ * uploads them to the current HIP device.  Requires N <= B (as every reference configuration). */
+int fec_codec_create(int max_payload, int T, int B, int N, fec_codec **out);
+int fec_codec_destroy(fec_codec *codec);
+int fec_codec_geometry(const fec_codec *codec, int *k, int *n, int *S, int *CW);
+/* Encoder::getG / Decoder::getG (src/Encoder.cpp:61, src/Decoder.cpp:68): k*n bytes row-major. */
+int fec_codec_generator(const fec_codec *codec, uint8_t *G);
+
+/* ---- batched device-resident encode --------------------------------------------------------
+ * Batched FEC_Encoder::onTransmit (src/FEC_Encoder.cpp:42-68) for P consecutive packets of one
+ * stream.  d_payload: P rows of max_payload bytes (row p = packet seq0+p); d_payload_len: P
+ * payload lengths (<= max_payload) or NULL = all max_payload.  `history` rows BEFORE d_payload
+ * (d_payload - history*max_payload, and d_payload_len - history) are earlier packets of the same
+ * stream; packets before those count as zero (encoder created there).  Writes d_codeword (P rows
+ * of CW bytes, untrimmed, zero padded exactly as the decoder re-pads) and d_codeword_len (P
+ * trimmed wire sizes). */
+int fec_encode_batch(fec_codec *codec, const uint8_t *d_payload, const int32_t *d_payload_len,
+                     int64_t history, int64_t P, uint8_t *d_codeword, int32_t *d_codeword_len,
+                     void *hip_stream);
+
+/* ---- batched device-resident decode --------------------------------------------------------
+ * A fresh FEC_Decoder (src/FEC_Decoder.cpp:26-72) fed packets seq 0..P-1 of one stream:
+ * d_codeword: P rows of CW bytes (zero padded; rows of erased packets are never read);
+ * d_erasure: P bytes, 1 = packet missing.  Produces the reference's output for packets
+ * 0..P-T-1: d_payload_out ((P-T) rows of max_payload bytes, zero beyond the payload) and
+ * d_payload_len ((P-T) ints, 0 = lost).  d_workspace: fec_decode_workspace_bytes(P) bytes. */
+size_t fec_decode_workspace_bytes(const fec_codec *codec, int64_t P);
+int fec_decode_batch(fec_codec *codec, const uint8_t *d_codeword, const uint8_t *d_erasure,
+                     int64_t P, uint8_t *d_payload_out, int32_t *d_payload_len, void *d_workspace,
+                     size_t workspace_bytes, void *hip_stream);
+/* After the stream has finished the decode: erasure episodes, recovered and lost packets. */
+int fec_decode_counters(const void *d_workspace, int64_t *episodes, int64_t *recovered,
+                        int64_t *lost);
+
+/* ---- per-kernel timing (HIP events recorded on the launch stream) --------------------------- */
+#define FEC_KERNEL_ENCODE 0
+#define FEC_KERNEL_DEC_SCAN 1
+#define FEC_KERNEL_DEC_PLAN 2
+#define FEC_KERNEL_DEC_COPY 3
+#define FEC_KERNEL_DEC_RECOVER 4
+#define FEC_KERNEL_COUNT 5
+int fec_timing_enable(fec_codec *codec, int enable);
+/* Synchronises the recorded events; total_ms[FEC_KERNEL_COUNT], launches[FEC_KERNEL_COUNT]. */
+int fec_timing_collect(fec_codec *codec, double *total_ms, int64_t *launches);
+
+/* ---- streaming per-packet API (host buffers) -----------------------------------------------
+ * fec_encoder_transmit = FEC_Encoder::onTransmit: data (payload bytes), payload (<= max_payload),
+ * seq (0,1,2,... consecutive); writes the wire codeword (cw_out must hold CW bytes; the trimmed
+ * length goes to *codeword_size, bytes past it are zero).
+ * fec_decoder_receive = FEC_Decoder::onReceive: codeword/codeword_size = wire bytes (ignored when
+ * erasure != 0), seq consecutive from 0; writes packet seq-T's payload to payload_out
+ * (max_payload bytes, zero beyond) and its length to *payload (0 = lost / not yet available). */
+int fec_encoder_create(int max_payload, int T, int B, int N, fec_encoder **out);
+int fec_encoder_destroy(fec_encoder *enc);
+int fec_encoder_transmit(fec_encoder *enc, const uint8_t *data, int payload, int seq,
+                         uint8_t *cw_out, int *codeword_size);
+int fec_decoder_create(int max_payload, int T, int B, int N, fec_decoder **out);
+int fec_decoder_destroy(fec_decoder *dec);
+int fec_decoder_receive(fec_decoder *dec, const uint8_t *codeword, int codeword_size, int seq,
+                        int erasure, uint8_t *payload_out, int *payload);
+
+/* ---- host-side planner probe (control plane only, no device needed) -------------------------
+ * Runs the symbolic decoder over an erasure pattern of P packets and reports, for packets
+ * 0..P-T-1, fate[x] (1 copy, 2 recovered, 3 lost).  Used by tests and by the streaming decoder. */
+int fec_plan_host(int max_payload, int T, int B, int N, const uint8_t *erasure, int64_t P,
+                  uint8_t *fate);
+
+/* ---- utility (tests / bench only, not on the coding path) ---------------------------------
+ * Synthetic payloads: byte b of packet t0+p = low 8 bits of splitmix64(seed ^ ((t0+p)*L + b)). */
+int fec_util_fill_payload(uint8_t *d_out, int64_t t0, int64_t count, int L, uint64_t seed,
+                          void *hip_stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

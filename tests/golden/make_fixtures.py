@@ -1,0 +1,100 @@
+"""Regenerate tests/golden/ from the reference checkout (run in the build container only).
+
+Inputs (all DATA files shipped by domanovi/FEC_Erasure_Code_Unit_Test_Relay, read as bytes):
+  bin/erasure.bin, bin/erasure2.bin, erasure.bin, Experimental_Logs/erasure{10..100}.bin
+      recorded erasure patterns, one byte per packet (1 = erased) -> bit-packed into
+      erasure_patterns.npz;
+  Experimental_Logs/Logs/Fixed/*Receiver*.rtf
+      the published "(T,B,N)=", "Final FEC loss rate" and "Final UDP loss rate" of each fixed-rate
+      run -> published_fixed_logs.json (lost packets = rate * 360000).
+Outputs computed by the oracle restatement (oracle/, pinned by the published logs):
+  oracle_vectors.json: lost-packet lists of the survey's configurations on bin/erasure.bin and
+      SHA-256 digests of encoder outputs for the synthetic payload generator.
+
+Usage:  python tests/golden/make_fixtures.py [/root/reference]
+"""
+from __future__ import annotations
+
+import glob
+import hashlib
+import json
+import os
+import re
+import sys
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.abspath(os.path.join(HERE, "..", ".."))
+sys.path.insert(0, ROOT)
+
+
+def pack_patterns(ref: str) -> None:
+    files = {"bin_erasure": "bin/erasure.bin", "bin_erasure2": "bin/erasure2.bin",
+             "root_erasure": "erasure.bin"}
+    for pct in range(10, 101, 10):
+        files[f"erasure{pct}"] = f"Experimental_Logs/erasure{pct}.bin"
+    arrays = {}
+    for key, rel in files.items():
+        raw = np.fromfile(os.path.join(ref, rel), dtype=np.uint8)
+        assert set(np.unique(raw).tolist()) <= {0, 1}, rel
+        arrays[key] = np.packbits(raw)
+        arrays[key + "_len"] = np.array([raw.size], dtype=np.int64)
+        arrays[key + "_sha256"] = np.frombuffer(hashlib.sha256(raw.tobytes()).digest(), dtype=np.uint8)
+    np.savez_compressed(os.path.join(HERE, "erasure_patterns.npz"), **arrays)
+
+
+def parse_logs(ref: str) -> None:
+    out = []
+    for path in sorted(glob.glob(os.path.join(ref, "Experimental_Logs/Logs/Fixed/*.rtf"))):
+        name = os.path.basename(path)
+        if "Rec" not in name:  # receiver logs only (one has the typo "Recevier")
+            continue
+        txt = open(path, "rb").read().decode("latin-1")
+        tbn = re.findall(r"\(T,B,N\)=\((\d+),(\d+),(\d+)\)", txt)
+        fec = re.findall(r"Final FEC loss rate = ([0-9.e-]+)", txt)
+        udp = re.findall(r"Final UDP loss rate = ([0-9.e-]+)", txt)
+        if not (tbn and fec and udp):
+            continue
+        pct = int(name.split("-")[0])
+        raw = np.fromfile(os.path.join(ref, f"Experimental_Logs/erasure{pct}.bin"), dtype=np.uint8)
+        udp_lost = int(round(float(udp[-1]) * 360000))
+        # the decoder's last "(T,B,N)=" line is the configuration the run ended with
+        out.append({"log": f"Experimental_Logs/Logs/Fixed/{name}", "pattern": f"erasure{pct}",
+                    "T": int(tbn[-1][0]), "B": int(tbn[-1][1]), "N": int(tbn[-1][2]),
+                    "usable": udp_lost == int(raw[:360000].sum()),
+                    "fec_loss_rate": float(fec[-1]), "udp_loss_rate": float(udp[-1]),
+                    "lost_packets": int(round(float(fec[-1]) * 360000)),
+                    "udp_lost_packets": udp_lost})
+    with open(os.path.join(HERE, "published_fixed_logs.json"), "w") as f:
+        json.dump({"packets": 360000, "note": "lost = Final FEC loss rate x 360000; a log is "
+                   "usable when its UDP loss equals the shipped pattern's erasure count",
+                   "runs": out}, f, indent=1)
+
+
+def oracle_vectors() -> None:
+    import oracle
+    pats = np.load(os.path.join(HERE, "erasure_patterns.npz"))
+    pat = np.unpackbits(pats["bin_erasure"])[: int(pats["bin_erasure_len"][0])]
+    vec = {"payload_seed": 0x5EED, "max_payload": 300, "lost": {}, "encode": {}}
+    for tbn in [(10, 5, 2), (10, 3, 3)]:
+        r = oracle.run_stream(300, *tbn, 360000, pat[:360000], loss_only=True)
+        vec["lost"]["%d,%d,%d" % tbn] = np.flatnonzero(r["out_len"] == 0).tolist()
+    for tbn, P in [((10, 3, 3), 20000), ((10, 5, 2), 20000), ((10, 10, 10), 4000), ((10, 9, 9), 4000)]:
+        e = oracle.encode_stream(300, *tbn, 0, P, seed=0x5EED)
+        vec["encode"]["%d,%d,%d" % tbn] = {
+            "packets": P,
+            "codeword_sha256": hashlib.sha256(e["cw"].tobytes()).hexdigest(),
+            "wire_len_sha256": hashlib.sha256(e["cw_len"].astype("<i4").tobytes()).hexdigest(),
+            "first_codeword": e["cw"][0].tolist(),
+        }
+    with open(os.path.join(HERE, "oracle_vectors.json"), "w") as f:
+        json.dump(vec, f)
+
+
+if __name__ == "__main__":
+    ref = sys.argv[1] if len(sys.argv) > 1 else "/root/reference"
+    pack_patterns(ref)
+    parse_logs(ref)
+    oracle_vectors()
+    print("fixtures written to", HERE)

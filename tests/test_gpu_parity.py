@@ -1,0 +1,192 @@
+"""Parity of the HIP path (through the C ABI) against the oracle.  Needs an MI355X: -m gpu.
+
+Bit-exact comparisons at sizes the oracle finishes in seconds, plus size-independent properties
+at BASELINE.json's full size (1M packets): encode -> erase -> decode round trip, lost set equal to
+the (oracle-validated) symbolic planner's, payload lengths.
+"""
+import hashlib
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+import oracle
+from conftest import ROOT, load_pattern
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+import fec_erasure_code_unit_test_relay_amd as fec  # noqa: E402
+
+L = 300
+SEED = 0x5EED
+
+
+@pytest.fixture(scope="module", autouse=True)
+def device():
+    assert torch.cuda.is_available(), "no HIP device"
+    torch.cuda.set_device(0)
+    yield
+
+
+def test_fill_payload_matches_oracle_generator():
+    g = fec.fill_payload(100, 50, L, SEED).cpu().numpy()
+    assert (g == oracle.fill_payload(100, 50, L, SEED)).all()
+
+
+ENC_CONFIGS = [(10, 3, 3), (10, 5, 2), (10, 1, 1), (10, 0, 0), (10, 2, 2), (10, 5, 5),
+               (10, 7, 7), (10, 9, 9), (10, 10, 10), (10, 8, 4), (10, 5, 4), (10, 9, 8), (10, 4, 1),
+               (4, 6, 2), (12, 4, 2)]
+
+
+@pytest.mark.parametrize("tbn", ENC_CONFIGS)
+def test_encode_bit_exact(tbn):
+    T, B, N = tbn
+    P = 2500
+    c = fec.Codec(L, T, B, N)
+    payload = fec.fill_payload(0, P, L, SEED)
+    cw, wl = c.encode(payload)
+    ref = oracle.encode_stream(L, T, B, N, 0, P, seed=SEED)
+    assert (cw.cpu().numpy() == ref["cw"]).all()
+    assert (wl.cpu().numpy() == ref["cw_len"]).all()
+    assert (c.generator() == oracle.gen_G(T, B, N)).all()
+
+
+def test_encode_digest_fixture(oracle_vectors):
+    for key, v in oracle_vectors["encode"].items():
+        T, B, N = map(int, key.split(","))
+        c = fec.Codec(L, T, B, N)
+        cw, wl = c.encode(fec.fill_payload(0, v["packets"], L, SEED))
+        assert hashlib.sha256(cw.cpu().numpy().tobytes()).hexdigest() == v["codeword_sha256"]
+        assert hashlib.sha256(wl.cpu().numpy().astype("<i4").tobytes()).hexdigest() == v["wire_len_sha256"]
+
+
+@pytest.mark.parametrize("tbn", [(10, 3, 3), (10, 5, 2), (10, 10, 10), (10, 9, 9)])
+def test_encode_variable_lengths_and_history(tbn):
+    T, B, N = tbn
+    P = 700
+    rng = np.random.default_rng(3)
+    lens = rng.integers(0, L + 1, size=P).astype(np.int32)
+    lens[::7] = 0
+    lens[1::11] = 1
+    payload = fec.fill_payload(0, P, L, 9)
+    enc = oracle.Encoder(L, T, B, N)
+    host = payload.cpu().numpy()
+    ref = np.stack([enc.onTransmit(host[t], int(lens[t]), t)[0] for t in range(P)])
+    c = fec.Codec(L, T, B, N)
+    dl = torch.from_numpy(lens).cuda()
+    cw, _ = c.encode(payload, dl)
+    assert (cw.cpu().numpy() == ref).all()
+    # the same stream in two batches: the second sees 37 packets of history
+    h, cut = 37, 400
+    cw1, _ = c.encode(payload[:cut], dl[:cut])
+    cw2, _ = c.encode(payload[cut - h:], dl[cut - h:], history=h)
+    assert (torch.cat([cw1, cw2]).cpu().numpy() == ref).all()
+
+
+def gpu_round_trip(T, B, N, pattern, P, garbage=True):
+    """GPU encode of packets 0..P+T-1, erase, GPU decode -> outputs for packets 0..P-1."""
+    c = fec.Codec(L, T, B, N)
+    Pf = P + T
+    pat = np.zeros(Pf, dtype=np.uint8)
+    m = min(pattern.size, Pf)
+    pat[:m] = pattern[:m]
+    payload = fec.fill_payload(0, Pf, L, SEED)
+    cw, _ = c.encode(payload)
+    er = torch.from_numpy(pat).cuda()
+    if garbage:  # the decoder must never read an erased packet's bytes
+        idx = torch.nonzero(er).flatten()
+        if idx.numel():
+            cw[idx] = torch.randint(0, 256, (idx.numel(), c.CW), dtype=torch.uint8, device="cuda")
+    out, ln = c.decode(cw, er)
+    torch.cuda.synchronize()
+    return c, payload, out, ln, pat
+
+
+DEC_CASES = [((10, 5, 2), "bin_erasure", 0, 8000), ((10, 3, 3), "bin_erasure", 0, 8000),
+             ((10, 9, 8), "erasure100", 0, 4000), ((10, 1, 1), "erasure10", 50000, 6000),
+             ((10, 4, 3), "erasure80", 10000, 6000), ((10, 10, 10), "erasure90", 0, 3000),
+             ((10, 0, 0), "erasure70", 0, 5000), ((10, 8, 4), "erasure60", 0, 5000),
+             ((12, 4, 2), "erasure100", 1000, 3000), ((4, 6, 2), "erasure100", 0, 3000)]
+
+
+@pytest.mark.parametrize("tbn,pattern,start,P", DEC_CASES)
+def test_decode_bit_exact_vs_oracle(tbn, pattern, start, P):
+    T, B, N = tbn
+    pat = load_pattern(pattern)[start:start + P + T]
+    ref = oracle.run_stream(L, T, B, N, P, pat, seed=SEED, want_data=True)
+    c, payload, out, ln, _ = gpu_round_trip(T, B, N, pat, P)
+    assert (ln.cpu().numpy() == ref["out_len"]).all()
+    assert (out.cpu().numpy() == ref["out_data"]).all()
+    eps, rec, lost = c.counters()
+    assert lost == int((ref["out_len"] == 0).sum())  # every lost packet is an erased one
+    assert rec + lost == int(pat[:P].sum())
+
+
+def test_decode_startup_and_dense_erasures():
+    P = 600
+    pat = np.zeros(P + 10, dtype=np.uint8)
+    pat[[0, 1, 3, 4, 5, 12, 13]] = 1
+    pat[30:37] = 1
+    pat[100:140:2] = 1
+    pat[300:330] = 1
+    for tbn in [(10, 3, 3), (10, 5, 2), (10, 10, 10), (10, 2, 2)]:
+        ref = oracle.run_stream(L, *tbn, P, pat, seed=SEED, want_data=True)
+        _, _, out, ln, _ = gpu_round_trip(*tbn, pat, P)
+        assert (ln.cpu().numpy() == ref["out_len"]).all()
+        assert (out.cpu().numpy() == ref["out_data"]).all()
+
+
+def test_full_size_round_trip_1M():
+    """BASELINE config 2/3 size: 1M packets at (10,3,3) with bin/erasure.bin tiled."""
+    T, B, N = 10, 3, 3
+    P = 1_000_000
+    base = load_pattern("bin_erasure")[:360000]
+    pat = np.resize(base, P + T).astype(np.uint8)
+    c, payload, out, ln, _ = gpu_round_trip(T, B, N, pat, P, garbage=False)
+    fate = fec.plan_host(L, T, B, N, pat)
+    lost = fate == 3
+    lnh = ln.cpu().numpy()
+    assert ((lnh == 0) == lost).all()
+    assert (lnh[~lost] == L).all()
+    ok = torch.from_numpy(~lost).cuda()
+    assert torch.equal(out[ok], payload[:P][ok])
+    assert int(out[~ok].count_nonzero()) == 0
+    eps, rec, nlost = c.counters()
+    assert nlost == int(lost.sum()) and rec == int((fate == 2).sum())
+
+
+def test_streaming_api_matches_oracle():
+    T, B, N = 10, 5, 2
+    P = 500
+    pat = load_pattern("bin_erasure")[2600:2600 + P + T].copy()
+    pat[[3, 4, 200, 201, 202, 203]] = 1
+    enc, dec = fec.FEC_Encoder(L, T, B, N), fec.FEC_Decoder(L, T, B, N)
+    oe, od = oracle.Encoder(L, T, B, N), oracle.Decoder(L, T, B, N)
+    src = oracle.fill_payload(0, P + T, L, SEED)
+    lens = np.full(P + T, L)
+    lens[50:60] = [0, 1, 2, 7, 100, 299, 300, 5, 33, 250]
+    for t in range(P + T):
+        wire, size = enc.onTransmit(src[t], int(lens[t]), t)
+        ocw, osize = oe.onTransmit(src[t], int(lens[t]), t)
+        assert size == osize and (wire == ocw[:size]).all()
+        erased = bool(pat[t])
+        got, p = dec.onReceive(None if erased else wire, size, t, erased)
+        ogot, op = od.onReceive(None if erased else ocw, osize, t, erased)
+        assert p == op and (got == ogot).all(), t
+
+
+def test_cpp_dropin_program(tmp_path):
+    """The reference-named C++ classes (include/fec_amd_dropin.h) in a host program."""
+    src = os.path.join(ROOT, "tests", "cpp", "dropin_test.cpp")
+    exe = str(tmp_path / "dropin_test")
+    libdir = os.path.dirname(fec.LIB_PATH)
+    orc = os.path.join(ROOT, "oracle", "fec_oracle.c")
+    subprocess.run(["gcc", "-O2", "-c", orc, "-o", str(tmp_path / "oracle.o")], check=True)
+    subprocess.run(["g++", "-O2", "-std=c++17", src, str(tmp_path / "oracle.o"), "-I",
+                    os.path.join(ROOT, "include"), "-L", libdir, "-lfec_amd",
+                    f"-Wl,-rpath,{libdir}", "-o", exe], check=True)
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "DROPIN OK" in r.stdout
