@@ -154,14 +154,14 @@ class Decoder:
             self._h = None
 
     def onReceive(self, codeword, size: int, seq: int, erasure: bool):
-        """Returns (payload length of packet seq-T, max_payload bytes zero-filled past it)."""
+        """Returns (max_payload bytes of packet seq-T zero-filled past the payload, payload length)."""
         out = np.zeros(self.L, dtype=np.uint8)
         if erasure or codeword is None:
             p = lib().or_decoder_receive(self._h, None, 0, seq, 1, _u8(out))
         else:
             c = np.ascontiguousarray(codeword, dtype=np.uint8)
             p = lib().or_decoder_receive(self._h, _u8(c), size, seq, 0, _u8(out))
-        return p, out
+        return out, p
 
 
 def run_stream(max_payload: int, T: int, B: int, N: int, P: int, pattern: np.ndarray,
