@@ -94,9 +94,19 @@ def main():
     ol = torch.empty(P, dtype=torch.int32, device="cuda")
     codec.workspace(Pf)
 
+    side = torch.cuda.Stream()
+
     def step():
+        # the decode plan needs only the erasure pattern: it runs on a side stream while the
+        # encoder runs on the main stream; joined before the byte half of the decode
+        fork = torch.cuda.Event()
+        fork.record()
+        with torch.cuda.stream(side):
+            side.wait_event(fork)
+            codec.plan(er)
         codec.encode(payload, out=cw, out_len=wl)
-        codec.decode(cw, er, out=out, out_len=ol)
+        torch.cuda.current_stream().wait_stream(side)
+        codec.apply(cw, er, out=out, out_len=ol)  # systematic copy + recovery
 
     def barrier():
         if world > 1:

@@ -58,6 +58,11 @@ class Codec:
         check(lib().fec_codec_generator(self._h, G.ctypes.data_as(ctypes.c_void_p)), "generator")
         return G.reshape(self.k, self.n)
 
+    def set_encode_path(self, path: str) -> None:
+        """'auto', 'generic' or 'fast' (the k, n-k specialised kernel)."""
+        code = {"auto": 0, "generic": 1, "fast": 2}[path]
+        check(lib().fec_codec_set_encode_path(self._h, code), "fec_codec_set_encode_path")
+
     # -- batched device-resident path -----------------------------------------------------------
     def encode(self, payload, lengths=None, history: int = 0, out=None, out_len=None):
         """Encode rows ``history..`` of ``payload`` ([rows, L] uint8 on the GPU).
@@ -104,6 +109,31 @@ class Codec:
         check(lib().fec_decode_batch(self._h, _ptr(codewords), _ptr(erasure), P, _ptr(out),
                                      _ptr(out_len), _ptr(ws), ws.numel(), _stream_handle(torch)),
               "fec_decode_batch")
+        return out, out_len
+
+    def plan(self, erasure, P: int | None = None):
+        """Erasure-only half of the decode (scan + per-episode replay) on the current stream."""
+        import torch
+        assert erasure.dtype == torch.uint8 and erasure.is_cuda
+        P = erasure.numel() if P is None else P
+        ws = self.workspace(P)
+        check(lib().fec_decode_plan(self._h, _ptr(erasure), P, _ptr(ws), ws.numel(),
+                                    _stream_handle(torch)), "fec_decode_plan")
+
+    def apply(self, codewords, erasure, out=None, out_len=None):
+        """Byte half of the decode (systematic copy + recovery); ordered after plan()."""
+        import torch
+        P = codewords.shape[0]
+        assert codewords.shape[1] == self.CW and codewords.is_contiguous()
+        Pout = max(0, P - self.T)
+        if out is None:
+            out = torch.empty((Pout, self.L), dtype=torch.uint8, device=codewords.device)
+        if out_len is None:
+            out_len = torch.empty(Pout, dtype=torch.int32, device=codewords.device)
+        ws = self.workspace(P)
+        check(lib().fec_decode_apply(self._h, _ptr(codewords), _ptr(erasure), P, _ptr(out),
+                                     _ptr(out_len), _ptr(ws), ws.numel(), _stream_handle(torch)),
+              "fec_decode_apply")
         return out, out_len
 
     def counters(self):

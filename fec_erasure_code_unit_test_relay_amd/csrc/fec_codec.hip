@@ -40,12 +40,20 @@ struct fec_codec {
     uint8_t* d_rules = nullptr;
     int64_t* d_wbase = nullptr;  // [n+1]
     uint8_t* d_gf = nullptr;     // exp[512], log[256]
-    int enc_tp = 0;              // encode tile (packets per workgroup)
+    int enc_tp = 0;              // encode tile (packets per workgroup), generic kernel
+    int fast_tp = 0;             // encode tile of the specialised kernel (0: not available)
+    const void* fast_kernel = nullptr;
+    int encode_path = 0;         // 0 auto, 1 generic, 2 specialised
     int copy_tp = 0;             // decode-copy tile
     bool timing = false;
     std::vector<EventPair> events;
+    hipStream_t side = nullptr;  // decode plan runs here, forked from the caller's stream
+    hipEvent_t ev_fork = nullptr, ev_join = nullptr;
 
     ~fec_codec() {
+        if (ev_fork) (void)hipEventDestroy(ev_fork);
+        if (ev_join) (void)hipEventDestroy(ev_join);
+        if (side) (void)hipStreamDestroy(side);
         for (auto& e : events) {
             (void)hipEventDestroy(e.a);
             (void)hipEventDestroy(e.b);
@@ -63,6 +71,10 @@ struct fec_codec {
         return round16(g.k * rows * SP) + round16(tp * g.CW) + 2 * ((Sk + 7) & ~7) + 4 * rows;
     }
     int copy_lds(int tp) const { return round16(tp * g.CW) + 2 * ((g.L + 2 + 7) & ~7) + 4 * tp; }
+    int ns4() const { return (g.S + 3) / 4; }
+    int fast_raw(int tp) const { return round16(std::max((tp + g.n - 1) * g.L + 32, tp * g.CW)); }
+    int fast_xin(int tp) const { return g.k * ns4() * (tp + g.n - 1) * 4; }
+    int fast_lds(int tp) const { return fast_raw(tp) + fast_xin(tp) + 4 * (tp + g.n - 1); }
 
     int begin(int kernel, hipStream_t s, hipEvent_t* stop) {
         *stop = nullptr;
@@ -135,11 +147,22 @@ int codec_init(fec_codec* c, int max_payload, int T, int B, int N) {
             break;
         }
     if (!c->enc_tp || !c->copy_tp) return FEC_ERR_ARG;
+    if ((g.L & 3) == 0) c->fast_kernel = fec::fec_encode_fast_kernel_for(g.k, g.n - g.k);
+    if (c->fast_kernel)
+        for (int tp = 64; tp >= 8; tp >>= 1)
+            if (c->fast_lds(tp) <= kLdsBudget) {
+                c->fast_tp = tp;
+                break;
+            }
+    if (!c->fast_tp) c->fast_kernel = nullptr;
+    HIP_TRY(hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking));
+    HIP_TRY(hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming));
+    HIP_TRY(hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming));
     return FEC_OK;
 }
 
 struct WsLayout {
-    size_t counters, episodes, rec_list, coef, total;
+    size_t counters, episodes, okcnt, rec_list, coef, total;
 };
 
 WsLayout ws_layout(const Geometry& g, int64_t P) {
@@ -147,16 +170,66 @@ WsLayout ws_layout(const Geometry& g, int64_t P) {
     WsLayout w;
     w.counters = 0;
     w.episodes = up(64);
-    w.rec_list = w.episodes + up(static_cast<size_t>(P) * 4);
+    w.okcnt = w.episodes + up(static_cast<size_t>(P) * 4);
+    w.rec_list = w.okcnt + up(static_cast<size_t>(P) * 4);
     w.coef = w.rec_list + up(static_cast<size_t>(P) * 4);
     w.total = w.coef + up(static_cast<size_t>(P) * g.k * g.n);
     return w;
+}
+
+struct Ws {
+    int32_t* counters;
+    int32_t* episodes;
+    int32_t* okcnt;
+    int32_t* rec_list;
+    uint8_t* coef;
+};
+
+Ws ws_carve(const Geometry& g, int64_t P, void* d_ws) {
+    const WsLayout w = ws_layout(g, P);
+    uint8_t* base = static_cast<uint8_t*>(d_ws);
+    return {reinterpret_cast<int32_t*>(base + w.counters), reinterpret_cast<int32_t*>(base + w.episodes),
+            reinterpret_cast<int32_t*>(base + w.okcnt), reinterpret_cast<int32_t*>(base + w.rec_list),
+            base + w.coef};
+}
+
+int launch_encode_fast(fec_codec* c, const uint8_t* d_payload, const int32_t* d_len, int64_t history,
+                       int64_t P, uint8_t* d_cw, int32_t* d_cwlen, hipStream_t s) {
+    const Geometry& g = c->g;
+    fec::EncFastArgs a;
+    a.payload = d_payload;
+    a.len = d_len;
+    a.history = std::max<int64_t>(0, history);
+    a.P = P;
+    a.cw = d_cw;
+    a.cw_len = d_cwlen;
+    a.ptab = c->d_ptab;
+    a.L = g.L;
+    a.S = g.S;
+    a.CW = g.CW;
+    a.NS4 = c->ns4();
+    a.TP = c->fast_tp;
+    a.ROWS = a.TP + g.n - 1;
+    a.raw_bytes = c->fast_raw(a.TP);
+    a.xin_bytes = c->fast_xin(a.TP);
+    const int64_t blocks = (P + a.TP - 1) / a.TP;
+    if (blocks > 0x7fffffff) return FEC_ERR_ARG;
+    hipEvent_t stop;
+    if (int st = c->begin(FEC_KERNEL_ENCODE, s, &stop)) return st;
+    void* args[] = {&a};
+    HIP_TRY(hipLaunchKernel(c->fast_kernel, dim3(static_cast<unsigned>(blocks)), dim3(256), args,
+                            c->fast_lds(a.TP), s));
+    return c->end(stop, s);
 }
 
 int launch_encode(fec_codec* c, const uint8_t* d_payload, const int32_t* d_len, int64_t history,
                   int64_t P, uint8_t* d_cw, int32_t* d_cwlen, hipStream_t s) {
     if (P <= 0) return FEC_OK;
     const Geometry& g = c->g;
+    const bool fast_ok = c->fast_kernel && (reinterpret_cast<uintptr_t>(d_payload) & 3) == 0;
+    if (c->encode_path == 2 && !fast_ok) return FEC_ERR_ARG;
+    if (fast_ok && c->encode_path != 1)
+        return launch_encode_fast(c, d_payload, d_len, history, P, d_cw, d_cwlen, s);
     fec::EncArgs a;
     a.payload = d_payload;
     a.len = d_len;
@@ -186,53 +259,58 @@ int launch_encode(fec_codec* c, const uint8_t* d_payload, const int32_t* d_len, 
     return c->end(stop, s);
 }
 
-int launch_decode(fec_codec* c, const uint8_t* d_cw, const uint8_t* d_er, int64_t P, uint8_t* d_out,
-                  int32_t* d_outlen, void* d_ws, size_t ws_bytes, hipStream_t s) {
+int check_ws(fec_codec* c, int64_t P, void* d_ws, size_t ws_bytes) {
+    if (P > 0x7fffffffLL) return FEC_ERR_ARG;
+    if (!d_ws || ws_bytes < ws_layout(c->g, P).total) return FEC_ERR_WORKSPACE;
+    return FEC_OK;
+}
+
+// Erasure-pattern-only half of the decode: resync points + per-(episode, diagonal) replay.
+int launch_plan(fec_codec* c, const uint8_t* d_er, int64_t P, void* d_ws, size_t ws_bytes,
+                hipStream_t s) {
     const Geometry& g = c->g;
     const int64_t Pout = P - g.T;
     if (Pout <= 0) return FEC_OK;
-    if (P > 0x7fffffffLL) return FEC_ERR_ARG;
-    const WsLayout w = ws_layout(g, P);
-    if (!d_ws || ws_bytes < w.total) return FEC_ERR_WORKSPACE;
-    uint8_t* ws = static_cast<uint8_t*>(d_ws);
-    int32_t* counters = reinterpret_cast<int32_t*>(ws + w.counters);
-    int32_t* episodes = reinterpret_cast<int32_t*>(ws + w.episodes);
-    int32_t* rec_list = reinterpret_cast<int32_t*>(ws + w.rec_list);
-    uint8_t* coef = ws + w.coef;
-    HIP_TRY(hipMemsetAsync(counters, 0, 64, s));
+    if (int st = check_ws(c, P, d_ws, ws_bytes)) return st;
+    const Ws w = ws_carve(g, P, d_ws);
+    HIP_TRY(hipMemsetAsync(w.counters, 0, 64, s));
     hipEvent_t stop;
-
-    // 1. resync points
     if (int st = c->begin(FEC_KERNEL_DEC_SCAN, s, &stop)) return st;
-    const int64_t sblocks = std::min<int64_t>((P + 255) / 256, 4096);
+    const int64_t sblocks = std::min<int64_t>((P + 1023) / 1024, 4096);
     hipLaunchKernelGGL(fec::fec_scan_kernel, dim3(static_cast<unsigned>(sblocks)), dim3(256), 0, s,
-                       d_er, P, g.T, counters, episodes);
+                       d_er, P, Pout, g.T, w.counters, w.episodes, w.okcnt);
     HIP_TRY(hipGetLastError());
     if (int st = c->end(stop, s)) return st;
 
-    // 2. symbolic replay per episode (one wavefront each)
     fec::PlanArgs pa;
     pa.er = d_er;
     pa.P = P;
     pa.Pout = Pout;
     pa.rules = c->d_rules;
-    pa.wbase = c->d_wbase;
+    for (int i = 0; i <= fec::kPlanMaxN; ++i)
+        pa.wbase[i] = (i < static_cast<int>(c->rules.w_base.size())) ? c->rules.w_base[i] : -1;
     pa.gf = c->d_gf;
     pa.ES = c->rules.entry_bytes;
     pa.k = g.k;
     pa.n = g.n;
     pa.T = g.T;
-    pa.counters = counters;
-    pa.episodes = episodes;
-    pa.rec_list = rec_list;
-    pa.coef = coef;
-    const int plan_lds = 768 + 128 + g.n * g.n * g.n + 2 * g.n * g.k * g.n;
+    pa.counters = w.counters;
+    pa.episodes = w.episodes;
+    pa.okcnt = w.okcnt;
+    pa.rec_list = w.rec_list;
+    pa.coef = w.coef;
+    const int plan_lds = 768 + g.n * g.n + 2 * g.k * g.n;
     if (int st = c->begin(FEC_KERNEL_DEC_PLAN, s, &stop)) return st;
-    hipLaunchKernelGGL(fec::fec_plan_kernel, dim3(4096), dim3(64), plan_lds, s, pa);
+    hipLaunchKernelGGL(fec::fec_plan_kernel, dim3(8192), dim3(64), plan_lds, s, pa);
     HIP_TRY(hipGetLastError());
-    if (int st = c->end(stop, s)) return st;
+    return c->end(stop, s);
+}
 
-    // 3. received packets
+int launch_copy(fec_codec* c, const uint8_t* d_cw, const uint8_t* d_er, int64_t P, uint8_t* d_out,
+                int32_t* d_outlen, hipStream_t s) {
+    const Geometry& g = c->g;
+    const int64_t Pout = P - g.T;
+    if (Pout <= 0) return FEC_OK;
     fec::CopyArgs ca;
     ca.cw = d_cw;
     ca.er = d_er;
@@ -249,19 +327,28 @@ int launch_decode(fec_codec* c, const uint8_t* d_cw, const uint8_t* d_er, int64_
     ca.TP = c->copy_tp;
     ca.cwt_bytes = round16(ca.TP * g.CW);
     const int64_t cblocks = (Pout + ca.TP - 1) / ca.TP;
+    hipEvent_t stop;
     if (int st = c->begin(FEC_KERNEL_DEC_COPY, s, &stop)) return st;
     hipLaunchKernelGGL(fec::fec_copy_kernel, dim3(static_cast<unsigned>(cblocks)), dim3(256),
                        c->copy_lds(ca.TP), s, ca);
     HIP_TRY(hipGetLastError());
-    if (int st = c->end(stop, s)) return st;
+    return c->end(stop, s);
+}
 
-    // 4. recovered packets
+int launch_recover(fec_codec* c, const uint8_t* d_cw, int64_t P, uint8_t* d_out, int32_t* d_outlen,
+                   void* d_ws, size_t ws_bytes, hipStream_t s) {
+    const Geometry& g = c->g;
+    const int64_t Pout = P - g.T;
+    if (Pout <= 0) return FEC_OK;
+    if (int st = check_ws(c, P, d_ws, ws_bytes)) return st;
+    const Ws w = ws_carve(g, P, d_ws);
     fec::RecArgs ra;
     ra.cw = d_cw;
     ra.P = P;
-    ra.counters = counters;
-    ra.rec_list = rec_list;
-    ra.coef = coef;
+    ra.Pout = Pout;
+    ra.counters = w.counters;
+    ra.rec_list = w.rec_list;
+    ra.coef = w.coef;
     ra.gf = c->d_gf;
     ra.out = d_out;
     ra.out_len = d_outlen;
@@ -270,10 +357,29 @@ int launch_decode(fec_codec* c, const uint8_t* d_cw, const uint8_t* d_er, int64_
     ra.n = g.n;
     ra.S = g.S;
     ra.CW = g.CW;
+    hipEvent_t stop;
     if (int st = c->begin(FEC_KERNEL_DEC_RECOVER, s, &stop)) return st;
-    hipLaunchKernelGGL(fec::fec_recover_kernel, dim3(2048), dim3(256), 0, s, ra);
+    int rec_lds = 2816 + (g.k + g.n - 1) * g.CW;
+    ra.stage = rec_lds <= kLdsBudget ? 1 : 0;
+    if (!ra.stage) rec_lds = 2816;
+    hipLaunchKernelGGL(fec::fec_recover_kernel, dim3(2048), dim3(256), rec_lds, s, ra);
     HIP_TRY(hipGetLastError());
     return c->end(stop, s);
+}
+
+// Full decode on `s`: the erasure-only plan runs on the codec's side stream concurrently with the
+// systematic copy, joined before the recovery pass (fork/join through events, capturable).
+int launch_decode(fec_codec* c, const uint8_t* d_cw, const uint8_t* d_er, int64_t P, uint8_t* d_out,
+                  int32_t* d_outlen, void* d_ws, size_t ws_bytes, hipStream_t s) {
+    if (P - c->g.T <= 0) return FEC_OK;
+    if (int st = check_ws(c, P, d_ws, ws_bytes)) return st;
+    HIP_TRY(hipEventRecord(c->ev_fork, s));
+    HIP_TRY(hipStreamWaitEvent(c->side, c->ev_fork, 0));
+    if (int st = launch_plan(c, d_er, P, d_ws, ws_bytes, c->side)) return st;
+    HIP_TRY(hipEventRecord(c->ev_join, c->side));
+    if (int st = launch_copy(c, d_cw, d_er, P, d_out, d_outlen, s)) return st;
+    HIP_TRY(hipStreamWaitEvent(s, c->ev_join, 0));
+    return launch_recover(c, d_cw, P, d_out, d_outlen, d_ws, ws_bytes, s);
 }
 
 template <class F>
@@ -399,14 +505,37 @@ int fec_decode_batch(fec_codec* c, const uint8_t* d_cw, const uint8_t* d_er, int
                          static_cast<hipStream_t>(stream));
 }
 
+int fec_decode_plan(fec_codec* c, const uint8_t* d_er, int64_t P, void* d_ws, size_t ws_bytes,
+                    void* stream) {
+    if (!c || P < 0 || (P > c->g.T && !d_er)) return FEC_ERR_ARG;
+    return launch_plan(c, d_er, P, d_ws, ws_bytes, static_cast<hipStream_t>(stream));
+}
+
+int fec_decode_apply(fec_codec* c, const uint8_t* d_cw, const uint8_t* d_er, int64_t P,
+                     uint8_t* d_out, int32_t* d_outlen, void* d_ws, size_t ws_bytes, void* stream) {
+    if (!c || P < 0) return FEC_ERR_ARG;
+    if (P > c->g.T && (!d_cw || !d_er || !d_out || !d_outlen)) return FEC_ERR_ARG;
+    if (int st = check_ws(c, P, d_ws, ws_bytes)) return P > c->g.T ? st : FEC_OK;
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    if (int st = launch_copy(c, d_cw, d_er, P, d_out, d_outlen, s)) return st;
+    return launch_recover(c, d_cw, P, d_out, d_outlen, d_ws, ws_bytes, s);
+}
+
 int fec_decode_counters(const void* d_ws, int64_t* episodes, int64_t* recovered, int64_t* lost) {
     if (!d_ws) return FEC_ERR_ARG;
     int32_t h[4];
     HIP_TRY(hipDeviceSynchronize());
     HIP_TRY(hipMemcpy(h, d_ws, sizeof(h), hipMemcpyDeviceToHost));
     if (episodes) *episodes = h[0];
-    if (recovered) *recovered = h[1];
-    if (lost) *lost = h[2];
+    if (recovered) *recovered = h[2];
+    if (lost) *lost = h[1] - h[2];  // erased outputs that were not recovered
+    return FEC_OK;
+}
+
+int fec_codec_set_encode_path(fec_codec* c, int path) {
+    if (!c || path < 0 || path > 2) return FEC_ERR_ARG;
+    if (path == 2 && !c->fast_kernel) return FEC_ERR_ARG;
+    c->encode_path = path;
     return FEC_OK;
 }
 

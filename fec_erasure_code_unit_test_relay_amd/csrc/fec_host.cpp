@@ -127,7 +127,7 @@ void DecodeRules::build(const std::vector<uint8_t>& G, int k_, int n_, int T_) {
     T = T_;
     if (n > kMaxRuleN) throw std::invalid_argument("decode rules need n <= 17");
     w_lo = std::min(T + 1, n);
-    entry_bytes = k * (1 + n);
+    entry_bytes = (k * (1 + n) + 3) & ~3;  // padded: the GPU loads an entry as dwords
     w_base.assign(n + 1, -1);
     int64_t total = 0;
     for (int w = w_lo; w <= n; ++w) {

@@ -89,7 +89,7 @@ std::vector<uint8_t> make_generator(int T, int B, int N);
 struct DecodeRules {
     int k = 0, n = 0, T = 0;
     int w_lo = 0;                      // smallest window that occurs: min(T+1, n)
-    int entry_bytes = 0;               // k * (1 + n)
+    int entry_bytes = 0;               // k * (1 + n) rounded up to a multiple of 4
     std::vector<int64_t> w_base;       // byte offset of window w's table (index w)
     std::vector<uint8_t> table;
     void build(const std::vector<uint8_t>& G, int k, int n, int T);

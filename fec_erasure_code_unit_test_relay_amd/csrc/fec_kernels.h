@@ -7,10 +7,11 @@
 //                          src/codingOperations.cpp:131-147);
 //   fec_scan_kernel        finds the packets where the reference decoder leaves its fast path
 //                          and resynchronises (src/Decoder.cpp:80-83, 109-133);
-//   fec_plan_kernel        one wavefront per erasure episode: symbolic replay of the reference's
-//                          per-symbol decode (decodeBlock / gf256_rref_matrix through the
-//                          precomputed decode rules), emitting per recovered packet k x n GF
-//                          coefficients over received codeword bytes;
+//   fec_plan_kernel        one wavefront per (erasure episode, diagonal block): symbolic replay of
+//                          the reference's per-symbol decode (decodeBlock / gf256_rref_matrix
+//                          through the precomputed decode rules), emitting for every erased
+//                          symbol whether it is recovered and its n GF coefficients over the
+//                          received symbols of its diagonal codeword;
 //   fec_copy_kernel        systematic gather + length parse for every received packet (the
 //                          decoder's fast path, src/Decoder.cpp:77-108, and the slow path's
 //                          received packets);
@@ -39,6 +40,24 @@ struct EncArgs {
     int xin_bytes, xout_bytes;  // 16-aligned LDS carve sizes
 };
 
+struct EncFastArgs {
+    const uint8_t* payload;     // row 0 = first packet of the batch (4-byte aligned, L % 4 == 0)
+    const int32_t* len;         // may be null (all L)
+    int64_t history;
+    int64_t P;
+    uint8_t* cw;
+    int32_t* cw_len;
+    const uint32_t* ptab;
+    int L, S, CW;
+    int NS4;                    // groups of 4 sub-streams
+    int TP, ROWS;               // packets per tile, TP + n - 1
+    int raw_bytes;              // LDS union of payload rows / output tile (16-aligned)
+    int xin_bytes;              // LDS position planes
+};
+
+// fec_encode_fast_kernel<k, n-k> for the instantiated pairs (fec_encode_fast.hip), else nullptr.
+const void* fec_encode_fast_kernel_for(int k, int np);
+
 struct CopyArgs {
     const uint8_t* cw;
     const uint8_t* er;
@@ -49,30 +68,34 @@ struct CopyArgs {
     int cwt_bytes;              // 16-aligned
 };
 
+constexpr int kPlanMaxN = 18;  // windows w <= n <= 17
+
 struct PlanArgs {
     const uint8_t* er;
     int64_t P, Pout;
     const uint8_t* rules;
-    const int64_t* wbase;
-    const uint8_t* gf;          // exp[512] then log[256]
-    int ES;                     // decode-rule entry bytes = k*(1+n)
+    int64_t wbase[kPlanMaxN + 1];  // byte offset of window w's rule table (-1: unused)
+    const uint8_t* gf;             // exp[512] then log[256]
+    int ES;                        // decode-rule entry stride (bytes, multiple of 4)
     int k, n, T;
-    int32_t* counters;          // [0] episodes, [1] recovered, [2] lost
+    int32_t* counters;             // [0] episodes, [2] recovered packets
     const int32_t* episodes;
-    int32_t* rec_list;
-    uint8_t* coef;              // [recovered][k][n]
+    int32_t* okcnt;                // [P]: recovered symbols of erased packet x (zeroed by scan)
+    int32_t* rec_list;             // recovered packets (appended by the last symbol's wave)
+    uint8_t* coef;                 // [P][k][n]: coefficients of symbol i over its diagonal
 };
 
 struct RecArgs {
     const uint8_t* cw;
-    int64_t P;
-    const int32_t* counters;
+    int64_t P, Pout;
+    const int32_t* counters;       // [2] recovered packets
     const int32_t* rec_list;
     const uint8_t* coef;
     const uint8_t* gf;
     uint8_t* out;
     int32_t* out_len;
     int L, k, n, S, CW;
+    int stage;                     // 1: source rows staged in LDS
 };
 
 struct StreamOutArgs {
@@ -88,8 +111,8 @@ struct StreamOutArgs {
 };
 
 __global__ void fec_encode_kernel(EncArgs a);
-__global__ void fec_scan_kernel(const uint8_t* er, int64_t P, int T, int32_t* counters,
-                                int32_t* episodes);
+__global__ void fec_scan_kernel(const uint8_t* er, int64_t P, int64_t Pout, int T,
+                                int32_t* counters, int32_t* episodes, int32_t* okcnt);
 __global__ void fec_plan_kernel(PlanArgs a);
 __global__ void fec_copy_kernel(CopyArgs a);
 __global__ void fec_recover_kernel(RecArgs a);

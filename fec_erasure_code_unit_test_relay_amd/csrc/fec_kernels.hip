@@ -144,174 +144,293 @@ __global__ __launch_bounds__(256) void fec_encode_kernel(EncArgs a) {
 }
 
 // ------------------------------------------------------------------------------------------
-// Decode, step 1: resynchronisation points.  The reference decoder is in its fast path at a
-// received packet t iff no packet of [t-T, t-1] was erased; at an erased packet it resyncs iff it
-// was in the fast path just before, i.e. no erasure in [t-T-1, t-1] (Decoder.cpp:80-83, 109-133).
-// Every resync starts an independent episode.
+// Decode, step 1: resynchronisation points and the list of erased packets.  The reference
+// decoder is in its fast path at a received packet t iff no packet of [t-T, t-1] was erased; at an
+// erased packet it resyncs iff it was in the fast path just before, i.e. no erasure in
+// [t-T-1, t-1] (Decoder.cpp:80-83, 109-133).  Every resync starts an independent episode.
 // ------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void fec_scan_kernel(const uint8_t* er, int64_t P, int T,
-                                                       int32_t* counters, int32_t* episodes) {
-    const int64_t stride = static_cast<int64_t>(gridDim.x) * blockDim.x;
-    for (int64_t t = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; t < P; t += stride) {
-        if (!er[t]) continue;
-        bool resync = true;
-        for (int d = 1; d <= T + 1 && t - d >= 0; ++d)
-            if (er[t - d]) {
-                resync = false;
-                break;
+__global__ __launch_bounds__(256) void fec_scan_kernel(const uint8_t* er, int64_t P, int64_t Pout,
+                                                       int T, int32_t* counters, int32_t* episodes,
+                                                       int32_t* okcnt) {
+    // 4 packets per lane (one dword of erasure flags); per-wave aggregated counter updates
+    const int64_t stride = static_cast<int64_t>(gridDim.x) * blockDim.x * 4;
+    const int lane = threadIdx.x & 63;
+    for (int64_t t0 = (static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x) * 4; t0 - lane * 4 < P;
+         t0 += stride) {
+        uint32_t v = 0;
+        if (t0 + 3 < P) {
+            v = *reinterpret_cast<const uint32_t*>(er + t0);
+        } else {
+            for (int e = 0; e < 4; ++e)
+                if (t0 + e < P && er[t0 + e]) v |= 1u << (8 * e);
+        }
+        uint32_t rmask = 0;  // bit e: packet t0+e starts an episode
+        int nout = 0;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            const int64_t t = t0 + e;
+            if (!((v >> (8 * e)) & 0xffu)) continue;
+            if (t < Pout) {
+                okcnt[t] = 0;
+                ++nout;
             }
-        if (resync) episodes[atomicAdd(&counters[0], 1)] = static_cast<int32_t>(t);
+            // no erasure in [t-T-1, t-1]: the bytes inside this dword come from v
+            bool resync = true;
+#pragma unroll
+            for (int q = 0; q < e; ++q)
+                if ((v >> (8 * q)) & 0xffu) resync = false;
+            for (int64_t u = t0 - 1; resync && u >= 0 && u >= t - T - 1; --u)
+                if (er[u]) resync = false;
+            if (resync) rmask |= 1u << e;
+        }
+        const int nres = __builtin_popcount(rmask);
+        // one atomic per wave for the erased-output count and for the episode list
+        int tot = nout;
+        for (int o = 32; o >= 1; o >>= 1) tot += __shfl_xor(tot, o);
+        if (lane == 0 && tot) atomicAdd(&counters[1], tot);
+        const unsigned long long any = __ballot(nres > 0);
+        if (!any) continue;
+        int incl = nres;
+        for (int o = 1; o < 64; o <<= 1) {
+            const int y = __shfl_up(incl, o);
+            if (lane >= o) incl += y;
+        }
+        const int total = __shfl(incl, 63);
+        int base = 0;
+        if (lane == 63) base = atomicAdd(&counters[0], total);
+        base = __shfl(base, 63);
+        int slot = base + incl - nres;
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+            if ((rmask >> e) & 1u) episodes[slot++] = static_cast<int32_t>(t0 + e);
     }
 }
 
 // ------------------------------------------------------------------------------------------
-// Decode, step 2: one wavefront replays one episode of the reference's block decoders
-// symbolically.  State per diagonal block b (n of them): erased-position mask er[b], and for
-// every stored codeword symbol p / data symbol i its GF coefficient vector over the symbols q of
-// the block's current round (lane q holds coefficient q).  Each episode starts from the decoders'
-// initial state: the resync overwrites every position that an output of the episode can reach
-// ("episode independence").
+// Decode, step 2: symbolic replay.  The reference's decoder is S x n independent diagonal block
+// decoders (Decoder_Basic / Decoder_Block_Code); all S sub-streams see the same erasure flags, and
+// the n diagonals never interact.  One wavefront replays ONE diagonal b through ONE episode
+// (resync .. return to the fast path), tracking the erased-position mask (wave-uniform) and, for
+// every stored symbol, its GF coefficient vector over the n symbols of the block's current round
+// (lane q holds coefficient q; LDS columns are lane-private).  Each episode starts from the
+// decoders' initial state: the resync overwrites every position an output of the episode can
+// reach ("episode independence").  For each erased packet x output in the episode the
+// diagonal holding its symbol i = (x-b) mod n < k writes sym_ok[x][i] and coef[x][i][:].
 // ------------------------------------------------------------------------------------------
 namespace {
-struct PlanState {
+struct BlockReplay {
     const PlanArgs* a;
-    uint8_t* gexp;
-    uint8_t* glog;
-    uint32_t* er;
-    uint8_t* cwc;    // [b][p][q]
-    uint8_t* datc;   // [b][i][q]
+    const uint8_t* gexp;
+    const uint8_t* glog;
+    uint8_t* cwc;    // [p][q]
+    uint8_t* datc;   // [i][q]
     uint8_t* fresh;  // [i][q]
     int lane, k, n, T;
+    uint32_t er;     // erased positions of the block (uniform)
 
-    __device__ uint8_t* cw(int b, int p) { return cwc + (b * n + p) * n; }
-    __device__ uint8_t* dat(int b, int i) { return datc + (b * k + i) * n; }
+    __device__ uint8_t mul(uint8_t f, uint8_t v) const {
+        return v ? gexp[glog[f] + glog[v]] : 0;
+    }
 
     // decodeBlock (codingOperations.cpp:149-232) on coefficient vectors.
-    __device__ void decode_block(int b, int t) {
-        const uint32_t mall = er[b];
-        if (t < k && !((mall >> t) & 1u) && lane < n) dat(b, t)[lane] = cw(b, t)[lane];
+    __device__ void decode_block(int t) {
+        if (t < k && !((er >> t) & 1u) && lane < n) datc[t * n + lane] = cwc[t * n + lane];
         const int w = min(t + T + 1, n);
         const uint32_t full = (1u << w) - 1u;
-        const uint32_t m = mall & full;
-        if (m == full) return;
-        if (!(m & ((1u << k) - 1u))) return;
-        const uint8_t* ent = a->rules + a->wbase[w] + static_cast<int64_t>(m) * a->ES;
-        const int selv = lane < k ? ent[lane] : 0xFF;
+        const uint32_t m = er & full;
+        if (m == full || !(m & ((1u << k) - 1u))) return;
+        // the whole rule entry {sel[k], col[k][n]} in one wave-wide load
+        const uint32_t* ent = reinterpret_cast<const uint32_t*>(
+            a->rules + a->wbase[w] + static_cast<int64_t>(m) * a->ES);
+        const uint32_t ev = (lane < (a->ES >> 2)) ? ent[lane] : 0u;
         uint32_t got = 0;
         for (int i = 0; i < k; ++i) {
             if (!((m >> i) & 1u)) continue;
-            const int s = __shfl(selv, i);
-            if (s == 0xFF) continue;
-            const int colv = lane < w ? ent[k + i * n + lane] : 0;
+            const uint32_t sel = (__builtin_amdgcn_readlane(ev, i >> 2) >> ((i & 3) * 8)) & 0xffu;
+            if (sel == 0xffu) continue;
             uint8_t acc = 0;
+            const int base = k + i * n;
             for (int c = 0; c < w; ++c) {
-                const int f = __shfl(colv, c);
+                const int idx = base + c;
+                const uint32_t f = (__builtin_amdgcn_readlane(ev, idx >> 2) >> ((idx & 3) * 8)) & 0xffu;
                 if (!f || ((m >> c) & 1u)) continue;
-                if (lane < n) acc ^= gf_mul_lds(gexp, glog, static_cast<uint8_t>(f), cw(b, c)[lane]);
+                if (lane < n) acc ^= mul(static_cast<uint8_t>(f), cwc[c * n + lane]);
             }
             if (lane < n) fresh[i * n + lane] = acc;
             got |= 1u << i;
         }
         if (!got) return;
-        for (int i = 0; i < k; ++i) {
-            if (!((got >> i) & 1u)) continue;
-            if (lane < n) {
+        for (int i = 0; i < k; ++i)
+            if (((got >> i) & 1u) && lane < n) {
                 const uint8_t v = fresh[i * n + lane];
-                dat(b, i)[lane] = v;
-                cw(b, i)[lane] = v;
+                datc[i * n + lane] = v;
+                cwc[i * n + lane] = v;
             }
-        }
-        er[b] = mall & ~got;  // every lane stores the same value
+        er &= ~got;
     }
 
-    // Decoder_Block_Code::decodeSymbol (Decoder_Block_Code.cpp:61-78).
-    __device__ void decode_symbol(int b, int p, bool erased) {
+    // Decoder_Block_Code::decodeSymbol (Decoder_Block_Code.cpp:61-78) at position p.
+    __device__ void symbol(int p, bool erased) {
         if (erased) {
-            er[b] = er[b] | (1u << p);
+            er |= 1u << p;
         } else {
-            er[b] = er[b] & ~(1u << p);
-            if (lane < n) cw(b, p)[lane] = (lane == p) ? 1 : 0;
+            er &= ~(1u << p);
+            if (lane < n) cwc[p * n + lane] = (lane == p) ? 1 : 0;
         }
         if (p < T) return;
-        decode_block(b, p - T);
+        decode_block(p - T);
         if (p == n - 1)
-            for (int j = p - T + 1; j < k; ++j) decode_block(b, j);
+            for (int j = p - T + 1; j < k; ++j) decode_block(j);
     }
 
-    // Decoder_Basic::decodeStream, input half: symbol p of the packet fed at `time` goes to
-    // block (time - p) mod n.
-    __device__ void feed(int64_t time, bool erased) {
-        const int r = static_cast<int>(time % n);
-        for (int p = 0; p < n; ++p) {
-            int b = r - p;
-            if (b < 0) b += n;
-            decode_symbol(b, p, erased);
-        }
+    // the packet fed at `time` reaches this block (b) at position (time - b) mod n
+    __device__ void feed(int64_t time, int b, bool erased) {
+        int p = static_cast<int>((time - b) % n);
+        if (p < 0) p += n;
+        symbol(p, erased);
     }
 };
 }  // namespace
 
+// Erasure flags of 256 consecutive packets held in one register per lane (4 per lane), read with
+// v_readlane: the serial replay then needs no dependent global load per packet.
+struct ErWindow {
+    const uint8_t* er;
+    int64_t P;
+    int64_t base = 0;
+    uint32_t v = 0;
+    int lane;
+    __device__ void load(int64_t b) {
+        base = b;
+        const int64_t i = b + lane * 4;
+        if (i >= 0 && i + 3 < P && ((reinterpret_cast<uintptr_t>(er + i) & 3) == 0)) {
+            v = *reinterpret_cast<const uint32_t*>(er + i);
+        } else {
+            v = 0;
+            for (int e = 0; e < 4; ++e)
+                if (i + e >= 0 && i + e < P && er[i + e]) v |= 1u << (8 * e);
+        }
+    }
+    __device__ bool get(int64_t t) const {  // t in [base, base + 256)
+        const int d = static_cast<int>(t - base);
+        return ((__builtin_amdgcn_readlane(v, d >> 2) >> ((d & 3) * 8)) & 0xffu) != 0;
+    }
+};
+
 __global__ __launch_bounds__(64) void fec_plan_kernel(PlanArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-    PlanState st;
-    st.a = &a;
-    st.gexp = smem;
-    st.glog = smem + 512;
-    st.er = reinterpret_cast<uint32_t*>(smem + 768);
-    st.cwc = smem + 768 + 128;
-    st.datc = st.cwc + a.n * a.n * a.n;
-    st.fresh = st.datc + a.n * a.k * a.n;
-    st.lane = threadIdx.x;
-    st.k = a.k;
-    st.n = a.n;
-    st.T = a.T;
     const int lane = threadIdx.x, k = a.k, n = a.n, T = a.T;
+    BlockReplay br;
+    br.a = &a;
+    br.gexp = smem;
+    br.glog = smem + 512;
+    br.cwc = smem + 768;
+    br.datc = br.cwc + n * n;
+    br.fresh = br.datc + k * n;
+    br.lane = lane;
+    br.k = k;
+    br.n = n;
+    br.T = T;
     for (int i = lane; i < 768; i += 64) smem[i] = a.gf[i];
     __syncthreads();
-    const int nep = a.counters[0];
-    const int state_bytes = n * n * n + n * k * n;
-    for (int ep = blockIdx.x; ep < nep; ep += gridDim.x) {
-        const int64_t tr = a.episodes[ep];
-        for (int i = lane; i < 32; i += 64) st.er[i] = 0;
-        for (int i = lane; i < state_bytes; i += 64) st.cwc[i] = 0;
-        __syncthreads();
+    const int64_t pairs = static_cast<int64_t>(a.counters[0]) * n;
+    for (int64_t pr = blockIdx.x; pr < pairs; pr += gridDim.x) {
+        const int64_t tr = a.episodes[pr / n];
+        const int b = static_cast<int>(pr % n);
+        if (tr < 0 || tr >= a.P) continue;  // defensive: the scan only lists packets of the batch
+        if (lane < n) {  // initial state of a Decoder_Block_Code: zeros, nothing erased
+            for (int p = 0; p < n; ++p) br.cwc[p * n + lane] = 0;
+            for (int i = 0; i < k; ++i) br.datc[i * n + lane] = 0;
+        }
+        br.er = 0;
+        // resync at tr (Decoder.cpp:111-133): the n-T older slots marked erased, the last T
+        // stored codewords (those that exist) replayed
+        for (int i = 0; i < n - T; ++i) br.feed(tr + i, b, true);
+        for (int i = 0; i < T; ++i)
+            if (tr - T + i >= 0) br.feed(tr - T + i, b, false);
+        ErWindow win;
+        win.er = a.er;
+        win.P = a.P;
+        win.lane = lane;
+        win.load((tr - T) & ~static_cast<int64_t>(3));
         int64_t latest = -1;
         for (int64_t t = tr; t < a.P; ++t) {
-            const bool e = a.er[t] != 0;
+            if (t >= win.base + 256) win.load((t - T) & ~static_cast<int64_t>(3));
+            const bool e = win.get(t);
             if (!e) {
                 if (t - latest > T) break;  // Decoder.cpp:80-83: back to the fast path
             } else {
-                if (latest == -1) {  // resync, Decoder.cpp:111-133
-                    for (int i = 0; i < n - T; ++i) st.feed(t + i, true);
-                    for (int i = 0; i < T; ++i)
-                        if (t - T + i >= 0) st.feed(t - T + i, false);
-                }
                 latest = t;
             }
-            st.feed(t, e);
+            br.feed(t, b, e);
             const int64_t x = t - T;
-            if (x < 0 || x >= a.Pout || !a.er[x]) continue;
-            // Decoder_Basic::decodeStream output half (Decoder_Basic.cpp:68-86).
-            bool lost = false;
-            for (int i = 0; i < k; ++i) {
-                const int b = static_cast<int>(((x - i) % n + n) % n);
-                if ((st.er[b] >> i) & 1u) lost = true;
-            }
-            if (lost) {
-                if (lane == 0) atomicAdd(&a.counters[2], 1);
-                continue;
-            }
-            int r = 0;
-            if (lane == 0) r = atomicAdd(&a.counters[1], 1);
-            r = __shfl(r, 0);
-            if (lane == 0) a.rec_list[r] = static_cast<int32_t>(x);
-            if (lane < n) {
-                for (int i = 0; i < k; ++i) {
-                    const int b = static_cast<int>(((x - i) % n + n) % n);
-                    a.coef[(static_cast<int64_t>(r) * k + i) * n + lane] = st.dat(b, i)[lane];
-                }
-            }
+            if (x < 0 || x >= a.Pout || !win.get(x)) continue;
+            int i = static_cast<int>((x - b) % n);
+            if (i < 0) i += n;
+            if (i >= k) continue;
+            if ((br.er >> i) & 1u) continue;  // symbol lost: the packet is lost
+            if (lane < n) a.coef[(x * k + i) * n + lane] = br.datc[i * n + lane];
+            // (the recovery kernel reads coef after this launch ends: no fence needed here)
+            if (lane == 0 && atomicAdd(&a.okcnt[x], 1) == k - 1)
+                a.rec_list[atomicAdd(&a.counters[2], 1)] = static_cast<int32_t>(x);
         }
+    }
+}
+
+// ------------------------------------------------------------------------------------------
+// Decode, step 4: erased packets.  A packet is recovered iff all k of its symbols are
+// (Decoder_Basic.cpp:76-79); byte h (sub-stream s = h/k, position i = h%k) is then
+// XOR_q coef[x][i][q] * cw[x-i+q][s*n+q] over the received symbols q of its diagonal.
+// ------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void fec_recover_kernel(RecArgs a) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    uint8_t* gexp = smem;
+    uint8_t* glog = smem + 512;
+    uint8_t* cf = smem + 768;          // k*n <= 512
+    uint8_t* ob = smem + 1280;         // L+2 <= 1536
+    uint8_t* rows = smem + 2816;       // (k+n-1) rows of CW bytes
+    const int tid = threadIdx.x;
+    const int L = a.L, k = a.k, n = a.n, CW = a.CW;
+    for (int i = tid; i < 512; i += 256) gexp[i] = a.gf[i];
+    for (int i = tid; i < 256; i += 256) glog[i] = a.gf[512 + i];
+    const int nrec = a.counters[2];
+    for (int r = blockIdx.x; r < nrec; r += gridDim.x) {
+        const int64_t x = a.rec_list[r];
+        // stage the diagonal's source rows x-k+1 .. x+n-1 (those inside the stream) in LDS
+        const int64_t r0 = max<int64_t>(0, x - k + 1), r1 = min<int64_t>(a.P, x + n);
+        const uint8_t* rbase;  // row (x-k+1) of the diagonal's window
+        if (a.stage) {
+            const int nbytes = static_cast<int>((r1 - r0) * CW);
+            const uint8_t* src = a.cw + r0 * CW;
+            uint8_t* dst = rows + (r0 - (x - k + 1)) * CW;
+            if ((reinterpret_cast<uintptr_t>(src) & 3) == 0 && (nbytes & 3) == 0 &&
+                (reinterpret_cast<uintptr_t>(dst) & 3) == 0) {
+                for (int o = tid * 4; o < nbytes; o += 1024)
+                    *reinterpret_cast<uint32_t*>(dst + o) = *reinterpret_cast<const uint32_t*>(src + o);
+            } else {
+                for (int o = tid; o < nbytes; o += 256) dst[o] = src[o];
+            }
+            rbase = rows;
+        } else {
+            rbase = a.cw + (x - k + 1) * CW;  // only rows r0..r1-1 are ever touched
+        }
+        for (int i = tid; i < k * n; i += 256) cf[i] = a.coef[x * k * n + i];
+        __syncthreads();
+        for (int h = tid; h < L + 2; h += 256) {
+            const int s = h / k, i = h - (h / k) * k;
+            uint8_t acc = 0;
+            for (int q = 0; q < n; ++q) {
+                const uint8_t c = cf[i * n + q];
+                if (!c) continue;
+                // source: symbol q of packet x-i+q = row (k-1-i+q) of the window
+                acc ^= gf_mul_lds(gexp, glog, c, rbase[(k - 1 - i + q) * CW + s * n + q]);
+            }
+            ob[h] = acc;
+        }
+        __syncthreads();
+        const int ln = min(ob[0] * 256 + ob[1], L);
+        for (int b = tid; b < L; b += 256) a.out[x * L + b] = (b < ln) ? ob[b + 2] : 0;
+        if (tid == 0) a.out_len[x] = ln;
         __syncthreads();
     }
 }
@@ -387,44 +506,6 @@ __global__ __launch_bounds__(256) void fec_copy_kernel(CopyArgs a) {
             const int b = o - tl * L;
             dst[o] = (b < clen[tl]) ? cwt[tl * CW + omap[b + 2]] : 0;
         }
-    }
-}
-
-// ------------------------------------------------------------------------------------------
-// Decode, step 4: recovered packets.  Byte h of packet x (sub-stream s = h/k, position i = h%k)
-// = XOR_q coef[i][q] * cw[x-i+q][s*n+q]  over the received symbols q of its diagonal.
-// ------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void fec_recover_kernel(RecArgs a) {
-    __shared__ uint8_t gexp[512];
-    __shared__ uint8_t glog[256];
-    __shared__ uint8_t cf[16 * 32];
-    __shared__ uint8_t ob[4096];
-    const int tid = threadIdx.x;
-    const int L = a.L, k = a.k, n = a.n, CW = a.CW;
-    for (int i = tid; i < 512; i += 256) gexp[i] = a.gf[i];
-    for (int i = tid; i < 256; i += 256) glog[i] = a.gf[512 + i];
-    const int nrec = a.counters[1];
-    for (int r = blockIdx.x; r < nrec; r += gridDim.x) {
-        const int64_t x = a.rec_list[r];
-        for (int i = tid; i < k * n; i += 256) cf[i] = a.coef[static_cast<int64_t>(r) * k * n + i];
-        __syncthreads();
-        for (int h = tid; h < L + 2; h += 256) {
-            const int s = h / k, i = h - (h / k) * k;
-            uint8_t acc = 0;
-            for (int q = 0; q < n; ++q) {
-                const uint8_t c = cf[i * n + q];
-                if (!c) continue;
-                const int64_t sp = x - i + q;
-                if (sp < 0 || sp >= a.P) continue;
-                acc ^= gf_mul_lds(gexp, glog, c, a.cw[sp * CW + s * n + q]);
-            }
-            ob[h] = acc;
-        }
-        __syncthreads();
-        const int ln = min(ob[0] * 256 + ob[1], L);
-        for (int b = tid; b < L; b += 256) a.out[x * L + b] = (b < ln) ? ob[b + 2] : 0;
-        if (tid == 0) a.out_len[x] = ln;
-        __syncthreads();
     }
 }
 

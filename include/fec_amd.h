@@ -48,6 +48,10 @@ int fec_version(void);
 int fec_codec_create(int max_payload, int T, int B, int N, fec_codec **out);
 int fec_codec_destroy(fec_codec *codec);
 int fec_codec_geometry(const fec_codec *codec, int *k, int *n, int *S, int *CW);
+/* Encode kernel selection: 0 = automatic (the specialised kernel when one is compiled for
+ * (k, n-k) and max_payload % 4 == 0), 1 = generic kernel, 2 = specialised kernel (FEC_ERR_ARG if
+ * unavailable).  Both produce identical bytes; the switch exists for tests and A/B timing. */
+int fec_codec_set_encode_path(fec_codec *codec, int path);
 /* Encoder::getG / Decoder::getG (src/Encoder.cpp:61, src/Decoder.cpp:68): k*n bytes row-major. */
 int fec_codec_generator(const fec_codec *codec, uint8_t *G);
 
@@ -71,6 +75,16 @@ int fec_encode_batch(fec_codec *codec, const uint8_t *d_payload, const int32_t *
  * d_payload_len ((P-T) ints, 0 = lost).  d_workspace: fec_decode_workspace_bytes(P) bytes. */
 size_t fec_decode_workspace_bytes(const fec_codec *codec, int64_t P);
 int fec_decode_batch(fec_codec *codec, const uint8_t *d_codeword, const uint8_t *d_erasure,
+                     int64_t P, uint8_t *d_payload_out, int32_t *d_payload_len, void *d_workspace,
+                     size_t workspace_bytes, void *hip_stream);
+/* The same decode in two halves.  fec_decode_plan needs only the erasure pattern (it can run
+ * while the codewords are still being produced or transferred); fec_decode_apply needs the
+ * codewords and must be ordered after the plan (same stream, or an event).  fec_decode_batch =
+ * plan on an internal side stream concurrently with the systematic copy, joined before the
+ * recovery pass. */
+int fec_decode_plan(fec_codec *codec, const uint8_t *d_erasure, int64_t P, void *d_workspace,
+                    size_t workspace_bytes, void *hip_stream);
+int fec_decode_apply(fec_codec *codec, const uint8_t *d_codeword, const uint8_t *d_erasure,
                      int64_t P, uint8_t *d_payload_out, int32_t *d_payload_len, void *d_workspace,
                      size_t workspace_bytes, void *hip_stream);
 /* After the stream has finished the decode: erasure episodes, recovered and lost packets. */

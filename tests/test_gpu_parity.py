@@ -40,17 +40,32 @@ ENC_CONFIGS = [(10, 3, 3), (10, 5, 2), (10, 1, 1), (10, 0, 0), (10, 2, 2), (10, 
                (4, 6, 2), (12, 4, 2)]
 
 
+@pytest.mark.parametrize("path", ["generic", "auto"])
 @pytest.mark.parametrize("tbn", ENC_CONFIGS)
-def test_encode_bit_exact(tbn):
+def test_encode_bit_exact(tbn, path):
     T, B, N = tbn
     P = 2500
     c = fec.Codec(L, T, B, N)
+    c.set_encode_path(path)
     payload = fec.fill_payload(0, P, L, SEED)
     cw, wl = c.encode(payload)
     ref = oracle.encode_stream(L, T, B, N, 0, P, seed=SEED)
     assert (cw.cpu().numpy() == ref["cw"]).all()
     assert (wl.cpu().numpy() == ref["cw_len"]).all()
     assert (c.generator() == oracle.gen_G(T, B, N)).all()
+
+
+def test_encode_fast_path_other_payload_sizes():
+    """The specialised kernel with payload sizes other than 300 (L % 4 == 0) and a tiny batch."""
+    for Lx, tbn, P in [(4, (10, 3, 3), 200), (64, (10, 5, 2), 300), (1500, (10, 3, 3), 130),
+                       (300, (10, 3, 3), 1), (300, (10, 1, 1), 7)]:
+        c = fec.Codec(Lx, *tbn)
+        c.set_encode_path("fast")
+        payload = fec.fill_payload(0, P, Lx, 11)
+        cw, wl = c.encode(payload)
+        ref = oracle.encode_stream(Lx, *tbn, 0, P, seed=11)
+        assert (cw.cpu().numpy() == ref["cw"]).all(), (Lx, tbn)
+        assert (wl.cpu().numpy() == ref["cw_len"]).all(), (Lx, tbn)
 
 
 def test_encode_digest_fixture(oracle_vectors):
@@ -62,8 +77,9 @@ def test_encode_digest_fixture(oracle_vectors):
         assert hashlib.sha256(wl.cpu().numpy().astype("<i4").tobytes()).hexdigest() == v["wire_len_sha256"]
 
 
-@pytest.mark.parametrize("tbn", [(10, 3, 3), (10, 5, 2), (10, 10, 10), (10, 9, 9)])
-def test_encode_variable_lengths_and_history(tbn):
+@pytest.mark.parametrize("path", ["generic", "fast"])
+@pytest.mark.parametrize("tbn", [(10, 3, 3), (10, 5, 2), (10, 10, 10), (10, 9, 9), (10, 0, 0)])
+def test_encode_variable_lengths_and_history(tbn, path):
     T, B, N = tbn
     P = 700
     rng = np.random.default_rng(3)
@@ -75,6 +91,7 @@ def test_encode_variable_lengths_and_history(tbn):
     host = payload.cpu().numpy()
     ref = np.stack([enc.onTransmit(host[t], int(lens[t]), t)[0] for t in range(P)])
     c = fec.Codec(L, T, B, N)
+    c.set_encode_path(path)
     dl = torch.from_numpy(lens).cuda()
     cw, _ = c.encode(payload, dl)
     assert (cw.cpu().numpy() == ref).all()
@@ -190,3 +207,22 @@ def test_cpp_dropin_program(tmp_path):
     r = subprocess.run([exe], capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "DROPIN OK" in r.stdout
+
+
+def test_plan_apply_split_on_two_streams_equals_decode():
+    T, B, N = 10, 5, 2
+    P = 20000
+    pat = np.resize(load_pattern("bin_erasure")[:360000], P + T).astype(np.uint8)
+    c, payload, out, ln, _ = gpu_round_trip(T, B, N, pat, P, garbage=False)
+    cw, _ = c.encode(payload)
+    er = torch.from_numpy(pat).cuda()
+    side = torch.cuda.Stream()
+    fork = torch.cuda.Event()
+    fork.record()
+    with torch.cuda.stream(side):
+        side.wait_event(fork)
+        c.plan(er)
+    torch.cuda.current_stream().wait_stream(side)
+    out2, ln2 = c.apply(cw, er)
+    torch.cuda.synchronize()
+    assert torch.equal(out, out2) and torch.equal(ln, ln2)
