@@ -98,15 +98,16 @@ def main():
 
     def step():
         # the decode plan needs only the erasure pattern: it runs on a side stream while the
-        # encoder runs on the main stream; joined before the byte half of the decode
+        # encoder and the received-packet copy run on the main stream; joined before recovery
         fork = torch.cuda.Event()
         fork.record()
         with torch.cuda.stream(side):
             side.wait_event(fork)
             codec.plan(er)
         codec.encode(payload, out=cw, out_len=wl)
+        codec.copy(cw, er, out=out, out_len=ol)  # received packets
         torch.cuda.current_stream().wait_stream(side)
-        codec.apply(cw, er, out=out, out_len=ol)  # systematic copy + recovery
+        codec.recover(cw, out, ol)  # erased packets
 
     def barrier():
         if world > 1:

@@ -136,6 +136,30 @@ class Codec:
               "fec_decode_apply")
         return out, out_len
 
+    def copy(self, codewords, erasure, out=None, out_len=None):
+        """Received packets only (independent of plan(); erased rows get length 0)."""
+        import torch
+        P = codewords.shape[0]
+        assert codewords.shape[1] == self.CW and codewords.is_contiguous()
+        Pout = max(0, P - self.T)
+        if out is None:
+            out = torch.empty((Pout, self.L), dtype=torch.uint8, device=codewords.device)
+        if out_len is None:
+            out_len = torch.empty(Pout, dtype=torch.int32, device=codewords.device)
+        check(lib().fec_decode_copy(self._h, _ptr(codewords), _ptr(erasure), P, _ptr(out),
+                                    _ptr(out_len), _stream_handle(torch)), "fec_decode_copy")
+        return out, out_len
+
+    def recover(self, codewords, out, out_len):
+        """Erased packets (after plan() and copy())."""
+        import torch
+        P = codewords.shape[0]
+        ws = self.workspace(P)
+        check(lib().fec_decode_recover(self._h, _ptr(codewords), P, _ptr(out), _ptr(out_len),
+                                       _ptr(ws), ws.numel(), _stream_handle(torch)),
+              "fec_decode_recover")
+        return out, out_len
+
     def counters(self):
         """(episodes, recovered, lost) of the last decode (synchronises the device)."""
         v = [ctypes.c_int64() for _ in range(3)]

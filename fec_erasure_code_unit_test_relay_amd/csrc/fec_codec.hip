@@ -40,6 +40,7 @@ struct fec_codec {
     uint8_t* d_rules = nullptr;
     int64_t* d_wbase = nullptr;  // [n+1]
     uint8_t* d_gf = nullptr;     // exp[512], log[256]
+    uint8_t* d_rstate = nullptr; // post-resync block states per phase
     int enc_tp = 0;              // encode tile (packets per workgroup), generic kernel
     int fast_tp = 0;             // encode tile of the specialised kernel (0: not available)
     const void* fast_kernel = nullptr;
@@ -62,6 +63,7 @@ struct fec_codec {
         if (d_rules) (void)hipFree(d_rules);
         if (d_wbase) (void)hipFree(d_wbase);
         if (d_gf) (void)hipFree(d_gf);
+        if (d_rstate) (void)hipFree(d_rstate);
     }
 
     int enc_lds(int tp) const {
@@ -134,6 +136,9 @@ int codec_init(fec_codec* c, int max_payload, int T, int B, int N) {
     std::memcpy(gf + 512, F.log, 256);
     HIP_TRY(hipMalloc(&c->d_gf, 768));
     HIP_TRY(hipMemcpy(c->d_gf, gf, 768, hipMemcpyHostToDevice));
+    const std::vector<uint8_t> rst = fec::build_resync_states(g, c->rules);
+    HIP_TRY(hipMalloc(&c->d_rstate, rst.size()));
+    HIP_TRY(hipMemcpy(c->d_rstate, rst.data(), rst.size(), hipMemcpyHostToDevice));
 
     // Largest power-of-two tiles (<= 64 packets) that fit the LDS budget.
     for (int tp = 64; tp >= 1; tp >>= 1)
@@ -162,7 +167,7 @@ int codec_init(fec_codec* c, int max_payload, int T, int B, int N) {
 }
 
 struct WsLayout {
-    size_t counters, episodes, okcnt, rec_list, coef, total;
+    size_t counters, episodes, erased, sym_ok, rec_list, coef, total;
 };
 
 WsLayout ws_layout(const Geometry& g, int64_t P) {
@@ -170,8 +175,9 @@ WsLayout ws_layout(const Geometry& g, int64_t P) {
     WsLayout w;
     w.counters = 0;
     w.episodes = up(64);
-    w.okcnt = w.episodes + up(static_cast<size_t>(P) * 4);
-    w.rec_list = w.okcnt + up(static_cast<size_t>(P) * 4);
+    w.erased = w.episodes + up(static_cast<size_t>(P) * 4);
+    w.sym_ok = w.erased + up(static_cast<size_t>(P) * 4);
+    w.rec_list = w.sym_ok + up(static_cast<size_t>(P) * g.k);
     w.coef = w.rec_list + up(static_cast<size_t>(P) * 4);
     w.total = w.coef + up(static_cast<size_t>(P) * g.k * g.n);
     return w;
@@ -180,7 +186,8 @@ WsLayout ws_layout(const Geometry& g, int64_t P) {
 struct Ws {
     int32_t* counters;
     int32_t* episodes;
-    int32_t* okcnt;
+    int32_t* erased;
+    uint8_t* sym_ok;
     int32_t* rec_list;
     uint8_t* coef;
 };
@@ -189,8 +196,8 @@ Ws ws_carve(const Geometry& g, int64_t P, void* d_ws) {
     const WsLayout w = ws_layout(g, P);
     uint8_t* base = static_cast<uint8_t*>(d_ws);
     return {reinterpret_cast<int32_t*>(base + w.counters), reinterpret_cast<int32_t*>(base + w.episodes),
-            reinterpret_cast<int32_t*>(base + w.okcnt), reinterpret_cast<int32_t*>(base + w.rec_list),
-            base + w.coef};
+            reinterpret_cast<int32_t*>(base + w.erased), base + w.sym_ok,
+            reinterpret_cast<int32_t*>(base + w.rec_list), base + w.coef};
 }
 
 int launch_encode_fast(fec_codec* c, const uint8_t* d_payload, const int32_t* d_len, int64_t history,
@@ -276,9 +283,9 @@ int launch_plan(fec_codec* c, const uint8_t* d_er, int64_t P, void* d_ws, size_t
     HIP_TRY(hipMemsetAsync(w.counters, 0, 64, s));
     hipEvent_t stop;
     if (int st = c->begin(FEC_KERNEL_DEC_SCAN, s, &stop)) return st;
-    const int64_t sblocks = std::min<int64_t>((P + 1023) / 1024, 4096);
+    const int64_t sblocks = std::min<int64_t>((P + 4095) / 4096, 2048);
     hipLaunchKernelGGL(fec::fec_scan_kernel, dim3(static_cast<unsigned>(sblocks)), dim3(256), 0, s,
-                       d_er, P, Pout, g.T, w.counters, w.episodes, w.okcnt);
+                       d_er, P, Pout, g.T, w.counters, w.episodes, w.erased);
     HIP_TRY(hipGetLastError());
     if (int st = c->end(stop, s)) return st;
 
@@ -296,12 +303,17 @@ int launch_plan(fec_codec* c, const uint8_t* d_er, int64_t P, void* d_ws, size_t
     pa.T = g.T;
     pa.counters = w.counters;
     pa.episodes = w.episodes;
-    pa.okcnt = w.okcnt;
-    pa.rec_list = w.rec_list;
+    pa.rstate = c->d_rstate;
+    pa.rs_bytes = fec::resync_state_bytes(g);
+    pa.sym_ok = w.sym_ok;
     pa.coef = w.coef;
     const int plan_lds = 768 + g.n * g.n + 2 * g.k * g.n;
     if (int st = c->begin(FEC_KERNEL_DEC_PLAN, s, &stop)) return st;
     hipLaunchKernelGGL(fec::fec_plan_kernel, dim3(8192), dim3(64), plan_lds, s, pa);
+    HIP_TRY(hipGetLastError());
+    // packets with all k symbols recovered -> rec_list (timed with the plan)
+    hipLaunchKernelGGL(fec::fec_compact_kernel, dim3(256), dim3(256), 0, s, w.counters, w.erased,
+                       w.sym_ok, g.k, w.rec_list);
     HIP_TRY(hipGetLastError());
     return c->end(stop, s);
 }
@@ -519,6 +531,21 @@ int fec_decode_apply(fec_codec* c, const uint8_t* d_cw, const uint8_t* d_er, int
     hipStream_t s = static_cast<hipStream_t>(stream);
     if (int st = launch_copy(c, d_cw, d_er, P, d_out, d_outlen, s)) return st;
     return launch_recover(c, d_cw, P, d_out, d_outlen, d_ws, ws_bytes, s);
+}
+
+int fec_decode_copy(fec_codec* c, const uint8_t* d_cw, const uint8_t* d_er, int64_t P, uint8_t* d_out,
+                    int32_t* d_outlen, void* stream) {
+    if (!c || P < 0) return FEC_ERR_ARG;
+    if (P > c->g.T && (!d_cw || !d_er || !d_out || !d_outlen)) return FEC_ERR_ARG;
+    return launch_copy(c, d_cw, d_er, P, d_out, d_outlen, static_cast<hipStream_t>(stream));
+}
+
+int fec_decode_recover(fec_codec* c, const uint8_t* d_cw, int64_t P, uint8_t* d_out,
+                       int32_t* d_outlen, void* d_ws, size_t ws_bytes, void* stream) {
+    if (!c || P < 0) return FEC_ERR_ARG;
+    if (P > c->g.T && (!d_cw || !d_out || !d_outlen)) return FEC_ERR_ARG;
+    return launch_recover(c, d_cw, P, d_out, d_outlen, d_ws, ws_bytes,
+                          static_cast<hipStream_t>(stream));
 }
 
 int fec_decode_counters(const void* d_ws, int64_t* episodes, int64_t* recovered, int64_t* lost) {

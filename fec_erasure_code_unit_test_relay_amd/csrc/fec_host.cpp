@@ -231,6 +231,36 @@ void StreamPlanner::feed(int64_t time, bool erased) {
     for (int p = 0; p < n_; ++p) decode_symbol((r - p + n_) % n_, p, erased);
 }
 
+void StreamPlanner::resync_at(int64_t t) {
+    for (int i = 0; i < n_ - T_; ++i) feed(t + i, true);
+    for (int i = 0; i < T_; ++i)
+        if (t - T_ + i >= 0) feed(t - T_ + i, false);
+}
+
+void StreamPlanner::block_state(int b, uint32_t* er, uint8_t* cwc, uint8_t* datc) const {
+    *er = er_[b];
+    std::memcpy(cwc, &cwc_[static_cast<size_t>(b) * n_ * n_], static_cast<size_t>(n_) * n_);
+    std::memcpy(datc, &datc_[static_cast<size_t>(b) * k_ * n_], static_cast<size_t>(k_) * n_);
+}
+
+int resync_state_bytes(const Geometry& g) { return (4 + g.n * g.n + g.k * g.n + 3) & ~3; }
+
+std::vector<uint8_t> build_resync_states(const Geometry& g, const DecodeRules& rules) {
+    const int sb = resync_state_bytes(g);
+    std::vector<uint8_t> out(static_cast<size_t>(g.n) * sb, 0);
+    StreamPlanner pl(g, &rules);
+    const int64_t tr = static_cast<int64_t>(g.n) * (g.T + 1);  // >= T and a multiple of n
+    pl.resync_at(tr);
+    for (int phi = 0; phi < g.n; ++phi) {
+        const int b = static_cast<int>(((tr - phi) % g.n + g.n) % g.n);
+        uint8_t* d = out.data() + static_cast<size_t>(phi) * sb;
+        uint32_t er;
+        pl.block_state(b, &er, d + 4, d + 4 + g.n * g.n);
+        std::memcpy(d, &er, 4);
+    }
+    return out;
+}
+
 StepResult StreamPlanner::step(int64_t t, bool erased) {
     StepResult out;
     out.x = t - T_;
@@ -243,11 +273,7 @@ StepResult StreamPlanner::step(int64_t t, bool erased) {
             return out;
         }
     } else {
-        if (latest_ == -1) {  // resync (Decoder.cpp:111-133)
-            for (int i = 0; i < n_ - T_; ++i) feed(t + i, true);
-            for (int i = 0; i < T_; ++i)
-                if (t - T_ + i >= 0) feed(t - T_ + i, false);
-        }
+        if (latest_ == -1) resync_at(t);  // Decoder.cpp:111-133
         latest_ = t;
     }
     feed(t, erased);

@@ -125,6 +125,10 @@ public:
     // Feed packet t (t must increase by one per call starting at 0); erased = packet t missing.
     StepResult step(int64_t t, bool erased);
     int64_t latest_erasure() const { return latest_; }
+    // The decoder's resynchronisation at erased packet t (Decoder.cpp:111-133) applied to the
+    // current state, and a copy of one block's state (er mask, cwc[n][n], datc[k][n]).
+    void resync_at(int64_t t);
+    void block_state(int b, uint32_t* er, uint8_t* cwc, uint8_t* datc) const;
 
 private:
     void feed(int64_t time, bool erased);
@@ -141,5 +145,11 @@ private:
     std::vector<uint8_t> hist_;    // erasure flags of the last T+1 packets (ring)
     int64_t latest_ = -1;          // Decoder::latest_erasure_seq
 };
+
+// Post-resync state of one diagonal block for every phase phi = (t_resync - b) mod n, for resyncs
+// at t >= T (all T replayed codewords exist), starting from the decoders' initial state.  Layout
+// per phase (resync_state_bytes(g) bytes): uint32 er | cwc[n][n] | datc[k][n] | pad to 4.
+int resync_state_bytes(const Geometry& g);
+std::vector<uint8_t> build_resync_states(const Geometry& g, const DecodeRules& rules);
 
 }  // namespace fec

@@ -78,10 +78,11 @@ struct PlanArgs {
     const uint8_t* gf;             // exp[512] then log[256]
     int ES;                        // decode-rule entry stride (bytes, multiple of 4)
     int k, n, T;
-    int32_t* counters;             // [0] episodes, [2] recovered packets
+    const int32_t* counters;       // [0] episodes
     const int32_t* episodes;
-    int32_t* okcnt;                // [P]: recovered symbols of erased packet x (zeroed by scan)
-    int32_t* rec_list;             // recovered packets (appended by the last symbol's wave)
+    const uint8_t* rstate;         // post-resync block state per phase (build_resync_states)
+    int rs_bytes;
+    uint8_t* sym_ok;               // [P][k]: symbol i of erased packet x recovered
     uint8_t* coef;                 // [P][k][n]: coefficients of symbol i over its diagonal
 };
 
@@ -112,7 +113,9 @@ struct StreamOutArgs {
 
 __global__ void fec_encode_kernel(EncArgs a);
 __global__ void fec_scan_kernel(const uint8_t* er, int64_t P, int64_t Pout, int T,
-                                int32_t* counters, int32_t* episodes, int32_t* okcnt);
+                                int32_t* counters, int32_t* episodes, int32_t* erased);
+__global__ void fec_compact_kernel(int32_t* counters, const int32_t* erased, const uint8_t* sym_ok,
+                                   int k, int32_t* rec_list);
 __global__ void fec_plan_kernel(PlanArgs a);
 __global__ void fec_copy_kernel(CopyArgs a);
 __global__ void fec_recover_kernel(RecArgs a);

@@ -149,60 +149,108 @@ __global__ __launch_bounds__(256) void fec_encode_kernel(EncArgs a) {
 // erased packet it resyncs iff it was in the fast path just before, i.e. no erasure in
 // [t-T-1, t-1] (Decoder.cpp:80-83, 109-133).  Every resync starts an independent episode.
 // ------------------------------------------------------------------------------------------
+namespace {
+__device__ __forceinline__ uint32_t nz_bytes_mask(uint32_t w) {  // bit e: byte e of w non-zero
+    return (((w & 0xffu) != 0) ? 1u : 0u) | (((w & 0xff00u) != 0) ? 2u : 0u) |
+           (((w & 0xff0000u) != 0) ? 4u : 0u) | (((w & 0xff000000u) != 0) ? 8u : 0u);
+}
+__device__ __forceinline__ int wave_incl_scan(int v, int lane) {
+    for (int o = 1; o < 64; o <<= 1) {
+        const int y = __shfl_up(v, o);
+        if (lane >= o) v += y;
+    }
+    return v;
+}
+}  // namespace
+
+// 16 packets per lane (one 16-byte load), 4096 per workgroup; both lists (erased outputs,
+// episode starts) get one atomic per workgroup.
 __global__ __launch_bounds__(256) void fec_scan_kernel(const uint8_t* er, int64_t P, int64_t Pout,
                                                        int T, int32_t* counters, int32_t* episodes,
-                                                       int32_t* okcnt) {
-    // 4 packets per lane (one dword of erasure flags); per-wave aggregated counter updates
-    const int64_t stride = static_cast<int64_t>(gridDim.x) * blockDim.x * 4;
-    const int lane = threadIdx.x & 63;
-    for (int64_t t0 = (static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x) * 4; t0 - lane * 4 < P;
-         t0 += stride) {
-        uint32_t v = 0;
-        if (t0 + 3 < P) {
-            v = *reinterpret_cast<const uint32_t*>(er + t0);
+                                                       int32_t* erased) {
+    __shared__ int wtot[2][4];
+    __shared__ int bbase[2];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    constexpr int64_t kPerBlock = 256 * 16;
+    for (int64_t blk0 = static_cast<int64_t>(blockIdx.x) * kPerBlock; blk0 < P;
+         blk0 += static_cast<int64_t>(gridDim.x) * kPerBlock) {
+        const int64_t t0 = blk0 + tid * 16;
+        uint32_t m = 0;  // bit e: packet t0+e erased
+        if (t0 + 15 < P && (reinterpret_cast<uintptr_t>(er + t0) & 15) == 0) {
+            const uint4 v = *reinterpret_cast<const uint4*>(er + t0);
+            m = nz_bytes_mask(v.x) | (nz_bytes_mask(v.y) << 4) | (nz_bytes_mask(v.z) << 8) |
+                (nz_bytes_mask(v.w) << 12);
         } else {
-            for (int e = 0; e < 4; ++e)
-                if (t0 + e < P && er[t0 + e]) v |= 1u << (8 * e);
+            for (int e = 0; e < 16; ++e)
+                if (t0 + e < P && er[t0 + e]) m |= 1u << e;
         }
-        uint32_t rmask = 0;  // bit e: packet t0+e starts an episode
-        int nout = 0;
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
+        uint32_t resm = 0;
+        for (uint32_t rest = m; rest; rest &= rest - 1) {
+            const int e = __builtin_ctz(rest);
             const int64_t t = t0 + e;
-            if (!((v >> (8 * e)) & 0xffu)) continue;
-            if (t < Pout) {
-                okcnt[t] = 0;
-                ++nout;
-            }
-            // no erasure in [t-T-1, t-1]: the bytes inside this dword come from v
-            bool resync = true;
-#pragma unroll
-            for (int q = 0; q < e; ++q)
-                if ((v >> (8 * q)) & 0xffu) resync = false;
-            for (int64_t u = t0 - 1; resync && u >= 0 && u >= t - T - 1; --u)
-                if (er[u]) resync = false;
-            if (resync) rmask |= 1u << e;
+            // resync iff no erasure in [t-T-1, t-1] (Decoder.cpp:80-83, 109-133)
+            const int lo = e - T - 1;
+            uint32_t inside = m & ((1u << e) - 1u);
+            if (lo > 0) inside &= ~((1u << lo) - 1u);
+            bool rs = inside == 0;
+            if (rs && lo < 0)
+                for (int64_t u = t0 - 1; u >= 0 && u >= t - T - 1; --u)
+                    if (er[u]) {
+                        rs = false;
+                        break;
+                    }
+            if (rs) resm |= 1u << e;
         }
-        const int nres = __builtin_popcount(rmask);
-        // one atomic per wave for the erased-output count and for the episode list
-        int tot = nout;
-        for (int o = 32; o >= 1; o >>= 1) tot += __shfl_xor(tot, o);
-        if (lane == 0 && tot) atomicAdd(&counters[1], tot);
-        const unsigned long long any = __ballot(nres > 0);
-        if (!any) continue;
-        int incl = nres;
-        for (int o = 1; o < 64; o <<= 1) {
-            const int y = __shfl_up(incl, o);
-            if (lane >= o) incl += y;
+        uint32_t outm = m;
+        if (t0 + 16 > Pout) outm &= (t0 >= Pout) ? 0u : ((1u << (Pout - t0)) - 1u);
+        const int nout = __builtin_popcount(outm), nres = __builtin_popcount(resm);
+        const int io = wave_incl_scan(nout, lane), ir = wave_incl_scan(nres, lane);
+        if (lane == 63) {
+            wtot[0][wave] = io;
+            wtot[1][wave] = ir;
         }
-        const int total = __shfl(incl, 63);
+        __syncthreads();
+        if (tid == 0) {
+            const int to = wtot[0][0] + wtot[0][1] + wtot[0][2] + wtot[0][3];
+            const int tr = wtot[1][0] + wtot[1][1] + wtot[1][2] + wtot[1][3];
+            bbase[0] = to ? atomicAdd(&counters[1], to) : 0;
+            bbase[1] = tr ? atomicAdd(&counters[0], tr) : 0;
+        }
+        __syncthreads();
+        int so = bbase[0] + io - nout, sr = bbase[1] + ir - nres;
+        for (int w = 0; w < wave; ++w) {
+            so += wtot[0][w];
+            sr += wtot[1][w];
+        }
+        for (uint32_t rest = outm; rest; rest &= rest - 1)
+            erased[so++] = static_cast<int32_t>(t0 + __builtin_ctz(rest));
+        for (uint32_t rest = resm; rest; rest &= rest - 1)
+            episodes[sr++] = static_cast<int32_t>(t0 + __builtin_ctz(rest));
+        __syncthreads();
+    }
+}
+
+// Packets whose k symbols were all recovered -> rec_list (one atomic per wave).
+__global__ __launch_bounds__(256) void fec_compact_kernel(int32_t* counters, const int32_t* erased,
+                                                          const uint8_t* sym_ok, int k,
+                                                          int32_t* rec_list) {
+    const int ner = counters[1];
+    const int lane = threadIdx.x & 63;
+    const int stride = gridDim.x * blockDim.x;
+    for (int idx = blockIdx.x * blockDim.x + threadIdx.x; idx - lane < ner; idx += stride) {
+        bool ok = false;
+        int64_t x = 0;
+        if (idx < ner) {
+            x = erased[idx];
+            ok = true;
+            for (int i = 0; i < k; ++i) ok = ok && sym_ok[x * k + i];
+        }
+        const unsigned long long bal = __ballot(ok);
+        if (!bal) continue;
         int base = 0;
-        if (lane == 63) base = atomicAdd(&counters[0], total);
-        base = __shfl(base, 63);
-        int slot = base + incl - nres;
-#pragma unroll
-        for (int e = 0; e < 4; ++e)
-            if ((rmask >> e) & 1u) episodes[slot++] = static_cast<int32_t>(t0 + e);
+        if (lane == 0) base = atomicAdd(&counters[2], __popcll(bal));
+        base = __shfl(base, 0);
+        if (ok) rec_list[base + __popcll(bal & ((1ull << lane) - 1ull))] = static_cast<int32_t>(x);
     }
 }
 
@@ -338,16 +386,27 @@ __global__ __launch_bounds__(64) void fec_plan_kernel(PlanArgs a) {
         const int64_t tr = a.episodes[pr / n];
         const int b = static_cast<int>(pr % n);
         if (tr < 0 || tr >= a.P) continue;  // defensive: the scan only lists packets of the batch
-        if (lane < n) {  // initial state of a Decoder_Block_Code: zeros, nothing erased
-            for (int p = 0; p < n; ++p) br.cwc[p * n + lane] = 0;
-            for (int i = 0; i < k; ++i) br.datc[i * n + lane] = 0;
+        if (tr >= T) {
+            // resync at tr (Decoder.cpp:111-133) from the initial state: precomputed per phase
+            int phi = static_cast<int>((tr - b) % n);
+            if (phi < 0) phi += n;
+            const uint8_t* st = a.rstate + static_cast<int64_t>(phi) * a.rs_bytes;
+            br.er = *reinterpret_cast<const uint32_t*>(st);
+            if (lane < n) {
+                for (int p = 0; p < n; ++p) br.cwc[p * n + lane] = st[4 + p * n + lane];
+                for (int i = 0; i < k; ++i) br.datc[i * n + lane] = st[4 + n * n + i * n + lane];
+            }
+        } else {
+            // startup: the replayed slots before packet 0 are empty (NULL), replay explicitly
+            if (lane < n) {  // initial state of a Decoder_Block_Code: zeros, nothing erased
+                for (int p = 0; p < n; ++p) br.cwc[p * n + lane] = 0;
+                for (int i = 0; i < k; ++i) br.datc[i * n + lane] = 0;
+            }
+            br.er = 0;
+            for (int i = 0; i < n - T; ++i) br.feed(tr + i, b, true);
+            for (int i = 0; i < T; ++i)
+                if (tr - T + i >= 0) br.feed(tr - T + i, b, false);
         }
-        br.er = 0;
-        // resync at tr (Decoder.cpp:111-133): the n-T older slots marked erased, the last T
-        // stored codewords (those that exist) replayed
-        for (int i = 0; i < n - T; ++i) br.feed(tr + i, b, true);
-        for (int i = 0; i < T; ++i)
-            if (tr - T + i >= 0) br.feed(tr - T + i, b, false);
         ErWindow win;
         win.er = a.er;
         win.P = a.P;
@@ -368,11 +427,9 @@ __global__ __launch_bounds__(64) void fec_plan_kernel(PlanArgs a) {
             int i = static_cast<int>((x - b) % n);
             if (i < 0) i += n;
             if (i >= k) continue;
-            if ((br.er >> i) & 1u) continue;  // symbol lost: the packet is lost
-            if (lane < n) a.coef[(x * k + i) * n + lane] = br.datc[i * n + lane];
-            // (the recovery kernel reads coef after this launch ends: no fence needed here)
-            if (lane == 0 && atomicAdd(&a.okcnt[x], 1) == k - 1)
-                a.rec_list[atomicAdd(&a.counters[2], 1)] = static_cast<int32_t>(x);
+            const bool ok = !((br.er >> i) & 1u);  // Decoder_Basic.cpp:76-79
+            if (lane == 0) a.sym_ok[x * k + i] = ok ? 1 : 0;
+            if (ok && lane < n) a.coef[(x * k + i) * n + lane] = br.datc[i * n + lane];
         }
     }
 }

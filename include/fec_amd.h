@@ -87,6 +87,13 @@ int fec_decode_plan(fec_codec *codec, const uint8_t *d_erasure, int64_t P, void 
 int fec_decode_apply(fec_codec *codec, const uint8_t *d_codeword, const uint8_t *d_erasure,
                      int64_t P, uint8_t *d_payload_out, int32_t *d_payload_len, void *d_workspace,
                      size_t workspace_bytes, void *hip_stream);
+/* fec_decode_apply = fec_decode_copy (received packets; independent of the plan, may run
+ * concurrently with it) followed by fec_decode_recover (erased packets; after the plan). */
+int fec_decode_copy(fec_codec *codec, const uint8_t *d_codeword, const uint8_t *d_erasure,
+                    int64_t P, uint8_t *d_payload_out, int32_t *d_payload_len, void *hip_stream);
+int fec_decode_recover(fec_codec *codec, const uint8_t *d_codeword, int64_t P,
+                       uint8_t *d_payload_out, int32_t *d_payload_len, void *d_workspace,
+                       size_t workspace_bytes, void *hip_stream);
 /* After the stream has finished the decode: erasure episodes, recovered and lost packets. */
 int fec_decode_counters(const void *d_workspace, int64_t *episodes, int64_t *recovered,
                         int64_t *lost);

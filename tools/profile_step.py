@@ -32,6 +32,7 @@ ol = torch.empty(P, dtype=torch.int32, device="cuda")
 for _ in range(args.iters):
     codec.plan(er)
     codec.encode(payload, out=cw, out_len=wl)
-    codec.apply(cw, er, out=out, out_len=ol)
+    codec.copy(cw, er, out=out, out_len=ol)
+    codec.recover(cw, out, ol)
 torch.cuda.synchronize()
 print("ok", codec.counters())
