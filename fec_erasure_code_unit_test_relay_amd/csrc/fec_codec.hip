@@ -45,6 +45,11 @@ struct fec_codec {
     int fast_tp = 0;             // encode tile of the specialised kernel (0: not available)
     const void* fast_kernel = nullptr;
     int encode_path = 0;         // 0 auto, 1 generic, 2 specialised
+    const void* copy_fast = nullptr;  // specialised decode copy kernel
+    int copyf_tp = 0;
+    int copy_path = 0;           // 0 auto, 1 generic, 2 specialised
+    uint64_t* d_stamps = nullptr;  // diagnostics: phase stamps of the next specialised launch
+    int stamp_kernel = -1;
     int copy_tp = 0;             // decode-copy tile
     bool timing = false;
     std::vector<EventPair> events;
@@ -74,6 +79,8 @@ struct fec_codec {
     }
     int copy_lds(int tp) const { return round16(tp * g.CW) + 2 * ((g.L + 2 + 7) & ~7) + 4 * tp; }
     int ns4() const { return (g.S + 3) / 4; }
+    int copyf_raw(int tp) const { return round16(16 + tp * g.CW + 4 * g.n + 16); }
+    int copyf_lds(int tp) const { return copyf_raw(tp) + round16(tp * g.L) + 4 * tp + tp + g.T + 16; }
     int fast_raw(int tp) const { return round16(std::max((tp + g.n - 1) * g.L + 32, tp * g.CW)); }
     int fast_xin(int tp) const { return g.k * ns4() * (tp + g.n - 1) * 4; }
     int fast_lds(int tp) const { return fast_raw(tp) + fast_xin(tp) + 4 * (tp + g.n - 1); }
@@ -160,6 +167,14 @@ int codec_init(fec_codec* c, int max_payload, int T, int B, int N) {
                 break;
             }
     if (!c->fast_tp) c->fast_kernel = nullptr;
+    if ((g.L & 3) == 0) c->copy_fast = fec::fec_copy_fast_kernel_for(g.k, g.n - g.k);
+    if (c->copy_fast)
+        for (int tp = 64; tp >= 8; tp >>= 1)
+            if (c->copyf_lds(tp) <= kLdsBudget) {
+                c->copyf_tp = tp;
+                break;
+            }
+    if (!c->copyf_tp) c->copy_fast = nullptr;
     HIP_TRY(hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking));
     HIP_TRY(hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming));
     HIP_TRY(hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming));
@@ -219,6 +234,7 @@ int launch_encode_fast(fec_codec* c, const uint8_t* d_payload, const int32_t* d_
     a.ROWS = a.TP + g.n - 1;
     a.raw_bytes = c->fast_raw(a.TP);
     a.xin_bytes = c->fast_xin(a.TP);
+    a.stamps = (c->stamp_kernel == FEC_KERNEL_ENCODE) ? c->d_stamps : nullptr;
     const int64_t blocks = (P + a.TP - 1) / a.TP;
     if (blocks > 0x7fffffff) return FEC_ERR_ARG;
     hipEvent_t stop;
@@ -323,6 +339,32 @@ int launch_copy(fec_codec* c, const uint8_t* d_cw, const uint8_t* d_er, int64_t 
     const Geometry& g = c->g;
     const int64_t Pout = P - g.T;
     if (Pout <= 0) return FEC_OK;
+    const bool fast_ok = c->copy_fast && (reinterpret_cast<uintptr_t>(d_out) & 3) == 0;
+    if (c->copy_path == 2 && !fast_ok) return FEC_ERR_ARG;
+    if (fast_ok && c->copy_path != 1) {
+        fec::CopyFastArgs fa;
+        fa.cw = d_cw;
+        fa.er = d_er;
+        fa.P = P;
+        fa.Pout = Pout;
+        fa.out = d_out;
+        fa.out_len = d_outlen;
+        fa.L = g.L;
+        fa.CW = g.CW;
+        fa.NS4 = c->ns4();
+        fa.T = g.T;
+        fa.TP = c->copyf_tp;
+        fa.raw_bytes = c->copyf_raw(fa.TP);
+        fa.out_bytes = round16(fa.TP * g.L);
+        fa.stamps = (c->stamp_kernel == FEC_KERNEL_DEC_COPY) ? c->d_stamps : nullptr;
+        const int64_t blocks = (Pout + fa.TP - 1) / fa.TP;
+        hipEvent_t stop;
+        if (int st = c->begin(FEC_KERNEL_DEC_COPY, s, &stop)) return st;
+        void* args[] = {&fa};
+        HIP_TRY(hipLaunchKernel(c->copy_fast, dim3(static_cast<unsigned>(blocks)), dim3(256), args,
+                                c->copyf_lds(fa.TP), s));
+        return c->end(stop, s);
+    }
     fec::CopyArgs ca;
     ca.cw = d_cw;
     ca.er = d_er;
@@ -556,6 +598,20 @@ int fec_decode_counters(const void* d_ws, int64_t* episodes, int64_t* recovered,
     if (episodes) *episodes = h[0];
     if (recovered) *recovered = h[2];
     if (lost) *lost = h[1] - h[2];  // erased outputs that were not recovered
+    return FEC_OK;
+}
+
+int fec_debug_stamps(fec_codec* c, int kernel, void* d_stamps) {
+    if (!c) return FEC_ERR_ARG;
+    c->stamp_kernel = d_stamps ? kernel : -1;
+    c->d_stamps = static_cast<uint64_t*>(d_stamps);
+    return FEC_OK;
+}
+
+int fec_codec_set_copy_path(fec_codec* c, int path) {
+    if (!c || path < 0 || path > 2) return FEC_ERR_ARG;
+    if (path == 2 && !c->copy_fast) return FEC_ERR_ARG;
+    c->copy_path = path;
     return FEC_OK;
 }
 

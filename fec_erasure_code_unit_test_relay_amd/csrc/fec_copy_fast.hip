@@ -1,0 +1,129 @@
+// fec_copy_fast.hip -- decode of received packets, specialised at compile time on k and n-k.
+//
+// The reference outputs a received packet's systematic bytes (fast path, Decoder.cpp:77-108; the
+// slow path returns the same bytes for received packets).  In the codeword each sub-stream s is
+// [k systematic | n-k parity]; the payload is the systematic bytes with the 2-byte length header
+// removed.  One lane per (packet, group of 4 sub-streams): the group's 4n codeword bytes are read
+// from the LDS tile as dwords, the 4k systematic bytes are picked with constant-selector
+// v_perm_b32, shifted by the header's 2 bytes and written to the LDS output tile (one 16-bit
+// store at each end, dwords in between).  Tiles move between HBM and LDS with 16-byte accesses.
+#include "fec_device.h"
+#include "fec_kernels.h"
+
+namespace fec {
+
+template <int K, int NP>
+__global__ __launch_bounds__(256) void fec_copy_fast_kernel(CopyFastArgs a) {
+    constexpr int n = K + NP;
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    uint8_t* raw = smem;                           // codeword tile (+ slack)
+    uint8_t* xo = smem + a.raw_bytes;              // payload tile
+    int32_t* clen = reinterpret_cast<int32_t*>(xo + a.out_bytes);  // bytes to copy per packet
+    uint8_t* erw = reinterpret_cast<uint8_t*>(clen + a.TP);         // erasure flags [x0, x0+TP+T)
+
+    const int tid = threadIdx.x;
+    phase_stamp(a.stamps, blockIdx.x, 0);
+    const int L = a.L, CW = a.CW, NS4 = a.NS4, T = a.T;
+    const int64_t x0 = static_cast<int64_t>(blockIdx.x) * a.TP;
+    const int ntile = static_cast<int>(min<int64_t>(a.TP, a.Pout - x0));
+
+    const uint8_t* gA = a.cw + x0 * CW;
+    const int delta = static_cast<int>(reinterpret_cast<uintptr_t>(gA) & 15);
+    stage_to_lds<8>(raw, gA - delta, delta, delta + ntile * CW, tid, 256);
+    for (int i = tid; i < ntile + T; i += 256) erw[i] = a.er[x0 + i];  // x0+ntile+T-1 < P
+    __syncthreads();
+    phase_stamp(a.stamps, blockIdx.x, 1);
+
+    for (int t = tid; t < ntile; t += 256) {
+        int ln = 0, copy = 0;
+        if (!erw[t]) {
+            const uint8_t* row = raw + delta + t * CW;
+            // header bytes h = 0, 1: sub-stream 0 position 0 and h=1 -> (1/k)*n + 1%k
+            const int hdr = row[0] * 256 + row[(1 / K) * n + 1 % K];
+            bool slow = false;
+            for (int d = 0; d <= T; ++d) slow = slow || erw[t + d];
+            ln = slow ? min(hdr, L) : hdr;  // Decoder.cpp:148-149 clamps in the slow path only
+            copy = min(ln, L);
+        }
+        clen[t] = copy;
+        a.out_len[x0 + t] = ln;
+    }
+    __syncthreads();
+
+    for (int it = tid; it < ntile * NS4; it += 256) {
+        const int g = it / ntile;
+        const int t = it - g * ntile;
+        const int cl = clen[t];
+        uint32_t W[K + 1];  // systematic bytes of the group: byte e*K+i = position i of sub-stream 4g+e
+        if (cl > 0) {
+            const int off = delta + t * CW + 4 * n * g;
+            const int a4 = off & ~3;
+            uint32_t D[n + 1];
+#pragma unroll
+            for (int m = 0; m <= n; ++m) D[m] = *reinterpret_cast<const uint32_t*>(raw + a4 + 4 * m);
+            uint32_t S[n];
+#pragma unroll
+            for (int m = 0; m < n; ++m) S[m] = __builtin_amdgcn_alignbyte(D[m + 1], D[m], off & 3);
+#pragma unroll
+            for (int m = 0; m < K; ++m) {
+                const int i0 = 4 * m, i1 = i0 + 1, i2 = i0 + 2, i3 = i0 + 3;
+                W[m] = gather4(S, (i0 / K) * n + i0 % K, (i1 / K) * n + i1 % K,
+                               (i2 / K) * n + i2 % K, (i3 / K) * n + i3 % K);
+            }
+        } else {
+#pragma unroll
+            for (int m = 0; m < K; ++m) W[m] = 0;
+        }
+        W[K] = 0;
+        // payload bytes b in [4gK-2, 4gK+4K-2): head (2 bytes), K-1 dwords, tail (2 bytes)
+        uint8_t* orow = xo + t * L;
+        const int bh = 4 * g * K - 2;
+        if (bh >= 0 && bh < L) {
+            const uint32_t v = W[0] & keep_bytes(cl - bh);
+            *reinterpret_cast<uint16_t*>(orow + bh) = static_cast<uint16_t>(v);
+        }
+#pragma unroll
+        for (int m = 0; m < K - 1; ++m) {
+            const int b = 4 * g * K + 4 * m;
+            if (b < L) {
+                const uint32_t v = __builtin_amdgcn_alignbyte(W[m + 1], W[m], 2) & keep_bytes(cl - b);
+                *reinterpret_cast<uint32_t*>(orow + b) = v;
+            }
+        }
+        const int bt = 4 * g * K + 4 * K - 4;
+        if (bt < L) {
+            const uint32_t v = (W[K - 1] >> 16) & keep_bytes(cl - bt);
+            *reinterpret_cast<uint16_t*>(orow + bt) = static_cast<uint16_t>(v);
+        }
+    }
+    __syncthreads();
+    phase_stamp(a.stamps, blockIdx.x, 2);
+
+    const int obytes = ntile * L;
+    uint8_t* dst = a.out + x0 * L;
+    if ((obytes & 15) == 0 && (reinterpret_cast<uintptr_t>(dst) & 15) == 0) {
+        for (int o = tid * 16; o < obytes; o += 256 * 16)
+            *reinterpret_cast<uint4*>(dst + o) = *reinterpret_cast<const uint4*>(xo + o);
+    } else {
+        for (int o = tid * 4; o < obytes; o += 256 * 4)
+            *reinterpret_cast<uint32_t*>(dst + o) = *reinterpret_cast<const uint32_t*>(xo + o);
+    }
+    phase_stamp(a.stamps, blockIdx.x, 3);
+}
+
+#define FEC_COPY_FAST_LIST(X) \
+    X(8, 3) X(9, 5) X(11, 0) X(10, 1) X(9, 2) X(7, 4) X(6, 5) X(5, 6) X(4, 7) X(3, 8) X(2, 9)  \
+    X(1, 10) X(10, 3) X(9, 3) X(10, 4) X(8, 4) X(10, 5) X(7, 5) X(3, 9)
+
+#define FEC_COPY_FAST_INST(K, NP) template __global__ void fec_copy_fast_kernel<K, NP>(CopyFastArgs);
+FEC_COPY_FAST_LIST(FEC_COPY_FAST_INST)
+
+const void* fec_copy_fast_kernel_for(int k, int np) {
+#define FEC_COPY_FAST_CASE(K, NP) \
+    if (k == K && np == NP) return reinterpret_cast<const void*>(&fec_copy_fast_kernel<K, NP>);
+    FEC_COPY_FAST_LIST(FEC_COPY_FAST_CASE)
+#undef FEC_COPY_FAST_CASE
+    return nullptr;
+}
+
+}  // namespace fec

@@ -1,0 +1,79 @@
+// fec_device.h -- device helpers shared by the specialised (k, n-k) kernels.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace fec {
+
+// GF(2^8) product of four packed bytes by one constant c (c*x is XOR-linear: three register
+// tables indexed per byte by v_perm_b32).  tab[0..1] = c*{0..7}, tab[2..3] = c*({0..7}<<3),
+// tab[4] = c*({0..3}<<6).
+__device__ __forceinline__ uint32_t gf_mul4x(const uint32_t* tab, uint32_t x) {
+    const uint32_t g0 = x & 0x07070707u;
+    const uint32_t g1 = (x >> 3) & 0x07070707u;
+    const uint32_t g2 = (x >> 6) & 0x03030303u;
+    return __builtin_amdgcn_perm(tab[1], tab[0], g0) ^ __builtin_amdgcn_perm(tab[3], tab[2], g1) ^
+           __builtin_amdgcn_perm(tab[4], tab[4], g2);
+}
+
+// selector of v_perm_b32(hi, lo, sel): byte codes 0-3 = lo bytes, 4-7 = hi bytes, 12 = 0x00
+constexpr uint32_t sel4(int b0, int b1, int b2, int b3) {
+    return uint32_t(b0) | (uint32_t(b1) << 8) | (uint32_t(b2) << 16) | (uint32_t(b3) << 24);
+}
+
+// The dword whose byte q is byte i_q of the concatenated words src[] (word c/4, byte c%4);
+// indices are compile-time constants after unrolling: two v_perm_b32 + one v_or_b32.
+template <int NW>
+__device__ __forceinline__ uint32_t gather4(const uint32_t (&src)[NW], int i0, int i1, int i2, int i3) {
+    const uint32_t lo = __builtin_amdgcn_perm(src[i1 >> 2], src[i0 >> 2],
+                                              sel4(i0 & 3, 4 + (i1 & 3), 12, 12));
+    const uint32_t hi = __builtin_amdgcn_perm(src[i3 >> 2], src[i2 >> 2],
+                                              sel4(12, 12, i2 & 3, 4 + (i3 & 3)));
+    return lo | hi;
+}
+
+__device__ __forceinline__ uint32_t keep_bytes(int c) {  // mask of the low c bytes (c clamped)
+    return c <= 0 ? 0u : (c >= 4 ? 0xffffffffu : ((1u << (8 * c)) - 1u));
+}
+
+// Copy global bytes [gbase + delta, gbase + total) into lds[delta, total) (same offsets).  gbase
+// is 16-byte aligned, delta and total are multiples of 4.  Interior 16-byte chunks use dwordx4
+// loads, BATCH of them in flight per thread before the LDS writes; the two edge chunks use dword
+// loads so nothing outside the range is read.
+template <int BATCH>
+__device__ __forceinline__ void stage_to_lds(uint8_t* lds, const uint8_t* gbase, int delta, int total,
+                                             int tid, int nthreads) {
+    const int nchunks = (total + 15) >> 4;
+    for (int c0 = 0; c0 < nchunks; c0 += nthreads * BATCH) {
+        uint4 v[BATCH];
+#pragma unroll
+        for (int q = 0; q < BATCH; ++q) {
+            const int lo = (c0 + q * nthreads + tid) << 4;
+            const bool full = lo >= delta && lo + 16 <= total;
+            v[q] = full ? *reinterpret_cast<const uint4*>(gbase + lo) : make_uint4(0, 0, 0, 0);
+        }
+#pragma unroll
+        for (int q = 0; q < BATCH; ++q) {
+            const int lo = (c0 + q * nthreads + tid) << 4;
+            if (lo >= delta && lo + 16 <= total) *reinterpret_cast<uint4*>(lds + lo) = v[q];
+        }
+    }
+    // the (at most two) partial chunks at the ends, dword by dword
+    for (int o = tid * 4; o < 32; o += nthreads * 4) {
+        const int lo16 = delta & ~15, hi16 = total & ~15;
+        const int oa = lo16 + o, ob = hi16 + (o - 16);
+        if (o < 16 && oa >= delta && oa + 4 <= total && !(lo16 >= delta && lo16 + 16 <= total))
+            *reinterpret_cast<uint32_t*>(lds + oa) = *reinterpret_cast<const uint32_t*>(gbase + oa);
+        if (o >= 16 && ob >= delta && ob + 4 <= total && hi16 != lo16)
+            *reinterpret_cast<uint32_t*>(lds + ob) = *reinterpret_cast<const uint32_t*>(gbase + ob);
+    }
+}
+
+// Diagnostic phase stamp (s_memtime, shader clock) of workgroup `wg`, slot `k` of 8; only when a
+// stamp buffer is given.  Stamps never feed an output.
+__device__ __forceinline__ void phase_stamp(uint64_t* stamps, int wg, int k) {
+    if (stamps && threadIdx.x == 0) stamps[static_cast<int64_t>(wg) * 8 + k] = __builtin_amdgcn_s_memtime();
+}
+
+}  // namespace fec

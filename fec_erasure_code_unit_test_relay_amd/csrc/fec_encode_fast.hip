@@ -14,41 +14,11 @@
 //      re-interleaved into the codeword layout [s][k systematic | n-k parity] with constant
 //      selectors and written to the LDS output tile;
 //   D. the tile leaves in 16-byte stores; trimmed wire sizes are taken from the tile.
+#include "fec_device.h"
 #include "fec_kernels.h"
 
 namespace fec {
 
-namespace {
-
-__device__ __forceinline__ uint32_t gf_mul4f(const uint32_t* tab, uint32_t x) {
-    const uint32_t g0 = x & 0x07070707u;
-    const uint32_t g1 = (x >> 3) & 0x07070707u;
-    const uint32_t g2 = (x >> 6) & 0x03030303u;
-    return __builtin_amdgcn_perm(tab[1], tab[0], g0) ^ __builtin_amdgcn_perm(tab[3], tab[2], g1) ^
-           __builtin_amdgcn_perm(tab[4], tab[4], g2);
-}
-
-// selector for v_perm_b32(hi, lo, sel): byte codes 0-3 = lo bytes, 4-7 = hi bytes, 12 = 0x00
-constexpr uint32_t sel4(int b0, int b1, int b2, int b3) {
-    return uint32_t(b0) | (uint32_t(b1) << 8) | (uint32_t(b2) << 16) | (uint32_t(b3) << 24);
-}
-
-// Byte c of the concatenation src[0..]: word c/4, byte c%4.  Builds the dword whose byte q is
-// source byte idx[q] (idx[q] < 0: zero) from at most two v_perm_b32 and one v_or.
-template <int NW>
-__device__ __forceinline__ uint32_t gather4(const uint32_t (&src)[NW], int i0, int i1, int i2, int i3) {
-    const uint32_t lo = __builtin_amdgcn_perm(src[i1 >> 2], src[i0 >> 2],
-                                              sel4(i0 & 3, 4 + (i1 & 3), 12, 12));
-    const uint32_t hi = __builtin_amdgcn_perm(src[i3 >> 2], src[i2 >> 2],
-                                              sel4(12, 12, i2 & 3, 4 + (i3 & 3)));
-    return lo | hi;
-}
-
-__device__ __forceinline__ uint32_t keep_bytes(int c) {  // low c bytes kept (c clamped to 0..4)
-    return c <= 0 ? 0u : (c >= 4 ? 0xffffffffu : ((1u << (8 * c)) - 1u));
-}
-
-}  // namespace
 
 template <int K, int NP>
 __global__ __launch_bounds__(256) void fec_encode_fast_kernel(EncFastArgs a) {
@@ -62,6 +32,7 @@ __global__ __launch_bounds__(256) void fec_encode_fast_kernel(EncFastArgs a) {
     int32_t* rowlen = reinterpret_cast<int32_t*>(smem + a.raw_bytes + a.xin_bytes);
 
     const int tid = threadIdx.x;
+    phase_stamp(a.stamps, blockIdx.x, 0);
     const int L = a.L, NS4 = a.NS4, ROWS = a.ROWS, CW = a.CW;
     const int64_t t0 = static_cast<int64_t>(blockIdx.x) * a.TP;
     const int ntile = static_cast<int>(min<int64_t>(a.TP, a.P - t0));
@@ -85,21 +56,9 @@ __global__ __launch_bounds__(256) void fec_encode_fast_kernel(EncFastArgs a) {
     const int delta = static_cast<int>(reinterpret_cast<uintptr_t>(gA) & 15);
     const uint8_t* gbase = gA - delta;
     const int total = delta + static_cast<int>(pb - pa) * L;
-    const int nchunks = (total + 15) >> 4;
-    for (int c = tid; c < nchunks; c += 256) {
-        const int lo = c << 4;
-        if (lo >= delta && lo + 16 <= total) {
-            *reinterpret_cast<uint4*>(raw + lo) = *reinterpret_cast<const uint4*>(gbase + lo);
-        } else {
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                const int o = lo + 4 * q;
-                if (o >= delta && o + 4 <= total)
-                    raw32[o >> 2] = *reinterpret_cast<const uint32_t*>(gbase + o);
-            }
-        }
-    }
+    stage_to_lds<8>(raw, gbase, delta, total, tid, 256);
     __syncthreads();
+    phase_stamp(a.stamps, blockIdx.x, 1);
 
     // B. transpose windows into position planes xin[(i*NS4 + g)*ROWS + r]
     const int planes = NS4 * ROWS;
@@ -136,58 +95,85 @@ __global__ __launch_bounds__(256) void fec_encode_fast_kernel(EncFastArgs a) {
         for (int i = 0; i < K; ++i) xin[i * planes + g * ROWS + r] = PW[i];
     }
     __syncthreads();
+    phase_stamp(a.stamps, blockIdx.x, 2);
 
-    // C. parity + interleave into the codeword layout
-    for (int it = tid; it < ntile * NS4; it += 256) {
-        const int g = it / ntile;
-        const int t = it - g * ntile;
-        const int r = t + H;
-        const uint32_t* col = xin + g * ROWS;
-        uint32_t src[n + 1];  // words 0..k-1: systematic positions, k..n-1: parity
+    // C. parity + interleave into the codeword layout.  Each thread holds up to IPT items so that
+    // every coefficient table is fetched once and applied to all of them (the tables are
+    // wave-uniform scalar loads), and their LDS reads are in flight together.
+    constexpr int IPT = 3;
+    const int nitems = ntile * NS4;
+    for (int base = 0; base < nitems; base += 256 * IPT) {
+        int rowoff[IPT];  // dword index of the item's row in plane 0
+        bool valid[IPT];
 #pragma unroll
-        for (int i = 0; i < K; ++i) src[i] = col[i * planes + r];
+        for (int q = 0; q < IPT; ++q) {
+            const int it = base + q * 256 + tid;
+            valid[q] = it < nitems;
+            const int itc = valid[q] ? it : 0;
+            const int g = itc / ntile;
+            const int t = itc - g * ntile;
+            rowoff[q] = g * ROWS + t + H;
+        }
+        uint32_t acc[IPT][NP > 0 ? NP : 1];
 #pragma unroll
-        for (int jj = 0; jj < NP; ++jj) {
-            constexpr int j0 = K;
-            uint32_t acc = 0;
+        for (int q = 0; q < IPT; ++q)
 #pragma unroll
-            for (int i = 0; i < K; ++i) {
-                const uint32_t* tab = a.ptab + (i * NP + jj) * 8;
-                if (tab[5]) acc ^= gf_mul4f(tab, col[i * planes + r - (j0 + jj - i)]);
+            for (int jj = 0; jj < NP; ++jj) acc[q][jj] = 0;
+#pragma unroll
+        for (int i = 0; i < K; ++i) {
+            const uint32_t* pl = xin + i * planes;
+#pragma unroll
+            for (int jj = 0; jj < NP; ++jj) {
+                const uint32_t* tab = a.ptab + (i * NP + jj) * 8;  // zero coefficient: zero tables
+                const int d = K + jj - i;
+#pragma unroll
+                for (int q = 0; q < IPT; ++q) acc[q][jj] ^= gf_mul4x(tab, pl[rowoff[q] - d]);
             }
-            src[K + jj] = acc;
         }
-        src[n] = 0;
-        // output byte o = e*n + j (e = sub-stream in the group) = word j, byte e
-        uint32_t O[n + 1];
 #pragma unroll
-        for (int m = 0; m < n; ++m) {
-            const int o0 = 4 * m, o1 = o0 + 1, o2 = o0 + 2, o3 = o0 + 3;
-            O[m] = gather4(src, (o0 % n) * 4 + o0 / n, (o1 % n) * 4 + o1 / n, (o2 % n) * 4 + o2 / n,
-                           (o3 % n) * 4 + o3 / n);
-        }
-        O[n] = 0;
-        // write bytes [off, off + valid) of the tile; off may be unaligned (CW odd/even)
-        const int off = t * CW + 4 * n * g;
-        const int valid = min(4 * n, CW - 4 * n * g);
-        const int head = (4 - (off & 3)) & 3;
-        const int hv = min(head, valid);
-        for (int q = 0; q < hv; ++q) xout[off + q] = static_cast<uint8_t>(O[0] >> (8 * q));
-        const int body = valid - hv;
-        const int nfull = body >> 2;
-        uint32_t* dst = reinterpret_cast<uint32_t*>(xout + off + hv);
-        uint32_t tailw = 0;
+        for (int q = 0; q < IPT; ++q) {
+            if (!valid[q]) continue;
+            const int it = base + q * 256 + tid;
+            const int g = it / ntile;
+            const int t = it - g * ntile;
+            uint32_t src[n + 1];  // words 0..k-1: systematic positions, k..n-1: parity
 #pragma unroll
-        for (int m = 0; m < n; ++m) {
-            const uint32_t w = __builtin_amdgcn_alignbyte(O[m + 1], O[m], head);
-            if (m < nfull) dst[m] = w;
-            if (m == nfull) tailw = w;
+            for (int i = 0; i < K; ++i) src[i] = xin[i * planes + rowoff[q]];
+#pragma unroll
+            for (int jj = 0; jj < NP; ++jj) src[K + jj] = acc[q][jj];
+            src[n] = 0;
+            // output byte o = e*n + j (e = sub-stream in the group) = word j, byte e
+            uint32_t O[n + 1];
+#pragma unroll
+            for (int m = 0; m < n; ++m) {
+                const int o0 = 4 * m, o1 = o0 + 1, o2 = o0 + 2, o3 = o0 + 3;
+                O[m] = gather4(src, (o0 % n) * 4 + o0 / n, (o1 % n) * 4 + o1 / n,
+                               (o2 % n) * 4 + o2 / n, (o3 % n) * 4 + o3 / n);
+            }
+            O[n] = 0;
+            // write bytes [off, off + valid) of the tile; off may be unaligned (CW odd/even)
+            const int off = t * CW + 4 * n * g;
+            const int vb = min(4 * n, CW - 4 * n * g);
+            const int head = (4 - (off & 3)) & 3;
+            const int hv = min(head, vb);
+            for (int e = 0; e < hv; ++e) xout[off + e] = static_cast<uint8_t>(O[0] >> (8 * e));
+            const int body = vb - hv;
+            const int nfull = body >> 2;
+            uint32_t* dst = reinterpret_cast<uint32_t*>(xout + off + hv);
+            uint32_t tailw = 0;
+#pragma unroll
+            for (int m = 0; m < n; ++m) {
+                const uint32_t w = __builtin_amdgcn_alignbyte(O[m + 1], O[m], head);
+                if (m < nfull) dst[m] = w;
+                if (m == nfull) tailw = w;
+            }
+            const int tail = body & 3;
+            uint8_t* tb = xout + off + hv + 4 * nfull;
+            for (int e = 0; e < tail; ++e) tb[e] = static_cast<uint8_t>(tailw >> (8 * e));
         }
-        const int tail = body & 3;
-        uint8_t* tb = xout + off + hv + 4 * nfull;
-        for (int q = 0; q < tail; ++q) tb[q] = static_cast<uint8_t>(tailw >> (8 * q));
     }
     __syncthreads();
+    phase_stamp(a.stamps, blockIdx.x, 3);
 
     // D. tile out + trimmed wire sizes (FEC_Encoder.cpp:55-60)
     const int bytes = ntile * CW;
@@ -204,6 +190,7 @@ __global__ __launch_bounds__(256) void fec_encode_fast_kernel(EncFastArgs a) {
         while (z >= 0 && row[z] == 0) --z;
         a.cw_len[t0 + tl] = z + 1;
     }
+    phase_stamp(a.stamps, blockIdx.x, 4);
 }
 
 // Instantiated (k, n-k): the adaptive estimator's (10,b,b) family (k = 11-b, n = 11), the BASELINE

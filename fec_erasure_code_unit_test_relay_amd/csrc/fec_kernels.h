@@ -53,10 +53,26 @@ struct EncFastArgs {
     int TP, ROWS;               // packets per tile, TP + n - 1
     int raw_bytes;              // LDS union of payload rows / output tile (16-aligned)
     int xin_bytes;              // LDS position planes
+    uint64_t* stamps;           // diagnostics: per-workgroup phase timestamps (null = off)
 };
 
 // fec_encode_fast_kernel<k, n-k> for the instantiated pairs (fec_encode_fast.hip), else nullptr.
 const void* fec_encode_fast_kernel_for(int k, int np);
+
+struct CopyFastArgs {
+    const uint8_t* cw;
+    const uint8_t* er;
+    int64_t P, Pout;
+    uint8_t* out;               // 4-byte aligned, L % 4 == 0
+    int32_t* out_len;
+    int L, CW, NS4, T, TP;
+    int raw_bytes;              // codeword tile + slack (16-aligned)
+    int out_bytes;              // payload tile (16-aligned)
+    uint64_t* stamps;           // diagnostics: per-workgroup phase timestamps (null = off)
+};
+
+// fec_copy_fast_kernel<k, n-k> for the instantiated pairs (fec_copy_fast.hip), else nullptr.
+const void* fec_copy_fast_kernel_for(int k, int np);
 
 struct CopyArgs {
     const uint8_t* cw;

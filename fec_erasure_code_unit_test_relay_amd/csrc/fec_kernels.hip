@@ -412,24 +412,32 @@ __global__ __launch_bounds__(64) void fec_plan_kernel(PlanArgs a) {
         win.P = a.P;
         win.lane = lane;
         win.load((tr - T) & ~static_cast<int64_t>(3));
-        int64_t latest = -1;
-        for (int64_t t = tr; t < a.P; ++t) {
-            if (t >= win.base + 256) win.load((t - T) & ~static_cast<int64_t>(3));
+        // positions are tracked incrementally (no 64-bit modulo per packet):
+        //   p  = (t - b) mod n      position of packet t in this block's round
+        //   ix = (t - T - b) mod n  position (= symbol index) of the output packet x = t - T
+        int p = static_cast<int>((tr - b) % n);
+        if (p < 0) p += n;
+        int ix = p - (T % n);
+        if (ix < 0) ix += n;
+        const int Pi = static_cast<int>(a.P), Pouti = static_cast<int>(a.Pout);
+        int latest = -1;
+        for (int t = static_cast<int>(tr); t < Pi; ++t) {
+            if (t >= win.base + 256) win.load((t - T) & ~3);
             const bool e = win.get(t);
             if (!e) {
                 if (t - latest > T) break;  // Decoder.cpp:80-83: back to the fast path
             } else {
                 latest = t;
             }
-            br.feed(t, b, e);
-            const int64_t x = t - T;
-            if (x < 0 || x >= a.Pout || !win.get(x)) continue;
-            int i = static_cast<int>((x - b) % n);
-            if (i < 0) i += n;
-            if (i >= k) continue;
+            br.symbol(p, e);
+            const int x = t - T;
+            const int i = ix;
+            if (++p == n) p = 0;
+            if (++ix == n) ix = 0;
+            if (x < 0 || x >= Pouti || i >= k || !win.get(x)) continue;
             const bool ok = !((br.er >> i) & 1u);  // Decoder_Basic.cpp:76-79
-            if (lane == 0) a.sym_ok[x * k + i] = ok ? 1 : 0;
-            if (ok && lane < n) a.coef[(x * k + i) * n + lane] = br.datc[i * n + lane];
+            if (lane == 0) a.sym_ok[static_cast<int64_t>(x) * k + i] = ok ? 1 : 0;
+            if (ok && lane < n) a.coef[(static_cast<int64_t>(x) * k + i) * n + lane] = br.datc[i * n + lane];
         }
     }
 }

@@ -52,6 +52,8 @@ int fec_codec_geometry(const fec_codec *codec, int *k, int *n, int *S, int *CW);
  * (k, n-k) and max_payload % 4 == 0), 1 = generic kernel, 2 = specialised kernel (FEC_ERR_ARG if
  * unavailable).  Both produce identical bytes; the switch exists for tests and A/B timing. */
 int fec_codec_set_encode_path(fec_codec *codec, int path);
+/* The same switch for the decoder's received-packet copy kernel. */
+int fec_codec_set_copy_path(fec_codec *codec, int path);
 /* Encoder::getG / Decoder::getG (src/Encoder.cpp:61, src/Decoder.cpp:68): k*n bytes row-major. */
 int fec_codec_generator(const fec_codec *codec, uint8_t *G);
 
@@ -108,6 +110,11 @@ int fec_decode_counters(const void *d_workspace, int64_t *episodes, int64_t *rec
 int fec_timing_enable(fec_codec *codec, int enable);
 /* Synchronises the recorded events; total_ms[FEC_KERNEL_COUNT], launches[FEC_KERNEL_COUNT]. */
 int fec_timing_collect(fec_codec *codec, double *total_ms, int64_t *launches);
+
+/* Diagnostics: the next launches of `kernel` (FEC_KERNEL_ENCODE or FEC_KERNEL_DEC_COPY, the
+ * specialised kernels) write s_memtime phase stamps, 8 uint64 per workgroup, to d_stamps
+ * (NULL switches it off).  Timing-only; no output depends on it. */
+int fec_debug_stamps(fec_codec *codec, int kernel, void *d_stamps);
 
 /* ---- streaming per-packet API (host buffers) -----------------------------------------------
  * fec_encoder_transmit = FEC_Encoder::onTransmit: data (payload bytes), payload (<= max_payload),

@@ -102,9 +102,10 @@ def test_encode_variable_lengths_and_history(tbn, path):
     assert (torch.cat([cw1, cw2]).cpu().numpy() == ref).all()
 
 
-def gpu_round_trip(T, B, N, pattern, P, garbage=True):
+def gpu_round_trip(T, B, N, pattern, P, garbage=True, copy_path="auto"):
     """GPU encode of packets 0..P+T-1, erase, GPU decode -> outputs for packets 0..P-1."""
     c = fec.Codec(L, T, B, N)
+    c.set_copy_path(copy_path)
     Pf = P + T
     pat = np.zeros(Pf, dtype=np.uint8)
     m = min(pattern.size, Pf)
@@ -128,17 +129,45 @@ DEC_CASES = [((10, 5, 2), "bin_erasure", 0, 8000), ((10, 3, 3), "bin_erasure", 0
              ((12, 4, 2), "erasure100", 1000, 3000), ((4, 6, 2), "erasure100", 0, 3000)]
 
 
+@pytest.mark.parametrize("copy_path", ["generic", "auto"])
 @pytest.mark.parametrize("tbn,pattern,start,P", DEC_CASES)
-def test_decode_bit_exact_vs_oracle(tbn, pattern, start, P):
+def test_decode_bit_exact_vs_oracle(tbn, pattern, start, P, copy_path):
     T, B, N = tbn
     pat = load_pattern(pattern)[start:start + P + T]
     ref = oracle.run_stream(L, T, B, N, P, pat, seed=SEED, want_data=True)
-    c, payload, out, ln, _ = gpu_round_trip(T, B, N, pat, P)
+    c, payload, out, ln, _ = gpu_round_trip(T, B, N, pat, P, copy_path=copy_path)
     assert (ln.cpu().numpy() == ref["out_len"]).all()
     assert (out.cpu().numpy() == ref["out_data"]).all()
     eps, rec, lost = c.counters()
     assert lost == int((ref["out_len"] == 0).sum())  # every lost packet is an erased one
     assert rec + lost == int(pat[:P].sum())
+
+
+def test_copy_fast_variable_lengths_and_sizes():
+    """Received packets of every length (and other payload sizes) through the specialised copy."""
+    for Lx, tbn in [(300, (10, 3, 3)), (300, (10, 10, 10)), (64, (10, 5, 2)), (1500, (10, 3, 3))]:
+        T, B, N = tbn
+        P = 700
+        rng = np.random.default_rng(Lx)
+        lens = rng.integers(0, Lx + 1, size=P + T).astype(np.int32)
+        lens[::9] = Lx
+        pat = (rng.random(P + T) < 0.05).astype(np.uint8)
+        enc = oracle.Encoder(Lx, T, B, N)
+        dec = oracle.Decoder(Lx, T, B, N)
+        src = oracle.fill_payload(0, P + T, Lx, 5)
+        cws, want_len, want = [], [], []
+        for t in range(P + T):
+            cw, size = enc.onTransmit(src[t], int(lens[t]), t)
+            cws.append(cw)
+            out, p = dec.onReceive(None if pat[t] else cw, size, t, bool(pat[t]))
+            if t >= T:
+                want.append(out)
+                want_len.append(p)
+        c = fec.Codec(Lx, T, B, N)
+        c.set_copy_path("fast")
+        out, ln = c.decode(torch.from_numpy(np.stack(cws)).cuda(), torch.from_numpy(pat).cuda())
+        assert (ln.cpu().numpy() == np.array(want_len)).all(), (Lx, tbn)
+        assert (out.cpu().numpy() == np.stack(want)).all(), (Lx, tbn)
 
 
 def test_decode_startup_and_dense_erasures():
