@@ -68,6 +68,11 @@ class Codec:
         code = {"auto": 0, "generic": 1, "fast": 2}[path]
         check(lib().fec_codec_set_copy_path(self._h, code), "fec_codec_set_copy_path")
 
+    def set_plan_path(self, path: str) -> None:
+        """'auto', 'generic' or 'fast' for the decoder's planner."""
+        code = {"auto": 0, "generic": 1, "fast": 2}[path]
+        check(lib().fec_codec_set_plan_path(self._h, code), "fec_codec_set_plan_path")
+
     # -- batched device-resident path -----------------------------------------------------------
     def encode(self, payload, lengths=None, history: int = 0, out=None, out_len=None):
         """Encode rows ``history..`` of ``payload`` ([rows, L] uint8 on the GPU).

@@ -39,6 +39,8 @@ struct fec_codec {
     uint32_t* d_ptab = nullptr;  // [k][n-k][8]
     uint8_t* d_rules = nullptr;
     int64_t* d_wbase = nullptr;  // [n+1]
+    uint8_t* d_rules_log = nullptr;  // rules with coefficients in log form (specialised planner)
+    const void* plan_fast = nullptr;
     uint8_t* d_gf = nullptr;     // exp[512], log[256]
     uint8_t* d_rstate = nullptr; // post-resync block states per phase
     int enc_tp = 0;              // encode tile (packets per workgroup), generic kernel
@@ -48,6 +50,7 @@ struct fec_codec {
     const void* copy_fast = nullptr;  // specialised decode copy kernel
     int copyf_tp = 0;
     int copy_path = 0;           // 0 auto, 1 generic, 2 specialised
+    int plan_path = 0;
     uint64_t* d_stamps = nullptr;  // diagnostics: phase stamps of the next specialised launch
     int stamp_kernel = -1;
     int copy_tp = 0;             // decode-copy tile
@@ -67,6 +70,7 @@ struct fec_codec {
         if (d_ptab) (void)hipFree(d_ptab);
         if (d_rules) (void)hipFree(d_rules);
         if (d_wbase) (void)hipFree(d_wbase);
+        if (d_rules_log) (void)hipFree(d_rules_log);
         if (d_gf) (void)hipFree(d_gf);
         if (d_rstate) (void)hipFree(d_rstate);
     }
@@ -135,6 +139,16 @@ int codec_init(fec_codec* c, int max_payload, int T, int B, int N) {
     HIP_TRY(hipMemcpy(c->d_ptab, ptab.data(), ptab.size() * 4, hipMemcpyHostToDevice));
     HIP_TRY(hipMalloc(&c->d_rules, std::max<size_t>(16, c->rules.table.size())));
     HIP_TRY(hipMemcpy(c->d_rules, c->rules.table.data(), c->rules.table.size(), hipMemcpyHostToDevice));
+    c->plan_fast = fec::fec_plan_fast_kernel_for(g.k, g.n - g.k);
+    if (c->plan_fast) {
+        // sel bytes unchanged; coefficient bytes (and padding) -> log2, 0 -> 0xff
+        std::vector<uint8_t> lt(c->rules.table);
+        const int ES = c->rules.entry_bytes;
+        for (size_t e = 0; e + ES <= lt.size(); e += ES)
+            for (int o = g.k; o < ES; ++o) lt[e + o] = lt[e + o] ? F.log[lt[e + o]] : 0xff;
+        HIP_TRY(hipMalloc(&c->d_rules_log, std::max<size_t>(16, lt.size())));
+        HIP_TRY(hipMemcpy(c->d_rules_log, lt.data(), lt.size(), hipMemcpyHostToDevice));
+    }
     std::vector<int64_t> wb(c->rules.w_base.begin(), c->rules.w_base.end());
     HIP_TRY(hipMalloc(&c->d_wbase, wb.size() * 8));
     HIP_TRY(hipMemcpy(c->d_wbase, wb.data(), wb.size() * 8, hipMemcpyHostToDevice));
@@ -323,9 +337,17 @@ int launch_plan(fec_codec* c, const uint8_t* d_er, int64_t P, void* d_ws, size_t
     pa.rs_bytes = fec::resync_state_bytes(g);
     pa.sym_ok = w.sym_ok;
     pa.coef = w.coef;
-    const int plan_lds = 768 + g.n * g.n + 2 * g.k * g.n;
     if (int st = c->begin(FEC_KERNEL_DEC_PLAN, s, &stop)) return st;
-    hipLaunchKernelGGL(fec::fec_plan_kernel, dim3(8192), dim3(64), plan_lds, s, pa);
+    const bool fast_ok = c->plan_fast && P < (int64_t(1) << 31) - 1024;
+    if (c->plan_path == 2 && !fast_ok) return FEC_ERR_ARG;
+    if (fast_ok && c->plan_path != 1) {
+        pa.rules = c->d_rules_log;
+        void* args[] = {&pa};
+        HIP_TRY(hipLaunchKernel(c->plan_fast, dim3(8192), dim3(64), args, 0, s));
+    } else {
+        const int plan_lds = 768 + g.n * g.n + 2 * g.k * g.n;
+        hipLaunchKernelGGL(fec::fec_plan_kernel, dim3(8192), dim3(64), plan_lds, s, pa);
+    }
     HIP_TRY(hipGetLastError());
     // packets with all k symbols recovered -> rec_list (timed with the plan)
     hipLaunchKernelGGL(fec::fec_compact_kernel, dim3(256), dim3(256), 0, s, w.counters, w.erased,
@@ -605,6 +627,13 @@ int fec_debug_stamps(fec_codec* c, int kernel, void* d_stamps) {
     if (!c) return FEC_ERR_ARG;
     c->stamp_kernel = d_stamps ? kernel : -1;
     c->d_stamps = static_cast<uint64_t*>(d_stamps);
+    return FEC_OK;
+}
+
+int fec_codec_set_plan_path(fec_codec* c, int path) {
+    if (!c || path < 0 || path > 2) return FEC_ERR_ARG;
+    if (path == 2 && !c->plan_fast) return FEC_ERR_ARG;
+    c->plan_path = path;
     return FEC_OK;
 }
 

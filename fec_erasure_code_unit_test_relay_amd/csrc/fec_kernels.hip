@@ -290,17 +290,24 @@ struct BlockReplay {
         // the whole rule entry {sel[k], col[k][n]} in one wave-wide load
         const uint32_t* ent = reinterpret_cast<const uint32_t*>(
             a->rules + a->wbase[w] + static_cast<int64_t>(m) * a->ES);
+        // entries reach 4*77 bytes (k = 15, n = 17): two dwords per lane
         const uint32_t ev = (lane < (a->ES >> 2)) ? ent[lane] : 0u;
+        const uint32_t ev2 = (lane + 64 < (a->ES >> 2)) ? ent[lane + 64] : 0u;
+        auto rd = [&](int idx) -> uint32_t {
+            const int d = idx >> 2;
+            const uint32_t wv = d < 64 ? __builtin_amdgcn_readlane(ev, d) : __builtin_amdgcn_readlane(ev2, d - 64);
+            return (wv >> ((idx & 3) * 8)) & 0xffu;
+        };
         uint32_t got = 0;
         for (int i = 0; i < k; ++i) {
             if (!((m >> i) & 1u)) continue;
-            const uint32_t sel = (__builtin_amdgcn_readlane(ev, i >> 2) >> ((i & 3) * 8)) & 0xffu;
+            const uint32_t sel = rd(i);
             if (sel == 0xffu) continue;
             uint8_t acc = 0;
             const int base = k + i * n;
             for (int c = 0; c < w; ++c) {
                 const int idx = base + c;
-                const uint32_t f = (__builtin_amdgcn_readlane(ev, idx >> 2) >> ((idx & 3) * 8)) & 0xffu;
+                const uint32_t f = rd(idx);
                 if (!f || ((m >> c) & 1u)) continue;
                 if (lane < n) acc ^= mul(static_cast<uint8_t>(f), cwc[c * n + lane]);
             }

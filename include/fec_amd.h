@@ -54,6 +54,8 @@ int fec_codec_geometry(const fec_codec *codec, int *k, int *n, int *S, int *CW);
 int fec_codec_set_encode_path(fec_codec *codec, int path);
 /* The same switch for the decoder's received-packet copy kernel. */
 int fec_codec_set_copy_path(fec_codec *codec, int path);
+/* The same switch for the decoder's planner (per-episode block replay). */
+int fec_codec_set_plan_path(fec_codec *codec, int path);
 /* Encoder::getG / Decoder::getG (src/Encoder.cpp:61, src/Decoder.cpp:68): k*n bytes row-major. */
 int fec_codec_generator(const fec_codec *codec, uint8_t *G);
 

@@ -102,10 +102,12 @@ def test_encode_variable_lengths_and_history(tbn, path):
     assert (torch.cat([cw1, cw2]).cpu().numpy() == ref).all()
 
 
-def gpu_round_trip(T, B, N, pattern, P, garbage=True, copy_path="auto"):
-    """GPU encode of packets 0..P+T-1, erase, GPU decode -> outputs for packets 0..P-1."""
+def gpu_round_trip(T, B, N, pattern, P, garbage=True, path="auto"):
+    """GPU encode of packets 0..P+T-1, erase, GPU decode -> outputs for packets 0..P-1.
+    path: kernel selection of the decoder's copy and planner ('auto' or 'generic')."""
     c = fec.Codec(L, T, B, N)
-    c.set_copy_path(copy_path)
+    c.set_copy_path(path)
+    c.set_plan_path(path)
     Pf = P + T
     pat = np.zeros(Pf, dtype=np.uint8)
     m = min(pattern.size, Pf)
@@ -126,16 +128,18 @@ DEC_CASES = [((10, 5, 2), "bin_erasure", 0, 8000), ((10, 3, 3), "bin_erasure", 0
              ((10, 9, 8), "erasure100", 0, 4000), ((10, 1, 1), "erasure10", 50000, 6000),
              ((10, 4, 3), "erasure80", 10000, 6000), ((10, 10, 10), "erasure90", 0, 3000),
              ((10, 0, 0), "erasure70", 0, 5000), ((10, 8, 4), "erasure60", 0, 5000),
-             ((12, 4, 2), "erasure100", 1000, 3000), ((4, 6, 2), "erasure100", 0, 3000)]
+             ((12, 4, 2), "erasure100", 1000, 3000), ((4, 6, 2), "erasure100", 0, 3000),
+             ((15, 2, 1), "erasure100", 0, 2000), ((16, 1, 1), "erasure90", 500, 2000),
+             ((10, 4, 4), "bin_erasure", 2000, 6000), ((10, 5, 5), "erasure80", 0, 4000)]
 
 
-@pytest.mark.parametrize("copy_path", ["generic", "auto"])
+@pytest.mark.parametrize("path", ["generic", "auto"])
 @pytest.mark.parametrize("tbn,pattern,start,P", DEC_CASES)
-def test_decode_bit_exact_vs_oracle(tbn, pattern, start, P, copy_path):
+def test_decode_bit_exact_vs_oracle(tbn, pattern, start, P, path):
     T, B, N = tbn
     pat = load_pattern(pattern)[start:start + P + T]
     ref = oracle.run_stream(L, T, B, N, P, pat, seed=SEED, want_data=True)
-    c, payload, out, ln, _ = gpu_round_trip(T, B, N, pat, P, copy_path=copy_path)
+    c, payload, out, ln, _ = gpu_round_trip(T, B, N, pat, P, path=path)
     assert (ln.cpu().numpy() == ref["out_len"]).all()
     assert (out.cpu().numpy() == ref["out_data"]).all()
     eps, rec, lost = c.counters()
