@@ -57,12 +57,14 @@ def lib() -> ctypes.CDLL:
     L.fec_codec_set_encode_path.argtypes = [vp, i32]
     L.fec_codec_set_copy_path.argtypes = [vp, i32]
     L.fec_codec_set_plan_path.argtypes = [vp, i32]
+    L.fec_codec_set_episode_dedup.argtypes = [vp, i32]
     L.fec_debug_stamps.argtypes = [vp, i32, vp]
     L.fec_encode_batch.argtypes = [vp, vp, vp, i64, i64, vp, vp, vp]
     L.fec_decode_workspace_bytes.restype = ctypes.c_size_t
     L.fec_decode_workspace_bytes.argtypes = [vp, i64]
     L.fec_decode_batch.argtypes = [vp, vp, vp, i64, vp, vp, vp, ctypes.c_size_t, vp]
     L.fec_decode_counters.argtypes = [vp, i64p, i64p, i64p]
+    L.fec_decode_plan_stats.argtypes = [vp, i64p, i64p]
     L.fec_decode_plan.argtypes = [vp, vp, i64, vp, ctypes.c_size_t, vp]
     L.fec_decode_apply.argtypes = [vp, vp, vp, i64, vp, vp, vp, ctypes.c_size_t, vp]
     L.fec_decode_copy.argtypes = [vp, vp, vp, i64, vp, vp, vp]
@@ -78,10 +80,10 @@ def lib() -> ctypes.CDLL:
     L.fec_plan_host.argtypes = [i32, i32, i32, i32, vp, i64, vp]
     L.fec_util_fill_payload.argtypes = [vp, i64, i64, i32, ctypes.c_uint64, vp]
     for name in ["fec_codec_create", "fec_codec_destroy", "fec_codec_set_encode_path",
-                 "fec_codec_set_copy_path", "fec_codec_set_plan_path", "fec_debug_stamps", "fec_codec_geometry",
+                 "fec_codec_set_copy_path", "fec_codec_set_plan_path", "fec_codec_set_episode_dedup", "fec_debug_stamps", "fec_codec_geometry",
                  "fec_codec_generator", "fec_encode_batch", "fec_decode_batch", "fec_decode_plan",
                  "fec_decode_apply", "fec_decode_copy", "fec_decode_recover",
-                 "fec_decode_counters", "fec_timing_enable", "fec_timing_collect",
+                 "fec_decode_counters", "fec_decode_plan_stats", "fec_timing_enable", "fec_timing_collect",
                  "fec_encoder_create", "fec_encoder_destroy", "fec_encoder_transmit",
                  "fec_decoder_create", "fec_decoder_destroy", "fec_decoder_receive",
                  "fec_plan_host", "fec_util_fill_payload"]:

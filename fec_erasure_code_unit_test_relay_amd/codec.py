@@ -73,6 +73,10 @@ class Codec:
         code = {"auto": 0, "generic": 1, "fast": 2}[path]
         check(lib().fec_codec_set_plan_path(self._h, code), "fec_codec_set_plan_path")
 
+    def set_episode_dedup(self, on: bool) -> None:
+        """Planner replays one episode per distinct loss shape (default) or every episode."""
+        check(lib().fec_codec_set_episode_dedup(self._h, int(bool(on))), "fec_codec_set_episode_dedup")
+
     # -- batched device-resident path -----------------------------------------------------------
     def encode(self, payload, lengths=None, history: int = 0, out=None, out_len=None):
         """Encode rows ``history..`` of ``payload`` ([rows, L] uint8 on the GPU).
@@ -169,6 +173,13 @@ class Codec:
                                        _ptr(ws), ws.numel(), _stream_handle(torch)),
               "fec_decode_recover")
         return out, out_len
+
+    def plan_stats(self):
+        """(replayed, filled) episodes of the last plan (synchronises the device)."""
+        v = [ctypes.c_int64() for _ in range(2)]
+        check(lib().fec_decode_plan_stats(_ptr(self._ws), *[ctypes.byref(x) for x in v]),
+              "fec_decode_plan_stats")
+        return tuple(int(x.value) for x in v)
 
     def counters(self):
         """(episodes, recovered, lost) of the last decode (synchronises the device)."""

@@ -51,6 +51,7 @@ struct fec_codec {
     int copyf_tp = 0;
     int copy_path = 0;           // 0 auto, 1 generic, 2 specialised
     int plan_path = 0;
+    int dedup = 1;               // episode-shape deduplication in the planner
     uint64_t* d_stamps = nullptr;  // diagnostics: phase stamps of the next specialised launch
     int stamp_kernel = -1;
     int copy_tp = 0;             // decode-copy tile
@@ -196,7 +197,9 @@ int codec_init(fec_codec* c, int max_payload, int T, int B, int N) {
 }
 
 struct WsLayout {
-    size_t counters, episodes, erased, sym_ok, rec_list, coef, total;
+    size_t counters, episodes, erased, sym_ok, rec_list, coef;
+    size_t ep_slot, ep_last, work, fill, keys, reps, total;
+    int tbits;
 };
 
 WsLayout ws_layout(const Geometry& g, int64_t P) {
@@ -208,7 +211,17 @@ WsLayout ws_layout(const Geometry& g, int64_t P) {
     w.sym_ok = w.erased + up(static_cast<size_t>(P) * 4);
     w.rec_list = w.sym_ok + up(static_cast<size_t>(P) * g.k);
     w.coef = w.rec_list + up(static_cast<size_t>(P) * 4);
-    w.total = w.coef + up(static_cast<size_t>(P) * g.k * g.n);
+    // episode starts are >= T+2 packets apart
+    const size_t maxep = static_cast<size_t>(P) / static_cast<size_t>(g.T + 2) + 2;
+    w.tbits = 8;
+    while ((size_t(1) << w.tbits) < 2 * maxep) ++w.tbits;
+    w.ep_slot = w.coef + up(static_cast<size_t>(P) * g.k * g.n);
+    w.ep_last = w.ep_slot + up(maxep * 4);
+    w.work = w.ep_last + up(maxep * 4);
+    w.fill = w.work + up(maxep * 4);
+    w.keys = w.fill + up(maxep * 4);
+    w.reps = w.keys + up((size_t(1) << w.tbits) * 8);
+    w.total = w.reps + up((size_t(1) << w.tbits) * 4);
     return w;
 }
 
@@ -219,14 +232,19 @@ struct Ws {
     uint8_t* sym_ok;
     int32_t* rec_list;
     uint8_t* coef;
+    int32_t *ep_slot, *ep_last, *work, *fill;
+    uint64_t* keys;
+    int32_t* reps;
+    int tbits;
 };
 
 Ws ws_carve(const Geometry& g, int64_t P, void* d_ws) {
     const WsLayout w = ws_layout(g, P);
     uint8_t* base = static_cast<uint8_t*>(d_ws);
-    return {reinterpret_cast<int32_t*>(base + w.counters), reinterpret_cast<int32_t*>(base + w.episodes),
-            reinterpret_cast<int32_t*>(base + w.erased), base + w.sym_ok,
-            reinterpret_cast<int32_t*>(base + w.rec_list), base + w.coef};
+    auto i32 = [&](size_t o) { return reinterpret_cast<int32_t*>(base + o); };
+    return {i32(w.counters), i32(w.episodes), i32(w.erased), base + w.sym_ok, i32(w.rec_list),
+            base + w.coef, i32(w.ep_slot), i32(w.ep_last), i32(w.work), i32(w.fill),
+            reinterpret_cast<uint64_t*>(base + w.keys), i32(w.reps), w.tbits};
 }
 
 int launch_encode_fast(fec_codec* c, const uint8_t* d_payload, const int32_t* d_len, int64_t history,
@@ -310,7 +328,10 @@ int launch_plan(fec_codec* c, const uint8_t* d_er, int64_t P, void* d_ws, size_t
     if (Pout <= 0) return FEC_OK;
     if (int st = check_ws(c, P, d_ws, ws_bytes)) return st;
     const Ws w = ws_carve(g, P, d_ws);
+    const bool fast_ok = c->plan_fast && P < (int64_t(1) << 31) - 1024;
+    if (c->plan_path == 2 && !fast_ok) return FEC_ERR_ARG;
     HIP_TRY(hipMemsetAsync(w.counters, 0, 64, s));
+    HIP_TRY(hipMemsetAsync(w.keys, 0, (size_t(1) << w.tbits) * 8, s));
     hipEvent_t stop;
     if (int st = c->begin(FEC_KERNEL_DEC_SCAN, s, &stop)) return st;
     const int64_t sblocks = std::min<int64_t>((P + 4095) / 4096, 2048);
@@ -318,6 +339,28 @@ int launch_plan(fec_codec* c, const uint8_t* d_er, int64_t P, void* d_ws, size_t
                        d_er, P, Pout, g.T, w.counters, w.episodes, w.erased);
     HIP_TRY(hipGetLastError());
     if (int st = c->end(stop, s)) return st;
+
+    fec::ShapeArgs sa;
+    sa.er = d_er;
+    sa.P = P;
+    sa.T = g.T;
+    sa.k = g.k;
+    sa.n = g.n;
+    sa.tbits = w.tbits;
+    sa.dedup = c->dedup;
+    sa.counters = w.counters;
+    sa.episodes = w.episodes;
+    sa.ep_slot = w.ep_slot;
+    sa.ep_last = w.ep_last;
+    sa.work = w.work;
+    sa.fill = w.fill;
+    sa.keys = w.keys;
+    sa.reps = w.reps;
+    sa.sym_ok = w.sym_ok;
+    sa.coef = w.coef;
+    if (int st = c->begin(FEC_KERNEL_DEC_PLAN, s, &stop)) return st;
+    hipLaunchKernelGGL(fec::fec_shape_kernel, dim3(4096), dim3(64), 0, s, sa);
+    HIP_TRY(hipGetLastError());
 
     fec::PlanArgs pa;
     pa.er = d_er;
@@ -333,13 +376,11 @@ int launch_plan(fec_codec* c, const uint8_t* d_er, int64_t P, void* d_ws, size_t
     pa.T = g.T;
     pa.counters = w.counters;
     pa.episodes = w.episodes;
+    pa.work = w.work;
     pa.rstate = c->d_rstate;
     pa.rs_bytes = fec::resync_state_bytes(g);
     pa.sym_ok = w.sym_ok;
     pa.coef = w.coef;
-    if (int st = c->begin(FEC_KERNEL_DEC_PLAN, s, &stop)) return st;
-    const bool fast_ok = c->plan_fast && P < (int64_t(1) << 31) - 1024;
-    if (c->plan_path == 2 && !fast_ok) return FEC_ERR_ARG;
     if (fast_ok && c->plan_path != 1) {
         pa.rules = c->d_rules_log;
         void* args[] = {&pa};
@@ -348,6 +389,8 @@ int launch_plan(fec_codec* c, const uint8_t* d_er, int64_t P, void* d_ws, size_t
         const int plan_lds = 768 + g.n * g.n + 2 * g.k * g.n;
         hipLaunchKernelGGL(fec::fec_plan_kernel, dim3(8192), dim3(64), plan_lds, s, pa);
     }
+    HIP_TRY(hipGetLastError());
+    hipLaunchKernelGGL(fec::fec_shape_fill_kernel, dim3(4096), dim3(64), 0, s, sa);
     HIP_TRY(hipGetLastError());
     // packets with all k symbols recovered -> rec_list (timed with the plan)
     hipLaunchKernelGGL(fec::fec_compact_kernel, dim3(256), dim3(256), 0, s, w.counters, w.erased,
@@ -623,10 +666,26 @@ int fec_decode_counters(const void* d_ws, int64_t* episodes, int64_t* recovered,
     return FEC_OK;
 }
 
+int fec_decode_plan_stats(const void* d_ws, int64_t* replayed, int64_t* filled) {
+    if (!d_ws) return FEC_ERR_ARG;
+    int32_t h[5];
+    HIP_TRY(hipDeviceSynchronize());
+    HIP_TRY(hipMemcpy(h, d_ws, sizeof(h), hipMemcpyDeviceToHost));
+    if (replayed) *replayed = h[3];
+    if (filled) *filled = h[4];
+    return FEC_OK;
+}
+
 int fec_debug_stamps(fec_codec* c, int kernel, void* d_stamps) {
     if (!c) return FEC_ERR_ARG;
     c->stamp_kernel = d_stamps ? kernel : -1;
     c->d_stamps = static_cast<uint64_t*>(d_stamps);
+    return FEC_OK;
+}
+
+int fec_codec_set_episode_dedup(fec_codec* c, int on) {
+    if (!c) return FEC_ERR_ARG;
+    c->dedup = on ? 1 : 0;
     return FEC_OK;
 }
 

@@ -97,12 +97,32 @@ struct PlanArgs {
     const uint8_t* gf;             // exp[512] then log[256]
     int ES;                        // decode-rule entry stride (bytes, multiple of 4)
     int k, n, T;
-    const int32_t* counters;       // [0] episodes
+    const int32_t* counters;       // [0] episodes, [3] episodes to replay
     const int32_t* episodes;
+    const int32_t* work;           // indices (into episodes) of the episodes to replay
     const uint8_t* rstate;         // post-resync block state per phase (build_resync_states)
     int rs_bytes;
     uint8_t* sym_ok;               // [P][k]: symbol i of erased packet x recovered
     uint8_t* coef;                 // [P][k][n]: coefficients of symbol i over its diagonal
+};
+
+// Episode-shape deduplication (fec_shapes.hip).
+struct ShapeArgs {
+    const uint8_t* er;
+    int64_t P;
+    int T, k, n;
+    int tbits;                     // log2 of the hash-table size
+    int dedup;                     // 0: every episode is replayed
+    int32_t* counters;             // [0] episodes (in), [3] replay count, [4] fill count (out)
+    const int32_t* episodes;
+    int32_t* ep_slot;              // [episodes] hash slot or -1
+    int32_t* ep_last;              // [episodes] latest erased packet
+    int32_t* work;                 // replay list
+    int32_t* fill;                 // fill list
+    uint64_t* keys;                // [2^tbits], zero = empty
+    int32_t* reps;                 // [2^tbits] representative episode of the slot
+    uint8_t* sym_ok;
+    uint8_t* coef;
 };
 
 struct RecArgs {
@@ -136,6 +156,8 @@ __global__ void fec_scan_kernel(const uint8_t* er, int64_t P, int64_t Pout, int 
 __global__ void fec_compact_kernel(int32_t* counters, const int32_t* erased, const uint8_t* sym_ok,
                                    int k, int32_t* rec_list);
 __global__ void fec_plan_kernel(PlanArgs a);
+__global__ void fec_shape_kernel(ShapeArgs a);
+__global__ void fec_shape_fill_kernel(ShapeArgs a);
 __global__ void fec_copy_kernel(CopyArgs a);
 __global__ void fec_recover_kernel(RecArgs a);
 __global__ void fec_stream_out_kernel(StreamOutArgs a);

@@ -388,9 +388,9 @@ __global__ __launch_bounds__(64) void fec_plan_kernel(PlanArgs a) {
     br.T = T;
     for (int i = lane; i < 768; i += 64) smem[i] = a.gf[i];
     __syncthreads();
-    const int64_t pairs = static_cast<int64_t>(a.counters[0]) * n;
+    const int64_t pairs = static_cast<int64_t>(a.counters[3]) * n;
     for (int64_t pr = blockIdx.x; pr < pairs; pr += gridDim.x) {
-        const int64_t tr = a.episodes[pr / n];
+        const int64_t tr = a.episodes[a.work[pr / n]];
         const int b = static_cast<int>(pr % n);
         if (tr < 0 || tr >= a.P) continue;  // defensive: the scan only lists packets of the batch
         if (tr >= T) {

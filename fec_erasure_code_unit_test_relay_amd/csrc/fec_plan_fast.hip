@@ -146,11 +146,11 @@ __global__ __launch_bounds__(64) void fec_plan_fast_kernel(PlanArgs a) {
     br.T = T;
     br.lane = lane;
     const int Pi = static_cast<int>(a.P), Pouti = static_cast<int>(a.Pout);  // P < 2^31 (host check)
-    const int pairs = a.counters[0] * N;
+    const int pairs = a.counters[3] * N;
     for (int pr = blockIdx.x; pr < pairs; pr += gridDim.x) {
         const int ep = pr / N;
         const int b = pr - ep * N;
-        const int tr = a.episodes[ep];
+        const int tr = a.episodes[a.work[ep]];
         if (tr < 0 || tr >= Pi) continue;
         if (tr >= T) {
             // resync at tr (Decoder.cpp:111-133) from the initial state, precomputed per phase

@@ -56,6 +56,9 @@ int fec_codec_set_encode_path(fec_codec *codec, int path);
 int fec_codec_set_copy_path(fec_codec *codec, int path);
 /* The same switch for the decoder's planner (per-episode block replay). */
 int fec_codec_set_plan_path(fec_codec *codec, int path);
+/* Planner: replay one episode per distinct loss shape and copy its results to the other episodes
+ * of that shape (default 1), or replay every episode (0).  Outputs are identical either way. */
+int fec_codec_set_episode_dedup(fec_codec *codec, int on);
 /* Encoder::getG / Decoder::getG (src/Encoder.cpp:61, src/Decoder.cpp:68): k*n bytes row-major. */
 int fec_codec_generator(const fec_codec *codec, uint8_t *G);
 
@@ -101,6 +104,9 @@ int fec_decode_recover(fec_codec *codec, const uint8_t *d_codeword, int64_t P,
 /* After the stream has finished the decode: erasure episodes, recovered and lost packets. */
 int fec_decode_counters(const void *d_workspace, int64_t *episodes, int64_t *recovered,
                         int64_t *lost);
+/* Planner statistics of the last plan in d_ws: episodes replayed and episodes filled from a
+ * replayed episode of the same loss shape (fec_codec_set_episode_dedup). */
+int fec_decode_plan_stats(const void *d_ws, int64_t *replayed, int64_t *filled);
 
 /* ---- per-kernel timing (HIP events recorded on the launch stream) --------------------------- */
 #define FEC_KERNEL_ENCODE 0

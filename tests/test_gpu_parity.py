@@ -102,12 +102,14 @@ def test_encode_variable_lengths_and_history(tbn, path):
     assert (torch.cat([cw1, cw2]).cpu().numpy() == ref).all()
 
 
-def gpu_round_trip(T, B, N, pattern, P, garbage=True, path="auto"):
+def gpu_round_trip(T, B, N, pattern, P, garbage=True, path="auto", dedup=True):
     """GPU encode of packets 0..P+T-1, erase, GPU decode -> outputs for packets 0..P-1.
-    path: kernel selection of the decoder's copy and planner ('auto' or 'generic')."""
+    path: kernel selection of the decoder's copy and planner ('auto' or 'generic');
+    dedup: planner replays one episode per loss shape (True) or every episode."""
     c = fec.Codec(L, T, B, N)
     c.set_copy_path(path)
     c.set_plan_path(path)
+    c.set_episode_dedup(dedup)
     Pf = P + T
     pat = np.zeros(Pf, dtype=np.uint8)
     m = min(pattern.size, Pf)
@@ -133,13 +135,13 @@ DEC_CASES = [((10, 5, 2), "bin_erasure", 0, 8000), ((10, 3, 3), "bin_erasure", 0
              ((10, 4, 4), "bin_erasure", 2000, 6000), ((10, 5, 5), "erasure80", 0, 4000)]
 
 
-@pytest.mark.parametrize("path", ["generic", "auto"])
+@pytest.mark.parametrize("path,dedup", [("generic", False), ("auto", False), ("auto", True)])
 @pytest.mark.parametrize("tbn,pattern,start,P", DEC_CASES)
-def test_decode_bit_exact_vs_oracle(tbn, pattern, start, P, path):
+def test_decode_bit_exact_vs_oracle(tbn, pattern, start, P, path, dedup):
     T, B, N = tbn
     pat = load_pattern(pattern)[start:start + P + T]
     ref = oracle.run_stream(L, T, B, N, P, pat, seed=SEED, want_data=True)
-    c, payload, out, ln, _ = gpu_round_trip(T, B, N, pat, P, path=path)
+    c, payload, out, ln, _ = gpu_round_trip(T, B, N, pat, P, path=path, dedup=dedup)
     assert (ln.cpu().numpy() == ref["out_len"]).all()
     assert (out.cpu().numpy() == ref["out_data"]).all()
     eps, rec, lost = c.counters()
@@ -205,6 +207,30 @@ def test_full_size_round_trip_1M():
     assert int(out[~ok].count_nonzero()) == 0
     eps, rec, nlost = c.counters()
     assert nlost == int(lost.sum()) and rec == int((fate == 2).sum())
+    replayed, filled = c.plan_stats()
+    assert replayed + filled == eps and filled > 0
+
+
+def test_episode_dedup_many_shapes():
+    """Dense random losses (thousands of distinct shapes, long and truncated episodes) with and
+    without deduplication: identical outputs, and equal to the host planner's fates."""
+    T, B, N = 10, 3, 3
+    P = 200_000
+    rng = np.random.default_rng(7)
+    pat = np.zeros(P + T, dtype=np.uint8)
+    for s in rng.integers(0, P + T, size=6000):  # bursts of random length and density
+        ln = int(rng.integers(1, 90))
+        pat[s:s + ln] |= (rng.random(min(ln, P + T - s)) < rng.uniform(0.2, 1.0)).astype(np.uint8)
+    pat[-5:] = 1  # an episode running into the batch end
+    res = []
+    for dedup in (False, True):
+        c, payload, out, ln, _ = gpu_round_trip(T, B, N, pat, P, garbage=False, dedup=dedup)
+        res.append((out.cpu().numpy(), ln.cpu().numpy(), c.counters(), c.plan_stats()))
+    assert (res[0][0] == res[1][0]).all() and (res[0][1] == res[1][1]).all()
+    assert res[0][2] == res[1][2]
+    assert res[0][3][1] == 0 and res[1][3][1] > 0
+    fate = fec.plan_host(L, T, B, N, pat)
+    assert ((res[1][1] == 0) == (fate == 3)).all()
 
 
 def test_streaming_api_matches_oracle():
