@@ -359,7 +359,9 @@ int launch_plan(fec_codec* c, const uint8_t* d_er, int64_t P, void* d_ws, size_t
     sa.sym_ok = w.sym_ok;
     sa.coef = w.coef;
     if (int st = c->begin(FEC_KERNEL_DEC_PLAN, s, &stop)) return st;
-    hipLaunchKernelGGL(fec::fec_shape_kernel, dim3(4096), dim3(64), 0, s, sa);
+    const int64_t maxep = P / (g.T + 2) + 2;  // ws_layout's bound on episode starts
+    hipLaunchKernelGGL(fec::fec_shape_kernel, dim3(static_cast<unsigned>(std::min<int64_t>((maxep + 255) / 256, 2048))),
+                       dim3(256), 0, s, sa);
     HIP_TRY(hipGetLastError());
 
     fec::PlanArgs pa;

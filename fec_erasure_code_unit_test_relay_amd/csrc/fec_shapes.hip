@@ -1,8 +1,9 @@
 // fec_shapes.hip -- loss-episode deduplication for the decode planner.
 //
 // An episode starts at an erased packet tr with no erasure in [tr-T-1, tr-1] (the decoder's
-// resynchronisation, Decoder.cpp:109-133) and lasts until T+1 packets after its latest erasure
-// have been received (Decoder.cpp:80-83).  Everything the planner derives for the episode's
+// resynchronisation, Decoder.cpp:109-133) and ends at the first received packet t with no erasure
+// in [t-T, t-1] (Decoder.cpp:80-83): packet latest+T+1 ends it only if it is received, an
+// erasure there continues the episode.  Everything the planner derives for the episode's
 // erased packets -- which symbols are recovered and their coefficient rows -- is a function of
 // the block states at tr and of the erasure flags inside the episode.  For tr >= T the block
 // state at tr is the post-resync state of the block's phase, and the phase of the block holding
@@ -11,7 +12,7 @@
 // results at equal offsets.
 //
 // Per batch (the table is cleared by every plan launch; nothing is carried between batches):
-//   fec_shape_kernel      one wave per episode: the shape (64-bit mask), hash-table insert;
+//   fec_shape_kernel      one thread per episode: the shape (64-bit mask), hash-table insert;
 //                         the first episode of a shape and every episode that cannot be keyed
 //                         (startup tr < T, span >= 64, or running into the batch end) go to the
 //                         replay work list, the others to the fill list;
@@ -22,67 +23,131 @@
 
 namespace fec {
 
-__global__ __launch_bounds__(64) void fec_shape_kernel(ShapeArgs a) {
-    const int lane = threadIdx.x;
+namespace {
+
+constexpr int kLocalSlots = 512;  // per-workgroup table (256 episodes per pass)
+
+__device__ __forceinline__ uint32_t shape_hash(uint64_t m, int bits) {
+    return static_cast<uint32_t>((m * 0x9E3779B97F4A7C15ull) >> (64 - bits));
+}
+
+// Wave-aggregated append of `item` for the lanes where `want` holds.
+__device__ __forceinline__ void wave_append(bool want, int32_t* counter, int32_t* list, int item) {
+    const uint64_t bal = __ballot(want);
+    if (!bal) return;
+    const int lane = threadIdx.x & 63;
+    const int leader = __builtin_ctzll(bal);
+    int base = 0;
+    if (lane == leader) base = atomicAdd(counter, __popcll(bal));
+    base = __shfl(base, leader);
+    if (want) list[base + __popcll(bal & ((uint64_t(1) << lane) - 1))] = item;
+}
+
+}  // namespace
+
+// One thread per episode.  Shapes are first deduplicated in a workgroup-local LDS table; only
+// the local representative of a shape touches the global table (one CAS per shape per
+// workgroup), so hot shapes do not serialise on one address.
+__global__ __launch_bounds__(256) void fec_shape_kernel(ShapeArgs a) {
+    __shared__ unsigned long long lkey[kLocalSlots];
+    __shared__ int32_t lslot[kLocalSlots];   // global slot of the local shape
+    __shared__ int32_t lrep[kLocalSlots];    // 1: the local representative won the global slot
+    const int tid = threadIdx.x;
     const int ne = a.counters[0];
     const int64_t TS = int64_t(1) << a.tbits;
-    for (int e = blockIdx.x; e < ne; e += gridDim.x) {
-        const int64_t tr = a.episodes[e];
-        // walk the episode in windows of 64 packets; positions relative to tr
-        int latest = 0;
+    for (int e0 = blockIdx.x * 256; e0 < ne; e0 += gridDim.x * 256) {
+        for (int i = tid; i < kLocalSlots; i += 256) lkey[i] = 0ull;
+        const int e = e0 + tid;
+        const bool valid = e < ne;
+        int64_t tr = 0, last = 0;
         uint64_t m = 1;
-        bool big = false, done = false, truncated = false;
-        for (int base = 1; !done; base += 64) {
-            const int64_t t = tr + base + lane;
-            const bool f = t < a.P && a.er[t] != 0;
-            uint64_t bits = __ballot(f);
-            while (bits) {
-                const int j = __builtin_ctzll(bits);
-                bits &= bits - 1;
-                const int pos = base + j;
-                if (pos - latest > a.T) {
+        bool keyed = false;
+        if (valid) {
+            tr = a.episodes[e];
+            // walk the episode: positions relative to tr, flags in windows of 64
+            int latest = 0;
+            bool big = false, done = false, truncated = false;
+            for (int base = 1; !done; base += 64) {
+                uint64_t fl = 0;
+#pragma unroll 16
+                for (int j = 0; j < 64; ++j) {
+                    const int64_t t = tr + base + j;
+                    if (t < a.P && a.er[t]) fl |= uint64_t(1) << j;
+                }
+                while (fl) {
+                    const int j = __builtin_ctzll(fl);
+                    fl &= fl - 1;
+                    const int pos = base + j;
+                    if (pos - latest > a.T + 1) {  // packet latest+T+1 was received: ended
+                        done = true;
+                        break;
+                    }
+                    latest = pos;
+                    if (pos < 64) m |= uint64_t(1) << pos;
+                    else big = true;
+                }
+                if (!done && latest + a.T + 1 <= base + 63) done = true;  // latest+T+1 seen, received
+                if (!done && tr + base + 64 >= a.P) {
                     done = true;
+                    truncated = true;
+                }
+            }
+            last = tr + latest;
+            a.ep_last[e] = static_cast<int32_t>(last);
+            keyed = a.dedup && tr >= a.T && !big && !truncated && last + a.T + 1 < a.P;
+        }
+        __syncthreads();
+        // local insert: the first thread of a shape in this workgroup is its local representative
+        int ls = -1;
+        bool lfirst = false;
+        if (keyed) {
+            uint32_t h = shape_hash(m, 9);
+            for (int probe = 0; probe < kLocalSlots; ++probe) {
+                const unsigned long long prev = atomicCAS(&lkey[h], 0ull, static_cast<unsigned long long>(m));
+                if (prev == 0ull || prev == m) {
+                    ls = static_cast<int>(h);
+                    lfirst = prev == 0ull;
                     break;
                 }
-                latest = pos;
-                if (pos < 64) m |= uint64_t(1) << pos;
-                else big = true;
-            }
-            if (!done && latest + a.T <= base + 63) done = true;  // the gap after latest is complete
-            if (!done && tr + base + 64 >= a.P) {
-                done = true;
-                truncated = true;
+                h = (h + 1) & (kLocalSlots - 1);
             }
         }
-        if (lane == 0) {
-            const int64_t last = tr + latest;
-            a.ep_last[e] = static_cast<int32_t>(last);
-            const bool keyed = a.dedup && tr >= a.T && !big && !truncated && last + a.T + 1 < a.P;
-            int32_t slot = -1;
-            bool rep = true;
-            if (keyed) {
-                int64_t h = static_cast<int64_t>((m * 0x9E3779B97F4A7C15ull) >> (64 - a.tbits));
-                // the table holds > 2x as many slots as a batch can have episodes: probing ends
-                for (int64_t probe = 0; probe < TS; ++probe) {
-                    const unsigned long long prev = atomicCAS(
-                        reinterpret_cast<unsigned long long*>(a.keys + h), 0ull, static_cast<unsigned long long>(m));
-                    if (prev == 0ull) {
-                        a.reps[h] = e;  // this episode represents the shape
-                        slot = static_cast<int32_t>(h);
-                        break;
-                    }
-                    if (prev == m) {
-                        rep = false;
-                        slot = static_cast<int32_t>(h);
-                        break;
-                    }
-                    h = (h + 1) & (TS - 1);
+        // global insert by the local representatives
+        if (lfirst) {
+            int64_t h = shape_hash(m, a.tbits);
+            int32_t gs = -1, won = 0;
+            for (int64_t probe = 0; probe < TS; ++probe) {  // the table has > 2x slots: ends
+                unsigned long long cur = __hip_atomic_load(reinterpret_cast<unsigned long long*>(a.keys + h),
+                                                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (cur == 0ull)
+                    cur = atomicCAS(reinterpret_cast<unsigned long long*>(a.keys + h), 0ull,
+                                    static_cast<unsigned long long>(m));
+                if (cur == 0ull) {
+                    a.reps[h] = e;
+                    gs = static_cast<int32_t>(h);
+                    won = 1;
+                    break;
                 }
+                if (cur == m) {
+                    gs = static_cast<int32_t>(h);
+                    break;
+                }
+                h = (h + 1) & (TS - 1);
             }
-            a.ep_slot[e] = slot;
-            if (rep) a.work[atomicAdd(&a.counters[3], 1)] = e;
-            else a.fill[atomicAdd(&a.counters[4], 1)] = e;
+            lslot[ls] = gs;
+            lrep[ls] = won;
         }
+        __syncthreads();
+        int32_t gslot = -1;
+        bool rep = valid;
+        if (keyed && ls >= 0) {
+            gslot = lslot[ls];
+            rep = lfirst && lrep[ls];
+        }
+        if (valid) a.ep_slot[e] = gslot;
+        wave_append(valid && rep, &a.counters[3], a.work, e);
+        wave_append(valid && !rep, &a.counters[4], a.fill, e);
+        __syncthreads();  // lkey is cleared for the next pass
     }
 }
 
