@@ -59,8 +59,9 @@ class Codec:
         return G.reshape(self.k, self.n)
 
     def set_encode_path(self, path: str) -> None:
-        """'auto', 'generic' or 'fast' (the k, n-k specialised kernel)."""
-        code = {"auto": 0, "generic": 1, "fast": 2}[path]
+        """'auto', 'generic', 'fast' (per-tile k, n-k specialised kernel) or 'stream' (the
+        persistent specialised kernel)."""
+        code = {"auto": 0, "generic": 1, "fast": 2, "stream": 3}[path]
         check(lib().fec_codec_set_encode_path(self._h, code), "fec_codec_set_encode_path")
 
     def set_copy_path(self, path: str) -> None:

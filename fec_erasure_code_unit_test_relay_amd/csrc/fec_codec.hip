@@ -2,6 +2,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <memory>
 #include <new>
@@ -46,6 +47,9 @@ struct fec_codec {
     int enc_tp = 0;              // encode tile (packets per workgroup), generic kernel
     int fast_tp = 0;             // encode tile of the specialised kernel (0: not available)
     const void* fast_kernel = nullptr;
+    const void* persist_kernel = nullptr;  // streaming encode (fec_encode_persist.hip)
+    int persist_tp = 0;
+    int persist_wgs = 0;                   // resident workgroups of it on the device
     int encode_path = 0;         // 0 auto, 1 generic, 2 specialised
     const void* copy_fast = nullptr;  // specialised decode copy kernel
     int copyf_tp = 0;
@@ -89,6 +93,11 @@ struct fec_codec {
     int fast_raw(int tp) const { return round16(std::max((tp + g.n - 1) * g.L + 32, tp * g.CW)); }
     int fast_xin(int tp) const { return g.k * ns4() * (tp + g.n - 1) * 4; }
     int fast_lds(int tp) const { return fast_raw(tp) + fast_xin(tp) + 4 * (tp + g.n - 1); }
+    // persistent encode: rows/output union, planes, row lengths, parity planes
+    int pers_raw(int tp) const { return round16(std::max({tp * g.L, tp * g.CW, (g.n - 1) * g.L})); }
+    int pers_lds(int tp) const {
+        return pers_raw(tp) + fast_xin(tp) + 4 * tp + 4 * (g.n - g.k) * ns4() * tp;
+    }
 
     int begin(int kernel, hipStream_t s, hipEvent_t* stop) {
         *stop = nullptr;
@@ -174,17 +183,44 @@ int codec_init(fec_codec* c, int max_payload, int T, int B, int N) {
             break;
         }
     if (!c->enc_tp || !c->copy_tp) return FEC_ERR_ARG;
+    // tuning overrides of the specialised kernels' largest tile (power of two, 8..64)
+    auto tile_cap = [](const char* name) {
+        const char* v = std::getenv(name);
+        const int t = v ? std::atoi(v) : 64;
+        return (t >= 8 && t <= 64) ? t : 64;
+    };
     if ((g.L & 3) == 0) c->fast_kernel = fec::fec_encode_fast_kernel_for(g.k, g.n - g.k);
     if (c->fast_kernel)
-        for (int tp = 64; tp >= 8; tp >>= 1)
+        for (int tp = tile_cap("FEC_ENCODE_TILE"); tp >= 8; tp >>= 1)
             if (c->fast_lds(tp) <= kLdsBudget) {
                 c->fast_tp = tp;
                 break;
             }
     if (!c->fast_tp) c->fast_kernel = nullptr;
+    if ((g.L & 3) == 0) c->persist_kernel = fec::fec_encode_persist_kernel_for(g.k, g.n - g.k);
+    if (c->persist_kernel) {
+        // tile: <= 64 packets, >= n-1 (halo carry), payload rows within the prefetch registers
+        // (6 x 16 bytes per thread), LDS within 80 KB (two workgroups per CU)
+        for (int tp = tile_cap("FEC_ENCODE_TILE"); tp >= 16; tp >>= 1)
+            if (c->pers_lds(tp) <= 80 * 1024 && tp * g.L <= 6 * 16 * 320 && tp >= g.n - 1) {
+                c->persist_tp = tp;
+                break;
+            }
+        int dev = 0, cus = 0, per_cu = 0;
+        if (c->persist_tp) {
+            HIP_TRY(hipGetDevice(&dev));
+            HIP_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+            HIP_TRY(hipFuncSetAttribute(c->persist_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                        c->pers_lds(c->persist_tp)));
+            HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, c->persist_kernel, 320,
+                                                                 c->pers_lds(c->persist_tp)));
+        }
+        c->persist_wgs = cus * per_cu;
+        if (!c->persist_tp || c->persist_wgs <= 0) c->persist_kernel = nullptr;
+    }
     if ((g.L & 3) == 0) c->copy_fast = fec::fec_copy_fast_kernel_for(g.k, g.n - g.k);
     if (c->copy_fast)
-        for (int tp = 64; tp >= 8; tp >>= 1)
+        for (int tp = tile_cap("FEC_COPY_TILE"); tp >= 8; tp >>= 1)
             if (c->copyf_lds(tp) <= kLdsBudget) {
                 c->copyf_tp = tp;
                 break;
@@ -277,10 +313,45 @@ int launch_encode_fast(fec_codec* c, const uint8_t* d_payload, const int32_t* d_
     return c->end(stop, s);
 }
 
+int launch_encode_persist(fec_codec* c, const uint8_t* d_payload, const int32_t* d_len, int64_t history,
+                          int64_t P, uint8_t* d_cw, int32_t* d_cwlen, hipStream_t s) {
+    const Geometry& g = c->g;
+    fec::EncFastArgs a;
+    a.payload = d_payload;
+    a.len = d_len;
+    a.history = std::max<int64_t>(0, history);
+    a.P = P;
+    a.cw = d_cw;
+    a.cw_len = d_cwlen;
+    a.ptab = c->d_ptab;
+    a.L = g.L;
+    a.S = g.S;
+    a.CW = g.CW;
+    a.NS4 = c->ns4();
+    a.TP = c->persist_tp;
+    a.ROWS = a.TP + g.n - 1;
+    a.raw_bytes = c->pers_raw(a.TP);
+    a.xin_bytes = c->fast_xin(a.TP);
+    a.stamps = nullptr;
+    const int64_t ntiles = (P + a.TP - 1) / a.TP;
+    a.tiles_per_wg = (ntiles + c->persist_wgs - 1) / c->persist_wgs;
+    const int64_t blocks = (ntiles + a.tiles_per_wg - 1) / a.tiles_per_wg;
+    hipEvent_t stop;
+    if (int st = c->begin(FEC_KERNEL_ENCODE, s, &stop)) return st;
+    void* args[] = {&a};
+    HIP_TRY(hipLaunchKernel(c->persist_kernel, dim3(static_cast<unsigned>(blocks)), dim3(320), args,
+                            c->pers_lds(a.TP), s));
+    return c->end(stop, s);
+}
+
 int launch_encode(fec_codec* c, const uint8_t* d_payload, const int32_t* d_len, int64_t history,
                   int64_t P, uint8_t* d_cw, int32_t* d_cwlen, hipStream_t s) {
     if (P <= 0) return FEC_OK;
     const Geometry& g = c->g;
+    const bool pers_ok = c->persist_kernel && (reinterpret_cast<uintptr_t>(d_payload) & 15) == 0;
+    if (c->encode_path == 3 && !pers_ok) return FEC_ERR_ARG;
+    if (pers_ok && (c->encode_path == 0 || c->encode_path == 3))
+        return launch_encode_persist(c, d_payload, d_len, history, P, d_cw, d_cwlen, s);
     const bool fast_ok = c->fast_kernel && (reinterpret_cast<uintptr_t>(d_payload) & 3) == 0;
     if (c->encode_path == 2 && !fast_ok) return FEC_ERR_ARG;
     if (fast_ok && c->encode_path != 1)
@@ -706,8 +777,9 @@ int fec_codec_set_copy_path(fec_codec* c, int path) {
 }
 
 int fec_codec_set_encode_path(fec_codec* c, int path) {
-    if (!c || path < 0 || path > 2) return FEC_ERR_ARG;
+    if (!c || path < 0 || path > 3) return FEC_ERR_ARG;
     if (path == 2 && !c->fast_kernel) return FEC_ERR_ARG;
+    if (path == 3 && !c->persist_kernel) return FEC_ERR_ARG;
     c->encode_path = path;
     return FEC_OK;
 }

@@ -54,7 +54,11 @@ struct EncFastArgs {
     int raw_bytes;              // LDS union of payload rows / output tile (16-aligned)
     int xin_bytes;              // LDS position planes
     uint64_t* stamps;           // diagnostics: per-workgroup phase timestamps (null = off)
+    int64_t tiles_per_wg;       // persistent kernel: contiguous tiles per workgroup
 };
+
+// fec_encode_persist_kernel<k, n-k> (fec_encode_persist.hip), else nullptr.  320 threads.
+const void* fec_encode_persist_kernel_for(int k, int np);
 
 // fec_encode_fast_kernel<k, n-k> for the instantiated pairs (fec_encode_fast.hip), else nullptr.
 const void* fec_encode_fast_kernel_for(int k, int np);

@@ -48,9 +48,11 @@ int fec_version(void);
 int fec_codec_create(int max_payload, int T, int B, int N, fec_codec **out);
 int fec_codec_destroy(fec_codec *codec);
 int fec_codec_geometry(const fec_codec *codec, int *k, int *n, int *S, int *CW);
-/* Encode kernel selection: 0 = automatic (the specialised kernel when one is compiled for
- * (k, n-k) and max_payload % 4 == 0), 1 = generic kernel, 2 = specialised kernel (FEC_ERR_ARG if
- * unavailable).  Both produce identical bytes; the switch exists for tests and A/B timing. */
+/* Encode kernel selection: 0 = automatic (the streaming kernel when one is compiled for
+ * (k, n-k), max_payload % 4 == 0 and the payload is 16-byte aligned, else the per-tile
+ * specialised kernel, else the generic one), 1 = generic kernel, 2 = per-tile specialised kernel,
+ * 3 = streaming (persistent) specialised kernel (FEC_ERR_ARG if unavailable).  All produce
+ * identical bytes; the switch exists for tests and A/B timing. */
 int fec_codec_set_encode_path(fec_codec *codec, int path);
 /* The same switch for the decoder's received-packet copy kernel. */
 int fec_codec_set_copy_path(fec_codec *codec, int path);

@@ -40,13 +40,16 @@ ENC_CONFIGS = [(10, 3, 3), (10, 5, 2), (10, 1, 1), (10, 0, 0), (10, 2, 2), (10, 
                (4, 6, 2), (12, 4, 2)]
 
 
-@pytest.mark.parametrize("path", ["generic", "auto"])
+@pytest.mark.parametrize("path", ["generic", "fast", "auto"])
 @pytest.mark.parametrize("tbn", ENC_CONFIGS)
 def test_encode_bit_exact(tbn, path):
     T, B, N = tbn
     P = 2500
     c = fec.Codec(L, T, B, N)
-    c.set_encode_path(path)
+    try:
+        c.set_encode_path(path)
+    except fec.FecError:
+        pytest.skip(f"no {path} kernel for {tbn}")
     payload = fec.fill_payload(0, P, L, SEED)
     cw, wl = c.encode(payload)
     ref = oracle.encode_stream(L, T, B, N, 0, P, seed=SEED)
@@ -58,14 +61,37 @@ def test_encode_bit_exact(tbn, path):
 def test_encode_fast_path_other_payload_sizes():
     """The specialised kernel with payload sizes other than 300 (L % 4 == 0) and a tiny batch."""
     for Lx, tbn, P in [(4, (10, 3, 3), 200), (64, (10, 5, 2), 300), (1500, (10, 3, 3), 130),
-                       (300, (10, 3, 3), 1), (300, (10, 1, 1), 7)]:
-        c = fec.Codec(Lx, *tbn)
-        c.set_encode_path("fast")
-        payload = fec.fill_payload(0, P, Lx, 11)
-        cw, wl = c.encode(payload)
+                       (300, (10, 3, 3), 1), (300, (10, 1, 1), 7), (1500, (10, 5, 2), 700)]:
         ref = oracle.encode_stream(Lx, *tbn, 0, P, seed=11)
-        assert (cw.cpu().numpy() == ref["cw"]).all(), (Lx, tbn)
-        assert (wl.cpu().numpy() == ref["cw_len"]).all(), (Lx, tbn)
+        for path in ("fast", "stream"):
+            c = fec.Codec(Lx, *tbn)
+            c.set_encode_path(path)
+            payload = fec.fill_payload(0, P, Lx, 11)
+            cw, wl = c.encode(payload)
+            assert (cw.cpu().numpy() == ref["cw"]).all(), (Lx, tbn, path)
+            assert (wl.cpu().numpy() == ref["cw_len"]).all(), (Lx, tbn, path)
+
+
+@pytest.mark.parametrize("tbn", [(10, 3, 3), (10, 5, 2), (10, 1, 1), (10, 10, 10), (10, 0, 0)])
+def test_encode_stream_many_tiles_per_workgroup(tbn):
+    """The persistent kernel carries plane rows from tile to tile inside a workgroup: compare it
+    with the per-tile kernel (itself checked against the oracle above) on a batch long enough for
+    tens of tiles per workgroup, with random lengths and a history window."""
+    P = 300_000
+    rng = np.random.default_rng(17)
+    lens = torch.from_numpy(rng.integers(0, L + 1, size=P).astype(np.int32)).cuda()
+    payload = fec.fill_payload(0, P, L, 23)
+    outs = []
+    for path in ("fast", "stream"):
+        c = fec.Codec(L, *tbn)
+        c.set_encode_path(path)
+        cw, wl = c.encode(payload, lens)
+        h = 64  # second half with a history window (row offsets stay 16-byte aligned)
+        cw2, wl2 = c.encode(payload[P // 2 - h:], lens[P // 2 - h:], history=h)
+        outs.append((cw, wl, cw2, wl2))
+    for a, b in zip(outs[0], outs[1]):
+        assert torch.equal(a, b)
+    assert torch.equal(outs[1][2], outs[1][0][P // 2:])
 
 
 def test_encode_digest_fixture(oracle_vectors):
@@ -77,7 +103,7 @@ def test_encode_digest_fixture(oracle_vectors):
         assert hashlib.sha256(wl.cpu().numpy().astype("<i4").tobytes()).hexdigest() == v["wire_len_sha256"]
 
 
-@pytest.mark.parametrize("path", ["generic", "fast"])
+@pytest.mark.parametrize("path", ["generic", "fast", "stream"])
 @pytest.mark.parametrize("tbn", [(10, 3, 3), (10, 5, 2), (10, 10, 10), (10, 9, 9), (10, 0, 0)])
 def test_encode_variable_lengths_and_history(tbn, path):
     T, B, N = tbn
@@ -91,12 +117,16 @@ def test_encode_variable_lengths_and_history(tbn, path):
     host = payload.cpu().numpy()
     ref = np.stack([enc.onTransmit(host[t], int(lens[t]), t)[0] for t in range(P)])
     c = fec.Codec(L, T, B, N)
-    c.set_encode_path(path)
+    try:
+        c.set_encode_path(path)
+    except fec.FecError:
+        pytest.skip(f"no {path} kernel for {tbn}")
     dl = torch.from_numpy(lens).cuda()
     cw, _ = c.encode(payload, dl)
     assert (cw.cpu().numpy() == ref).all()
-    # the same stream in two batches: the second sees 37 packets of history
-    h, cut = 37, 400
+    # the same stream in two batches: the second sees 36 packets of history (the slice start
+    # stays 16-byte aligned, which the streaming kernel requires)
+    h, cut = 36, 400
     cw1, _ = c.encode(payload[:cut], dl[:cut])
     cw2, _ = c.encode(payload[cut - h:], dl[cut - h:], history=h)
     assert (torch.cat([cw1, cw2]).cpu().numpy() == ref).all()

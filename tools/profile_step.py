@@ -17,12 +17,14 @@ ap = argparse.ArgumentParser()
 ap.add_argument("--packets", type=int, default=1_000_000)
 ap.add_argument("--iters", type=int, default=5)
 ap.add_argument("--tbn", default="10,3,3")
+ap.add_argument("--encode-path", default="auto")
 args = ap.parse_args()
 T, B, N = map(int, args.tbn.split(","))
 torch.cuda.set_device(0)
 P = args.packets
 Pf = P + T
 codec = Codec(L, T, B, N)
+codec.set_encode_path(args.encode_path)
 payload = fill_payload(0, Pf, L, 0x5EED)
 er = torch.from_numpy(stream_pattern(Pf, 0)).cuda()
 cw = torch.empty((Pf, codec.CW), dtype=torch.uint8, device="cuda")
