@@ -57,6 +57,7 @@ def lib() -> ctypes.CDLL:
     L.fec_codec_set_encode_path.argtypes = [vp, i32]
     L.fec_codec_set_copy_path.argtypes = [vp, i32]
     L.fec_codec_set_plan_path.argtypes = [vp, i32]
+    L.fec_codec_info.argtypes = [vp, ctypes.c_char_p, ctypes.c_size_t]
     L.fec_codec_set_episode_dedup.argtypes = [vp, i32]
     L.fec_debug_stamps.argtypes = [vp, i32, vp]
     L.fec_encode_batch.argtypes = [vp, vp, vp, i64, i64, vp, vp, vp]
@@ -80,7 +81,7 @@ def lib() -> ctypes.CDLL:
     L.fec_plan_host.argtypes = [i32, i32, i32, i32, vp, i64, vp]
     L.fec_util_fill_payload.argtypes = [vp, i64, i64, i32, ctypes.c_uint64, vp]
     for name in ["fec_codec_create", "fec_codec_destroy", "fec_codec_set_encode_path",
-                 "fec_codec_set_copy_path", "fec_codec_set_plan_path", "fec_codec_set_episode_dedup", "fec_debug_stamps", "fec_codec_geometry",
+                 "fec_codec_set_copy_path", "fec_codec_set_plan_path", "fec_codec_info", "fec_codec_set_episode_dedup", "fec_debug_stamps", "fec_codec_geometry",
                  "fec_codec_generator", "fec_encode_batch", "fec_decode_batch", "fec_decode_plan",
                  "fec_decode_apply", "fec_decode_copy", "fec_decode_recover",
                  "fec_decode_counters", "fec_decode_plan_stats", "fec_timing_enable", "fec_timing_collect",

@@ -69,6 +69,13 @@ class Codec:
         code = {"auto": 0, "generic": 1, "fast": 2}[path]
         check(lib().fec_codec_set_copy_path(self._h, code), "fec_codec_set_copy_path")
 
+    def info(self) -> dict:
+        """Kernel configuration chosen for this codec on this device."""
+        import json
+        buf = ctypes.create_string_buffer(512)
+        check(lib().fec_codec_info(self._h, buf, 512), "fec_codec_info")
+        return json.loads(buf.value.decode())
+
     def set_plan_path(self, path: str) -> None:
         """'auto', 'generic' or 'fast' for the decoder's planner."""
         code = {"auto": 0, "generic": 1, "fast": 2}[path]

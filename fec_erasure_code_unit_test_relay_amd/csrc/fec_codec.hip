@@ -2,6 +2,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <memory>
@@ -201,11 +202,13 @@ int codec_init(fec_codec* c, int max_payload, int T, int B, int N) {
     if (c->persist_kernel) {
         // tile: <= 64 packets, >= n-1 (halo carry), payload rows within the prefetch registers
         // (6 x 16 bytes per thread), LDS within 80 KB (two workgroups per CU)
-        for (int tp = tile_cap("FEC_ENCODE_TILE"); tp >= 16; tp >>= 1)
-            if (c->pers_lds(tp) <= 80 * 1024 && tp * g.L <= 6 * 16 * 320 && tp >= g.n - 1) {
-                c->persist_tp = tp;
-                break;
-            }
+        // (or, for large codewords, the smallest valid tile within 150 KB: one workgroup per CU)
+        for (int budget : {80 * 1024, 150 * 1024}) {
+            for (int tp = tile_cap("FEC_ENCODE_TILE"); tp >= 16 && !c->persist_tp; tp >>= 1)
+                if (c->pers_lds(tp) <= budget && tp * g.L <= 6 * 16 * 320 && tp >= g.n - 1)
+                    c->persist_tp = tp;
+            if (c->persist_tp) break;
+        }
         int dev = 0, cus = 0, per_cu = 0;
         if (c->persist_tp) {
             HIP_TRY(hipGetDevice(&dev));
@@ -332,7 +335,7 @@ int launch_encode_persist(fec_codec* c, const uint8_t* d_payload, const int32_t*
     a.ROWS = a.TP + g.n - 1;
     a.raw_bytes = c->pers_raw(a.TP);
     a.xin_bytes = c->fast_xin(a.TP);
-    a.stamps = nullptr;
+    a.stamps = (c->stamp_kernel == FEC_KERNEL_ENCODE) ? c->d_stamps : nullptr;
     const int64_t ntiles = (P + a.TP - 1) / a.TP;
     a.tiles_per_wg = (ntiles + c->persist_wgs - 1) / c->persist_wgs;
     const int64_t blocks = (ntiles + a.tiles_per_wg - 1) / a.tiles_per_wg;
@@ -736,6 +739,17 @@ int fec_decode_counters(const void* d_ws, int64_t* episodes, int64_t* recovered,
     if (episodes) *episodes = h[0];
     if (recovered) *recovered = h[2];
     if (lost) *lost = h[1] - h[2];  // erased outputs that were not recovered
+    return FEC_OK;
+}
+
+int fec_codec_info(const fec_codec* c, char* buf, size_t size) {
+    if (!c || !buf || size == 0) return FEC_ERR_ARG;
+    std::snprintf(buf, size,
+                  "{\"k\": %d, \"n\": %d, \"S\": %d, \"CW\": %d, \"encode_tile\": %d, "
+                  "\"encode_stream_tile\": %d, \"encode_stream_workgroups\": %d, "
+                  "\"encode_stream_lds\": %d, \"copy_tile\": %d, \"plan_specialised\": %d}",
+                  c->g.k, c->g.n, c->g.S, c->g.CW, c->fast_tp, c->persist_tp, c->persist_wgs,
+                  c->persist_tp ? c->pers_lds(c->persist_tp) : 0, c->copyf_tp, c->plan_fast ? 1 : 0);
     return FEC_OK;
 }
 

@@ -63,6 +63,20 @@ __device__ __forceinline__ void transpose_rows(const uint32_t* raw32, const int3
     }
 }
 
+// native 16-byte vector (HIP's uint4 class keeps arrays of it in scratch memory)
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+// 16-byte chunks q*nth + tid (q < kPrefetchMax, chunk < nch) of a tile into registers.
+__device__ __forceinline__ void prefetch_tile(u32x4 (&pf)[kPrefetchMax], const uint8_t* tile, int nch,
+                                              int tid, int nth) {
+    const u32x4* g = reinterpret_cast<const u32x4*>(tile);
+#pragma clang loop unroll(full)
+    for (int q = 0; q < kPrefetchMax; ++q) {
+        const int c = q * nth + tid;
+        pf[q] = g[c < nch ? c : nch - 1];  // unconditional: keeps pf[] in registers
+    }
+}
+
 // Selectors of v_perm_b32 for the three tables of gf_mul4x.
 struct Sel3 {
     uint32_t s0, s1, s2;
@@ -145,6 +159,17 @@ __global__ __launch_bounds__(kPersistThreads) void fec_encode_persist_kernel(Enc
     const int64_t tb = static_cast<int64_t>(blockIdx.x) * a.tiles_per_wg;
     const int64_t te = min<int64_t>(ntiles, tb + a.tiles_per_wg);
     if (tb >= te) return;
+    // diagnostics: cycles per phase summed over the workgroup's tiles (thread 0, s_memtime)
+    uint64_t ph[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    uint64_t tprev = a.stamps ? __builtin_amdgcn_s_memtime() : 0;
+    const uint64_t tstart = tprev;
+    auto mark = [&](int k) {
+        if (a.stamps) {
+            const uint64_t now = __builtin_amdgcn_s_memtime();
+            ph[k] += now - tprev;
+            tprev = now;
+        }
+    };
     for (int q = tid; q < K * NP * 2; q += nth) tabs[q] = reinterpret_cast<const uint4*>(a.ptab)[q];
 
     // ---- prologue: the n-1 rows in front of the range -> plane rows [0, H)
@@ -169,49 +194,42 @@ __global__ __launch_bounds__(kPersistThreads) void fec_encode_persist_kernel(Enc
         __syncthreads();
         transpose_rows<K>(raw32, rowlen, xin, H, 0, L, NS4, ROWS, tid, nth);
     }
+    mark(0);
 
-    // prefetch registers: chunk q of this thread = 16-byte chunk (q * nth + tid) of the tile
-    uint4 pf[kPrefetchMax];
-    auto prefetch = [&](int64_t tile) {
-        const int64_t t0 = tile * TP;
-        const int bytes = static_cast<int>(min<int64_t>(TP, a.P - t0)) * L;
-        const uint8_t* g = a.payload + t0 * L;
-#pragma unroll
-        for (int q = 0; q < kPrefetchMax; ++q) {
-            const int o = (q * nth + tid) * 16;
-            if (o + 16 <= bytes) {
-                pf[q] = *reinterpret_cast<const uint4*>(g + o);
-            } else if (o < bytes) {  // L % 4 == 0: the tile ends on a dword
-                const uint32_t* g4 = reinterpret_cast<const uint32_t*>(g + o);
-                const int nd = (bytes - o) >> 2;
-                pf[q] = make_uint4(g4[0], nd > 1 ? g4[1] : 0u, nd > 2 ? g4[2] : 0u, 0u);
-            }
-        }
-    };
-    prefetch(tb);
+    // prefetch registers (full tiles only, TP*L % 16 == 0): 16-byte chunk q*nth + tid of the tile
+    const int64_t full_end = a.P / TP;  // tiles [0, full_end) are full
+    const int nch = (TP * L) >> 4;
+    u32x4 pf[kPrefetchMax];
+    if (tb < full_end) prefetch_tile(pf, a.payload + tb * TP * L, nch, tid, nth);
 
     for (int64_t tile = tb; tile < te; ++tile) {
         const int64_t t0 = tile * TP;
         const int ntile = static_cast<int>(min<int64_t>(TP, a.P - t0));
         __syncthreads();  // the previous tile's output (aliasing raw) has left LDS; halo copied
-        {
-            const int bytes = ntile * L;
-#pragma unroll
+        if (tile < full_end) {
+            u32x4* raw4 = reinterpret_cast<u32x4*>(raw);
+#pragma clang loop unroll(full)
             for (int q = 0; q < kPrefetchMax; ++q) {
-                const int o = (q * nth + tid) * 16;
-                if (o < bytes) *reinterpret_cast<uint4*>(raw + o) = pf[q];
+                const int c = q * nth + tid;
+                if (c < nch) raw4[c] = pf[q];
             }
-            for (int r = tid; r < ntile; r += nth) {
-                int ln = a.len ? a.len[t0 + r] : L;
-                rowlen[r] = ln < 0 ? 0 : (ln > L ? L : ln);
-            }
+        } else {  // the stream's last, partial tile: direct dword loads (L % 4 == 0)
+            const uint32_t* g4 = reinterpret_cast<const uint32_t*>(a.payload + t0 * L);
+            for (int o = tid; o < (ntile * L) >> 2; o += nth) raw32[o] = g4[o];
         }
-        if (tile + 1 < te) prefetch(tile + 1);
+        for (int r = tid; r < ntile; r += nth) {
+            int ln = a.len ? a.len[t0 + r] : L;
+            rowlen[r] = ln < 0 ? 0 : (ln > L ? L : ln);
+        }
+        if (tile + 1 < te && tile + 1 < full_end)
+            prefetch_tile(pf, a.payload + (tile + 1) * TP * L, nch, tid, nth);
         __syncthreads();
+        mark(1);
 
         // B. new rows -> plane rows [H, H + ntile)
         transpose_rows<K>(raw32, rowlen, xin, ntile, H, L, NS4, ROWS, tid, nth);
         __syncthreads();
+        mark(2);
 
         // C1. parity words of two consecutive packets (2p, 2p+1) of group g per item.  Packet t
         // reads plane i at rows t + H - (K + jj - i) = t + i + NP - 1 - jj: for the pair, rows
@@ -255,6 +273,7 @@ __global__ __launch_bounds__(kPersistThreads) void fec_encode_persist_kernel(Enc
             }
             __syncthreads();
         }
+        mark(3);
 
         // C2. codeword interleave of each (packet, group) into the LDS output tile
         for (int it = tid; it < NS4 * ntile; it += nth) {
@@ -269,6 +288,7 @@ __global__ __launch_bounds__(kPersistThreads) void fec_encode_persist_kernel(Enc
             write_group<K, NP>(xout, src, t * CW + 4 * n * g, min(4 * n, CW - 4 * n * g));
         }
         __syncthreads();
+        mark(4);
 
         // D. tile out + trimmed wire sizes (FEC_Encoder.cpp:55-60); halo planes for the next tile
         const int bytes = ntile * CW;
@@ -292,6 +312,13 @@ __global__ __launch_bounds__(kPersistThreads) void fec_encode_persist_kernel(Enc
                 xin[pl * ROWS + r] = xin[pl * ROWS + TP + r];
             }
         }
+        mark(5);
+    }
+    if (a.stamps && tid == 0) {
+        uint64_t* st = a.stamps + static_cast<int64_t>(blockIdx.x) * 8;
+        for (int k = 0; k < 6; ++k) st[k] = ph[k];
+        st[6] = __builtin_amdgcn_s_memtime() - tstart;
+        st[7] = static_cast<uint64_t>(te - tb);
     }
 }
 

@@ -48,6 +48,9 @@ int fec_version(void);
 int fec_codec_create(int max_payload, int T, int B, int N, fec_codec **out);
 int fec_codec_destroy(fec_codec *codec);
 int fec_codec_geometry(const fec_codec *codec, int *k, int *n, int *S, int *CW);
+/* Kernel configuration chosen for this codec and device (tiles, resident workgroups), as a JSON
+ * object written to buf (NUL-terminated, truncated to size). */
+int fec_codec_info(const fec_codec *codec, char *buf, size_t size);
 /* Encode kernel selection: 0 = automatic (the streaming kernel when one is compiled for
  * (k, n-k), max_payload % 4 == 0 and the payload is 16-byte aligned, else the per-tile
  * specialised kernel, else the generic one), 1 = generic kernel, 2 = per-tile specialised kernel,

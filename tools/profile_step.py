@@ -37,4 +37,4 @@ for _ in range(args.iters):
     codec.copy(cw, er, out=out, out_len=ol)
     codec.recover(cw, out, ol)
 torch.cuda.synchronize()
-print("ok", codec.counters())
+print("ok", codec.counters(), codec.info())
