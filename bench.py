@@ -20,25 +20,30 @@ import os
 import sys
 import time
 
-import numpy as np
+import numpy as np  # noqa: F401
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
+
+from fec_erasure_code_unit_test_relay_amd.streams import (max_over_ranks, reduce_counters,  # noqa: E402
+                                                            stream_pattern, stream_seed)
 
 L = 300
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak, /opt/skills/guides/MI355X_MICROARCH.md
 
 
-def load_pattern(name="bin_erasure"):
-    z = np.load(os.path.join(ROOT, "tests", "golden", "erasure_patterns.npz"))
-    return np.unpackbits(z[name])[: int(z[name + "_len"][0])].astype(np.uint8)
-
-
-def stream_pattern(P_fed, rank):
-    """bin/erasure.bin's first 360000 packets, replayed cyclically; each rank starts at its own
-    phase so that the streams differ."""
-    base = load_pattern("bin_erasure")[:360000]
-    return np.roll(np.resize(base, P_fed + 36000 * rank), -36000 * rank)[:P_fed].copy()
+def pmc_traffic(kernel_symbol):
+    """HBM bytes per launch of `kernel_symbol` from the newest committed rocprofv3 FETCH_SIZE /
+    WRITE_SIZE passes (profiles/*/*_traffic.json, made by tools/pmc_traffic.{sh,py} over the same
+    step at the same size); None when no pass covers this kernel."""
+    import glob
+    best = None
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*", "*_traffic.json"))):
+        with open(path) as f:
+            entry = json.load(f).get(kernel_symbol)
+        if entry:
+            best = (entry["traffic_bytes"], os.path.relpath(path, ROOT))
+    return best
 
 
 def cpu_baseline(T, B, N, packets, rank_pattern):
@@ -84,7 +89,7 @@ def main():
     P = args.packets
     Pf = P + T  # fed packets: the last T only complete the outputs of packets P-T..P-1
     codec = Codec(L, T, B, N)
-    seed = 0x5EED + rank
+    seed = stream_seed(rank)
     pat = stream_pattern(Pf, rank)
     payload = fill_payload(0, Pf, L, seed)
     er = torch.from_numpy(pat).cuda()
@@ -125,10 +130,7 @@ def main():
     barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    elapsed = max_over_ranks(elapsed, dist, "cuda")
 
     # correctness of the timed work (outside the timed region): round trip + planner agreement
     eps, rec, lost = codec.counters()
@@ -136,11 +138,9 @@ def main():
     ok_rows = ~lost_mask
     verified = bool(torch.equal(out[ok_rows], payload[:P][ok_rows])) and \
         int((ol[ok_rows] != L).sum()) == 0 and int(lost_mask.sum()) == lost
-    stats = torch.tensor([rec, lost, int(pat[:P].sum()), int(verified)], dtype=torch.int64,
-                         device="cuda")
-    if world > 1:
-        dist.all_reduce(stats)  # trivial counter reduction over RCCL
-    rec_all, lost_all, erased_all, verified_all = (int(x) for x in stats.tolist())
+    # trivial counter reduction over RCCL
+    rec_all, lost_all, erased_all, verified_all = reduce_counters(
+        [rec, lost, int(pat[:P].sum()), int(verified)], dist, "cuda")
 
     # per-kernel durations: HIP events on the launch stream, separate pass
     codec.timing(True)
@@ -185,6 +185,12 @@ def main():
                          "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None},
         }
+        symbol = codec.info()["encode_kernel"] if dominant == "fec_encode_kernel" else None
+        tr = pmc_traffic(symbol) if symbol and P == 1_000_000 else None
+        if tr:
+            result["roofline"].update(traffic=tr[0], traffic_unit="bytes per launch",
+                                      algorithmic_bytes=algo[dominant], traffic_kernel=symbol,
+                                      traffic_source=tr[1])
     if world == 1 and not args.no_host_inclusive:
         # end-to-end from/to host memory (pinned): H2D payload, encode, D2H wire codewords,
         # H2D codewords + erasures, decode, D2H payloads + lengths

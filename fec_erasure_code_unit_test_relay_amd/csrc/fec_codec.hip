@@ -744,11 +744,21 @@ int fec_decode_counters(const void* d_ws, int64_t* episodes, int64_t* recovered,
 
 int fec_codec_info(const fec_codec* c, char* buf, size_t size) {
     if (!c || !buf || size == 0) return FEC_ERR_ARG;
+    // kernel symbol the encoder launches for a 16-byte aligned payload (rocprofv3 naming)
+    char enc[64];
+    const int np = c->g.n - c->g.k;
+    if (c->persist_kernel && (c->encode_path == 0 || c->encode_path == 3))
+        std::snprintf(enc, sizeof(enc), "fec_encode_persist_kernel<%d, %d>", c->g.k, np);
+    else if (c->fast_kernel && c->encode_path != 1)
+        std::snprintf(enc, sizeof(enc), "fec_encode_fast_kernel<%d, %d>", c->g.k, np);
+    else
+        std::snprintf(enc, sizeof(enc), "fec_encode_kernel");
     std::snprintf(buf, size,
-                  "{\"k\": %d, \"n\": %d, \"S\": %d, \"CW\": %d, \"encode_tile\": %d, "
+                  "{\"k\": %d, \"n\": %d, \"S\": %d, \"CW\": %d, \"encode_kernel\": \"%s\", "
+                  "\"encode_tile\": %d, "
                   "\"encode_stream_tile\": %d, \"encode_stream_workgroups\": %d, "
                   "\"encode_stream_lds\": %d, \"copy_tile\": %d, \"plan_specialised\": %d}",
-                  c->g.k, c->g.n, c->g.S, c->g.CW, c->fast_tp, c->persist_tp, c->persist_wgs,
+                  c->g.k, c->g.n, c->g.S, c->g.CW, enc, c->fast_tp, c->persist_tp, c->persist_wgs,
                   c->persist_tp ? c->pers_lds(c->persist_tp) : 0, c->copyf_tp, c->plan_fast ? 1 : 0);
     return FEC_OK;
 }
