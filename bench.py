@@ -71,6 +71,7 @@ def main():
     ap.add_argument("--cpu-packets", type=int, default=60000)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-host-inclusive", action="store_true")
+    ap.add_argument("--encode-path", default="auto", help="A/B: auto|generic|fast|stream|wave")
     args = ap.parse_args()
     T, B, N = map(int, args.tbn.split(","))
 
@@ -89,6 +90,8 @@ def main():
     P = args.packets
     Pf = P + T  # fed packets: the last T only complete the outputs of packets P-T..P-1
     codec = Codec(L, T, B, N)
+    if args.encode_path != "auto":
+        codec.set_encode_path(args.encode_path)
     seed = stream_seed(rank)
     pat = stream_pattern(Pf, rank)
     payload = fill_payload(0, Pf, L, seed)

@@ -51,7 +51,9 @@ struct fec_codec {
     const void* persist_kernel = nullptr;  // streaming encode (fec_encode_persist.hip)
     int persist_tp = 0;
     int persist_wgs = 0;                   // resident workgroups of it on the device
-    int encode_path = 0;         // 0 auto, 1 generic, 2 specialised
+    int encode_path = 0;         // 0 auto, 1 generic, 2 specialised, 3 streaming, 4 wave
+    const void* wave_kernel = nullptr;  // wave-private sequence encode (fec_encode_wave.hip)
+    int wave_slots = 0;                 // resident waves of it on the device
     const void* copy_fast = nullptr;  // specialised decode copy kernel
     int copyf_tp = 0;
     int copy_path = 0;           // 0 auto, 1 generic, 2 specialised
@@ -221,6 +223,16 @@ int codec_init(fec_codec* c, int max_payload, int T, int B, int N) {
         c->persist_wgs = cus * per_cu;
         if (!c->persist_tp || c->persist_wgs <= 0) c->persist_kernel = nullptr;
     }
+    if ((g.L & 3) == 0 && (g.S + 3) / 4 <= 64)
+        c->wave_kernel = fec::fec_encode_wave_kernel_for(g.k, g.n - g.k);
+    if (c->wave_kernel) {
+        int dev = 0, cus = 0, per_cu = 0;
+        HIP_TRY(hipGetDevice(&dev));
+        HIP_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+        HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, c->wave_kernel, 256, 0));
+        c->wave_slots = cus * per_cu * 4;
+        if (c->wave_slots <= 0) c->wave_kernel = nullptr;
+    }
     if ((g.L & 3) == 0) c->copy_fast = fec::fec_copy_fast_kernel_for(g.k, g.n - g.k);
     if (c->copy_fast)
         for (int tp = tile_cap("FEC_COPY_TILE"); tp >= 8; tp >>= 1)
@@ -347,10 +359,66 @@ int launch_encode_persist(fec_codec* c, const uint8_t* d_payload, const int32_t*
     return c->end(stop, s);
 }
 
+int launch_encode_wave(fec_codec* c, const uint8_t* d_payload, const int32_t* d_len, int64_t history,
+                       int64_t P, uint8_t* d_cw, int32_t* d_cwlen, hipStream_t s) {
+    const Geometry& g = c->g;
+    history = std::max<int64_t>(0, history);
+    // the kernel addresses rows [-history, P) with 32-bit buffer offsets: batches beyond 2 GB of
+    // payload go in chunks (each sees the n-1 rows in front of it as history)
+    const int64_t max_rows = (int64_t(0x7fffffff) - 4096) / std::max(g.L, g.CW) - g.n;
+    if (history + P > max_rows) {
+        const int64_t chunk = max_rows - g.n;
+        for (int64_t r = 0; r < P; r += chunk) {
+            const int64_t h = r == 0 ? history : std::min<int64_t>(history + r, g.n - 1);
+            if (int st = launch_encode_wave(c, d_payload + r * g.L, d_len ? d_len + r : nullptr, h,
+                                            std::min(chunk, P - r), d_cw + r * g.CW, d_cwlen + r, s))
+                return st;
+        }
+        return FEC_OK;
+    }
+    fec::EncWaveArgs a;
+    a.payload_base = d_payload - history * g.L;
+    a.len_base = d_len ? d_len - history : nullptr;
+    a.payload_bytes = static_cast<int>((history + P) * g.L);
+    a.len_bytes = static_cast<int>((history + P) * 4);
+    a.history = static_cast<int>(history);
+    a.P = static_cast<int>(P);
+    a.cw = d_cw;
+    a.cw_bytes = static_cast<int>(P * g.CW);
+    a.cw_len = d_cwlen;
+    a.ptab = c->d_ptab;
+    a.L = g.L;
+    a.S = g.S;
+    a.CW = g.CW;
+    a.NS4 = c->ns4();
+    a.SPW = 64 / a.NS4;
+    a.rem = g.S - 4 * (a.NS4 - 1);
+    // sequence length: enough sequences for every resident wave slot, a multiple of 4 packets
+    const int64_t slots = static_cast<int64_t>(c->wave_slots) * a.SPW;
+    int64_t M = (P + slots - 1) / slots;
+    if (const char* v = std::getenv("FEC_WAVE_M")) M = std::max<int64_t>(M, std::atoll(v));
+    M = std::max<int64_t>(4, (M + 3) & ~int64_t(3));
+    a.M = static_cast<int>(M);
+    a.nseq = static_cast<int>((P + M - 1) / M);
+    const int64_t waves = (a.nseq + a.SPW - 1) / a.SPW;
+    const int64_t blocks = (waves + 3) / 4;
+    hipEvent_t stop;
+    if (int st = c->begin(FEC_KERNEL_ENCODE, s, &stop)) return st;
+    void* args[] = {&a};
+    HIP_TRY(hipLaunchKernel(c->wave_kernel, dim3(static_cast<unsigned>(blocks)), dim3(256), args, 0, s));
+    return c->end(stop, s);
+}
+
 int launch_encode(fec_codec* c, const uint8_t* d_payload, const int32_t* d_len, int64_t history,
                   int64_t P, uint8_t* d_cw, int32_t* d_cwlen, hipStream_t s) {
     if (P <= 0) return FEC_OK;
     const Geometry& g = c->g;
+    const bool wave_ok = c->wave_kernel && (reinterpret_cast<uintptr_t>(d_payload) & 3) == 0 &&
+                         (reinterpret_cast<uintptr_t>(d_cw) & 3) == 0;
+    if (c->encode_path == 4) {
+        if (!wave_ok) return FEC_ERR_ARG;
+        return launch_encode_wave(c, d_payload, d_len, history, P, d_cw, d_cwlen, s);
+    }
     const bool pers_ok = c->persist_kernel && (reinterpret_cast<uintptr_t>(d_payload) & 15) == 0;
     if (c->encode_path == 3 && !pers_ok) return FEC_ERR_ARG;
     if (pers_ok && (c->encode_path == 0 || c->encode_path == 3))
@@ -747,7 +815,9 @@ int fec_codec_info(const fec_codec* c, char* buf, size_t size) {
     // kernel symbol the encoder launches for a 16-byte aligned payload (rocprofv3 naming)
     char enc[64];
     const int np = c->g.n - c->g.k;
-    if (c->persist_kernel && (c->encode_path == 0 || c->encode_path == 3))
+    if (c->wave_kernel && c->encode_path == 4)
+        std::snprintf(enc, sizeof(enc), "fec_encode_wave_kernel<%d, %d>", c->g.k, np);
+    else if (c->persist_kernel && (c->encode_path == 0 || c->encode_path == 3))
         std::snprintf(enc, sizeof(enc), "fec_encode_persist_kernel<%d, %d>", c->g.k, np);
     else if (c->fast_kernel && c->encode_path != 1)
         std::snprintf(enc, sizeof(enc), "fec_encode_fast_kernel<%d, %d>", c->g.k, np);
@@ -801,9 +871,10 @@ int fec_codec_set_copy_path(fec_codec* c, int path) {
 }
 
 int fec_codec_set_encode_path(fec_codec* c, int path) {
-    if (!c || path < 0 || path > 3) return FEC_ERR_ARG;
+    if (!c || path < 0 || path > 4) return FEC_ERR_ARG;
     if (path == 2 && !c->fast_kernel) return FEC_ERR_ARG;
     if (path == 3 && !c->persist_kernel) return FEC_ERR_ARG;
+    if (path == 4 && !c->wave_kernel) return FEC_ERR_ARG;
     c->encode_path = path;
     return FEC_OK;
 }

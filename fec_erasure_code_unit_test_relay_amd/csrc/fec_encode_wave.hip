@@ -1,0 +1,458 @@
+// fec_encode_wave.hip -- encode kernel with wave-private packet sequences, specialised on (k, n-k).
+//
+// Same closed form as every encode kernel here (fec_kernels.hip): for packet t, sub-stream s,
+//     cw_t[s*n + j] = X_t[s][j]                                   j <  k
+//     cw_t[s*n + j] = XOR_i G[i][j] * X_{t-(j-i)}[s][i]           j >= k
+// with X_t[s] = bytes [s*k, s*k+k) of [len_hi, len_lo, payload, zero pad] (Encoder.cpp:65-98,
+// Encoder_Basic.cpp:48-74, codingOperations.cpp:131-147).
+//
+// Organisation (no workgroup barrier after the one that publishes the coefficient tables):
+//   * a lane owns one group of 4 sub-streams (g) of one packet SEQUENCE (M consecutive packets);
+//     a wave holds 64 / NS4 sequences side by side and walks them in lockstep, one packet per
+//     step, so the waves of a CU interleave freely and hide each other's memory latency;
+//   * a lane reads its k+1 payload dwords of the packet straight from HBM (buffer loads: rows
+//     before the stream start come back as zero, the encoder-creation semantics), prefetched one
+//     packet pair ahead, and transposes them into k "position words" (byte e = position i of
+//     sub-stream 4g+e) with constant-selector v_perm_b32;
+//   * parity is accumulated FORWARD: position word i of packet t contributes G[i][k+jj] * word to
+//     parity jj of packet t+(k+jj-i), i.e. into an (n-1)-slot register ring of accumulators; the
+//     loop body is unrolled over n-1 packets so every ring index is a compile-time register;
+//     a packet's parity is complete when its slot comes round.  GF products are gf_mul4x
+//     (three v_perm_b32 table lookups, tables in LDS read as wave-wide broadcasts, one read per
+//     coefficient per packet pair);
+//   * the n codeword words of the group are re-interleaved with constant selectors and stored
+//     straight to HBM (dword-aligned 16-byte stores: when a codeword row starts at a = t*CW mod 4
+//     != 0 the words are shifted by a bytes and each lane takes its first a bytes from the lane to
+//     its left, ds_bpermute; a sequence's lane 0 takes them from the previous packet's last lane);
+//   * each sequence starts with an (n-1)-packet warm-up over the packets in front of it (no stores).
+#include "fec_device.h"
+#include "fec_kernels.h"
+
+#include <utility>
+
+namespace fec {
+namespace {
+
+constexpr int kWaveThreads = 256;
+
+typedef uint32_t u32x4a __attribute__((ext_vector_type(4), aligned(4)));
+typedef uint32_t u32x3a __attribute__((ext_vector_type(3), aligned(4)));
+typedef uint32_t u32x2a __attribute__((ext_vector_type(2), aligned(4)));
+typedef uint32_t v4u32 __attribute__((ext_vector_type(4)));
+typedef uint32_t v3u32 __attribute__((ext_vector_type(3)));
+typedef uint32_t v2u32 __attribute__((ext_vector_type(2)));
+
+template <typename F, int... Is>
+__device__ __forceinline__ void static_for_impl(F&& f, std::integer_sequence<int, Is...>) {
+    (f(std::integral_constant<int, Is>{}), ...);
+}
+// f(integral_constant<int, 0>) ... f(integral_constant<int, N-1>), unrolled at compile time
+template <int N, typename F>
+__device__ __forceinline__ void static_for(F&& f) {
+    static_for_impl(f, std::make_integer_sequence<int, N>{});
+}
+
+__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
+    return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
+}
+
+struct Sel3 {
+    uint32_t s0, s1, s2;
+};
+__device__ __forceinline__ Sel3 split_sel(uint32_t x) {
+    return {x & 0x07070707u, (x >> 3) & 0x07070707u, (x >> 6) & 0x03030303u};
+}
+// acc ^ c*x for the packed bytes of x (selectors s), c's tables t (0..3) and t4.  Both XORs are
+// bitop3 intrinsics on purpose: plain XOR chains get reassociated across the whole unrolled block,
+// which keeps every product of the block live at once.
+__device__ __forceinline__ uint32_t mul_acc(uint32_t acc, const uint4& t, uint32_t t4, const Sel3& s) {
+    const uint32_t a = xor3(acc, __builtin_amdgcn_perm(t.y, t.x, s.s0), __builtin_amdgcn_perm(t.w, t.z, s.s1));
+    return xor3(a, __builtin_amdgcn_perm(t4, t4, s.s2), 0u);
+}
+
+// Materialise v here: stops the compiler from sinking its computation towards a far-away use
+// (the accumulator ring is only read a whole block later), which would keep every table and
+// selector of the block live at once.
+__device__ __forceinline__ void pin(uint32_t& v) { asm volatile("" : "+v"(v)); }
+
+__device__ __forceinline__ uint32_t bperm(int src_lane, uint32_t v) {
+    return static_cast<uint32_t>(__builtin_amdgcn_ds_bpermute(src_lane << 2, static_cast<int>(v)));
+}
+
+// payload dwords of one (packet, group): D[0] = dword gK-1 (the header slot for g = 0), D[1..K] =
+// dwords gK .. gK+K-1 of the payload row
+template <int K>
+struct RowIn {
+    uint32_t D[K + 1];
+    int ln;  // payload length (0 = the packet does not exist: before the stream start)
+};
+
+template <int K>
+__device__ __forceinline__ void load_row(RowIn<K>& r, __amdgpu_buffer_rsrc_t rs, __amdgpu_buffer_rsrc_t rl,
+                                         bool has_len, int voff_row, int lane_off, int row_rel, bool exists,
+                                         int L) {
+    const int o = voff_row + lane_off;  // byte offset of dword gK
+    r.D[0] = __builtin_amdgcn_raw_buffer_load_b32(rs, o - 4, 0, 0);
+#pragma unroll
+    for (int c = 0; c < K; c += 4) {
+        if (c + 4 <= K) {
+            const u32x4a v = __builtin_bit_cast(u32x4a, __builtin_amdgcn_raw_buffer_load_b128(rs, o + 4 * c, 0, 0));
+            r.D[1 + c] = v.x;
+            r.D[2 + c] = v.y;
+            r.D[3 + c] = v.z;
+            r.D[4 + c] = v.w;
+        } else if (c + 3 == K) {
+            const u32x3a v = __builtin_bit_cast(u32x3a, __builtin_amdgcn_raw_buffer_load_b96(rs, o + 4 * c, 0, 0));
+            r.D[1 + c] = v.x;
+            r.D[2 + c] = v.y;
+            r.D[3 + c] = v.z;
+        } else if (c + 2 == K) {
+            const u32x2a v = __builtin_bit_cast(u32x2a, __builtin_amdgcn_raw_buffer_load_b64(rs, o + 4 * c, 0, 0));
+            r.D[1 + c] = v.x;
+            r.D[2 + c] = v.y;
+        } else {
+            r.D[1 + c] = __builtin_amdgcn_raw_buffer_load_b32(rs, o + 4 * c, 0, 0);
+        }
+    }
+    if (has_len) {
+        const int v = static_cast<int>(__builtin_amdgcn_raw_buffer_load_b32(rl, row_rel * 4, 0, 0));
+        r.ln = v < 0 ? 0 : (v > L ? L : v);
+    } else {
+        r.ln = exists ? L : 0;
+    }
+}
+
+// Header, length mask and position words of one (packet, group).  H[m] = dword m of the group's
+// 4K-byte window of [len_hi, len_lo, payload, 0 pad]; P[i] = position word i.
+template <int K>
+__device__ __forceinline__ void row_words(const RowIn<K>& r, int g, int L, const uint32_t (&fullmask)[K],
+                                          uint32_t (&H)[K], uint32_t (&P)[K]) {
+    const uint32_t hdr = (static_cast<uint32_t>(r.ln & 0xff) << 24) | (static_cast<uint32_t>((r.ln >> 8) & 0xff) << 16);
+    const uint32_t d0 = g == 0 ? hdr : r.D[0];
+    H[0] = __builtin_amdgcn_alignbyte(r.D[1], d0, 2);
+#pragma unroll
+    for (int m = 1; m < K; ++m) H[m] = __builtin_amdgcn_alignbyte(r.D[m + 1], r.D[m], 2);
+    if (r.ln == L) {
+#pragma unroll
+        for (int m = 0; m < K; ++m) H[m] &= fullmask[m];
+    } else if (r.ln > 0) {  // short packet: bytes at payload offsets >= ln are zero
+        const int lim = r.ln + 2 - 4 * K * g;
+#pragma unroll
+        for (int m = 0; m < K; ++m) H[m] &= keep_bytes(lim - 4 * m);
+    } else {  // empty or not-yet-existing packet: all zero, header included
+#pragma unroll
+        for (int m = 0; m < K; ++m) H[m] = 0;
+    }
+#pragma unroll
+    for (int i = 0; i < K; ++i) P[i] = gather4(H, i, K + i, 2 * K + i, 3 * K + i);
+}
+
+// Codeword words of the group: bytes [e*n, e*n+n) = sub-stream 4g+e: K systematic bytes, NP parity.
+template <int K, int NP>
+__device__ __forceinline__ void group_words(const uint32_t (&H)[K], const uint32_t (&Q)[NP > 0 ? NP : 1],
+                                            uint32_t (&X)[K + NP]) {
+    constexpr int n = K + NP;
+    uint32_t src[n];
+#pragma unroll
+    for (int m = 0; m < K; ++m) src[m] = H[m];
+#pragma unroll
+    for (int jj = 0; jj < NP; ++jj) src[K + jj] = Q[jj];
+    auto idx = [](int b) {  // byte b of the group -> source byte index (word*4 + byte)
+        const int e = b / n, j = b % n;
+        return j < K ? (e * K + j) : (4 * (K + j - K) + e);
+    };
+#pragma unroll
+    for (int q = 0; q < n; ++q) X[q] = gather4(src, idx(4 * q), idx(4 * q + 1), idx(4 * q + 2), idx(4 * q + 3));
+}
+
+// Last 4 valid bytes of the group's words (bytes [vb-4, vb)), vb = n * rem for the last group.
+template <int n, int REM>
+__device__ __forceinline__ uint32_t tail_word_rem(const uint32_t (&X)[n]) {
+    constexpr int b = n * REM - 4;
+    if constexpr (b < 0) {
+        return X[0] << (8 * (4 - n * REM));
+    } else if constexpr (b % 4 == 0) {
+        return X[b / 4];
+    } else {
+        return __builtin_amdgcn_alignbyte(X[b / 4 + 1], X[b / 4], b % 4);
+    }
+}
+
+// W[idx] for a runtime idx without indexing registers (idx >= n -> 0)
+template <int n>
+__device__ __forceinline__ uint32_t word_at(const uint32_t (&W)[n], int idx) {
+    uint32_t r = 0;
+#pragma unroll
+    for (int q = 0; q < n; ++q) r = q == idx ? W[q] : r;
+    return r;
+}
+
+// Store `cnt` words W[0..cnt) at byte offset o (dword aligned) of the codeword resource.
+template <int n>
+__device__ __forceinline__ void store_words(__amdgpu_buffer_rsrc_t rc, int o, const uint32_t (&W)[n], int cnt) {
+#pragma unroll
+    for (int c = 0; c < n; c += 4) {
+        const int w = (n - c) < 4 ? (n - c) : 4;
+        if (c + w <= cnt) {
+            if (w == 4) {
+                u32x4a v = {W[c], W[c + 1 < n ? c + 1 : c], W[c + 2 < n ? c + 2 : c], W[c + 3 < n ? c + 3 : c]};
+                __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u32, v), rc, o + 4 * c, 0, 0);
+            } else if (w == 3) {
+                u32x3a v = {W[c], W[c + 1 < n ? c + 1 : c], W[c + 2 < n ? c + 2 : c]};
+                __builtin_amdgcn_raw_buffer_store_b96(__builtin_bit_cast(v3u32, v), rc, o + 4 * c, 0, 0);
+            } else if (w == 2) {
+                u32x2a v = {W[c], W[c + 1 < n ? c + 1 : c]};
+                __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(v2u32, v), rc, o + 4 * c, 0, 0);
+            } else {
+                __builtin_amdgcn_raw_buffer_store_b32(W[c], rc, o + 4 * c, 0, 0);
+            }
+        } else {
+#pragma unroll
+            for (int q = c; q < c + w; ++q)
+                if (q < cnt) __builtin_amdgcn_raw_buffer_store_b32(W[q], rc, o + 4 * q, 0, 0);
+        }
+    }
+}
+
+// Rare path (a codeword whose last byte is zero): trimmed size = 1 + position of the last non-zero
+// byte over the sequence's lanes, reduced towards lane g = 0, which stores it.
+template <int n>
+__device__ __forceinline__ void slow_trim(const uint32_t (&X)[n], int g, int lane, int NS4, int last_g,
+                                                    bool need, bool alive, __amdgpu_buffer_rsrc_t rw, int off) {
+    int z = -1;
+#pragma unroll
+    for (int q = n - 1; q >= 0; --q)
+        if (z < 0 && X[q] != 0) z = 4 * q + 3 - (__builtin_clz(X[q]) >> 3);
+    int best = z < 0 ? 0 : 4 * n * g + z + 1;
+    for (int d = 1; d < NS4; d <<= 1) {
+        const int src = (g + d < NS4) ? lane + d : lane;
+        const int o = static_cast<int>(bperm(src, static_cast<uint32_t>(best)));
+        best = o > best ? o : best;
+    }
+    const bool need0 = bperm(lane + last_g, need ? 1u : 0u) != 0;  // lane 0 asks its last lane
+    if (alive && g == 0 && need0) __builtin_amdgcn_raw_buffer_store_b32(static_cast<uint32_t>(best), rw, off, 0, 0);
+}
+
+}  // namespace
+
+template <int K, int NP>
+__global__ __launch_bounds__(kWaveThreads) void fec_encode_wave_kernel(EncWaveArgs a) {
+    constexpr int n = K + NP;
+    constexpr int W = n - 1;            // parity reaches back n-1 packets
+    constexpr int NPA = NP > 0 ? NP : 1;
+    __shared__ uint4 tabs[(K * NP > 0 ? K * NP : 1) * 2];
+    for (int q = threadIdx.x; q < K * NP * 2; q += blockDim.x)
+        tabs[q] = reinterpret_cast<const uint4*>(a.ptab)[q];
+    __syncthreads();
+
+    const int lane = threadIdx.x & 63;
+    const int wave = blockIdx.x * (kWaveThreads / 64) + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int NS4 = a.NS4, SPW = a.SPW, M = a.M, L = a.L, CW = a.CW, P = a.P, hist = a.history;
+    const int seq0 = wave * SPW;        // first sequence of the wave
+    if (seq0 >= a.nseq) return;
+    const int sq = lane / NS4;
+    const int g = lane - sq * NS4;
+    const bool alive = sq < SPW && seq0 + sq < a.nseq;
+    const int r0 = (seq0 + sq) * M;     // first packet of the lane's sequence (batch-relative)
+    const int last_g = NS4 - 1;
+    const int vb = g == last_g ? n * a.rem : 4 * n;  // valid codeword bytes of the lane's group
+
+    // buffer resources built from kernel arguments only (provably wave-uniform).  Payload rows
+    // [-history, P): rows outside read as zero -- the packets before the encoder's first one.
+    // Codeword rows [0, P): stores outside are dropped.
+    const __amdgpu_buffer_rsrc_t rs =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(a.payload_base), 0, a.payload_bytes, 0x00020000);
+    const bool has_len = a.len_base != nullptr;
+    const __amdgpu_buffer_rsrc_t rl =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<int32_t*>(a.len_base), 0, a.len_bytes, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rc = __builtin_amdgcn_make_buffer_rsrc(a.cw, 0, a.cw_bytes, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc(a.cw_len, 0, 4 * P, 0x00020000);
+    const int lane_off = 4 * K * g;      // byte offset of dword gK in a payload row
+
+    // full-length packet: bytes of the group window at payload offsets >= L are zero
+    uint32_t fullmask[K];
+#pragma unroll
+    for (int m = 0; m < K; ++m) fullmask[m] = keep_bytes(L + 2 - 4 * K * g - 4 * m);
+
+    // lane holding the group to the left (lane 0: the last group, i.e. the previous packet's tail)
+    const int left = g == 0 ? lane + last_g : lane - 1;
+
+    uint32_t acc[W][NPA];
+#pragma unroll
+    for (int u = 0; u < W; ++u)
+#pragma unroll
+        for (int jj = 0; jj < NPA; ++jj) acc[u][jj] = 0;
+    uint32_t tsave = 0;  // lane 0 of a sequence: previous packet's tail word
+
+    const int nblk = (M + W + W - 1) / W;  // W warm-up packets, then the sequence's M packets
+
+    auto load = [&](RowIn<K>& r, int s) __attribute__((always_inline)) {
+        const int t = r0 - W + s;
+        const int rel = t + hist;  // row index in the payload / length resources
+        load_row<K>(r, rs, rl, has_len, rel * L, lane_off, rel, t >= -hist && t < P, L);
+        if (t == P - 1 && 4 * (g * K + K) > L) {  // chunks straddling the buffer end: dword loads
+            const int o = rel * L + lane_off;
+#pragma unroll
+            for (int m = 0; m < K; ++m) r.D[1 + m] = __builtin_amdgcn_raw_buffer_load_b32(rs, o + 4 * m, 0, 0);
+        }
+    };
+
+    // one packet: its parity Q is complete; codeword words, stores, trimmed wire size
+    auto emit = [&](int s, const uint32_t (&H)[K], const uint32_t (&Q)[NPA]) __attribute__((always_inline)) {
+        uint32_t X[n];
+        group_words<K, NP>(H, Q, X);
+        uint32_t tw = X[n - 1];
+        if (g == last_g) {
+            switch (a.rem) {
+                case 1: tw = tail_word_rem<n, 1>(X); break;
+                case 2: tw = tail_word_rem<n, 2>(X); break;
+                case 3: tw = tail_word_rem<n, 3>(X); break;
+                default: break;
+            }
+        }
+        const uint32_t lv = bperm(left, tw);
+        const uint32_t prev = g == 0 ? tsave : lv;
+        tsave = lv;
+        const int t = r0 - W + s;
+        const bool store = alive && s >= W && s < W + M;  // s bounds are wave-uniform
+        const int A = t * CW;
+        const int al = A & 3;  // identical for all lanes of the wave (sequences start at t % 4 == 0)
+        const int o = A + 4 * n * g - al;  // dword-aligned store offset
+        uint32_t Z[n];
+        if (al == 0) {
+#pragma unroll
+            for (int q = 0; q < n; ++q) Z[q] = X[q];
+        } else {
+            const int sh = 4 - al;
+            Z[0] = __builtin_amdgcn_alignbyte(X[0], prev, sh);
+#pragma unroll
+            for (int q = 1; q < n; ++q) Z[q] = __builtin_amdgcn_alignbyte(X[q], X[q - 1], sh);
+        }
+        const int cnt = (vb + al) >> 2;
+        if (store) store_words<n>(rc, o, Z, cnt);
+        const int rbytes = (vb + al) & 3;
+        if (store && t == P - 1 && g == last_g && rbytes) {  // batch end: the final partial dword
+            const uint32_t v = al == 0 ? word_at<n>(X, cnt)
+                                       : __builtin_amdgcn_alignbyte(word_at<n>(X, cnt), word_at<n>(X, cnt - 1), 4 - al);
+            for (int b = 0; b < rbytes; ++b)
+                __builtin_amdgcn_raw_buffer_store_b8(static_cast<uint8_t>(v >> (8 * b)), rc, o + 4 * cnt + b, 0, 0);
+        }
+        // trimmed wire size (FEC_Encoder.cpp:55-60): fast path = the codeword's last byte is set
+        uint32_t lw = X[n - 1];
+        switch (a.rem) {
+            case 1: lw = tail_word_rem<n, 1>(X); break;
+            case 2: lw = tail_word_rem<n, 2>(X); break;
+            case 3: lw = tail_word_rem<n, 3>(X); break;
+            default: break;
+        }
+        const bool full = (lw >> 24) != 0;
+        if (store && g == last_g && full) __builtin_amdgcn_raw_buffer_store_b32(static_cast<uint32_t>(CW), rw, 4 * t, 0, 0);
+        const bool need = store && g == last_g && !full;
+        if (__builtin_amdgcn_ballot_w64(need)) slow_trim<n>(X, g, lane, NS4, last_g, need, alive, rw, 4 * t);
+    };
+
+    RowIn<K> ra, rb, na, nb;
+    load(ra, 0);
+    load(rb, 1);
+    for (int blk = 0; blk < nblk; ++blk) {
+        // one block = W packets: the accumulator ring comes round once, every slot index below is
+        // a compile-time constant.  Packets go in pairs (tables read once per pair).
+        static_for<(W + 1) / 2>([&](auto ic) __attribute__((always_inline)) {
+            constexpr int U = 2 * decltype(ic)::value;
+            constexpr bool TWO = U + 1 < W;
+            const int s = blk * W + U;
+            // prefetch the packets of the next step: (s+2, s+3) after a pair, s+2 after a single
+            if constexpr (TWO) {
+                load(na, s + 2);
+                load(nb, s + 3);
+            } else {
+                load(nb, s + 2);
+            }
+            uint32_t QA[NPA], QB[NPA];
+#pragma unroll
+            for (int jj = 0; jj < NPA; ++jj) {
+                QA[jj] = acc[U][jj];
+                acc[U][jj] = 0;
+                QB[jj] = 0;
+            }
+            uint32_t PA[K], PB[K];
+            {
+                uint32_t HA[K];
+                row_words<K>(ra, g, L, fullmask, HA, PA);
+#pragma unroll
+                for (int i = 0; i < K; ++i) pin(PA[i]);
+                emit(s, HA, QA);  // packet s's parity slot was complete before this step
+            }
+            __builtin_amdgcn_sched_barrier(0);
+            uint32_t HB[K];
+            if constexpr (TWO) {
+                row_words<K>(rb, g, L, fullmask, HB, PB);
+#pragma unroll
+                for (int i = 0; i < K; ++i) {
+                    pin(PB[i]);
+                    pin(HB[i]);
+                }
+            }
+            static_for<K>([&](auto ii) __attribute__((always_inline)) {
+                constexpr int I = K - 1 - decltype(ii)::value;  // delay-1 term (i = K-1) first
+                int z;
+                asm volatile("s_mov_b32 %0, 0" : "=s"(z));  // keeps the table reads in this step
+                const uint4* tp = tabs + z + I * NP * 2;
+                const Sel3 sa = split_sel(PA[I]);
+                Sel3 sb = sa;
+                if constexpr (TWO) sb = split_sel(PB[I]);
+                static_for<NP>([&](auto jc) __attribute__((always_inline)) {
+                    constexpr int JJ = decltype(jc)::value;
+                    const uint4 t = tp[JJ * 2];
+                    const uint32_t t4 = tp[JJ * 2 + 1].x;
+                    constexpr int DA = (U + K + JJ - I) % W;
+                    acc[DA][JJ] = mul_acc(acc[DA][JJ], t, t4, sa);
+                    pin(acc[DA][JJ]);
+                    if constexpr (TWO && I == K - 1 && JJ == 0) {
+                        // packet s+1's slot is complete once packet s's delay-1 term is in
+#pragma unroll
+                        for (int j2 = 0; j2 < NPA; ++j2) {
+                            QB[j2] = acc[(U + 1) % W][j2];
+                            acc[(U + 1) % W][j2] = 0;
+                        }
+                    }
+                    if constexpr (TWO) {
+                        constexpr int DB = (U + 1 + K + JJ - I) % W;
+                        acc[DB][JJ] = mul_acc(acc[DB][JJ], t, t4, sb);
+                        pin(acc[DB][JJ]);
+                    }
+                });
+                __builtin_amdgcn_sched_barrier(0);  // one position word (and its tables) at a time
+            });
+            if constexpr (TWO) {
+                emit(s + 1, HB, QB);
+                ra = na;
+                rb = nb;
+            } else {  // odd W: the next block's first pair is (s+1, s+2)
+                ra = rb;
+                rb = nb;
+            }
+        });
+    }
+}
+
+#ifdef FEC_WAVE_ONLY  // quick builds while tuning: -DFEC_WAVE_ONLY
+#define FEC_ENC_WAVE_LIST(X) X(8, 3)
+#else
+#define FEC_ENC_WAVE_LIST(X) \
+    X(8, 3) X(9, 5) X(11, 0) X(10, 1) X(9, 2) X(7, 4) X(6, 5) X(5, 6) X(4, 7) X(3, 8) X(2, 9)  \
+    X(10, 3) X(9, 3) X(10, 4) X(8, 4) X(10, 5) X(7, 5) X(3, 9)
+#endif
+
+#define FEC_ENC_WAVE_INST(K, NP) template __global__ void fec_encode_wave_kernel<K, NP>(EncWaveArgs);
+FEC_ENC_WAVE_LIST(FEC_ENC_WAVE_INST)
+
+const void* fec_encode_wave_kernel_for(int k, int np) {
+#define FEC_ENC_WAVE_CASE(K, NP) \
+    if (k == K && np == NP) return reinterpret_cast<const void*>(&fec_encode_wave_kernel<K, NP>);
+    FEC_ENC_WAVE_LIST(FEC_ENC_WAVE_CASE)
+#undef FEC_ENC_WAVE_CASE
+    return nullptr;
+}
+
+}  // namespace fec

@@ -57,6 +57,27 @@ struct EncFastArgs {
     int64_t tiles_per_wg;       // persistent kernel: contiguous tiles per workgroup
 };
 
+// Wave-private sequence encode (fec_encode_wave.hip).  Lane = (sequence, group of 4 sub-streams);
+// SPW = 64 / NS4 sequences per wave, each of M packets (M % 4 == 0).
+struct EncWaveArgs {
+    const uint8_t* payload_base;  // row -history (4-byte aligned, L % 4 == 0)
+    const int32_t* len_base;      // lengths of rows -history.. (null: all L)
+    int payload_bytes;            // (history + P) * L < 2^31 (the launcher splits larger batches)
+    int len_bytes;                // (history + P) * 4
+    int history;                  // valid rows before row 0
+    int P;
+    uint8_t* cw;                  // 4-byte aligned
+    int cw_bytes;                 // P * CW < 2^31
+    int32_t* cw_len;
+    const uint32_t* ptab;
+    int L, S, CW, NS4, SPW, M;
+    int rem;                      // sub-streams in the last group (1..4)
+    int nseq;                     // ceil(P / M)
+};
+
+// fec_encode_wave_kernel<k, n-k> (fec_encode_wave.hip), else nullptr.  256 threads.
+const void* fec_encode_wave_kernel_for(int k, int np);
+
 // fec_encode_persist_kernel<k, n-k> (fec_encode_persist.hip), else nullptr.  320 threads.
 const void* fec_encode_persist_kernel_for(int k, int np);
 
