@@ -54,6 +54,8 @@ struct fec_codec {
     int encode_path = 0;         // 0 auto, 1 generic, 2 specialised, 3 streaming, 4 wave
     const void* wave_kernel = nullptr;  // wave-private sequence encode (fec_encode_wave.hip)
     int wave_slots = 0;                 // resident waves of it on the device
+    int wave_ring = 0;                  // bytes of its per-sequence LDS output ring
+    int wave_lds = 0;                   // its dynamic LDS per workgroup
     const void* copy_fast = nullptr;  // specialised decode copy kernel
     int copyf_tp = 0;
     int copy_path = 0;           // 0 auto, 1 generic, 2 specialised
@@ -226,10 +228,19 @@ int codec_init(fec_codec* c, int max_payload, int T, int B, int N) {
     if ((g.L & 3) == 0 && (g.S + 3) / 4 <= 64)
         c->wave_kernel = fec::fec_encode_wave_kernel_for(g.k, g.n - g.k);
     if (c->wave_kernel) {
+        const int ns4 = c->ns4();
+        c->wave_ring = 64;
+        while (c->wave_ring < 2 * g.CW + 4 * g.n + 32) c->wave_ring <<= 1;
+        c->wave_lds = 4 * (64 / ns4 + 1) * c->wave_ring;
+        if (c->wave_lds > 128 * 1024) c->wave_kernel = nullptr;
+    }
+    if (c->wave_kernel)
+        HIP_TRY(hipFuncSetAttribute(c->wave_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, c->wave_lds));
+    if (c->wave_kernel) {
         int dev = 0, cus = 0, per_cu = 0;
         HIP_TRY(hipGetDevice(&dev));
         HIP_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
-        HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, c->wave_kernel, 256, 0));
+        HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, c->wave_kernel, 256, c->wave_lds));
         c->wave_slots = cus * per_cu * 4;
         if (c->wave_slots <= 0) c->wave_kernel = nullptr;
     }
@@ -400,12 +411,16 @@ int launch_encode_wave(fec_codec* c, const uint8_t* d_payload, const int32_t* d_
     M = std::max<int64_t>(4, (M + 3) & ~int64_t(3));
     a.M = static_cast<int>(M);
     a.nseq = static_cast<int>((P + M - 1) / M);
+    a.dbg = 0;
+    if (const char* v = std::getenv("FEC_WAVE_DBG")) a.dbg = std::atoi(v);
+    a.ring_bytes = c->wave_ring;
     const int64_t waves = (a.nseq + a.SPW - 1) / a.SPW;
     const int64_t blocks = (waves + 3) / 4;
     hipEvent_t stop;
     if (int st = c->begin(FEC_KERNEL_ENCODE, s, &stop)) return st;
     void* args[] = {&a};
-    HIP_TRY(hipLaunchKernel(c->wave_kernel, dim3(static_cast<unsigned>(blocks)), dim3(256), args, 0, s));
+    HIP_TRY(hipLaunchKernel(c->wave_kernel, dim3(static_cast<unsigned>(blocks)), dim3(256), args,
+                            c->wave_lds, s));
     return c->end(stop, s);
 }
 

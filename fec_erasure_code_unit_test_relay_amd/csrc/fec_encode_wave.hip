@@ -123,18 +123,20 @@ __device__ __forceinline__ void load_row(RowIn<K>& r, __amdgpu_buffer_rsrc_t rs,
 }
 
 // Header, length mask and position words of one (packet, group).  H[m] = dword m of the group's
-// 4K-byte window of [len_hi, len_lo, payload, 0 pad]; P[i] = position word i.
+// 4K-byte window of [len_hi, len_lo, payload, 0 pad]; P[i] = position word i.  nvalid = payload
+// dwords of the row from dword gK on (L/4 - gK): the dwords past the row end, which belong to the
+// next packet, are zeroed (the window's zero pad).
 template <int K>
-__device__ __forceinline__ void row_words(const RowIn<K>& r, int g, int L, const uint32_t (&fullmask)[K],
-                                          uint32_t (&H)[K], uint32_t (&P)[K]) {
+__device__ __forceinline__ void row_words(const RowIn<K>& r, int g, int L, int nvalid, uint32_t (&H)[K],
+                                          uint32_t (&P)[K]) {
     const uint32_t hdr = (static_cast<uint32_t>(r.ln & 0xff) << 24) | (static_cast<uint32_t>((r.ln >> 8) & 0xff) << 16);
-    const uint32_t d0 = g == 0 ? hdr : r.D[0];
-    H[0] = __builtin_amdgcn_alignbyte(r.D[1], d0, 2);
+    uint32_t D[K + 1];
+    D[0] = g == 0 ? hdr : r.D[0];
 #pragma unroll
-    for (int m = 1; m < K; ++m) H[m] = __builtin_amdgcn_alignbyte(r.D[m + 1], r.D[m], 2);
+    for (int m = 0; m < K; ++m) D[m + 1] = m < nvalid ? r.D[m + 1] : 0u;
+#pragma unroll
+    for (int m = 0; m < K; ++m) H[m] = __builtin_amdgcn_alignbyte(D[m + 1], D[m], 2);
     if (r.ln == L) {
-#pragma unroll
-        for (int m = 0; m < K; ++m) H[m] &= fullmask[m];
     } else if (r.ln > 0) {  // short packet: bytes at payload offsets >= ln are zero
         const int lim = r.ln + 2 - 4 * K * g;
 #pragma unroll
@@ -236,7 +238,7 @@ __device__ __forceinline__ void slow_trim(const uint32_t (&X)[n], int g, int lan
 }  // namespace
 
 template <int K, int NP>
-__global__ __launch_bounds__(kWaveThreads) void fec_encode_wave_kernel(EncWaveArgs a) {
+__global__ __launch_bounds__(kWaveThreads, 4) void fec_encode_wave_kernel(EncWaveArgs a) {
     constexpr int n = K + NP;
     constexpr int W = n - 1;            // parity reaches back n-1 packets
     constexpr int NPA = NP > 0 ? NP : 1;
@@ -255,7 +257,6 @@ __global__ __launch_bounds__(kWaveThreads) void fec_encode_wave_kernel(EncWaveAr
     const bool alive = sq < SPW && seq0 + sq < a.nseq;
     const int r0 = (seq0 + sq) * M;     // first packet of the lane's sequence (batch-relative)
     const int last_g = NS4 - 1;
-    const int vb = g == last_g ? n * a.rem : 4 * n;  // valid codeword bytes of the lane's group
 
     // buffer resources built from kernel arguments only (provably wave-uniform).  Payload rows
     // [-history, P): rows outside read as zero -- the packets before the encoder's first one.
@@ -269,10 +270,7 @@ __global__ __launch_bounds__(kWaveThreads) void fec_encode_wave_kernel(EncWaveAr
     const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc(a.cw_len, 0, 4 * P, 0x00020000);
     const int lane_off = 4 * K * g;      // byte offset of dword gK in a payload row
 
-    // full-length packet: bytes of the group window at payload offsets >= L are zero
-    uint32_t fullmask[K];
-#pragma unroll
-    for (int m = 0; m < K; ++m) fullmask[m] = keep_bytes(L + 2 - 4 * K * g - 4 * m);
+    const int nvalid = (L >> 2) - K * g;  // payload dwords of the row from dword gK on
 
     // lane holding the group to the left (lane 0: the last group, i.e. the previous packet's tail)
     const int left = g == 0 ? lane + last_g : lane - 1;
@@ -284,7 +282,9 @@ __global__ __launch_bounds__(kWaveThreads) void fec_encode_wave_kernel(EncWaveAr
         for (int jj = 0; jj < NPA; ++jj) acc[u][jj] = 0;
     uint32_t tsave = 0;  // lane 0 of a sequence: previous packet's tail word
 
-    const int nblk = (M + W + W - 1) / W;  // W warm-up packets, then the sequence's M packets
+    // W warm-up packets, the sequence's M packets, then at least one more: its lane 0 completes the
+    // last packet's final partial dword (batch end)
+    const int nblk = (M + W + 1 + W - 1) / W;
 
     auto load = [&](RowIn<K>& r, int s) __attribute__((always_inline)) {
         const int t = r0 - W + s;
@@ -298,6 +298,16 @@ __global__ __launch_bounds__(kWaveThreads) void fec_encode_wave_kernel(EncWaveAr
     };
 
     // one packet: its parity Q is complete; codeword words, stores, trimmed wire size
+    // Output staging: each sequence's codewords form one contiguous byte stream in HBM, assembled
+    // in a per-sequence LDS ring (absolute byte x at ring offset x & rmask) and flushed in
+    // 16-byte aligned chunks; the chunks shared with the neighbouring sequences go out as dwords.
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    const int rmask = a.ring_bytes - 1;
+    uint8_t* ring = smem + ((threadIdx.x >> 6) * (SPW + 1) + (sq < SPW ? sq : SPW)) * a.ring_bytes;
+    const int A0 = r0 * CW;                                    // sequence start (4-byte aligned)
+    const int Aend = (r0 + M < P ? r0 + M : P) * CW;            // sequence end
+    int fl = A0;                                               // next byte to flush
+
     auto emit = [&](int s, const uint32_t (&H)[K], const uint32_t (&Q)[NPA]) __attribute__((always_inline)) {
         uint32_t X[n];
         group_words<K, NP>(H, Q, X);
@@ -314,10 +324,10 @@ __global__ __launch_bounds__(kWaveThreads) void fec_encode_wave_kernel(EncWaveAr
         const uint32_t prev = g == 0 ? tsave : lv;
         tsave = lv;
         const int t = r0 - W + s;
-        const bool store = alive && s >= W && s < W + M;  // s bounds are wave-uniform
         const int A = t * CW;
-        const int al = A & 3;  // identical for all lanes of the wave (sequences start at t % 4 == 0)
-        const int o = A + 4 * n * g - al;  // dword-aligned store offset
+        // t % 4 = (s - W) % 4 for every lane: the alignment is wave-uniform
+        const int al = (((s - W) & 3) * CW) & 3;
+        const int o = A + 4 * n * g - al;  // dword-aligned; the lane covers [o, o + 4n)
         uint32_t Z[n];
         if (al == 0) {
 #pragma unroll
@@ -328,16 +338,12 @@ __global__ __launch_bounds__(kWaveThreads) void fec_encode_wave_kernel(EncWaveAr
 #pragma unroll
             for (int q = 1; q < n; ++q) Z[q] = __builtin_amdgcn_alignbyte(X[q], X[q - 1], sh);
         }
-        const int cnt = (vb + al) >> 2;
-        if (store) store_words<n>(rc, o, Z, cnt);
-        const int rbytes = (vb + al) & 3;
-        if (store && t == P - 1 && g == last_g && rbytes) {  // batch end: the final partial dword
-            const uint32_t v = al == 0 ? word_at<n>(X, cnt)
-                                       : __builtin_amdgcn_alignbyte(word_at<n>(X, cnt), word_at<n>(X, cnt - 1), 4 - al);
-            for (int b = 0; b < rbytes; ++b)
-                __builtin_amdgcn_raw_buffer_store_b8(static_cast<uint8_t>(v >> (8 * b)), rc, o + 4 * cnt + b, 0, 0);
-        }
+        // all n words, also past the row end for the last group: the next packet's words overwrite
+        // them before they are flushed
+#pragma unroll
+        for (int q = 0; q < n; ++q) *reinterpret_cast<uint32_t*>(ring + ((o + 4 * q) & rmask)) = Z[q];
         // trimmed wire size (FEC_Encoder.cpp:55-60): fast path = the codeword's last byte is set
+        const bool store = alive && s >= W && s < W + M && !(a.dbg & 1);  // s bounds are wave-uniform
         uint32_t lw = X[n - 1];
         switch (a.rem) {
             case 1: lw = tail_word_rem<n, 1>(X); break;
@@ -351,7 +357,36 @@ __global__ __launch_bounds__(kWaveThreads) void fec_encode_wave_kernel(EncWaveAr
         if (__builtin_amdgcn_ballot_w64(need)) slow_trim<n>(X, g, lane, NS4, last_g, need, alive, rw, 4 * t);
     };
 
-    RowIn<K> ra, rb, na, nb;
+    // Flush the sequence's final bytes below hi (hi: 4-aligned, or the batch end).
+    auto flush = [&](int hi) __attribute__((always_inline)) {
+        hi = hi < Aend ? hi : Aend;
+        if (!alive || (a.dbg & 1) || hi <= fl) return;
+        if (fl & 15) {  // sequence start inside a chunk: its dwords up to the chunk boundary
+            const int e = min((fl + 15) & ~15, hi & ~3);
+            for (int x = fl + 4 * g; x + 4 <= e; x += 4 * NS4)
+                __builtin_amdgcn_raw_buffer_store_b32(*reinterpret_cast<const uint32_t*>(ring + (x & rmask)), rc, x, 0, 0);
+            fl = e;
+        }
+        const int cend = hi & ~15;
+        for (int c = fl + 16 * g; c < cend; c += 16 * NS4) {
+            const v4u32 v = *reinterpret_cast<const v4u32*>(ring + (c & rmask));
+            __builtin_amdgcn_raw_buffer_store_b128(v, rc, c, 0, 0);
+        }
+        if (cend > fl) fl = cend;
+        if (hi == Aend && fl < Aend) {  // sequence end inside a chunk: dwords, then bytes (batch end)
+            for (int x = fl + 4 * g; x + 4 <= Aend; x += 4 * NS4)
+                __builtin_amdgcn_raw_buffer_store_b32(*reinterpret_cast<const uint32_t*>(ring + (x & rmask)), rc, x, 0, 0);
+            const int b0 = Aend & ~3;
+            if (g == 0 && b0 < Aend) {
+                const uint32_t v = *reinterpret_cast<const uint32_t*>(ring + (b0 & rmask));
+                for (int b = 0; b < Aend - b0; ++b)
+                    __builtin_amdgcn_raw_buffer_store_b8(static_cast<uint8_t>(v >> (8 * b)), rc, b0 + b, 0, 0);
+            }
+            fl = Aend;
+        }
+    };
+
+    RowIn<K> ra, rb, na;
     load(ra, 0);
     load(rb, 1);
     for (int blk = 0; blk < nblk; ++blk) {
@@ -361,13 +396,6 @@ __global__ __launch_bounds__(kWaveThreads) void fec_encode_wave_kernel(EncWaveAr
             constexpr int U = 2 * decltype(ic)::value;
             constexpr bool TWO = U + 1 < W;
             const int s = blk * W + U;
-            // prefetch the packets of the next step: (s+2, s+3) after a pair, s+2 after a single
-            if constexpr (TWO) {
-                load(na, s + 2);
-                load(nb, s + 3);
-            } else {
-                load(nb, s + 2);
-            }
             uint32_t QA[NPA], QB[NPA];
 #pragma unroll
             for (int jj = 0; jj < NPA; ++jj) {
@@ -375,25 +403,31 @@ __global__ __launch_bounds__(kWaveThreads) void fec_encode_wave_kernel(EncWaveAr
                 acc[U][jj] = 0;
                 QB[jj] = 0;
             }
+            // each row's registers are refilled with the packet two ahead as soon as its words are
+            // built: (s+2, s+3) after a pair, s+2 after a single
             uint32_t PA[K], PB[K];
             {
                 uint32_t HA[K];
-                row_words<K>(ra, g, L, fullmask, HA, PA);
+                row_words<K>(ra, g, L, nvalid, HA, PA);
 #pragma unroll
                 for (int i = 0; i < K; ++i) pin(PA[i]);
+                if constexpr (TWO) load(ra, s + 2);
                 emit(s, HA, QA);  // packet s's parity slot was complete before this step
             }
             __builtin_amdgcn_sched_barrier(0);
             uint32_t HB[K];
             if constexpr (TWO) {
-                row_words<K>(rb, g, L, fullmask, HB, PB);
+                row_words<K>(rb, g, L, nvalid, HB, PB);
 #pragma unroll
                 for (int i = 0; i < K; ++i) {
                     pin(PB[i]);
                     pin(HB[i]);
                 }
+                load(rb, s + 3);
+            } else {
+                load(na, s + 2);
             }
-            static_for<K>([&](auto ii) __attribute__((always_inline)) {
+            if (!(a.dbg & 2)) static_for<K>([&](auto ii) __attribute__((always_inline)) {
                 constexpr int I = K - 1 - decltype(ii)::value;  // delay-1 term (i = K-1) first
                 int z;
                 asm volatile("s_mov_b32 %0, 0" : "=s"(z));  // keeps the table reads in this step
@@ -426,11 +460,11 @@ __global__ __launch_bounds__(kWaveThreads) void fec_encode_wave_kernel(EncWaveAr
             });
             if constexpr (TWO) {
                 emit(s + 1, HB, QB);
-                ra = na;
-                rb = nb;
+                flush(((r0 - W + s + 2) * CW) & ~3);  // rows up to s+1 final but their last partial dword
             } else {  // odd W: the next block's first pair is (s+1, s+2)
+                flush(((r0 - W + s + 1) * CW) & ~3);
                 ra = rb;
-                rb = nb;
+                rb = na;
             }
         });
     }

@@ -73,6 +73,8 @@ struct EncWaveArgs {
     int L, S, CW, NS4, SPW, M;
     int rem;                      // sub-streams in the last group (1..4)
     int nseq;                     // ceil(P / M)
+    int ring_bytes;               // per-sequence LDS output ring (power of two >= 2*CW + 4n + 32)
+    int dbg;                      // timing experiments only (FEC_WAVE_DBG): 1 no stores, 2 no parity
 };
 
 // fec_encode_wave_kernel<k, n-k> (fec_encode_wave.hip), else nullptr.  256 threads.
