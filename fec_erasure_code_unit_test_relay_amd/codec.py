@@ -59,8 +59,8 @@ class Codec:
         return G.reshape(self.k, self.n)
 
     def set_encode_path(self, path: str) -> None:
-        """'auto', 'generic', 'fast' (per-tile k, n-k specialised kernel) or 'stream' (the
-        persistent specialised kernel)."""
+        """'auto', 'generic', 'fast' (per-tile k, n-k specialised kernel), 'stream' (the
+        persistent specialised kernel) or 'wave' (the wave-sequence kernel)."""
         code = {"auto": 0, "generic": 1, "fast": 2, "stream": 3, "wave": 4}[path]
         check(lib().fec_codec_set_encode_path(self._h, code), "fec_codec_set_encode_path")
 

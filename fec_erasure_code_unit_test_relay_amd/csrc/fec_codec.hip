@@ -430,10 +430,9 @@ int launch_encode(fec_codec* c, const uint8_t* d_payload, const int32_t* d_len, 
     const Geometry& g = c->g;
     const bool wave_ok = c->wave_kernel && (reinterpret_cast<uintptr_t>(d_payload) & 3) == 0 &&
                          (reinterpret_cast<uintptr_t>(d_cw) & 3) == 0;
-    if (c->encode_path == 4) {
-        if (!wave_ok) return FEC_ERR_ARG;
+    if (c->encode_path == 4 && !wave_ok) return FEC_ERR_ARG;
+    if (wave_ok && (c->encode_path == 0 || c->encode_path == 4))
         return launch_encode_wave(c, d_payload, d_len, history, P, d_cw, d_cwlen, s);
-    }
     const bool pers_ok = c->persist_kernel && (reinterpret_cast<uintptr_t>(d_payload) & 15) == 0;
     if (c->encode_path == 3 && !pers_ok) return FEC_ERR_ARG;
     if (pers_ok && (c->encode_path == 0 || c->encode_path == 3))
@@ -830,7 +829,7 @@ int fec_codec_info(const fec_codec* c, char* buf, size_t size) {
     // kernel symbol the encoder launches for a 16-byte aligned payload (rocprofv3 naming)
     char enc[64];
     const int np = c->g.n - c->g.k;
-    if (c->wave_kernel && c->encode_path == 4)
+    if (c->wave_kernel && (c->encode_path == 0 || c->encode_path == 4))
         std::snprintf(enc, sizeof(enc), "fec_encode_wave_kernel<%d, %d>", c->g.k, np);
     else if (c->persist_kernel && (c->encode_path == 0 || c->encode_path == 3))
         std::snprintf(enc, sizeof(enc), "fec_encode_persist_kernel<%d, %d>", c->g.k, np);

@@ -34,6 +34,7 @@ namespace fec {
 namespace {
 
 constexpr int kWaveThreads = 256;
+constexpr int kTabAhead = 2;  // coefficient tables are read this many (word, parity) items early
 
 typedef uint32_t u32x4a __attribute__((ext_vector_type(4), aligned(4)));
 typedef uint32_t u32x3a __attribute__((ext_vector_type(3), aligned(4)));
@@ -305,7 +306,6 @@ __global__ __launch_bounds__(kWaveThreads, 4) void fec_encode_wave_kernel(EncWav
     const int rmask = a.ring_bytes - 1;
     uint8_t* ring = smem + ((threadIdx.x >> 6) * (SPW + 1) + (sq < SPW ? sq : SPW)) * a.ring_bytes;
     const int A0 = r0 * CW;                                    // sequence start (4-byte aligned)
-    const int Aend = (r0 + M < P ? r0 + M : P) * CW;            // sequence end
     int fl = A0;                                               // next byte to flush
 
     auto emit = [&](int s, const uint32_t (&H)[K], const uint32_t (&Q)[NPA]) __attribute__((always_inline)) {
@@ -358,31 +358,45 @@ __global__ __launch_bounds__(kWaveThreads, 4) void fec_encode_wave_kernel(EncWav
     };
 
     // Flush the sequence's final bytes below hi (hi: 4-aligned, or the batch end).
-    auto flush = [&](int hi) __attribute__((always_inline)) {
-        hi = hi < Aend ? hi : Aend;
-        if (!alive || (a.dbg & 1) || hi <= fl) return;
-        if (fl & 15) {  // sequence start inside a chunk: its dwords up to the chunk boundary
-            const int e = min((fl + 15) & ~15, hi & ~3);
-            for (int x = fl + 4 * g; x + 4 <= e; x += 4 * NS4)
-                __builtin_amdgcn_raw_buffer_store_b32(*reinterpret_cast<const uint32_t*>(ring + (x & rmask)), rc, x, 0, 0);
-            fl = e;
-        }
-        const int cend = hi & ~15;
-        for (int c = fl + 16 * g; c < cend; c += 16 * NS4) {
-            const v4u32 v = *reinterpret_cast<const v4u32*>(ring + (c & rmask));
-            __builtin_amdgcn_raw_buffer_store_b128(v, rc, c, 0, 0);
-        }
-        if (cend > fl) fl = cend;
-        if (hi == Aend && fl < Aend) {  // sequence end inside a chunk: dwords, then bytes (batch end)
-            for (int x = fl + 4 * g; x + 4 <= Aend; x += 4 * NS4)
-                __builtin_amdgcn_raw_buffer_store_b32(*reinterpret_cast<const uint32_t*>(ring + (x & rmask)), rc, x, 0, 0);
-            const int b0 = Aend & ~3;
-            if (g == 0 && b0 < Aend) {
-                const uint32_t v = *reinterpret_cast<const uint32_t*>(ring + (b0 & rmask));
-                for (int b = 0; b < Aend - b0; ++b)
-                    __builtin_amdgcn_raw_buffer_store_b8(static_cast<uint8_t>(v >> (8 * b)), rc, b0 + b, 0, 0);
+    // Flush every sequence's final bytes below row srow (relative to the sequence start): all 64
+    // lanes store one sequence at a time, so each store instruction covers one contiguous run.
+    // The rows' last partial dwords are final only once the next row has been assembled.
+    const int nseq_w = min(SPW, a.nseq - seq0);  // sequences of this wave (uniform)
+    auto flush = [&](int srow) __attribute__((always_inline)) {
+        if (a.dbg & 1) return;
+        for (int j = 0; j < nseq_w; ++j) {
+            const int r0j = (seq0 + j) * M;
+            const int Aendj = min(r0j + M, P) * CW;
+            const int hi = min(((r0j + srow) * CW) & ~3, Aendj);
+            int flj = __builtin_amdgcn_readlane(fl, j * NS4);
+            if (hi <= flj) continue;
+            const uint8_t* rj = smem + ((threadIdx.x >> 6) * (SPW + 1) + j) * a.ring_bytes;
+            if (flj & 15) {  // sequence start inside a chunk: its dwords up to the chunk boundary
+                const int e = min((flj + 15) & ~15, hi & ~3);
+                const int x = flj + 4 * lane;
+                if (x + 4 <= e)
+                    __builtin_amdgcn_raw_buffer_store_b32(*reinterpret_cast<const uint32_t*>(rj + (x & rmask)), rc, x, 0, 0);
+                flj = e;
             }
-            fl = Aend;
+            const int cend = hi & ~15;
+            for (int c = flj + 16 * lane; c < cend; c += 16 * 64) {
+                const v4u32 v = *reinterpret_cast<const v4u32*>(rj + (c & rmask));
+                __builtin_amdgcn_raw_buffer_store_b128(v, rc, c, 0, 0);
+            }
+            flj = max(flj, cend);
+            if (hi == Aendj && flj < Aendj) {  // sequence end inside a chunk: dwords, bytes (batch end)
+                const int x = flj + 4 * lane;
+                if (x + 4 <= Aendj)
+                    __builtin_amdgcn_raw_buffer_store_b32(*reinterpret_cast<const uint32_t*>(rj + (x & rmask)), rc, x, 0, 0);
+                const int b0 = Aendj & ~3;
+                if (lane == 0 && b0 < Aendj) {
+                    const uint32_t v = *reinterpret_cast<const uint32_t*>(rj + (b0 & rmask));
+                    for (int b = 0; b < Aendj - b0; ++b)
+                        __builtin_amdgcn_raw_buffer_store_b8(static_cast<uint8_t>(v >> (8 * b)), rc, b0 + b, 0, 0);
+                }
+                flj = Aendj;
+            }
+            if (sq == j) fl = flj;
         }
     };
 
@@ -427,18 +441,33 @@ __global__ __launch_bounds__(kWaveThreads, 4) void fec_encode_wave_kernel(EncWav
             } else {
                 load(na, s + 2);
             }
-            if (!(a.dbg & 2)) static_for<K>([&](auto ii) __attribute__((always_inline)) {
-                constexpr int I = K - 1 - decltype(ii)::value;  // delay-1 term (i = K-1) first
-                int z;
-                asm volatile("s_mov_b32 %0, 0" : "=s"(z));  // keeps the table reads in this step
-                const uint4* tp = tabs + z + I * NP * 2;
-                const Sel3 sa = split_sel(PA[I]);
-                Sel3 sb = sa;
-                if constexpr (TWO) sb = split_sel(PB[I]);
-                static_for<NP>([&](auto jc) __attribute__((always_inline)) {
-                    constexpr int JJ = decltype(jc)::value;
-                    const uint4 t = tp[JJ * 2];
-                    const uint32_t t4 = tp[JJ * 2 + 1].x;
+            // parity contributions: K*NP (position word, parity) items in the order i = K-1..0,
+            // jj = 0..NP-1; each item's tables are read from LDS kTabAhead items early
+            if (!(a.dbg & 2)) {
+                constexpr int NIT = K * NP;
+                constexpr int NB = kTabAhead + 1;
+                uint4 tb[NB];
+                uint32_t t4b[NB];
+                auto tload = [&](auto kc) __attribute__((always_inline)) {
+                    constexpr int k = decltype(kc)::value;
+                    constexpr int I = K - 1 - k / (NP > 0 ? NP : 1), JJ = k % (NP > 0 ? NP : 1);
+                    int z;
+                    asm volatile("s_mov_b32 %0, 0" : "=s"(z));  // keeps the table reads in this step
+                    tb[k % NB] = tabs[z + (I * NP + JJ) * 2];
+                    t4b[k % NB] = tabs[z + (I * NP + JJ) * 2 + 1].x;
+                };
+                static_for<(kTabAhead < NIT ? kTabAhead : NIT)>([&](auto kc) __attribute__((always_inline)) { tload(kc); });
+                Sel3 sa{0, 0, 0}, sb{0, 0, 0};
+                static_for<NIT>([&](auto kc) __attribute__((always_inline)) {
+                    constexpr int k = decltype(kc)::value;
+                    constexpr int I = K - 1 - k / (NP > 0 ? NP : 1), JJ = k % (NP > 0 ? NP : 1);
+                    if constexpr (k + kTabAhead < NIT) tload(std::integral_constant<int, k + kTabAhead>{});
+                    if constexpr (JJ == 0) {
+                        sa = split_sel(PA[I]);
+                        if constexpr (TWO) sb = split_sel(PB[I]);
+                    }
+                    const uint4 t = tb[k % NB];
+                    const uint32_t t4 = t4b[k % NB];
                     constexpr int DA = (U + K + JJ - I) % W;
                     acc[DA][JJ] = mul_acc(acc[DA][JJ], t, t4, sa);
                     pin(acc[DA][JJ]);
@@ -456,13 +485,12 @@ __global__ __launch_bounds__(kWaveThreads, 4) void fec_encode_wave_kernel(EncWav
                         pin(acc[DB][JJ]);
                     }
                 });
-                __builtin_amdgcn_sched_barrier(0);  // one position word (and its tables) at a time
-            });
+            }
             if constexpr (TWO) {
                 emit(s + 1, HB, QB);
-                flush(((r0 - W + s + 2) * CW) & ~3);  // rows up to s+1 final but their last partial dword
+                flush(s + 2 - W);
             } else {  // odd W: the next block's first pair is (s+1, s+2)
-                flush(((r0 - W + s + 1) * CW) & ~3);
+                flush(s + 1 - W);
                 ra = rb;
                 rb = na;
             }

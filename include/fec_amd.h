@@ -51,11 +51,12 @@ int fec_codec_geometry(const fec_codec *codec, int *k, int *n, int *S, int *CW);
 /* Kernel configuration chosen for this codec and device (tiles, resident workgroups), as a JSON
  * object written to buf (NUL-terminated, truncated to size). */
 int fec_codec_info(const fec_codec *codec, char *buf, size_t size);
-/* Encode kernel selection: 0 = automatic (the streaming kernel when one is compiled for
- * (k, n-k), max_payload % 4 == 0 and the payload is 16-byte aligned, else the per-tile
- * specialised kernel, else the generic one), 1 = generic kernel, 2 = per-tile specialised kernel,
- * 3 = streaming (persistent) specialised kernel (FEC_ERR_ARG if unavailable).  All produce
- * identical bytes; the switch exists for tests and A/B timing. */
+/* Encode kernel selection: 0 = automatic (the wave-sequence kernel when one is compiled for
+ * (k, n-k), max_payload % 4 == 0, payload and codeword buffers are 4-byte aligned and its LDS
+ * rings fit; else the streaming kernel when the payload is 16-byte aligned; else the per-tile
+ * specialised kernel; else the generic one), 1 = generic kernel, 2 = per-tile specialised kernel,
+ * 3 = streaming (persistent) specialised kernel, 4 = wave-sequence kernel (FEC_ERR_ARG if
+ * unavailable).  All produce identical bytes; the switch exists for tests and A/B timing. */
 int fec_codec_set_encode_path(fec_codec *codec, int path);
 /* The same switch for the decoder's received-packet copy kernel. */
 int fec_codec_set_copy_path(fec_codec *codec, int path);

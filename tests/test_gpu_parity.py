@@ -65,7 +65,11 @@ def test_encode_fast_path_other_payload_sizes():
         ref = oracle.encode_stream(Lx, *tbn, 0, P, seed=11)
         for path in ("fast", "stream", "wave"):
             c = fec.Codec(Lx, *tbn)
-            c.set_encode_path(path)
+            try:
+                c.set_encode_path(path)
+            except fec.FecError:
+                assert path == "wave" and Lx > 300  # prefetch width limit
+                continue
             payload = fec.fill_payload(0, P, Lx, 11)
             cw, wl = c.encode(payload)
             assert (cw.cpu().numpy() == ref["cw"]).all(), (Lx, tbn, path)
