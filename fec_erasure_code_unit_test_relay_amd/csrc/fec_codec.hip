@@ -636,10 +636,7 @@ int launch_recover(fec_codec* c, const uint8_t* d_cw, int64_t P, uint8_t* d_out,
     ra.CW = g.CW;
     hipEvent_t stop;
     if (int st = c->begin(FEC_KERNEL_DEC_RECOVER, s, &stop)) return st;
-    int rec_lds = 2816 + (g.k + g.n - 1) * g.CW;
-    ra.stage = rec_lds <= kLdsBudget ? 1 : 0;
-    if (!ra.stage) rec_lds = 2816;
-    hipLaunchKernelGGL(fec::fec_recover_kernel, dim3(2048), dim3(256), rec_lds, s, ra);
+    hipLaunchKernelGGL(fec::fec_recover_kernel, dim3(1024), dim3(256), 0, s, ra);
     HIP_TRY(hipGetLastError());
     return c->end(stop, s);
 }

@@ -57,6 +57,11 @@ __device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
     return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
 }
 
+// Materialise v here: stops the compiler from sinking its computation towards a far-away use
+// (the accumulator ring is only read a whole block later), which would keep every table and
+// selector of the block live at once.
+__device__ __forceinline__ void pin(uint32_t& v) { asm volatile("" : "+v"(v)); }
+
 struct Sel3 {
     uint32_t s0, s1, s2;
 };
@@ -67,14 +72,10 @@ __device__ __forceinline__ Sel3 split_sel(uint32_t x) {
 // bitop3 intrinsics on purpose: plain XOR chains get reassociated across the whole unrolled block,
 // which keeps every product of the block live at once.
 __device__ __forceinline__ uint32_t mul_acc(uint32_t acc, const uint4& t, uint32_t t4, const Sel3& s) {
-    const uint32_t a = xor3(acc, __builtin_amdgcn_perm(t.y, t.x, s.s0), __builtin_amdgcn_perm(t.w, t.z, s.s1));
-    return xor3(a, __builtin_amdgcn_perm(t4, t4, s.s2), 0u);
+    uint32_t a = xor3(acc, __builtin_amdgcn_perm(t.y, t.x, s.s0), __builtin_amdgcn_perm(t.w, t.z, s.s1));
+    pin(a);
+    return a ^ __builtin_amdgcn_perm(t4, t4, s.s2);  // VOP2: half the issue cost of a bitop3
 }
-
-// Materialise v here: stops the compiler from sinking its computation towards a far-away use
-// (the accumulator ring is only read a whole block later), which would keep every table and
-// selector of the block live at once.
-__device__ __forceinline__ void pin(uint32_t& v) { asm volatile("" : "+v"(v)); }
 
 __device__ __forceinline__ uint32_t bperm(int src_lane, uint32_t v) {
     return static_cast<uint32_t>(__builtin_amdgcn_ds_bpermute(src_lane << 2, static_cast<int>(v)));
@@ -357,20 +358,22 @@ __global__ __launch_bounds__(kWaveThreads, 4) void fec_encode_wave_kernel(EncWav
         if (__builtin_amdgcn_ballot_w64(need)) slow_trim<n>(X, g, lane, NS4, last_g, need, alive, rw, 4 * t);
     };
 
-    // Flush the sequence's final bytes below hi (hi: 4-aligned, or the batch end).
     // Flush every sequence's final bytes below row srow (relative to the sequence start): all 64
     // lanes store one sequence at a time, so each store instruction covers one contiguous run.
     // The rows' last partial dwords are final only once the next row has been assembled.
+    // dprev: rows since the previous flush (2 after a packet pair, 1 after a single packet).
     const int nseq_w = min(SPW, a.nseq - seq0);  // sequences of this wave (uniform)
-    auto flush = [&](int srow) __attribute__((always_inline)) {
-        if (a.dbg & 1) return;
+    const int wbase = (threadIdx.x >> 6) * (SPW + 1);  // first ring of this wave
+    const int r0_last = (seq0 + nseq_w - 1) * M;
+    const bool fast_fit = 2 * CW + 16 <= 16 * 64;   // a pair's chunks fit one store per sequence
+    auto flush_slow = [&](int srow) __attribute__((always_inline)) {
         for (int j = 0; j < nseq_w; ++j) {
             const int r0j = (seq0 + j) * M;
             const int Aendj = min(r0j + M, P) * CW;
             const int hi = min(((r0j + srow) * CW) & ~3, Aendj);
             int flj = __builtin_amdgcn_readlane(fl, j * NS4);
             if (hi <= flj) continue;
-            const uint8_t* rj = smem + ((threadIdx.x >> 6) * (SPW + 1) + j) * a.ring_bytes;
+            const uint8_t* rj = smem + (wbase + j) * a.ring_bytes;
             if (flj & 15) {  // sequence start inside a chunk: its dwords up to the chunk boundary
                 const int e = min((flj + 15) & ~15, hi & ~3);
                 const int x = flj + 4 * lane;
@@ -399,17 +402,51 @@ __global__ __launch_bounds__(kWaveThreads, 4) void fec_encode_wave_kernel(EncWav
             if (sq == j) fl = flj;
         }
     };
+    // Steady state (neither a sequence's first flush nor its last): sequence j's window is
+    // [(r0j + srow - dprev) * CW & ~15, (r0j + srow) * CW & ~15), 16-byte chunks only, at most one
+    // per lane.  Scalar addressing; the LDS reads of four sequences are issued before their stores.
+    auto flush = [&](int srow, int dprev) __attribute__((always_inline)) {
+        if (a.dbg & 1) return;
+        if (!(fast_fit && srow - dprev >= 1 && srow < M && r0_last + srow < P)) {
+            flush_slow(srow);
+            return;
+        }
+        for (int j0 = 0; j0 < nseq_w; j0 += 4) {
+            v4u32 v[4];
+            int c[4];
+            bool ok[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const int j = j0 + u;
+                const int r0j = (seq0 + j) * M;
+                const int lo = ((r0j + srow - dprev) * CW) & ~15;
+                const int hi = ((r0j + srow) * CW) & ~15;
+                c[u] = lo + 16 * lane;
+                ok[u] = j < nseq_w && c[u] < hi;
+                const uint8_t* rj = smem + (wbase + j) * a.ring_bytes;
+                v[u] = ok[u] ? *reinterpret_cast<const v4u32*>(rj + (c[u] & rmask)) : v4u32{0, 0, 0, 0};
+            }
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+                if (ok[u]) __builtin_amdgcn_raw_buffer_store_b128(v[u], rc, c[u], 0, 0);
+        }
+        fl = ((r0 + srow) * CW) & ~15;
+    };
 
+    // One block = W packets: the accumulator ring comes round once, every slot index below is a
+    // compile-time constant.  Packets go in pairs (tables read once per pair).  The first block
+    // (WARM) covers the W packets in front of the sequence: it only accumulates the parity terms
+    // that land on the sequence's own packets, and builds no codewords.  The walk ends after the
+    // flush that reaches row M (uniform).
+    bool done = false;
     RowIn<K> ra, rb, na;
-    load(ra, 0);
-    load(rb, 1);
-    for (int blk = 0; blk < nblk; ++blk) {
-        // one block = W packets: the accumulator ring comes round once, every slot index below is
-        // a compile-time constant.  Packets go in pairs (tables read once per pair).
+    auto run_block = [&](auto warmc, int blk) __attribute__((always_inline)) {
+        constexpr bool WARM = decltype(warmc)::value;
         static_for<(W + 1) / 2>([&](auto ic) __attribute__((always_inline)) {
             constexpr int U = 2 * decltype(ic)::value;
             constexpr bool TWO = U + 1 < W;
-            const int s = blk * W + U;
+            if (!WARM && done) return;
+            const int s = WARM ? U : blk * W + U;
             uint32_t QA[NPA], QB[NPA];
 #pragma unroll
             for (int jj = 0; jj < NPA; ++jj) {
@@ -426,7 +463,7 @@ __global__ __launch_bounds__(kWaveThreads, 4) void fec_encode_wave_kernel(EncWav
 #pragma unroll
                 for (int i = 0; i < K; ++i) pin(PA[i]);
                 if constexpr (TWO) load(ra, s + 2);
-                emit(s, HA, QA);  // packet s's parity slot was complete before this step
+                if constexpr (!WARM) emit(s, HA, QA);  // packet s's parity slot was complete before this step
             }
             __builtin_amdgcn_sched_barrier(0);
             uint32_t HB[K];
@@ -435,7 +472,7 @@ __global__ __launch_bounds__(kWaveThreads, 4) void fec_encode_wave_kernel(EncWav
 #pragma unroll
                 for (int i = 0; i < K; ++i) {
                     pin(PB[i]);
-                    pin(HB[i]);
+                    if constexpr (!WARM) pin(HB[i]);
                 }
                 load(rb, s + 3);
             } else {
@@ -461,6 +498,9 @@ __global__ __launch_bounds__(kWaveThreads, 4) void fec_encode_wave_kernel(EncWav
                 static_for<NIT>([&](auto kc) __attribute__((always_inline)) {
                     constexpr int k = decltype(kc)::value;
                     constexpr int I = K - 1 - k / (NP > 0 ? NP : 1), JJ = k % (NP > 0 ? NP : 1);
+                    // warm-up: only terms reaching packet W (the sequence's first) or later
+                    constexpr bool NEEDA = !WARM || U + K + JJ - I >= W;
+                    constexpr bool NEEDB = TWO && (!WARM || U + 1 + K + JJ - I >= W);
                     if constexpr (k + kTabAhead < NIT) tload(std::integral_constant<int, k + kTabAhead>{});
                     if constexpr (JJ == 0) {
                         sa = split_sel(PA[I]);
@@ -469,8 +509,10 @@ __global__ __launch_bounds__(kWaveThreads, 4) void fec_encode_wave_kernel(EncWav
                     const uint4 t = tb[k % NB];
                     const uint32_t t4 = t4b[k % NB];
                     constexpr int DA = (U + K + JJ - I) % W;
-                    acc[DA][JJ] = mul_acc(acc[DA][JJ], t, t4, sa);
-                    pin(acc[DA][JJ]);
+                    if constexpr (NEEDA) {
+                        acc[DA][JJ] = mul_acc(acc[DA][JJ], t, t4, sa);
+                        pin(acc[DA][JJ]);
+                    }
                     if constexpr (TWO && I == K - 1 && JJ == 0) {
                         // packet s+1's slot is complete once packet s's delay-1 term is in
 #pragma unroll
@@ -479,7 +521,7 @@ __global__ __launch_bounds__(kWaveThreads, 4) void fec_encode_wave_kernel(EncWav
                             acc[(U + 1) % W][j2] = 0;
                         }
                     }
-                    if constexpr (TWO) {
+                    if constexpr (NEEDB) {
                         constexpr int DB = (U + 1 + K + JJ - I) % W;
                         acc[DB][JJ] = mul_acc(acc[DB][JJ], t, t4, sb);
                         pin(acc[DB][JJ]);
@@ -487,15 +529,26 @@ __global__ __launch_bounds__(kWaveThreads, 4) void fec_encode_wave_kernel(EncWav
                 });
             }
             if constexpr (TWO) {
-                emit(s + 1, HB, QB);
-                flush(s + 2 - W);
+                if constexpr (!WARM) {
+                    emit(s + 1, HB, QB);
+                    flush(s + 2 - W, 2);
+                    done = s + 2 - W >= M;
+                }
             } else {  // odd W: the next block's first pair is (s+1, s+2)
-                flush(s + 1 - W);
+                if constexpr (!WARM) {
+                    flush(s + 1 - W, 1);
+                    done = s + 1 - W >= M;
+                }
                 ra = rb;
                 rb = na;
             }
         });
-    }
+    };
+
+    load(ra, 0);
+    load(rb, 1);
+    run_block(std::true_type{}, 0);
+    for (int blk = 1; blk < nblk && !done; ++blk) run_block(std::false_type{}, blk);
 }
 
 #ifdef FEC_WAVE_ONLY  // quick builds while tuning: -DFEC_WAVE_ONLY

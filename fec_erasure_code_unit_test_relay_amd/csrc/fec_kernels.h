@@ -162,7 +162,6 @@ struct RecArgs {
     uint8_t* out;
     int32_t* out_len;
     int L, k, n, S, CW;
-    int stage;                     // 1: source rows staged in LDS
 };
 
 struct StreamOutArgs {

@@ -454,56 +454,66 @@ __global__ __launch_bounds__(64) void fec_plan_kernel(PlanArgs a) {
 // (Decoder_Basic.cpp:76-79); byte h (sub-stream s = h/k, position i = h%k) is then
 // XOR_q coef[x][i][q] * cw[x-i+q][s*n+q] over the received symbols q of its diagonal.
 // ------------------------------------------------------------------------------------------
+constexpr int kRecMaxK = 16;  // = kMaxK (fec_host.h)
+constexpr int kRecMaxN = 17;  // = kMaxRuleN: codecs with n > 17 are refused
+
 __global__ __launch_bounds__(256) void fec_recover_kernel(RecArgs a) {
-    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-    uint8_t* gexp = smem;
-    uint8_t* glog = smem + 512;
-    uint8_t* cf = smem + 768;          // k*n <= 512
-    uint8_t* ob = smem + 1280;         // L+2 <= 1536
-    uint8_t* rows = smem + 2816;       // (k+n-1) rows of CW bytes
+    // One wave per recovered packet, no workgroup barrier after the table load: lane h computes
+    // bytes h, h+64, ... of [len_hi, len_lo, payload]; its n sources are byte loads straight from
+    // the diagonal's rows (a ~(k+n)*CW-byte window, L2-resident), all issued before the lookups.
+    __shared__ uint8_t gexp[512];
+    __shared__ uint8_t glog[256];
+    __shared__ uint8_t lcf[4][kRecMaxK * kRecMaxN];  // per wave: coefficient logs, 255 = zero coefficient
     const int tid = threadIdx.x;
-    const int L = a.L, k = a.k, n = a.n, CW = a.CW;
     for (int i = tid; i < 512; i += 256) gexp[i] = a.gf[i];
     for (int i = tid; i < 256; i += 256) glog[i] = a.gf[512 + i];
+    __syncthreads();
+    const int lane = tid & 63, wl = tid >> 6;
+    const int L = a.L, k = a.k, n = a.n, CW = a.CW;
     const int nrec = a.counters[2];
-    for (int r = blockIdx.x; r < nrec; r += gridDim.x) {
+    uint8_t* lc = lcf[wl];
+    const int waves = gridDim.x * 4;
+    for (int r = blockIdx.x * 4 + wl; r < nrec; r += waves) {
         const int64_t x = a.rec_list[r];
-        // stage the diagonal's source rows x-k+1 .. x+n-1 (those inside the stream) in LDS
-        const int64_t r0 = max<int64_t>(0, x - k + 1), r1 = min<int64_t>(a.P, x + n);
-        const uint8_t* rbase;  // row (x-k+1) of the diagonal's window
-        if (a.stage) {
-            const int nbytes = static_cast<int>((r1 - r0) * CW);
-            const uint8_t* src = a.cw + r0 * CW;
-            uint8_t* dst = rows + (r0 - (x - k + 1)) * CW;
-            if ((reinterpret_cast<uintptr_t>(src) & 3) == 0 && (nbytes & 3) == 0 &&
-                (reinterpret_cast<uintptr_t>(dst) & 3) == 0) {
-                for (int o = tid * 4; o < nbytes; o += 1024)
-                    *reinterpret_cast<uint32_t*>(dst + o) = *reinterpret_cast<const uint32_t*>(src + o);
-            } else {
-                for (int o = tid; o < nbytes; o += 256) dst[o] = src[o];
-            }
-            rbase = rows;
-        } else {
-            rbase = a.cw + (x - k + 1) * CW;  // only rows r0..r1-1 are ever touched
+        for (int i = lane; i < k * n; i += 64) {
+            const uint8_t c = a.coef[x * k * n + i];
+            lc[i] = c ? glog[c] : 255;
         }
-        for (int i = tid; i < k * n; i += 256) cf[i] = a.coef[x * k * n + i];
-        __syncthreads();
-        for (int h = tid; h < L + 2; h += 256) {
-            const int s = h / k, i = h - (h / k) * k;
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        int ln = 0;
+        for (int h0 = 0; h0 < L + 2; h0 += 64) {
+            const int h = h0 + lane;
             uint8_t acc = 0;
-            for (int q = 0; q < n; ++q) {
-                const uint8_t c = cf[i * n + q];
-                if (!c) continue;
-                // source: symbol q of packet x-i+q = row (k-1-i+q) of the window
-                acc ^= gf_mul_lds(gexp, glog, c, rbase[(k - 1 - i + q) * CW + s * n + q]);
+            if (h < L + 2) {
+                const int sidx = h / k, i = h - sidx * k;
+                uint8_t v[kRecMaxN];
+#pragma unroll
+                for (int q = 0; q < kRecMaxN; ++q) {
+                    v[q] = 0;
+                    if (q < n) {
+                        const int64_t row = x - i + q;
+                        if (lc[i * n + q] != 255 && row >= 0 && row < a.P) v[q] = a.cw[row * CW + sidx * n + q];
+                    }
+                }
+#pragma unroll
+                for (int q = 0; q < kRecMaxN; ++q) {
+                    if (q < n && v[q]) {
+                        const int lq = lc[i * n + q];
+                        if (lq != 255) acc ^= gexp[lq + glog[v[q]]];
+                    }
+                }
             }
-            ob[h] = acc;
+            if (h0 == 0) {  // recovered length (Decoder.cpp:141-149): bytes 0 and 1, clamped to L
+                const int hi = __builtin_amdgcn_readlane(static_cast<int>(acc), 0);
+                const int lo = __builtin_amdgcn_readlane(static_cast<int>(acc), 1);
+                ln = min(hi * 256 + lo, L);
+            }
+            const int b = h - 2;
+            if (b >= 0 && b < L) a.out[x * L + b] = b < ln ? acc : 0;
         }
-        __syncthreads();
-        const int ln = min(ob[0] * 256 + ob[1], L);
-        for (int b = tid; b < L; b += 256) a.out[x * L + b] = (b < ln) ? ob[b + 2] : 0;
-        if (tid == 0) a.out_len[x] = ln;
-        __syncthreads();
+        if (lane == 0) a.out_len[x] = ln;
+        __builtin_amdgcn_wave_barrier();  // lc is rewritten by the next packet
     }
 }
 
