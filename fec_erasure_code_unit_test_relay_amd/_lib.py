@@ -80,6 +80,13 @@ def lib() -> ctypes.CDLL:
     L.fec_decoder_receive.argtypes = [vp, vp, i32, i32, i32, vp, ip]
     L.fec_plan_host.argtypes = [i32, i32, i32, i32, vp, i64, vp]
     L.fec_util_fill_payload.argtypes = [vp, i64, i64, i32, ctypes.c_uint64, vp]
+    f32 = ctypes.c_float
+    L.fec_erasure_iid.argtypes = [vp, i32, f32, i32]
+    L.fec_erasure_three_sections_iid.argtypes = [vp, i32, f32, i32, f32, i32, f32, i32]
+    L.fec_erasure_ge.argtypes = [vp, i32, f32, f32, f32, i32, ip]
+    L.fec_erasure_ge_varying.argtypes = [vp, i32, f32, f32, f32, i32, ip]
+    L.fec_erasure_fritchman_varying.argtypes = [vp, i32, f32, f32, f32, i32, i32]
+    L.fec_erasure_periodic.argtypes = [vp, i32, i32, i32, i32]
     for name in ["fec_codec_create", "fec_codec_destroy", "fec_codec_set_encode_path",
                  "fec_codec_set_copy_path", "fec_codec_set_plan_path", "fec_codec_info", "fec_codec_set_episode_dedup", "fec_debug_stamps", "fec_codec_geometry",
                  "fec_codec_generator", "fec_encode_batch", "fec_decode_batch", "fec_decode_plan",
@@ -87,7 +94,9 @@ def lib() -> ctypes.CDLL:
                  "fec_decode_counters", "fec_decode_plan_stats", "fec_timing_enable", "fec_timing_collect",
                  "fec_encoder_create", "fec_encoder_destroy", "fec_encoder_transmit",
                  "fec_decoder_create", "fec_decoder_destroy", "fec_decoder_receive",
-                 "fec_plan_host", "fec_util_fill_payload"]:
+                 "fec_plan_host", "fec_util_fill_payload", "fec_erasure_iid",
+                 "fec_erasure_three_sections_iid", "fec_erasure_ge", "fec_erasure_ge_varying",
+                 "fec_erasure_fritchman_varying", "fec_erasure_periodic"]:
         getattr(L, name).restype = i32
     _lib = L
     return _lib

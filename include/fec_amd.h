@@ -152,6 +152,29 @@ int fec_decoder_receive(fec_decoder *dec, const uint8_t *codeword, int codeword_
 int fec_plan_host(int max_payload, int T, int B, int N, const uint8_t *erasure, int64_t P,
                   uint8_t *fate);
 
+/* ---- erasure patterns (inputs of the decode path; host only, no device needed) ---------------
+ * Byte-exact restatements of Erasure_File_Generator (src/Erasure_File_Generator.cpp:25-287): out[i]
+ * = 1 if packet i is erased.  Same engine (mt19937), same draw order and the same libstdc++
+ * uniform_real_distribution<double> arithmetic as the reference; probabilities are float as in
+ * its signatures.  The reference writes these bytes to erasure.bin (read back by
+ * Erasure_Simulator, src/Erasure_Simulator.cpp:13-30). */
+/* generate_IID (:25-63); seed 0 = SEED_ARTIFICIAL_ERASURE */
+int fec_erasure_iid(uint8_t *out, int count, float erasure_prob, int seed);
+/* generate_three_sections_IID (:65-121) */
+int fec_erasure_three_sections_iid(uint8_t *out, int count1, float prob1, int count2, float prob2,
+                                   int count3, float prob3, int seed);
+/* generate_GE (:123-170) / generate_GE_varying (:172-213); good_state: the generator object's
+ * state carried across calls (in/out, NULL = a fresh object, i.e. good) */
+int fec_erasure_ge(uint8_t *out, int count, float alpha, float beta, float erasure_prob, int seed,
+                   int *good_state);
+int fec_erasure_ge_varying(uint8_t *out, int count, float alpha, float beta, float erasure_prob,
+                           int seed, int *good_state);
+/* generate_Fritchman_varying (:215-264) */
+int fec_erasure_fritchman_varying(uint8_t *out, int count, float alpha, float beta,
+                                  float erasure_prob, int number_of_states, int seed);
+/* generate_periodic (:266-287) */
+int fec_erasure_periodic(uint8_t *out, int count, int T, int B, int N);
+
 /* ---- utility (tests / bench only, not on the coding path) ---------------------------------
  * Synthetic payloads: byte b of packet t0+p = low 8 bits of splitmix64(seed ^ ((t0+p)*L + b)). */
 int fec_util_fill_payload(uint8_t *d_out, int64_t t0, int64_t count, int L, uint64_t seed,
