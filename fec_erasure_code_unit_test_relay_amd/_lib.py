@@ -43,6 +43,13 @@ def lib() -> ctypes.CDLL:
         raise RuntimeError(
             f"{LIB_PATH} is missing: the HIP extension must be built first "
             "(make -C fec_erasure_code_unit_test_relay_amd/csrc); there is no fallback")
+    # torch ships its own libamdhip64.so.7 (same SONAME as /opt/rocm's): whichever is loaded first
+    # serves the whole process.  Load torch's first so that the tensors torch allocates and the
+    # kernels this library launches share one HIP runtime.
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     L = ctypes.CDLL(LIB_PATH)
     vp, i32, i64 = ctypes.c_void_p, ctypes.c_int, ctypes.c_int64
     ip = ctypes.POINTER(ctypes.c_int)
@@ -87,6 +94,13 @@ def lib() -> ctypes.CDLL:
     L.fec_erasure_ge_varying.argtypes = [vp, i32, f32, f32, f32, i32, ip]
     L.fec_erasure_fritchman_varying.argtypes = [vp, i32, f32, f32, f32, i32, i32]
     L.fec_erasure_periodic.argtypes = [vp, i32, i32, i32, i32]
+    L.fec_vr_plan_create.argtypes = [i32, i32, i32, i32, i32, vp, i64, i64, ctypes.POINTER(vp)]
+    L.fec_vr_plan_destroy.argtypes = [vp]
+    L.fec_vr_plan_stats.argtypes = [vp, i64p, i64p, ctypes.POINTER(ctypes.c_double), i64p, ip, ip, ip]
+    L.fec_vr_plan_instances.argtypes = [vp, vp, vp]
+    L.fec_vr_plan_packets.argtypes = [vp, vp, vp, vp, vp]
+    L.fec_vr_encode_batch.argtypes = [vp, vp, vp, vp, vp, vp, vp, vp]
+    L.fec_vr_decode_batch.argtypes = [vp, vp, vp, vp, vp, vp, vp]
     for name in ["fec_codec_create", "fec_codec_destroy", "fec_codec_set_encode_path",
                  "fec_codec_set_copy_path", "fec_codec_set_plan_path", "fec_codec_info", "fec_codec_set_episode_dedup", "fec_debug_stamps", "fec_codec_geometry",
                  "fec_codec_generator", "fec_encode_batch", "fec_decode_batch", "fec_decode_plan",
@@ -96,7 +110,9 @@ def lib() -> ctypes.CDLL:
                  "fec_decoder_create", "fec_decoder_destroy", "fec_decoder_receive",
                  "fec_plan_host", "fec_util_fill_payload", "fec_erasure_iid",
                  "fec_erasure_three_sections_iid", "fec_erasure_ge", "fec_erasure_ge_varying",
-                 "fec_erasure_fritchman_varying", "fec_erasure_periodic"]:
+                 "fec_erasure_fritchman_varying", "fec_erasure_periodic", "fec_vr_plan_create",
+                 "fec_vr_plan_destroy", "fec_vr_plan_stats", "fec_vr_plan_instances", "fec_vr_plan_packets",
+                 "fec_vr_encode_batch", "fec_vr_decode_batch"]:
         getattr(L, name).restype = i32
     _lib = L
     return _lib

@@ -1,0 +1,554 @@
+// fec_vr.cpp -- variable-rate (adaptive) coding, BASELINE config 4: the symbolic P2P loop
+// (VrPlan, see fec_vr.h) and the batched device execution of its schedule.
+#include "fec_vr.h"
+
+#include <hip/hip_runtime_api.h>
+
+#include <algorithm>
+#include <cstring>
+#include <new>
+#include <stdexcept>
+
+#include "fec_amd.h"
+
+namespace fec {
+
+// ---- Parameter_Estimator::estimate (Parameter_Estimator.cpp:58-190) -------------------------
+void ParameterEstimator::estimate(int64_t seq, int msg_T) {
+    if (T == 0) return;
+    if (previous_win_end == -2) {  // first packet seen: reset the window (:66-73)
+        T = msg_T;
+        previous_win_end = seq - 1;
+    }
+    const int64_t current_win_end = seq;
+    if (current_win_end - previous_win_end < 1) return;  // out of order (:84-86)
+    for (int64_t s = previous_win_end + 1; s <= current_win_end; ++s) {
+        for (int i = T; i >= 1; --i) erasure[i] = erasure[i - 1];
+        erasure[0] = s < current_win_end;  // the packets in between were lost
+        int sum = 0;
+        for (int i = 0; i <= T; ++i) sum += erasure[i] ? 1 : 0;
+        if (sum == T + 1 || sum == 0) continue;  // (:104-105)
+        if (B == 0) B = 1;
+        if (N == 0) N = 1;
+        if (sum > N_max) N_max = sum;
+        int first = 0, last = T;
+        while (first <= T && !erasure[first]) ++first;
+        while (last >= 0 && !erasure[last]) --last;
+        const int span = last - first + 1;
+        if (span == T + 1) {  // (:131-136)
+            if (sum > N) {
+                N = sum;
+                B = N;
+            }
+        } else {  // (:137-166)
+            const int max_B_and_sum = sum > B ? sum : B;
+            const int max_B_and_span = span > B ? span : B;
+            if ((T - N + 1) * (T - sum + 1 + max_B_and_sum) >= (T - sum + 1) * (T - N + 1 + max_B_and_span)) {
+                if (span > B) {
+                    B = span;
+                    N = span;
+                }
+            } else {
+                if (sum > N) {
+                    N = sum;
+                    B = sum;
+                }
+                if (N > B) B = N;
+            }
+        }
+        if ((T - N_max + 1) * (T - N + 1 + B) > (T - N + 1) * (T + 1)) {  // (:169-173)
+            B = N_max;
+            N = N_max;
+        }
+    }
+    previous_win_end = current_win_end;
+    if ((T - N_current + 1) * (T - N + 1 + B) >= (T - N + 1) * (T - N_current + 1 + B_current)) {  // (:177-181)
+        B_current = B;
+        N_current = N;
+    }
+    if (adaptive_mode_MDS) make_MDS_estimates();
+}
+
+// Parameter_Estimator::make_MDS_estimates (:209-221)
+void ParameterEstimator::make_MDS_estimates() {
+    if (B_current > N_current) {
+        while ((T - N_current) * (T - N_current + 1 + B_current) > (T + 1) * (T - N_current + 1)) ++N_current;
+        B_current = N_current;
+    }
+}
+
+const DecodeRules& VrPlan::rules_for(int T, int B, int N) {
+    const int key = T * 1024 + B * 32 + N;
+    auto it = rules_.find(key);
+    if (it != rules_.end()) return *it->second;
+    const Geometry g = Geometry::make(L, T, B, N);
+    std::unique_ptr<DecodeRules> r(new DecodeRules());
+    r->build(make_generator(T, B, N), g.k, g.n, g.T);
+    return *rules_.emplace(key, std::move(r)).first->second;
+}
+
+namespace {
+
+constexpr int kTTot = 10;                 // T_TOT (FEC_Macro.h:32)
+constexpr int kEstimationCycle = 1000 / 10;  // ESTIMATION_WINDOW_SIZE / ..._REDUCTION_FACTOR (:54-55)
+
+struct SymDecoder {  // one FEC_Decoder instance, symbolically
+    Geometry g;
+    std::unique_ptr<StreamPlanner> planner;
+    int64_t first = 0, next = 0;
+    StepResult call(int64_t seq, bool erased) {
+        if (seq != next) throw std::logic_error("vr: decoder calls out of order");
+        ++next;
+        return planner->step(seq - first, erased);
+    }
+};
+
+}  // namespace
+
+void VrPlan::run(int max_payload, int T, int B, int N, bool mds, const uint8_t* pattern, int64_t n_pattern,
+                 int64_t P_value) {
+    L = max_payload;
+    T_init = T;
+    B_init = B;
+    N_init = N;
+    adaptive_mode_MDS = mds;
+    P = P_value;
+    frames.clear();
+    enc.clear();
+    dec.clear();
+    erased.clear();
+    fate.assign(static_cast<size_t>(P), kNone);
+    fate_dec.assign(static_cast<size_t>(P), -1);
+    lost = switches = 0;
+    sum_coding_rate = 0;
+
+    // ---- sender (Application_Layer_Sender.cpp:9-31, 64-93, 221-224) ----
+    const bool adaptive = B == -1 || N == -1;
+    int sT = T, sB = adaptive ? 0 : B, sN = adaptive ? 0 : N;
+    int sT_ack = sT, sB_ack = sB, sN_ack = sN;
+    // ---- Variable_Rate_FEC_Encoder (Variable_Rate_FEC_Encoder.cpp:25-58, 74-235) ----
+    int eT = 0, eB = 0, eN = 0, eN_old = 0;
+    int cur = -1, old = -1;
+    int counter_transition = 0;
+    bool transition_flag = true, double_coding_flag = true;
+    // ---- receiver (Application_Layer_Receiver.cpp:10-31, 321-468) ----
+    std::unique_ptr<ParameterEstimator> est(new ParameterEstimator(kTTot, mds));
+    std::unique_ptr<ParameterEstimator> bg(new ParameterEstimator(kTTot, mds));
+    int64_t cycle = 1;
+    uint8_t udp[12] = {};
+    // ---- Variable_Rate_FEC_Decoder (Variable_Rate_FEC_Decoder.cpp:25-80, 2133-2400, 2440-2514) ----
+    int64_t seq_start = -1, latest_seq = -1, sdc = -1, sde = -1;
+    int dT = 0, dB = 0, dN = 0;
+    int dcur = -1, dold = -1;
+    bool dcf = false;
+    std::vector<SymDecoder> sd;
+
+    auto new_decoder = [&](int T_, int B_, int N_, int64_t first) {
+        SymDecoder d;
+        d.g = Geometry::make(L, T_, B_, N_);
+        d.planner.reset(new StreamPlanner(d.g, &rules_for(T_, B_, N_)));
+        d.first = d.next = first;
+        sd.push_back(std::move(d));
+        VrInstance v;
+        v.T = T_;
+        v.B = B_;
+        v.N = N_;
+        v.first = v.end = first;
+        v.role_switch = -1;  // set when it becomes the old decoder
+        dec.push_back(v);
+        return static_cast<int>(sd.size()) - 1;
+    };
+    auto call = [&](int id, int64_t seq, bool er) {
+        const StepResult r = sd[id].call(seq, er);
+        dec[id].end = seq + 1;
+        return r;
+    };
+    // onDecodedMessage (:2403-2436): packets seq - T >= seq_start are reported once
+    auto report = [&](int id, int64_t seq, const StepResult& r) {
+        const int64_t x = seq - dT;
+        if (x < seq_start || x >= P) return;
+        const PacketFate f = r.fate == kNone ? kLost : r.fate;
+        fate[x] = f;
+        fate_dec[x] = id;
+        if (f == kLost) ++lost;
+    };
+    auto update_decoder = [&](int T_, int B_, int N_, int64_t first) {  // (:2520-2536)
+        dold = dcur;
+        dT = T_;
+        dB = B_;
+        dN = N_;
+        dcur = new_decoder(T_, B_, N_, first);
+        dec[dold].role_switch = first;
+    };
+
+    for (int64_t seq = 0;; ++seq) {
+        // ---- Application_Layer_Sender::generate_message_and_encode ----
+        if (adaptive && udp[0] != 0) {
+            sT = udp[0];
+            sB = udp[1];
+            sN = udp[2];
+            sT_ack = udp[3];
+            sB_ack = udp[4];
+            sN_ack = udp[5];
+        }
+        (void)sN_ack;
+        int mT = sT, mB = sB, mN = sN;
+        // ---- Variable_Rate_FEC_Encoder::encode ----
+        if (cur < 0) {
+            eT = mT;
+            eB = mB;
+            eN = mN;
+            enc.push_back(VrInstance{eT, eB, eN, seq, seq, -1});
+            cur = 0;
+            transition_flag = true;
+            double_coding_flag = false;
+        } else if ((mT != eT || mB != eB || mN != eN) && !transition_flag && sT_ack == eT && sB_ack == eB) {
+            ++switches;  // "Start double coding at the source"
+            eN_old = eN;
+            eT = mT;
+            eB = mB;
+            eN = mN;
+            transition_flag = true;
+            double_coding_flag = true;
+            counter_transition = 0;
+            old = cur;
+            enc[old].role_switch = seq;
+            enc.push_back(VrInstance{eT, eB, eN, seq, seq, -1});
+            cur = static_cast<int>(enc.size()) - 1;
+        } else {
+            mT = eT;
+            mB = eB;
+            mN = eN;
+        }
+        VrFrame fr;
+        fr.T = mT;
+        fr.B = mB;
+        fr.N = mN;
+        fr.enc_cur = cur;
+        enc[cur].end = seq + 1;
+        fr.counter = counter_transition;
+        if (counter_transition <= eT) {
+            if (counter_transition == eT) double_coding_flag = false;
+            ++counter_transition;
+            if (old >= 0 && double_coding_flag) {
+                fr.enc_old = old;
+                enc[old].end = seq + 1;
+            }
+        } else {
+            transition_flag = false;
+        }
+        if (!double_coding_flag)
+            sum_coding_rate += static_cast<float>(eT - eN + 1) / (eT - eN + 1 + eB);
+        else
+            sum_coding_rate += static_cast<float>(eT - eN + 1) / ((eT - eN + 1 + eB) + (eT - eN_old + 1) + (eT - eN_old + 1 + eB));
+        frames.push_back(fr);
+        const bool drop = seq < P + T && seq < n_pattern && pattern[seq] == 1;
+        erased.push_back(drop ? 1 : 0);
+        sent = seq + 1;
+
+        // ---- Application_Layer_Receiver::receive_message_and_decode ----
+        if (drop) continue;  // artificial erasure: returns -1, feedback unchanged
+        est->estimate(seq, fr.T);
+        bg->estimate(seq, fr.T);
+        if (seq + 1 > cycle * kEstimationCycle) {
+            est = std::move(bg);
+            bg.reset(new ParameterEstimator(kTTot, false));
+            ++cycle;
+        }
+        // ---- Variable_Rate_FEC_Decoder::decode ----
+        if (seq_start == -1) {  // initialize_decoder (:2478-2494)
+            seq_start = 0;
+            latest_seq = 0;
+            dT = fr.T;
+            dB = fr.B;
+            dN = fr.N;
+            dcur = new_decoder(dT, dB, dN, 0);
+        }
+        if (seq >= latest_seq) {
+            if (dT != fr.T || dB != fr.B || dN != fr.N) sdc = seq - fr.counter;
+            for (int64_t s = latest_seq; s < seq; ++s) {  // the missing packets (:2200-2330)
+                if (s > sde && dcf) dcf = false;
+                if (s == sdc) {
+                    update_decoder(fr.T, fr.B, fr.N, s);
+                    sde = sdc + dT - 1;
+                    dcf = true;
+                }
+                if (!dcf) {
+                    report(dcur, s, call(dcur, s, true));
+                } else {
+                    if (dold >= 0) report(dold, s, call(dold, s, true));
+                    call(dcur, s, true);
+                }
+            }
+            if (seq > sde && dcf) dcf = false;
+            if (seq == sdc) {
+                update_decoder(fr.T, fr.B, fr.N, seq);
+                sde = sdc + dT - 1;
+                dcf = true;
+            }
+            if (!dcf) {
+                report(dcur, seq, call(dcur, seq, false));
+            } else {
+                if (dold >= 0) report(dold, seq, call(dold, seq, false));
+                call(dcur, seq, false);
+            }
+            latest_seq = seq + 1;
+        }
+        udp[0] = static_cast<uint8_t>(est->T);
+        udp[1] = static_cast<uint8_t>(est->B_current);
+        udp[2] = static_cast<uint8_t>(est->N_current);
+        udp[3] = static_cast<uint8_t>(fr.T);
+        udp[4] = static_cast<uint8_t>(fr.B);
+        udp[5] = static_cast<uint8_t>(fr.N);
+        if (seq >= P + T - 1) break;  // application_local_simulation.cpp:813
+    }
+    for (auto* list : {&enc, &dec})
+        for (auto& e : *list)
+            if (e.role_switch < 0) e.role_switch = e.end;  // never became the old instance
+}
+
+}  // namespace fec
+
+// ------------------------------------------------------------------------------------------
+// C ABI
+// ------------------------------------------------------------------------------------------
+struct fec_vr_plan {
+    fec::VrPlan plan;
+    int cw_max = 0;
+    // device execution state (created on first use)
+    std::map<int, fec_codec*> codecs;  // key T*1024 + B*32 + N
+    uint8_t* d_gather = nullptr;
+    size_t gather_bytes = 0;
+    void* d_ws = nullptr;
+    size_t ws_bytes = 0;
+    ~fec_vr_plan() {
+        for (auto& kv : codecs) fec_codec_destroy(kv.second);
+        if (d_gather) (void)hipFree(d_gather);
+        if (d_ws) (void)hipFree(d_ws);
+    }
+    int codec(const fec::VrInstance& v, fec_codec** out) {
+        const int key = v.T * 1024 + v.B * 32 + v.N;
+        auto it = codecs.find(key);
+        if (it == codecs.end()) {
+            fec_codec* c = nullptr;
+            if (int st = fec_codec_create(plan.L, v.T, v.B, v.N, &c)) return st;
+            it = codecs.emplace(key, c).first;
+        }
+        *out = it->second;
+        return FEC_OK;
+    }
+};
+
+namespace {
+template <typename F>
+int vr_guarded(F&& f) {
+    try {
+        return f();
+    } catch (const std::bad_alloc&) {
+        return FEC_ERR_NOMEM;
+    } catch (...) {
+        return FEC_ERR_ARG;
+    }
+}
+int cw_of(const fec::VrPlan& p, const fec::VrInstance& v) { return fec::Geometry::make(p.L, v.T, v.B, v.N).CW; }
+}  // namespace
+
+extern "C" {
+
+int fec_vr_plan_create(int max_payload, int T, int B, int N, int adaptive_mode_MDS, const uint8_t* erasure,
+                       int64_t n_erasure, int64_t P, fec_vr_plan** out) {
+    if (!out || P < 1 || n_erasure < 0 || (n_erasure > 0 && !erasure) || T < 1 || T > 11) return FEC_ERR_ARG;
+    *out = nullptr;
+    return vr_guarded([&] {
+        std::unique_ptr<fec_vr_plan> v(new fec_vr_plan());
+        v->plan.run(max_payload, T, B, N, adaptive_mode_MDS != 0, erasure, n_erasure, P);
+        for (const auto& e : v->plan.enc) v->cw_max = std::max(v->cw_max, cw_of(v->plan, e));
+        for (const auto& d : v->plan.dec) v->cw_max = std::max(v->cw_max, cw_of(v->plan, d));
+        *out = v.release();
+        return FEC_OK;
+    });
+}
+
+int fec_vr_plan_destroy(fec_vr_plan* v) {
+    delete v;
+    return FEC_OK;
+}
+
+int fec_vr_plan_stats(const fec_vr_plan* v, int64_t* lost, int64_t* switches, double* coding_rate,
+                      int64_t* sent, int* n_encoders, int* n_decoders, int* cw_max) {
+    if (!v) return FEC_ERR_ARG;
+    if (lost) *lost = v->plan.lost;
+    if (switches) *switches = v->plan.switches;
+    if (coding_rate) *coding_rate = v->plan.coding_rate();
+    if (sent) *sent = v->plan.sent;
+    if (n_encoders) *n_encoders = static_cast<int>(v->plan.enc.size());
+    if (n_decoders) *n_decoders = static_cast<int>(v->plan.dec.size());
+    if (cw_max) *cw_max = v->cw_max;
+    return FEC_OK;
+}
+
+static void put_instances(const std::vector<fec::VrInstance>& in, int64_t* out) {
+    for (size_t i = 0; i < in.size(); ++i) {
+        int64_t* o = out + 6 * i;
+        o[0] = in[i].T;
+        o[1] = in[i].B;
+        o[2] = in[i].N;
+        o[3] = in[i].first;
+        o[4] = in[i].role_switch;
+        o[5] = in[i].end;
+    }
+}
+
+int fec_vr_plan_instances(const fec_vr_plan* v, int64_t* encoders, int64_t* decoders) {
+    if (!v) return FEC_ERR_ARG;
+    if (encoders) put_instances(v->plan.enc, encoders);
+    if (decoders) put_instances(v->plan.dec, decoders);
+    return FEC_OK;
+}
+
+int fec_vr_plan_packets(const fec_vr_plan* v, int32_t* frames, uint8_t* erased, uint8_t* fate,
+                        int32_t* fate_decoder) {
+    if (!v) return FEC_ERR_ARG;
+    const auto& p = v->plan;
+    for (int64_t s = 0; s < p.sent; ++s) {
+        if (frames) {
+            int32_t* o = frames + 6 * s;
+            o[0] = p.frames[s].T;
+            o[1] = p.frames[s].B;
+            o[2] = p.frames[s].N;
+            o[3] = p.frames[s].counter;
+            o[4] = p.frames[s].enc_cur;
+            o[5] = p.frames[s].enc_old;
+        }
+        if (erased) erased[s] = p.erased[s];
+    }
+    if (fate) std::memcpy(fate, p.fate.data(), p.fate.size());
+    if (fate_decoder) std::memcpy(fate_decoder, p.fate_dec.data(), p.fate_dec.size() * 4);
+    return FEC_OK;
+}
+
+// Encode every packet the sender produced: row s of d_cw_cur (stride cw_max) = the codeword of
+// frame s's current encoder, row s of d_cw_old = its old encoder's (double coding; rows of frames
+// without one are left alone), trimmed sizes in d_len_*.  One fec_encode_batch per instance role:
+// an instance created at seq f encodes rows [f, role_switch) as current and [role_switch, end) as
+// old, the second launch with the rows in front of it as history (X_{t'<f} = 0 at row f).
+int fec_vr_encode_batch(fec_vr_plan* v, const uint8_t* d_payload, const int32_t* d_payload_len, uint8_t* d_cw_cur,
+                        int32_t* d_len_cur, uint8_t* d_cw_old, int32_t* d_len_old, void* hip_stream) {
+    if (!v || !d_payload || !d_cw_cur || !d_len_cur || !d_cw_old || !d_len_old) return FEC_ERR_ARG;
+    const auto& p = v->plan;
+    const hipStream_t s = static_cast<hipStream_t>(hip_stream);
+    const int64_t W = v->cw_max;
+    for (const auto& e : p.enc) {
+        fec_codec* c = nullptr;
+        if (int st = v->codec(e, &c)) return st;
+        int CW = 0;
+        fec_codec_geometry(c, nullptr, nullptr, nullptr, &CW);
+        if (CW == W) {
+            // rows go straight to the strided arrays
+            const int64_t n1 = e.role_switch - e.first, n2 = e.end - e.role_switch;
+            if (n1 > 0) {
+                if (int st = fec_encode_batch(c, d_payload + e.first * p.L, d_payload_len ? d_payload_len + e.first : nullptr,
+                                              0, n1, d_cw_cur + e.first * W, d_len_cur + e.first, hip_stream))
+                    return st;
+            }
+            if (n2 > 0) {
+                if (int st = fec_encode_batch(c, d_payload + e.role_switch * p.L,
+                                              d_payload_len ? d_payload_len + e.role_switch : nullptr, n1, n2,
+                                              d_cw_old + e.role_switch * W, d_len_old + e.role_switch, hip_stream))
+                    return st;
+            }
+            continue;
+        }
+        // narrower codewords: encode densely, then scatter into the cw_max-stride rows
+        const int64_t rows = e.end - e.first;
+        const size_t need = static_cast<size_t>(rows) * CW;
+        if (need > v->gather_bytes) {
+            if (v->d_gather) (void)hipFree(v->d_gather);
+            v->d_gather = nullptr;
+            v->gather_bytes = 0;
+            if (hipMalloc(&v->d_gather, need) != hipSuccess) return FEC_ERR_NOMEM;
+            v->gather_bytes = need;
+        }
+        const int64_t n1 = e.role_switch - e.first, n2 = e.end - e.role_switch;
+        if (n1 > 0) {
+            if (int st = fec_encode_batch(c, d_payload + e.first * p.L, d_payload_len ? d_payload_len + e.first : nullptr, 0,
+                                          n1, v->d_gather, d_len_cur + e.first, hip_stream))
+                return st;
+            if (hipMemcpy2DAsync(d_cw_cur + e.first * W, W, v->d_gather, CW, CW, n1, hipMemcpyDeviceToDevice, s) != hipSuccess)
+                return FEC_ERR_HIP;
+        }
+        if (n2 > 0) {
+            if (int st = fec_encode_batch(c, d_payload + e.role_switch * p.L,
+                                          d_payload_len ? d_payload_len + e.role_switch : nullptr, n1, n2,
+                                          v->d_gather + n1 * CW, d_len_old + e.role_switch, hip_stream))
+                return st;
+            if (hipMemcpy2DAsync(d_cw_old + e.role_switch * W, W, v->d_gather + n1 * CW, CW, CW, n2,
+                                 hipMemcpyDeviceToDevice, s) != hipSuccess)
+                return FEC_ERR_HIP;
+        }
+    }
+    return FEC_OK;
+}
+
+// Decode the schedule: decoder instance j is fed, at seq s in [first, end), the codeword the frame
+// carries for its role (current part while s < role_switch, old part after), zero padded to its
+// CW (the frame's wire parts are trimmed codewords; rows beyond an encoder's CW are zero), and
+// erasure flag erased[s].  It reports packets [first, role_switch) (the reference reports through
+// the old decoder during double coding): fec_decode_batch writes its outputs straight into rows
+// first.. of d_out, instances in increasing order, so each later instance overwrites the rows past
+// its predecessor's range.  d_cw_* rows must be zero beyond each encoder's CW.
+int fec_vr_decode_batch(fec_vr_plan* v, const uint8_t* d_cw_cur, const uint8_t* d_cw_old, const uint8_t* d_erased,
+                        uint8_t* d_out, int32_t* d_out_len, void* hip_stream) {
+    if (!v || !d_cw_cur || !d_cw_old || !d_erased || !d_out || !d_out_len) return FEC_ERR_ARG;
+    const auto& p = v->plan;
+    const hipStream_t s = static_cast<hipStream_t>(hip_stream);
+    const int64_t W = v->cw_max;
+    for (size_t j = 0; j < p.dec.size(); ++j) {
+        const auto& d = p.dec[j];
+        fec_codec* c = nullptr;
+        if (int st = v->codec(d, &c)) return st;
+        int CW = 0;
+        fec_codec_geometry(c, nullptr, nullptr, nullptr, &CW);
+        const int64_t rows = d.end - d.first;
+        if (rows <= d.T) continue;  // outputs only for packets before its first call
+        const size_t need = static_cast<size_t>(rows) * CW;
+        if (need > v->gather_bytes) {
+            if (v->d_gather) (void)hipFree(v->d_gather);
+            v->d_gather = nullptr;
+            v->gather_bytes = 0;
+            if (hipMalloc(&v->d_gather, need) != hipSuccess) return FEC_ERR_NOMEM;
+            v->gather_bytes = need;
+        }
+        const int64_t n1 = d.role_switch - d.first, n2 = d.end - d.role_switch;
+        if (n1 > 0 && hipMemcpy2DAsync(v->d_gather, CW, d_cw_cur + d.first * W, W, CW, n1, hipMemcpyDeviceToDevice, s) !=
+                          hipSuccess)
+            return FEC_ERR_HIP;
+        if (n2 > 0 && hipMemcpy2DAsync(v->d_gather + n1 * CW, CW, d_cw_old + d.role_switch * W, W, CW, n2,
+                                       hipMemcpyDeviceToDevice, s) != hipSuccess)
+            return FEC_ERR_HIP;
+        const size_t ws = fec_decode_workspace_bytes(c, rows);
+        if (ws > v->ws_bytes) {
+            if (v->d_ws) (void)hipFree(v->d_ws);
+            v->d_ws = nullptr;
+            v->ws_bytes = 0;
+            if (hipMalloc(&v->d_ws, ws) != hipSuccess) return FEC_ERR_NOMEM;
+            v->ws_bytes = ws;
+        }
+        // rows past P are not part of the output
+        const int64_t out_rows = std::min<int64_t>(rows - d.T, p.P - d.first);
+        if (out_rows <= 0) continue;
+        if (out_rows == rows - d.T) {
+            if (int st = fec_decode_batch(c, v->d_gather, d_erased + d.first, rows, d_out + d.first * p.L,
+                                          d_out_len + d.first, v->d_ws, v->ws_bytes, hip_stream))
+                return st;
+        } else {  // the last instance: decode fewer calls so that no row past P is written
+            const int64_t r2 = out_rows + d.T;
+            if (int st = fec_decode_batch(c, v->d_gather, d_erased + d.first, r2, d_out + d.first * p.L,
+                                          d_out_len + d.first, v->d_ws, v->ws_bytes, hip_stream))
+                return st;
+        }
+    }
+    return FEC_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,76 @@
+// fec_vr.h -- variable-rate (adaptive) coding: the control plane of BASELINE config 4.
+//
+// The reference's P2P loop (application_local_simulation.cpp:328-345, RELAYING_TYPE 0) chains
+//   Application_Layer_Sender::generate_message_and_encode   (src/Application_Layer_Sender.cpp:64-282)
+//     -> Variable_Rate_FEC_Encoder::encode                  (src/Variable_Rate_FEC_Encoder.cpp:74-235)
+//   Application_Layer_Receiver::receive_message_and_decode  (src/Application_Layer_Receiver.cpp:321-468)
+//     -> Parameter_Estimator::estimate x2 (foreground / background, swapped every
+//        ESTIMATION_WINDOW_SIZE / ESTIMATION_WINDOW_SIZE_REDUCTION_FACTOR packets)
+//     -> Variable_Rate_FEC_Decoder::decode                  (src/Variable_Rate_FEC_Decoder.cpp:2133-2400)
+// with the receiver's 6-byte feedback [T, B_est, N_est, T_ack, B_ack, N_ack] read by the sender at
+// the next packet.  Which (T,B,N) encodes which packet, when double coding starts and stops, which
+// decoder instance reports which packet and whether it is lost depend only on the erasure
+// pattern, never on payload bytes (recovered headers always carry max_payload here).  VrPlan runs
+// that loop symbolically (StreamPlanner per decoder instance) and records the schedule: encoder
+// and decoder instances with their sequence ranges, per-packet frame headers and the reported
+// fate of every packet.  The byte work of the schedule then runs batched on the GPU
+// (fec_vr_encode_batch / fec_vr_decode_batch in fec_vr.cpp): one launch pair per instance.
+#pragma once
+
+#include <cstdint>
+#include <map>
+#include <memory>
+#include <vector>
+
+#include "fec_host.h"
+
+namespace fec {
+
+// Parameter_Estimator (src/Parameter_Estimator.cpp:21-223), RELAYING_TYPE 0.
+struct ParameterEstimator {
+    bool adaptive_mode_MDS = false;
+    int T = 0, B = 0, N = 0, N_max = 0, B_current = 0, N_current = 0;
+    bool erasure[12] = {};
+    int64_t previous_win_end = -2;
+    ParameterEstimator(int T_value, bool mds) : adaptive_mode_MDS(mds), T(T_value) {}
+    void estimate(int64_t seq, int msg_T);
+    void make_MDS_estimates();
+};
+
+struct VrInstance {
+    int T = 0, B = 0, N = 0;
+    int64_t first = 0;   // seq of its first call
+    int64_t end = 0;     // one past the seq of its last call (calls are consecutive)
+    int64_t role_switch = -1;  // seq from which it is the old instance (double coding); == end if never
+};
+
+struct VrFrame {  // Application_Layer_Sender header (Application_Layer_Sender.cpp:259-269) + VR frame
+    int T = 0, B = 0, N = 0, counter = 0;
+    int enc_cur = -1, enc_old = -1;  // encoder instances whose codewords the frame carries
+};
+
+struct VrPlan {
+    int L = 0, T_init = 0, B_init = 0, N_init = 0;
+    bool adaptive_mode_MDS = false;
+    int64_t P = 0;                    // NUMBER_OF_ITERATIONS: packets whose output is counted
+    int64_t sent = 0;                 // packets the sender produced (>= P + T)
+    std::vector<uint8_t> erased;      // [sent]: dropped before the receiver (Application_Layer_Receiver.cpp:352-360)
+    std::vector<VrFrame> frames;      // [sent]
+    std::vector<VrInstance> enc, dec;
+    std::vector<uint8_t> fate;        // [P]: PacketFate of the output reported for packet x
+    std::vector<int32_t> fate_dec;    // [P]: decoder instance that reported it
+    int64_t lost = 0, switches = 0;   // "Start double coding at the source" count
+    float sum_coding_rate = 0;        // Variable_Rate_FEC_Encoder final_sum_coding_rate
+    double coding_rate() const { return sent ? sum_coding_rate / static_cast<float>(sent) : 0.0; }
+
+    // Runs the loop until the receiver has processed seq P+T-1 (application_local_simulation.cpp:813).
+    // B_init = N_init = -1: adaptive (the sender starts at (T, 0, 0)).
+    void run(int max_payload, int T, int B, int N, bool mds, const uint8_t* pattern, int64_t n_pattern,
+             int64_t P_value);
+
+private:
+    std::map<int, std::unique_ptr<DecodeRules>> rules_;  // key T*1024 + B*32 + N
+    const DecodeRules& rules_for(int T, int B, int N);
+};
+
+}  // namespace fec

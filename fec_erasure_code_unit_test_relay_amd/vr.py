@@ -1,0 +1,84 @@
+"""Variable-rate (adaptive) coding -- BASELINE config 4 -- over the C ABI (fec_vr.cpp).
+
+``VrPlan`` runs the reference's P2P loop (Application_Layer_Sender -> Variable_Rate_FEC_Encoder
+-> erasure -> Application_Layer_Receiver with its Parameter_Estimator pair ->
+Variable_Rate_FEC_Decoder, 6-byte feedback to the sender; application_local_simulation.cpp:328-345)
+symbolically on the host: which (T,B,N) encodes each packet, where double coding starts and
+stops, which decoder instance reports each packet and whether it is lost.  ``encode`` /
+``decode`` then do the byte work of that schedule on the GPU, batched per coder instance.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+
+from ._lib import check, lib
+from .codec import _ptr, _stream_handle
+
+
+class VrPlan:
+    def __init__(self, erasure: np.ndarray, P: int, max_payload: int = 300, T: int = 10, B: int = -1,
+                 N: int = -1, adaptive_mode_MDS: bool = False):
+        pat = np.ascontiguousarray(erasure, dtype=np.uint8)
+        h = ctypes.c_void_p()
+        check(lib().fec_vr_plan_create(max_payload, T, B, N, int(adaptive_mode_MDS),
+                                       pat.ctypes.data_as(ctypes.c_void_p), pat.size, P, ctypes.byref(h)),
+              "fec_vr_plan_create")
+        self._h = h
+        self.L, self.T, self.P = max_payload, T, P
+        lost, sw, sent = ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int64()
+        rate = ctypes.c_double()
+        ne, nd, cwm = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+        check(lib().fec_vr_plan_stats(h, ctypes.byref(lost), ctypes.byref(sw), ctypes.byref(rate),
+                                      ctypes.byref(sent), ctypes.byref(ne), ctypes.byref(nd), ctypes.byref(cwm)),
+              "fec_vr_plan_stats")
+        self.lost, self.switches, self.coding_rate = lost.value, sw.value, rate.value
+        self.sent, self.cw_max = sent.value, cwm.value
+        self.encoders = np.zeros((ne.value, 6), dtype=np.int64)
+        self.decoders = np.zeros((nd.value, 6), dtype=np.int64)
+        check(lib().fec_vr_plan_instances(h, self.encoders.ctypes.data_as(ctypes.c_void_p),
+                                          self.decoders.ctypes.data_as(ctypes.c_void_p)), "fec_vr_plan_instances")
+        self.frames = np.zeros((self.sent, 6), dtype=np.int32)
+        self.erased = np.zeros(self.sent, dtype=np.uint8)
+        self.fate = np.zeros(P, dtype=np.uint8)
+        self.fate_decoder = np.zeros(P, dtype=np.int32)
+        check(lib().fec_vr_plan_packets(h, *(a.ctypes.data_as(ctypes.c_void_p) for a in
+                                             (self.frames, self.erased, self.fate, self.fate_decoder))),
+              "fec_vr_plan_packets")
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h:
+            lib().fec_vr_plan_destroy(h)
+            self._h = None
+
+    def tuples(self) -> set:
+        return {tuple(int(v) for v in r[:3]) for r in self.encoders}
+
+    # -- batched device-resident path -----------------------------------------------------------
+    def encode(self, payload, lengths=None):
+        """payload: [sent, L] uint8 on the GPU -> (cw_cur, len_cur, cw_old, len_old): row s = the
+        codewords frame s carries (stride cw_max, zero padded), trimmed sizes (old: 0 if none)."""
+        import torch
+        assert payload.dtype == torch.uint8 and payload.is_cuda and tuple(payload.shape) == (self.sent, self.L)
+        dev = payload.device
+        cw_cur = torch.zeros((self.sent, self.cw_max), dtype=torch.uint8, device=dev)
+        cw_old = torch.zeros((self.sent, self.cw_max), dtype=torch.uint8, device=dev)
+        len_cur = torch.zeros(self.sent, dtype=torch.int32, device=dev)
+        len_old = torch.zeros(self.sent, dtype=torch.int32, device=dev)
+        check(lib().fec_vr_encode_batch(self._h, _ptr(payload), _ptr(lengths), _ptr(cw_cur), _ptr(len_cur),
+                                        _ptr(cw_old), _ptr(len_old), _stream_handle(torch)), "fec_vr_encode_batch")
+        return cw_cur, len_cur, cw_old, len_old
+
+    def decode(self, cw_cur, cw_old, erased=None):
+        """-> (payload out [P, L], lengths [P], 0 = lost): the receiver's reported outputs."""
+        import torch
+        dev = cw_cur.device
+        if erased is None:
+            erased = torch.from_numpy(self.erased).to(dev)
+        out = torch.zeros((self.P, self.L), dtype=torch.uint8, device=dev)
+        out_len = torch.zeros(self.P, dtype=torch.int32, device=dev)
+        check(lib().fec_vr_decode_batch(self._h, _ptr(cw_cur), _ptr(cw_old), _ptr(erased), _ptr(out), _ptr(out_len),
+                                        _stream_handle(torch)), "fec_vr_decode_batch")
+        return out, out_len

@@ -152,6 +152,44 @@ int fec_decoder_receive(fec_decoder *dec, const uint8_t *codeword, int codeword_
 int fec_plan_host(int max_payload, int T, int B, int N, const uint8_t *erasure, int64_t P,
                   uint8_t *fate);
 
+/* ---- variable-rate (adaptive) coding: BASELINE config 4 --------------------------------------
+ * The reference's P2P loop (application_local_simulation.cpp:328-345): Application_Layer_Sender +
+ * Variable_Rate_FEC_Encoder (src/Variable_Rate_FEC_Encoder.cpp:74-235) with double coding at every
+ * (T,B,N) switch, Application_Layer_Receiver + foreground/background Parameter_Estimator
+ * (src/Parameter_Estimator.cpp:58-190, swapped every 100 packets) + Variable_Rate_FEC_Decoder
+ * (src/Variable_Rate_FEC_Decoder.cpp:2133-2400), the receiver's 6-byte feedback read by the sender at
+ * the next packet.  Everything but the coding bytes depends only on the erasure pattern, so a plan
+ * runs the loop symbolically on the host and records the schedule; the byte work then runs batched
+ * on the device.  T = T_INITIAL, B = N = -1 for adaptive (else fixed (T,B,N)); the pattern is the
+ * receiver's erasure.bin (ERASURE_TYPE 5: packets seq < P+T with pattern byte 1 are dropped); P =
+ * NUMBER_OF_ITERATIONS, the packets whose outputs are counted. */
+typedef struct fec_vr_plan fec_vr_plan;
+int fec_vr_plan_create(int max_payload, int T, int B, int N, int adaptive_mode_MDS,
+                       const uint8_t *erasure, int64_t n_erasure, int64_t P, fec_vr_plan **out);
+int fec_vr_plan_destroy(fec_vr_plan *plan);
+/* lost: packets among 0..P-1 the receiver outputs empty ("Final FEC loss rate" x P); switches:
+ * "Start double coding at the source" count; coding_rate: Variable_Rate_FEC_Encoder's final rate;
+ * sent: packets the sender produced; cw_max: row stride of the codeword arrays below. */
+int fec_vr_plan_stats(const fec_vr_plan *plan, int64_t *lost, int64_t *switches, double *coding_rate,
+                      int64_t *sent, int *n_encoders, int *n_decoders, int *cw_max);
+/* instances, 6 int64 each: T, B, N, first seq, seq from which it is the old one, end seq */
+int fec_vr_plan_instances(const fec_vr_plan *plan, int64_t *encoders, int64_t *decoders);
+/* per sent packet: frames (6 int32: header T, B, N, counter_for_start_and_end, current encoder,
+ * old encoder or -1), erased (1 = dropped); per counted packet x < P: fate (1 received, 2
+ * recovered, 3 lost) and the decoder instance that reported it.  NULL pointers are skipped. */
+int fec_vr_plan_packets(const fec_vr_plan *plan, int32_t *frames, uint8_t *erased, uint8_t *fate,
+                        int32_t *fate_decoder);
+/* Device-resident execution (one fec_encode_batch / fec_decode_batch per instance role).  Encode:
+ * d_payload (sent rows of max_payload bytes) -> row s of d_cw_cur / d_cw_old (stride cw_max, rows
+ * zero beyond each codeword: clear them first) = the codewords frame s carries, trimmed sizes in
+ * d_len_cur / d_len_old.  Decode: those arrays + d_erased (sent bytes) -> d_out (P rows of
+ * max_payload) and d_out_len (P ints, 0 = lost), the receiver's reported outputs. */
+int fec_vr_encode_batch(fec_vr_plan *plan, const uint8_t *d_payload, const int32_t *d_payload_len,
+                        uint8_t *d_cw_cur, int32_t *d_len_cur, uint8_t *d_cw_old, int32_t *d_len_old,
+                        void *hip_stream);
+int fec_vr_decode_batch(fec_vr_plan *plan, const uint8_t *d_cw_cur, const uint8_t *d_cw_old,
+                        const uint8_t *d_erased, uint8_t *d_out, int32_t *d_out_len, void *hip_stream);
+
 /* ---- erasure patterns (inputs of the decode path; host only, no device needed) ---------------
  * Byte-exact restatements of Erasure_File_Generator (src/Erasure_File_Generator.cpp:25-287): out[i]
  * = 1 if packet i is erased.  Same engine (mt19937), same draw order and the same libstdc++
