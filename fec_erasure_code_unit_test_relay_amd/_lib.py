@@ -94,6 +94,8 @@ def lib() -> ctypes.CDLL:
     L.fec_erasure_ge_varying.argtypes = [vp, i32, f32, f32, f32, i32, ip]
     L.fec_erasure_fritchman_varying.argtypes = [vp, i32, f32, f32, f32, i32, i32]
     L.fec_erasure_periodic.argtypes = [vp, i32, i32, i32, i32]
+    L.fec_block_encode_batch.argtypes = [vp, vp, i64, vp, vp]
+    L.fec_block_decode_batch.argtypes = [vp, vp, vp, i64, vp, vp, vp]
     L.fec_vr_plan_create.argtypes = [i32, i32, i32, i32, i32, vp, i64, i64, ctypes.POINTER(vp)]
     L.fec_vr_plan_destroy.argtypes = [vp]
     L.fec_vr_plan_stats.argtypes = [vp, i64p, i64p, ctypes.POINTER(ctypes.c_double), i64p, ip, ip, ip]
@@ -112,7 +114,8 @@ def lib() -> ctypes.CDLL:
                  "fec_erasure_three_sections_iid", "fec_erasure_ge", "fec_erasure_ge_varying",
                  "fec_erasure_fritchman_varying", "fec_erasure_periodic", "fec_vr_plan_create",
                  "fec_vr_plan_destroy", "fec_vr_plan_stats", "fec_vr_plan_instances", "fec_vr_plan_packets",
-                 "fec_vr_encode_batch", "fec_vr_decode_batch"]:
+                 "fec_vr_encode_batch", "fec_vr_decode_batch", "fec_block_encode_batch",
+                 "fec_block_decode_batch"]:
         getattr(L, name).restype = i32
     _lib = L
     return _lib

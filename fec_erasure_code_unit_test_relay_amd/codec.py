@@ -85,6 +85,33 @@ class Codec:
         """Planner replays one episode per distinct loss shape (default) or every episode."""
         check(lib().fec_codec_set_episode_dedup(self._h, int(bool(on))), "fec_codec_set_episode_dedup")
 
+    # -- block mode (relay): many independent code blocks ----------------------------------------
+    def encode_blocks(self, data, out=None):
+        """encodeBlock(t = k-1) per block (src/codingOperations.cpp:131-147): data [nblk, k] uint8 on
+        the GPU -> codewords [nblk, n] = [data, parity]."""
+        import torch
+        assert data.dtype == torch.uint8 and data.is_cuda and data.dim() == 2 and data.shape[1] == self.k
+        data = data.contiguous()
+        if out is None:
+            out = torch.empty((data.shape[0], self.n), dtype=torch.uint8, device=data.device)
+        check(lib().fec_block_encode_batch(self._h, _ptr(data), data.shape[0], _ptr(out), _stream_handle(torch)),
+              "fec_block_encode_batch")
+        return out
+
+    def decode_blocks(self, cw, erasure):
+        """decodeBlock(T = n-1, t = 0) per block (src/codingOperations.cpp:149-232): codewords and
+        erasure flags [nblk, n] uint8 on the GPU -> (codewords with the recovered data symbols
+        written in, updated erasure flags)."""
+        import torch
+        assert cw.dtype == torch.uint8 and cw.is_cuda and cw.dim() == 2 and cw.shape[1] == self.n
+        assert erasure.dtype == torch.uint8 and erasure.shape == cw.shape
+        cw, erasure = cw.contiguous(), erasure.contiguous()
+        out = torch.empty_like(cw)
+        er_out = torch.empty_like(erasure)
+        check(lib().fec_block_decode_batch(self._h, _ptr(cw), _ptr(erasure), cw.shape[0], _ptr(out), _ptr(er_out),
+                                           _stream_handle(torch)), "fec_block_decode_batch")
+        return out, er_out
+
     # -- batched device-resident path -----------------------------------------------------------
     def encode(self, payload, lengths=None, history: int = 0, out=None, out_len=None):
         """Encode rows ``history..`` of ``payload`` ([rows, L] uint8 on the GPU).

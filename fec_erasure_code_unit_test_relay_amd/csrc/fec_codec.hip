@@ -44,6 +44,7 @@ struct fec_codec {
     uint8_t* d_rules_log = nullptr;  // rules with coefficients in log form (specialised planner)
     const void* plan_fast = nullptr;
     uint8_t* d_gf = nullptr;     // exp[512], log[256]
+    uint8_t* d_G = nullptr;      // k x n generator (block mode)
     uint8_t* d_rstate = nullptr; // post-resync block states per phase
     int enc_tp = 0;              // encode tile (packets per workgroup), generic kernel
     int fast_tp = 0;             // encode tile of the specialised kernel (0: not available)
@@ -82,6 +83,7 @@ struct fec_codec {
         if (d_wbase) (void)hipFree(d_wbase);
         if (d_rules_log) (void)hipFree(d_rules_log);
         if (d_gf) (void)hipFree(d_gf);
+        if (d_G) (void)hipFree(d_G);
         if (d_rstate) (void)hipFree(d_rstate);
     }
 
@@ -172,6 +174,8 @@ int codec_init(fec_codec* c, int max_payload, int T, int B, int N) {
     std::memcpy(gf + 512, F.log, 256);
     HIP_TRY(hipMalloc(&c->d_gf, 768));
     HIP_TRY(hipMemcpy(c->d_gf, gf, 768, hipMemcpyHostToDevice));
+    HIP_TRY(hipMalloc(&c->d_G, c->G.size()));
+    HIP_TRY(hipMemcpy(c->d_G, c->G.data(), c->G.size(), hipMemcpyHostToDevice));
     const std::vector<uint8_t> rst = fec::build_resync_states(g, c->rules);
     HIP_TRY(hipMalloc(&c->d_rstate, rst.size()));
     HIP_TRY(hipMemcpy(c->d_rstate, rst.data(), rst.size(), hipMemcpyHostToDevice));
@@ -1063,6 +1067,46 @@ int fec_plan_host(int max_payload, int T, int B, int N, const uint8_t* erasure, 
         }
         return FEC_OK;
     });
+}
+
+// ---- block mode (fec_block.hip) ------------------------------------------------------------
+static int launch_block(fec_codec* c, bool decode, const uint8_t* d_in, const uint8_t* d_er, int64_t nblk,
+                        uint8_t* d_out, uint8_t* d_er_out, void* stream) {
+    if (!c || nblk < 0 || (nblk > 0 && (!d_in || !d_out || (decode && !d_er)))) return FEC_ERR_ARG;
+    if (nblk == 0) return FEC_OK;
+    const Geometry& g = c->g;
+    fec::BlockArgs a;
+    a.in = d_in;
+    a.er = d_er;
+    a.out = d_out;
+    a.er_out = d_er_out;
+    a.nblk = nblk;
+    a.k = g.k;
+    a.n = g.n;
+    a.G = c->d_G;
+    a.gf = c->d_gf;
+    a.rules = c->d_rules;
+    a.wbase_n = c->rules.w_base[g.n];
+    a.ES = c->rules.entry_bytes;
+    const int64_t grid = std::min<int64_t>((nblk + 255) / 256, 4096);
+    const size_t lds = decode ? 768 + 2 * 256 * g.n : 768 + 1024 + 256 * (g.k + g.n);
+    if (decode)
+        hipLaunchKernelGGL(fec::fec_block_decode_kernel, dim3(static_cast<unsigned>(grid)), dim3(256), lds,
+                           static_cast<hipStream_t>(stream), a);
+    else
+        hipLaunchKernelGGL(fec::fec_block_encode_kernel, dim3(static_cast<unsigned>(grid)), dim3(256), lds,
+                           static_cast<hipStream_t>(stream), a);
+    HIP_TRY(hipGetLastError());
+    return FEC_OK;
+}
+
+int fec_block_encode_batch(fec_codec* c, const uint8_t* d_data, int64_t nblk, uint8_t* d_codeword, void* stream) {
+    return launch_block(c, false, d_data, nullptr, nblk, d_codeword, nullptr, stream);
+}
+
+int fec_block_decode_batch(fec_codec* c, const uint8_t* d_codeword, const uint8_t* d_erasure, int64_t nblk,
+                           uint8_t* d_out, uint8_t* d_erasure_out, void* stream) {
+    return launch_block(c, true, d_codeword, d_erasure, nblk, d_out, d_erasure_out, stream);
 }
 
 int fec_util_fill_payload(uint8_t* d_out, int64_t t0, int64_t count, int L, uint64_t seed,

@@ -176,6 +176,23 @@ struct StreamOutArgs {
     int clamp;                  // 1: slow path (payload clamped to L)
 };
 
+// Block mode (fec_block.hip): many independent code blocks of n symbols.
+struct BlockArgs {
+    const uint8_t* in;          // encode: nblk x k data; decode: nblk x n codewords
+    const uint8_t* er;          // decode: nblk x n erasure flags (1 = erased)
+    uint8_t* out;               // nblk x n
+    uint8_t* er_out;            // decode: updated flags (may be null)
+    int64_t nblk;
+    int k, n;
+    const uint8_t* G;           // k x n generator
+    const uint8_t* gf;          // exp[512], log[256]
+    const uint8_t* rules;       // decode rule table
+    int64_t wbase_n;            // byte offset of window n's table
+    int ES;                     // rule entry bytes
+};
+__global__ void fec_block_encode_kernel(BlockArgs a);
+__global__ void fec_block_decode_kernel(BlockArgs a);
+
 __global__ void fec_encode_kernel(EncArgs a);
 __global__ void fec_scan_kernel(const uint8_t* er, int64_t P, int64_t Pout, int T,
                                 int32_t* counters, int32_t* episodes, int32_t* erased);

@@ -152,6 +152,21 @@ int fec_decoder_receive(fec_decoder *dec, const uint8_t *codeword, int codeword_
 int fec_plan_host(int max_payload, int T, int B, int N, const uint8_t *erasure, int64_t P,
                   uint8_t *fate);
 
+/* ---- block mode: many independent code blocks ------------------------------------------------
+ * Batched forms of the reference's free functions as the relay (Decoder_Symbol_Wise,
+ * src/Decoder_Symbol_Wise.cpp:322-328, 532-533, 573-575, 610, 643) calls them per code block:
+ *   encodeBlock(data, G, cw, k, n, t = k-1)  (src/codingOperations.cpp:131-147): d_data nblk x k ->
+ *     d_codeword nblk x n = [data, parity] (the relay pre-fills cw with the data, so the k-1
+ *     systematic bytes encodeBlock leaves alone are the data too);
+ *   decodeBlock(cw, G, cw, erasure, k, n, T = n-1, t = 0)  (src/codingOperations.cpp:149-232):
+ *     d_codeword nblk x n + d_erasure nblk x n (1 = erased) -> d_out nblk x n with every data symbol
+ *     the reference recovers written in, d_erasure_out (may be NULL) with those flags cleared.
+ * G is the codec's generator (init_at_sender for its (T,B,N)). */
+int fec_block_encode_batch(fec_codec *codec, const uint8_t *d_data, int64_t nblk, uint8_t *d_codeword,
+                           void *hip_stream);
+int fec_block_decode_batch(fec_codec *codec, const uint8_t *d_codeword, const uint8_t *d_erasure,
+                           int64_t nblk, uint8_t *d_out, uint8_t *d_erasure_out, void *hip_stream);
+
 /* ---- variable-rate (adaptive) coding: BASELINE config 4 --------------------------------------
  * The reference's P2P loop (application_local_simulation.cpp:328-345): Application_Layer_Sender +
  * Variable_Rate_FEC_Encoder (src/Variable_Rate_FEC_Encoder.cpp:74-235) with double coding at every

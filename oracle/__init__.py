@@ -43,6 +43,7 @@ def lib() -> ctypes.CDLL:
         L.or_gen_G.argtypes = [u8p] + [ctypes.c_int] * 5
         L.or_rref_matrix.argtypes = [u8p, u8p, u8p, ctypes.c_int, ctypes.c_int]
         L.or_decode_block.argtypes = [u8p, u8p, u8p, u8p] + [ctypes.c_int] * 4
+        L.or_encode_block.argtypes = [u8p, u8p, u8p] + [ctypes.c_int] * 3
         L.or_geometry.argtypes = [ctypes.c_int] * 4 + [ip] * 4
         L.or_encoder_new.restype = ctypes.c_void_p
         L.or_encoder_new.argtypes = [ctypes.c_int] * 4
@@ -106,6 +107,26 @@ def rref(mat: np.ndarray):
     act = np.zeros((n, n), dtype=np.uint8)
     lib().or_rref_matrix(_u8(inp), _u8(out), _u8(act), m, n)
     return out, act
+
+
+def encode_block(data: np.ndarray, G: np.ndarray, cw: np.ndarray, t: int) -> np.ndarray:
+    """encodeBlock (codingOperations.cpp:131-147) on one block; cw is updated in place."""
+    k, n = G.shape
+    d = np.ascontiguousarray(data, dtype=np.uint8)
+    g = np.ascontiguousarray(G, dtype=np.uint8)
+    lib().or_encode_block(_u8(d), _u8(g), _u8(cw), k, n, t)
+    return cw
+
+
+def decode_block(cw: np.ndarray, G: np.ndarray, erasure: np.ndarray, T: int, t: int):
+    """decodeBlock (codingOperations.cpp:149-232) in the relay's in-place form
+    decodeBlock(cw, G, cw, erasure, k, n, T, t); returns (cw, erasure) updated."""
+    k, n = G.shape
+    c = np.array(cw, dtype=np.uint8)
+    e = np.array(erasure, dtype=np.uint8)
+    g = np.ascontiguousarray(G, dtype=np.uint8)
+    lib().or_decode_block(_u8(c), _u8(g), _u8(c), _u8(e), k, n, T, t)
+    return c, e
 
 
 def fill_payload(t0: int, count: int, L: int, seed: int) -> np.ndarray:
