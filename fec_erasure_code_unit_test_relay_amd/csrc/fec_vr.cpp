@@ -119,6 +119,10 @@ void VrPlan::run(int max_payload, int T, int B, int N, bool mds, const uint8_t* 
     erased.clear();
     fate.assign(static_cast<size_t>(P), kNone);
     fate_dec.assign(static_cast<size_t>(P), -1);
+    slow.assign(static_cast<size_t>(P), 0);
+    rec_x.clear();
+    rec_dec.clear();
+    rec_coef.clear();
     lost = switches = 0;
     sum_coding_rate = 0;
 
@@ -170,7 +174,16 @@ void VrPlan::run(int max_payload, int T, int B, int N, bool mds, const uint8_t* 
         const PacketFate f = r.fate == kNone ? kLost : r.fate;
         fate[x] = f;
         fate_dec[x] = id;
+        slow[x] = r.slow ? 1 : 0;
         if (f == kLost) ++lost;
+        if (f == kRecovered) {
+            rec_x.push_back(x);
+            rec_dec.push_back(id);
+            const size_t o = rec_coef.size();
+            rec_coef.resize(o + kVrCoefStride, 0);
+            const Geometry& g = sd[id].g;
+            std::memcpy(&rec_coef[o], r.coef, static_cast<size_t>(g.k) * g.n);
+        }
     };
     auto update_decoder = [&](int T_, int B_, int N_, int64_t first) {  // (:2520-2536)
         dold = dcur;
@@ -315,29 +328,139 @@ void VrPlan::run(int max_payload, int T, int B, int N, bool mds, const uint8_t* 
 struct fec_vr_plan {
     fec::VrPlan plan;
     int cw_max = 0;
-    // device execution state (created on first use)
+    // ---- device execution state (created on first use) ----
     std::map<int, fec_codec*> codecs;  // key T*1024 + B*32 + N
-    uint8_t* d_gather = nullptr;
-    size_t gather_bytes = 0;
-    void* d_ws = nullptr;
-    size_t ws_bytes = 0;
+    struct Tuple {                     // encode work of one (T,B,N)
+        int T, B, N, CW;
+        int64_t nrows = 0;             // dense rows: per instance n-1 zero rows + its calls
+        int64_t* d_rows = nullptr;     // dense row -> payload row (-1 = zero packet)
+        int64_t* d_dst = nullptr;      // dense row -> (frame row << 1) | old (-1 = discard)
+    };
+    std::vector<Tuple> tuples;
+    uint8_t* d_pay = nullptr;          // dense payload rows (max over tuples)
+    int32_t* d_len = nullptr;
+    uint8_t* d_cw = nullptr;           // dense codewords
+    int32_t* d_cwlen = nullptr;
+    // decode tables
+    int32_t* d_pk_dec = nullptr;
+    int32_t* d_inst = nullptr;
+    int64_t* d_inst_switch = nullptr;
+    uint8_t* d_fate = nullptr;
+    uint8_t* d_slow = nullptr;
+    int64_t* d_rec_x = nullptr;
+    int32_t* d_rec_dec = nullptr;
+    uint8_t* d_rec_coef = nullptr;
+    uint8_t* d_gf = nullptr;
+    bool enc_ready = false, dec_ready = false;
+
     ~fec_vr_plan() {
         for (auto& kv : codecs) fec_codec_destroy(kv.second);
-        if (d_gather) (void)hipFree(d_gather);
-        if (d_ws) (void)hipFree(d_ws);
+        for (auto& t : tuples) {
+            if (t.d_rows) (void)hipFree(t.d_rows);
+            if (t.d_dst) (void)hipFree(t.d_dst);
+        }
+        for (void* p : {static_cast<void*>(d_pay), static_cast<void*>(d_len), static_cast<void*>(d_cw),
+                        static_cast<void*>(d_cwlen), static_cast<void*>(d_pk_dec), static_cast<void*>(d_inst),
+                        static_cast<void*>(d_inst_switch), static_cast<void*>(d_fate), static_cast<void*>(d_slow),
+                        static_cast<void*>(d_rec_x), static_cast<void*>(d_rec_dec), static_cast<void*>(d_rec_coef),
+                        static_cast<void*>(d_gf)})
+            if (p) (void)hipFree(p);
     }
-    int codec(const fec::VrInstance& v, fec_codec** out) {
-        const int key = v.T * 1024 + v.B * 32 + v.N;
+    int codec(int T, int B, int N, fec_codec** out) {
+        const int key = T * 1024 + B * 32 + N;
         auto it = codecs.find(key);
         if (it == codecs.end()) {
             fec_codec* c = nullptr;
-            if (int st = fec_codec_create(plan.L, v.T, v.B, v.N, &c)) return st;
+            if (int st = fec_codec_create(plan.L, T, B, N, &c)) return st;
             it = codecs.emplace(key, c).first;
         }
         *out = it->second;
         return FEC_OK;
     }
 };
+
+namespace {
+template <typename T>
+int upload(T** d, const std::vector<T>& h) {
+    const size_t bytes = std::max<size_t>(sizeof(T), h.size() * sizeof(T));
+    if (hipMalloc(reinterpret_cast<void**>(d), bytes) != hipSuccess) return FEC_ERR_NOMEM;
+    if (!h.empty() && hipMemcpy(*d, h.data(), h.size() * sizeof(T), hipMemcpyHostToDevice) != hipSuccess)
+        return FEC_ERR_HIP;
+    return FEC_OK;
+}
+
+// Encode tables: instances grouped by (T,B,N); each instance contributes n-1 all-zero rows (its
+// encoder starts with X = 0 history) followed by its calls [first, end), scattered back to the
+// current array for [first, role_switch) and to the old array after.
+int prepare_encode(fec_vr_plan* v) {
+    if (v->enc_ready) return FEC_OK;
+    const auto& p = v->plan;
+    std::map<int, std::pair<std::vector<int64_t>, std::vector<int64_t>>> rows;
+    std::map<int, fec::VrInstance> proto;
+    for (const auto& e : p.enc) {
+        const int key = e.T * 1024 + e.B * 32 + e.N;
+        proto[key] = e;
+        auto& rr = rows[key];
+        const int n = (e.T - e.N + 1) + e.B;
+        for (int z = 0; z < n - 1; ++z) {
+            rr.first.push_back(-1);
+            rr.second.push_back(-1);
+        }
+        for (int64_t sq = e.first; sq < e.end; ++sq) {
+            rr.first.push_back(sq);
+            rr.second.push_back((sq << 1) | (sq >= e.role_switch ? 1 : 0));
+        }
+    }
+    int64_t max_rows = 0, max_cw = 0;
+    for (auto& kv : rows) {
+        const auto& e = proto[kv.first];
+        fec_vr_plan::Tuple t;
+        t.T = e.T;
+        t.B = e.B;
+        t.N = e.N;
+        t.CW = fec::Geometry::make(p.L, e.T, e.B, e.N).CW;
+        t.nrows = static_cast<int64_t>(kv.second.first.size());
+        if (int st = upload(&t.d_rows, kv.second.first)) return st;
+        if (int st = upload(&t.d_dst, kv.second.second)) return st;
+        v->tuples.push_back(t);
+        max_rows = std::max(max_rows, t.nrows);
+        max_cw = std::max<int64_t>(max_cw, t.nrows * t.CW);
+    }
+    if (hipMalloc(reinterpret_cast<void**>(&v->d_pay), std::max<int64_t>(16, max_rows * p.L)) != hipSuccess ||
+        hipMalloc(reinterpret_cast<void**>(&v->d_len), std::max<int64_t>(16, max_rows * 4)) != hipSuccess ||
+        hipMalloc(reinterpret_cast<void**>(&v->d_cw), std::max<int64_t>(16, max_cw)) != hipSuccess ||
+        hipMalloc(reinterpret_cast<void**>(&v->d_cwlen), std::max<int64_t>(16, max_rows * 4)) != hipSuccess)
+        return FEC_ERR_NOMEM;
+    v->enc_ready = true;
+    return FEC_OK;
+}
+
+int prepare_decode(fec_vr_plan* v) {
+    if (v->dec_ready) return FEC_OK;
+    const auto& p = v->plan;
+    std::vector<int32_t> inst;
+    std::vector<int64_t> sw;
+    for (const auto& d : p.dec) {
+        const fec::Geometry g = fec::Geometry::make(p.L, d.T, d.B, d.N);
+        inst.insert(inst.end(), {g.k, g.n, g.CW, 0});
+        sw.push_back(d.role_switch);
+    }
+    if (int st = upload(&v->d_pk_dec, p.fate_dec)) return st;
+    if (int st = upload(&v->d_inst, inst)) return st;
+    if (int st = upload(&v->d_inst_switch, sw)) return st;
+    if (int st = upload(&v->d_fate, p.fate)) return st;
+    if (int st = upload(&v->d_slow, p.slow)) return st;
+    if (int st = upload(&v->d_rec_x, p.rec_x)) return st;
+    if (int st = upload(&v->d_rec_dec, p.rec_dec)) return st;
+    if (int st = upload(&v->d_rec_coef, p.rec_coef)) return st;
+    const fec::Field& F = fec::field();
+    std::vector<uint8_t> gf(F.exp, F.exp + 512);
+    gf.insert(gf.end(), F.log, F.log + 256);
+    if (int st = upload(&v->d_gf, gf)) return st;
+    v->dec_ready = true;
+    return FEC_OK;
+}
+}  // namespace
 
 namespace {
 template <typename F>
@@ -429,126 +552,42 @@ int fec_vr_plan_packets(const fec_vr_plan* v, int32_t* frames, uint8_t* erased, 
 
 // Encode every packet the sender produced: row s of d_cw_cur (stride cw_max) = the codeword of
 // frame s's current encoder, row s of d_cw_old = its old encoder's (double coding; rows of frames
-// without one are left alone), trimmed sizes in d_len_*.  One fec_encode_batch per instance role:
-// an instance created at seq f encodes rows [f, role_switch) as current and [role_switch, end) as
-// old, the second launch with the rows in front of it as history (X_{t'<f} = 0 at row f).
+// without one are left alone), trimmed sizes in d_len_*.  Three launches per (T,B,N) tuple:
+// gather the tuple's instances into dense rows (n-1 zero rows in front of each: X_{t'<first} = 0),
+// the tuple's encode kernel over all of them at once, scatter back into the frames' rows.
 int fec_vr_encode_batch(fec_vr_plan* v, const uint8_t* d_payload, const int32_t* d_payload_len, uint8_t* d_cw_cur,
                         int32_t* d_len_cur, uint8_t* d_cw_old, int32_t* d_len_old, void* hip_stream) {
     if (!v || !d_payload || !d_cw_cur || !d_len_cur || !d_cw_old || !d_len_old) return FEC_ERR_ARG;
-    const auto& p = v->plan;
-    const hipStream_t s = static_cast<hipStream_t>(hip_stream);
-    const int64_t W = v->cw_max;
-    for (const auto& e : p.enc) {
+    if ((v->plan.L & 3) || (reinterpret_cast<uintptr_t>(d_payload) & 3)) return FEC_ERR_ARG;
+    if (int st = vr_guarded([&] { return prepare_encode(v); })) return st;
+    for (const auto& t : v->tuples) {
         fec_codec* c = nullptr;
-        if (int st = v->codec(e, &c)) return st;
-        int CW = 0;
-        fec_codec_geometry(c, nullptr, nullptr, nullptr, &CW);
-        if (CW == W) {
-            // rows go straight to the strided arrays
-            const int64_t n1 = e.role_switch - e.first, n2 = e.end - e.role_switch;
-            if (n1 > 0) {
-                if (int st = fec_encode_batch(c, d_payload + e.first * p.L, d_payload_len ? d_payload_len + e.first : nullptr,
-                                              0, n1, d_cw_cur + e.first * W, d_len_cur + e.first, hip_stream))
-                    return st;
-            }
-            if (n2 > 0) {
-                if (int st = fec_encode_batch(c, d_payload + e.role_switch * p.L,
-                                              d_payload_len ? d_payload_len + e.role_switch : nullptr, n1, n2,
-                                              d_cw_old + e.role_switch * W, d_len_old + e.role_switch, hip_stream))
-                    return st;
-            }
-            continue;
-        }
-        // narrower codewords: encode densely, then scatter into the cw_max-stride rows
-        const int64_t rows = e.end - e.first;
-        const size_t need = static_cast<size_t>(rows) * CW;
-        if (need > v->gather_bytes) {
-            if (v->d_gather) (void)hipFree(v->d_gather);
-            v->d_gather = nullptr;
-            v->gather_bytes = 0;
-            if (hipMalloc(&v->d_gather, need) != hipSuccess) return FEC_ERR_NOMEM;
-            v->gather_bytes = need;
-        }
-        const int64_t n1 = e.role_switch - e.first, n2 = e.end - e.role_switch;
-        if (n1 > 0) {
-            if (int st = fec_encode_batch(c, d_payload + e.first * p.L, d_payload_len ? d_payload_len + e.first : nullptr, 0,
-                                          n1, v->d_gather, d_len_cur + e.first, hip_stream))
-                return st;
-            if (hipMemcpy2DAsync(d_cw_cur + e.first * W, W, v->d_gather, CW, CW, n1, hipMemcpyDeviceToDevice, s) != hipSuccess)
-                return FEC_ERR_HIP;
-        }
-        if (n2 > 0) {
-            if (int st = fec_encode_batch(c, d_payload + e.role_switch * p.L,
-                                          d_payload_len ? d_payload_len + e.role_switch : nullptr, n1, n2,
-                                          v->d_gather + n1 * CW, d_len_old + e.role_switch, hip_stream))
-                return st;
-            if (hipMemcpy2DAsync(d_cw_old + e.role_switch * W, W, v->d_gather + n1 * CW, CW, CW, n2,
-                                 hipMemcpyDeviceToDevice, s) != hipSuccess)
-                return FEC_ERR_HIP;
-        }
+        if (int st = v->codec(t.T, t.B, t.N, &c)) return st;
+        fec::VrGatherArgs g{d_payload, d_payload_len, t.d_rows, t.nrows, v->plan.L, v->d_pay, v->d_len};
+        if (int st = fec::vr_launch_gather(g, hip_stream)) return st;
+        if (int st = fec_encode_batch(c, v->d_pay, v->d_len, 0, t.nrows, v->d_cw, v->d_cwlen, hip_stream)) return st;
+        fec::VrScatterArgs sc{v->d_cw, v->d_cwlen, t.d_dst, t.nrows, t.CW, v->cw_max, d_cw_cur, d_cw_old,
+                              d_len_cur, d_len_old};
+        if (int st = fec::vr_launch_scatter(sc, hip_stream)) return st;
     }
     return FEC_OK;
 }
 
-// Decode the schedule: decoder instance j is fed, at seq s in [first, end), the codeword the frame
-// carries for its role (current part while s < role_switch, old part after), zero padded to its
-// CW (the frame's wire parts are trimmed codewords; rows beyond an encoder's CW are zero), and
-// erasure flag erased[s].  It reports packets [first, role_switch) (the reference reports through
-// the old decoder during double coding): fec_decode_batch writes its outputs straight into rows
-// first.. of d_out, instances in increasing order, so each later instance overwrites the rows past
-// its predecessor's range.  d_cw_* rows must be zero beyond each encoder's CW.
+// Decode the schedule from the frames' arrays: every packet x < P was reported by one decoder
+// instance j (fate_decoder); a received one is the systematic part of cur[x] in j's geometry, a
+// recovered one the host plan's coefficient rows over j's inputs (cur rows before j became the
+// old decoder, old rows after).  Two launches.  d_erased is not read (the plan holds the pattern).
 int fec_vr_decode_batch(fec_vr_plan* v, const uint8_t* d_cw_cur, const uint8_t* d_cw_old, const uint8_t* d_erased,
                         uint8_t* d_out, int32_t* d_out_len, void* hip_stream) {
-    if (!v || !d_cw_cur || !d_cw_old || !d_erased || !d_out || !d_out_len) return FEC_ERR_ARG;
+    (void)d_erased;
+    if (!v || !d_cw_cur || !d_cw_old || !d_out || !d_out_len) return FEC_ERR_ARG;
+    if (int st = vr_guarded([&] { return prepare_decode(v); })) return st;
     const auto& p = v->plan;
-    const hipStream_t s = static_cast<hipStream_t>(hip_stream);
-    const int64_t W = v->cw_max;
-    for (size_t j = 0; j < p.dec.size(); ++j) {
-        const auto& d = p.dec[j];
-        fec_codec* c = nullptr;
-        if (int st = v->codec(d, &c)) return st;
-        int CW = 0;
-        fec_codec_geometry(c, nullptr, nullptr, nullptr, &CW);
-        const int64_t rows = d.end - d.first;
-        if (rows <= d.T) continue;  // outputs only for packets before its first call
-        const size_t need = static_cast<size_t>(rows) * CW;
-        if (need > v->gather_bytes) {
-            if (v->d_gather) (void)hipFree(v->d_gather);
-            v->d_gather = nullptr;
-            v->gather_bytes = 0;
-            if (hipMalloc(&v->d_gather, need) != hipSuccess) return FEC_ERR_NOMEM;
-            v->gather_bytes = need;
-        }
-        const int64_t n1 = d.role_switch - d.first, n2 = d.end - d.role_switch;
-        if (n1 > 0 && hipMemcpy2DAsync(v->d_gather, CW, d_cw_cur + d.first * W, W, CW, n1, hipMemcpyDeviceToDevice, s) !=
-                          hipSuccess)
-            return FEC_ERR_HIP;
-        if (n2 > 0 && hipMemcpy2DAsync(v->d_gather + n1 * CW, CW, d_cw_old + d.role_switch * W, W, CW, n2,
-                                       hipMemcpyDeviceToDevice, s) != hipSuccess)
-            return FEC_ERR_HIP;
-        const size_t ws = fec_decode_workspace_bytes(c, rows);
-        if (ws > v->ws_bytes) {
-            if (v->d_ws) (void)hipFree(v->d_ws);
-            v->d_ws = nullptr;
-            v->ws_bytes = 0;
-            if (hipMalloc(&v->d_ws, ws) != hipSuccess) return FEC_ERR_NOMEM;
-            v->ws_bytes = ws;
-        }
-        // rows past P are not part of the output
-        const int64_t out_rows = std::min<int64_t>(rows - d.T, p.P - d.first);
-        if (out_rows <= 0) continue;
-        if (out_rows == rows - d.T) {
-            if (int st = fec_decode_batch(c, v->d_gather, d_erased + d.first, rows, d_out + d.first * p.L,
-                                          d_out_len + d.first, v->d_ws, v->ws_bytes, hip_stream))
-                return st;
-        } else {  // the last instance: decode fewer calls so that no row past P is written
-            const int64_t r2 = out_rows + d.T;
-            if (int st = fec_decode_batch(c, v->d_gather, d_erased + d.first, r2, d_out + d.first * p.L,
-                                          d_out_len + d.first, v->d_ws, v->ws_bytes, hip_stream))
-                return st;
-        }
-    }
-    return FEC_OK;
+    fec::VrCopyArgs ca{d_cw_cur, v->cw_max, v->d_pk_dec, v->d_inst, v->d_fate, v->d_slow, p.P, p.L, d_out, d_out_len};
+    if (int st = fec::vr_launch_copy(ca, hip_stream)) return st;
+    fec::VrRecArgs ra{d_cw_cur, d_cw_old, v->cw_max, p.sent, v->d_rec_x, v->d_rec_dec, v->d_rec_coef,
+                      static_cast<int>(p.rec_x.size()), v->d_inst, v->d_inst_switch, v->d_gf, p.L, d_out, d_out_len};
+    return fec::vr_launch_recover(ra, hip_stream);
 }
 
 }  // extern "C"

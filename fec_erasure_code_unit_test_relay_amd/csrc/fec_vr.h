@@ -37,6 +37,8 @@ struct ParameterEstimator {
     void make_MDS_estimates();
 };
 
+constexpr int kVrCoefStride = kMaxK * kMaxRuleN;
+
 struct VrInstance {
     int T = 0, B = 0, N = 0;
     int64_t first = 0;   // seq of its first call
@@ -59,6 +61,11 @@ struct VrPlan {
     std::vector<VrInstance> enc, dec;
     std::vector<uint8_t> fate;        // [P]: PacketFate of the output reported for packet x
     std::vector<int32_t> fate_dec;    // [P]: decoder instance that reported it
+    std::vector<uint8_t> slow;        // [P]: reported by the block decoders (length clamped)
+    // recovered packets: x, reporting decoder, its k x n coefficient rows (stride kVrCoefStride)
+    std::vector<int64_t> rec_x;
+    std::vector<int32_t> rec_dec;
+    std::vector<uint8_t> rec_coef;
     int64_t lost = 0, switches = 0;   // "Start double coding at the source" count
     float sum_coding_rate = 0;        // Variable_Rate_FEC_Encoder final_sum_coding_rate
     double coding_rate() const { return sent ? sum_coding_rate / static_cast<float>(sent) : 0.0; }
@@ -72,5 +79,60 @@ private:
     std::map<int, std::unique_ptr<DecodeRules>> rules_;  // key T*1024 + B*32 + N
     const DecodeRules& rules_for(int T, int B, int N);
 };
+
+// Device side of the schedule (fec_vr_kernels.hip).  All launches go to `s`.
+struct VrGatherArgs {   // dense encode input: row r = payload row rows[r] (-1: all-zero packet)
+    const uint8_t* payload;
+    const int32_t* len;   // may be null (all L)
+    const int64_t* rows;
+    int64_t nrows;
+    int L;
+    uint8_t* out;         // nrows x L
+    int32_t* out_len;     // nrows
+};
+struct VrScatterArgs {  // dense codewords -> the frames' arrays: dst[r] = (row << 1) | old, -1 skip
+    const uint8_t* cw;
+    const int32_t* cw_len;
+    const int64_t* dst;
+    int64_t nrows;
+    int CW;
+    int64_t W;
+    uint8_t* cur;
+    uint8_t* old;
+    int32_t* len_cur;
+    int32_t* len_old;
+};
+struct VrCopyArgs {     // received packets: systematic bytes of cur[x] in its decoder's geometry
+    const uint8_t* cur;
+    int64_t W;
+    const int32_t* pk_dec;   // [P] reporting decoder
+    const int32_t* inst;     // [ndec][4]: k, n, CW, 0
+    const uint8_t* fate;     // [P]
+    const uint8_t* slow;     // [P]
+    int64_t P;
+    int L;
+    uint8_t* out;
+    int32_t* out_len;
+};
+struct VrRecArgs {      // recovered packets: coefficient rows over the reporting decoder's inputs
+    const uint8_t* cur;
+    const uint8_t* old;
+    int64_t W;
+    int64_t rows;            // sent packets (valid rows of cur / old)
+    const int64_t* rec_x;
+    const int32_t* rec_dec;
+    const uint8_t* rec_coef; // stride kVrCoefStride
+    int nrec;
+    const int32_t* inst;
+    const int64_t* inst_switch;  // [ndec]: rows >= it come from `old`
+    const uint8_t* gf;
+    int L;
+    uint8_t* out;
+    int32_t* out_len;
+};
+int vr_launch_gather(const VrGatherArgs& a, void* s);
+int vr_launch_scatter(const VrScatterArgs& a, void* s);
+int vr_launch_copy(const VrCopyArgs& a, void* s);
+int vr_launch_recover(const VrRecArgs& a, void* s);
 
 }  // namespace fec

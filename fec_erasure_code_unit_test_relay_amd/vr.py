@@ -57,28 +57,39 @@ class VrPlan:
         return {tuple(int(v) for v in r[:3]) for r in self.encoders}
 
     # -- batched device-resident path -----------------------------------------------------------
-    def encode(self, payload, lengths=None):
+    def alloc_frames(self, device="cuda", zero=True):
+        """(cw_cur, len_cur, cw_old, len_old) buffers for encode().  Zeroed by default (rows read
+        beyond an encoder's CW only when a decoder's (T,B,N) differs from the frame's); the
+        decoders of this plan read each row within its own codeword, so `zero=False` is enough to
+        reproduce the receiver here."""
+        import torch
+        mk = torch.zeros if zero else torch.empty
+        return (mk((self.sent, self.cw_max), dtype=torch.uint8, device=device),
+                torch.zeros(self.sent, dtype=torch.int32, device=device),
+                mk((self.sent, self.cw_max), dtype=torch.uint8, device=device),
+                torch.zeros(self.sent, dtype=torch.int32, device=device))
+
+    def encode(self, payload, lengths=None, frames=None):
         """payload: [sent, L] uint8 on the GPU -> (cw_cur, len_cur, cw_old, len_old): row s = the
-        codewords frame s carries (stride cw_max, zero padded), trimmed sizes (old: 0 if none)."""
+        codewords frame s carries (stride cw_max), trimmed sizes (old: 0 if none)."""
         import torch
         assert payload.dtype == torch.uint8 and payload.is_cuda and tuple(payload.shape) == (self.sent, self.L)
-        dev = payload.device
-        cw_cur = torch.zeros((self.sent, self.cw_max), dtype=torch.uint8, device=dev)
-        cw_old = torch.zeros((self.sent, self.cw_max), dtype=torch.uint8, device=dev)
-        len_cur = torch.zeros(self.sent, dtype=torch.int32, device=dev)
-        len_old = torch.zeros(self.sent, dtype=torch.int32, device=dev)
+        cw_cur, len_cur, cw_old, len_old = frames if frames is not None else self.alloc_frames(payload.device)
         check(lib().fec_vr_encode_batch(self._h, _ptr(payload), _ptr(lengths), _ptr(cw_cur), _ptr(len_cur),
                                         _ptr(cw_old), _ptr(len_old), _stream_handle(torch)), "fec_vr_encode_batch")
         return cw_cur, len_cur, cw_old, len_old
 
-    def decode(self, cw_cur, cw_old, erased=None):
-        """-> (payload out [P, L], lengths [P], 0 = lost): the receiver's reported outputs."""
+    def decode(self, cw_cur, cw_old, erased=None, out=None, out_len=None):
+        """-> (payload out [P, L], lengths [P], 0 = lost): the receiver's reported outputs (every
+        row is written)."""
         import torch
         dev = cw_cur.device
         if erased is None:
             erased = torch.from_numpy(self.erased).to(dev)
-        out = torch.zeros((self.P, self.L), dtype=torch.uint8, device=dev)
-        out_len = torch.zeros(self.P, dtype=torch.int32, device=dev)
+        if out is None:
+            out = torch.empty((self.P, self.L), dtype=torch.uint8, device=dev)
+        if out_len is None:
+            out_len = torch.empty(self.P, dtype=torch.int32, device=dev)
         check(lib().fec_vr_decode_batch(self._h, _ptr(cw_cur), _ptr(cw_old), _ptr(erased), _ptr(out), _ptr(out_len),
                                         _stream_handle(torch)), "fec_vr_decode_batch")
         return out, out_len

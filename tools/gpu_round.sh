@@ -11,5 +11,8 @@ tail -3 $OUT/pytest_gpu.log
 timeout -k 10 300 python -u bench.py > $OUT/bench.json 2> $OUT/bench.err || { echo "bench failed"; tail -30 $OUT/bench.err; exit 1; }
 cat $OUT/bench.json
 cd /tmp && export TMPDIR=/tmp
-timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o bench -- python3 $R/bench.py --no-cpu-baseline --no-host-inclusive > $OUT/bench_prof.json 2> $OUT/bench_prof.err || { echo "rocprof failed"; tail -30 $OUT/bench_prof.err; exit 1; }
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o bench -- python3 $R/bench.py --no-cpu-baseline --no-host-inclusive --no-extra-configs > $OUT/bench_prof.json 2> $OUT/bench_prof.err || { echo "rocprof failed"; tail -30 $OUT/bench_prof.err; exit 1; }
 find $OUT/prof -name "*stats*"
+# HBM traffic of the step's kernels (FETCH_SIZE / WRITE_SIZE passes) -> profiles-ready JSON
+bash $R/tools/pmc_traffic.sh $TAG > /dev/null 2>&1 || { echo "pmc passes failed"; exit 1; }
+python3 $R/tools/pmc_traffic.py $OUT/traffic.json $TAG $OUT/pmc/p1 $OUT/pmc/p2
