@@ -169,20 +169,13 @@ def main():
     ol = torch.empty(P, dtype=torch.int32, device="cuda")
     codec.workspace(Pf)
 
-    side = torch.cuda.Stream()
-
     def step():
-        # the decode plan needs only the erasure pattern: it runs on a side stream while the
-        # encoder and the received-packet copy run on the main stream; joined before recovery
-        fork = torch.cuda.Event()
-        fork.record()
-        with torch.cuda.stream(side):
-            side.wait_event(fork)
-            codec.plan(er)
+        # encode the batch, then decode it (fec_decode_batch: the erasure-only plan runs on the
+        # codec's side stream beside the received-packet copy, joined before the recovery pass).
+        # The plan is not started beside the encoder: the encoder leaves wave slots free on
+        # purpose (fec_codec.hip, launch_encode_wave), and planner kernels there cost it ~45 us.
         codec.encode(payload, out=cw, out_len=wl)
-        codec.copy(cw, er, out=out, out_len=ol)  # received packets
-        torch.cuda.current_stream().wait_stream(side)
-        codec.recover(cw, out, ol)  # erased packets
+        codec.decode(cw, er, out=out, out_len=ol)
 
     def barrier():
         if world > 1:

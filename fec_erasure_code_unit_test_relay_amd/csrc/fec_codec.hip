@@ -57,6 +57,8 @@ struct fec_codec {
     int wave_slots = 0;                 // resident waves of it on the device
     int wave_ring = 0;                  // bytes of its per-sequence LDS output ring
     int wave_lds = 0;                   // its dynamic LDS per workgroup
+    int wave_pad = 0;                   // 1: per-sequence ring padding (LDS bank spread)
+    int wave_cus = 0;                   // compute units of the device
     const void* copy_fast = nullptr;  // specialised decode copy kernel
     int copyf_tp = 0;
     int copy_path = 0;           // 0 auto, 1 generic, 2 specialised
@@ -234,18 +236,28 @@ int codec_init(fec_codec* c, int max_payload, int T, int B, int N) {
     if (c->wave_kernel) {
         const int ns4 = c->ns4();
         c->wave_ring = 64;
-        while (c->wave_ring < 2 * g.CW + 4 * g.n + 32) c->wave_ring <<= 1;
+        while (c->wave_ring < 2 * g.CW + 4 * g.n + 80) c->wave_ring <<= 1;
         c->wave_lds = 4 * (64 / ns4 + 1) * c->wave_ring;
         if (c->wave_lds > 128 * 1024) c->wave_kernel = nullptr;
     }
-    if (c->wave_kernel)
-        HIP_TRY(hipFuncSetAttribute(c->wave_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, c->wave_lds));
     if (c->wave_kernel) {
-        int dev = 0, cus = 0, per_cu = 0;
+        // per-sequence ring padding (up to 64 dwords) that puts the sequences of a wave on
+        // disjoint LDS banks for the codeword writes; used when it costs no occupancy
+        const int ns4 = c->ns4();
+        const int lds_pad = 4 * (64 / ns4 + 1) * (c->wave_ring + 256);
+        HIP_TRY(hipFuncSetAttribute(c->wave_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                    std::min(lds_pad, 160 * 1024)));
+        int dev = 0, cus = 0, per_cu = 0, per_cu_pad = 0;
         HIP_TRY(hipGetDevice(&dev));
         HIP_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
         HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, c->wave_kernel, 256, c->wave_lds));
+        if (lds_pad <= 160 * 1024)
+            HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu_pad, c->wave_kernel, 256, lds_pad));
+        c->wave_pad = (per_cu_pad >= per_cu && (g.n & 1)) ? 1 : 0;
+        if (const char* v = std::getenv("FEC_WAVE_PAD")) c->wave_pad = std::atoi(v) && per_cu_pad >= per_cu;
+        if (c->wave_pad) c->wave_lds = lds_pad;
         c->wave_slots = cus * per_cu * 4;
+        c->wave_cus = cus;
         if (c->wave_slots <= 0) c->wave_kernel = nullptr;
     }
     if ((g.L & 3) == 0) c->copy_fast = fec::fec_copy_fast_kernel_for(g.k, g.n - g.k);
@@ -408,16 +420,47 @@ int launch_encode_wave(fec_codec* c, const uint8_t* d_payload, const int32_t* d_
     a.NS4 = c->ns4();
     a.SPW = 64 / a.NS4;
     a.rem = g.S - 4 * (a.NS4 - 1);
-    // sequence length: enough sequences for every resident wave slot, a multiple of 4 packets
-    const int64_t slots = static_cast<int64_t>(c->wave_slots) * a.SPW;
-    int64_t M = (P + slots - 1) / slots;
-    if (const char* v = std::getenv("FEC_WAVE_M")) M = std::max<int64_t>(M, std::atoll(v));
-    M = std::max<int64_t>(4, (M + 3) & ~int64_t(3));
+    // Sequence length M (M*CW % 4 == 0 so that every sequence starts dword aligned).  All
+    // workgroups are resident at once, so the kernel takes as long as its busiest CU: pick the
+    // workgroups per CU w (1..resident) that minimises (M_w + n-1) * load / f(load), load = the
+    // most workgroups any CU gets and f the relative throughput of a CU running that many
+    // (measured on MI355X at (10,3,3): 0.6, 0.9, 1.0, 1.02 for 1..4).  M_w + n-1 is one
+    // sequence's walk (warm-up included).  Landing just above a multiple of the CU count is what
+    // this avoids: at M = 54, 772 workgroups put 4 on four CUs and took 234 us against 195 at M = 56.
+    const int64_t unit = (g.CW & 3) == 0 ? 1 : ((g.CW & 1) == 0 ? 2 : 4);
+    const int cus = std::max(1, c->wave_cus);
+    const int per_cu = std::max(1, c->wave_slots / (4 * cus));
+    auto m_for = [&](int64_t seq_slots) {
+        int64_t m = (P + seq_slots - 1) / seq_slots;
+        return std::max<int64_t>(4, (m + unit - 1) / unit * unit);
+    };
+    auto load_of = [&](int64_t m) {
+        const int64_t wgs = ((P + m - 1) / m + 4 * a.SPW - 1) / (4 * a.SPW);
+        return (wgs + cus - 1) / cus;
+    };
+    static const double f_rel[] = {0.0, 0.6, 0.9, 1.0, 1.02, 1.03, 1.04, 1.05, 1.05};
+    int64_t M = 0;
+    double best = 1e300;
+    for (int w = 1; w <= std::min(per_cu, 8); ++w) {
+        const int64_t m = m_for(static_cast<int64_t>(cus) * w * 4 * a.SPW);
+        const int64_t ld = std::min<int64_t>(load_of(m), 8);
+        const double cost = double(m + g.n - 1) * double(ld) / f_rel[ld];
+        if (cost < best) {
+            best = cost;
+            M = m;
+        }
+    }
+    if (const char* v = std::getenv("FEC_WAVE_SHARE")) {  // experiments: size for a share of the slots
+        const int share = std::atoi(v);
+        if (share > 0) M = m_for(std::max<int64_t>(4, int64_t(c->wave_slots) * share / 100) * a.SPW);
+    }
+    if (const char* v = std::getenv("FEC_WAVE_M")) M = std::max<int64_t>(4, (std::atoll(v) + unit - 1) / unit * unit);
     a.M = static_cast<int>(M);
     a.nseq = static_cast<int>((P + M - 1) / M);
     a.dbg = 0;
     if (const char* v = std::getenv("FEC_WAVE_DBG")) a.dbg = std::atoi(v);
     a.ring_bytes = c->wave_ring;
+    a.ring_pad = c->wave_pad;
     const int64_t waves = (a.nseq + a.SPW - 1) / a.SPW;
     const int64_t blocks = (waves + 3) / 4;
     hipEvent_t stop;
@@ -543,16 +586,20 @@ int launch_plan(fec_codec* c, const uint8_t* d_er, int64_t P, void* d_ws, size_t
     pa.rs_bytes = fec::resync_state_bytes(g);
     pa.sym_ok = w.sym_ok;
     pa.coef = w.coef;
+    // The work lists live on the device.  Measured in the full step (encode + decode): grids of
+    // 8192 / 1024 / 256 / 64 workgroups give 0.388 / 0.397 / 0.437 / 0.609 ms.
+    int pgrid = 8192;
+    if (const char* v = std::getenv("FEC_PLAN_GRID")) pgrid = std::max(1, std::atoi(v));
     if (fast_ok && c->plan_path != 1) {
         pa.rules = c->d_rules_log;
         void* args[] = {&pa};
-        HIP_TRY(hipLaunchKernel(c->plan_fast, dim3(8192), dim3(64), args, 0, s));
+        HIP_TRY(hipLaunchKernel(c->plan_fast, dim3(pgrid), dim3(64), args, 0, s));
     } else {
         const int plan_lds = 768 + g.n * g.n + 2 * g.k * g.n;
-        hipLaunchKernelGGL(fec::fec_plan_kernel, dim3(8192), dim3(64), plan_lds, s, pa);
+        hipLaunchKernelGGL(fec::fec_plan_kernel, dim3(pgrid), dim3(64), plan_lds, s, pa);
     }
     HIP_TRY(hipGetLastError());
-    hipLaunchKernelGGL(fec::fec_shape_fill_kernel, dim3(4096), dim3(64), 0, s, sa);
+    hipLaunchKernelGGL(fec::fec_shape_fill_kernel, dim3(pgrid), dim3(64), 0, s, sa);
     HIP_TRY(hipGetLastError());
     // packets with all k symbols recovered -> rec_list (timed with the plan)
     hipLaunchKernelGGL(fec::fec_compact_kernel, dim3(256), dim3(256), 0, s, w.counters, w.erased,

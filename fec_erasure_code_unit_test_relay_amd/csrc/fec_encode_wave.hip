@@ -305,7 +305,18 @@ __global__ __launch_bounds__(kWaveThreads, 4) void fec_encode_wave_kernel(EncWav
     // 16-byte aligned chunks; the chunks shared with the neighbouring sequences go out as dwords.
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const int rmask = a.ring_bytes - 1;
-    uint8_t* ring = smem + ((threadIdx.x >> 6) * (SPW + 1) + (sq < SPW ? sq : SPW)) * a.ring_bytes;
+    // Ring of sequence j of this wave.  Lane g of sequence j writes dword q of its group at bank
+    // (A_j/4 + n*g + q) mod 64, and A_j - A_0 = j*M*CW.  With padding, sequence j is shifted so that
+    // its lanes continue sequence j-1's bank run: lane (j, g) lands where lane NS4*j + g of one long
+    // sequence would, and for odd n the 64 lanes then hit 64 different banks.
+    const int wbase = (threadIdx.x >> 6) * (SPW + 1);  // first ring of this wave
+    const int ring_stride = a.ring_bytes + (a.ring_pad ? 256 : 0);
+    const int mcw64 = (((M & 255) * (CW & 255)) & 255) >> 2;  // (M*CW/4) mod 64 (M*CW % 4 == 0)
+    auto ring_of = [&](int j) __attribute__((always_inline)) {
+        const int pad = a.ring_pad ? ((NS4 * n * j - j * mcw64) & 63) : 0;
+        return smem + (wbase + j) * ring_stride + pad * 4;
+    };
+    uint8_t* ring = ring_of(sq < SPW ? sq : SPW);
     const int A0 = r0 * CW;                                    // sequence start (4-byte aligned)
     int fl = A0;                                               // next byte to flush
 
@@ -363,9 +374,11 @@ __global__ __launch_bounds__(kWaveThreads, 4) void fec_encode_wave_kernel(EncWav
     // The rows' last partial dwords are final only once the next row has been assembled.
     // dprev: rows since the previous flush (2 after a packet pair, 1 after a single packet).
     const int nseq_w = min(SPW, a.nseq - seq0);  // sequences of this wave (uniform)
-    const int wbase = (threadIdx.x >> 6) * (SPW + 1);  // first ring of this wave
     const int r0_last = (seq0 + nseq_w - 1) * M;
-    const bool fast_fit = 2 * CW + 16 <= 16 * 64;   // a pair's chunks fit one store per sequence
+    const bool fast_fit = 2 * CW + 64 <= 16 * 64;   // a pair's chunks fit one store per sequence
+    // Flush boundaries: 64-byte aligned (a line is written by one flush, not split across two
+    // whose halves would reach HBM separately), except at the sequence's end.
+    const int fmask = (a.dbg & 8) ? ~15 : ~63;
     auto flush_slow = [&](int srow) __attribute__((always_inline)) {
         for (int j = 0; j < nseq_w; ++j) {
             const int r0j = (seq0 + j) * M;
@@ -373,7 +386,7 @@ __global__ __launch_bounds__(kWaveThreads, 4) void fec_encode_wave_kernel(EncWav
             const int hi = min(((r0j + srow) * CW) & ~3, Aendj);
             int flj = __builtin_amdgcn_readlane(fl, j * NS4);
             if (hi <= flj) continue;
-            const uint8_t* rj = smem + (wbase + j) * a.ring_bytes;
+            const uint8_t* rj = ring_of(j);
             if (flj & 15) {  // sequence start inside a chunk: its dwords up to the chunk boundary
                 const int e = min((flj + 15) & ~15, hi & ~3);
                 const int x = flj + 4 * lane;
@@ -381,7 +394,7 @@ __global__ __launch_bounds__(kWaveThreads, 4) void fec_encode_wave_kernel(EncWav
                     __builtin_amdgcn_raw_buffer_store_b32(*reinterpret_cast<const uint32_t*>(rj + (x & rmask)), rc, x, 0, 0);
                 flj = e;
             }
-            const int cend = hi & ~15;
+            const int cend = hi == Aendj ? (hi & ~15) : (hi & fmask);
             for (int c = flj + 16 * lane; c < cend; c += 16 * 64) {
                 const v4u32 v = *reinterpret_cast<const v4u32*>(rj + (c & rmask));
                 __builtin_amdgcn_raw_buffer_store_b128(v, rc, c, 0, 0);
@@ -419,18 +432,18 @@ __global__ __launch_bounds__(kWaveThreads, 4) void fec_encode_wave_kernel(EncWav
             for (int u = 0; u < 4; ++u) {
                 const int j = j0 + u;
                 const int r0j = (seq0 + j) * M;
-                const int lo = ((r0j + srow - dprev) * CW) & ~15;
-                const int hi = ((r0j + srow) * CW) & ~15;
+                const int lo = ((r0j + srow - dprev) * CW) & fmask;
+                const int hi = ((r0j + srow) * CW) & fmask;
                 c[u] = lo + 16 * lane;
                 ok[u] = j < nseq_w && c[u] < hi;
-                const uint8_t* rj = smem + (wbase + j) * a.ring_bytes;
+                const uint8_t* rj = ring_of(j);
                 v[u] = ok[u] ? *reinterpret_cast<const v4u32*>(rj + (c[u] & rmask)) : v4u32{0, 0, 0, 0};
             }
 #pragma unroll
             for (int u = 0; u < 4; ++u)
                 if (ok[u]) __builtin_amdgcn_raw_buffer_store_b128(v[u], rc, c[u], 0, 0);
         }
-        fl = ((r0 + srow) * CW) & ~15;
+        fl = ((r0 + srow) * CW) & fmask;
     };
 
     // One block = W packets: the accumulator ring comes round once, every slot index below is a

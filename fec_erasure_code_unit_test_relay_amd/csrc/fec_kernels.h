@@ -73,8 +73,11 @@ struct EncWaveArgs {
     int L, S, CW, NS4, SPW, M;
     int rem;                      // sub-streams in the last group (1..4)
     int nseq;                     // ceil(P / M)
-    int ring_bytes;               // per-sequence LDS output ring (power of two >= 2*CW + 4n + 32)
-    int dbg;                      // timing experiments only (FEC_WAVE_DBG): 1 no stores, 2 no parity
+    int ring_bytes;               // per-sequence LDS output ring (power of two >= 2*CW + 4n + 80)
+    int ring_pad;                 // 1: rings ring_bytes + 256 apart, sequence j shifted so that the
+                                  //    wave's codeword writes fall on disjoint banks (odd n)
+    int dbg;                      // timing experiments only (FEC_WAVE_DBG): 1 no stores, 2 no parity,
+                                  // 8 16-byte flush boundaries
 };
 
 // fec_encode_wave_kernel<k, n-k> (fec_encode_wave.hip), else nullptr.  256 threads.

@@ -31,10 +31,8 @@ cw = torch.empty((Pf, codec.CW), dtype=torch.uint8, device="cuda")
 wl = torch.empty(Pf, dtype=torch.int32, device="cuda")
 out = torch.empty((P, L), dtype=torch.uint8, device="cuda")
 ol = torch.empty(P, dtype=torch.int32, device="cuda")
-for _ in range(args.iters):
-    codec.plan(er)
+for _ in range(args.iters):  # bench.py's step
     codec.encode(payload, out=cw, out_len=wl)
-    codec.copy(cw, er, out=out, out_len=ol)
-    codec.recover(cw, out, ol)
+    codec.decode(cw, er, out=out, out_len=ol)
 torch.cuda.synchronize()
 print("ok", codec.counters(), codec.info())
