@@ -248,7 +248,8 @@ def main():
                          "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None},
         }
-        symbol = codec.info()["encode_kernel"] if dominant == "fec_encode_kernel" else None
+        info = codec.info()
+        symbol = info["encode_kernel"] if dominant == "fec_encode_kernel" else info.get("copy_kernel")
         tr = pmc_traffic(symbol) if symbol and P == 1_000_000 else None
         if tr:
             result["roofline"].update(traffic=tr[0], traffic_unit="bytes per launch",

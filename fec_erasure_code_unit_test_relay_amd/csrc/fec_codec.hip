@@ -885,13 +885,20 @@ int fec_codec_info(const fec_codec* c, char* buf, size_t size) {
         std::snprintf(enc, sizeof(enc), "fec_encode_fast_kernel<%d, %d>", c->g.k, np);
     else
         std::snprintf(enc, sizeof(enc), "fec_encode_kernel");
+    char cpy[64];
+    if (c->copy_fast && c->copy_path != 1)
+        std::snprintf(cpy, sizeof(cpy), "fec_copy_fast_kernel<%d, %d>", c->g.k, np);
+    else
+        std::snprintf(cpy, sizeof(cpy), "fec_copy_kernel");
     std::snprintf(buf, size,
                   "{\"k\": %d, \"n\": %d, \"S\": %d, \"CW\": %d, \"encode_kernel\": \"%s\", "
-                  "\"encode_tile\": %d, "
+                  "\"copy_kernel\": \"%s\", \"encode_tile\": %d, "
                   "\"encode_stream_tile\": %d, \"encode_stream_workgroups\": %d, "
-                  "\"encode_stream_lds\": %d, \"copy_tile\": %d, \"plan_specialised\": %d}",
-                  c->g.k, c->g.n, c->g.S, c->g.CW, enc, c->fast_tp, c->persist_tp, c->persist_wgs,
-                  c->persist_tp ? c->pers_lds(c->persist_tp) : 0, c->copyf_tp, c->plan_fast ? 1 : 0);
+                  "\"encode_stream_lds\": %d, \"copy_tile\": %d, \"plan_specialised\": %d, "
+                  "\"wave_ring_pad\": %d}",
+                  c->g.k, c->g.n, c->g.S, c->g.CW, enc, cpy, c->fast_tp, c->persist_tp, c->persist_wgs,
+                  c->persist_tp ? c->pers_lds(c->persist_tp) : 0, c->copyf_tp, c->plan_fast ? 1 : 0,
+                  c->wave_pad);
     return FEC_OK;
 }
 
