@@ -34,7 +34,10 @@ namespace fec {
 namespace {
 
 constexpr int kWaveThreads = 256;
-constexpr int kTabAhead = 2;  // coefficient tables are read this many (word, parity) items early
+#ifndef FEC_TAB_AHEAD
+#define FEC_TAB_AHEAD 2
+#endif
+constexpr int kTabAhead = FEC_TAB_AHEAD;  // coefficient tables are read this many (word, parity) items early
 
 typedef uint32_t u32x4a __attribute__((ext_vector_type(4), aligned(4)));
 typedef uint32_t u32x3a __attribute__((ext_vector_type(3), aligned(4)));
@@ -501,8 +504,12 @@ __global__ __launch_bounds__(kWaveThreads, 4) void fec_encode_wave_kernel(EncWav
                 auto tload = [&](auto kc) __attribute__((always_inline)) {
                     constexpr int k = decltype(kc)::value;
                     constexpr int I = K - 1 - k / (NP > 0 ? NP : 1), JJ = k % (NP > 0 ? NP : 1);
+#ifdef FEC_VAR_NOZ
+                    const int z = 0;
+#else
                     int z;
                     asm volatile("s_mov_b32 %0, 0" : "=s"(z));  // keeps the table reads in this step
+#endif
                     tb[k % NB] = tabs[z + (I * NP + JJ) * 2];
                     t4b[k % NB] = tabs[z + (I * NP + JJ) * 2 + 1].x;
                 };

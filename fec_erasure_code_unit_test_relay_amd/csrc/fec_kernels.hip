@@ -456,6 +456,7 @@ __global__ __launch_bounds__(64) void fec_plan_kernel(PlanArgs a) {
 // ------------------------------------------------------------------------------------------
 constexpr int kRecMaxK = 16;  // = kMaxK (fec_host.h)
 constexpr int kRecMaxN = 17;  // = kMaxRuleN: codecs with n > 17 are refused
+constexpr int kRecRounds = 5;  // 64-byte rounds per pass of fec_recover_kernel (L = 300: one pass)
 
 __global__ __launch_bounds__(256) void fec_recover_kernel(RecArgs a) {
     // One wave per recovered packet, no workgroup barrier after the table load: lane h computes
@@ -481,36 +482,48 @@ __global__ __launch_bounds__(256) void fec_recover_kernel(RecArgs a) {
         }
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        // kRecRounds rounds of 64 bytes per pass: every source byte of the pass is loaded before
+        // the first lookup, so the pass costs one memory round trip instead of one per round
+        const uint8_t* __restrict__ cwp = a.cw;
+        uint8_t* __restrict__ outp = a.out;
         int ln = 0;
-        for (int h0 = 0; h0 < L + 2; h0 += 64) {
-            const int h = h0 + lane;
-            uint8_t acc = 0;
-            if (h < L + 2) {
+        for (int h0 = 0; h0 < L + 2; h0 += 64 * kRecRounds) {
+            uint8_t v[kRecRounds][kRecMaxN];
+            int iw[kRecRounds];
+#pragma unroll
+            for (int rr = 0; rr < kRecRounds; ++rr) {
+                const int h = h0 + 64 * rr + lane;
                 const int sidx = h / k, i = h - sidx * k;
-                uint8_t v[kRecMaxN];
+                iw[rr] = i;
 #pragma unroll
                 for (int q = 0; q < kRecMaxN; ++q) {
-                    v[q] = 0;
-                    if (q < n) {
+                    v[rr][q] = 0;
+                    if (q < n && h < L + 2) {
                         const int64_t row = x - i + q;
-                        if (lc[i * n + q] != 255 && row >= 0 && row < a.P) v[q] = a.cw[row * CW + sidx * n + q];
+                        if (lc[i * n + q] != 255 && row >= 0 && row < a.P) v[rr][q] = cwp[row * CW + sidx * n + q];
                     }
                 }
+            }
+#pragma unroll
+            for (int rr = 0; rr < kRecRounds; ++rr) {
+                const int h = h0 + 64 * rr + lane;
+                const int i = iw[rr];
+                uint8_t acc = 0;
 #pragma unroll
                 for (int q = 0; q < kRecMaxN; ++q) {
-                    if (q < n && v[q]) {
+                    if (q < n && v[rr][q]) {
                         const int lq = lc[i * n + q];
-                        if (lq != 255) acc ^= gexp[lq + glog[v[q]]];
+                        if (lq != 255) acc ^= gexp[lq + glog[v[rr][q]]];
                     }
                 }
+                if (h0 == 0 && rr == 0) {  // recovered length (Decoder.cpp:141-149): bytes 0, 1, clamped to L
+                    const int hi = __builtin_amdgcn_readlane(static_cast<int>(acc), 0);
+                    const int lo = __builtin_amdgcn_readlane(static_cast<int>(acc), 1);
+                    ln = min(hi * 256 + lo, L);
+                }
+                const int b = h - 2;
+                if (b >= 0 && b < L) outp[x * L + b] = b < ln ? acc : 0;
             }
-            if (h0 == 0) {  // recovered length (Decoder.cpp:141-149): bytes 0 and 1, clamped to L
-                const int hi = __builtin_amdgcn_readlane(static_cast<int>(acc), 0);
-                const int lo = __builtin_amdgcn_readlane(static_cast<int>(acc), 1);
-                ln = min(hi * 256 + lo, L);
-            }
-            const int b = h - 2;
-            if (b >= 0 && b < L) a.out[x * L + b] = b < ln ? acc : 0;
         }
         if (lane == 0) a.out_len[x] = ln;
         __builtin_amdgcn_wave_barrier();  // lc is rewritten by the next packet
