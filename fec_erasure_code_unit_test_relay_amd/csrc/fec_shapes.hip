@@ -31,6 +31,35 @@ __device__ __forceinline__ uint32_t shape_hash(uint64_t m, int bits) {
     return static_cast<uint32_t>((m * 0x9E3779B97F4A7C15ull) >> (64 - bits));
 }
 
+// Erasure flags of packets t0 .. t0+63 as bits (bit j = packet t0+j erased; past P: 0).  Nine
+// aligned 8-byte loads instead of 64 byte loads: one thread walks one episode, so these loads
+// are scattered, and their number is what the planner pays beside the copy kernel.
+__device__ __forceinline__ uint64_t erasure_bits64(const uint8_t* er, int64_t P, int64_t t0) {
+    uint64_t fl = 0;
+    const uintptr_t ad = reinterpret_cast<uintptr_t>(er + t0);
+    const uintptr_t a0 = ad & ~uintptr_t(7);  // the nine words cover [a0, a0 + 72) inside er[0, P)
+    if (t0 >= 8 && t0 + 72 <= P) {
+        const int sh = static_cast<int>(ad - a0) * 8;
+        const uint64_t* p = reinterpret_cast<const uint64_t*>(a0);
+        uint64_t w[9];
+#pragma unroll
+        for (int i = 0; i < 9; ++i) w[i] = p[i];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const uint64_t x = sh ? ((w[i] >> sh) | (w[i + 1] << (64 - sh))) : w[i];
+            // byte != 0 -> 0x01, then bit b of the result = byte b
+            const uint64_t nz = ((((x & 0x7F7F7F7F7F7F7F7Full) + 0x7F7F7F7F7F7F7F7Full) | x) >> 7) & 0x0101010101010101ull;
+            fl |= ((nz * 0x0102040810204080ull) >> 56) << (8 * i);
+        }
+    } else {
+        for (int j = 0; j < 64; ++j) {
+            const int64_t t = t0 + j;
+            if (t < P && er[t]) fl |= uint64_t(1) << j;
+        }
+    }
+    return fl;
+}
+
 // Wave-aggregated append of `item` for the lanes where `want` holds.
 __device__ __forceinline__ void wave_append(bool want, int32_t* counter, int32_t* list, int item) {
     const uint64_t bal = __ballot(want);
@@ -68,12 +97,7 @@ __global__ __launch_bounds__(256) void fec_shape_kernel(ShapeArgs a) {
             int latest = 0;
             bool big = false, done = false, truncated = false;
             for (int base = 1; !done; base += 64) {
-                uint64_t fl = 0;
-#pragma unroll 16
-                for (int j = 0; j < 64; ++j) {
-                    const int64_t t = tr + base + j;
-                    if (t < a.P && a.er[t]) fl |= uint64_t(1) << j;
-                }
+                uint64_t fl = erasure_bits64(a.er, a.P, tr + base);
                 while (fl) {
                     const int j = __builtin_ctzll(fl);
                     fl &= fl - 1;
