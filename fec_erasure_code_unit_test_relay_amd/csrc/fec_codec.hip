@@ -725,20 +725,27 @@ int guarded(F&& f) {
 // ------------------------------------------------------------------------------------------
 // Streaming objects
 // ------------------------------------------------------------------------------------------
+// One call per packet is one GPU round trip: the packet goes up (pinned staging, async), one kernel,
+// the result comes down (async), one stream synchronisation.  Everything the coder needs from
+// earlier packets stays on the device.
 struct fec_encoder {
+    static constexpr int kRows = 256;  // device window: the n-1 packets in front + appended packets
     std::unique_ptr<fec_codec> codec;
     int64_t next = 0;              // expected seq
-    std::vector<uint8_t> hist;     // last n-1 payload rows (oldest first) + current row
-    std::vector<int32_t> hlen;
-    uint8_t* d_in = nullptr;       // n rows x L
-    int32_t* d_len = nullptr;      // n
-    uint8_t* d_cw = nullptr;       // CW
-    int32_t* d_cwlen = nullptr;    // 1
+    int pos = 0;                   // window row of the next packet
+    int res_len_off = 0;           // offset of the trimmed size in the result block (4-aligned)
+    hipStream_t s = nullptr;
+    uint8_t* d_rows = nullptr;     // kRows x L
+    int32_t* d_len = nullptr;      // kRows
+    uint8_t* d_res = nullptr;      // codeword (CW) | trimmed size
+    uint8_t* h_stage = nullptr;    // pinned: payload row (L, padded to 4) | length
+    uint8_t* h_res = nullptr;      // pinned copy of d_res
     ~fec_encoder() {
-        if (d_in) (void)hipFree(d_in);
-        if (d_len) (void)hipFree(d_len);
-        if (d_cw) (void)hipFree(d_cw);
-        if (d_cwlen) (void)hipFree(d_cwlen);
+        if (s) (void)hipStreamDestroy(s);
+        for (void* p : {static_cast<void*>(d_rows), static_cast<void*>(d_len), static_cast<void*>(d_res)})
+            if (p) (void)hipFree(p);
+        if (h_stage) (void)hipHostFree(h_stage);
+        if (h_res) (void)hipHostFree(h_res);
     }
 };
 
@@ -747,16 +754,23 @@ struct fec_decoder {
     std::unique_ptr<fec_codec> codec;
     std::unique_ptr<fec::StreamPlanner> planner;
     int64_t next = 0;
-    std::vector<uint8_t> pad;      // CW-byte staging row
+    int res_len_off = 0;
+    bool pending = false;          // an upload from h_cw may still be in flight
+    hipStream_t s = nullptr;
     uint8_t* d_ring = nullptr;     // RR x CW
-    uint8_t* d_coef = nullptr;     // k x n
-    uint8_t* d_out = nullptr;      // L
-    int32_t* d_outlen = nullptr;   // 1
+    uint8_t* d_coef = nullptr;     // k x n (recovered packets)
+    uint8_t* d_ident = nullptr;    // k x n identity (received packets)
+    uint8_t* d_res = nullptr;      // payload (L) | length
+    uint8_t* h_cw = nullptr;       // pinned CW-byte staging row
+    uint8_t* h_coef = nullptr;     // pinned k x n
+    uint8_t* h_res = nullptr;      // pinned copy of d_res
     ~fec_decoder() {
-        if (d_ring) (void)hipFree(d_ring);
-        if (d_coef) (void)hipFree(d_coef);
-        if (d_out) (void)hipFree(d_out);
-        if (d_outlen) (void)hipFree(d_outlen);
+        if (s) (void)hipStreamDestroy(s);
+        for (void* p : {static_cast<void*>(d_ring), static_cast<void*>(d_coef), static_cast<void*>(d_ident),
+                        static_cast<void*>(d_res)})
+            if (p) (void)hipFree(p);
+        for (void* p : {static_cast<void*>(h_cw), static_cast<void*>(h_coef), static_cast<void*>(h_res)})
+            if (p) (void)hipHostFree(p);
     }
 };
 
@@ -983,12 +997,14 @@ int fec_encoder_create(int max_payload, int T, int B, int N, fec_encoder** out) 
         if (int st = fec_codec_create(max_payload, T, B, N, &c)) return st;
         e->codec.reset(c);
         const Geometry& g = c->g;
-        e->hist.assign(static_cast<size_t>(g.n) * g.L, 0);
-        e->hlen.assign(g.n, 0);
-        HIP_TRY(hipMalloc(&e->d_in, static_cast<size_t>(g.n) * g.L));
-        HIP_TRY(hipMalloc(&e->d_len, g.n * 4));
-        HIP_TRY(hipMalloc(&e->d_cw, g.CW));
-        HIP_TRY(hipMalloc(&e->d_cwlen, 4));
+        if (g.n > fec_encoder::kRows / 2) return FEC_ERR_ARG;
+        e->res_len_off = (g.CW + 3) & ~3;
+        HIP_TRY(hipStreamCreateWithFlags(&e->s, hipStreamNonBlocking));
+        HIP_TRY(hipMalloc(&e->d_rows, static_cast<size_t>(fec_encoder::kRows) * g.L));
+        HIP_TRY(hipMalloc(&e->d_len, fec_encoder::kRows * 4));
+        HIP_TRY(hipMalloc(&e->d_res, e->res_len_off + 4));
+        HIP_TRY(hipHostMalloc(&e->h_stage, ((g.L + 3) & ~3) + 4));
+        HIP_TRY(hipHostMalloc(&e->h_res, e->res_len_off + 4));
         *out = e.release();
         return FEC_OK;
     });
@@ -1006,21 +1022,30 @@ int fec_encoder_transmit(fec_encoder* e, const uint8_t* data, int payload, int s
     const Geometry& g = e->codec->g;
     if (payload > g.L) payload = g.L;
     const int n = g.n;
-    // slide the (n-1)-packet history window and append packet seq as the last row
-    std::memmove(e->hist.data(), e->hist.data() + g.L, static_cast<size_t>(n - 1) * g.L);
-    std::memmove(e->hlen.data(), e->hlen.data() + 1, static_cast<size_t>(n - 1) * 4);
-    uint8_t* row = e->hist.data() + static_cast<size_t>(n - 1) * g.L;
-    std::memset(row, 0, g.L);
-    if (payload > 0) std::memcpy(row, data, payload);
-    e->hlen[n - 1] = payload;
-    HIP_TRY(hipMemcpy(e->d_in, e->hist.data(), e->hist.size(), hipMemcpyHostToDevice));
-    HIP_TRY(hipMemcpy(e->d_len, e->hlen.data(), n * 4, hipMemcpyHostToDevice));
-    const int64_t history = std::min<int64_t>(seq, n - 1);
-    if (int st = launch_encode(e->codec.get(), e->d_in + static_cast<size_t>(n - 1) * g.L,
-                               e->d_len + (n - 1), history, 1, e->d_cw, e->d_cwlen, nullptr))
+    if (e->pos == fec_encoder::kRows) {  // window full: its last n-1 rows move to the front
+        const int keep = n - 1;
+        HIP_TRY(hipMemcpyAsync(e->d_rows, e->d_rows + static_cast<size_t>(fec_encoder::kRows - keep) * g.L,
+                               static_cast<size_t>(keep) * g.L, hipMemcpyDeviceToDevice, e->s));
+        HIP_TRY(hipMemcpyAsync(e->d_len, e->d_len + (fec_encoder::kRows - keep), keep * 4,
+                               hipMemcpyDeviceToDevice, e->s));
+        e->pos = keep;
+    }
+    const int lrow = (g.L + 3) & ~3;
+    std::memset(e->h_stage, 0, g.L);
+    if (payload > 0) std::memcpy(e->h_stage, data, payload);
+    std::memcpy(e->h_stage + lrow, &payload, 4);
+    uint8_t* row = e->d_rows + static_cast<size_t>(e->pos) * g.L;
+    HIP_TRY(hipMemcpyAsync(row, e->h_stage, g.L, hipMemcpyHostToDevice, e->s));
+    HIP_TRY(hipMemcpyAsync(e->d_len + e->pos, e->h_stage + lrow, 4, hipMemcpyHostToDevice, e->s));
+    const int64_t history = std::min<int64_t>(std::min<int64_t>(seq, n - 1), e->pos);
+    int32_t* d_size = reinterpret_cast<int32_t*>(e->d_res + e->res_len_off);
+    if (int st = launch_encode(e->codec.get(), row, e->d_len + e->pos, history, 1, e->d_res, d_size, e->s))
         return st;
-    HIP_TRY(hipMemcpy(cw_out, e->d_cw, g.CW, hipMemcpyDeviceToHost));
-    HIP_TRY(hipMemcpy(cw_size, e->d_cwlen, 4, hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemcpyAsync(e->h_res, e->d_res, e->res_len_off + 4, hipMemcpyDeviceToHost, e->s));
+    HIP_TRY(hipStreamSynchronize(e->s));
+    std::memcpy(cw_out, e->h_res, g.CW);
+    std::memcpy(cw_size, e->h_res + e->res_len_off, 4);
+    ++e->pos;
     ++e->next;
     return FEC_OK;
 }
@@ -1037,12 +1062,19 @@ int fec_decoder_create(int max_payload, int T, int B, int N, fec_decoder** out) 
         const Geometry& g = c->g;
         if (g.T + g.k > fec_decoder::RR) return FEC_ERR_ARG;
         d->planner.reset(new fec::StreamPlanner(g, &c->rules));
-        d->pad.assign(g.CW, 0);
+        d->res_len_off = (g.L + 3) & ~3;
+        HIP_TRY(hipStreamCreateWithFlags(&d->s, hipStreamNonBlocking));
         HIP_TRY(hipMalloc(&d->d_ring, static_cast<size_t>(fec_decoder::RR) * g.CW));
         HIP_TRY(hipMemset(d->d_ring, 0, static_cast<size_t>(fec_decoder::RR) * g.CW));
         HIP_TRY(hipMalloc(&d->d_coef, g.k * g.n));
-        HIP_TRY(hipMalloc(&d->d_out, g.L));
-        HIP_TRY(hipMalloc(&d->d_outlen, 4));
+        HIP_TRY(hipMalloc(&d->d_ident, g.k * g.n));
+        std::vector<uint8_t> ident(static_cast<size_t>(g.k) * g.n, 0);
+        for (int i = 0; i < g.k; ++i) ident[i * g.n + i] = 1;
+        HIP_TRY(hipMemcpy(d->d_ident, ident.data(), ident.size(), hipMemcpyHostToDevice));
+        HIP_TRY(hipMalloc(&d->d_res, d->res_len_off + 4));
+        HIP_TRY(hipHostMalloc(&d->h_cw, g.CW));
+        HIP_TRY(hipHostMalloc(&d->h_coef, g.k * g.n));
+        HIP_TRY(hipHostMalloc(&d->h_res, d->res_len_off + 4));
         *out = d.release();
         return FEC_OK;
     });
@@ -1059,12 +1091,17 @@ int fec_decoder_receive(fec_decoder* d, const uint8_t* cw, int cw_size, int seq,
     if (seq != d->next) return FEC_ERR_SEQUENCE;
     const Geometry& g = d->codec->g;
     const bool er = erasure != 0 || cw == nullptr;
+    if (d->pending) {  // the staging row of an earlier call may still be uploading
+        HIP_TRY(hipStreamSynchronize(d->s));
+        d->pending = false;
+    }
     if (!er) {  // FEC_Decoder.cpp:55-63: keep a zero-padded copy of the wire codeword
         int sz = std::max(0, std::min(cw_size, g.CW));
-        std::memset(d->pad.data(), 0, g.CW);
-        if (sz) std::memcpy(d->pad.data(), cw, sz);
-        HIP_TRY(hipMemcpy(d->d_ring + static_cast<size_t>(seq % fec_decoder::RR) * g.CW,
-                          d->pad.data(), g.CW, hipMemcpyHostToDevice));
+        std::memset(d->h_cw, 0, g.CW);
+        if (sz) std::memcpy(d->h_cw, cw, sz);
+        HIP_TRY(hipMemcpyAsync(d->d_ring + static_cast<size_t>(seq % fec_decoder::RR) * g.CW, d->h_cw, g.CW,
+                               hipMemcpyHostToDevice, d->s));
+        d->pending = true;
     }
     fec::StepResult r;
     int st = guarded([&] {
@@ -1078,31 +1115,32 @@ int fec_decoder_receive(fec_decoder* d, const uint8_t* cw, int cw_size, int seq,
         *payload = 0;
         return FEC_OK;
     }
-    uint8_t coef[fec::kMaxK * fec::kMaxN];
-    if (r.fate == fec::kCopy) {
-        std::memset(coef, 0, sizeof(coef));
-        for (int i = 0; i < g.k; ++i) coef[i * g.n + i] = 1;
-    } else {
-        std::memcpy(coef, r.coef, g.k * g.n);
+    const uint8_t* coef = d->d_ident;
+    if (r.fate == fec::kRecovered) {
+        std::memcpy(d->h_coef, r.coef, g.k * g.n);
+        HIP_TRY(hipMemcpyAsync(d->d_coef, d->h_coef, g.k * g.n, hipMemcpyHostToDevice, d->s));
+        coef = d->d_coef;
     }
-    HIP_TRY(hipMemcpy(d->d_coef, coef, g.k * g.n, hipMemcpyHostToDevice));
     fec::StreamOutArgs a;
     a.ring = d->d_ring;
     a.RR = fec_decoder::RR;
     a.x = r.x;
-    a.coef = d->d_coef;
+    a.coef = coef;
     a.gf = d->codec->d_gf;
-    a.out = d->d_out;
-    a.out_len = d->d_outlen;
+    a.out = d->d_res;
+    a.out_len = reinterpret_cast<int32_t*>(d->d_res + d->res_len_off);
     a.L = g.L;
     a.k = g.k;
     a.n = g.n;
     a.CW = g.CW;
     a.clamp = r.slow ? 1 : 0;
-    hipLaunchKernelGGL(fec::fec_stream_out_kernel, dim3(1), dim3(256), 0, nullptr, a);
+    hipLaunchKernelGGL(fec::fec_stream_out_kernel, dim3(1), dim3(256), 0, d->s, a);
     HIP_TRY(hipGetLastError());
-    HIP_TRY(hipMemcpy(payload_out, d->d_out, g.L, hipMemcpyDeviceToHost));
-    HIP_TRY(hipMemcpy(payload, d->d_outlen, 4, hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemcpyAsync(d->h_res, d->d_res, d->res_len_off + 4, hipMemcpyDeviceToHost, d->s));
+    HIP_TRY(hipStreamSynchronize(d->s));
+    d->pending = false;
+    std::memcpy(payload_out, d->h_res, g.L);
+    std::memcpy(payload, d->h_res + d->res_len_off, 4);
     return FEC_OK;
 }
 
