@@ -103,3 +103,24 @@ def test_gpu_adaptive_codewords_match_fixed_encoders(adaptive):
         n1 = sw - first
         assert bool((cw_cur[first:sw, :c.CW] == ref[:n1]).all()) and bool((len_cur[first:sw] == ref_len[:n1]).all())
         assert bool((cw_old[sw:end, :c.CW] == ref[n1:]).all()) and bool((len_old[sw:end] == ref_len[n1:]).all())
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("pattern,mds", [("bin_erasure2", False), ("bin_erasure", True), ("erasure50", False)])
+def test_gpu_schedule_round_trip_other_patterns(pattern, mds):
+    """Other shipped patterns and the MDS estimator mode: every packet the plan reports received or
+    recovered comes back bit-exact, the others come back empty."""
+    import torch
+    from fec_erasure_code_unit_test_relay_amd import fill_payload
+    torch.cuda.set_device(0)
+    pat = load_pattern(pattern)
+    P = min(120000, pat.size - 20)
+    v = VrPlan(pat, P, adaptive_mode_MDS=mds)
+    assert v.fate.min() >= 1 and int((v.fate == 3).sum()) == v.lost
+    payload = fill_payload(0, v.sent, 300, 0x5EED)
+    cw_cur, _, cw_old, _ = v.encode(payload)
+    out, out_len = v.decode(cw_cur, cw_old)
+    torch.cuda.synchronize()
+    ok = torch.from_numpy(v.fate != 3).cuda()
+    assert int((out_len == 0).sum()) == v.lost
+    assert bool((out[ok] == payload[:P][ok]).all()) and bool((out_len[ok] == 300).all())
