@@ -237,21 +237,22 @@ int codec_init(fec_codec* c, int max_payload, int T, int B, int N) {
         const int ns4 = c->ns4();
         c->wave_ring = 64;
         while (c->wave_ring < 2 * g.CW + 4 * g.n + 80) c->wave_ring <<= 1;
-        c->wave_lds = 4 * (64 / ns4 + 1) * c->wave_ring;
+        c->wave_lds = 4 * (64 / ns4 + 1) * (c->wave_ring + 128);  // rings + 128-byte size rings
         if (c->wave_lds > 128 * 1024) c->wave_kernel = nullptr;
     }
     if (c->wave_kernel) {
         // per-sequence ring padding (up to 64 dwords) that puts the sequences of a wave on
         // disjoint LDS banks for the codeword writes; used when it costs no occupancy
         const int ns4 = c->ns4();
-        const int lds_pad = 4 * (64 / ns4 + 1) * (c->wave_ring + 256);
+        const int lds_pad = 4 * (64 / ns4 + 1) * (c->wave_ring + 256 + 128);
+        const bool pad_fits = lds_pad <= 128 * 1024;
         HIP_TRY(hipFuncSetAttribute(c->wave_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                    std::min(lds_pad, 160 * 1024)));
+                                    pad_fits ? lds_pad : c->wave_lds));
         int dev = 0, cus = 0, per_cu = 0, per_cu_pad = 0;
         HIP_TRY(hipGetDevice(&dev));
         HIP_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
         HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, c->wave_kernel, 256, c->wave_lds));
-        if (lds_pad <= 160 * 1024)
+        if (pad_fits)
             HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu_pad, c->wave_kernel, 256, lds_pad));
         c->wave_pad = (per_cu_pad >= per_cu && (g.n & 1)) ? 1 : 0;
         if (const char* v = std::getenv("FEC_WAVE_PAD")) c->wave_pad = std::atoi(v) && per_cu_pad >= per_cu;

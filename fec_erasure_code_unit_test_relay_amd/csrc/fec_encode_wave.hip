@@ -225,7 +225,8 @@ __device__ __forceinline__ void store_words(__amdgpu_buffer_rsrc_t rc, int o, co
 // byte over the sequence's lanes, reduced towards lane g = 0, which stores it.
 template <int n>
 __device__ __forceinline__ void slow_trim(const uint32_t (&X)[n], int g, int lane, int NS4, int last_g,
-                                                    bool need, bool alive, __amdgpu_buffer_rsrc_t rw, int off) {
+                                                    bool need, bool alive, __amdgpu_buffer_rsrc_t rw, int off,
+                                                    uint32_t* lslot) {
     int z = -1;
 #pragma unroll
     for (int q = n - 1; q >= 0; --q)
@@ -237,7 +238,12 @@ __device__ __forceinline__ void slow_trim(const uint32_t (&X)[n], int g, int lan
         best = o > best ? o : best;
     }
     const bool need0 = bperm(lane + last_g, need ? 1u : 0u) != 0;  // lane 0 asks its last lane
-    if (alive && g == 0 && need0) __builtin_amdgcn_raw_buffer_store_b32(static_cast<uint32_t>(best), rw, off, 0, 0);
+    if (alive && g == 0 && need0) {
+        if (lslot)
+            *lslot = static_cast<uint32_t>(best);
+        else
+            __builtin_amdgcn_raw_buffer_store_b32(static_cast<uint32_t>(best), rw, off, 0, 0);
+    }
 }
 
 }  // namespace
@@ -320,6 +326,14 @@ __global__ __launch_bounds__(kWaveThreads, 4) void fec_encode_wave_kernel(EncWav
         return smem + (wbase + j) * ring_stride + pad * 4;
     };
     uint8_t* ring = ring_of(sq < SPW ? sq : SPW);
+    // Trimmed sizes: a 32-entry LDS ring per sequence (slot t & 31), flushed to HBM one 64-byte
+    // line of 16 packets at a time -- one size per packet stored straight to HBM would be one
+    // partial-line write per packet (~32 MB of extra write traffic per 1M packets).
+    const bool len_lds = !(a.dbg & 16);
+    auto lring_of = [&](int j) __attribute__((always_inline)) {
+        return reinterpret_cast<uint32_t*>(smem + 4 * (SPW + 1) * ring_stride + (wbase + j) * 128);
+    };
+    uint32_t* lring = lring_of(sq < SPW ? sq : SPW);
     const int A0 = r0 * CW;                                    // sequence start (4-byte aligned)
     int fl = A0;                                               // next byte to flush
 
@@ -367,9 +381,15 @@ __global__ __launch_bounds__(kWaveThreads, 4) void fec_encode_wave_kernel(EncWav
             default: break;
         }
         const bool full = (lw >> 24) != 0;
-        if (store && g == last_g && full) __builtin_amdgcn_raw_buffer_store_b32(static_cast<uint32_t>(CW), rw, 4 * t, 0, 0);
+        if (store && g == last_g && full) {
+            if (len_lds)
+                lring[t & 31] = static_cast<uint32_t>(CW);
+            else
+                __builtin_amdgcn_raw_buffer_store_b32(static_cast<uint32_t>(CW), rw, 4 * t, 0, 0);
+        }
         const bool need = store && g == last_g && !full;
-        if (__builtin_amdgcn_ballot_w64(need)) slow_trim<n>(X, g, lane, NS4, last_g, need, alive, rw, 4 * t);
+        if (__builtin_amdgcn_ballot_w64(need))
+            slow_trim<n>(X, g, lane, NS4, last_g, need, alive, rw, 4 * t, len_lds ? &lring[t & 31] : nullptr);
     };
 
     // Flush every sequence's final bytes below row srow (relative to the sequence start): all 64
@@ -418,11 +438,27 @@ __global__ __launch_bounds__(kWaveThreads, 4) void fec_encode_wave_kernel(EncWav
             if (sq == j) fl = flj;
         }
     };
+    // Trimmed sizes of the rows emitted so far: whole 16-packet groups (64-byte lines), and at the
+    // sequence's end the rest.  Stateless: the previous flush ended at (r0j + srow - dprev) & ~15.
+    auto flush_len = [&](int srow, int dprev) __attribute__((always_inline)) {
+        if (!len_lds || (a.dbg & 1)) return;
+        for (int j = 0; j < nseq_w; ++j) {
+            const int r0j = (seq0 + j) * M;
+            const int endj = min(r0j + M, P);
+            const int lo = srow - dprev <= 0 ? r0j : max(r0j, (r0j + srow - dprev) & ~15);
+            const int hi = r0j + srow >= endj ? endj : max(lo, (r0j + srow) & ~15);
+            if (hi <= lo) continue;
+            const int row = lo + lane;
+            if (row < hi) __builtin_amdgcn_raw_buffer_store_b32(lring_of(j)[row & 31], rw, 4 * row, 0, 0);
+        }
+    };
+
     // Steady state (neither a sequence's first flush nor its last): sequence j's window is
     // [(r0j + srow - dprev) * CW & ~15, (r0j + srow) * CW & ~15), 16-byte chunks only, at most one
     // per lane.  Scalar addressing; the LDS reads of four sequences are issued before their stores.
     auto flush = [&](int srow, int dprev) __attribute__((always_inline)) {
         if (a.dbg & 1) return;
+        flush_len(srow, dprev);
         if (!(fast_fit && srow - dprev >= 1 && srow < M && r0_last + srow < P)) {
             flush_slow(srow);
             return;

@@ -77,7 +77,7 @@ struct EncWaveArgs {
     int ring_pad;                 // 1: rings ring_bytes + 256 apart, sequence j shifted so that the
                                   //    wave's codeword writes fall on disjoint banks (odd n)
     int dbg;                      // timing experiments only (FEC_WAVE_DBG): 1 no stores, 2 no parity,
-                                  // 8 16-byte flush boundaries
+                                  // 8 16-byte flush boundaries, 16 sizes stored per packet
 };
 
 // fec_encode_wave_kernel<k, n-k> (fec_encode_wave.hip), else nullptr.  256 threads.
