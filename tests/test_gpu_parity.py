@@ -264,6 +264,40 @@ def test_full_size_round_trip_1M():
     assert replayed + filled == eps and filled > 0
 
 
+def _check_recovered_equal_source(payload, out, ln, P):
+    lnh = ln.cpu().numpy()
+    ok = torch.from_numpy(lnh != 0).cuda()
+    assert (lnh[lnh != 0] == L).all()
+    assert torch.equal(out[ok], payload[:P][ok])
+    return np.flatnonzero(lnh == 0)
+
+
+def test_gpu_decode_reproduces_published_loss_counts(published_runs):
+    """The reference's own published results (Experimental_Logs/Logs/Fixed/*Receiver*.rtf: `Final FEC
+    loss rate` x 360000 on the shipped pattern) reproduced by the HIP decoder itself:
+    12 (T,B,N, pattern) runs, 360 000 packets each, lost count exact, every other packet recovered
+    byte for byte."""
+    P = 360000
+    for run in published_runs:
+        T, B, N = run["T"], run["B"], run["N"]
+        pat = load_pattern(run["pattern"])[:P]
+        c, payload, out, ln, _ = gpu_round_trip(T, B, N, pat, P)
+        lost = _check_recovered_equal_source(payload, out, ln, P)
+        assert lost.size == run["lost_packets"], run["log"]
+
+
+def test_gpu_lost_sets_equal_oracle_recorded_lists(oracle_vectors):
+    """BASELINE config 3 (10,5,2) and (10,3,3) on bin/erasure.bin, 360 000 packets: the GPU's lost
+    packets are exactly the oracle's recorded index lists (565 and 4662 packets)."""
+    P = 360000
+    pat = load_pattern("bin_erasure")[:P]
+    for key, want in oracle_vectors["lost"].items():
+        T, B, N = map(int, key.split(","))
+        c, payload, out, ln, _ = gpu_round_trip(T, B, N, pat, P)
+        lost = _check_recovered_equal_source(payload, out, ln, P)
+        assert lost.tolist() == want, key
+
+
 def test_episode_dedup_many_shapes():
     """Dense random losses (thousands of distinct shapes, long and truncated episodes) with and
     without deduplication: identical outputs, and equal to the host planner's fates."""
