@@ -18,6 +18,7 @@ using fec::Geometry;
 namespace {
 
 constexpr int kLdsBudget = 64 * 1024;
+constexpr int kCopyLdsBudget = 32 * 1024;  // decode copy tiles (see the tile choice below)
 constexpr int kMaxPayload = 1500;  // UDP MTU; bounds the LDS tiles
 
 inline int round16(int v) { return (v + 15) & ~15; }
@@ -262,9 +263,13 @@ int codec_init(fec_codec* c, int max_payload, int T, int B, int N) {
         if (c->wave_slots <= 0) c->wave_kernel = nullptr;
     }
     if ((g.L & 3) == 0) c->copy_fast = fec::fec_copy_fast_kernel_for(g.k, g.n - g.k);
+    // The copy stages its whole tile, converts, then stores (no overlap inside a workgroup), so
+    // smaller tiles with more resident workgroups per CU overlap better: at (10,3,3) 32 packets
+    // (23 KB LDS) take 135 us per 1M packets against 148 us at 64 and 154 us at 16
+    // (profiles/r01/decode_diag/copy_tile_ab.txt, same-process A/B).
     if (c->copy_fast)
         for (int tp = tile_cap("FEC_COPY_TILE"); tp >= 8; tp >>= 1)
-            if (c->copyf_lds(tp) <= kLdsBudget) {
+            if (c->copyf_lds(tp) <= (tp == 8 ? kLdsBudget : kCopyLdsBudget)) {
                 c->copyf_tp = tp;
                 break;
             }
