@@ -32,17 +32,35 @@ L = 300
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak, /opt/skills/guides/MI355X_MICROARCH.md
 
 
+def kernel_sources_digest():
+    """SHA-256 over the HIP/C++ sources of libfec_amd.so (csrc/*.hip, *.h, *.cpp): a PMC traffic
+    figure is only valid for the kernels it was measured on."""
+    import glob
+    import hashlib
+    h = hashlib.sha256()
+    csrc = os.path.join(ROOT, "fec_erasure_code_unit_test_relay_amd", "csrc")
+    for path in sorted(glob.glob(os.path.join(csrc, "*.hip")) + glob.glob(os.path.join(csrc, "*.h")) +
+                       glob.glob(os.path.join(csrc, "*.cpp"))):
+        h.update(os.path.basename(path).encode())
+        with open(path, "rb") as f:
+            h.update(f.read())
+    return h.hexdigest()
+
+
 def pmc_traffic(kernel_symbol):
     """HBM bytes per launch of `kernel_symbol` from the newest committed rocprofv3 FETCH_SIZE /
     WRITE_SIZE passes (profiles/*/*_traffic.json, made by tools/pmc_traffic.{sh,py} over the same
-    step at the same size); None when no pass covers this kernel."""
+    step at the same size).  Returns (bytes, source, fresh): fresh is False when the pass was made
+    on other kernel sources than the ones built here (then the figure is not reported)."""
     import glob
     best = None
+    digest = kernel_sources_digest()
     for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*", "*_traffic.json"))):
         with open(path) as f:
             entry = json.load(f).get(kernel_symbol)
         if entry:
-            best = (entry["traffic_bytes"], os.path.relpath(path, ROOT))
+            best = (entry["traffic_bytes"], os.path.relpath(path, ROOT),
+                    entry.get("sources_sha256") == digest)
     return best
 
 
@@ -130,8 +148,8 @@ def extra_configs(steps=5):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=100)
-    ap.add_argument("--warmup", type=int, default=50)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--packets", type=int, default=1_000_000, help="decoded packets per GPU")
     ap.add_argument("--tbn", default="10,3,3")
     ap.add_argument("--cpu-packets", type=int, default=60000)
@@ -139,6 +157,8 @@ def main():
     ap.add_argument("--no-host-inclusive", action="store_true")
     ap.add_argument("--encode-path", default="auto", help="A/B: auto|generic|fast|stream|wave")
     ap.add_argument("--no-extra-configs", action="store_true", help="skip BASELINE configs 3 and 4")
+    ap.add_argument("--no-graph", action="store_true",
+                    help="launch the step's kernels one by one instead of replaying a captured hipGraph")
     args = ap.parse_args()
     T, B, N = map(int, args.tbn.split(","))
 
@@ -181,14 +201,30 @@ def main():
         if world > 1:
             dist.barrier()
 
+    # The step (encode; fork; plan on the codec's side stream | copy; join; recover: 9 kernels and
+    # 2 memsets) is captured once into a hipGraph and replayed: one launch per step instead of 11.
+    run = step
+    if not args.no_graph:
+        side = torch.cuda.Stream()
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):
+            for _ in range(3):
+                step()
+        torch.cuda.current_stream().wait_stream(side)
+        torch.cuda.synchronize()
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph):
+            step()
+        run = graph.replay
+
     for _ in range(args.warmup):
-        step()
+        run()
     torch.cuda.synchronize()
     barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        step()
+        run()
     torch.cuda.synchronize()
     barrier()
     torch.cuda.synchronize()
@@ -243,6 +279,7 @@ def main():
                        "codeword_bytes": codec.CW, "packets_per_gpu": P,
                        "parallelism": f"streams{world} (one independent stream per GPU)"},
             "verified": bool(verified_all == world),
+            "step_launch": "hipGraph replay" if not args.no_graph else "eager launches",
             "decode": {"erased": erased_all, "recovered": rec_all, "lost": lost_all},
             "algorithmic_bytes_per_packet": L + codec.CW + codec.CW + 1 + L,
             "algorithmic_GBps": round(world * P * (2 * L + 2 * codec.CW + 1) / (elapsed / args.steps) / 1e9, 1),
@@ -254,10 +291,12 @@ def main():
         info = codec.info()
         symbol = info["encode_kernel"] if dominant == "fec_encode_kernel" else info.get("copy_kernel")
         tr = pmc_traffic(symbol) if symbol and P == 1_000_000 else None
-        if tr:
+        result["roofline"].update(algorithmic_bytes=algo[dominant], traffic_kernel=symbol)
+        if tr and tr[2]:
             result["roofline"].update(traffic=tr[0], traffic_unit="bytes per launch",
-                                      algorithmic_bytes=algo[dominant], traffic_kernel=symbol,
                                       traffic_source=tr[1])
+        elif tr:
+            result["roofline"].update(traffic_stale=f"{tr[1]} was measured on other kernel sources")
     if world == 1 and not args.no_host_inclusive:
         # end-to-end from/to host memory (pinned): H2D payload, encode, D2H wire codewords,
         # H2D codewords + erasures, decode, D2H payloads + lengths

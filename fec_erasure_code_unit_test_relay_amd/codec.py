@@ -26,6 +26,30 @@ def _ptr(t):
     return ctypes.c_void_p(t.data_ptr()) if t is not None else None
 
 
+def _check_out(torch, out, out_len, rows: int, width: int, device):
+    """Allocate, or validate caller-supplied, output buffers of at least [rows, width] uint8 and
+    [rows] int32 (the C side writes that many rows through raw pointers)."""
+    if out is None:
+        out = torch.empty((rows, width), dtype=torch.uint8, device=device)
+    else:
+        assert out.dtype == torch.uint8 and out.is_cuda and out.is_contiguous(), "out: contiguous uint8 GPU tensor"
+        assert out.dim() == 2 and out.shape[1] == width and out.shape[0] >= rows, \
+            f"out must be at least [{rows}, {width}], got {tuple(out.shape)}"
+    if out_len is None:
+        out_len = torch.empty(rows, dtype=torch.int32, device=device)
+    else:
+        assert out_len.dtype == torch.int32 and out_len.is_cuda and out_len.is_contiguous(), \
+            "out_len: contiguous int32 GPU tensor"
+        assert out_len.numel() >= rows, f"out_len must hold at least {rows} entries"
+    return out, out_len
+
+
+def _check_erasure(torch, erasure, P: int):
+    assert erasure.dtype == torch.uint8 and erasure.is_cuda and erasure.is_contiguous(), \
+        "erasure: contiguous uint8 GPU tensor"
+    assert erasure.numel() >= P, f"erasure must hold at least {P} flags"
+
+
 class Codec:
     """One (max_payload, T, B, N) configuration on the current HIP device.
 
@@ -123,12 +147,11 @@ class Codec:
         assert payload.dtype == torch.uint8 and payload.is_cuda and payload.dim() == 2
         assert payload.shape[1] == self.L and payload.is_contiguous()
         P = payload.shape[0] - history
+        assert 0 <= history <= payload.shape[0]
         if lengths is not None:
             assert lengths.dtype == torch.int32 and lengths.is_cuda and lengths.numel() == payload.shape[0]
-        if out is None:
-            out = torch.empty((P, self.CW), dtype=torch.uint8, device=payload.device)
-        if out_len is None:
-            out_len = torch.empty(P, dtype=torch.int32, device=payload.device)
+            assert lengths.is_contiguous()
+        out, out_len = _check_out(torch, out, out_len, P, self.CW, payload.device)
         row0 = payload[history:] if P > 0 else payload
         len0 = lengths[history:] if lengths is not None else None
         check(lib().fec_encode_batch(self._h, _ptr(row0), _ptr(len0), history, P, _ptr(out),
@@ -148,12 +171,9 @@ class Codec:
         assert codewords.dtype == torch.uint8 and codewords.is_cuda and codewords.is_contiguous()
         assert codewords.shape[1] == self.CW
         P = codewords.shape[0]
-        assert erasure.dtype == torch.uint8 and erasure.numel() == P and erasure.is_cuda
+        _check_erasure(torch, erasure, P)
         Pout = max(0, P - self.T)
-        if out is None:
-            out = torch.empty((Pout, self.L), dtype=torch.uint8, device=codewords.device)
-        if out_len is None:
-            out_len = torch.empty(Pout, dtype=torch.int32, device=codewords.device)
+        out, out_len = _check_out(torch, out, out_len, Pout, self.L, codewords.device)
         ws = self.workspace(P)
         check(lib().fec_decode_batch(self._h, _ptr(codewords), _ptr(erasure), P, _ptr(out),
                                      _ptr(out_len), _ptr(ws), ws.numel(), _stream_handle(torch)),
@@ -163,8 +183,8 @@ class Codec:
     def plan(self, erasure, P: int | None = None):
         """Erasure-only half of the decode (scan + per-episode replay) on the current stream."""
         import torch
-        assert erasure.dtype == torch.uint8 and erasure.is_cuda
         P = erasure.numel() if P is None else P
+        _check_erasure(torch, erasure, P)
         ws = self.workspace(P)
         check(lib().fec_decode_plan(self._h, _ptr(erasure), P, _ptr(ws), ws.numel(),
                                     _stream_handle(torch)), "fec_decode_plan")
@@ -173,12 +193,11 @@ class Codec:
         """Byte half of the decode (systematic copy + recovery); ordered after plan()."""
         import torch
         P = codewords.shape[0]
+        assert codewords.dtype == torch.uint8 and codewords.is_cuda
         assert codewords.shape[1] == self.CW and codewords.is_contiguous()
+        _check_erasure(torch, erasure, P)
         Pout = max(0, P - self.T)
-        if out is None:
-            out = torch.empty((Pout, self.L), dtype=torch.uint8, device=codewords.device)
-        if out_len is None:
-            out_len = torch.empty(Pout, dtype=torch.int32, device=codewords.device)
+        out, out_len = _check_out(torch, out, out_len, Pout, self.L, codewords.device)
         ws = self.workspace(P)
         check(lib().fec_decode_apply(self._h, _ptr(codewords), _ptr(erasure), P, _ptr(out),
                                      _ptr(out_len), _ptr(ws), ws.numel(), _stream_handle(torch)),
@@ -189,12 +208,11 @@ class Codec:
         """Received packets only (independent of plan(); erased rows get length 0)."""
         import torch
         P = codewords.shape[0]
+        assert codewords.dtype == torch.uint8 and codewords.is_cuda
         assert codewords.shape[1] == self.CW and codewords.is_contiguous()
+        _check_erasure(torch, erasure, P)
         Pout = max(0, P - self.T)
-        if out is None:
-            out = torch.empty((Pout, self.L), dtype=torch.uint8, device=codewords.device)
-        if out_len is None:
-            out_len = torch.empty(Pout, dtype=torch.int32, device=codewords.device)
+        out, out_len = _check_out(torch, out, out_len, Pout, self.L, codewords.device)
         check(lib().fec_decode_copy(self._h, _ptr(codewords), _ptr(erasure), P, _ptr(out),
                                     _ptr(out_len), _stream_handle(torch)), "fec_decode_copy")
         return out, out_len
@@ -203,6 +221,9 @@ class Codec:
         """Erased packets (after plan() and copy())."""
         import torch
         P = codewords.shape[0]
+        assert codewords.dtype == torch.uint8 and codewords.is_cuda and codewords.is_contiguous()
+        assert codewords.shape[1] == self.CW
+        _check_out(torch, out, out_len, max(0, P - self.T), self.L, codewords.device)
         ws = self.workspace(P)
         check(lib().fec_decode_recover(self._h, _ptr(codewords), P, _ptr(out), _ptr(out_len),
                                        _ptr(ws), ws.numel(), _stream_handle(torch)),
@@ -260,6 +281,8 @@ class FEC_Encoder:
     def onTransmit(self, data, payload: int, seq: int):
         """Returns (wire codeword bytes (trimmed), codeword_size)."""
         d = np.ascontiguousarray(np.frombuffer(bytes(data), dtype=np.uint8) if isinstance(data, (bytes, bytearray)) else data, dtype=np.uint8)
+        if not 0 <= payload <= d.size:
+            raise ValueError(f"payload {payload} exceeds the {d.size} data bytes given")
         size = ctypes.c_int()
         check(lib().fec_encoder_transmit(self._h, d.ctypes.data_as(ctypes.c_void_p), payload, seq,
                                          self._cw.ctypes.data_as(ctypes.c_void_p), ctypes.byref(size)),
@@ -293,6 +316,8 @@ class FEC_Decoder:
                                            self._out.ctypes.data_as(ctypes.c_void_p), ctypes.byref(p))
         else:
             c = np.ascontiguousarray(codeword, dtype=np.uint8)
+            if not 0 <= codeword_size <= c.size:
+                raise ValueError(f"codeword_size {codeword_size} exceeds the {c.size} bytes given")
             st = lib().fec_decoder_receive(self._h, c.ctypes.data_as(ctypes.c_void_p), codeword_size,
                                            seq, 0, self._out.ctypes.data_as(ctypes.c_void_p),
                                            ctypes.byref(p))

@@ -395,14 +395,16 @@ int launch_encode_persist(fec_codec* c, const uint8_t* d_payload, const int32_t*
 int launch_encode_wave(fec_codec* c, const uint8_t* d_payload, const int32_t* d_len, int64_t history,
                        int64_t P, uint8_t* d_cw, int32_t* d_cwlen, hipStream_t s) {
     const Geometry& g = c->g;
-    history = std::max<int64_t>(0, history);
+    // parity of a packet reads only the n-1 packets in front of it, so more history is never read
+    history = std::min<int64_t>(std::max<int64_t>(0, history), g.n - 1);
     // the kernel addresses rows [-history, P) with 32-bit buffer offsets: batches beyond 2 GB of
-    // payload go in chunks (each sees the n-1 rows in front of it as history)
+    // payload go in chunks (each sees the n-1 rows in front of it as history; history <= n-1
+    // makes every chunk strictly smaller than the call that made it)
     const int64_t max_rows = (int64_t(0x7fffffff) - 4096) / std::max(g.L, g.CW) - g.n;
     if (history + P > max_rows) {
         const int64_t chunk = max_rows - g.n;
         for (int64_t r = 0; r < P; r += chunk) {
-            const int64_t h = r == 0 ? history : std::min<int64_t>(history + r, g.n - 1);
+            const int64_t h = std::min<int64_t>(history + r, g.n - 1);
             if (int st = launch_encode_wave(c, d_payload + r * g.L, d_len ? d_len + r : nullptr, h,
                                             std::min(chunk, P - r), d_cw + r * g.CW, d_cwlen + r, s))
                 return st;
@@ -737,6 +739,7 @@ int guarded(F&& f) {
 struct fec_encoder {
     static constexpr int kRows = 256;  // device window: the n-1 packets in front + appended packets
     std::unique_ptr<fec_codec> codec;
+    int64_t origin = -1;           // seq of the first call (the encoder's creation point)
     int64_t next = 0;              // expected seq
     int pos = 0;                   // window row of the next packet
     int res_len_off = 0;           // offset of the trimmed size in the result block (4-aligned)
@@ -759,6 +762,7 @@ struct fec_decoder {
     static constexpr int RR = 64;  // device ring rows (>= T + k)
     std::unique_ptr<fec_codec> codec;
     std::unique_ptr<fec::StreamPlanner> planner;
+    int64_t origin = -1;           // seq of the first call; the planner runs on seq - origin
     int64_t next = 0;
     int res_len_off = 0;
     bool pending = false;          // an upload from h_cw may still be in flight
@@ -792,7 +796,7 @@ const char* fec_strerror(int status) {
         case FEC_ERR_HIP: return "HIP runtime error";
         case FEC_ERR_NOMEM: return "out of memory";
         case FEC_ERR_WORKSPACE: return "decode workspace too small";
-        case FEC_ERR_SEQUENCE: return "sequence numbers must be consecutive from 0";
+        case FEC_ERR_SEQUENCE: return "sequence numbers must be consecutive from the first call's";
         default: return "unknown error";
     }
 }
@@ -1023,7 +1027,15 @@ int fec_encoder_destroy(fec_encoder* e) {
 
 int fec_encoder_transmit(fec_encoder* e, const uint8_t* data, int payload, int seq, uint8_t* cw_out,
                          int* cw_size) {
-    if (!e || !cw_out || !cw_size || payload < 0 || (payload > 0 && !data)) return FEC_ERR_ARG;
+    if (!e || !cw_out || !cw_size || payload < 0 || (payload > 0 && !data) || seq < 0) return FEC_ERR_ARG;
+    // The reference coder indexes its diagonals by seq % n and starts from an all-zero state, so
+    // it accepts any first seq (Variable_Rate_FEC_Encoder creates encoders mid-stream,
+    // Variable_Rate_FEC_Encoder.cpp:126/144/185); the first call fixes the origin, later calls
+    // must be consecutive.
+    if (e->origin < 0) {
+        e->origin = seq;
+        e->next = seq;
+    }
     if (seq != e->next) return FEC_ERR_SEQUENCE;
     const Geometry& g = e->codec->g;
     if (payload > g.L) payload = g.L;
@@ -1043,7 +1055,7 @@ int fec_encoder_transmit(fec_encoder* e, const uint8_t* data, int payload, int s
     uint8_t* row = e->d_rows + static_cast<size_t>(e->pos) * g.L;
     HIP_TRY(hipMemcpyAsync(row, e->h_stage, g.L, hipMemcpyHostToDevice, e->s));
     HIP_TRY(hipMemcpyAsync(e->d_len + e->pos, e->h_stage + lrow, 4, hipMemcpyHostToDevice, e->s));
-    const int64_t history = std::min<int64_t>(std::min<int64_t>(seq, n - 1), e->pos);
+    const int64_t history = std::min<int64_t>(std::min<int64_t>(seq - e->origin, n - 1), e->pos);
     int32_t* d_size = reinterpret_cast<int32_t*>(e->d_res + e->res_len_off);
     if (int st = launch_encode(e->codec.get(), row, e->d_len + e->pos, history, 1, e->d_res, d_size, e->s))
         return st;
@@ -1093,8 +1105,16 @@ int fec_decoder_destroy(fec_decoder* d) {
 
 int fec_decoder_receive(fec_decoder* d, const uint8_t* cw, int cw_size, int seq, int erasure,
                         uint8_t* payload_out, int* payload) {
-    if (!d || !payload_out || !payload) return FEC_ERR_ARG;
+    if (!d || !payload_out || !payload || seq < 0) return FEC_ERR_ARG;
+    // first call = origin (Variable_Rate_FEC_Decoder creates decoders mid-stream,
+    // Variable_Rate_FEC_Decoder.cpp:2472/2559); the decoder state is a function of seq - origin
+    // (all diagonal blocks start identical, so relabelling them by the origin is exact)
+    if (d->origin < 0) {
+        d->origin = seq;
+        d->next = seq;
+    }
     if (seq != d->next) return FEC_ERR_SEQUENCE;
+    const int64_t rel = seq - d->origin;
     const Geometry& g = d->codec->g;
     const bool er = erasure != 0 || cw == nullptr;
     if (d->pending) {  // the staging row of an earlier call may still be uploading
@@ -1105,13 +1125,13 @@ int fec_decoder_receive(fec_decoder* d, const uint8_t* cw, int cw_size, int seq,
         int sz = std::max(0, std::min(cw_size, g.CW));
         std::memset(d->h_cw, 0, g.CW);
         if (sz) std::memcpy(d->h_cw, cw, sz);
-        HIP_TRY(hipMemcpyAsync(d->d_ring + static_cast<size_t>(seq % fec_decoder::RR) * g.CW, d->h_cw, g.CW,
+        HIP_TRY(hipMemcpyAsync(d->d_ring + static_cast<size_t>(rel % fec_decoder::RR) * g.CW, d->h_cw, g.CW,
                                hipMemcpyHostToDevice, d->s));
         d->pending = true;
     }
     fec::StepResult r;
     int st = guarded([&] {
-        r = d->planner->step(seq, er);
+        r = d->planner->step(rel, er);
         return FEC_OK;
     });
     if (st) return st;

@@ -9,7 +9,11 @@ Inputs (all DATA files shipped by domanovi/FEC_Erasure_Code_Unit_Test_Relay, rea
       run -> published_fixed_logs.json (lost packets = rate * 360000).
 Outputs computed by the oracle restatement (oracle/, pinned by the published logs):
   oracle_vectors.json: lost-packet lists of the survey's configurations on bin/erasure.bin and
-      SHA-256 digests of encoder outputs for the synthetic payload generator.
+      SHA-256 digests of encoder outputs for the synthetic payload generator;
+  config_vectors.json: BASELINE config 1 ((10,3,3), 361000 packets, i.i.d. erasures from
+      generate_IID(361010, eps, seed 0) for eps = 1e-4 and 1e-2: erased/lost lists and digests of
+      the oracle's decoded lengths and bytes) and config 2 (SHA-256 of the oracle's 1,000,010
+      (10,3,3) codewords and wire sizes, the bench's encoded batch).
 
 Usage:  python tests/golden/make_fixtures.py [/root/reference]
 """
@@ -92,9 +96,37 @@ def oracle_vectors() -> None:
         json.dump(vec, f)
 
 
+def config_vectors() -> None:
+    """BASELINE configs 1 and 2 at their full sizes (oracle; a few minutes of CPU)."""
+    import oracle
+    from fec_erasure_code_unit_test_relay_amd.erasure import Erasure_File_Generator
+    vec = {"payload_seed": 0x5EED, "max_payload": 300, "config1": {}, "config2": {}}
+    P = 361000
+    for eps in (1e-4, 1e-2):
+        pat = Erasure_File_Generator().generate_IID(P + 10, eps, seed=0)
+        r = oracle.run_stream(300, 10, 3, 3, P, pat, seed=0x5EED, want_data=True)
+        vec["config1"]["%g" % eps] = {
+            "packets": P, "pattern": "generate_IID(%d, %g, seed=0)" % (P + 10, eps),
+            "pattern_sha256": hashlib.sha256(pat.tobytes()).hexdigest(),
+            "erased": np.flatnonzero(pat[:P + 10]).tolist(),
+            "lost": np.flatnonzero(r["out_len"] == 0).tolist(),
+            "out_len_sha256": hashlib.sha256(r["out_len"].astype("<i4").tobytes()).hexdigest(),
+            "out_data_sha256": hashlib.sha256(r["out_data"].tobytes()).hexdigest()}
+    P2 = 1_000_010
+    e = oracle.encode_stream(300, 10, 3, 3, 0, P2, seed=0x5EED)
+    vec["config2"] = {"T": 10, "B": 3, "N": 3, "packets": P2,
+                      "codeword_sha256": hashlib.sha256(e["cw"].tobytes()).hexdigest(),
+                      "wire_len_sha256": hashlib.sha256(e["cw_len"].astype("<i4").tobytes()).hexdigest()}
+    with open(os.path.join(HERE, "config_vectors.json"), "w") as f:
+        json.dump(vec, f)
+
+
 if __name__ == "__main__":
-    ref = sys.argv[1] if len(sys.argv) > 1 else "/root/reference"
-    pack_patterns(ref)
-    parse_logs(ref)
-    oracle_vectors()
+    args = [a for a in sys.argv[1:] if not a.startswith("--")]
+    ref = args[0] if args else "/root/reference"
+    if "--configs-only" not in sys.argv:
+        pack_patterns(ref)
+        parse_logs(ref)
+        oracle_vectors()
+    config_vectors()
     print("fixtures written to", HERE)

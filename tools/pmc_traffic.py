@@ -13,7 +13,11 @@ import json
 import os
 import sys
 
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
+from bench import kernel_sources_digest  # noqa: E402
+
 out, tag, dirs = sys.argv[1], sys.argv[2], sys.argv[3:]
+digest = kernel_sources_digest()
 vals = collections.defaultdict(lambda: collections.defaultdict(list))
 for d in dirs:
     for path in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
@@ -31,6 +35,7 @@ for name, cs in vals.items():
     write = 1024 * sum(cs["WRITE_SIZE"]) / len(cs["WRITE_SIZE"])
     res[name] = {"fetch_bytes": round(fetch), "write_bytes": round(write),
                  "traffic_bytes": round(fetch + write), "run": tag,
+                 "sources_sha256": digest,
                  "note": "FETCH_SIZE x2 (gfx950 correction), WRITE_SIZE as read; per launch"}
 json.dump(res, open(out, "w"), indent=1, sort_keys=True)
 print(json.dumps(res, indent=1))
