@@ -1187,6 +1187,29 @@ int fec_plan_host(int max_payload, int T, int B, int N, const uint8_t* erasure, 
     });
 }
 
+}  // extern "C"
+
+int fec::codec_view(const fec_codec* c, fec::CodecView* v) {
+    if (!c || !v) return FEC_ERR_ARG;
+    const Geometry& g = c->g;
+    v->L = g.L;
+    v->T = g.T;
+    v->B = g.B;
+    v->N = g.N;
+    v->k = g.k;
+    v->n = g.n;
+    v->S = g.S;
+    v->CW = g.CW;
+    v->G = c->d_G;
+    v->gf = c->d_gf;
+    v->rules = c->d_rules;
+    v->wbase_n = c->rules.w_base[g.n];
+    v->ES = c->rules.entry_bytes;
+    return FEC_OK;
+}
+
+extern "C" {
+
 // ---- block mode (fec_block.hip) ------------------------------------------------------------
 static int launch_block(fec_codec* c, bool decode, const uint8_t* d_in, const uint8_t* d_er, int64_t nblk,
                         uint8_t* d_out, uint8_t* d_er_out, void* stream) {

@@ -194,6 +194,16 @@ struct BlockArgs {
     int ES;                     // rule entry bytes
 };
 __global__ void fec_block_encode_kernel(BlockArgs a);
+
+// Host view of a codec's device-resident constants (fec_codec.hip), for other launchers.
+struct CodecView {
+    int L, T, B, N, k, n, S, CW;
+    const uint8_t* G;           // k x n generator (device)
+    const uint8_t* gf;          // exp[512], log[256] (device)
+    const uint8_t* rules;       // decode rule table, raw coefficients (device)
+    int64_t wbase_n;            // byte offset of window n's rules
+    int ES;                     // rule entry bytes
+};
 __global__ void fec_block_decode_kernel(BlockArgs a);
 
 __global__ void fec_encode_kernel(EncArgs a);
@@ -209,4 +219,9 @@ __global__ void fec_recover_kernel(RecArgs a);
 __global__ void fec_stream_out_kernel(StreamOutArgs a);
 __global__ void fec_fill_kernel(uint8_t* out, int64_t t0, int64_t count, int L, uint64_t seed);
 
+}  // namespace fec
+
+struct fec_codec;
+namespace fec {
+int codec_view(const ::fec_codec* c, CodecView* v);
 }  // namespace fec

@@ -1,0 +1,84 @@
+"""Relay symbol-wise decode-and-forward (SWDF) over the MI355X C ABI (include/fec_amd.h,
+fec_swdf_*).
+
+Mirrors what Decoder_Symbol_Wise (src/Decoder_Symbol_Wise.cpp) does at the relay
+(``symbol_wise_encode_1`` after ``push_current_codeword`` / ``rotate_pointers_and_insert_zero_word``,
+driven by Variable_Rate_FEC_Decoder::receive_message_and_symbol_wise_encode, :950-1601) and at the
+destination (``symbol_wise_decode_1`` + ``extract_data``, :1603-1879), batched over many packets
+of one relay stream held in HBM.
+"""
+from __future__ import annotations
+
+import ctypes
+
+from ._lib import check, lib
+
+
+def _ptr(t):
+    return ctypes.c_void_p(t.data_ptr()) if t is not None else None
+
+
+class SymbolWiseRelay:
+    """Fixed-rate SWDF chain: source (T1, N1, N1) -> relay -> destination with (T2, N2), where
+    k = T1-N1+1 = T2-N2+1 (the relay keeps the data symbols and changes the code length)."""
+
+    def __init__(self, max_payload: int, T1: int, N1: int, T2: int, N2: int):
+        h = ctypes.c_void_p()
+        check(lib().fec_swdf_create(max_payload, T1, N1, T2, N2, ctypes.byref(h)), "fec_swdf_create")
+        self._h = h
+        v = [ctypes.c_int() for _ in range(6)]
+        check(lib().fec_swdf_geometry(h, *[ctypes.byref(x) for x in v]), "fec_swdf_geometry")
+        self.k, self.n1, self.n2, self.S, self.frame_bytes, self.delay = (x.value for x in v)
+        self.L = max_payload
+        self._work = None
+
+    def __del__(self):
+        if getattr(self, "_h", None):
+            try:
+                lib().fec_swdf_destroy(self._h)
+            except Exception:
+                pass
+            self._h = None
+
+    def relay(self, codewords, erasure, frames=None, flag=None):
+        """symbol_wise_encode_1 for seqs 0..P-1: source codewords [P, >= S*n1] uint8 (zero-padded
+        rows) and hop-1 erasure flags [P] -> (frames [P, frame_bytes], flags [P] uint8)."""
+        import torch
+        assert codewords.dtype == torch.uint8 and codewords.is_cuda and codewords.is_contiguous()
+        assert codewords.dim() == 2 and codewords.shape[1] >= self.S * self.n1
+        P = codewords.shape[0]
+        assert erasure.dtype == torch.uint8 and erasure.is_cuda and erasure.is_contiguous() and erasure.numel() >= P
+        if frames is None:
+            frames = torch.empty((P, self.frame_bytes), dtype=torch.uint8, device=codewords.device)
+        assert frames.shape == (P, self.frame_bytes) and frames.is_contiguous() and frames.dtype == torch.uint8
+        if flag is None:
+            flag = torch.empty(P, dtype=torch.uint8, device=codewords.device)
+        assert flag.numel() >= P and flag.dtype == torch.uint8 and flag.is_contiguous()
+        nbytes = int(lib().fec_swdf_workspace_bytes(self._h, P))
+        if self._work is None or self._work.numel() < nbytes:
+            self._work = torch.empty(max(nbytes, 1), dtype=torch.uint8, device=codewords.device)
+        stream = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+        check(lib().fec_swdf_relay_batch(self._h, _ptr(codewords), codewords.shape[1], _ptr(erasure), P,
+                                         _ptr(frames), _ptr(flag), _ptr(self._work), self._work.numel(),
+                                         stream), "fec_swdf_relay_batch")
+        return frames, flag
+
+    def destination(self, frames, erasure, out=None, flag=None):
+        """symbol_wise_decode_1 + extract_data for seqs 0..P-1: relay frames [P, frame_bytes] and
+        hop-2 erasure flags [P] -> (data_with_header rows [P, S*k] (row t = source packet
+        t - delay), flags [P] uint8)."""
+        import torch
+        assert frames.dtype == torch.uint8 and frames.is_cuda and frames.is_contiguous()
+        assert frames.dim() == 2 and frames.shape[1] == self.frame_bytes
+        P = frames.shape[0]
+        assert erasure.dtype == torch.uint8 and erasure.is_cuda and erasure.is_contiguous() and erasure.numel() >= P
+        if out is None:
+            out = torch.empty((P, self.S * self.k), dtype=torch.uint8, device=frames.device)
+        assert out.shape == (P, self.S * self.k) and out.is_contiguous() and out.dtype == torch.uint8
+        if flag is None:
+            flag = torch.empty(P, dtype=torch.uint8, device=frames.device)
+        assert flag.numel() >= P and flag.dtype == torch.uint8 and flag.is_contiguous()
+        stream = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+        check(lib().fec_swdf_destination_batch(self._h, _ptr(frames), _ptr(erasure), P, _ptr(out), _ptr(flag),
+                                               stream), "fec_swdf_destination_batch")
+        return out, flag

@@ -205,6 +205,34 @@ int fec_vr_encode_batch(fec_vr_plan *plan, const uint8_t *d_payload, const int32
 int fec_vr_decode_batch(fec_vr_plan *plan, const uint8_t *d_cw_cur, const uint8_t *d_cw_old,
                         const uint8_t *d_erased, uint8_t *d_out, int32_t *d_out_len, void *hip_stream);
 
+/* ---- relay: symbol-wise decode-and-forward (SWDF, RELAYING_TYPE 2) ---------------------------
+ * Decoder_Symbol_Wise (src/Decoder_Symbol_Wise.cpp) as the relay and the destination drive it
+ * (src/Variable_Rate_FEC_Decoder.cpp:950-1601 relay, :1603-1879 destination; one relay frame per
+ * seq as with FLAG_FOR_CONSTANT_TRANS = 1, application_local_simulation.cpp:532-587), fixed rate.
+ * Hop 1 carries the source's FEC_Encoder(max_payload, T1, N1, N1) codewords; the relay decodes
+ * with window n1 = T1+1 and re-encodes for n2 = T2+1 with k = T1-N1+1 = T2-N2+1 (k2 == k, the
+ * only case the reference handles).  Batches run a fresh relay / destination over seqs 0..P-1.
+ *   fec_swdf_relay_batch: d_cw P rows of cw_stride bytes (the source codewords, zero-padded to at
+ *     least S*n1 bytes; rows of erased packets are never read), d_erasure P hop-1 flags ->
+ *     d_frames P rows of frame_bytes (the relay's transmitted frame: [size BE16][codeword_new_vector
+ *     [n2-1][0..size)], size = (S+1)*n2), d_flag P bytes (may be NULL): 1 when the window held too
+ *     many erasures to decode (the relay's loss counter).  d_work: fec_swdf_workspace_bytes(P).
+ *   fec_swdf_destination_batch: d_frames + d_erasure P hop-2 flags -> d_out P rows of S*k bytes:
+ *     row t = data_with_header ([len BE16][payload][zero pad]) of source packet t - delay, as
+ *     symbol_wise_decode_1 + extract_data produce it; d_flag as above (may be NULL). */
+typedef struct fec_swdf fec_swdf;
+int fec_swdf_create(int max_payload, int T1, int N1, int T2, int N2, fec_swdf **out);
+int fec_swdf_destroy(fec_swdf *swdf);
+/* delay = n1 + n2 - k - 1: destination row t carries source packet t - delay */
+int fec_swdf_geometry(const fec_swdf *swdf, int *k, int *n1, int *n2, int *S, int *frame_bytes,
+                      int *delay);
+size_t fec_swdf_workspace_bytes(const fec_swdf *swdf, int64_t P);
+int fec_swdf_relay_batch(fec_swdf *swdf, const uint8_t *d_cw, int64_t cw_stride, const uint8_t *d_erasure,
+                         int64_t P, uint8_t *d_frames, uint8_t *d_flag, void *d_work, size_t work_bytes,
+                         void *hip_stream);
+int fec_swdf_destination_batch(fec_swdf *swdf, const uint8_t *d_frames, const uint8_t *d_erasure, int64_t P,
+                               uint8_t *d_out, uint8_t *d_flag, void *hip_stream);
+
 /* ---- erasure patterns (inputs of the decode path; host only, no device needed) ---------------
  * Byte-exact restatements of Erasure_File_Generator (src/Erasure_File_Generator.cpp:25-287): out[i]
  * = 1 if packet i is erased.  Same engine (mt19937), same draw order and the same libstdc++

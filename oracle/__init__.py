@@ -64,6 +64,9 @@ def lib() -> ctypes.CDLL:
         L.or_encode_stream.restype = ctypes.c_int64
         L.or_encode_stream.argtypes = [ctypes.c_int] * 4 + [ctypes.c_int64, ctypes.c_int64,
                                        ctypes.c_uint64, u8p, ip]
+        L.or_swdf_run.restype = ctypes.c_int
+        L.or_swdf_run.argtypes = [ctypes.c_int] * 5 + [ctypes.c_int64, u8p, u8p, ctypes.c_uint64,
+                                                        u8p, u8p, u8p, u8p]
         _lib = L
     return _lib
 
@@ -216,3 +219,26 @@ def encode_stream(max_payload: int, T: int, B: int, N: int, seq0: int, P: int, s
                                    _u8(cw) if want_codewords else None,
                                    _i32(cw_len) if want_codewords else None)
     return dict(total=int(total), cw=cw, cw_len=cw_len)
+
+
+def swdf_run(max_payload: int, T1: int, N1: int, T2: int, N2: int, P: int, e1: np.ndarray,
+             e2: np.ndarray, seed: int = 0x5EED):
+    """The local simulation's SWDF chain (source FEC_Encoder -> hop 1 -> relay
+    Decoder_Symbol_Wise::symbol_wise_encode_1 -> hop 2 -> destination symbol_wise_decode_1 +
+    extract_data, one relay frame per seq): returns dict(frames [P, 2+(S+1)*n2], relay_flag [P],
+    dest_out [P, S*k] (data_with_header), dest_flag [P], delay = n1+n2-k-1)."""
+    k, n1, n2 = T1 - N1 + 1, T1 + 1, T2 + 1
+    S = -(-(max_payload + 2) // k)
+    F = 2 + (S + 1) * n2
+    a = np.ascontiguousarray(e1[:P], dtype=np.uint8)
+    b = np.ascontiguousarray(e2[:P], dtype=np.uint8)
+    assert a.size == P and b.size == P
+    frames = np.zeros((P, F), dtype=np.uint8)
+    rf = np.zeros(P, dtype=np.uint8)
+    out = np.zeros((P, S * k), dtype=np.uint8)
+    df = np.zeros(P, dtype=np.uint8)
+    st = lib().or_swdf_run(max_payload, T1, N1, T2, N2, P, _u8(a), _u8(b), seed, _u8(frames), _u8(rf),
+                           _u8(out), _u8(df))
+    if st != 0:
+        raise ValueError("unsupported SWDF configuration")
+    return dict(frames=frames, relay_flag=rf, dest_out=out, dest_flag=df, delay=n1 + n2 - k - 1, S=S, k=k)

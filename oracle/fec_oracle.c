@@ -552,3 +552,213 @@ int64_t or_encode_stream(int max_payload, int T, int B, int N, int64_t seq0, int
     or_encoder_free(e);
     return total;
 }
+
+/* ------------------------------------------------------------------------------------------ */
+/* Decoder_Symbol_Wise (src/Decoder_Symbol_Wise.cpp) -- the relay's symbol-wise decode-and-      */
+/* forward (SWDF, RELAYING_TYPE 2) and the destination's symbol-wise decode, kept in the         */
+/* reference's shape: windows of whole packets shifted by memcpy, one diagonal per code block    */
+/* pulled out of the window, decodeBlock(T = n-1, t = 0) / encodeBlock(t = k2-1) per block.      */
+/* Defined-away undefined behaviour:                                              */
+/*   - the erasure vector handed to decodeBlock is malloc(T_TOT) (relay, :561) or                 */
+/*     malloc(T_INITIAL) = 5 bytes (destination, :633) with only n-1 entries written and n read   */
+/*     (:571-573, :641-643): here it holds all n window flags;                                    */
+/*   - the block count is `ceil(max_payload / k) + 1` in integer arithmetic (:553, :632), which    */
+/*     differs from the codeword's S = ceil((max_payload+2)/k) sub-streams for some k (k = 1, 7,   */
+/*     ...): here it is S;                                                                         */
+/*   - push_current_codeword copies GLOBAL_MAX_SIZE_OF_CODEWORD bytes to offset 2 of a buffer of   */
+/*     that size (:136) and reads past the received packet: here the slot holds the packet        */
+/*     zero-padded (a trimmed wire codeword re-padded, as FEC_Decoder does);                      */
+/*   - k2 != k leaves stale symbols in the relay's data (:587-609): k2 == k is required.          */
+/* ------------------------------------------------------------------------------------------ */
+#define OR_SW_WIN 33
+#define OR_SW_SLOT 20000 /* GLOBAL_MAX_SIZE_OF_CODEWORD (FEC_Macro.h:49) */
+
+struct or_swdf {
+    int L, k, n, n2, S;
+    uint8_t *cv[OR_SW_WIN];  /* codeword_vector (received packet at offset 2) */
+    uint8_t *cnv[OR_SW_WIN]; /* codeword_new_vector (relay output, symbols at offset 2) */
+    uint8_t er[OR_SW_WIN];   /* temp_erasure_vector */
+    uint8_t G1[OR_MAXK * OR_MAXN]; /* decoder_current->getG(): Decoder(n-1, n-k, n-k) */
+    uint8_t G2[OR_MAXK * OR_MAXN]; /* encoder_current->getG(): Encoder(n2-1, n2-k2, n2-k2) */
+    uint8_t *cnsw;           /* codeword_new_symbol_wise */
+};
+
+or_swdf *or_swdf_new(int max_payload, int k, int n, int n2) {
+    or_gf_init();
+    if (k < 1 || n < k || n >= OR_SW_WIN || n2 < 0 || n2 >= OR_SW_WIN || (n2 > 0 && n2 < k)) return NULL;
+    or_swdf *s = (or_swdf *)calloc(1, sizeof(or_swdf));
+    s->L = max_payload;
+    s->k = k;
+    s->n = n;
+    s->n2 = n2;
+    s->S = or_ceil_div(max_payload + 2, k);
+    for (int i = 0; i < OR_SW_WIN; i++) {
+        s->cv[i] = (uint8_t *)calloc(OR_SW_SLOT, 1);
+        s->cnv[i] = (uint8_t *)calloc(OR_SW_SLOT, 1);
+    }
+    s->cnsw = (uint8_t *)calloc(30000, 1);
+    or_gen_G(s->G1, n - 1, n - k, n - k, k, n); /* Decoder_Symbol_Wise callers, e.g.           */
+    if (n2 > 0) or_gen_G(s->G2, n2 - 1, n2 - k, n2 - k, k, n2); /* Variable_Rate_FEC_Decoder.cpp:953-954 */
+    return s;
+}
+
+void or_swdf_free(or_swdf *s) {
+    if (!s) return;
+    for (int i = 0; i < OR_SW_WIN; i++) {
+        free(s->cv[i]);
+        free(s->cnv[i]);
+    }
+    free(s->cnsw);
+    free(s);
+}
+
+/* shift of the windows common to push_current_codeword (:119-135) and
+ * rotate_pointers_and_insert_zero_word (:142-171) */
+static void or_swdf_shift(or_swdf *s, int n, int n2) {
+    for (int i = 0; i < n - 1; i++) {
+        memcpy(s->cv[i], s->cv[i + 1], OR_SW_SLOT);
+        s->er[i] = s->er[i + 1];
+    }
+    for (int i = 0; i < n2 - 1; i++) memcpy(s->cnv[i], s->cnv[i + 1], OR_SW_SLOT);
+}
+
+/* push_current_codeword, Decoder_Symbol_Wise.cpp:119-140 */
+void or_swdf_push(or_swdf *s, const uint8_t *message, int size, int n, int n2) {
+    or_swdf_shift(s, n, n2);
+    memset(s->cv[n - 1], 0, OR_SW_SLOT);
+    if (size > OR_SW_SLOT - 2) size = OR_SW_SLOT - 2;
+    if (size > 0) memcpy(s->cv[n - 1] + 2, message, (size_t)size);
+    s->er[n - 1] = 0;
+}
+
+/* rotate_pointers_and_insert_zero_word, Decoder_Symbol_Wise.cpp:142-176 */
+void or_swdf_rotate(or_swdf *s, int n, int n2) {
+    or_swdf_shift(s, n, n2);
+    memset(s->cv[n - 1], 0, OR_SW_SLOT);
+    s->er[n - 1] = 1;
+}
+
+/* symbol_wise_encode_1, Decoder_Symbol_Wise.cpp:547-619.  Returns the flag (too many erasures in
+ * the window to decode). */
+int or_swdf_encode_1(or_swdf *s) {
+    const int k = s->k, n = s->n, k2 = s->k, n2 = s->n2;
+    int erasure_counter = 0;
+    for (int i = 0; i < n; i++) erasure_counter += s->er[i] == 1;
+    const int blocks = s->S;
+    uint8_t temp_codeword[OR_MAXN], temp_encoded_codeword[OR_MAXN], stam[OR_MAXN];
+    int flag = 0;
+    for (int j = 0; j < blocks; j++) {
+        for (int i = 0; i < n; i++) temp_codeword[i] = s->cv[i][2 + j * n + i]; /* diagonal, :564-568 */
+        if (erasure_counter > 0 && erasure_counter < n - k + 1) {           /* :570-573 */
+            for (int aa = 0; aa < n; aa++) stam[aa] = s->er[aa];
+            or_decode_block(temp_codeword, s->G1, temp_codeword, stam, k, n, n - 1, 0);
+        } else if (erasure_counter >= n - k + 1) {
+            flag = 1;
+        }
+        for (int i = 0; i < k; i++) s->cnsw[2 + j * n + i] = temp_codeword[k - 1 - i]; /* :577-578 */
+    }
+    /* encoding, :586-618 (k_min = k, delta_k = 0 since k2 == k) */
+    for (int j = 0; j < blocks; j++)
+        for (int i = 0; i < k; i++) s->cnv[n2 - 1][2 + j * n2 + i] = s->cnsw[2 + j * n + i];
+    for (int j = 0; j < blocks; j++) {
+        for (int delta = 0; delta < n2 - k2; delta++) {
+            for (int i = delta; i < k + delta; i++)
+                temp_codeword[i - delta] = s->cnv[i][2 + j * n2 + i - delta]; /* :603-605 */
+            memcpy(temp_encoded_codeword, temp_codeword, (size_t)k);
+            or_encode_block(temp_codeword, s->G2, temp_encoded_codeword, k2, n2, k2 - 1);
+            s->cnv[n2 - 1][2 + j * n2 + n2 - 1 - delta] = temp_encoded_codeword[n2 - 1 - delta];
+        }
+    }
+    return flag;
+}
+
+/* The relay's transmitted frame (Variable_Rate_FEC_Decoder.cpp:1482-1491, RELAYING_TYPE 2):
+ * [codeword_r_d_size BE16][codeword_new_vector[n2-1][0 .. codeword_r_d_size)] with
+ * codeword_r_d_size = (ceil((max_payload+2)/k2) + 1) * n2 (:998).  Returns the frame bytes. */
+int or_swdf_frame(const or_swdf *s, uint8_t *frame) {
+    const int size = (s->S + 1) * s->n2;
+    frame[0] = (uint8_t)(size / 256);
+    frame[1] = (uint8_t)size;
+    memcpy(frame + 2, s->cnv[s->n2 - 1], (size_t)size);
+    return size + 2;
+}
+
+/* symbol_wise_decode_1 (Decoder_Symbol_Wise.cpp:621-651) followed by extract_data (:653-665):
+ * out receives S*k bytes, the data_with_header the destination recovers.  Returns the flag. */
+int or_swdf_decode_1(or_swdf *s, uint8_t *out) {
+    const int k = s->k, n = s->n;
+    int erasure_counter = 0;
+    for (int i = 0; i < n; i++) erasure_counter += s->er[i] == 1;
+    uint8_t temp_codeword[OR_MAXN], stam[OR_MAXN];
+    uint8_t *buffer = (uint8_t *)calloc((size_t)s->S * n, 1);
+    int flag = 0;
+    for (int j = 0; j < s->S; j++) {
+        for (int i = 0; i < n; i++)
+            temp_codeword[n - 1 - i] = s->cv[n - 1 - i][4 + (j + 1) * n - 1 - i]; /* :636-639 */
+        if (erasure_counter > 0 && erasure_counter < n - k + 1) {
+            for (int aa = 0; aa < n; aa++) stam[aa] = s->er[aa];
+            or_decode_block(temp_codeword, s->G1, temp_codeword, stam, k, n, n - 1, 0);
+        } else if (erasure_counter >= n - k + 1) {
+            flag = 1;
+        }
+        for (int i = 0; i < n; i++) buffer[j * n + i] = temp_codeword[n - 1 - i]; /* :647-649 */
+    }
+    int ind = 0; /* extract_data, :653-661 */
+    for (int j = 0; j < s->S; j++)
+        for (int i = 0; i < k; i++) out[ind++] = buffer[j * n + n - k + i];
+    free(buffer);
+    return flag;
+}
+
+/* The local simulation's SWDF chain (application_local_simulation.cpp:532-587 with
+ * FLAG_FOR_CONSTANT_TRANS = 1, FEC_Macro.h:30: the relay handles every seq as it comes and sends
+ * one frame per seq): FEC_Encoder(L, T1, N1, N1) at the source, hop-1 erasures e1, the relay's
+ * Decoder_Symbol_Wise(n1 = T1+1, k = T1-N1+1) re-encoding for n2 = T2+1 (k2 = T2-N2+1 = k),
+ * hop-2 erasures e2, the destination's Decoder_Symbol_Wise(n2, k).  Outputs per seq t < P:
+ * frames (P x (2 + (S+1)*n2)), relay_flag, dest_out (P x S*k data_with_header), dest_flag.
+ * Returns 0, or -1 for an unsupported configuration. */
+int or_swdf_run(int max_payload, int T1, int N1, int T2, int N2, int64_t P, const uint8_t *e1,
+                const uint8_t *e2, uint64_t seed, uint8_t *frames, uint8_t *relay_flag,
+                uint8_t *dest_out, uint8_t *dest_flag) {
+    const int k = T1 - N1 + 1, n1 = T1 + 1, n2 = T2 + 1;
+    if (T2 - N2 + 1 != k) return -1;
+    or_encoder *src = or_encoder_new(max_payload, T1, N1, N1);
+    or_swdf *relay = or_swdf_new(max_payload, k, n1, n2);
+    or_swdf *dest = or_swdf_new(max_payload, k, n2, 0);
+    if (!src || !relay || !dest) {
+        or_encoder_free(src);
+        or_swdf_free(relay);
+        or_swdf_free(dest);
+        return -1;
+    }
+    int kk, nn, S, CW;
+    or_geometry(max_payload, T1, N1, N1, &kk, &nn, &S, &CW);
+    const int F = 2 + (S + 1) * n2;
+    uint8_t *payload = (uint8_t *)malloc((size_t)max_payload);
+    uint8_t *cw = (uint8_t *)malloc((size_t)CW);
+    uint8_t *frame = (uint8_t *)malloc((size_t)F);
+    for (int64_t t = 0; t < P; t++) {
+        or_fill_payload(payload, t, 1, max_payload, seed);
+        or_encoder_transmit(src, payload, max_payload, (int)t, cw);
+        if (e1[t]) or_swdf_rotate(relay, n1, n2);
+        else or_swdf_push(relay, cw, CW, n1, n2);
+        const int rf = or_swdf_encode_1(relay);
+        or_swdf_frame(relay, frame);
+        if (frames) memcpy(frames + t * F, frame, (size_t)F);
+        if (relay_flag) relay_flag[t] = (uint8_t)rf;
+        if (e2[t]) or_swdf_rotate(dest, n2, 0);
+        else or_swdf_push(dest, frame + 2, F - 2, n2, 0);
+        uint8_t *o = dest_out ? dest_out + t * (int64_t)S * k : NULL;
+        uint8_t *tmp = o ? o : (uint8_t *)malloc((size_t)S * k);
+        const int df = or_swdf_decode_1(dest, tmp);
+        if (!o) free(tmp);
+        if (dest_flag) dest_flag[t] = (uint8_t)df;
+    }
+    free(payload);
+    free(cw);
+    free(frame);
+    or_encoder_free(src);
+    or_swdf_free(relay);
+    or_swdf_free(dest);
+    return 0;
+}

@@ -67,6 +67,20 @@ int64_t or_run_stream(int max_payload, int T, int B, int N, int64_t P, const uin
 int64_t or_encode_stream(int max_payload, int T, int B, int N, int64_t seq0, int64_t P,
                          uint64_t seed, uint8_t *cw_out, int *cw_len);
 
+/* Decoder_Symbol_Wise (src/Decoder_Symbol_Wise.cpp): relay SWDF and destination symbol-wise
+ * decode, reference-structured (see fec_oracle.c for the defined-away undefined behaviour). */
+typedef struct or_swdf or_swdf;
+or_swdf *or_swdf_new(int max_payload, int k, int n, int n2);
+void or_swdf_free(or_swdf *s);
+void or_swdf_push(or_swdf *s, const uint8_t *message, int size, int n, int n2);
+void or_swdf_rotate(or_swdf *s, int n, int n2);
+int or_swdf_encode_1(or_swdf *s);
+int or_swdf_frame(const or_swdf *s, uint8_t *frame);
+int or_swdf_decode_1(or_swdf *s, uint8_t *out);
+int or_swdf_run(int max_payload, int T1, int N1, int T2, int N2, int64_t P, const uint8_t *e1,
+                const uint8_t *e2, uint64_t seed, uint8_t *frames, uint8_t *relay_flag,
+                uint8_t *dest_out, uint8_t *dest_flag);
+
 #ifdef __cplusplus
 }
 #endif

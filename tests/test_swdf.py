@@ -1,0 +1,115 @@
+"""Relay symbol-wise decode-and-forward (Decoder_Symbol_Wise, RELAYING_TYPE 2).
+
+CPU: the oracle's reference-structured SWDF chain (oracle/fec_oracle.c, or_swdf_*) delivers every
+source packet unchanged through relay and destination when the hops are clean or lightly erased,
+with the delay n1 + n2 - k - 1.  GPU: the HIP relay frames, relay flags, destination outputs and
+destination flags equal the oracle's per seq on the reference's shipped patterns.
+"""
+import numpy as np
+import pytest
+
+import oracle
+from conftest import load_pattern
+
+L = 300
+SEED = 0x5EED
+
+SWDF_CASES = [(10, 3, 10, 3), (10, 3, 9, 2), (10, 1, 12, 3), (10, 10, 10, 10), (10, 5, 8, 3), (6, 2, 10, 6)]
+
+
+
+def source_dwh(P, S, k):
+    src = oracle.fill_payload(0, P, L, SEED)
+    d = np.zeros((P, S * k), dtype=np.uint8)
+    d[:, 0] = L >> 8
+    d[:, 1] = L & 255
+    d[:, 2:2 + L] = src
+    return d
+
+
+@pytest.mark.parametrize("cfg", SWDF_CASES)
+def test_oracle_swdf_clean_hops_deliver_every_packet(cfg):
+    P = 160
+    z = np.zeros(P, dtype=np.uint8)
+    r = oracle.swdf_run(L, *cfg, P, z, z, seed=SEED)
+    D, S, k = r["delay"], r["S"], r["k"]
+    want = source_dwh(P, S, k)
+    assert (r["dest_out"][D:] == want[:P - D]).all()
+    assert r["relay_flag"].sum() == 0 and r["dest_flag"].sum() == 0
+
+
+def test_oracle_swdf_corrects_within_both_hops():
+    """(10,3) -> (10,3): erasures the per-diagonal MDS code corrects on each hop (at most N = 3 per
+    window of n = 11) leave the destination output unchanged."""
+    P = 400
+    e1 = np.zeros(P, dtype=np.uint8)
+    e2 = np.zeros(P, dtype=np.uint8)
+    e1[[40, 41, 42, 120, 200, 205]] = 1
+    e2[[60, 61, 150, 152, 154, 300]] = 1
+    r = oracle.swdf_run(L, 10, 3, 10, 3, P, e1, e2, seed=SEED)
+    want = source_dwh(P, r["S"], r["k"])
+    D = r["delay"]
+    assert (r["dest_out"][D:] == want[:P - D]).all()
+    e1[[44, 45]] = 1  # 5 erasures in one window: beyond the hop-1 code
+    r2 = oracle.swdf_run(L, 10, 3, 10, 3, P, e1, e2, seed=SEED)
+    assert r2["relay_flag"].sum() > 0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cfg", SWDF_CASES)
+def test_gpu_swdf_bit_exact_vs_oracle(cfg):
+    """Relay frames, relay flags, destination data_with_header rows and destination flags per seq,
+    against the oracle, with hop 1 = bin/erasure.bin and hop 2 = bin/erasure2.bin (the
+    reference's two shipped Fritchman recordings), windows chosen to contain bursts."""
+    torch = pytest.importorskip("torch")
+    import fec_erasure_code_unit_test_relay_amd as fec
+    from fec_erasure_code_unit_test_relay_amd.relay import SymbolWiseRelay
+    T1, N1, T2, N2 = cfg
+    P = 6000
+    e1 = load_pattern("bin_erasure")[3000:3000 + P].copy()
+    e2 = load_pattern("bin_erasure2")[9000:9000 + P].copy()
+    e1[[0, 1, 2, 3, 500, 501, 503, 505, 507]] = 1  # start-up and dense windows
+    e2[[5, 6, 900, 902, 904, 906]] = 1
+    ref = oracle.swdf_run(L, *cfg, P, e1, e2, seed=SEED)
+    assert ref["relay_flag"].sum() > 0 or ref["dest_flag"].sum() > 0 or cfg[1] >= 3
+    torch.cuda.set_device(0)
+    c = fec.Codec(L, T1, N1, N1)
+    cw, _ = c.encode(fec.fill_payload(0, P, L, SEED))
+    er1 = torch.from_numpy(e1).cuda()
+    idx = torch.nonzero(er1).flatten()  # the relay must never read an erased packet
+    cw[idx] = torch.randint(0, 256, (idx.numel(), c.CW), dtype=torch.uint8, device="cuda")
+    r = SymbolWiseRelay(L, *cfg)
+    assert r.delay == ref["delay"] and r.frame_bytes == ref["frames"].shape[1]
+    frames, rflag = r.relay(cw, er1)
+    er2 = torch.from_numpy(e2).cuda()
+    fr2 = frames.clone()
+    idx2 = torch.nonzero(er2).flatten()
+    fr2[idx2] = torch.randint(0, 256, (idx2.numel(), r.frame_bytes), dtype=torch.uint8, device="cuda")
+    out, dflag = r.destination(fr2, er2)
+    torch.cuda.synchronize()
+    assert (frames.cpu().numpy() == ref["frames"]).all()
+    assert (rflag.cpu().numpy() == ref["relay_flag"]).all()
+    assert (out.cpu().numpy() == ref["dest_out"]).all()
+    assert (dflag.cpu().numpy() == ref["dest_flag"]).all()
+
+
+@pytest.mark.gpu
+def test_gpu_swdf_large_batch_round_trip():
+    """1M packets through relay and destination on clean hops: every destination row equals the
+    source packet delay seqs earlier (size-independent property at BASELINE scale)."""
+    torch = pytest.importorskip("torch")
+    import fec_erasure_code_unit_test_relay_amd as fec
+    from fec_erasure_code_unit_test_relay_amd.relay import SymbolWiseRelay
+    P = 1_000_000
+    torch.cuda.set_device(0)
+    c = fec.Codec(L, 10, 3, 3)
+    payload = fec.fill_payload(0, P, L, SEED)
+    cw, _ = c.encode(payload)
+    z = torch.zeros(P, dtype=torch.uint8, device="cuda")
+    r = SymbolWiseRelay(L, 10, 3, 10, 3)
+    frames, rflag = r.relay(cw, z)
+    out, dflag = r.destination(frames, z)
+    D = r.delay
+    assert int(rflag.sum()) == 0 and int(dflag.sum()) == 0
+    assert torch.equal(out[D:, 2:2 + L], payload[:P - D])
+    assert bool((out[D:, 0] == (L >> 8)).all()) and bool((out[D:, 1] == (L & 255)).all())
