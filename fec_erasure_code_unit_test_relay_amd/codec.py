@@ -89,8 +89,9 @@ class Codec:
         check(lib().fec_codec_set_encode_path(self._h, code), "fec_codec_set_encode_path")
 
     def set_copy_path(self, path: str) -> None:
-        """'auto', 'generic' or 'fast' for the decoder's received-packet kernel."""
-        code = {"auto": 0, "generic": 1, "fast": 2}[path]
+        """'auto', 'generic', 'fast' (LDS tiles) or 'wave' (barrier-free) for the decoder's
+        received-packet kernel."""
+        code = {"auto": 0, "generic": 1, "fast": 2, "wave": 3}[path]
         check(lib().fec_codec_set_copy_path(self._h, code), "fec_codec_set_copy_path")
 
     def info(self) -> dict:
@@ -205,7 +206,8 @@ class Codec:
         return out, out_len
 
     def copy(self, codewords, erasure, out=None, out_len=None):
-        """Received packets only (independent of plan(); erased rows get length 0)."""
+        """Received packets' rows and lengths (independent of plan()); erased packets' rows are
+        written by recover()."""
         import torch
         P = codewords.shape[0]
         assert codewords.dtype == torch.uint8 and codewords.is_cuda
@@ -218,7 +220,7 @@ class Codec:
         return out, out_len
 
     def recover(self, codewords, out, out_len):
-        """Erased packets (after plan() and copy())."""
+        """Erased packets' rows and lengths: recovered bytes, or zeros and length 0 (after plan())."""
         import torch
         P = codewords.shape[0]
         assert codewords.dtype == torch.uint8 and codewords.is_cuda and codewords.is_contiguous()

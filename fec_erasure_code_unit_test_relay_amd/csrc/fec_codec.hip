@@ -60,9 +60,10 @@ struct fec_codec {
     int wave_lds = 0;                   // its dynamic LDS per workgroup
     int wave_pad = 0;                   // 1: per-sequence ring padding (LDS bank spread)
     int wave_cus = 0;                   // compute units of the device
-    const void* copy_fast = nullptr;  // specialised decode copy kernel
+    const void* copy_fast = nullptr;  // specialised decode copy kernel (LDS tiles)
     int copyf_tp = 0;
-    int copy_path = 0;           // 0 auto, 1 generic, 2 specialised
+    const void* copy_wave = nullptr;  // barrier-free decode copy (fec_copy_wave.hip)
+    int copy_path = 0;           // 0 auto, 1 generic, 2 specialised (LDS tiles), 3 wave
     int plan_path = 0;
     int dedup = 1;               // episode-shape deduplication in the planner
     uint64_t* d_stamps = nullptr;  // diagnostics: phase stamps of the next specialised launch
@@ -262,6 +263,12 @@ int codec_init(fec_codec* c, int max_payload, int T, int B, int N) {
         c->wave_cus = cus;
         if (c->wave_slots <= 0) c->wave_kernel = nullptr;
     }
+    {
+        int dev = 0, cus = 0;
+        HIP_TRY(hipGetDevice(&dev));
+        HIP_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+        if (!c->wave_cus) c->wave_cus = cus;
+    }
     if ((g.L & 3) == 0) c->copy_fast = fec::fec_copy_fast_kernel_for(g.k, g.n - g.k);
     // The copy stages its whole tile, converts, then stores (no overlap inside a workgroup), so
     // smaller tiles with more resident workgroups per CU overlap better: at (10,3,3) 32 packets
@@ -274,6 +281,7 @@ int codec_init(fec_codec* c, int max_payload, int T, int B, int N) {
                 break;
             }
     if (!c->copyf_tp) c->copy_fast = nullptr;
+    if ((g.L & 3) == 0 && (g.S + 3) / 4 <= 64) c->copy_wave = fec::fec_copy_wave_kernel_for(g.k, g.n - g.k);
     HIP_TRY(hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking));
     HIP_TRY(hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming));
     HIP_TRY(hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming));
@@ -609,11 +617,15 @@ int launch_plan(fec_codec* c, const uint8_t* d_er, int64_t P, void* d_ws, size_t
     HIP_TRY(hipGetLastError());
     hipLaunchKernelGGL(fec::fec_shape_fill_kernel, dim3(pgrid), dim3(64), 0, s, sa);
     HIP_TRY(hipGetLastError());
-    // packets with all k symbols recovered -> rec_list (timed with the plan)
-    hipLaunchKernelGGL(fec::fec_compact_kernel, dim3(256), dim3(256), 0, s, w.counters, w.erased,
-                       w.sym_ok, g.k, w.rec_list);
-    HIP_TRY(hipGetLastError());
     return c->end(stop, s);
+}
+
+// The barrier-free copy applies (it leaves erased packets' rows to fec_recover_kernel, which may
+// then run concurrently with it).
+bool copy_wave_ok(const fec_codec* c, const uint8_t* d_out, int64_t P) {
+    const Geometry& g = c->g;
+    return c->copy_wave && (c->copy_path == 0 || c->copy_path == 3) &&
+           (reinterpret_cast<uintptr_t>(d_out) & 3) == 0 && P * g.CW < (int64_t(1) << 31) - 64;
 }
 
 int launch_copy(fec_codec* c, const uint8_t* d_cw, const uint8_t* d_er, int64_t P, uint8_t* d_out,
@@ -621,6 +633,35 @@ int launch_copy(fec_codec* c, const uint8_t* d_cw, const uint8_t* d_er, int64_t 
     const Geometry& g = c->g;
     const int64_t Pout = P - g.T;
     if (Pout <= 0) return FEC_OK;
+    if (c->copy_path == 3 && !copy_wave_ok(c, d_out, P)) return FEC_ERR_ARG;
+    if (copy_wave_ok(c, d_out, P)) {
+        fec::CopyWaveArgs wa;
+        wa.cw = d_cw;
+        wa.er = d_er;
+        wa.out = d_out;
+        wa.out_len = d_outlen;
+        wa.P = P;
+        wa.Pout = Pout;
+        wa.cw_bytes = static_cast<int>(P * g.CW);
+        wa.out_bytes = static_cast<int>(std::min<int64_t>(Pout * g.L, 0x7fffffff));
+        wa.L = g.L;
+        wa.CW = g.CW;
+        wa.T = g.T;
+        wa.NS4 = c->ns4();
+        wa.SPW = 64 / wa.NS4;
+        wa.nsteps = (Pout + wa.SPW - 1) / wa.SPW;
+        // enough waves for every CU several times over, each a contiguous run of steps
+        const int64_t waves_max = static_cast<int64_t>(std::max(1, c->wave_cus)) * 32;
+        wa.steps_per_wave = std::max<int64_t>(1, (wa.nsteps + waves_max - 1) / waves_max);
+        if (const char* v = std::getenv("FEC_COPY_STEPS")) wa.steps_per_wave = std::max(1, std::atoi(v));
+        const int64_t waves = (wa.nsteps + wa.steps_per_wave - 1) / wa.steps_per_wave;
+        const int64_t blocks = (waves + 3) / 4;
+        hipEvent_t stop;
+        if (int st = c->begin(FEC_KERNEL_DEC_COPY, s, &stop)) return st;
+        void* args[] = {&wa};
+        HIP_TRY(hipLaunchKernel(c->copy_wave, dim3(static_cast<unsigned>(blocks)), dim3(256), args, 0, s));
+        return c->end(stop, s);
+    }
     const bool fast_ok = c->copy_fast && (reinterpret_cast<uintptr_t>(d_out) & 3) == 0;
     if (c->copy_path == 2 && !fast_ok) return FEC_ERR_ARG;
     if (fast_ok && c->copy_path != 1) {
@@ -683,7 +724,8 @@ int launch_recover(fec_codec* c, const uint8_t* d_cw, int64_t P, uint8_t* d_out,
     ra.P = P;
     ra.Pout = Pout;
     ra.counters = w.counters;
-    ra.rec_list = w.rec_list;
+    ra.erased = w.erased;
+    ra.sym_ok = w.sym_ok;
     ra.coef = w.coef;
     ra.gf = c->d_gf;
     ra.out = d_out;
@@ -709,9 +751,15 @@ int launch_decode(fec_codec* c, const uint8_t* d_cw, const uint8_t* d_er, int64_
     HIP_TRY(hipEventRecord(c->ev_fork, s));
     HIP_TRY(hipStreamWaitEvent(c->side, c->ev_fork, 0));
     if (int st = launch_plan(c, d_er, P, d_ws, ws_bytes, c->side)) return st;
+    // The barrier-free copy writes received rows only: the recovery (erased rows) then runs on
+    // the side stream right after the plan, concurrently with the copy.
+    const bool concurrent = copy_wave_ok(c, d_out, P);
+    if (concurrent)
+        if (int st = launch_recover(c, d_cw, P, d_out, d_outlen, d_ws, ws_bytes, c->side)) return st;
     HIP_TRY(hipEventRecord(c->ev_join, c->side));
     if (int st = launch_copy(c, d_cw, d_er, P, d_out, d_outlen, s)) return st;
     HIP_TRY(hipStreamWaitEvent(s, c->ev_join, 0));
+    if (concurrent) return FEC_OK;
     return launch_recover(c, d_cw, P, d_out, d_outlen, d_ws, ws_bytes, s);
 }
 
@@ -910,7 +958,9 @@ int fec_codec_info(const fec_codec* c, char* buf, size_t size) {
     else
         std::snprintf(enc, sizeof(enc), "fec_encode_kernel");
     char cpy[64];
-    if (c->copy_fast && c->copy_path != 1)
+    if (c->copy_wave && (c->copy_path == 0 || c->copy_path == 3))
+        std::snprintf(cpy, sizeof(cpy), "fec_copy_wave_kernel<%d, %d>", c->g.k, np);
+    else if (c->copy_fast && c->copy_path != 1)
         std::snprintf(cpy, sizeof(cpy), "fec_copy_fast_kernel<%d, %d>", c->g.k, np);
     else
         std::snprintf(cpy, sizeof(cpy), "fec_copy_kernel");
@@ -957,8 +1007,9 @@ int fec_codec_set_plan_path(fec_codec* c, int path) {
 }
 
 int fec_codec_set_copy_path(fec_codec* c, int path) {
-    if (!c || path < 0 || path > 2) return FEC_ERR_ARG;
+    if (!c || path < 0 || path > 3) return FEC_ERR_ARG;
     if (path == 2 && !c->copy_fast) return FEC_ERR_ARG;
+    if (path == 3 && !c->copy_wave) return FEC_ERR_ARG;
     c->copy_path = path;
     return FEC_OK;
 }

@@ -101,6 +101,21 @@ struct CopyFastArgs {
     uint64_t* stamps;           // diagnostics: per-workgroup phase timestamps (null = off)
 };
 
+// Barrier-free received-packet decode (fec_copy_wave.hip): lane = (packet, group of 4 sub-streams),
+// SPW = 64 / NS4 packets per wave step; erased packets are not touched.
+struct CopyWaveArgs {
+    const uint8_t* cw;          // P rows of CW bytes
+    const uint8_t* er;
+    uint8_t* out;               // Pout rows of L bytes (4-byte aligned, L % 4 == 0)
+    int32_t* out_len;
+    int64_t P, Pout;
+    int cw_bytes, out_bytes;    // P*CW, Pout*L (< 2^31: the launcher falls back otherwise)
+    int L, CW, T, NS4, SPW;
+    int64_t nsteps;             // ceil(Pout / SPW)
+    int64_t steps_per_wave;
+};
+const void* fec_copy_wave_kernel_for(int k, int np);
+
 // fec_copy_fast_kernel<k, n-k> for the instantiated pairs (fec_copy_fast.hip), else nullptr.
 const void* fec_copy_fast_kernel_for(int k, int np);
 // Specialised planner for (k, n-k), or nullptr (then fec_plan_kernel runs); its rule table is
@@ -158,8 +173,9 @@ struct ShapeArgs {
 struct RecArgs {
     const uint8_t* cw;
     int64_t P, Pout;
-    const int32_t* counters;       // [2] recovered packets
-    const int32_t* rec_list;
+    int32_t* counters;             // [1] erased outputs (in), [2] recovered packets (counted here)
+    const int32_t* erased;         // erased output packets (fec_scan_kernel)
+    const uint8_t* sym_ok;         // [P][k] from the planner
     const uint8_t* coef;
     const uint8_t* gf;
     uint8_t* out;

@@ -58,7 +58,10 @@ int fec_codec_info(const fec_codec *codec, char *buf, size_t size);
  * 3 = streaming (persistent) specialised kernel, 4 = wave-sequence kernel (FEC_ERR_ARG if
  * unavailable).  All produce identical bytes; the switch exists for tests and A/B timing. */
 int fec_codec_set_encode_path(fec_codec *codec, int path);
-/* The same switch for the decoder's received-packet copy kernel. */
+/* The same switch for the decoder's received-packet copy kernel: 0 automatic (the barrier-free
+ * wave kernel when one is compiled for (k, n-k), max_payload % 4 == 0 and the output is 4-byte
+ * aligned; it writes received packets' rows only, so fec_decode_batch then runs the recovery of
+ * erased packets concurrently with it), 1 generic, 2 LDS-tile specialised, 3 wave. */
 int fec_codec_set_copy_path(fec_codec *codec, int path);
 /* The same switch for the decoder's planner (per-episode block replay). */
 int fec_codec_set_plan_path(fec_codec *codec, int path);
@@ -100,8 +103,9 @@ int fec_decode_plan(fec_codec *codec, const uint8_t *d_erasure, int64_t P, void 
 int fec_decode_apply(fec_codec *codec, const uint8_t *d_codeword, const uint8_t *d_erasure,
                      int64_t P, uint8_t *d_payload_out, int32_t *d_payload_len, void *d_workspace,
                      size_t workspace_bytes, void *hip_stream);
-/* fec_decode_apply = fec_decode_copy (received packets; independent of the plan, may run
- * concurrently with it) followed by fec_decode_recover (erased packets; after the plan). */
+/* fec_decode_apply = fec_decode_copy (received packets' rows and lengths; independent of the plan,
+ * may run concurrently with it) followed by fec_decode_recover (erased packets' rows and lengths:
+ * recovered bytes, or zeros and length 0 when lost; after the plan). */
 int fec_decode_copy(fec_codec *codec, const uint8_t *d_codeword, const uint8_t *d_erasure,
                     int64_t P, uint8_t *d_payload_out, int32_t *d_payload_len, void *hip_stream);
 int fec_decode_recover(fec_codec *codec, const uint8_t *d_codeword, int64_t P,

@@ -160,8 +160,11 @@ def gpu_round_trip(T, B, N, pattern, P, garbage=True, path="auto", dedup=True):
     path: kernel selection of the decoder's copy and planner ('auto' or 'generic');
     dedup: planner replays one episode per loss shape (True) or every episode."""
     c = fec.Codec(L, T, B, N)
-    c.set_copy_path(path)
-    c.set_plan_path(path)
+    try:
+        c.set_copy_path(path)
+        c.set_plan_path(path)
+    except fec.FecError:
+        pytest.skip(f"no {path} kernel for {(T, B, N)}")
     c.set_episode_dedup(dedup)
     Pf = P + T
     pat = np.zeros(Pf, dtype=np.uint8)
@@ -188,7 +191,7 @@ DEC_CASES = [((10, 5, 2), "bin_erasure", 0, 8000), ((10, 3, 3), "bin_erasure", 0
              ((10, 4, 4), "bin_erasure", 2000, 6000), ((10, 5, 5), "erasure80", 0, 4000)]
 
 
-@pytest.mark.parametrize("path,dedup", [("generic", False), ("auto", False), ("auto", True)])
+@pytest.mark.parametrize("path,dedup", [("generic", False), ("fast", True), ("auto", False), ("auto", True)])
 @pytest.mark.parametrize("tbn,pattern,start,P", DEC_CASES)
 def test_decode_bit_exact_vs_oracle(tbn, pattern, start, P, path, dedup):
     T, B, N = tbn
@@ -222,11 +225,12 @@ def test_copy_fast_variable_lengths_and_sizes():
             if t >= T:
                 want.append(out)
                 want_len.append(p)
-        c = fec.Codec(Lx, T, B, N)
-        c.set_copy_path("fast")
-        out, ln = c.decode(torch.from_numpy(np.stack(cws)).cuda(), torch.from_numpy(pat).cuda())
-        assert (ln.cpu().numpy() == np.array(want_len)).all(), (Lx, tbn)
-        assert (out.cpu().numpy() == np.stack(want)).all(), (Lx, tbn)
+        for cpath in ("fast", "wave"):
+            c = fec.Codec(Lx, T, B, N)
+            c.set_copy_path(cpath)
+            out, ln = c.decode(torch.from_numpy(np.stack(cws)).cuda(), torch.from_numpy(pat).cuda())
+            assert (ln.cpu().numpy() == np.array(want_len)).all(), (Lx, tbn, cpath)
+            assert (out.cpu().numpy() == np.stack(want)).all(), (Lx, tbn, cpath)
 
 
 def test_decode_startup_and_dense_erasures():
