@@ -227,7 +227,11 @@ def test_copy_fast_variable_lengths_and_sizes():
                 want_len.append(p)
         for cpath in ("fast", "wave"):
             c = fec.Codec(Lx, T, B, N)
-            c.set_copy_path(cpath)
+            try:
+                c.set_copy_path(cpath)
+            except fec.FecError:
+                assert cpath == "wave" and c.S > 4 * 64  # one wave holds at most 64 groups
+                continue
             out, ln = c.decode(torch.from_numpy(np.stack(cws)).cuda(), torch.from_numpy(pat).cuda())
             assert (ln.cpu().numpy() == np.array(want_len)).all(), (Lx, tbn, cpath)
             assert (out.cpu().numpy() == np.stack(want)).all(), (Lx, tbn, cpath)
