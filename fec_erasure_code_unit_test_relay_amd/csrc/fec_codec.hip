@@ -281,7 +281,8 @@ int codec_init(fec_codec* c, int max_payload, int T, int B, int N) {
                 break;
             }
     if (!c->copyf_tp) c->copy_fast = nullptr;
-    if ((g.L & 3) == 0 && (g.S + 3) / 4 <= 64) c->copy_wave = fec::fec_copy_wave_kernel_for(g.k, g.n - g.k);
+    if ((g.L & 3) == 0 && (g.S + 3) / 4 <= 64 && g.T < 4 * ((g.S + 3) / 4))
+        c->copy_wave = fec::fec_copy_wave_kernel_for(g.k, g.n - g.k);
     HIP_TRY(hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking));
     HIP_TRY(hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming));
     HIP_TRY(hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming));
@@ -625,7 +626,8 @@ int launch_plan(fec_codec* c, const uint8_t* d_er, int64_t P, void* d_ws, size_t
 bool copy_wave_ok(const fec_codec* c, const uint8_t* d_out, int64_t P) {
     const Geometry& g = c->g;
     return c->copy_wave && (c->copy_path == 0 || c->copy_path == 3) &&
-           (reinterpret_cast<uintptr_t>(d_out) & 3) == 0 && P * g.CW < (int64_t(1) << 31) - 64;
+           (reinterpret_cast<uintptr_t>(d_out) & 3) == 0 && P * g.CW < (int64_t(1) << 31) - 64 &&
+           g.T < 4 * c->ns4();
 }
 
 int launch_copy(fec_codec* c, const uint8_t* d_cw, const uint8_t* d_er, int64_t P, uint8_t* d_out,
@@ -644,14 +646,18 @@ int launch_copy(fec_codec* c, const uint8_t* d_cw, const uint8_t* d_er, int64_t 
         wa.Pout = Pout;
         wa.cw_bytes = static_cast<int>(P * g.CW);
         wa.out_bytes = static_cast<int>(std::min<int64_t>(Pout * g.L, 0x7fffffff));
+        wa.er_bytes = static_cast<int>(P);
         wa.L = g.L;
         wa.CW = g.CW;
         wa.T = g.T;
         wa.NS4 = c->ns4();
         wa.SPW = 64 / wa.NS4;
         wa.nsteps = (Pout + wa.SPW - 1) / wa.SPW;
-        // enough waves for every CU several times over, each a contiguous run of steps
-        const int64_t waves_max = static_cast<int64_t>(std::max(1, c->wave_cus)) * 32;
+        // 16 waves per CU (half the resident capacity: the planner chain and the recovery run
+        // beside it on the side stream), each a contiguous run of steps
+        int wpc = 16;
+        if (const char* v = std::getenv("FEC_COPY_WPC")) wpc = std::max(1, std::atoi(v));
+        const int64_t waves_max = static_cast<int64_t>(std::max(1, c->wave_cus)) * wpc;
         wa.steps_per_wave = std::max<int64_t>(1, (wa.nsteps + waves_max - 1) / waves_max);
         if (const char* v = std::getenv("FEC_COPY_STEPS")) wa.steps_per_wave = std::max(1, std::atoi(v));
         const int64_t waves = (wa.nsteps + wa.steps_per_wave - 1) / wa.steps_per_wave;

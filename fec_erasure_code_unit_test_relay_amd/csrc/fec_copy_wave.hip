@@ -106,11 +106,24 @@ __global__ __launch_bounds__(256) void fec_copy_wave_kernel(CopyWaveArgs a) {
     const int right = (g + 1 < NS4) ? lane + 1 : lane;  // the next group of the same packet
     const uint64_t pmask = ((NS4 >= 64) ? ~0ull : ((1ull << NS4) - 1ull)) << (p < SPW ? p * NS4 : 0);
 
+    // Everything a step needs from memory -- the codeword words and the erasure flags x..x+T (4
+    // per lane at most: T < 4*NS4, host check) -- is loaded one step ahead: vmcnt waits are in
+    // issue order, so a load issued after the prefetch would wait for the prefetch too.
+    const __amdgpu_buffer_rsrc_t re = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(a.er), 0, a.er_bytes, 0x00020000);
     uint32_t D[n + 1];
+    uint32_t E[4];
     auto issue = [&](int64_t step) __attribute__((always_inline)) {
         const int64_t x = step * SPW + p;
         const int o = static_cast<int>(x * CW) + 4 * n * g;
         load_words<n + 1>(D, rs, o & ~3);
+        const bool pv = live_lane && x < a.Pout;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int d = g + j * NS4;
+            // past T (or an invalid lane): an offset beyond the resource, which reads as zero
+            const int eo = (pv && d <= T) ? static_cast<int>(x) + d : a.er_bytes;
+            E[j] = __builtin_amdgcn_raw_buffer_load_b8(re, eo, 0, 0);
+        }
     };
     issue(step0);
     for (int64_t step = step0; step < step_end; ++step) {
@@ -120,17 +133,10 @@ __global__ __launch_bounds__(256) void fec_copy_wave_kernel(CopyWaveArgs a) {
         uint32_t S[n];
 #pragma unroll
         for (int m = 0; m < n; ++m) S[m] = __builtin_amdgcn_alignbyte(D[m + 1], D[m], sh);
-        if (step + 1 < step_end) issue(step + 1);
-
         // erasure flags x..x+T of the packet, spread over its lanes; x+T < P for x < Pout
-        bool own = false, any = false;
-        if (valid) {
-            for (int d = g; d <= T; d += NS4) {
-                const bool e = a.er[x + d] != 0;
-                any = any || e;
-                if (d == 0) own = e;
-            }
-        }
+        const bool own = g == 0 && E[0] != 0;
+        const bool any = (E[0] | E[1] | E[2] | E[3]) != 0;
+        if (step + 1 < step_end) issue(step + 1);
         const uint64_t bal_any = __ballot(any);
         const uint64_t bal_own = __ballot(own);
         const bool erased = (bal_own & pmask) != 0;

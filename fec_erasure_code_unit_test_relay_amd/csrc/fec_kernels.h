@@ -102,7 +102,7 @@ struct CopyFastArgs {
 };
 
 // Barrier-free received-packet decode (fec_copy_wave.hip): lane = (packet, group of 4 sub-streams),
-// SPW = 64 / NS4 packets per wave step; erased packets are not touched.
+// SPW = 64 / NS4 packets per wave step; erased packets are not touched.  Needs T < 4*NS4.
 struct CopyWaveArgs {
     const uint8_t* cw;          // P rows of CW bytes
     const uint8_t* er;
@@ -110,6 +110,7 @@ struct CopyWaveArgs {
     int32_t* out_len;
     int64_t P, Pout;
     int cw_bytes, out_bytes;    // P*CW, Pout*L (< 2^31: the launcher falls back otherwise)
+    int er_bytes;               // P
     int L, CW, T, NS4, SPW;
     int64_t nsteps;             // ceil(Pout / SPW)
     int64_t steps_per_wave;
