@@ -625,9 +625,19 @@ int launch_plan(fec_codec* c, const uint8_t* d_er, int64_t P, void* d_ws, size_t
 // then run concurrently with it).
 bool copy_wave_ok(const fec_codec* c, const uint8_t* d_out, int64_t P) {
     const Geometry& g = c->g;
-    return c->copy_wave && (c->copy_path == 0 || c->copy_path == 3) &&
+    return c->copy_wave && c->copy_path == 3 &&
            (reinterpret_cast<uintptr_t>(d_out) & 3) == 0 && P * g.CW < (int64_t(1) << 31) - 64 &&
            g.T < 4 * c->ns4();
+}
+
+bool copy_fast_ok(const fec_codec* c, const uint8_t* d_out) {
+    return c->copy_fast && (c->copy_path == 0 || c->copy_path == 2) && (reinterpret_cast<uintptr_t>(d_out) & 3) == 0;
+}
+
+// The copy kernel in use writes received packets' rows only (erased ones are left to the
+// recovery, which can then run concurrently with it).
+bool copy_skips_erased(const fec_codec* c, const uint8_t* d_out, int64_t P) {
+    return copy_wave_ok(c, d_out, P) || copy_fast_ok(c, d_out);
 }
 
 int launch_copy(fec_codec* c, const uint8_t* d_cw, const uint8_t* d_er, int64_t P, uint8_t* d_out,
@@ -686,6 +696,7 @@ int launch_copy(fec_codec* c, const uint8_t* d_cw, const uint8_t* d_er, int64_t 
         fa.raw_bytes = c->copyf_raw(fa.TP);
         fa.out_bytes = round16(fa.TP * g.L);
         fa.stamps = (c->stamp_kernel == FEC_KERNEL_DEC_COPY) ? c->d_stamps : nullptr;
+        fa.skip_erased = 1;
         const int64_t blocks = (Pout + fa.TP - 1) / fa.TP;
         hipEvent_t stop;
         if (int st = c->begin(FEC_KERNEL_DEC_COPY, s, &stop)) return st;
@@ -732,6 +743,7 @@ int launch_recover(fec_codec* c, const uint8_t* d_cw, int64_t P, uint8_t* d_out,
     ra.counters = w.counters;
     ra.erased = w.erased;
     ra.sym_ok = w.sym_ok;
+    ra.zero_lost = copy_skips_erased(c, d_out, P) ? 1 : 0;
     ra.coef = w.coef;
     ra.gf = c->d_gf;
     ra.out = d_out;
@@ -759,7 +771,8 @@ int launch_decode(fec_codec* c, const uint8_t* d_cw, const uint8_t* d_er, int64_
     if (int st = launch_plan(c, d_er, P, d_ws, ws_bytes, c->side)) return st;
     // The barrier-free copy writes received rows only: the recovery (erased rows) then runs on
     // the side stream right after the plan, concurrently with the copy.
-    const bool concurrent = copy_wave_ok(c, d_out, P);
+    bool concurrent = copy_skips_erased(c, d_out, P);
+    if (const char* v = std::getenv("FEC_RECOVER_SERIAL")) concurrent = concurrent && !std::atoi(v);
     if (concurrent)
         if (int st = launch_recover(c, d_cw, P, d_out, d_outlen, d_ws, ws_bytes, c->side)) return st;
     HIP_TRY(hipEventRecord(c->ev_join, c->side));
@@ -964,7 +977,7 @@ int fec_codec_info(const fec_codec* c, char* buf, size_t size) {
     else
         std::snprintf(enc, sizeof(enc), "fec_encode_kernel");
     char cpy[64];
-    if (c->copy_wave && (c->copy_path == 0 || c->copy_path == 3))
+    if (c->copy_wave && c->copy_path == 3)
         std::snprintf(cpy, sizeof(cpy), "fec_copy_wave_kernel<%d, %d>", c->g.k, np);
     else if (c->copy_fast && c->copy_path != 1)
         std::snprintf(cpy, sizeof(cpy), "fec_copy_fast_kernel<%d, %d>", c->g.k, np);

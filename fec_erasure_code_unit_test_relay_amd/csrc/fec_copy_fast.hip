@@ -46,7 +46,7 @@ __global__ __launch_bounds__(256) void fec_copy_fast_kernel(CopyFastArgs a) {
             copy = min(ln, L);
         }
         clen[t] = copy;
-        a.out_len[x0 + t] = ln;
+        if (!(a.skip_erased && erw[t])) a.out_len[x0 + t] = ln;
     }
     __syncthreads();
 
@@ -99,14 +99,27 @@ __global__ __launch_bounds__(256) void fec_copy_fast_kernel(CopyFastArgs a) {
     __syncthreads();
     phase_stamp(a.stamps, blockIdx.x, 2);
 
+    // With skip_erased the rows of erased packets are left to fec_recover_kernel (running
+    // concurrently): a chunk touching one goes out dword by dword (L % 4 == 0: a dword never
+    // straddles two rows).
     const int obytes = ntile * L;
     uint8_t* dst = a.out + x0 * L;
+    const bool skip = a.skip_erased != 0;
     if ((obytes & 15) == 0 && (reinterpret_cast<uintptr_t>(dst) & 15) == 0) {
-        for (int o = tid * 16; o < obytes; o += 256 * 16)
-            *reinterpret_cast<uint4*>(dst + o) = *reinterpret_cast<const uint4*>(xo + o);
+        for (int o = tid * 16; o < obytes; o += 256 * 16) {
+            if (!skip || (!erw[o / L] && !erw[(o + 15) / L])) {
+                *reinterpret_cast<uint4*>(dst + o) = *reinterpret_cast<const uint4*>(xo + o);
+            } else {
+#pragma unroll
+                for (int q = 0; q < 16; q += 4)
+                    if (!erw[(o + q) / L])
+                        *reinterpret_cast<uint32_t*>(dst + o + q) = *reinterpret_cast<const uint32_t*>(xo + o + q);
+            }
+        }
     } else {
         for (int o = tid * 4; o < obytes; o += 256 * 4)
-            *reinterpret_cast<uint32_t*>(dst + o) = *reinterpret_cast<const uint32_t*>(xo + o);
+            if (!skip || !erw[o / L])
+                *reinterpret_cast<uint32_t*>(dst + o) = *reinterpret_cast<const uint32_t*>(xo + o);
     }
     phase_stamp(a.stamps, blockIdx.x, 3);
 }

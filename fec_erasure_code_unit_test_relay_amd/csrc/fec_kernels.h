@@ -99,6 +99,7 @@ struct CopyFastArgs {
     int raw_bytes;              // codeword tile + slack (16-aligned)
     int out_bytes;              // payload tile (16-aligned)
     uint64_t* stamps;           // diagnostics: per-workgroup phase timestamps (null = off)
+    int skip_erased;            // 1: leave erased packets' rows and lengths to fec_recover_kernel
 };
 
 // Barrier-free received-packet decode (fec_copy_wave.hip): lane = (packet, group of 4 sub-streams),
@@ -177,6 +178,7 @@ struct RecArgs {
     int32_t* counters;             // [1] erased outputs (in), [2] recovered packets (counted here)
     const int32_t* erased;         // erased output packets (fec_scan_kernel)
     const uint8_t* sym_ok;         // [P][k] from the planner
+    int zero_lost;                 // 1: write lost packets' rows (zeros) and lengths (0) too
     const uint8_t* coef;
     const uint8_t* gf;
     uint8_t* out;

@@ -482,8 +482,10 @@ __global__ __launch_bounds__(256) void fec_recover_kernel(RecArgs a) {
         bool ok = true;
         for (int i = 0; i < k; ++i) ok = ok && a.sym_ok[x * k + i];
         if (!ok) {  // lost: payload 0 (FEC_Decoder returns no data), zero row
-            for (int b = lane; b < L; b += 64) a.out[x * L + b] = 0;
-            if (lane == 0) a.out_len[x] = 0;
+            if (a.zero_lost) {
+                for (int b = lane; b < L; b += 64) a.out[x * L + b] = 0;
+                if (lane == 0) a.out_len[x] = 0;
+            }
             continue;
         }
         if (lane == 0) atomicAdd(const_cast<int32_t*>(&a.counters[2]), 1);

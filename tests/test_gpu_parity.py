@@ -157,12 +157,13 @@ def test_encode_variable_lengths_and_history(tbn, path):
 
 def gpu_round_trip(T, B, N, pattern, P, garbage=True, path="auto", dedup=True):
     """GPU encode of packets 0..P+T-1, erase, GPU decode -> outputs for packets 0..P-1.
-    path: kernel selection of the decoder's copy and planner ('auto' or 'generic');
+    path: kernel selection of the decoder's copy and planner ('auto', 'generic' or 'wave' =
+    the barrier-free copy);
     dedup: planner replays one episode per loss shape (True) or every episode."""
     c = fec.Codec(L, T, B, N)
     try:
         c.set_copy_path(path)
-        c.set_plan_path(path)
+        c.set_plan_path("auto" if path == "wave" else path)
     except fec.FecError:
         pytest.skip(f"no {path} kernel for {(T, B, N)}")
     c.set_episode_dedup(dedup)
@@ -191,7 +192,7 @@ DEC_CASES = [((10, 5, 2), "bin_erasure", 0, 8000), ((10, 3, 3), "bin_erasure", 0
              ((10, 4, 4), "bin_erasure", 2000, 6000), ((10, 5, 5), "erasure80", 0, 4000)]
 
 
-@pytest.mark.parametrize("path,dedup", [("generic", False), ("fast", True), ("auto", False), ("auto", True)])
+@pytest.mark.parametrize("path,dedup", [("generic", False), ("wave", True), ("auto", False), ("auto", True)])
 @pytest.mark.parametrize("tbn,pattern,start,P", DEC_CASES)
 def test_decode_bit_exact_vs_oracle(tbn, pattern, start, P, path, dedup):
     T, B, N = tbn
