@@ -630,14 +630,13 @@ bool copy_wave_ok(const fec_codec* c, const uint8_t* d_out, int64_t P) {
            g.T < 4 * c->ns4();
 }
 
-bool copy_fast_ok(const fec_codec* c, const uint8_t* d_out) {
-    return c->copy_fast && (c->copy_path == 0 || c->copy_path == 2) && (reinterpret_cast<uintptr_t>(d_out) & 3) == 0;
-}
-
 // The copy kernel in use writes received packets' rows only (erased ones are left to the
-// recovery, which can then run concurrently with it).
+// recovery, which can then run concurrently with it).  Measured at (10,3,3), 1M packets
+// (profiles/r02/r02e_*): letting the LDS-tile copy skip erased rows and running the recovery beside
+// it made the step slower (0.450 vs 0.416 ms; copy 181 vs 157 us, recovery 89 vs 20 us), so only
+// the wave copy (copy path 3) does it.
 bool copy_skips_erased(const fec_codec* c, const uint8_t* d_out, int64_t P) {
-    return copy_wave_ok(c, d_out, P) || copy_fast_ok(c, d_out);
+    return copy_wave_ok(c, d_out, P);
 }
 
 int launch_copy(fec_codec* c, const uint8_t* d_cw, const uint8_t* d_er, int64_t P, uint8_t* d_out,
@@ -696,7 +695,7 @@ int launch_copy(fec_codec* c, const uint8_t* d_cw, const uint8_t* d_er, int64_t 
         fa.raw_bytes = c->copyf_raw(fa.TP);
         fa.out_bytes = round16(fa.TP * g.L);
         fa.stamps = (c->stamp_kernel == FEC_KERNEL_DEC_COPY) ? c->d_stamps : nullptr;
-        fa.skip_erased = 1;
+        fa.skip_erased = 0;
         const int64_t blocks = (Pout + fa.TP - 1) / fa.TP;
         hipEvent_t stop;
         if (int st = c->begin(FEC_KERNEL_DEC_COPY, s, &stop)) return st;
