@@ -38,7 +38,7 @@ struct EventPair {
 struct fec_codec {
     Geometry g;
     std::vector<uint8_t> G;
-    fec::DecodeRules rules;
+    std::shared_ptr<const fec::DecodeRules> rules;  // process-wide cache (shared_decode_rules)
     uint32_t* d_ptab = nullptr;  // [k][n-k][8]
     uint8_t* d_rules = nullptr;
     int64_t* d_wbase = nullptr;  // [n+1]
@@ -134,7 +134,7 @@ int codec_init(fec_codec* c, int max_payload, int T, int B, int N) {
     const Geometry& g = c->g;
     if (g.L > kMaxPayload || g.B < g.N || g.n > fec::kMaxRuleN) return FEC_ERR_ARG;
     c->G = fec::make_generator(T, B, N);
-    c->rules.build(c->G, g.k, g.n, g.T);
+    c->rules = fec::shared_decode_rules(T, B, N);
     const fec::Field& F = fec::field();
 
     // Per parity coefficient: the three register tables of gf_mul4 plus a non-zero flag.
@@ -158,19 +158,19 @@ int codec_init(fec_codec* c, int max_payload, int T, int B, int N) {
         }
     HIP_TRY(hipMalloc(&c->d_ptab, ptab.size() * 4));
     HIP_TRY(hipMemcpy(c->d_ptab, ptab.data(), ptab.size() * 4, hipMemcpyHostToDevice));
-    HIP_TRY(hipMalloc(&c->d_rules, std::max<size_t>(16, c->rules.table.size())));
-    HIP_TRY(hipMemcpy(c->d_rules, c->rules.table.data(), c->rules.table.size(), hipMemcpyHostToDevice));
+    HIP_TRY(hipMalloc(&c->d_rules, std::max<size_t>(16, c->rules->table.size())));
+    HIP_TRY(hipMemcpy(c->d_rules, c->rules->table.data(), c->rules->table.size(), hipMemcpyHostToDevice));
     c->plan_fast = fec::fec_plan_fast_kernel_for(g.k, g.n - g.k);
     if (c->plan_fast) {
         // sel bytes unchanged; coefficient bytes (and padding) -> log2, 0 -> 0xff
-        std::vector<uint8_t> lt(c->rules.table);
-        const int ES = c->rules.entry_bytes;
+        std::vector<uint8_t> lt(c->rules->table);
+        const int ES = c->rules->entry_bytes;
         for (size_t e = 0; e + ES <= lt.size(); e += ES)
             for (int o = g.k; o < ES; ++o) lt[e + o] = lt[e + o] ? F.log[lt[e + o]] : 0xff;
         HIP_TRY(hipMalloc(&c->d_rules_log, std::max<size_t>(16, lt.size())));
         HIP_TRY(hipMemcpy(c->d_rules_log, lt.data(), lt.size(), hipMemcpyHostToDevice));
     }
-    std::vector<int64_t> wb(c->rules.w_base.begin(), c->rules.w_base.end());
+    std::vector<int64_t> wb(c->rules->w_base.begin(), c->rules->w_base.end());
     HIP_TRY(hipMalloc(&c->d_wbase, wb.size() * 8));
     HIP_TRY(hipMemcpy(c->d_wbase, wb.data(), wb.size() * 8, hipMemcpyHostToDevice));
     uint8_t gf[768];
@@ -180,7 +180,7 @@ int codec_init(fec_codec* c, int max_payload, int T, int B, int N) {
     HIP_TRY(hipMemcpy(c->d_gf, gf, 768, hipMemcpyHostToDevice));
     HIP_TRY(hipMalloc(&c->d_G, c->G.size()));
     HIP_TRY(hipMemcpy(c->d_G, c->G.data(), c->G.size(), hipMemcpyHostToDevice));
-    const std::vector<uint8_t> rst = fec::build_resync_states(g, c->rules);
+    const std::vector<uint8_t> rst = fec::build_resync_states(g, *c->rules);
     HIP_TRY(hipMalloc(&c->d_rstate, rst.size()));
     HIP_TRY(hipMemcpy(c->d_rstate, rst.data(), rst.size(), hipMemcpyHostToDevice));
 
@@ -590,9 +590,9 @@ int launch_plan(fec_codec* c, const uint8_t* d_er, int64_t P, void* d_ws, size_t
     pa.Pout = Pout;
     pa.rules = c->d_rules;
     for (int i = 0; i <= fec::kPlanMaxN; ++i)
-        pa.wbase[i] = (i < static_cast<int>(c->rules.w_base.size())) ? c->rules.w_base[i] : -1;
+        pa.wbase[i] = (i < static_cast<int>(c->rules->w_base.size())) ? c->rules->w_base[i] : -1;
     pa.gf = c->d_gf;
-    pa.ES = c->rules.entry_bytes;
+    pa.ES = c->rules->entry_bytes;
     pa.k = g.k;
     pa.n = g.n;
     pa.T = g.T;
@@ -1148,7 +1148,7 @@ int fec_decoder_create(int max_payload, int T, int B, int N, fec_decoder** out) 
         d->codec.reset(c);
         const Geometry& g = c->g;
         if (g.T + g.k > fec_decoder::RR) return FEC_ERR_ARG;
-        d->planner.reset(new fec::StreamPlanner(g, &c->rules));
+        d->planner.reset(new fec::StreamPlanner(g, c->rules.get()));
         d->res_len_off = (g.L + 3) & ~3;
         HIP_TRY(hipStreamCreateWithFlags(&d->s, hipStreamNonBlocking));
         HIP_TRY(hipMalloc(&d->d_ring, static_cast<size_t>(fec_decoder::RR) * g.CW));
@@ -1245,9 +1245,8 @@ int fec_plan_host(int max_payload, int T, int B, int N, const uint8_t* erasure, 
     return guarded([&] {
         const Geometry g = Geometry::make(max_payload, T, B, N);
         if (g.B < g.N || g.n > fec::kMaxRuleN) return FEC_ERR_ARG;
-        fec::DecodeRules rules;
-        rules.build(fec::make_generator(T, B, N), g.k, g.n, g.T);
-        fec::StreamPlanner pl(g, &rules);
+        const auto rules = fec::shared_decode_rules(T, B, N);
+        fec::StreamPlanner pl(g, rules.get());
         for (int64_t t = 0; t < P; ++t) {
             const fec::StepResult r = pl.step(t, erasure[t] != 0);
             if (r.x >= 0) fate[r.x] = static_cast<uint8_t>(r.fate);
@@ -1272,8 +1271,8 @@ int fec::codec_view(const fec_codec* c, fec::CodecView* v) {
     v->G = c->d_G;
     v->gf = c->d_gf;
     v->rules = c->d_rules;
-    v->wbase_n = c->rules.w_base[g.n];
-    v->ES = c->rules.entry_bytes;
+    v->wbase_n = c->rules->w_base[g.n];
+    v->ES = c->rules->entry_bytes;
     return FEC_OK;
 }
 
@@ -1296,8 +1295,8 @@ static int launch_block(fec_codec* c, bool decode, const uint8_t* d_in, const ui
     a.G = c->d_G;
     a.gf = c->d_gf;
     a.rules = c->d_rules;
-    a.wbase_n = c->rules.w_base[g.n];
-    a.ES = c->rules.entry_bytes;
+    a.wbase_n = c->rules->w_base[g.n];
+    a.ES = c->rules->entry_bytes;
     const int64_t grid = std::min<int64_t>((nblk + 255) / 256, 4096);
     const size_t lds = decode ? 768 + 2 * 256 * g.n : 768 + 1024 + 256 * (g.k + g.n);
     if (decode)

@@ -3,6 +3,8 @@
 
 #include <algorithm>
 #include <atomic>
+#include <map>
+#include <mutex>
 #include <thread>
 
 namespace fec {
@@ -163,6 +165,20 @@ void DecodeRules::build(const std::vector<uint8_t>& G, int k_, int n_, int T_) {
     }
 }
 
+std::shared_ptr<const DecodeRules> shared_decode_rules(int T, int B, int N) {
+    static std::mutex mu;
+    static std::map<int64_t, std::shared_ptr<const DecodeRules>> cache;
+    const int64_t key = (int64_t(T) << 32) | (int64_t(B) << 16) | int64_t(N);
+    std::lock_guard<std::mutex> lock(mu);
+    auto it = cache.find(key);
+    if (it != cache.end()) return it->second;
+    const int k = T - N + 1, n = k + B;
+    auto r = std::make_shared<DecodeRules>();
+    r->build(make_generator(T, B, N), k, n, T);
+    cache.emplace(key, r);
+    return r;
+}
+
 // ------------------------------------------------------------------------------------------
 // StreamPlanner
 // ------------------------------------------------------------------------------------------
@@ -196,7 +212,8 @@ void StreamPlanner::decode_block(int b, int t) {
             const uint8_t f = colv[c];
             if (!f || ((m >> c) & 1u)) continue;
             const uint8_t* src = cw(b, c);
-            for (int q = 0; q < n_; ++q) fresh[i][q] ^= F.mul(f, src[q]);
+            const uint8_t* row = F.mt[f];
+            for (int q = 0; q < n_; ++q) fresh[i][q] ^= row[src[q]];
         }
         got |= 1u << i;
     }

@@ -20,6 +20,7 @@
 
 #include <cstdint>
 #include <cstring>
+#include <memory>
 #include <stdexcept>
 #include <vector>
 
@@ -35,6 +36,7 @@ constexpr int kMaxRuleN = 17;  // decode-rule tables are built for n <= 17 (2^17
 struct Field {
     uint8_t exp[512];  // exp[i] = 2^(i mod 255)
     uint8_t log[256];  // log[0] unused
+    uint8_t mt[256][256];  // mt[a][b] = a*b (host planners: one lookup per product)
     Field() {
         unsigned v = 1;
         for (int i = 0; i < 255; ++i) {
@@ -45,6 +47,8 @@ struct Field {
         }
         for (int i = 255; i < 512; ++i) exp[i] = exp[i - 255];
         log[0] = 0;
+        for (int a = 0; a < 256; ++a)
+            for (int b = 0; b < 256; ++b) mt[a][b] = (a && b) ? exp[log[a] + log[b]] : 0;
     }
     uint8_t mul(uint8_t a, uint8_t b) const {
         return (a && b) ? exp[log[a] + log[b]] : 0;
@@ -97,6 +101,10 @@ struct DecodeRules {
         return table.data() + w_base[w] + static_cast<int64_t>(mask) * entry_bytes;
     }
 };
+
+// The rule table of (T,B,N) (G = make_generator(T,B,N)), built once per process and shared by
+// every codec, streaming decoder and variable-rate plan of that configuration (thread-safe).
+std::shared_ptr<const DecodeRules> shared_decode_rules(int T, int B, int N);
 
 // The rule for one (w, mask), computed directly (used to build the table and by tests).
 void decode_rule(const uint8_t* G, int k, int n, int w, uint32_t mask, uint8_t* sel,

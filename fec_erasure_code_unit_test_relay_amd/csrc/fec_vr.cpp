@@ -5,9 +5,11 @@
 #include <hip/hip_runtime_api.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cstring>
 #include <new>
 #include <stdexcept>
+#include <thread>
 
 #include "fec_amd.h"
 
@@ -81,10 +83,7 @@ const DecodeRules& VrPlan::rules_for(int T, int B, int N) {
     const int key = T * 1024 + B * 32 + N;
     auto it = rules_.find(key);
     if (it != rules_.end()) return *it->second;
-    const Geometry g = Geometry::make(L, T, B, N);
-    std::unique_ptr<DecodeRules> r(new DecodeRules());
-    r->build(make_generator(T, B, N), g.k, g.n, g.T);
-    return *rules_.emplace(key, std::move(r)).first->second;
+    return *rules_.emplace(key, shared_decode_rules(T, B, N)).first->second;
 }
 
 namespace {
@@ -92,19 +91,18 @@ namespace {
 constexpr int kTTot = 10;                 // T_TOT (FEC_Macro.h:32)
 constexpr int kEstimationCycle = 1000 / 10;  // ESTIMATION_WINDOW_SIZE / ..._REDUCTION_FACTOR (:54-55)
 
-struct SymDecoder {  // one FEC_Decoder instance, symbolically
-    Geometry g;
-    std::unique_ptr<StreamPlanner> planner;
-    int64_t first = 0, next = 0;
-    StepResult call(int64_t seq, bool erased) {
-        if (seq != next) throw std::logic_error("vr: decoder calls out of order");
-        ++next;
-        return planner->step(seq - first, erased);
-    }
+struct Report {        // decoder instance `id` reports packet x at its call for seq
+    int64_t seq, x;
 };
 
 }  // namespace
 
+// Two phases.  (1) The control loop -- sender, estimators, encoder switches, the receiver's
+// decoder swaps -- never looks at a decoder's output (FEC_Decoder::onReceive results only feed
+// onDecodedMessage), so it runs first and records, per decoder instance, its calls (consecutive
+// seqs from `first`, erased = the packet was dropped) and which of them report which packet.
+// (2) The symbolic decoders are independent of each other: they replay their calls in parallel
+// (one StreamPlanner per instance) and fill in the reported fates and coefficient rows.
 void VrPlan::run(int max_payload, int T, int B, int N, bool mds, const uint8_t* pattern, int64_t n_pattern,
                  int64_t P_value) {
     L = max_payload;
@@ -145,14 +143,9 @@ void VrPlan::run(int max_payload, int T, int B, int N, bool mds, const uint8_t* 
     int dT = 0, dB = 0, dN = 0;
     int dcur = -1, dold = -1;
     bool dcf = false;
-    std::vector<SymDecoder> sd;
+    std::vector<std::vector<Report>> reports;  // per decoder instance, in call order
 
     auto new_decoder = [&](int T_, int B_, int N_, int64_t first) {
-        SymDecoder d;
-        d.g = Geometry::make(L, T_, B_, N_);
-        d.planner.reset(new StreamPlanner(d.g, &rules_for(T_, B_, N_)));
-        d.first = d.next = first;
-        sd.push_back(std::move(d));
         VrInstance v;
         v.T = T_;
         v.B = B_;
@@ -160,30 +153,19 @@ void VrPlan::run(int max_payload, int T, int B, int N, bool mds, const uint8_t* 
         v.first = v.end = first;
         v.role_switch = -1;  // set when it becomes the old decoder
         dec.push_back(v);
-        return static_cast<int>(sd.size()) - 1;
+        reports.emplace_back();
+        return static_cast<int>(dec.size()) - 1;
     };
-    auto call = [&](int id, int64_t seq, bool er) {
-        const StepResult r = sd[id].call(seq, er);
+    auto call = [&](int id, int64_t seq) {
+        if (seq != dec[id].end) throw std::logic_error("vr: decoder calls out of order");
         dec[id].end = seq + 1;
-        return r;
     };
     // onDecodedMessage (:2403-2436): packets seq - T >= seq_start are reported once
-    auto report = [&](int id, int64_t seq, const StepResult& r) {
+    auto report = [&](int id, int64_t seq) {
         const int64_t x = seq - dT;
         if (x < seq_start || x >= P) return;
-        const PacketFate f = r.fate == kNone ? kLost : r.fate;
-        fate[x] = f;
+        reports[id].push_back(Report{seq, x});
         fate_dec[x] = id;
-        slow[x] = r.slow ? 1 : 0;
-        if (f == kLost) ++lost;
-        if (f == kRecovered) {
-            rec_x.push_back(x);
-            rec_dec.push_back(id);
-            const size_t o = rec_coef.size();
-            rec_coef.resize(o + kVrCoefStride, 0);
-            const Geometry& g = sd[id].g;
-            std::memcpy(&rec_coef[o], r.coef, static_cast<size_t>(g.k) * g.n);
-        }
     };
     auto update_decoder = [&](int T_, int B_, int N_, int64_t first) {  // (:2520-2536)
         dold = dcur;
@@ -287,10 +269,14 @@ void VrPlan::run(int max_payload, int T, int B, int N, bool mds, const uint8_t* 
                     dcf = true;
                 }
                 if (!dcf) {
-                    report(dcur, s, call(dcur, s, true));
+                    call(dcur, s);
+                    report(dcur, s);
                 } else {
-                    if (dold >= 0) report(dold, s, call(dold, s, true));
-                    call(dcur, s, true);
+                    if (dold >= 0) {
+                        call(dold, s);
+                        report(dold, s);
+                    }
+                    call(dcur, s);
                 }
             }
             if (seq > sde && dcf) dcf = false;
@@ -300,10 +286,14 @@ void VrPlan::run(int max_payload, int T, int B, int N, bool mds, const uint8_t* 
                 dcf = true;
             }
             if (!dcf) {
-                report(dcur, seq, call(dcur, seq, false));
+                call(dcur, seq);
+                report(dcur, seq);
             } else {
-                if (dold >= 0) report(dold, seq, call(dold, seq, false));
-                call(dcur, seq, false);
+                if (dold >= 0) {
+                    call(dold, seq);
+                    report(dold, seq);
+                }
+                call(dcur, seq);
             }
             latest_seq = seq + 1;
         }
@@ -318,6 +308,63 @@ void VrPlan::run(int max_payload, int T, int B, int N, bool mds, const uint8_t* 
     for (auto* list : {&enc, &dec})
         for (auto& e : *list)
             if (e.role_switch < 0) e.role_switch = e.end;  // never became the old instance
+
+    // ---- phase 2: the decoder instances, symbolically and in parallel ----
+    for (const auto& d : dec) rules_for(d.T, d.B, d.N);  // built before the workers share the map
+    struct Rec {
+        int64_t x;
+        uint8_t coef[kMaxK * kMaxRuleN];
+    };
+    std::vector<std::vector<Rec>> recs(dec.size());
+    std::atomic<size_t> next{0};
+    auto worker = [&]() {
+        for (size_t id; (id = next.fetch_add(1)) < dec.size();) {
+            const VrInstance& d = dec[id];
+            const Geometry g = Geometry::make(L, d.T, d.B, d.N);
+            StreamPlanner pl(g, rules_.at(d.T * 1024 + d.B * 32 + d.N).get());
+            const std::vector<Report>& rp = reports[id];
+            size_t ri = 0;
+            for (int64_t s = d.first; s < d.end; ++s) {
+                const StepResult r = pl.step(s - d.first, erased[static_cast<size_t>(s)] != 0);
+                if (ri == rp.size() || rp[ri].seq != s) continue;
+                const int64_t x = rp[ri++].x;
+                const PacketFate f = r.fate == kNone ? kLost : r.fate;
+                fate[x] = f;
+                slow[x] = r.slow ? 1 : 0;
+                if (f == kRecovered) {
+                    Rec rc;
+                    rc.x = x;
+                    std::memset(rc.coef, 0, sizeof(rc.coef));
+                    std::memcpy(rc.coef, r.coef, static_cast<size_t>(g.k) * g.n);
+                    recs[id].push_back(rc);
+                }
+            }
+        }
+    };
+    const unsigned hw = std::thread::hardware_concurrency();
+    const size_t nth = std::min<size_t>({dec.size(), hw ? hw : 1u, 16u});
+    if (nth <= 1) {
+        worker();
+    } else {
+        std::vector<std::thread> pool;
+        for (size_t i = 0; i < nth; ++i) pool.emplace_back(worker);
+        for (auto& th : pool) th.join();
+    }
+    for (int64_t x = 0; x < P; ++x)
+        if (fate[x] == kLost) ++lost;
+    std::vector<std::pair<int64_t, const Rec*>> order;
+    for (size_t id = 0; id < recs.size(); ++id)
+        for (const Rec& rc : recs[id]) order.emplace_back(rc.x, &rc);
+    std::sort(order.begin(), order.end(),
+              [](const std::pair<int64_t, const Rec*>& a, const std::pair<int64_t, const Rec*>& b) {
+                  return a.first < b.first;
+              });
+    rec_coef.resize(order.size() * kVrCoefStride);
+    for (size_t i = 0; i < order.size(); ++i) {
+        rec_x.push_back(order[i].first);
+        rec_dec.push_back(fate_dec[order[i].first]);
+        std::memcpy(&rec_coef[i * kVrCoefStride], order[i].second->coef, kVrCoefStride);
+    }
 }
 
 }  // namespace fec

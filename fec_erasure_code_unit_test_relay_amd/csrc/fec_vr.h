@@ -76,7 +76,7 @@ struct VrPlan {
              int64_t P_value);
 
 private:
-    std::map<int, std::unique_ptr<DecodeRules>> rules_;  // key T*1024 + B*32 + N
+    std::map<int, std::shared_ptr<const DecodeRules>> rules_;  // key T*1024 + B*32 + N
     const DecodeRules& rules_for(int T, int B, int N);
 };
 

@@ -19,7 +19,9 @@ from .codec import _ptr, _stream_handle
 
 class VrPlan:
     def __init__(self, erasure: np.ndarray, P: int, max_payload: int = 300, T: int = 10, B: int = -1,
-                 N: int = -1, adaptive_mode_MDS: bool = False):
+                 N: int = -1, adaptive_mode_MDS: bool = False, light: bool = False):
+        """light=True: only the statistics are read back (the schedule arrays stay in the C plan,
+        which is all encode()/decode() need)."""
         pat = np.ascontiguousarray(erasure, dtype=np.uint8)
         h = ctypes.c_void_p()
         check(lib().fec_vr_plan_create(max_payload, T, B, N, int(adaptive_mode_MDS),
@@ -35,6 +37,8 @@ class VrPlan:
               "fec_vr_plan_stats")
         self.lost, self.switches, self.coding_rate = lost.value, sw.value, rate.value
         self.sent, self.cw_max = sent.value, cwm.value
+        if light:
+            return
         self.encoders = np.zeros((ne.value, 6), dtype=np.int64)
         self.decoders = np.zeros((nd.value, 6), dtype=np.int64)
         check(lib().fec_vr_plan_instances(h, self.encoders.ctypes.data_as(ctypes.c_void_p),
@@ -84,8 +88,8 @@ class VrPlan:
         row is written)."""
         import torch
         dev = cw_cur.device
-        if erased is None:
-            erased = torch.from_numpy(self.erased).to(dev)
+        if erased is None:  # the device decode does not read it (the plan holds the pattern)
+            erased = out
         if out is None:
             out = torch.empty((self.P, self.L), dtype=torch.uint8, device=dev)
         if out_len is None:
