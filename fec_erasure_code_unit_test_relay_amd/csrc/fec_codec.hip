@@ -618,6 +618,10 @@ int launch_plan(fec_codec* c, const uint8_t* d_er, int64_t P, void* d_ws, size_t
     HIP_TRY(hipGetLastError());
     hipLaunchKernelGGL(fec::fec_shape_fill_kernel, dim3(pgrid), dim3(64), 0, s, sa);
     HIP_TRY(hipGetLastError());
+    // packets with all k symbols recovered -> rec_list (timed with the plan)
+    hipLaunchKernelGGL(fec::fec_compact_kernel, dim3(256), dim3(256), 0, s, w.counters, w.erased,
+                       w.sym_ok, g.k, w.rec_list);
+    HIP_TRY(hipGetLastError());
     return c->end(stop, s);
 }
 
@@ -740,9 +744,7 @@ int launch_recover(fec_codec* c, const uint8_t* d_cw, int64_t P, uint8_t* d_out,
     ra.P = P;
     ra.Pout = Pout;
     ra.counters = w.counters;
-    ra.erased = w.erased;
-    ra.sym_ok = w.sym_ok;
-    ra.zero_lost = copy_skips_erased(c, d_out, P) ? 1 : 0;
+    ra.rec_list = w.rec_list;
     ra.coef = w.coef;
     ra.gf = c->d_gf;
     ra.out = d_out;
@@ -754,6 +756,11 @@ int launch_recover(fec_codec* c, const uint8_t* d_cw, int64_t P, uint8_t* d_out,
     ra.CW = g.CW;
     hipEvent_t stop;
     if (int st = c->begin(FEC_KERNEL_DEC_RECOVER, s, &stop)) return st;
+    // when the copy kernel leaves erased rows alone (wave copy), the lost ones get their zero row
+    // and length 0 here
+    ra.erased = w.erased;
+    ra.sym_ok = w.sym_ok;
+    ra.zero_lost = copy_skips_erased(c, d_out, P) ? 1 : 0;
     hipLaunchKernelGGL(fec::fec_recover_kernel, dim3(1024), dim3(256), 0, s, ra);
     HIP_TRY(hipGetLastError());
     return c->end(stop, s);

@@ -175,10 +175,11 @@ struct ShapeArgs {
 struct RecArgs {
     const uint8_t* cw;
     int64_t P, Pout;
-    int32_t* counters;             // [1] erased outputs (in), [2] recovered packets (counted here)
+    const int32_t* counters;       // [1] erased outputs, [2] recovered packets
+    const int32_t* rec_list;       // recovered packets (fec_compact_kernel)
     const int32_t* erased;         // erased output packets (fec_scan_kernel)
     const uint8_t* sym_ok;         // [P][k] from the planner
-    int zero_lost;                 // 1: write lost packets' rows (zeros) and lengths (0) too
+    int zero_lost;                 // 1: also write lost packets' rows (zeros) and lengths (0)
     const uint8_t* coef;
     const uint8_t* gf;
     uint8_t* out;

@@ -459,12 +459,10 @@ constexpr int kRecMaxN = 17;  // = kMaxRuleN: codecs with n > 17 are refused
 constexpr int kRecRounds = 5;  // 64-byte rounds per pass of fec_recover_kernel (L = 300: one pass)
 
 __global__ __launch_bounds__(256) void fec_recover_kernel(RecArgs a) {
-    // One wave per erased output packet (the scan's erased list), no workgroup barrier after the
-    // table load.  Lost packets (a symbol not recovered) get a zero row and length 0.  Recovered
-    // ones: lane h computes bytes h, h+64, ... of [len_hi, len_lo, payload]; its n sources are byte
-    // loads straight from the diagonal's rows (a ~(k+n)*CW-byte window, L2-resident), all issued
-    // before the lookups.  This kernel writes only erased packets' rows, the copy kernels only
-    // received ones, so the two can run concurrently.
+    // One wave per recovered packet (fec_compact_kernel's list), no workgroup barrier after the
+    // table load: lane h computes bytes h, h+64, ... of [len_hi, len_lo, payload]; its n sources
+    // are byte loads straight from the diagonal's rows (a ~(k+n)*CW-byte window, L2-resident), all
+    // issued before the lookups.
     __shared__ uint8_t gexp[512];
     __shared__ uint8_t glog[256];
     __shared__ uint8_t lcf[4][kRecMaxK * kRecMaxN];  // per wave: coefficient logs, 255 = zero coefficient
@@ -474,21 +472,22 @@ __global__ __launch_bounds__(256) void fec_recover_kernel(RecArgs a) {
     __syncthreads();
     const int lane = tid & 63, wl = tid >> 6;
     const int L = a.L, k = a.k, n = a.n, CW = a.CW;
-    const int ner = a.counters[1];
+    const int nrec = a.counters[2];
     uint8_t* lc = lcf[wl];
     const int waves = gridDim.x * 4;
-    for (int r = blockIdx.x * 4 + wl; r < ner; r += waves) {
-        const int64_t x = a.erased[r];
-        bool ok = true;
-        for (int i = 0; i < k; ++i) ok = ok && a.sym_ok[x * k + i];
-        if (!ok) {  // lost: payload 0 (FEC_Decoder returns no data), zero row
-            if (a.zero_lost) {
-                for (int b = lane; b < L; b += 64) a.out[x * L + b] = 0;
-                if (lane == 0) a.out_len[x] = 0;
-            }
-            continue;
+    if (a.zero_lost) {  // lost packets: payload 0 (FEC_Decoder returns no data), zero row
+        const int ner = a.counters[1];
+        for (int r = blockIdx.x * 4 + wl; r < ner; r += waves) {
+            const int64_t x = a.erased[r];
+            bool ok = true;
+            for (int i = 0; i < k; ++i) ok = ok && a.sym_ok[x * k + i];
+            if (ok) continue;
+            for (int b = lane; b < L; b += 64) a.out[x * L + b] = 0;
+            if (lane == 0) a.out_len[x] = 0;
         }
-        if (lane == 0) atomicAdd(const_cast<int32_t*>(&a.counters[2]), 1);
+    }
+    for (int r = blockIdx.x * 4 + wl; r < nrec; r += waves) {
+        const int64_t x = a.rec_list[r];
         for (int i = lane; i < k * n; i += 64) {
             const uint8_t c = a.coef[x * k * n + i];
             lc[i] = c ? glog[c] : 255;

@@ -67,6 +67,11 @@ def lib() -> ctypes.CDLL:
         L.or_swdf_run.restype = ctypes.c_int
         L.or_swdf_run.argtypes = [ctypes.c_int] * 5 + [ctypes.c_int64, u8p, u8p, ctypes.c_uint64,
                                                         u8p, u8p, u8p, u8p]
+        L.or_vr_run.restype = ctypes.c_int64
+        i64p = ctypes.POINTER(ctypes.c_int64)
+        L.or_vr_run.argtypes = [ctypes.c_int] * 5 + [u8p, ctypes.c_int64, ctypes.c_int64, ctypes.c_uint64, ip,
+                                                      u8p, u8p, ctypes.c_int64, i64p, ctypes.c_int64,
+                                                      i64p, ctypes.POINTER(ctypes.c_double)]
         _lib = L
     return _lib
 
@@ -242,3 +247,29 @@ def swdf_run(max_payload: int, T1: int, N1: int, T2: int, N2: int, P: int, e1: n
     if st != 0:
         raise ValueError("unsupported SWDF configuration")
     return dict(frames=frames, relay_flag=rf, dest_out=out, dest_flag=df, delay=n1 + n2 - k - 1, S=S, k=k)
+
+
+def vr_run(pattern: np.ndarray, P: int, max_payload: int = 300, T: int = 10, B: int = -1, N: int = -1,
+           mds: bool = False, seed: int = 0x5EED, want_data: bool = False, max_sent: int = 0,
+           packets_cap: int = 0):
+    """The adaptive P2P loop (sender -> Variable_Rate_FEC_Encoder -> erasure -> receiver with its
+    Parameter_Estimator pair -> Variable_Rate_FEC_Decoder), reference-structured on real bytes.
+    Returns dict(lost, switches, sent, coding_rate, out_len [P], out_data?, packets?, packet_off?):
+    packets = the first max_sent P2P wire packets back to back, packet_off their offsets."""
+    pat = np.ascontiguousarray(pattern, dtype=np.uint8)
+    out_len = np.zeros(P, dtype=np.int32)
+    out_data = np.zeros((P, max_payload), dtype=np.uint8) if want_data else None
+    packets = np.zeros(packets_cap, dtype=np.uint8) if packets_cap else None
+    packet_off = np.zeros(max_sent + 1, dtype=np.int64) if max_sent else None
+    stats = (ctypes.c_int64 * 3)()
+    rate = ctypes.c_double()
+    lib().or_vr_run(max_payload, T, B, N, int(mds), _u8(pat), pat.size, P, seed, _i32(out_len),
+                    _u8(out_data) if want_data else None, _u8(packets) if packets_cap else None, packets_cap,
+                    packet_off.ctypes.data_as(ctypes.POINTER(ctypes.c_int64)) if max_sent else None, max_sent,
+                    stats, ctypes.byref(rate))
+    res = dict(lost=int(stats[0]), switches=int(stats[1]), sent=int(stats[2]), coding_rate=rate.value,
+               out_len=out_len, out_data=out_data, packets=None, packet_off=packet_off)
+    if packets_cap:
+        assert packet_off[-1] <= packets_cap, "packets_cap too small"
+        res["packets"] = packets[: packet_off[-1]]
+    return res

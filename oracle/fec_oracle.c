@@ -762,3 +762,361 @@ int or_swdf_run(int max_payload, int T1, int N1, int T2, int N2, int64_t P, cons
     or_swdf_free(dest);
     return 0;
 }
+
+/* ------------------------------------------------------------------------------------------ */
+/* The adaptive P2P loop (BASELINE config 4): application_local_simulation.cpp:328-345 with    */
+/* RELAYING_TYPE 0 -- Application_Layer_Sender::generate_message_and_encode ->                 */
+/* Variable_Rate_FEC_Encoder::encode -> erasure -> Application_Layer_Receiver::                */
+/* receive_message_and_decode (Parameter_Estimator pair) -> Variable_Rate_FEC_Decoder::decode,  */
+/* the receiver's 6-byte feedback read by the sender at the next packet.  Kept in the           */
+/* reference's object shape, on real bytes (or_encoder / or_decoder), so that it is a checker   */
+/* of the product's symbolic plan (fec_vr.cpp) and not a copy of it.                            */
+/* ------------------------------------------------------------------------------------------ */
+#define OR_T_TOT 10             /* FEC_Macro.h:32 */
+#define OR_EST_CYCLE (1000 / 10) /* ESTIMATION_WINDOW_SIZE / ..._REDUCTION_FACTOR, FEC_Macro.h:54-55 */
+
+typedef struct { /* Parameter_Estimator, Parameter_Estimator.cpp:24-42 */
+    int mds, T, B, N, N_max, B_current, N_current;
+    uint8_t erasure[12];
+    int64_t previous_win_end;
+} or_estimator;
+
+static void or_est_init(or_estimator *e, int T, int mds) {
+    memset(e, 0, sizeof(*e));
+    e->mds = mds;
+    e->T = T;
+    e->previous_win_end = -2;
+}
+
+/* make_MDS_estimates, :213-223 */
+static void or_est_mds(or_estimator *e) {
+    if (e->B_current > e->N_current) {
+        while ((e->T - e->N_current) * (e->T - e->N_current + 1 + e->B_current) >
+               (e->T + 1) * (e->T - e->N_current + 1))
+            e->N_current++;
+        e->B_current = e->N_current;
+    }
+}
+
+/* estimate, :58-186 (RELAYING_TYPE 0: T comes from the first message) */
+static void or_est_estimate(or_estimator *e, int64_t seq, int msg_T) {
+    if (e->T == 0) return;
+    if (e->previous_win_end == -2) {
+        e->T = msg_T;
+        e->previous_win_end = seq - 1;
+    }
+    const int64_t current_win_end = seq;
+    if (current_win_end - e->previous_win_end < 1) return;
+    const int T = e->T;
+    for (int64_t s = e->previous_win_end + 1; s <= current_win_end; s++) {
+        for (int i = T; i >= 1; i--) e->erasure[i] = e->erasure[i - 1];
+        e->erasure[0] = (s < current_win_end) ? 1 : 0;
+        int sum = 0;
+        for (int i = 0; i <= T; i++) sum += e->erasure[i] == 1;
+        if (sum == T + 1 || sum == 0) continue;
+        if (e->B == 0) e->B = 1;
+        if (e->N == 0) e->N = 1;
+        if (sum > e->N_max) e->N_max = sum;
+        int i;
+        for (i = 0; i <= T; i++)
+            if (e->erasure[i] != 0) break;
+        const int first_nonzero = i;
+        for (i = T; i >= 0; i--)
+            if (e->erasure[i] != 0) break;
+        const int last_nonzero = i;
+        const int span = last_nonzero - first_nonzero + 1;
+        if (span == T + 1) {
+            if (sum > e->N) {
+                e->N = sum;
+                e->B = e->N;
+            }
+        } else {
+            const int max_B_and_sum = sum > e->B ? sum : e->B;
+            const int max_B_and_span = span > e->B ? span : e->B;
+            if ((T - e->N + 1) * (T - sum + 1 + max_B_and_sum) >= (T - sum + 1) * (T - e->N + 1 + max_B_and_span)) {
+                if (span > e->B) {
+                    e->B = span;
+                    e->N = span;
+                }
+            } else {
+                if (sum > e->N) {
+                    e->N = sum;
+                    e->B = sum;
+                }
+                if (e->N > e->B) e->B = e->N;
+            }
+        }
+        if ((T - e->N_max + 1) * (T - e->N + 1 + e->B) > (T - e->N + 1) * (T + 1)) {
+            e->B = e->N_max;
+            e->N = e->N_max;
+        }
+    }
+    e->previous_win_end = current_win_end;
+    if ((T - e->N_current + 1) * (T - e->N + 1 + e->B) >= (T - e->N + 1) * (T - e->N_current + 1 + e->B_current)) {
+        e->B_current = e->B;
+        e->N_current = e->N;
+    }
+    if (e->mds) or_est_mds(e);
+}
+
+typedef struct { /* Variable_Rate_FEC_Encoder, Variable_Rate_FEC_Encoder.cpp:25-72 */
+    int L;
+    or_encoder *cur, *old;
+    int T, B, N, T_old, B_old, N_old;
+    int counter_transition, transition_flag, double_coding_flag;
+    float final_sum_coding_rate;
+    int64_t final_number_of_encoded_total, switches;
+    uint8_t *cw_cur, *cw_old;
+} or_vr_encoder;
+
+/* encode, :74-235 (RELAYING_TYPE 0).  In/out: the message's (T,B,N); out: the VR frame
+ * [size_current BE16][codeword_current][codeword_old] and counter_for_start_and_end. */
+static int or_vre_encode(or_vr_encoder *v, int *mT, int *mB, int *mN, const uint8_t *data, int size, int seq,
+                         int T_ack, int B_ack, uint8_t *frame, int *counter) {
+    if (v->cur == NULL) {
+        v->T = *mT;
+        v->B = *mB;
+        v->N = *mN;
+        v->cur = or_encoder_new(v->L, v->T, v->B, v->N);
+        v->transition_flag = 1;
+        v->double_coding_flag = 0;
+    } else if ((*mT != v->T || *mB != v->B || *mN != v->N) && v->transition_flag == 0 && T_ack == v->T &&
+               B_ack == v->B) {
+        v->switches++; /* "Start double coding at the source" */
+        v->T_old = v->T;
+        v->B_old = v->B;
+        v->N_old = v->N;
+        v->T = *mT;
+        v->B = *mB;
+        v->N = *mN;
+        v->transition_flag = 1;
+        v->double_coding_flag = 1;
+        v->counter_transition = 0;
+        if (v->old) or_encoder_free(v->old);
+        v->old = v->cur;
+        v->cur = or_encoder_new(v->L, v->T, v->B, v->N);
+    } else {
+        *mT = v->T;
+        *mB = v->B;
+        *mN = v->N;
+    }
+    const int size_cur = or_encoder_transmit(v->cur, data, size, seq, v->cw_cur);
+    int size_old = 0;
+    *counter = v->counter_transition;
+    if (v->counter_transition <= v->T) {
+        if (v->counter_transition == v->T) v->double_coding_flag = 0;
+        v->counter_transition++;
+        if (v->old != NULL && v->double_coding_flag == 1)
+            size_old = or_encoder_transmit(v->old, data, size, seq, v->cw_old);
+    } else {
+        v->transition_flag = 0;
+    }
+    frame[0] = (uint8_t)((size_cur - size_cur % 256) / 256);
+    frame[1] = (uint8_t)(size_cur % 256);
+    memcpy(frame + 2, v->cw_cur, (size_t)size_cur);
+    if (size_old) memcpy(frame + 2 + size_cur, v->cw_old, (size_t)size_old);
+    v->final_number_of_encoded_total++;
+    const int T = v->T, B = v->B, N = v->N;
+    if (v->double_coding_flag == 0)
+        v->final_sum_coding_rate += (float)(T - N + 1) / (T - N + 1 + B);
+    else
+        v->final_sum_coding_rate += (float)(T - N + 1) / ((T - N + 1 + B) + (T - v->N_old + 1) + (T - v->N_old + 1 + B));
+    return size_cur + size_old + 2;
+}
+
+typedef struct { /* Variable_Rate_FEC_Decoder, Variable_Rate_FEC_Decoder.cpp:24-80 */
+    int L;
+    int64_t seq_start, latest_seq, sdc, sde; /* seq_start_double_coding, seq_end_double_coding */
+    int T, B, N, dcf;
+    or_decoder *cur, *old;
+    int64_t P, lost;
+    int *out_len;
+    uint8_t *out_data, *buf;
+} or_vr_decoder;
+
+/* onDecodedMessage, :2400-2459: a NULL buffer (payload 0) counts as lost */
+static void or_vrd_report(or_vr_decoder *d, int64_t x, int payload) {
+    if (x < 0 || x >= d->P) return;
+    d->out_len[x] = payload;
+    if (payload <= 0) d->lost++;
+    if (d->out_data) {
+        uint8_t *o = d->out_data + x * (int64_t)d->L;
+        memset(o, 0, (size_t)d->L);
+        if (payload > 0) memcpy(o, d->buf, (size_t)(payload < d->L ? payload : d->L));
+    }
+}
+
+/* update_decoder, :2548-2565 */
+static void or_vrd_update(or_vr_decoder *d, int T, int B, int N) {
+    if (d->old) or_decoder_free(d->old);
+    d->old = d->cur;
+    d->T = T;
+    d->B = B;
+    d->N = N;
+    d->cur = or_decoder_new(d->L, T, B, N, 0);
+}
+
+/* decode, :2133-2398 (RELAYING_TYPE 0, receiver_index 0) */
+static void or_vrd_decode(or_vr_decoder *d, int64_t received_seq, int mT, int mB, int mN, int counter,
+                          const uint8_t *frame, int size) {
+    if (d->seq_start == -1) { /* initialize_decoder, :2462-2478 */
+        d->seq_start = 0;
+        d->latest_seq = d->seq_start;
+        d->T = mT;
+        d->B = mB;
+        d->N = mN;
+        d->cur = or_decoder_new(d->L, mT, mB, mN, 0);
+    }
+    if (received_seq < d->latest_seq) return;
+    if (d->T != mT || d->B != mB || d->N != mN) d->sdc = received_seq - counter;
+    const uint8_t *cw = frame + 2;
+    const int size_cur = frame[0] * 256 + frame[1];
+    const uint8_t *cw_trans = cw + size_cur;
+    const int size_trans = size - 2 - size_cur;
+    for (int64_t seq = d->latest_seq; seq < received_seq; seq++) { /* :2200-2319 */
+        if (seq > d->sde && d->dcf == 1) d->dcf = 0;
+        if (seq == d->sdc) {
+            d->sde = d->sdc + d->T - 1;
+            or_vrd_update(d, mT, mB, mN);
+            d->dcf = 1;
+        }
+        if (d->dcf == 0) {
+            const int p = or_decoder_receive(d->cur, NULL, 0, (int)seq, 1, d->buf);
+            if (seq - d->T >= d->seq_start) or_vrd_report(d, seq - d->T, p);
+        } else {
+            if (d->old != NULL) {
+                const int p = or_decoder_receive(d->old, NULL, 0, (int)seq, 1, d->buf);
+                if (seq - d->T >= d->seq_start) or_vrd_report(d, seq - d->T, p);
+            }
+            or_decoder_receive(d->cur, NULL, 0, (int)seq, 1, d->buf);
+        }
+    }
+    if (received_seq > d->sde && d->dcf == 1) d->dcf = 0;
+    if (received_seq == d->sdc) {
+        d->sde = d->sdc + d->T - 1;
+        or_vrd_update(d, mT, mB, mN);
+        d->dcf = 1;
+    }
+    if (d->dcf == 0) { /* :2337-2357 */
+        const int p = or_decoder_receive(d->cur, cw, size_cur, (int)received_seq, 0, d->buf);
+        if (received_seq - d->T >= d->seq_start) or_vrd_report(d, received_seq - d->T, p);
+    } else { /* :2359-2386 */
+        if (d->old != NULL) {
+            const int p = or_decoder_receive(d->old, cw_trans, size_trans, (int)received_seq, 0, d->buf);
+            if (received_seq - d->T >= d->seq_start) or_vrd_report(d, received_seq - d->T, p);
+        }
+        or_decoder_receive(d->cur, cw, size_cur, (int)received_seq, 0, d->buf);
+    }
+    d->latest_seq = received_seq + 1;
+}
+
+int64_t or_vr_run(int max_payload, int T, int B, int N, int mds, const uint8_t *pattern, int64_t n_pattern,
+                  int64_t P, uint64_t seed, int *out_len, uint8_t *out_data, uint8_t *packets,
+                  int64_t packets_cap, int64_t *packet_off, int64_t max_sent, int64_t *stats, double *coding_rate) {
+    const int L = max_payload;
+    const int adaptive = (B == -1 || N == -1);
+    /* Application_Layer_Sender (Application_Layer_Sender.cpp:9-31) */
+    int sT = T, sB = adaptive ? 0 : B, sN = adaptive ? 0 : N, T_ack = sT, B_ack = sB;
+    int64_t seq_number = 0;
+    uint8_t udp[12] = {0};
+    or_vr_encoder enc;
+    memset(&enc, 0, sizeof(enc));
+    enc.L = L;
+    enc.transition_flag = 1;
+    enc.double_coding_flag = 1;
+    const int bufsz = 64 * (L + 64); /* > the largest codeword, (T,T,T): S*n <= (L+2)*(T+1) */
+    enc.cw_cur = (uint8_t *)calloc((size_t)bufsz, 1);
+    enc.cw_old = (uint8_t *)calloc((size_t)bufsz, 1);
+    uint8_t *payload = (uint8_t *)malloc((size_t)L);
+    uint8_t *pkt = (uint8_t *)calloc((size_t)(2 * bufsz + 16), 1);
+    /* Application_Layer_Receiver (Application_Layer_Receiver.cpp:10-31) */
+    or_estimator *est = (or_estimator *)malloc(sizeof(or_estimator));
+    or_estimator *bg = (or_estimator *)malloc(sizeof(or_estimator));
+    or_est_init(est, OR_T_TOT, mds);
+    or_est_init(bg, OR_T_TOT, mds);
+    int64_t cycle = 1;
+    or_vr_decoder dec;
+    memset(&dec, 0, sizeof(dec));
+    dec.L = L;
+    dec.seq_start = dec.latest_seq = dec.sdc = dec.sde = -1;
+    dec.P = P;
+    dec.out_len = out_len;
+    dec.out_data = out_data;
+    dec.buf = (uint8_t *)calloc((size_t)L, 1);
+    for (int64_t i = 0; i < P; i++) out_len[i] = 0;
+
+    for (;;) {
+        /* ---- generate_message_and_encode, Application_Layer_Sender.cpp:64-282 ---- */
+        or_fill_payload(payload, seq_number, 1, L, seed);
+        if (adaptive && udp[0] != 0) {
+            sT = udp[0];
+            sB = udp[1];
+            sN = udp[2];
+            T_ack = udp[3];
+            B_ack = udp[4];
+        }
+        int mT = sT, mB = sB, mN = sN, counter = 0;
+        const int fsize = or_vre_encode(&enc, &mT, &mB, &mN, payload, L, (int)seq_number, T_ack, B_ack, pkt + 8, &counter);
+        pkt[0] = (uint8_t)((seq_number / 256 / 256 / 256) % 256); /* :259-269 */
+        pkt[1] = (uint8_t)((seq_number / 256 / 256) % 256);
+        pkt[2] = (uint8_t)((seq_number / 256) % 256);
+        pkt[3] = (uint8_t)(seq_number % 256);
+        pkt[4] = (uint8_t)mT;
+        pkt[5] = (uint8_t)mB;
+        pkt[6] = (uint8_t)mN;
+        pkt[7] = (uint8_t)counter;
+        const int psize = 8 + fsize;
+        if (packet_off && seq_number < max_sent) { /* packets back to back, offsets [max_sent + 1] */
+            if (seq_number == 0) packet_off[0] = 0;
+            const int64_t o = packet_off[seq_number];
+            if (packets && o + psize <= packets_cap) memcpy(packets + o, pkt, (size_t)psize);
+            packet_off[seq_number + 1] = o + psize;
+        }
+        const int64_t sent_seq = seq_number;
+        seq_number++;
+        /* ---- receive_message_and_decode, Application_Layer_Receiver.cpp:321-468 ---- */
+        int64_t ret = -1;
+        const int64_t tseq = (int64_t)pkt[3] + 256 * (int64_t)pkt[2] + 65536 * (int64_t)pkt[1] + 16777216 * (int64_t)pkt[0];
+        const int dropped = tseq < P + T && tseq < n_pattern && pattern[tseq] == 1; /* :351-359 */
+        if (!dropped) {
+            const int hT = pkt[4], hB = pkt[5], hN = pkt[6], hc = pkt[7];
+            or_est_estimate(est, tseq, hT);
+            or_est_estimate(bg, tseq, hT);
+            if (tseq + 1 > cycle * OR_EST_CYCLE) { /* :385-398 */
+                free(est);
+                est = bg;
+                bg = (or_estimator *)malloc(sizeof(or_estimator));
+                or_est_init(bg, OR_T_TOT, 0);
+                cycle++;
+            }
+            or_vrd_decode(&dec, tseq, hT, hB, hN, hc, pkt + 8, psize - 8);
+            udp[0] = (uint8_t)est->T;
+            udp[1] = (uint8_t)est->B_current;
+            udp[2] = (uint8_t)est->N_current;
+            udp[3] = (uint8_t)hT;
+            udp[4] = (uint8_t)hB;
+            udp[5] = (uint8_t)hN;
+            ret = tseq;
+        }
+        (void)sent_seq;
+        if (ret >= P + T - 1) break; /* application_local_simulation.cpp:813 (T2 = 0 for P2P) */
+    }
+    if (stats) {
+        stats[0] = dec.lost;
+        stats[1] = enc.switches;
+        stats[2] = seq_number;
+    }
+    if (coding_rate) *coding_rate = enc.final_sum_coding_rate / (float)enc.final_number_of_encoded_total;
+    or_encoder_free(enc.cur);
+    or_encoder_free(enc.old);
+    or_decoder_free(dec.cur);
+    or_decoder_free(dec.old);
+    free(est);
+    free(bg);
+    free(enc.cw_cur);
+    free(enc.cw_old);
+    free(payload);
+    free(pkt);
+    free(dec.buf);
+    return dec.lost;
+}

@@ -81,6 +81,15 @@ int or_swdf_run(int max_payload, int T1, int N1, int T2, int N2, int64_t P, cons
                 const uint8_t *e2, uint64_t seed, uint8_t *frames, uint8_t *relay_flag,
                 uint8_t *dest_out, uint8_t *dest_flag);
 
+/* The adaptive P2P loop (BASELINE config 4), reference-structured on real bytes: returns the
+ * packets lost among 0..P-1; out_len[P] (0 = lost), out_data (P*max_payload or NULL); packets
+ * (packets_cap bytes, or NULL) receives the first max_sent P2P wire packets [seq BE32][T][B][N]
+ * [counter][size_current BE16][codeword_current][codeword_old] back to back, packet_off
+ * (max_sent + 1 entries, or NULL) their offsets; stats = {lost, switches, sent}. */
+int64_t or_vr_run(int max_payload, int T, int B, int N, int mds, const uint8_t *pattern, int64_t n_pattern,
+                  int64_t P, uint64_t seed, int *out_len, uint8_t *out_data, uint8_t *packets,
+                  int64_t packets_cap, int64_t *packet_off, int64_t max_sent, int64_t *stats, double *coding_rate);
+
 #ifdef __cplusplus
 }
 #endif
