@@ -398,6 +398,7 @@ struct fec_vr_plan {
     int32_t* d_rec_dec = nullptr;
     uint8_t* d_rec_coef = nullptr;
     uint8_t* d_gf = nullptr;
+    int32_t* d_hdr = nullptr;          // [sent][4]: frame header T, B, N, counter
     bool enc_ready = false, dec_ready = false;
 
     ~fec_vr_plan() {
@@ -410,7 +411,7 @@ struct fec_vr_plan {
                         static_cast<void*>(d_cwlen), static_cast<void*>(d_pk_dec), static_cast<void*>(d_inst),
                         static_cast<void*>(d_inst_switch), static_cast<void*>(d_fate), static_cast<void*>(d_slow),
                         static_cast<void*>(d_rec_x), static_cast<void*>(d_rec_dec), static_cast<void*>(d_rec_coef),
-                        static_cast<void*>(d_gf)})
+                        static_cast<void*>(d_gf), static_cast<void*>(d_hdr)})
             if (p) (void)hipFree(p);
     }
     int codec(int T, int B, int N, fec_codec** out) {
@@ -620,6 +621,30 @@ int fec_vr_encode_batch(fec_vr_plan* v, const uint8_t* d_payload, const int32_t*
     return FEC_OK;
 }
 
+// The P2P wire packets of every frame: row s of d_packets (stride >= 10 + 2*cw_max bytes) =
+// [seq BE32][T][B][N][counter_for_start_and_end] (Application_Layer_Sender.cpp:259-269) +
+// [len_cur BE16][cur][old] (Variable_Rate_FEC_Encoder.cpp:194-217), sizes in d_packet_len.
+int fec_vr_frames_batch(fec_vr_plan* v, const uint8_t* d_cw_cur, const int32_t* d_len_cur, const uint8_t* d_cw_old,
+                        const int32_t* d_len_old, uint8_t* d_packets, int64_t stride, int32_t* d_packet_len,
+                        void* hip_stream) {
+    if (!v || !d_cw_cur || !d_len_cur || !d_cw_old || !d_len_old || !d_packets || !d_packet_len) return FEC_ERR_ARG;
+    if (stride < 10 + 2 * static_cast<int64_t>(v->cw_max)) return FEC_ERR_ARG;
+    const auto& p = v->plan;
+    if (!v->d_hdr) {
+        std::vector<int32_t> h(static_cast<size_t>(p.sent) * 4);
+        for (int64_t s = 0; s < p.sent; ++s) {
+            h[4 * s] = p.frames[s].T;
+            h[4 * s + 1] = p.frames[s].B;
+            h[4 * s + 2] = p.frames[s].N;
+            h[4 * s + 3] = p.frames[s].counter;
+        }
+        if (int st = upload(&v->d_hdr, h)) return st;
+    }
+    fec::VrFrameArgs a{d_cw_cur, d_len_cur, d_cw_old, d_len_old, v->cw_max, v->d_hdr, p.sent, d_packets, stride,
+                       d_packet_len};
+    return fec::vr_launch_frames(a, hip_stream);
+}
+
 // Decode the schedule from the frames' arrays: every packet x < P was reported by one decoder
 // instance j (fate_decoder); a received one is the systematic part of cur[x] in j's geometry, a
 // recovered one the host plan's coefficient rows over j's inputs (cur rows before j became the
@@ -635,6 +660,14 @@ int fec_vr_decode_batch(fec_vr_plan* v, const uint8_t* d_cw_cur, const uint8_t* 
     fec::VrRecArgs ra{d_cw_cur, d_cw_old, v->cw_max, p.sent, v->d_rec_x, v->d_rec_dec, v->d_rec_coef,
                       static_cast<int>(p.rec_x.size()), v->d_inst, v->d_inst_switch, v->d_gf, p.L, d_out, d_out_len};
     return fec::vr_launch_recover(ra, hip_stream);
+}
+
+int fec_vr_parse_batch(const uint8_t* d_packets, int64_t stride, const int32_t* d_packet_len, int64_t rows,
+                       int cw_max, uint8_t* d_cw_cur, uint8_t* d_cw_old, int32_t* d_header, void* hip_stream) {
+    if (rows < 0 || cw_max < 1 || (rows > 0 && (!d_packets || !d_packet_len || !d_cw_cur || !d_cw_old)))
+        return FEC_ERR_ARG;
+    fec::VrParseArgs a{d_packets, stride, d_packet_len, rows, cw_max, d_cw_cur, d_cw_old, d_header};
+    return fec::vr_launch_parse(a, hip_stream);
 }
 
 }  // extern "C"

@@ -130,6 +130,34 @@ struct VrRecArgs {      // recovered packets: coefficient rows over the reportin
     uint8_t* out;
     int32_t* out_len;
 };
+// P2P wire packets (Application_Layer_Sender.cpp:259-269 over Variable_Rate_FEC_Encoder.cpp:194-217):
+// row s (stride bytes) = [seq BE32][T][B][N][counter][len_cur BE16][cur: len_cur][old: len_old].
+struct VrFrameArgs {
+    const uint8_t* cur;
+    const int32_t* len_cur;
+    const uint8_t* old;
+    const int32_t* len_old;
+    int64_t W;               // row stride of cur / old
+    const int32_t* hdr;      // [rows][4]: T, B, N, counter
+    int64_t rows;
+    uint8_t* packets;
+    int64_t stride;
+    int32_t* packet_len;
+};
+// The receiver's split of a wire packet (Application_Layer_Receiver.cpp:361-366,
+// Variable_Rate_FEC_Decoder.cpp:2156-2160): cur / old rows zero-padded to W, header fields out.
+struct VrParseArgs {
+    const uint8_t* packets;
+    int64_t stride;
+    const int32_t* packet_len;
+    int64_t rows;
+    int64_t W;
+    uint8_t* cur;
+    uint8_t* old;
+    int32_t* hdr;            // [rows][5]: seq, T, B, N, counter (may be null)
+};
+int vr_launch_frames(const VrFrameArgs& a, void* s);
+int vr_launch_parse(const VrParseArgs& a, void* s);
 int vr_launch_gather(const VrGatherArgs& a, void* s);
 int vr_launch_scatter(const VrScatterArgs& a, void* s);
 int vr_launch_copy(const VrCopyArgs& a, void* s);

@@ -5,11 +5,67 @@
 // recovery launch over the host plan's coefficient rows.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+
 #include "fec_amd.h"
 #include "fec_vr.h"
 
 namespace fec {
 namespace {
+
+// One wave per packet row.
+__global__ __launch_bounds__(256) void fec_vr_frame_kernel(VrFrameArgs a) {
+    const int lane = threadIdx.x & 63;
+    for (int64_t r = static_cast<int64_t>(blockIdx.x) * 4 + (threadIdx.x >> 6); r < a.rows;
+         r += static_cast<int64_t>(gridDim.x) * 4) {
+        const int lc = a.len_cur[r], lo = a.len_old[r];
+        uint8_t* o = a.packets + r * a.stride;
+        const uint8_t* c = a.cur + r * a.W;
+        const uint8_t* d = a.old + r * a.W;
+        if (lane < 10) {
+            const int32_t* h = a.hdr + 4 * r;
+            uint8_t v;
+            switch (lane) {
+                case 0: v = static_cast<uint8_t>((r >> 24) & 0xff); break;
+                case 1: v = static_cast<uint8_t>((r >> 16) & 0xff); break;
+                case 2: v = static_cast<uint8_t>((r >> 8) & 0xff); break;
+                case 3: v = static_cast<uint8_t>(r & 0xff); break;
+                case 8: v = static_cast<uint8_t>((lc - lc % 256) / 256); break;
+                case 9: v = static_cast<uint8_t>(lc % 256); break;
+                default: v = static_cast<uint8_t>(h[lane - 4]); break;
+            }
+            o[lane] = v;
+        }
+        for (int b = lane; b < lc; b += 64) o[10 + b] = c[b];
+        for (int b = lane; b < lo; b += 64) o[10 + lc + b] = d[b];
+        if (lane == 0) a.packet_len[r] = 10 + lc + lo;
+    }
+}
+
+__global__ __launch_bounds__(256) void fec_vr_parse_kernel(VrParseArgs a) {
+    const int lane = threadIdx.x & 63;
+    for (int64_t r = static_cast<int64_t>(blockIdx.x) * 4 + (threadIdx.x >> 6); r < a.rows;
+         r += static_cast<int64_t>(gridDim.x) * 4) {
+        const uint8_t* p = a.packets + r * a.stride;
+        const int plen = a.packet_len[r];
+        const int lc = plen >= 10 ? p[8] * 256 + p[9] : 0;
+        const int64_t lo = plen - 10 - lc;
+        uint8_t* c = a.cur + r * a.W;
+        uint8_t* d = a.old + r * a.W;
+        for (int64_t b = lane; b < a.W; b += 64) {
+            c[b] = b < lc ? p[10 + b] : 0;
+            d[b] = b < lo ? p[10 + lc + b] : 0;
+        }
+        if (a.hdr && lane == 0) {
+            int32_t* h = a.hdr + 5 * r;
+            h[0] = (p[0] << 24) | (p[1] << 16) | (p[2] << 8) | p[3];
+            h[1] = p[4];
+            h[2] = p[5];
+            h[3] = p[6];
+            h[4] = p[7];
+        }
+    }
+}
 
 __global__ __launch_bounds__(256) void fec_vr_gather_kernel(VrGatherArgs a) {
     const int L4 = a.L >> 2;
@@ -131,6 +187,22 @@ __global__ __launch_bounds__(256) void fec_vr_recover_kernel(VrRecArgs a) {
 unsigned grid_for(int64_t work) { return static_cast<unsigned>(std::max<int64_t>(1, std::min<int64_t>((work + 255) / 256, 8192))); }
 
 }  // namespace
+
+int vr_launch_frames(const VrFrameArgs& a, void* s) {
+    if (a.rows <= 0) return FEC_OK;
+    const int64_t blocks = std::min<int64_t>((a.rows + 3) / 4, 16384);
+    hipLaunchKernelGGL(fec_vr_frame_kernel, dim3(static_cast<unsigned>(blocks)), dim3(256), 0,
+                       static_cast<hipStream_t>(s), a);
+    return hipGetLastError() == hipSuccess ? FEC_OK : FEC_ERR_HIP;
+}
+
+int vr_launch_parse(const VrParseArgs& a, void* s) {
+    if (a.rows <= 0) return FEC_OK;
+    const int64_t blocks = std::min<int64_t>((a.rows + 3) / 4, 16384);
+    hipLaunchKernelGGL(fec_vr_parse_kernel, dim3(static_cast<unsigned>(blocks)), dim3(256), 0,
+                       static_cast<hipStream_t>(s), a);
+    return hipGetLastError() == hipSuccess ? FEC_OK : FEC_ERR_HIP;
+}
 
 int vr_launch_gather(const VrGatherArgs& a, void* s) {
     if (a.nrows <= 0) return FEC_OK;

@@ -97,3 +97,35 @@ class VrPlan:
         check(lib().fec_vr_decode_batch(self._h, _ptr(cw_cur), _ptr(cw_old), _ptr(erased), _ptr(out), _ptr(out_len),
                                         _stream_handle(torch)), "fec_vr_decode_batch")
         return out, out_len
+
+    # -- wire framing above the boundary ---------------------------------------------------------
+    def frames(self, cw_cur, len_cur, cw_old, len_old, packets=None, packet_len=None):
+        """The P2P wire packets the sender emits (Application_Layer_Sender.cpp:259-269 +
+        Variable_Rate_FEC_Encoder.cpp:194-217): rows [sent, 10 + 2*cw_max] uint8 and sizes [sent]."""
+        import torch
+        stride = 10 + 2 * self.cw_max
+        dev = cw_cur.device
+        if packets is None:
+            packets = torch.zeros((self.sent, stride), dtype=torch.uint8, device=dev)
+        if packet_len is None:
+            packet_len = torch.empty(self.sent, dtype=torch.int32, device=dev)
+        assert packets.shape == (self.sent, stride) and packets.is_contiguous() and packet_len.numel() >= self.sent
+        check(lib().fec_vr_frames_batch(self._h, _ptr(cw_cur), _ptr(len_cur), _ptr(cw_old), _ptr(len_old),
+                                        _ptr(packets), stride, _ptr(packet_len), _stream_handle(torch)),
+              "fec_vr_frames_batch")
+        return packets, packet_len
+
+
+def parse_packets(packets, packet_len, cw_max: int):
+    """The receiver's split of P2P wire packets (rows [R, stride] uint8 on the GPU) into the current
+    / old codewords (zero-padded to cw_max) and header fields [R, 5] (seq, T, B, N, counter)."""
+    import torch
+    assert packets.dtype == torch.uint8 and packets.is_cuda and packets.is_contiguous() and packets.dim() == 2
+    R = packets.shape[0]
+    assert packet_len.dtype == torch.int32 and packet_len.numel() >= R
+    cur = torch.empty((R, cw_max), dtype=torch.uint8, device=packets.device)
+    old = torch.empty((R, cw_max), dtype=torch.uint8, device=packets.device)
+    hdr = torch.empty((R, 5), dtype=torch.int32, device=packets.device)
+    check(lib().fec_vr_parse_batch(_ptr(packets), packets.shape[1], _ptr(packet_len), R, cw_max, _ptr(cur), _ptr(old),
+                                   _ptr(hdr), _stream_handle(torch)), "fec_vr_parse_batch")
+    return cur, old, hdr

@@ -208,6 +208,20 @@ int fec_vr_encode_batch(fec_vr_plan *plan, const uint8_t *d_payload, const int32
                         void *hip_stream);
 int fec_vr_decode_batch(fec_vr_plan *plan, const uint8_t *d_cw_cur, const uint8_t *d_cw_old,
                         const uint8_t *d_erased, uint8_t *d_out, int32_t *d_out_len, void *hip_stream);
+/* Wire framing above the boundary.  Sender: row s of d_packets (stride >= 10 + 2*cw_max) = the P2P
+ * packet Application_Layer_Sender sends (Application_Layer_Sender.cpp:259-269): [seq BE32][T][B][N]
+ * [counter_for_start_and_end] + Variable_Rate_FEC_Encoder's frame (Variable_Rate_FEC_Encoder.cpp:
+ * 194-217): [size_current BE16][codeword_current (trimmed)][codeword_old (trimmed)]; sizes in
+ * d_packet_len.  Receiver (no plan needed): the split of rows packets into the current / old
+ * codewords, zero-padded to cw_max bytes (Application_Layer_Receiver.cpp:361-366,
+ * Variable_Rate_FEC_Decoder.cpp:2156-2160), header fields to d_header (rows x 5 int32: seq, T, B,
+ * N, counter; may be NULL). */
+int fec_vr_frames_batch(fec_vr_plan *plan, const uint8_t *d_cw_cur, const int32_t *d_len_cur,
+                        const uint8_t *d_cw_old, const int32_t *d_len_old, uint8_t *d_packets,
+                        int64_t stride, int32_t *d_packet_len, void *hip_stream);
+int fec_vr_parse_batch(const uint8_t *d_packets, int64_t stride, const int32_t *d_packet_len, int64_t rows,
+                       int cw_max, uint8_t *d_cw_cur, uint8_t *d_cw_old, int32_t *d_header,
+                       void *hip_stream);
 
 /* ---- relay: symbol-wise decode-and-forward (SWDF, RELAYING_TYPE 2) ---------------------------
  * Decoder_Symbol_Wise (src/Decoder_Symbol_Wise.cpp) as the relay and the destination drive it

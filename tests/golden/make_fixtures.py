@@ -12,8 +12,12 @@ Outputs computed by the oracle restatement (oracle/, pinned by the published log
       SHA-256 digests of encoder outputs for the synthetic payload generator;
   config_vectors.json: BASELINE config 1 ((10,3,3), 361000 packets, i.i.d. erasures from
       generate_IID(361010, eps, seed 0) for eps = 1e-4 and 1e-2: erased/lost lists and digests of
-      the oracle's decoded lengths and bytes) and config 2 (SHA-256 of the oracle's 1,000,010
-      (10,3,3) codewords and wire sizes, the bench's encoded batch).
+      the oracle's decoded lengths and bytes), config 2 (SHA-256 of the oracle's 1,000,010
+      (10,3,3) codewords and wire sizes, the bench's encoded batch) and config 4 (the adaptive P2P
+      loop on bin/erasure.bin: lost list, switches, coding rate, digests of the outputs and of the
+      P2P wire packets; lost counts on erasure10/50/90);
+  published_adaptive_logs.json: the adaptive experiment logs' final numbers (not reproducible
+      with the current code, see tests/test_vr.py).
 
 Usage:  python tests/golden/make_fixtures.py [/root/reference]
 """
@@ -76,6 +80,29 @@ def parse_logs(ref: str) -> None:
                    "runs": out}, f, indent=1)
 
 
+def parse_adaptive_logs(ref: str) -> None:
+    """Experimental_Logs/Logs/Adaptive: receiver "Final FEC/UDP loss rate", sender "Final coding
+    rate".  Recorded for reference: the adaptive runs predate the current estimator and do not
+    reproduce with the current code; tests/test_vr.py documents the comparison."""
+    out = []
+    base = os.path.join(ref, "Experimental_Logs/Logs/Adaptive")
+    for pct in range(10, 101, 10):
+        rx = open(os.path.join(base, f"{pct}-Congestion-Austin-MiamiReceiver-Adaptive.rtf"), "rb").read().decode("latin-1")
+        tx = open(os.path.join(base, f"{pct}-Congestion-Miami-AustinSender-Adaptive.rtf"), "rb").read().decode("latin-1")
+        fec = re.findall(r"Final FEC loss rate = ([0-9.e-]+)", rx)
+        udp = re.findall(r"Final UDP loss rate = ([0-9.e-]+)", rx)
+        rate = re.findall(r"Final coding rate = ([0-9.e-]+)", tx)
+        raw = np.fromfile(os.path.join(ref, f"Experimental_Logs/erasure{pct}.bin"), dtype=np.uint8)
+        out.append({"pattern": f"erasure{pct}",
+                    "receiver_log": f"Experimental_Logs/Logs/Adaptive/{pct}-Congestion-Austin-MiamiReceiver-Adaptive.rtf",
+                    "fec_loss_rate": float(fec[-1]), "udp_loss_rate": float(udp[-1]),
+                    "lost_packets": int(round(float(fec[-1]) * 360000)),
+                    "udp_matches_pattern": int(round(float(udp[-1]) * 360000)) == int(raw[:360000].sum()),
+                    "coding_rates": [float(x) for x in rate]})
+    with open(os.path.join(HERE, "published_adaptive_logs.json"), "w") as f:
+        json.dump({"packets": 360000, "runs": out}, f, indent=1)
+
+
 def oracle_vectors() -> None:
     import oracle
     pats = np.load(os.path.join(HERE, "erasure_patterns.npz"))
@@ -112,6 +139,33 @@ def config_vectors() -> None:
             "lost": np.flatnonzero(r["out_len"] == 0).tolist(),
             "out_len_sha256": hashlib.sha256(r["out_len"].astype("<i4").tobytes()).hexdigest(),
             "out_data_sha256": hashlib.sha256(r["out_data"].tobytes()).hexdigest()}
+    # config 4: the adaptive P2P loop (oracle.vr_run: reference-structured, real bytes) on
+    # bin/erasure.bin, P = 360000
+    pats = np.load(os.path.join(HERE, "erasure_patterns.npz"))
+
+    def pattern(name):
+        return np.unpackbits(pats[name])[: int(pats[name + "_len"][0])]
+
+    r = oracle.vr_run(pattern("bin_erasure"), 360000, want_data=True, max_sent=360010,
+                      packets_cap=1 << 30)
+    off = r["packet_off"]
+    vec["config4"] = {
+        "pattern": "bin_erasure", "packets": 360000, "T": 10, "B": -1, "N": -1, "adaptive_mode_MDS": False,
+        "lost": np.flatnonzero(r["out_len"] == 0).tolist(), "switches": r["switches"], "sent": r["sent"],
+        "coding_rate": r["coding_rate"],
+        "out_len_sha256": hashlib.sha256(r["out_len"].astype("<i4").tobytes()).hexdigest(),
+        "out_data_sha256": hashlib.sha256(r["out_data"].tobytes()).hexdigest(),
+        "wire_packets": int(len(off) - 1),
+        "wire_bytes": int(off[-1]),
+        "wire_sha256": hashlib.sha256(r["packets"].tobytes()).hexdigest(),
+        "wire_len_sha256": hashlib.sha256(np.diff(off).astype("<i4").tobytes()).hexdigest(),
+        "first_wire_packets": [r["packets"][off[i]:off[i + 1]].tolist() for i in range(3)]}
+    vec["config4_other_patterns"] = {}
+    for name in ("erasure10", "erasure50", "erasure90"):
+        r = oracle.vr_run(pattern(name), 360000)
+        vec["config4_other_patterns"][name] = {
+            "lost": r["lost"], "switches": r["switches"], "coding_rate": r["coding_rate"],
+            "lost_sha256": hashlib.sha256(np.flatnonzero(r["out_len"] == 0).astype("<i4").tobytes()).hexdigest()}
     P2 = 1_000_010
     e = oracle.encode_stream(300, 10, 3, 3, 0, P2, seed=0x5EED)
     vec["config2"] = {"T": 10, "B": 3, "N": 3, "packets": P2,
@@ -128,5 +182,6 @@ if __name__ == "__main__":
         pack_patterns(ref)
         parse_logs(ref)
         oracle_vectors()
+    parse_adaptive_logs(ref)
     config_vectors()
     print("fixtures written to", HERE)

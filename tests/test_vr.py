@@ -1,17 +1,32 @@
 """Variable-rate (adaptive) coding, BASELINE config 4 (fec_vr.cpp).
 
-The control plane is pinned by the reference's own runs recorded in SURVEY.md §8(d)/(c): on
-bin/erasure.bin with P = 360000 the adaptive P2P loop loses 2982 packets, switches (T,B,N) 1933 times
-("Start double coding at the source") at a final coding rate of 0.822 using the tuples (10,b,b),
-b in {0,1,2,5..10}; the fixed-rate full stack loses 4662 packets at (10,3,3) and 565 at (10,5,2),
-the same as the FEC-level decoder.  The GPU test runs the schedule's byte work and checks every
-reported packet against its source."""
+Pins, strongest first:
+  * per packet: the oracle's reference-structured restatement of the whole P2P loop on real bytes
+    (oracle/fec_oracle.c or_vr_run: sender, Variable_Rate_FEC_Encoder with double coding, the
+    Parameter_Estimator pair, Variable_Rate_FEC_Decoder over FEC_Decoder objects) -- its lost list,
+    output digests and P2P wire-packet digests on bin/erasure.bin are committed in
+    tests/golden/config_vectors.json (made by tests/golden/make_fixtures.py);
+  * the reference's own runs recorded in SURVEY.md §8(c)/(d) (the reference compiled with an ISA-L
+    restatement in the survey container): bin/erasure.bin -> 2982 lost, 1933 switches, coding rate
+    0.822, tuples (10,b,b) for b in {0,1,2,5..10}; erasure10 / 50 / 90 -> FEC loss rate 0.000725 /
+    0.00688 / 0.0238;
+  * the published adaptive experiment logs (Experimental_Logs/Logs/Adaptive) do NOT reproduce: their
+    UDP losses equal the shipped patterns, but they were recorded before the estimator changed
+    (SURVEY §8(c)); test_published_adaptive_logs_are_not_the_current_code records the gap."""
 import numpy as np
 import pytest
 
-from conftest import load_pattern
+import hashlib
+
+import oracle
+from conftest import load_json, load_pattern
 from fec_erasure_code_unit_test_relay_amd import plan_host
-from fec_erasure_code_unit_test_relay_amd.vr import VrPlan
+from fec_erasure_code_unit_test_relay_amd.vr import VrPlan, parse_packets
+
+
+@pytest.fixture(scope="module")
+def c4():
+    return load_json("config_vectors.json")["config4"]
 
 
 @pytest.fixture(scope="module")
@@ -27,6 +42,48 @@ def test_adaptive_matches_reference_run(adaptive):
     assert v.tuples() == {(10, b, b) for b in (0, 1, 2, 5, 6, 7, 8, 9, 10)}
     assert int((v.fate == 3).sum()) == v.lost and v.fate.min() >= 1  # every packet reported once
     assert v.sent == 360010
+
+
+def test_adaptive_plan_equals_oracle_per_packet(adaptive, c4):
+    """The product's symbolic plan reports exactly the packets the oracle's byte-level P2P loop
+    loses (2982 indices), with the same switch count, packets sent and coding rate."""
+    v = adaptive
+    assert np.flatnonzero(v.fate == 3).tolist() == c4["lost"]
+    assert v.switches == c4["switches"] and v.sent == c4["sent"]
+    assert abs(v.coding_rate - c4["coding_rate"]) < 1e-6
+
+
+def test_oracle_vr_loop_prefix_equals_plan():
+    """Live (not from the fixture): the oracle's P2P loop and the plan on a 30000-packet prefix of
+    another pattern, per packet."""
+    pat = load_pattern("bin_erasure2")
+    r = oracle.vr_run(pat, 30000)
+    v = VrPlan(pat, 30000)
+    assert ((r["out_len"] == 0) == (v.fate == 3)).all()
+    assert r["switches"] == v.switches and r["sent"] == v.sent and abs(r["coding_rate"] - v.coding_rate) < 1e-6
+
+
+@pytest.mark.parametrize("name,rate", [("erasure10", 0.000725), ("erasure50", 0.00688), ("erasure90", 0.0238)])
+def test_adaptive_other_patterns_match_survey_reference_runs(name, rate):
+    """The survey ran the reference itself on these patterns: its FEC loss rates,
+    to the digits it recorded, and the oracle's lost sets (config_vectors.json)."""
+    want = load_json("config_vectors.json")["config4_other_patterns"][name]
+    v = VrPlan(load_pattern(name), 360000)
+    assert v.lost == want["lost"] and v.switches == want["switches"]
+    lost = np.flatnonzero(v.fate == 3).astype("<i4")
+    assert hashlib.sha256(lost.tobytes()).hexdigest() == want["lost_sha256"]
+    assert float(f"{v.lost / 360000:.3g}") == rate
+
+
+def test_published_adaptive_logs_are_not_the_current_code():
+    """Experimental_Logs/Logs/Adaptive: same erasure patterns (UDP loss = the pattern's erasures),
+    different FEC loss than the current adaptation code gives -- the logs predate the estimator
+    now in the reference; the erasure10 run is the closest (250 vs 261 packets)."""
+    runs = load_json("published_adaptive_logs.json")["runs"]
+    assert all(r["udp_matches_pattern"] for r in runs)
+    r10 = next(r for r in runs if r["pattern"] == "erasure10")
+    v = VrPlan(load_pattern("erasure10"), 360000)
+    assert r10["lost_packets"] == 250 and v.lost == 261
 
 
 def test_schedule_structure(adaptive):
@@ -124,3 +181,33 @@ def test_gpu_schedule_round_trip_other_patterns(pattern, mds):
     ok = torch.from_numpy(v.fate != 3).cuda()
     assert int((out_len == 0).sum()) == v.lost
     assert bool((out[ok] == payload[:P][ok]).all()) and bool((out_len[ok] == 300).all())
+
+
+@pytest.mark.gpu
+def test_gpu_adaptive_wire_packets_and_outputs_equal_oracle(adaptive, c4):
+    """Sender -> wire -> receiver on the GPU: the P2P wire packets the product frames equal the
+    oracle's byte for byte (SHA-256 over all 360 010 packets), and the receiver's split of them
+    decodes to exactly the oracle's outputs (lengths and bytes, SHA-256) and lost list."""
+    import torch
+    from fec_erasure_code_unit_test_relay_amd import fill_payload
+    torch.cuda.set_device(0)
+    v = adaptive
+    payload = fill_payload(0, v.sent, 300, 0x5EED)
+    cw_cur, len_cur, cw_old, len_old = v.encode(payload)
+    packets, plen = v.frames(cw_cur, len_cur, cw_old, len_old)
+    torch.cuda.synchronize()
+    pk, pl = packets.cpu().numpy(), plen.cpu().numpy()
+    assert int(pl.sum()) == c4["wire_bytes"]
+    assert hashlib.sha256(pl.astype("<i4").tobytes()).hexdigest() == c4["wire_len_sha256"]
+    mask = np.arange(pk.shape[1])[None, :] < pl[:, None]
+    assert hashlib.sha256(pk[mask].tobytes()).hexdigest() == c4["wire_sha256"]
+    for i, want in enumerate(c4["first_wire_packets"]):
+        assert pk[i, :pl[i]].tolist() == want
+    cur, old, hdr = parse_packets(packets, plen, v.cw_max)
+    assert bool((hdr[:, 0] == torch.arange(v.sent, device="cuda", dtype=torch.int32)).all())
+    out, out_len = v.decode(cur, old)
+    torch.cuda.synchronize()
+    ol = out_len.cpu().numpy()
+    assert np.flatnonzero(ol == 0).tolist() == c4["lost"]
+    assert hashlib.sha256(ol.astype("<i4").tobytes()).hexdigest() == c4["out_len_sha256"]
+    assert hashlib.sha256(out.cpu().numpy().tobytes()).hexdigest() == c4["out_data_sha256"]
