@@ -99,7 +99,7 @@ class VrPlan:
         return out, out_len
 
     # -- wire framing above the boundary ---------------------------------------------------------
-    def frames(self, cw_cur, len_cur, cw_old, len_old, packets=None, packet_len=None):
+    def wire_packets(self, cw_cur, len_cur, cw_old, len_old, packets=None, packet_len=None):
         """The P2P wire packets the sender emits (Application_Layer_Sender.cpp:259-269 +
         Variable_Rate_FEC_Encoder.cpp:194-217): rows [sent, 10 + 2*cw_max] uint8 and sizes [sent]."""
         import torch

@@ -194,7 +194,7 @@ def test_gpu_adaptive_wire_packets_and_outputs_equal_oracle(adaptive, c4):
     v = adaptive
     payload = fill_payload(0, v.sent, 300, 0x5EED)
     cw_cur, len_cur, cw_old, len_old = v.encode(payload)
-    packets, plen = v.frames(cw_cur, len_cur, cw_old, len_old)
+    packets, plen = v.wire_packets(cw_cur, len_cur, cw_old, len_old)
     torch.cuda.synchronize()
     pk, pl = packets.cpu().numpy(), plen.cpu().numpy()
     assert int(pl.sum()) == c4["wire_bytes"]
