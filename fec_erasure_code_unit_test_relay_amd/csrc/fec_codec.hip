@@ -53,13 +53,18 @@ struct fec_codec {
     const void* persist_kernel = nullptr;  // streaming encode (fec_encode_persist.hip)
     int persist_tp = 0;
     int persist_wgs = 0;                   // resident workgroups of it on the device
-    int encode_path = 0;         // 0 auto, 1 generic, 2 specialised, 3 streaming, 4 wave
+    int encode_path = 0;         // 0 auto, 1 generic, 2 specialised, 3 streaming, 4 wave, 5 tile
     const void* wave_kernel = nullptr;  // wave-private sequence encode (fec_encode_wave.hip)
     int wave_slots = 0;                 // resident waves of it on the device
     int wave_ring = 0;                  // bytes of its per-sequence LDS output ring
     int wave_lds = 0;                   // its dynamic LDS per workgroup
     int wave_pad = 0;                   // 1: per-sequence ring padding (LDS bank spread)
     int wave_cus = 0;                   // compute units of the device
+    const void* tile_kernel = nullptr;  // contiguous-chunk LDS-tile encode (fec_encode_tile.hip)
+    int tile_ppw = 0;                   // its packets per wave slice (tile = 4 * tile_ppw packets)
+    int tile_lds = 0, tile_lds_len = 0; // its dynamic LDS per workgroup (without / with lengths)
+    int tile_per_cu = 0;                // its resident workgroups per CU
+    int tile_off[8] = {};               // off_in, in_bytes, off_pw, off_q, off_out, off_len, ngl, nso
     const void* copy_fast = nullptr;  // specialised decode copy kernel (LDS tiles)
     int copyf_tp = 0;
     const void* copy_wave = nullptr;  // barrier-free decode copy (fec_copy_wave.hip)
@@ -268,6 +273,52 @@ int codec_init(fec_codec* c, int max_payload, int T, int B, int N) {
         HIP_TRY(hipGetDevice(&dev));
         HIP_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
         if (!c->wave_cus) c->wave_cus = cus;
+    }
+    if ((g.L & 3) == 0 && g.n - g.k >= 0) {
+        // tile encode: a wave slice holds whole packets (PPW * NS4 <= 64) whose codewords end on a
+        // dword (PPW * CW % 4 == 0), and a tile (4 * PPW packets) covers the n-1 packets of parity
+        // history, so that the parity rows move down by one tile
+        const int ns4 = c->ns4();
+        const int unit = (g.CW & 3) == 0 ? 1 : ((g.CW & 1) == 0 ? 2 : 4);
+        int ppw = ns4 > 0 ? (64 / ns4) / unit * unit : 0;
+        if (ppw > 0 && 4 * ppw >= g.n - 1) c->tile_kernel = fec::fec_encode_tile_kernel_for(g.k, g.n - g.k);
+        if (c->tile_kernel) {
+            const int R = 4 * ppw;
+            const int ngl = (R * g.L + 4 * g.k + 8 + 4095) / 4096;
+            const int pws = g.k | 1;
+            const int rows = R + g.n - 1;
+            const int npa = std::max(1, g.n - g.k);
+            auto al16 = [](int x) { return (x + 15) & ~15; };
+            int off = 64;  // guard in front of the input buffers (the first row's dword -1)
+            const int in_bytes = ngl * 4096;
+            const int off_in = off;
+            off += 2 * in_bytes;
+            const int off_pw = off;
+            off = al16(off + 4 * R * ns4 * pws);
+            const int off_q = off;
+            off = al16(off + 4 * npa * rows * ns4);
+            const int off_out = off;
+            off = al16(off + R * g.CW);
+            c->tile_lds = off;
+            c->tile_lds_len = off + 2048;
+            c->tile_ppw = ppw;
+            c->tile_off[0] = off_in;
+            c->tile_off[1] = in_bytes;
+            c->tile_off[2] = off_pw;
+            c->tile_off[3] = off_q;
+            c->tile_off[4] = off_out;
+            c->tile_off[5] = off;  // lengths (only with a length array)
+            c->tile_off[6] = ngl;
+            c->tile_off[7] = (R * g.CW / 16 + 255) / 256;
+            if (c->tile_lds_len > 160 * 1024) c->tile_kernel = nullptr;
+        }
+        if (c->tile_kernel) {
+            HIP_TRY(hipFuncSetAttribute(c->tile_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, c->tile_lds_len));
+            int per_cu = 0;
+            HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, c->tile_kernel, 256, c->tile_lds));
+            c->tile_per_cu = per_cu;
+            if (per_cu <= 0) c->tile_kernel = nullptr;
+        }
     }
     if ((g.L & 3) == 0) c->copy_fast = fec::fec_copy_fast_kernel_for(g.k, g.n - g.k);
     // The copy stages its whole tile, converts, then stores (no overlap inside a workgroup), so
@@ -488,9 +539,76 @@ int launch_encode_wave(fec_codec* c, const uint8_t* d_payload, const int32_t* d_
     return c->end(stop, s);
 }
 
+int launch_encode_tile(fec_codec* c, const uint8_t* d_payload, const int32_t* d_len, int64_t history,
+                       int64_t P, uint8_t* d_cw, int32_t* d_cwlen, hipStream_t s) {
+    const Geometry& g = c->g;
+    history = std::min<int64_t>(std::max<int64_t>(0, history), g.n - 1);
+    const int R = 4 * c->tile_ppw;
+    // 32-bit buffer offsets: batches beyond 2 GB go in chunks of whole tiles (each chunk sees the
+    // n-1 rows in front of it as history; the chunk start stays 16-byte aligned in the output)
+    const int64_t max_rows = ((int64_t(0x7fffffff) - 65536) / std::max(g.L, g.CW) - g.n) / R * R;
+    if (history + P > max_rows) {
+        const int64_t chunk = max_rows - R;
+        for (int64_t r = 0; r < P; r += chunk) {
+            const int64_t h = std::min<int64_t>(history + r, g.n - 1);
+            if (int st = launch_encode_tile(c, d_payload + r * g.L, d_len ? d_len + r : nullptr, h,
+                                            std::min(chunk, P - r), d_cw + r * g.CW, d_cwlen + r, s))
+                return st;
+        }
+        return FEC_OK;
+    }
+    fec::EncTileArgs a;
+    a.payload_base = d_payload - history * g.L;
+    a.len_base = d_len ? d_len - history : nullptr;
+    a.payload_bytes = static_cast<int>((history + P) * g.L);
+    a.len_bytes = static_cast<int>((history + P) * 4);
+    a.history = static_cast<int>(history);
+    a.P = static_cast<int>(P);
+    a.cw = d_cw;
+    a.cw_bytes = static_cast<int>(P * g.CW);
+    a.cw_len = d_cwlen;
+    a.ptab = c->d_ptab;
+    a.L = g.L;
+    a.CW = g.CW;
+    a.NS4 = c->ns4();
+    a.PPW = c->tile_ppw;
+    a.rem = g.S - 4 * (a.NS4 - 1);
+    a.nvl = g.L / 4 - g.k * (a.NS4 - 1);
+    const int64_t ntiles = (P + R - 1) / R;
+    // one wave of resident workgroups, each a contiguous run of tiles (plus the tile in front)
+    int64_t slots = static_cast<int64_t>(std::max(1, c->wave_cus)) * c->tile_per_cu;
+    if (const char* v = std::getenv("FEC_TILE_WPC"))
+        slots = static_cast<int64_t>(std::max(1, c->wave_cus)) * std::max(1, std::min(c->tile_per_cu, std::atoi(v)));
+    const int64_t tpw = (ntiles + slots - 1) / slots;
+    a.tiles_per_wg = static_cast<int>(tpw);
+    a.ntiles = static_cast<int>(ntiles);
+    a.off_in = c->tile_off[0];
+    a.in_bytes = c->tile_off[1];
+    a.off_pw = c->tile_off[2];
+    a.off_q = c->tile_off[3];
+    a.off_out = c->tile_off[4];
+    a.off_len = c->tile_off[5];
+    a.ngl = c->tile_off[6];
+    a.nso = c->tile_off[7];
+    const int64_t blocks = (ntiles + tpw - 1) / tpw;
+    hipEvent_t stop;
+    if (int st = c->begin(FEC_KERNEL_ENCODE, s, &stop)) return st;
+    void* args[] = {&a};
+    HIP_TRY(hipLaunchKernel(c->tile_kernel, dim3(static_cast<unsigned>(blocks)), dim3(256), args,
+                            d_len ? c->tile_lds_len : c->tile_lds, s));
+    return c->end(stop, s);
+}
+
 int launch_encode(fec_codec* c, const uint8_t* d_payload, const int32_t* d_len, int64_t history,
                   int64_t P, uint8_t* d_cw, int32_t* d_cwlen, hipStream_t s) {
     if (P <= 0) return FEC_OK;
+    {
+        const bool tile_ok = c->tile_kernel && (reinterpret_cast<uintptr_t>(d_payload) & 3) == 0 &&
+                             (reinterpret_cast<uintptr_t>(d_cw) & 15) == 0;
+        if (c->encode_path == 5 && !tile_ok) return FEC_ERR_ARG;
+        if (tile_ok && c->encode_path == 5)
+            return launch_encode_tile(c, d_payload, d_len, history, P, d_cw, d_cwlen, s);
+    }
     const Geometry& g = c->g;
     const bool wave_ok = c->wave_kernel && (reinterpret_cast<uintptr_t>(d_payload) & 3) == 0 &&
                          (reinterpret_cast<uintptr_t>(d_cw) & 3) == 0;
@@ -974,7 +1092,9 @@ int fec_codec_info(const fec_codec* c, char* buf, size_t size) {
     // kernel symbol the encoder launches for a 16-byte aligned payload (rocprofv3 naming)
     char enc[64];
     const int np = c->g.n - c->g.k;
-    if (c->wave_kernel && (c->encode_path == 0 || c->encode_path == 4))
+    if (c->tile_kernel && c->encode_path == 5)
+        std::snprintf(enc, sizeof(enc), "fec_encode_tile_kernel<%d, %d>", c->g.k, np);
+    else if (c->wave_kernel && (c->encode_path == 0 || c->encode_path == 4))
         std::snprintf(enc, sizeof(enc), "fec_encode_wave_kernel<%d, %d>", c->g.k, np);
     else if (c->persist_kernel && (c->encode_path == 0 || c->encode_path == 3))
         std::snprintf(enc, sizeof(enc), "fec_encode_persist_kernel<%d, %d>", c->g.k, np);
@@ -1040,7 +1160,8 @@ int fec_codec_set_copy_path(fec_codec* c, int path) {
 }
 
 int fec_codec_set_encode_path(fec_codec* c, int path) {
-    if (!c || path < 0 || path > 4) return FEC_ERR_ARG;
+    if (!c || path < 0 || path > 5) return FEC_ERR_ARG;
+    if (path == 5 && !c->tile_kernel) return FEC_ERR_ARG;
     if (path == 2 && !c->fast_kernel) return FEC_ERR_ARG;
     if (path == 3 && !c->persist_kernel) return FEC_ERR_ARG;
     if (path == 4 && !c->wave_kernel) return FEC_ERR_ARG;

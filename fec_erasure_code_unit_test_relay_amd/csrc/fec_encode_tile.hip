@@ -1,0 +1,449 @@
+// fec_encode_tile.hip -- encode kernel over contiguous packet chunks, staged through LDS tiles.
+//
+// Same closed form as every encode kernel here (fec_kernels.hip): for packet t, sub-stream s,
+//     cw_t[s*n + j] = X_t[s][j]                                   j <  k
+//     cw_t[s*n + j] = XOR_i G[i][j] * X_{t-(j-i)}[s][i]           j >= k
+// with X_t[s] = bytes [s*k, s*k+k) of [len_hi, len_lo, payload, zero pad] (Encoder.cpp:65-98,
+// Encoder_Basic.cpp:48-74, codingOperations.cpp:131-147).
+//
+// Organisation: a workgroup (4 waves) owns a contiguous run of tiles of R = 4*PPW packets and walks
+// it; only the tile in front of its first one is read twice (the n-1 packets of parity history), so
+// HBM reads are L bytes per packet plus ~1/tiles_per_wg.  Per tile:
+//   * the tile's payload rows (one contiguous R*L-byte slab) arrive in LDS by LDS-DMA
+//     (buffer_load ... lds), issued two tiles ahead: no registers hold loads in flight, and rows
+//     outside [-history, P) come back as zero (buffer range check) -- the X_{t'<t0} = 0 semantics;
+//   * A: item (p, g) = packet p of the tile, group g of 4 sub-streams; its thread builds the K
+//     window words H (header, zero pad) and the K position words (byte e of word i = position i of
+//     sub-stream 4g+e) and writes the position words to LDS;
+//   * B: parity forward: position word i of packet p contributes G[i][K+jj] * word to parity jj of
+//     packet p + (K+jj-i).  The K*NP (i, jj) products are split over the 4 waves at compile time, so
+//     a wave's coefficient tables stay in its registers for the whole kernel; each wave sweeps every
+//     item of the tile and XORs its products into the tile's parity rows in LDS (ds_xor, rows
+//     [0, R+n-1); the rows past R are the next tile's first n-1 packets);
+//   * C: item (p, g) reads its finished parity, interleaves the n codeword words of its 4
+//     sub-streams, shifts them to the packet's byte alignment (the bytes in front come from the lane
+//     to its left: every wave holds whole packets) and writes them into the LDS output tile; the
+//     parity rows move down by R;
+//   * D: the output tile (R*CW bytes, a multiple of 16 at a 16-byte aligned offset) goes to HBM in
+//     16-byte stores, 1 KB contiguous per wave instruction; one lane per packet computes the
+//     trimmed wire size (FEC_Encoder.cpp:55-60) from the LDS tile.
+// Three workgroup barriers per tile; several workgroups per CU overlap one another's phases.
+#include "fec_device.h"
+#include "fec_kernels.h"
+
+#include <utility>
+
+namespace fec {
+namespace {
+
+constexpr int kTileThreads = 256;
+
+template <typename F, int... Is>
+__device__ __forceinline__ void tfor_impl(F&& f, std::integer_sequence<int, Is...>) {
+    (f(std::integral_constant<int, Is>{}), ...);
+}
+template <int N, typename F>
+__device__ __forceinline__ void tfor(F&& f) {
+    tfor_impl(f, std::make_integer_sequence<int, N>{});
+}
+
+__device__ __forceinline__ uint32_t txor3(uint32_t a, uint32_t b, uint32_t c) {
+    return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
+}
+
+struct TSel {
+    uint32_t s0, s1, s2;
+};
+__device__ __forceinline__ TSel tsplit(uint32_t x) {
+    return {x & 0x07070707u, (x >> 3) & 0x07070707u, (x >> 6) & 0x03030303u};
+}
+struct TTab {
+    uint32_t x, y, z, w, t4;  // c*{0..7} (x: 0..3, y: 4..7), c*({0..7}<<3) (z, w), c*({0..3}<<6)
+};
+__device__ __forceinline__ uint32_t tprod(const TTab& t, const TSel& s) {
+    return txor3(__builtin_amdgcn_perm(t.y, t.x, s.s0), __builtin_amdgcn_perm(t.w, t.z, s.s1),
+                 __builtin_amdgcn_perm(t.t4, t.t4, s.s2));
+}
+
+__device__ __forceinline__ uint32_t tbperm(int src_lane, uint32_t v) {
+    return static_cast<uint32_t>(__builtin_amdgcn_ds_bpermute(src_lane << 2, static_cast<int>(v)));
+}
+
+// s_waitcnt vmcnt(n) (expcnt, lgkmcnt: no wait); n is a run-time value, the immediate is not
+__device__ __forceinline__ void wait_vm(int n) {
+#define FEC_VM_CASE(N) \
+    case N: __builtin_amdgcn_s_waitcnt((N & 15) | (7 << 4) | (15 << 8) | ((N >> 4) << 14)); break;
+    switch (n < 0 ? 0 : n) {
+        FEC_VM_CASE(0) FEC_VM_CASE(1) FEC_VM_CASE(2) FEC_VM_CASE(3) FEC_VM_CASE(4) FEC_VM_CASE(5)
+        FEC_VM_CASE(6) FEC_VM_CASE(7) FEC_VM_CASE(8) FEC_VM_CASE(9) FEC_VM_CASE(10) FEC_VM_CASE(11)
+        FEC_VM_CASE(12) FEC_VM_CASE(13) FEC_VM_CASE(14) FEC_VM_CASE(15) FEC_VM_CASE(16) FEC_VM_CASE(17)
+        FEC_VM_CASE(18) FEC_VM_CASE(19) FEC_VM_CASE(20) FEC_VM_CASE(21) FEC_VM_CASE(22) FEC_VM_CASE(23)
+        default: FEC_VM_CASE(24)
+    }
+#undef FEC_VM_CASE
+}
+
+__device__ __forceinline__ void wait_lds_barrier() {
+    __builtin_amdgcn_s_waitcnt((15) | (7 << 4) | (0 << 8) | (3 << 14));  // lgkmcnt(0) only
+    __builtin_amdgcn_s_barrier();
+}
+
+typedef __attribute__((address_space(3))) void* lds_void_ptr;
+
+// Codeword words of the group: bytes [e*n, e*n+n) = sub-stream 4g+e: K systematic bytes, NP parity.
+template <int K, int NP>
+__device__ __forceinline__ void tgroup_words(const uint32_t (&H)[K], const uint32_t (&Q)[NP > 0 ? NP : 1],
+                                             uint32_t (&X)[K + NP]) {
+    constexpr int n = K + NP;
+    uint32_t src[n];
+#pragma unroll
+    for (int m = 0; m < K; ++m) src[m] = H[m];
+#pragma unroll
+    for (int jj = 0; jj < NP; ++jj) src[K + jj] = Q[jj];
+    auto idx = [](int b) {
+        const int e = b / n, j = b % n;
+        return j < K ? (e * K + j) : (4 * (K + j - K) + e);
+    };
+#pragma unroll
+    for (int q = 0; q < n; ++q) X[q] = gather4(src, idx(4 * q), idx(4 * q + 1), idx(4 * q + 2), idx(4 * q + 3));
+}
+
+// Last 4 valid bytes of the group's words (bytes [vb-4, vb)), vb = n * REM for the last group.
+template <int n, int REM>
+__device__ __forceinline__ uint32_t ttail_rem(const uint32_t (&X)[n]) {
+    constexpr int b = n * REM - 4;
+    if constexpr (b < 0) {
+        return X[0] << (8 * (4 - n * REM));
+    } else if constexpr (b % 4 == 0) {
+        return X[b / 4];
+    } else {
+        return __builtin_amdgcn_alignbyte(X[b / 4 + 1], X[b / 4], b % 4);
+    }
+}
+
+template <int K, int NP, int W>
+__device__ __forceinline__ void tile_walk(const EncTileArgs& a, uint8_t* smem) {
+    constexpr int n = K + NP;
+    constexpr int NPA = NP > 0 ? NP : 1;
+    constexpr int KNP = K * NP;
+    constexpr int k0 = W * KNP / 4, k1 = (W + 1) * KNP / 4;  // this wave's (i, jj) products
+    constexpr int NPW = k1 - k0;
+    constexpr int NPWA = NPW > 0 ? NPW : 1;
+    constexpr int i_lo = NPW > 0 ? k0 / NPA : 0;
+    constexpr int i_hi = NPW > 0 ? (k1 - 1) / NPA : -1;
+    constexpr int PWS = K | 1;  // position words per item in LDS (odd: conflict-free item strides)
+
+    const int lane = threadIdx.x & 63;
+    const int tid = threadIdx.x;
+    const int L = a.L, CW = a.CW, NS4 = a.NS4, PPW = a.PPW, R = 4 * a.PPW, P = a.P;
+    const int last_g = NS4 - 1;
+    const int ipw = PPW * NS4;                 // items per wave slice
+    const bool active = lane < ipw;
+    const int pl = active ? lane / NS4 : 0;    // packet of the lane inside its wave slice
+    const int g = active ? lane - pl * NS4 : 0;
+    const int p = W * PPW + pl;                // own packet in the tile
+    const int item = p * NS4 + g;
+    const bool is_last = g == last_g;
+    const int ROWS = R + n - 1;
+    const int QJ = ROWS * NS4;                 // dwords per parity plane
+
+    // LDS carve-up (byte offsets from the launcher)
+    uint32_t* pw = reinterpret_cast<uint32_t*>(smem + a.off_pw);
+    uint32_t* q = reinterpret_cast<uint32_t*>(smem + a.off_q);
+    uint8_t* out = smem + a.off_out;
+    const uint32_t* lensl = reinterpret_cast<const uint32_t*>(smem + a.off_len);
+
+    // coefficient tables of this wave's products, in registers for the whole walk
+    TTab tab[NPWA];
+    tfor<NPW>([&](auto kc) __attribute__((always_inline)) {
+        constexpr int kk = k0 + decltype(kc)::value;
+        constexpr int I = kk / NPA, JJ = kk % NPA;
+        const uint32_t* t = a.ptab + (I * NP + JJ) * 8;
+        TTab& d = tab[decltype(kc)::value];
+        d = {t[0], t[1], t[2], t[3], t[4]};
+        // in VGPRs: scalar copies of 5 dwords per product would crowd out the SGPRs
+        asm volatile("" : "+v"(d.x), "+v"(d.y), "+v"(d.z), "+v"(d.w), "+v"(d.t4));
+    });
+
+    const __amdgpu_buffer_rsrc_t rs =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(a.payload_base), 0, a.payload_bytes, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rl =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<int32_t*>(a.len_base), 0, a.len_bytes, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rc = __builtin_amdgcn_make_buffer_rsrc(a.cw, 0, a.cw_bytes, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc(a.cw_len, 0, 4 * P, 0x00020000);
+    const bool has_len = a.len_base != nullptr;
+
+    const int first = blockIdx.x * a.tiles_per_wg;
+    const int cnt = min(a.tiles_per_wg, a.ntiles - first);  // real tiles of this workgroup (>= 1)
+    const int ngl = a.ngl;                                   // payload LDS-DMA instructions per wave per tile
+    const int nglt = ngl + (has_len ? 1 : 0);
+    const int nso = a.nso;                                   // 16-byte stores per thread per tile
+    const int ns = nso + 1;                                  // + the trimmed-size store
+
+    // tile it (0 = the tile in front of the first one) -> LDS input buffer (it & 1)
+    auto issue = [&](int it) __attribute__((always_inline)) {
+        const int row0 = (first - 1 + it) * R;
+        uint8_t* dst = smem + a.off_in + (it & 1) * a.in_bytes;
+        const int wv = tid >> 6;
+        const int base = (row0 + a.history) * L;  // may be negative: those chunks read as zero
+        for (int j = 0; j < ngl; ++j) {
+            const int c = (j * 4 + wv) * 64 + lane;
+            const int o = base + c * 16;
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(
+                rs, (lds_void_ptr)(dst + __builtin_amdgcn_readfirstlane((j * 4 + wv) * 1024)), 16,
+                static_cast<uint32_t>(o < 0 ? 0x7fffffff : o), 0, 0, 0);
+        }
+        if (has_len) {
+            uint8_t* ld = smem + a.off_len + (it & 1) * 1024 + __builtin_amdgcn_readfirstlane(wv * 256);
+            const int r = row0 + a.history + lane;
+            const bool ok = wv == 0 && lane < R && r >= 0;
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(rl, (lds_void_ptr)ld, 4,
+                                                     static_cast<uint32_t>(ok ? r * 4 : 0x7fffffff), 0, 0, 0);
+        }
+    };
+
+    // parity rows start zeroed
+    for (int x = tid; x < NPA * QJ; x += kTileThreads) q[x] = 0;
+
+    issue(0);
+    if (cnt >= 1) issue(1);
+
+    uint32_t H[K];
+    for (int it = 0; it <= cnt; ++it) {
+        // tile it's input: every VMEM instruction issued after it may still be in flight
+        {
+            const int s2 = it - 2 >= 1 ? ns : 0, s1 = it - 1 >= 1 ? ns : 0;
+            const int g1 = it + 1 <= cnt ? nglt : 0;
+            wait_vm(s2 + g1 + s1);
+        }
+        wait_lds_barrier();  // B1: the tile is in LDS everywhere; last tile's output stored
+        const int row0 = (first - 1 + it) * R;
+        const uint8_t* in = smem + a.off_in + (it & 1) * a.in_bytes;
+        const uint32_t* inw = reinterpret_cast<const uint32_t*>(in);
+        {
+            // A 16-byte piece straddling the start (history rows) or the end of the payload rows is
+            // out of range as a whole for the LDS-DMA (zeros): its valid dwords again, one by one
+            // (rare: the first / last tile of the batch when (history + P) * L % 16 != 0).
+            const int base = (row0 + a.history) * L;
+            const int span = ngl * 4096;
+            bool need = false;
+#pragma unroll
+            for (int e = 0; e < 2; ++e) {
+                const int B = e == 0 ? 0 : a.payload_bytes;
+                need |= B > base && B < base + span && ((B - base) & 15) != 0;
+            }
+            if (need) {
+                if (tid < 8) {
+                    const int e = tid >> 2;
+                    const int B = e == 0 ? 0 : a.payload_bytes;
+                    if (B > base && B < base + span && ((B - base) & 15) != 0) {
+                        const int c = (B - base) >> 4;
+                        const int off = base + 16 * c + 4 * (tid & 3);
+                        if (off >= 0 && off < a.payload_bytes)
+                            reinterpret_cast<uint32_t*>(smem + a.off_in + (it & 1) * a.in_bytes)[4 * c + (tid & 3)] =
+                                __builtin_amdgcn_raw_buffer_load_b32(rs, off, 0, 0);
+                    }
+                }
+                wait_vm(0);
+                wait_lds_barrier();
+            }
+        }
+
+        // ---- A: window words and position words of the own item
+        if (active) {
+            const int t = row0 + p;
+            int ln;
+            if (t < -a.history || t >= P) {
+                ln = 0;
+            } else if (has_len) {
+                const int v = static_cast<int>(lensl[(it & 1) * 256 + p]);
+                ln = v < 0 ? 0 : (v > L ? L : v);
+            } else {
+                ln = L;
+            }
+            const int rdw = (p * L >> 2) + K * g - 1;  // row dword K*g - 1
+            uint32_t D[K + 1];
+#pragma unroll
+            for (int m = 0; m <= K; ++m) D[m] = inw[rdw + m];
+            const uint32_t hdr =
+                (static_cast<uint32_t>(ln & 0xff) << 24) | (static_cast<uint32_t>((ln >> 8) & 0xff) << 16);
+            D[0] = g == 0 ? hdr : D[0];
+#pragma unroll
+            for (int m = 0; m < K; ++m)  // the last group's dwords past the row end: zero pad
+                if (m >= a.nvl) D[m + 1] = is_last ? 0u : D[m + 1];
+#pragma unroll
+            for (int m = 0; m < K; ++m) H[m] = __builtin_amdgcn_alignbyte(D[m + 1], D[m], 2);
+            if (ln != L) {
+                const int lim = ln > 0 ? ln + 2 - 4 * K * g : 0;  // empty / missing packet: no header
+#pragma unroll
+                for (int m = 0; m < K; ++m) H[m] &= keep_bytes(lim - 4 * m);
+            }
+#pragma unroll
+            for (int i = 0; i < K; ++i) pw[item * PWS + i] = gather4(H, i, K + i, 2 * K + i, 3 * K + i);
+        }
+        wait_lds_barrier();  // position words of the whole tile written
+
+        // ---- B: this wave's products over every item of the tile, XORed into the parity rows
+        if constexpr (NPW > 0) {
+            if (active) {
+#pragma unroll 1
+                for (int sl = 0; sl < 4; ++sl) {
+                    const int it_item = (sl * PPW + pl) * NS4 + g;
+                    const int pp = sl * PPW + pl;
+                    const uint32_t* src = pw + it_item * PWS;
+                    uint32_t* qb = q + pp * NS4 + g;
+                    tfor<i_hi - i_lo + 1>([&](auto ic) __attribute__((always_inline)) {
+                        constexpr int I = i_lo + decltype(ic)::value;
+                        const TSel s = tsplit(src[I]);
+                        tfor<NPA>([&](auto jc) __attribute__((always_inline)) {
+                            constexpr int JJ = decltype(jc)::value;
+                            constexpr int kk = I * NPA + JJ;
+                            if constexpr (kk >= k0 && kk < k1) {
+                                const uint32_t v = tprod(tab[kk - k0], s);
+                                __hip_atomic_fetch_xor(qb + JJ * QJ + (K + JJ - I) * NS4, v, __ATOMIC_RELAXED,
+                                                       __HIP_MEMORY_SCOPE_WORKGROUP);
+                            }
+                        });
+                    });
+                }
+            }
+        }
+        wait_lds_barrier();  // B2: parity of rows [0, R) complete; the input buffer is free
+        if (it + 2 <= cnt) issue(it + 2);
+
+        // ---- C: codeword words of the own item into the output tile; parity rows move down by R
+        {
+            uint32_t Qv[NPA];
+#pragma unroll
+            for (int jj = 0; jj < NPA; ++jj) Qv[jj] = 0;
+            if (active) {
+#pragma unroll
+                for (int jj = 0; jj < NP; ++jj) {
+                    uint32_t* r0p = q + jj * QJ + p * NS4 + g;
+                    Qv[jj] = *r0p;
+                    if (p < n - 1) {
+                        uint32_t* r1p = r0p + R * NS4;
+                        *r0p = *r1p;
+                        *r1p = 0;
+                    } else {
+                        *r0p = 0;
+                    }
+                }
+            }
+            const int t = row0 + p;
+            // the batch's last codeword may end inside a dword: the packet after it (not emitted)
+            // still writes its first dword, which carries that codeword's last bytes
+            const bool emit = it > 0 && active && (t < P || (t == P && g == 0));
+            uint32_t X[n];
+            tgroup_words<K, NP>(H, Qv, X);
+            uint32_t tw = X[n - 1];
+            if (is_last) {
+                switch (a.rem) {
+                    case 1: tw = ttail_rem<n, 1>(X); break;
+                    case 2: tw = ttail_rem<n, 2>(X); break;
+                    case 3: tw = ttail_rem<n, 3>(X); break;
+                    default: break;
+                }
+            }
+            const uint32_t prev = tbperm(lane - 1 < 0 ? 0 : lane - 1, tw);
+            const int o = p * CW + 4 * n * g;  // byte offset of the item in the output tile
+            const int al = o & 3;
+            const int sh = (4 - al) & 3;
+            const int d0 = (o - al) >> 2;
+            // dwords written: n, except the last group of a packet: up to the packet end (the dword
+            // shared with the next packet is that packet's first lane's)
+            const int cntw = t >= P ? 1 : (is_last ? ((p + 1) * CW >> 2) - d0 : n);
+            uint32_t* outw = reinterpret_cast<uint32_t*>(out) + d0;
+            if (emit) {
+#pragma unroll
+                for (int qq = 0; qq < n; ++qq) {
+                    const uint32_t lo = qq == 0 ? prev : X[qq - 1];
+                    const uint32_t z = al == 0 ? X[qq] : __builtin_amdgcn_alignbyte(X[qq], lo, sh);
+                    if (qq < cntw) outw[qq] = z;
+                }
+            }
+        }
+        wait_lds_barrier();  // B3: output tile complete
+        if (it == 0) continue;
+
+        // ---- D: output tile -> HBM (16-byte chunks); trimmed sizes
+        {
+            const int gbase = row0 * CW;  // 16-byte aligned
+            const int lim = P * CW - gbase;
+            const int tb = R * CW;
+            for (int j = 0; j < nso; ++j) {
+                const int c = (tid + j * kTileThreads) * 16;
+                const bool inb = c < tb;
+                const uint4 v = inb ? *reinterpret_cast<const uint4*>(out + c) : make_uint4(0, 0, 0, 0);
+                if (inb && c + 16 > lim && c < lim) {  // the batch end inside this chunk: dwords, bytes
+                    const uint32_t w4[4] = {v.x, v.y, v.z, v.w};
+                    for (int b = 0; b < lim - c; b += 4) {
+                        if (b + 4 <= lim - c) {
+                            __builtin_amdgcn_raw_buffer_store_b32(w4[b >> 2], rc, gbase + c + b, 0, 0);
+                        } else {
+                            for (int y = b; y < lim - c; ++y)
+                                __builtin_amdgcn_raw_buffer_store_b8(static_cast<uint8_t>(w4[b >> 2] >> (8 * (y - b))),
+                                                                     rc, gbase + c + y, 0, 0);
+                        }
+                    }
+                }
+                const bool full = inb && c + 16 <= lim;
+                typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+                const v4u vv = {v.x, v.y, v.z, v.w};
+                __builtin_amdgcn_raw_buffer_store_b128(vv, rc, full ? gbase + c : 0x7ffffff0, 0, 0);
+            }
+            // trimmed wire size of packet tid (FEC_Encoder.cpp:55-60): 1 + last non-zero byte
+            int sz = 0;
+            const bool own = tid < R && row0 + tid < P;
+            if (own) {
+                const uint8_t* cwp = out + tid * CW;
+                sz = CW;
+                if (cwp[CW - 1] == 0) {
+                    sz = 0;
+                    for (int b = CW - 2; b >= 0; --b)
+                        if (cwp[b] != 0) {
+                            sz = b + 1;
+                            break;
+                        }
+                }
+            }
+            __builtin_amdgcn_raw_buffer_store_b32(static_cast<uint32_t>(sz), rw, own ? 4 * (row0 + tid) : 0x7ffffff0,
+                                                  0, 0);
+        }
+    }
+    wait_vm(0);
+}
+
+}  // namespace
+
+template <int K, int NP>
+__global__ __launch_bounds__(kTileThreads) void fec_encode_tile_kernel(EncTileArgs a) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t tsmem[];
+    switch (__builtin_amdgcn_readfirstlane(threadIdx.x >> 6)) {
+        case 0: tile_walk<K, NP, 0>(a, tsmem); break;
+        case 1: tile_walk<K, NP, 1>(a, tsmem); break;
+        case 2: tile_walk<K, NP, 2>(a, tsmem); break;
+        default: tile_walk<K, NP, 3>(a, tsmem); break;
+    }
+}
+
+#ifdef FEC_WAVE_ONLY
+#define FEC_ENC_TILE_LIST(X) X(8, 3)
+#else
+#define FEC_ENC_TILE_LIST(X) \
+    X(8, 3) X(9, 5) X(11, 0) X(10, 1) X(9, 2) X(7, 4) X(6, 5) X(5, 6) X(4, 7) X(3, 8) X(2, 9)  \
+    X(10, 3) X(9, 3) X(10, 4) X(8, 4) X(10, 5) X(7, 5) X(3, 9)
+#endif
+
+#define FEC_ENC_TILE_INST(K, NP) template __global__ void fec_encode_tile_kernel<K, NP>(EncTileArgs);
+FEC_ENC_TILE_LIST(FEC_ENC_TILE_INST)
+
+const void* fec_encode_tile_kernel_for(int k, int np) {
+#define FEC_ENC_TILE_CASE(K, NP) \
+    if (k == K && np == NP) return reinterpret_cast<const void*>(&fec_encode_tile_kernel<K, NP>);
+    FEC_ENC_TILE_LIST(FEC_ENC_TILE_CASE)
+#undef FEC_ENC_TILE_CASE
+    return nullptr;
+}
+
+}  // namespace fec

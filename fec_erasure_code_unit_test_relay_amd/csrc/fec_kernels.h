@@ -83,6 +83,30 @@ struct EncWaveArgs {
 // fec_encode_wave_kernel<k, n-k> (fec_encode_wave.hip), else nullptr.  256 threads.
 const void* fec_encode_wave_kernel_for(int k, int np);
 
+struct EncTileArgs {
+    const uint8_t* payload_base;  // row -history (4-byte aligned, L % 4 == 0)
+    const int32_t* len_base;      // lengths of rows -history.. (null: all L)
+    int payload_bytes;            // (history + P) * L < 2^31 (the launcher splits larger batches)
+    int len_bytes;                // (history + P) * 4
+    int history;                  // valid rows before row 0 (<= n-1)
+    int P;
+    uint8_t* cw;                  // 16-byte aligned
+    int cw_bytes;                 // P * CW < 2^31
+    int32_t* cw_len;
+    const uint32_t* ptab;         // [k][n-k][8] register tables of G's parity coefficients
+    int L, CW, NS4;
+    int PPW;                      // packets per wave slice (tile R = 4 * PPW packets, PPW*CW % 4 == 0)
+    int rem;                      // sub-streams in the last group (1..4)
+    int nvl;                      // payload dwords of a row from dword K*(NS4-1) on (last group)
+    int tiles_per_wg, ntiles;     // consecutive tiles per workgroup; ceil(P / R)
+    int ngl;                      // 1 KB LDS-DMA pieces per wave per tile (4 * ngl KB >= R*L + 4K + 8)
+    int nso;                      // 16-byte output stores per thread per tile (ceil(R*CW / 4096))
+    int off_in, in_bytes, off_pw, off_q, off_out, off_len;  // dynamic LDS carve-up (bytes)
+};
+
+// fec_encode_tile_kernel<k, n-k> (fec_encode_tile.hip), else nullptr.  256 threads.
+const void* fec_encode_tile_kernel_for(int k, int np);
+
 // fec_encode_persist_kernel<k, n-k> (fec_encode_persist.hip), else nullptr.  320 threads.
 const void* fec_encode_persist_kernel_for(int k, int np);
 

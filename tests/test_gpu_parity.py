@@ -40,7 +40,7 @@ ENC_CONFIGS = [(10, 3, 3), (10, 5, 2), (10, 1, 1), (10, 0, 0), (10, 2, 2), (10, 
                (4, 6, 2), (12, 4, 2)]
 
 
-@pytest.mark.parametrize("path", ["generic", "fast", "auto", "wave"])
+@pytest.mark.parametrize("path", ["generic", "fast", "auto", "wave", "tile"])
 @pytest.mark.parametrize("tbn", ENC_CONFIGS)
 def test_encode_bit_exact(tbn, path):
     T, B, N = tbn
@@ -63,12 +63,13 @@ def test_encode_fast_path_other_payload_sizes():
     for Lx, tbn, P in [(4, (10, 3, 3), 200), (64, (10, 5, 2), 300), (1500, (10, 3, 3), 130),
                        (300, (10, 3, 3), 1), (300, (10, 1, 1), 7), (1500, (10, 5, 2), 700)]:
         ref = oracle.encode_stream(Lx, *tbn, 0, P, seed=11)
-        for path in ("fast", "stream", "wave"):
+        for path in ("fast", "stream", "wave", "tile"):
             c = fec.Codec(Lx, *tbn)
             try:
                 c.set_encode_path(path)
             except fec.FecError:
-                assert path == "wave" and Lx > 300  # prefetch width limit
+                # wave: prefetch width limit; tile: a tile must cover the n-1 packets of history
+                assert (path == "wave" and Lx > 300) or (path == "tile" and Lx > 300)
                 continue
             payload = fec.fill_payload(0, P, Lx, 11)
             cw, wl = c.encode(payload)
@@ -86,7 +87,7 @@ def test_encode_stream_many_tiles_per_workgroup(tbn):
     lens = torch.from_numpy(rng.integers(0, L + 1, size=P).astype(np.int32)).cuda()
     payload = fec.fill_payload(0, P, L, 23)
     outs = []
-    for path in ("fast", "stream", "wave"):
+    for path in ("fast", "stream", "wave", "tile"):
         c = fec.Codec(L, *tbn)
         try:
             c.set_encode_path(path)
@@ -102,15 +103,20 @@ def test_encode_stream_many_tiles_per_workgroup(tbn):
         assert torch.equal(o[2], o[0][P // 2:])
 
 
+@pytest.mark.parametrize("path", ["wave", "tile"])
 @pytest.mark.parametrize("tbn", [(10, 3, 3), (10, 5, 2), (10, 1, 1), (10, 0, 0), (10, 9, 9)])
-def test_encode_wave_sequences_and_batch_edges(tbn):
+def test_encode_wave_sequences_and_batch_edges(tbn, path):
     """The wave kernel splits a batch into packet sequences with a warm-up over the packets in
-    front of each: sizes around the sequence length, odd batch ends (the last codeword's final
-    partial dword) and both codeword alignments, against the oracle."""
-    for P in (1, 2, 3, 5, 41, 64, 1001, 4099):
+    front of each, the tile kernel into workgroup runs of tiles with the tile in front: sizes
+    around the sequence / tile length, odd batch ends (the last codeword's final partial dword)
+    and both codeword alignments, against the oracle."""
+    for P in (1, 2, 3, 5, 23, 24, 25, 41, 64, 1001, 4099, 70001):
         ref = oracle.encode_stream(L, *tbn, 0, P, seed=5)
         c = fec.Codec(L, *tbn)
-        c.set_encode_path("wave")
+        try:
+            c.set_encode_path(path)
+        except fec.FecError:
+            pytest.skip(f"no {path} kernel for {tbn}")
         payload = fec.fill_payload(0, P, L, 5)
         cw, wl = c.encode(payload)
         assert (cw.cpu().numpy() == ref["cw"]).all(), (tbn, P)
@@ -126,7 +132,7 @@ def test_encode_digest_fixture(oracle_vectors):
         assert hashlib.sha256(wl.cpu().numpy().astype("<i4").tobytes()).hexdigest() == v["wire_len_sha256"]
 
 
-@pytest.mark.parametrize("path", ["generic", "fast", "stream", "wave"])
+@pytest.mark.parametrize("path", ["generic", "fast", "stream", "wave", "tile"])
 @pytest.mark.parametrize("tbn", [(10, 3, 3), (10, 5, 2), (10, 10, 10), (10, 9, 9), (10, 0, 0)])
 def test_encode_variable_lengths_and_history(tbn, path):
     T, B, N = tbn
