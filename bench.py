@@ -196,7 +196,7 @@ def main():
     ap.add_argument("--cpu-packets", type=int, default=30000)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-host-inclusive", action="store_true")
-    ap.add_argument("--encode-path", default="auto", help="A/B: auto|generic|fast|stream|wave")
+    ap.add_argument("--encode-path", default="auto", help="A/B: auto|generic|fast|stream|wave|tile")
     ap.add_argument("--no-extra-configs", action="store_true", help="skip BASELINE configs 3 and 4")
     ap.add_argument("--no-graph", action="store_true",
                     help="launch the step's kernels one by one instead of replaying a captured hipGraph")

@@ -84,7 +84,8 @@ class Codec:
 
     def set_encode_path(self, path: str) -> None:
         """'auto', 'generic', 'fast' (per-tile k, n-k specialised kernel), 'stream' (the
-        persistent specialised kernel) or 'wave' (the wave-sequence kernel)."""
+        persistent specialised kernel), 'wave' (the wave-sequence kernel) or 'tile' (contiguous
+        LDS-tile runs per workgroup; auto's first choice)."""
         code = {"auto": 0, "generic": 1, "fast": 2, "stream": 3, "wave": 4, "tile": 5}[path]
         check(lib().fec_codec_set_encode_path(self._h, code), "fec_codec_set_encode_path")
 

@@ -64,7 +64,7 @@ struct fec_codec {
     int tile_ppw = 0;                   // its packets per wave slice (tile = 4 * tile_ppw packets)
     int tile_lds = 0, tile_lds_len = 0; // its dynamic LDS per workgroup (without / with lengths)
     int tile_per_cu = 0;                // its resident workgroups per CU
-    int tile_off[8] = {};               // off_in, in_bytes, off_pw, off_q, off_out, off_len, ngl, nso
+    int tile_off[9] = {};               // off_in, in_bytes, off_pw, off_q, off_out, off_len, ngl, nso, off_scratch
     const void* copy_fast = nullptr;  // specialised decode copy kernel (LDS tiles)
     int copyf_tp = 0;
     const void* copy_wave = nullptr;  // barrier-free decode copy (fec_copy_wave.hip)
@@ -284,7 +284,8 @@ int codec_init(fec_codec* c, int max_payload, int T, int B, int N) {
         if (ppw > 0 && 4 * ppw >= g.n - 1) c->tile_kernel = fec::fec_encode_tile_kernel_for(g.k, g.n - g.k);
         if (c->tile_kernel) {
             const int R = 4 * ppw;
-            const int ngl = (R * g.L + 4 * g.k + 8 + 4095) / 4096;
+            const int rs = (g.L + 15) & ~15;  // LDS row stride of the input tile
+            const int ngl = (R * rs + 16 + 4095) / 4096;
             const int pws = g.k | 1;
             const int rows = R + g.n - 1;
             const int npa = std::max(1, g.n - g.k);
@@ -293,12 +294,17 @@ int codec_init(fec_codec* c, int max_payload, int T, int B, int N) {
             const int in_bytes = ngl * 4096;
             const int off_in = off;
             off += 2 * in_bytes;
+            // the position words (read before the second barrier of a tile) and the output tile
+            // (written after it) share one region
             const int off_pw = off;
-            off = al16(off + 4 * R * ns4 * pws);
+            const int off_out = off;
+            off = al16(off + std::max(4 * R * ns4 * pws, R * g.CW));
             const int off_q = off;
             off = al16(off + 4 * npa * rows * ns4);
-            const int off_out = off;
-            off = al16(off + R * g.CW);
+            const int off_scratch = off;
+            off += 1024;
+            c->tile_off[8] = off_scratch;
+            if (ngl > 4) c->tile_kernel = nullptr;
             c->tile_lds = off;
             c->tile_lds_len = off + 2048;
             c->tile_ppw = ppw;
@@ -590,6 +596,9 @@ int launch_encode_tile(fec_codec* c, const uint8_t* d_payload, const int32_t* d_
     a.off_len = c->tile_off[5];
     a.ngl = c->tile_off[6];
     a.nso = c->tile_off[7];
+    a.off_scratch = c->tile_off[8];
+    a.dbg = 0;
+    if (const char* v = std::getenv("FEC_TILE_DBG")) a.dbg = std::atoi(v);
     const int64_t blocks = (ntiles + tpw - 1) / tpw;
     hipEvent_t stop;
     if (int st = c->begin(FEC_KERNEL_ENCODE, s, &stop)) return st;
@@ -606,7 +615,7 @@ int launch_encode(fec_codec* c, const uint8_t* d_payload, const int32_t* d_len, 
         const bool tile_ok = c->tile_kernel && (reinterpret_cast<uintptr_t>(d_payload) & 3) == 0 &&
                              (reinterpret_cast<uintptr_t>(d_cw) & 15) == 0;
         if (c->encode_path == 5 && !tile_ok) return FEC_ERR_ARG;
-        if (tile_ok && c->encode_path == 5)
+        if (tile_ok && (c->encode_path == 0 || c->encode_path == 5))
             return launch_encode_tile(c, d_payload, d_len, history, P, d_cw, d_cwlen, s);
     }
     const Geometry& g = c->g;
@@ -1092,7 +1101,7 @@ int fec_codec_info(const fec_codec* c, char* buf, size_t size) {
     // kernel symbol the encoder launches for a 16-byte aligned payload (rocprofv3 naming)
     char enc[64];
     const int np = c->g.n - c->g.k;
-    if (c->tile_kernel && c->encode_path == 5)
+    if (c->tile_kernel && (c->encode_path == 0 || c->encode_path == 5))
         std::snprintf(enc, sizeof(enc), "fec_encode_tile_kernel<%d, %d>", c->g.k, np);
     else if (c->wave_kernel && (c->encode_path == 0 || c->encode_path == 4))
         std::snprintf(enc, sizeof(enc), "fec_encode_wave_kernel<%d, %d>", c->g.k, np);

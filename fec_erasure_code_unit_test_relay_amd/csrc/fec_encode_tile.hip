@@ -37,6 +37,9 @@ namespace fec {
 namespace {
 
 constexpr int kTileThreads = 256;
+#ifndef FEC_TILE_MINWG
+#define FEC_TILE_MINWG 5  // workgroups per CU the register budget is sized for
+#endif
 
 template <typename F, int... Is>
 __device__ __forceinline__ void tfor_impl(F&& f, std::integer_sequence<int, Is...>) {
@@ -89,6 +92,55 @@ __device__ __forceinline__ void wait_lds_barrier() {
 }
 
 typedef __attribute__((address_space(3))) void* lds_void_ptr;
+typedef uint32_t tv4u __attribute__((ext_vector_type(4)));
+
+// Buffer descriptor as four SGPRs (raw buffer, stride 0, num_records bytes; gfx950 dword 3 flags).
+__device__ __forceinline__ tv4u raw_rsrc(const void* base, int num_records) {
+    const uint64_t b = reinterpret_cast<uint64_t>(base);
+    return tv4u{static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(b & 0xffffffffu))),
+                static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<int>((b >> 32) & 0xffffu))),
+                static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(num_records)), 0x00020000u};
+}
+
+// LDS-DMA (buffer_load ... lds): lane i's SIZE bytes at byte voff of the buffer land at LDS byte
+// lds + SIZE*i.  Issued from asm so that hipcc does not treat every later LDS access as possibly
+// reading the DMA's destination (it would wait vmcnt(0) in front of each, draining the prefetch);
+// completion is counted here with wait_vm.  M0 is written and restored inside the statement.
+__device__ __forceinline__ void dma16(tv4u rsrc, uint32_t voff, uint32_t lds) {
+    unsigned keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep) : "v"(voff), "s"(rsrc), "s"(lds) : "memory");
+}
+__device__ __forceinline__ void dma4(tv4u rsrc, uint32_t voff, uint32_t lds) {
+    unsigned keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dword %1, %2, 0 offen lds\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep) : "v"(voff), "s"(rsrc), "s"(lds) : "memory");
+}
+__device__ __forceinline__ uint32_t lds_addr(const void* p) {
+    return static_cast<uint32_t>(reinterpret_cast<uintptr_t>((lds_void_ptr)(p)));
+}
+
+// The dword whose byte q is byte I_q of the concatenated words src[] (compile-time indices): a
+// plain copy when the four bytes are one word in place, one v_perm_b32 when they come from at most
+// two words, else two v_perm_b32 and an OR.
+template <int NW, int I0, int I1, int I2, int I3>
+__device__ __forceinline__ uint32_t tgather4(const uint32_t (&src)[NW]) {
+    constexpr int w0 = I0 >> 2, w1 = I1 >> 2, w2 = I2 >> 2, w3 = I3 >> 2;
+    if constexpr (w0 == w1 && w1 == w2 && w2 == w3 && (I0 & 3) == 0 && (I1 & 3) == 1 && (I2 & 3) == 2 &&
+                  (I3 & 3) == 3) {
+        return src[w0];
+    } else {
+        constexpr int a = w0;  // first source word; the other one, if any
+        constexpr int b = (w1 != a) ? w1 : (w2 != a) ? w2 : w3;
+        if constexpr ((w1 == a || w1 == b) && (w2 == a || w2 == b) && (w3 == a || w3 == b)) {
+            constexpr auto code = [](int w, int i) constexpr { return w == a ? (i & 3) : 4 + (i & 3); };
+            constexpr uint32_t sel = sel4(code(w0, I0), code(w1, I1), code(w2, I2), code(w3, I3));
+            return __builtin_amdgcn_perm(src[b], src[a], sel);
+        } else {
+            return gather4(src, I0, I1, I2, I3);
+        }
+    }
+}
 
 // Codeword words of the group: bytes [e*n, e*n+n) = sub-stream 4g+e: K systematic bytes, NP parity.
 template <int K, int NP>
@@ -100,12 +152,14 @@ __device__ __forceinline__ void tgroup_words(const uint32_t (&H)[K], const uint3
     for (int m = 0; m < K; ++m) src[m] = H[m];
 #pragma unroll
     for (int jj = 0; jj < NP; ++jj) src[K + jj] = Q[jj];
-    auto idx = [](int b) {
+    constexpr auto idx = [](int b) constexpr {
         const int e = b / n, j = b % n;
         return j < K ? (e * K + j) : (4 * (K + j - K) + e);
     };
-#pragma unroll
-    for (int q = 0; q < n; ++q) X[q] = gather4(src, idx(4 * q), idx(4 * q + 1), idx(4 * q + 2), idx(4 * q + 3));
+    tfor<n>([&](auto qc) __attribute__((always_inline)) {
+        constexpr int qq = decltype(qc)::value;
+        X[qq] = tgather4<n, idx(4 * qq), idx(4 * qq + 1), idx(4 * qq + 2), idx(4 * qq + 3)>(src);
+    });
 }
 
 // Last 4 valid bytes of the group's words (bytes [vb-4, vb)), vb = n * REM for the last group.
@@ -151,6 +205,7 @@ __device__ __forceinline__ void tile_walk(const EncTileArgs& a, uint8_t* smem) {
     uint32_t* pw = reinterpret_cast<uint32_t*>(smem + a.off_pw);
     uint32_t* q = reinterpret_cast<uint32_t*>(smem + a.off_q);
     uint8_t* out = smem + a.off_out;
+    uint32_t* scratch = reinterpret_cast<uint32_t*>(smem + a.off_scratch);  // one dword per thread
     const uint32_t* lensl = reinterpret_cast<const uint32_t*>(smem + a.off_len);
 
     // coefficient tables of this wave's products, in registers for the whole walk
@@ -181,24 +236,38 @@ __device__ __forceinline__ void tile_walk(const EncTileArgs& a, uint8_t* smem) {
     const int ns = nso + 1;                                  // + the trimmed-size store
 
     // tile it (0 = the tile in front of the first one) -> LDS input buffer (it & 1)
+    const tv4u rs4 = raw_rsrc(a.payload_base, a.payload_bytes);
+    const tv4u rl4 = raw_rsrc(a.len_base, a.len_bytes);
+    const uint32_t lds_in = lds_addr(smem + a.off_in), lds_len = lds_addr(smem + a.off_len);
+    // LDS image of a tile: row p at p*RS (RS = L rounded up to 16 bytes), so that every row starts
+    // 16-byte aligned; the DMA's destination is lane-linear, its per-lane source picks the row
+    // piece (tile-invariant offsets, computed once).  A row's last piece also brings the first
+    // bytes of the next row (never read as payload: past L they are the zero pad's business).
+    const int CPR = (L + 15) >> 4;  // 16-byte pieces per row
+    const int RS = CPR * 16;
+    int srel[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const int c = (j * 4 + (tid >> 6)) * 64 + lane;
+        const int row = c / CPR;
+        srel[j] = row * L + (c - row * CPR) * 16;
+    }
     auto issue = [&](int it) __attribute__((always_inline)) {
         const int row0 = (first - 1 + it) * R;
-        uint8_t* dst = smem + a.off_in + (it & 1) * a.in_bytes;
-        const int wv = tid >> 6;
-        const int base = (row0 + a.history) * L;  // may be negative: those chunks read as zero
-        for (int j = 0; j < ngl; ++j) {
-            const int c = (j * 4 + wv) * 64 + lane;
-            const int o = base + c * 16;
-            __builtin_amdgcn_raw_ptr_buffer_load_lds(
-                rs, (lds_void_ptr)(dst + __builtin_amdgcn_readfirstlane((j * 4 + wv) * 1024)), 16,
-                static_cast<uint32_t>(o < 0 ? 0x7fffffff : o), 0, 0, 0);
+        const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+        const uint32_t dst = lds_in + (it & 1) * a.in_bytes;
+        const int base = (row0 + a.history) * L;  // may be negative: those pieces read as zero
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            if (j < ngl) {
+                const int o = base + srel[j];
+                dma16(rs4, static_cast<uint32_t>(o < 0 ? 0x7fffffff : o), dst + (j * 4 + wv) * 1024);
+            }
         }
         if (has_len) {
-            uint8_t* ld = smem + a.off_len + (it & 1) * 1024 + __builtin_amdgcn_readfirstlane(wv * 256);
             const int r = row0 + a.history + lane;
             const bool ok = wv == 0 && lane < R && r >= 0;
-            __builtin_amdgcn_raw_ptr_buffer_load_lds(rl, (lds_void_ptr)ld, 4,
-                                                     static_cast<uint32_t>(ok ? r * 4 : 0x7fffffff), 0, 0, 0);
+            dma4(rl4, static_cast<uint32_t>(ok ? r * 4 : 0x7fffffff), lds_len + (it & 1) * 1024 + wv * 256);
         }
     };
 
@@ -220,29 +289,16 @@ __device__ __forceinline__ void tile_walk(const EncTileArgs& a, uint8_t* smem) {
         const int row0 = (first - 1 + it) * R;
         const uint8_t* in = smem + a.off_in + (it & 1) * a.in_bytes;
         const uint32_t* inw = reinterpret_cast<const uint32_t*>(in);
-        {
-            // A 16-byte piece straddling the start (history rows) or the end of the payload rows is
-            // out of range as a whole for the LDS-DMA (zeros): its valid dwords again, one by one
-            // (rare: the first / last tile of the batch when (history + P) * L % 16 != 0).
-            const int base = (row0 + a.history) * L;
-            const int span = ngl * 4096;
-            bool need = false;
-#pragma unroll
-            for (int e = 0; e < 2; ++e) {
-                const int B = e == 0 ? 0 : a.payload_bytes;
-                need |= B > base && B < base + span && ((B - base) & 15) != 0;
-            }
-            if (need) {
-                if (tid < 8) {
-                    const int e = tid >> 2;
-                    const int B = e == 0 ? 0 : a.payload_bytes;
-                    if (B > base && B < base + span && ((B - base) & 15) != 0) {
-                        const int c = (B - base) >> 4;
-                        const int off = base + 16 * c + 4 * (tid & 3);
-                        if (off >= 0 && off < a.payload_bytes)
-                            reinterpret_cast<uint32_t*>(smem + a.off_in + (it & 1) * a.in_bytes)[4 * c + (tid & 3)] =
-                                __builtin_amdgcn_raw_buffer_load_b32(rs, off, 0, 0);
-                    }
+        if (L & 15) {
+            // the batch's last row: its last piece runs past the end of the payload rows, and an
+            // LDS-DMA out of range as a whole reads zeros: its valid dwords again, one by one
+            const int pl_last = P - 1 - row0;
+            if (pl_last >= 0 && pl_last < R) {
+                if (tid < 4) {
+                    const int b = (CPR - 1) * 16 + 4 * tid;
+                    if (b < L)
+                        reinterpret_cast<uint32_t*>(smem + a.off_in + (it & 1) * a.in_bytes)[(pl_last * RS + b) >> 2] =
+                            __builtin_amdgcn_raw_buffer_load_b32(rs, (P - 1 + a.history) * L + b, 0, 0);
                 }
                 wait_vm(0);
                 wait_lds_barrier();
@@ -252,19 +308,28 @@ __device__ __forceinline__ void tile_walk(const EncTileArgs& a, uint8_t* smem) {
         // ---- A: window words and position words of the own item
         if (active) {
             const int t = row0 + p;
-            int ln;
-            if (t < -a.history || t >= P) {
-                ln = 0;
-            } else if (has_len) {
-                const int v = static_cast<int>(lensl[(it & 1) * 256 + p]);
-                ln = v < 0 ? 0 : (v > L ? L : v);
-            } else {
-                ln = L;
+            int lv = L;
+            if (has_len) {
+                lv = static_cast<int>(lensl[(it & 1) * 256 + p]);
+                lv = lv < 0 ? 0 : (lv > L ? L : lv);
             }
-            const int rdw = (p * L >> 2) + K * g - 1;  // row dword K*g - 1
+            const int ln = (t < -a.history || t >= P) ? 0 : lv;
+            const int rb = p * RS + 4 * K * g;  // byte of row dword K*g
             uint32_t D[K + 1];
+            D[0] = *reinterpret_cast<const uint32_t*>(in + rb - 4);
+            if constexpr (K % 4 == 0) {
 #pragma unroll
-            for (int m = 0; m <= K; ++m) D[m] = inw[rdw + m];
+                for (int m = 0; m < K; m += 4) {
+                    const uint4 v = *reinterpret_cast<const uint4*>(in + rb + 4 * m);
+                    D[m + 1] = v.x;
+                    D[m + 2] = v.y;
+                    D[m + 3] = v.z;
+                    D[m + 4] = v.w;
+                }
+            } else {
+#pragma unroll
+                for (int m = 0; m < K; ++m) D[m + 1] = *reinterpret_cast<const uint32_t*>(in + rb + 4 * m);
+            }
             const uint32_t hdr =
                 (static_cast<uint32_t>(ln & 0xff) << 24) | (static_cast<uint32_t>((ln >> 8) & 0xff) << 16);
             D[0] = g == 0 ? hdr : D[0];
@@ -278,14 +343,16 @@ __device__ __forceinline__ void tile_walk(const EncTileArgs& a, uint8_t* smem) {
 #pragma unroll
                 for (int m = 0; m < K; ++m) H[m] &= keep_bytes(lim - 4 * m);
             }
-#pragma unroll
-            for (int i = 0; i < K; ++i) pw[item * PWS + i] = gather4(H, i, K + i, 2 * K + i, 3 * K + i);
+            tfor<K>([&](auto ic) __attribute__((always_inline)) {
+                constexpr int i = decltype(ic)::value;
+                pw[item * PWS + i] = tgather4<K, i, K + i, 2 * K + i, 3 * K + i>(H);
+            });
         }
         wait_lds_barrier();  // position words of the whole tile written
 
         // ---- B: this wave's products over every item of the tile, XORed into the parity rows
         if constexpr (NPW > 0) {
-            if (active) {
+            if (active && !(a.dbg & 1)) {
 #pragma unroll 1
                 for (int sl = 0; sl < 4; ++sl) {
                     const int it_item = (sl * PPW + pl) * NS4 + g;
@@ -317,17 +384,17 @@ __device__ __forceinline__ void tile_walk(const EncTileArgs& a, uint8_t* smem) {
 #pragma unroll
             for (int jj = 0; jj < NPA; ++jj) Qv[jj] = 0;
             if (active) {
+                // rows [0, n-1) take over rows [R, R+n-1) (zeroed); the other rows are zeroed
+                const bool mv = p < n - 1;
+                uint32_t* zdst = scratch + tid;  // writes that must not land anywhere
 #pragma unroll
                 for (int jj = 0; jj < NP; ++jj) {
                     uint32_t* r0p = q + jj * QJ + p * NS4 + g;
-                    Qv[jj] = *r0p;
-                    if (p < n - 1) {
-                        uint32_t* r1p = r0p + R * NS4;
-                        *r0p = *r1p;
-                        *r1p = 0;
-                    } else {
-                        *r0p = 0;
-                    }
+                    uint32_t* r1p = q + jj * QJ + (R + (mv ? p : 0)) * NS4 + g;
+                    const uint32_t v0 = *r0p, v1 = *r1p;
+                    Qv[jj] = v0;
+                    *r0p = mv ? v1 : 0u;
+                    *(mv ? r1p : zdst) = 0u;
                 }
             }
             const int t = row0 + p;
@@ -348,18 +415,19 @@ __device__ __forceinline__ void tile_walk(const EncTileArgs& a, uint8_t* smem) {
             const uint32_t prev = tbperm(lane - 1 < 0 ? 0 : lane - 1, tw);
             const int o = p * CW + 4 * n * g;  // byte offset of the item in the output tile
             const int al = o & 3;
-            const int sh = (4 - al) & 3;
+            // word qq of the shifted image = bytes [4 - al, 8 - al) of {X[qq-1] (or prev), X[qq]}
+            const uint32_t shsel = 0x03020100u + static_cast<uint32_t>(4 - al) * 0x01010101u;
             const int d0 = (o - al) >> 2;
             // dwords written: n, except the last group of a packet: up to the packet end (the dword
             // shared with the next packet is that packet's first lane's)
-            const int cntw = t >= P ? 1 : (is_last ? ((p + 1) * CW >> 2) - d0 : n);
-            uint32_t* outw = reinterpret_cast<uint32_t*>(out) + d0;
-            if (emit) {
+            const int cntw = !emit ? 0 : (t >= P ? 1 : (is_last ? ((p + 1) * CW >> 2) - d0 : n));
+            if (!(a.dbg & 2)) {
+                uint32_t* outw = reinterpret_cast<uint32_t*>(out) + d0;
+                uint32_t* zdst = scratch + tid;
 #pragma unroll
                 for (int qq = 0; qq < n; ++qq) {
                     const uint32_t lo = qq == 0 ? prev : X[qq - 1];
-                    const uint32_t z = al == 0 ? X[qq] : __builtin_amdgcn_alignbyte(X[qq], lo, sh);
-                    if (qq < cntw) outw[qq] = z;
+                    *(qq < cntw ? outw + qq : zdst) = __builtin_amdgcn_perm(X[qq], lo, shsel);
                 }
             }
         }
@@ -371,11 +439,12 @@ __device__ __forceinline__ void tile_walk(const EncTileArgs& a, uint8_t* smem) {
             const int gbase = row0 * CW;  // 16-byte aligned
             const int lim = P * CW - gbase;
             const int tb = R * CW;
+            const bool tail_tile = lim < tb;  // the batch ends inside this tile (uniform)
             for (int j = 0; j < nso; ++j) {
                 const int c = (tid + j * kTileThreads) * 16;
                 const bool inb = c < tb;
-                const uint4 v = inb ? *reinterpret_cast<const uint4*>(out + c) : make_uint4(0, 0, 0, 0);
-                if (inb && c + 16 > lim && c < lim) {  // the batch end inside this chunk: dwords, bytes
+                const uint4 v = *reinterpret_cast<const uint4*>(out + (inb ? c : 0));
+                if (tail_tile && inb && c + 16 > lim && c < lim) {  // the batch end inside this chunk: dwords, bytes
                     const uint32_t w4[4] = {v.x, v.y, v.z, v.w};
                     for (int b = 0; b < lim - c; b += 4) {
                         if (b + 4 <= lim - c) {
@@ -390,15 +459,15 @@ __device__ __forceinline__ void tile_walk(const EncTileArgs& a, uint8_t* smem) {
                 const bool full = inb && c + 16 <= lim;
                 typedef uint32_t v4u __attribute__((ext_vector_type(4)));
                 const v4u vv = {v.x, v.y, v.z, v.w};
-                __builtin_amdgcn_raw_buffer_store_b128(vv, rc, full ? gbase + c : 0x7ffffff0, 0, 0);
+                __builtin_amdgcn_raw_buffer_store_b128(vv, rc, full && !(a.dbg & 4) ? gbase + c : 0x7ffffff0, 0, 0);
             }
             // trimmed wire size of packet tid (FEC_Encoder.cpp:55-60): 1 + last non-zero byte
-            int sz = 0;
             const bool own = tid < R && row0 + tid < P;
-            if (own) {
-                const uint8_t* cwp = out + tid * CW;
-                sz = CW;
-                if (cwp[CW - 1] == 0) {
+            const uint8_t* cwp = out + (own ? tid : 0) * CW;
+            const bool zlast = cwp[CW - 1] == 0;
+            int sz = CW;
+            if (__builtin_amdgcn_ballot_w64(own && zlast)) {  // rare: a codeword ending in zero bytes
+                if (own && zlast) {
                     sz = 0;
                     for (int b = CW - 2; b >= 0; --b)
                         if (cwp[b] != 0) {
@@ -417,7 +486,7 @@ __device__ __forceinline__ void tile_walk(const EncTileArgs& a, uint8_t* smem) {
 }  // namespace
 
 template <int K, int NP>
-__global__ __launch_bounds__(kTileThreads) void fec_encode_tile_kernel(EncTileArgs a) {
+__global__ __launch_bounds__(kTileThreads, FEC_TILE_MINWG) void fec_encode_tile_kernel(EncTileArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t tsmem[];
     switch (__builtin_amdgcn_readfirstlane(threadIdx.x >> 6)) {
         case 0: tile_walk<K, NP, 0>(a, tsmem); break;

@@ -102,6 +102,9 @@ struct EncTileArgs {
     int ngl;                      // 1 KB LDS-DMA pieces per wave per tile (4 * ngl KB >= R*L + 4K + 8)
     int nso;                      // 16-byte output stores per thread per tile (ceil(R*CW / 4096))
     int off_in, in_bytes, off_pw, off_q, off_out, off_len;  // dynamic LDS carve-up (bytes)
+    int off_scratch;              // 1 KB: a dword per thread for writes that must land nowhere
+    int dbg;                      // timing experiments only (FEC_TILE_DBG): 1 no parity products,
+                                  // 2 no codeword words, 4 no output stores
 };
 
 // fec_encode_tile_kernel<k, n-k> (fec_encode_tile.hip), else nullptr.  256 threads.

@@ -51,17 +51,20 @@ int fec_codec_geometry(const fec_codec *codec, int *k, int *n, int *S, int *CW);
 /* Kernel configuration chosen for this codec and device (tiles, resident workgroups), as a JSON
  * object written to buf (NUL-terminated, truncated to size). */
 int fec_codec_info(const fec_codec *codec, char *buf, size_t size);
-/* Encode kernel selection: 0 = automatic (the wave-sequence kernel when one is compiled for
- * (k, n-k), max_payload % 4 == 0, payload and codeword buffers are 4-byte aligned and its LDS
- * rings fit; else the streaming kernel when the payload is 16-byte aligned; else the per-tile
- * specialised kernel; else the generic one), 1 = generic kernel, 2 = per-tile specialised kernel,
- * 3 = streaming (persistent) specialised kernel, 4 = wave-sequence kernel (FEC_ERR_ARG if
- * unavailable).  All produce identical bytes; the switch exists for tests and A/B timing. */
+/* Encode kernel selection: 0 = automatic (the tile kernel -- contiguous runs of LDS-staged packet
+ * tiles per workgroup -- when one is compiled for (k, n-k), max_payload % 4 == 0, the payload is
+ * 4-byte and the codeword buffer 16-byte aligned and a tile covers the n-1 packets of parity
+ * history; else the wave-sequence kernel; else the streaming kernel when the payload is 16-byte
+ * aligned; else the per-tile specialised kernel; else the generic one), 1 = generic kernel,
+ * 2 = per-tile specialised kernel, 3 = streaming (persistent) specialised kernel, 4 = wave-sequence
+ * kernel, 5 = tile kernel (FEC_ERR_ARG if unavailable).  All produce identical bytes; the switch
+ * exists for tests and A/B timing. */
 int fec_codec_set_encode_path(fec_codec *codec, int path);
-/* The same switch for the decoder's received-packet copy kernel: 0 automatic (the barrier-free
- * wave kernel when one is compiled for (k, n-k), max_payload % 4 == 0 and the output is 4-byte
- * aligned; it writes received packets' rows only, so fec_decode_batch then runs the recovery of
- * erased packets concurrently with it), 1 generic, 2 LDS-tile specialised, 3 wave. */
+/* The same switch for the decoder's received-packet copy kernel: 0 automatic (the LDS-tile
+ * specialised kernel when one is compiled for (k, n-k) and max_payload % 4 == 0, else the generic
+ * one), 1 generic, 2 LDS-tile specialised, 3 barrier-free wave kernel (it writes received packets'
+ * rows only, so fec_decode_batch then runs the recovery of erased packets concurrently with it;
+ * measured slower in the step, kept for A/B). */
 int fec_codec_set_copy_path(fec_codec *codec, int path);
 /* The same switch for the decoder's planner (per-episode block replay). */
 int fec_codec_set_plan_path(fec_codec *codec, int path);

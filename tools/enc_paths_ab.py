@@ -18,6 +18,7 @@ ap.add_argument("--packets", type=int, default=1_000_010)
 ap.add_argument("--iters", type=int, default=20)
 ap.add_argument("--reps", type=int, default=7)
 ap.add_argument("--env", default="", help="VAR=v1|v2|...: extra variants of the last path")
+ap.add_argument("--nocheck", action="store_true", help="timing experiments whose outputs differ")
 args = ap.parse_args()
 T, B, N = map(int, args.tbn.split(","))
 torch.cuda.set_device(0)
@@ -46,7 +47,7 @@ for v in variants:
     h = (cw.clone(), wl.clone())
     if ref is None:
         ref = h
-    else:
+    elif not args.nocheck:
         assert torch.equal(ref[0], h[0]) and torch.equal(ref[1], h[1]), f"{v} differs from {variants[0]}"
 print("outputs identical across", [f"{p}{'' if e is None else ':' + '='.join(e)}" for p, e in variants], flush=True)
 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
