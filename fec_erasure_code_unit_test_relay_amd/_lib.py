@@ -19,6 +19,7 @@ FEC_ERR_HIP = -2
 FEC_ERR_NOMEM = -3
 FEC_ERR_WORKSPACE = -4
 FEC_ERR_SEQUENCE = -5
+FEC_ERR_HISTORY = -6
 
 KERNEL_NAMES = ["fec_encode_kernel", "fec_scan_kernel", "fec_plan_kernel", "fec_copy_kernel",
                 "fec_recover_kernel"]
@@ -72,6 +73,10 @@ def lib() -> ctypes.CDLL:
     L.fec_decode_workspace_bytes.argtypes = [vp, i64]
     L.fec_decode_batch.argtypes = [vp, vp, vp, i64, vp, vp, vp, ctypes.c_size_t, vp]
     L.fec_decode_counters.argtypes = [vp, i64p, i64p, i64p]
+    L.fec_decode_stream_create.argtypes = [ctypes.POINTER(vp)]
+    L.fec_decode_stream_destroy.argtypes = [vp]
+    L.fec_decode_stream_state.argtypes = [vp, i64p, i64p]
+    L.fec_decode_stream_push.argtypes = [vp, vp, vp, vp, vp, i64, i64, vp, vp, i64p, vp, ctypes.c_size_t, vp]
     L.fec_decode_plan_stats.argtypes = [vp, i64p, i64p]
     L.fec_decode_plan.argtypes = [vp, vp, i64, vp, ctypes.c_size_t, vp]
     L.fec_decode_apply.argtypes = [vp, vp, vp, i64, vp, vp, vp, ctypes.c_size_t, vp]
@@ -116,6 +121,8 @@ def lib() -> ctypes.CDLL:
                  "fec_swdf_destination_batch", "fec_codec_create", "fec_codec_destroy", "fec_codec_set_encode_path",
                  "fec_codec_set_copy_path", "fec_codec_set_plan_path", "fec_codec_info", "fec_codec_set_episode_dedup", "fec_debug_stamps", "fec_codec_geometry",
                  "fec_codec_generator", "fec_encode_batch", "fec_decode_batch", "fec_decode_plan",
+                 "fec_decode_stream_create", "fec_decode_stream_destroy", "fec_decode_stream_state",
+                 "fec_decode_stream_push",
                  "fec_decode_apply", "fec_decode_copy", "fec_decode_recover",
                  "fec_decode_counters", "fec_decode_plan_stats", "fec_timing_enable", "fec_timing_collect",
                  "fec_encoder_create", "fec_encoder_destroy", "fec_encoder_transmit",

@@ -260,6 +260,56 @@ class Codec:
         return {KERNEL_NAMES[i]: (ms[i], cnt[i]) for i in range(n)}
 
 
+class DecodeStream:
+    """One stream decoded in consecutive batches (fec_decode_stream_push): the decoder state of
+    src/Decoder.cpp:72-175 carries over from call to call, so the rows returned by successive
+    push() calls, concatenated, equal Codec.decode over the whole stream."""
+
+    def __init__(self, codec: Codec):
+        self.codec = codec
+        h = ctypes.c_void_p()
+        check(lib().fec_decode_stream_create(ctypes.byref(h)), "fec_decode_stream_create")
+        self._h = h
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h:
+            lib().fec_decode_stream_destroy(h)
+            self._h = None
+
+    def state(self) -> tuple[int, int]:
+        """(packets pushed so far, packet the last push restarted the decode at)."""
+        a, b = ctypes.c_int64(), ctypes.c_int64()
+        check(lib().fec_decode_stream_state(self._h, ctypes.byref(a), ctypes.byref(b)), "fec_decode_stream_state")
+        return a.value, b.value
+
+    def push(self, codewords, erasure, erasure_host, history: int = 0, out=None, out_len=None):
+        """codewords [history + P, CW], erasure [history + P] (GPU) and erasure_host (numpy, the
+        same flags): the last P rows are the new packets, the first `history` rows the stream's
+        packets in front of them.  Returns (payload [n, L], lengths [n]) for the packets whose
+        output became available (all but the last T pushed)."""
+        import torch
+        c = self.codec
+        assert codewords.dtype == torch.uint8 and codewords.is_cuda and codewords.is_contiguous()
+        assert codewords.shape[1] == c.CW
+        rows = codewords.shape[0]
+        P = rows - history
+        assert 0 <= history <= rows
+        _check_erasure(torch, erasure, rows)
+        eh = np.ascontiguousarray(erasure_host, dtype=np.uint8)
+        assert eh.size >= rows
+        out, out_len = _check_out(torch, out, out_len, max(P, 1), c.L, codewords.device)
+        ws = c.workspace(rows)
+        n = ctypes.c_int64()
+        cw0 = ctypes.c_void_p(codewords.data_ptr() + history * c.CW)
+        er0 = ctypes.c_void_p(erasure.data_ptr() + history)
+        eh0 = ctypes.c_void_p(eh.ctypes.data + history)
+        check(lib().fec_decode_stream_push(c._h, self._h, cw0, er0, eh0, P, history, _ptr(out), _ptr(out_len),
+                                           ctypes.byref(n), _ptr(ws), ws.numel(), _stream_handle(torch)),
+              "fec_decode_stream_push")
+        return out[:n.value], out_len[:n.value]
+
+
 class FEC_Encoder:
     """FEC_Encoder(max_payload, T, B, N) -- per-packet interface (src/FEC_Encoder.cpp:22-68)."""
 

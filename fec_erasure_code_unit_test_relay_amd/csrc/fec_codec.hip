@@ -35,6 +35,11 @@ struct EventPair {
 
 }  // namespace
 
+struct fec_decode_stream {
+    int64_t consumed = 0;  // packets pushed so far
+    int64_t last_cut = 0;  // where the last push restarted the decode (diagnostics)
+};
+
 struct fec_codec {
     Geometry g;
     std::vector<uint8_t> G;
@@ -860,7 +865,7 @@ int launch_copy(fec_codec* c, const uint8_t* d_cw, const uint8_t* d_er, int64_t 
 }
 
 int launch_recover(fec_codec* c, const uint8_t* d_cw, int64_t P, uint8_t* d_out, int32_t* d_outlen,
-                   void* d_ws, size_t ws_bytes, hipStream_t s) {
+                   void* d_ws, size_t ws_bytes, hipStream_t s, int64_t row_off = 0) {
     const Geometry& g = c->g;
     const int64_t Pout = P - g.T;
     if (Pout <= 0) return FEC_OK;
@@ -888,6 +893,7 @@ int launch_recover(fec_codec* c, const uint8_t* d_cw, int64_t P, uint8_t* d_out,
     ra.erased = w.erased;
     ra.sym_ok = w.sym_ok;
     ra.zero_lost = copy_skips_erased(c, d_out, P) ? 1 : 0;
+    ra.row_off = row_off;
     hipLaunchKernelGGL(fec::fec_recover_kernel, dim3(1024), dim3(256), 0, s, ra);
     HIP_TRY(hipGetLastError());
     return c->end(stop, s);
@@ -913,6 +919,67 @@ int launch_decode(fec_codec* c, const uint8_t* d_cw, const uint8_t* d_er, int64_
     HIP_TRY(hipStreamWaitEvent(s, c->ev_join, 0));
     if (concurrent) return FEC_OK;
     return launch_recover(c, d_cw, P, d_out, d_outlen, d_ws, ws_bytes, s);
+}
+
+// Continuing decode (fec_decode_stream_push): the next P packets of a stream whose earlier packets
+// were pushed before.  The decoder state at the first packet still owed an output depends only on
+// the erasure pattern from the start of the episode it lies in, so the decode restarts, as a fresh
+// decoder, at a cut c <= that packet where the reference decoder is on its fast path and stays
+// there for T more packets (no erasure in [c-T-1, c+T]): from c on a fresh FEC_Decoder and the
+// stream's decoder agree (Decoder.cpp:77-133: the fast path reads only the stored codeword, a
+// resync replays the last T codewords, which lie after c).  The plan covers [c, end); the copy
+// and the recovery write only the rows [next_out, end-T).
+int launch_decode_stream(fec_codec* c, fec_decode_stream* st, const uint8_t* d_cw, const uint8_t* d_er,
+                         const uint8_t* h_er, int64_t P, int64_t history, uint8_t* d_out, int32_t* d_outlen,
+                         int64_t* n_out, void* d_ws, size_t ws_bytes, hipStream_t s) {
+    const int T = c->g.T;
+    const int64_t s0 = st->consumed;                 // absolute index of the first new packet
+    const int64_t next_out = std::max<int64_t>(0, s0 - T);
+    const int64_t end = s0 + P;
+    const int64_t avail = s0 - history;              // first packet in memory
+    *n_out = 0;
+    if (P < 0 || history < 0 || avail < 0) return FEC_ERR_ARG;
+    if (end - T <= next_out) {  // nothing to output yet (stream shorter than T so far)
+        st->consumed = end;
+        return FEC_OK;
+    }
+    if (s0 - next_out > history) return FEC_ERR_HISTORY;  // the copy reads the T packets before s0
+    auto er_at = [&](int64_t x) -> bool { return x >= 0 && x < end && h_er[x - s0] != 0; };
+    // largest valid cut c <= next_out whose check window [c-T-1, c+T] is known (or the stream start)
+    int64_t cut = -1;
+    for (int64_t x = next_out; x >= avail; --x) {
+        if (x - T - 1 < avail && x - T - 1 >= 0) break;  // flags in front of x are not in memory
+        bool ok = true;
+        for (int64_t y = x - T - 1; y <= x + T && ok; ++y) ok = !er_at(y);
+        if (ok || x == 0) {
+            cut = x;
+            break;
+        }
+    }
+    if (cut < 0) return FEC_ERR_HISTORY;
+    const int64_t Pp = end - cut;
+    if (int st2 = check_ws(c, Pp, d_ws, ws_bytes)) return st2;
+    const uint8_t* cw_c = d_cw - (s0 - cut) * c->g.CW;
+    const uint8_t* er_c = d_er - (s0 - cut);
+    HIP_TRY(hipEventRecord(c->ev_fork, s));
+    HIP_TRY(hipStreamWaitEvent(c->side, c->ev_fork, 0));
+    if (int e = launch_plan(c, er_c, Pp, d_ws, ws_bytes, c->side)) return e;
+    HIP_TRY(hipEventRecord(c->ev_join, c->side));
+    // received rows [next_out, end - T): a copy over packets [next_out, end)
+    const int64_t Pc = end - next_out;
+    const uint8_t* cw_o = d_cw - (s0 - next_out) * c->g.CW;
+    const uint8_t* er_o = d_er - (s0 - next_out);
+    const int saved = c->copy_path;
+    if (saved == 3) c->copy_path = 0;  // the wave copy leaves erased rows to the recovery's zero_lost
+    int e = launch_copy(c, cw_o, er_o, Pc, d_out, d_outlen, s);
+    c->copy_path = saved;
+    if (e) return e;
+    HIP_TRY(hipStreamWaitEvent(s, c->ev_join, 0));
+    if (int e2 = launch_recover(c, cw_c, Pp, d_out, d_outlen, d_ws, ws_bytes, s, next_out - cut)) return e2;
+    *n_out = end - T - next_out;
+    st->consumed = end;
+    st->last_cut = cut;
+    return FEC_OK;
 }
 
 template <class F>
@@ -997,6 +1064,7 @@ const char* fec_strerror(int status) {
         case FEC_ERR_NOMEM: return "out of memory";
         case FEC_ERR_WORKSPACE: return "decode workspace too small";
         case FEC_ERR_SEQUENCE: return "sequence numbers must be consecutive from the first call's";
+        case FEC_ERR_HISTORY: return "continuing decode: not enough earlier packets kept in memory";
         default: return "unknown error";
     }
 }
@@ -1052,6 +1120,37 @@ int fec_decode_batch(fec_codec* c, const uint8_t* d_cw, const uint8_t* d_er, int
     if (P > c->g.T && (!d_cw || !d_er || !d_out || !d_outlen)) return FEC_ERR_ARG;
     return launch_decode(c, d_cw, d_er, P, d_out, d_outlen, d_ws, ws_bytes,
                          static_cast<hipStream_t>(stream));
+}
+
+int fec_decode_stream_create(fec_decode_stream** out) {
+    if (!out) return FEC_ERR_ARG;
+    *out = nullptr;
+    return guarded([&] {
+        *out = new fec_decode_stream();
+        return FEC_OK;
+    });
+}
+
+int fec_decode_stream_destroy(fec_decode_stream* st) {
+    delete st;
+    return FEC_OK;
+}
+
+int fec_decode_stream_state(const fec_decode_stream* st, int64_t* consumed, int64_t* last_cut) {
+    if (!st) return FEC_ERR_ARG;
+    if (consumed) *consumed = st->consumed;
+    if (last_cut) *last_cut = st->last_cut;
+    return FEC_OK;
+}
+
+int fec_decode_stream_push(fec_codec* c, fec_decode_stream* st, const uint8_t* d_cw, const uint8_t* d_er,
+                           const uint8_t* h_er, int64_t P, int64_t history, uint8_t* d_out, int32_t* d_outlen,
+                           int64_t* n_out, void* d_ws, size_t ws_bytes, void* stream) {
+    if (!c || !st || !d_cw || !d_er || !h_er || !n_out || !d_out || !d_outlen) return FEC_ERR_ARG;
+    return guarded([&] {
+        return launch_decode_stream(c, st, d_cw, d_er, h_er, P, history, d_out, d_outlen, n_out, d_ws, ws_bytes,
+                                    static_cast<hipStream_t>(stream));
+    });
 }
 
 int fec_decode_plan(fec_codec* c, const uint8_t* d_er, int64_t P, void* d_ws, size_t ws_bytes,

@@ -59,6 +59,12 @@ __device__ __forceinline__ void stage_to_lds(uint8_t* lds, const uint8_t* gbase,
             if (lo >= delta && lo + 16 <= total) *reinterpret_cast<uint4*>(lds + lo) = v[q];
         }
     }
+    // bytes of a range that does not start or end on a dword (a row at an odd / 2-mod-4 offset:
+    // the continuing decode starts mid-buffer), byte by byte
+    if (tid == 0) {
+        for (int b = delta; b < total && (b & 3); ++b) lds[b] = gbase[b];
+        for (int b = total & ~3; b < total && b >= ((delta + 3) & ~3); ++b) lds[b] = gbase[b];
+    }
     // the (at most two) partial chunks at the ends, dword by dword
     for (int o = tid * 4; o < 32; o += nthreads * 4) {
         const int lo16 = delta & ~15, hi16 = total & ~15;

@@ -212,6 +212,7 @@ struct RecArgs {
     uint8_t* out;
     int32_t* out_len;
     int L, k, n, S, CW;
+    int64_t row_off;               // packet x goes to output row x - row_off (x < row_off: skipped)
 };
 
 struct StreamOutArgs {

@@ -479,15 +479,17 @@ __global__ __launch_bounds__(256) void fec_recover_kernel(RecArgs a) {
         const int ner = a.counters[1];
         for (int r = blockIdx.x * 4 + wl; r < ner; r += waves) {
             const int64_t x = a.erased[r];
+            if (x < a.row_off) continue;
             bool ok = true;
             for (int i = 0; i < k; ++i) ok = ok && a.sym_ok[x * k + i];
             if (ok) continue;
-            for (int b = lane; b < L; b += 64) a.out[x * L + b] = 0;
-            if (lane == 0) a.out_len[x] = 0;
+            for (int b = lane; b < L; b += 64) a.out[(x - a.row_off) * L + b] = 0;
+            if (lane == 0) a.out_len[x - a.row_off] = 0;
         }
     }
     for (int r = blockIdx.x * 4 + wl; r < nrec; r += waves) {
         const int64_t x = a.rec_list[r];
+        if (x < a.row_off) continue;  // before the caller's first output row (wave-uniform)
         for (int i = lane; i < k * n; i += 64) {
             const uint8_t c = a.coef[x * k * n + i];
             lc[i] = c ? glog[c] : 255;
@@ -534,10 +536,10 @@ __global__ __launch_bounds__(256) void fec_recover_kernel(RecArgs a) {
                     ln = min(hi * 256 + lo, L);
                 }
                 const int b = h - 2;
-                if (b >= 0 && b < L) outp[x * L + b] = b < ln ? acc : 0;
+                if (b >= 0 && b < L) outp[(x - a.row_off) * L + b] = b < ln ? acc : 0;
             }
         }
-        if (lane == 0) a.out_len[x] = ln;
+        if (lane == 0) a.out_len[x - a.row_off] = ln;
         __builtin_amdgcn_wave_barrier();  // lc is rewritten by the next packet
     }
 }

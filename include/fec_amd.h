@@ -32,6 +32,7 @@ extern "C" {
 #define FEC_ERR_NOMEM (-3)        /* allocation failed */
 #define FEC_ERR_WORKSPACE (-4)    /* decode workspace too small */
 #define FEC_ERR_SEQUENCE (-5)     /* streaming call out of sequence order */
+#define FEC_ERR_HISTORY (-6)      /* continuing decode: not enough earlier packets in memory */
 
 typedef struct fec_codec fec_codec;        /* one (max_payload,T,B,N) configuration on a device */
 typedef struct fec_encoder fec_encoder;    /* one streaming encoder (per stream) */
@@ -96,6 +97,28 @@ size_t fec_decode_workspace_bytes(const fec_codec *codec, int64_t P);
 int fec_decode_batch(fec_codec *codec, const uint8_t *d_codeword, const uint8_t *d_erasure,
                      int64_t P, uint8_t *d_payload_out, int32_t *d_payload_len, void *d_workspace,
                      size_t workspace_bytes, void *hip_stream);
+/* ---- continuing batched decode --------------------------------------------------------------
+ * One stream decoded in consecutive batches, each call continuing where the previous one ended
+ * (the state of src/Decoder.cpp:72-175 -- latest erasure, stored codewords, open episode -- carried
+ * across calls): equal, row for row, to fec_decode_batch over the concatenated stream.
+ * fec_decode_stream_push takes the next P packets (d_codeword, d_erasure on the device; h_erasure
+ * the same P flags on the host -- the receiver knows which packets arrived); `history` rows
+ * BEFORE each of the three pointers are the stream's preceding packets (at least T of them after
+ * the first call).  It writes *n_out rows (the packets whose output became available: from the
+ * first packet not yet output up to the T-th last packet pushed) to d_payload_out / d_payload_len.
+ * Internally the decode restarts at the latest packet where the reference decoder is on its fast
+ * path for T+1 packets on both sides; FEC_ERR_HISTORY if no such packet lies within `history`
+ * (keep more earlier packets: an erasure episode never exceeds the burst length + 2T + 2).
+ * Workspace: fec_decode_workspace_bytes(P + history). */
+typedef struct fec_decode_stream fec_decode_stream;
+int fec_decode_stream_create(fec_decode_stream **out);
+int fec_decode_stream_destroy(fec_decode_stream *st);
+int fec_decode_stream_push(fec_codec *codec, fec_decode_stream *st, const uint8_t *d_codeword,
+                           const uint8_t *d_erasure, const uint8_t *h_erasure, int64_t P, int64_t history,
+                           uint8_t *d_payload_out, int32_t *d_payload_len, int64_t *n_out,
+                           void *d_workspace, size_t workspace_bytes, void *hip_stream);
+/* Packets pushed so far and the packet the last push restarted the decode at. */
+int fec_decode_stream_state(const fec_decode_stream *st, int64_t *consumed, int64_t *last_cut);
 /* The same decode in two halves.  fec_decode_plan needs only the erasure pattern (it can run
  * while the codewords are still being produced or transferred); fec_decode_apply needs the
  * codewords and must be ordered after the plan (same stream, or an event).  fec_decode_batch =

@@ -464,3 +464,83 @@ def test_streaming_api_starts_mid_stream(tbn, start):
         assert p == op and (got == ogot).all(), t
     with pytest.raises(fec.FecError):
         enc.onTransmit(src[0], L, start + P + T + 5)  # later calls stay consecutive
+
+
+def _stream_in_batches(c, cw, er_dev, pat, cuts, history_cap=None):
+    """Push packets [cuts[i], cuts[i+1]) one batch at a time; every push gets the whole stream in
+    front of it as history (or at most history_cap packets).  Returns the concatenated outputs."""
+    ds = fec.DecodeStream(c)
+    outs, lens = [], []
+    for a, b in zip(cuts[:-1], cuts[1:]):
+        h = a if history_cap is None else min(a, history_cap)
+        o, ln = ds.push(cw[a - h:b], er_dev[a - h:b], pat[a - h:b], history=h)
+        outs.append(o.clone())
+        lens.append(ln.clone())
+    return torch.cat(outs), torch.cat(lens), ds
+
+
+def test_continuing_decode_1M_in_uneven_batches_equals_one_shot():
+    """One 1M-packet stream (bin/erasure.bin tiled, (10,3,3)) decoded in 7 uneven batches through
+    fec_decode_stream_push (the decoder state carried across calls) equals the one-shot decode,
+    row for row, with cuts that fall inside erasure episodes."""
+    T, B, N = 10, 3, 3
+    P = 1_000_000
+    pat = np.resize(load_pattern("bin_erasure")[:360000], P + T).astype(np.uint8)
+    c = fec.Codec(L, T, B, N)
+    payload = fec.fill_payload(0, P + T, L, SEED)
+    cw, _ = c.encode(payload)
+    er = torch.from_numpy(pat).cuda()
+    ref, ref_len = c.decode(cw, er)
+    # batch ends on and next to erased packets (mid-episode restarts)
+    ers = np.flatnonzero(pat[:P])
+    cuts = [0, 1, 7, int(ers[100]) + 1, int(ers[2000]) + 3, 400_001, int(ers[9000]), P + T]
+    out, ln, ds = _stream_in_batches(c, cw, er, pat, cuts)
+    torch.cuda.synchronize()
+    assert out.shape[0] == P
+    assert torch.equal(ln, ref_len)
+    assert torch.equal(out, ref)
+    assert ds.state()[0] == P + T
+
+
+@pytest.mark.parametrize("tbn,pattern", [((10, 3, 3), "erasure50"), ((10, 5, 2), "bin_erasure"),
+                                         ((10, 1, 1), "erasure90")])
+def test_continuing_decode_vs_oracle(tbn, pattern):
+    """Continuing decode in batches of 1..997 packets, with only the last 300 packets kept as
+    history, against the oracle's FEC_Decoder fed the same stream packet by packet."""
+    T, B, N = tbn
+    P = 12000
+    pat = load_pattern(pattern)[:P + T].astype(np.uint8)
+    c = fec.Codec(L, T, B, N)
+    payload = fec.fill_payload(0, P + T, L, SEED)
+    cw, _ = c.encode(payload)
+    er = torch.from_numpy(pat).cuda()
+    rng = np.random.default_rng(5)
+    cuts = [0]
+    while cuts[-1] < P + T:
+        cuts.append(min(P + T, cuts[-1] + int(rng.choice([1, 2, 11, 64, 250, 997]))))
+    try:
+        out, ln, _ = _stream_in_batches(c, cw, er, pat, cuts, history_cap=300)
+    except fec.FecError as e:  # an episode longer than the history kept: say so, keep more
+        assert e.status == fec._lib.FEC_ERR_HISTORY
+        out, ln, _ = _stream_in_batches(c, cw, er, pat, cuts)
+    torch.cuda.synchronize()
+    ref = oracle.run_stream(L, T, B, N, P, pat, seed=SEED, want_data=True)
+    assert (ln.cpu().numpy() == ref["out_len"]).all()
+    assert (out.cpu().numpy() == ref["out_data"]).all()
+
+
+def test_continuing_decode_reports_short_history():
+    """A push whose kept history holds no restart point (an erasure every few packets) fails with
+    FEC_ERR_HISTORY instead of decoding from a wrong state."""
+    T, B, N = 10, 3, 3
+    P = 400
+    pat = np.zeros(P + T, dtype=np.uint8)
+    pat[::5] = 1
+    c = fec.Codec(L, T, B, N)
+    cw, _ = c.encode(fec.fill_payload(0, P + T, L, SEED))
+    er = torch.from_numpy(pat).cuda()
+    ds = fec.DecodeStream(c)
+    ds.push(cw[:200], er[:200], pat[:200], history=0)
+    with pytest.raises(fec.FecError) as e:
+        ds.push(cw[200 - 20:P + T], er[200 - 20:P + T], pat[200 - 20:P + T], history=20)
+    assert e.value.status == fec._lib.FEC_ERR_HISTORY
