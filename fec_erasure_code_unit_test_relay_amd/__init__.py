@@ -7,8 +7,8 @@ package mirrors the reference's FEC_Encoder / FEC_Decoder interface and exposes 
 device-resident API used by bench.py and the tests.
 """
 from ._lib import LIB_PATH, FecError, lib  # noqa: F401
-from .codec import Codec, DecodeStream, FEC_Decoder, FEC_Encoder, plan_host  # noqa: F401
+from .codec import Codec, DecodeStream, FEC_Decoder, FEC_Encoder, StreamGroup, plan_host  # noqa: F401
 from .payload import fill_payload  # noqa: F401
 
-__all__ = ["Codec", "DecodeStream", "FEC_Encoder", "FEC_Decoder", "FecError", "plan_host", "fill_payload", "lib",
+__all__ = ["Codec", "DecodeStream", "StreamGroup", "FEC_Encoder", "FEC_Decoder", "FecError", "plan_host", "fill_payload", "lib",
            "LIB_PATH"]

@@ -73,6 +73,11 @@ def lib() -> ctypes.CDLL:
     L.fec_decode_workspace_bytes.argtypes = [vp, i64]
     L.fec_decode_batch.argtypes = [vp, vp, vp, i64, vp, vp, vp, ctypes.c_size_t, vp]
     L.fec_decode_counters.argtypes = [vp, i64p, i64p, i64p]
+    L.fec_streams_create.argtypes = [i32, i32, i32, i32, i32, ctypes.POINTER(vp)]
+    L.fec_streams_destroy.argtypes = [vp]
+    L.fec_streams_encode.argtypes = [vp, vp, i32, vp, vp, vp, vp, vp]
+    L.fec_streams_decode.argtypes = [vp, vp, i32, vp, vp, vp, vp, vp]
+    L.fec_streams_state.argtypes = [vp, i32, i64p, i64p]
     L.fec_decode_stream_create.argtypes = [ctypes.POINTER(vp)]
     L.fec_decode_stream_destroy.argtypes = [vp]
     L.fec_decode_stream_state.argtypes = [vp, i64p, i64p]
@@ -122,7 +127,8 @@ def lib() -> ctypes.CDLL:
                  "fec_codec_set_copy_path", "fec_codec_set_plan_path", "fec_codec_info", "fec_codec_set_episode_dedup", "fec_debug_stamps", "fec_codec_geometry",
                  "fec_codec_generator", "fec_encode_batch", "fec_decode_batch", "fec_decode_plan",
                  "fec_decode_stream_create", "fec_decode_stream_destroy", "fec_decode_stream_state",
-                 "fec_decode_stream_push",
+                 "fec_decode_stream_push", "fec_streams_create", "fec_streams_destroy", "fec_streams_encode",
+                 "fec_streams_decode", "fec_streams_state",
                  "fec_decode_apply", "fec_decode_copy", "fec_decode_recover",
                  "fec_decode_counters", "fec_decode_plan_stats", "fec_timing_enable", "fec_timing_collect",
                  "fec_encoder_create", "fec_encoder_destroy", "fec_encoder_transmit",

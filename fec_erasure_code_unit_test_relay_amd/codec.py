@@ -310,6 +310,56 @@ class DecodeStream:
         return out[:n.value], out_len[:n.value]
 
 
+class StreamGroup:
+    """Many independent streams of one (T,B,N) (fec_streams_*): each call codes the next packet
+    of every listed stream in one launch -- one FEC_Encoder and one FEC_Decoder per stream, held
+    on the device."""
+
+    def __init__(self, max_payload: int, T: int, B: int, N: int, nstreams: int):
+        h = ctypes.c_void_p()
+        check(lib().fec_streams_create(max_payload, T, B, N, nstreams, ctypes.byref(h)), "fec_streams_create")
+        self._h = h
+        self.L, self.T, self.nstreams = max_payload, T, nstreams
+        c = Codec(max_payload, T, B, N)
+        self.k, self.n, self.S, self.CW = c.k, c.n, c.S, c.CW
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h:
+            lib().fec_streams_destroy(h)
+            self._h = None
+
+    def encode(self, ids, payload, lengths=None, out=None, out_len=None):
+        """ids: host int32 [M] distinct stream ids; payload [M, L] uint8 GPU -> (cw [M, CW], sizes [M])."""
+        import torch
+        ids = np.ascontiguousarray(ids, dtype=np.int32)
+        M = ids.size
+        assert payload.dtype == torch.uint8 and payload.is_cuda and payload.is_contiguous()
+        assert tuple(payload.shape) == (M, self.L)
+        if lengths is not None:
+            assert lengths.dtype == torch.int32 and lengths.is_cuda and lengths.numel() == M
+        out, out_len = _check_out(torch, out, out_len, M, self.CW, payload.device)
+        check(lib().fec_streams_encode(self._h, ids.ctypes.data_as(ctypes.c_void_p), M, _ptr(payload), _ptr(lengths),
+                                       _ptr(out), _ptr(out_len), _stream_handle(torch)), "fec_streams_encode")
+        return out, out_len
+
+    def decode(self, ids, erasure, codewords, out=None, out_len=None):
+        """ids: host int32 [M]; erasure: host uint8 [M]; codewords [M, CW] GPU -> (payload [M, L],
+        lengths [M]): row m = packet seq-T of stream ids[m]."""
+        import torch
+        ids = np.ascontiguousarray(ids, dtype=np.int32)
+        er = np.ascontiguousarray(erasure, dtype=np.uint8)
+        M = ids.size
+        assert er.size == M
+        assert codewords.dtype == torch.uint8 and codewords.is_cuda and codewords.is_contiguous()
+        assert tuple(codewords.shape) == (M, self.CW)
+        out, out_len = _check_out(torch, out, out_len, M, self.L, codewords.device)
+        check(lib().fec_streams_decode(self._h, ids.ctypes.data_as(ctypes.c_void_p), M,
+                                       er.ctypes.data_as(ctypes.c_void_p), _ptr(codewords), _ptr(out), _ptr(out_len),
+                                       _stream_handle(torch)), "fec_streams_decode")
+        return out, out_len
+
+
 class FEC_Encoder:
     """FEC_Encoder(max_payload, T, B, N) -- per-packet interface (src/FEC_Encoder.cpp:22-68)."""
 

@@ -222,8 +222,6 @@ __device__ __forceinline__ void tile_walk(const EncTileArgs& a, uint8_t* smem) {
 
     const __amdgpu_buffer_rsrc_t rs =
         __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(a.payload_base), 0, a.payload_bytes, 0x00020000);
-    const __amdgpu_buffer_rsrc_t rl =
-        __builtin_amdgcn_make_buffer_rsrc(const_cast<int32_t*>(a.len_base), 0, a.len_bytes, 0x00020000);
     const __amdgpu_buffer_rsrc_t rc = __builtin_amdgcn_make_buffer_rsrc(a.cw, 0, a.cw_bytes, 0x00020000);
     const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc(a.cw_len, 0, 4 * P, 0x00020000);
     const bool has_len = a.len_base != nullptr;
@@ -288,7 +286,6 @@ __device__ __forceinline__ void tile_walk(const EncTileArgs& a, uint8_t* smem) {
         wait_lds_barrier();  // B1: the tile is in LDS everywhere; last tile's output stored
         const int row0 = (first - 1 + it) * R;
         const uint8_t* in = smem + a.off_in + (it & 1) * a.in_bytes;
-        const uint32_t* inw = reinterpret_cast<const uint32_t*>(in);
         if (L & 15) {
             // the batch's last row: its last piece runs past the end of the payload rows, and an
             // LDS-DMA out of range as a whole reads zeros: its valid dwords again, one by one

@@ -1,0 +1,383 @@
+// fec_streams.hip -- many independent streams of one (T,B,N), one packet of each per call, coded in
+// one launch (north_star: "many independent (T,B,N) coding windows batched across wavefronts").
+//
+// The reference runs one FEC_Encoder / FEC_Decoder per stream (include/FEC_Encoder.h:26-48,
+// FEC_Decoder.h:27-46), one packet per onTransmit / onReceive call, and keeps each stream's state
+// inside those objects.  Here a group holds the state of N streams in HBM:
+//   * encoder: the last n-1 windows X_{t-1..t-n+1} of every stream (bytes [len_hi, len_lo,
+//     payload, zero pad] of S*k bytes, Encoder.cpp:73-95), a ring indexed by seq % (n-1);
+//   * decoder: the last RR received codewords of every stream (zero padded like
+//     FEC_Decoder.cpp:55-63), a ring indexed by seq % RR, and per stream the symbolic planner
+//     (fec::StreamPlanner, the reference decoder's state machine without the bytes) on the host.
+// A call names M distinct streams and hands over one packet of each; one wave per packet does
+// its byte work: the encoder's closed form (Encoder.cpp:65-98 -> codingOperations.cpp:131-147)
+// over the stream's window, or the decoder's output for packet seq - T (fast path copy,
+// Decoder.cpp:77-108, or the planner's recovery coefficients, codingOperations.cpp:149-232).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <algorithm>
+#include <cstring>
+#include <memory>
+#include <new>
+#include <vector>
+
+#include "fec_amd.h"
+#include "fec_host.h"
+#include "fec_kernels.h"
+
+namespace fec {
+namespace {
+
+constexpr int kRR = 64;  // decoder ring rows per stream (>= T + k, the per-packet decoder's)
+
+struct StreamsEncArgs {
+    const uint8_t* payload;  // M rows of L bytes
+    const int32_t* len;      // M payload sizes (null: all L)
+    const int32_t* ids;      // M stream ids
+    const int64_t* seq;      // M: packets the stream sent before this one
+    uint8_t* win;            // [streams][W][SK] window ring
+    uint8_t* cw;             // M rows of CW bytes
+    int32_t* cw_len;         // M trimmed sizes
+    const uint8_t* G;        // k x n
+    const uint8_t* gf;       // exp[512], log[256]
+    int M, L, k, n, S, CW, SK, W;
+};
+
+struct StreamItem {
+    int32_t id;
+    int32_t fate;    // PacketFate of the packet output by this call (x = seq - T)
+    int32_t clamp;   // slow path: payload clamped to L (Decoder.cpp:148-149)
+    int32_t coef;    // kRecovered: index of its k x n block in coefs
+    int64_t seq;     // packets the stream received before this one
+    int64_t x;       // packet output by this call
+    int32_t erased;  // this call's packet is missing
+    int32_t pad;
+};
+
+struct StreamsDecArgs {
+    const uint8_t* cw_in;    // M rows of CW bytes (rows of erased packets are not read)
+    const StreamItem* items;
+    const uint8_t* coefs;    // recovered outputs' coefficient blocks
+    uint8_t* ring;           // [streams][RR][CW]
+    const uint8_t* gf;
+    uint8_t* out;            // M rows of L bytes
+    int32_t* out_len;
+    int M, L, k, n, CW, RR;
+};
+
+__device__ __forceinline__ uint8_t gmul(const uint8_t* gexp, const uint8_t* glog, uint8_t a, uint8_t b) {
+    return (a && b) ? gexp[glog[a] + glog[b]] : 0;
+}
+
+// One wave per packet: lane = sub-stream (and sub-stream + 64, ...).
+__global__ __launch_bounds__(256) void fec_streams_encode_kernel(StreamsEncArgs a) {
+    __shared__ uint8_t gexp[512];
+    __shared__ uint8_t glog[256];
+    __shared__ uint8_t Gs[16 * 32];
+    const int tid = threadIdx.x;
+    for (int i = tid; i < 512; i += 256) gexp[i] = a.gf[i];
+    for (int i = tid; i < 256; i += 256) glog[i] = a.gf[512 + i];
+    for (int i = tid; i < a.k * a.n; i += 256) Gs[i] = a.G[i];
+    __syncthreads();
+    const int m = blockIdx.x * 4 + (tid >> 6), lane = tid & 63;
+    if (m >= a.M) return;
+    const int L = a.L, k = a.k, n = a.n, S = a.S, CW = a.CW, SK = a.SK, W = a.W;
+    const int ln = a.len ? min(max(a.len[m], 0), L) : L;
+    const int64_t seq = a.seq[m];
+    uint8_t* win = a.win + static_cast<int64_t>(a.ids[m]) * W * SK;
+    const uint8_t* pay = a.payload + static_cast<int64_t>(m) * L;
+    uint8_t* cwo = a.cw + static_cast<int64_t>(m) * CW;
+    int last = -1;  // last non-zero codeword byte of this lane's sub-streams
+    for (int s = lane; s < S; s += 64) {
+        uint8_t x[16];
+        for (int i = 0; i < k; ++i) {  // window bytes s*k + i (Encoder.cpp:75-83, zero padded)
+            const int b = s * k + i;
+            x[i] = b == 0 ? static_cast<uint8_t>(ln >> 8)
+                          : b == 1 ? static_cast<uint8_t>(ln & 0xff) : (b - 2 < ln ? pay[b - 2] : 0);
+        }
+        for (int j = 0; j < n; ++j) {
+            uint8_t v;
+            if (j < k) {
+                v = x[j];
+            } else {  // parity: XOR_i G[i][j] * X_{t-(j-i)}[s][i], rows before the stream start = 0
+                v = 0;
+                for (int i = 0; i < k; ++i) {
+                    const int d = j - i;
+                    if (seq - d < 0) continue;
+                    const uint8_t xb = win[((seq - d) % W) * SK + s * k + i];
+                    v ^= gmul(gexp, glog, Gs[i * n + j], xb);
+                }
+            }
+            cwo[s * n + j] = v;
+            if (v) last = s * n + j;
+        }
+        // this lane's own bytes of slot seq % W: read above (d = W), now overwritten
+        for (int i = 0; i < k; ++i) win[(seq % W) * SK + s * k + i] = x[i];
+    }
+    for (int d = 32; d >= 1; d >>= 1) last = max(last, __shfl_xor(last, d, 64));
+    if (lane == 0) a.cw_len[m] = last + 1;  // FEC_Encoder.cpp:55-60
+}
+
+// One wave per packet: store the received codeword in the stream's ring, output packet x.
+__global__ __launch_bounds__(256) void fec_streams_decode_kernel(StreamsDecArgs a) {
+    __shared__ uint8_t gexp[512];
+    __shared__ uint8_t glog[256];
+    const int tid = threadIdx.x;
+    for (int i = tid; i < 512; i += 256) gexp[i] = a.gf[i];
+    for (int i = tid; i < 256; i += 256) glog[i] = a.gf[512 + i];
+    __syncthreads();
+    const int m = blockIdx.x * 4 + (tid >> 6), lane = tid & 63;
+    if (m >= a.M) return;
+    const StreamItem it = a.items[m];
+    const int L = a.L, k = a.k, n = a.n, CW = a.CW, RR = a.RR;
+    uint8_t* ring = a.ring + static_cast<int64_t>(it.id) * RR * CW;
+    const uint8_t* cwin = a.cw_in + static_cast<int64_t>(m) * CW;
+    if (!it.erased)  // FEC_Decoder.cpp:55-59: the decoder keeps its own copy
+        for (int b = lane; b < CW; b += 64) ring[(it.seq % RR) * CW + b] = cwin[b];
+    // symbol (s, q) of packet sp: this call's codeword straight from the input (the ring row it
+    // was just written to is not read back), older ones from the ring
+    auto sym = [&](int64_t sp, int o) -> uint8_t {
+        return sp == it.seq ? cwin[o] : ring[(((sp % RR) + RR) % RR) * CW + o];  // sp < 0: a zero row
+    };
+    uint8_t* orow = a.out + static_cast<int64_t>(m) * L;
+    if (it.fate == kNone || it.fate == kLost) {
+        for (int b = lane; b < L; b += 64) orow[b] = 0;
+        if (lane == 0) a.out_len[m] = 0;
+        return;
+    }
+    const uint8_t* coef = a.coefs + static_cast<int64_t>(it.coef) * k * n;
+    // header bytes 0, 1 (sub-stream 0, positions 0 and 1 -> (1/k)*n + 1%k) first: they bound the copy
+    auto byte_at = [&](int h) -> uint8_t {
+        const int s = h / k, i = h - s * k;
+        if (it.fate == kCopy) return sym(it.x, s * n + i);
+        uint8_t acc = 0;
+        for (int q = 0; q < n; ++q) {
+            const uint8_t c = coef[i * n + q];
+            if (c) acc ^= gmul(gexp, glog, c, sym(it.x - i + q, s * n + q));
+        }
+        return acc;
+    };
+    const int hdr = byte_at(0) * 256 + byte_at(1);
+    const int ln = it.clamp ? min(hdr, L) : hdr;
+    const int cp = min(ln, L);
+    for (int b = lane; b < L; b += 64) orow[b] = b < cp ? byte_at(b + 2) : 0;
+    if (lane == 0) a.out_len[m] = ln;
+}
+
+}  // namespace
+}  // namespace fec
+
+struct fec_streams {
+    fec_codec* codec = nullptr;
+    fec::Geometry g;
+    int nstreams = 0, W = 1, SK = 0;
+    std::shared_ptr<const fec::DecodeRules> rules;
+    std::vector<std::unique_ptr<fec::StreamPlanner>> planners;
+    std::vector<int64_t> enc_seq, dec_seq;   // packets sent / received so far per stream
+    std::vector<uint32_t> mark;              // duplicate-id check (call stamp per stream)
+    uint32_t stamp = 0;
+    uint8_t* d_win = nullptr;                // encoder windows
+    uint8_t* d_ring = nullptr;               // decoder rings
+    void* d_stage = nullptr;                 // per-call records (ids + seqs / items + coefs)
+    void* h_stage = nullptr;                 // pinned twin of d_stage
+    size_t stage_bytes = 0;
+    hipEvent_t staged = nullptr;             // the last upload from h_stage
+    ~fec_streams() {
+        if (staged) (void)hipEventDestroy(staged);
+        for (void* p : {static_cast<void*>(d_win), static_cast<void*>(d_ring), d_stage})
+            if (p) (void)hipFree(p);
+        if (h_stage) (void)hipHostFree(h_stage);
+        if (codec) fec_codec_destroy(codec);
+    }
+};
+
+namespace {
+
+#define FS_TRY(expr)                              \
+    do {                                          \
+        if ((expr) != hipSuccess) return FEC_ERR_HIP; \
+    } while (0)
+
+// ids distinct and in range
+int check_ids(fec_streams* h, const int32_t* ids, int M) {
+    if (++h->stamp == 0) {
+        std::fill(h->mark.begin(), h->mark.end(), 0u);
+        h->stamp = 1;
+    }
+    for (int m = 0; m < M; ++m) {
+        const int id = ids[m];
+        if (id < 0 || id >= h->nstreams || h->mark[id] == h->stamp) return FEC_ERR_ARG;
+        h->mark[id] = h->stamp;
+    }
+    return FEC_OK;
+}
+
+// the previous call's records have left the pinned staging buffer
+int stage_free(fec_streams* h) {
+    FS_TRY(hipEventSynchronize(h->staged));
+    return FEC_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int fec_streams_create(int max_payload, int T, int B, int N, int nstreams, fec_streams** out) {
+    if (!out || nstreams <= 0) return FEC_ERR_ARG;
+    *out = nullptr;
+    try {
+        std::unique_ptr<fec_streams> h(new fec_streams());
+        if (int st = fec_codec_create(max_payload, T, B, N, &h->codec)) return st;
+        fec::CodecView v;
+        if (int st = fec::codec_view(h->codec, &v)) return st;
+        h->g = fec::Geometry::make(max_payload, T, B, N);
+        const fec::Geometry& g = h->g;
+        if (g.T + g.k > fec::kRR || g.k > 16 || g.k * g.n > 16 * 32) return FEC_ERR_ARG;
+        h->nstreams = nstreams;
+        h->W = std::max(1, g.n - 1);
+        h->SK = g.S * g.k;
+        h->rules = fec::shared_decode_rules(T, B, N);
+        h->planners.resize(nstreams);
+        for (auto& p : h->planners) p.reset(new fec::StreamPlanner(g, h->rules.get()));
+        h->enc_seq.assign(nstreams, 0);
+        h->dec_seq.assign(nstreams, 0);
+        h->mark.assign(nstreams, 0);
+        const size_t wb = static_cast<size_t>(nstreams) * h->W * h->SK;
+        const size_t rb = static_cast<size_t>(nstreams) * fec::kRR * g.CW;
+        FS_TRY(hipMalloc(&h->d_win, wb));
+        FS_TRY(hipMemset(h->d_win, 0, wb));
+        FS_TRY(hipMalloc(&h->d_ring, rb));
+        FS_TRY(hipMemset(h->d_ring, 0, rb));
+        h->stage_bytes = static_cast<size_t>(nstreams) * (sizeof(fec::StreamItem) + g.k * g.n + 16) + 64;
+        FS_TRY(hipMalloc(&h->d_stage, h->stage_bytes));
+        FS_TRY(hipHostMalloc(&h->h_stage, h->stage_bytes));
+        FS_TRY(hipEventCreateWithFlags(&h->staged, hipEventDisableTiming));
+        FS_TRY(hipEventRecord(h->staged, nullptr));
+        *out = h.release();
+        return FEC_OK;
+    } catch (const std::bad_alloc&) {
+        return FEC_ERR_NOMEM;
+    } catch (...) {
+        return FEC_ERR_ARG;
+    }
+}
+
+int fec_streams_destroy(fec_streams* h) {
+    delete h;
+    return FEC_OK;
+}
+
+int fec_streams_encode(fec_streams* h, const int32_t* ids, int M, const uint8_t* d_payload,
+                       const int32_t* d_payload_len, uint8_t* d_codeword, int32_t* d_codeword_len,
+                       void* stream) {
+    if (!h || M < 0 || M > h->nstreams || (M > 0 && (!ids || !d_payload || !d_codeword || !d_codeword_len)))
+        return FEC_ERR_ARG;
+    if (M == 0) return FEC_OK;
+    if (int st = check_ids(h, ids, M)) return st;
+    if (int st = stage_free(h)) return st;
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    int64_t* hseq = static_cast<int64_t*>(h->h_stage);
+    int32_t* hid = reinterpret_cast<int32_t*>(hseq + M);
+    for (int m = 0; m < M; ++m) {
+        hseq[m] = h->enc_seq[ids[m]]++;
+        hid[m] = ids[m];
+    }
+    const size_t bytes = static_cast<size_t>(M) * 12;
+    FS_TRY(hipMemcpyAsync(h->d_stage, h->h_stage, bytes, hipMemcpyHostToDevice, s));
+    FS_TRY(hipEventRecord(h->staged, s));
+    fec::CodecView v;
+    fec::codec_view(h->codec, &v);
+    fec::StreamsEncArgs a;
+    a.payload = d_payload;
+    a.len = d_payload_len;
+    a.seq = static_cast<const int64_t*>(h->d_stage);
+    a.ids = reinterpret_cast<const int32_t*>(static_cast<const int64_t*>(h->d_stage) + M);
+    a.win = h->d_win;
+    a.cw = d_codeword;
+    a.cw_len = d_codeword_len;
+    a.G = v.G;
+    a.gf = v.gf;
+    a.M = M;
+    a.L = h->g.L;
+    a.k = h->g.k;
+    a.n = h->g.n;
+    a.S = h->g.S;
+    a.CW = h->g.CW;
+    a.SK = h->SK;
+    a.W = h->W;
+    hipLaunchKernelGGL(fec::fec_streams_encode_kernel, dim3((M + 3) / 4), dim3(256), 0, s, a);
+    FS_TRY(hipGetLastError());
+    return FEC_OK;
+}
+
+int fec_streams_decode(fec_streams* h, const int32_t* ids, int M, const uint8_t* erasure,
+                       const uint8_t* d_codeword, uint8_t* d_payload_out, int32_t* d_payload_len,
+                       void* stream) {
+    if (!h || M < 0 || M > h->nstreams || (M > 0 && (!ids || !erasure || !d_codeword || !d_payload_out ||
+                                                     !d_payload_len)))
+        return FEC_ERR_ARG;
+    if (M == 0) return FEC_OK;
+    if (int st = check_ids(h, ids, M)) return st;
+    if (int st = stage_free(h)) return st;
+    const fec::Geometry& g = h->g;
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    fec::StreamItem* items = static_cast<fec::StreamItem*>(h->h_stage);
+    uint8_t* coefs = reinterpret_cast<uint8_t*>(items + M);
+    const int kn = g.k * g.n;
+    int ncoef = 0;
+    try {
+        for (int m = 0; m < M; ++m) {
+            const int id = ids[m];
+            const bool er = erasure[m] != 0;
+            const int64_t seq = h->dec_seq[id]++;
+            const fec::StepResult r = h->planners[id]->step(seq, er);
+            fec::StreamItem& it = items[m];
+            it.id = id;
+            it.fate = r.fate;
+            it.clamp = r.slow ? 1 : 0;
+            it.coef = 0;
+            it.seq = seq;
+            it.x = r.x;
+            it.erased = er ? 1 : 0;
+            it.pad = 0;
+            if (r.fate == fec::kRecovered) {
+                std::memcpy(coefs + static_cast<size_t>(ncoef) * kn, r.coef, kn);
+                it.coef = ncoef++;
+            }
+        }
+    } catch (...) {
+        return FEC_ERR_ARG;
+    }
+    const size_t bytes = static_cast<size_t>(M) * sizeof(fec::StreamItem) + static_cast<size_t>(ncoef) * kn;
+    FS_TRY(hipMemcpyAsync(h->d_stage, h->h_stage, bytes, hipMemcpyHostToDevice, s));
+    FS_TRY(hipEventRecord(h->staged, s));
+    fec::CodecView v;
+    fec::codec_view(h->codec, &v);
+    fec::StreamsDecArgs a;
+    a.cw_in = d_codeword;
+    a.items = static_cast<const fec::StreamItem*>(h->d_stage);
+    a.coefs = reinterpret_cast<const uint8_t*>(a.items + M);
+    a.ring = h->d_ring;
+    a.gf = v.gf;
+    a.out = d_payload_out;
+    a.out_len = d_payload_len;
+    a.M = M;
+    a.L = g.L;
+    a.k = g.k;
+    a.n = g.n;
+    a.CW = g.CW;
+    a.RR = fec::kRR;
+    hipLaunchKernelGGL(fec::fec_streams_decode_kernel, dim3((M + 3) / 4), dim3(256), 0, s, a);
+    FS_TRY(hipGetLastError());
+    return FEC_OK;
+}
+
+int fec_streams_state(const fec_streams* h, int id, int64_t* sent, int64_t* received) {
+    if (!h || id < 0 || id >= h->nstreams) return FEC_ERR_ARG;
+    if (sent) *sent = h->enc_seq[id];
+    if (received) *received = h->dec_seq[id];
+    return FEC_OK;
+}
+
+}  // extern "C"

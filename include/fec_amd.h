@@ -144,6 +144,33 @@ int fec_decode_counters(const void *d_workspace, int64_t *episodes, int64_t *rec
  * replayed episode of the same loss shape (fec_codec_set_episode_dedup). */
 int fec_decode_plan_stats(const void *d_ws, int64_t *replayed, int64_t *filled);
 
+/* ---- many independent streams, one packet of each per call ---------------------------------
+ * A group of `nstreams` independent streams of one (max_payload,T,B,N): the state of one
+ * FEC_Encoder and one FEC_Decoder per stream (include/FEC_Encoder.h:26-48, FEC_Decoder.h:27-46)
+ * held in HBM (encoder windows, decoder codeword rings) plus the decoders' symbolic state on the
+ * host.  One call hands over the next packet of each of M distinct streams (ids[m], host array)
+ * and codes all of them in one launch -- the relay / receiver load of many 300-byte streams.
+ *   fec_streams_encode  = FEC_Encoder::onTransmit per stream: d_payload M rows of max_payload
+ *                         bytes, d_payload_len M sizes (NULL = all max_payload) -> d_codeword M rows
+ *                         of CW bytes (untrimmed) + d_codeword_len M trimmed wire sizes.
+ *   fec_streams_decode  = FEC_Decoder::onReceive per stream: erasure M host flags (1 = packet
+ *                         missing), d_codeword M rows of CW bytes (zero padded; rows of missing
+ *                         packets are not read) -> d_payload_out row m = the stream's packet seq-T
+ *                         (seq = packets that stream had received before), d_payload_len m
+ *                         (0 = lost or not available yet).
+ * Asynchronous on hip_stream; ids must be distinct within a call (FEC_ERR_ARG otherwise). */
+typedef struct fec_streams fec_streams;
+int fec_streams_create(int max_payload, int T, int B, int N, int nstreams, fec_streams **out);
+int fec_streams_destroy(fec_streams *group);
+int fec_streams_encode(fec_streams *group, const int32_t *ids, int M, const uint8_t *d_payload,
+                       const int32_t *d_payload_len, uint8_t *d_codeword, int32_t *d_codeword_len,
+                       void *hip_stream);
+int fec_streams_decode(fec_streams *group, const int32_t *ids, int M, const uint8_t *erasure,
+                       const uint8_t *d_codeword, uint8_t *d_payload_out, int32_t *d_payload_len,
+                       void *hip_stream);
+/* Packets stream `id` has sent (encoded) and received (decoded) so far. */
+int fec_streams_state(const fec_streams *group, int id, int64_t *sent, int64_t *received);
+
 /* ---- per-kernel timing (HIP events recorded on the launch stream) --------------------------- */
 #define FEC_KERNEL_ENCODE 0
 #define FEC_KERNEL_DEC_SCAN 1

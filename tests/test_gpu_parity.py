@@ -544,3 +544,57 @@ def test_continuing_decode_reports_short_history():
     with pytest.raises(fec.FecError) as e:
         ds.push(cw[200 - 20:P + T], er[200 - 20:P + T], pat[200 - 20:P + T], history=20)
     assert e.value.status == fec._lib.FEC_ERR_HISTORY
+
+
+@pytest.mark.parametrize("tbn,pattern", [((10, 3, 3), "bin_erasure"), ((10, 5, 2), "erasure50"),
+                                         ((10, 1, 1), "erasure90"), ((10, 0, 0), "erasure10")])
+def test_stream_group_equals_per_stream_coders(tbn, pattern):
+    """37 independent streams, each call carrying the next packet of a random subset of them (one
+    launch per call): every stream's codewords and sizes equal a fresh FEC_Encoder's over that
+    stream alone, and every stream's decoded rows equal the one-shot decoder's (the oracle-checked
+    batch decode) over its own erasure pattern -- a different phase of the shipped pattern each."""
+    T, B, N = tbn
+    ns, P = 37, 600
+    base = load_pattern(pattern).astype(np.uint8)
+    pats = [base[(s * 7919) % (base.size - P - T):][:P + T] for s in range(ns)]
+    payloads = [fec.fill_payload(0, P + T, L, SEED + s) for s in range(ns)]
+    c = fec.Codec(L, T, B, N)
+    ref_cw, ref_out = [], []
+    for s in range(ns):
+        cw, wl = c.encode(payloads[s])
+        o, ol = c.decode(cw, torch.from_numpy(pats[s]).cuda())
+        ref_cw.append((cw, wl))
+        ref_out.append((o, ol))
+    grp = fec.StreamGroup(L, T, B, N, ns)
+    rng = np.random.default_rng(11)
+    sent = np.zeros(ns, dtype=np.int64)
+    got_cw = [[] for _ in range(ns)]
+    got_out = [[] for _ in range(ns)]
+    while (sent < P + T).any():
+        live = np.flatnonzero(sent < P + T)
+        ids = rng.permutation(live)[:max(1, int(rng.integers(1, live.size + 1)))].astype(np.int32)
+        pay = torch.stack([payloads[s][sent[s]] for s in ids])
+        cw, wl = grp.encode(ids, pay)
+        er = np.array([pats[s][sent[s]] for s in ids], dtype=np.uint8)
+        out, ol = grp.decode(ids, er, cw)
+        torch.cuda.synchronize()
+        for j, s in enumerate(ids):
+            got_cw[s].append((cw[j].clone(), wl[j].clone()))
+            got_out[s].append((out[j].clone(), ol[j].clone()))
+        sent[ids] += 1
+    for s in range(ns):
+        cw = torch.stack([x[0] for x in got_cw[s]])
+        wl = torch.stack([x[1] for x in got_cw[s]])
+        assert torch.equal(cw, ref_cw[s][0]) and torch.equal(wl, ref_cw[s][1]), s
+        out = torch.stack([x[0] for x in got_out[s]])[T:]
+        ol = torch.stack([x[1] for x in got_out[s]])
+        assert bool((ol[:T] == 0).all()), s
+        assert torch.equal(ol[T:], ref_out[s][1]), s
+        assert torch.equal(out, ref_out[s][0]), s
+
+
+def test_stream_group_rejects_repeated_ids():
+    grp = fec.StreamGroup(L, 10, 3, 3, 8)
+    pay = fec.fill_payload(0, 2, L, SEED)
+    with pytest.raises(fec.FecError):
+        grp.encode(np.array([3, 3], dtype=np.int32), pay)
