@@ -142,7 +142,9 @@ namespace {
 int codec_init(fec_codec* c, int max_payload, int T, int B, int N) {
     c->g = Geometry::make(max_payload, T, B, N);
     const Geometry& g = c->g;
-    if (g.L > kMaxPayload || g.B < g.N || g.n > fec::kMaxRuleN) return FEC_ERR_ARG;
+    // n <= 17: decode rules tabulated per (window, erasure mask); n up to 31: computed on demand
+    // (host) and by the planner's wave (device)
+    if (g.L > kMaxPayload || g.B < g.N || g.n > fec::kMaxN - 1) return FEC_ERR_ARG;
     c->G = fec::make_generator(T, B, N);
     c->rules = fec::shared_decode_rules(T, B, N);
     const fec::Field& F = fec::field();
@@ -721,6 +723,7 @@ int launch_plan(fec_codec* c, const uint8_t* d_er, int64_t P, void* d_ws, size_t
     pa.P = P;
     pa.Pout = Pout;
     pa.rules = c->d_rules;
+    pa.G = c->d_G;
     for (int i = 0; i <= fec::kPlanMaxN; ++i)
         pa.wbase[i] = (i < static_cast<int>(c->rules->w_base.size())) ? c->rules->w_base[i] : -1;
     pa.gf = c->d_gf;
@@ -744,7 +747,7 @@ int launch_plan(fec_codec* c, const uint8_t* d_er, int64_t P, void* d_ws, size_t
         void* args[] = {&pa};
         HIP_TRY(hipLaunchKernel(c->plan_fast, dim3(pgrid), dim3(64), args, 0, s));
     } else {
-        const int plan_lds = 768 + g.n * g.n + 2 * g.k * g.n;
+        const int plan_lds = 768 + g.n * g.n + 2 * g.k * g.n + 32 * 16 + 32 * 32 + g.k * (1 + g.n);
         hipLaunchKernelGGL(fec::fec_plan_kernel, dim3(pgrid), dim3(64), plan_lds, s, pa);
     }
     HIP_TRY(hipGetLastError());
@@ -894,7 +897,10 @@ int launch_recover(fec_codec* c, const uint8_t* d_cw, int64_t P, uint8_t* d_out,
     ra.sym_ok = w.sym_ok;
     ra.zero_lost = copy_skips_erased(c, d_out, P) ? 1 : 0;
     ra.row_off = row_off;
-    hipLaunchKernelGGL(fec::fec_recover_kernel, dim3(1024), dim3(256), 0, s, ra);
+    if (g.n <= 17)
+        hipLaunchKernelGGL(fec::fec_recover_kernel_t<17>, dim3(1024), dim3(256), 0, s, ra);
+    else
+        hipLaunchKernelGGL(fec::fec_recover_kernel_t<32>, dim3(1024), dim3(256), 0, s, ra);
     HIP_TRY(hipGetLastError());
     return c->end(stop, s);
 }
@@ -1480,7 +1486,7 @@ int fec_plan_host(int max_payload, int T, int B, int N, const uint8_t* erasure, 
     if (!erasure || !fate || P < 0) return FEC_ERR_ARG;
     return guarded([&] {
         const Geometry g = Geometry::make(max_payload, T, B, N);
-        if (g.B < g.N || g.n > fec::kMaxRuleN) return FEC_ERR_ARG;
+        if (g.B < g.N || g.n > fec::kMaxN - 1) return FEC_ERR_ARG;
         const auto rules = fec::shared_decode_rules(T, B, N);
         fec::StreamPlanner pl(g, rules.get());
         for (int64_t t = 0; t < P; ++t) {
@@ -1520,6 +1526,7 @@ static int launch_block(fec_codec* c, bool decode, const uint8_t* d_in, const ui
     if (!c || nblk < 0 || (nblk > 0 && (!d_in || !d_out || (decode && !d_er)))) return FEC_ERR_ARG;
     if (nblk == 0) return FEC_OK;
     const Geometry& g = c->g;
+    if (decode && c->rules->lazy) return FEC_ERR_ARG;  // block decode reads the window-n rule table
     fec::BlockArgs a;
     a.in = d_in;
     a.er = d_er;

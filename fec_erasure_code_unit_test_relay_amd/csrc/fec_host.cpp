@@ -127,10 +127,14 @@ void DecodeRules::build(const std::vector<uint8_t>& G, int k_, int n_, int T_) {
     k = k_;
     n = n_;
     T = T_;
-    if (n > kMaxRuleN) throw std::invalid_argument("decode rules need n <= 17");
     w_lo = std::min(T + 1, n);
     entry_bytes = (k * (1 + n) + 3) & ~3;  // padded: the GPU loads an entry as dwords
     w_base.assign(n + 1, -1);
+    this->G = G;
+    if (n > kMaxRuleN) {  // 2^n masks: no table, rules on demand (host) / in the wave (device)
+        lazy = true;
+        return;
+    }
     int64_t total = 0;
     for (int w = w_lo; w <= n; ++w) {
         w_base[w] = total;
@@ -163,6 +167,20 @@ void DecodeRules::build(const std::vector<uint8_t>& G, int k_, int n_, int T_) {
         for (unsigned i = 0; i < nth; ++i) pool.emplace_back(worker);
         for (auto& th : pool) th.join();
     }
+}
+
+const uint8_t* DecodeRules::lazy_entry(int w, uint32_t mask) const {
+    const uint64_t key = (uint64_t(w) << 32) | mask;
+    std::lock_guard<std::mutex> lock(mu_);
+    auto it = cache_.find(key);
+    if (it != cache_.end()) return it->second.get();
+    std::unique_ptr<uint8_t[]> e(new uint8_t[entry_bytes]());
+    uint8_t col[kMaxK * kMaxN];
+    decode_rule(G.data(), k, n, w, mask, e.get(), col);
+    for (int i = 0; i < k; ++i) std::memcpy(e.get() + k + i * n, col + i * w, w);
+    const uint8_t* p = e.get();
+    cache_.emplace(key, std::move(e));
+    return p;
 }
 
 std::shared_ptr<const DecodeRules> shared_decode_rules(int T, int B, int N) {

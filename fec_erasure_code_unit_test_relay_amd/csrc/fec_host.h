@@ -22,6 +22,8 @@
 #include <cstring>
 #include <memory>
 #include <stdexcept>
+#include <mutex>
+#include <unordered_map>
 #include <vector>
 
 namespace fec {
@@ -94,12 +96,22 @@ struct DecodeRules {
     int k = 0, n = 0, T = 0;
     int w_lo = 0;                      // smallest window that occurs: min(T+1, n)
     int entry_bytes = 0;               // k * (1 + n) rounded up to a multiple of 4
-    std::vector<int64_t> w_base;       // byte offset of window w's table (index w)
+    std::vector<int64_t> w_base;       // byte offset of window w's table (index w; -1: no table)
     std::vector<uint8_t> table;
+    // n > kMaxRuleN: no table (2^n masks); each (w, mask) that occurs is computed on first use
+    // and kept (the device planner computes its own, fec_kernels.hip wave_rule)
+    bool lazy = false;
+    std::vector<uint8_t> G;
     void build(const std::vector<uint8_t>& G, int k, int n, int T);
     const uint8_t* entry(int w, uint32_t mask) const {
+        if (lazy) return lazy_entry(w, mask);
         return table.data() + w_base[w] + static_cast<int64_t>(mask) * entry_bytes;
     }
+
+private:
+    const uint8_t* lazy_entry(int w, uint32_t mask) const;
+    mutable std::mutex mu_;
+    mutable std::unordered_map<uint64_t, std::unique_ptr<uint8_t[]>> cache_;
 };
 
 // The rule table of (T,B,N) (G = make_generator(T,B,N)), built once per process and shared by

@@ -161,12 +161,13 @@ struct CopyArgs {
     int cwt_bytes;              // 16-aligned
 };
 
-constexpr int kPlanMaxN = 18;  // windows w <= n <= 17
+constexpr int kPlanMaxN = 31;  // windows w <= n <= 31 (n > 17: no rule table, rules computed in the wave)
 
 struct PlanArgs {
     const uint8_t* er;
     int64_t P, Pout;
     const uint8_t* rules;
+    const uint8_t* G;              // k x n generator (rules computed in the wave when wbase[w] < 0)
     int64_t wbase[kPlanMaxN + 1];  // byte offset of window w's rule table (-1: unused)
     const uint8_t* gf;             // exp[512] then log[256]
     int ES;                        // decode-rule entry stride (bytes, multiple of 4)
@@ -214,6 +215,8 @@ struct RecArgs {
     int L, k, n, S, CW;
     int64_t row_off;               // packet x goes to output row x - row_off (x < row_off: skipped)
 };
+template <int MAXN>
+__global__ void fec_recover_kernel_t(RecArgs a);
 
 struct StreamOutArgs {
     const uint8_t* ring;        // RR rows of CW bytes, row = seq % RR
@@ -263,7 +266,7 @@ __global__ void fec_plan_kernel(PlanArgs a);
 __global__ void fec_shape_kernel(ShapeArgs a);
 __global__ void fec_shape_fill_kernel(ShapeArgs a);
 __global__ void fec_copy_kernel(CopyArgs a);
-__global__ void fec_recover_kernel(RecArgs a);
+
 __global__ void fec_stream_out_kernel(StreamOutArgs a);
 __global__ void fec_fill_kernel(uint8_t* out, int64_t t0, int64_t count, int L, uint64_t seed);
 

@@ -273,11 +273,87 @@ struct BlockReplay {
     uint8_t* cwc;    // [p][q]
     uint8_t* datc;   // [i][q]
     uint8_t* fresh;  // [i][q]
+    uint8_t* rv;     // wave rule: matrix columns [w][16]
+    uint8_t* ra;     // wave rule: action columns [w][32]
+    uint8_t* rent;   // wave rule: the entry {sel[k], col[k][n]}
     int lane, k, n, T;
     uint32_t er;     // erased positions of the block (uniform)
 
     __device__ uint8_t mul(uint8_t f, uint8_t v) const {
         return v ? gexp[glog[f] + glog[v]] : 0;
+    }
+    __device__ static void wsync() {  // LDS written by other lanes of this wave is visible
+        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+    }
+
+    // The decode rule of (window w, erasure mask m) computed by the wave (codecs with n > 17 have
+    // no rule table): gf256_rref_matrix (basicOperations.cpp:43-122) on the k x w matrix G[:, :w]
+    // with erased columns zeroed, column by column -- pivot in row i+offset, a zero pivot swapped
+    // with the first later column non-zero in that row (ballot), a row without one bumps the
+    // offset, the pivot column normalised and eliminated from every other column (lane = column,
+    // element-parallel swaps and scaling) -- then codingOperations.cpp:204-230's unit-column test
+    // per erased data symbol (lane = symbol).  Same result as fec_host.cpp decode_rule.
+    __device__ void wave_rule(int w, uint32_t m) {
+        if (lane < w) {
+            const bool e = (m >> lane) & 1u;
+            for (int r = 0; r < k; ++r) rv[lane * 16 + r] = e ? 0 : a->G[r * n + lane];
+            for (int r = 0; r < w; ++r) ra[lane * 32 + r] = r == lane ? 1 : 0;
+        }
+        wsync();
+        int row = 0;
+        for (int i = 0; i < w && row < k;) {
+            if (rv[i * 16 + row] == 0) {
+                const bool cand = lane > i && lane < w && rv[lane * 16 + row] != 0;
+                const uint64_t bal = __builtin_amdgcn_ballot_w64(cand);
+                if (!bal) {
+                    ++row;
+                    continue;
+                }
+                const int j = static_cast<int>(__builtin_ctzll(bal));
+                if (lane < 16) {
+                    const uint8_t x = rv[i * 16 + lane], y = rv[j * 16 + lane];
+                    rv[i * 16 + lane] = y;
+                    rv[j * 16 + lane] = x;
+                }
+                if (lane < 32) {
+                    const uint8_t x = ra[i * 32 + lane], y = ra[j * 32 + lane];
+                    ra[i * 32 + lane] = y;
+                    ra[j * 32 + lane] = x;
+                }
+                wsync();
+            }
+            const uint8_t p = rv[i * 16 + row];
+            const uint8_t s = gexp[255 - glog[p]];  // gf_inv
+            wsync();
+            if (lane < k) rv[i * 16 + lane] = mul(s, rv[i * 16 + lane]);
+            if (lane < w) ra[i * 32 + lane] = mul(s, ra[i * 32 + lane]);
+            wsync();
+            if (lane < w && lane != i) {
+                const uint8_t f = rv[lane * 16 + row];
+                if (f) {
+                    for (int r = 0; r < k; ++r) rv[lane * 16 + r] ^= mul(f, rv[i * 16 + r]);
+                    for (int r = 0; r < w; ++r) ra[lane * 32 + r] ^= mul(f, ra[i * 32 + r]);
+                }
+            }
+            wsync();
+            ++i;
+            ++row;
+        }
+        if (lane < k) {
+            const int i = lane;
+            uint8_t sel = 0xff;
+            int j = i;
+            while (j < k && rv[j * 16 + i] != 1) ++j;
+            if (j < k) {
+                bool unit = true;
+                for (int r = i + 1; r < k; ++r) unit = unit && rv[j * 16 + r] == 0;
+                if (unit) sel = static_cast<uint8_t>(j);
+            }
+            rent[i] = sel;
+            for (int c = 0; c < w; ++c) rent[k + i * n + c] = sel == 0xff ? 0 : ra[j * 32 + c];
+        }
+        wsync();
     }
 
     // decodeBlock (codingOperations.cpp:149-232) on coefficient vectors.
@@ -287,13 +363,20 @@ struct BlockReplay {
         const uint32_t full = (1u << w) - 1u;
         const uint32_t m = er & full;
         if (m == full || !(m & ((1u << k) - 1u))) return;
-        // the whole rule entry {sel[k], col[k][n]} in one wave-wide load
-        const uint32_t* ent = reinterpret_cast<const uint32_t*>(
-            a->rules + a->wbase[w] + static_cast<int64_t>(m) * a->ES);
-        // entries reach 4*77 bytes (k = 15, n = 17): two dwords per lane
-        const uint32_t ev = (lane < (a->ES >> 2)) ? ent[lane] : 0u;
-        const uint32_t ev2 = (lane + 64 < (a->ES >> 2)) ? ent[lane + 64] : 0u;
+        uint32_t ev = 0, ev2 = 0;
+        const bool tab = a->wbase[w] >= 0;
+        if (tab) {
+            // the whole rule entry {sel[k], col[k][n]} in one wave-wide load
+            const uint32_t* ent = reinterpret_cast<const uint32_t*>(
+                a->rules + a->wbase[w] + static_cast<int64_t>(m) * a->ES);
+            // entries reach 4*77 bytes (k = 15, n = 17): two dwords per lane
+            ev = (lane < (a->ES >> 2)) ? ent[lane] : 0u;
+            ev2 = (lane + 64 < (a->ES >> 2)) ? ent[lane + 64] : 0u;
+        } else {
+            wave_rule(w, m);
+        }
         auto rd = [&](int idx) -> uint32_t {
+            if (!tab) return rent[idx];
             const int d = idx >> 2;
             const uint32_t wv = d < 64 ? __builtin_amdgcn_readlane(ev, d) : __builtin_amdgcn_readlane(ev2, d - 64);
             return (wv >> ((idx & 3) * 8)) & 0xffu;
@@ -382,6 +465,9 @@ __global__ __launch_bounds__(64) void fec_plan_kernel(PlanArgs a) {
     br.cwc = smem + 768;
     br.datc = br.cwc + n * n;
     br.fresh = br.datc + k * n;
+    br.rv = br.fresh + k * n;
+    br.ra = br.rv + 32 * 16;
+    br.rent = br.ra + 32 * 32;
     br.lane = lane;
     br.k = k;
     br.n = n;
@@ -455,10 +541,11 @@ __global__ __launch_bounds__(64) void fec_plan_kernel(PlanArgs a) {
 // XOR_q coef[x][i][q] * cw[x-i+q][s*n+q] over the received symbols q of its diagonal.
 // ------------------------------------------------------------------------------------------
 constexpr int kRecMaxK = 16;  // = kMaxK (fec_host.h)
-constexpr int kRecMaxN = 17;  // = kMaxRuleN: codecs with n > 17 are refused
 constexpr int kRecRounds = 5;  // 64-byte rounds per pass of fec_recover_kernel (L = 300: one pass)
 
-__global__ __launch_bounds__(256) void fec_recover_kernel(RecArgs a) {
+// kRecMaxN = 17 (codecs with a rule table, the common case) or 32 (n up to 31)
+template <int kRecMaxN>
+__global__ __launch_bounds__(256) void fec_recover_kernel_t(RecArgs a) {
     // One wave per recovered packet (fec_compact_kernel's list), no workgroup barrier after the
     // table load: lane h computes bytes h, h+64, ... of [len_hi, len_lo, payload]; its n sources
     // are byte loads straight from the diagonal's rows (a ~(k+n)*CW-byte window, L2-resident), all
@@ -543,6 +630,9 @@ __global__ __launch_bounds__(256) void fec_recover_kernel(RecArgs a) {
         __builtin_amdgcn_wave_barrier();  // lc is rewritten by the next packet
     }
 }
+
+template __global__ void fec_recover_kernel_t<17>(RecArgs);
+template __global__ void fec_recover_kernel_t<32>(RecArgs);
 
 // ------------------------------------------------------------------------------------------
 // Decode, step 3: every received packet's systematic bytes (fast path Decoder.cpp:77-108; the

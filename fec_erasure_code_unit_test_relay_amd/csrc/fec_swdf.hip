@@ -182,6 +182,7 @@ int launch_diag_decode(const fec::CodecView& v, const uint8_t* in, int64_t in_st
     a.k = v.k;
     a.n = v.n;
     a.S = v.S;
+    if (v.wbase_n < 0) return FEC_ERR_ARG;  // n > 17: no window-n rule table
     a.rules = v.rules + v.wbase_n;
     a.ES = v.ES;
     a.gf = v.gf;

@@ -37,7 +37,7 @@ def test_fill_payload_matches_oracle_generator():
 
 ENC_CONFIGS = [(10, 3, 3), (10, 5, 2), (10, 1, 1), (10, 0, 0), (10, 2, 2), (10, 5, 5),
                (10, 7, 7), (10, 9, 9), (10, 10, 10), (10, 8, 4), (10, 5, 4), (10, 9, 8), (10, 4, 1),
-               (4, 6, 2), (12, 4, 2)]
+               (4, 6, 2), (12, 4, 2), (10, 9, 1), (10, 10, 1)]
 
 
 @pytest.mark.parametrize("path", ["generic", "fast", "auto", "wave", "tile"])
@@ -195,7 +195,10 @@ DEC_CASES = [((10, 5, 2), "bin_erasure", 0, 8000), ((10, 3, 3), "bin_erasure", 0
              ((10, 0, 0), "erasure70", 0, 5000), ((10, 8, 4), "erasure60", 0, 5000),
              ((12, 4, 2), "erasure100", 1000, 3000), ((4, 6, 2), "erasure100", 0, 3000),
              ((15, 2, 1), "erasure100", 0, 2000), ((16, 1, 1), "erasure90", 500, 2000),
-             ((10, 4, 4), "bin_erasure", 2000, 6000), ((10, 5, 5), "erasure80", 0, 4000)]
+             ((10, 4, 4), "bin_erasure", 2000, 6000), ((10, 5, 5), "erasure80", 0, 4000),
+             # n = 18..21: no rule table, the planner's wave computes gf256_rref_matrix itself
+             ((10, 9, 1), "erasure100", 0, 6000), ((10, 10, 1), "erasure100", 0, 6000),
+             ((10, 8, 1), "erasure90", 2000, 5000), ((10, 9, 2), "erasure100", 7000, 5000)]
 
 
 @pytest.mark.parametrize("path,dedup", [("generic", False), ("wave", True), ("auto", False), ("auto", True)])

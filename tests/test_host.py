@@ -114,3 +114,17 @@ def test_planner_matches_oracle_random_bursts(tbn):
     r = oracle.run_stream(300, T, B, N, P, pat, loss_only=True)
     fate = host_lost(T, B, N, pat, P)
     assert ((r["out_len"] == 0) == (fate == 3)).all()
+
+
+@pytest.mark.parametrize("tbn", [(10, 9, 1), (10, 10, 1), (10, 8, 1), (10, 9, 2)])
+def test_planner_without_rule_table_matches_oracle(tbn):
+    """n = 18..21 (T = 10 allows it): no (window, mask) rule table, every rule computed on first
+    use -- the planner still reproduces the oracle's lost list (restated gf256_rref_matrix per
+    symbol, oracle/fec_oracle.c) packet for packet on the shipped erasure100 pattern."""
+    T, B, N = tbn
+    P = 30000
+    pat = load_pattern("erasure100")[:P + T].astype(np.uint8)
+    fate = host_lost(T, B, N, pat, P)
+    ref = oracle.run_stream(300, T, B, N, P, pat, loss_only=True)
+    assert (fate == 3).sum() > 0
+    assert np.flatnonzero(fate == 3).tolist() == np.flatnonzero(ref["out_len"] == 0).tolist()
