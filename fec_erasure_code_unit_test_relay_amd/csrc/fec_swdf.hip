@@ -24,7 +24,7 @@
 // the codec's decode rule for (w = n, erasure mask) (fec_host.cpp DecodeRules).  So the byte work
 // is two data-parallel kernels: a diagonal decode (one thread per (packet, block)) used by both
 // the relay and the destination, and the relay's re-encode.  Undefined behaviour of the reference
-// defined away: n flags (not n-1 plus garbage) reach decodeBlock, the block count
+// defined away ("Relay"): n flags (not n-1 plus garbage) reach decodeBlock, the block count
 // is S = ceil((L+2)/k) (not max_payload/k + 1), slots hold zero-padded packets, k2 == k.
 #include <hip/hip_runtime.h>
 
