@@ -70,6 +70,8 @@ struct fec_codec {
     int tile_lds = 0, tile_lds_len = 0; // its dynamic LDS per workgroup (without / with lengths)
     int tile_per_cu = 0;                // its resident workgroups per CU
     int tile_off[9] = {};               // off_in, in_bytes, off_pw, off_q, off_out, off_len, ngl, nso, off_scratch
+    const void* copy_tile = nullptr;  // persistent decode copy (fec_copy_tile.hip)
+    int copyt_tp = 0, copyt_lds = 0, copyt_per_cu = 0;
     const void* copy_fast = nullptr;  // specialised decode copy kernel (LDS tiles)
     int copyf_tp = 0;
     const void* copy_wave = nullptr;  // barrier-free decode copy (fec_copy_wave.hip)
@@ -331,6 +333,21 @@ int codec_init(fec_codec* c, int max_payload, int T, int B, int N) {
             HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, c->tile_kernel, 256, c->tile_lds));
             c->tile_per_cu = per_cu;
             if (per_cu <= 0) c->tile_kernel = nullptr;
+        }
+    }
+    if ((g.L & 3) == 0 && g.T + 32 <= 64) {
+        // tile of TP = 32 packets (TP*CW and TP*L multiples of 16 for any CW, L % 4 == 0)
+        const int tp = 32;
+        if (tp * g.CW <= 256 * 16 * 4) c->copy_tile = fec::fec_copy_tile_kernel_for(g.k, g.n - g.k);
+        if (c->copy_tile) {
+            c->copyt_tp = tp;
+            c->copyt_lds = round16(tp * g.CW + 64) + round16(tp * g.L);
+            int dev = 0, cus = 0, per_cu = 0;
+            HIP_TRY(hipGetDevice(&dev));
+            HIP_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+            HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, c->copy_tile, 256, c->copyt_lds));
+            c->copyt_per_cu = per_cu;
+            if (per_cu <= 0) c->copy_tile = nullptr;
         }
     }
     if ((g.L & 3) == 0) c->copy_fast = fec::fec_copy_fast_kernel_for(g.k, g.n - g.k);
@@ -816,6 +833,38 @@ int launch_copy(fec_codec* c, const uint8_t* d_cw, const uint8_t* d_er, int64_t 
         HIP_TRY(hipLaunchKernel(c->copy_wave, dim3(static_cast<unsigned>(blocks)), dim3(256), args, 0, s));
         return c->end(stop, s);
     }
+    const bool tile_ok = c->copy_tile && (reinterpret_cast<uintptr_t>(d_out) & 15) == 0 &&
+                         (reinterpret_cast<uintptr_t>(d_cw) & 15) == 0;
+    if (c->copy_path == 4 && !tile_ok) return FEC_ERR_ARG;
+    // Copy path 4 only: the persistent copy holds every CU's slots until it ends, so the planner
+    // chain on the side stream starts only after it (scan 81 vs 23 us) and the step gets slower
+    // (0.373 - 0.393 vs 0.353 ms per step, tools/step_ab.py, same process), although the copy
+    // alone is faster (166 vs 174 us in the step)
+    if (tile_ok && c->copy_path == 4) {
+        fec::CopyTileArgs ta;
+        ta.cw = d_cw;
+        ta.er = d_er;
+        ta.out = d_out;
+        ta.out_len = d_outlen;
+        ta.Pout = Pout;
+        ta.L = g.L;
+        ta.CW = g.CW;
+        ta.NS4 = c->ns4();
+        ta.T = g.T;
+        ta.TP = c->copyt_tp;
+        ta.raw_bytes = round16(ta.TP * g.CW + 64);
+        ta.ntiles = (Pout + ta.TP - 1) / ta.TP;
+        int wpc = c->copyt_per_cu;
+        if (const char* v = std::getenv("FEC_COPY_TILE_WPC")) wpc = std::max(1, std::min(wpc, std::atoi(v)));
+        const int64_t slots = static_cast<int64_t>(std::max(1, c->wave_cus)) * std::max(1, wpc);
+        ta.tiles_per_wg = (ta.ntiles + slots - 1) / slots;
+        const int64_t blocks = (ta.ntiles + ta.tiles_per_wg - 1) / ta.tiles_per_wg;
+        hipEvent_t stop;
+        if (int st = c->begin(FEC_KERNEL_DEC_COPY, s, &stop)) return st;
+        void* args[] = {&ta};
+        HIP_TRY(hipLaunchKernel(c->copy_tile, dim3(static_cast<unsigned>(blocks)), dim3(256), args, c->copyt_lds, s));
+        return c->end(stop, s);
+    }
     const bool fast_ok = c->copy_fast && (reinterpret_cast<uintptr_t>(d_out) & 3) == 0;
     if (c->copy_path == 2 && !fast_ok) return FEC_ERR_ARG;
     if (fast_ok && c->copy_path != 1) {
@@ -1219,6 +1268,8 @@ int fec_codec_info(const fec_codec* c, char* buf, size_t size) {
     char cpy[64];
     if (c->copy_wave && c->copy_path == 3)
         std::snprintf(cpy, sizeof(cpy), "fec_copy_wave_kernel<%d, %d>", c->g.k, np);
+    else if (c->copy_tile && c->copy_path == 4)
+        std::snprintf(cpy, sizeof(cpy), "fec_copy_tile_kernel<%d, %d>", c->g.k, np);
     else if (c->copy_fast && c->copy_path != 1)
         std::snprintf(cpy, sizeof(cpy), "fec_copy_fast_kernel<%d, %d>", c->g.k, np);
     else
@@ -1266,7 +1317,8 @@ int fec_codec_set_plan_path(fec_codec* c, int path) {
 }
 
 int fec_codec_set_copy_path(fec_codec* c, int path) {
-    if (!c || path < 0 || path > 3) return FEC_ERR_ARG;
+    if (!c || path < 0 || path > 4) return FEC_ERR_ARG;
+    if (path == 4 && !c->copy_tile) return FEC_ERR_ARG;
     if (path == 2 && !c->copy_fast) return FEC_ERR_ARG;
     if (path == 3 && !c->copy_wave) return FEC_ERR_ARG;
     c->copy_path = path;

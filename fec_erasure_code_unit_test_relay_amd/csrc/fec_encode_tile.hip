@@ -350,7 +350,11 @@ __device__ __forceinline__ void tile_walk(const EncTileArgs& a, uint8_t* smem) {
         // ---- B: this wave's products over every item of the tile, XORed into the parity rows
         if constexpr (NPW > 0) {
             if (active && !(a.dbg & 1)) {
+#ifdef FEC_TILE_BUNROLL
+#pragma unroll
+#else
 #pragma unroll 1
+#endif
                 for (int sl = 0; sl < 4; ++sl) {
                     const int it_item = (sl * PPW + pl) * NS4 + g;
                     const int pp = sl * PPW + pl;

@@ -129,6 +129,19 @@ struct CopyFastArgs {
     int skip_erased;            // 1: leave erased packets' rows and lengths to fec_recover_kernel
 };
 
+// Received-packet decode over contiguous per-workgroup tile runs (fec_copy_tile.hip).
+struct CopyTileArgs {
+    const uint8_t* cw;          // 16-byte aligned, P rows of CW bytes
+    const uint8_t* er;          // P flags
+    uint8_t* out;               // 16-byte aligned, Pout rows of L bytes (L % 4 == 0)
+    int32_t* out_len;
+    int64_t Pout;
+    int L, CW, NS4, T, TP;      // TP * CW <= 16 KB, TP * L % 16 == 0, TP * CW % 16 == 0, TP + T <= 64
+    int raw_bytes;              // LDS codeword tile (16-aligned)
+    int64_t tiles_per_wg, ntiles;
+};
+const void* fec_copy_tile_kernel_for(int k, int np);
+
 // Barrier-free received-packet decode (fec_copy_wave.hip): lane = (packet, group of 4 sub-streams),
 // SPW = 64 / NS4 packets per wave step; erased packets are not touched.  Needs T < 4*NS4.
 struct CopyWaveArgs {
