@@ -65,7 +65,9 @@ int fec_codec_set_encode_path(fec_codec *codec, int path);
  * specialised kernel when one is compiled for (k, n-k) and max_payload % 4 == 0, else the generic
  * one), 1 generic, 2 LDS-tile specialised, 3 barrier-free wave kernel (it writes received packets'
  * rows only, so fec_decode_batch then runs the recovery of erased packets concurrently with it;
- * measured slower in the step, kept for A/B). */
+ * measured slower in the step, kept for A/B), 4 persistent tile runs with register-staged prefetch
+ * (16-byte aligned buffers; faster alone, slower in the step: it holds the CUs the side-stream
+ * planner chain needs). */
 int fec_codec_set_copy_path(fec_codec *codec, int path);
 /* The same switch for the decoder's planner (per-episode block replay). */
 int fec_codec_set_plan_path(fec_codec *codec, int path);
