@@ -24,18 +24,17 @@ void ParameterEstimator::estimate(int64_t seq, int msg_T) {
     }
     const int64_t current_win_end = seq;
     if (current_win_end - previous_win_end < 1) return;  // out of order (:84-86)
+    const uint32_t wmask = (T + 1 >= 32) ? 0xffffffffu : ((1u << (T + 1)) - 1u);
     for (int64_t s = previous_win_end + 1; s <= current_win_end; ++s) {
-        for (int i = T; i >= 1; --i) erasure[i] = erasure[i - 1];
-        erasure[0] = s < current_win_end;  // the packets in between were lost
-        int sum = 0;
-        for (int i = 0; i <= T; ++i) sum += erasure[i] ? 1 : 0;
+        // shift the window by one (erasure[i] = erasure[i-1]) and insert the new flag at 0
+        erasure = ((erasure << 1) | (s < current_win_end ? 1u : 0u)) & wmask;  // in between: lost
+        const int sum = __builtin_popcount(erasure);
         if (sum == T + 1 || sum == 0) continue;  // (:104-105)
         if (B == 0) B = 1;
         if (N == 0) N = 1;
         if (sum > N_max) N_max = sum;
-        int first = 0, last = T;
-        while (first <= T && !erasure[first]) ++first;
-        while (last >= 0 && !erasure[last]) --last;
+        const int first = __builtin_ctz(erasure);        // first erased index
+        const int last = 31 - __builtin_clz(erasure);    // last erased index
         const int span = last - first + 1;
         if (span == T + 1) {  // (:131-136)
             if (sum > N) {
@@ -176,6 +175,8 @@ void VrPlan::run(int max_payload, int T, int B, int N, bool mds, const uint8_t* 
         dec[dold].role_switch = first;
     };
 
+    frames.reserve(static_cast<size_t>(P + T + 1));
+    erased.reserve(static_cast<size_t>(P + T + 1));
     for (int64_t seq = 0;; ++seq) {
         // ---- Application_Layer_Sender::generate_message_and_encode ----
         if (adaptive && udp[0] != 0) {

@@ -30,7 +30,7 @@ namespace fec {
 struct ParameterEstimator {
     bool adaptive_mode_MDS = false;
     int T = 0, B = 0, N = 0, N_max = 0, B_current = 0, N_current = 0;
-    bool erasure[12] = {};
+    uint32_t erasure = 0;  // bit i = the reference's erasure[i] (window of T+1 flags, newest at 0)
     int64_t previous_win_end = -2;
     ParameterEstimator(int T_value, bool mds) : adaptive_mode_MDS(mds), T(T_value) {}
     void estimate(int64_t seq, int msg_T);
