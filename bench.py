@@ -265,9 +265,18 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # FEC_BENCH_BACKEND=gloo rehearses the multi-rank bench on a box with fewer GPUs than ranks
+    # (ranks share devices round-robin, collectives on host tensors); the driver's runs use RCCL.
+    backend = os.environ.get("FEC_BENCH_BACKEND", "nccl")
+    if backend != "nccl":
+        local = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
+    comm_dev = "cuda" if backend == "nccl" else "cpu"
     if world > 1:
-        dist.init_process_group(backend="nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group(backend="nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend=backend)
 
     from fec_erasure_code_unit_test_relay_amd import Codec, fill_payload
 
@@ -326,7 +335,7 @@ def main():
     barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
-    elapsed = max_over_ranks(elapsed, dist, "cuda")
+    elapsed = max_over_ranks(elapsed, dist, comm_dev)
 
     # correctness of the timed work (outside the timed region): round trip + planner agreement
     eps, rec, lost = codec.counters()
@@ -336,7 +345,7 @@ def main():
         int((ol[ok_rows] != L).sum()) == 0 and int(lost_mask.sum()) == lost
     # trivial counter reduction over RCCL
     rec_all, lost_all, erased_all, verified_all = reduce_counters(
-        [rec, lost, int(pat[:P].sum()), int(verified)], dist, "cuda")
+        [rec, lost, int(pat[:P].sum()), int(verified)], dist, comm_dev)
 
     # per-kernel durations: HIP events on the launch stream, separate pass
     # (warm-up launches first, so the averages are the steady state the rocprofv3 trace sees)

@@ -376,110 +376,105 @@ void VrPlan::run(int max_payload, int T, int B, int N, bool mds, const uint8_t* 
 struct fec_vr_plan {
     fec::VrPlan plan;
     int cw_max = 0;
-    // ---- device execution state (created on first use) ----
-    std::map<int, fec_codec*> codecs;  // key T*1024 + B*32 + N
-    struct Tuple {                     // encode work of one (T,B,N)
-        int T, B, N, CW;
-        int64_t nrows = 0;             // dense rows: per instance n-1 zero rows + its calls
-        int64_t* d_rows = nullptr;     // dense row -> payload row (-1 = zero packet)
-        int64_t* d_dst = nullptr;      // dense row -> (frame row << 1) | old (-1 = discard)
-    };
-    std::vector<Tuple> tuples;
-    uint8_t* d_pay = nullptr;          // dense payload rows (max over tuples)
-    int32_t* d_len = nullptr;
-    uint8_t* d_cw = nullptr;           // dense codewords
-    int32_t* d_cwlen = nullptr;
-    // decode tables
-    int32_t* d_pk_dec = nullptr;
-    int32_t* d_inst = nullptr;
-    int64_t* d_inst_switch = nullptr;
-    uint8_t* d_fate = nullptr;
-    uint8_t* d_slow = nullptr;
-    int64_t* d_rec_x = nullptr;
-    int32_t* d_rec_dec = nullptr;
-    uint8_t* d_rec_coef = nullptr;
-    uint8_t* d_gf = nullptr;
-    int32_t* d_hdr = nullptr;          // [sent][4]: frame header T, B, N, counter
+    // ---- device tables (uploaded on first use, one allocation each for encode / decode) ----
+    void* d_enc_arena = nullptr;
+    void* d_dec_arena = nullptr;
+    const int32_t* d_enc_inst = nullptr;   // [nenc][4]: k, n, CW, glog offset
+    const int64_t* d_enc_span = nullptr;   // [nenc][2]: first, role_switch
+    const int64_t* d_enc_cum = nullptr;    // [nenc+1]
+    const uint8_t* d_glog = nullptr;
+    const int32_t* d_pk_dec = nullptr;
+    const int32_t* d_inst = nullptr;
+    const int64_t* d_inst_switch = nullptr;
+    const uint8_t* d_fate = nullptr;
+    const uint8_t* d_slow = nullptr;
+    const int64_t* d_rec_x = nullptr;
+    const int32_t* d_rec_dec = nullptr;
+    const uint8_t* d_rec_coef = nullptr;
+    const uint8_t* d_gf = nullptr;
+    const int32_t* d_hdr = nullptr;    // [sent][4]: frame header T, B, N, counter
+    void* d_hdr_arena = nullptr;
+    int64_t enc_total = 0;             // codewords of all encoder instances
+    int enc_slot = 0, enc_ring = 0;    // fec_vr_encode_kernel's LDS ring geometry
     bool enc_ready = false, dec_ready = false;
 
     ~fec_vr_plan() {
-        for (auto& kv : codecs) fec_codec_destroy(kv.second);
-        for (auto& t : tuples) {
-            if (t.d_rows) (void)hipFree(t.d_rows);
-            if (t.d_dst) (void)hipFree(t.d_dst);
-        }
-        for (void* p : {static_cast<void*>(d_pay), static_cast<void*>(d_len), static_cast<void*>(d_cw),
-                        static_cast<void*>(d_cwlen), static_cast<void*>(d_pk_dec), static_cast<void*>(d_inst),
-                        static_cast<void*>(d_inst_switch), static_cast<void*>(d_fate), static_cast<void*>(d_slow),
-                        static_cast<void*>(d_rec_x), static_cast<void*>(d_rec_dec), static_cast<void*>(d_rec_coef),
-                        static_cast<void*>(d_gf), static_cast<void*>(d_hdr)})
+        for (void* p : {d_enc_arena, d_dec_arena, d_hdr_arena})
             if (p) (void)hipFree(p);
-    }
-    int codec(int T, int B, int N, fec_codec** out) {
-        const int key = T * 1024 + B * 32 + N;
-        auto it = codecs.find(key);
-        if (it == codecs.end()) {
-            fec_codec* c = nullptr;
-            if (int st = fec_codec_create(plan.L, T, B, N, &c)) return st;
-            it = codecs.emplace(key, c).first;
-        }
-        *out = it->second;
-        return FEC_OK;
     }
 };
 
 namespace {
-template <typename T>
-int upload(T** d, const std::vector<T>& h) {
-    const size_t bytes = std::max<size_t>(sizeof(T), h.size() * sizeof(T));
-    if (hipMalloc(reinterpret_cast<void**>(d), bytes) != hipSuccess) return FEC_ERR_NOMEM;
-    if (!h.empty() && hipMemcpy(*d, h.data(), h.size() * sizeof(T), hipMemcpyHostToDevice) != hipSuccess)
-        return FEC_ERR_HIP;
-    return FEC_OK;
+// Host tables packed into one buffer (256-byte aligned pieces) and uploaded with one allocation
+// and one copy.
+struct Arena {
+    std::vector<uint8_t> host;
+    std::vector<std::pair<const void**, size_t>> fix;
+    template <typename T>
+    void add(const T** d, const T* h, size_t count) {
+        const size_t off = (host.size() + 255) & ~size_t(255);
+        host.resize(off + std::max<size_t>(1, count) * sizeof(T));
+        if (count) std::memcpy(host.data() + off, h, count * sizeof(T));
+        fix.emplace_back(reinterpret_cast<const void**>(d), off);
+    }
+    template <typename T>
+    void add(const T** d, const std::vector<T>& h) { add(d, h.data(), h.size()); }
+    int commit(void** base) {
+        if (hipMalloc(base, std::max<size_t>(16, host.size())) != hipSuccess) return FEC_ERR_NOMEM;
+        if (hipMemcpy(*base, host.data(), host.size(), hipMemcpyHostToDevice) != hipSuccess) return FEC_ERR_HIP;
+        for (auto& f : fix) *f.first = static_cast<const uint8_t*>(*base) + f.second;
+        return FEC_OK;
+    }
+};
+
+std::vector<uint8_t> gf_tables() {
+    const fec::Field& F = fec::field();
+    std::vector<uint8_t> gf(F.exp, F.exp + 512);
+    gf.insert(gf.end(), F.log, F.log + 256);
+    return gf;
 }
 
-// Encode tables: instances grouped by (T,B,N); each instance contributes n-1 all-zero rows (its
-// encoder starts with X = 0 history) followed by its calls [first, end), scattered back to the
-// current array for [first, role_switch) and to the old array after.
+// Encode tables: per encoder instance its geometry, first call, role switch and the running
+// count of codewords; per (T,B,N) tuple the logs of G's parity columns.
 int prepare_encode(fec_vr_plan* v) {
     if (v->enc_ready) return FEC_OK;
     const auto& p = v->plan;
-    std::map<int, std::pair<std::vector<int64_t>, std::vector<int64_t>>> rows;
-    std::map<int, fec::VrInstance> proto;
+    const fec::Field& F = fec::field();
+    std::map<int, int> goff;  // tuple -> offset in glog
+    std::vector<uint8_t> glog;
+    std::vector<int32_t> inst;
+    std::vector<int64_t> span, cum{0};
+    int slot = 4, nmax = 1;
     for (const auto& e : p.enc) {
+        const fec::Geometry g = fec::Geometry::make(p.L, e.T, e.B, e.N);
+        slot = std::max(slot, 4 + 4 * ((g.S * g.k - 2 + 3) / 4));
+        nmax = std::max(nmax, g.n);
         const int key = e.T * 1024 + e.B * 32 + e.N;
-        proto[key] = e;
-        auto& rr = rows[key];
-        const int n = (e.T - e.N + 1) + e.B;
-        for (int z = 0; z < n - 1; ++z) {
-            rr.first.push_back(-1);
-            rr.second.push_back(-1);
+        auto it = goff.find(key);
+        if (it == goff.end()) {
+            const std::vector<uint8_t> G = fec::make_generator(e.T, e.B, e.N);
+            it = goff.emplace(key, static_cast<int>(glog.size())).first;
+            for (int i = 0; i < g.k; ++i)
+                for (int j = g.k; j < g.n; ++j) {
+                    const uint8_t c = G[static_cast<size_t>(i) * g.n + j];
+                    glog.push_back(c ? F.log[c] : 255);
+                }
         }
-        for (int64_t sq = e.first; sq < e.end; ++sq) {
-            rr.first.push_back(sq);
-            rr.second.push_back((sq << 1) | (sq >= e.role_switch ? 1 : 0));
-        }
+        inst.insert(inst.end(), {g.k, g.n, g.CW, it->second});
+        span.insert(span.end(), {e.first, e.role_switch});
+        cum.push_back(cum.back() + (e.end - e.first));
     }
-    int64_t max_rows = 0, max_cw = 0;
-    for (auto& kv : rows) {
-        const auto& e = proto[kv.first];
-        fec_vr_plan::Tuple t;
-        t.T = e.T;
-        t.B = e.B;
-        t.N = e.N;
-        t.CW = fec::Geometry::make(p.L, e.T, e.B, e.N).CW;
-        t.nrows = static_cast<int64_t>(kv.second.first.size());
-        if (int st = upload(&t.d_rows, kv.second.first)) return st;
-        if (int st = upload(&t.d_dst, kv.second.second)) return st;
-        v->tuples.push_back(t);
-        max_rows = std::max(max_rows, t.nrows);
-        max_cw = std::max<int64_t>(max_cw, t.nrows * t.CW);
-    }
-    if (hipMalloc(reinterpret_cast<void**>(&v->d_pay), std::max<int64_t>(16, max_rows * p.L)) != hipSuccess ||
-        hipMalloc(reinterpret_cast<void**>(&v->d_len), std::max<int64_t>(16, max_rows * 4)) != hipSuccess ||
-        hipMalloc(reinterpret_cast<void**>(&v->d_cw), std::max<int64_t>(16, max_cw)) != hipSuccess ||
-        hipMalloc(reinterpret_cast<void**>(&v->d_cwlen), std::max<int64_t>(16, max_rows * 4)) != hipSuccess)
-        return FEC_ERR_NOMEM;
+    Arena ar;
+    ar.add(&v->d_enc_inst, inst);
+    ar.add(&v->d_enc_span, span);
+    ar.add(&v->d_enc_cum, cum);
+    ar.add(&v->d_glog, glog);
+    const std::vector<uint8_t> gf = gf_tables();
+    ar.add(&v->d_gf, gf);
+    if (int st = ar.commit(&v->d_enc_arena)) return st;
+    v->enc_total = cum.back();
+    v->enc_slot = slot;
+    v->enc_ring = slot * nmax;
     v->enc_ready = true;
     return FEC_OK;
 }
@@ -494,18 +489,20 @@ int prepare_decode(fec_vr_plan* v) {
         inst.insert(inst.end(), {g.k, g.n, g.CW, 0});
         sw.push_back(d.role_switch);
     }
-    if (int st = upload(&v->d_pk_dec, p.fate_dec)) return st;
-    if (int st = upload(&v->d_inst, inst)) return st;
-    if (int st = upload(&v->d_inst_switch, sw)) return st;
-    if (int st = upload(&v->d_fate, p.fate)) return st;
-    if (int st = upload(&v->d_slow, p.slow)) return st;
-    if (int st = upload(&v->d_rec_x, p.rec_x)) return st;
-    if (int st = upload(&v->d_rec_dec, p.rec_dec)) return st;
-    if (int st = upload(&v->d_rec_coef, p.rec_coef)) return st;
-    const fec::Field& F = fec::field();
-    std::vector<uint8_t> gf(F.exp, F.exp + 512);
-    gf.insert(gf.end(), F.log, F.log + 256);
-    if (int st = upload(&v->d_gf, gf)) return st;
+    Arena ar;
+    ar.add(&v->d_pk_dec, p.fate_dec);
+    ar.add(&v->d_inst, inst);
+    ar.add(&v->d_inst_switch, sw);
+    ar.add(&v->d_fate, p.fate);
+    ar.add(&v->d_slow, p.slow);
+    ar.add(&v->d_rec_x, p.rec_x);
+    ar.add(&v->d_rec_dec, p.rec_dec);
+    ar.add(&v->d_rec_coef, p.rec_coef);
+    const uint8_t* gf_dec = nullptr;
+    const std::vector<uint8_t> gf = gf_tables();
+    ar.add(&gf_dec, gf);
+    if (int st = ar.commit(&v->d_dec_arena)) return st;
+    if (!v->d_gf) v->d_gf = gf_dec;
     v->dec_ready = true;
     return FEC_OK;
 }
@@ -601,25 +598,16 @@ int fec_vr_plan_packets(const fec_vr_plan* v, int32_t* frames, uint8_t* erased, 
 
 // Encode every packet the sender produced: row s of d_cw_cur (stride cw_max) = the codeword of
 // frame s's current encoder, row s of d_cw_old = its old encoder's (double coding; rows of frames
-// without one are left alone), trimmed sizes in d_len_*.  Three launches per (T,B,N) tuple:
-// gather the tuple's instances into dense rows (n-1 zero rows in front of each: X_{t'<first} = 0),
-// the tuple's encode kernel over all of them at once, scatter back into the frames' rows.
+// without one are left alone), trimmed sizes in d_len_*.  One launch for every instance of every
+// (T,B,N) tuple (fec_vr_encode_kernel), straight from the payload rows.
 int fec_vr_encode_batch(fec_vr_plan* v, const uint8_t* d_payload, const int32_t* d_payload_len, uint8_t* d_cw_cur,
                         int32_t* d_len_cur, uint8_t* d_cw_old, int32_t* d_len_old, void* hip_stream) {
     if (!v || !d_payload || !d_cw_cur || !d_len_cur || !d_cw_old || !d_len_old) return FEC_ERR_ARG;
-    if ((v->plan.L & 3) || (reinterpret_cast<uintptr_t>(d_payload) & 3)) return FEC_ERR_ARG;
     if (int st = vr_guarded([&] { return prepare_encode(v); })) return st;
-    for (const auto& t : v->tuples) {
-        fec_codec* c = nullptr;
-        if (int st = v->codec(t.T, t.B, t.N, &c)) return st;
-        fec::VrGatherArgs g{d_payload, d_payload_len, t.d_rows, t.nrows, v->plan.L, v->d_pay, v->d_len};
-        if (int st = fec::vr_launch_gather(g, hip_stream)) return st;
-        if (int st = fec_encode_batch(c, v->d_pay, v->d_len, 0, t.nrows, v->d_cw, v->d_cwlen, hip_stream)) return st;
-        fec::VrScatterArgs sc{v->d_cw, v->d_cwlen, t.d_dst, t.nrows, t.CW, v->cw_max, d_cw_cur, d_cw_old,
-                              d_len_cur, d_len_old};
-        if (int st = fec::vr_launch_scatter(sc, hip_stream)) return st;
-    }
-    return FEC_OK;
+    fec::VrEncodeArgs a{d_payload, d_payload_len, v->plan.L, v->d_enc_inst, v->d_enc_span, v->d_enc_cum,
+                        static_cast<int>(v->plan.enc.size()), v->enc_total, v->enc_slot, v->enc_ring, v->d_glog, v->d_gf, v->cw_max, d_cw_cur, d_cw_old,
+                        d_len_cur, d_len_old};
+    return fec::vr_launch_encode(a, hip_stream);
 }
 
 // The P2P wire packets of every frame: row s of d_packets (stride >= 10 + 2*cw_max bytes) =
@@ -639,7 +627,9 @@ int fec_vr_frames_batch(fec_vr_plan* v, const uint8_t* d_cw_cur, const int32_t* 
             h[4 * s + 2] = p.frames[s].N;
             h[4 * s + 3] = p.frames[s].counter;
         }
-        if (int st = upload(&v->d_hdr, h)) return st;
+        Arena ar;
+        ar.add(&v->d_hdr, h);
+        if (int st = ar.commit(&v->d_hdr_arena)) return st;
     }
     fec::VrFrameArgs a{d_cw_cur, d_len_cur, d_cw_old, d_len_old, v->cw_max, v->d_hdr, p.sent, d_packets, stride,
                        d_packet_len};

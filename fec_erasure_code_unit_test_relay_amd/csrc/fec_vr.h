@@ -81,22 +81,23 @@ private:
 };
 
 // Device side of the schedule (fec_vr_kernels.hip).  All launches go to `s`.
-struct VrGatherArgs {   // dense encode input: row r = payload row rows[r] (-1: all-zero packet)
-    const uint8_t* payload;
-    const int32_t* len;   // may be null (all L)
-    const int64_t* rows;
-    int64_t nrows;
+// Every encoder instance of the schedule in one launch (any mix of (T,B,N)): codeword c of the
+// list = instance e's call for seq = first_e + (c - cum[e]), written to cur[seq] before e's
+// role switch and to old[seq] after (Variable_Rate_FEC_Encoder.cpp:140-217).
+struct VrEncodeArgs {
+    const uint8_t* payload;   // [sent][L]
+    const int32_t* len;       // may be null (all L)
     int L;
-    uint8_t* out;         // nrows x L
-    int32_t* out_len;     // nrows
-};
-struct VrScatterArgs {  // dense codewords -> the frames' arrays: dst[r] = (row << 1) | old, -1 skip
-    const uint8_t* cw;
-    const int32_t* cw_len;
-    const int64_t* dst;
-    int64_t nrows;
-    int CW;
-    int64_t W;
+    const int32_t* inst;      // [nenc][4]: k, n, CW, offset of the tuple's parity-coefficient logs
+    const int64_t* span;      // [nenc][2]: first, role_switch
+    const int64_t* cum;       // [nenc+1]: codewords of instances < e
+    int nenc;
+    int64_t cum_host_total;   // cum[nenc] (host copy: sizes the grid)
+    int slot_bytes;           // LDS ring slot: 4 + payload-region words of the widest row, x4
+    int ring_bytes;           // per wave: n_max slots
+    const uint8_t* glog;      // per tuple [k][n-k]: log G[i][k+jj] (255 = zero coefficient)
+    const uint8_t* gf;        // exp[512] ++ log[256]
+    int64_t W;                // row stride of cur / old
     uint8_t* cur;
     uint8_t* old;
     int32_t* len_cur;
@@ -158,8 +159,7 @@ struct VrParseArgs {
 };
 int vr_launch_frames(const VrFrameArgs& a, void* s);
 int vr_launch_parse(const VrParseArgs& a, void* s);
-int vr_launch_gather(const VrGatherArgs& a, void* s);
-int vr_launch_scatter(const VrScatterArgs& a, void* s);
+int vr_launch_encode(const VrEncodeArgs& a, void* s);
 int vr_launch_copy(const VrCopyArgs& a, void* s);
 int vr_launch_recover(const VrRecArgs& a, void* s);
 
