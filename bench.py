@@ -166,8 +166,9 @@ def extra_configs(steps=5):
     torch.cuda.synchronize()
     dt = (time.perf_counter() - t0) / nst
     t0 = time.perf_counter()
+    phases = []
     for _ in range(nst):
-        VrPlan(pat, P, light=True)
+        phases.append(VrPlan(pat, P, light=True).plan_ms)
     plan_s = (time.perf_counter() - t0) / nst
     dev_dt = timed(lambda: (v.encode(pl, frames=frames), v.decode(frames[0], frames[2], out=out4, out_len=ol4)), nst)
     fate = torch.from_numpy(v.fate).cuda()
@@ -177,10 +178,12 @@ def extra_configs(steps=5):
         "instances": int(len(v.encoders)), "switches": v.switches, "coding_rate": round(v.coding_rate, 4),
         "lost": int((ol4 == 0).sum()), "expected_lost": 2982,
         "host_plan_ms": round(plan_s * 1e3, 3),
+        "host_plan_phases_ms": {k: round(sum(p[k] for p in phases) / len(phases), 3) for k in phases[0]},
         "device_only": {"GiB_s": round(P * L / dev_dt / 2**30, 2), "ms": round(dev_dt * 1e3, 3)},
         "note": "ms includes the host plan (symbolic P2P loop, parallel symbolic decoders) and its "
-                "table uploads; device: per tuple one gather + encode + scatter launch, decode = one "
-                "copy launch + one recovery launch over the plan's coefficient rows",
+                "table uploads; device: one encode launch over every encoder instance of every "
+                "(T,B,N), decode = one copy launch + one recovery launch over the plan's "
+                "coefficient rows",
         "verified": bool(torch.equal(out4[ok4], pl[:P][ok4])) and v.lost == 2982 and
         int((ol4 == 0).sum()) == 2982 and w.lost == 2982}
     res["multistream_10k"] = multistream(steps)

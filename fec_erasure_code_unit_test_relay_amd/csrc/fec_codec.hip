@@ -152,24 +152,7 @@ int codec_init(fec_codec* c, int max_payload, int T, int B, int N) {
     const fec::Field& F = fec::field();
 
     // Per parity coefficient: the three register tables of gf_mul4 plus a non-zero flag.
-    const int np = g.n - g.k;
-    std::vector<uint32_t> ptab(static_cast<size_t>(std::max(1, g.k * np)) * 8, 0);
-    for (int i = 0; i < g.k; ++i)
-        for (int jj = 0; jj < np; ++jj) {
-            const uint8_t c0 = c->G[i * g.n + g.k + jj];
-            uint32_t* t = &ptab[(i * np + jj) * 8];
-            auto pack = [&](int shift, int base) {
-                uint32_t v = 0;
-                for (int e = 0; e < 4; ++e) v |= uint32_t(F.mul(c0, uint8_t((base + e) << shift))) << (8 * e);
-                return v;
-            };
-            t[0] = pack(0, 0);
-            t[1] = pack(0, 4);
-            t[2] = pack(3, 0);
-            t[3] = pack(3, 4);
-            t[4] = pack(6, 0);
-            t[5] = c0 ? 1u : 0u;
-        }
+    const std::vector<uint32_t> ptab = fec::parity_mul_tables(c->G, g.k, g.n);
     HIP_TRY(hipMalloc(&c->d_ptab, ptab.size() * 4));
     HIP_TRY(hipMemcpy(c->d_ptab, ptab.data(), ptab.size() * 4, hipMemcpyHostToDevice));
     HIP_TRY(hipMalloc(&c->d_rules, std::max<size_t>(16, c->rules->table.size())));

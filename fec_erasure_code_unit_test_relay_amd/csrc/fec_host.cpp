@@ -57,6 +57,29 @@ std::vector<uint8_t> make_generator(int T, int B, int N) {
     return G;
 }
 
+std::vector<uint32_t> parity_mul_tables(const std::vector<uint8_t>& G, int k, int n) {
+    const Field& F = field();
+    const int np = n - k;
+    std::vector<uint32_t> tab(static_cast<size_t>(std::max(1, k * np)) * 8, 0);
+    for (int i = 0; i < k; ++i)
+        for (int jj = 0; jj < np; ++jj) {
+            const uint8_t c = G[static_cast<size_t>(i) * n + k + jj];
+            uint32_t* t = &tab[static_cast<size_t>(i * np + jj) * 8];
+            auto pack = [&](int shift, int base) {
+                uint32_t v = 0;
+                for (int e = 0; e < 4; ++e) v |= uint32_t(F.mul(c, uint8_t((base + e) << shift))) << (8 * e);
+                return v;
+            };
+            t[0] = pack(0, 0);
+            t[1] = pack(0, 4);
+            t[2] = pack(3, 0);
+            t[3] = pack(3, 4);
+            t[4] = pack(6, 0);
+            t[5] = c ? 1u : 0u;
+        }
+    return tab;
+}
+
 // One column of the k x w decoding matrix together with its column of the action matrix.
 struct Column {
     uint8_t v[kMaxK];

@@ -86,6 +86,10 @@ struct Geometry {
 // transposed, then the burst-structure zeros of gen_G_cauchy (codingOperations.cpp:48-95).
 std::vector<uint8_t> make_generator(int T, int B, int N);
 
+// Per parity coefficient G[i][k+jj] (index i*(n-k)+jj): the three register tables of gf_mul4x
+// (fec_device.h) and a non-zero flag, 8 words each.
+std::vector<uint32_t> parity_mul_tables(const std::vector<uint8_t>& G, int k, int n);
+
 // ------------------------------------------------------------------------------------------
 // Decode rules.  For window w (columns 0..w-1 of the current diagonal codeword) and erasure mask m
 // (bit c = column c erased), entry = { sel[k] ; col[k][w] }: sel[i] = column j whose action-matrix

@@ -5,6 +5,7 @@
 #include <hip/hip_runtime_api.h>
 
 #include <algorithm>
+#include <chrono>
 #include <atomic>
 #include <cstring>
 #include <new>
@@ -175,6 +176,7 @@ void VrPlan::run(int max_payload, int T, int B, int N, bool mds, const uint8_t* 
         dec[dold].role_switch = first;
     };
 
+    const auto t_start = std::chrono::steady_clock::now();
     frames.reserve(static_cast<size_t>(P + T + 1));
     erased.reserve(static_cast<size_t>(P + T + 1));
     for (int64_t seq = 0;; ++seq) {
@@ -310,6 +312,7 @@ void VrPlan::run(int max_payload, int T, int B, int N, bool mds, const uint8_t* 
         for (auto& e : *list)
             if (e.role_switch < 0) e.role_switch = e.end;  // never became the old instance
 
+    const auto t_control = std::chrono::steady_clock::now();
     // ---- phase 2: the decoder instances, symbolically and in parallel ----
     for (const auto& d : dec) rules_for(d.T, d.B, d.N);  // built before the workers share the map
     struct Rec {
@@ -351,6 +354,9 @@ void VrPlan::run(int max_payload, int T, int B, int N, bool mds, const uint8_t* 
         for (size_t i = 0; i < nth; ++i) pool.emplace_back(worker);
         for (auto& th : pool) th.join();
     }
+    const auto t_decoders = std::chrono::steady_clock::now();
+    control_ms = std::chrono::duration<double, std::milli>(t_control - t_start).count();
+    decoders_ms = std::chrono::duration<double, std::milli>(t_decoders - t_control).count();
     for (int64_t x = 0; x < P; ++x)
         if (fate[x] == kLost) ++lost;
     std::vector<std::pair<int64_t, const Rec*>> order;
@@ -382,7 +388,7 @@ struct fec_vr_plan {
     const int32_t* d_enc_inst = nullptr;   // [nenc][4]: k, n, CW, glog offset
     const int64_t* d_enc_span = nullptr;   // [nenc][2]: first, role_switch
     const int64_t* d_enc_cum = nullptr;    // [nenc+1]
-    const uint8_t* d_glog = nullptr;
+    const uint32_t* d_gtab = nullptr;
     const int32_t* d_pk_dec = nullptr;
     const int32_t* d_inst = nullptr;
     const int64_t* d_inst_switch = nullptr;
@@ -395,7 +401,7 @@ struct fec_vr_plan {
     const int32_t* d_hdr = nullptr;    // [sent][4]: frame header T, B, N, counter
     void* d_hdr_arena = nullptr;
     int64_t enc_total = 0;             // codewords of all encoder instances
-    int enc_slot = 0, enc_ring = 0;    // fec_vr_encode_kernel's LDS ring geometry
+    int enc_tab = 0, enc_out = 0, enc_slot = 0, enc_wave = 0;  // fec_vr_encode_kernel's LDS layout
     bool enc_ready = false, dec_ready = false;
 
     ~fec_vr_plan() {
@@ -435,31 +441,28 @@ std::vector<uint8_t> gf_tables() {
 }
 
 // Encode tables: per encoder instance its geometry, first call, role switch and the running
-// count of codewords; per (T,B,N) tuple the logs of G's parity columns.
+// count of codewords; per (T,B,N) tuple the gf_mul4 register tables of G's parity columns.
 int prepare_encode(fec_vr_plan* v) {
     if (v->enc_ready) return FEC_OK;
     const auto& p = v->plan;
-    const fec::Field& F = fec::field();
-    std::map<int, int> goff;  // tuple -> offset in glog
-    std::vector<uint8_t> glog;
+    std::map<int, int> toff;  // tuple -> dword offset in gtab
+    std::vector<uint32_t> gtab;
     std::vector<int32_t> inst;
     std::vector<int64_t> span, cum{0};
-    int slot = 4, nmax = 1;
+    int tab = 32, out = 16, slot = 16, nmax = 1;
     for (const auto& e : p.enc) {
         const fec::Geometry g = fec::Geometry::make(p.L, e.T, e.B, e.N);
-        slot = std::max(slot, 4 + 4 * ((g.S * g.k - 2 + 3) / 4));
-        nmax = std::max(nmax, g.n);
         const int key = e.T * 1024 + e.B * 32 + e.N;
-        auto it = goff.find(key);
-        if (it == goff.end()) {
-            const std::vector<uint8_t> G = fec::make_generator(e.T, e.B, e.N);
-            it = goff.emplace(key, static_cast<int>(glog.size())).first;
-            for (int i = 0; i < g.k; ++i)
-                for (int j = g.k; j < g.n; ++j) {
-                    const uint8_t c = G[static_cast<size_t>(i) * g.n + j];
-                    glog.push_back(c ? F.log[c] : 255);
-                }
+        auto it = toff.find(key);
+        if (it == toff.end()) {
+            const std::vector<uint32_t> t = fec::parity_mul_tables(fec::make_generator(e.T, e.B, e.N), g.k, g.n);
+            it = toff.emplace(key, static_cast<int>(gtab.size())).first;
+            gtab.insert(gtab.end(), t.begin(), t.end());
         }
+        tab = std::max(tab, g.k * (g.n - g.k) * 32);
+        out = std::max(out, (g.CW + 8 + 15) / 16 * 16);
+        slot = std::max(slot, g.k * 4 * ((g.S + 3) / 4));
+        nmax = std::max(nmax, g.n);
         inst.insert(inst.end(), {g.k, g.n, g.CW, it->second});
         span.insert(span.end(), {e.first, e.role_switch});
         cum.push_back(cum.back() + (e.end - e.first));
@@ -468,13 +471,13 @@ int prepare_encode(fec_vr_plan* v) {
     ar.add(&v->d_enc_inst, inst);
     ar.add(&v->d_enc_span, span);
     ar.add(&v->d_enc_cum, cum);
-    ar.add(&v->d_glog, glog);
-    const std::vector<uint8_t> gf = gf_tables();
-    ar.add(&v->d_gf, gf);
+    ar.add(&v->d_gtab, gtab);
     if (int st = ar.commit(&v->d_enc_arena)) return st;
     v->enc_total = cum.back();
+    v->enc_tab = tab;
+    v->enc_out = out;
     v->enc_slot = slot;
-    v->enc_ring = slot * nmax;
+    v->enc_wave = tab + out + nmax * slot;
     v->enc_ready = true;
     return FEC_OK;
 }
@@ -498,11 +501,9 @@ int prepare_decode(fec_vr_plan* v) {
     ar.add(&v->d_rec_x, p.rec_x);
     ar.add(&v->d_rec_dec, p.rec_dec);
     ar.add(&v->d_rec_coef, p.rec_coef);
-    const uint8_t* gf_dec = nullptr;
     const std::vector<uint8_t> gf = gf_tables();
-    ar.add(&gf_dec, gf);
+    ar.add(&v->d_gf, gf);
     if (int st = ar.commit(&v->d_dec_arena)) return st;
-    if (!v->d_gf) v->d_gf = gf_dec;
     v->dec_ready = true;
     return FEC_OK;
 }
@@ -556,6 +557,13 @@ int fec_vr_plan_stats(const fec_vr_plan* v, int64_t* lost, int64_t* switches, do
     return FEC_OK;
 }
 
+int fec_vr_plan_timing(const fec_vr_plan* v, double* control_ms, double* decoders_ms) {
+    if (!v) return FEC_ERR_ARG;
+    if (control_ms) *control_ms = v->plan.control_ms;
+    if (decoders_ms) *decoders_ms = v->plan.decoders_ms;
+    return FEC_OK;
+}
+
 static void put_instances(const std::vector<fec::VrInstance>& in, int64_t* out) {
     for (size_t i = 0; i < in.size(); ++i) {
         int64_t* o = out + 6 * i;
@@ -605,8 +613,8 @@ int fec_vr_encode_batch(fec_vr_plan* v, const uint8_t* d_payload, const int32_t*
     if (!v || !d_payload || !d_cw_cur || !d_len_cur || !d_cw_old || !d_len_old) return FEC_ERR_ARG;
     if (int st = vr_guarded([&] { return prepare_encode(v); })) return st;
     fec::VrEncodeArgs a{d_payload, d_payload_len, v->plan.L, v->d_enc_inst, v->d_enc_span, v->d_enc_cum,
-                        static_cast<int>(v->plan.enc.size()), v->enc_total, v->enc_slot, v->enc_ring, v->d_glog, v->d_gf, v->cw_max, d_cw_cur, d_cw_old,
-                        d_len_cur, d_len_old};
+                        static_cast<int>(v->plan.enc.size()), v->enc_total, v->enc_tab, v->enc_out, v->enc_slot,
+                        v->enc_wave, v->d_gtab, v->cw_max, d_cw_cur, d_cw_old, d_len_cur, d_len_old};
     return fec::vr_launch_encode(a, hip_stream);
 }
 

@@ -68,6 +68,7 @@ struct VrPlan {
     std::vector<uint8_t> rec_coef;
     int64_t lost = 0, switches = 0;   // "Start double coding at the source" count
     float sum_coding_rate = 0;        // Variable_Rate_FEC_Encoder final_sum_coding_rate
+    double control_ms = 0, decoders_ms = 0;  // wall time of run()'s two phases
     double coding_rate() const { return sent ? sum_coding_rate / static_cast<float>(sent) : 0.0; }
 
     // Runs the loop until the receiver has processed seq P+T-1 (application_local_simulation.cpp:813).
@@ -88,15 +89,16 @@ struct VrEncodeArgs {
     const uint8_t* payload;   // [sent][L]
     const int32_t* len;       // may be null (all L)
     int L;
-    const int32_t* inst;      // [nenc][4]: k, n, CW, offset of the tuple's parity-coefficient logs
+    const int32_t* inst;      // [nenc][4]: k, n, CW, offset (dwords) of the tuple's gf_mul4 tables
     const int64_t* span;      // [nenc][2]: first, role_switch
     const int64_t* cum;       // [nenc+1]: codewords of instances < e
     int nenc;
     int64_t cum_host_total;   // cum[nenc] (host copy: sizes the grid)
-    int slot_bytes;           // LDS ring slot: 4 + payload-region words of the widest row, x4
-    int ring_bytes;           // per wave: n_max slots
-    const uint8_t* glog;      // per tuple [k][n-k]: log G[i][k+jj] (255 = zero coefficient)
-    const uint8_t* gf;        // exp[512] ++ log[256]
+    int tab_bytes;            // per wave LDS: tables of the widest tuple (k*(n-k)*32)
+    int out_bytes;            //   output row (max CW + 8, rounded to 16)
+    int slot_bytes;           //   one ring slot (k planes of ceil(S/4) words, max over tuples)
+    int wave_bytes;           //   tab + out + n_max * slot
+    const uint32_t* gtab;     // per tuple [k][n-k][8]: gf_mul4 tables of G[i][k+jj] (+ non-zero flag)
     int64_t W;                // row stride of cur / old
     uint8_t* cur;
     uint8_t* old;

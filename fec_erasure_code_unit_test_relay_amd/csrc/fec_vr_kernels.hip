@@ -74,27 +74,29 @@ __device__ __forceinline__ void wave_sync() {
 }
 
 // Each wave encodes a contiguous run of the codeword list, closed form of the diagonal
-// interleaving (as fec_encode_kernel) with the instance's geometry at run time: byte p =
-// (sub-stream s = p / n, position j = p % n) is X_seq[s][j] for j < k, else
-// XOR_i G[i][j] * X_{seq-(j-i)}[s][i] over the instance's own packets (X before its first call =
-// 0).  X_r = [len_hi, len_lo, payload, zero pad] (byte s*k+i = X_r[s][i]).  The wave keeps the
-// last n rows X_r in an LDS ring (slot r % n) and loads one new row per codeword while it stays
-// in one instance.  Lanes own the output row's 4-byte-aligned words (dword stores inside the row,
-// bytes at its two ends); the trimmed size is the last non-zero byte + 1 (FEC_Encoder.cpp:55-60).
+// interleaving (as fec_encode_kernel) with the instance's geometry at run time:
+//     cw_seq[s*n + j] = X_seq[s][j]                                  j <  k
+//     cw_seq[s*n + j] = XOR_{i<k} G[i][j] * X_{seq-(j-i)}[s][i]      j >= k
+// over the instance's own packets (X before its first call = 0), X_r[s][i] = byte s*k+i of
+// [len_hi, len_lo, payload, zero pad].  The wave keeps the last n rows in an LDS ring (slot
+// r % n), each transposed to k planes of ceil(S/4) words (word g of plane i = X_r[4g..4g+3][i]),
+// and loads one new row per codeword while it stays in one instance.  One lane task = (position j,
+// group g of 4 sub-streams): a plane word, or k packed gf_mul4 products with the instance's
+// register tables (staged in LDS per instance); its 4 bytes go to the LDS output row, which
+// leaves as dword stores (bytes at the row's two ends).  The trimmed size is the last non-zero
+// byte + 1 (FEC_Encoder.cpp:55-60), a wave max.
 __global__ __launch_bounds__(256) void fec_vr_encode_kernel(VrEncodeArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-    uint8_t* gexp = smem;          // 512
-    uint8_t* glg = smem + 512;     // 256
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-    uint8_t* glw = smem + 768 + wv * 512;           // the instance's parity-coefficient logs
-    uint8_t* ring = smem + 768 + 4 * 512 + wv * a.ring_bytes;  // n_max slots of slot_bytes
-    for (int i = tid; i < 768; i += 256) smem[i] = a.gf[i];
-    __syncthreads();
+    uint8_t* base = smem + wv * a.wave_bytes;
+    uint32_t* tabw = reinterpret_cast<uint32_t*>(base);              // [k*(n-k)][8]
+    uint8_t* outb = base + a.tab_bytes;                               // output row at offset head
+    uint8_t* ring = outb + a.out_bytes;                               // n_max slots
     const int L = a.L;
     const int64_t total = a.cum[a.nenc];
-    const int64_t nwaves = static_cast<int64_t>(gridDim.x) * 4;
+    const int64_t nwaves = static_cast<int64_t>(gridDim.x) * (blockDim.x >> 6);
     const int64_t chunk = (total + nwaves - 1) / nwaves;
-    const int64_t c0 = (static_cast<int64_t>(blockIdx.x) * 4 + wv) * chunk;
+    const int64_t c0 = (static_cast<int64_t>(blockIdx.x) * (blockDim.x >> 6) + wv) * chunk;
     const int64_t c1 = min(total, c0 + chunk);
     if (c0 >= c1) return;
     int lo = 0, hi = a.nenc - 1;  // last e with cum[e] <= c0
@@ -102,29 +104,35 @@ __global__ __launch_bounds__(256) void fec_vr_encode_kernel(VrEncodeArgs a) {
         const int mid = (lo + hi + 1) >> 1;
         if (a.cum[mid] <= c0) lo = mid; else hi = mid - 1;
     }
-    int e = lo, k = 0, n = 0, CW = 0, SK4 = 0;
-    float rn = 1.0f;
+    int e = lo, k = 0, n = 0, CW = 0, S = 0, NSG = 0, PL = 0, SB = 0;
+    float rk = 1.0f;
     int64_t first = 0, sw = 0, next_row = 0;  // next_row: first row not yet in the ring
     const bool words = (L & 3) == 0 && (reinterpret_cast<uintptr_t>(a.payload) & 3) == 0;
-    auto load_row = [&](int64_t r) {  // X_r -> slot r % n (all-zero before the instance's first call)
-        uint8_t* slot = ring + static_cast<int>(((r % n) + n) % n) * a.slot_bytes;  // X byte q at slot[q + 2]
-        int ln = 0;
-        if (r >= first) {
-            ln = a.len ? a.len[r] : L;
-            ln = ln < 0 ? 0 : (ln > L ? L : ln);
+    auto put = [&](uint8_t* slot, int q, uint32_t v) {  // X byte q -> plane q % k, column q / k
+        const int sidx = static_cast<int>((static_cast<float>(q) + 0.5f) * rk);
+        slot[(q - sidx * k) * PL + sidx] = static_cast<uint8_t>(v);
+    };
+    auto load_row = [&](int64_t r) {
+        uint8_t* slot = ring + static_cast<int>(((r % n) + n) % n) * SB;
+        for (int d = lane; d < k * NSG; d += 64) reinterpret_cast<uint32_t*>(slot)[d] = 0;
+        if (r < first) return;  // all-zero row before the instance's first call
+        int ln = a.len ? a.len[r] : L;
+        ln = ln < 0 ? 0 : (ln > L ? L : ln);
+        __builtin_amdgcn_wave_barrier();
+        if (lane == 0) {
+            put(slot, 0, static_cast<uint32_t>(ln >> 8));
+            put(slot, 1, static_cast<uint32_t>(ln & 0xff));
         }
-        if (lane == 0)
-            *reinterpret_cast<uint16_t*>(slot + 2) =
-                static_cast<uint16_t>((ln >> 8) | ((ln & 0xff) << 8));
         const uint8_t* src = a.payload + r * L;
         if (words) {
-            for (int w = lane; w < SK4; w += 64) {  // payload bytes 4w..4w+3 at slot[4 + 4w]
-                uint32_t v = 0;
-                if (4 * w < ln) v = *reinterpret_cast<const uint32_t*>(src + 4 * w) & keep_bytes(ln - 4 * w);
-                *reinterpret_cast<uint32_t*>(slot + 4 + 4 * w) = v;
+            for (int w = lane; 4 * w < ln; w += 64) {
+                const uint32_t v = *reinterpret_cast<const uint32_t*>(src + 4 * w);
+#pragma unroll
+                for (int b = 0; b < 4; ++b)
+                    if (4 * w + b < ln) put(slot, 4 * w + b + 2, v >> (8 * b));
             }
         } else {
-            for (int b = lane; b < 4 * SK4; b += 64) slot[4 + b] = b < ln ? src[b] : 0;
+            for (int b = lane; b < ln; b += 64) put(slot, b + 2, src[b]);
         }
     };
     for (int64_t c = c0; c < c1; ++c) {
@@ -137,62 +145,69 @@ __global__ __launch_bounds__(256) void fec_vr_encode_kernel(VrEncodeArgs a) {
             k = a.inst[4 * e];
             n = a.inst[4 * e + 1];
             CW = a.inst[4 * e + 2];
-            rn = 1.0f / static_cast<float>(n);
-            SK4 = (((CW / n) * k - 2) + 3) >> 2;  // payload-region words of a row
+            S = CW / n;
+            NSG = (S + 3) >> 2;
+            PL = 4 * NSG;
+            SB = k * PL;
+            rk = 1.0f / static_cast<float>(k);
             first = a.span[2 * e];
             sw = a.span[2 * e + 1];
         }
         const int64_t seq = first + (c - a.cum[e]);
-        wave_sync();  // earlier reads of the ring are done
+        wave_sync();  // earlier reads of the ring, tables and output row are done
         if (fresh) {
-            const uint8_t* gl = a.glog + a.inst[4 * e + 3];
-            for (int i = lane; i < k * (n - k); i += 64) glw[i] = gl[i];
+            const uint32_t* gt = a.gtab + a.inst[4 * e + 3];
+            for (int i = lane; i < k * (n - k) * 8; i += 64) tabw[i] = gt[i];
             for (int64_t r = seq - (n - 1); r <= seq; ++r) load_row(r);
         } else {
             for (int64_t r = next_row; r <= seq; ++r) load_row(r);
         }
         next_row = seq + 1;
-        wave_sync();
         const bool to_old = seq >= sw;
         uint8_t* row = (to_old ? a.old : a.cur) + seq * a.W;
         const int head = static_cast<int>(reinterpret_cast<uintptr_t>(row) & 3);
-        const int nw = (head + CW + 3) >> 2;
+        wave_sync();
         const int slot_seq = static_cast<int>(seq % n);
+        const float rg = 1.0f / static_cast<float>(NSG);
+        for (int task = lane; task < n * NSG; task += 64) {
+            const int j = static_cast<int>((static_cast<float>(task) + 0.5f) * rg);
+            const int g = task - j * NSG;
+            uint32_t v;
+            if (j < k) {
+                v = reinterpret_cast<const uint32_t*>(ring + slot_seq * SB + j * PL)[g];
+            } else {
+                v = 0;
+                for (int i = 0; i < k; ++i) {
+                    const uint32_t* t = tabw + (i * (n - k) + (j - k)) * 8;
+                    if (!t[5]) continue;
+                    int sl = slot_seq - (j - i);
+                    sl += sl < 0 ? n : 0;
+                    v ^= gf_mul4x(t, reinterpret_cast<const uint32_t*>(ring + sl * SB + i * PL)[g]);
+                }
+            }
+#pragma unroll
+            for (int b = 0; b < 4; ++b)
+                if (4 * g + b < S) outb[head + (4 * g + b) * n + j] = static_cast<uint8_t>(v >> (8 * b));
+        }
+        wave_sync();
+        const int nw = (head + CW + 3) >> 2;
         int last_nz = -1;
         for (int w = lane; w < nw; w += 64) {
-            uint32_t v = 0;
-            int valid = 0;
-#pragma unroll
-            for (int b = 0; b < 4; ++b) {
-                const int p = 4 * w + b - head;
-                if (p < 0 || p >= CW) continue;
-                valid |= 1 << b;
-                const int s = static_cast<int>((static_cast<float>(p) + 0.5f) * rn), j = p - s * n;
-                uint32_t byte;
-                if (j < k) {
-                    byte = ring[slot_seq * a.slot_bytes + s * k + j + 2];
-                } else {
-                    uint32_t acc = 0;
-                    for (int i = 0; i < k; ++i) {
-                        const int lg = glw[i * (n - k) + (j - k)];
-                        if (lg == 255) continue;
-                        int sl = slot_seq - (j - i);
-                        sl += sl < 0 ? n : 0;
-                        const uint32_t x = ring[sl * a.slot_bytes + s * k + i + 2];
-                        if (x) acc ^= gexp[lg + glg[x]];
-                    }
-                    byte = acc;
-                }
-                if (byte) last_nz = p;
-                v |= byte << (8 * b);
-            }
+            const uint32_t v = reinterpret_cast<const uint32_t*>(outb)[w];
             uint8_t* dst = row - head + 4 * w;
-            if (valid == 15) {
+            const int p0 = 4 * w - head;  // row byte of word byte 0
+            if (p0 >= 0 && p0 + 4 <= CW) {
                 *reinterpret_cast<uint32_t*>(dst) = v;
+                if (v) last_nz = p0 + 3 - (__builtin_clz(v) >> 3);
             } else {
 #pragma unroll
-                for (int b = 0; b < 4; ++b)
-                    if (valid & (1 << b)) dst[b] = static_cast<uint8_t>(v >> (8 * b));
+                for (int b = 0; b < 4; ++b) {
+                    const int p = p0 + b;
+                    if (p < 0 || p >= CW) continue;
+                    const uint8_t x = static_cast<uint8_t>(v >> (8 * b));
+                    dst[b] = x;
+                    if (x) last_nz = p;
+                }
             }
         }
         for (int o = 32; o > 0; o >>= 1) last_nz = max(last_nz, __shfl_xor(last_nz, o));
@@ -320,11 +335,12 @@ int vr_launch_parse(const VrParseArgs& a, void* s) {
 
 int vr_launch_encode(const VrEncodeArgs& a, void* s) {
     if (a.nenc <= 0) return FEC_OK;
-    const size_t lds = 768 + 4 * 512 + 4 * static_cast<size_t>(a.ring_bytes);
-    if (lds > 64 * 1024) return FEC_ERR_ARG;
-    const int64_t total = a.cum_host_total;
-    const unsigned grid = static_cast<unsigned>(std::max<int64_t>(1, std::min<int64_t>((total + 63) / 64, 4096)));
-    hipLaunchKernelGGL(fec_vr_encode_kernel, dim3(grid), dim3(256), lds, static_cast<hipStream_t>(s), a);
+    const int wpb = std::min(4, 65536 / std::max(1, a.wave_bytes));
+    if (wpb < 1) return FEC_ERR_ARG;
+    const int64_t waves = std::max<int64_t>(1, std::min<int64_t>((a.cum_host_total + 15) / 16, 16384));
+    const unsigned grid = static_cast<unsigned>((waves + wpb - 1) / wpb);
+    hipLaunchKernelGGL(fec_vr_encode_kernel, dim3(grid), dim3(64 * wpb), static_cast<size_t>(wpb) * a.wave_bytes,
+                       static_cast<hipStream_t>(s), a);
     return hipGetLastError() == hipSuccess ? FEC_OK : FEC_ERR_HIP;
 }
 int vr_launch_copy(const VrCopyArgs& a, void* s) {

@@ -37,6 +37,9 @@ class VrPlan:
               "fec_vr_plan_stats")
         self.lost, self.switches, self.coding_rate = lost.value, sw.value, rate.value
         self.sent, self.cw_max = sent.value, cwm.value
+        c_ms, d_ms = ctypes.c_double(), ctypes.c_double()
+        check(lib().fec_vr_plan_timing(h, ctypes.byref(c_ms), ctypes.byref(d_ms)), "fec_vr_plan_timing")
+        self.plan_ms = {"control_loop": c_ms.value, "decoder_instances": d_ms.value}
         if light:
             return
         self.encoders = np.zeros((ne.value, 6), dtype=np.int64)

@@ -246,6 +246,9 @@ int fec_vr_plan_destroy(fec_vr_plan *plan);
  * sent: packets the sender produced; cw_max: row stride of the codeword arrays below. */
 int fec_vr_plan_stats(const fec_vr_plan *plan, int64_t *lost, int64_t *switches, double *coding_rate,
                       int64_t *sent, int *n_encoders, int *n_decoders, int *cw_max);
+/* wall time of the plan's two phases: the serial control loop (sender, estimators, switches,
+ * decoder swaps) and the parallel symbolic decoder instances, in ms */
+int fec_vr_plan_timing(const fec_vr_plan *plan, double *control_ms, double *decoders_ms);
 /* instances, 6 int64 each: T, B, N, first seq, seq from which it is the old one, end seq */
 int fec_vr_plan_instances(const fec_vr_plan *plan, int64_t *encoders, int64_t *decoders);
 /* per sent packet: frames (6 int32: header T, B, N, counter_for_start_and_end, current encoder,
