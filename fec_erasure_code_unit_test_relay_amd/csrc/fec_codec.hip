@@ -347,15 +347,36 @@ int codec_init(fec_codec* c, int max_payload, int T, int B, int N) {
     if (!c->copyf_tp) c->copy_fast = nullptr;
     if ((g.L & 3) == 0 && (g.S + 3) / 4 <= 64 && g.T < 4 * ((g.S + 3) / 4))
         c->copy_wave = fec::fec_copy_wave_kernel_for(g.k, g.n - g.k);
-    HIP_TRY(hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking));
+    // experiments (FEC_SIDE_CUS / FEC_SIDE_PRIO): the planner's side stream on a CU subset, or at
+    // the lowest / highest stream priority
+    const char* side_cus = std::getenv("FEC_SIDE_CUS");
+    const char* side_prio = std::getenv("FEC_SIDE_PRIO");
+    if (side_cus && std::atoi(side_cus) > 0) {
+        int dev = 0, cus = 0;
+        HIP_TRY(hipGetDevice(&dev));
+        HIP_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+        const int want = std::min(cus, std::atoi(side_cus));
+        std::vector<uint32_t> mask((cus + 31) / 32, 0u);
+        for (int i = 0; i < want; ++i) {
+            const int cu = static_cast<int>(static_cast<int64_t>(i) * cus / want);
+            mask[cu / 32] |= 1u << (cu % 32);
+        }
+        HIP_TRY(hipExtStreamCreateWithCUMask(&c->side, static_cast<uint32_t>(mask.size()), mask.data()));
+    } else if (side_prio) {
+        int least = 0, greatest = 0;
+        HIP_TRY(hipDeviceGetStreamPriorityRange(&least, &greatest));
+        HIP_TRY(hipStreamCreateWithPriority(&c->side, hipStreamNonBlocking,
+                                            std::strcmp(side_prio, "high") == 0 ? greatest : least));
+    } else {
+        HIP_TRY(hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking));
+    }
     HIP_TRY(hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming));
     HIP_TRY(hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming));
     return FEC_OK;
 }
 
 struct WsLayout {
-    size_t counters, episodes, erased, sym_ok, rec_list, coef;
-    size_t ep_slot, ep_last, work, fill, keys, reps, total;
+    size_t counters, erased, src_d, rec_list, sym_ok, coef, work, dups, keys, reps_tr, total;
     int tbits;
 };
 
@@ -363,35 +384,33 @@ WsLayout ws_layout(const Geometry& g, int64_t P) {
     auto up = [](size_t v) { return (v + 255) & ~size_t(255); };
     WsLayout w;
     w.counters = 0;
-    w.episodes = up(64);
-    w.erased = w.episodes + up(static_cast<size_t>(P) * 4);
-    w.sym_ok = w.erased + up(static_cast<size_t>(P) * 4);
-    w.rec_list = w.sym_ok + up(static_cast<size_t>(P) * g.k);
-    w.coef = w.rec_list + up(static_cast<size_t>(P) * 4);
+    w.erased = up(64);
+    w.src_d = w.erased + up(static_cast<size_t>(P) * 4);
+    w.rec_list = w.src_d + up(static_cast<size_t>(P) * 4);
+    w.sym_ok = w.rec_list + up(static_cast<size_t>(P) * 8);
+    w.coef = w.sym_ok + up(static_cast<size_t>(P) * g.k);
     // episode starts are >= T+2 packets apart
     const size_t maxep = static_cast<size_t>(P) / static_cast<size_t>(g.T + 2) + 2;
     w.tbits = 8;
     while ((size_t(1) << w.tbits) < 2 * maxep) ++w.tbits;
-    w.ep_slot = w.coef + up(static_cast<size_t>(P) * g.k * g.n);
-    w.ep_last = w.ep_slot + up(maxep * 4);
-    w.work = w.ep_last + up(maxep * 4);
-    w.fill = w.work + up(maxep * 4);
-    w.keys = w.fill + up(maxep * 4);
-    w.reps = w.keys + up((size_t(1) << w.tbits) * 8);
-    w.total = w.reps + up((size_t(1) << w.tbits) * 4);
+    w.work = w.coef + up(static_cast<size_t>(P) * g.k * g.n);
+    w.dups = w.work + up(maxep * 4);
+    w.keys = w.dups + up(maxep * 8);
+    w.reps_tr = w.keys + up((size_t(1) << w.tbits) * 8);
+    w.total = w.reps_tr + up((size_t(1) << w.tbits) * 4);
     return w;
 }
 
 struct Ws {
-    int32_t* counters;
-    int32_t* episodes;
+    int32_t* counters;  // [1] erased outputs, [2] recovered, [6] replayed, [7] duplicates
     int32_t* erased;
-    uint8_t* sym_ok;
+    int32_t* src_d;
     int32_t* rec_list;
+    uint8_t* sym_ok;
     uint8_t* coef;
-    int32_t *ep_slot, *ep_last, *work, *fill;
+    int32_t *work, *dups;
     uint64_t* keys;
-    int32_t* reps;
+    int32_t* reps_tr;
     int tbits;
 };
 
@@ -399,10 +418,10 @@ Ws ws_carve(const Geometry& g, int64_t P, void* d_ws) {
     const WsLayout w = ws_layout(g, P);
     uint8_t* base = static_cast<uint8_t*>(d_ws);
     auto i32 = [&](size_t o) { return reinterpret_cast<int32_t*>(base + o); };
-    return {i32(w.counters), i32(w.episodes), i32(w.erased), base + w.sym_ok, i32(w.rec_list),
-            base + w.coef, i32(w.ep_slot), i32(w.ep_last), i32(w.work), i32(w.fill),
-            reinterpret_cast<uint64_t*>(base + w.keys), i32(w.reps), w.tbits};
+    return {i32(w.counters), i32(w.erased), i32(w.src_d), i32(w.rec_list), base + w.sym_ok, base + w.coef, i32(w.work),
+            i32(w.dups), reinterpret_cast<uint64_t*>(base + w.keys), i32(w.reps_tr), w.tbits};
 }
+
 
 int launch_encode_fast(fec_codec* c, const uint8_t* d_payload, const int32_t* d_len, int64_t history,
                        int64_t P, uint8_t* d_cw, int32_t* d_cwlen, hipStream_t s) {
@@ -674,7 +693,10 @@ int check_ws(fec_codec* c, int64_t P, void* d_ws, size_t ws_bytes) {
     return FEC_OK;
 }
 
-// Erasure-pattern-only half of the decode: resync points + per-(episode, diagonal) replay.
+// Erasure-pattern-only half of the decode: two launches.  fec_episode_kernel finds the resync
+// points, the loss episodes and their shapes and lists the erased outputs; the plan kernel replays
+// one episode per shape per diagonal and points the other episodes' erased outputs at their
+// representative's rows.
 int launch_plan(fec_codec* c, const uint8_t* d_er, int64_t P, void* d_ws, size_t ws_bytes,
                 hipStream_t s) {
     const Geometry& g = c->g;
@@ -684,39 +706,30 @@ int launch_plan(fec_codec* c, const uint8_t* d_er, int64_t P, void* d_ws, size_t
     const Ws w = ws_carve(g, P, d_ws);
     const bool fast_ok = c->plan_fast && P < (int64_t(1) << 31) - 1024;
     if (c->plan_path == 2 && !fast_ok) return FEC_ERR_ARG;
+    if (g.T >= 64) return FEC_ERR_ARG;  // fec_episode_kernel's resync look-back is one 64-packet word
     HIP_TRY(hipMemsetAsync(w.counters, 0, 64, s));
     HIP_TRY(hipMemsetAsync(w.keys, 0, (size_t(1) << w.tbits) * 8, s));
     hipEvent_t stop;
     if (int st = c->begin(FEC_KERNEL_DEC_SCAN, s, &stop)) return st;
-    const int64_t sblocks = std::min<int64_t>((P + 4095) / 4096, 2048);
-    hipLaunchKernelGGL(fec::fec_scan_kernel, dim3(static_cast<unsigned>(sblocks)), dim3(256), 0, s,
-                       d_er, P, Pout, g.T, w.counters, w.episodes, w.erased);
+    fec::EpisodeArgs ea;
+    ea.er = d_er;
+    ea.P = P;
+    ea.Pout = Pout;
+    ea.T = g.T;
+    ea.tbits = w.tbits;
+    ea.dedup = c->dedup;
+    ea.counters = w.counters;
+    ea.erased = w.erased;
+    ea.src_d = w.src_d;
+    ea.work = w.work;
+    ea.dups = w.dups;
+    ea.keys = w.keys;
+    ea.reps_tr = w.reps_tr;
+    ea.stamps = (c->stamp_kernel == FEC_KERNEL_DEC_SCAN) ? c->d_stamps : nullptr;
+    const int64_t sblocks = std::min<int64_t>((P + 4095) / 4096, 8192);
+    hipLaunchKernelGGL(fec::fec_episode_kernel, dim3(static_cast<unsigned>(sblocks)), dim3(64), 0, s, ea);
     HIP_TRY(hipGetLastError());
     if (int st = c->end(stop, s)) return st;
-
-    fec::ShapeArgs sa;
-    sa.er = d_er;
-    sa.P = P;
-    sa.T = g.T;
-    sa.k = g.k;
-    sa.n = g.n;
-    sa.tbits = w.tbits;
-    sa.dedup = c->dedup;
-    sa.counters = w.counters;
-    sa.episodes = w.episodes;
-    sa.ep_slot = w.ep_slot;
-    sa.ep_last = w.ep_last;
-    sa.work = w.work;
-    sa.fill = w.fill;
-    sa.keys = w.keys;
-    sa.reps = w.reps;
-    sa.sym_ok = w.sym_ok;
-    sa.coef = w.coef;
-    if (int st = c->begin(FEC_KERNEL_DEC_PLAN, s, &stop)) return st;
-    const int64_t maxep = P / (g.T + 2) + 2;  // ws_layout's bound on episode starts
-    hipLaunchKernelGGL(fec::fec_shape_kernel, dim3(static_cast<unsigned>(std::min<int64_t>((maxep + 255) / 256, 2048))),
-                       dim3(256), 0, s, sa);
-    HIP_TRY(hipGetLastError());
 
     fec::PlanArgs pa;
     pa.er = d_er;
@@ -732,15 +745,20 @@ int launch_plan(fec_codec* c, const uint8_t* d_er, int64_t P, void* d_ws, size_t
     pa.n = g.n;
     pa.T = g.T;
     pa.counters = w.counters;
-    pa.episodes = w.episodes;
     pa.work = w.work;
+    pa.dups = w.dups;
+    pa.keys = w.keys;
+    pa.reps_tr = w.reps_tr;
+    pa.src_d = w.src_d;
     pa.rstate = c->d_rstate;
     pa.rs_bytes = fec::resync_state_bytes(g);
     pa.sym_ok = w.sym_ok;
     pa.coef = w.coef;
-    // The work lists live on the device.  Measured in the full step (encode + decode): grids of
-    // 8192 / 1024 / 256 / 64 workgroups give 0.388 / 0.397 / 0.437 / 0.609 ms.
-    int pgrid = 8192;
+    if (int st = c->begin(FEC_KERNEL_DEC_PLAN, s, &stop)) return st;
+    // The work lists live on the device: (episode, diagonal) replays of one episode per shape
+    // (41 x 11 at (10,3,3) on bin/erasure.bin) and one item per duplicate episode.  Graph-replayed
+    // plan beside the copy: 8192 / 512 workgroups 175 / 169 us (tools/graph_parts.py).
+    int pgrid = 1024;
     if (const char* v = std::getenv("FEC_PLAN_GRID")) pgrid = std::max(1, std::atoi(v));
     if (fast_ok && c->plan_path != 1) {
         pa.rules = c->d_rules_log;
@@ -750,12 +768,6 @@ int launch_plan(fec_codec* c, const uint8_t* d_er, int64_t P, void* d_ws, size_t
         const int plan_lds = 768 + g.n * g.n + 2 * g.k * g.n + 32 * 16 + 32 * 32 + g.k * (1 + g.n);
         hipLaunchKernelGGL(fec::fec_plan_kernel, dim3(pgrid), dim3(64), plan_lds, s, pa);
     }
-    HIP_TRY(hipGetLastError());
-    hipLaunchKernelGGL(fec::fec_shape_fill_kernel, dim3(pgrid), dim3(64), 0, s, sa);
-    HIP_TRY(hipGetLastError());
-    // packets with all k symbols recovered -> rec_list (timed with the plan)
-    hipLaunchKernelGGL(fec::fec_compact_kernel, dim3(256), dim3(256), 0, s, w.counters, w.erased,
-                       w.sym_ok, g.k, w.rec_list);
     HIP_TRY(hipGetLastError());
     return c->end(stop, s);
 }
@@ -867,6 +879,8 @@ int launch_copy(fec_codec* c, const uint8_t* d_cw, const uint8_t* d_er, int64_t 
         fa.out_bytes = round16(fa.TP * g.L);
         fa.stamps = (c->stamp_kernel == FEC_KERNEL_DEC_COPY) ? c->d_stamps : nullptr;
         fa.skip_erased = 0;
+        fa.nt = 0;
+        if (const char* v = std::getenv("FEC_COPY_NT")) fa.nt = std::atoi(v) ? 1 : 0;
         const int64_t blocks = (Pout + fa.TP - 1) / fa.TP;
         hipEvent_t stop;
         if (int st = c->begin(FEC_KERNEL_DEC_COPY, s, &stop)) return st;
@@ -899,12 +913,43 @@ int launch_copy(fec_codec* c, const uint8_t* d_cw, const uint8_t* d_er, int64_t 
     return c->end(stop, s);
 }
 
+// Recovered packets -> rec_list (fec_compact_kernel), on `s` after the plan.
+int launch_compact(fec_codec* c, int64_t P, uint8_t* d_out, int32_t* d_outlen, void* d_ws, size_t ws_bytes,
+                   hipStream_t s, int64_t row_off = 0) {
+    const Geometry& g = c->g;
+    if (P - g.T <= 0) return FEC_OK;
+    if (int st = check_ws(c, P, d_ws, ws_bytes)) return st;
+    const Ws w = ws_carve(g, P, d_ws);
+    fec::CompactArgs ca;
+    ca.counters = w.counters;
+    ca.erased = w.erased;
+    ca.src_d = w.src_d;
+    ca.sym_ok = w.sym_ok;
+    ca.k = g.k;
+    ca.rec_list = w.rec_list;
+    // when the copy kernel leaves erased rows alone (wave copy), the lost ones get their zero row
+    // and length 0 here
+    ca.zero_lost = copy_skips_erased(c, d_out, P) ? 1 : 0;
+    ca.out = d_out;
+    ca.out_len = d_outlen;
+    ca.L = g.L;
+    ca.row_off = row_off;
+    HIP_TRY(hipMemsetAsync(w.counters + 2, 0, 4, s));  // a second compaction of one plan starts over
+    hipLaunchKernelGGL(fec::fec_compact_kernel, dim3(256), dim3(256), 0, s, ca);
+    HIP_TRY(hipGetLastError());
+    return FEC_OK;
+}
+
+// Byte half of the erased packets: one wave per recovered packet of rec_list.  `compacted`: the
+// list was built on this stream's side already (launch_decode); otherwise it is built here first.
 int launch_recover(fec_codec* c, const uint8_t* d_cw, int64_t P, uint8_t* d_out, int32_t* d_outlen,
-                   void* d_ws, size_t ws_bytes, hipStream_t s, int64_t row_off = 0) {
+                   void* d_ws, size_t ws_bytes, hipStream_t s, int64_t row_off = 0, bool compacted = false) {
     const Geometry& g = c->g;
     const int64_t Pout = P - g.T;
     if (Pout <= 0) return FEC_OK;
     if (int st = check_ws(c, P, d_ws, ws_bytes)) return st;
+    if (!compacted)
+        if (int st = launch_compact(c, P, d_out, d_outlen, d_ws, ws_bytes, s, row_off)) return st;
     const Ws w = ws_carve(g, P, d_ws);
     fec::RecArgs ra;
     ra.cw = d_cw;
@@ -923,16 +968,23 @@ int launch_recover(fec_codec* c, const uint8_t* d_cw, int64_t P, uint8_t* d_out,
     ra.CW = g.CW;
     hipEvent_t stop;
     if (int st = c->begin(FEC_KERNEL_DEC_RECOVER, s, &stop)) return st;
-    // when the copy kernel leaves erased rows alone (wave copy), the lost ones get their zero row
-    // and length 0 here
-    ra.erased = w.erased;
-    ra.sym_ok = w.sym_ok;
-    ra.zero_lost = copy_skips_erased(c, d_out, P) ? 1 : 0;
     ra.row_off = row_off;
-    if (g.n <= 17)
-        hipLaunchKernelGGL(fec::fec_recover_kernel_t<17>, dim3(1024), dim3(256), 0, s, ra);
+    ra.stamps = (c->stamp_kernel == FEC_KERNEL_DEC_RECOVER) ? c->d_stamps : nullptr;
+    // the k+n-1 rows a recovered packet reads, staged in LDS when they fit 12 KB per wave
+    // (fec_recover_kernel_t's kRecStageChunks)
+    const int span = (g.k + g.n - 1) * g.CW + 32;
+    ra.stage_bytes = (span <= 12 * 1024 && g.n <= 17) ? ((span + 15) & ~15) : 0;
+    if (const char* v = std::getenv("FEC_REC_STAGE")) ra.stage_bytes = std::atoi(v) ? ra.stage_bytes : 0;
+    // a wave per recovered packet: up to 4096 waves
+    const unsigned rgrid = static_cast<unsigned>(std::min<int64_t>((Pout + 3) / 4, 1024));
+    const int maxn = g.n <= 17 ? 17 : 32;
+    const int lds = fec::recover_lds_bytes(maxn, ra.stage_bytes);
+    if (g.n > 17)
+        hipLaunchKernelGGL((fec::fec_recover_kernel_t<32, false>), dim3(rgrid), dim3(256), lds, s, ra);
+    else if (ra.stage_bytes)
+        hipLaunchKernelGGL((fec::fec_recover_kernel_t<17, true>), dim3(rgrid), dim3(256), lds, s, ra);
     else
-        hipLaunchKernelGGL(fec::fec_recover_kernel_t<32>, dim3(1024), dim3(256), 0, s, ra);
+        hipLaunchKernelGGL((fec::fec_recover_kernel_t<17, false>), dim3(rgrid), dim3(256), lds, s, ra);
     HIP_TRY(hipGetLastError());
     return c->end(stop, s);
 }
@@ -946,17 +998,18 @@ int launch_decode(fec_codec* c, const uint8_t* d_cw, const uint8_t* d_er, int64_
     HIP_TRY(hipEventRecord(c->ev_fork, s));
     HIP_TRY(hipStreamWaitEvent(c->side, c->ev_fork, 0));
     if (int st = launch_plan(c, d_er, P, d_ws, ws_bytes, c->side)) return st;
+    if (int st = launch_compact(c, P, d_out, d_outlen, d_ws, ws_bytes, c->side)) return st;
     // The barrier-free copy writes received rows only: the recovery (erased rows) then runs on
     // the side stream right after the plan, concurrently with the copy.
     bool concurrent = copy_skips_erased(c, d_out, P);
     if (const char* v = std::getenv("FEC_RECOVER_SERIAL")) concurrent = concurrent && !std::atoi(v);
     if (concurrent)
-        if (int st = launch_recover(c, d_cw, P, d_out, d_outlen, d_ws, ws_bytes, c->side)) return st;
+        if (int st = launch_recover(c, d_cw, P, d_out, d_outlen, d_ws, ws_bytes, c->side, 0, true)) return st;
     HIP_TRY(hipEventRecord(c->ev_join, c->side));
     if (int st = launch_copy(c, d_cw, d_er, P, d_out, d_outlen, s)) return st;
     HIP_TRY(hipStreamWaitEvent(s, c->ev_join, 0));
     if (concurrent) return FEC_OK;
-    return launch_recover(c, d_cw, P, d_out, d_outlen, d_ws, ws_bytes, s);
+    return launch_recover(c, d_cw, P, d_out, d_outlen, d_ws, ws_bytes, s, 0, true);
 }
 
 // Continuing decode (fec_decode_stream_push): the next P packets of a stream whose earlier packets
@@ -1002,6 +1055,7 @@ int launch_decode_stream(fec_codec* c, fec_decode_stream* st, const uint8_t* d_c
     HIP_TRY(hipEventRecord(c->ev_fork, s));
     HIP_TRY(hipStreamWaitEvent(c->side, c->ev_fork, 0));
     if (int e = launch_plan(c, er_c, Pp, d_ws, ws_bytes, c->side)) return e;
+    if (int e = launch_compact(c, Pp, d_out, d_outlen, d_ws, ws_bytes, c->side, next_out - cut)) return e;
     HIP_TRY(hipEventRecord(c->ev_join, c->side));
     // received rows [next_out, end - T): a copy over packets [next_out, end)
     const int64_t Pc = end - next_out;
@@ -1013,7 +1067,7 @@ int launch_decode_stream(fec_codec* c, fec_decode_stream* st, const uint8_t* d_c
     c->copy_path = saved;
     if (e) return e;
     HIP_TRY(hipStreamWaitEvent(s, c->ev_join, 0));
-    if (int e2 = launch_recover(c, cw_c, Pp, d_out, d_outlen, d_ws, ws_bytes, s, next_out - cut)) return e2;
+    if (int e2 = launch_recover(c, cw_c, Pp, d_out, d_outlen, d_ws, ws_bytes, s, next_out - cut, true)) return e2;
     *n_out = end - T - next_out;
     st->consumed = end;
     st->last_cut = cut;
@@ -1224,10 +1278,10 @@ int fec_decode_recover(fec_codec* c, const uint8_t* d_cw, int64_t P, uint8_t* d_
 
 int fec_decode_counters(const void* d_ws, int64_t* episodes, int64_t* recovered, int64_t* lost) {
     if (!d_ws) return FEC_ERR_ARG;
-    int32_t h[4];
+    int32_t h[8];
     HIP_TRY(hipDeviceSynchronize());
     HIP_TRY(hipMemcpy(h, d_ws, sizeof(h), hipMemcpyDeviceToHost));
-    if (episodes) *episodes = h[0];
+    if (episodes) *episodes = h[6] + h[7];  // every episode is replayed or a duplicate
     if (recovered) *recovered = h[2];
     if (lost) *lost = h[1] - h[2];  // erased outputs that were not recovered
     return FEC_OK;
@@ -1271,11 +1325,11 @@ int fec_codec_info(const fec_codec* c, char* buf, size_t size) {
 
 int fec_decode_plan_stats(const void* d_ws, int64_t* replayed, int64_t* filled) {
     if (!d_ws) return FEC_ERR_ARG;
-    int32_t h[5];
+    int32_t h[8];
     HIP_TRY(hipDeviceSynchronize());
     HIP_TRY(hipMemcpy(h, d_ws, sizeof(h), hipMemcpyDeviceToHost));
-    if (replayed) *replayed = h[3];
-    if (filled) *filled = h[4];
+    if (replayed) *replayed = h[6];
+    if (filled) *filled = h[7];
     return FEC_OK;
 }
 

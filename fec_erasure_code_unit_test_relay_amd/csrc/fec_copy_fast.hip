@@ -29,7 +29,10 @@ __global__ __launch_bounds__(256) void fec_copy_fast_kernel(CopyFastArgs a) {
 
     const uint8_t* gA = a.cw + x0 * CW;
     const int delta = static_cast<int>(reinterpret_cast<uintptr_t>(gA) & 15);
-    stage_to_lds<8>(raw, gA - delta, delta, delta + ntile * CW, tid, 256);
+    if (a.nt)
+        stage_to_lds<8, true>(raw, gA - delta, delta, delta + ntile * CW, tid, 256);
+    else
+        stage_to_lds<8>(raw, gA - delta, delta, delta + ntile * CW, tid, 256);
     for (int i = tid; i < ntile + T; i += 256) erw[i] = a.er[x0 + i];  // x0+ntile+T-1 < P
     __syncthreads();
     phase_stamp(a.stamps, blockIdx.x, 1);
@@ -108,7 +111,11 @@ __global__ __launch_bounds__(256) void fec_copy_fast_kernel(CopyFastArgs a) {
     if ((obytes & 15) == 0 && (reinterpret_cast<uintptr_t>(dst) & 15) == 0) {
         for (int o = tid * 16; o < obytes; o += 256 * 16) {
             if (!skip || (!erw[o / L] && !erw[(o + 15) / L])) {
-                *reinterpret_cast<uint4*>(dst + o) = *reinterpret_cast<const uint4*>(xo + o);
+                const uint4 v = *reinterpret_cast<const uint4*>(xo + o);
+                if (a.nt)
+                    nt_store16(dst + o, v);
+                else
+                    *reinterpret_cast<uint4*>(dst + o) = v;
             } else {
 #pragma unroll
                 for (int q = 0; q < 16; q += 4)

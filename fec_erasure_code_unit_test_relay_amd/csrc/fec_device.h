@@ -37,11 +37,23 @@ __device__ __forceinline__ uint32_t keep_bytes(int c) {  // mask of the low c by
     return c <= 0 ? 0u : (c >= 4 ? 0xffffffffu : ((1u << (8 * c)) - 1u));
 }
 
+// Non-temporal (streaming) 16-byte global load / store: data touched once, kept out of the way
+// of the caches' other users.
+typedef uint32_t nt_u32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ uint4 nt_load16(const void* p) {
+    const nt_u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const nt_u32x4*>(p));
+    return make_uint4(v.x, v.y, v.z, v.w);
+}
+__device__ __forceinline__ void nt_store16(void* p, uint4 v) {
+    const nt_u32x4 w = {v.x, v.y, v.z, v.w};
+    __builtin_nontemporal_store(w, reinterpret_cast<nt_u32x4*>(p));
+}
+
 // Copy global bytes [gbase + delta, gbase + total) into lds[delta, total) (same offsets).  gbase
 // is 16-byte aligned, delta and total are multiples of 4.  Interior 16-byte chunks use dwordx4
 // loads, BATCH of them in flight per thread before the LDS writes; the two edge chunks use dword
 // loads so nothing outside the range is read.
-template <int BATCH>
+template <int BATCH, bool NT = false>
 __device__ __forceinline__ void stage_to_lds(uint8_t* lds, const uint8_t* gbase, int delta, int total,
                                              int tid, int nthreads) {
     const int nchunks = (total + 15) >> 4;
@@ -51,7 +63,11 @@ __device__ __forceinline__ void stage_to_lds(uint8_t* lds, const uint8_t* gbase,
         for (int q = 0; q < BATCH; ++q) {
             const int lo = (c0 + q * nthreads + tid) << 4;
             const bool full = lo >= delta && lo + 16 <= total;
-            v[q] = full ? *reinterpret_cast<const uint4*>(gbase + lo) : make_uint4(0, 0, 0, 0);
+            if constexpr (NT) {
+                v[q] = full ? nt_load16(gbase + lo) : make_uint4(0, 0, 0, 0);
+            } else {
+                v[q] = full ? *reinterpret_cast<const uint4*>(gbase + lo) : make_uint4(0, 0, 0, 0);
+            }
         }
 #pragma unroll
         for (int q = 0; q < BATCH; ++q) {

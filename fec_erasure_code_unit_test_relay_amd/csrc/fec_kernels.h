@@ -5,8 +5,9 @@
 //                          (replaces Encoder::encodeStream -> Encoder_Basic -> encodeBlock,
 //                          src/Encoder.cpp:65-98, src/Encoder_Basic.cpp:48-74,
 //                          src/codingOperations.cpp:131-147);
-//   fec_scan_kernel        finds the packets where the reference decoder leaves its fast path
-//                          and resynchronises (src/Decoder.cpp:80-83, 109-133);
+//   fec_episode_kernel     finds the packets where the reference decoder leaves its fast path
+//                          and resynchronises (src/Decoder.cpp:80-83, 109-133), the loss
+//                          episodes they start and their shapes (fec_shapes.hip);
 //   fec_plan_kernel        one wavefront per (erasure episode, diagonal block): symbolic replay of
 //                          the reference's per-symbol decode (decodeBlock / gf256_rref_matrix
 //                          through the precomputed decode rules), emitting for every erased
@@ -127,6 +128,7 @@ struct CopyFastArgs {
     int out_bytes;              // payload tile (16-aligned)
     uint64_t* stamps;           // diagnostics: per-workgroup phase timestamps (null = off)
     int skip_erased;            // 1: leave erased packets' rows and lengths to fec_recover_kernel
+    int nt;                     // 1: non-temporal codeword loads and payload stores
 };
 
 // Received-packet decode over contiguous per-workgroup tile runs (fec_copy_tile.hip).
@@ -185,50 +187,81 @@ struct PlanArgs {
     const uint8_t* gf;             // exp[512] then log[256]
     int ES;                        // decode-rule entry stride (bytes, multiple of 4)
     int k, n, T;
-    const int32_t* counters;       // [0] episodes, [3] episodes to replay
-    const int32_t* episodes;
-    const int32_t* work;           // indices (into episodes) of the episodes to replay
+    const int32_t* counters;       // [6] episodes to replay, [7] duplicate episodes
+    const int32_t* work;           // start packets of the episodes to replay
+    const int32_t* dups;           // duplicate episodes: (start packet, shape slot) pairs
+    const uint64_t* keys;          // shape of each slot
+    const int32_t* reps_tr;        // start packet of each slot's representative
+    int32_t* src_d;                // [P] erased output x uses the plan rows of x + src_d[x]
     const uint8_t* rstate;         // post-resync block state per phase (build_resync_states)
     int rs_bytes;
     uint8_t* sym_ok;               // [P][k]: symbol i of erased packet x recovered
     uint8_t* coef;                 // [P][k][n]: coefficients of symbol i over its diagonal
 };
 
-// Episode-shape deduplication (fec_shapes.hip).
-struct ShapeArgs {
+// Plan item d >= replay pairs: duplicate episode d's erased outputs point at the representative's
+// plan rows (one wave; a keyed shape spans < 64 packets).
+__device__ __forceinline__ void episode_dup_fill(const PlanArgs& a, int d, int lane) {
+    const int64_t tr = a.dups[2 * d];
+    const int slot = a.dups[2 * d + 1];
+    const uint64_t m = a.keys[slot];
+    const int64_t x = tr + lane;
+    if (((m >> lane) & 1u) && x < a.Pout) a.src_d[x] = a.reps_tr[slot] - static_cast<int32_t>(tr);
+}
+
+// Resync points, episodes and shapes in one pass (fec_shapes.hip).
+struct EpisodeArgs {
     const uint8_t* er;
-    int64_t P;
-    int T, k, n;
+    int64_t P, Pout;
+    int T;
     int tbits;                     // log2 of the hash-table size
     int dedup;                     // 0: every episode is replayed
-    int32_t* counters;             // [0] episodes (in), [3] replay count, [4] fill count (out)
-    const int32_t* episodes;
-    int32_t* ep_slot;              // [episodes] hash slot or -1
-    int32_t* ep_last;              // [episodes] latest erased packet
-    int32_t* work;                 // replay list
-    int32_t* fill;                 // fill list
+    int32_t* counters;             // [1] erased outputs, [6] replay count, [7] duplicates (one 64-bit word)
+    int32_t* erased;               // erased output packets
+    int32_t* src_d;                // [P]: 0 for every erased output (duplicates: set by the plan)
+    int32_t* work;                 // replay list (episode start packets)
+    int32_t* dups;                 // duplicate list ((start packet, slot) pairs)
     uint64_t* keys;                // [2^tbits], zero = empty
-    int32_t* reps;                 // [2^tbits] representative episode of the slot
-    uint8_t* sym_ok;
-    uint8_t* coef;
+    int32_t* reps_tr;              // [2^tbits] start packet of the slot's representative
+    uint64_t* stamps;              // diagnostics: per-workgroup phase timestamps (null = off)
 };
+__global__ void fec_episode_kernel(EpisodeArgs a);
+
+// Recovered packets -> rec_list (fec_compact_kernel).
+struct CompactArgs {
+    int32_t* counters;             // [1] erased outputs (in), [2] recovered packets (out)
+    const int32_t* erased;         // erased output packets (fec_episode_kernel)
+    const int32_t* src_d;          // plan rows of erased output x: those of x + src_d[x]
+    const uint8_t* sym_ok;         // [P][k] from the planner
+    int k;
+    int32_t* rec_list;             // (x, x + src_d[x]) pairs
+    int zero_lost;                 // 1: lost packets' rows (zeros) and lengths (0) written here
+    uint8_t* out;
+    int32_t* out_len;
+    int L;
+    int64_t row_off;               // packet x goes to output row x - row_off (x < row_off: skipped)
+};
+__global__ void fec_compact_kernel(CompactArgs a);
 
 struct RecArgs {
     const uint8_t* cw;
     int64_t P, Pout;
-    const int32_t* counters;       // [1] erased outputs, [2] recovered packets
-    const int32_t* rec_list;       // recovered packets (fec_compact_kernel)
-    const int32_t* erased;         // erased output packets (fec_scan_kernel)
-    const uint8_t* sym_ok;         // [P][k] from the planner
-    int zero_lost;                 // 1: also write lost packets' rows (zeros) and lengths (0)
+    const int32_t* counters;       // [2] recovered packets
+    const int32_t* rec_list;       // (x, plan-row packet) pairs (fec_compact_kernel)
     const uint8_t* coef;
     const uint8_t* gf;
     uint8_t* out;
     int32_t* out_len;
     int L, k, n, S, CW;
     int64_t row_off;               // packet x goes to output row x - row_off (x < row_off: skipped)
+    int stage_bytes;               // per-wave LDS for the k+n-1 codeword rows of a packet (0: none)
+    uint64_t* stamps;              // diagnostics: per-workgroup phase timestamps (null = off)
 };
-template <int MAXN>
+// dynamic LDS of fec_recover_kernel_t<MAXN, .>: tables + 4 waves x (coefficient logs + staged rows)
+inline int recover_lds_bytes(int maxn, int stage_bytes) {
+    return 1552 + 4 * (((2 * 16 * maxn + 15) & ~15) + stage_bytes);
+}
+template <int MAXN, bool STAGED>
 __global__ void fec_recover_kernel_t(RecArgs a);
 
 struct StreamOutArgs {
@@ -271,13 +304,7 @@ struct CodecView {
 __global__ void fec_block_decode_kernel(BlockArgs a);
 
 __global__ void fec_encode_kernel(EncArgs a);
-__global__ void fec_scan_kernel(const uint8_t* er, int64_t P, int64_t Pout, int T,
-                                int32_t* counters, int32_t* episodes, int32_t* erased);
-__global__ void fec_compact_kernel(int32_t* counters, const int32_t* erased, const uint8_t* sym_ok,
-                                   int k, int32_t* rec_list);
 __global__ void fec_plan_kernel(PlanArgs a);
-__global__ void fec_shape_kernel(ShapeArgs a);
-__global__ void fec_shape_fill_kernel(ShapeArgs a);
 __global__ void fec_copy_kernel(CopyArgs a);
 
 __global__ void fec_stream_out_kernel(StreamOutArgs a);

@@ -1,4 +1,5 @@
 // fec_kernels.hip -- see fec_kernels.h for the map from reference functions to kernels.
+#include "fec_device.h"
 #include "fec_kernels.h"
 
 namespace fec {
@@ -143,116 +144,8 @@ __global__ __launch_bounds__(256) void fec_encode_kernel(EncArgs a) {
     }
 }
 
-// ------------------------------------------------------------------------------------------
-// Decode, step 1: resynchronisation points and the list of erased packets.  The reference
-// decoder is in its fast path at a received packet t iff no packet of [t-T, t-1] was erased; at an
-// erased packet it resyncs iff it was in the fast path just before, i.e. no erasure in
-// [t-T-1, t-1] (Decoder.cpp:80-83, 109-133).  Every resync starts an independent episode.
-// ------------------------------------------------------------------------------------------
-namespace {
-__device__ __forceinline__ uint32_t nz_bytes_mask(uint32_t w) {  // bit e: byte e of w non-zero
-    return (((w & 0xffu) != 0) ? 1u : 0u) | (((w & 0xff00u) != 0) ? 2u : 0u) |
-           (((w & 0xff0000u) != 0) ? 4u : 0u) | (((w & 0xff000000u) != 0) ? 8u : 0u);
-}
-__device__ __forceinline__ int wave_incl_scan(int v, int lane) {
-    for (int o = 1; o < 64; o <<= 1) {
-        const int y = __shfl_up(v, o);
-        if (lane >= o) v += y;
-    }
-    return v;
-}
-}  // namespace
-
-// 16 packets per lane (one 16-byte load), 4096 per workgroup; both lists (erased outputs,
-// episode starts) get one atomic per workgroup.
-__global__ __launch_bounds__(256) void fec_scan_kernel(const uint8_t* er, int64_t P, int64_t Pout,
-                                                       int T, int32_t* counters, int32_t* episodes,
-                                                       int32_t* erased) {
-    __shared__ int wtot[2][4];
-    __shared__ int bbase[2];
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    constexpr int64_t kPerBlock = 256 * 16;
-    for (int64_t blk0 = static_cast<int64_t>(blockIdx.x) * kPerBlock; blk0 < P;
-         blk0 += static_cast<int64_t>(gridDim.x) * kPerBlock) {
-        const int64_t t0 = blk0 + tid * 16;
-        uint32_t m = 0;  // bit e: packet t0+e erased
-        if (t0 + 15 < P && (reinterpret_cast<uintptr_t>(er + t0) & 15) == 0) {
-            const uint4 v = *reinterpret_cast<const uint4*>(er + t0);
-            m = nz_bytes_mask(v.x) | (nz_bytes_mask(v.y) << 4) | (nz_bytes_mask(v.z) << 8) |
-                (nz_bytes_mask(v.w) << 12);
-        } else {
-            for (int e = 0; e < 16; ++e)
-                if (t0 + e < P && er[t0 + e]) m |= 1u << e;
-        }
-        uint32_t resm = 0;
-        for (uint32_t rest = m; rest; rest &= rest - 1) {
-            const int e = __builtin_ctz(rest);
-            const int64_t t = t0 + e;
-            // resync iff no erasure in [t-T-1, t-1] (Decoder.cpp:80-83, 109-133)
-            const int lo = e - T - 1;
-            uint32_t inside = m & ((1u << e) - 1u);
-            if (lo > 0) inside &= ~((1u << lo) - 1u);
-            bool rs = inside == 0;
-            if (rs && lo < 0)
-                for (int64_t u = t0 - 1; u >= 0 && u >= t - T - 1; --u)
-                    if (er[u]) {
-                        rs = false;
-                        break;
-                    }
-            if (rs) resm |= 1u << e;
-        }
-        uint32_t outm = m;
-        if (t0 + 16 > Pout) outm &= (t0 >= Pout) ? 0u : ((1u << (Pout - t0)) - 1u);
-        const int nout = __builtin_popcount(outm), nres = __builtin_popcount(resm);
-        const int io = wave_incl_scan(nout, lane), ir = wave_incl_scan(nres, lane);
-        if (lane == 63) {
-            wtot[0][wave] = io;
-            wtot[1][wave] = ir;
-        }
-        __syncthreads();
-        if (tid == 0) {
-            const int to = wtot[0][0] + wtot[0][1] + wtot[0][2] + wtot[0][3];
-            const int tr = wtot[1][0] + wtot[1][1] + wtot[1][2] + wtot[1][3];
-            bbase[0] = to ? atomicAdd(&counters[1], to) : 0;
-            bbase[1] = tr ? atomicAdd(&counters[0], tr) : 0;
-        }
-        __syncthreads();
-        int so = bbase[0] + io - nout, sr = bbase[1] + ir - nres;
-        for (int w = 0; w < wave; ++w) {
-            so += wtot[0][w];
-            sr += wtot[1][w];
-        }
-        for (uint32_t rest = outm; rest; rest &= rest - 1)
-            erased[so++] = static_cast<int32_t>(t0 + __builtin_ctz(rest));
-        for (uint32_t rest = resm; rest; rest &= rest - 1)
-            episodes[sr++] = static_cast<int32_t>(t0 + __builtin_ctz(rest));
-        __syncthreads();
-    }
-}
-
-// Packets whose k symbols were all recovered -> rec_list (one atomic per wave).
-__global__ __launch_bounds__(256) void fec_compact_kernel(int32_t* counters, const int32_t* erased,
-                                                          const uint8_t* sym_ok, int k,
-                                                          int32_t* rec_list) {
-    const int ner = counters[1];
-    const int lane = threadIdx.x & 63;
-    const int stride = gridDim.x * blockDim.x;
-    for (int idx = blockIdx.x * blockDim.x + threadIdx.x; idx - lane < ner; idx += stride) {
-        bool ok = false;
-        int64_t x = 0;
-        if (idx < ner) {
-            x = erased[idx];
-            ok = true;
-            for (int i = 0; i < k; ++i) ok = ok && sym_ok[x * k + i];
-        }
-        const unsigned long long bal = __ballot(ok);
-        if (!bal) continue;
-        int base = 0;
-        if (lane == 0) base = atomicAdd(&counters[2], __popcll(bal));
-        base = __shfl(base, 0);
-        if (ok) rec_list[base + __popcll(bal & ((1ull << lane) - 1ull))] = static_cast<int32_t>(x);
-    }
-}
+// Decode, step 1 (resync points, episodes, shapes, erased outputs): fec_episode_kernel,
+// fec_shapes.hip.
 
 // ------------------------------------------------------------------------------------------
 // Decode, step 2: symbolic replay.  The reference's decoder is S x n independent diagonal block
@@ -474,9 +367,14 @@ __global__ __launch_bounds__(64) void fec_plan_kernel(PlanArgs a) {
     br.T = T;
     for (int i = lane; i < 768; i += 64) smem[i] = a.gf[i];
     __syncthreads();
-    const int64_t pairs = static_cast<int64_t>(a.counters[3]) * n;
-    for (int64_t pr = blockIdx.x; pr < pairs; pr += gridDim.x) {
-        const int64_t tr = a.episodes[a.work[pr / n]];
+    const int64_t pairs = static_cast<int64_t>(a.counters[6]) * n;
+    const int64_t items = pairs + a.counters[7];
+    for (int64_t pr = blockIdx.x; pr < items; pr += gridDim.x) {
+        if (pr >= pairs) {
+            episode_dup_fill(a, static_cast<int>(pr - pairs), lane);
+            continue;
+        }
+        const int64_t tr = a.work[pr / n];
         const int b = static_cast<int>(pr % n);
         if (tr < 0 || tr >= a.P) continue;  // defensive: the scan only lists packets of the batch
         if (tr >= T) {
@@ -540,99 +438,182 @@ __global__ __launch_bounds__(64) void fec_plan_kernel(PlanArgs a) {
 // (Decoder_Basic.cpp:76-79); byte h (sub-stream s = h/k, position i = h%k) is then
 // XOR_q coef[x][i][q] * cw[x-i+q][s*n+q] over the received symbols q of its diagonal.
 // ------------------------------------------------------------------------------------------
-constexpr int kRecMaxK = 16;  // = kMaxK (fec_host.h)
-constexpr int kRecRounds = 5;  // 64-byte rounds per pass of fec_recover_kernel (L = 300: one pass)
-
-// kRecMaxN = 17 (codecs with a rule table, the common case) or 32 (n up to 31)
-template <int kRecMaxN>
-__global__ __launch_bounds__(256) void fec_recover_kernel_t(RecArgs a) {
-    // One wave per recovered packet (fec_compact_kernel's list), no workgroup barrier after the
-    // table load: lane h computes bytes h, h+64, ... of [len_hi, len_lo, payload]; its n sources
-    // are byte loads straight from the diagonal's rows (a ~(k+n)*CW-byte window, L2-resident), all
-    // issued before the lookups.
-    __shared__ uint8_t gexp[512];
-    __shared__ uint8_t glog[256];
-    __shared__ uint8_t lcf[4][kRecMaxK * kRecMaxN];  // per wave: coefficient logs, 255 = zero coefficient
-    const int tid = threadIdx.x;
-    for (int i = tid; i < 512; i += 256) gexp[i] = a.gf[i];
-    for (int i = tid; i < 256; i += 256) glog[i] = a.gf[512 + i];
-    __syncthreads();
-    const int lane = tid & 63, wl = tid >> 6;
-    const int L = a.L, k = a.k, n = a.n, CW = a.CW;
-    const int nrec = a.counters[2];
-    uint8_t* lc = lcf[wl];
-    const int waves = gridDim.x * 4;
-    if (a.zero_lost) {  // lost packets: payload 0 (FEC_Decoder returns no data), zero row
-        const int ner = a.counters[1];
-        for (int r = blockIdx.x * 4 + wl; r < ner; r += waves) {
-            const int64_t x = a.erased[r];
-            if (x < a.row_off) continue;
-            bool ok = true;
-            for (int i = 0; i < k; ++i) ok = ok && a.sym_ok[x * k + i];
-            if (ok) continue;
-            for (int b = lane; b < L; b += 64) a.out[(x - a.row_off) * L + b] = 0;
-            if (lane == 0) a.out_len[x - a.row_off] = 0;
+// Erased output packets whose k symbols are all recovered (their plan rows -- or their shape
+// representative's -- say so, Decoder_Basic.cpp:76-79) -> rec_list as (x, x + src_d[x]) pairs,
+// counted in counters[2]; the others are lost (zero_lost: their rows and lengths zeroed here).
+// Lane (j, i) = symbol i of entry j, J = 64 / k entries per wave and round, one append atomic
+// per wave and round.
+__global__ __launch_bounds__(256) void fec_compact_kernel(CompactArgs a) {
+    const int lane = threadIdx.x & 63, k = a.k;
+    const int ner = a.counters[1];
+    const int J = 64 / k;
+    const int jl = lane / k, il = lane - jl * k;
+    const int waves = gridDim.x * (blockDim.x >> 6);
+    for (int r0 = (blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) * J; r0 < ner; r0 += waves * J) {
+        const int r = r0 + jl;
+        const bool valid = jl < J && r < ner;
+        int x = 0, xr = 0;
+        bool bad = false;
+        if (valid) {
+            x = a.erased[r];
+            xr = x + a.src_d[x];
+            bad = !a.sym_ok[static_cast<int64_t>(xr) * k + il];
+        }
+        const uint64_t badm = __builtin_amdgcn_ballot_w64(bad);
+        // a group's verdict on its first lane: no bad lane in [l0, l0 + k)
+        const bool lead = valid && il == 0;
+        uint64_t gbad = 0;
+        for (int s = 0; s < k; ++s) gbad |= badm >> s;
+        const bool ok = lead && !((gbad >> lane) & 1u);
+        const uint64_t okm = __builtin_amdgcn_ballot_w64(ok);
+        if (okm) {
+            int base = 0;
+            if (lane == __builtin_ctzll(okm)) base = atomicAdd(&a.counters[2], __builtin_popcountll(okm));
+            base = __shfl(base, __builtin_ctzll(okm));
+            if (ok) {
+                const int at = base + __builtin_popcountll(okm & ((1ull << lane) - 1ull));
+                a.rec_list[2 * at] = x;
+                a.rec_list[2 * at + 1] = xr;
+            }
+        }
+        if (a.zero_lost) {
+            uint64_t lost = __builtin_amdgcn_ballot_w64(lead && !ok);
+            while (lost) {
+                const int l0 = __builtin_ctzll(lost);
+                lost &= lost - 1;
+                const int xl = __builtin_amdgcn_readlane(x, l0);
+                if (xl < a.row_off) continue;
+                for (int b = lane; b < a.L; b += 64) a.out[static_cast<int64_t>(xl - a.row_off) * a.L + b] = 0;
+                if (lane == 0) a.out_len[xl - a.row_off] = 0;
+            }
         }
     }
-    for (int r = blockIdx.x * 4 + wl; r < nrec; r += waves) {
-        const int64_t x = a.rec_list[r];
-        if (x < a.row_off) continue;  // before the caller's first output row (wave-uniform)
-        for (int i = lane; i < k * n; i += 64) {
-            const uint8_t c = a.coef[x * k * n + i];
-            lc[i] = c ? glog[c] : 255;
-        }
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        // kRecRounds rounds of 64 bytes per pass: every source byte of the pass is loaded before
-        // the first lookup, so the pass costs one memory round trip instead of one per round
-        const uint8_t* __restrict__ cwp = a.cw;
-        uint8_t* __restrict__ outp = a.out;
-        int ln = 0;
-        for (int h0 = 0; h0 < L + 2; h0 += 64 * kRecRounds) {
-            uint8_t v[kRecRounds][kRecMaxN];
-            int iw[kRecRounds];
+}
+
+constexpr int kRecMaxK = 16;      // = kMaxK (fec_host.h)
+constexpr int kRecLogZero = 512;  // log of 0: any sum with it indexes the zero tail of ex[]
+constexpr int kRecStageChunks = 12;  // 16-byte pieces per lane of a staged span (<= 12 KB)
+
+// One wave per erased output packet entry, 4 waves per workgroup, a grid of resident size: the
+// wave's entries r = w, w + waves, ... are checked J = 64 / k at a time (lane (j, i) = symbol i
+// of entry j: the dependent loads erased -> src_d -> sym_ok of all of them overlap), then the
+// recovered ones (their plan rows -- or their shape representative's -- say all k symbols are,
+// Decoder_Basic.cpp:76-79) are rebuilt one after the other:
+//   * the k x n coefficient rows go to LDS as logs (0 -> kRecLogZero);
+//   * STAGED: the k+n-1 codeword rows x-k+1 .. x+n-1 the diagonals of packet x touch are one
+//     contiguous span of the codeword buffer; it lands in the wave's LDS region with 16-byte
+//     loads issued together with the coefficient loads (one memory round trip), and every source
+//     byte is an LDS read; otherwise (large codewords) every source byte is a byte load;
+//   * lane h computes bytes h, h+64, ... of [len_hi, len_lo, payload]: sub-stream s = h / k,
+//     position i = h % k, XOR_q coef[i][q] * cw[x-i+q][s*n+q] over the received symbols q, as n
+//     independent branch-free terms ex[log coef + log byte] (a zero either way lands in the zero
+//     tail of ex).
+template <int MAXN, bool STAGED>
+__global__ __launch_bounds__(256) void fec_recover_kernel_t(RecArgs a) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t rsm[];
+    uint8_t* ex = rsm;                                        // 1040: 2^i, zero from 512
+    uint16_t* lg = reinterpret_cast<uint16_t*>(rsm + 1040);   // 256: log2 v, lg[0] = kRecLogZero
+    const int tid = threadIdx.x;
+    const int lane = tid & 63, wl = tid >> 6;
+    const int L = a.L, k = a.k, n = a.n, CW = a.CW;
+    constexpr int kLcBytes = (2 * kRecMaxK * MAXN + 15) & ~15;
+    uint16_t* lc = reinterpret_cast<uint16_t*>(rsm + 1552 + wl * (kLcBytes + a.stage_bytes));
+    uint8_t* rows = rsm + 1552 + wl * (kLcBytes + a.stage_bytes) + kLcBytes;
+    phase_stamp(a.stamps, blockIdx.x, 0);
+    for (int i = tid; i < 1040; i += 256) ex[i] = i < 512 ? a.gf[i] : 0;
+    for (int i = tid; i < 256; i += 256) lg[i] = i ? a.gf[512 + i] : static_cast<uint16_t>(kRecLogZero);
+    __syncthreads();
+    phase_stamp(a.stamps, blockIdx.x, 1);
+    const int nrec = a.counters[2];
+    const int waves = gridDim.x * 4;
+    const int64_t cw_total = a.P * CW;
+    {
+        for (int r = blockIdx.x * 4 + wl; r < nrec; r += waves) {
+            const int x = a.rec_list[2 * r], xr = a.rec_list[2 * r + 1];
+            if (x < a.row_off) continue;  // before the caller's first output row (wave-uniform)
+            uint8_t* orow = a.out + static_cast<int64_t>(x - a.row_off) * L;
+            // rows x-k+1 .. x+n-1 inside [0, P): bytes [s0, s1) of the codeword buffer
+            const int rlo = x - k + 1 > 0 ? x - k + 1 : 0;
+            const int64_t s0 = static_cast<int64_t>(rlo) * CW;
+            const int64_t s1 = static_cast<int64_t>(x + n < a.P ? x + n : a.P) * CW;
+            const int64_t a0 = s0 & ~int64_t(15);
+            uint4 piece[STAGED ? kRecStageChunks : 1];
+            const int nb = STAGED ? static_cast<int>((s1 - a0 + 15) >> 4) : 0;
+            if constexpr (STAGED) {
 #pragma unroll
-            for (int rr = 0; rr < kRecRounds; ++rr) {
-                const int h = h0 + 64 * rr + lane;
-                const int sidx = h / k, i = h - sidx * k;
-                iw[rr] = i;
-#pragma unroll
-                for (int q = 0; q < kRecMaxN; ++q) {
-                    v[rr][q] = 0;
-                    if (q < n && h < L + 2) {
-                        const int64_t row = x - i + q;
-                        if (lc[i * n + q] != 255 && row >= 0 && row < a.P) v[rr][q] = cwp[row * CW + sidx * n + q];
+                for (int j = 0; j < kRecStageChunks; ++j) {
+                    const int c = lane + 64 * j;
+                    const int64_t o = a0 + 16 * c;
+                    piece[j] = make_uint4(0u, 0u, 0u, 0u);
+                    if (c < nb) {
+                        if (o + 16 <= cw_total) {
+                            piece[j] = *reinterpret_cast<const uint4*>(a.cw + o);
+                        } else {  // the buffer's last piece
+                            uint32_t t[4] = {0u, 0u, 0u, 0u};
+                            for (int e = 0; e < 16; ++e)
+                                if (o + e < cw_total) t[e >> 2] |= static_cast<uint32_t>(a.cw[o + e]) << (8 * (e & 3));
+                            piece[j] = make_uint4(t[0], t[1], t[2], t[3]);
+                        }
                     }
                 }
             }
+            constexpr int kCf = (kRecMaxK * MAXN + 63) / 64;
+            uint32_t cf[kCf];
+            const uint8_t* cfp = a.coef + static_cast<int64_t>(xr) * k * n;
 #pragma unroll
-            for (int rr = 0; rr < kRecRounds; ++rr) {
-                const int h = h0 + 64 * rr + lane;
-                const int i = iw[rr];
-                uint8_t acc = 0;
+            for (int j = 0; j < kCf; ++j) cf[j] = lane + 64 * j < k * n ? cfp[lane + 64 * j] : 0u;
+            if constexpr (STAGED) {
 #pragma unroll
-                for (int q = 0; q < kRecMaxN; ++q) {
-                    if (q < n && v[rr][q]) {
-                        const int lq = lc[i * n + q];
-                        if (lq != 255) acc ^= gexp[lq + glog[v[rr][q]]];
+                for (int j = 0; j < kRecStageChunks; ++j)
+                    if (lane + 64 * j < nb) *reinterpret_cast<uint4*>(rows + 16 * (lane + 64 * j)) = piece[j];
+            }
+#pragma unroll
+            for (int j = 0; j < kCf; ++j)
+                if (lane + 64 * j < k * n) lc[lane + 64 * j] = lg[cf[j]];
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            int ln = 0;
+            for (int h0 = 0; h0 < L + 2; h0 += 64) {
+                const int h = h0 + lane;
+                const int sidx = h / k, i = h - sidx * k;
+                // term q is row x-i+q: inside [0, P) for q in [qlo, qhi)
+                const int qlo = i - x > 0 ? i - x : 0;
+                const int qhi = h < L + 2 ? min(n, static_cast<int>(a.P - x) + i) : 0;
+                // staged: byte (row, s*n+q) sits at base + q*(CW+1) of the span
+                const int base = (x - i - rlo) * CW + static_cast<int>(s0 - a0) + sidx * n;
+                uint32_t lq[MAXN], v[MAXN];
+#pragma unroll
+                for (int q = 0; q < MAXN; ++q) {
+                    const bool use = q >= qlo && q < qhi;
+                    lq[q] = lc[i * n + (q < n ? q : 0)];
+                    if constexpr (STAGED) {
+                        v[q] = use ? rows[base + q * (CW + 1)] : 0u;
+                    } else {
+                        v[q] = use ? a.cw[static_cast<int64_t>(x - i + q) * CW + sidx * n + q] : 0u;
                     }
                 }
-                if (h0 == 0 && rr == 0) {  // recovered length (Decoder.cpp:141-149): bytes 0, 1, clamped to L
+                uint32_t acc = 0;
+#pragma unroll
+                for (int q = 0; q < MAXN; ++q) acc ^= ex[lq[q] + lg[v[q]]];
+                if (h0 == 0) {  // recovered length (Decoder.cpp:141-149): bytes 0, 1, clamped to L
                     const int hi = __builtin_amdgcn_readlane(static_cast<int>(acc), 0);
                     const int lo = __builtin_amdgcn_readlane(static_cast<int>(acc), 1);
                     ln = min(hi * 256 + lo, L);
                 }
                 const int b = h - 2;
-                if (b >= 0 && b < L) outp[(x - a.row_off) * L + b] = b < ln ? acc : 0;
+                if (b >= 0 && b < L) orow[b] = b < ln ? static_cast<uint8_t>(acc) : 0;
             }
+            if (lane == 0) a.out_len[x - a.row_off] = ln;
+            __builtin_amdgcn_wave_barrier();  // lc and rows are rewritten by the next packet
         }
-        if (lane == 0) a.out_len[x - a.row_off] = ln;
-        __builtin_amdgcn_wave_barrier();  // lc is rewritten by the next packet
     }
+    phase_stamp(a.stamps, blockIdx.x, 2);  // wave 0 done
 }
 
-template __global__ void fec_recover_kernel_t<17>(RecArgs);
-template __global__ void fec_recover_kernel_t<32>(RecArgs);
+template __global__ void fec_recover_kernel_t<17, true>(RecArgs);
+template __global__ void fec_recover_kernel_t<17, false>(RecArgs);
+template __global__ void fec_recover_kernel_t<32, false>(RecArgs);
 
 // ------------------------------------------------------------------------------------------
 // Decode, step 3: every received packet's systematic bytes (fast path Decoder.cpp:77-108; the

@@ -29,6 +29,9 @@ struct RegReplay {
     const int64_t* wbase;
     int ES, T, lane;
     uint32_t er;                 // erased positions (uniform)
+    uint32_t memo_key = ~0u;     // (w << 26 | m) of the last rule loaded (uniform)
+    bool memo_none = false;      // ... and it recovered nothing
+    uint32_t memo_ev = 0;        // ... its entry, one dword per lane
     uint32_t cw[N];              // lane q: cwc[p][q]
     uint32_t dat[K];             // lane q: datc[i][q]
 
@@ -42,9 +45,19 @@ struct RegReplay {
         const uint32_t full = (1u << w) - 1u;
         const uint32_t m = er & full;
         if (m == full || !(m & ((1u << K) - 1u))) return;
-        // entry {sel[K], logcol[K][N]} (K*(N+1) <= 256 bytes for every instantiation)
-        const uint32_t* ent = reinterpret_cast<const uint32_t*>(rules + wbase[w] + static_cast<int64_t>(m) * ES);
-        const uint32_t ev = (lane < (ES >> 2)) ? ent[lane] : 0u;
+        // The outcome (which symbols come back) is a function of (w, m) alone: a rule that
+        // recovered nothing at (w, m) recovers nothing until the mask changes, and the entry of
+        // the last (w, m) is still in ev.  Within a round the k blocks' decodes mostly see one mask,
+        // so this saves most of the dependent rule loads of the serial replay.
+        const uint32_t key = (static_cast<uint32_t>(w) << 26) | m;
+        if (key == memo_key && memo_none) return;
+        if (key != memo_key) {
+            // entry {sel[K], logcol[K][N]} (K*(N+1) <= 256 bytes for every instantiation)
+            const uint32_t* ent = reinterpret_cast<const uint32_t*>(rules + wbase[w] + static_cast<int64_t>(m) * ES);
+            memo_ev = (lane < (ES >> 2)) ? ent[lane] : 0u;
+            memo_key = key;
+        }
+        const uint32_t ev = memo_ev;
         uint32_t lv[N];
 #pragma unroll
         for (int c = 0; c < N; ++c) lv[c] = lg[cw[c]];
@@ -68,6 +81,7 @@ struct RegReplay {
             fresh[i] = acc;
             got |= 1u << i;
         }
+        memo_none = got == 0;
         if (!got) return;
 #pragma unroll
         for (int i = 0; i < K; ++i)
@@ -146,11 +160,16 @@ __global__ __launch_bounds__(64) void fec_plan_fast_kernel(PlanArgs a) {
     br.T = T;
     br.lane = lane;
     const int Pi = static_cast<int>(a.P), Pouti = static_cast<int>(a.Pout);  // P < 2^31 (host check)
-    const int pairs = a.counters[3] * N;
-    for (int pr = blockIdx.x; pr < pairs; pr += gridDim.x) {
+    const int pairs = a.counters[6] * N;
+    const int items = pairs + a.counters[7];
+    for (int pr = blockIdx.x; pr < items; pr += gridDim.x) {
+        if (pr >= pairs) {
+            episode_dup_fill(a, pr - pairs, lane);
+            continue;
+        }
         const int ep = pr / N;
         const int b = pr - ep * N;
-        const int tr = a.episodes[a.work[ep]];
+        const int tr = a.work[ep];
         if (tr < 0 || tr >= Pi) continue;
         if (tr >= T) {
             // resync at tr (Decoder.cpp:111-133) from the initial state, precomputed per phase

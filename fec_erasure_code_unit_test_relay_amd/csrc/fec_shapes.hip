@@ -1,39 +1,40 @@
-// fec_shapes.hip -- loss-episode deduplication for the decode planner.
+// fec_shapes.hip -- the decode planner's first launch: resync points, loss episodes and their
+// shapes, erased outputs, in one pass over the erasure flags.
 //
 // An episode starts at an erased packet tr with no erasure in [tr-T-1, tr-1] (the decoder's
 // resynchronisation, Decoder.cpp:109-133) and ends at the first received packet t with no erasure
 // in [t-T, t-1] (Decoder.cpp:80-83): packet latest+T+1 ends it only if it is received, an
-// erasure there continues the episode.  Everything the planner derives for the episode's
-// erased packets -- which symbols are recovered and their coefficient rows -- is a function of
-// the block states at tr and of the erasure flags inside the episode.  For tr >= T the block
-// state at tr is the post-resync state of the block's phase, and the phase of the block holding
-// symbol i of packet x is (tr - x + i) mod n: the results depend on x - tr, not on tr.  Two
-// episodes with the same erasure shape (bit j = packet tr+j erased) therefore have identical
-// results at equal offsets.
+// erasure there continues the episode.  Every erased packet lies in exactly one episode.
+// Everything the planner derives for the episode's erased packets -- which symbols are recovered
+// and their coefficient rows -- is a function of the block states at tr and of the erasure flags
+// inside the episode.  For tr >= T the block state at tr is the post-resync state of the block's
+// phase, and the phase of the block holding symbol i of packet x is (tr - x + i) mod n: the
+// results depend on x - tr, not on tr.  Two episodes with the same erasure shape (bit j = packet
+// tr+j erased) therefore have identical results at equal offsets.
 //
-// Per batch (the table is cleared by every plan launch; nothing is carried between batches):
-//   fec_shape_kernel      one thread per episode: the shape (64-bit mask), hash-table insert;
-//                         the first episode of a shape and every episode that cannot be keyed
-//                         (startup tr < T, span >= 64, or running into the batch end) go to the
-//                         replay work list, the others to the fill list;
-//   (fec_plan_kernel / fec_plan_fast_kernel replay the work list)
-//   fec_shape_fill_kernel one wave per filled episode: sym_ok and coef rows of each erased
-//                         packet copied from the representative's packet at the same offset.
+// fec_episode_kernel (64 packets per lane, 4096 per wave):
+//   * erased output packets -> `erased` (one atomic per wave), src_d[x] = 0;
+//   * each resync point tr found by a thread: the thread walks the episode (flags in 64-packet
+//     windows) to its shape and last erasure, and inserts keyable shapes (tr >= T, span < 64, not
+//     running into the batch end) into the hash table `keys` (relaxed load first, CAS on a miss);
+//     the winner of a shape records its tr in reps_tr and goes to the replay list `work` with every
+//     unkeyed episode; the others go to `dups` as (tr, slot).
+// The plan kernels (fec_plan_fast.hip / fec_kernels.hip) replay `work` and, for each entry of
+// `dups`, point src_d of its erased packets at the representative's (x + reps_tr - tr): the
+// recovery reads the representative's rows there, so nothing is copied.
+#include "fec_device.h"
 #include "fec_kernels.h"
 
 namespace fec {
 
 namespace {
 
-constexpr int kLocalSlots = 512;  // per-workgroup table (256 episodes per pass)
-
 __device__ __forceinline__ uint32_t shape_hash(uint64_t m, int bits) {
     return static_cast<uint32_t>((m * 0x9E3779B97F4A7C15ull) >> (64 - bits));
 }
 
 // Erasure flags of packets t0 .. t0+63 as bits (bit j = packet t0+j erased; past P: 0).  Nine
-// aligned 8-byte loads instead of 64 byte loads: one thread walks one episode, so these loads
-// are scattered, and their number is what the planner pays beside the copy kernel.
+// aligned 8-byte loads instead of 64 byte loads.
 __device__ __forceinline__ uint64_t erasure_bits64(const uint8_t* er, int64_t P, int64_t t0) {
     uint64_t fl = 0;
     const uintptr_t ad = reinterpret_cast<uintptr_t>(er + t0);
@@ -54,147 +55,188 @@ __device__ __forceinline__ uint64_t erasure_bits64(const uint8_t* er, int64_t P,
     } else {
         for (int j = 0; j < 64; ++j) {
             const int64_t t = t0 + j;
-            if (t < P && er[t]) fl |= uint64_t(1) << j;
+            if (t >= 0 && t < P && er[t]) fl |= uint64_t(1) << j;
         }
     }
     return fl;
 }
 
-// Wave-aggregated append of `item` for the lanes where `want` holds.
-__device__ __forceinline__ void wave_append(bool want, int32_t* counter, int32_t* list, int item) {
-    const uint64_t bal = __ballot(want);
-    if (!bal) return;
+__device__ __forceinline__ uint32_t nz_bytes_mask(uint32_t w) {  // bit e: byte e of w non-zero
+    return (((w & 0xffu) != 0) ? 1u : 0u) | (((w & 0xff00u) != 0) ? 2u : 0u) |
+           (((w & 0xff0000u) != 0) ? 4u : 0u) | (((w & 0xff000000u) != 0) ? 8u : 0u);
+}
+
+__device__ __forceinline__ int wave_incl_scan(int v, int lane) {
+    for (int o = 1; o < 64; o <<= 1) {
+        const int y = __shfl_up(v, o);
+        if (lane >= o) v += y;
+    }
+    return v;
+}
+
+// Wave-aggregated append of `n` items for the lanes where n > 0; returns the lane's first index.
+__device__ __forceinline__ int wave_reserve(int n, int32_t* counter) {
     const int lane = threadIdx.x & 63;
-    const int leader = __builtin_ctzll(bal);
+    const int incl = wave_incl_scan(n, lane);
+    const int tot = __shfl(incl, 63);
+    if (tot == 0) return 0;
     int base = 0;
-    if (lane == leader) base = atomicAdd(counter, __popcll(bal));
-    base = __shfl(base, leader);
-    if (want) list[base + __popcll(bal & ((uint64_t(1) << lane) - 1))] = item;
+    if (lane == 63) base = atomicAdd(counter, tot);
+    base = __shfl(base, 63);
+    return base + incl - n;
 }
 
 }  // namespace
 
-// One thread per episode.  Shapes are first deduplicated in a workgroup-local LDS table; only
-// the local representative of a shape touches the global table (one CAS per shape per
-// workgroup), so hot shapes do not serialise on one address.
-__global__ __launch_bounds__(256) void fec_shape_kernel(ShapeArgs a) {
-    __shared__ unsigned long long lkey[kLocalSlots];
-    __shared__ int32_t lslot[kLocalSlots];   // global slot of the local shape
-    __shared__ int32_t lrep[kLocalSlots];    // 1: the local representative won the global slot
-    const int tid = threadIdx.x;
-    const int ne = a.counters[0];
+// One wave per workgroup, 64 packets per lane, 4096 per wave and pass.  Device-scope atomics are
+// performed beyond the XCDs' L2s and serialise per address, so a wave issues few of them: one for
+// its erased outputs, one 64-bit one per round for its replay and duplicate entries; the shape
+// table is probed with plain loads (a key never changes once set, so a stale line can only read
+// as empty, and the CAS that follows returns the real key) by one lane per distinct shape of the
+// wave.
+__global__ __launch_bounds__(64) void fec_episode_kernel(EpisodeArgs a) {
+    const int lane = threadIdx.x;
+    const int T = a.T;  // < 64 (host check): the look-back of a resync test fits one word
     const int64_t TS = int64_t(1) << a.tbits;
-    for (int e0 = blockIdx.x * 256; e0 < ne; e0 += gridDim.x * 256) {
-        for (int i = tid; i < kLocalSlots; i += 256) lkey[i] = 0ull;
-        const int e = e0 + tid;
-        const bool valid = e < ne;
-        int64_t tr = 0, last = 0;
-        uint64_t m = 1;
-        bool keyed = false;
-        if (valid) {
-            tr = a.episodes[e];
-            // walk the episode: positions relative to tr, flags in windows of 64
-            int latest = 0;
-            bool big = false, done = false, truncated = false;
-            for (int base = 1; !done; base += 64) {
-                uint64_t fl = erasure_bits64(a.er, a.P, tr + base);
-                while (fl) {
-                    const int j = __builtin_ctzll(fl);
-                    fl &= fl - 1;
-                    const int pos = base + j;
-                    if (pos - latest > a.T + 1) {  // packet latest+T+1 was received: ended
+    constexpr int64_t kPerWave = 64 * 64;
+    unsigned long long* wd = reinterpret_cast<unsigned long long*>(a.counters + 6);  // (replayed, dups)
+    phase_stamp(a.stamps, blockIdx.x, 0);
+    for (int64_t w0 = static_cast<int64_t>(blockIdx.x) * kPerWave; w0 < a.P;
+         w0 += static_cast<int64_t>(gridDim.x) * kPerWave) {
+        const int64_t t0 = w0 + lane * 64;
+        uint64_t m64 = 0;  // bit e: packet t0+e erased
+        if (t0 + 63 < a.P && (reinterpret_cast<uintptr_t>(a.er + t0) & 15) == 0) {
+            const uint4* p = reinterpret_cast<const uint4*>(a.er + t0);
+            uint4 v[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) v[j] = p[j];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const uint64_t m16 = nz_bytes_mask(v[j].x) | (nz_bytes_mask(v[j].y) << 4) |
+                                     (nz_bytes_mask(v[j].z) << 8) | (nz_bytes_mask(v[j].w) << 12);
+                m64 |= m16 << (16 * j);
+            }
+        } else {
+            m64 = erasure_bits64(a.er, a.P, t0);
+        }
+        // resync points: erased t with no erasure in [t-T-1, t-1] (Decoder.cpp:80-83, 109-133)
+        uint64_t resm = 0;
+        if (m64) {
+            const uint64_t before = __shfl_up(m64, 1);  // packets t0-64 .. t0-1 (lane 0: below)
+            const uint64_t bw = lane == 0 ? erasure_bits64(a.er, a.P, t0 - 64) : before;
+            for (uint64_t rest = m64; rest; rest &= rest - 1) {
+                const int e = __builtin_ctzll(rest);
+                const int lo = e - T - 1;
+                uint64_t inside = m64 & ((uint64_t(1) << e) - 1u);
+                if (lo > 0) inside &= ~((uint64_t(1) << lo) - 1u);
+                const bool rs = inside == 0 && (lo >= 0 || (bw >> (64 + lo)) == 0);
+                if (rs) resm |= uint64_t(1) << e;
+            }
+        }
+        phase_stamp(a.stamps, blockIdx.x, 1);
+        // erased outputs (src_d: own plan rows until the plan says otherwise)
+        uint64_t outm = m64;
+        if (t0 + 64 > a.Pout) outm &= (t0 >= a.Pout) ? 0u : ((uint64_t(1) << (a.Pout - t0)) - 1u);
+        int so = wave_reserve(__builtin_popcountll(outm), &a.counters[1]);
+        for (uint64_t rest = outm; rest; rest &= rest - 1) {
+            const int64_t x = t0 + __builtin_ctzll(rest);
+            a.erased[so++] = static_cast<int32_t>(x);
+            a.src_d[x] = 0;
+        }
+        phase_stamp(a.stamps, blockIdx.x, 2);
+
+        // episodes of this lane, one per round (wave-uniform loop)
+        uint64_t rest = resm;
+        while (__builtin_amdgcn_ballot_w64(rest != 0)) {
+            const bool have = rest != 0;
+            int64_t tr = 0;
+            uint64_t m = 1;
+            bool keyed = false;
+            if (have) {
+                tr = t0 + __builtin_ctzll(rest);
+                rest &= rest - 1;
+                // walk the episode: positions relative to tr, flags in windows of 64
+                int latest = 0;
+                bool big = false, done = false, truncated = false;
+                for (int base = 1; !done; base += 64) {
+                    uint64_t fl = erasure_bits64(a.er, a.P, tr + base);
+                    while (fl) {
+                        const int j = __builtin_ctzll(fl);
+                        fl &= fl - 1;
+                        const int pos = base + j;
+                        if (pos - latest > T + 1) {  // packet latest+T+1 was received: ended
+                            done = true;
+                            break;
+                        }
+                        latest = pos;
+                        if (pos < 64) m |= uint64_t(1) << pos;
+                        else big = true;
+                    }
+                    if (!done && latest + T + 1 <= base + 63) done = true;  // latest+T+1 seen, received
+                    if (!done && tr + base + 64 >= a.P) {
                         done = true;
+                        truncated = true;
+                    }
+                }
+                keyed = a.dedup && tr >= T && !big && !truncated && tr + latest + T + 1 < a.P;
+            }
+            // one lane per distinct shape of the wave probes the table
+            int leader = lane;
+            {
+                uint64_t pend = __builtin_amdgcn_ballot_w64(keyed);
+                while (pend) {
+                    const int l = __builtin_ctzll(pend);
+                    const uint64_t ml = (static_cast<uint64_t>(static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(m >> 32), l))) << 32) |
+                                        static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(m), l));
+                    const uint64_t grp = __builtin_amdgcn_ballot_w64(keyed && m == ml);
+                    if ((grp >> lane) & 1u) leader = l;
+                    pend &= ~grp;
+                }
+            }
+            int32_t slot = -1;
+            bool won = false;
+            if (keyed && leader == lane) {
+                int64_t h = shape_hash(m, a.tbits);
+                for (int64_t probe = 0; probe < TS; ++probe) {  // the table has > 2x slots: ends
+                    unsigned long long cur = *reinterpret_cast<volatile unsigned long long*>(a.keys + h);
+                    if (cur == 0ull)
+                        cur = atomicCAS(reinterpret_cast<unsigned long long*>(a.keys + h), 0ull,
+                                        static_cast<unsigned long long>(m));
+                    if (cur == 0ull) {
+                        a.reps_tr[h] = static_cast<int32_t>(tr);
+                        slot = static_cast<int32_t>(h);
+                        won = true;
                         break;
                     }
-                    latest = pos;
-                    if (pos < 64) m |= uint64_t(1) << pos;
-                    else big = true;
-                }
-                if (!done && latest + a.T + 1 <= base + 63) done = true;  // latest+T+1 seen, received
-                if (!done && tr + base + 64 >= a.P) {
-                    done = true;
-                    truncated = true;
+                    if (cur == m) {
+                        slot = static_cast<int32_t>(h);
+                        break;
+                    }
+                    h = (h + 1) & (TS - 1);
                 }
             }
-            last = tr + latest;
-            a.ep_last[e] = static_cast<int32_t>(last);
-            keyed = a.dedup && tr >= a.T && !big && !truncated && last + a.T + 1 < a.P;
-        }
-        __syncthreads();
-        // local insert: the first thread of a shape in this workgroup is its local representative
-        int ls = -1;
-        bool lfirst = false;
-        if (keyed) {
-            uint32_t h = shape_hash(m, 9);
-            for (int probe = 0; probe < kLocalSlots; ++probe) {
-                const unsigned long long prev = atomicCAS(&lkey[h], 0ull, static_cast<unsigned long long>(m));
-                if (prev == 0ull || prev == m) {
-                    ls = static_cast<int>(h);
-                    lfirst = prev == 0ull;
-                    break;
-                }
-                h = (h + 1) & (kLocalSlots - 1);
+            const int gslot = __shfl(slot, leader);
+            const bool gwon = __shfl(won ? 1 : 0, leader) != 0;
+            // the representative replays (and every unkeyed episode); the rest reuse its rows
+            const bool rep = have && (!keyed || (leader == lane && gwon));
+            const bool dup = have && !rep;
+            if (keyed) slot = gslot;
+            // one 64-bit atomic reserves the wave's replay (low half) and duplicate (high) entries
+            const int ir = wave_incl_scan(rep ? 1 : 0, lane), id = wave_incl_scan(dup ? 1 : 0, lane);
+            const int nr = __shfl(ir, 63), nd = __shfl(id, 63);
+            unsigned long long base = 0;
+            if (lane == 63 && (nr | nd))
+                base = atomicAdd(wd, (static_cast<unsigned long long>(nd) << 32) | static_cast<unsigned>(nr));
+            base = __shfl(base, 63);
+            if (rep) a.work[static_cast<int>(base & 0xffffffffu) + ir - 1] = static_cast<int32_t>(tr);
+            if (dup) {
+                const int di = static_cast<int>(base >> 32) + id - 1;
+                a.dups[2 * di] = static_cast<int32_t>(tr);
+                a.dups[2 * di + 1] = slot;
             }
-        }
-        // global insert by the local representatives
-        if (lfirst) {
-            int64_t h = shape_hash(m, a.tbits);
-            int32_t gs = -1, won = 0;
-            for (int64_t probe = 0; probe < TS; ++probe) {  // the table has > 2x slots: ends
-                unsigned long long cur = __hip_atomic_load(reinterpret_cast<unsigned long long*>(a.keys + h),
-                                                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                if (cur == 0ull)
-                    cur = atomicCAS(reinterpret_cast<unsigned long long*>(a.keys + h), 0ull,
-                                    static_cast<unsigned long long>(m));
-                if (cur == 0ull) {
-                    a.reps[h] = e;
-                    gs = static_cast<int32_t>(h);
-                    won = 1;
-                    break;
-                }
-                if (cur == m) {
-                    gs = static_cast<int32_t>(h);
-                    break;
-                }
-                h = (h + 1) & (TS - 1);
-            }
-            lslot[ls] = gs;
-            lrep[ls] = won;
-        }
-        __syncthreads();
-        int32_t gslot = -1;
-        bool rep = valid;
-        if (keyed && ls >= 0) {
-            gslot = lslot[ls];
-            rep = lfirst && lrep[ls];
-        }
-        if (valid) a.ep_slot[e] = gslot;
-        wave_append(valid && rep, &a.counters[3], a.work, e);
-        wave_append(valid && !rep, &a.counters[4], a.fill, e);
-        __syncthreads();  // lkey is cleared for the next pass
-    }
-}
-
-__global__ __launch_bounds__(64) void fec_shape_fill_kernel(ShapeArgs a) {
-    const int lane = threadIdx.x;
-    const int nf = a.counters[4];
-    const int k = a.k, kn = a.k * a.n;
-    for (int f = blockIdx.x; f < nf; f += gridDim.x) {
-        const int e = a.fill[f];
-        const int rep = a.reps[a.ep_slot[e]];
-        const int64_t tr = a.episodes[e];
-        const int64_t d = static_cast<int64_t>(a.episodes[rep]) - tr;
-        const int64_t last = a.ep_last[e];  // last - tr < 64 for a keyed episode
-        const int64_t xl = tr + lane;
-        uint64_t bits = __ballot(xl <= last && a.er[xl] != 0);
-        while (bits) {
-            const int j = __builtin_ctzll(bits);
-            bits &= bits - 1;
-            const int64_t x = tr + j, xr = x + d;
-            for (int o = lane; o < kn; o += 64) a.coef[x * kn + o] = a.coef[xr * kn + o];
-            if (lane < k) a.sym_ok[x * k + lane] = a.sym_ok[xr * k + lane];
         }
     }
+    phase_stamp(a.stamps, blockIdx.x, 3);
 }
 
 }  // namespace fec
