@@ -267,48 +267,21 @@ int codec_init(fec_codec* c, int max_payload, int T, int B, int N) {
         if (!c->wave_cus) c->wave_cus = cus;
     }
     if ((g.L & 3) == 0 && g.n - g.k >= 0) {
-        // tile encode: a wave slice holds whole packets (PPW * NS4 <= 64) whose codewords end on a
-        // dword (PPW * CW % 4 == 0), and a tile (4 * PPW packets) covers the n-1 packets of parity
-        // history, so that the parity rows move down by one tile
-        const int ns4 = c->ns4();
-        const int unit = (g.CW & 3) == 0 ? 1 : ((g.CW & 1) == 0 ? 2 : 4);
-        int ppw = ns4 > 0 ? (64 / ns4) / unit * unit : 0;
-        if (ppw > 0 && 4 * ppw >= g.n - 1) c->tile_kernel = fec::fec_encode_tile_kernel_for(g.k, g.n - g.k);
+        const fec::TileGeom tg = fec::tile_geometry(g.k, g.n - g.k, g.L);
+        if (tg.ok) c->tile_kernel = fec::fec_encode_tile_kernel_for(g.k, g.n - g.k, g.L);
         if (c->tile_kernel) {
-            const int R = 4 * ppw;
-            const int rs = (g.L + 15) & ~15;  // LDS row stride of the input tile
-            const int ngl = (R * rs + 16 + 4095) / 4096;
-            const int pws = g.k | 1;
-            const int rows = R + g.n - 1;
-            const int npa = std::max(1, g.n - g.k);
-            auto al16 = [](int x) { return (x + 15) & ~15; };
-            int off = 64;  // guard in front of the input buffers (the first row's dword -1)
-            const int in_bytes = ngl * 4096;
-            const int off_in = off;
-            off += 2 * in_bytes;
-            // the position words (read before the second barrier of a tile) and the output tile
-            // (written after it) share one region
-            const int off_pw = off;
-            const int off_out = off;
-            off = al16(off + std::max(4 * R * ns4 * pws, R * g.CW));
-            const int off_q = off;
-            off = al16(off + 4 * npa * rows * ns4);
-            const int off_scratch = off;
-            off += 1024;
-            c->tile_off[8] = off_scratch;
-            if (ngl > 4) c->tile_kernel = nullptr;
-            c->tile_lds = off;
-            c->tile_lds_len = off + 2048;
-            c->tile_ppw = ppw;
-            c->tile_off[0] = off_in;
-            c->tile_off[1] = in_bytes;
-            c->tile_off[2] = off_pw;
-            c->tile_off[3] = off_q;
-            c->tile_off[4] = off_out;
-            c->tile_off[5] = off;  // lengths (only with a length array)
-            c->tile_off[6] = ngl;
-            c->tile_off[7] = (R * g.CW / 16 + 255) / 256;
-            if (c->tile_lds_len > 160 * 1024) c->tile_kernel = nullptr;
+            c->tile_lds = tg.lds;
+            c->tile_lds_len = tg.lds_len;
+            c->tile_ppw = tg.PPW;
+            c->tile_off[0] = tg.off_in;
+            c->tile_off[1] = tg.in_bytes;
+            c->tile_off[2] = tg.off_pw;
+            c->tile_off[3] = tg.off_q;
+            c->tile_off[4] = tg.off_out;
+            c->tile_off[5] = tg.off_len;
+            c->tile_off[6] = tg.ngl;
+            c->tile_off[7] = tg.nso;
+            c->tile_off[8] = tg.off_scratch;
         }
         if (c->tile_kernel) {
             HIP_TRY(hipFuncSetAttribute(c->tile_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, c->tile_lds_len));
@@ -1293,7 +1266,8 @@ int fec_codec_info(const fec_codec* c, char* buf, size_t size) {
     char enc[64];
     const int np = c->g.n - c->g.k;
     if (c->tile_kernel && (c->encode_path == 0 || c->encode_path == 5))
-        std::snprintf(enc, sizeof(enc), "fec_encode_tile_kernel<%d, %d>", c->g.k, np);
+        std::snprintf(enc, sizeof(enc), "fec_encode_tile_kernel<%d, %d, %d>", c->g.k, np,
+                      c->tile_kernel == fec::fec_encode_tile_kernel_for(c->g.k, np, 0) ? 0 : c->g.L);
     else if (c->wave_kernel && (c->encode_path == 0 || c->encode_path == 4))
         std::snprintf(enc, sizeof(enc), "fec_encode_wave_kernel<%d, %d>", c->g.k, np);
     else if (c->persist_kernel && (c->encode_path == 0 || c->encode_path == 3))

@@ -31,6 +31,7 @@
 #include "fec_device.h"
 #include "fec_kernels.h"
 
+#include <cstdlib>
 #include <utility>
 
 namespace fec {
@@ -175,9 +176,13 @@ __device__ __forceinline__ uint32_t ttail_rem(const uint32_t (&X)[n]) {
     }
 }
 
-template <int K, int NP, int W>
+// LC > 0: L (and every size derived from it) fixed at compile time; LC = 0: from the arguments.
+template <int K, int NP, int W, int LC>
 __device__ __forceinline__ void tile_walk(const EncTileArgs& a, uint8_t* smem) {
     constexpr int n = K + NP;
+    constexpr TileGeom CG = tile_geometry(K, NP, LC > 0 ? LC : 300);
+    constexpr bool CL = LC > 0;
+    static_assert(!CL || CG.ok, "no tile geometry for this (k, n-k, L)");
     constexpr int NPA = NP > 0 ? NP : 1;
     constexpr int KNP = K * NP;
     constexpr int k0 = W * KNP / 4, k1 = (W + 1) * KNP / 4;  // this wave's (i, jj) products
@@ -189,7 +194,14 @@ __device__ __forceinline__ void tile_walk(const EncTileArgs& a, uint8_t* smem) {
 
     const int lane = threadIdx.x & 63;
     const int tid = threadIdx.x;
-    const int L = a.L, CW = a.CW, NS4 = a.NS4, PPW = a.PPW, R = 4 * a.PPW, P = a.P;
+    const int L = CL ? LC : a.L, CW = CL ? CG.CW : a.CW, NS4 = CL ? CG.NS4 : a.NS4;
+    const int PPW = CL ? CG.PPW : a.PPW, R = 4 * PPW, P = a.P;
+    const int dbg = CL ? 0 : a.dbg;  // timing experiments: the runtime-L kernel only
+    const int nvl = CL ? CG.nvl : a.nvl, rem = CL ? CG.rem : a.rem;
+    const int off_in = CL ? CG.off_in : a.off_in, in_bytes = CL ? CG.in_bytes : a.in_bytes;
+    const int off_pw = CL ? CG.off_pw : a.off_pw, off_q = CL ? CG.off_q : a.off_q;
+    const int off_out = CL ? CG.off_out : a.off_out, off_len = CL ? CG.off_len : a.off_len;
+    const int off_scratch = CL ? CG.off_scratch : a.off_scratch;
     const int last_g = NS4 - 1;
     const int ipw = PPW * NS4;                 // items per wave slice
     const bool active = lane < ipw;
@@ -202,11 +214,11 @@ __device__ __forceinline__ void tile_walk(const EncTileArgs& a, uint8_t* smem) {
     const int QJ = ROWS * NS4;                 // dwords per parity plane
 
     // LDS carve-up (byte offsets from the launcher)
-    uint32_t* pw = reinterpret_cast<uint32_t*>(smem + a.off_pw);
-    uint32_t* q = reinterpret_cast<uint32_t*>(smem + a.off_q);
-    uint8_t* out = smem + a.off_out;
-    uint32_t* scratch = reinterpret_cast<uint32_t*>(smem + a.off_scratch);  // one dword per thread
-    const uint32_t* lensl = reinterpret_cast<const uint32_t*>(smem + a.off_len);
+    uint32_t* pw = reinterpret_cast<uint32_t*>(smem + off_pw);
+    uint32_t* q = reinterpret_cast<uint32_t*>(smem + off_q);
+    uint8_t* out = smem + off_out;
+    uint32_t* scratch = reinterpret_cast<uint32_t*>(smem + off_scratch);  // one dword per thread
+    const uint32_t* lensl = reinterpret_cast<const uint32_t*>(smem + off_len);
 
     // coefficient tables of this wave's products, in registers for the whole walk
     TTab tab[NPWA];
@@ -228,15 +240,15 @@ __device__ __forceinline__ void tile_walk(const EncTileArgs& a, uint8_t* smem) {
 
     const int first = blockIdx.x * a.tiles_per_wg;
     const int cnt = min(a.tiles_per_wg, a.ntiles - first);  // real tiles of this workgroup (>= 1)
-    const int ngl = a.ngl;                                   // payload LDS-DMA instructions per wave per tile
+    const int ngl = CL ? CG.ngl : a.ngl;                     // payload LDS-DMA instructions per wave per tile
     const int nglt = ngl + (has_len ? 1 : 0);
-    const int nso = a.nso;                                   // 16-byte stores per thread per tile
+    const int nso = CL ? CG.nso : a.nso;                     // 16-byte stores per thread per tile
     const int ns = nso + 1;                                  // + the trimmed-size store
 
     // tile it (0 = the tile in front of the first one) -> LDS input buffer (it & 1)
     const tv4u rs4 = raw_rsrc(a.payload_base, a.payload_bytes);
     const tv4u rl4 = raw_rsrc(a.len_base, a.len_bytes);
-    const uint32_t lds_in = lds_addr(smem + a.off_in), lds_len = lds_addr(smem + a.off_len);
+    const uint32_t lds_in = lds_addr(smem + off_in), lds_len = lds_addr(smem + off_len);
     // LDS image of a tile: row p at p*RS (RS = L rounded up to 16 bytes), so that every row starts
     // 16-byte aligned; the DMA's destination is lane-linear, its per-lane source picks the row
     // piece (tile-invariant offsets, computed once).  A row's last piece also brings the first
@@ -253,7 +265,7 @@ __device__ __forceinline__ void tile_walk(const EncTileArgs& a, uint8_t* smem) {
     auto issue = [&](int it) __attribute__((always_inline)) {
         const int row0 = (first - 1 + it) * R;
         const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
-        const uint32_t dst = lds_in + (it & 1) * a.in_bytes;
+        const uint32_t dst = lds_in + (it & 1) * in_bytes;
         const int base = (row0 + a.history) * L;  // may be negative: those pieces read as zero
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
@@ -285,7 +297,7 @@ __device__ __forceinline__ void tile_walk(const EncTileArgs& a, uint8_t* smem) {
         }
         wait_lds_barrier();  // B1: the tile is in LDS everywhere; last tile's output stored
         const int row0 = (first - 1 + it) * R;
-        const uint8_t* in = smem + a.off_in + (it & 1) * a.in_bytes;
+        const uint8_t* in = smem + off_in + (it & 1) * in_bytes;
         if (L & 15) {
             // the batch's last row: its last piece runs past the end of the payload rows, and an
             // LDS-DMA out of range as a whole reads zeros: its valid dwords again, one by one
@@ -294,7 +306,7 @@ __device__ __forceinline__ void tile_walk(const EncTileArgs& a, uint8_t* smem) {
                 if (tid < 4) {
                     const int b = (CPR - 1) * 16 + 4 * tid;
                     if (b < L)
-                        reinterpret_cast<uint32_t*>(smem + a.off_in + (it & 1) * a.in_bytes)[(pl_last * RS + b) >> 2] =
+                        reinterpret_cast<uint32_t*>(smem + off_in + (it & 1) * in_bytes)[(pl_last * RS + b) >> 2] =
                             __builtin_amdgcn_raw_buffer_load_b32(rs, (P - 1 + a.history) * L + b, 0, 0);
                 }
                 wait_vm(0);
@@ -332,7 +344,7 @@ __device__ __forceinline__ void tile_walk(const EncTileArgs& a, uint8_t* smem) {
             D[0] = g == 0 ? hdr : D[0];
 #pragma unroll
             for (int m = 0; m < K; ++m)  // the last group's dwords past the row end: zero pad
-                if (m >= a.nvl) D[m + 1] = is_last ? 0u : D[m + 1];
+                if (m >= nvl) D[m + 1] = is_last ? 0u : D[m + 1];
 #pragma unroll
             for (int m = 0; m < K; ++m) H[m] = __builtin_amdgcn_alignbyte(D[m + 1], D[m], 2);
             if (ln != L) {
@@ -349,7 +361,7 @@ __device__ __forceinline__ void tile_walk(const EncTileArgs& a, uint8_t* smem) {
 
         // ---- B: this wave's products over every item of the tile, XORed into the parity rows
         if constexpr (NPW > 0) {
-            if (active && !(a.dbg & 1)) {
+            if (active && !(dbg & 1)) {
 #ifdef FEC_TILE_BUNROLL
 #pragma unroll
 #else
@@ -406,7 +418,7 @@ __device__ __forceinline__ void tile_walk(const EncTileArgs& a, uint8_t* smem) {
             tgroup_words<K, NP>(H, Qv, X);
             uint32_t tw = X[n - 1];
             if (is_last) {
-                switch (a.rem) {
+                switch (rem) {
                     case 1: tw = ttail_rem<n, 1>(X); break;
                     case 2: tw = ttail_rem<n, 2>(X); break;
                     case 3: tw = ttail_rem<n, 3>(X); break;
@@ -422,7 +434,7 @@ __device__ __forceinline__ void tile_walk(const EncTileArgs& a, uint8_t* smem) {
             // dwords written: n, except the last group of a packet: up to the packet end (the dword
             // shared with the next packet is that packet's first lane's)
             const int cntw = !emit ? 0 : (t >= P ? 1 : (is_last ? ((p + 1) * CW >> 2) - d0 : n));
-            if (!(a.dbg & 2)) {
+            if (!(dbg & 2)) {
                 uint32_t* outw = reinterpret_cast<uint32_t*>(out) + d0;
                 uint32_t* zdst = scratch + tid;
 #pragma unroll
@@ -460,10 +472,7 @@ __device__ __forceinline__ void tile_walk(const EncTileArgs& a, uint8_t* smem) {
                 const bool full = inb && c + 16 <= lim;
                 typedef uint32_t v4u __attribute__((ext_vector_type(4)));
                 const v4u vv = {v.x, v.y, v.z, v.w};
-                if (a.dbg & 8)  // experiment: non-temporal codeword stores
-                    __builtin_amdgcn_raw_buffer_store_b128(vv, rc, full && !(a.dbg & 4) ? gbase + c : 0x7ffffff0, 0, 2);
-                else
-                    __builtin_amdgcn_raw_buffer_store_b128(vv, rc, full && !(a.dbg & 4) ? gbase + c : 0x7ffffff0, 0, 0);
+                __builtin_amdgcn_raw_buffer_store_b128(vv, rc, full && !(dbg & 4) ? gbase + c : 0x7ffffff0, 0, 0);
             }
             // trimmed wire size of packet tid (FEC_Encoder.cpp:55-60): 1 + last non-zero byte
             const bool own = tid < R && row0 + tid < P;
@@ -489,31 +498,49 @@ __device__ __forceinline__ void tile_walk(const EncTileArgs& a, uint8_t* smem) {
 
 }  // namespace
 
+// Workgroups per CU the register budget is sized for: five (96 VGPRs), or four / three when a
+// wave's share of the K*NP coefficient tables would not fit beside the rest (it spilled to scratch).
 template <int K, int NP>
-__global__ __launch_bounds__(kTileThreads, FEC_TILE_MINWG) void fec_encode_tile_kernel(EncTileArgs a) {
+constexpr int tile_min_wg() {
+    return K * NP > 36 ? 3 : (K * NP >= 27 ? 4 : FEC_TILE_MINWG);
+}
+
+template <int K, int NP, int LC>
+__global__ __launch_bounds__(kTileThreads, (tile_min_wg<K, NP>())) void fec_encode_tile_kernel(EncTileArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t tsmem[];
     switch (__builtin_amdgcn_readfirstlane(threadIdx.x >> 6)) {
-        case 0: tile_walk<K, NP, 0>(a, tsmem); break;
-        case 1: tile_walk<K, NP, 1>(a, tsmem); break;
-        case 2: tile_walk<K, NP, 2>(a, tsmem); break;
-        default: tile_walk<K, NP, 3>(a, tsmem); break;
+        case 0: tile_walk<K, NP, 0, LC>(a, tsmem); break;
+        case 1: tile_walk<K, NP, 1, LC>(a, tsmem); break;
+        case 2: tile_walk<K, NP, 2, LC>(a, tsmem); break;
+        default: tile_walk<K, NP, 3, LC>(a, tsmem); break;
     }
 }
 
 #ifdef FEC_WAVE_ONLY
 #define FEC_ENC_TILE_LIST(X) X(8, 3)
+#define FEC_ENC_TILE_L300_LIST(X) X(8, 3)
 #else
 #define FEC_ENC_TILE_LIST(X) \
     X(8, 3) X(9, 5) X(11, 0) X(10, 1) X(9, 2) X(7, 4) X(6, 5) X(5, 6) X(4, 7) X(3, 8) X(2, 9)  \
     X(10, 3) X(9, 3) X(10, 4) X(8, 4) X(10, 5) X(7, 5) X(3, 9)
+// L = 300 specialisations: the (T,B,N) of BASELINE configs 1-3 and 5
+#define FEC_ENC_TILE_L300_LIST(X) X(8, 3) X(9, 5)
 #endif
 
-#define FEC_ENC_TILE_INST(K, NP) template __global__ void fec_encode_tile_kernel<K, NP>(EncTileArgs);
+#define FEC_ENC_TILE_INST(K, NP) template __global__ void fec_encode_tile_kernel<K, NP, 0>(EncTileArgs);
+#define FEC_ENC_TILE_INST300(K, NP) template __global__ void fec_encode_tile_kernel<K, NP, 300>(EncTileArgs);
 FEC_ENC_TILE_LIST(FEC_ENC_TILE_INST)
+FEC_ENC_TILE_L300_LIST(FEC_ENC_TILE_INST300)
 
-const void* fec_encode_tile_kernel_for(int k, int np) {
+const void* fec_encode_tile_kernel_for(int k, int np, int L) {
+    if (!std::getenv("FEC_TILE_RUNTIME_L") && L == 300) {
+#define FEC_ENC_TILE_CASE300(K, NP) \
+    if (k == K && np == NP) return reinterpret_cast<const void*>(&fec_encode_tile_kernel<K, NP, 300>);
+        FEC_ENC_TILE_L300_LIST(FEC_ENC_TILE_CASE300)
+#undef FEC_ENC_TILE_CASE300
+    }
 #define FEC_ENC_TILE_CASE(K, NP) \
-    if (k == K && np == NP) return reinterpret_cast<const void*>(&fec_encode_tile_kernel<K, NP>);
+    if (k == K && np == NP) return reinterpret_cast<const void*>(&fec_encode_tile_kernel<K, NP, 0>);
     FEC_ENC_TILE_LIST(FEC_ENC_TILE_CASE)
 #undef FEC_ENC_TILE_CASE
     return nullptr;

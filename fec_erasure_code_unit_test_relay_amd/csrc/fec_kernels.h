@@ -108,8 +108,59 @@ struct EncTileArgs {
                                   // 2 no codeword words, 4 no output stores
 };
 
-// fec_encode_tile_kernel<k, n-k> (fec_encode_tile.hip), else nullptr.  256 threads.
-const void* fec_encode_tile_kernel_for(int k, int np);
+// Geometry of the tile encoder for (k, n-k, L): one definition for the host launcher and the
+// kernels specialised on L at compile time.  ok = 0: the tile form does not apply.
+struct TileGeom {
+    int ok;
+    int S, CW, NS4, PPW, R, rem, nvl, ngl, nso;
+    int off_in, in_bytes, off_pw, off_q, off_out, off_len, off_scratch;
+    int lds, lds_len;  // dynamic LDS without / with the length rows
+};
+constexpr TileGeom tile_geometry(int k, int np, int L) {
+    TileGeom t{};
+    const int n = k + np;
+    t.S = (L + 2 + k - 1) / k;
+    t.CW = t.S * n;
+    t.NS4 = (t.S + 3) / 4;
+    // a wave slice holds whole packets (PPW * NS4 <= 64) whose codewords end on a dword
+    // (PPW * CW % 4 == 0), and a tile (4 * PPW packets) covers the n-1 packets of parity history
+    const int unit = (t.CW & 3) == 0 ? 1 : ((t.CW & 1) == 0 ? 2 : 4);
+    const int ppw = t.NS4 > 0 && t.NS4 <= 64 ? (64 / t.NS4) / unit * unit : 0;
+    if ((L & 3) != 0 || np < 0 || ppw <= 0 || 4 * ppw < n - 1) return t;
+    t.PPW = ppw;
+    t.R = 4 * ppw;
+    const int rs = (L + 15) & ~15;  // LDS row stride of the input tile
+    t.ngl = (t.R * rs + 16 + 4095) / 4096;
+    const int pws = k | 1;
+    const int rows = t.R + n - 1;
+    const int npa = np > 0 ? np : 1;
+    int off = 64;  // guard in front of the input buffers (the first row's dword -1)
+    t.in_bytes = t.ngl * 4096;
+    t.off_in = off;
+    off += 2 * t.in_bytes;
+    // the position words (read before the second barrier of a tile) and the output tile (written
+    // after it) share one region
+    t.off_pw = off;
+    t.off_out = off;
+    const int pwb = 4 * t.R * t.NS4 * pws, outb = t.R * t.CW;
+    off = (off + (pwb > outb ? pwb : outb) + 15) & ~15;
+    t.off_q = off;
+    off = (off + 4 * npa * rows * t.NS4 + 15) & ~15;
+    t.off_scratch = off;
+    off += 1024;
+    t.lds = off;
+    t.off_len = off;  // lengths (only with a length array)
+    t.lds_len = off + 2048;
+    t.nso = (t.R * t.CW / 16 + 255) / 256;
+    t.rem = t.S - 4 * (t.NS4 - 1);
+    t.nvl = L / 4 - k * (t.NS4 - 1);
+    t.ok = t.ngl <= 4 && t.lds_len <= 160 * 1024;
+    return t;
+}
+
+// fec_encode_tile_kernel<k, n-k, L> for L = 300 (the reference's payload size, L fixed at compile
+// time) or <k, n-k, 0> (L from the arguments) (fec_encode_tile.hip), else nullptr.  256 threads.
+const void* fec_encode_tile_kernel_for(int k, int np, int L);
 
 // fec_encode_persist_kernel<k, n-k> (fec_encode_persist.hip), else nullptr.  320 threads.
 const void* fec_encode_persist_kernel_for(int k, int np);
