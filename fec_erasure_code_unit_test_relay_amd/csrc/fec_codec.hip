@@ -1065,9 +1065,10 @@ int guarded(F&& f) {
 // ------------------------------------------------------------------------------------------
 // Streaming objects
 // ------------------------------------------------------------------------------------------
-// One call per packet is one GPU round trip: the packet goes up (pinned staging, async), one kernel,
-// the result comes down (async), one stream synchronisation.  Everything the coder needs from
-// earlier packets stays on the device.
+// One call per packet is one GPU round trip with no DMA command: the caller's packet is written into a
+// host-visible staging row (pinned, coherent, mapped), a staging kernel moves it into the device
+// window / ring, the coding kernel writes its result straight into a host-visible result row, one
+// stream synchronisation.  Everything the coder needs from earlier packets stays on the device.
 struct fec_encoder {
     static constexpr int kRows = 256;  // device window: the n-1 packets in front + appended packets
     std::unique_ptr<fec_codec> codec;
@@ -1078,12 +1079,13 @@ struct fec_encoder {
     hipStream_t s = nullptr;
     uint8_t* d_rows = nullptr;     // kRows x L
     int32_t* d_len = nullptr;      // kRows
-    uint8_t* d_res = nullptr;      // codeword (CW) | trimmed size
-    uint8_t* h_stage = nullptr;    // pinned: payload row (L, padded to 4) | length
-    uint8_t* h_res = nullptr;      // pinned copy of d_res
+    uint8_t* h_stage = nullptr;    // pinned, coherent: payload row (L, padded to 4) | length
+    uint8_t* h_res = nullptr;      // pinned, coherent: codeword (CW) | trimmed size (written by the kernel)
+    uint8_t* m_stage = nullptr;    // device addresses of h_stage / h_res
+    uint8_t* m_res = nullptr;
     ~fec_encoder() {
         if (s) (void)hipStreamDestroy(s);
-        for (void* p : {static_cast<void*>(d_rows), static_cast<void*>(d_len), static_cast<void*>(d_res)})
+        for (void* p : {static_cast<void*>(d_rows), static_cast<void*>(d_len)})
             if (p) (void)hipFree(p);
         if (h_stage) (void)hipHostFree(h_stage);
         if (h_res) (void)hipHostFree(h_res);
@@ -1100,16 +1102,16 @@ struct fec_decoder {
     bool pending = false;          // an upload from h_cw may still be in flight
     hipStream_t s = nullptr;
     uint8_t* d_ring = nullptr;     // RR x CW
-    uint8_t* d_coef = nullptr;     // k x n (recovered packets)
     uint8_t* d_ident = nullptr;    // k x n identity (received packets)
-    uint8_t* d_res = nullptr;      // payload (L) | length
-    uint8_t* h_cw = nullptr;       // pinned CW-byte staging row
-    uint8_t* h_coef = nullptr;     // pinned k x n
-    uint8_t* h_res = nullptr;      // pinned copy of d_res
+    uint8_t* h_cw = nullptr;       // pinned, coherent: CW-byte staging row
+    uint8_t* h_coef = nullptr;     // pinned, coherent: k x n (read by the output kernel)
+    uint8_t* h_res = nullptr;      // pinned, coherent: payload (L) | length (written by the kernel)
+    uint8_t* m_cw = nullptr;       // device addresses of h_cw / h_coef / h_res
+    uint8_t* m_coef = nullptr;
+    uint8_t* m_res = nullptr;
     ~fec_decoder() {
         if (s) (void)hipStreamDestroy(s);
-        for (void* p : {static_cast<void*>(d_ring), static_cast<void*>(d_coef), static_cast<void*>(d_ident),
-                        static_cast<void*>(d_res)})
+        for (void* p : {static_cast<void*>(d_ring), static_cast<void*>(d_ident)})
             if (p) (void)hipFree(p);
         for (void* p : {static_cast<void*>(h_cw), static_cast<void*>(h_coef), static_cast<void*>(h_res)})
             if (p) (void)hipHostFree(p);
@@ -1372,6 +1374,19 @@ int fec_timing_collect(fec_codec* c, double* total_ms, int64_t* launches) {
 }
 
 // ---- streaming encoder --------------------------------------------------------------------
+namespace {
+// Pinned host memory the kernels read and write directly (coherent: never cached in the GPU's L2, so a
+// row the host rewrote between calls is seen fresh, and a result row is complete at the stream
+// synchronisation).
+hipError_t host_mapped(uint8_t** host, uint8_t** dev, size_t bytes) {
+    if (hipError_t e = hipHostMalloc(reinterpret_cast<void**>(host), bytes,
+                                     hipHostMallocMapped | hipHostMallocCoherent))
+        return e;
+    std::memset(*host, 0, bytes);
+    return hipHostGetDevicePointer(reinterpret_cast<void**>(dev), *host, 0);
+}
+}  // namespace
+
 int fec_encoder_create(int max_payload, int T, int B, int N, fec_encoder** out) {
     if (!out) return FEC_ERR_ARG;
     *out = nullptr;
@@ -1386,9 +1401,8 @@ int fec_encoder_create(int max_payload, int T, int B, int N, fec_encoder** out) 
         HIP_TRY(hipStreamCreateWithFlags(&e->s, hipStreamNonBlocking));
         HIP_TRY(hipMalloc(&e->d_rows, static_cast<size_t>(fec_encoder::kRows) * g.L));
         HIP_TRY(hipMalloc(&e->d_len, fec_encoder::kRows * 4));
-        HIP_TRY(hipMalloc(&e->d_res, e->res_len_off + 4));
-        HIP_TRY(hipHostMalloc(&e->h_stage, ((g.L + 3) & ~3) + 4));
-        HIP_TRY(hipHostMalloc(&e->h_res, e->res_len_off + 4));
+        HIP_TRY(host_mapped(&e->h_stage, &e->m_stage, ((g.L + 3) & ~3) + 4));
+        HIP_TRY(host_mapped(&e->h_res, &e->m_res, e->res_len_off + 4));
         *out = e.release();
         return FEC_OK;
     });
@@ -1427,13 +1441,14 @@ int fec_encoder_transmit(fec_encoder* e, const uint8_t* data, int payload, int s
     if (payload > 0) std::memcpy(e->h_stage, data, payload);
     std::memcpy(e->h_stage + lrow, &payload, 4);
     uint8_t* row = e->d_rows + static_cast<size_t>(e->pos) * g.L;
-    HIP_TRY(hipMemcpyAsync(row, e->h_stage, g.L, hipMemcpyHostToDevice, e->s));
-    HIP_TRY(hipMemcpyAsync(e->d_len + e->pos, e->h_stage + lrow, 4, hipMemcpyHostToDevice, e->s));
+    hipLaunchKernelGGL(fec::fec_stage_row_kernel, dim3(1), dim3(256), 0, e->s, e->m_stage, row, g.L,
+                       reinterpret_cast<const int32_t*>(e->m_stage + lrow), e->d_len + e->pos);
+    HIP_TRY(hipGetLastError());
     const int64_t history = std::min<int64_t>(std::min<int64_t>(seq - e->origin, n - 1), e->pos);
-    int32_t* d_size = reinterpret_cast<int32_t*>(e->d_res + e->res_len_off);
-    if (int st = launch_encode(e->codec.get(), row, e->d_len + e->pos, history, 1, e->d_res, d_size, e->s))
+    // the codeword and its trimmed size go straight into the host-visible result row
+    int32_t* m_size = reinterpret_cast<int32_t*>(e->m_res + e->res_len_off);
+    if (int st = launch_encode(e->codec.get(), row, e->d_len + e->pos, history, 1, e->m_res, m_size, e->s))
         return st;
-    HIP_TRY(hipMemcpyAsync(e->h_res, e->d_res, e->res_len_off + 4, hipMemcpyDeviceToHost, e->s));
     HIP_TRY(hipStreamSynchronize(e->s));
     std::memcpy(cw_out, e->h_res, g.CW);
     std::memcpy(cw_size, e->h_res + e->res_len_off, 4);
@@ -1458,15 +1473,13 @@ int fec_decoder_create(int max_payload, int T, int B, int N, fec_decoder** out) 
         HIP_TRY(hipStreamCreateWithFlags(&d->s, hipStreamNonBlocking));
         HIP_TRY(hipMalloc(&d->d_ring, static_cast<size_t>(fec_decoder::RR) * g.CW));
         HIP_TRY(hipMemset(d->d_ring, 0, static_cast<size_t>(fec_decoder::RR) * g.CW));
-        HIP_TRY(hipMalloc(&d->d_coef, g.k * g.n));
         HIP_TRY(hipMalloc(&d->d_ident, g.k * g.n));
         std::vector<uint8_t> ident(static_cast<size_t>(g.k) * g.n, 0);
         for (int i = 0; i < g.k; ++i) ident[i * g.n + i] = 1;
         HIP_TRY(hipMemcpy(d->d_ident, ident.data(), ident.size(), hipMemcpyHostToDevice));
-        HIP_TRY(hipMalloc(&d->d_res, d->res_len_off + 4));
-        HIP_TRY(hipHostMalloc(&d->h_cw, g.CW));
-        HIP_TRY(hipHostMalloc(&d->h_coef, g.k * g.n));
-        HIP_TRY(hipHostMalloc(&d->h_res, d->res_len_off + 4));
+        HIP_TRY(host_mapped(&d->h_cw, &d->m_cw, g.CW));
+        HIP_TRY(host_mapped(&d->h_coef, &d->m_coef, g.k * g.n));
+        HIP_TRY(host_mapped(&d->h_res, &d->m_res, d->res_len_off + 4));
         *out = d.release();
         return FEC_OK;
     });
@@ -1499,8 +1512,10 @@ int fec_decoder_receive(fec_decoder* d, const uint8_t* cw, int cw_size, int seq,
         int sz = std::max(0, std::min(cw_size, g.CW));
         std::memset(d->h_cw, 0, g.CW);
         if (sz) std::memcpy(d->h_cw, cw, sz);
-        HIP_TRY(hipMemcpyAsync(d->d_ring + static_cast<size_t>(rel % fec_decoder::RR) * g.CW, d->h_cw, g.CW,
-                               hipMemcpyHostToDevice, d->s));
+        hipLaunchKernelGGL(fec::fec_stage_row_kernel, dim3(1), dim3(256), 0, d->s, d->m_cw,
+                           d->d_ring + static_cast<size_t>(rel % fec_decoder::RR) * g.CW, g.CW,
+                           static_cast<const int32_t*>(nullptr), static_cast<int32_t*>(nullptr));
+        HIP_TRY(hipGetLastError());
         d->pending = true;
     }
     fec::StepResult r;
@@ -1517,9 +1532,8 @@ int fec_decoder_receive(fec_decoder* d, const uint8_t* cw, int cw_size, int seq,
     }
     const uint8_t* coef = d->d_ident;
     if (r.fate == fec::kRecovered) {
-        std::memcpy(d->h_coef, r.coef, g.k * g.n);
-        HIP_TRY(hipMemcpyAsync(d->d_coef, d->h_coef, g.k * g.n, hipMemcpyHostToDevice, d->s));
-        coef = d->d_coef;
+        std::memcpy(d->h_coef, r.coef, g.k * g.n);  // read by the kernel below, synchronised before return
+        coef = d->m_coef;
     }
     fec::StreamOutArgs a;
     a.ring = d->d_ring;
@@ -1527,8 +1541,8 @@ int fec_decoder_receive(fec_decoder* d, const uint8_t* cw, int cw_size, int seq,
     a.x = r.x;
     a.coef = coef;
     a.gf = d->codec->d_gf;
-    a.out = d->d_res;
-    a.out_len = reinterpret_cast<int32_t*>(d->d_res + d->res_len_off);
+    a.out = d->m_res;
+    a.out_len = reinterpret_cast<int32_t*>(d->m_res + d->res_len_off);
     a.L = g.L;
     a.k = g.k;
     a.n = g.n;
@@ -1536,7 +1550,6 @@ int fec_decoder_receive(fec_decoder* d, const uint8_t* cw, int cw_size, int seq,
     a.clamp = r.slow ? 1 : 0;
     hipLaunchKernelGGL(fec::fec_stream_out_kernel, dim3(1), dim3(256), 0, d->s, a);
     HIP_TRY(hipGetLastError());
-    HIP_TRY(hipMemcpyAsync(d->h_res, d->d_res, d->res_len_off + 4, hipMemcpyDeviceToHost, d->s));
     HIP_TRY(hipStreamSynchronize(d->s));
     d->pending = false;
     std::memcpy(payload_out, d->h_res, g.L);

@@ -359,6 +359,8 @@ __global__ void fec_plan_kernel(PlanArgs a);
 __global__ void fec_copy_kernel(CopyArgs a);
 
 __global__ void fec_stream_out_kernel(StreamOutArgs a);
+__global__ void fec_stage_row_kernel(const uint8_t* src, uint8_t* dst, int bytes, const int32_t* src_word,
+                                     int32_t* dst_word);
 __global__ void fec_fill_kernel(uint8_t* out, int64_t t0, int64_t count, int L, uint64_t seed);
 
 }  // namespace fec
