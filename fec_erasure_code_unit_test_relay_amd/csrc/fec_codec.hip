@@ -2,6 +2,8 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
+#include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -1070,25 +1072,24 @@ int guarded(F&& f) {
 // window / ring, the coding kernel writes its result straight into a host-visible result row, one
 // stream synchronisation.  Everything the coder needs from earlier packets stays on the device.
 struct fec_encoder {
-    static constexpr int kRows = 256;  // device window: the n-1 packets in front + appended packets
     std::unique_ptr<fec_codec> codec;
     int64_t origin = -1;           // seq of the first call (the encoder's creation point)
     int64_t next = 0;              // expected seq
-    int pos = 0;                   // window row of the next packet
     int res_len_off = 0;           // offset of the trimmed size in the result block (4-aligned)
     hipStream_t s = nullptr;
-    uint8_t* d_rows = nullptr;     // kRows x L
-    int32_t* d_len = nullptr;      // kRows
-    uint8_t* h_stage = nullptr;    // pinned, coherent: payload row (L, padded to 4) | length
+    uint8_t* d_win = nullptr;      // the n-1 windows in front, a ring by seq % (n-1) (fec_streams layout)
+    uint8_t* h_stage = nullptr;    // pinned, coherent: payload row (read by the kernel)
     uint8_t* h_res = nullptr;      // pinned, coherent: codeword (CW) | trimmed size (written by the kernel)
     uint8_t* m_stage = nullptr;    // device addresses of h_stage / h_res
     uint8_t* m_res = nullptr;
+    uint8_t* h_done = nullptr;     // pinned, coherent: completion word (ticket of the last finished call)
+    uint8_t* m_done = nullptr;
+    uint32_t ticket = 0;
     ~fec_encoder() {
         if (s) (void)hipStreamDestroy(s);
-        for (void* p : {static_cast<void*>(d_rows), static_cast<void*>(d_len)})
-            if (p) (void)hipFree(p);
-        if (h_stage) (void)hipHostFree(h_stage);
-        if (h_res) (void)hipHostFree(h_res);
+        if (d_win) (void)hipFree(d_win);
+        for (void* p : {static_cast<void*>(h_stage), static_cast<void*>(h_res), static_cast<void*>(h_done)})
+            if (p) (void)hipHostFree(p);
     }
 };
 
@@ -1099,21 +1100,24 @@ struct fec_decoder {
     int64_t origin = -1;           // seq of the first call; the planner runs on seq - origin
     int64_t next = 0;
     int res_len_off = 0;
-    bool pending = false;          // an upload from h_cw may still be in flight
     hipStream_t s = nullptr;
     uint8_t* d_ring = nullptr;     // RR x CW
-    uint8_t* d_ident = nullptr;    // k x n identity (received packets)
+    uint8_t* d_coef = nullptr;     // k x n coefficients of a recovered packet
     uint8_t* h_cw = nullptr;       // pinned, coherent: CW-byte staging row
     uint8_t* h_coef = nullptr;     // pinned, coherent: k x n (read by the output kernel)
     uint8_t* h_res = nullptr;      // pinned, coherent: payload (L) | length (written by the kernel)
     uint8_t* m_cw = nullptr;       // device addresses of h_cw / h_coef / h_res
     uint8_t* m_coef = nullptr;
     uint8_t* m_res = nullptr;
+    uint8_t* h_done = nullptr;     // pinned, coherent: completion word (ticket of the last finished call)
+    uint8_t* m_done = nullptr;
+    uint32_t ticket = 0;
     ~fec_decoder() {
         if (s) (void)hipStreamDestroy(s);
-        for (void* p : {static_cast<void*>(d_ring), static_cast<void*>(d_ident)})
+        for (void* p : {static_cast<void*>(d_ring), static_cast<void*>(d_coef)})
             if (p) (void)hipFree(p);
-        for (void* p : {static_cast<void*>(h_cw), static_cast<void*>(h_coef), static_cast<void*>(h_res)})
+        for (void* p : {static_cast<void*>(h_cw), static_cast<void*>(h_coef), static_cast<void*>(h_res),
+                        static_cast<void*>(h_done)})
             if (p) (void)hipHostFree(p);
     }
 };
@@ -1385,6 +1389,30 @@ hipError_t host_mapped(uint8_t** host, uint8_t** dev, size_t bytes) {
     std::memset(*host, 0, bytes);
     return hipHostGetDevicePointer(reinterpret_cast<void**>(dev), *host, 0);
 }
+
+// End of a streaming call: the call's last kernel stores `ticket` into the host-visible completion
+// word after its results; the host polls that word (a stream synchronisation's wake-up costs several
+// microseconds more).  A call that takes longer than 20 ms, or FEC_STREAM_SPIN=0, falls back to
+// hipStreamSynchronize, which also reports a failed kernel.
+hipError_t wait_done(const uint8_t* h_done, uint32_t ticket, hipStream_t s) {
+    static const bool spin = [] {
+        const char* v = std::getenv("FEC_STREAM_SPIN");
+        return !v || std::atoi(v) != 0;
+    }();
+    if (spin) {
+        const volatile uint32_t* w = reinterpret_cast<const volatile uint32_t*>(h_done);
+        const auto t0 = std::chrono::steady_clock::now();
+        for (uint32_t i = 1;; ++i) {
+            if (*w == ticket) {
+                std::atomic_thread_fence(std::memory_order_acquire);
+                return hipSuccess;
+            }
+            if ((i & 4095) == 0 && std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(20)) break;
+            __builtin_ia32_pause();
+        }
+    }
+    return hipStreamSynchronize(s);
+}
 }  // namespace
 
 int fec_encoder_create(int max_payload, int T, int B, int N, fec_encoder** out) {
@@ -1396,13 +1424,16 @@ int fec_encoder_create(int max_payload, int T, int B, int N, fec_encoder** out) 
         if (int st = fec_codec_create(max_payload, T, B, N, &c)) return st;
         e->codec.reset(c);
         const Geometry& g = c->g;
-        if (g.n > fec_encoder::kRows / 2) return FEC_ERR_ARG;
+        if (g.k > 16 || g.k * g.n > 16 * 32) return FEC_ERR_ARG;  // fec_streams_encode_kernel's bounds
         e->res_len_off = (g.CW + 3) & ~3;
         HIP_TRY(hipStreamCreateWithFlags(&e->s, hipStreamNonBlocking));
-        HIP_TRY(hipMalloc(&e->d_rows, static_cast<size_t>(fec_encoder::kRows) * g.L));
-        HIP_TRY(hipMalloc(&e->d_len, fec_encoder::kRows * 4));
-        HIP_TRY(host_mapped(&e->h_stage, &e->m_stage, ((g.L + 3) & ~3) + 4));
+        const size_t wb = static_cast<size_t>(std::max(1, g.n - 1)) * g.S * g.k;
+        HIP_TRY(hipMalloc(&e->d_win, wb));
+        HIP_TRY(hipMemset(e->d_win, 0, wb));
+        HIP_TRY(host_mapped(&e->h_stage, &e->m_stage, (g.L + 3) & ~3));
         HIP_TRY(host_mapped(&e->h_res, &e->m_res, e->res_len_off + 4));
+        HIP_TRY(host_mapped(&e->h_done, &e->m_done, 4));
+        HIP_TRY(hipDeviceSynchronize());  // the window is zero before the first call's kernel
         *out = e.release();
         return FEC_OK;
     });
@@ -1427,32 +1458,21 @@ int fec_encoder_transmit(fec_encoder* e, const uint8_t* data, int payload, int s
     if (seq != e->next) return FEC_ERR_SEQUENCE;
     const Geometry& g = e->codec->g;
     if (payload > g.L) payload = g.L;
-    const int n = g.n;
-    if (e->pos == fec_encoder::kRows) {  // window full: its last n-1 rows move to the front
-        const int keep = n - 1;
-        HIP_TRY(hipMemcpyAsync(e->d_rows, e->d_rows + static_cast<size_t>(fec_encoder::kRows - keep) * g.L,
-                               static_cast<size_t>(keep) * g.L, hipMemcpyDeviceToDevice, e->s));
-        HIP_TRY(hipMemcpyAsync(e->d_len, e->d_len + (fec_encoder::kRows - keep), keep * 4,
-                               hipMemcpyDeviceToDevice, e->s));
-        e->pos = keep;
-    }
-    const int lrow = (g.L + 3) & ~3;
-    std::memset(e->h_stage, 0, g.L);
+    // one launch: the closed form over the device-resident window (fec_streams_encode_kernel reads
+    // the payload from the mapped staging row, writes codeword and size into the mapped result row,
+    // then the completion word)
+    if (e->ticket) HIP_TRY(wait_done(e->h_done, e->ticket, e->s));  // h_stage is free again
     if (payload > 0) std::memcpy(e->h_stage, data, payload);
-    std::memcpy(e->h_stage + lrow, &payload, 4);
-    uint8_t* row = e->d_rows + static_cast<size_t>(e->pos) * g.L;
-    hipLaunchKernelGGL(fec::fec_stage_row_kernel, dim3(1), dim3(256), 0, e->s, e->m_stage, row, g.L,
-                       reinterpret_cast<const int32_t*>(e->m_stage + lrow), e->d_len + e->pos);
-    HIP_TRY(hipGetLastError());
-    const int64_t history = std::min<int64_t>(std::min<int64_t>(seq - e->origin, n - 1), e->pos);
-    // the codeword and its trimmed size go straight into the host-visible result row
-    int32_t* m_size = reinterpret_cast<int32_t*>(e->m_res + e->res_len_off);
-    if (int st = launch_encode(e->codec.get(), row, e->d_len + e->pos, history, 1, e->m_res, m_size, e->s))
+    fec::CodecView v;
+    if (int st = fec::codec_view(e->codec.get(), &v)) return st;
+    const uint32_t ticket = ++e->ticket;
+    if (int st = fec::stream_encode_one(v, e->d_win, e->m_stage, payload, seq - e->origin, e->m_res,
+                                        reinterpret_cast<int32_t*>(e->m_res + e->res_len_off),
+                                        reinterpret_cast<uint32_t*>(e->m_done), ticket, e->s))
         return st;
-    HIP_TRY(hipStreamSynchronize(e->s));
+    HIP_TRY(wait_done(e->h_done, ticket, e->s));
     std::memcpy(cw_out, e->h_res, g.CW);
     std::memcpy(cw_size, e->h_res + e->res_len_off, 4);
-    ++e->pos;
     ++e->next;
     return FEC_OK;
 }
@@ -1473,13 +1493,12 @@ int fec_decoder_create(int max_payload, int T, int B, int N, fec_decoder** out) 
         HIP_TRY(hipStreamCreateWithFlags(&d->s, hipStreamNonBlocking));
         HIP_TRY(hipMalloc(&d->d_ring, static_cast<size_t>(fec_decoder::RR) * g.CW));
         HIP_TRY(hipMemset(d->d_ring, 0, static_cast<size_t>(fec_decoder::RR) * g.CW));
-        HIP_TRY(hipMalloc(&d->d_ident, g.k * g.n));
-        std::vector<uint8_t> ident(static_cast<size_t>(g.k) * g.n, 0);
-        for (int i = 0; i < g.k; ++i) ident[i * g.n + i] = 1;
-        HIP_TRY(hipMemcpy(d->d_ident, ident.data(), ident.size(), hipMemcpyHostToDevice));
-        HIP_TRY(host_mapped(&d->h_cw, &d->m_cw, g.CW));
+        HIP_TRY(hipMalloc(&d->d_coef, g.k * g.n));
+        HIP_TRY(host_mapped(&d->h_cw, &d->m_cw, (g.CW + 3) & ~3));
         HIP_TRY(host_mapped(&d->h_coef, &d->m_coef, g.k * g.n));
         HIP_TRY(host_mapped(&d->h_res, &d->m_res, d->res_len_off + 4));
+        HIP_TRY(host_mapped(&d->h_done, &d->m_done, 4));
+        HIP_TRY(hipDeviceSynchronize());  // the ring is zero before the first call's kernel
         *out = d.release();
         return FEC_OK;
     });
@@ -1504,20 +1523,8 @@ int fec_decoder_receive(fec_decoder* d, const uint8_t* cw, int cw_size, int seq,
     const int64_t rel = seq - d->origin;
     const Geometry& g = d->codec->g;
     const bool er = erasure != 0 || cw == nullptr;
-    if (d->pending) {  // the staging row of an earlier call may still be uploading
-        HIP_TRY(hipStreamSynchronize(d->s));
-        d->pending = false;
-    }
-    if (!er) {  // FEC_Decoder.cpp:55-63: keep a zero-padded copy of the wire codeword
-        int sz = std::max(0, std::min(cw_size, g.CW));
-        std::memset(d->h_cw, 0, g.CW);
-        if (sz) std::memcpy(d->h_cw, cw, sz);
-        hipLaunchKernelGGL(fec::fec_stage_row_kernel, dim3(1), dim3(256), 0, d->s, d->m_cw,
-                           d->d_ring + static_cast<size_t>(rel % fec_decoder::RR) * g.CW, g.CW,
-                           static_cast<const int32_t*>(nullptr), static_cast<int32_t*>(nullptr));
-        HIP_TRY(hipGetLastError());
-        d->pending = true;
-    }
+    // the previous call's kernel has read h_cw / h_coef (its completion word is set)
+    if (d->ticket) HIP_TRY(wait_done(d->h_done, d->ticket, d->s));
     fec::StepResult r;
     int st = guarded([&] {
         r = d->planner->step(rel, er);
@@ -1525,33 +1532,34 @@ int fec_decoder_receive(fec_decoder* d, const uint8_t* cw, int cw_size, int seq,
     });
     if (st) return st;
     ++d->next;
-    if (r.fate == fec::kNone || r.fate == fec::kLost) {
+    const bool no_output = r.fate == fec::kNone || r.fate == fec::kLost;
+    if (no_output) {
         std::memset(payload_out, 0, g.L);
         *payload = 0;
-        return FEC_OK;
+        if (er) return FEC_OK;  // nothing to keep, nothing to compute
     }
-    const uint8_t* coef = d->d_ident;
+    if (!er) {  // FEC_Decoder.cpp:55-63: keep a zero-padded copy of the wire codeword
+        const int sz = std::max(0, std::min(cw_size, g.CW));
+        std::memset(d->h_cw, 0, (g.CW + 3) & ~3);
+        if (sz) std::memcpy(d->h_cw, cw, sz);
+    }
+    const uint8_t* coef = nullptr;
     if (r.fate == fec::kRecovered) {
-        std::memcpy(d->h_coef, r.coef, g.k * g.n);  // read by the kernel below, synchronised before return
-        coef = d->m_coef;
+        std::memcpy(d->h_coef, r.coef, g.k * g.n);
+        HIP_TRY(hipMemcpyAsync(d->d_coef, d->h_coef, g.k * g.n, hipMemcpyHostToDevice, d->s));
+        coef = d->d_coef;
     }
-    fec::StreamOutArgs a;
-    a.ring = d->d_ring;
-    a.RR = fec_decoder::RR;
-    a.x = r.x;
-    a.coef = coef;
-    a.gf = d->codec->d_gf;
-    a.out = d->m_res;
-    a.out_len = reinterpret_cast<int32_t*>(d->m_res + d->res_len_off);
-    a.L = g.L;
-    a.k = g.k;
-    a.n = g.n;
-    a.CW = g.CW;
-    a.clamp = r.slow ? 1 : 0;
-    hipLaunchKernelGGL(fec::fec_stream_out_kernel, dim3(1), dim3(256), 0, d->s, a);
-    HIP_TRY(hipGetLastError());
-    HIP_TRY(hipStreamSynchronize(d->s));
-    d->pending = false;
+    // one launch (fec_streams_decode_kernel): the codeword into the device ring, packet r.x into the
+    // mapped result row, then the completion word
+    fec::CodecView v;
+    if (int e = fec::codec_view(d->codec.get(), &v)) return e;
+    const uint32_t ticket = ++d->ticket;
+    if (int e = fec::stream_decode_one(v, d->d_ring, er ? nullptr : d->m_cw, rel, er ? 1 : 0, r.fate, r.slow ? 1 : 0,
+                                       r.x, coef, d->m_res, reinterpret_cast<int32_t*>(d->m_res + d->res_len_off),
+                                       reinterpret_cast<uint32_t*>(d->m_done), ticket, d->s))
+        return e;
+    if (no_output) return FEC_OK;  // the codeword is stored asynchronously; the next call waits for it
+    HIP_TRY(wait_done(d->h_done, ticket, d->s));
     std::memcpy(payload_out, d->h_res, g.L);
     std::memcpy(payload, d->h_res + d->res_len_off, 4);
     return FEC_OK;

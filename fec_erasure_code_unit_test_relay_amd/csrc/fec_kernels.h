@@ -16,8 +16,8 @@
 //   fec_copy_kernel        systematic gather + length parse for every received packet (the
 //                          decoder's fast path, src/Decoder.cpp:77-108, and the slow path's
 //                          received packets);
-//   fec_recover_kernel     applies the coefficients to the bytes of every recovered packet;
-//   fec_stream_out_kernel  single-packet output for the streaming (per-call) decoder.
+//   fec_recover_kernel     applies the coefficients to the bytes of every recovered packet.
+// The per-packet coders run on fec_streams.hip's kernels (stream_encode_one / stream_decode_one).
 #pragma once
 
 #include <hip/hip_runtime.h>
@@ -315,17 +315,6 @@ inline int recover_lds_bytes(int maxn, int stage_bytes) {
 template <int MAXN, bool STAGED>
 __global__ void fec_recover_kernel_t(RecArgs a);
 
-struct StreamOutArgs {
-    const uint8_t* ring;        // RR rows of CW bytes, row = seq % RR
-    int RR;
-    int64_t x;                  // packet to output
-    const uint8_t* coef;        // k x n
-    const uint8_t* gf;
-    uint8_t* out;               // L bytes
-    int32_t* out_len;           // 1 int
-    int L, k, n, CW;
-    int clamp;                  // 1: slow path (payload clamped to L)
-};
 
 // Block mode (fec_block.hip): many independent code blocks of n symbols.
 struct BlockArgs {
@@ -358,9 +347,6 @@ __global__ void fec_encode_kernel(EncArgs a);
 __global__ void fec_plan_kernel(PlanArgs a);
 __global__ void fec_copy_kernel(CopyArgs a);
 
-__global__ void fec_stream_out_kernel(StreamOutArgs a);
-__global__ void fec_stage_row_kernel(const uint8_t* src, uint8_t* dst, int bytes, const int32_t* src_word,
-                                     int32_t* dst_word);
 __global__ void fec_fill_kernel(uint8_t* out, int64_t t0, int64_t count, int L, uint64_t seed);
 
 }  // namespace fec
@@ -368,4 +354,16 @@ __global__ void fec_fill_kernel(uint8_t* out, int64_t t0, int64_t count, int L, 
 struct fec_codec;
 namespace fec {
 int codec_view(const ::fec_codec* c, CodecView* v);
+// The per-packet FEC_Encoder's call (fec_codec.hip): packet `seq` (relative to the encoder's first)
+// of one stream whose window ring `win` ([n-1][S*k], fec_streams.hip's layout) lives on the device,
+// through fec_streams_encode_kernel in one launch.  payload / cw / cw_len may be host-visible
+// (mapped) rows; after them the kernel stores `ticket` into `done`.
+int stream_encode_one(const CodecView& v, uint8_t* win, const uint8_t* payload, int payload_len, int64_t seq,
+                      uint8_t* cw, int32_t* cw_len, uint32_t* done, uint32_t ticket, hipStream_t s);
+// The per-packet FEC_Decoder's call: store packet `seq`'s codeword `cw` (a host-visible row padded to
+// whole dwords; not read when erased) in the 64-row device ring `ring`, output packet x with the
+// planner's fate (coef: k x n device block when recovered) into out / out_len, then `ticket` into `done`.
+int stream_decode_one(const CodecView& v, uint8_t* ring, const uint8_t* cw, int64_t seq, int erased, int fate,
+                      int clamp, int64_t x, const uint8_t* coef, uint8_t* out, int32_t* out_len, uint32_t* done,
+                      uint32_t ticket, hipStream_t s);
 }  // namespace fec

@@ -689,67 +689,6 @@ __global__ __launch_bounds__(256) void fec_copy_kernel(CopyArgs a) {
     }
 }
 
-// ------------------------------------------------------------------------------------------
-// Streaming decoder output of one packet: same formula with an identity matrix for a copy.
-// ------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void fec_stream_out_kernel(StreamOutArgs a) {
-    __shared__ uint8_t gexp[512];
-    __shared__ uint8_t glog[256];
-    __shared__ uint8_t ob[4096];
-    const int tid = threadIdx.x;
-    const int L = a.L, k = a.k, n = a.n, CW = a.CW;
-    for (int i = tid; i < 512; i += 256) gexp[i] = a.gf[i];
-    for (int i = tid; i < 256; i += 256) glog[i] = a.gf[512 + i];
-    __syncthreads();
-    for (int h = tid; h < L + 2; h += 256) {
-        const int s = h / k, i = h - (h / k) * k;
-        uint8_t acc = 0;
-        for (int q = 0; q < n; ++q) {
-            const uint8_t c = a.coef[i * n + q];
-            if (!c) continue;
-            const int64_t sp = a.x - i + q;
-            const int64_t row = ((sp % a.RR) + a.RR) % a.RR;
-            acc ^= gf_mul_lds(gexp, glog, c, a.ring[row * CW + s * n + q]);
-        }
-        ob[h] = acc;
-    }
-    __syncthreads();
-    const int hdr = ob[0] * 256 + ob[1];
-    const int ln = a.clamp ? min(hdr, L) : hdr;
-    const int cp = min(ln, L);
-    // a.out is usually the caller's host-visible result row (mapped, coherent): dword stores
-    if ((L & 3) == 0 && (reinterpret_cast<uintptr_t>(a.out) & 3) == 0) {
-        for (int b = 4 * tid; b < L; b += 1024) {
-            uint32_t w = 0;
-#pragma unroll
-            for (int e = 0; e < 4; ++e) w |= static_cast<uint32_t>(b + e < cp ? ob[b + e + 2] : 0) << (8 * e);
-            *reinterpret_cast<uint32_t*>(a.out + b) = w;
-        }
-    } else {
-        for (int b = tid; b < L; b += 256) a.out[b] = (b < cp) ? ob[b + 2] : 0;
-    }
-    if (tid == 0) *a.out_len = ln;
-}
-
-// Per-call staging of the streaming coders: `bytes` bytes from the caller's host-visible row
-// (mapped, coherent) into device memory, and optionally one 32-bit word.  One launch in the
-// call's stream replaces the DMA copies (each a separate command with its own latency).
-__global__ __launch_bounds__(256) void fec_stage_row_kernel(const uint8_t* src, uint8_t* dst, int bytes,
-                                                            const int32_t* src_word, int32_t* dst_word) {
-    const int tid = threadIdx.x;
-    if (((reinterpret_cast<uintptr_t>(src) | reinterpret_cast<uintptr_t>(dst)) & 3) == 0) {
-        for (int b = 4 * tid; b < bytes; b += 1024) {
-            if (b + 4 <= bytes)
-                *reinterpret_cast<uint32_t*>(dst + b) = *reinterpret_cast<const uint32_t*>(src + b);
-            else
-                for (int q = b; q < bytes; ++q) dst[q] = src[q];
-        }
-    } else {
-        for (int b = tid; b < bytes; b += 256) dst[b] = src[b];
-    }
-    if (src_word && tid == 0) *dst_word = *src_word;
-}
-
 }  // namespace fec
 
 namespace fec {

@@ -42,6 +42,12 @@ struct StreamsEncArgs {
     const uint8_t* G;        // k x n
     const uint8_t* gf;       // exp[512], log[256]
     int M, L, k, n, S, CW, SK, W;
+    // single-packet calls (stream_encode_one): seq / ids / len null -> seq1, stream 0, len1; after the
+    // packet's outputs the wave stores ticket into the host-visible word `done` (null: none)
+    int64_t seq1;
+    int len1;
+    uint32_t* done;
+    uint32_t ticket;
 };
 
 struct StreamItem {
@@ -64,10 +70,66 @@ struct StreamsDecArgs {
     uint8_t* out;            // M rows of L bytes
     int32_t* out_len;
     int M, L, k, n, CW, RR;
+    // single-packet calls (stream_decode_one): items null -> item1; after the outputs the wave stores
+    // ticket into the host-visible word `done` (null: none)
+    StreamItem item1;
+    uint32_t* done;
+    uint32_t ticket;
 };
 
 __device__ __forceinline__ uint8_t gmul(const uint8_t* gexp, const uint8_t* glog, uint8_t a, uint8_t b) {
     return (a && b) ? gexp[glog[a] + glog[b]] : 0;
+}
+
+// Single-packet calls (stream_encode_one, M == 1): the whole workgroup on the one codeword, a thread
+// per codeword byte, so that no thread walks a long chain of table lookups (the per-packet
+// FEC_Encoder's latency).  prow / wst / rowoff / cwl are the kernel's LDS (wave 0's slices).
+__device__ __forceinline__ void single_packet_encode(const StreamsEncArgs& a, int tid, const uint8_t* gexp,
+                                                     const uint8_t* glog, const uint8_t* Gs, const uint8_t* pay,
+                                                     const uint32_t* wst, int* ro, uint32_t* cwl) {
+    __shared__ int last_nz;
+    const int L = a.L, k = a.k, n = a.n, CW = a.CW, SK = a.SK, W = a.W;
+    const int ln = min(max(a.len1, 0), L);
+    const int64_t seq = a.seq1;
+    if (tid < 32) ro[tid] = (tid >= 1 && seq - tid >= 0) ? static_cast<int>((seq - tid) % W) * SK : -1;
+    if (tid == 0) last_nz = -1;
+    __syncthreads();  // payload row, window, offsets
+    auto xbyte = [&](int b) -> uint8_t {  // [len_hi, len_lo, payload, zero pad] (Encoder.cpp:75-83)
+        return b == 0 ? static_cast<uint8_t>(ln >> 8)
+                      : b == 1 ? static_cast<uint8_t>(ln & 0xff) : (b - 2 < ln ? pay[b - 2] : 0);
+    };
+    const bool lds_out = CW <= 2048 && (reinterpret_cast<uintptr_t>(a.cw) & 3) == 0;
+    uint8_t* cwb = lds_out ? reinterpret_cast<uint8_t*>(cwl) : a.cw;
+    int last = -1;
+    for (int c = tid; c < CW; c += 256) {
+        const int s = c / n, j = c - s * n;
+        uint8_t v = 0;
+        if (j < k) {
+            v = xbyte(s * k + j);
+        } else {  // parity: XOR_i G[i][j] * X_{t-(j-i)}[s][i], rows before the stream start = 0
+            for (int i = 0; i < k; ++i) {
+                const int r = ro[j - i];
+                if (r < 0) continue;
+                const int o = r + s * k + i;
+                const uint8_t xb = wst ? reinterpret_cast<const uint8_t*>(wst)[o] : a.win[o];
+                v ^= gmul(gexp, glog, Gs[i * n + j], xb);
+            }
+        }
+        cwb[c] = v;
+        if (v) last = c;
+    }
+    if (last >= 0) atomicMax(&last_nz, last);
+    __syncthreads();  // codeword complete; the window slot of seq - W (= seq % W) has been read
+    const int own = static_cast<int>(seq % W) * SK;
+    for (int b = tid; b < SK; b += 256) a.win[own + b] = xbyte(b);
+    if (lds_out)
+        for (int w = tid; 4 * w < CW; w += 256) reinterpret_cast<uint32_t*>(a.cw)[w] = cwl[w];
+    if (tid == 0) a.cw_len[0] = last_nz + 1;  // FEC_Encoder.cpp:55-60
+    if (a.done) {  // every thread's stores complete, then the completion word
+        __threadfence_system();
+        __syncthreads();
+        if (tid == 0) *reinterpret_cast<volatile uint32_t*>(a.done) = a.ticket;
+    }
 }
 
 // One wave per packet: lane = sub-stream (and sub-stream + 64, ...).
@@ -75,49 +137,100 @@ __global__ __launch_bounds__(256) void fec_streams_encode_kernel(StreamsEncArgs 
     __shared__ uint8_t gexp[512];
     __shared__ uint8_t glog[256];
     __shared__ uint8_t Gs[16 * 32];
+    __shared__ uint32_t prow[4][376];  // each wave's payload row (L <= 1500), read once with dword loads
+    __shared__ uint32_t wst[4][1024];  // each wave's window ring when it fits 4 KB: all loads in flight
+    __shared__ uint32_t cwst[512];     // single-packet calls: the codeword (CW <= 2048)
+    __shared__ int rowoff[4][32];      // per wave: window offset of packet seq - d (-1: before the stream)
     const int tid = threadIdx.x;
     for (int i = tid; i < 512; i += 256) gexp[i] = a.gf[i];
     for (int i = tid; i < 256; i += 256) glog[i] = a.gf[512 + i];
     for (int i = tid; i < a.k * a.n; i += 256) Gs[i] = a.G[i];
-    __syncthreads();
     const int m = blockIdx.x * 4 + (tid >> 6), lane = tid & 63;
+    if (m < a.M) {  // the payload may be a host-visible row: all loads in flight at once
+        const uint8_t* src = a.payload + static_cast<int64_t>(m) * a.L;
+        uint8_t* dst = reinterpret_cast<uint8_t*>(prow[tid >> 6]);
+        if (((a.L | static_cast<int>(reinterpret_cast<uintptr_t>(src))) & 3) == 0) {
+            for (int w = lane; 4 * w < a.L; w += 64) prow[tid >> 6][w] = reinterpret_cast<const uint32_t*>(src)[w];
+        } else {
+            for (int b = lane; b < a.L; b += 64) dst[b] = src[b];
+        }
+    }
+    const int wbytes = a.W * a.SK;
+    const bool wlds = wbytes <= 4096 && (wbytes & 3) == 0;
+    if (m < a.M && wlds) {
+        const uint32_t* wsrc = reinterpret_cast<const uint32_t*>(a.win + static_cast<int64_t>(a.ids ? a.ids[m] : 0) * wbytes);
+        for (int w = lane; 4 * w < wbytes; w += 64) wst[tid >> 6][w] = wsrc[w];
+    }
+    if (!a.ids) {
+        single_packet_encode(a, tid, gexp, glog, Gs, reinterpret_cast<const uint8_t*>(prow[0]), wlds ? wst[0] : nullptr,
+                             rowoff[0], cwst);
+        return;
+    }
+    __syncthreads();
     if (m >= a.M) return;
     const int L = a.L, k = a.k, n = a.n, S = a.S, CW = a.CW, SK = a.SK, W = a.W;
-    const int ln = a.len ? min(max(a.len[m], 0), L) : L;
-    const int64_t seq = a.seq[m];
-    uint8_t* win = a.win + static_cast<int64_t>(a.ids[m]) * W * SK;
-    const uint8_t* pay = a.payload + static_cast<int64_t>(m) * L;
+    const int ln = min(max(a.len ? a.len[m] : a.len1, 0), L);
+    const int64_t seq = a.seq ? a.seq[m] : a.seq1;
+    uint8_t* win = a.win + static_cast<int64_t>(a.ids ? a.ids[m] : 0) * W * SK;
+    const uint8_t* pay = reinterpret_cast<const uint8_t*>(prow[tid >> 6]);
     uint8_t* cwo = a.cw + static_cast<int64_t>(m) * CW;
+    // single-packet calls write the codeword into LDS first, then to the (host-visible) result row
+    // in dwords (the row is padded to whole dwords)
+    const bool lds_out = !a.ids && CW <= 2048 && (reinterpret_cast<uintptr_t>(cwo) & 3) == 0;
+    uint8_t* cwl = reinterpret_cast<uint8_t*>(cwst);
+    // window byte b of this packet: [len_hi, len_lo, payload, zero pad] (Encoder.cpp:75-83)
+    auto xbyte = [&](int b) -> uint8_t {
+        return b == 0 ? static_cast<uint8_t>(ln >> 8)
+                      : b == 1 ? static_cast<uint8_t>(ln & 0xff) : (b - 2 < ln ? pay[b - 2] : 0);
+    };
+    int* ro = rowoff[tid >> 6];
+    if (lane < 32) ro[lane] = (lane >= 1 && seq - lane >= 0) ? static_cast<int>((seq - lane) % W) * SK : -1;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    const int own = static_cast<int>(seq % W) * SK;
     int last = -1;  // last non-zero codeword byte of this lane's sub-streams
     for (int s = lane; s < S; s += 64) {
-        uint8_t x[16];
-        for (int i = 0; i < k; ++i) {  // window bytes s*k + i (Encoder.cpp:75-83, zero padded)
-            const int b = s * k + i;
-            x[i] = b == 0 ? static_cast<uint8_t>(ln >> 8)
-                          : b == 1 ? static_cast<uint8_t>(ln & 0xff) : (b - 2 < ln ? pay[b - 2] : 0);
-        }
         for (int j = 0; j < n; ++j) {
             uint8_t v;
             if (j < k) {
-                v = x[j];
+                v = xbyte(s * k + j);
             } else {  // parity: XOR_i G[i][j] * X_{t-(j-i)}[s][i], rows before the stream start = 0
                 v = 0;
                 for (int i = 0; i < k; ++i) {
-                    const int d = j - i;
-                    if (seq - d < 0) continue;
-                    const uint8_t xb = win[((seq - d) % W) * SK + s * k + i];
+                    const int r = ro[j - i];
+                    if (r < 0) continue;
+                    const int o = r + s * k + i;
+                    const uint8_t xb = wlds ? reinterpret_cast<const uint8_t*>(wst[tid >> 6])[o] : win[o];
                     v ^= gmul(gexp, glog, Gs[i * n + j], xb);
                 }
             }
-            cwo[s * n + j] = v;
+            if (lds_out)
+                cwl[s * n + j] = v;
+            else
+                cwo[s * n + j] = v;
             if (v) last = s * n + j;
         }
         // this lane's own bytes of slot seq % W: read above (d = W), now overwritten
-        for (int i = 0; i < k; ++i) win[(seq % W) * SK + s * k + i] = x[i];
+        for (int i = 0; i < k; ++i) win[own + s * k + i] = xbyte(s * k + i);
+    }
+    if (lds_out) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        for (int w = lane; 4 * w < CW; w += 64) reinterpret_cast<uint32_t*>(cwo)[w] = cwst[w];
     }
     for (int d = 32; d >= 1; d >>= 1) last = max(last, __shfl_xor(last, d, 64));
     if (lane == 0) a.cw_len[m] = last + 1;  // FEC_Encoder.cpp:55-60
+    if (a.done) {  // every lane's stores complete, then the completion word (one wave: M == 1)
+        __threadfence_system();
+        if (lane == 0) *reinterpret_cast<volatile uint32_t*>(a.done) = a.ticket;
+    }
 }
+
+template <class Sym>
+__device__ __forceinline__ void stream_output(const StreamsDecArgs& a, const StreamItem& it, uint8_t* orow, int m,
+                                              int lane, const uint8_t* gexp, const uint8_t* glog, Sym sym);
 
 // One wave per packet: store the received codeword in the stream's ring, output packet x.
 __global__ __launch_bounds__(256) void fec_streams_decode_kernel(StreamsDecArgs a) {
@@ -129,12 +242,24 @@ __global__ __launch_bounds__(256) void fec_streams_decode_kernel(StreamsDecArgs 
     __syncthreads();
     const int m = blockIdx.x * 4 + (tid >> 6), lane = tid & 63;
     if (m >= a.M) return;
-    const StreamItem it = a.items[m];
-    const int L = a.L, k = a.k, n = a.n, CW = a.CW, RR = a.RR;
+    const StreamItem it = a.items ? a.items[m] : a.item1;
+    const int L = a.L, CW = a.CW, RR = a.RR;
     uint8_t* ring = a.ring + static_cast<int64_t>(it.id) * RR * CW;
     const uint8_t* cwin = a.cw_in + static_cast<int64_t>(m) * CW;
-    if (!it.erased)  // FEC_Decoder.cpp:55-59: the decoder keeps its own copy
-        for (int b = lane; b < CW; b += 64) ring[(it.seq % RR) * CW + b] = cwin[b];
+    if (!it.erased) {  // FEC_Decoder.cpp:55-59: the decoder keeps its own copy
+        uint8_t* dst = ring + (it.seq % RR) * CW;
+        if (!a.items && (reinterpret_cast<uintptr_t>(cwin) & 3) == 0) {
+            // single packet from a host-visible row padded to whole dwords: dword loads, all in flight
+            for (int w = lane; 4 * w < CW; w += 64) {
+                const uint32_t v = reinterpret_cast<const uint32_t*>(cwin)[w];
+#pragma unroll
+                for (int e = 0; e < 4; ++e)
+                    if (4 * w + e < CW) dst[4 * w + e] = static_cast<uint8_t>(v >> (8 * e));
+            }
+        } else {
+            for (int b = lane; b < CW; b += 64) dst[b] = cwin[b];
+        }
+    }
     // symbol (s, q) of packet sp: this call's codeword straight from the input (the ring row it
     // was just written to is not read back), older ones from the ring
     auto sym = [&](int64_t sp, int o) -> uint8_t {
@@ -144,8 +269,19 @@ __global__ __launch_bounds__(256) void fec_streams_decode_kernel(StreamsDecArgs 
     if (it.fate == kNone || it.fate == kLost) {
         for (int b = lane; b < L; b += 64) orow[b] = 0;
         if (lane == 0) a.out_len[m] = 0;
-        return;
+    } else {
+        stream_output(a, it, orow, m, lane, gexp, glog, sym);
     }
+    if (a.done) {  // every lane's stores complete, then the completion word (one wave: M == 1)
+        __threadfence_system();
+        if (lane == 0) *reinterpret_cast<volatile uint32_t*>(a.done) = a.ticket;
+    }
+}
+
+template <class Sym>
+__device__ __forceinline__ void stream_output(const StreamsDecArgs& a, const StreamItem& it, uint8_t* orow, int m,
+                                              int lane, const uint8_t* gexp, const uint8_t* glog, Sym sym) {
+    const int L = a.L, k = a.k, n = a.n;
     const uint8_t* coef = a.coefs + static_cast<int64_t>(it.coef) * k * n;
     // header bytes 0, 1 (sub-stream 0, positions 0 and 1 -> (1/k)*n + 1%k) first: they bound the copy
     auto byte_at = [&](int h) -> uint8_t {
@@ -220,6 +356,65 @@ int stage_free(fec_streams* h) {
 }
 
 }  // namespace
+
+extern "C" {
+
+}  // extern "C"
+
+int fec::stream_encode_one(const CodecView& v, uint8_t* win, const uint8_t* payload, int payload_len, int64_t seq,
+                           uint8_t* cw, int32_t* cw_len, uint32_t* done, uint32_t ticket, hipStream_t s) {
+    if (v.k > 16 || v.k * v.n > 16 * 32) return FEC_ERR_ARG;  // the kernel's register / LDS bounds
+    fec::StreamsEncArgs a;
+    a.payload = payload;
+    a.len = nullptr;
+    a.ids = nullptr;
+    a.seq = nullptr;
+    a.win = win;
+    a.cw = cw;
+    a.cw_len = cw_len;
+    a.G = v.G;
+    a.gf = v.gf;
+    a.M = 1;
+    a.L = v.L;
+    a.k = v.k;
+    a.n = v.n;
+    a.S = v.S;
+    a.CW = v.CW;
+    a.SK = v.S * v.k;
+    a.W = std::max(1, v.n - 1);
+    a.seq1 = seq;
+    a.len1 = payload_len;
+    a.done = done;
+    a.ticket = ticket;
+    hipLaunchKernelGGL(fec::fec_streams_encode_kernel, dim3(1), dim3(256), 0, s, a);  // 256: the table loads
+    FS_TRY(hipGetLastError());
+    return FEC_OK;
+}
+
+int fec::stream_decode_one(const CodecView& v, uint8_t* ring, const uint8_t* cw, int64_t seq, int erased,
+                           int fate, int clamp, int64_t x, const uint8_t* coef, uint8_t* out, int32_t* out_len,
+                           uint32_t* done, uint32_t ticket, hipStream_t s) {
+    fec::StreamsDecArgs a;
+    a.cw_in = cw;
+    a.items = nullptr;
+    a.coefs = coef;
+    a.ring = ring;
+    a.gf = v.gf;
+    a.out = out;
+    a.out_len = out_len;
+    a.M = 1;
+    a.L = v.L;
+    a.k = v.k;
+    a.n = v.n;
+    a.CW = v.CW;
+    a.RR = kRR;
+    a.item1 = fec::StreamItem{0, fate, clamp, 0, seq, x, erased, 0};
+    a.done = done;
+    a.ticket = ticket;
+    hipLaunchKernelGGL(fec::fec_streams_decode_kernel, dim3(1), dim3(256), 0, s, a);  // 256: the table loads
+    FS_TRY(hipGetLastError());
+    return FEC_OK;
+}
 
 extern "C" {
 
@@ -306,6 +501,10 @@ int fec_streams_encode(fec_streams* h, const int32_t* ids, int M, const uint8_t*
     a.CW = h->g.CW;
     a.SK = h->SK;
     a.W = h->W;
+    a.seq1 = 0;
+    a.len1 = h->g.L;
+    a.done = nullptr;
+    a.ticket = 0;
     hipLaunchKernelGGL(fec::fec_streams_encode_kernel, dim3((M + 3) / 4), dim3(256), 0, s, a);
     FS_TRY(hipGetLastError());
     return FEC_OK;
@@ -368,6 +567,8 @@ int fec_streams_decode(fec_streams* h, const int32_t* ids, int M, const uint8_t*
     a.n = g.n;
     a.CW = g.CW;
     a.RR = fec::kRR;
+    a.done = nullptr;
+    a.ticket = 0;
     hipLaunchKernelGGL(fec::fec_streams_decode_kernel, dim3((M + 3) / 4), dim3(256), 0, s, a);
     FS_TRY(hipGetLastError());
     return FEC_OK;
