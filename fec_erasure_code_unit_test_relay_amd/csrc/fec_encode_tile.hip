@@ -326,7 +326,24 @@ __device__ __forceinline__ void tile_walk(const EncTileArgs& a, uint8_t* smem) {
             const int rb = p * RS + 4 * K * g;  // byte of row dword K*g
             uint32_t D[K + 1];
             D[0] = *reinterpret_cast<const uint32_t*>(in + rb - 4);
-            if constexpr (K % 4 == 0) {
+            if constexpr (K == 8) {
+                // 16-byte reads from asm: left to the compiler, the L = 300 instance's loads are
+                // re-paired with D[0] into ds_read2_b32 (32-bank groups: 4-way conflicts here,
+                // SQ_LDS_BANK_CONFLICT 19.3 M per launch vs 8.3 M with ds_read_b128)
+                tv4u v0, v1;
+                asm volatile("ds_read_b128 %0, %2\n\tds_read_b128 %1, %2 offset:16\n\ts_waitcnt lgkmcnt(0)"
+                             : "=&v"(v0), "=&v"(v1)
+                             : "v"(lds_addr(in + rb))
+                             : "memory");
+                D[1] = v0.x;
+                D[2] = v0.y;
+                D[3] = v0.z;
+                D[4] = v0.w;
+                D[5] = v1.x;
+                D[6] = v1.y;
+                D[7] = v1.z;
+                D[8] = v1.w;
+            } else if constexpr (K % 4 == 0) {
 #pragma unroll
                 for (int m = 0; m < K; m += 4) {
                     const uint4 v = *reinterpret_cast<const uint4*>(in + rb + 4 * m);

@@ -17,16 +17,17 @@ ap.add_argument("--reps", type=int, default=7)
 ap.add_argument("--ab", default="", help="comma-separated FEC_WAVE_DBG values (or VAR=value) timed in one process")
 ap.add_argument("--tbn", default="10,3,3")
 ap.add_argument("--packets", type=int, default=1_000_010)
+ap.add_argument("--L", type=int, default=300, help="payload size (300: the kernels specialised on L = 300)")
 args = ap.parse_args()
 T, B, N = map(int, args.tbn.split(","))
 torch.cuda.set_device(0)
-c = Codec(300, T, B, N)
+c = Codec(args.L, T, B, N)
 c.set_encode_path(args.path)
 P = args.packets
 ap2 = os.environ.get("ENC_SHIFT_MB")
 if ap2:  # experiment: shift the allocations by a dummy block
     _dummy = torch.empty(int(float(ap2) * 2**20), dtype=torch.uint8, device="cuda")
-payload = fill_payload(0, P, 300, 0x5EED)
+payload = fill_payload(0, P, args.L, 0x5EED)
 cw = torch.empty((P, c.CW), dtype=torch.uint8, device="cuda")
 wl = torch.empty(P, dtype=torch.int32, device="cuda")
 for _ in range(3):
@@ -58,5 +59,5 @@ for _ in range(args.reps):  # median of several timed batches (box-to-box and cl
     samples.append(e0.elapsed_time(e1) * 1e3 / args.iters)
 us = sorted(samples)[len(samples) // 2]
 print(f"payload@{payload.data_ptr():#x} cw@{cw.data_ptr():#x} "
-      f"{args.path} {args.tbn} P={P}: {us:.1f} us/launch, {(300 + c.CW) * P / us / 1e3:.0f} GB/s algorithmic",
+      f"{args.path} {args.tbn} P={P}: {us:.1f} us/launch, {(args.L + c.CW) * P / us / 1e3:.0f} GB/s algorithmic",
       flush=True)
