@@ -600,6 +600,8 @@ int launch_encode_tile(fec_codec* c, const uint8_t* d_payload, const int32_t* d_
     a.off_scratch = c->tile_off[8];
     a.dbg = 0;
     if (const char* v = std::getenv("FEC_TILE_DBG")) a.dbg = std::atoi(v);
+    a.nt = 0;
+    if (const char* v = std::getenv("FEC_TILE_NT")) a.nt = std::atoi(v) ? 1 : 0;
     const int64_t blocks = (ntiles + tpw - 1) / tpw;
     hipEvent_t stop;
     if (int st = c->begin(FEC_KERNEL_ENCODE, s, &stop)) return st;
@@ -854,7 +856,9 @@ int launch_copy(fec_codec* c, const uint8_t* d_cw, const uint8_t* d_er, int64_t 
         fa.out_bytes = round16(fa.TP * g.L);
         fa.stamps = (c->stamp_kernel == FEC_KERNEL_DEC_COPY) ? c->d_stamps : nullptr;
         fa.skip_erased = 0;
-        fa.nt = 0;
+        // non-temporal codeword loads and payload stores: 0.318 vs 0.338 ms per bench step
+        // (tools/step_ab.py, same process, profiles/r02/decode_diag/copy_nt_ab.txt)
+        fa.nt = 1;
         if (const char* v = std::getenv("FEC_COPY_NT")) fa.nt = std::atoi(v) ? 1 : 0;
         const int64_t blocks = (Pout + fa.TP - 1) / fa.TP;
         hipEvent_t stop;

@@ -489,7 +489,11 @@ __device__ __forceinline__ void tile_walk(const EncTileArgs& a, uint8_t* smem) {
                 const bool full = inb && c + 16 <= lim;
                 typedef uint32_t v4u __attribute__((ext_vector_type(4)));
                 const v4u vv = {v.x, v.y, v.z, v.w};
-                __builtin_amdgcn_raw_buffer_store_b128(vv, rc, full && !(dbg & 4) ? gbase + c : 0x7ffffff0, 0, 0);
+                const int so = full && !(dbg & 4) ? gbase + c : 0x7ffffff0;
+                if (a.nt)
+                    __builtin_amdgcn_raw_buffer_store_b128(vv, rc, so, 0, 2);  // nt
+                else
+                    __builtin_amdgcn_raw_buffer_store_b128(vv, rc, so, 0, 0);
             }
             // trimmed wire size of packet tid (FEC_Encoder.cpp:55-60): 1 + last non-zero byte
             const bool own = tid < R && row0 + tid < P;

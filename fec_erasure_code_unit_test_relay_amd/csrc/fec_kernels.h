@@ -106,6 +106,7 @@ struct EncTileArgs {
     int off_scratch;              // 1 KB: a dword per thread for writes that must land nowhere
     int dbg;                      // timing experiments only (FEC_TILE_DBG): 1 no parity products,
                                   // 2 no codeword words, 4 no output stores
+    int nt;                       // 1: codeword stores non-temporal (FEC_TILE_NT)
 };
 
 // Geometry of the tile encoder for (k, n-k, L): one definition for the host launcher and the
