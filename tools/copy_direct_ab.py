@@ -16,7 +16,7 @@ P, T = 1_000_000, 10
 Pf = P + T
 payload = fill_payload(0, Pf, L, 0x5EED)
 er = torch.from_numpy(stream_pattern(Pf, 0)).cuda()
-variants = [(32, 0), (32, 1), (64, 1), (16, 1), (32, 0), (32, 1)]
+variants = [(int(v.split(":")[0]), int(v.split(":")[1])) for v in sys.argv[1:]] or [(32, 0), (32, 1), (64, 1), (16, 1), (32, 0), (32, 1)]
 ref = None
 for tp, d in variants:
     os.environ["FEC_COPY_TILE"] = str(tp)
