@@ -195,7 +195,10 @@ int fec_debug_stamps(fec_codec *codec, int kernel, void *d_stamps);
  * length goes to *codeword_size, bytes past it are zero).
  * fec_decoder_receive = FEC_Decoder::onReceive: codeword/codeword_size = wire bytes (ignored when
  * erasure != 0), seq consecutive from 0; writes packet seq-T's payload to payload_out
- * (max_payload bytes, zero beyond) and its length to *payload (0 = lost / not yet available). */
+ * (max_payload bytes, zero beyond) and its length to *payload (0 = lost / not yet available).
+ * Each call is one kernel launch (the stream-group kernels of fec_streams.hip on a one-stream
+ * window / ring) reading and writing pinned, mapped host rows, and a poll of a completion word
+ * (FEC_STREAM_SPIN=0: hipStreamSynchronize instead).  The encoder needs k = T-N+1 <= 16. */
 int fec_encoder_create(int max_payload, int T, int B, int N, fec_encoder **out);
 int fec_encoder_destroy(fec_encoder *enc);
 int fec_encoder_transmit(fec_encoder *enc, const uint8_t *data, int payload, int seq,
