@@ -105,6 +105,126 @@ def cpu_baseline(T, B, N, packets, rank_pattern, threads=None):
                             "erased": res1[0][0], "lost": res1[0][1]}}
 
 
+def host_inclusive(codec, payload, pat, er, cw, wl, out, ol, P, Pf, world, barrier, max_time, reduce):
+    """End-to-end rate from/to pinned host memory on every rank (north_star: the path starts and
+    ends in UDP socket buffers): H2D payload, encode, D2H wire codewords, H2D codewords + erasures,
+    decode, D2H payloads + lengths.  Each rank drives its own GPU's PCIe link; the job's time is the
+    slowest rank's between two barriers, and `value` is the payload of all ranks over that time."""
+    import torch
+    from fec_erasure_code_unit_test_relay_amd import DecodeStream
+    h_payload = payload.cpu().pin_memory()
+    h_cw = torch.empty_like(cw, device="cpu").pin_memory()
+    h_wl = torch.empty_like(wl, device="cpu").pin_memory()
+    h_out = torch.empty_like(out, device="cpu").pin_memory()
+    h_ol = torch.empty_like(ol, device="cpu").pin_memory()
+    h_er = torch.from_numpy(pat).pin_memory()
+    d_in = torch.empty_like(payload)
+    d_cw2 = torch.empty_like(cw)
+    d_er2 = torch.empty_like(er)
+
+    def host_step():
+        d_in.copy_(h_payload, non_blocking=True)
+        codec.encode(d_in, out=cw, out_len=wl)
+        h_cw.copy_(cw, non_blocking=True)
+        h_wl.copy_(wl, non_blocking=True)
+        d_cw2.copy_(h_cw, non_blocking=True)
+        d_er2.copy_(h_er, non_blocking=True)
+        codec.decode(d_cw2, d_er2, out=out, out_len=ol)
+        h_out.copy_(out, non_blocking=True)
+        h_ol.copy_(ol, non_blocking=True)
+
+    # The same work in NC chunks on two streams, one per PCIe direction, software-pipelined
+    # (chunk i+1 goes up and is encoded while chunk i's codewords come down): the encoder sees
+    # the chunk in front as history, the decoder is the continuing one
+    # (fec_decode_stream_push), so the outputs are the one-shot decode's.  Measured on the box
+    # (tools/pcie_duplex.py): one large H2D and one large D2H on two streams do not overlap
+    # (57 GB/s together, as either alone); interleaved 64 MB chunks reach 83 GB/s.  4 chunks
+    # beat 8, 16 and 32 here (tools/host_pipe_exp.py: 21.4 / 26.6 / 39.1 / 38.5 ms).
+    NC = 4
+    cuts = [Pf * i // NC for i in range(NC + 1)]
+    s_up, s_dn = torch.cuda.Stream(), torch.cuda.Stream()
+
+    def host_step_pipelined():
+        ds = DecodeStream(codec)
+        cur = torch.cuda.current_stream()
+        s_up.wait_stream(cur)
+        s_dn.wait_stream(cur)
+        ev_d = [None] * NC
+        nout = [0]
+
+        def send(i):
+            a, b = cuts[i], cuts[i + 1]
+            with torch.cuda.stream(s_up):
+                d_in[a:b].copy_(h_payload[a:b], non_blocking=True)
+                h = min(a, codec.n - 1)
+                codec.encode(d_in[a - h:b], history=h, out=cw[a:b], out_len=wl[a:b])
+                ev = torch.cuda.Event()
+                ev.record()
+            with torch.cuda.stream(s_dn):
+                s_dn.wait_event(ev)
+                h_cw[a:b].copy_(cw[a:b], non_blocking=True)
+                h_wl[a:b].copy_(wl[a:b], non_blocking=True)
+                ev_d[i] = torch.cuda.Event()
+                ev_d[i].record()
+
+        def receive(i):
+            a, b = cuts[i], cuts[i + 1]
+            n0 = nout[0]
+            with torch.cuda.stream(s_up):
+                s_up.wait_event(ev_d[i])
+                d_cw2[a:b].copy_(h_cw[a:b], non_blocking=True)
+                d_er2[a:b].copy_(h_er[a:b], non_blocking=True)
+                o, _ = ds.push(d_cw2[:b], d_er2[:b], pat[:b], history=a, out=out[n0:], out_len=ol[n0:])
+                ev = torch.cuda.Event()
+                ev.record()
+            m = o.shape[0]
+            with torch.cuda.stream(s_dn):
+                s_dn.wait_event(ev)
+                h_out[n0:n0 + m].copy_(out[n0:n0 + m], non_blocking=True)
+                h_ol[n0:n0 + m].copy_(ol[n0:n0 + m], non_blocking=True)
+            nout[0] += m
+
+        send(0)
+        for i in range(NC):
+            if i + 1 < NC:
+                send(i + 1)
+            receive(i)
+        cur.wait_stream(s_up)
+        cur.wait_stream(s_dn)
+        return nout[0]
+
+    def timed_all(fn, reps):
+        fn()
+        torch.cuda.synchronize()
+        barrier()
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            r = fn()
+        torch.cuda.synchronize()
+        barrier()
+        return max_time((time.perf_counter() - t0) / reps), r
+
+    hs = 3
+    he, _ = timed_all(host_step, hs)
+    ref_out, ref_ol = h_out.clone(), h_ol.clone()
+    h_out.zero_()
+    hp, nout = timed_all(host_step_pipelined, hs)
+    pipe_ok = nout == P and bool(torch.equal(h_out, ref_out)) and bool(torch.equal(h_ol, ref_ol))
+    # the serialised run's output against the source payloads (lost rows are zero-length)
+    ok_rows = ref_ol != 0
+    ser_ok = bool(torch.equal(ref_out[ok_rows], h_payload[:P][ok_rows]))
+    (verified_ranks,) = reduce([int(pipe_ok and ser_ok)])
+    return {"value": round(world * P * L / hp / 2**30, 3), "unit": "GiB/s",
+            "ms_per_step": round(hp * 1e3, 3), "n_gpus": world,
+            "note": f"pinned host buffers; per rank: H2D payload, encode, D2H codewords, H2D "
+                    f"codewords+erasures, continuing decode, D2H payloads+lengths in {NC} chunks on 2 "
+                    f"streams (one per PCIe direction, pipelined); value = payload of all {world} "
+                    f"rank(s) / slowest rank's time",
+            "verified": verified_ranks == world,
+            "serialised_one_stream": {"value": round(world * P * L / he / 2**30, 3),
+                                      "ms_per_step": round(he * 1e3, 3)}}
+
+
 def timed(fn, steps):
     import torch
     fn()
@@ -245,6 +365,81 @@ def multistream(steps, NS=10000):
             "verified": ok}
 
 
+def launch_mode(gpus: int, env) -> str:
+    """How this process takes part in a --gpus N run.
+
+    'spawn': no WORLD_SIZE in the environment and N > 1 -- this process is the launcher; it starts N
+    rank processes (spawn_ranks) and never touches the GPU itself.  'run': it is a rank (WORLD_SIZE
+    set by torchrun or by spawn_ranks, or N == 1).  A WORLD_SIZE that disagrees with --gpus is an
+    error: the JSON line would report a different n_gpus than the one asked for."""
+    if gpus < 1:
+        raise SystemExit(f"bench.py: --gpus must be >= 1 (got {gpus})")
+    ws = env.get("WORLD_SIZE")
+    if ws is None or ws == "":
+        return "spawn" if gpus > 1 else "run"
+    if int(ws) != gpus:
+        raise SystemExit(f"bench.py: WORLD_SIZE={ws} but --gpus {gpus}: launch {gpus} ranks "
+                         f"(torchrun --nproc-per-node {gpus}) or drop WORLD_SIZE")
+    return "run"
+
+
+def _free_port() -> int:
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def spawn_ranks(n: int, argv) -> int:
+    """Start n rank processes of this script (one per GPU: RANK = LOCAL_RANK = r, WORLD_SIZE = n,
+    rendezvous on 127.0.0.1) and wait for them.  The launcher never initialises the GPU, so the
+    ranks are fresh processes, not forks or execs of a GPU process.  If a rank fails, the others
+    (which would wait forever in a collective) are terminated; the exit code is the first failing
+    rank's, else 0.  Rank 0 prints the JSON line on the inherited stdout."""
+    import subprocess
+    port = os.environ.get("MASTER_PORT") or str(_free_port())
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n),
+                   LOCAL_WORLD_SIZE=str(n), GROUP_RANK="0", MASTER_ADDR="127.0.0.1",
+                   MASTER_PORT=port)
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + list(argv), env=env))
+    rc = 0
+    live = list(procs)
+    while live:
+        for p in list(live):
+            code = p.poll()
+            if code is None:
+                continue
+            live.remove(p)
+            if code != 0 and rc == 0:
+                rc = code if code > 0 else 128 - code
+                for q in live:
+                    q.terminate()
+        time.sleep(0.05)
+    for p in procs:
+        p.wait()
+    return rc
+
+
+def launch_selftest(world: int, rank: int) -> None:
+    """--launch-selftest: the rank side of spawn_ranks without a GPU (CPU test of the launcher):
+    gloo rendezvous, one all-reduce of the ranks, rank 0 prints what it saw."""
+    import torch
+    import torch.distributed as dist
+    if world > 1:
+        dist.init_process_group(backend="gloo")
+    t = torch.tensor([rank, 1], dtype=torch.int64)
+    if world > 1:
+        dist.all_reduce(t)
+    if rank == 0:
+        print(json.dumps({"n_gpus": world, "rank_sum": int(t[0]), "ranks": int(t[1]),
+                          "master": os.environ.get("MASTER_ADDR")}), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -263,20 +458,32 @@ def main():
                          "(20 timed steps after 5 warm-up: 0.400 ms/step, after 100: 0.355)")
     ap.add_argument("--no-graph", action="store_true",
                     help="launch the step's kernels one by one instead of replaying a captured hipGraph")
+    ap.add_argument("--launch-selftest", action="store_true",
+                    help="CPU test of the --gpus launcher: ranks rendezvous over gloo, no GPU work")
     args = ap.parse_args()
     T, B, N = map(int, args.tbn.split(","))
+
+    if launch_mode(args.gpus, os.environ) == "spawn":
+        sys.exit(spawn_ranks(args.gpus, sys.argv[1:]))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.launch_selftest:
+        launch_selftest(world, rank)
+        return
 
     import torch
     import torch.distributed as dist
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
     # FEC_BENCH_BACKEND=gloo rehearses the multi-rank bench on a box with fewer GPUs than ranks
     # (ranks share devices round-robin, collectives on host tensors); the driver's runs use RCCL.
     backend = os.environ.get("FEC_BENCH_BACKEND", "nccl")
+    ndev = torch.cuda.device_count()
     if backend != "nccl":
-        local = local % max(1, torch.cuda.device_count())
+        local = local % max(1, ndev)
+    elif local >= ndev:
+        raise SystemExit(f"bench.py: rank {rank} has LOCAL_RANK {local} but only {ndev} GPUs are "
+                         f"visible (set FEC_BENCH_BACKEND=gloo to rehearse ranks on shared GPUs)")
     torch.cuda.set_device(local)
     comm_dev = "cuda" if backend == "nccl" else "cpu"
     if world > 1:
@@ -442,117 +649,12 @@ def main():
                                       traffic_source=tr[1])
         elif tr:
             result["roofline"].update(traffic_stale=f"{tr[1]} was measured on other kernel sources")
-    if world == 1 and not args.no_host_inclusive:
-        # end-to-end from/to host memory (pinned): H2D payload, encode, D2H wire codewords,
-        # H2D codewords + erasures, decode, D2H payloads + lengths
-        h_payload = payload.cpu().pin_memory()
-        h_cw = torch.empty_like(cw, device="cpu").pin_memory()
-        h_wl = torch.empty_like(wl, device="cpu").pin_memory()
-        h_out = torch.empty_like(out, device="cpu").pin_memory()
-        h_ol = torch.empty_like(ol, device="cpu").pin_memory()
-        h_er = torch.from_numpy(pat).pin_memory()
-        d_in = torch.empty_like(payload)
-        d_cw2 = torch.empty_like(cw)
-        d_er2 = torch.empty_like(er)
-
-        def host_step():
-            d_in.copy_(h_payload, non_blocking=True)
-            codec.encode(d_in, out=cw, out_len=wl)
-            h_cw.copy_(cw, non_blocking=True)
-            h_wl.copy_(wl, non_blocking=True)
-            d_cw2.copy_(h_cw, non_blocking=True)
-            d_er2.copy_(h_er, non_blocking=True)
-            codec.decode(d_cw2, d_er2, out=out, out_len=ol)
-            h_out.copy_(out, non_blocking=True)
-            h_ol.copy_(ol, non_blocking=True)
-
-        # The same work in NC chunks on two streams, one per PCIe direction, software-pipelined
-        # (chunk i+1 goes up and is encoded while chunk i's codewords come down): the encoder sees
-        # the chunk in front as history, the decoder is the continuing one
-        # (fec_decode_stream_push), so the outputs are the one-shot decode's.  Measured on the box
-        # (tools/pcie_duplex.py): one large H2D and one large D2H on two streams do not overlap
-        # (57 GB/s together, as either alone); interleaved 64 MB chunks reach 83 GB/s.  4 chunks
-        # beat 8, 16 and 32 here (tools/host_pipe_exp.py: 21.4 / 26.6 / 39.1 / 38.5 ms).
-        from fec_erasure_code_unit_test_relay_amd import DecodeStream
-        NC = 4
-        cuts = [Pf * i // NC for i in range(NC + 1)]
-        s_up, s_dn = torch.cuda.Stream(), torch.cuda.Stream()
-
-        def host_step_pipelined():
-            ds = DecodeStream(codec)
-            cur = torch.cuda.current_stream()
-            s_up.wait_stream(cur)
-            s_dn.wait_stream(cur)
-            ev_d = [None] * NC
-            nout = [0]
-
-            def send(i):
-                a, b = cuts[i], cuts[i + 1]
-                with torch.cuda.stream(s_up):
-                    d_in[a:b].copy_(h_payload[a:b], non_blocking=True)
-                    h = min(a, codec.n - 1)
-                    codec.encode(d_in[a - h:b], history=h, out=cw[a:b], out_len=wl[a:b])
-                    ev = torch.cuda.Event()
-                    ev.record()
-                with torch.cuda.stream(s_dn):
-                    s_dn.wait_event(ev)
-                    h_cw[a:b].copy_(cw[a:b], non_blocking=True)
-                    h_wl[a:b].copy_(wl[a:b], non_blocking=True)
-                    ev_d[i] = torch.cuda.Event()
-                    ev_d[i].record()
-
-            def receive(i):
-                a, b = cuts[i], cuts[i + 1]
-                n0 = nout[0]
-                with torch.cuda.stream(s_up):
-                    s_up.wait_event(ev_d[i])
-                    d_cw2[a:b].copy_(h_cw[a:b], non_blocking=True)
-                    d_er2[a:b].copy_(h_er[a:b], non_blocking=True)
-                    o, _ = ds.push(d_cw2[:b], d_er2[:b], pat[:b], history=a, out=out[n0:], out_len=ol[n0:])
-                    ev = torch.cuda.Event()
-                    ev.record()
-                m = o.shape[0]
-                with torch.cuda.stream(s_dn):
-                    s_dn.wait_event(ev)
-                    h_out[n0:n0 + m].copy_(out[n0:n0 + m], non_blocking=True)
-                    h_ol[n0:n0 + m].copy_(ol[n0:n0 + m], non_blocking=True)
-                nout[0] += m
-
-            send(0)
-            for i in range(NC):
-                if i + 1 < NC:
-                    send(i + 1)
-                receive(i)
-            cur.wait_stream(s_up)
-            cur.wait_stream(s_dn)
-            return nout[0]
-
-        host_step()
-        torch.cuda.synchronize()
-        hs = 3
-        t0 = time.perf_counter()
-        for _ in range(hs):
-            host_step()
-        torch.cuda.synchronize()
-        he = (time.perf_counter() - t0) / hs
-        ref_out, ref_ol = h_out.clone(), h_ol.clone()
-        h_out.zero_()
-        nout = host_step_pipelined()
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        for _ in range(hs):
-            host_step_pipelined()
-        torch.cuda.synchronize()
-        hp = (time.perf_counter() - t0) / hs
-        pipe_ok = nout == P and bool(torch.equal(h_out, ref_out)) and bool(torch.equal(h_ol, ref_ol))
-        result["host_inclusive"] = {"value": round(P * L / hp / 2**30, 3), "unit": "GiB/s",
-                                    "ms_per_step": round(hp * 1e3, 3),
-                                    "note": f"pinned host buffers; H2D payload, encode, D2H codewords, H2D "
-                                            f"codewords+erasures, continuing decode, D2H payloads+lengths in "
-                                            f"{NC} chunks on 2 streams (one per PCIe direction, pipelined)",
-                                    "verified": pipe_ok,
-                                    "serialised_one_stream": {"value": round(P * L / he / 2**30, 3),
-                                                              "ms_per_step": round(he * 1e3, 3)}}
+    if not args.no_host_inclusive:
+        hi = host_inclusive(codec, payload, pat, er, cw, wl, out, ol, P, Pf, world, barrier,
+                            lambda x: max_over_ranks(x, dist, comm_dev),
+                            lambda v: reduce_counters(v, dist, comm_dev))
+        if rank == 0:
+            result["host_inclusive"] = hi
     if rank == 0 and world == 1 and not args.no_extra_configs:
         result["configs"] = extra_configs()
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
