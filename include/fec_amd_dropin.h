@@ -1,6 +1,6 @@
 // fec_amd_dropin.h -- the reference's C++ API for the coding path, re-implemented over the
 // MI355X C ABI (fec_amd.h) so that Variable_Rate_FEC_Encoder / Variable_Rate_FEC_Decoder /
-// Application_Layer_Sender / Application_Layer_Receiver build against it unchanged.
+// Application_Layer_Sender / Application_Layer_Receiver compile against it (tests/test_dropin_compile.py).
 //
 //   reference header                     | here
 //   include/Memory_Allocator.h:17-31     | Memory_Allocator (ring of 33000-byte buffers)
@@ -20,7 +20,23 @@
 // std::runtime_error -- the reference has no error channel at all.
 #pragma once
 
+// The transitive surface of the six reference headers this one replaces (FEC_Encoder.h:17-24,
+// FEC_Decoder.h:17-25, Memory_Allocator.h:17, Encoder.h -> Encoder_Basic.h -> ... ): their callers
+// (Variable_Rate_FEC_Encoder.cpp, Variable_Rate_FEC_Decoder.cpp, Decoder_Symbol_Wise.cpp,
+// Application_Layer_Sender/Receiver.cpp) use std::string, std::ofstream, ceil, memcpy and the
+// <random> engines without including them.  tests/test_dropin_compile.py compiles those callers
+// against this header.
+#include <cmath>
 #include <cstdint>
+#include <cstdlib>
+#include <cstring>
+#include <fstream>
+#include <iostream>
+#include <random>
+#include <string>
+
+using std::string;
+using std::ofstream;
 
 struct fec_encoder;
 struct fec_decoder;
