@@ -90,10 +90,11 @@ class Codec:
         check(lib().fec_codec_set_encode_path(self._h, code), "fec_codec_set_encode_path")
 
     def set_copy_path(self, path: str) -> None:
-        """'auto', 'generic', 'fast' (LDS tiles), 'wave' (barrier-free) or 'tile' (persistent
+        """'auto', 'generic', 'fast' (LDS tiles), 'wave' (barrier-free), 'chunk' (a lane per 16-byte
+        output piece, k | 16) or 'tile' (persistent
         per-workgroup tile runs, register-staged prefetch) for the decoder's received-packet
         kernel."""
-        code = {"auto": 0, "generic": 1, "fast": 2, "wave": 3, "tile": 4}[path]
+        code = {"auto": 0, "generic": 1, "fast": 2, "wave": 3, "tile": 4, "chunk": 5}[path]
         check(lib().fec_codec_set_copy_path(self._h, code), "fec_codec_set_copy_path")
 
     def info(self) -> dict:

@@ -77,6 +77,8 @@ struct fec_codec {
     const void* copy_fast = nullptr;  // specialised decode copy kernel (LDS tiles)
     int copyf_tp = 0;
     const void* copy_wave = nullptr;  // barrier-free decode copy (fec_copy_wave.hip)
+    const void* copy_chunk = nullptr; // one lane per 16-byte output piece (fec_copy_chunk.hip), k | 16
+    int copyc_grid = 0;               // its grid: resident workgroups
     int copy_path = 0;           // 0 auto, 1 generic, 2 specialised (LDS tiles), 3 wave
     int plan_path = 0;
     int dedup = 1;               // episode-shape deduplication in the planner
@@ -322,6 +324,19 @@ int codec_init(fec_codec* c, int max_payload, int T, int B, int N) {
     if (!c->copyf_tp) c->copy_fast = nullptr;
     if ((g.L & 3) == 0 && (g.S + 3) / 4 <= 64 && g.T < 4 * ((g.S + 3) / 4))
         c->copy_wave = fec::fec_copy_wave_kernel_for(g.k, g.n - g.k);
+    if ((g.L & 3) == 0 && g.T <= 12) {
+        c->copy_chunk = fec::fec_copy_chunk_kernel_for(g.k, g.n - g.k);
+        if (c->copy_chunk) {
+            int dev = 0, cus = 0, per_cu = 0;
+            HIP_TRY(hipGetDevice(&dev));
+            HIP_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+            HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, c->copy_chunk, 256, 0));
+            int wpc = per_cu;
+            if (const char* v = std::getenv("FEC_CHUNK_WGPC")) wpc = std::max(1, std::min(per_cu, std::atoi(v)));
+            c->copyc_grid = cus * wpc;
+            if (c->copyc_grid <= 0) c->copy_chunk = nullptr;
+        }
+    }
     // experiments (FEC_SIDE_CUS / FEC_SIDE_PRIO): the planner's side stream on a CU subset, or at
     // the lowest / highest stream priority
     const char* side_cus = std::getenv("FEC_SIDE_CUS");
@@ -803,6 +818,37 @@ int launch_copy(fec_codec* c, const uint8_t* d_cw, const uint8_t* d_er, int64_t 
         if (int st = c->begin(FEC_KERNEL_DEC_COPY, s, &stop)) return st;
         void* args[] = {&wa};
         HIP_TRY(hipLaunchKernel(c->copy_wave, dim3(static_cast<unsigned>(blocks)), dim3(256), args, 0, s));
+        return c->end(stop, s);
+    }
+    // one lane per 16-byte output piece: every offset fits 31 bits, with two grid strides to spare
+    const int64_t nchunks = Pout * ((g.L + 15) / 16);
+    const bool chunk_ok = c->copy_chunk && (reinterpret_cast<uintptr_t>(d_out) & 3) == 0 &&
+                          P * g.CW < (int64_t(1) << 31) - 64 &&
+                          nchunks + 2 * int64_t(c->copyc_grid) * 256 < (int64_t(1) << 31);
+    if (c->copy_path == 5 && !chunk_ok) return FEC_ERR_ARG;
+    if (chunk_ok && c->copy_path == 5) {
+        fec::CopyChunkArgs ka;
+        ka.cw = d_cw;
+        ka.er = d_er;
+        ka.out = d_out;
+        ka.out_len = d_outlen;
+        ka.cw_bytes = static_cast<int>(P * g.CW);
+        ka.er_bytes = static_cast<int>(P);
+        ka.out_bytes = static_cast<int>(Pout * g.L);
+        ka.L = g.L;
+        ka.CW = g.CW;
+        ka.T = g.T;
+        ka.C = (g.L + 15) / 16;
+        ka.cmagic = static_cast<uint32_t>((uint64_t(1) << 32) / uint64_t(ka.C) + 1);
+        ka.nchunks = static_cast<int>(nchunks);
+        ka.nt = 1;
+        if (const char* v = std::getenv("FEC_COPY_NT")) ka.nt = std::atoi(v) ? 1 : 0;
+        const int64_t need = (nchunks + 511) / 512;  // two chunks per lane
+        const unsigned blocks = static_cast<unsigned>(std::max<int64_t>(1, std::min<int64_t>(need, c->copyc_grid)));
+        hipEvent_t stop;
+        if (int st = c->begin(FEC_KERNEL_DEC_COPY, s, &stop)) return st;
+        void* args[] = {&ka};
+        HIP_TRY(hipLaunchKernel(c->copy_chunk, dim3(blocks), dim3(256), args, 0, s));
         return c->end(stop, s);
     }
     const bool tile_ok = c->copy_tile && (reinterpret_cast<uintptr_t>(d_out) & 15) == 0 &&
@@ -1287,7 +1333,9 @@ int fec_codec_info(const fec_codec* c, char* buf, size_t size) {
     else
         std::snprintf(enc, sizeof(enc), "fec_encode_kernel");
     char cpy[64];
-    if (c->copy_wave && c->copy_path == 3)
+    if (c->copy_chunk && c->copy_path == 5)
+        std::snprintf(cpy, sizeof(cpy), "fec_copy_chunk_kernel<%d, %d>", c->g.k, np);
+    else if (c->copy_wave && c->copy_path == 3)
         std::snprintf(cpy, sizeof(cpy), "fec_copy_wave_kernel<%d, %d>", c->g.k, np);
     else if (c->copy_tile && c->copy_path == 4)
         std::snprintf(cpy, sizeof(cpy), "fec_copy_tile_kernel<%d, %d>", c->g.k, np);
@@ -1338,7 +1386,8 @@ int fec_codec_set_plan_path(fec_codec* c, int path) {
 }
 
 int fec_codec_set_copy_path(fec_codec* c, int path) {
-    if (!c || path < 0 || path > 4) return FEC_ERR_ARG;
+    if (!c || path < 0 || path > 5) return FEC_ERR_ARG;
+    if (path == 5 && !c->copy_chunk) return FEC_ERR_ARG;
     if (path == 4 && !c->copy_tile) return FEC_ERR_ARG;
     if (path == 2 && !c->copy_fast) return FEC_ERR_ARG;
     if (path == 3 && !c->copy_wave) return FEC_ERR_ARG;

@@ -212,6 +212,20 @@ struct CopyWaveArgs {
 };
 const void* fec_copy_wave_kernel_for(int k, int np);
 
+// Received-packet decode, one lane per 16-byte output piece, no LDS (fec_copy_chunk.hip); k | 16.
+struct CopyChunkArgs {
+    const uint8_t* cw;          // P rows of CW bytes
+    const uint8_t* er;          // P flags
+    uint8_t* out;               // Pout rows of L bytes (4-byte aligned, L % 4 == 0)
+    int32_t* out_len;
+    int cw_bytes, er_bytes, out_bytes;  // P*CW, P, Pout*L (all < 2^31, launcher check)
+    int L, CW, T, C;            // C = ceil(L / 16) chunks per row; T <= 12
+    uint32_t cmagic;            // floor(2^32 / C) + 1: i / C by one __umulhi (+1 correction)
+    int nchunks;                // Pout * C
+    int nt;                     // 1: non-temporal codeword loads and payload stores
+};
+const void* fec_copy_chunk_kernel_for(int k, int np);
+
 // fec_copy_fast_kernel<k, n-k> for the instantiated pairs (fec_copy_fast.hip), else nullptr.
 const void* fec_copy_fast_kernel_for(int k, int np);
 // Specialised planner for (k, n-k), or nullptr (then fec_plan_kernel runs); its rule table is

@@ -169,7 +169,7 @@ def gpu_round_trip(T, B, N, pattern, P, garbage=True, path="auto", dedup=True):
     c = fec.Codec(L, T, B, N)
     try:
         c.set_copy_path(path)
-        c.set_plan_path("auto" if path in ("wave", "tile") else path)
+        c.set_plan_path("auto" if path in ("wave", "tile", "chunk") else path)
     except fec.FecError:
         pytest.skip(f"no {path} kernel for {(T, B, N)}")
     c.set_episode_dedup(dedup)
@@ -201,8 +201,8 @@ DEC_CASES = [((10, 5, 2), "bin_erasure", 0, 8000), ((10, 3, 3), "bin_erasure", 0
              ((10, 8, 1), "erasure90", 2000, 5000), ((10, 9, 2), "erasure100", 7000, 5000)]
 
 
-@pytest.mark.parametrize("path,dedup", [("generic", False), ("wave", True), ("tile", True), ("auto", False),
-                                        ("auto", True)])
+@pytest.mark.parametrize("path,dedup", [("generic", False), ("wave", True), ("tile", True), ("chunk", True),
+                                        ("auto", False), ("auto", True)])
 @pytest.mark.parametrize("tbn,pattern,start,P", DEC_CASES)
 def test_decode_bit_exact_vs_oracle(tbn, pattern, start, P, path, dedup):
     T, B, N = tbn
@@ -236,13 +236,15 @@ def test_copy_fast_variable_lengths_and_sizes():
             if t >= T:
                 want.append(out)
                 want_len.append(p)
-        for cpath in ("fast", "wave", "tile"):
+        for cpath in ("fast", "wave", "tile", "chunk"):
             c = fec.Codec(Lx, T, B, N)
             try:
                 c.set_copy_path(cpath)
             except fec.FecError:
-                # a wave holds <= 64 groups, T < 4*NS4; a copy tile (32 packets) holds <= 16 KB
-                assert (cpath == "wave" and (c.S > 4 * 64 or T >= c.S)) or (cpath == "tile" and 32 * c.CW > 16384)
+                # a wave holds <= 64 groups, T < 4*NS4; a copy tile (32 packets) holds <= 16 KB;
+                # the chunk copy exists for k | 16 (instances (8,3), (8,4), (4,7))
+                assert (cpath == "wave" and (c.S > 4 * 64 or T >= c.S)) or \
+                    (cpath == "tile" and 32 * c.CW > 16384) or (cpath == "chunk" and c.k not in (4, 8))
                 continue
             out, ln = c.decode(torch.from_numpy(np.stack(cws)).cuda(), torch.from_numpy(pat).cuda())
             assert (ln.cpu().numpy() == np.array(want_len)).all(), (Lx, tbn, cpath)
