@@ -91,10 +91,10 @@ class Codec:
 
     def set_copy_path(self, path: str) -> None:
         """'auto', 'generic', 'fast' (LDS tiles), 'wave' (barrier-free), 'chunk' (a lane per 16-byte
-        output piece, k | 16) or 'tile' (persistent
+        output piece, k | 16), 'pipe' (one LDS-DMA pipeline per wave) or 'tile' (persistent
         per-workgroup tile runs, register-staged prefetch) for the decoder's received-packet
         kernel."""
-        code = {"auto": 0, "generic": 1, "fast": 2, "wave": 3, "tile": 4, "chunk": 5}[path]
+        code = {"auto": 0, "generic": 1, "fast": 2, "wave": 3, "tile": 4, "chunk": 5, "pipe": 6}[path]
         check(lib().fec_codec_set_copy_path(self._h, code), "fec_codec_set_copy_path")
 
     def info(self) -> dict:
@@ -322,8 +322,12 @@ class StreamGroup:
         check(lib().fec_streams_create(max_payload, T, B, N, nstreams, ctypes.byref(h)), "fec_streams_create")
         self._h = h
         self.L, self.T, self.nstreams = max_payload, T, nstreams
-        c = Codec(max_payload, T, B, N)
-        self.k, self.n, self.S, self.CW = c.k, c.n, c.S, c.CW
+        # the geometry of Encoder.cpp:31-45 (k = T-N+1, n = k+B, S = ceil((L+2)/k), CW = S*n);
+        # fec_streams_create has validated (T,B,N) against it
+        self.k = T - N + 1
+        self.n = self.k + B
+        self.S = -(-(max_payload + 2) // self.k)
+        self.CW = self.S * self.n
 
     def __del__(self):
         h = getattr(self, "_h", None)

@@ -79,6 +79,8 @@ struct fec_codec {
     const void* copy_wave = nullptr;  // barrier-free decode copy (fec_copy_wave.hip)
     const void* copy_chunk = nullptr; // one lane per 16-byte output piece (fec_copy_chunk.hip), k | 16
     int copyc_grid = 0;               // its grid: resident workgroups
+    const void* copy_pipe = nullptr;  // one LDS-DMA pipeline per wave (fec_copy_pipe.hip)
+    int copyp_q = 0, copyp_lds = 0, copyp_slot = 0, copyp_waves = 0;
     int copy_path = 0;           // 0 auto, 1 generic, 2 specialised (LDS tiles), 3 wave
     int plan_path = 0;
     int dedup = 1;               // episode-shape deduplication in the planner
@@ -324,6 +326,28 @@ int codec_init(fec_codec* c, int max_payload, int T, int B, int N) {
     if (!c->copyf_tp) c->copy_fast = nullptr;
     if ((g.L & 3) == 0 && (g.S + 3) / 4 <= 64 && g.T < 4 * ((g.S + 3) / 4))
         c->copy_wave = fec::fec_copy_wave_kernel_for(g.k, g.n - g.k);
+    if ((g.L & 3) == 0) {
+        // tile of Q packets: Q*CW and Q*L multiples of 16, Q + T <= 64 (one flag ballot); a wave's
+        // three codeword slots and output tile in LDS
+        int q = 16;
+        if (const char* v = std::getenv("FEC_PIPE_Q")) q = std::atoi(v);
+        while (q >= 4 && ((q * g.CW) % 16 || (q * g.L) % 16 || q % 4 || q + g.T > 64)) q -= 4;
+        if (q >= 4 && (int64_t(g.T) * g.CW >= 16)) {
+            c->copy_pipe = fec::fec_copy_pipe_kernel_for(g.k, g.n - g.k);
+            if (c->copy_pipe) {
+                c->copyp_q = q;
+                c->copyp_slot = round16(15 + q * g.CW);
+                c->copyp_lds = 3 * (c->copyp_slot + 256) + q * g.L;
+                int dev = 0, cus = 0, per_cu = 0;
+                HIP_TRY(hipGetDevice(&dev));
+                HIP_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+                HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, c->copy_pipe, 64, c->copyp_lds));
+                if (const char* v = std::getenv("FEC_PIPE_WPC")) per_cu = std::max(1, std::min(per_cu, std::atoi(v)));
+                c->copyp_waves = cus * per_cu;
+                if (c->copyp_waves <= 0) c->copy_pipe = nullptr;
+            }
+        }
+    }
     if ((g.L & 3) == 0 && g.T <= 12) {
         c->copy_chunk = fec::fec_copy_chunk_kernel_for(g.k, g.n - g.k);
         if (c->copy_chunk) {
@@ -825,6 +849,47 @@ int launch_copy(fec_codec* c, const uint8_t* d_cw, const uint8_t* d_er, int64_t 
     const bool chunk_ok = c->copy_chunk && (reinterpret_cast<uintptr_t>(d_out) & 3) == 0 &&
                           P * g.CW < (int64_t(1) << 31) - 64 &&
                           nchunks + 2 * int64_t(c->copyc_grid) * 256 < (int64_t(1) << 31);
+    // one LDS-DMA pipeline per wave: 16-byte aligned output, every offset within 31 bits
+    const bool pipe_ok = c->copy_pipe && (reinterpret_cast<uintptr_t>(d_out) & 15) == 0 &&
+                         P * g.CW + c->copyp_slot + 2048 < (int64_t(1) << 31) &&
+                         Pout * g.L < (int64_t(1) << 31) - 64 && P + 4 * 64 + 64 < (int64_t(1) << 31);
+    if (c->copy_path == 6 && !pipe_ok) return FEC_ERR_ARG;
+    if (pipe_ok && c->copy_path == 6) {
+        fec::CopyPipeArgs pa;
+        const uintptr_t cwp = reinterpret_cast<uintptr_t>(d_cw), erp = reinterpret_cast<uintptr_t>(d_er);
+        pa.cw_base = reinterpret_cast<const uint8_t*>(cwp & ~uintptr_t(15));
+        pa.er_base = reinterpret_cast<const uint8_t*>(erp & ~uintptr_t(3));
+        pa.delta = static_cast<int>(cwp & 15);
+        pa.edelta = static_cast<int>(erp & 3);
+        pa.cw_records = static_cast<int>(pa.delta + P * g.CW);
+        pa.er_records = static_cast<int>(pa.edelta + P);
+        pa.out = d_out;
+        pa.out_len = d_outlen;
+        pa.out_records = static_cast<int>(Pout * g.L);
+        pa.len_records = static_cast<int>(4 * Pout);
+        pa.L = g.L;
+        pa.CW = g.CW;
+        pa.T = g.T;
+        pa.NS4 = c->ns4();
+        pa.Q = c->copyp_q;
+        pa.ns4magic = static_cast<uint32_t>((uint64_t(1) << 32) / uint64_t(pa.NS4) + 1);
+        pa.slot_bytes = c->copyp_slot;
+        pa.nd = (pa.slot_bytes + 1023) / 1024;
+        pa.npass = (pa.Q * pa.NS4 + 63) / 64;
+        pa.ns = (pa.Q * g.L / 16 + 63) / 64;
+        pa.Pout = Pout;
+        pa.nsteps = (Pout + pa.Q - 1) / pa.Q;
+        const int64_t waves = std::max<int64_t>(1, std::min<int64_t>(pa.nsteps, c->copyp_waves));
+        pa.steps_per_wave = (pa.nsteps + waves - 1) / waves;
+        pa.nt = 1;
+        if (const char* v = std::getenv("FEC_COPY_NT")) pa.nt = std::atoi(v) ? 1 : 0;
+        const int64_t blocks = (pa.nsteps + pa.steps_per_wave - 1) / pa.steps_per_wave;
+        hipEvent_t stop;
+        if (int st = c->begin(FEC_KERNEL_DEC_COPY, s, &stop)) return st;
+        void* args[] = {&pa};
+        HIP_TRY(hipLaunchKernel(c->copy_pipe, dim3(static_cast<unsigned>(blocks)), dim3(64), args, c->copyp_lds, s));
+        return c->end(stop, s);
+    }
     if (c->copy_path == 5 && !chunk_ok) return FEC_ERR_ARG;
     if (chunk_ok && c->copy_path == 5) {
         fec::CopyChunkArgs ka;
@@ -843,6 +908,8 @@ int launch_copy(fec_codec* c, const uint8_t* d_cw, const uint8_t* d_er, int64_t 
         ka.nchunks = static_cast<int>(nchunks);
         ka.nt = 1;
         if (const char* v = std::getenv("FEC_COPY_NT")) ka.nt = std::atoi(v) ? 1 : 0;
+        ka.dbg = 0;
+        if (const char* v = std::getenv("FEC_CHUNK_DBG")) ka.dbg = std::atoi(v);
         const int64_t need = (nchunks + 511) / 512;  // two chunks per lane
         const unsigned blocks = static_cast<unsigned>(std::max<int64_t>(1, std::min<int64_t>(need, c->copyc_grid)));
         hipEvent_t stop;
@@ -1333,7 +1400,9 @@ int fec_codec_info(const fec_codec* c, char* buf, size_t size) {
     else
         std::snprintf(enc, sizeof(enc), "fec_encode_kernel");
     char cpy[64];
-    if (c->copy_chunk && c->copy_path == 5)
+    if (c->copy_pipe && c->copy_path == 6)
+        std::snprintf(cpy, sizeof(cpy), "fec_copy_pipe_kernel<%d, %d>", c->g.k, np);
+    else if (c->copy_chunk && c->copy_path == 5)
         std::snprintf(cpy, sizeof(cpy), "fec_copy_chunk_kernel<%d, %d>", c->g.k, np);
     else if (c->copy_wave && c->copy_path == 3)
         std::snprintf(cpy, sizeof(cpy), "fec_copy_wave_kernel<%d, %d>", c->g.k, np);
@@ -1386,7 +1455,8 @@ int fec_codec_set_plan_path(fec_codec* c, int path) {
 }
 
 int fec_codec_set_copy_path(fec_codec* c, int path) {
-    if (!c || path < 0 || path > 5) return FEC_ERR_ARG;
+    if (!c || path < 0 || path > 6) return FEC_ERR_ARG;
+    if (path == 6 && !c->copy_pipe) return FEC_ERR_ARG;
     if (path == 5 && !c->copy_chunk) return FEC_ERR_ARG;
     if (path == 4 && !c->copy_tile) return FEC_ERR_ARG;
     if (path == 2 && !c->copy_fast) return FEC_ERR_ARG;
@@ -1396,7 +1466,8 @@ int fec_codec_set_copy_path(fec_codec* c, int path) {
 }
 
 int fec_codec_set_encode_path(fec_codec* c, int path) {
-    if (!c || path < 0 || path > 5) return FEC_ERR_ARG;
+    if (!c || path < 0 || path > 6) return FEC_ERR_ARG;
+    if (path == 6 && !c->copy_pipe) return FEC_ERR_ARG;
     if (path == 5 && !c->tile_kernel) return FEC_ERR_ARG;
     if (path == 2 && !c->fast_kernel) return FEC_ERR_ARG;
     if (path == 3 && !c->persist_kernel) return FEC_ERR_ARG;

@@ -145,8 +145,9 @@ __global__ __launch_bounds__(256) void fec_copy_chunk_kernel(CopyChunkArgs a) {
         const int row = t * CW;
         const int src = row + (16 / K) * j * n + G::lo;
         load_dwords<G::NW>(ld.D, rs, ok ? (src & ~3) : 0x7ffffff0, nt);
-        ld.E = __builtin_amdgcn_raw_buffer_load_b128(re, ok ? (t & ~3) : 0x7ffffff0, 0, 0);
-        ld.H = __builtin_amdgcn_raw_buffer_load_b64(rs, ok ? (row & ~3) : 0x7ffffff0, 0, 0);
+        const bool fh = ok && !(a.dbg & 4);
+        ld.E = __builtin_amdgcn_raw_buffer_load_b128(re, fh ? (t & ~3) : 0x7ffffff0, 0, 0);
+        ld.H = __builtin_amdgcn_raw_buffer_load_b64(rs, fh ? (row & ~3) : 0x7ffffff0, 0, 0);
     };
     auto finish = [&](int i, const ChunkLoads<G::NW>& ld) __attribute__((always_inline)) {
         if (i >= nchunks) return;
@@ -182,7 +183,7 @@ __global__ __launch_bounds__(256) void fec_copy_chunk_kernel(CopyChunkArgs a) {
         const int b0 = 16 * j;
 #pragma unroll
         for (int qq = 0; qq < 4; ++qq) O[qq] &= keep_bytes(cl - (b0 + 4 * qq));
-        const int o = t * L + b0;
+        const int o = (a.dbg & 2) ? 0x7ffffff0 : ((a.dbg & 1) ? ((t * L + b0) & ~15) : t * L + b0);
         const int rem = L - b0;  // >= 4, a multiple of 4
         if (rem >= 16) {
             const cc_v4u v = {O[0], O[1], O[2], O[3]};

@@ -223,8 +223,27 @@ struct CopyChunkArgs {
     uint32_t cmagic;            // floor(2^32 / C) + 1: i / C by one __umulhi (+1 correction)
     int nchunks;                // Pout * C
     int nt;                     // 1: non-temporal codeword loads and payload stores
+    int dbg;                    // timing experiments only (FEC_CHUNK_DBG): 1 stores rounded down to
+                                // 16 bytes, 2 no stores, 4 no flag/header loads; 0 in the product
 };
 const void* fec_copy_chunk_kernel_for(int k, int np);
+
+// Received-packet decode, one LDS-DMA pipeline per wave (fec_copy_pipe.hip).
+struct CopyPipeArgs {
+    const uint8_t* cw_base;     // codewords rounded down to 16 bytes; row x at cw_base + delta + x*CW
+    const uint8_t* er_base;     // erasure flags rounded down to 4 bytes; flag x at er_base + edelta + x
+    uint8_t* out;               // 16-byte aligned, Pout rows of L bytes (L % 4 == 0)
+    int32_t* out_len;
+    int cw_records, er_records, out_records, len_records;  // bytes addressable through each (< 2^31)
+    int delta, edelta;
+    int L, CW, T, NS4, Q;       // Q packets per tile: Q*CW % 16 == 0, Q*L % 16 == 0, Q % 4 == 0, Q+T <= 64
+    uint32_t ns4magic;          // floor(2^32 / NS4) + 1: item / NS4 by one __umulhi
+    int slot_bytes;             // LDS bytes of a tile's codeword rows (>= delta + Q*CW, multiple of 16)
+    int nd, npass, ns;          // per tile: 1 KB DMA instructions, 64-item passes, 16-byte store rounds
+    int64_t Pout, nsteps, steps_per_wave;
+    int nt;                     // 1: non-temporal codeword loads and payload stores
+};
+const void* fec_copy_pipe_kernel_for(int k, int np);
 
 // fec_copy_fast_kernel<k, n-k> for the instantiated pairs (fec_copy_fast.hip), else nullptr.
 const void* fec_copy_fast_kernel_for(int k, int np);

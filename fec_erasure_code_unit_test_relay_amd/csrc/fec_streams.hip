@@ -318,9 +318,12 @@ struct fec_streams {
     void* d_stage = nullptr;                 // per-call records (ids + seqs / items + coefs)
     void* h_stage = nullptr;                 // pinned twin of d_stage
     size_t stage_bytes = 0;
-    hipEvent_t staged = nullptr;             // the last upload from h_stage
+    hipEvent_t staged = nullptr;             // the last upload from h_stage (h_stage reusable)
+    hipEvent_t done = nullptr;               // the last call's kernel (d_stage, windows, rings free)
+    bool poisoned = false;                   // a failed call left host and device state apart
     ~fec_streams() {
         if (staged) (void)hipEventDestroy(staged);
+        if (done) (void)hipEventDestroy(done);
         for (void* p : {static_cast<void*>(d_win), static_cast<void*>(d_ring), d_stage})
             if (p) (void)hipFree(p);
         if (h_stage) (void)hipHostFree(h_stage);
@@ -349,17 +352,17 @@ int check_ids(fec_streams* h, const int32_t* ids, int M) {
     return FEC_OK;
 }
 
-// the previous call's records have left the pinned staging buffer
-int stage_free(fec_streams* h) {
+// The previous call's records have left the pinned staging buffer (host wait), and its kernel --
+// which reads d_stage and reads / writes the windows and rings -- comes before anything this call
+// enqueues on `s`, whichever stream the previous call used (device-side wait).
+int stage_free(fec_streams* h, hipStream_t s) {
+    if (h->poisoned) return FEC_ERR_HIP;
     FS_TRY(hipEventSynchronize(h->staged));
+    FS_TRY(hipStreamWaitEvent(s, h->done, 0));
     return FEC_OK;
 }
 
 }  // namespace
-
-extern "C" {
-
-}  // extern "C"
 
 int fec::stream_encode_one(const CodecView& v, uint8_t* win, const uint8_t* payload, int payload_len, int64_t seq,
                            uint8_t* cw, int32_t* cw_len, uint32_t* done, uint32_t ticket, hipStream_t s) {
@@ -449,6 +452,8 @@ int fec_streams_create(int max_payload, int T, int B, int N, int nstreams, fec_s
         FS_TRY(hipHostMalloc(&h->h_stage, h->stage_bytes));
         FS_TRY(hipEventCreateWithFlags(&h->staged, hipEventDisableTiming));
         FS_TRY(hipEventRecord(h->staged, nullptr));
+        FS_TRY(hipEventCreateWithFlags(&h->done, hipEventDisableTiming));
+        FS_TRY(hipEventRecord(h->done, nullptr));
         *out = h.release();
         return FEC_OK;
     } catch (const std::bad_alloc&) {
@@ -470,12 +475,12 @@ int fec_streams_encode(fec_streams* h, const int32_t* ids, int M, const uint8_t*
         return FEC_ERR_ARG;
     if (M == 0) return FEC_OK;
     if (int st = check_ids(h, ids, M)) return st;
-    if (int st = stage_free(h)) return st;
     hipStream_t s = static_cast<hipStream_t>(stream);
+    if (int st = stage_free(h, s)) return st;
     int64_t* hseq = static_cast<int64_t*>(h->h_stage);
     int32_t* hid = reinterpret_cast<int32_t*>(hseq + M);
     for (int m = 0; m < M; ++m) {
-        hseq[m] = h->enc_seq[ids[m]]++;
+        hseq[m] = h->enc_seq[ids[m]];  // committed below, once the launch is in
         hid[m] = ids[m];
     }
     const size_t bytes = static_cast<size_t>(M) * 12;
@@ -507,6 +512,8 @@ int fec_streams_encode(fec_streams* h, const int32_t* ids, int M, const uint8_t*
     a.ticket = 0;
     hipLaunchKernelGGL(fec::fec_streams_encode_kernel, dim3((M + 3) / 4), dim3(256), 0, s, a);
     FS_TRY(hipGetLastError());
+    FS_TRY(hipEventRecord(h->done, s));
+    for (int m = 0; m < M; ++m) ++h->enc_seq[ids[m]];
     return FEC_OK;
 }
 
@@ -518,9 +525,16 @@ int fec_streams_decode(fec_streams* h, const int32_t* ids, int M, const uint8_t*
         return FEC_ERR_ARG;
     if (M == 0) return FEC_OK;
     if (int st = check_ids(h, ids, M)) return st;
-    if (int st = stage_free(h)) return st;
-    const fec::Geometry& g = h->g;
     hipStream_t s = static_cast<hipStream_t>(stream);
+    if (int st = stage_free(h, s)) return st;
+    const fec::Geometry& g = h->g;
+    // The symbolic decoders advance below, before the upload and the launch; if either fails, the
+    // host planners are ahead of the device rings and the group refuses every later call.
+    struct Poison {
+        fec_streams* h;
+        bool armed = true;
+        ~Poison() { if (armed) h->poisoned = true; }
+    } poison{h};
     fec::StreamItem* items = static_cast<fec::StreamItem*>(h->h_stage);
     uint8_t* coefs = reinterpret_cast<uint8_t*>(items + M);
     const int kn = g.k * g.n;
@@ -571,6 +585,8 @@ int fec_streams_decode(fec_streams* h, const int32_t* ids, int M, const uint8_t*
     a.ticket = 0;
     hipLaunchKernelGGL(fec::fec_streams_decode_kernel, dim3((M + 3) / 4), dim3(256), 0, s, a);
     FS_TRY(hipGetLastError());
+    FS_TRY(hipEventRecord(h->done, s));
+    poison.armed = false;
     return FEC_OK;
 }
 
