@@ -329,9 +329,11 @@ int codec_init(fec_codec* c, int max_payload, int T, int B, int N) {
     if ((g.L & 3) == 0) {
         // tile of Q packets: Q*CW and Q*L multiples of 16, Q + T <= 64 (one flag ballot); a wave's
         // three codeword slots and output tile in LDS
+        auto pipe_lds = [&](int q) { return 3 * (round16(15 + q * g.CW) + 256) + q * g.L; };
         int q = 16;
         if (const char* v = std::getenv("FEC_PIPE_Q")) q = std::atoi(v);
-        while (q >= 4 && ((q * g.CW) % 16 || (q * g.L) % 16 || q % 4 || q + g.T > 64)) q -= 4;
+        while (q >= 4 && ((q * g.CW) % 16 || (q * g.L) % 16 || q % 4 || q + g.T > 64 || pipe_lds(q) > kLdsBudget))
+            q -= 4;
         if (q >= 4 && (int64_t(g.T) * g.CW >= 16)) {
             c->copy_pipe = fec::fec_copy_pipe_kernel_for(g.k, g.n - g.k);
             if (c->copy_pipe) {
@@ -1144,6 +1146,15 @@ int launch_decode_stream(fec_codec* c, fec_decode_stream* st, const uint8_t* d_c
     if (int st2 = check_ws(c, Pp, d_ws, ws_bytes)) return st2;
     const uint8_t* cw_c = d_cw - (s0 - cut) * c->g.CW;
     const uint8_t* er_c = d_er - (s0 - cut);
+    // The copy below writes every row it covers, erased ones included, and the recovery runs
+    // after it: the wave copy (path 3, which leaves erased rows to a concurrent recovery) is
+    // switched off for the whole push, so the compaction does not zero lost rows beside the copy.
+    struct CopyPathOverride {
+        fec_codec* c;
+        int saved;
+        ~CopyPathOverride() { c->copy_path = saved; }
+    } keep{c, c->copy_path};
+    if (c->copy_path == 3) c->copy_path = 0;
     HIP_TRY(hipEventRecord(c->ev_fork, s));
     HIP_TRY(hipStreamWaitEvent(c->side, c->ev_fork, 0));
     if (int e = launch_plan(c, er_c, Pp, d_ws, ws_bytes, c->side)) return e;
@@ -1153,11 +1164,7 @@ int launch_decode_stream(fec_codec* c, fec_decode_stream* st, const uint8_t* d_c
     const int64_t Pc = end - next_out;
     const uint8_t* cw_o = d_cw - (s0 - next_out) * c->g.CW;
     const uint8_t* er_o = d_er - (s0 - next_out);
-    const int saved = c->copy_path;
-    if (saved == 3) c->copy_path = 0;  // the wave copy leaves erased rows to the recovery's zero_lost
-    int e = launch_copy(c, cw_o, er_o, Pc, d_out, d_outlen, s);
-    c->copy_path = saved;
-    if (e) return e;
+    if (int e = launch_copy(c, cw_o, er_o, Pc, d_out, d_outlen, s)) return e;
     HIP_TRY(hipStreamWaitEvent(s, c->ev_join, 0));
     if (int e2 = launch_recover(c, cw_c, Pp, d_out, d_outlen, d_ws, ws_bytes, s, next_out - cut, true)) return e2;
     *n_out = end - T - next_out;

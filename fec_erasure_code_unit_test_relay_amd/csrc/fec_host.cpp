@@ -206,18 +206,28 @@ const uint8_t* DecodeRules::lazy_entry(int w, uint32_t mask) const {
     return p;
 }
 
+// One table per (T,B,N) for the life of the process (codecs, planners and variable-rate plans of one
+// configuration share it).  The global lock only guards the map: each table is built outside it,
+// once, by the first caller (std::call_once; a build that throws leaves the slot for the next
+// caller), so a configuration being built does not hold up callers of the others.
 std::shared_ptr<const DecodeRules> shared_decode_rules(int T, int B, int N) {
+    struct Slot {
+        std::once_flag once;
+        DecodeRules rules;
+    };
     static std::mutex mu;
-    static std::map<int64_t, std::shared_ptr<const DecodeRules>> cache;
+    static std::map<int64_t, std::shared_ptr<Slot>> cache;
     const int64_t key = (int64_t(T) << 32) | (int64_t(B) << 16) | int64_t(N);
-    std::lock_guard<std::mutex> lock(mu);
-    auto it = cache.find(key);
-    if (it != cache.end()) return it->second;
+    std::shared_ptr<Slot> slot;
+    {
+        std::lock_guard<std::mutex> lock(mu);
+        std::shared_ptr<Slot>& e = cache[key];
+        if (!e) e = std::make_shared<Slot>();
+        slot = e;
+    }
     const int k = T - N + 1, n = k + B;
-    auto r = std::make_shared<DecodeRules>();
-    r->build(make_generator(T, B, N), k, n, T);
-    cache.emplace(key, r);
-    return r;
+    std::call_once(slot->once, [&] { slot->rules.build(make_generator(T, B, N), k, n, T); });
+    return std::shared_ptr<const DecodeRules>(slot, &slot->rules);
 }
 
 // ------------------------------------------------------------------------------------------
