@@ -179,7 +179,69 @@ void VrPlan::run(int max_payload, int T, int B, int N, bool mds, const uint8_t* 
     const auto t_start = std::chrono::steady_clock::now();
     frames.reserve(static_cast<size_t>(P + T + 1));
     erased.reserve(static_cast<size_t>(P + T + 1));
+    const int64_t n_drop = std::min<int64_t>(P + T, n_pattern);  // packets the pattern can drop
+    int64_t next_drop = -1;                                        // cache of the next dropped seq
     for (int64_t seq = 0;; ++seq) {
+        // ---- steady stretch: the same frame, every packet received, nothing switching ----
+        // Every branch below is then fixed: the feedback repeats (both estimators at their fixed
+        // point, no estimator swap before the next cycle boundary), the encoder has no switch to
+        // make and no transition running, the decoder has no gap, no parameter change and no
+        // double decoding.  Such packets are appended directly, in the same order and with the
+        // same float accumulation of the coding rate as the loop below; the stretch ends before
+        // the next drop, the next cycle boundary and the last packet.
+        if (cur >= 0 && !transition_flag && !double_coding_flag && counter_transition > eT && seq_start >= 0 &&
+            latest_seq == seq && !dcf && sdc < seq && dT == eT && dB == eB && dN == eN && seq < P + T - 1) {
+            const int fT = adaptive && udp[0] != 0 ? udp[0] : sT, fB = adaptive && udp[0] != 0 ? udp[1] : sB,
+                      fN = adaptive && udp[0] != 0 ? udp[2] : sN;
+            const int aT = adaptive && udp[0] != 0 ? udp[3] : sT_ack, aB = adaptive && udp[0] != 0 ? udp[4] : sB_ack;
+            const bool would_switch = (fT != eT || fB != eB || fN != eN) && aT == eT && aB == eB;
+            if (!would_switch && est->steady(seq, eT) && bg->steady(seq, eT) && udp[3] == eT && udp[4] == eB &&
+                udp[5] == eN && udp[0] == est->T && udp[1] == est->B_current && udp[2] == est->N_current) {
+                if (next_drop < seq) {
+                    next_drop = n_drop;
+                    if (seq < n_drop) {
+                        const void* hit = std::memchr(pattern + seq, 1, static_cast<size_t>(n_drop - seq));
+                        if (hit) next_drop = static_cast<const uint8_t*>(hit) - pattern;
+                    }
+                }
+                const int64_t end = std::min({next_drop, cycle * kEstimationCycle, P + T - 1});
+                if (end > seq) {
+                    if (adaptive && udp[0] != 0) {
+                        sT = udp[0];
+                        sB = udp[1];
+                        sN = udp[2];
+                        sT_ack = udp[3];
+                        sB_ack = udp[4];
+                        sN_ack = udp[5];
+                    }
+                    VrFrame fr;
+                    fr.T = eT;
+                    fr.B = eB;
+                    fr.N = eN;
+                    fr.enc_cur = cur;
+                    fr.counter = counter_transition;
+                    const float rate = static_cast<float>(eT - eN + 1) / (eT - eN + 1 + eB);
+                    frames.insert(frames.end(), static_cast<size_t>(end - seq), fr);
+                    erased.insert(erased.end(), static_cast<size_t>(end - seq), uint8_t(0));
+                    std::vector<Report>& rp = reports[dcur];
+                    for (int64_t s = seq; s < end; ++s) {
+                        sum_coding_rate += rate;
+                        const int64_t x = s - dT;  // report(dcur, s)
+                        if (x >= seq_start && x < P) {
+                            rp.push_back(Report{s, x});
+                            fate_dec[x] = dcur;
+                        }
+                    }
+                    enc[cur].end = end;
+                    dec[dcur].end = end;  // call(dcur, s) for every s
+                    est->previous_win_end = end - 1;
+                    bg->previous_win_end = end - 1;
+                    latest_seq = end;
+                    sent = end;
+                    seq = end;
+                }
+            }
+        }
         // ---- Application_Layer_Sender::generate_message_and_encode ----
         if (adaptive && udp[0] != 0) {
             sT = udp[0];

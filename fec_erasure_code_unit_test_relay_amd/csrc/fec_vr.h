@@ -35,6 +35,17 @@ struct ParameterEstimator {
     ParameterEstimator(int T_value, bool mds) : adaptive_mode_MDS(mds), T(T_value) {}
     void estimate(int64_t seq, int msg_T);
     void make_MDS_estimates();
+    // estimate(seq, T) for the next in-order seq would change nothing but previous_win_end: the
+    // window holds no erasure (a received packet shifts in a 0: sum == 0 skips the update,
+    // Parameter_Estimator.cpp:104-105) and the closing recommendation step is at its fixed point
+    // (:177-181, and make_MDS_estimates when on).
+    bool steady(int64_t seq, int msg_T) const {
+        if (T == 0 || previous_win_end != seq - 1 || erasure != 0 || msg_T != T) return false;
+        if ((T - N_current + 1) * (T - N + 1 + B) >= (T - N + 1) * (T - N_current + 1 + B_current) &&
+            (B_current != B || N_current != N))
+            return false;
+        return !(adaptive_mode_MDS && B_current > N_current);
+    }
 };
 
 constexpr int kVrCoefStride = kMaxK * kMaxRuleN;
