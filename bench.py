@@ -64,6 +64,21 @@ def pmc_traffic(kernel_symbol):
     return best
 
 
+def rocprof_kernel_time(kernel_symbol):
+    """Average duration (ns) of `kernel_symbol` per launch from the newest committed rocprofv3
+    --kernel-trace --stats summary of the bench command (profiles/*/*_kernel_time.json, made by
+    tools/kernel_time.py).  Returns (avg_ns, source, fresh) like pmc_traffic, or None."""
+    import glob
+    best = None
+    digest = kernel_sources_digest()
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*", "*_kernel_time.json"))):
+        with open(path) as f:
+            entry = json.load(f).get(kernel_symbol)
+        if entry:
+            best = (entry["avg_ns"], os.path.relpath(path, ROOT), entry.get("sources_sha256") == digest)
+    return best
+
+
 def cpu_baseline(T, B, N, packets, rank_pattern, threads=None):
     """The oracle's reference-structured encoder+decoder on a bounded sample: one stream per
     thread (the reference is single-threaded; BASELINE.md §2 plans 1 core and one stream per
@@ -649,6 +664,15 @@ def main():
                                       traffic_source=tr[1])
         elif tr:
             result["roofline"].update(traffic_stale=f"{tr[1]} was measured on other kernel sources")
+        # the same kernel's average duration under rocprofv3 (the bench command itself, committed
+        # summary): the kernel without the event packets around each launch
+        kt = rocprof_kernel_time(symbol) if symbol and P == 1_000_000 else None
+        if kt and kt[2]:
+            a_rp = algo[dominant] / (kt[0] * 1e-9) / 1e9
+            result["roofline"].update(rocprof_avg_us=round(kt[0] / 1e3, 2), achieved_rocprof=round(a_rp, 1),
+                                      frac_rocprof=round(a_rp / HBM_PEAK_GBS, 4), rocprof_source=kt[1])
+        elif kt:
+            result["roofline"].update(rocprof_stale=f"{kt[1]} was measured on other kernel sources")
     if not args.no_host_inclusive:
         hi = host_inclusive(codec, payload, pat, er, cw, wl, out, ol, P, Pf, world, barrier,
                             lambda x: max_over_ranks(x, dist, comm_dev),

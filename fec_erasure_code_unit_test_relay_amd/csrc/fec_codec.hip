@@ -641,8 +641,8 @@ int launch_encode_tile(fec_codec* c, const uint8_t* d_payload, const int32_t* d_
     a.off_scratch = c->tile_off[8];
     a.dbg = 0;
     if (const char* v = std::getenv("FEC_TILE_DBG")) a.dbg = std::atoi(v);
-    a.nt = 0;
-    if (const char* v = std::getenv("FEC_TILE_NT")) a.nt = std::atoi(v) ? 1 : 0;
+    a.nt = 0;  // bit 0: non-temporal codeword stores, bit 1: non-temporal payload loads
+    if (const char* v = std::getenv("FEC_TILE_NT")) a.nt = std::atoi(v) & 3;
     const int64_t blocks = (ntiles + tpw - 1) / tpw;
     hipEvent_t stop;
     if (int st = c->begin(FEC_KERNEL_ENCODE, s, &stop)) return st;
@@ -971,10 +971,12 @@ int launch_copy(fec_codec* c, const uint8_t* d_cw, const uint8_t* d_er, int64_t 
         fa.out_bytes = round16(fa.TP * g.L);
         fa.stamps = (c->stamp_kernel == FEC_KERNEL_DEC_COPY) ? c->d_stamps : nullptr;
         fa.skip_erased = 0;
+        if (const char* v = std::getenv("FEC_COPY_SKIP")) fa.skip_erased = std::atoi(v) ? 1 : 0;  // experiment
         // non-temporal codeword loads and payload stores: 0.318 vs 0.338 ms per bench step
         // (tools/step_ab.py, same process, profiles/r02/decode_diag/copy_nt_ab.txt)
         fa.nt = 1;
         if (const char* v = std::getenv("FEC_COPY_NT")) fa.nt = std::atoi(v) ? 1 : 0;
+        if (const char* v = std::getenv("FEC_COPY_REV")) fa.nt |= std::atoi(v) ? 2 : 0;  // experiment: tiles in reverse order
         const int64_t blocks = (Pout + fa.TP - 1) / fa.TP;
         hipEvent_t stop;
         if (int st = c->begin(FEC_KERNEL_DEC_COPY, s, &stop)) return st;
@@ -1024,6 +1026,7 @@ int launch_compact(fec_codec* c, int64_t P, uint8_t* d_out, int32_t* d_outlen, v
     // when the copy kernel leaves erased rows alone (wave copy), the lost ones get their zero row
     // and length 0 here
     ca.zero_lost = copy_skips_erased(c, d_out, P) ? 1 : 0;
+    if (const char* v = std::getenv("FEC_COPY_SKIP")) ca.zero_lost = std::atoi(v) ? 1 : ca.zero_lost;  // experiment
     ca.out = d_out;
     ca.out_len = d_outlen;
     ca.L = g.L;

@@ -112,6 +112,11 @@ __device__ __forceinline__ void dma16(tv4u rsrc, uint32_t voff, uint32_t lds) {
     asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds\n\ts_mov_b32 m0, %0"
                  : "=&s"(keep) : "v"(voff), "s"(rsrc), "s"(lds) : "memory");
 }
+__device__ __forceinline__ void dma16_nt(tv4u rsrc, uint32_t voff, uint32_t lds) {
+    unsigned keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, 0 offen nt lds\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep) : "v"(voff), "s"(rsrc), "s"(lds) : "memory");
+}
 __device__ __forceinline__ void dma4(tv4u rsrc, uint32_t voff, uint32_t lds) {
     unsigned keep;
     asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dword %1, %2, 0 offen lds\n\ts_mov_b32 m0, %0"
@@ -271,7 +276,10 @@ __device__ __forceinline__ void tile_walk(const EncTileArgs& a, uint8_t* smem) {
         for (int j = 0; j < 4; ++j) {
             if (j < ngl) {
                 const int o = base + srel[j];
-                dma16(rs4, static_cast<uint32_t>(o < 0 ? 0x7fffffff : o), dst + (j * 4 + wv) * 1024);
+                if (a.nt & 2)
+                    dma16_nt(rs4, static_cast<uint32_t>(o < 0 ? 0x7fffffff : o), dst + (j * 4 + wv) * 1024);
+                else
+                    dma16(rs4, static_cast<uint32_t>(o < 0 ? 0x7fffffff : o), dst + (j * 4 + wv) * 1024);
             }
         }
         if (has_len) {
@@ -490,7 +498,7 @@ __device__ __forceinline__ void tile_walk(const EncTileArgs& a, uint8_t* smem) {
                 typedef uint32_t v4u __attribute__((ext_vector_type(4)));
                 const v4u vv = {v.x, v.y, v.z, v.w};
                 const int so = full && !(dbg & 4) ? gbase + c : 0x7ffffff0;
-                if (a.nt)
+                if (a.nt & 1)
                     __builtin_amdgcn_raw_buffer_store_b128(vv, rc, so, 0, 2);  // nt
                 else
                     __builtin_amdgcn_raw_buffer_store_b128(vv, rc, so, 0, 0);

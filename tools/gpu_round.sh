@@ -14,6 +14,8 @@ cat $OUT/bench.json
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o bench -- python3 $R/bench.py --no-cpu-baseline --no-host-inclusive --no-extra-configs > $OUT/bench_prof.json 2> $OUT/bench_prof.err || { echo "rocprof failed"; tail -30 $OUT/bench_prof.err; exit 1; }
 find $OUT/prof -name "*stats*"
+KS=$(find $OUT/prof -name "*kernel_stats.csv" | head -1)
+python3 $R/tools/kernel_time.py $OUT/kernel_time.json $TAG "$KS" > /dev/null || { echo "kernel_time failed"; exit 1; }
 # HBM traffic of the step's kernels (FETCH_SIZE / WRITE_SIZE passes) -> profiles-ready JSON
 bash $R/tools/pmc_traffic.sh $TAG > /dev/null 2>&1 || { echo "pmc passes failed"; exit 1; }
 python3 $R/tools/pmc_traffic.py $OUT/traffic.json $TAG $OUT/pmc/p1 $OUT/pmc/p2

@@ -12,7 +12,9 @@ from fec_erasure_code_unit_test_relay_amd import fill_payload  # noqa: E402
 from fec_erasure_code_unit_test_relay_amd.streams import load_pattern  # noqa: E402
 from fec_erasure_code_unit_test_relay_amd.vr import VrPlan  # noqa: E402
 
-reps = int(sys.argv[1]) if len(sys.argv) > 1 else 5
+reps = int(sys.argv[1]) if len(sys.argv) > 1 and not sys.argv[1].startswith("-") else 5
+if "--iters" in sys.argv:
+    reps = int(sys.argv[sys.argv.index("--iters") + 1])
 torch.cuda.set_device(0)
 pat = load_pattern("bin_erasure")
 P = 360000
