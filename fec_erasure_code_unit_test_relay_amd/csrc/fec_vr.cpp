@@ -122,6 +122,7 @@ void VrPlan::run(int max_payload, int T, int B, int N, bool mds, const uint8_t* 
     rec_dec.clear();
     rec_coef.clear();
     lost = switches = 0;
+    steady_packets = 0;
     sum_coding_rate = 0;
 
     // ---- sender (Application_Layer_Sender.cpp:9-31, 64-93, 221-224) ----
@@ -238,6 +239,7 @@ void VrPlan::run(int max_payload, int T, int B, int N, bool mds, const uint8_t* 
                     bg->previous_win_end = end - 1;
                     latest_seq = end;
                     sent = end;
+                    steady_packets += end - seq;
                     seq = end;
                 }
             }

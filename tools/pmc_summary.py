@@ -10,7 +10,7 @@ for path in sys.argv[1:]:
         name = r["Kernel_Name"]
         if "fec::" not in name:
             continue
-        name = name.split("(")[0].replace("void ", "").replace("fec::", "")
+        name = name.replace("(anonymous namespace)::", "").split("(")[0].replace("void ", "").replace("fec::", "")
         agg[name][r["Counter_Name"]] += float(r["Counter_Value"])
         disp[(name, r["Counter_Name"])].add(r["Dispatch_Id"])
 for name, cs in agg.items():

@@ -25,7 +25,7 @@ for d in dirs:
             name = r["Kernel_Name"]
             if "fec::" not in name:
                 continue
-            name = name.split("(")[0].replace("void ", "").replace("fec::", "")
+            name = name.replace("(anonymous namespace)::", "").split("(")[0].replace("void ", "").replace("fec::", "")
             vals[name][r["Counter_Name"]].append(float(r["Counter_Value"]))
 res = {}
 for name, cs in vals.items():
