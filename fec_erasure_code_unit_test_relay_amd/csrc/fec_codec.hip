@@ -4,6 +4,7 @@
 #include <algorithm>
 #include <atomic>
 #include <chrono>
+#include <functional>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -1198,8 +1199,18 @@ int guarded(F&& f) {
 // host-visible staging row (pinned, coherent, mapped), a staging kernel moves it into the device
 // window / ring, the coding kernel writes its result straight into a host-visible result row, one
 // stream synchronisation.  Everything the coder needs from earlier packets stays on the device.
+// A per-packet coder's resident server (fec_server.hip): its mailbox and whether a launch of it
+// may still be running.
+struct ServerHost {
+    fec::ServerBox* h_box = nullptr;  // pinned, coherent, mapped
+    fec::ServerBox* m_box = nullptr;  // its device address
+    bool on = false;                  // this coder runs on a server (else one launch per call)
+    bool live = false;                // a server launch may be running on the coder's stream
+};
+
 struct fec_encoder {
     std::unique_ptr<fec_codec> codec;
+    ServerHost sv;
     int64_t origin = -1;           // seq of the first call (the encoder's creation point)
     int64_t next = 0;              // expected seq
     int res_len_off = 0;           // offset of the trimmed size in the result block (4-aligned)
@@ -1212,17 +1223,13 @@ struct fec_encoder {
     uint8_t* h_done = nullptr;     // pinned, coherent: completion word (ticket of the last finished call)
     uint8_t* m_done = nullptr;
     uint32_t ticket = 0;
-    ~fec_encoder() {
-        if (s) (void)hipStreamDestroy(s);
-        if (d_win) (void)hipFree(d_win);
-        for (void* p : {static_cast<void*>(h_stage), static_cast<void*>(h_res), static_cast<void*>(h_done)})
-            if (p) (void)hipHostFree(p);
-    }
+    ~fec_encoder();
 };
 
 struct fec_decoder {
     static constexpr int RR = 64;  // device ring rows (>= T + k)
     std::unique_ptr<fec_codec> codec;
+    ServerHost sv;
     std::unique_ptr<fec::StreamPlanner> planner;
     int64_t origin = -1;           // seq of the first call; the planner runs on seq - origin
     int64_t next = 0;
@@ -1239,15 +1246,39 @@ struct fec_decoder {
     uint8_t* h_done = nullptr;     // pinned, coherent: completion word (ticket of the last finished call)
     uint8_t* m_done = nullptr;
     uint32_t ticket = 0;
-    ~fec_decoder() {
-        if (s) (void)hipStreamDestroy(s);
-        for (void* p : {static_cast<void*>(d_ring), static_cast<void*>(d_coef)})
-            if (p) (void)hipFree(p);
-        for (void* p : {static_cast<void*>(h_cw), static_cast<void*>(h_coef), static_cast<void*>(h_res),
-                        static_cast<void*>(h_done)})
-            if (p) (void)hipHostFree(p);
-    }
+    ~fec_decoder();
 };
+
+namespace {
+// The server ends on its stop word; the stream then holds no running launch.
+void server_stop(ServerHost& sv, hipStream_t s) {
+    if (sv.live && sv.h_box && s) {
+        reinterpret_cast<volatile fec::ServerBox*>(sv.h_box)->stop = 1;
+        std::atomic_thread_fence(std::memory_order_seq_cst);
+        (void)hipStreamSynchronize(s);
+        sv.live = false;
+    }
+}
+}  // namespace
+
+fec_encoder::~fec_encoder() {
+    server_stop(sv, s);
+    if (s) (void)hipStreamDestroy(s);
+    if (d_win) (void)hipFree(d_win);
+    for (void* p : {static_cast<void*>(h_stage), static_cast<void*>(h_res), static_cast<void*>(h_done),
+                    static_cast<void*>(sv.h_box)})
+        if (p) (void)hipHostFree(p);
+}
+
+fec_decoder::~fec_decoder() {
+    server_stop(sv, s);
+    if (s) (void)hipStreamDestroy(s);
+    for (void* p : {static_cast<void*>(d_ring), static_cast<void*>(d_coef)})
+        if (p) (void)hipFree(p);
+    for (void* p : {static_cast<void*>(h_cw), static_cast<void*>(h_coef), static_cast<void*>(h_res),
+                    static_cast<void*>(h_done), static_cast<void*>(sv.h_box)})
+        if (p) (void)hipHostFree(p);
+}
 
 // ------------------------------------------------------------------------------------------
 // C ABI
@@ -1547,6 +1578,69 @@ hipError_t wait_done(const uint8_t* h_done, uint32_t ticket, hipStream_t s) {
     }
     return hipStreamSynchronize(s);
 }
+
+// Resident servers (fec_server.hip).  FEC_SERVER=0 restores one launch per call.
+bool server_enabled() {
+    static const bool on = [] {
+        const char* v = std::getenv("FEC_SERVER");
+        return !v || std::atoi(v) != 0;
+    }();
+    return on;
+}
+constexpr int64_t kServerIdleTicks = 5000000;  // 50 ms of the 100 MHz counter without a request
+
+// Post request `ticket` (its fields and rows are written) and make sure a server serves it.  A
+// server that announced its exit (alive = 0) is waited for; it is relaunched unless it served this
+// request on its way out (fec_server.hip: the exit handshake).
+hipError_t server_post(ServerHost& sv, uint32_t ticket, hipStream_t s,
+                       const std::function<hipError_t(uint32_t)>& launch) {
+    volatile fec::ServerBox* b = sv.h_box;
+    if (!sv.live) {
+        b->alive = 1;
+        std::atomic_thread_fence(std::memory_order_seq_cst);
+        if (hipError_t e = launch(ticket - 1)) return e;
+        sv.live = true;
+    }
+    std::atomic_thread_fence(std::memory_order_release);
+    b->req = ticket;
+    std::atomic_thread_fence(std::memory_order_seq_cst);
+    if (b->alive == 0) {
+        if (hipError_t e = hipStreamSynchronize(s)) return e;
+        sv.live = false;
+        if (b->done != ticket) {
+            b->alive = 1;
+            std::atomic_thread_fence(std::memory_order_seq_cst);
+            if (hipError_t e = launch(ticket - 1)) return e;
+            sv.live = true;
+        }
+    }
+    return hipSuccess;
+}
+
+// Wait for the server's done ticket (in host memory: no PCIe round trip per poll).  A launch that
+// failed, or a server that stopped (alive = 0) before finishing, is reported after the stream is
+// drained; ten seconds without an answer are reported as an error.
+hipError_t server_wait(ServerHost& sv, uint32_t ticket, hipStream_t s) {
+    const volatile fec::ServerBox* b = sv.h_box;
+    const auto t0 = std::chrono::steady_clock::now();
+    for (uint32_t i = 1;; ++i) {
+        if (b->done == ticket) {
+            std::atomic_thread_fence(std::memory_order_acquire);
+            return hipSuccess;
+        }
+        if ((i & 4095) == 0) {
+            if (b->alive == 0) {  // the server is gone without this request's answer
+                const hipError_t e = hipStreamSynchronize(s);
+                sv.live = false;
+                if (b->done == ticket) return hipSuccess;
+                return e != hipSuccess ? e : hipErrorLaunchFailure;
+            }
+            if (hipError_t e = hipStreamQuery(s); e != hipSuccess && e != hipErrorNotReady) return e;
+            if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(10)) return hipErrorLaunchTimeOut;
+        }
+        __builtin_ia32_pause();
+    }
+}
 }  // namespace
 
 int fec_encoder_create(int max_payload, int T, int B, int N, fec_encoder** out) {
@@ -1567,6 +1661,12 @@ int fec_encoder_create(int max_payload, int T, int B, int N, fec_encoder** out) 
         HIP_TRY(host_mapped(&e->h_stage, &e->m_stage, (g.L + 3) & ~3));
         HIP_TRY(host_mapped(&e->h_res, &e->m_res, e->res_len_off + 4));
         HIP_TRY(host_mapped(&e->h_done, &e->m_done, 4));
+        const int W = std::max(1, g.n - 1), SK = g.S * g.k;
+        e->sv.on = server_enabled() && g.CW <= 2048 && g.L <= 1500 && g.k * g.n <= 16 * 32 &&
+                   static_cast<int64_t>(W) * SK <= 48 * 1024;
+        if (e->sv.on)
+            HIP_TRY(host_mapped(reinterpret_cast<uint8_t**>(&e->sv.h_box), reinterpret_cast<uint8_t**>(&e->sv.m_box),
+                                sizeof(fec::ServerBox)));
         HIP_TRY(hipDeviceSynchronize());  // the window is zero before the first call's kernel
         *out = e.release();
         return FEC_OK;
@@ -1592,13 +1692,47 @@ int fec_encoder_transmit(fec_encoder* e, const uint8_t* data, int payload, int s
     if (seq != e->next) return FEC_ERR_SEQUENCE;
     const Geometry& g = e->codec->g;
     if (payload > g.L) payload = g.L;
+    fec::CodecView v;
+    if (int st = fec::codec_view(e->codec.get(), &v)) return st;
+    if (e->sv.on) {
+        // the resident server: payload and request into the mailbox, no launch (fec_server.hip)
+        if (payload > 0) std::memcpy(e->h_stage, data, payload);
+        volatile fec::ServerBox* b = e->sv.h_box;
+        b->len = payload;
+        b->seq = seq - e->origin;
+        const uint32_t ticket = ++e->ticket;
+        auto launch = [&](uint32_t last) -> hipError_t {
+            fec::EncServerArgs a;
+            a.box = e->sv.m_box;
+            a.stage = e->m_stage;
+            a.res = e->m_res;
+            a.res_len_off = e->res_len_off;
+            a.win_home = e->d_win;
+            a.G = v.G;
+            a.gf = v.gf;
+            a.L = g.L;
+            a.k = g.k;
+            a.n = g.n;
+            a.S = g.S;
+            a.CW = g.CW;
+            a.SK = g.S * g.k;
+            a.W = std::max(1, g.n - 1);
+            a.last = last;
+            a.idle_ticks = kServerIdleTicks;
+            return fec::server_encode_launch(a, e->s) == FEC_OK ? hipSuccess : hipErrorLaunchFailure;
+        };
+        HIP_TRY(server_post(e->sv, ticket, e->s, launch));
+        HIP_TRY(server_wait(e->sv, ticket, e->s));
+        std::memcpy(cw_out, e->h_res, g.CW);
+        std::memcpy(cw_size, e->h_res + e->res_len_off, 4);
+        ++e->next;
+        return FEC_OK;
+    }
     // one launch: the closed form over the device-resident window (fec_streams_encode_kernel reads
     // the payload from the mapped staging row, writes codeword and size into the mapped result row,
     // then the completion word)
     if (e->ticket) HIP_TRY(wait_done(e->h_done, e->ticket, e->s));  // h_stage is free again
     if (payload > 0) std::memcpy(e->h_stage, data, payload);
-    fec::CodecView v;
-    if (int st = fec::codec_view(e->codec.get(), &v)) return st;
     const uint32_t ticket = ++e->ticket;
     if (int st = fec::stream_encode_one(v, e->d_win, e->m_stage, payload, seq - e->origin, e->m_res,
                                         reinterpret_cast<int32_t*>(e->m_res + e->res_len_off),
@@ -1629,9 +1763,14 @@ int fec_decoder_create(int max_payload, int T, int B, int N, fec_decoder** out) 
         HIP_TRY(hipMemset(d->d_ring, 0, static_cast<size_t>(fec_decoder::RR) * g.CW));
         HIP_TRY(hipMalloc(&d->d_coef, g.k * g.n));
         HIP_TRY(host_mapped(&d->h_cw, &d->m_cw, (g.CW + 3) & ~3));
-        HIP_TRY(host_mapped(&d->h_coef, &d->m_coef, g.k * g.n));
+        HIP_TRY(host_mapped(&d->h_coef, &d->m_coef, (g.k * g.n + 3) & ~3));
         HIP_TRY(host_mapped(&d->h_res, &d->m_res, d->res_len_off + 4));
         HIP_TRY(host_mapped(&d->h_done, &d->m_done, 4));
+        d->sv.on = server_enabled() && g.k * g.n <= 16 * 32 &&
+                   static_cast<int64_t>(fec_decoder::RR) * g.CW <= 48 * 1024;
+        if (d->sv.on)
+            HIP_TRY(host_mapped(reinterpret_cast<uint8_t**>(&d->sv.h_box), reinterpret_cast<uint8_t**>(&d->sv.m_box),
+                                sizeof(fec::ServerBox)));
         HIP_TRY(hipDeviceSynchronize());  // the ring is zero before the first call's kernel
         *out = d.release();
         return FEC_OK;
@@ -1658,7 +1797,7 @@ int fec_decoder_receive(fec_decoder* d, const uint8_t* cw, int cw_size, int seq,
     const Geometry& g = d->codec->g;
     const bool er = erasure != 0 || cw == nullptr;
     // the previous call's kernel has read h_cw / h_coef (its completion word is set)
-    if (d->ticket) HIP_TRY(wait_done(d->h_done, d->ticket, d->s));
+    if (d->ticket) HIP_TRY(d->sv.on ? server_wait(d->sv, d->ticket, d->s) : wait_done(d->h_done, d->ticket, d->s));
     fec::StepResult r;
     int st = guarded([&] {
         r = d->planner->step(rel, er);
@@ -1676,6 +1815,43 @@ int fec_decoder_receive(fec_decoder* d, const uint8_t* cw, int cw_size, int seq,
         const int sz = std::max(0, std::min(cw_size, g.CW));
         std::memset(d->h_cw, 0, (g.CW + 3) & ~3);
         if (sz) std::memcpy(d->h_cw, cw, sz);
+    }
+    if (d->sv.on) {
+        // the resident server: codeword / coefficients and request into the mailbox, no launch
+        if (r.fate == fec::kRecovered) std::memcpy(d->h_coef, r.coef, g.k * g.n);
+        volatile fec::ServerBox* b = d->sv.h_box;
+        b->erased = er ? 1 : 0;
+        b->fate = r.fate;
+        b->clamp = r.slow ? 1 : 0;
+        b->seq = rel;
+        b->x = r.x;
+        fec::CodecView v;
+        if (int e = fec::codec_view(d->codec.get(), &v)) return e;
+        const uint32_t ticket = ++d->ticket;
+        auto launch = [&](uint32_t last) -> hipError_t {
+            fec::DecServerArgs a;
+            a.box = d->sv.m_box;
+            a.stage = d->m_cw;
+            a.coef = d->m_coef;
+            a.res = d->m_res;
+            a.res_len_off = d->res_len_off;
+            a.ring_home = d->d_ring;
+            a.gf = v.gf;
+            a.L = g.L;
+            a.k = g.k;
+            a.n = g.n;
+            a.CW = g.CW;
+            a.RR = fec_decoder::RR;
+            a.last = last;
+            a.idle_ticks = kServerIdleTicks;
+            return fec::server_decode_launch(a, d->s) == FEC_OK ? hipSuccess : hipErrorLaunchFailure;
+        };
+        HIP_TRY(server_post(d->sv, ticket, d->s, launch));
+        if (no_output) return FEC_OK;  // the codeword is stored asynchronously; the next call waits for it
+        HIP_TRY(server_wait(d->sv, ticket, d->s));
+        std::memcpy(payload_out, d->h_res, g.L);
+        std::memcpy(payload, d->h_res + d->res_len_off, 4);
+        return FEC_OK;
     }
     const uint8_t* coef = nullptr;
     if (r.fate == fec::kRecovered) {

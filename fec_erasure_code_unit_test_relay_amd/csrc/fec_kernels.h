@@ -392,6 +392,49 @@ int codec_view(const ::fec_codec* c, CodecView* v);
 // of one stream whose window ring `win` ([n-1][S*k], fec_streams.hip's layout) lives on the device,
 // through fec_streams_encode_kernel in one launch.  payload / cw / cw_len may be host-visible
 // (mapped) rows; after them the kernel stores `ticket` into `done`.
+// ---- resident per-packet servers (fec_server.hip) ----------------------------------------
+// Mailbox shared by a per-packet coder (host) and its server workgroup (device), in pinned,
+// coherent, mapped host memory.  The host writes the request fields, then `req`; the server
+// writes the result row, then `done`; `stop` ends the server, `alive` is its exit handshake.
+struct ServerBox {
+    uint32_t req;     // ticket of the latest request (host, written last)
+    uint32_t stop;    // host: 1 = exit now
+    uint32_t alive;   // 1 while a server polls (host sets it before a launch; the server clears it on exit)
+    uint32_t done;    // ticket of the latest finished request (server, written last)
+    int32_t len;      // encoder: payload size
+    int32_t erased;   // decoder: this call's packet is missing
+    int32_t fate;     // decoder: PacketFate of packet x
+    int32_t clamp;    // decoder: slow path (length clamped to max_payload, Decoder.cpp:148-149)
+    int64_t seq;      // seq relative to the coder's origin
+    int64_t x;        // decoder: packet output by this call (relative)
+};
+struct EncServerArgs {
+    ServerBox* box;
+    const uint8_t* stage;       // mapped payload row (dword padded)
+    uint8_t* res;               // mapped result row: codeword (dword padded) | trimmed size at res_len_off
+    int res_len_off;
+    uint8_t* win_home;          // HBM home of the W x SK window ring between launches
+    const uint8_t* G;
+    const uint8_t* gf;
+    int L, k, n, S, CW, SK, W;
+    uint32_t last;              // ticket served before this launch
+    int64_t idle_ticks;         // exit after this long without a request (100 MHz real-time counter)
+};
+struct DecServerArgs {
+    ServerBox* box;
+    const uint8_t* stage;       // mapped codeword row (dword padded)
+    const uint8_t* coef;        // mapped k x n coefficients (dword padded)
+    uint8_t* res;               // mapped result row: payload (dword padded) | length at res_len_off
+    int res_len_off;
+    uint8_t* ring_home;         // HBM home of the RR x CW ring between launches
+    const uint8_t* gf;
+    int L, k, n, CW, RR;
+    uint32_t last;
+    int64_t idle_ticks;
+};
+int server_encode_launch(const EncServerArgs& a, hipStream_t s);
+int server_decode_launch(const DecServerArgs& a, hipStream_t s);
+
 int stream_encode_one(const CodecView& v, uint8_t* win, const uint8_t* payload, int payload_len, int64_t seq,
                       uint8_t* cw, int32_t* cw_len, uint32_t* done, uint32_t ticket, hipStream_t s);
 // The per-packet FEC_Decoder's call: store packet `seq`'s codeword `cw` (a host-visible row padded to

@@ -1,0 +1,258 @@
+// fec_server.hip -- the per-packet coders' resident servers: one workgroup per FEC_Encoder /
+// FEC_Decoder that stays on the GPU between calls and takes each call's packet from a host-visible
+// mailbox, so that a call costs no kernel launch.
+//
+// The reference's contract is synchronous and per packet (FEC_Encoder::onTransmit,
+// FEC_Encoder.cpp:42-68; FEC_Decoder::onReceive, FEC_Decoder.cpp:49-72): the codeword (payload)
+// comes back from the call.  A launch per call costs more than the reference's whole CPU encode
+// (DESIGN.md §4), so the coder keeps a server workgroup polling its mailbox instead:
+//   host:   payload / codeword -> mapped staging row, request fields, then the request ticket;
+//   server: sees the ticket, does the packet's byte work against its state, which it keeps in LDS
+//           for its whole life (the encoder's n-1 windows, Encoder.cpp:73-95 / the decoder's ring of
+//           received codewords, FEC_Decoder.cpp:55-63), writes the result row, then the done ticket;
+//   host:   polls the done ticket in its own (coherent) memory.
+// Every poll also reads a stop word (set when the coder is destroyed), and a server that has seen
+// no request for `idle_ticks` of the 100 MHz real-time counter writes its state back to HBM and
+// exits; the next call launches a new one.  So every launch ends: on the stop word, on idle, or on
+// the process's exit.  The exit handshake (alive = 0, then one more look at the request word) and
+// the host's check of `alive` after posting are Dekker-ordered by sequentially consistent fences on
+// both sides; a host that sees alive = 0 waits for the launch to end before relaunching, so a
+// request is never served twice.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "fec_amd.h"
+#include "fec_host.h"
+#include "fec_kernels.h"
+
+namespace fec {
+namespace {
+
+__device__ __forceinline__ uint32_t sys_load(const uint32_t* p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ int64_t sys_load64(const int64_t* p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ void sys_store(uint32_t* p, uint32_t v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ uint8_t sgmul(const uint8_t* gexp, const uint8_t* glog, uint8_t a, uint8_t b) {
+    return (a && b) ? gexp[glog[a] + glog[b]] : 0;
+}
+
+enum : uint32_t { kCmdIdle = 0, kCmdStop = 1, kCmdWork = 2 };
+
+// Thread 0 waits for the next request (a ticket other than `last`), the stop word or the idle limit;
+// the command lands in `cmd` for the whole workgroup.
+__device__ __forceinline__ uint32_t server_wait(ServerBox* box, uint32_t last, int64_t idle_ticks, uint32_t* cmd,
+                                                uint32_t* ticket) {
+    if (threadIdx.x == 0) {
+        uint32_t c = kCmdIdle, t = last;
+        const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+        for (;;) {
+            if (sys_load(&box->stop)) {
+                c = kCmdStop;
+                break;
+            }
+            t = sys_load(&box->req);
+            if (t != last) {
+                c = kCmdWork;
+                break;
+            }
+            if (static_cast<int64_t>(__builtin_amdgcn_s_memrealtime() - t0) > idle_ticks) {
+                // exit handshake: announce, then one more look (a request posted meanwhile is served)
+                sys_store(&box->alive, 0u);
+                __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "");
+                t = sys_load(&box->req);
+                if (t != last && !sys_load(&box->stop)) {
+                    sys_store(&box->alive, 1u);
+                    c = kCmdWork;
+                }
+                break;
+            }
+            __builtin_amdgcn_s_sleep(2);
+        }
+        if (c == kCmdWork) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // the request's fields and rows
+        *cmd = c;
+        *ticket = t;
+    }
+    __syncthreads();
+    return *cmd;
+}
+
+// After every thread's result stores: the done ticket, behind a system-scope release.
+__device__ __forceinline__ void server_done(ServerBox* box, uint32_t ticket) {
+    __threadfence_system();
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        sys_store(&box->done, ticket);
+    }
+}
+
+}  // namespace
+
+// Encoder server.  Per request (seq relative to the coder's origin, payload size): the codeword
+// of the closed form (Encoder.cpp:65-98 -> codingOperations.cpp:131-147) over the LDS windows, a
+// thread per codeword byte; then the packet's own window row replaces row seq - W.
+__global__ __launch_bounds__(256) void fec_encoder_server_kernel(EncServerArgs a) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t win[];  // W x SK window ring (slot seq % W)
+    __shared__ uint8_t gexp[512];
+    __shared__ uint8_t glog[256];
+    __shared__ uint8_t Gs[16 * 32];
+    __shared__ uint32_t prow[376];  // payload row (L <= 1500)
+    __shared__ uint32_t cwl[512];   // codeword (CW <= 2048)
+    __shared__ int ro[32];          // window offset of packet seq - d (-1: before the coder's origin)
+    __shared__ int last_nz;
+    __shared__ uint32_t cmd, ticket;
+    __shared__ int s_len;
+    __shared__ long long s_seq;
+    const int tid = threadIdx.x;
+    const int L = a.L, k = a.k, n = a.n, CW = a.CW, SK = a.SK, W = a.W;
+    for (int i = tid; i < 512; i += 256) gexp[i] = a.gf[i];
+    for (int i = tid; i < 256; i += 256) glog[i] = a.gf[512 + i];
+    for (int i = tid; i < k * n; i += 256) Gs[i] = a.G[i];
+    for (int b = tid; b < W * SK; b += 256) win[b] = a.win_home[b];
+    __syncthreads();
+    uint32_t last = a.last;
+    while (server_wait(a.box, last, a.idle_ticks, &cmd, &ticket) == kCmdWork) {
+        const uint32_t tk = ticket;
+        if (tid == 0) {
+            s_len = static_cast<int>(sys_load(reinterpret_cast<const uint32_t*>(&a.box->len)));
+            s_seq = sys_load64(&a.box->seq);
+            last_nz = -1;
+        }
+        for (int w = tid; 4 * w < L; w += 256) prow[w] = sys_load(reinterpret_cast<const uint32_t*>(a.stage) + w);
+        __syncthreads();
+        const int ln = min(max(s_len, 0), L);
+        const int64_t seq = s_seq;
+        if (tid < 32) ro[tid] = (tid >= 1 && seq - tid >= 0) ? static_cast<int>((seq - tid) % W) * SK : -1;
+        __syncthreads();
+        const uint8_t* pay = reinterpret_cast<const uint8_t*>(prow);
+        auto xbyte = [&](int b) -> uint8_t {  // [len_hi, len_lo, payload, zero pad] (Encoder.cpp:75-83)
+            return b == 0 ? static_cast<uint8_t>(ln >> 8)
+                          : b == 1 ? static_cast<uint8_t>(ln & 0xff) : (b - 2 < ln ? pay[b - 2] : 0);
+        };
+        uint8_t* cwb = reinterpret_cast<uint8_t*>(cwl);
+        int lastc = -1;
+        for (int c = tid; c < CW; c += 256) {
+            const int s = c / n, j = c - s * n;
+            uint8_t v = 0;
+            if (j < k) {
+                v = xbyte(s * k + j);
+            } else {  // parity: XOR_i G[i][j] * X_{t-(j-i)}[s][i], rows before the origin = 0
+                for (int i = 0; i < k; ++i) {
+                    const int r = ro[j - i];
+                    if (r >= 0) v ^= sgmul(gexp, glog, Gs[i * n + j], win[r + s * k + i]);
+                }
+            }
+            cwb[c] = v;
+            if (v) lastc = c;
+        }
+        for (int c = CW + tid; c < ((CW + 3) & ~3); c += 256) cwb[c] = 0;  // the row's dword padding
+        if (lastc >= 0) atomicMax(&last_nz, lastc);
+        __syncthreads();  // codeword complete; window slot seq % W (row seq - W) has been read
+        const int own = static_cast<int>(seq % W) * SK;
+        for (int b = tid; b < SK; b += 256) win[own + b] = xbyte(b);
+        for (int w = tid; 4 * w < CW; w += 256) reinterpret_cast<uint32_t*>(a.res)[w] = cwl[w];
+        if (tid == 0) *reinterpret_cast<int32_t*>(a.res + a.res_len_off) = last_nz + 1;  // FEC_Encoder.cpp:55-60
+        server_done(a.box, tk);
+        last = tk;
+        __syncthreads();  // the window row is in place before the next request's reads
+    }
+    // stop or idle: the windows go back to HBM for the next launch (kernel end makes them visible)
+    for (int b = tid; b < W * SK; b += 256) a.win_home[b] = win[b];
+}
+
+// Decoder server.  Per request (the host planner's step for seq: the packet's erasure, and the
+// fate of packet x = seq - T with its recovery coefficients): store the received codeword in the
+// LDS ring (FEC_Decoder.cpp:55-63), then output packet x -- the fast-path copy (Decoder.cpp:77-108)
+// or the recovery (codingOperations.cpp:149-232) -- into the result row.
+__global__ __launch_bounds__(256) void fec_decoder_server_kernel(DecServerArgs a) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t ring[];  // RR x CW (slot seq % RR)
+    __shared__ uint8_t gexp[512];
+    __shared__ uint8_t glog[256];
+    __shared__ uint8_t coef[16 * 32];
+    __shared__ uint32_t cmd, ticket;
+    __shared__ int s_erased, s_fate, s_clamp, s_hdr;
+    __shared__ long long s_seq, s_x;
+    const int tid = threadIdx.x;
+    const int L = a.L, k = a.k, n = a.n, CW = a.CW, RR = a.RR;
+    for (int i = tid; i < 512; i += 256) gexp[i] = a.gf[i];
+    for (int i = tid; i < 256; i += 256) glog[i] = a.gf[512 + i];
+    for (int b = tid; b < RR * CW; b += 256) ring[b] = a.ring_home[b];
+    __syncthreads();
+    uint32_t last = a.last;
+    while (server_wait(a.box, last, a.idle_ticks, &cmd, &ticket) == kCmdWork) {
+        const uint32_t tk = ticket;
+        if (tid == 0) {
+            s_erased = static_cast<int>(sys_load(reinterpret_cast<const uint32_t*>(&a.box->erased)));
+            s_fate = static_cast<int>(sys_load(reinterpret_cast<const uint32_t*>(&a.box->fate)));
+            s_clamp = static_cast<int>(sys_load(reinterpret_cast<const uint32_t*>(&a.box->clamp)));
+            s_seq = sys_load64(&a.box->seq);
+            s_x = sys_load64(&a.box->x);
+        }
+        __syncthreads();
+        const int64_t seq = s_seq, x = s_x;
+        const int fate = s_fate;
+        if (!s_erased) {  // the decoder keeps its own copy of the (zero-padded) codeword
+            uint8_t* dst = ring + (seq % RR) * CW;
+            for (int w = tid; 4 * w < CW; w += 256) {
+                const uint32_t v = sys_load(reinterpret_cast<const uint32_t*>(a.stage) + w);
+#pragma unroll
+                for (int e = 0; e < 4; ++e)
+                    if (4 * w + e < CW) dst[4 * w + e] = static_cast<uint8_t>(v >> (8 * e));
+            }
+        }
+        if (fate == kRecovered)
+            for (int w = tid; 4 * w < k * n; w += 256)
+                reinterpret_cast<uint32_t*>(coef)[w] = sys_load(reinterpret_cast<const uint32_t*>(a.coef) + w);
+        __syncthreads();
+        // symbol (s, q) of packet sp from the ring (sp < 0: a zero row, never with a non-zero coefficient)
+        auto sym = [&](int64_t sp, int o) -> uint8_t { return sp < 0 ? 0 : ring[(sp % RR) * CW + o]; };
+        auto byte_at = [&](int h) -> uint8_t {
+            const int s = h / k, i = h - s * k;
+            if (fate == kCopy) return sym(x, s * n + i);
+            uint8_t acc = 0;
+            for (int q = 0; q < n; ++q) {
+                const uint8_t c = coef[i * n + q];
+                if (c) acc ^= sgmul(gexp, glog, c, sym(x - i + q, s * n + q));
+            }
+            return acc;
+        };
+        const bool out = fate == kCopy || fate == kRecovered;
+        if (tid == 0) s_hdr = out ? byte_at(0) * 256 + byte_at(1) : 0;
+        __syncthreads();
+        const int ln = out ? (s_clamp ? min(s_hdr, L) : s_hdr) : 0;
+        const int cp = min(ln, L);
+        uint8_t* orow = a.res;
+        for (int w = tid; 4 * w < L; w += 256) {
+            uint32_t v = 0;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const int b = 4 * w + e;
+                if (b < cp) v |= static_cast<uint32_t>(byte_at(b + 2)) << (8 * e);
+            }
+            reinterpret_cast<uint32_t*>(orow)[w] = v;
+        }
+        if (tid == 0) *reinterpret_cast<int32_t*>(a.res + a.res_len_off) = ln;
+        server_done(a.box, tk);
+        last = tk;
+        __syncthreads();
+    }
+    for (int b = tid; b < RR * CW; b += 256) a.ring_home[b] = ring[b];
+}
+
+int server_encode_launch(const EncServerArgs& a, hipStream_t s) {
+    hipLaunchKernelGGL(fec_encoder_server_kernel, dim3(1), dim3(256), static_cast<size_t>(a.W) * a.SK, s, a);
+    return hipGetLastError() == hipSuccess ? FEC_OK : FEC_ERR_HIP;
+}
+
+int server_decode_launch(const DecServerArgs& a, hipStream_t s) {
+    hipLaunchKernelGGL(fec_decoder_server_kernel, dim3(1), dim3(256), static_cast<size_t>(a.RR) * a.CW, s, a);
+    return hipGetLastError() == hipSuccess ? FEC_OK : FEC_ERR_HIP;
+}
+
+}  // namespace fec
