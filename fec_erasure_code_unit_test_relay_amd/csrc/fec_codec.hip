@@ -1766,7 +1766,7 @@ int fec_decoder_create(int max_payload, int T, int B, int N, fec_decoder** out) 
         HIP_TRY(host_mapped(&d->h_coef, &d->m_coef, (g.k * g.n + 3) & ~3));
         HIP_TRY(host_mapped(&d->h_res, &d->m_res, d->res_len_off + 4));
         HIP_TRY(host_mapped(&d->h_done, &d->m_done, 4));
-        d->sv.on = server_enabled() && g.k * g.n <= 16 * 32 &&
+        d->sv.on = server_enabled() && g.k * g.n <= 16 * 32 && g.CW <= 4096 &&
                    static_cast<int64_t>(fec_decoder::RR) * g.CW <= 48 * 1024;
         if (d->sv.on)
             HIP_TRY(host_mapped(reinterpret_cast<uint8_t**>(&d->sv.h_box), reinterpret_cast<uint8_t**>(&d->sv.m_box),

@@ -21,6 +21,7 @@
 #pragma once
 
 #include <hip/hip_runtime.h>
+#include <cstddef>
 #include <stdint.h>
 
 namespace fec {
@@ -408,6 +409,8 @@ struct ServerBox {
     int64_t seq;      // seq relative to the coder's origin
     int64_t x;        // decoder: packet output by this call (relative)
 };
+static_assert(offsetof(ServerBox, len) == 16 && offsetof(ServerBox, x) == 40 && sizeof(ServerBox) == 48,
+              "the server loads the 8 field dwords after the 4 control words");
 struct EncServerArgs {
     ServerBox* box;
     const uint8_t* stage;       // mapped payload row (dword padded)

@@ -31,9 +31,6 @@ namespace {
 __device__ __forceinline__ uint32_t sys_load(const uint32_t* p) {
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
-__device__ __forceinline__ int64_t sys_load64(const int64_t* p) {
-    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-}
 __device__ __forceinline__ void sys_store(uint32_t* p, uint32_t v) {
     __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
@@ -51,11 +48,13 @@ __device__ __forceinline__ uint32_t server_wait(ServerBox* box, uint32_t last, i
         uint32_t c = kCmdIdle, t = last;
         const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
         for (;;) {
-            if (sys_load(&box->stop)) {
+            // both words in one round trip
+            const uint32_t st = sys_load(&box->stop);
+            t = sys_load(&box->req);
+            if (st) {
                 c = kCmdStop;
                 break;
             }
-            t = sys_load(&box->req);
             if (t != last) {
                 c = kCmdWork;
                 break;
@@ -79,6 +78,11 @@ __device__ __forceinline__ uint32_t server_wait(ServerBox* box, uint32_t last, i
     }
     __syncthreads();
     return *cmd;
+}
+
+// The request's 8 field dwords (len, erased, fate, clamp, seq, x), one per thread 0..7.
+__device__ __forceinline__ void load_fields(const ServerBox* box, uint32_t* fld) {
+    if (threadIdx.x < 8) fld[threadIdx.x] = sys_load(reinterpret_cast<const uint32_t*>(&box->len) + threadIdx.x);
 }
 
 // After every thread's result stores: the done ticket, behind a system-scope release.
@@ -107,8 +111,7 @@ __global__ __launch_bounds__(256) void fec_encoder_server_kernel(EncServerArgs a
     __shared__ int ro[32];          // window offset of packet seq - d (-1: before the coder's origin)
     __shared__ int last_nz;
     __shared__ uint32_t cmd, ticket;
-    __shared__ int s_len;
-    __shared__ long long s_seq;
+    __shared__ uint32_t fld[8];
     const int tid = threadIdx.x;
     const int L = a.L, k = a.k, n = a.n, CW = a.CW, SK = a.SK, W = a.W;
     for (int i = tid; i < 512; i += 256) gexp[i] = a.gf[i];
@@ -119,15 +122,14 @@ __global__ __launch_bounds__(256) void fec_encoder_server_kernel(EncServerArgs a
     uint32_t last = a.last;
     while (server_wait(a.box, last, a.idle_ticks, &cmd, &ticket) == kCmdWork) {
         const uint32_t tk = ticket;
-        if (tid == 0) {
-            s_len = static_cast<int>(sys_load(reinterpret_cast<const uint32_t*>(&a.box->len)));
-            s_seq = sys_load64(&a.box->seq);
-            last_nz = -1;
-        }
+        // the request's fields (8 dwords after the control words) and the payload row, all loads
+        // in flight together: one PCIe round trip
+        load_fields(a.box, fld);
         for (int w = tid; 4 * w < L; w += 256) prow[w] = sys_load(reinterpret_cast<const uint32_t*>(a.stage) + w);
+        if (tid == 0) last_nz = -1;
         __syncthreads();
-        const int ln = min(max(s_len, 0), L);
-        const int64_t seq = s_seq;
+        const int ln = min(max(static_cast<int>(fld[0]), 0), L);
+        const int64_t seq = static_cast<int64_t>(fld[4]) | (static_cast<int64_t>(fld[5]) << 32);
         if (tid < 32) ro[tid] = (tid >= 1 && seq - tid >= 0) ? static_cast<int>((seq - tid) % W) * SK : -1;
         __syncthreads();
         const uint8_t* pay = reinterpret_cast<const uint8_t*>(prow);
@@ -176,8 +178,8 @@ __global__ __launch_bounds__(256) void fec_decoder_server_kernel(DecServerArgs a
     __shared__ uint8_t glog[256];
     __shared__ uint8_t coef[16 * 32];
     __shared__ uint32_t cmd, ticket;
-    __shared__ int s_erased, s_fate, s_clamp, s_hdr;
-    __shared__ long long s_seq, s_x;
+    __shared__ uint32_t fld[8];
+    __shared__ int s_hdr;
     const int tid = threadIdx.x;
     const int L = a.L, k = a.k, n = a.n, CW = a.CW, RR = a.RR;
     for (int i = tid; i < 512; i += 256) gexp[i] = a.gf[i];
@@ -187,28 +189,33 @@ __global__ __launch_bounds__(256) void fec_decoder_server_kernel(DecServerArgs a
     uint32_t last = a.last;
     while (server_wait(a.box, last, a.idle_ticks, &cmd, &ticket) == kCmdWork) {
         const uint32_t tk = ticket;
-        if (tid == 0) {
-            s_erased = static_cast<int>(sys_load(reinterpret_cast<const uint32_t*>(&a.box->erased)));
-            s_fate = static_cast<int>(sys_load(reinterpret_cast<const uint32_t*>(&a.box->fate)));
-            s_clamp = static_cast<int>(sys_load(reinterpret_cast<const uint32_t*>(&a.box->clamp)));
-            s_seq = sys_load64(&a.box->seq);
-            s_x = sys_load64(&a.box->x);
+        // the request's fields, the staged codeword and the coefficients, all loads in flight
+        // together (one PCIe round trip); the codeword and coefficients are used only when the
+        // fields say so
+        load_fields(a.box, fld);
+        uint32_t cwv[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int w = tid + 256 * q;
+            cwv[q] = 4 * w < CW ? sys_load(reinterpret_cast<const uint32_t*>(a.stage) + w) : 0u;
         }
+        for (int w = tid; 4 * w < k * n; w += 256)
+            reinterpret_cast<uint32_t*>(coef)[w] = sys_load(reinterpret_cast<const uint32_t*>(a.coef) + w);
         __syncthreads();
-        const int64_t seq = s_seq, x = s_x;
-        const int fate = s_fate;
-        if (!s_erased) {  // the decoder keeps its own copy of the (zero-padded) codeword
+        const int64_t seq = static_cast<int64_t>(fld[4]) | (static_cast<int64_t>(fld[5]) << 32);
+        const int64_t x = static_cast<int64_t>(fld[6]) | (static_cast<int64_t>(fld[7]) << 32);
+        const int fate = static_cast<int>(fld[2]);
+        const int clamp = static_cast<int>(fld[3]);
+        if (!fld[1]) {  // the decoder keeps its own copy of the (zero-padded) codeword
             uint8_t* dst = ring + (seq % RR) * CW;
-            for (int w = tid; 4 * w < CW; w += 256) {
-                const uint32_t v = sys_load(reinterpret_cast<const uint32_t*>(a.stage) + w);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int w = tid + 256 * q;
 #pragma unroll
                 for (int e = 0; e < 4; ++e)
-                    if (4 * w + e < CW) dst[4 * w + e] = static_cast<uint8_t>(v >> (8 * e));
+                    if (4 * w + e < CW) dst[4 * w + e] = static_cast<uint8_t>(cwv[q] >> (8 * e));
             }
         }
-        if (fate == kRecovered)
-            for (int w = tid; 4 * w < k * n; w += 256)
-                reinterpret_cast<uint32_t*>(coef)[w] = sys_load(reinterpret_cast<const uint32_t*>(a.coef) + w);
         __syncthreads();
         // symbol (s, q) of packet sp from the ring (sp < 0: a zero row, never with a non-zero coefficient)
         auto sym = [&](int64_t sp, int o) -> uint8_t { return sp < 0 ? 0 : ring[(sp % RR) * CW + o]; };
@@ -225,7 +232,7 @@ __global__ __launch_bounds__(256) void fec_decoder_server_kernel(DecServerArgs a
         const bool out = fate == kCopy || fate == kRecovered;
         if (tid == 0) s_hdr = out ? byte_at(0) * 256 + byte_at(1) : 0;
         __syncthreads();
-        const int ln = out ? (s_clamp ? min(s_hdr, L) : s_hdr) : 0;
+        const int ln = out ? (clamp ? min(s_hdr, L) : s_hdr) : 0;
         const int cp = min(ln, L);
         uint8_t* orow = a.res;
         for (int w = tid; 4 * w < L; w += 256) {
