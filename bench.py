@@ -465,7 +465,7 @@ def main():
     ap.add_argument("--cpu-packets", type=int, default=30000)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-host-inclusive", action="store_true")
-    ap.add_argument("--encode-path", default="auto", help="A/B: auto|generic|fast|stream|wave|tile")
+    ap.add_argument("--encode-path", default="auto", help="A/B: auto|generic|tile")
     ap.add_argument("--no-extra-configs", action="store_true", help="skip BASELINE configs 3 and 4")
     ap.add_argument("--warm-seconds", type=float, default=1.0,
                     help="untimed replays of the step for this much wall time before the W warm-up "

@@ -83,18 +83,15 @@ class Codec:
         return G.reshape(self.k, self.n)
 
     def set_encode_path(self, path: str) -> None:
-        """'auto', 'generic', 'fast' (per-tile k, n-k specialised kernel), 'stream' (the
-        persistent specialised kernel), 'wave' (the wave-sequence kernel) or 'tile' (contiguous
-        LDS-tile runs per workgroup; auto's first choice)."""
-        code = {"auto": 0, "generic": 1, "fast": 2, "stream": 3, "wave": 4, "tile": 5}[path]
+        """'auto', 'generic' (fec_encode_kernel, any geometry and alignment) or 'tile' (the
+        (k, n-k)-specialised LDS-tile kernel, auto's choice when it applies)."""
+        code = {"auto": 0, "generic": 1, "tile": 5}[path]
         check(lib().fec_codec_set_encode_path(self._h, code), "fec_codec_set_encode_path")
 
     def set_copy_path(self, path: str) -> None:
-        """'auto', 'generic', 'fast' (LDS tiles), 'wave' (barrier-free), 'chunk' (a lane per 16-byte
-        output piece, k | 16), 'pipe' (one LDS-DMA pipeline per wave) or 'tile' (persistent
-        per-workgroup tile runs, register-staged prefetch) for the decoder's received-packet
-        kernel."""
-        code = {"auto": 0, "generic": 1, "fast": 2, "wave": 3, "tile": 4, "chunk": 5, "pipe": 6}[path]
+        """'auto', 'generic' (fec_copy_kernel) or 'fast' (the (k, n-k)-specialised LDS-tile kernel,
+        auto's choice when it applies) for the decoder's received-packet kernel."""
+        code = {"auto": 0, "generic": 1, "fast": 2}[path]
         check(lib().fec_codec_set_copy_path(self._h, code), "fec_codec_set_copy_path")
 
     def info(self) -> dict:

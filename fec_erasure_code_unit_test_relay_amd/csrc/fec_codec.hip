@@ -56,33 +56,16 @@ struct fec_codec {
     uint8_t* d_G = nullptr;      // k x n generator (block mode)
     uint8_t* d_rstate = nullptr; // post-resync block states per phase
     int enc_tp = 0;              // encode tile (packets per workgroup), generic kernel
-    int fast_tp = 0;             // encode tile of the specialised kernel (0: not available)
-    const void* fast_kernel = nullptr;
-    const void* persist_kernel = nullptr;  // streaming encode (fec_encode_persist.hip)
-    int persist_tp = 0;
-    int persist_wgs = 0;                   // resident workgroups of it on the device
-    int encode_path = 0;         // 0 auto, 1 generic, 2 specialised, 3 streaming, 4 wave, 5 tile
-    const void* wave_kernel = nullptr;  // wave-private sequence encode (fec_encode_wave.hip)
-    int wave_slots = 0;                 // resident waves of it on the device
-    int wave_ring = 0;                  // bytes of its per-sequence LDS output ring
-    int wave_lds = 0;                   // its dynamic LDS per workgroup
-    int wave_pad = 0;                   // 1: per-sequence ring padding (LDS bank spread)
-    int wave_cus = 0;                   // compute units of the device
+    int encode_path = 0;         // 0 auto, 1 generic, 5 tile (the ids of round 2's paths are kept)
+    int cus = 0;                        // compute units of the device
     const void* tile_kernel = nullptr;  // contiguous-chunk LDS-tile encode (fec_encode_tile.hip)
     int tile_ppw = 0;                   // its packets per wave slice (tile = 4 * tile_ppw packets)
     int tile_lds = 0, tile_lds_len = 0; // its dynamic LDS per workgroup (without / with lengths)
     int tile_per_cu = 0;                // its resident workgroups per CU
     int tile_off[9] = {};               // off_in, in_bytes, off_pw, off_q, off_out, off_len, ngl, nso, off_scratch
-    const void* copy_tile = nullptr;  // persistent decode copy (fec_copy_tile.hip)
-    int copyt_tp = 0, copyt_lds = 0, copyt_per_cu = 0;
     const void* copy_fast = nullptr;  // specialised decode copy kernel (LDS tiles)
     int copyf_tp = 0;
-    const void* copy_wave = nullptr;  // barrier-free decode copy (fec_copy_wave.hip)
-    const void* copy_chunk = nullptr; // one lane per 16-byte output piece (fec_copy_chunk.hip), k | 16
-    int copyc_grid = 0;               // its grid: resident workgroups
-    const void* copy_pipe = nullptr;  // one LDS-DMA pipeline per wave (fec_copy_pipe.hip)
-    int copyp_q = 0, copyp_lds = 0, copyp_slot = 0, copyp_waves = 0;
-    int copy_path = 0;           // 0 auto, 1 generic, 2 specialised (LDS tiles), 3 wave
+    int copy_path = 0;           // 0 auto, 1 generic, 2 specialised (LDS tiles)
     int plan_path = 0;
     int dedup = 1;               // episode-shape deduplication in the planner
     uint64_t* d_stamps = nullptr;  // diagnostics: phase stamps of the next specialised launch
@@ -120,14 +103,6 @@ struct fec_codec {
     int ns4() const { return (g.S + 3) / 4; }
     int copyf_raw(int tp) const { return round16(16 + tp * g.CW + 4 * g.n + 16); }
     int copyf_lds(int tp) const { return copyf_raw(tp) + round16(tp * g.L) + 4 * tp + tp + g.T + 16; }
-    int fast_raw(int tp) const { return round16(std::max((tp + g.n - 1) * g.L + 32, tp * g.CW)); }
-    int fast_xin(int tp) const { return g.k * ns4() * (tp + g.n - 1) * 4; }
-    int fast_lds(int tp) const { return fast_raw(tp) + fast_xin(tp) + 4 * (tp + g.n - 1); }
-    // persistent encode: rows/output union, planes, row lengths, parity planes
-    int pers_raw(int tp) const { return round16(std::max({tp * g.L, tp * g.CW, (g.n - 1) * g.L})); }
-    int pers_lds(int tp) const {
-        return pers_raw(tp) + fast_xin(tp) + 4 * tp + 4 * (g.n - g.k) * ns4() * tp;
-    }
 
     int begin(int kernel, hipStream_t s, hipEvent_t* stop) {
         *stop = nullptr;
@@ -206,72 +181,10 @@ int codec_init(fec_codec* c, int max_payload, int T, int B, int N) {
         const int t = v ? std::atoi(v) : 64;
         return (t >= 8 && t <= 64) ? t : 64;
     };
-    if ((g.L & 3) == 0) c->fast_kernel = fec::fec_encode_fast_kernel_for(g.k, g.n - g.k);
-    if (c->fast_kernel)
-        for (int tp = tile_cap("FEC_ENCODE_TILE"); tp >= 8; tp >>= 1)
-            if (c->fast_lds(tp) <= kLdsBudget) {
-                c->fast_tp = tp;
-                break;
-            }
-    if (!c->fast_tp) c->fast_kernel = nullptr;
-    if ((g.L & 3) == 0) c->persist_kernel = fec::fec_encode_persist_kernel_for(g.k, g.n - g.k);
-    if (c->persist_kernel) {
-        // tile: <= 64 packets, >= n-1 (halo carry), payload rows within the prefetch registers
-        // (6 x 16 bytes per thread), LDS within 80 KB (two workgroups per CU)
-        // (or, for large codewords, the smallest valid tile within 150 KB: one workgroup per CU)
-        for (int budget : {80 * 1024, 150 * 1024}) {
-            for (int tp = tile_cap("FEC_ENCODE_TILE"); tp >= 16 && !c->persist_tp; tp >>= 1)
-                if (c->pers_lds(tp) <= budget && tp * g.L <= 6 * 16 * 320 && tp >= g.n - 1)
-                    c->persist_tp = tp;
-            if (c->persist_tp) break;
-        }
-        int dev = 0, cus = 0, per_cu = 0;
-        if (c->persist_tp) {
-            HIP_TRY(hipGetDevice(&dev));
-            HIP_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
-            HIP_TRY(hipFuncSetAttribute(c->persist_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                        c->pers_lds(c->persist_tp)));
-            HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, c->persist_kernel, 320,
-                                                                 c->pers_lds(c->persist_tp)));
-        }
-        c->persist_wgs = cus * per_cu;
-        if (!c->persist_tp || c->persist_wgs <= 0) c->persist_kernel = nullptr;
-    }
-    if ((g.L & 3) == 0 && (g.S + 3) / 4 <= 64)
-        c->wave_kernel = fec::fec_encode_wave_kernel_for(g.k, g.n - g.k);
-    if (c->wave_kernel) {
-        const int ns4 = c->ns4();
-        c->wave_ring = 64;
-        while (c->wave_ring < 2 * g.CW + 4 * g.n + 80) c->wave_ring <<= 1;
-        c->wave_lds = 4 * (64 / ns4 + 1) * (c->wave_ring + 128);  // rings + 128-byte size rings
-        if (c->wave_lds > 128 * 1024) c->wave_kernel = nullptr;
-    }
-    if (c->wave_kernel) {
-        // per-sequence ring padding (up to 64 dwords) that puts the sequences of a wave on
-        // disjoint LDS banks for the codeword writes; used when it costs no occupancy
-        const int ns4 = c->ns4();
-        const int lds_pad = 4 * (64 / ns4 + 1) * (c->wave_ring + 256 + 128);
-        const bool pad_fits = lds_pad <= 128 * 1024;
-        HIP_TRY(hipFuncSetAttribute(c->wave_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                    pad_fits ? lds_pad : c->wave_lds));
-        int dev = 0, cus = 0, per_cu = 0, per_cu_pad = 0;
-        HIP_TRY(hipGetDevice(&dev));
-        HIP_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
-        HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, c->wave_kernel, 256, c->wave_lds));
-        if (pad_fits)
-            HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu_pad, c->wave_kernel, 256, lds_pad));
-        c->wave_pad = (per_cu_pad >= per_cu && (g.n & 1)) ? 1 : 0;
-        if (const char* v = std::getenv("FEC_WAVE_PAD")) c->wave_pad = std::atoi(v) && per_cu_pad >= per_cu;
-        if (c->wave_pad) c->wave_lds = lds_pad;
-        c->wave_slots = cus * per_cu * 4;
-        c->wave_cus = cus;
-        if (c->wave_slots <= 0) c->wave_kernel = nullptr;
-    }
     {
-        int dev = 0, cus = 0;
+        int dev = 0;
         HIP_TRY(hipGetDevice(&dev));
-        HIP_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
-        if (!c->wave_cus) c->wave_cus = cus;
+        HIP_TRY(hipDeviceGetAttribute(&c->cus, hipDeviceAttributeMultiprocessorCount, dev));
     }
     if ((g.L & 3) == 0 && g.n - g.k >= 0) {
         const fec::TileGeom tg = fec::tile_geometry(g.k, g.n - g.k, g.L);
@@ -298,21 +211,6 @@ int codec_init(fec_codec* c, int max_payload, int T, int B, int N) {
             if (per_cu <= 0) c->tile_kernel = nullptr;
         }
     }
-    if ((g.L & 3) == 0 && g.T + 32 <= 64) {
-        // tile of TP = 32 packets (TP*CW and TP*L multiples of 16 for any CW, L % 4 == 0)
-        const int tp = 32;
-        if (tp * g.CW <= 256 * 16 * 4) c->copy_tile = fec::fec_copy_tile_kernel_for(g.k, g.n - g.k);
-        if (c->copy_tile) {
-            c->copyt_tp = tp;
-            c->copyt_lds = round16(tp * g.CW + 64) + round16(tp * g.L);
-            int dev = 0, cus = 0, per_cu = 0;
-            HIP_TRY(hipGetDevice(&dev));
-            HIP_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
-            HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, c->copy_tile, 256, c->copyt_lds));
-            c->copyt_per_cu = per_cu;
-            if (per_cu <= 0) c->copy_tile = nullptr;
-        }
-    }
     if ((g.L & 3) == 0) c->copy_fast = fec::fec_copy_fast_kernel_for(g.k, g.n - g.k);
     // The copy stages its whole tile, converts, then stores (no overlap inside a workgroup), so
     // smaller tiles with more resident workgroups per CU overlap better: at (10,3,3) 32 packets
@@ -325,45 +223,6 @@ int codec_init(fec_codec* c, int max_payload, int T, int B, int N) {
                 break;
             }
     if (!c->copyf_tp) c->copy_fast = nullptr;
-    if ((g.L & 3) == 0 && (g.S + 3) / 4 <= 64 && g.T < 4 * ((g.S + 3) / 4))
-        c->copy_wave = fec::fec_copy_wave_kernel_for(g.k, g.n - g.k);
-    if ((g.L & 3) == 0) {
-        // tile of Q packets: Q*CW and Q*L multiples of 16, Q + T <= 64 (one flag ballot); a wave's
-        // three codeword slots and output tile in LDS
-        auto pipe_lds = [&](int q) { return 3 * (round16(15 + q * g.CW) + 256) + q * g.L; };
-        int q = 16;
-        if (const char* v = std::getenv("FEC_PIPE_Q")) q = std::atoi(v);
-        while (q >= 4 && ((q * g.CW) % 16 || (q * g.L) % 16 || q % 4 || q + g.T > 64 || pipe_lds(q) > kLdsBudget))
-            q -= 4;
-        if (q >= 4 && (int64_t(g.T) * g.CW >= 16)) {
-            c->copy_pipe = fec::fec_copy_pipe_kernel_for(g.k, g.n - g.k);
-            if (c->copy_pipe) {
-                c->copyp_q = q;
-                c->copyp_slot = round16(15 + q * g.CW);
-                c->copyp_lds = 3 * (c->copyp_slot + 256) + q * g.L;
-                int dev = 0, cus = 0, per_cu = 0;
-                HIP_TRY(hipGetDevice(&dev));
-                HIP_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
-                HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, c->copy_pipe, 64, c->copyp_lds));
-                if (const char* v = std::getenv("FEC_PIPE_WPC")) per_cu = std::max(1, std::min(per_cu, std::atoi(v)));
-                c->copyp_waves = cus * per_cu;
-                if (c->copyp_waves <= 0) c->copy_pipe = nullptr;
-            }
-        }
-    }
-    if ((g.L & 3) == 0 && g.T <= 12) {
-        c->copy_chunk = fec::fec_copy_chunk_kernel_for(g.k, g.n - g.k);
-        if (c->copy_chunk) {
-            int dev = 0, cus = 0, per_cu = 0;
-            HIP_TRY(hipGetDevice(&dev));
-            HIP_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
-            HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, c->copy_chunk, 256, 0));
-            int wpc = per_cu;
-            if (const char* v = std::getenv("FEC_CHUNK_WGPC")) wpc = std::max(1, std::min(per_cu, std::atoi(v)));
-            c->copyc_grid = cus * wpc;
-            if (c->copyc_grid <= 0) c->copy_chunk = nullptr;
-        }
-    }
     // experiments (FEC_SIDE_CUS / FEC_SIDE_PRIO): the planner's side stream on a CU subset, or at
     // the lowest / highest stream priority
     const char* side_cus = std::getenv("FEC_SIDE_CUS");
@@ -440,154 +299,6 @@ Ws ws_carve(const Geometry& g, int64_t P, void* d_ws) {
 }
 
 
-int launch_encode_fast(fec_codec* c, const uint8_t* d_payload, const int32_t* d_len, int64_t history,
-                       int64_t P, uint8_t* d_cw, int32_t* d_cwlen, hipStream_t s) {
-    const Geometry& g = c->g;
-    fec::EncFastArgs a;
-    a.payload = d_payload;
-    a.len = d_len;
-    a.history = std::max<int64_t>(0, history);
-    a.P = P;
-    a.cw = d_cw;
-    a.cw_len = d_cwlen;
-    a.ptab = c->d_ptab;
-    a.L = g.L;
-    a.S = g.S;
-    a.CW = g.CW;
-    a.NS4 = c->ns4();
-    a.TP = c->fast_tp;
-    a.ROWS = a.TP + g.n - 1;
-    a.raw_bytes = c->fast_raw(a.TP);
-    a.xin_bytes = c->fast_xin(a.TP);
-    a.stamps = (c->stamp_kernel == FEC_KERNEL_ENCODE) ? c->d_stamps : nullptr;
-    const int64_t blocks = (P + a.TP - 1) / a.TP;
-    if (blocks > 0x7fffffff) return FEC_ERR_ARG;
-    hipEvent_t stop;
-    if (int st = c->begin(FEC_KERNEL_ENCODE, s, &stop)) return st;
-    void* args[] = {&a};
-    HIP_TRY(hipLaunchKernel(c->fast_kernel, dim3(static_cast<unsigned>(blocks)), dim3(256), args,
-                            c->fast_lds(a.TP), s));
-    return c->end(stop, s);
-}
-
-int launch_encode_persist(fec_codec* c, const uint8_t* d_payload, const int32_t* d_len, int64_t history,
-                          int64_t P, uint8_t* d_cw, int32_t* d_cwlen, hipStream_t s) {
-    const Geometry& g = c->g;
-    fec::EncFastArgs a;
-    a.payload = d_payload;
-    a.len = d_len;
-    a.history = std::max<int64_t>(0, history);
-    a.P = P;
-    a.cw = d_cw;
-    a.cw_len = d_cwlen;
-    a.ptab = c->d_ptab;
-    a.L = g.L;
-    a.S = g.S;
-    a.CW = g.CW;
-    a.NS4 = c->ns4();
-    a.TP = c->persist_tp;
-    a.ROWS = a.TP + g.n - 1;
-    a.raw_bytes = c->pers_raw(a.TP);
-    a.xin_bytes = c->fast_xin(a.TP);
-    a.stamps = (c->stamp_kernel == FEC_KERNEL_ENCODE) ? c->d_stamps : nullptr;
-    const int64_t ntiles = (P + a.TP - 1) / a.TP;
-    a.tiles_per_wg = (ntiles + c->persist_wgs - 1) / c->persist_wgs;
-    const int64_t blocks = (ntiles + a.tiles_per_wg - 1) / a.tiles_per_wg;
-    hipEvent_t stop;
-    if (int st = c->begin(FEC_KERNEL_ENCODE, s, &stop)) return st;
-    void* args[] = {&a};
-    HIP_TRY(hipLaunchKernel(c->persist_kernel, dim3(static_cast<unsigned>(blocks)), dim3(320), args,
-                            c->pers_lds(a.TP), s));
-    return c->end(stop, s);
-}
-
-int launch_encode_wave(fec_codec* c, const uint8_t* d_payload, const int32_t* d_len, int64_t history,
-                       int64_t P, uint8_t* d_cw, int32_t* d_cwlen, hipStream_t s) {
-    const Geometry& g = c->g;
-    // parity of a packet reads only the n-1 packets in front of it, so more history is never read
-    history = std::min<int64_t>(std::max<int64_t>(0, history), g.n - 1);
-    // the kernel addresses rows [-history, P) with 32-bit buffer offsets: batches beyond 2 GB of
-    // payload go in chunks (each sees the n-1 rows in front of it as history; history <= n-1
-    // makes every chunk strictly smaller than the call that made it)
-    const int64_t max_rows = (int64_t(0x7fffffff) - 4096) / std::max(g.L, g.CW) - g.n;
-    if (history + P > max_rows) {
-        const int64_t chunk = max_rows - g.n;
-        for (int64_t r = 0; r < P; r += chunk) {
-            const int64_t h = std::min<int64_t>(history + r, g.n - 1);
-            if (int st = launch_encode_wave(c, d_payload + r * g.L, d_len ? d_len + r : nullptr, h,
-                                            std::min(chunk, P - r), d_cw + r * g.CW, d_cwlen + r, s))
-                return st;
-        }
-        return FEC_OK;
-    }
-    fec::EncWaveArgs a;
-    a.payload_base = d_payload - history * g.L;
-    a.len_base = d_len ? d_len - history : nullptr;
-    a.payload_bytes = static_cast<int>((history + P) * g.L);
-    a.len_bytes = static_cast<int>((history + P) * 4);
-    a.history = static_cast<int>(history);
-    a.P = static_cast<int>(P);
-    a.cw = d_cw;
-    a.cw_bytes = static_cast<int>(P * g.CW);
-    a.cw_len = d_cwlen;
-    a.ptab = c->d_ptab;
-    a.L = g.L;
-    a.S = g.S;
-    a.CW = g.CW;
-    a.NS4 = c->ns4();
-    a.SPW = 64 / a.NS4;
-    a.rem = g.S - 4 * (a.NS4 - 1);
-    // Sequence length M (M*CW % 4 == 0 so that every sequence starts dword aligned).  All
-    // workgroups are resident at once, so the kernel takes as long as its busiest CU: pick the
-    // workgroups per CU w (1..resident) that minimises (M_w + n-1) * load / f(load), load = the
-    // most workgroups any CU gets and f the relative throughput of a CU running that many
-    // (measured on MI355X at (10,3,3): 0.6, 0.9, 1.0, 1.02 for 1..4).  M_w + n-1 is one
-    // sequence's walk (warm-up included).  Landing just above a multiple of the CU count is what
-    // this avoids: at M = 54, 772 workgroups put 4 on four CUs and took 234 us against 195 at M = 56.
-    const int64_t unit = (g.CW & 3) == 0 ? 1 : ((g.CW & 1) == 0 ? 2 : 4);
-    const int cus = std::max(1, c->wave_cus);
-    const int per_cu = std::max(1, c->wave_slots / (4 * cus));
-    auto m_for = [&](int64_t seq_slots) {
-        int64_t m = (P + seq_slots - 1) / seq_slots;
-        return std::max<int64_t>(4, (m + unit - 1) / unit * unit);
-    };
-    auto load_of = [&](int64_t m) {
-        const int64_t wgs = ((P + m - 1) / m + 4 * a.SPW - 1) / (4 * a.SPW);
-        return (wgs + cus - 1) / cus;
-    };
-    static const double f_rel[] = {0.0, 0.6, 0.9, 1.0, 1.02, 1.03, 1.04, 1.05, 1.05};
-    int64_t M = 0;
-    double best = 1e300;
-    for (int w = 1; w <= std::min(per_cu, 8); ++w) {
-        const int64_t m = m_for(static_cast<int64_t>(cus) * w * 4 * a.SPW);
-        const int64_t ld = std::min<int64_t>(load_of(m), 8);
-        const double cost = double(m + g.n - 1) * double(ld) / f_rel[ld];
-        if (cost < best) {
-            best = cost;
-            M = m;
-        }
-    }
-    if (const char* v = std::getenv("FEC_WAVE_SHARE")) {  // experiments: size for a share of the slots
-        const int share = std::atoi(v);
-        if (share > 0) M = m_for(std::max<int64_t>(4, int64_t(c->wave_slots) * share / 100) * a.SPW);
-    }
-    if (const char* v = std::getenv("FEC_WAVE_M")) M = std::max<int64_t>(4, (std::atoll(v) + unit - 1) / unit * unit);
-    a.M = static_cast<int>(M);
-    a.nseq = static_cast<int>((P + M - 1) / M);
-    a.dbg = 0;
-    if (const char* v = std::getenv("FEC_WAVE_DBG")) a.dbg = std::atoi(v);
-    a.ring_bytes = c->wave_ring;
-    a.ring_pad = c->wave_pad;
-    const int64_t waves = (a.nseq + a.SPW - 1) / a.SPW;
-    const int64_t blocks = (waves + 3) / 4;
-    hipEvent_t stop;
-    if (int st = c->begin(FEC_KERNEL_ENCODE, s, &stop)) return st;
-    void* args[] = {&a};
-    HIP_TRY(hipLaunchKernel(c->wave_kernel, dim3(static_cast<unsigned>(blocks)), dim3(256), args,
-                            c->wave_lds, s));
-    return c->end(stop, s);
-}
-
 int launch_encode_tile(fec_codec* c, const uint8_t* d_payload, const int32_t* d_len, int64_t history,
                        int64_t P, uint8_t* d_cw, int32_t* d_cwlen, hipStream_t s) {
     const Geometry& g = c->g;
@@ -625,9 +336,9 @@ int launch_encode_tile(fec_codec* c, const uint8_t* d_payload, const int32_t* d_
     a.nvl = g.L / 4 - g.k * (a.NS4 - 1);
     const int64_t ntiles = (P + R - 1) / R;
     // one wave of resident workgroups, each a contiguous run of tiles (plus the tile in front)
-    int64_t slots = static_cast<int64_t>(std::max(1, c->wave_cus)) * c->tile_per_cu;
+    int64_t slots = static_cast<int64_t>(std::max(1, c->cus)) * c->tile_per_cu;
     if (const char* v = std::getenv("FEC_TILE_WPC"))
-        slots = static_cast<int64_t>(std::max(1, c->wave_cus)) * std::max(1, std::min(c->tile_per_cu, std::atoi(v)));
+        slots = static_cast<int64_t>(std::max(1, c->cus)) * std::max(1, std::min(c->tile_per_cu, std::atoi(v)));
     const int64_t tpw = (ntiles + slots - 1) / slots;
     a.tiles_per_wg = static_cast<int>(tpw);
     a.ntiles = static_cast<int>(ntiles);
@@ -663,20 +374,8 @@ int launch_encode(fec_codec* c, const uint8_t* d_payload, const int32_t* d_len, 
         if (tile_ok && (c->encode_path == 0 || c->encode_path == 5))
             return launch_encode_tile(c, d_payload, d_len, history, P, d_cw, d_cwlen, s);
     }
+    if (c->encode_path != 0 && c->encode_path != 1) return FEC_ERR_ARG;
     const Geometry& g = c->g;
-    const bool wave_ok = c->wave_kernel && (reinterpret_cast<uintptr_t>(d_payload) & 3) == 0 &&
-                         (reinterpret_cast<uintptr_t>(d_cw) & 3) == 0;
-    if (c->encode_path == 4 && !wave_ok) return FEC_ERR_ARG;
-    if (wave_ok && (c->encode_path == 0 || c->encode_path == 4))
-        return launch_encode_wave(c, d_payload, d_len, history, P, d_cw, d_cwlen, s);
-    const bool pers_ok = c->persist_kernel && (reinterpret_cast<uintptr_t>(d_payload) & 15) == 0;
-    if (c->encode_path == 3 && !pers_ok) return FEC_ERR_ARG;
-    if (pers_ok && (c->encode_path == 0 || c->encode_path == 3))
-        return launch_encode_persist(c, d_payload, d_len, history, P, d_cw, d_cwlen, s);
-    const bool fast_ok = c->fast_kernel && (reinterpret_cast<uintptr_t>(d_payload) & 3) == 0;
-    if (c->encode_path == 2 && !fast_ok) return FEC_ERR_ARG;
-    if (fast_ok && c->encode_path != 1)
-        return launch_encode_fast(c, d_payload, d_len, history, P, d_cw, d_cwlen, s);
     fec::EncArgs a;
     a.payload = d_payload;
     a.len = d_len;
@@ -791,168 +490,12 @@ int launch_plan(fec_codec* c, const uint8_t* d_er, int64_t P, void* d_ws, size_t
     return c->end(stop, s);
 }
 
-// The barrier-free copy applies (it leaves erased packets' rows to fec_recover_kernel, which may
-// then run concurrently with it).
-bool copy_wave_ok(const fec_codec* c, const uint8_t* d_out, int64_t P) {
-    const Geometry& g = c->g;
-    return c->copy_wave && c->copy_path == 3 &&
-           (reinterpret_cast<uintptr_t>(d_out) & 3) == 0 && P * g.CW < (int64_t(1) << 31) - 64 &&
-           g.T < 4 * c->ns4();
-}
-
-// The copy kernel in use writes received packets' rows only (erased ones are left to the
-// recovery, which can then run concurrently with it).  Measured at (10,3,3), 1M packets
-// (profiles/r02/r02e_*): letting the LDS-tile copy skip erased rows and running the recovery beside
-// it made the step slower (0.450 vs 0.416 ms; copy 181 vs 157 us, recovery 89 vs 20 us), so only
-// the wave copy (copy path 3) does it.
-bool copy_skips_erased(const fec_codec* c, const uint8_t* d_out, int64_t P) {
-    return copy_wave_ok(c, d_out, P);
-}
-
 int launch_copy(fec_codec* c, const uint8_t* d_cw, const uint8_t* d_er, int64_t P, uint8_t* d_out,
                 int32_t* d_outlen, hipStream_t s) {
     const Geometry& g = c->g;
     const int64_t Pout = P - g.T;
     if (Pout <= 0) return FEC_OK;
-    if (c->copy_path == 3 && !copy_wave_ok(c, d_out, P)) return FEC_ERR_ARG;
-    if (copy_wave_ok(c, d_out, P)) {
-        fec::CopyWaveArgs wa;
-        wa.cw = d_cw;
-        wa.er = d_er;
-        wa.out = d_out;
-        wa.out_len = d_outlen;
-        wa.P = P;
-        wa.Pout = Pout;
-        wa.cw_bytes = static_cast<int>(P * g.CW);
-        wa.out_bytes = static_cast<int>(std::min<int64_t>(Pout * g.L, 0x7fffffff));
-        wa.er_bytes = static_cast<int>(P);
-        wa.L = g.L;
-        wa.CW = g.CW;
-        wa.T = g.T;
-        wa.NS4 = c->ns4();
-        wa.SPW = 64 / wa.NS4;
-        wa.nsteps = (Pout + wa.SPW - 1) / wa.SPW;
-        // 16 waves per CU (half the resident capacity: the planner chain and the recovery run
-        // beside it on the side stream), each a contiguous run of steps
-        int wpc = 16;
-        if (const char* v = std::getenv("FEC_COPY_WPC")) wpc = std::max(1, std::atoi(v));
-        const int64_t waves_max = static_cast<int64_t>(std::max(1, c->wave_cus)) * wpc;
-        wa.steps_per_wave = std::max<int64_t>(1, (wa.nsteps + waves_max - 1) / waves_max);
-        if (const char* v = std::getenv("FEC_COPY_STEPS")) wa.steps_per_wave = std::max(1, std::atoi(v));
-        const int64_t waves = (wa.nsteps + wa.steps_per_wave - 1) / wa.steps_per_wave;
-        const int64_t blocks = (waves + 3) / 4;
-        hipEvent_t stop;
-        if (int st = c->begin(FEC_KERNEL_DEC_COPY, s, &stop)) return st;
-        void* args[] = {&wa};
-        HIP_TRY(hipLaunchKernel(c->copy_wave, dim3(static_cast<unsigned>(blocks)), dim3(256), args, 0, s));
-        return c->end(stop, s);
-    }
-    // one lane per 16-byte output piece: every offset fits 31 bits, with two grid strides to spare
-    const int64_t nchunks = Pout * ((g.L + 15) / 16);
-    const bool chunk_ok = c->copy_chunk && (reinterpret_cast<uintptr_t>(d_out) & 3) == 0 &&
-                          P * g.CW < (int64_t(1) << 31) - 64 &&
-                          nchunks + 2 * int64_t(c->copyc_grid) * 256 < (int64_t(1) << 31);
-    // one LDS-DMA pipeline per wave: 16-byte aligned output, every offset within 31 bits
-    const bool pipe_ok = c->copy_pipe && (reinterpret_cast<uintptr_t>(d_out) & 15) == 0 &&
-                         P * g.CW + c->copyp_slot + 2048 < (int64_t(1) << 31) &&
-                         Pout * g.L < (int64_t(1) << 31) - 64 && P + 4 * 64 + 64 < (int64_t(1) << 31);
-    if (c->copy_path == 6 && !pipe_ok) return FEC_ERR_ARG;
-    if (pipe_ok && c->copy_path == 6) {
-        fec::CopyPipeArgs pa;
-        const uintptr_t cwp = reinterpret_cast<uintptr_t>(d_cw), erp = reinterpret_cast<uintptr_t>(d_er);
-        pa.cw_base = reinterpret_cast<const uint8_t*>(cwp & ~uintptr_t(15));
-        pa.er_base = reinterpret_cast<const uint8_t*>(erp & ~uintptr_t(3));
-        pa.delta = static_cast<int>(cwp & 15);
-        pa.edelta = static_cast<int>(erp & 3);
-        pa.cw_records = static_cast<int>(pa.delta + P * g.CW);
-        pa.er_records = static_cast<int>(pa.edelta + P);
-        pa.out = d_out;
-        pa.out_len = d_outlen;
-        pa.out_records = static_cast<int>(Pout * g.L);
-        pa.len_records = static_cast<int>(4 * Pout);
-        pa.L = g.L;
-        pa.CW = g.CW;
-        pa.T = g.T;
-        pa.NS4 = c->ns4();
-        pa.Q = c->copyp_q;
-        pa.ns4magic = static_cast<uint32_t>((uint64_t(1) << 32) / uint64_t(pa.NS4) + 1);
-        pa.slot_bytes = c->copyp_slot;
-        pa.nd = (pa.slot_bytes + 1023) / 1024;
-        pa.npass = (pa.Q * pa.NS4 + 63) / 64;
-        pa.ns = (pa.Q * g.L / 16 + 63) / 64;
-        pa.Pout = Pout;
-        pa.nsteps = (Pout + pa.Q - 1) / pa.Q;
-        const int64_t waves = std::max<int64_t>(1, std::min<int64_t>(pa.nsteps, c->copyp_waves));
-        pa.steps_per_wave = (pa.nsteps + waves - 1) / waves;
-        pa.nt = 1;
-        if (const char* v = std::getenv("FEC_COPY_NT")) pa.nt = std::atoi(v) ? 1 : 0;
-        const int64_t blocks = (pa.nsteps + pa.steps_per_wave - 1) / pa.steps_per_wave;
-        hipEvent_t stop;
-        if (int st = c->begin(FEC_KERNEL_DEC_COPY, s, &stop)) return st;
-        void* args[] = {&pa};
-        HIP_TRY(hipLaunchKernel(c->copy_pipe, dim3(static_cast<unsigned>(blocks)), dim3(64), args, c->copyp_lds, s));
-        return c->end(stop, s);
-    }
-    if (c->copy_path == 5 && !chunk_ok) return FEC_ERR_ARG;
-    if (chunk_ok && c->copy_path == 5) {
-        fec::CopyChunkArgs ka;
-        ka.cw = d_cw;
-        ka.er = d_er;
-        ka.out = d_out;
-        ka.out_len = d_outlen;
-        ka.cw_bytes = static_cast<int>(P * g.CW);
-        ka.er_bytes = static_cast<int>(P);
-        ka.out_bytes = static_cast<int>(Pout * g.L);
-        ka.L = g.L;
-        ka.CW = g.CW;
-        ka.T = g.T;
-        ka.C = (g.L + 15) / 16;
-        ka.cmagic = static_cast<uint32_t>((uint64_t(1) << 32) / uint64_t(ka.C) + 1);
-        ka.nchunks = static_cast<int>(nchunks);
-        ka.nt = 1;
-        if (const char* v = std::getenv("FEC_COPY_NT")) ka.nt = std::atoi(v) ? 1 : 0;
-        ka.dbg = 0;
-        if (const char* v = std::getenv("FEC_CHUNK_DBG")) ka.dbg = std::atoi(v);
-        const int64_t need = (nchunks + 511) / 512;  // two chunks per lane
-        const unsigned blocks = static_cast<unsigned>(std::max<int64_t>(1, std::min<int64_t>(need, c->copyc_grid)));
-        hipEvent_t stop;
-        if (int st = c->begin(FEC_KERNEL_DEC_COPY, s, &stop)) return st;
-        void* args[] = {&ka};
-        HIP_TRY(hipLaunchKernel(c->copy_chunk, dim3(blocks), dim3(256), args, 0, s));
-        return c->end(stop, s);
-    }
-    const bool tile_ok = c->copy_tile && (reinterpret_cast<uintptr_t>(d_out) & 15) == 0 &&
-                         (reinterpret_cast<uintptr_t>(d_cw) & 15) == 0;
-    if (c->copy_path == 4 && !tile_ok) return FEC_ERR_ARG;
-    // Copy path 4 only: the persistent copy holds every CU's slots until it ends, so the planner
-    // chain on the side stream starts only after it (scan 81 vs 23 us) and the step gets slower
-    // (0.373 - 0.393 vs 0.353 ms per step, tools/step_ab.py, same process), although the copy
-    // alone is faster (166 vs 174 us in the step)
-    if (tile_ok && c->copy_path == 4) {
-        fec::CopyTileArgs ta;
-        ta.cw = d_cw;
-        ta.er = d_er;
-        ta.out = d_out;
-        ta.out_len = d_outlen;
-        ta.Pout = Pout;
-        ta.L = g.L;
-        ta.CW = g.CW;
-        ta.NS4 = c->ns4();
-        ta.T = g.T;
-        ta.TP = c->copyt_tp;
-        ta.raw_bytes = round16(ta.TP * g.CW + 64);
-        ta.ntiles = (Pout + ta.TP - 1) / ta.TP;
-        int wpc = c->copyt_per_cu;
-        if (const char* v = std::getenv("FEC_COPY_TILE_WPC")) wpc = std::max(1, std::min(wpc, std::atoi(v)));
-        const int64_t slots = static_cast<int64_t>(std::max(1, c->wave_cus)) * std::max(1, wpc);
-        ta.tiles_per_wg = (ta.ntiles + slots - 1) / slots;
-        const int64_t blocks = (ta.ntiles + ta.tiles_per_wg - 1) / ta.tiles_per_wg;
-        hipEvent_t stop;
-        if (int st = c->begin(FEC_KERNEL_DEC_COPY, s, &stop)) return st;
-        void* args[] = {&ta};
-        HIP_TRY(hipLaunchKernel(c->copy_tile, dim3(static_cast<unsigned>(blocks)), dim3(256), args, c->copyt_lds, s));
-        return c->end(stop, s);
-    }
+    if (c->copy_path != 0 && c->copy_path != 1 && c->copy_path != 2) return FEC_ERR_ARG;
     const bool fast_ok = c->copy_fast && (reinterpret_cast<uintptr_t>(d_out) & 3) == 0;
     if (c->copy_path == 2 && !fast_ok) return FEC_ERR_ARG;
     if (fast_ok && c->copy_path != 1) {
@@ -972,12 +515,10 @@ int launch_copy(fec_codec* c, const uint8_t* d_cw, const uint8_t* d_er, int64_t 
         fa.out_bytes = round16(fa.TP * g.L);
         fa.stamps = (c->stamp_kernel == FEC_KERNEL_DEC_COPY) ? c->d_stamps : nullptr;
         fa.skip_erased = 0;
-        if (const char* v = std::getenv("FEC_COPY_SKIP")) fa.skip_erased = std::atoi(v) ? 1 : 0;  // experiment
         // non-temporal codeword loads and payload stores: 0.318 vs 0.338 ms per bench step
         // (tools/step_ab.py, same process, profiles/r02/decode_diag/copy_nt_ab.txt)
         fa.nt = 1;
         if (const char* v = std::getenv("FEC_COPY_NT")) fa.nt = std::atoi(v) ? 1 : 0;
-        if (const char* v = std::getenv("FEC_COPY_REV")) fa.nt |= std::atoi(v) ? 2 : 0;  // experiment: tiles in reverse order
         const int64_t blocks = (Pout + fa.TP - 1) / fa.TP;
         hipEvent_t stop;
         if (int st = c->begin(FEC_KERNEL_DEC_COPY, s, &stop)) return st;
@@ -1024,10 +565,9 @@ int launch_compact(fec_codec* c, int64_t P, uint8_t* d_out, int32_t* d_outlen, v
     ca.sym_ok = w.sym_ok;
     ca.k = g.k;
     ca.rec_list = w.rec_list;
-    // when the copy kernel leaves erased rows alone (wave copy), the lost ones get their zero row
-    // and length 0 here
-    ca.zero_lost = copy_skips_erased(c, d_out, P) ? 1 : 0;
-    if (const char* v = std::getenv("FEC_COPY_SKIP")) ca.zero_lost = std::atoi(v) ? 1 : ca.zero_lost;  // experiment
+    // the copy writes every row (zero rows and length 0 for erased packets); recovered rows are
+    // overwritten by the recovery, which runs after it
+    ca.zero_lost = 0;
     ca.out = d_out;
     ca.out_len = d_outlen;
     ca.L = g.L;
@@ -1097,16 +637,13 @@ int launch_decode(fec_codec* c, const uint8_t* d_cw, const uint8_t* d_er, int64_
     HIP_TRY(hipStreamWaitEvent(c->side, c->ev_fork, 0));
     if (int st = launch_plan(c, d_er, P, d_ws, ws_bytes, c->side)) return st;
     if (int st = launch_compact(c, P, d_out, d_outlen, d_ws, ws_bytes, c->side)) return st;
-    // The barrier-free copy writes received rows only: the recovery (erased rows) then runs on
-    // the side stream right after the plan, concurrently with the copy.
-    bool concurrent = copy_skips_erased(c, d_out, P);
-    if (const char* v = std::getenv("FEC_RECOVER_SERIAL")) concurrent = concurrent && !std::atoi(v);
-    if (concurrent)
-        if (int st = launch_recover(c, d_cw, P, d_out, d_outlen, d_ws, ws_bytes, c->side, 0, true)) return st;
     HIP_TRY(hipEventRecord(c->ev_join, c->side));
+    // The copy writes every row (erased ones as zero rows, length 0); the recovery overwrites the
+    // recovered ones after the join.  Round 2 and 3 measured the alternatives slower in the step
+    // (a copy that leaves erased rows to a recovery running beside it; the plan beside the
+    // encoder; profiles/r02/decode_diag, tools/step_overlap2.py).
     if (int st = launch_copy(c, d_cw, d_er, P, d_out, d_outlen, s)) return st;
     HIP_TRY(hipStreamWaitEvent(s, c->ev_join, 0));
-    if (concurrent) return FEC_OK;
     return launch_recover(c, d_cw, P, d_out, d_outlen, d_ws, ws_bytes, s, 0, true);
 }
 
@@ -1150,15 +687,6 @@ int launch_decode_stream(fec_codec* c, fec_decode_stream* st, const uint8_t* d_c
     if (int st2 = check_ws(c, Pp, d_ws, ws_bytes)) return st2;
     const uint8_t* cw_c = d_cw - (s0 - cut) * c->g.CW;
     const uint8_t* er_c = d_er - (s0 - cut);
-    // The copy below writes every row it covers, erased ones included, and the recovery runs
-    // after it: the wave copy (path 3, which leaves erased rows to a concurrent recovery) is
-    // switched off for the whole push, so the compaction does not zero lost rows beside the copy.
-    struct CopyPathOverride {
-        fec_codec* c;
-        int saved;
-        ~CopyPathOverride() { c->copy_path = saved; }
-    } keep{c, c->copy_path};
-    if (c->copy_path == 3) c->copy_path = 0;
     HIP_TRY(hipEventRecord(c->ev_fork, s));
     HIP_TRY(hipStreamWaitEvent(c->side, c->ev_fork, 0));
     if (int e = launch_plan(c, er_c, Pp, d_ws, ws_bytes, c->side)) return e;
@@ -1432,36 +960,19 @@ int fec_codec_info(const fec_codec* c, char* buf, size_t size) {
     if (c->tile_kernel && (c->encode_path == 0 || c->encode_path == 5))
         std::snprintf(enc, sizeof(enc), "fec_encode_tile_kernel<%d, %d, %d>", c->g.k, np,
                       c->tile_kernel == fec::fec_encode_tile_kernel_for(c->g.k, np, 0) ? 0 : c->g.L);
-    else if (c->wave_kernel && (c->encode_path == 0 || c->encode_path == 4))
-        std::snprintf(enc, sizeof(enc), "fec_encode_wave_kernel<%d, %d>", c->g.k, np);
-    else if (c->persist_kernel && (c->encode_path == 0 || c->encode_path == 3))
-        std::snprintf(enc, sizeof(enc), "fec_encode_persist_kernel<%d, %d>", c->g.k, np);
-    else if (c->fast_kernel && c->encode_path != 1)
-        std::snprintf(enc, sizeof(enc), "fec_encode_fast_kernel<%d, %d>", c->g.k, np);
     else
         std::snprintf(enc, sizeof(enc), "fec_encode_kernel");
     char cpy[64];
-    if (c->copy_pipe && c->copy_path == 6)
-        std::snprintf(cpy, sizeof(cpy), "fec_copy_pipe_kernel<%d, %d>", c->g.k, np);
-    else if (c->copy_chunk && c->copy_path == 5)
-        std::snprintf(cpy, sizeof(cpy), "fec_copy_chunk_kernel<%d, %d>", c->g.k, np);
-    else if (c->copy_wave && c->copy_path == 3)
-        std::snprintf(cpy, sizeof(cpy), "fec_copy_wave_kernel<%d, %d>", c->g.k, np);
-    else if (c->copy_tile && c->copy_path == 4)
-        std::snprintf(cpy, sizeof(cpy), "fec_copy_tile_kernel<%d, %d>", c->g.k, np);
-    else if (c->copy_fast && c->copy_path != 1)
+    if (c->copy_fast && c->copy_path != 1)
         std::snprintf(cpy, sizeof(cpy), "fec_copy_fast_kernel<%d, %d>", c->g.k, np);
     else
         std::snprintf(cpy, sizeof(cpy), "fec_copy_kernel");
     std::snprintf(buf, size,
                   "{\"k\": %d, \"n\": %d, \"S\": %d, \"CW\": %d, \"encode_kernel\": \"%s\", "
-                  "\"copy_kernel\": \"%s\", \"encode_tile\": %d, "
-                  "\"encode_stream_tile\": %d, \"encode_stream_workgroups\": %d, "
-                  "\"encode_stream_lds\": %d, \"copy_tile\": %d, \"plan_specialised\": %d, "
-                  "\"wave_ring_pad\": %d}",
-                  c->g.k, c->g.n, c->g.S, c->g.CW, enc, cpy, c->fast_tp, c->persist_tp, c->persist_wgs,
-                  c->persist_tp ? c->pers_lds(c->persist_tp) : 0, c->copyf_tp, c->plan_fast ? 1 : 0,
-                  c->wave_pad);
+                  "\"copy_kernel\": \"%s\", \"encode_tile_packets\": %d, \"encode_tile_workgroups_per_cu\": %d, "
+                  "\"copy_tile\": %d, \"plan_specialised\": %d}",
+                  c->g.k, c->g.n, c->g.S, c->g.CW, enc, cpy, 4 * c->tile_ppw, c->tile_per_cu, c->copyf_tp,
+                  c->plan_fast ? 1 : 0);
     return FEC_OK;
 }
 
@@ -1496,23 +1007,15 @@ int fec_codec_set_plan_path(fec_codec* c, int path) {
 }
 
 int fec_codec_set_copy_path(fec_codec* c, int path) {
-    if (!c || path < 0 || path > 6) return FEC_ERR_ARG;
-    if (path == 6 && !c->copy_pipe) return FEC_ERR_ARG;
-    if (path == 5 && !c->copy_chunk) return FEC_ERR_ARG;
-    if (path == 4 && !c->copy_tile) return FEC_ERR_ARG;
+    if (!c || path < 0 || path > 2) return FEC_ERR_ARG;
     if (path == 2 && !c->copy_fast) return FEC_ERR_ARG;
-    if (path == 3 && !c->copy_wave) return FEC_ERR_ARG;
     c->copy_path = path;
     return FEC_OK;
 }
 
 int fec_codec_set_encode_path(fec_codec* c, int path) {
-    if (!c || path < 0 || path > 6) return FEC_ERR_ARG;
-    if (path == 6 && !c->copy_pipe) return FEC_ERR_ARG;
+    if (!c || !(path == 0 || path == 1 || path == 5)) return FEC_ERR_ARG;
     if (path == 5 && !c->tile_kernel) return FEC_ERR_ARG;
-    if (path == 2 && !c->fast_kernel) return FEC_ERR_ARG;
-    if (path == 3 && !c->persist_kernel) return FEC_ERR_ARG;
-    if (path == 4 && !c->wave_kernel) return FEC_ERR_ARG;
     c->encode_path = path;
     return FEC_OK;
 }

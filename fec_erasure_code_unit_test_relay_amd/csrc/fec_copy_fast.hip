@@ -24,13 +24,12 @@ __global__ __launch_bounds__(256) void fec_copy_fast_kernel(CopyFastArgs a) {
     const int tid = threadIdx.x;
     phase_stamp(a.stamps, blockIdx.x, 0);
     const int L = a.L, CW = a.CW, NS4 = a.NS4, T = a.T;
-    const int64_t blk = (a.nt & 2) ? static_cast<int64_t>(gridDim.x) - 1 - blockIdx.x : blockIdx.x;
-    const int64_t x0 = blk * a.TP;
+    const int64_t x0 = static_cast<int64_t>(blockIdx.x) * a.TP;
     const int ntile = static_cast<int>(min<int64_t>(a.TP, a.Pout - x0));
 
     const uint8_t* gA = a.cw + x0 * CW;
     const int delta = static_cast<int>(reinterpret_cast<uintptr_t>(gA) & 15);
-    if (a.nt & 1)
+    if (a.nt)
         stage_to_lds<8, true>(raw, gA - delta, delta, delta + ntile * CW, tid, 256);
     else
         stage_to_lds<8>(raw, gA - delta, delta, delta + ntile * CW, tid, 256);
@@ -113,7 +112,7 @@ __global__ __launch_bounds__(256) void fec_copy_fast_kernel(CopyFastArgs a) {
         for (int o = tid * 16; o < obytes; o += 256 * 16) {
             if (!skip || (!erw[o / L] && !erw[(o + 15) / L])) {
                 const uint4 v = *reinterpret_cast<const uint4*>(xo + o);
-                if (a.nt & 1)
+                if (a.nt)
                     nt_store16(dst + o, v);
                 else
                     *reinterpret_cast<uint4*>(dst + o) = v;

@@ -42,49 +42,6 @@ struct EncArgs {
     int xin_bytes, xout_bytes;  // 16-aligned LDS carve sizes
 };
 
-struct EncFastArgs {
-    const uint8_t* payload;     // row 0 = first packet of the batch (4-byte aligned, L % 4 == 0)
-    const int32_t* len;         // may be null (all L)
-    int64_t history;
-    int64_t P;
-    uint8_t* cw;
-    int32_t* cw_len;
-    const uint32_t* ptab;
-    int L, S, CW;
-    int NS4;                    // groups of 4 sub-streams
-    int TP, ROWS;               // packets per tile, TP + n - 1
-    int raw_bytes;              // LDS union of payload rows / output tile (16-aligned)
-    int xin_bytes;              // LDS position planes
-    uint64_t* stamps;           // diagnostics: per-workgroup phase timestamps (null = off)
-    int64_t tiles_per_wg;       // persistent kernel: contiguous tiles per workgroup
-};
-
-// Wave-private sequence encode (fec_encode_wave.hip).  Lane = (sequence, group of 4 sub-streams);
-// SPW = 64 / NS4 sequences per wave, each of M packets (M % 4 == 0).
-struct EncWaveArgs {
-    const uint8_t* payload_base;  // row -history (4-byte aligned, L % 4 == 0)
-    const int32_t* len_base;      // lengths of rows -history.. (null: all L)
-    int payload_bytes;            // (history + P) * L < 2^31 (the launcher splits larger batches)
-    int len_bytes;                // (history + P) * 4
-    int history;                  // valid rows before row 0
-    int P;
-    uint8_t* cw;                  // 4-byte aligned
-    int cw_bytes;                 // P * CW < 2^31
-    int32_t* cw_len;
-    const uint32_t* ptab;
-    int L, S, CW, NS4, SPW, M;
-    int rem;                      // sub-streams in the last group (1..4)
-    int nseq;                     // ceil(P / M)
-    int ring_bytes;               // per-sequence LDS output ring (power of two >= 2*CW + 4n + 80)
-    int ring_pad;                 // 1: rings ring_bytes + 256 apart, sequence j shifted so that the
-                                  //    wave's codeword writes fall on disjoint banks (odd n)
-    int dbg;                      // timing experiments only (FEC_WAVE_DBG): 1 no stores, 2 no parity,
-                                  // 8 16-byte flush boundaries, 16 sizes stored per packet
-};
-
-// fec_encode_wave_kernel<k, n-k> (fec_encode_wave.hip), else nullptr.  256 threads.
-const void* fec_encode_wave_kernel_for(int k, int np);
-
 struct EncTileArgs {
     const uint8_t* payload_base;  // row -history (4-byte aligned, L % 4 == 0)
     const int32_t* len_base;      // lengths of rows -history.. (null: all L)
@@ -164,12 +121,6 @@ constexpr TileGeom tile_geometry(int k, int np, int L) {
 // time) or <k, n-k, 0> (L from the arguments) (fec_encode_tile.hip), else nullptr.  256 threads.
 const void* fec_encode_tile_kernel_for(int k, int np, int L);
 
-// fec_encode_persist_kernel<k, n-k> (fec_encode_persist.hip), else nullptr.  320 threads.
-const void* fec_encode_persist_kernel_for(int k, int np);
-
-// fec_encode_fast_kernel<k, n-k> for the instantiated pairs (fec_encode_fast.hip), else nullptr.
-const void* fec_encode_fast_kernel_for(int k, int np);
-
 struct CopyFastArgs {
     const uint8_t* cw;
     const uint8_t* er;
@@ -183,68 +134,6 @@ struct CopyFastArgs {
     int skip_erased;            // 1: leave erased packets' rows and lengths to fec_recover_kernel
     int nt;                     // 1: non-temporal codeword loads and payload stores
 };
-
-// Received-packet decode over contiguous per-workgroup tile runs (fec_copy_tile.hip).
-struct CopyTileArgs {
-    const uint8_t* cw;          // 16-byte aligned, P rows of CW bytes
-    const uint8_t* er;          // P flags
-    uint8_t* out;               // 16-byte aligned, Pout rows of L bytes (L % 4 == 0)
-    int32_t* out_len;
-    int64_t Pout;
-    int L, CW, NS4, T, TP;      // TP * CW <= 16 KB, TP * L % 16 == 0, TP * CW % 16 == 0, TP + T <= 64
-    int raw_bytes;              // LDS codeword tile (16-aligned)
-    int64_t tiles_per_wg, ntiles;
-};
-const void* fec_copy_tile_kernel_for(int k, int np);
-
-// Barrier-free received-packet decode (fec_copy_wave.hip): lane = (packet, group of 4 sub-streams),
-// SPW = 64 / NS4 packets per wave step; erased packets are not touched.  Needs T < 4*NS4.
-struct CopyWaveArgs {
-    const uint8_t* cw;          // P rows of CW bytes
-    const uint8_t* er;
-    uint8_t* out;               // Pout rows of L bytes (4-byte aligned, L % 4 == 0)
-    int32_t* out_len;
-    int64_t P, Pout;
-    int cw_bytes, out_bytes;    // P*CW, Pout*L (< 2^31: the launcher falls back otherwise)
-    int er_bytes;               // P
-    int L, CW, T, NS4, SPW;
-    int64_t nsteps;             // ceil(Pout / SPW)
-    int64_t steps_per_wave;
-};
-const void* fec_copy_wave_kernel_for(int k, int np);
-
-// Received-packet decode, one lane per 16-byte output piece, no LDS (fec_copy_chunk.hip); k | 16.
-struct CopyChunkArgs {
-    const uint8_t* cw;          // P rows of CW bytes
-    const uint8_t* er;          // P flags
-    uint8_t* out;               // Pout rows of L bytes (4-byte aligned, L % 4 == 0)
-    int32_t* out_len;
-    int cw_bytes, er_bytes, out_bytes;  // P*CW, P, Pout*L (all < 2^31, launcher check)
-    int L, CW, T, C;            // C = ceil(L / 16) chunks per row; T <= 12
-    uint32_t cmagic;            // floor(2^32 / C) + 1: i / C by one __umulhi (+1 correction)
-    int nchunks;                // Pout * C
-    int nt;                     // 1: non-temporal codeword loads and payload stores
-    int dbg;                    // timing experiments only (FEC_CHUNK_DBG): 1 stores rounded down to
-                                // 16 bytes, 2 no stores, 4 no flag/header loads; 0 in the product
-};
-const void* fec_copy_chunk_kernel_for(int k, int np);
-
-// Received-packet decode, one LDS-DMA pipeline per wave (fec_copy_pipe.hip).
-struct CopyPipeArgs {
-    const uint8_t* cw_base;     // codewords rounded down to 16 bytes; row x at cw_base + delta + x*CW
-    const uint8_t* er_base;     // erasure flags rounded down to 4 bytes; flag x at er_base + edelta + x
-    uint8_t* out;               // 16-byte aligned, Pout rows of L bytes (L % 4 == 0)
-    int32_t* out_len;
-    int cw_records, er_records, out_records, len_records;  // bytes addressable through each (< 2^31)
-    int delta, edelta;
-    int L, CW, T, NS4, Q;       // Q packets per tile: Q*CW % 16 == 0, Q*L % 16 == 0, Q % 4 == 0, Q+T <= 64
-    uint32_t ns4magic;          // floor(2^32 / NS4) + 1: item / NS4 by one __umulhi
-    int slot_bytes;             // LDS bytes of a tile's codeword rows (>= delta + Q*CW, multiple of 16)
-    int nd, npass, ns;          // per tile: 1 KB DMA instructions, 64-item passes, 16-byte store rounds
-    int64_t Pout, nsteps, steps_per_wave;
-    int nt;                     // 1: non-temporal codeword loads and payload stores
-};
-const void* fec_copy_pipe_kernel_for(int k, int np);
 
 // fec_copy_fast_kernel<k, n-k> for the instantiated pairs (fec_copy_fast.hip), else nullptr.
 const void* fec_copy_fast_kernel_for(int k, int np);
@@ -389,10 +278,6 @@ __global__ void fec_fill_kernel(uint8_t* out, int64_t t0, int64_t count, int L, 
 struct fec_codec;
 namespace fec {
 int codec_view(const ::fec_codec* c, CodecView* v);
-// The per-packet FEC_Encoder's call (fec_codec.hip): packet `seq` (relative to the encoder's first)
-// of one stream whose window ring `win` ([n-1][S*k], fec_streams.hip's layout) lives on the device,
-// through fec_streams_encode_kernel in one launch.  payload / cw / cw_len may be host-visible
-// (mapped) rows; after them the kernel stores `ticket` into `done`.
 // ---- resident per-packet servers (fec_server.hip) ----------------------------------------
 // Mailbox shared by a per-packet coder (host) and its server workgroup (device), in pinned,
 // coherent, mapped host memory.  The host writes the request fields, then `req`; the server
@@ -438,6 +323,10 @@ struct DecServerArgs {
 int server_encode_launch(const EncServerArgs& a, hipStream_t s);
 int server_decode_launch(const DecServerArgs& a, hipStream_t s);
 
+// The per-packet FEC_Encoder's call (fec_codec.hip): packet `seq` (relative to the encoder's first)
+// of one stream whose window ring `win` ([n-1][S*k], fec_streams.hip's layout) lives on the device,
+// through fec_streams_encode_kernel in one launch.  payload / cw / cw_len may be host-visible
+// (mapped) rows; after them the kernel stores `ticket` into `done`.
 int stream_encode_one(const CodecView& v, uint8_t* win, const uint8_t* payload, int payload_len, int64_t seq,
                       uint8_t* cw, int32_t* cw_len, uint32_t* done, uint32_t ticket, hipStream_t s);
 // The per-packet FEC_Decoder's call: store packet `seq`'s codeword `cw` (a host-visible row padded to

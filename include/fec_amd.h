@@ -54,20 +54,15 @@ int fec_codec_geometry(const fec_codec *codec, int *k, int *n, int *S, int *CW);
 int fec_codec_info(const fec_codec *codec, char *buf, size_t size);
 /* Encode kernel selection: 0 = automatic (the tile kernel -- contiguous runs of LDS-staged packet
  * tiles per workgroup -- when one is compiled for (k, n-k), max_payload % 4 == 0, the payload is
- * 4-byte and the codeword buffer 16-byte aligned and a tile covers the n-1 packets of parity
- * history; else the wave-sequence kernel; else the streaming kernel when the payload is 16-byte
- * aligned; else the per-tile specialised kernel; else the generic one), 1 = generic kernel,
- * 2 = per-tile specialised kernel, 3 = streaming (persistent) specialised kernel, 4 = wave-sequence
- * kernel, 5 = tile kernel (FEC_ERR_ARG if unavailable).  All produce identical bytes; the switch
- * exists for tests and A/B timing. */
+ * 4-byte and the codeword buffer 16-byte aligned; else the generic one), 1 = generic kernel,
+ * 5 = tile kernel (FEC_ERR_ARG if unavailable).  Ids 2-4 (round 2's per-tile, streaming and
+ * wave-sequence kernels, all slower) are retired and return FEC_ERR_ARG.  Every path produces
+ * identical bytes; the switch exists for tests and A/B timing. */
 int fec_codec_set_encode_path(fec_codec *codec, int path);
 /* The same switch for the decoder's received-packet copy kernel: 0 automatic (the LDS-tile
  * specialised kernel when one is compiled for (k, n-k) and max_payload % 4 == 0, else the generic
- * one), 1 generic, 2 LDS-tile specialised, 3 barrier-free wave kernel (it writes received packets'
- * rows only, so fec_decode_batch then runs the recovery of erased packets concurrently with it;
- * measured slower in the step, kept for A/B), 4 persistent tile runs with register-staged prefetch
- * (16-byte aligned buffers; faster alone, slower in the step: it holds the CUs the side-stream
- * planner chain needs). */
+ * one), 1 generic, 2 LDS-tile specialised.  Ids 3-6 (barrier-free wave, persistent tile, chunk and
+ * per-wave LDS-DMA pipeline copies, all measured slower in the step) are retired. */
 int fec_codec_set_copy_path(fec_codec *codec, int path);
 /* The same switch for the decoder's planner (per-episode block replay). */
 int fec_codec_set_plan_path(fec_codec *codec, int path);

@@ -40,7 +40,7 @@ ENC_CONFIGS = [(10, 3, 3), (10, 5, 2), (10, 1, 1), (10, 0, 0), (10, 2, 2), (10, 
                (4, 6, 2), (12, 4, 2), (10, 9, 1), (10, 10, 1)]
 
 
-@pytest.mark.parametrize("path", ["generic", "fast", "auto", "wave", "tile"])
+@pytest.mark.parametrize("path", ["generic", "auto", "tile"])
 @pytest.mark.parametrize("tbn", ENC_CONFIGS)
 def test_encode_bit_exact(tbn, path):
     T, B, N = tbn
@@ -58,18 +58,18 @@ def test_encode_bit_exact(tbn, path):
     assert (c.generator() == oracle.gen_G(T, B, N)).all()
 
 
-def test_encode_fast_path_other_payload_sizes():
-    """The specialised kernel with payload sizes other than 300 (L % 4 == 0) and a tiny batch."""
+def test_encode_other_payload_sizes():
+    """Both encoders with payload sizes other than 300 (L % 4 == 0) and tiny batches."""
     for Lx, tbn, P in [(4, (10, 3, 3), 200), (64, (10, 5, 2), 300), (1500, (10, 3, 3), 130),
                        (300, (10, 3, 3), 1), (300, (10, 1, 1), 7), (1500, (10, 5, 2), 700)]:
         ref = oracle.encode_stream(Lx, *tbn, 0, P, seed=11)
-        for path in ("fast", "stream", "wave", "tile"):
+        for path in ("generic", "tile"):
             c = fec.Codec(Lx, *tbn)
             try:
                 c.set_encode_path(path)
             except fec.FecError:
-                # wave: prefetch width limit; tile: a tile must cover the n-1 packets of history
-                assert (path == "wave" and Lx > 300) or (path == "tile" and Lx > 300)
+                # tile: its LDS tile must hold the rows and the n-1 packets of parity history
+                assert path == "tile" and Lx > 300
                 continue
             payload = fec.fill_payload(0, P, Lx, 11)
             cw, wl = c.encode(payload)
@@ -78,16 +78,16 @@ def test_encode_fast_path_other_payload_sizes():
 
 
 @pytest.mark.parametrize("tbn", [(10, 3, 3), (10, 5, 2), (10, 1, 1), (10, 10, 10), (10, 0, 0)])
-def test_encode_stream_many_tiles_per_workgroup(tbn):
-    """The persistent kernel carries plane rows from tile to tile inside a workgroup: compare it
-    with the per-tile kernel (itself checked against the oracle above) on a batch long enough for
-    tens of tiles per workgroup, with random lengths and a history window."""
+def test_encode_many_tiles_per_workgroup(tbn):
+    """The tile kernel carries parity rows from tile to tile inside a workgroup: compare it with
+    the generic kernel (itself checked against the oracle above) on a batch long enough for tens of
+    tiles per workgroup, with random lengths and a history window."""
     P = 300_000
     rng = np.random.default_rng(17)
     lens = torch.from_numpy(rng.integers(0, L + 1, size=P).astype(np.int32)).cuda()
     payload = fec.fill_payload(0, P, L, 23)
     outs = []
-    for path in ("fast", "stream", "wave", "tile"):
+    for path in ("generic", "tile"):
         c = fec.Codec(L, *tbn)
         try:
             c.set_encode_path(path)
@@ -103,13 +103,12 @@ def test_encode_stream_many_tiles_per_workgroup(tbn):
         assert torch.equal(o[2], o[0][P // 2:])
 
 
-@pytest.mark.parametrize("path", ["wave", "tile"])
+@pytest.mark.parametrize("path", ["tile", "generic"])
 @pytest.mark.parametrize("tbn", [(10, 3, 3), (10, 5, 2), (10, 1, 1), (10, 0, 0), (10, 9, 9)])
-def test_encode_wave_sequences_and_batch_edges(tbn, path):
-    """The wave kernel splits a batch into packet sequences with a warm-up over the packets in
-    front of each, the tile kernel into workgroup runs of tiles with the tile in front: sizes
-    around the sequence / tile length, odd batch ends (the last codeword's final partial dword)
-    and both codeword alignments, against the oracle."""
+def test_encode_batch_edges(tbn, path):
+    """The tile kernel splits a batch into workgroup runs of tiles with the tile in front: sizes
+    around the tile length, odd batch ends (the last codeword's final partial dword) and both
+    codeword alignments, against the oracle."""
     for P in (1, 2, 3, 5, 23, 24, 25, 41, 64, 1001, 4099, 70001):
         ref = oracle.encode_stream(L, *tbn, 0, P, seed=5)
         c = fec.Codec(L, *tbn)
@@ -132,7 +131,7 @@ def test_encode_digest_fixture(oracle_vectors):
         assert hashlib.sha256(wl.cpu().numpy().astype("<i4").tobytes()).hexdigest() == v["wire_len_sha256"]
 
 
-@pytest.mark.parametrize("path", ["generic", "fast", "stream", "wave", "tile"])
+@pytest.mark.parametrize("path", ["generic", "tile"])
 @pytest.mark.parametrize("tbn", [(10, 3, 3), (10, 5, 2), (10, 10, 10), (10, 9, 9), (10, 0, 0)])
 def test_encode_variable_lengths_and_history(tbn, path):
     T, B, N = tbn
@@ -153,8 +152,7 @@ def test_encode_variable_lengths_and_history(tbn, path):
     dl = torch.from_numpy(lens).cuda()
     cw, _ = c.encode(payload, dl)
     assert (cw.cpu().numpy() == ref).all()
-    # the same stream in two batches: the second sees 36 packets of history (the slice start
-    # stays 16-byte aligned, which the streaming kernel requires)
+    # the same stream in two batches: the second sees 36 packets of history
     h, cut = 36, 400
     cw1, _ = c.encode(payload[:cut], dl[:cut])
     cw2, _ = c.encode(payload[cut - h:], dl[cut - h:], history=h)
@@ -163,13 +161,12 @@ def test_encode_variable_lengths_and_history(tbn, path):
 
 def gpu_round_trip(T, B, N, pattern, P, garbage=True, path="auto", dedup=True):
     """GPU encode of packets 0..P+T-1, erase, GPU decode -> outputs for packets 0..P-1.
-    path: kernel selection of the decoder's copy and planner ('auto', 'generic' or 'wave' =
-    the barrier-free copy);
+    path: kernel selection of the decoder's copy and planner ('auto', 'generic' or 'fast');
     dedup: planner replays one episode per loss shape (True) or every episode."""
     c = fec.Codec(L, T, B, N)
     try:
         c.set_copy_path(path)
-        c.set_plan_path("auto" if path in ("wave", "tile", "chunk", "pipe") else path)
+        c.set_plan_path(path if path in ("generic", "auto") else "auto")
     except fec.FecError:
         pytest.skip(f"no {path} kernel for {(T, B, N)}")
     c.set_episode_dedup(dedup)
@@ -201,8 +198,7 @@ DEC_CASES = [((10, 5, 2), "bin_erasure", 0, 8000), ((10, 3, 3), "bin_erasure", 0
              ((10, 8, 1), "erasure90", 2000, 5000), ((10, 9, 2), "erasure100", 7000, 5000)]
 
 
-@pytest.mark.parametrize("path,dedup", [("generic", False), ("wave", True), ("tile", True), ("chunk", True),
-                                        ("pipe", True), ("auto", False), ("auto", True)])
+@pytest.mark.parametrize("path,dedup", [("generic", False), ("fast", True), ("auto", False), ("auto", True)])
 @pytest.mark.parametrize("tbn,pattern,start,P", DEC_CASES)
 def test_decode_bit_exact_vs_oracle(tbn, pattern, start, P, path, dedup):
     T, B, N = tbn
@@ -236,18 +232,9 @@ def test_copy_fast_variable_lengths_and_sizes():
             if t >= T:
                 want.append(out)
                 want_len.append(p)
-        for cpath in ("fast", "wave", "tile", "chunk", "pipe"):
+        for cpath in ("fast", "generic"):
             c = fec.Codec(Lx, T, B, N)
-            try:
-                c.set_copy_path(cpath)
-            except fec.FecError:
-                # a wave holds <= 64 groups, T < 4*NS4; a copy tile (32 packets) holds <= 16 KB;
-                # the chunk copy exists for k | 16 (instances (8,3), (8,4), (4,7)); the pipe copy
-                # for tiles whose LDS ring fits 64 KB per wave
-                assert (cpath == "wave" and (c.S > 4 * 64 or T >= c.S)) or \
-                    (cpath == "tile" and 32 * c.CW > 16384) or (cpath == "chunk" and c.k not in (4, 8)) or \
-                    (cpath == "pipe" and (Lx, tbn) not in [(300, (10, 3, 3)), (64, (10, 5, 2))])
-                continue
+            c.set_copy_path(cpath)
             out, ln = c.decode(torch.from_numpy(np.stack(cws)).cuda(), torch.from_numpy(pat).cuda())
             assert (ln.cpu().numpy() == np.array(want_len)).all(), (Lx, tbn, cpath)
             assert (out.cpu().numpy() == np.stack(want)).all(), (Lx, tbn, cpath)

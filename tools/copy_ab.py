@@ -1,6 +1,6 @@
 """Decode copy kernels A/B in one process on the same buffers: bytes and lengths equal to the
 LDS-tile copy ('fast'), then the kernel time alone and right after the encoder (as in the step).
-  python tools/copy_ab.py fast chunk [--tbn 10,3,3] [--packets 1000000]"""
+  python tools/copy_ab.py fast generic [--tbn 10,3,3] [--packets 1000000]"""
 import argparse
 import os
 import sys

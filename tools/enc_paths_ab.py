@@ -1,6 +1,6 @@
 """In-process A/B of encode kernel paths on the same buffers: 1M packets at (10,3,3) by default,
 alternating batches, median per path.
-  python tools/enc_paths_ab.py [--paths wave,tile] [--tbn 10,3,3] [--packets 1000010] [--env VAR=a|b]"""
+  python tools/enc_paths_ab.py [--paths generic,tile] [--tbn 10,3,3] [--packets 1000010] [--env VAR=a|b]"""
 import argparse
 import os
 import sys
@@ -12,7 +12,7 @@ import torch  # noqa: E402
 from fec_erasure_code_unit_test_relay_amd import Codec, fill_payload  # noqa: E402
 
 ap = argparse.ArgumentParser()
-ap.add_argument("--paths", default="wave,tile")
+ap.add_argument("--paths", default="generic,tile")
 ap.add_argument("--tbn", default="10,3,3")
 ap.add_argument("--packets", type=int, default=1_000_010)
 ap.add_argument("--iters", type=int, default=20)

@@ -1,5 +1,5 @@
 """Encode kernel alone: average time per launch over 1M packets (10,3,3), no concurrent kernels.
-  python tools/enc_time.py [--path wave] [--iters 20] [--tbn 10,3,3] [--packets 1000010]"""
+  python tools/enc_time.py [--path tile] [--iters 20] [--tbn 10,3,3] [--packets 1000010]"""
 import argparse
 import os
 import sys

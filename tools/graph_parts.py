@@ -85,7 +85,7 @@ for variant in (args.env or ["-"]):
         for kv in variant.split(","):
             k, v = kv.split("=", 1)
             os.environ[k] = v
-    c.set_copy_path(os.environ.get("FEC_GP_COPY", "auto"))  # e.g. FEC_GP_COPY=tile
+    c.set_copy_path(os.environ.get("FEC_GP_COPY", "auto"))  # e.g. FEC_GP_COPY=generic
     graphs = [(name, capture(fn)) for name, fn in PARTS]
     res = {name: timed(g, args.reps) for name, g in graphs}
     c.decode(cw, er, out=out, out_len=ol)

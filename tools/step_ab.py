@@ -1,6 +1,6 @@
 """In-process A/B of the bench step (encode + fec_decode_batch) over codec switches:
-  python tools/step_ab.py dedup=1 dedup=0 plan=fast plan=generic copy=fast copy=wave
-  combo=copy:wave,env:FEC_COPY_WPC:8   (settings persist: give every variant all its switches)"""
+  python tools/step_ab.py dedup=1 dedup=0 plan=fast plan=generic copy=fast copy=generic
+  combo=copy:fast,env:FEC_COPY_WPC:8   (settings persist: give every variant all its switches)"""
 import os
 import sys
 import time
@@ -33,7 +33,7 @@ def apply(cfg):
         c.set_plan_path(v)
     elif k == "copy":
         c.set_copy_path(v)
-    elif k == "combo":  # combo=copy:wave,env:FEC_COPY_WPC:16
+    elif k == "combo":  # combo=copy:fast,env:FEC_COPY_WPC:16
         for part in v.split(","):
             kk, vv = part.split(":", 1)
             apply(f"{kk}={vv}")

@@ -1,7 +1,7 @@
 """Bench step (encode + fec_decode_batch, eager launches) under environment settings read at each
-launch (FEC_TILE_NT, FEC_COPY_NT, FEC_COPY_REV, ...), one process, same buffers; every variant's
+launch (FEC_TILE_NT, FEC_COPY_NT, ...), one process, same buffers; every variant's
 outputs are checked (round trip + lost count).  Per-kernel event times are printed beside the step.
-  python tools/step_env_ab.py "" "FEC_TILE_NT=2" "FEC_COPY_REV=1,FEC_TILE_NT=2" """
+  python tools/step_env_ab.py "" "FEC_TILE_NT=2" "FEC_COPY_NT=1,FEC_TILE_NT=2" """
 import os
 import sys
 import time
