@@ -226,7 +226,10 @@ std::shared_ptr<const DecodeRules> shared_decode_rules(int T, int B, int N) {
         slot = e;
     }
     const int k = T - N + 1, n = k + B;
-    std::call_once(slot->once, [&] { slot->rules.build(make_generator(T, B, N), k, n, T); });
+    std::call_once(slot->once, [&] {
+        slot->rules.build(make_generator(T, B, N), k, n, T);
+        slot->rules.build_resync();
+    });
     return std::shared_ptr<const DecodeRules>(slot, &slot->rules);
 }
 
@@ -242,16 +245,26 @@ StreamPlanner::StreamPlanner(const Geometry& g, const DecodeRules* rules)
     if (g.B < g.N) throw std::invalid_argument("the streaming planner needs B >= N");
 }
 
-// Decode of data symbol t of block b with window min(t+T+1, n) (decodeBlock semantics).
-void StreamPlanner::decode_block(int b, int t) {
-    const Field& F = field();
-    if (t < k_ && !((er_[b] >> t) & 1u)) std::memcpy(dat(b, t), cw(b, t), n_);
-    const int w = std::min(t + T_ + 1, n_);
-    const uint32_t full = (w >= 32) ? 0xffffffffu : ((1u << w) - 1u);
-    const uint32_t m = er_[b] & full;
-    if (m == full) return;
+// decode_block(b, t) for t in [t0, t1): decode of data symbol t of block b with window
+// min(t+T+1, n) (decodeBlock semantics).  The cheap part (the received symbol's own row, the
+// masks) stays in the loop; the recovery runs out of line.
+void StreamPlanner::decode_blocks(int b, int t0, int t1) {
     const uint32_t kmask = (1u << k_) - 1u;
-    if (!(m & kmask)) return;  // no erased data symbol: nothing to recover
+    for (int t = t0; t < t1; ++t) {
+        if (t < k_ && !((er_[b] >> t) & 1u)) std::memcpy(dat(b, t), cw(b, t), n_);
+        const int w = std::min(t + T_ + 1, n_);
+        const uint32_t full = (w >= 32) ? 0xffffffffu : ((1u << w) - 1u);
+        const uint32_t m = er_[b] & full;
+        if (m == full) continue;
+        if (!(m & kmask)) continue;  // no erased data symbol: nothing to recover
+        // (w, m) alone decides whether anything is recovered: a repeat of a fruitless call is one too
+        if (w == memo_w_ && m == memo_m_) continue;
+        recover(b, w, m);
+    }
+}
+
+void StreamPlanner::recover(int b, int w, uint32_t m) {
+    const Field& F = field();
     const uint8_t* e = rules_->entry(w, m);
     uint8_t fresh[kMaxK][kMaxN];
     uint32_t got = 0;
@@ -267,6 +280,10 @@ void StreamPlanner::decode_block(int b, int t) {
             for (int q = 0; q < n_; ++q) fresh[i][q] ^= row[src[q]];
         }
         got |= 1u << i;
+    }
+    if (!got) {
+        memo_w_ = w;
+        memo_m_ = m;
     }
     for (int i = 0; i < k_; ++i) {
         if (!((got >> i) & 1u)) continue;
@@ -287,9 +304,7 @@ void StreamPlanner::decode_symbol(int b, int p, bool erased) {
         v[p] = 1;
     }
     if (p < T_) return;
-    decode_block(b, p - T_);
-    if (p == n_ - 1)
-        for (int j = p - T_ + 1; j < k_; ++j) decode_block(b, j);
+    decode_blocks(b, p - T_, p == n_ - 1 ? std::max(k_, p - T_ + 1) : p - T_ + 1);
 }
 
 // Decoder_Basic::decodeStream input half: symbol p of a packet fed at `time` goes to block
@@ -299,7 +314,43 @@ void StreamPlanner::feed(int64_t time, bool erased) {
     for (int p = 0; p < n_; ++p) decode_symbol((r - p + n_) % n_, p, erased);
 }
 
+void StreamPlanner::save_state(uint8_t* dst) const {
+    std::memcpy(dst, er_.data(), er_.size() * 4);
+    std::memcpy(dst + er_.size() * 4, cwc_.data(), cwc_.size());
+    std::memcpy(dst + er_.size() * 4 + cwc_.size(), datc_.data(), datc_.size());
+}
+
+void StreamPlanner::load_state(const uint8_t* src) {
+    std::memcpy(er_.data(), src, er_.size() * 4);
+    std::memcpy(cwc_.data(), src + er_.size() * 4, cwc_.size());
+    std::memcpy(datc_.data(), src + er_.size() * 4 + cwc_.size(), datc_.size());
+}
+
+void DecodeRules::build_resync() {
+    Geometry g;
+    g.k = k;
+    g.n = n;
+    g.T = T;
+    g.B = n - k;
+    g.N = T - k + 1;
+    if (g.B < g.N) return;  // no streaming planner for this configuration
+    StreamPlanner pl(g, this);
+    const size_t sb = pl.state_bytes();
+    std::vector<uint8_t> img(static_cast<size_t>(n) * sb);
+    const int64_t base = static_cast<int64_t>(n) * (T + 1);  // >= T and a multiple of n
+    for (int phi = 0; phi < n; ++phi) {
+        pl.resync_at(base + phi);
+        pl.save_state(img.data() + static_cast<size_t>(phi) * sb);
+    }
+    resync_full_bytes = sb;
+    resync_full.swap(img);
+}
+
 void StreamPlanner::resync_at(int64_t t) {
+    if (t >= T_ && rules_ && !rules_->resync_full.empty()) {  // the per-phase image (DecodeRules::build_resync)
+        load_state(rules_->resync_full.data() + static_cast<size_t>(t % n_) * rules_->resync_full_bytes);
+        return;
+    }
     for (int i = 0; i < n_ - T_; ++i) feed(t + i, true);
     for (int i = 0; i < T_; ++i)
         if (t - T_ + i >= 0) feed(t - T_ + i, false);

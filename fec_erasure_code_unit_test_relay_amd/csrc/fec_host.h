@@ -18,6 +18,7 @@
 //     (fec_plan_kernel in fec_codec.hip); this host copy serves the per-packet drop-in API.
 #pragma once
 
+#include <algorithm>
 #include <cstdint>
 #include <cstring>
 #include <memory>
@@ -106,7 +107,14 @@ struct DecodeRules {
     // and kept (the device planner computes its own, fec_kernels.hip wave_rule)
     bool lazy = false;
     std::vector<uint8_t> G;
+    // The whole symbolic decoder state right after a resynchronisation at time t >= T
+    // (StreamPlanner::resync_at), per phase t mod n: the resync rewrites every symbol of every
+    // diagonal block, so the state after it depends only on the phase (the device planner's
+    // build_resync_states rests on the same fact).  Filled by build_resync; empty = replay.
+    std::vector<uint8_t> resync_full;
+    size_t resync_full_bytes = 0;
     void build(const std::vector<uint8_t>& G, int k, int n, int T);
+    void build_resync();
     const uint8_t* entry(int w, uint32_t mask) const {
         if (lazy) return lazy_entry(w, mask);
         return table.data() + w_base[w] + static_cast<int64_t>(mask) * entry_bytes;
@@ -149,15 +157,33 @@ public:
     // Feed packet t (t must increase by one per call starting at 0); erased = packet t missing.
     StepResult step(int64_t t, bool erased);
     int64_t latest_erasure() const { return latest_; }
+    // True when a received packet t would take the fast path (Decoder.cpp:77-108): no erasure in
+    // the last T packets.  Then every received packet up to the next erasure does too, and
+    // skip_received(t, count) stands for count such steps (their outputs are kCopy once t >= T,
+    // never slow): the block state is not touched on the fast path, only the flag ring is.
+    bool fast_at(int64_t t) const { return latest_ == -1 || t - latest_ > T_; }
+    void skip_received(int64_t t, int64_t count) {
+        latest_ = -1;
+        if (count >= T_ + 1) {
+            std::fill(hist_.begin(), hist_.end(), uint8_t(0));
+        } else {
+            for (int64_t i = 0; i < count; ++i) hist_[(t + i) % (T_ + 1)] = 0;
+        }
+    }
     // The decoder's resynchronisation at erased packet t (Decoder.cpp:111-133) applied to the
     // current state, and a copy of one block's state (er mask, cwc[n][n], datc[k][n]).
     void resync_at(int64_t t);
     void block_state(int b, uint32_t* er, uint8_t* cwc, uint8_t* datc) const;
+    // the block state of every diagonal (er, cwc, datc) as one byte image, and back
+    size_t state_bytes() const { return er_.size() * 4 + cwc_.size() + datc_.size(); }
+    void save_state(uint8_t* dst) const;
+    void load_state(const uint8_t* src);
 
 private:
     void feed(int64_t time, bool erased);
     void decode_symbol(int b, int p, bool erased);
-    void decode_block(int b, int t);
+    void decode_blocks(int b, int t0, int t1);
+    void recover(int b, int w, uint32_t m);
     uint8_t* cw(int b, int p) { return &cwc_[(b * n_ + p) * n_]; }
     uint8_t* dat(int b, int i) { return &datc_[(b * k_ + i) * n_]; }
 
@@ -168,6 +194,8 @@ private:
     std::vector<uint8_t> datc_;    // [b][i][q] same for the recovered/received data symbol i
     std::vector<uint8_t> hist_;    // erasure flags of the last T+1 packets (ring)
     int64_t latest_ = -1;          // Decoder::latest_erasure_seq
+    int memo_w_ = -1;              // the last (window, mask) whose decode recovered nothing
+    uint32_t memo_m_ = 0;
 };
 
 // Post-resync state of one diagonal block for every phase phi = (t_resync - b) mod n, for resyncs

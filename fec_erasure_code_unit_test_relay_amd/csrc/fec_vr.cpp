@@ -7,6 +7,8 @@
 #include <algorithm>
 #include <chrono>
 #include <atomic>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <new>
 #include <stdexcept>
@@ -97,33 +99,311 @@ struct Report {        // decoder instance `id` reports packet x at its call for
 
 }  // namespace
 
-// Two phases.  (1) The control loop -- sender, estimators, encoder switches, the receiver's
-// decoder swaps -- never looks at a decoder's output (FEC_Decoder::onReceive results only feed
-// onDecodedMessage), so it runs first and records, per decoder instance, its calls (consecutive
+// Host memory for the plan's per-packet arrays: page-locked when the HIP runtime can provide it
+// (a 64-byte header records which allocator the block came from).
+void* vr_host_alloc(size_t bytes) {
+    void* p = nullptr;
+    if (hipHostMalloc(&p, bytes + 64, hipHostMallocDefault) == hipSuccess && p) {
+        static_cast<uint8_t*>(p)[0] = 1;
+    } else {
+        (void)hipGetLastError();
+        p = std::malloc(bytes + 64);
+        if (!p) throw std::bad_alloc();
+        static_cast<uint8_t*>(p)[0] = 0;
+    }
+    return static_cast<uint8_t*>(p) + 64;
+}
+
+void vr_host_free(void* q) {
+    if (!q) return;
+    uint8_t* p = static_cast<uint8_t*>(q) - 64;
+    if (p[0] == 1)
+        (void)hipHostFree(p);
+    else
+        std::free(p);
+}
+
+const VrFrame& VrPlan::frame(int64_t s) const {
+    auto it = std::upper_bound(frame_runs.begin(), frame_runs.end(), s,
+                               [](int64_t v, const FrameRun& r) { return v < r.first; });
+    return std::prev(it)->f;
+}
+
+// Two parts that overlap.  (1) The control loop -- sender, estimator feedback, encoder switches,
+// the receiver's decoder swaps -- never looks at a decoder's output (FEC_Decoder::onReceive
+// results only feed onDecodedMessage): it records, per decoder instance, its calls (consecutive
 // seqs from `first`, erased = the packet was dropped) and which of them report which packet.
-// (2) The symbolic decoders are independent of each other: they replay their calls in parallel
-// (one StreamPlanner per instance) and fill in the reported fates and coefficient rows.
+// (2) The symbolic decoders are independent of each other: as soon as the control loop is done
+// with an instance (it is no longer the current or the old decoder), a worker thread replays its
+// calls (one StreamPlanner per instance, erasure-free stretches on the fast path skipped in one
+// step) and fills in the reported fates and coefficient rows; at the end one worker adds up the
+// coding rate in the reference's order.
 void VrPlan::run(int max_payload, int T, int B, int N, bool mds, const uint8_t* pattern, int64_t n_pattern,
-                 int64_t P_value) {
+                 int64_t P_value, bool async) {
+    finish();
     L = max_payload;
     T_init = T;
     B_init = B;
     N_init = N;
     adaptive_mode_MDS = mds;
     P = P_value;
-    frames.clear();
+    const auto t_start = std::chrono::steady_clock::now();
+    try {
+        control(pattern, n_pattern, T, B, N, mds);
+    } catch (...) {
+        close_jobs();
+        finish();
+        throw;
+    }
+    t_dec_ = std::chrono::steady_clock::now();
+    control_ms = std::chrono::duration<double, std::milli>(t_dec_ - t_start).count();
+    if (!async) finish();
+}
+
+void VrPlan::start_workers() {
+    const unsigned hw = std::thread::hardware_concurrency();
+    size_t nth = std::max<size_t>(1, std::min<size_t>(hw > 1 ? hw - 1 : 1u, 8u));
+    if (const char* e = std::getenv("FEC_VR_THREADS")) nth = std::max(1, std::atoi(e));
+    {
+        std::lock_guard<std::mutex> lk(qmu_);
+        q_.clear();
+        qclosed_ = false;
+    }
+    batch_.clear();
+    recs_.resize(nth);
+    for (auto& r : recs_) r.clear();
+    pending_ = true;
+    for (size_t w = 0; w < nth; ++w) {
+        workers_.emplace_back([this, w] {
+            for (;;) {
+                DecJob j;
+                {
+                    std::unique_lock<std::mutex> lk(qmu_);
+                    qcv_.wait(lk, [&] { return !q_.empty() || qclosed_; });
+                    if (q_.empty()) break;
+                    j = std::move(q_.front());
+                    q_.pop_front();
+                }
+                if (j.id < 0) {  // final_sum_coding_rate, one float add per packet in sending order
+                    float s = 0;
+                    for (const RateRun& r : rate_runs)
+                        for (int64_t i = 0; i < r.count; ++i) s += r.rate;
+                    sum_coding_rate = s;
+                } else {
+                    decode_instance(j, recs_[w]);
+                }
+            }
+        });
+    }
+}
+
+// Jobs go to the workers in batches (one lock and one wake-up per batch: a wake-up per small job
+// would cost the control thread more than the job).
+void VrPlan::publish(DecJob&& j, bool flush) {
+    batch_.push_back(std::move(j));
+    if (!flush && batch_.size() < 32) return;
+    {
+        std::lock_guard<std::mutex> lk(qmu_);
+        for (DecJob& b : batch_) q_.push_back(std::move(b));
+    }
+    batch_.clear();
+    qcv_.notify_all();
+}
+
+void VrPlan::close_jobs() {
+    {
+        std::lock_guard<std::mutex> lk(qmu_);
+        qclosed_ = true;
+    }
+    qcv_.notify_all();
+}
+
+void VrPlan::finish() {
+    if (!pending_) return;
+    close_jobs();
+    for (auto& th : workers_) th.join();
+    workers_.clear();
+    pending_ = false;
+    lost = std::count(fate.begin(), fate.end(), static_cast<uint8_t>(kLost));
+    // recovered packets in x order (each worker's list is in its own job order)
+    std::vector<const RecEntry*> all;
+    for (const auto& r : recs_)
+        for (const RecEntry& e : r) all.push_back(&e);
+    std::sort(all.begin(), all.end(), [](const RecEntry* a, const RecEntry* b) { return a->x < b->x; });
+    const size_t nrec = all.size();
+    rec_x.resize(nrec);
+    rec_dec.resize(nrec);
+    rec_coef.resize(nrec * kVrCoefStride);
+    for (size_t i = 0; i < nrec; ++i) {
+        rec_x[i] = all[i]->x;
+        rec_dec[i] = fate_dec[static_cast<size_t>(all[i]->x)];
+        std::memcpy(&rec_coef[i * kVrCoefStride], all[i]->coef.data(), kVrCoefStride);
+    }
+    decoders_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_dec_).count();
+}
+
+// One decoder instance's calls (Decoder::decodeStream, Decoder.cpp:72-175) through a symbolic
+// StreamPlanner.  Between erasures the planner is on the fast path: such a stretch is skipped in
+// one step and its reported packets are copies (or, within the instance's first T calls, nothing
+// -- reported as lost, like any kNone output).
+void VrPlan::decode_instance(const DecJob& job, std::vector<RecEntry>& recs) {
+    const VrInstance& d = job.d;
+    const Geometry g = Geometry::make(L, d.T, d.B, d.N);
+    StreamPlanner pl(g, job.rules);
+    const Reports* rp = job.reps.data();
+    const Reports* rp_end = rp + job.reps.size();
+    size_t di = static_cast<size_t>(std::lower_bound(drops.begin(), drops.end(), d.first) - drops.begin());
+    int64_t s = d.first;
+    while (s < d.end) {
+        const int64_t t = s - d.first;
+        const int64_t nxt = di < drops.size() ? drops[di] : INT64_MAX;
+        while (rp != rp_end && rp->hi <= s) ++rp;
+        if (nxt > s && pl.fast_at(t)) {
+            const int64_t e = std::min(nxt, d.end);
+            pl.skip_received(t, e - s);
+            // reported packets of [s, e): copies once the instance is T calls old
+            for (const Reports* r = rp; r != rp_end && r->lo < e; ++r) {
+                const int64_t lo = std::max(r->lo, s), hi = std::min(r->hi, e);
+                if (lo >= hi) continue;
+                const int64_t c = std::min(hi, std::max(lo, d.first + g.T));  // seqs before c: kNone
+                if (c > lo) std::memset(&fate[static_cast<size_t>(lo - r->xoff)], kLost, static_cast<size_t>(c - lo));
+                if (hi > c) std::memset(&fate[static_cast<size_t>(c - r->xoff)], kCopy, static_cast<size_t>(hi - c));
+                std::memset(&slow[static_cast<size_t>(lo - r->xoff)], 0, static_cast<size_t>(hi - lo));
+            }
+            s = e;
+            continue;
+        }
+        const bool er = nxt == s;
+        if (er) ++di;
+        const StepResult r = pl.step(t, er);
+        if (rp != rp_end && rp->lo <= s) {
+            const int64_t x = s - rp->xoff;
+            const PacketFate f = r.fate == kNone ? kLost : r.fate;
+            fate[static_cast<size_t>(x)] = f;
+            slow[static_cast<size_t>(x)] = r.slow ? 1 : 0;
+            if (f == kRecovered) {
+                recs.emplace_back();
+                recs.back().x = x;
+                recs.back().coef.fill(0);
+                std::memcpy(recs.back().coef.data(), r.coef, static_cast<size_t>(g.k) * g.n);
+            }
+        }
+        ++s;
+    }
+}
+
+// The receiver's estimator feedback [T, B_est, N_est] after each received packet
+// (Application_Layer_Receiver.cpp:375-393, :430-436) depends only on which packets arrive: the
+// message T the estimators see is the sender's T, which never changes (the feedback's T is the
+// estimators' own).  The foreground estimator after received packet s is
+//   * s < r_2: the initial pair's (both fed from the start, so identical);
+//   * r_c <= s < r_{c+1} (c >= 2): the background one created at swap c-1, fed (r_{c-1}, s];
+// where r_c, the c-th swap, is the first received packet s >= max(100c, r_{c-1} + 1)
+// (`seq + 1 > cycle * 100`, one swap per received packet).  So the feedback splits into
+// independent jobs, one per swap, run here on worker threads; within a job, erasure-free
+// stretches at the estimator's fixed point are skipped to the next drop (estimate() would change
+// only previous_win_end there).  Output: fb_changes, the received packets at which the feedback
+// differs from the one before (the value before the first received packet is 0,0,0).
+void VrPlan::feedback(int T, bool mds, int64_t end) {
+    fb_changes.clear();
+    auto next_received = [&](int64_t s) {  // first received seq >= s
+        auto it = std::lower_bound(drops.begin(), drops.end(), s);
+        while (it != drops.end() && *it == s) {
+            ++s;
+            ++it;
+        }
+        return s;
+    };
+    std::vector<int64_t> r{-1, -1};  // r[c] = c-th swap (c >= 1); r[0] unused
+    for (int64_t c = 1;; ++c) {
+        const int64_t s = next_received(std::max(c * kEstimationCycle, r.back() + 1));
+        if (s >= end) break;
+        if (c == 1) r[1] = s; else r.push_back(s);
+    }
+    const int64_t nswap = r[1] < 0 ? 0 : static_cast<int64_t>(r.size()) - 1;  // swaps r[1..nswap]
+    auto swap_at = [&](int64_t c) { return c <= nswap ? r[static_cast<size_t>(c)] : end; };
+    // job 0: the initial estimator over [0, r_2); job c >= 2: fresh one fed from r_{c-1}+1,
+    // recording [r_c, r_{c+1})
+    const int64_t njobs = 1 + std::max<int64_t>(0, nswap - 1);
+    std::vector<std::vector<FbChange>> out(static_cast<size_t>(njobs));
+    auto job = [&](int64_t j) {
+        const bool init = j == 0;
+        const int64_t c = j + 1;                        // job j >= 1 is swap c = j + 1
+        ParameterEstimator e(kTTot, init ? mds : false);
+        const int64_t from = init ? 0 : swap_at(c - 1) + 1;
+        const int64_t rec = init ? 0 : swap_at(c);      // first seq whose feedback it gives
+        const int64_t to = init ? swap_at(2) : swap_at(c + 1);
+        std::vector<FbChange>& o = out[static_cast<size_t>(j)];
+        uint32_t last = 0xffffffffu;
+        auto di = std::lower_bound(drops.begin(), drops.end(), from);
+        for (int64_t s = from; s < to;) {
+            if (di != drops.end() && *di == s) {  // dropped: nothing reaches the receiver
+                ++di;
+                ++s;
+                continue;
+            }
+            const int64_t nd = di != drops.end() ? std::min(*di, to) : to;
+            if (e.steady(s, T)) {  // every received packet of [s, nd) leaves the estimator as it is
+                if (s >= rec || nd > rec) {
+                    const uint32_t v = uint32_t(e.T) | uint32_t(e.B_current) << 8 | uint32_t(e.N_current) << 16;
+                    if (v != last) {
+                        o.push_back(FbChange{std::max(s, rec), v});
+                        last = v;
+                    }
+                }
+                e.previous_win_end = nd - 1;
+                s = nd;
+                continue;
+            }
+            e.estimate(s, T);
+            if (s >= rec) {
+                const uint32_t v = uint32_t(e.T) | uint32_t(e.B_current) << 8 | uint32_t(e.N_current) << 16;
+                if (v != last) {
+                    o.push_back(FbChange{s, v});
+                    last = v;
+                }
+            }
+            ++s;
+        }
+    };
+    const unsigned hw = std::thread::hardware_concurrency();
+    size_t nth = std::max<size_t>(1, std::min<size_t>({static_cast<size_t>(njobs) / 64 + 1, hw ? hw : 1u, 8u}));
+    if (const char* ev = std::getenv("FEC_VR_THREADS")) nth = std::max(1, std::atoi(ev));
+    if (nth <= 1) {
+        for (int64_t j = 0; j < njobs; ++j) job(j);
+    } else {
+        std::atomic<int64_t> next{0};
+        std::vector<std::thread> pool;
+        for (size_t w = 0; w < nth; ++w)
+            pool.emplace_back([&] {
+                for (int64_t j; (j = next.fetch_add(1)) < njobs;) job(j);
+            });
+        for (auto& th : pool) th.join();
+    }
+    uint32_t cur = 0;
+    for (const auto& o : out)
+        for (const FbChange& f : o)
+            if (f.v != cur) {
+                fb_changes.push_back(f);
+                cur = f.v;
+            }
+}
+
+void VrPlan::control(const uint8_t* pattern, int64_t n_pattern, int T, int B, int N, bool mds) {
+    frame_runs.clear();
+    rate_runs.clear();
+    fb_changes.clear();
+    drops.clear();
     enc.clear();
     dec.clear();
-    erased.clear();
     fate.assign(static_cast<size_t>(P), kNone);
     fate_dec.assign(static_cast<size_t>(P), -1);
     slow.assign(static_cast<size_t>(P), 0);
-    rec_x.clear();
-    rec_dec.clear();
-    rec_coef.clear();
     lost = switches = 0;
     steady_packets = 0;
     sum_coding_rate = 0;
+    std::vector<std::vector<Reports>> reps;   // per decoder instance, in call order
+    std::vector<const DecodeRules*> drules;   // per decoder instance
 
     // ---- sender (Application_Layer_Sender.cpp:9-31, 64-93, 221-224) ----
     const bool adaptive = B == -1 || N == -1;
@@ -135,16 +415,26 @@ void VrPlan::run(int max_payload, int T, int B, int N, bool mds, const uint8_t* 
     int counter_transition = 0;
     bool transition_flag = true, double_coding_flag = true;
     // ---- receiver (Application_Layer_Receiver.cpp:10-31, 321-468) ----
-    std::unique_ptr<ParameterEstimator> est(new ParameterEstimator(kTTot, mds));
-    std::unique_ptr<ParameterEstimator> bg(new ParameterEstimator(kTTot, mds));
-    int64_t cycle = 1;
+    // dropped packets (ERASURE_TYPE 5: pattern byte 1 for seq < P+T), then the feedback stream
+    const auto tc0 = std::chrono::steady_clock::now();
+    const int64_t n_drop = std::min<int64_t>(P + T, n_pattern);  // packets the pattern can drop
+    for (int64_t q = 0; q < n_drop;) {
+        const void* hit = std::memchr(pattern + q, 1, static_cast<size_t>(n_drop - q));
+        if (!hit) break;
+        q = static_cast<const uint8_t*>(hit) - pattern;
+        drops.push_back(q++);
+    }
+    feedback(T, mds, P + T + 1);
+    const auto tc1 = std::chrono::steady_clock::now();
+    start_workers();
+    size_t fi = 0;        // next feedback change
+    size_t dri = 0;       // next drop
     uint8_t udp[12] = {};
     // ---- Variable_Rate_FEC_Decoder (Variable_Rate_FEC_Decoder.cpp:25-80, 2133-2400, 2440-2514) ----
     int64_t seq_start = -1, latest_seq = -1, sdc = -1, sde = -1;
     int dT = 0, dB = 0, dN = 0;
     int dcur = -1, dold = -1;
     bool dcf = false;
-    std::vector<std::vector<Report>> reports;  // per decoder instance, in call order
 
     auto new_decoder = [&](int T_, int B_, int N_, int64_t first) {
         VrInstance v;
@@ -154,21 +444,39 @@ void VrPlan::run(int max_payload, int T, int B, int N, bool mds, const uint8_t* 
         v.first = v.end = first;
         v.role_switch = -1;  // set when it becomes the old decoder
         dec.push_back(v);
-        reports.emplace_back();
+        reps.emplace_back();
+        drules.push_back(&rules_for(T_, B_, N_));
         return static_cast<int>(dec.size()) - 1;
+    };
+    // an instance the control loop is done with (neither the current nor the old decoder)
+    auto done_with = [&](int id) {
+        DecJob j;
+        j.id = id;
+        j.d = dec[static_cast<size_t>(id)];
+        j.rules = drules[static_cast<size_t>(id)];
+        j.reps.swap(reps[static_cast<size_t>(id)]);
+        publish(std::move(j));
     };
     auto call = [&](int id, int64_t seq) {
         if (seq != dec[id].end) throw std::logic_error("vr: decoder calls out of order");
         dec[id].end = seq + 1;
     };
-    // onDecodedMessage (:2403-2436): packets seq - T >= seq_start are reported once
-    auto report = [&](int id, int64_t seq) {
-        const int64_t x = seq - dT;
-        if (x < seq_start || x >= P) return;
-        reports[id].push_back(Report{seq, x});
-        fate_dec[x] = id;
+    // onDecodedMessage (:2403-2436): packets seq - T >= seq_start are reported once.  Instance id
+    // reports the seqs [lo, hi) (packets x = seq - dT in [seq_start, P)), extending its newest range.
+    auto report_range = [&](int id, int64_t lo, int64_t hi) {
+        lo = std::max(lo, seq_start + dT);
+        hi = std::min(hi, P + dT);
+        if (lo >= hi) return;
+        std::vector<Reports>& rv = reps[static_cast<size_t>(id)];
+        if (!rv.empty() && rv.back().hi == lo && rv.back().xoff == dT)
+            rv.back().hi = hi;
+        else
+            rv.push_back(Reports{id, lo, hi, dT});
+        std::fill(fate_dec.begin() + (lo - dT), fate_dec.begin() + (hi - dT), id);
     };
+    auto report = [&](int id, int64_t seq) { report_range(id, seq, seq + 1); };
     auto update_decoder = [&](int T_, int B_, int N_, int64_t first) {  // (:2520-2536)
+        if (dold >= 0) done_with(dold);
         dold = dcur;
         dT = T_;
         dB = B_;
@@ -176,36 +484,34 @@ void VrPlan::run(int max_payload, int T, int B, int N, bool mds, const uint8_t* 
         dcur = new_decoder(T_, B_, N_, first);
         dec[dold].role_switch = first;
     };
+    auto put_frame = [&](int64_t seq, const VrFrame& f) {
+        if (frame_runs.empty() || !(frame_runs.back().f == f)) frame_runs.push_back(FrameRun{seq, f});
+    };
+    auto put_rate = [&](int64_t count, float rate) {
+        if (!rate_runs.empty() && rate_runs.back().rate == rate)
+            rate_runs.back().count += count;
+        else
+            rate_runs.push_back(RateRun{count, rate});
+    };
 
-    const auto t_start = std::chrono::steady_clock::now();
-    frames.reserve(static_cast<size_t>(P + T + 1));
-    erased.reserve(static_cast<size_t>(P + T + 1));
-    const int64_t n_drop = std::min<int64_t>(P + T, n_pattern);  // packets the pattern can drop
-    int64_t next_drop = -1;                                        // cache of the next dropped seq
     for (int64_t seq = 0;; ++seq) {
         // ---- steady stretch: the same frame, every packet received, nothing switching ----
-        // Every branch below is then fixed: the feedback repeats (both estimators at their fixed
-        // point, no estimator swap before the next cycle boundary), the encoder has no switch to
-        // make and no transition running, the decoder has no gap, no parameter change and no
-        // double decoding.  Such packets are appended directly, in the same order and with the
-        // same float accumulation of the coding rate as the loop below; the stretch ends before
-        // the next drop, the next cycle boundary and the last packet.
+        // Every branch below is then fixed: the feedback repeats (no change in the feedback
+        // stream), the encoder has no switch to make and no transition running, the decoder has
+        // no gap, no parameter change and no double decoding.  Such packets are appended in one
+        // step (frames, coding-rate terms and reports as runs); the stretch ends before the next
+        // drop, the next feedback change and the last packet.
         if (cur >= 0 && !transition_flag && !double_coding_flag && counter_transition > eT && seq_start >= 0 &&
             latest_seq == seq && !dcf && sdc < seq && dT == eT && dB == eB && dN == eN && seq < P + T - 1) {
             const int fT = adaptive && udp[0] != 0 ? udp[0] : sT, fB = adaptive && udp[0] != 0 ? udp[1] : sB,
                       fN = adaptive && udp[0] != 0 ? udp[2] : sN;
             const int aT = adaptive && udp[0] != 0 ? udp[3] : sT_ack, aB = adaptive && udp[0] != 0 ? udp[4] : sB_ack;
             const bool would_switch = (fT != eT || fB != eB || fN != eN) && aT == eT && aB == eB;
-            if (!would_switch && est->steady(seq, eT) && bg->steady(seq, eT) && udp[3] == eT && udp[4] == eB &&
-                udp[5] == eN && udp[0] == est->T && udp[1] == est->B_current && udp[2] == est->N_current) {
-                if (next_drop < seq) {
-                    next_drop = n_drop;
-                    if (seq < n_drop) {
-                        const void* hit = std::memchr(pattern + seq, 1, static_cast<size_t>(n_drop - seq));
-                        if (hit) next_drop = static_cast<const uint8_t*>(hit) - pattern;
-                    }
-                }
-                const int64_t end = std::min({next_drop, cycle * kEstimationCycle, P + T - 1});
+            if (!would_switch && udp[3] == eT && udp[4] == eB && udp[5] == eN) {
+                while (dri < drops.size() && drops[dri] < seq) ++dri;
+                const int64_t next_drop = dri < drops.size() ? drops[dri] : INT64_MAX;
+                const int64_t next_fb = fi < fb_changes.size() ? fb_changes[fi].seq : INT64_MAX;
+                const int64_t end = std::min({next_drop, next_fb, P + T - 1});
                 if (end > seq) {
                     if (adaptive && udp[0] != 0) {
                         sT = udp[0];
@@ -221,22 +527,11 @@ void VrPlan::run(int max_payload, int T, int B, int N, bool mds, const uint8_t* 
                     fr.N = eN;
                     fr.enc_cur = cur;
                     fr.counter = counter_transition;
-                    const float rate = static_cast<float>(eT - eN + 1) / (eT - eN + 1 + eB);
-                    frames.insert(frames.end(), static_cast<size_t>(end - seq), fr);
-                    erased.insert(erased.end(), static_cast<size_t>(end - seq), uint8_t(0));
-                    std::vector<Report>& rp = reports[dcur];
-                    for (int64_t s = seq; s < end; ++s) {
-                        sum_coding_rate += rate;
-                        const int64_t x = s - dT;  // report(dcur, s)
-                        if (x >= seq_start && x < P) {
-                            rp.push_back(Report{s, x});
-                            fate_dec[x] = dcur;
-                        }
-                    }
+                    put_frame(seq, fr);
+                    put_rate(end - seq, static_cast<float>(eT - eN + 1) / (eT - eN + 1 + eB));
+                    report_range(dcur, seq, end);
                     enc[cur].end = end;
                     dec[dcur].end = end;  // call(dcur, s) for every s
-                    est->previous_win_end = end - 1;
-                    bg->previous_win_end = end - 1;
                     latest_seq = end;
                     sent = end;
                     steady_packets += end - seq;
@@ -300,23 +595,17 @@ void VrPlan::run(int max_payload, int T, int B, int N, bool mds, const uint8_t* 
             transition_flag = false;
         }
         if (!double_coding_flag)
-            sum_coding_rate += static_cast<float>(eT - eN + 1) / (eT - eN + 1 + eB);
+            put_rate(1, static_cast<float>(eT - eN + 1) / (eT - eN + 1 + eB));
         else
-            sum_coding_rate += static_cast<float>(eT - eN + 1) / ((eT - eN + 1 + eB) + (eT - eN_old + 1) + (eT - eN_old + 1 + eB));
-        frames.push_back(fr);
+            put_rate(1, static_cast<float>(eT - eN + 1) / ((eT - eN + 1 + eB) + (eT - eN_old + 1) + (eT - eN_old + 1 + eB)));
+        put_frame(seq, fr);
         const bool drop = seq < P + T && seq < n_pattern && pattern[seq] == 1;
-        erased.push_back(drop ? 1 : 0);
         sent = seq + 1;
 
         // ---- Application_Layer_Receiver::receive_message_and_decode ----
         if (drop) continue;  // artificial erasure: returns -1, feedback unchanged
-        est->estimate(seq, fr.T);
-        bg->estimate(seq, fr.T);
-        if (seq + 1 > cycle * kEstimationCycle) {
-            est = std::move(bg);
-            bg.reset(new ParameterEstimator(kTTot, false));
-            ++cycle;
-        }
+        uint32_t fbv = fi > 0 ? fb_changes[fi - 1].v : 0u;  // the estimators' feedback after seq
+        while (fi < fb_changes.size() && fb_changes[fi].seq <= seq) fbv = fb_changes[fi++].v;
         // ---- Variable_Rate_FEC_Decoder::decode ----
         if (seq_start == -1) {  // initialize_decoder (:2478-2494)
             seq_start = 0;
@@ -364,9 +653,9 @@ void VrPlan::run(int max_payload, int T, int B, int N, bool mds, const uint8_t* 
             }
             latest_seq = seq + 1;
         }
-        udp[0] = static_cast<uint8_t>(est->T);
-        udp[1] = static_cast<uint8_t>(est->B_current);
-        udp[2] = static_cast<uint8_t>(est->N_current);
+        udp[0] = static_cast<uint8_t>(fbv);
+        udp[1] = static_cast<uint8_t>(fbv >> 8);
+        udp[2] = static_cast<uint8_t>(fbv >> 16);
         udp[3] = static_cast<uint8_t>(fr.T);
         udp[4] = static_cast<uint8_t>(fr.B);
         udp[5] = static_cast<uint8_t>(fr.N);
@@ -375,67 +664,22 @@ void VrPlan::run(int max_payload, int T, int B, int N, bool mds, const uint8_t* 
     for (auto* list : {&enc, &dec})
         for (auto& e : *list)
             if (e.role_switch < 0) e.role_switch = e.end;  // never became the old instance
-
-    const auto t_control = std::chrono::steady_clock::now();
-    // ---- phase 2: the decoder instances, symbolically and in parallel ----
-    for (const auto& d : dec) rules_for(d.T, d.B, d.N);  // built before the workers share the map
-    struct Rec {
-        int64_t x;
-        uint8_t coef[kMaxK * kMaxRuleN];
-    };
-    std::vector<std::vector<Rec>> recs(dec.size());
-    std::atomic<size_t> next{0};
-    auto worker = [&]() {
-        for (size_t id; (id = next.fetch_add(1)) < dec.size();) {
-            const VrInstance& d = dec[id];
-            const Geometry g = Geometry::make(L, d.T, d.B, d.N);
-            StreamPlanner pl(g, rules_.at(d.T * 1024 + d.B * 32 + d.N).get());
-            const std::vector<Report>& rp = reports[id];
-            size_t ri = 0;
-            for (int64_t s = d.first; s < d.end; ++s) {
-                const StepResult r = pl.step(s - d.first, erased[static_cast<size_t>(s)] != 0);
-                if (ri == rp.size() || rp[ri].seq != s) continue;
-                const int64_t x = rp[ri++].x;
-                const PacketFate f = r.fate == kNone ? kLost : r.fate;
-                fate[x] = f;
-                slow[x] = r.slow ? 1 : 0;
-                if (f == kRecovered) {
-                    Rec rc;
-                    rc.x = x;
-                    std::memset(rc.coef, 0, sizeof(rc.coef));
-                    std::memcpy(rc.coef, r.coef, static_cast<size_t>(g.k) * g.n);
-                    recs[id].push_back(rc);
-                }
-            }
-        }
-    };
-    const unsigned hw = std::thread::hardware_concurrency();
-    const size_t nth = std::min<size_t>({dec.size(), hw ? hw : 1u, 16u});
-    if (nth <= 1) {
-        worker();
-    } else {
-        std::vector<std::thread> pool;
-        for (size_t i = 0; i < nth; ++i) pool.emplace_back(worker);
-        for (auto& th : pool) th.join();
+    // dropped flags of every sent packet
+    erased.assign(static_cast<size_t>(sent), 0);
+    for (int64_t s : drops) erased[static_cast<size_t>(s)] = 1;
+    if (std::getenv("FEC_VR_DEBUG")) {
+        const auto tc2 = std::chrono::steady_clock::now();
+        std::fprintf(stderr, "vr control: drops+feedback %.3f ms (%zu changes), loop %.3f ms\n",
+                     std::chrono::duration<double, std::milli>(tc1 - tc0).count(), fb_changes.size(),
+                     std::chrono::duration<double, std::milli>(tc2 - tc1).count());
     }
-    const auto t_decoders = std::chrono::steady_clock::now();
-    control_ms = std::chrono::duration<double, std::milli>(t_control - t_start).count();
-    decoders_ms = std::chrono::duration<double, std::milli>(t_decoders - t_control).count();
-    for (int64_t x = 0; x < P; ++x)
-        if (fate[x] == kLost) ++lost;
-    std::vector<std::pair<int64_t, const Rec*>> order;
-    for (size_t id = 0; id < recs.size(); ++id)
-        for (const Rec& rc : recs[id]) order.emplace_back(rc.x, &rc);
-    std::sort(order.begin(), order.end(),
-              [](const std::pair<int64_t, const Rec*>& a, const std::pair<int64_t, const Rec*>& b) {
-                  return a.first < b.first;
-              });
-    rec_coef.resize(order.size() * kVrCoefStride);
-    for (size_t i = 0; i < order.size(); ++i) {
-        rec_x.push_back(order[i].first);
-        rec_dec.push_back(fate_dec[order[i].first]);
-        std::memcpy(&rec_coef[i * kVrCoefStride], order[i].second->coef, kVrCoefStride);
-    }
+    // the last two decoder instances, then the coding-rate sum; no more jobs
+    if (dold >= 0) done_with(dold);
+    if (dcur >= 0) done_with(dcur);
+    DecJob rate;
+    rate.id = -1;
+    publish(std::move(rate), true);
+    close_jobs();
 }
 
 }  // namespace fec
@@ -443,12 +687,92 @@ void VrPlan::run(int max_payload, int T, int B, int N, bool mds, const uint8_t* 
 // ------------------------------------------------------------------------------------------
 // C ABI
 // ------------------------------------------------------------------------------------------
+struct fec_vr_plan;
+
+namespace {
+// Host tables sent to the device: one device buffer (grown on demand, kept across re-runs) and a
+// page-locked staging buffer filled by add() and sent with one asynchronous copy.  The staging
+// buffer is rewritten only after the copy out of it has completed, the device buffer only after
+// the launches that read it (events `sent` / `used`).
+struct Upload {
+    std::vector<std::pair<const void**, size_t>> fix;
+    uint8_t* h = nullptr;
+    size_t hcap = 0, size = 0;
+    void* d = nullptr;
+    size_t dcap = 0;
+    hipEvent_t sent = nullptr, used = nullptr;
+
+    Upload() = default;
+    Upload(const Upload&) = delete;
+    Upload& operator=(const Upload&) = delete;
+    ~Upload() {
+        if (sent) (void)hipEventSynchronize(sent);
+        if (used) (void)hipEventSynchronize(used);
+        if (d) (void)hipFree(d);
+        fec::vr_host_free(h);
+        if (sent) (void)hipEventDestroy(sent);
+        if (used) (void)hipEventDestroy(used);
+    }
+    int begin() {
+        if (!sent && hipEventCreateWithFlags(&sent, hipEventDisableTiming) != hipSuccess) return FEC_ERR_HIP;
+        if (!used && hipEventCreateWithFlags(&used, hipEventDisableTiming) != hipSuccess) return FEC_ERR_HIP;
+        if (hipEventSynchronize(sent) != hipSuccess) return FEC_ERR_HIP;
+        size = 0;
+        fix.clear();
+        return FEC_OK;
+    }
+    template <typename T>
+    void add(const T** dptr, const T* src, size_t count) {
+        const size_t off = (size + 255) & ~size_t(255);
+        const size_t need = off + std::max<size_t>(1, count) * sizeof(T);
+        if (need > hcap) {
+            const size_t cap = std::max(need, hcap + hcap / 2);
+            uint8_t* nh = static_cast<uint8_t*>(fec::vr_host_alloc(cap));
+            if (size) std::memcpy(nh, h, size);
+            fec::vr_host_free(h);
+            h = nh;
+            hcap = cap;
+        }
+        if (count) std::memcpy(h + off, src, count * sizeof(T));
+        fix.emplace_back(reinterpret_cast<const void**>(dptr), off);
+        size = need;
+    }
+    template <typename T, typename A>
+    void add(const T** dptr, const std::vector<T, A>& v) { add(dptr, v.data(), v.size()); }
+    // device buffer of at least `bytes`, free of earlier readers on stream s
+    static int reserve(void** dp, size_t* cap, size_t bytes, hipEvent_t used, hipStream_t s) {
+        if (hipStreamWaitEvent(s, used, 0) != hipSuccess) return FEC_ERR_HIP;
+        if (bytes <= *cap) return FEC_OK;
+        if (*dp) {
+            if (hipEventSynchronize(used) != hipSuccess) return FEC_ERR_HIP;
+            (void)hipFree(*dp);
+            *dp = nullptr;
+            *cap = 0;
+        }
+        const size_t c = bytes + bytes / 4;
+        if (hipMalloc(dp, c) != hipSuccess) return FEC_ERR_NOMEM;
+        *cap = c;
+        return FEC_OK;
+    }
+    int commit(hipStream_t s) {
+        if (int st = reserve(&d, &dcap, std::max<size_t>(16, size), used, s)) return st;
+        if (hipMemcpyAsync(d, h, size, hipMemcpyHostToDevice, s) != hipSuccess) return FEC_ERR_HIP;
+        if (hipEventRecord(sent, s) != hipSuccess) return FEC_ERR_HIP;
+        for (auto& f : fix) *f.first = static_cast<const uint8_t*>(d) + f.second;
+        return FEC_OK;
+    }
+    int done_reading(hipStream_t s) { return hipEventRecord(used, s) == hipSuccess ? FEC_OK : FEC_ERR_HIP; }
+};
+}  // namespace
+
 struct fec_vr_plan {
     fec::VrPlan plan;
     int cw_max = 0;
-    // ---- device tables (uploaded on first use, one allocation each for encode / decode) ----
-    void* d_enc_arena = nullptr;
-    void* d_dec_arena = nullptr;
+    // ---- device tables, rebuilt per run ----
+    Upload enc_up, dec_up, hdr_up;
+    void* d_pk = nullptr;                  // per-packet decoder id, fate, slow flag [P] each
+    size_t d_pk_cap = 0;
+    hipEvent_t pk_sent = nullptr;          // the per-packet copies out of the plan's arrays
     const int32_t* d_enc_inst = nullptr;   // [nenc][4]: k, n, CW, glog offset
     const int64_t* d_enc_span = nullptr;   // [nenc][2]: first, role_switch
     const int64_t* d_enc_cum = nullptr;    // [nenc+1]
@@ -463,40 +787,26 @@ struct fec_vr_plan {
     const uint8_t* d_rec_coef = nullptr;
     const uint8_t* d_gf = nullptr;
     const int32_t* d_hdr = nullptr;    // [sent][4]: frame header T, B, N, counter
-    void* d_hdr_arena = nullptr;
     int64_t enc_total = 0;             // codewords of all encoder instances
     int enc_tab = 0, enc_out = 0, enc_slot = 0, enc_wave = 0;  // fec_vr_encode_kernel's LDS layout
-    bool enc_ready = false, dec_ready = false;
+    bool enc_ready = false, dec_ready = false, hdr_ready = false;
 
     ~fec_vr_plan() {
-        for (void* p : {d_enc_arena, d_dec_arena, d_hdr_arena})
-            if (p) (void)hipFree(p);
+        if (pk_sent) {
+            (void)hipEventSynchronize(pk_sent);
+            (void)hipEventDestroy(pk_sent);
+        }
+        if (d_pk) {
+            (void)hipEventSynchronize(dec_up.used);
+            (void)hipFree(d_pk);
+        }
     }
+    // (re)plans; the per-packet arrays are rewritten only once their last copy has left them
+    void run(int max_payload, int T, int B, int N, bool mds, const uint8_t* erasure, int64_t n_erasure, int64_t P,
+             bool async);
 };
 
 namespace {
-// Host tables packed into one buffer (256-byte aligned pieces) and uploaded with one allocation
-// and one copy.
-struct Arena {
-    std::vector<uint8_t> host;
-    std::vector<std::pair<const void**, size_t>> fix;
-    template <typename T>
-    void add(const T** d, const T* h, size_t count) {
-        const size_t off = (host.size() + 255) & ~size_t(255);
-        host.resize(off + std::max<size_t>(1, count) * sizeof(T));
-        if (count) std::memcpy(host.data() + off, h, count * sizeof(T));
-        fix.emplace_back(reinterpret_cast<const void**>(d), off);
-    }
-    template <typename T>
-    void add(const T** d, const std::vector<T>& h) { add(d, h.data(), h.size()); }
-    int commit(void** base) {
-        if (hipMalloc(base, std::max<size_t>(16, host.size())) != hipSuccess) return FEC_ERR_NOMEM;
-        if (hipMemcpy(*base, host.data(), host.size(), hipMemcpyHostToDevice) != hipSuccess) return FEC_ERR_HIP;
-        for (auto& f : fix) *f.first = static_cast<const uint8_t*>(*base) + f.second;
-        return FEC_OK;
-    }
-};
-
 std::vector<uint8_t> gf_tables() {
     const fec::Field& F = fec::field();
     std::vector<uint8_t> gf(F.exp, F.exp + 512);
@@ -504,15 +814,20 @@ std::vector<uint8_t> gf_tables() {
     return gf;
 }
 
+int cw_of(const fec::VrPlan& p, const fec::VrInstance& v) { return fec::Geometry::make(p.L, v.T, v.B, v.N).CW; }
+
 // Encode tables: per encoder instance its geometry, first call, role switch and the running
 // count of codewords; per (T,B,N) tuple the gf_mul4 register tables of G's parity columns.
-int prepare_encode(fec_vr_plan* v) {
+int prepare_encode(fec_vr_plan* v, hipStream_t s) {
     if (v->enc_ready) return FEC_OK;
     const auto& p = v->plan;
     std::map<int, int> toff;  // tuple -> dword offset in gtab
     std::vector<uint32_t> gtab;
     std::vector<int32_t> inst;
     std::vector<int64_t> span, cum{0};
+    inst.reserve(p.enc.size() * 4);
+    span.reserve(p.enc.size() * 2);
+    cum.reserve(p.enc.size() + 1);
     int tab = 32, out = 16, slot = 16, nmax = 1;
     for (const auto& e : p.enc) {
         const fec::Geometry g = fec::Geometry::make(p.L, e.T, e.B, e.N);
@@ -531,12 +846,13 @@ int prepare_encode(fec_vr_plan* v) {
         span.insert(span.end(), {e.first, e.role_switch});
         cum.push_back(cum.back() + (e.end - e.first));
     }
-    Arena ar;
-    ar.add(&v->d_enc_inst, inst);
-    ar.add(&v->d_enc_span, span);
-    ar.add(&v->d_enc_cum, cum);
-    ar.add(&v->d_gtab, gtab);
-    if (int st = ar.commit(&v->d_enc_arena)) return st;
+    Upload& u = v->enc_up;
+    if (int st = u.begin()) return st;
+    u.add(&v->d_enc_inst, inst);
+    u.add(&v->d_enc_span, span);
+    u.add(&v->d_enc_cum, cum);
+    u.add(&v->d_gtab, gtab);
+    if (int st = u.commit(s)) return st;
     v->enc_total = cum.back();
     v->enc_tab = tab;
     v->enc_out = out;
@@ -546,34 +862,46 @@ int prepare_encode(fec_vr_plan* v) {
     return FEC_OK;
 }
 
-int prepare_decode(fec_vr_plan* v) {
+int prepare_decode(fec_vr_plan* v, hipStream_t s) {
     if (v->dec_ready) return FEC_OK;
     const auto& p = v->plan;
     std::vector<int32_t> inst;
     std::vector<int64_t> sw;
+    inst.reserve(p.dec.size() * 4);
+    sw.reserve(p.dec.size());
     for (const auto& d : p.dec) {
         const fec::Geometry g = fec::Geometry::make(p.L, d.T, d.B, d.N);
         inst.insert(inst.end(), {g.k, g.n, g.CW, 0});
         sw.push_back(d.role_switch);
     }
-    Arena ar;
-    ar.add(&v->d_pk_dec, p.fate_dec);
-    ar.add(&v->d_inst, inst);
-    ar.add(&v->d_inst_switch, sw);
-    ar.add(&v->d_fate, p.fate);
-    ar.add(&v->d_slow, p.slow);
-    ar.add(&v->d_rec_x, p.rec_x);
-    ar.add(&v->d_rec_dec, p.rec_dec);
-    ar.add(&v->d_rec_coef, p.rec_coef);
-    const std::vector<uint8_t> gf = gf_tables();
-    ar.add(&v->d_gf, gf);
-    if (int st = ar.commit(&v->d_dec_arena)) return st;
+    Upload& u = v->dec_up;
+    if (int st = u.begin()) return st;
+    u.add(&v->d_inst, inst);
+    u.add(&v->d_inst_switch, sw);
+    u.add(&v->d_rec_x, p.rec_x);
+    u.add(&v->d_rec_dec, p.rec_dec);
+    u.add(&v->d_rec_coef, p.rec_coef);
+    static const std::vector<uint8_t> gf = gf_tables();
+    u.add(&v->d_gf, gf);
+    if (int st = u.commit(s)) return st;
+    // the per-packet arrays go straight from the plan's (page-locked) buffers
+    const size_t P = static_cast<size_t>(p.P);
+    const size_t o_fate = (P * 4 + 255) & ~size_t(255), o_slow = (o_fate + P + 255) & ~size_t(255);
+    if (int st = Upload::reserve(&v->d_pk, &v->d_pk_cap, o_slow + std::max<size_t>(P, 1), u.used, s)) return st;
+    uint8_t* d = static_cast<uint8_t*>(v->d_pk);
+    if (hipMemcpyAsync(d, p.fate_dec.data(), P * 4, hipMemcpyHostToDevice, s) != hipSuccess ||
+        hipMemcpyAsync(d + o_fate, p.fate.data(), P, hipMemcpyHostToDevice, s) != hipSuccess ||
+        hipMemcpyAsync(d + o_slow, p.slow.data(), P, hipMemcpyHostToDevice, s) != hipSuccess)
+        return FEC_ERR_HIP;
+    if (!v->pk_sent && hipEventCreateWithFlags(&v->pk_sent, hipEventDisableTiming) != hipSuccess) return FEC_ERR_HIP;
+    if (hipEventRecord(v->pk_sent, s) != hipSuccess) return FEC_ERR_HIP;
+    v->d_pk_dec = reinterpret_cast<const int32_t*>(d);
+    v->d_fate = d + o_fate;
+    v->d_slow = d + o_slow;
     v->dec_ready = true;
     return FEC_OK;
 }
-}  // namespace
 
-namespace {
 template <typename F>
 int vr_guarded(F&& f) {
     try {
@@ -584,8 +912,17 @@ int vr_guarded(F&& f) {
         return FEC_ERR_ARG;
     }
 }
-int cw_of(const fec::VrPlan& p, const fec::VrInstance& v) { return fec::Geometry::make(p.L, v.T, v.B, v.N).CW; }
 }  // namespace
+
+void fec_vr_plan::run(int max_payload, int T, int B, int N, bool mds, const uint8_t* erasure, int64_t n_erasure,
+                      int64_t P, bool async) {
+    if (pk_sent) (void)hipEventSynchronize(pk_sent);
+    plan.run(max_payload, T, B, N, mds, erasure, n_erasure, P, async);
+    cw_max = 0;
+    for (const auto& e : plan.enc) cw_max = std::max(cw_max, cw_of(plan, e));
+    for (const auto& d : plan.dec) cw_max = std::max(cw_max, cw_of(plan, d));
+    enc_ready = dec_ready = hdr_ready = false;
+}
 
 extern "C" {
 
@@ -595,10 +932,17 @@ int fec_vr_plan_create(int max_payload, int T, int B, int N, int adaptive_mode_M
     *out = nullptr;
     return vr_guarded([&] {
         std::unique_ptr<fec_vr_plan> v(new fec_vr_plan());
-        v->plan.run(max_payload, T, B, N, adaptive_mode_MDS != 0, erasure, n_erasure, P);
-        for (const auto& e : v->plan.enc) v->cw_max = std::max(v->cw_max, cw_of(v->plan, e));
-        for (const auto& d : v->plan.dec) v->cw_max = std::max(v->cw_max, cw_of(v->plan, d));
+        v->run(max_payload, T, B, N, adaptive_mode_MDS != 0, erasure, n_erasure, P, false);
         *out = v.release();
+        return FEC_OK;
+    });
+}
+
+int fec_vr_plan_rerun(fec_vr_plan* v, const uint8_t* erasure, int64_t n_erasure, int64_t P, int async) {
+    if (!v || P < 1 || n_erasure < 0 || (n_erasure > 0 && !erasure)) return FEC_ERR_ARG;
+    return vr_guarded([&] {
+        const fec::VrPlan& p = v->plan;
+        v->run(p.L, p.T_init, p.B_init, p.N_init, p.adaptive_mode_MDS, erasure, n_erasure, P, async != 0);
         return FEC_OK;
     });
 }
@@ -608,9 +952,11 @@ int fec_vr_plan_destroy(fec_vr_plan* v) {
     return FEC_OK;
 }
 
-int fec_vr_plan_stats(const fec_vr_plan* v, int64_t* lost, int64_t* switches, double* coding_rate,
+int fec_vr_plan_stats(const fec_vr_plan* vc, int64_t* lost, int64_t* switches, double* coding_rate,
                       int64_t* sent, int* n_encoders, int* n_decoders, int* cw_max) {
-    if (!v) return FEC_ERR_ARG;
+    if (!vc) return FEC_ERR_ARG;
+    fec_vr_plan* v = const_cast<fec_vr_plan*>(vc);
+    if (lost || coding_rate) v->plan.finish();  // the rest is final after the control loop
     if (lost) *lost = v->plan.lost;
     if (switches) *switches = v->plan.switches;
     if (coding_rate) *coding_rate = v->plan.coding_rate();
@@ -621,8 +967,10 @@ int fec_vr_plan_stats(const fec_vr_plan* v, int64_t* lost, int64_t* switches, do
     return FEC_OK;
 }
 
-int fec_vr_plan_timing(const fec_vr_plan* v, double* control_ms, double* decoders_ms) {
-    if (!v) return FEC_ERR_ARG;
+int fec_vr_plan_timing(const fec_vr_plan* vc, double* control_ms, double* decoders_ms) {
+    if (!vc) return FEC_ERR_ARG;
+    fec_vr_plan* v = const_cast<fec_vr_plan*>(vc);
+    v->plan.finish();
     if (control_ms) *control_ms = v->plan.control_ms;
     if (decoders_ms) *decoders_ms = v->plan.decoders_ms;
     return FEC_OK;
@@ -647,22 +995,28 @@ int fec_vr_plan_instances(const fec_vr_plan* v, int64_t* encoders, int64_t* deco
     return FEC_OK;
 }
 
-int fec_vr_plan_packets(const fec_vr_plan* v, int32_t* frames, uint8_t* erased, uint8_t* fate,
+int fec_vr_plan_packets(const fec_vr_plan* vc, int32_t* frames, uint8_t* erased, uint8_t* fate,
                         int32_t* fate_decoder) {
-    if (!v) return FEC_ERR_ARG;
+    if (!vc) return FEC_ERR_ARG;
+    fec_vr_plan* v = const_cast<fec_vr_plan*>(vc);
+    v->plan.finish();
     const auto& p = v->plan;
-    for (int64_t s = 0; s < p.sent; ++s) {
-        if (frames) {
-            int32_t* o = frames + 6 * s;
-            o[0] = p.frames[s].T;
-            o[1] = p.frames[s].B;
-            o[2] = p.frames[s].N;
-            o[3] = p.frames[s].counter;
-            o[4] = p.frames[s].enc_cur;
-            o[5] = p.frames[s].enc_old;
+    if (frames) {
+        for (size_t r = 0; r < p.frame_runs.size(); ++r) {
+            const int64_t hi = r + 1 < p.frame_runs.size() ? p.frame_runs[r + 1].first : p.sent;
+            const fec::VrFrame& f = p.frame_runs[r].f;
+            for (int64_t s = p.frame_runs[r].first; s < hi; ++s) {
+                int32_t* o = frames + 6 * s;
+                o[0] = f.T;
+                o[1] = f.B;
+                o[2] = f.N;
+                o[3] = f.counter;
+                o[4] = f.enc_cur;
+                o[5] = f.enc_old;
+            }
         }
-        if (erased) erased[s] = p.erased[s];
     }
+    if (erased) std::memcpy(erased, p.erased.data(), p.erased.size());
     if (fate) std::memcpy(fate, p.fate.data(), p.fate.size());
     if (fate_decoder) std::memcpy(fate_decoder, p.fate_dec.data(), p.fate_dec.size() * 4);
     return FEC_OK;
@@ -671,15 +1025,18 @@ int fec_vr_plan_packets(const fec_vr_plan* v, int32_t* frames, uint8_t* erased, 
 // Encode every packet the sender produced: row s of d_cw_cur (stride cw_max) = the codeword of
 // frame s's current encoder, row s of d_cw_old = its old encoder's (double coding; rows of frames
 // without one are left alone), trimmed sizes in d_len_*.  One launch for every instance of every
-// (T,B,N) tuple (fec_vr_encode_kernel), straight from the payload rows.
+// (T,B,N) tuple (fec_vr_encode_kernel), straight from the payload rows.  Needs only the control
+// loop's results: after an asynchronous fec_vr_plan_rerun it overlaps the symbolic decoders.
 int fec_vr_encode_batch(fec_vr_plan* v, const uint8_t* d_payload, const int32_t* d_payload_len, uint8_t* d_cw_cur,
                         int32_t* d_len_cur, uint8_t* d_cw_old, int32_t* d_len_old, void* hip_stream) {
     if (!v || !d_payload || !d_cw_cur || !d_len_cur || !d_cw_old || !d_len_old) return FEC_ERR_ARG;
-    if (int st = vr_guarded([&] { return prepare_encode(v); })) return st;
+    hipStream_t s = static_cast<hipStream_t>(hip_stream);
+    if (int st = vr_guarded([&] { return prepare_encode(v, s); })) return st;
     fec::VrEncodeArgs a{d_payload, d_payload_len, v->plan.L, v->d_enc_inst, v->d_enc_span, v->d_enc_cum,
                         static_cast<int>(v->plan.enc.size()), v->enc_total, v->enc_tab, v->enc_out, v->enc_slot,
                         v->enc_wave, v->d_gtab, v->cw_max, d_cw_cur, d_cw_old, d_len_cur, d_len_old};
-    return fec::vr_launch_encode(a, hip_stream);
+    if (int st = fec::vr_launch_encode(a, hip_stream)) return st;
+    return v->enc_up.done_reading(s);
 }
 
 // The P2P wire packets of every frame: row s of d_packets (stride >= 10 + 2*cw_max bytes) =
@@ -690,22 +1047,33 @@ int fec_vr_frames_batch(fec_vr_plan* v, const uint8_t* d_cw_cur, const int32_t* 
                         void* hip_stream) {
     if (!v || !d_cw_cur || !d_len_cur || !d_cw_old || !d_len_old || !d_packets || !d_packet_len) return FEC_ERR_ARG;
     if (stride < 10 + 2 * static_cast<int64_t>(v->cw_max)) return FEC_ERR_ARG;
+    hipStream_t s = static_cast<hipStream_t>(hip_stream);
     const auto& p = v->plan;
-    if (!v->d_hdr) {
-        std::vector<int32_t> h(static_cast<size_t>(p.sent) * 4);
-        for (int64_t s = 0; s < p.sent; ++s) {
-            h[4 * s] = p.frames[s].T;
-            h[4 * s + 1] = p.frames[s].B;
-            h[4 * s + 2] = p.frames[s].N;
-            h[4 * s + 3] = p.frames[s].counter;
-        }
-        Arena ar;
-        ar.add(&v->d_hdr, h);
-        if (int st = ar.commit(&v->d_hdr_arena)) return st;
+    if (!v->hdr_ready) {
+        int st = vr_guarded([&] {
+            std::vector<int32_t> h(static_cast<size_t>(p.sent) * 4);
+            for (size_t r = 0; r < p.frame_runs.size(); ++r) {
+                const int64_t hi = r + 1 < p.frame_runs.size() ? p.frame_runs[r + 1].first : p.sent;
+                const fec::VrFrame& f = p.frame_runs[r].f;
+                for (int64_t q = p.frame_runs[r].first; q < hi; ++q) {
+                    h[4 * q] = f.T;
+                    h[4 * q + 1] = f.B;
+                    h[4 * q + 2] = f.N;
+                    h[4 * q + 3] = f.counter;
+                }
+            }
+            Upload& u = v->hdr_up;
+            if (int e = u.begin()) return e;
+            u.add(&v->d_hdr, h);
+            return u.commit(s);
+        });
+        if (st) return st;
+        v->hdr_ready = true;
     }
     fec::VrFrameArgs a{d_cw_cur, d_len_cur, d_cw_old, d_len_old, v->cw_max, v->d_hdr, p.sent, d_packets, stride,
                        d_packet_len};
-    return fec::vr_launch_frames(a, hip_stream);
+    if (int st = fec::vr_launch_frames(a, hip_stream)) return st;
+    return v->hdr_up.done_reading(s);
 }
 
 // Decode the schedule from the frames' arrays: every packet x < P was reported by one decoder
@@ -716,13 +1084,19 @@ int fec_vr_decode_batch(fec_vr_plan* v, const uint8_t* d_cw_cur, const uint8_t* 
                         uint8_t* d_out, int32_t* d_out_len, void* hip_stream) {
     (void)d_erased;
     if (!v || !d_cw_cur || !d_cw_old || !d_out || !d_out_len) return FEC_ERR_ARG;
-    if (int st = vr_guarded([&] { return prepare_decode(v); })) return st;
+    hipStream_t s = static_cast<hipStream_t>(hip_stream);
+    if (int st = vr_guarded([&] {
+            v->plan.finish();
+            return prepare_decode(v, s);
+        }))
+        return st;
     const auto& p = v->plan;
     fec::VrCopyArgs ca{d_cw_cur, v->cw_max, v->d_pk_dec, v->d_inst, v->d_fate, v->d_slow, p.P, p.L, d_out, d_out_len};
     if (int st = fec::vr_launch_copy(ca, hip_stream)) return st;
     fec::VrRecArgs ra{d_cw_cur, d_cw_old, v->cw_max, p.sent, v->d_rec_x, v->d_rec_dec, v->d_rec_coef,
                       static_cast<int>(p.rec_x.size()), v->d_inst, v->d_inst_switch, v->d_gf, p.L, d_out, d_out_len};
-    return fec::vr_launch_recover(ra, hip_stream);
+    if (int st = fec::vr_launch_recover(ra, hip_stream)) return st;
+    return v->dec_up.done_reading(s);
 }
 
 int fec_vr_parse_batch(const uint8_t* d_packets, int64_t stride, const int32_t* d_packet_len, int64_t rows,

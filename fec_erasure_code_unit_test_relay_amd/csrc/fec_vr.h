@@ -17,9 +17,16 @@
 // (fec_vr_encode_batch / fec_vr_decode_batch in fec_vr.cpp): one launch pair per instance.
 #pragma once
 
+#include <array>
+#include <chrono>
+#include <condition_variable>
+#include <deque>
 #include <cstdint>
 #include <map>
 #include <memory>
+#include <mutex>
+#include <thread>
+#include <utility>
 #include <vector>
 
 #include "fec_host.h"
@@ -60,19 +67,63 @@ struct VrInstance {
 struct VrFrame {  // Application_Layer_Sender header (Application_Layer_Sender.cpp:259-269) + VR frame
     int T = 0, B = 0, N = 0, counter = 0;
     int enc_cur = -1, enc_old = -1;  // encoder instances whose codewords the frame carries
+    bool operator==(const VrFrame& o) const {
+        return T == o.T && B == o.B && N == o.N && counter == o.counter && enc_cur == o.enc_cur && enc_old == o.enc_old;
+    }
 };
 
+// Page-locked host memory (hipHostMalloc) when a GPU runtime is present, plain heap memory
+// otherwise: the plan's per-packet arrays go to the device with asynchronous copies straight from
+// where the plan wrote them, and stay allocated across re-runs of one plan.
+void* vr_host_alloc(size_t bytes);
+void vr_host_free(void* p);
+template <typename T>
+struct VrHostAlloc {
+    using value_type = T;
+    VrHostAlloc() = default;
+    template <typename U>
+    VrHostAlloc(const VrHostAlloc<U>&) {}
+    T* allocate(size_t n) { return static_cast<T*>(vr_host_alloc(n * sizeof(T))); }
+    void deallocate(T* p, size_t) { vr_host_free(p); }
+    template <typename U>
+    bool operator==(const VrHostAlloc<U>&) const { return true; }
+    template <typename U>
+    bool operator!=(const VrHostAlloc<U>&) const { return false; }
+};
+template <typename T>
+using VrHostVec = std::vector<T, VrHostAlloc<T>>;
+
 struct VrPlan {
+    struct FrameRun {      // frames[first .. next run's first) are all `f`
+        int64_t first;
+        VrFrame f;
+    };
+    struct RateRun {       // `count` packets adding `rate` to final_sum_coding_rate, in order
+        int64_t count;
+        float rate;
+    };
+    struct Reports {       // decoder instance `id` reports packet seq - xoff at its calls for seq in [lo, hi)
+        int32_t id;
+        int64_t lo, hi, xoff;
+    };
+
     int L = 0, T_init = 0, B_init = 0, N_init = 0;
     bool adaptive_mode_MDS = false;
     int64_t P = 0;                    // NUMBER_OF_ITERATIONS: packets whose output is counted
     int64_t sent = 0;                 // packets the sender produced (>= P + T)
     std::vector<uint8_t> erased;      // [sent]: dropped before the receiver (Application_Layer_Receiver.cpp:352-360)
-    std::vector<VrFrame> frames;      // [sent]
+    std::vector<int64_t> drops;       // the seqs with erased == 1, increasing
+    struct FbChange {      // the receiver's feedback (T | B_est << 8 | N_est << 16) from received seq on
+        int64_t seq;
+        uint32_t v;
+    };
+    std::vector<FbChange> fb_changes;
+    std::vector<FrameRun> frame_runs; // frames of [0, sent), run-length coded
+    std::vector<RateRun> rate_runs;
     std::vector<VrInstance> enc, dec;
-    std::vector<uint8_t> fate;        // [P]: PacketFate of the output reported for packet x
-    std::vector<int32_t> fate_dec;    // [P]: decoder instance that reported it
-    std::vector<uint8_t> slow;        // [P]: reported by the block decoders (length clamped)
+    VrHostVec<uint8_t> fate;          // [P]: PacketFate of the output reported for packet x
+    VrHostVec<int32_t> fate_dec;      // [P]: decoder instance that reported it
+    VrHostVec<uint8_t> slow;          // [P]: reported by the block decoders (length clamped)
     // recovered packets: x, reporting decoder, its k x n coefficient rows (stride kVrCoefStride)
     std::vector<int64_t> rec_x;
     std::vector<int32_t> rec_dec;
@@ -83,14 +134,49 @@ struct VrPlan {
     double control_ms = 0, decoders_ms = 0;  // wall time of run()'s two phases
     double coding_rate() const { return sent ? sum_coding_rate / static_cast<float>(sent) : 0.0; }
 
+    VrPlan() = default;
+    VrPlan(const VrPlan&) = delete;
+    VrPlan& operator=(const VrPlan&) = delete;
+    ~VrPlan() { finish(); }
+
     // Runs the loop until the receiver has processed seq P+T-1 (application_local_simulation.cpp:813).
-    // B_init = N_init = -1: adaptive (the sender starts at (T, 0, 0)).
+    // B_init = N_init = -1: adaptive (the sender starts at (T, 0, 0)).  Re-running one plan reuses
+    // its buffers.  async: return after the control loop (enc, dec, frames, erased, sent, switches
+    // are final); the symbolic decoders (fate, slow, rec_*, lost, coding rate) run on worker
+    // threads until finish().
     void run(int max_payload, int T, int B, int N, bool mds, const uint8_t* pattern, int64_t n_pattern,
-             int64_t P_value);
+             int64_t P_value, bool async = false);
+    void finish();  // waits for the decoder phase of an async run (no-op otherwise)
+    const VrFrame& frame(int64_t s) const;  // frame of sent packet s
 
 private:
+    struct DecJob {        // a decoder instance the control loop is done with (id < 0: the rate sum)
+        int id = -1;
+        VrInstance d;
+        const DecodeRules* rules = nullptr;
+        std::vector<Reports> reps;
+    };
+    struct RecEntry {      // a recovered packet and its k x n coefficient rows
+        int64_t x;
+        std::array<uint8_t, kVrCoefStride> coef;
+    };
+    void control(const uint8_t* pattern, int64_t n_pattern, int T, int B, int N, bool mds);
+    void feedback(int T, bool mds, int64_t end);
+    void start_workers();
+    void publish(DecJob&& j, bool flush = false);
+    void close_jobs();
+    void decode_instance(const DecJob& job, std::vector<RecEntry>& recs);
     std::map<int, std::shared_ptr<const DecodeRules>> rules_;  // key T*1024 + B*32 + N
     const DecodeRules& rules_for(int T, int B, int N);
+    std::vector<std::thread> workers_;
+    std::vector<std::vector<RecEntry>> recs_;  // per worker
+    std::mutex qmu_;
+    std::condition_variable qcv_;
+    std::deque<DecJob> q_;
+    std::vector<DecJob> batch_;  // jobs not yet handed to the workers
+    bool qclosed_ = false;
+    std::chrono::steady_clock::time_point t_dec_;
+    bool pending_ = false;
 };
 
 // Device side of the schedule (fec_vr_kernels.hip).  All launches go to `s`.

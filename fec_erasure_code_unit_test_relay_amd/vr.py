@@ -29,6 +29,27 @@ class VrPlan:
               "fec_vr_plan_create")
         self._h = h
         self.L, self.T, self.P = max_payload, T, P
+        self._load(light)
+
+    def rerun(self, erasure: np.ndarray, P: int, wait: bool = True, light: bool = True):
+        """Plan again in place (same configuration) on another pattern / P, reusing the plan's
+        buffers.  wait=False returns after the control loop: the symbolic decoders run on worker
+        threads meanwhile (encode() can launch at once; decode() and the statistics wait for them)."""
+        pat = np.ascontiguousarray(erasure, dtype=np.uint8)
+        check(lib().fec_vr_plan_rerun(self._h, pat.ctypes.data_as(ctypes.c_void_p), pat.size, P, 0 if wait else 1),
+              "fec_vr_plan_rerun")
+        self.P = P
+        if wait:
+            self._load(light)
+        else:
+            sent, cwm = ctypes.c_int64(), ctypes.c_int()
+            check(lib().fec_vr_plan_stats(self._h, None, None, None, ctypes.byref(sent), None, None, ctypes.byref(cwm)),
+                  "fec_vr_plan_stats")
+            self.sent, self.cw_max = sent.value, cwm.value
+        return self
+
+    def _load(self, light):
+        h, P = self._h, self.P
         lost, sw, sent = ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int64()
         rate = ctypes.c_double()
         ne, nd, cwm = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()

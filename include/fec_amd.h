@@ -239,6 +239,12 @@ typedef struct fec_vr_plan fec_vr_plan;
 int fec_vr_plan_create(int max_payload, int T, int B, int N, int adaptive_mode_MDS,
                        const uint8_t *erasure, int64_t n_erasure, int64_t P, fec_vr_plan **out);
 int fec_vr_plan_destroy(fec_vr_plan *plan);
+/* Plan again, in place, with the plan's (max_payload, T, B, N, adaptive_mode_MDS) on a new pattern
+ * and P: the host buffers, device tables and worker threads of the plan are reused.  async != 0:
+ * returns after the serial control loop (instances, frames, sent, switches final); the symbolic
+ * decoder instances run on worker threads meanwhile, so fec_vr_encode_batch's launch overlaps them;
+ * every call that needs their results (stats, timing, packets, decode) waits for them. */
+int fec_vr_plan_rerun(fec_vr_plan *plan, const uint8_t *erasure, int64_t n_erasure, int64_t P, int async);
 /* lost: packets among 0..P-1 the receiver outputs empty ("Final FEC loss rate" x P); switches:
  * "Start double coding at the source" count; coding_rate: Variable_Rate_FEC_Encoder's final rate;
  * sent: packets the sender produced; cw_max: row stride of the codeword arrays below. */
