@@ -491,7 +491,7 @@ int launch_plan(fec_codec* c, const uint8_t* d_er, int64_t P, void* d_ws, size_t
 }
 
 int launch_copy(fec_codec* c, const uint8_t* d_cw, const uint8_t* d_er, int64_t P, uint8_t* d_out,
-                int32_t* d_outlen, hipStream_t s) {
+                int32_t* d_outlen, hipStream_t s, bool skip_erased = false) {
     const Geometry& g = c->g;
     const int64_t Pout = P - g.T;
     if (Pout <= 0) return FEC_OK;
@@ -514,7 +514,7 @@ int launch_copy(fec_codec* c, const uint8_t* d_cw, const uint8_t* d_er, int64_t 
         fa.raw_bytes = c->copyf_raw(fa.TP);
         fa.out_bytes = round16(fa.TP * g.L);
         fa.stamps = (c->stamp_kernel == FEC_KERNEL_DEC_COPY) ? c->d_stamps : nullptr;
-        fa.skip_erased = 0;
+        fa.skip_erased = skip_erased ? 1 : 0;
         // non-temporal codeword loads and payload stores: 0.318 vs 0.338 ms per bench step
         // (tools/step_ab.py, same process, profiles/r02/decode_diag/copy_nt_ab.txt)
         fa.nt = 1;
@@ -553,7 +553,7 @@ int launch_copy(fec_codec* c, const uint8_t* d_cw, const uint8_t* d_er, int64_t 
 
 // Recovered packets -> rec_list (fec_compact_kernel), on `s` after the plan.
 int launch_compact(fec_codec* c, int64_t P, uint8_t* d_out, int32_t* d_outlen, void* d_ws, size_t ws_bytes,
-                   hipStream_t s, int64_t row_off = 0) {
+                   hipStream_t s, int64_t row_off = 0, bool zero_lost = false) {
     const Geometry& g = c->g;
     if (P - g.T <= 0) return FEC_OK;
     if (int st = check_ws(c, P, d_ws, ws_bytes)) return st;
@@ -567,7 +567,7 @@ int launch_compact(fec_codec* c, int64_t P, uint8_t* d_out, int32_t* d_outlen, v
     ca.rec_list = w.rec_list;
     // the copy writes every row (zero rows and length 0 for erased packets); recovered rows are
     // overwritten by the recovery, which runs after it
-    ca.zero_lost = 0;
+    ca.zero_lost = zero_lost ? 1 : 0;
     ca.out = d_out;
     ca.out_len = d_outlen;
     ca.L = g.L;
@@ -636,6 +636,20 @@ int launch_decode(fec_codec* c, const uint8_t* d_cw, const uint8_t* d_er, int64_
     HIP_TRY(hipEventRecord(c->ev_fork, s));
     HIP_TRY(hipStreamWaitEvent(c->side, c->ev_fork, 0));
     if (int st = launch_plan(c, d_er, P, d_ws, ws_bytes, c->side)) return st;
+    static const bool beside = [] {
+        const char* v = std::getenv("FEC_REC_BESIDE");
+        return v && std::atoi(v) != 0;
+    }();
+    if (beside && c->copy_fast && c->copy_path != 1 && (reinterpret_cast<uintptr_t>(d_out) & 3) == 0) {
+        // experiment: the recovery on the side stream, beside the copy; the copy leaves the erased
+        // rows alone and the compaction writes the lost ones (zero rows, length 0)
+        if (int st = launch_compact(c, P, d_out, d_outlen, d_ws, ws_bytes, c->side, 0, true)) return st;
+        if (int st = launch_recover(c, d_cw, P, d_out, d_outlen, d_ws, ws_bytes, c->side, 0, true)) return st;
+        HIP_TRY(hipEventRecord(c->ev_join, c->side));
+        if (int st = launch_copy(c, d_cw, d_er, P, d_out, d_outlen, s, true)) return st;
+        HIP_TRY(hipStreamWaitEvent(s, c->ev_join, 0));
+        return FEC_OK;
+    }
     if (int st = launch_compact(c, P, d_out, d_outlen, d_ws, ws_bytes, c->side)) return st;
     HIP_TRY(hipEventRecord(c->ev_join, c->side));
     // The copy writes every row (erased ones as zero rows, length 0); the recovery overwrites the

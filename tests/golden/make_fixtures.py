@@ -100,7 +100,36 @@ def parse_adaptive_logs(ref: str) -> None:
                     "udp_matches_pattern": int(round(float(udp[-1]) * 360000)) == int(raw[:360000].sum()),
                     "coding_rates": [float(x) for x in rate]})
     with open(os.path.join(HERE, "published_adaptive_logs.json"), "w") as f:
-        json.dump({"packets": 360000, "runs": out}, f, indent=1)
+        json.dump({"packets": 360000, "runs": out, "mds": parse_adaptive_mds_log(ref)}, f, indent=1)
+
+
+def parse_adaptive_mds_log(ref: str) -> dict:
+    """Experimental_Logs/Logs/Adaptive_MDS/adaptive_{receiver,sender}_MDS_50.odt (ADAPTIVE_MODE_MDS
+    runs; the .odt is a zip whose content.xml holds the terminal text): final FEC / UDP loss rates,
+    the final coding rate and every (T,B,N) the sender announced.  The pattern is the one whose
+    erasure count equals the UDP loss."""
+    import html
+    import zipfile
+
+    def text(name):
+        x = zipfile.ZipFile(os.path.join(ref, "Experimental_Logs/Logs/Adaptive_MDS", name)).read("content.xml").decode()
+        x = re.sub(r"<text:tab/>", "\t", x)
+        x = re.sub(r"</text:p>", "\n", x)
+        return html.unescape(re.sub(r"<[^>]+>", "", x))
+    rx, tx = text("adaptive_receiver_MDS_50.odt"), text("adaptive_sender_MDS_50.odt")
+    fec = float(re.findall(r"Final FEC loss rate = ([0-9.e-]+)", rx)[-1])
+    udp = float(re.findall(r"Final UDP loss rate = ([0-9.e-]+)", rx)[-1])
+    rate = float(re.findall(r"Final coding rate = ([0-9.e-]+)", tx)[-1])
+    tuples = sorted({tuple(int(v) for v in m) for m in re.findall(r"\(T,B,N\)=\((\d+),(\d+),(\d+)\)", tx)})
+    pattern = None
+    for pct in range(10, 101, 10):
+        raw = np.fromfile(os.path.join(ref, f"Experimental_Logs/erasure{pct}.bin"), dtype=np.uint8)
+        if int(raw[:360000].sum()) == int(round(udp * 360000)):
+            pattern = f"erasure{pct}"
+    return {"receiver_log": "Experimental_Logs/Logs/Adaptive_MDS/adaptive_receiver_MDS_50.odt",
+            "sender_log": "Experimental_Logs/Logs/Adaptive_MDS/adaptive_sender_MDS_50.odt",
+            "pattern": pattern, "fec_loss_rate": fec, "udp_loss_rate": udp,
+            "lost_packets": int(round(fec * 360000)), "coding_rate": rate, "tuples": [list(t) for t in tuples]}
 
 
 def oracle_vectors() -> None:

@@ -86,6 +86,30 @@ def test_published_adaptive_logs_are_not_the_current_code():
     assert r10["lost_packets"] == 250 and v.lost == 261
 
 
+def test_oracle_vr_loop_mds_mode_equals_plan():
+    """ADAPTIVE_MODE_MDS (make_MDS_estimates on): the oracle's byte-level P2P loop and the plan on a
+    40000-packet prefix of erasure50, per packet."""
+    pat = load_pattern("erasure50")
+    r = oracle.vr_run(pat, 40000, mds=True)
+    v = VrPlan(pat, 40000, adaptive_mode_MDS=True)
+    assert ((r["out_len"] == 0) == (v.fate == 3)).all() and r["lost"] == v.lost
+    assert r["switches"] == v.switches and r["sent"] == v.sent and abs(r["coding_rate"] - v.coding_rate) < 1e-6
+
+
+def test_published_adaptive_mds_log_is_not_the_current_code():
+    """Experimental_Logs/Logs/Adaptive_MDS (adaptive_{receiver,sender}_MDS_50.odt): its UDP losses are
+    erasure50's erasures, but its sender announced tuples with N < B ((10,2,1), (10,10,1), ...),
+    which the current Parameter_Estimator::make_MDS_estimates (Parameter_Estimator.cpp:209-221:
+    B_current = N_current) never produces -- the run predates it, like the adaptive logs.  The
+    current code on the same pattern: every tuple (10,b,b), 2478 lost against the log's 2822."""
+    log = load_json("published_adaptive_logs.json")["mds"]
+    assert log["pattern"] == "erasure50" and log["lost_packets"] == 2822
+    assert any(b != n for _, b, n in log["tuples"])
+    v = VrPlan(load_pattern("erasure50"), 360000, adaptive_mode_MDS=True)
+    assert all(b == n for _, b, n in v.tuples())
+    assert v.lost == 2478 and v.fate.min() >= 1
+
+
 def test_schedule_structure(adaptive):
     v = adaptive
     enc, dec, fr = v.encoders, v.decoders, v.frames
