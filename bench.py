@@ -481,8 +481,9 @@ def main():
                     help="untimed replays of the step for this much wall time before the W warm-up "
                          "steps: a fresh box's clocks (and the new buffers) need >100 steps to settle "
                          "(20 timed steps after 5 warm-up: 0.400 ms/step, after 100: 0.355)")
-    ap.add_argument("--no-graph", action="store_true",
-                    help="launch the step's kernels one by one instead of replaying a captured hipGraph")
+    ap.add_argument("--graph", action="store_true",
+                    help="replay the step as a captured hipGraph instead of launching its kernels one by one")
+    ap.add_argument("--no-graph", action="store_true", help="(the default) eager launches")
     ap.add_argument("--launch-selftest", action="store_true",
                     help="CPU test of the --gpus launcher: ranks rendezvous over gloo, no GPU work")
     args = ap.parse_args()
@@ -546,10 +547,14 @@ def main():
         if world > 1:
             dist.barrier()
 
-    # The step (encode; fork; plan on the codec's side stream | copy; join; recover: 9 kernels and
-    # 2 memsets) is captured once into a hipGraph and replayed: one launch per step instead of 11.
+    # The step (encode; fork; plan on the codec's side stream | copy; join; recover: 6 kernels and
+    # 3 memsets) is launched eagerly: the kernels queue ahead of the GPU, and on a replayed hipGraph
+    # of the same step the copy waits for the side stream's first memset and the recovery starts
+    # later after the copy (0.3208 / 0.3210 / 0.3199 ms graph vs 0.3159 / 0.3127 / 0.3145 ms eager
+    # at 20 / 20 / 100 steps, alternating processes on one box: tools/graph_ab.sh,
+    # profiles/r03/r03y_graph_ab.txt).  --graph replays the captured step instead.
     run = step
-    if not args.no_graph:
+    if args.graph:
         side = torch.cuda.Stream()
         side.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(side):
@@ -652,7 +657,7 @@ def main():
                        "codeword_bytes": codec.CW, "packets_per_gpu": P,
                        "parallelism": f"streams{world} (one independent stream per GPU)"},
             "verified": bool(verified_all == world),
-            "step_launch": "hipGraph replay" if not args.no_graph else "eager launches",
+            "step_launch": "hipGraph replay" if args.graph else "eager launches",
             "device_warmup": {"seconds": args.warm_seconds, "untimed_steps": warm_steps,
                               "note": "untimed replays of the same step before the W warm-up steps "
                                       "(clock / first-touch settling); the timed K steps are unchanged"},

@@ -636,26 +636,12 @@ int launch_decode(fec_codec* c, const uint8_t* d_cw, const uint8_t* d_er, int64_
     HIP_TRY(hipEventRecord(c->ev_fork, s));
     HIP_TRY(hipStreamWaitEvent(c->side, c->ev_fork, 0));
     if (int st = launch_plan(c, d_er, P, d_ws, ws_bytes, c->side)) return st;
-    static const bool beside = [] {
-        const char* v = std::getenv("FEC_REC_BESIDE");
-        return v && std::atoi(v) != 0;
-    }();
-    if (beside && c->copy_fast && c->copy_path != 1 && (reinterpret_cast<uintptr_t>(d_out) & 3) == 0) {
-        // experiment: the recovery on the side stream, beside the copy; the copy leaves the erased
-        // rows alone and the compaction writes the lost ones (zero rows, length 0)
-        if (int st = launch_compact(c, P, d_out, d_outlen, d_ws, ws_bytes, c->side, 0, true)) return st;
-        if (int st = launch_recover(c, d_cw, P, d_out, d_outlen, d_ws, ws_bytes, c->side, 0, true)) return st;
-        HIP_TRY(hipEventRecord(c->ev_join, c->side));
-        if (int st = launch_copy(c, d_cw, d_er, P, d_out, d_outlen, s, true)) return st;
-        HIP_TRY(hipStreamWaitEvent(s, c->ev_join, 0));
-        return FEC_OK;
-    }
     if (int st = launch_compact(c, P, d_out, d_outlen, d_ws, ws_bytes, c->side)) return st;
     HIP_TRY(hipEventRecord(c->ev_join, c->side));
     // The copy writes every row (erased ones as zero rows, length 0); the recovery overwrites the
-    // recovered ones after the join.  Round 2 and 3 measured the alternatives slower in the step
-    // (a copy that leaves erased rows to a recovery running beside it; the plan beside the
-    // encoder; profiles/r02/decode_diag, tools/step_overlap2.py).
+    // recovered ones after the join.  Rounds 2 and 3 measured the alternatives slower in the step
+    // (a copy that leaves erased rows to a recovery running beside it: 0.3198 vs 0.3162 ms,
+    // profiles/r03/r03y_recover_beside_ab.txt; the plan beside the encoder; profiles/r02/decode_diag).
     if (int st = launch_copy(c, d_cw, d_er, P, d_out, d_outlen, s)) return st;
     HIP_TRY(hipStreamWaitEvent(s, c->ev_join, 0));
     return launch_recover(c, d_cw, P, d_out, d_outlen, d_ws, ws_bytes, s, 0, true);

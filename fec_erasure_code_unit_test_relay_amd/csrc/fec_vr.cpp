@@ -300,12 +300,11 @@ void VrPlan::decode_instance(const DecJob& job, std::vector<RecEntry>& recs) {
 //   * r_c <= s < r_{c+1} (c >= 2): the background one created at swap c-1, fed (r_{c-1}, s];
 // where r_c, the c-th swap, is the first received packet s >= max(100c, r_{c-1} + 1)
 // (`seq + 1 > cycle * 100`, one swap per received packet).  So the feedback splits into
-// independent jobs, one per swap, run here on worker threads; within a job, erasure-free
-// stretches at the estimator's fixed point are skipped to the next drop (estimate() would change
-// only previous_win_end there).  Output: fb_changes, the received packets at which the feedback
-// differs from the one before (the value before the first received packet is 0,0,0).
-void VrPlan::feedback(int T, bool mds, int64_t end) {
-    fb_changes.clear();
+// independent jobs, one per swap; within a job, erasure-free stretches at the estimator's fixed
+// point are skipped to the next drop (estimate() would change only previous_win_end there).  The
+// jobs run in order on a producer thread while the control loop consumes their results (FbCursor):
+// job j's list of (received seq, value) changes is published once complete.
+void VrPlan::feedback_plan(int64_t end) {
     auto next_received = [&](int64_t s) {  // first received seq >= s
         auto it = std::lower_bound(drops.begin(), drops.end(), s);
         while (it != drops.end() && *it == s) {
@@ -314,85 +313,121 @@ void VrPlan::feedback(int T, bool mds, int64_t end) {
         }
         return s;
     };
-    std::vector<int64_t> r{-1, -1};  // r[c] = c-th swap (c >= 1); r[0] unused
+    fb_swaps_.assign({-1, -1});  // [c] = c-th swap (c >= 1); [0] unused
     for (int64_t c = 1;; ++c) {
-        const int64_t s = next_received(std::max(c * kEstimationCycle, r.back() + 1));
+        const int64_t s = next_received(std::max(c * kEstimationCycle, fb_swaps_.back() + 1));
         if (s >= end) break;
-        if (c == 1) r[1] = s; else r.push_back(s);
+        if (c == 1) fb_swaps_[1] = s; else fb_swaps_.push_back(s);
     }
-    const int64_t nswap = r[1] < 0 ? 0 : static_cast<int64_t>(r.size()) - 1;  // swaps r[1..nswap]
-    auto swap_at = [&](int64_t c) { return c <= nswap ? r[static_cast<size_t>(c)] : end; };
-    // job 0: the initial estimator over [0, r_2); job c >= 2: fresh one fed from r_{c-1}+1,
-    // recording [r_c, r_{c+1})
+    const int64_t nswap = fb_swaps_[1] < 0 ? 0 : static_cast<int64_t>(fb_swaps_.size()) - 1;
+    auto swap_at = [&](int64_t c) { return c <= nswap ? fb_swaps_[static_cast<size_t>(c)] : end; };
+    // job 0: the initial estimator over [0, r_2); job j >= 1 (swap c = j + 1): a fresh one fed
+    // from r_{c-1}+1, recording [r_c, r_{c+1})
     const int64_t njobs = 1 + std::max<int64_t>(0, nswap - 1);
-    std::vector<std::vector<FbChange>> out(static_cast<size_t>(njobs));
-    auto job = [&](int64_t j) {
-        const bool init = j == 0;
-        const int64_t c = j + 1;                        // job j >= 1 is swap c = j + 1
-        ParameterEstimator e(kTTot, init ? mds : false);
-        const int64_t from = init ? 0 : swap_at(c - 1) + 1;
-        const int64_t rec = init ? 0 : swap_at(c);      // first seq whose feedback it gives
-        const int64_t to = init ? swap_at(2) : swap_at(c + 1);
-        std::vector<FbChange>& o = out[static_cast<size_t>(j)];
+    fb_jobs_.resize(static_cast<size_t>(njobs));
+    for (int64_t j = 0; j < njobs; ++j) {
+        FbJob& b = fb_jobs_[static_cast<size_t>(j)];
+        const int64_t c = j + 1;
+        b.from = j == 0 ? 0 : swap_at(c - 1) + 1;
+        b.rec = j == 0 ? 0 : swap_at(c);
+        b.to = j == 0 ? swap_at(2) : swap_at(c + 1);
+        b.changes.clear();
+    }
+    fb_done_.store(0, std::memory_order_relaxed);
+}
+
+void VrPlan::feedback_run(int T, bool mds) {
+    const int64_t njobs = static_cast<int64_t>(fb_jobs_.size());
+    for (int64_t j = 0; j < njobs; ++j) {
+        FbJob& b = fb_jobs_[static_cast<size_t>(j)];
+        ParameterEstimator e(kTTot, j == 0 ? mds : false);
         uint32_t last = 0xffffffffu;
-        auto di = std::lower_bound(drops.begin(), drops.end(), from);
-        for (int64_t s = from; s < to;) {
+        auto di = std::lower_bound(drops.begin(), drops.end(), b.from);
+        auto put = [&](int64_t s) {
+            const uint32_t v = uint32_t(e.T) | uint32_t(e.B_current) << 8 | uint32_t(e.N_current) << 16;
+            if (v != last) {
+                b.changes.push_back(FbChange{s, v});
+                last = v;
+            }
+        };
+        for (int64_t s = b.from; s < b.to;) {
             if (di != drops.end() && *di == s) {  // dropped: nothing reaches the receiver
                 ++di;
                 ++s;
                 continue;
             }
-            const int64_t nd = di != drops.end() ? std::min(*di, to) : to;
+            const int64_t nd = di != drops.end() ? std::min(*di, b.to) : b.to;
             if (e.steady(s, T)) {  // every received packet of [s, nd) leaves the estimator as it is
-                if (s >= rec || nd > rec) {
-                    const uint32_t v = uint32_t(e.T) | uint32_t(e.B_current) << 8 | uint32_t(e.N_current) << 16;
-                    if (v != last) {
-                        o.push_back(FbChange{std::max(s, rec), v});
-                        last = v;
-                    }
-                }
+                if (nd > b.rec) put(std::max(s, b.rec));
                 e.previous_win_end = nd - 1;
                 s = nd;
                 continue;
             }
             e.estimate(s, T);
-            if (s >= rec) {
-                const uint32_t v = uint32_t(e.T) | uint32_t(e.B_current) << 8 | uint32_t(e.N_current) << 16;
-                if (v != last) {
-                    o.push_back(FbChange{s, v});
-                    last = v;
-                }
-            }
+            if (s >= b.rec) put(s);
             ++s;
         }
-    };
-    const unsigned hw = std::thread::hardware_concurrency();
-    size_t nth = std::max<size_t>(1, std::min<size_t>({static_cast<size_t>(njobs) / 64 + 1, hw ? hw : 1u, 8u}));
-    if (const char* ev = std::getenv("FEC_VR_THREADS")) nth = std::max(1, std::atoi(ev));
-    if (nth <= 1) {
-        for (int64_t j = 0; j < njobs; ++j) job(j);
-    } else {
-        std::atomic<int64_t> next{0};
-        std::vector<std::thread> pool;
-        for (size_t w = 0; w < nth; ++w)
-            pool.emplace_back([&] {
-                for (int64_t j; (j = next.fetch_add(1)) < njobs;) job(j);
-            });
-        for (auto& th : pool) th.join();
+        fb_done_.store(j + 1, std::memory_order_release);
     }
-    uint32_t cur = 0;
-    for (const auto& o : out)
-        for (const FbChange& f : o)
-            if (f.v != cur) {
-                fb_changes.push_back(f);
-                cur = f.v;
-            }
 }
+
+// The control loop's view of the feedback stream: value(s) = the feedback after received packet s
+// (packets in increasing order), next() = the first change after the last value() asked for, or
+// the end of what the producer has published so far.
+struct VrPlan::FbCursor {
+    VrPlan& p;
+    size_t j = 0, e = 0;
+    uint32_t cur = 0;
+    size_t changes = 0;
+    explicit FbCursor(VrPlan& plan) : p(plan) {}
+    bool ready(size_t job) const {
+        return static_cast<int64_t>(job) < p.fb_done_.load(std::memory_order_acquire);
+    }
+    void wait(size_t job) const {
+        while (!ready(job)) std::this_thread::yield();
+    }
+    // skip to the next entry that changes the value; false at the end of the published jobs
+    bool peek(int64_t* seq, bool block) {
+        for (;;) {
+            if (j >= p.fb_jobs_.size()) return false;
+            if (!ready(j)) {
+                if (!block) return false;
+                wait(j);
+            }
+            const auto& ch = p.fb_jobs_[j].changes;
+            if (e >= ch.size()) {
+                ++j;
+                e = 0;
+                continue;
+            }
+            if (ch[e].v == cur) {
+                ++e;
+                continue;
+            }
+            *seq = ch[e].seq;
+            return true;
+        }
+    }
+    uint32_t value(int64_t s) {
+        int64_t q;
+        while (peek(&q, true) && q <= s) {
+            cur = p.fb_jobs_[j].changes[e++].v;
+            ++changes;
+        }
+        return cur;
+    }
+    // first seq >= s at which the value may change (a bound when the producer is behind)
+    int64_t next(int64_t s) {
+        int64_t q;
+        if (peek(&q, false)) return q;
+        if (j >= p.fb_jobs_.size()) return INT64_MAX;
+        return std::max(s, p.fb_jobs_[j].rec);  // the first seq of the job not yet published
+    }
+};
 
 void VrPlan::control(const uint8_t* pattern, int64_t n_pattern, int T, int B, int N, bool mds) {
     frame_runs.clear();
     rate_runs.clear();
-    fb_changes.clear();
     drops.clear();
     enc.clear();
     dec.clear();
@@ -424,10 +459,15 @@ void VrPlan::control(const uint8_t* pattern, int64_t n_pattern, int T, int B, in
         q = static_cast<const uint8_t*>(hit) - pattern;
         drops.push_back(q++);
     }
-    feedback(T, mds, P + T + 1);
+    feedback_plan(P + T + 1);
+    std::thread fb_thread([this, T, mds] { feedback_run(T, mds); });
+    struct Joiner {
+        std::thread& t;
+        ~Joiner() { t.join(); }
+    } fb_join{fb_thread};
+    FbCursor fb(*this);
     const auto tc1 = std::chrono::steady_clock::now();
     start_workers();
-    size_t fi = 0;        // next feedback change
     size_t dri = 0;       // next drop
     uint8_t udp[12] = {};
     // ---- Variable_Rate_FEC_Decoder (Variable_Rate_FEC_Decoder.cpp:25-80, 2133-2400, 2440-2514) ----
@@ -510,7 +550,7 @@ void VrPlan::control(const uint8_t* pattern, int64_t n_pattern, int T, int B, in
             if (!would_switch && udp[3] == eT && udp[4] == eB && udp[5] == eN) {
                 while (dri < drops.size() && drops[dri] < seq) ++dri;
                 const int64_t next_drop = dri < drops.size() ? drops[dri] : INT64_MAX;
-                const int64_t next_fb = fi < fb_changes.size() ? fb_changes[fi].seq : INT64_MAX;
+                const int64_t next_fb = fb.next(seq);
                 const int64_t end = std::min({next_drop, next_fb, P + T - 1});
                 if (end > seq) {
                     if (adaptive && udp[0] != 0) {
@@ -604,8 +644,7 @@ void VrPlan::control(const uint8_t* pattern, int64_t n_pattern, int T, int B, in
 
         // ---- Application_Layer_Receiver::receive_message_and_decode ----
         if (drop) continue;  // artificial erasure: returns -1, feedback unchanged
-        uint32_t fbv = fi > 0 ? fb_changes[fi - 1].v : 0u;  // the estimators' feedback after seq
-        while (fi < fb_changes.size() && fb_changes[fi].seq <= seq) fbv = fb_changes[fi++].v;
+        const uint32_t fbv = fb.value(seq);  // the estimators' feedback after seq
         // ---- Variable_Rate_FEC_Decoder::decode ----
         if (seq_start == -1) {  // initialize_decoder (:2478-2494)
             seq_start = 0;
@@ -669,8 +708,8 @@ void VrPlan::control(const uint8_t* pattern, int64_t n_pattern, int T, int B, in
     for (int64_t s : drops) erased[static_cast<size_t>(s)] = 1;
     if (std::getenv("FEC_VR_DEBUG")) {
         const auto tc2 = std::chrono::steady_clock::now();
-        std::fprintf(stderr, "vr control: drops+feedback %.3f ms (%zu changes), loop %.3f ms\n",
-                     std::chrono::duration<double, std::milli>(tc1 - tc0).count(), fb_changes.size(),
+        std::fprintf(stderr, "vr control: drops %.3f ms, loop %.3f ms (%zu feedback changes)\n",
+                     std::chrono::duration<double, std::milli>(tc1 - tc0).count(), fb.changes,
                      std::chrono::duration<double, std::milli>(tc2 - tc1).count());
     }
     // the last two decoder instances, then the coding-rate sum; no more jobs

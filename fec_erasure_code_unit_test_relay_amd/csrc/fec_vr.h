@@ -18,6 +18,7 @@
 #pragma once
 
 #include <array>
+#include <atomic>
 #include <chrono>
 #include <condition_variable>
 #include <deque>
@@ -113,11 +114,6 @@ struct VrPlan {
     int64_t sent = 0;                 // packets the sender produced (>= P + T)
     std::vector<uint8_t> erased;      // [sent]: dropped before the receiver (Application_Layer_Receiver.cpp:352-360)
     std::vector<int64_t> drops;       // the seqs with erased == 1, increasing
-    struct FbChange {      // the receiver's feedback (T | B_est << 8 | N_est << 16) from received seq on
-        int64_t seq;
-        uint32_t v;
-    };
-    std::vector<FbChange> fb_changes;
     std::vector<FrameRun> frame_runs; // frames of [0, sent), run-length coded
     std::vector<RateRun> rate_runs;
     std::vector<VrInstance> enc, dec;
@@ -161,7 +157,20 @@ private:
         std::array<uint8_t, kVrCoefStride> coef;
     };
     void control(const uint8_t* pattern, int64_t n_pattern, int T, int B, int N, bool mds);
-    void feedback(int T, bool mds, int64_t end);
+    struct FbChange {      // the receiver's feedback (T | B_est << 8 | N_est << 16) from received seq on
+        int64_t seq;
+        uint32_t v;
+    };
+    struct FbJob {         // one estimator's stretch: fed from `from`, its feedback for [rec, to)
+        int64_t from = 0, rec = 0, to = 0;
+        std::vector<FbChange> changes;
+    };
+    struct FbCursor;
+    void feedback_plan(int64_t end);
+    void feedback_run(int T, bool mds);
+    std::vector<int64_t> fb_swaps_;
+    std::vector<FbJob> fb_jobs_;
+    std::atomic<int64_t> fb_done_{0};   // jobs published by the producer thread
     void start_workers();
     void publish(DecJob&& j, bool flush = false);
     void close_jobs();

@@ -9,7 +9,7 @@ OUT=$R/gpurun_out/$TAG
 mkdir -p $OUT
 B="--no-cpu-baseline --no-host-inclusive --no-extra-configs $*"
 i=0
-for a in "" "--no-graph" "" "--no-graph" "--steps 100" "--no-graph --steps 100"; do
+for a in "--graph" "" "--graph" "" "--graph --steps 100" "--steps 100"; do
     i=$((i + 1))
     timeout -k 10 120 python -u $R/bench.py $B $a > $OUT/run$i.json 2> $OUT/run$i.err || { echo "bench failed: $a"; tail -20 $OUT/run$i.err; exit 1; }
     python3 - "$OUT/run$i.json" "$a" <<'EOF'
