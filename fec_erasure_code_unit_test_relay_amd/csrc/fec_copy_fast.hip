@@ -13,7 +13,7 @@
 namespace fec {
 
 template <int K, int NP>
-__global__ __launch_bounds__(256) void fec_copy_fast_kernel(CopyFastArgs a) {
+__global__ __launch_bounds__(512) void fec_copy_fast_kernel(CopyFastArgs a) {
     constexpr int n = K + NP;
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     uint8_t* raw = smem;                           // codeword tile (+ slack)
@@ -21,7 +21,7 @@ __global__ __launch_bounds__(256) void fec_copy_fast_kernel(CopyFastArgs a) {
     int32_t* clen = reinterpret_cast<int32_t*>(xo + a.out_bytes);  // bytes to copy per packet
     uint8_t* erw = reinterpret_cast<uint8_t*>(clen + a.TP);         // erasure flags [x0, x0+TP+T)
 
-    const int tid = threadIdx.x;
+    const int tid = threadIdx.x, NT = blockDim.x;
     phase_stamp(a.stamps, blockIdx.x, 0);
     const int L = a.L, CW = a.CW, NS4 = a.NS4, T = a.T;
     const int64_t x0 = static_cast<int64_t>(blockIdx.x) * a.TP;
@@ -30,14 +30,14 @@ __global__ __launch_bounds__(256) void fec_copy_fast_kernel(CopyFastArgs a) {
     const uint8_t* gA = a.cw + x0 * CW;
     const int delta = static_cast<int>(reinterpret_cast<uintptr_t>(gA) & 15);
     if (a.nt)
-        stage_to_lds<8, true>(raw, gA - delta, delta, delta + ntile * CW, tid, 256);
+        stage_to_lds<8, true>(raw, gA - delta, delta, delta + ntile * CW, tid, NT);
     else
-        stage_to_lds<8>(raw, gA - delta, delta, delta + ntile * CW, tid, 256);
-    for (int i = tid; i < ntile + T; i += 256) erw[i] = a.er[x0 + i];  // x0+ntile+T-1 < P
+        stage_to_lds<8>(raw, gA - delta, delta, delta + ntile * CW, tid, NT);
+    for (int i = tid; i < ntile + T; i += NT) erw[i] = a.er[x0 + i];  // x0+ntile+T-1 < P
     __syncthreads();
     phase_stamp(a.stamps, blockIdx.x, 1);
 
-    for (int t = tid; t < ntile; t += 256) {
+    for (int t = tid; t < ntile; t += NT) {
         int ln = 0, copy = 0;
         if (!erw[t]) {
             const uint8_t* row = raw + delta + t * CW;
@@ -53,7 +53,7 @@ __global__ __launch_bounds__(256) void fec_copy_fast_kernel(CopyFastArgs a) {
     }
     __syncthreads();
 
-    for (int it = tid; it < ntile * NS4; it += 256) {
+    for (int it = tid; it < ntile * NS4; it += NT) {
         const int g = it / ntile;
         const int t = it - g * ntile;
         const int cl = clen[t];
@@ -109,7 +109,7 @@ __global__ __launch_bounds__(256) void fec_copy_fast_kernel(CopyFastArgs a) {
     uint8_t* dst = a.out + x0 * L;
     const bool skip = a.skip_erased != 0;
     if ((obytes & 15) == 0 && (reinterpret_cast<uintptr_t>(dst) & 15) == 0) {
-        for (int o = tid * 16; o < obytes; o += 256 * 16) {
+        for (int o = tid * 16; o < obytes; o += NT * 16) {
             if (!skip || (!erw[o / L] && !erw[(o + 15) / L])) {
                 const uint4 v = *reinterpret_cast<const uint4*>(xo + o);
                 if (a.nt)
@@ -124,7 +124,7 @@ __global__ __launch_bounds__(256) void fec_copy_fast_kernel(CopyFastArgs a) {
             }
         }
     } else {
-        for (int o = tid * 4; o < obytes; o += 256 * 4)
+        for (int o = tid * 4; o < obytes; o += NT * 4)
             if (!skip || !erw[o / L])
                 *reinterpret_cast<uint32_t*>(dst + o) = *reinterpret_cast<const uint32_t*>(xo + o);
     }

@@ -200,7 +200,27 @@ __device__ __forceinline__ void tile_walk(const EncTileArgs& a, uint8_t* smem) {
     const int lane = threadIdx.x & 63;
     const int tid = threadIdx.x;
     const int L = CL ? LC : a.L, CW = CL ? CG.CW : a.CW, NS4 = CL ? CG.NS4 : a.NS4;
-    const int PPW = CL ? CG.PPW : a.PPW, R = 4 * PPW, P = a.P;
+    const int PPW = CL ? CG.PPW : a.PPW, R = 4 * PPW;
+    // Segment mode (a.seg, the variable-rate schedule): this workgroup encodes tiles [t0, t0+cnt)
+    // of one encoder instance -- a fresh encoder over the payload rows [sfirst, sfirst+P) -- and
+    // writes row t to the frames' array of its role (cur before the role switch, old after) at
+    // row sfirst+t, stride a.W.
+    const bool segm = a.seg != nullptr;
+    int P = a.P;
+    int64_t sfirst = 0, ssw = 0;
+    int seg_t0 = 0, seg_cnt = 0;
+    if (segm) {
+        const int64_t* sg = a.seg + 4 * blockIdx.x;
+        sfirst = sg[0];
+        ssw = sg[1];
+        P = static_cast<int>(sg[2]);
+        seg_t0 = static_cast<int>(sg[3] & 0xffffffff);
+        seg_cnt = static_cast<int>(sg[3] >> 32);
+    }
+    const uint8_t* pay_base = segm ? a.payload_base + sfirst * (CL ? LC : a.L) : a.payload_base;
+    const int pay_bytes = segm ? P * (CL ? LC : a.L) : a.payload_bytes;
+    const int32_t* len_base = segm ? (a.len_base ? a.len_base + sfirst : nullptr) : a.len_base;
+    const int len_bytes = segm ? 4 * P : a.len_bytes;
     const int dbg = CL ? 0 : a.dbg;  // timing experiments: the runtime-L kernel only
     const int nvl = CL ? CG.nvl : a.nvl, rem = CL ? CG.rem : a.rem;
     const int off_in = CL ? CG.off_in : a.off_in, in_bytes = CL ? CG.in_bytes : a.in_bytes;
@@ -238,21 +258,21 @@ __device__ __forceinline__ void tile_walk(const EncTileArgs& a, uint8_t* smem) {
     });
 
     const __amdgpu_buffer_rsrc_t rs =
-        __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(a.payload_base), 0, a.payload_bytes, 0x00020000);
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(pay_base), 0, pay_bytes, 0x00020000);
     const __amdgpu_buffer_rsrc_t rc = __builtin_amdgcn_make_buffer_rsrc(a.cw, 0, a.cw_bytes, 0x00020000);
     const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc(a.cw_len, 0, 4 * P, 0x00020000);
-    const bool has_len = a.len_base != nullptr;
+    const bool has_len = len_base != nullptr;
 
-    const int first = blockIdx.x * a.tiles_per_wg;
-    const int cnt = min(a.tiles_per_wg, a.ntiles - first);  // real tiles of this workgroup (>= 1)
+    const int first = segm ? seg_t0 : static_cast<int>(blockIdx.x) * a.tiles_per_wg;
+    const int cnt = segm ? seg_cnt : min(a.tiles_per_wg, a.ntiles - first);  // real tiles of this workgroup (>= 1)
     const int ngl = CL ? CG.ngl : a.ngl;                     // payload LDS-DMA instructions per wave per tile
     const int nglt = ngl + (has_len ? 1 : 0);
     const int nso = CL ? CG.nso : a.nso;                     // 16-byte stores per thread per tile
     const int ns = nso + 1;                                  // + the trimmed-size store
 
     // tile it (0 = the tile in front of the first one) -> LDS input buffer (it & 1)
-    const tv4u rs4 = raw_rsrc(a.payload_base, a.payload_bytes);
-    const tv4u rl4 = raw_rsrc(a.len_base, a.len_bytes);
+    const tv4u rs4 = raw_rsrc(pay_base, pay_bytes);
+    const tv4u rl4 = raw_rsrc(len_base, len_bytes);
     const uint32_t lds_in = lds_addr(smem + off_in), lds_len = lds_addr(smem + off_len);
     // LDS image of a tile: row p at p*RS (RS = L rounded up to 16 bytes), so that every row starts
     // 16-byte aligned; the DMA's destination is lane-linear, its per-lane source picks the row
@@ -473,7 +493,45 @@ __device__ __forceinline__ void tile_walk(const EncTileArgs& a, uint8_t* smem) {
         if (it == 0) continue;
 
         // ---- D: output tile -> HBM (16-byte chunks); trimmed sizes
-        {
+        if (segm) {
+            // row by row into the frames' arrays (stride W, a multiple of 16): chunk c of row p is
+            // LDS bytes [p*CW + 16c, +16), the bytes past the codeword zeroed
+            const int nch = (CW + 15) >> 4;
+            typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+            for (int q = tid; q < R * nch; q += kTileThreads) {
+                const int p = q / nch, c = q - p * nch;
+                const int t = row0 + p;
+                if (t >= P) continue;
+                const int64_t seqg = sfirst + t;
+                const int lb = p * CW + 16 * c;
+                const uint32_t* lw = reinterpret_cast<const uint32_t*>(out + (lb & ~3));
+                const int sh = lb & 3;
+                uint32_t d5[5];
+#pragma unroll
+                for (int m = 0; m < 5; ++m) d5[m] = lw[m];
+                const int left = CW - 16 * c;  // valid bytes of this chunk (> 0)
+                v4u vv;
+#pragma unroll
+                for (int m = 0; m < 4; ++m) vv[m] = __builtin_amdgcn_alignbyte(d5[m + 1], d5[m], sh) & keep_bytes(left - 4 * m);
+                uint8_t* dst = (seqg >= ssw ? a.old_rows : a.cur_rows) + seqg * a.W + 16 * c;
+                *reinterpret_cast<v4u*>(dst) = vv;
+            }
+            const bool own = tid < R && row0 + tid < P;
+            const uint8_t* cwp = out + (own ? tid : 0) * CW;
+            int sz = CW;
+            if (own && cwp[CW - 1] == 0) {  // rare: a codeword ending in zero bytes
+                sz = 0;
+                for (int b = CW - 2; b >= 0; --b)
+                    if (cwp[b] != 0) {
+                        sz = b + 1;
+                        break;
+                    }
+            }
+            if (own) {
+                const int64_t seqg = sfirst + row0 + tid;
+                (seqg >= ssw ? a.old_len : a.cur_len)[seqg] = sz;
+            }
+        } else {
             const int gbase = row0 * CW;  // 16-byte aligned
             const int lim = P * CW - gbase;
             const int tb = R * CW;

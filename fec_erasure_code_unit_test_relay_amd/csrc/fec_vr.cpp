@@ -11,10 +11,13 @@
 #include <cstdlib>
 #include <cstring>
 #include <new>
+#include <mutex>
+#include <set>
 #include <stdexcept>
 #include <thread>
 
 #include "fec_amd.h"
+#include "fec_kernels.h"
 
 namespace fec {
 
@@ -828,6 +831,22 @@ struct fec_vr_plan {
     const int32_t* d_hdr = nullptr;    // [sent][4]: frame header T, B, N, counter
     int64_t enc_total = 0;             // codewords of all encoder instances
     int enc_tab = 0, enc_out = 0, enc_slot = 0, enc_wave = 0;  // fec_vr_encode_kernel's LDS layout
+    // the same instances without the ones the tile encoder takes (tuples with a tile geometry)
+    const int32_t* d_lo_inst = nullptr;
+    const int64_t* d_lo_span = nullptr;
+    const int64_t* d_lo_cum = nullptr;
+    int n_lo = 0;
+    int64_t lo_total = 0;
+    // per tuple with a tile geometry: one launch of fec_encode_tile_kernel<k, n-k> in segment mode
+    struct TileTuple {
+        const void* kfn;
+        fec::TileGeom tg;
+        int toff;        // dword offset of its gf_mul4 tables in gtab
+        size_t seg0;     // its first segment in d_seg
+        int nseg;
+    };
+    std::vector<TileTuple> tiles;
+    const int64_t* d_seg = nullptr;
     bool enc_ready = false, dec_ready = false, hdr_ready = false;
 
     ~fec_vr_plan() {
@@ -856,17 +875,26 @@ std::vector<uint8_t> gf_tables() {
 int cw_of(const fec::VrPlan& p, const fec::VrInstance& v) { return fec::Geometry::make(p.L, v.T, v.B, v.N).CW; }
 
 // Encode tables: per encoder instance its geometry, first call, role switch and the running
-// count of codewords; per (T,B,N) tuple the gf_mul4 register tables of G's parity columns.
+// count of codewords (every instance, and the ones the tile encoder does not take); per (T,B,N)
+// tuple the gf_mul4 register tables of G's parity columns; per tuple with a tile geometry the
+// segment list of its instances (units of at most `unit` tiles; each unit re-reads the tile in
+// front of it as parity history).
 int prepare_encode(fec_vr_plan* v, hipStream_t s) {
     if (v->enc_ready) return FEC_OK;
     const auto& p = v->plan;
     std::map<int, int> toff;  // tuple -> dword offset in gtab
+    std::map<int, int> tix;   // tuple -> index in v->tiles (-1: no tile geometry)
     std::vector<uint32_t> gtab;
-    std::vector<int32_t> inst;
-    std::vector<int64_t> span, cum{0};
+    std::vector<int32_t> inst, lo_inst;
+    std::vector<int64_t> span, cum{0}, lo_span, lo_cum{0};
+    std::vector<std::vector<int64_t>> segs;
     inst.reserve(p.enc.size() * 4);
     span.reserve(p.enc.size() * 2);
     cum.reserve(p.enc.size() + 1);
+    v->tiles.clear();
+    int unit = 4;
+    if (const char* e = std::getenv("FEC_VR_TILE_UNIT")) unit = std::max(1, std::atoi(e));
+    const bool tiles_on = !std::getenv("FEC_VR_NO_TILE");
     int tab = 32, out = 16, slot = 16, nmax = 1;
     for (const auto& e : p.enc) {
         const fec::Geometry g = fec::Geometry::make(p.L, e.T, e.B, e.N);
@@ -876,6 +904,15 @@ int prepare_encode(fec_vr_plan* v, hipStream_t s) {
             const std::vector<uint32_t> t = fec::parity_mul_tables(fec::make_generator(e.T, e.B, e.N), g.k, g.n);
             it = toff.emplace(key, static_cast<int>(gtab.size())).first;
             gtab.insert(gtab.end(), t.begin(), t.end());
+            int ti = -1;
+            const fec::TileGeom tg = fec::tile_geometry(g.k, g.n - g.k, p.L);
+            const void* kfn = fec::fec_encode_tile_kernel_for(g.k, g.n - g.k, p.L);
+            if (tiles_on && tg.ok && kfn && (p.L & 3) == 0) {
+                ti = static_cast<int>(v->tiles.size());
+                v->tiles.push_back({kfn, tg, it->second, 0, 0});
+                segs.emplace_back();
+            }
+            tix[key] = ti;
         }
         tab = std::max(tab, g.k * (g.n - g.k) * 32);
         out = std::max(out, (g.CW + 8 + 15) / 16 * 16);
@@ -884,6 +921,26 @@ int prepare_encode(fec_vr_plan* v, hipStream_t s) {
         inst.insert(inst.end(), {g.k, g.n, g.CW, it->second});
         span.insert(span.end(), {e.first, e.role_switch});
         cum.push_back(cum.back() + (e.end - e.first));
+        const int ti = tix[key];
+        if (ti >= 0) {
+            const int64_t rows = e.end - e.first, R = v->tiles[static_cast<size_t>(ti)].tg.R;
+            const int64_t nt = (rows + R - 1) / R;
+            for (int64_t t0 = 0; t0 < nt; t0 += unit) {
+                const int64_t c = std::min<int64_t>(unit, nt - t0);
+                segs[static_cast<size_t>(ti)].insert(segs[static_cast<size_t>(ti)].end(),
+                                                     {e.first, e.role_switch, rows, t0 | (c << 32)});
+            }
+        } else {
+            lo_inst.insert(lo_inst.end(), {g.k, g.n, g.CW, it->second});
+            lo_span.insert(lo_span.end(), {e.first, e.role_switch});
+            lo_cum.push_back(lo_cum.back() + (e.end - e.first));
+        }
+    }
+    std::vector<int64_t> seg;
+    for (size_t i = 0; i < v->tiles.size(); ++i) {
+        v->tiles[i].seg0 = seg.size() / 4;
+        v->tiles[i].nseg = static_cast<int>(segs[i].size() / 4);
+        seg.insert(seg.end(), segs[i].begin(), segs[i].end());
     }
     Upload& u = v->enc_up;
     if (int st = u.begin()) return st;
@@ -891,13 +948,78 @@ int prepare_encode(fec_vr_plan* v, hipStream_t s) {
     u.add(&v->d_enc_span, span);
     u.add(&v->d_enc_cum, cum);
     u.add(&v->d_gtab, gtab);
+    u.add(&v->d_lo_inst, lo_inst);
+    u.add(&v->d_lo_span, lo_span);
+    u.add(&v->d_lo_cum, lo_cum);
+    u.add(&v->d_seg, seg);
     if (int st = u.commit(s)) return st;
     v->enc_total = cum.back();
+    v->n_lo = static_cast<int>(lo_span.size() / 2);
+    v->lo_total = lo_cum.back();
     v->enc_tab = tab;
     v->enc_out = out;
     v->enc_slot = slot;
     v->enc_wave = tab + out + nmax * slot;
     v->enc_ready = true;
+    return FEC_OK;
+}
+
+// The instances of one tuple through the tile encoder, one workgroup per segment.
+int launch_tile_tuple(const fec_vr_plan* v, const fec_vr_plan::TileTuple& tt, const uint8_t* d_payload,
+                      const int32_t* d_len, uint8_t* d_cw_cur, int32_t* d_len_cur, uint8_t* d_cw_old,
+                      int32_t* d_len_old, hipStream_t s) {
+    if (tt.nseg <= 0) return FEC_OK;
+    static std::mutex mu;
+    static std::set<const void*> ready;  // kernels whose dynamic LDS limit is raised
+    {
+        std::lock_guard<std::mutex> lk(mu);
+        if (!ready.count(tt.kfn)) {
+            if (hipFuncSetAttribute(tt.kfn, hipFuncAttributeMaxDynamicSharedMemorySize, tt.tg.lds_len) != hipSuccess)
+                return FEC_ERR_HIP;
+            ready.insert(tt.kfn);
+        }
+    }
+    const fec::TileGeom& tg = tt.tg;
+    fec::EncTileArgs a{};
+    a.payload_base = d_payload;
+    a.len_base = d_len;
+    a.payload_bytes = 0;
+    a.len_bytes = 0;
+    a.history = 0;
+    a.P = 0;
+    a.cw = nullptr;
+    a.cw_bytes = 0;
+    a.cw_len = nullptr;
+    a.ptab = v->d_gtab + tt.toff;
+    a.L = v->plan.L;
+    a.CW = tg.CW;
+    a.NS4 = tg.NS4;
+    a.PPW = tg.PPW;
+    a.rem = tg.rem;
+    a.nvl = tg.nvl;
+    a.tiles_per_wg = 0;
+    a.ntiles = 0;
+    a.ngl = tg.ngl;
+    a.nso = tg.nso;
+    a.off_in = tg.off_in;
+    a.in_bytes = tg.in_bytes;
+    a.off_pw = tg.off_pw;
+    a.off_q = tg.off_q;
+    a.off_out = tg.off_out;
+    a.off_len = tg.off_len;
+    a.off_scratch = tg.off_scratch;
+    a.dbg = 0;
+    a.nt = 0;
+    a.seg = v->d_seg + 4 * tt.seg0;
+    a.cur_rows = d_cw_cur;
+    a.old_rows = d_cw_old;
+    a.cur_len = d_len_cur;
+    a.old_len = d_len_old;
+    a.W = v->cw_max;
+    void* args[] = {&a};
+    if (hipLaunchKernel(tt.kfn, dim3(static_cast<unsigned>(tt.nseg)), dim3(256), args, d_len ? tg.lds_len : tg.lds, s) !=
+        hipSuccess)
+        return FEC_ERR_HIP;
     return FEC_OK;
 }
 
@@ -960,6 +1082,7 @@ void fec_vr_plan::run(int max_payload, int T, int B, int N, bool mds, const uint
     cw_max = 0;
     for (const auto& e : plan.enc) cw_max = std::max(cw_max, cw_of(plan, e));
     for (const auto& d : plan.dec) cw_max = std::max(cw_max, cw_of(plan, d));
+    cw_max = (cw_max + 15) & ~15;  // row stride: rows start 16-byte aligned (the tile encoder's stores)
     enc_ready = dec_ready = hdr_ready = false;
 }
 
@@ -1071,9 +1194,21 @@ int fec_vr_encode_batch(fec_vr_plan* v, const uint8_t* d_payload, const int32_t*
     if (!v || !d_payload || !d_cw_cur || !d_len_cur || !d_cw_old || !d_len_old) return FEC_ERR_ARG;
     hipStream_t s = static_cast<hipStream_t>(hip_stream);
     if (int st = vr_guarded([&] { return prepare_encode(v, s); })) return st;
-    fec::VrEncodeArgs a{d_payload, d_payload_len, v->plan.L, v->d_enc_inst, v->d_enc_span, v->d_enc_cum,
-                        static_cast<int>(v->plan.enc.size()), v->enc_total, v->enc_tab, v->enc_out, v->enc_slot,
-                        v->enc_wave, v->d_gtab, v->cw_max, d_cw_cur, d_cw_old, d_len_cur, d_len_old};
+    // the tile encoder writes 16-byte chunks of rows at stride cw_max (a multiple of 16)
+    auto al = [](const void* q, uintptr_t m) { return (reinterpret_cast<uintptr_t>(q) & m) == 0; };
+    const bool tiled = !v->tiles.empty() && v->cw_max % 16 == 0 && al(d_cw_cur, 15) && al(d_cw_old, 15) &&
+                       al(d_payload, 3) && al(d_len_cur, 3) && al(d_len_old, 3);
+    if (tiled) {
+        for (const auto& tt : v->tiles)
+            if (int st = launch_tile_tuple(v, tt, d_payload, d_payload_len, d_cw_cur, d_len_cur, d_cw_old, d_len_old, s))
+                return st;
+    }
+    fec::VrEncodeArgs a{d_payload, d_payload_len, v->plan.L,
+                        tiled ? v->d_lo_inst : v->d_enc_inst, tiled ? v->d_lo_span : v->d_enc_span,
+                        tiled ? v->d_lo_cum : v->d_enc_cum,
+                        tiled ? v->n_lo : static_cast<int>(v->plan.enc.size()), tiled ? v->lo_total : v->enc_total,
+                        v->enc_tab, v->enc_out, v->enc_slot, v->enc_wave, v->d_gtab, v->cw_max, d_cw_cur, d_cw_old,
+                        d_len_cur, d_len_old};
     if (int st = fec::vr_launch_encode(a, hip_stream)) return st;
     return v->enc_up.done_reading(s);
 }
@@ -1130,7 +1265,8 @@ int fec_vr_decode_batch(fec_vr_plan* v, const uint8_t* d_cw_cur, const uint8_t* 
         }))
         return st;
     const auto& p = v->plan;
-    fec::VrCopyArgs ca{d_cw_cur, v->cw_max, v->d_pk_dec, v->d_inst, v->d_fate, v->d_slow, p.P, p.L, d_out, d_out_len};
+    fec::VrCopyArgs ca{d_cw_cur, v->cw_max, v->d_pk_dec, v->d_inst, v->d_fate, v->d_slow, p.P, p.L, d_out, d_out_len,
+                       std::max(1, 256 / ((p.L + 3) / 4))};
     if (int st = fec::vr_launch_copy(ca, hip_stream)) return st;
     fec::VrRecArgs ra{d_cw_cur, d_cw_old, v->cw_max, p.sent, v->d_rec_x, v->d_rec_dec, v->d_rec_coef,
                       static_cast<int>(p.rec_x.size()), v->d_inst, v->d_inst_switch, v->d_gf, p.L, d_out, d_out_len};

@@ -223,6 +223,7 @@ struct VrCopyArgs {     // received packets: systematic bytes of cur[x] in its d
     int L;
     uint8_t* out;
     int32_t* out_len;
+    int ppb;                 // packets per 256-thread workgroup: max(1, 256 / ceil(L / 4))
 };
 struct VrRecArgs {      // recovered packets: coefficient rows over the reporting decoder's inputs
     const uint8_t* cur;

@@ -215,43 +215,70 @@ __global__ __launch_bounds__(256) void fec_vr_encode_kernel(VrEncodeArgs a) {
     }
 }
 
-// One wave per packet, lanes over its output words.  Header at symbols 0 and 1 of sub-stream 0
-// (k = 1: position 0 of sub-streams 0 and 1), Decoder.cpp:89-96; the slow path clamps the length
-// (:148-149).  Payload byte b is codeword byte (h / k) * n + h % k, h = b + 2.
+// One thread per output dword of kVrCopyU packets: a workgroup covers kVrCopyU * a.ppb consecutive
+// packets, thread t takes word t % L4 of packets u * ppb + t / L4 (u < kVrCopyU), their chains of
+// dependent loads (fate -> decoder -> geometry -> header / bytes) interleaved.  (One wave per
+// packet left each packet's chain exposed: 229 us per 360 000 packets, r03y.)  Payload byte b is
+// codeword byte (h / k) * n + h % k of the reporting decoder's geometry, h = b + 2; the header is
+// at symbols 0 and 1 of sub-stream 0 (k = 1: position 0 of sub-streams 0 and 1), Decoder.cpp:89-96;
+// the slow path clamps the length (:148-149).
+constexpr int kVrCopyU = 4;
 __global__ __launch_bounds__(256) void fec_vr_copy_kernel(VrCopyArgs a) {
-    const int L = a.L, L4 = (L + 3) >> 2, lane = threadIdx.x & 63;
-    for (int64_t xx = static_cast<int64_t>(blockIdx.x) * 4 + (threadIdx.x >> 6); xx < a.P;
-         xx += static_cast<int64_t>(gridDim.x) * 4) {
-        const int64_t x = static_cast<int64_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(xx)));
-        const uint8_t fate = a.fate[x];
-        if (fate == 2) continue;  // recovered: fec_vr_recover_kernel
-        int ln = 0, cp = 0, k = 1, n = 1;
-        const uint8_t* src = a.cur + x * a.W;
-        if (fate == 1) {
-            const int* g = a.inst + 4 * a.pk_dec[x];
-            k = g[0];
-            n = g[1];
-            const int hdr = src[0] * 256 + src[k > 1 ? 1 : n];
-            ln = a.slow[x] ? min(hdr, L) : hdr;
-            cp = min(ln, L);
-        }
-        const float rk = 1.0f / static_cast<float>(k);
-        uint8_t* o = a.out + x * L;
-        for (int w = lane; w < L4; w += 64) {
-            const int b0 = 4 * w;
+    const int L = a.L, L4 = (L + 3) >> 2;
+    const int pl = static_cast<int>(threadIdx.x) / L4;
+    const int w = static_cast<int>(threadIdx.x) - pl * L4;
+    if (pl >= a.ppb) return;
+    int64_t x[kVrCopyU];
+    uint32_t fate[kVrCopyU];
+    int k[kVrCopyU], n[kVrCopyU], cp[kVrCopyU], ln[kVrCopyU];
+    const uint8_t* src[kVrCopyU];
+#pragma unroll
+    for (int u = 0; u < kVrCopyU; ++u) {
+        x[u] = (static_cast<int64_t>(blockIdx.x) * kVrCopyU + u) * a.ppb + pl;
+        fate[u] = x[u] < a.P ? a.fate[x[u]] : 2u;  // 2: recovered (fec_vr_recover_kernel) or none
+    }
+    int dj[kVrCopyU];
+    uint32_t sl[kVrCopyU];
+#pragma unroll
+    for (int u = 0; u < kVrCopyU; ++u) {
+        dj[u] = fate[u] == 1 ? a.pk_dec[x[u]] : 0;
+        sl[u] = fate[u] == 1 ? a.slow[x[u]] : 0u;
+        src[u] = a.cur + (fate[u] == 1 ? x[u] : 0) * a.W;
+    }
+#pragma unroll
+    for (int u = 0; u < kVrCopyU; ++u) {
+        k[u] = fate[u] == 1 ? a.inst[4 * dj[u]] : 1;
+        n[u] = fate[u] == 1 ? a.inst[4 * dj[u] + 1] : 1;
+    }
+#pragma unroll
+    for (int u = 0; u < kVrCopyU; ++u) {
+        int hdr = 0;
+        if (fate[u] == 1) hdr = src[u][0] * 256 + src[u][k[u] > 1 ? 1 : n[u]];
+        ln[u] = fate[u] == 1 ? (sl[u] ? min(hdr, L) : hdr) : 0;
+        cp[u] = min(ln[u], L);
+    }
+#pragma unroll
+    for (int u = 0; u < kVrCopyU; ++u) {
+        if (fate[u] == 2) continue;
+        const float rk = 1.0f / static_cast<float>(k[u]);
+        uint8_t* o = a.out + x[u] * L;
+        for (int ww = w; ww < L4; ww += 256) {  // one pass unless L > 1024 (then ppb = 1)
+            const int b0 = 4 * ww;
             uint32_t v = 0;
-            if (b0 < cp) {
-                int h = b0 + 2;
+            if (b0 < cp[u]) {
+                const int h = b0 + 2;
                 int sidx = static_cast<int>((static_cast<float>(h) + 0.5f) * rk);
-                int i = h - sidx * k;
+                int i = h - sidx * k[u];
+                uint32_t byte[4];
 #pragma unroll
                 for (int e = 0; e < 4; ++e) {
-                    if (b0 + e < cp) v |= static_cast<uint32_t>(src[sidx * n + i]) << (8 * e);
-                    if (++i == k) {
+                    byte[e] = b0 + e < cp[u] ? src[u][sidx * n[u] + i] : 0u;
+                    if (++i == k[u]) {
                         i = 0;
                         ++sidx;
                     }
                 }
+                v = byte[0] | (byte[1] << 8) | (byte[2] << 16) | (byte[3] << 24);
             }
             if (b0 + 4 <= L && (L & 3) == 0) {
                 *reinterpret_cast<uint32_t*>(o + b0) = v;
@@ -259,7 +286,7 @@ __global__ __launch_bounds__(256) void fec_vr_copy_kernel(VrCopyArgs a) {
                 for (int e = 0; e < 4 && b0 + e < L; ++e) o[b0 + e] = static_cast<uint8_t>(v >> (8 * e));
             }
         }
-        if (lane == 0) a.out_len[x] = ln;
+        if (w == 0) a.out_len[x[u]] = ln[u];
     }
 }
 
@@ -345,7 +372,8 @@ int vr_launch_encode(const VrEncodeArgs& a, void* s) {
 }
 int vr_launch_copy(const VrCopyArgs& a, void* s) {
     if (a.P <= 0) return FEC_OK;
-    hipLaunchKernelGGL(fec_vr_copy_kernel, dim3(static_cast<unsigned>(std::min<int64_t>((a.P + 3) / 4, 16384))), dim3(256), 0,
+    const int64_t per_wg = static_cast<int64_t>(kVrCopyU) * a.ppb;
+    hipLaunchKernelGGL(fec_vr_copy_kernel, dim3(static_cast<unsigned>((a.P + per_wg - 1) / per_wg)), dim3(256), 0,
                        static_cast<hipStream_t>(s), a);
     return hipGetLastError() == hipSuccess ? FEC_OK : FEC_ERR_HIP;
 }
