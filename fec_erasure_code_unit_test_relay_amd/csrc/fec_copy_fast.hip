@@ -13,7 +13,7 @@
 namespace fec {
 
 template <int K, int NP>
-__global__ __launch_bounds__(512) void fec_copy_fast_kernel(CopyFastArgs a) {
+__global__ __launch_bounds__(256) void fec_copy_fast_kernel(CopyFastArgs a) {
     constexpr int n = K + NP;
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     uint8_t* raw = smem;                           // codeword tile (+ slack)
