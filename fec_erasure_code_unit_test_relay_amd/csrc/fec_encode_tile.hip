@@ -268,7 +268,12 @@ __device__ __forceinline__ void tile_walk(const EncTileArgs& a, uint8_t* smem) {
     const int ngl = CL ? CG.ngl : a.ngl;                     // payload LDS-DMA instructions per wave per tile
     const int nglt = ngl + (has_len ? 1 : 0);
     const int nso = CL ? CG.nso : a.nso;                     // 16-byte stores per thread per tile
-    const int ns = nso + 1;                                  // + the trimmed-size store
+    // VMEM store instructions per wave per tile, the same in every wave (the vmcnt arithmetic of
+    // wait_vm below counts them): nso 16-byte stores + the trimmed-size store; in segment mode
+    // nit row-chunk iterations of two stores (cur and old resources) + two size stores
+    const int nch_seg = (CW + 15) >> 4;
+    const int nit_seg = (R * nch_seg + kTileThreads - 1) / kTileThreads;
+    const int ns = segm ? 2 * nit_seg + 2 : nso + 1;
 
     // tile it (0 = the tile in front of the first one) -> LDS input buffer (it & 1)
     const tv4u rs4 = raw_rsrc(pay_base, pay_bytes);
@@ -495,42 +500,53 @@ __device__ __forceinline__ void tile_walk(const EncTileArgs& a, uint8_t* smem) {
         // ---- D: output tile -> HBM (16-byte chunks); trimmed sizes
         if (segm) {
             // row by row into the frames' arrays (stride W, a multiple of 16): chunk c of row p is
-            // LDS bytes [p*CW + 16c, +16), the bytes past the codeword zeroed
-            const int nch = (CW + 15) >> 4;
+            // LDS bytes [p*CW + 16c, +16), the bytes past the codeword zeroed.  Every wave issues
+            // the same stores (ns above): one into the cur rows and one into the old rows per
+            // chunk, a lane's other one out of range (buffer stores drop it).
             typedef uint32_t v4u __attribute__((ext_vector_type(4)));
-            for (int q = tid; q < R * nch; q += kTileThreads) {
-                const int p = q / nch, c = q - p * nch;
-                const int t = row0 + p;
-                if (t >= P) continue;
-                const int64_t seqg = sfirst + t;
-                const int lb = p * CW + 16 * c;
+            const int64_t W64 = a.W;
+            const __amdgpu_buffer_rsrc_t rcur =
+                __builtin_amdgcn_make_buffer_rsrc(a.cur_rows + sfirst * W64, 0, static_cast<int>(P * W64), 0x00020000);
+            const __amdgpu_buffer_rsrc_t rold =
+                __builtin_amdgcn_make_buffer_rsrc(a.old_rows + sfirst * W64, 0, static_cast<int>(P * W64), 0x00020000);
+            const int nsw = static_cast<int>(ssw - sfirst);  // rows from nsw on go to old
+            for (int j = 0; j < nit_seg; ++j) {
+                const int qq = tid + j * kTileThreads;
+                const int pq = qq / nch_seg, c = qq - pq * nch_seg;
+                const int t = row0 + pq;
+                const bool ok = qq < R * nch_seg && t < P;
+                const int lb = ok ? pq * CW + 16 * c : 0;
                 const uint32_t* lw = reinterpret_cast<const uint32_t*>(out + (lb & ~3));
                 const int sh = lb & 3;
                 uint32_t d5[5];
 #pragma unroll
                 for (int m = 0; m < 5; ++m) d5[m] = lw[m];
-                const int left = CW - 16 * c;  // valid bytes of this chunk (> 0)
+                const int left = CW - 16 * c;  // valid bytes of this chunk
                 v4u vv;
 #pragma unroll
                 for (int m = 0; m < 4; ++m) vv[m] = __builtin_amdgcn_alignbyte(d5[m + 1], d5[m], sh) & keep_bytes(left - 4 * m);
-                uint8_t* dst = (seqg >= ssw ? a.old_rows : a.cur_rows) + seqg * a.W + 16 * c;
-                *reinterpret_cast<v4u*>(dst) = vv;
+                const int off = t * static_cast<int>(W64) + 16 * c;
+                __builtin_amdgcn_raw_buffer_store_b128(vv, rcur, ok && t < nsw ? off : 0x7ffffff0, 0, 0);
+                __builtin_amdgcn_raw_buffer_store_b128(vv, rold, ok && t >= nsw ? off : 0x7ffffff0, 0, 0);
             }
             const bool own = tid < R && row0 + tid < P;
             const uint8_t* cwp = out + (own ? tid : 0) * CW;
             int sz = CW;
-            if (own && cwp[CW - 1] == 0) {  // rare: a codeword ending in zero bytes
-                sz = 0;
-                for (int b = CW - 2; b >= 0; --b)
-                    if (cwp[b] != 0) {
-                        sz = b + 1;
-                        break;
-                    }
+            if (__builtin_amdgcn_ballot_w64(own && cwp[CW - 1] == 0)) {  // rare: a codeword ending in zero bytes
+                if (own && cwp[CW - 1] == 0) {
+                    sz = 0;
+                    for (int b = CW - 2; b >= 0; --b)
+                        if (cwp[b] != 0) {
+                            sz = b + 1;
+                            break;
+                        }
+                }
             }
-            if (own) {
-                const int64_t seqg = sfirst + row0 + tid;
-                (seqg >= ssw ? a.old_len : a.cur_len)[seqg] = sz;
-            }
+            const __amdgpu_buffer_rsrc_t rlc = __builtin_amdgcn_make_buffer_rsrc(a.cur_len + sfirst, 0, 4 * P, 0x00020000);
+            const __amdgpu_buffer_rsrc_t rlo = __builtin_amdgcn_make_buffer_rsrc(a.old_len + sfirst, 0, 4 * P, 0x00020000);
+            const int tl = row0 + tid;
+            __builtin_amdgcn_raw_buffer_store_b32(static_cast<uint32_t>(sz), rlc, own && tl < nsw ? 4 * tl : 0x7ffffff0, 0, 0);
+            __builtin_amdgcn_raw_buffer_store_b32(static_cast<uint32_t>(sz), rlo, own && tl >= nsw ? 4 * tl : 0x7ffffff0, 0, 0);
         } else {
             const int gbase = row0 * CW;  // 16-byte aligned
             const int lim = P * CW - gbase;

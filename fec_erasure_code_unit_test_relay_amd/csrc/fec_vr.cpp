@@ -921,7 +921,8 @@ int prepare_encode(fec_vr_plan* v, hipStream_t s) {
         inst.insert(inst.end(), {g.k, g.n, g.CW, it->second});
         span.insert(span.end(), {e.first, e.role_switch});
         cum.push_back(cum.back() + (e.end - e.first));
-        const int ti = tix[key];
+        int ti = tix[key];
+        if (ti >= 0 && (e.end - e.first) * static_cast<int64_t>(v->cw_max) >= 0x7fff0000) ti = -1;  // 32-bit buffer offsets
         if (ti >= 0) {
             const int64_t rows = e.end - e.first, R = v->tiles[static_cast<size_t>(ti)].tg.R;
             const int64_t nt = (rows + R - 1) / R;
