@@ -235,3 +235,27 @@ def test_gpu_adaptive_wire_packets_and_outputs_equal_oracle(adaptive, c4):
     assert np.flatnonzero(ol == 0).tolist() == c4["lost"]
     assert hashlib.sha256(ol.astype("<i4").tobytes()).hexdigest() == c4["out_len_sha256"]
     assert hashlib.sha256(out.cpu().numpy().tobytes()).hexdigest() == c4["out_data_sha256"]
+
+
+@pytest.mark.gpu
+def test_gpu_adaptive_tile_encode_equals_generic_kernel(monkeypatch):
+    """Config 4's encode through the tile encoder (one launch per (T,B,N) tuple, segment mode)
+    equals the generic variable-rate kernel (FEC_VR_NO_TILE, itself checked against the oracle's
+    wire packets above) row for row, over repeated launches: the tile path's hand-counted vmcnt
+    waits once let a tile's input be read before its LDS-DMA landed, 1 launch in 3."""
+    import torch
+    from fec_erasure_code_unit_test_relay_amd import fill_payload
+    torch.cuda.set_device(0)
+    pat = load_pattern("bin_erasure")
+    monkeypatch.setenv("FEC_VR_NO_TILE", "1")
+    v_gen = VrPlan(pat, 120000)
+    ref = v_gen.encode(fill_payload(0, v_gen.sent, 300, 0x5EED))
+    monkeypatch.delenv("FEC_VR_NO_TILE")
+    v = VrPlan(pat, 120000)
+    payload = fill_payload(0, v.sent, 300, 0x5EED)
+    frames = v.alloc_frames()
+    for _ in range(6):
+        got = v.encode(payload, frames=frames)
+        torch.cuda.synchronize()
+        for a, b in zip(got, ref):
+            assert torch.equal(a, b)
