@@ -182,7 +182,9 @@ __device__ __forceinline__ uint32_t ttail_rem(const uint32_t (&X)[n]) {
 }
 
 // LC > 0: L (and every size derived from it) fixed at compile time; LC = 0: from the arguments.
-template <int K, int NP, int W, int LC>
+// SEG: segment mode (the variable-rate schedule's instances, a.seg) compiled in; the one-stream
+// kernels are built without it (its branches cost the headline encoder 10 %: 158 vs 144 us).
+template <int K, int NP, int W, int LC, bool SEG>
 __device__ __forceinline__ void tile_walk(const EncTileArgs& a, uint8_t* smem) {
     constexpr int n = K + NP;
     constexpr TileGeom CG = tile_geometry(K, NP, LC > 0 ? LC : 300);
@@ -205,7 +207,7 @@ __device__ __forceinline__ void tile_walk(const EncTileArgs& a, uint8_t* smem) {
     // of one encoder instance -- a fresh encoder over the payload rows [sfirst, sfirst+P) -- and
     // writes row t to the frames' array of its role (cur before the role switch, old after) at
     // row sfirst+t, stride a.W.
-    const bool segm = a.seg != nullptr;
+    constexpr bool segm = SEG;
     int P = a.P;
     int64_t sfirst = 0, ssw = 0;
     int seg_t0 = 0, seg_cnt = 0;
@@ -608,14 +610,14 @@ constexpr int tile_min_wg() {
     return K * NP > 36 ? 3 : (K * NP >= 27 ? 4 : FEC_TILE_MINWG);
 }
 
-template <int K, int NP, int LC>
+template <int K, int NP, int LC, bool SEG>
 __global__ __launch_bounds__(kTileThreads, (tile_min_wg<K, NP>())) void fec_encode_tile_kernel(EncTileArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t tsmem[];
     switch (__builtin_amdgcn_readfirstlane(threadIdx.x >> 6)) {
-        case 0: tile_walk<K, NP, 0, LC>(a, tsmem); break;
-        case 1: tile_walk<K, NP, 1, LC>(a, tsmem); break;
-        case 2: tile_walk<K, NP, 2, LC>(a, tsmem); break;
-        default: tile_walk<K, NP, 3, LC>(a, tsmem); break;
+        case 0: tile_walk<K, NP, 0, LC, SEG>(a, tsmem); break;
+        case 1: tile_walk<K, NP, 1, LC, SEG>(a, tsmem); break;
+        case 2: tile_walk<K, NP, 2, LC, SEG>(a, tsmem); break;
+        default: tile_walk<K, NP, 3, LC, SEG>(a, tsmem); break;
     }
 }
 
@@ -630,22 +632,33 @@ __global__ __launch_bounds__(kTileThreads, (tile_min_wg<K, NP>())) void fec_enco
 #define FEC_ENC_TILE_L300_LIST(X) X(8, 3) X(9, 5)
 #endif
 
-#define FEC_ENC_TILE_INST(K, NP) template __global__ void fec_encode_tile_kernel<K, NP, 0>(EncTileArgs);
-#define FEC_ENC_TILE_INST300(K, NP) template __global__ void fec_encode_tile_kernel<K, NP, 300>(EncTileArgs);
+#define FEC_ENC_TILE_INST(K, NP) \
+    template __global__ void fec_encode_tile_kernel<K, NP, 0, false>(EncTileArgs); \
+    template __global__ void fec_encode_tile_kernel<K, NP, 0, true>(EncTileArgs);
+#define FEC_ENC_TILE_INST300(K, NP) template __global__ void fec_encode_tile_kernel<K, NP, 300, false>(EncTileArgs);
 FEC_ENC_TILE_LIST(FEC_ENC_TILE_INST)
 FEC_ENC_TILE_L300_LIST(FEC_ENC_TILE_INST300)
 
 const void* fec_encode_tile_kernel_for(int k, int np, int L) {
     if (!std::getenv("FEC_TILE_RUNTIME_L") && L == 300) {
 #define FEC_ENC_TILE_CASE300(K, NP) \
-    if (k == K && np == NP) return reinterpret_cast<const void*>(&fec_encode_tile_kernel<K, NP, 300>);
+    if (k == K && np == NP) return reinterpret_cast<const void*>(&fec_encode_tile_kernel<K, NP, 300, false>);
         FEC_ENC_TILE_L300_LIST(FEC_ENC_TILE_CASE300)
 #undef FEC_ENC_TILE_CASE300
     }
 #define FEC_ENC_TILE_CASE(K, NP) \
-    if (k == K && np == NP) return reinterpret_cast<const void*>(&fec_encode_tile_kernel<K, NP, 0>);
+    if (k == K && np == NP) return reinterpret_cast<const void*>(&fec_encode_tile_kernel<K, NP, 0, false>);
     FEC_ENC_TILE_LIST(FEC_ENC_TILE_CASE)
 #undef FEC_ENC_TILE_CASE
+    return nullptr;
+}
+
+// The segment-mode instance (runtime L) for the variable-rate schedule, or nullptr.
+const void* fec_encode_tile_seg_kernel_for(int k, int np) {
+#define FEC_ENC_TILE_SEG_CASE(K, NP) \
+    if (k == K && np == NP) return reinterpret_cast<const void*>(&fec_encode_tile_kernel<K, NP, 0, true>);
+    FEC_ENC_TILE_LIST(FEC_ENC_TILE_SEG_CASE)
+#undef FEC_ENC_TILE_SEG_CASE
     return nullptr;
 }
 
