@@ -712,8 +712,8 @@ void VrPlan::control(const uint8_t* pattern, int64_t n_pattern, int T, int B, in
     if (std::getenv("FEC_VR_DEBUG")) {
         const auto tc2 = std::chrono::steady_clock::now();
         std::fprintf(stderr, "vr control: drops %.3f ms, loop %.3f ms (%zu feedback changes)\n",
-                     std::chrono::duration<double, std::milli>(tc1 - tc0).count(), fb.changes,
-                     std::chrono::duration<double, std::milli>(tc2 - tc1).count());
+                     std::chrono::duration<double, std::milli>(tc1 - tc0).count(),
+                     std::chrono::duration<double, std::milli>(tc2 - tc1).count(), fb.changes);
     }
     // the last two decoder instances, then the coding-rate sum; no more jobs
     if (dold >= 0) done_with(dold);
@@ -805,6 +805,68 @@ struct Upload {
     }
     int done_reading(hipStream_t s) { return hipEventRecord(used, s) == hipSuccess ? FEC_OK : FEC_ERR_HIP; }
 };
+
+// Side streams for the independent launches of one batch (the tuples' tile encoders, the generic
+// encoder, the recovery next to the copy): each is forked from the caller's stream by an event and
+// joined back into it before the call returns, so the caller sees one ordered stream.  The small
+// launches are latency-bound walks (a tuple of a few thousand packets: ~21 us whatever its size,
+// r03z); on one stream their times add up.
+struct Fork {
+    static constexpr int kSide = 3;
+    hipStream_t st[kSide] = {};
+    hipEvent_t ev_fork = nullptr, ev_join[kSide] = {};
+    bool forked[kSide] = {};
+    hipStream_t caller = nullptr;
+
+    Fork() = default;
+    Fork(const Fork&) = delete;
+    Fork& operator=(const Fork&) = delete;
+    ~Fork() {
+        for (int i = 0; i < kSide; ++i) {
+            if (st[i]) {
+                (void)hipStreamSynchronize(st[i]);
+                (void)hipStreamDestroy(st[i]);
+            }
+            if (ev_join[i]) (void)hipEventDestroy(ev_join[i]);
+        }
+        if (ev_fork) (void)hipEventDestroy(ev_fork);
+    }
+    int begin(hipStream_t s) {
+        if (!ev_fork) {
+            if (hipEventCreateWithFlags(&ev_fork, hipEventDisableTiming) != hipSuccess) return FEC_ERR_HIP;
+            for (int i = 0; i < kSide; ++i)
+                if (hipStreamCreateWithFlags(&st[i], hipStreamNonBlocking) != hipSuccess ||
+                    hipEventCreateWithFlags(&ev_join[i], hipEventDisableTiming) != hipSuccess)
+                    return FEC_ERR_HIP;
+        }
+        caller = s;
+        for (bool& f : forked) f = false;
+        return hipEventRecord(ev_fork, s) == hipSuccess ? FEC_OK : FEC_ERR_HIP;
+    }
+    // launch slot i: 0 = the caller's stream, i > 0 = side stream (i - 1) % kSide
+    int stream(int i, hipStream_t* out) {
+        if (i <= 0) {
+            *out = caller;
+            return FEC_OK;
+        }
+        const int j = (i - 1) % kSide;
+        if (!forked[j]) {
+            if (hipStreamWaitEvent(st[j], ev_fork, 0) != hipSuccess) return FEC_ERR_HIP;
+            forked[j] = true;
+        }
+        *out = st[j];
+        return FEC_OK;
+    }
+    int join() {
+        for (int j = 0; j < kSide; ++j) {
+            if (!forked[j]) continue;
+            if (hipEventRecord(ev_join[j], st[j]) != hipSuccess || hipStreamWaitEvent(caller, ev_join[j], 0) != hipSuccess)
+                return FEC_ERR_HIP;
+            forked[j] = false;
+        }
+        return FEC_OK;
+    }
+};
 }  // namespace
 
 struct fec_vr_plan {
@@ -824,6 +886,7 @@ struct fec_vr_plan {
     const int64_t* d_inst_switch = nullptr;
     const uint8_t* d_fate = nullptr;
     const uint8_t* d_slow = nullptr;
+    uint32_t* d_geo = nullptr;
     const int64_t* d_rec_x = nullptr;
     const int32_t* d_rec_dec = nullptr;
     const uint8_t* d_rec_coef = nullptr;
@@ -848,6 +911,7 @@ struct fec_vr_plan {
     std::vector<TileTuple> tiles;
     const int64_t* d_seg = nullptr;
     bool enc_ready = false, dec_ready = false, hdr_ready = false;
+    Fork fork;  // side streams (declared after the uploads: destroyed, and drained, first)
 
     ~fec_vr_plan() {
         if (pk_sent) {
@@ -943,6 +1007,8 @@ int prepare_encode(fec_vr_plan* v, hipStream_t s) {
         v->tiles[i].nseg = static_cast<int>(segs[i].size() / 4);
         seg.insert(seg.end(), segs[i].begin(), segs[i].end());
     }
+    std::stable_sort(v->tiles.begin(), v->tiles.end(),
+                     [](const fec_vr_plan::TileTuple& x, const fec_vr_plan::TileTuple& y) { return x.nseg > y.nseg; });
     Upload& u = v->enc_up;
     if (int st = u.begin()) return st;
     u.add(&v->d_enc_inst, inst);
@@ -1049,7 +1115,8 @@ int prepare_decode(fec_vr_plan* v, hipStream_t s) {
     // the per-packet arrays go straight from the plan's (page-locked) buffers
     const size_t P = static_cast<size_t>(p.P);
     const size_t o_fate = (P * 4 + 255) & ~size_t(255), o_slow = (o_fate + P + 255) & ~size_t(255);
-    if (int st = Upload::reserve(&v->d_pk, &v->d_pk_cap, o_slow + std::max<size_t>(P, 1), u.used, s)) return st;
+    const size_t o_geo = (o_slow + P + 255) & ~size_t(255);  // device scratch of the copy
+    if (int st = Upload::reserve(&v->d_pk, &v->d_pk_cap, o_geo + 4 * std::max<size_t>(P, 1), u.used, s)) return st;
     uint8_t* d = static_cast<uint8_t*>(v->d_pk);
     if (hipMemcpyAsync(d, p.fate_dec.data(), P * 4, hipMemcpyHostToDevice, s) != hipSuccess ||
         hipMemcpyAsync(d + o_fate, p.fate.data(), P, hipMemcpyHostToDevice, s) != hipSuccess ||
@@ -1060,6 +1127,7 @@ int prepare_decode(fec_vr_plan* v, hipStream_t s) {
     v->d_pk_dec = reinterpret_cast<const int32_t*>(d);
     v->d_fate = d + o_fate;
     v->d_slow = d + o_slow;
+    v->d_geo = reinterpret_cast<uint32_t*>(d + o_geo);
     v->dec_ready = true;
     return FEC_OK;
 }
@@ -1199,18 +1267,32 @@ int fec_vr_encode_batch(fec_vr_plan* v, const uint8_t* d_payload, const int32_t*
     auto al = [](const void* q, uintptr_t m) { return (reinterpret_cast<uintptr_t>(q) & m) == 0; };
     const bool tiled = !v->tiles.empty() && v->cw_max % 16 == 0 && al(d_cw_cur, 15) && al(d_cw_old, 15) &&
                        al(d_payload, 3) && al(d_len_cur, 3) && al(d_len_old, 3);
-    if (tiled) {
-        for (const auto& tt : v->tiles)
-            if (int st = launch_tile_tuple(v, tt, d_payload, d_payload_len, d_cw_cur, d_len_cur, d_cw_old, d_len_old, s))
-                return st;
-    }
+    // Independent launches on the caller's stream and the side streams: the generic encoder (a
+    // latency-bound walk over the few tuples without a tile geometry) first, on a side stream, then
+    // the tuples largest first, round robin.
+    if (int st = v->fork.begin(s)) return st;
+    hipStream_t sg = s;
+    if (tiled && v->n_lo > 0)
+        if (int st = v->fork.stream(1, &sg)) return st;
     fec::VrEncodeArgs a{d_payload, d_payload_len, v->plan.L,
                         tiled ? v->d_lo_inst : v->d_enc_inst, tiled ? v->d_lo_span : v->d_enc_span,
                         tiled ? v->d_lo_cum : v->d_enc_cum,
                         tiled ? v->n_lo : static_cast<int>(v->plan.enc.size()), tiled ? v->lo_total : v->enc_total,
                         v->enc_tab, v->enc_out, v->enc_slot, v->enc_wave, v->d_gtab, v->cw_max, d_cw_cur, d_cw_old,
                         d_len_cur, d_len_old};
-    if (int st = fec::vr_launch_encode(a, hip_stream)) return st;
+    if (int st = fec::vr_launch_encode(a, sg)) return st;
+    if (tiled) {
+        int i = 0;  // the largest on the caller's stream, the rest round robin after the generic one
+        for (const auto& tt : v->tiles) {  // prepare_encode sorted them by segments, descending
+            hipStream_t st_i;
+            if (int st = v->fork.stream(i == 0 || v->n_lo == 0 ? i : i + 1, &st_i)) return st;
+            ++i;
+            if (int st = launch_tile_tuple(v, tt, d_payload, d_payload_len, d_cw_cur, d_len_cur, d_cw_old, d_len_old,
+                                           st_i))
+                return st;
+        }
+    }
+    if (int st = v->fork.join()) return st;
     return v->enc_up.done_reading(s);
 }
 
@@ -1267,11 +1349,16 @@ int fec_vr_decode_batch(fec_vr_plan* v, const uint8_t* d_cw_cur, const uint8_t* 
         return st;
     const auto& p = v->plan;
     fec::VrCopyArgs ca{d_cw_cur, v->cw_max, v->d_pk_dec, v->d_inst, v->d_fate, v->d_slow, p.P, p.L, d_out, d_out_len,
-                       std::max(1, 256 / ((p.L + 3) / 4))};
+                       std::max(1, 256 / ((p.L + 3) / 4)), v->d_geo};
+    // the recovery writes only the rows (and lengths) the copy leaves alone: side by side
+    if (int st = v->fork.begin(s)) return st;
+    hipStream_t sr;
+    if (int st = v->fork.stream(p.rec_x.empty() ? 0 : 1, &sr)) return st;
     if (int st = fec::vr_launch_copy(ca, hip_stream)) return st;
     fec::VrRecArgs ra{d_cw_cur, d_cw_old, v->cw_max, p.sent, v->d_rec_x, v->d_rec_dec, v->d_rec_coef,
                       static_cast<int>(p.rec_x.size()), v->d_inst, v->d_inst_switch, v->d_gf, p.L, d_out, d_out_len};
-    if (int st = fec::vr_launch_recover(ra, hip_stream)) return st;
+    if (int st = fec::vr_launch_recover(ra, sr)) return st;
+    if (int st = v->fork.join()) return st;
     return v->dec_up.done_reading(s);
 }
 

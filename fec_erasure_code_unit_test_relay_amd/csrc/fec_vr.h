@@ -224,6 +224,7 @@ struct VrCopyArgs {     // received packets: systematic bytes of cur[x] in its d
     uint8_t* out;
     int32_t* out_len;
     int ppb;                 // packets per 256-thread workgroup: max(1, 256 / ceil(L / 4))
+    uint32_t* geo;           // [P] scratch: k | n << 8 | fate << 16 | slow << 24 (fec_vr_geo_kernel)
 };
 struct VrRecArgs {      // recovered packets: coefficient rows over the reporting decoder's inputs
     const uint8_t* cur;

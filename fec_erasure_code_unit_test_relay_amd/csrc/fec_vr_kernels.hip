@@ -215,78 +215,96 @@ __global__ __launch_bounds__(256) void fec_vr_encode_kernel(VrEncodeArgs a) {
     }
 }
 
+// The copy's per-packet word, one thread per packet: geo[x] = k | n << 8 | fate << 16 | slow << 24
+// in the reporting decoder's geometry (fate != 1: fate << 16 only).  Paying the chain fate ->
+// decoder -> geometry once here, with a thread per packet, leaves the copy one level of dependent
+// loads (its word) in front of the row bytes.
+__global__ __launch_bounds__(256) void fec_vr_geo_kernel(VrCopyArgs a) {
+    const int64_t x = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x;
+    if (x >= a.P) return;
+    const uint32_t f = a.fate[x];
+    uint32_t g = f << 16;
+    if (f == 1) {
+        const int j = a.pk_dec[x];
+        g |= static_cast<uint32_t>(a.inst[4 * j]) | static_cast<uint32_t>(a.inst[4 * j + 1]) << 8 |
+             (a.slow[x] ? 1u << 24 : 0u);
+    }
+    a.geo[x] = g;
+}
+
 // One thread per output dword of kVrCopyU packets: a workgroup covers kVrCopyU * a.ppb consecutive
-// packets, thread t takes word t % L4 of packets u * ppb + t / L4 (u < kVrCopyU), their chains of
-// dependent loads (fate -> decoder -> geometry -> header / bytes) interleaved.  (One wave per
-// packet left each packet's chain exposed: 229 us per 360 000 packets, r03y.)  Payload byte b is
-// codeword byte (h / k) * n + h % k of the reporting decoder's geometry, h = b + 2; the header is
-// at symbols 0 and 1 of sub-stream 0 (k = 1: position 0 of sub-streams 0 and 1), Decoder.cpp:89-96;
-// the slow path clamps the length (:148-149).
+// packets, thread t takes word t % L4 of packets u * ppb + t / L4 (u < kVrCopyU).  Per packet: its
+// word (fec_vr_geo_kernel), then the header and the word's 4 bytes together (the byte positions
+// depend only on k and n; the bytes past the copied length are masked afterwards), then the store.
+// (The chain fate -> decoder -> geometry -> header -> bytes in this kernel: 220 us per 360 000
+// packets, r03z.)  Payload byte b is codeword byte (h / k) * n + h % k of the reporting decoder's
+// geometry, h = b + 2; the header is at symbols 0 and 1 of sub-stream 0 (k = 1: position 0 of
+// sub-streams 0 and 1), Decoder.cpp:89-96; the slow path clamps the length (:148-149).
 constexpr int kVrCopyU = 4;
 __global__ __launch_bounds__(256) void fec_vr_copy_kernel(VrCopyArgs a) {
     const int L = a.L, L4 = (L + 3) >> 2;
     const int pl = static_cast<int>(threadIdx.x) / L4;
     const int w = static_cast<int>(threadIdx.x) - pl * L4;
     if (pl >= a.ppb) return;
+    const int64_t wmax = a.W - 1;
     int64_t x[kVrCopyU];
-    uint32_t fate[kVrCopyU];
-    int k[kVrCopyU], n[kVrCopyU], cp[kVrCopyU], ln[kVrCopyU];
-    const uint8_t* src[kVrCopyU];
+    uint32_t g[kVrCopyU];
 #pragma unroll
     for (int u = 0; u < kVrCopyU; ++u) {
         x[u] = (static_cast<int64_t>(blockIdx.x) * kVrCopyU + u) * a.ppb + pl;
-        fate[u] = x[u] < a.P ? a.fate[x[u]] : 2u;  // 2: recovered (fec_vr_recover_kernel) or none
+        g[u] = x[u] < a.P ? a.geo[x[u]] : 2u << 16;  // 2: recovered (fec_vr_recover_kernel) or none
     }
-    int dj[kVrCopyU];
-    uint32_t sl[kVrCopyU];
+    int k[kVrCopyU], n[kVrCopyU], cp[kVrCopyU], ln[kVrCopyU];
+    const uint8_t* src[kVrCopyU];
+    uint32_t h0[kVrCopyU], h1[kVrCopyU];
 #pragma unroll
     for (int u = 0; u < kVrCopyU; ++u) {
-        dj[u] = fate[u] == 1 ? a.pk_dec[x[u]] : 0;
-        sl[u] = fate[u] == 1 ? a.slow[x[u]] : 0u;
-        src[u] = a.cur + (fate[u] == 1 ? x[u] : 0) * a.W;
+        const bool rx = (g[u] >> 16 & 0xff) == 1;
+        k[u] = rx ? static_cast<int>(g[u] & 0xff) : 1;
+        n[u] = rx ? static_cast<int>(g[u] >> 8 & 0xff) : 1;
+        src[u] = a.cur + (rx ? x[u] : 0) * a.W;
+        h0[u] = rx ? src[u][0] : 0u;
+        h1[u] = rx ? src[u][k[u] > 1 ? 1 : n[u]] : 0u;
     }
+    for (int ww = w; ww < L4; ww += 256) {  // one pass unless L > 1024 (then ppb = 1)
+        const int b0 = 4 * ww;
+        uint32_t byte[kVrCopyU][4];
 #pragma unroll
-    for (int u = 0; u < kVrCopyU; ++u) {
-        k[u] = fate[u] == 1 ? a.inst[4 * dj[u]] : 1;
-        n[u] = fate[u] == 1 ? a.inst[4 * dj[u] + 1] : 1;
-    }
+        for (int u = 0; u < kVrCopyU; ++u) {
+            const bool rx = (g[u] >> 16 & 0xff) == 1;
+            const int h = b0 + 2;
+            int sidx = static_cast<int>((static_cast<float>(h) + 0.5f) / static_cast<float>(k[u]));
+            int i = h - sidx * k[u];
 #pragma unroll
-    for (int u = 0; u < kVrCopyU; ++u) {
-        int hdr = 0;
-        if (fate[u] == 1) hdr = src[u][0] * 256 + src[u][k[u] > 1 ? 1 : n[u]];
-        ln[u] = fate[u] == 1 ? (sl[u] ? min(hdr, L) : hdr) : 0;
-        cp[u] = min(ln[u], L);
-    }
-#pragma unroll
-    for (int u = 0; u < kVrCopyU; ++u) {
-        if (fate[u] == 2) continue;
-        const float rk = 1.0f / static_cast<float>(k[u]);
-        uint8_t* o = a.out + x[u] * L;
-        for (int ww = w; ww < L4; ww += 256) {  // one pass unless L > 1024 (then ppb = 1)
-            const int b0 = 4 * ww;
-            uint32_t v = 0;
-            if (b0 < cp[u]) {
-                const int h = b0 + 2;
-                int sidx = static_cast<int>((static_cast<float>(h) + 0.5f) * rk);
-                int i = h - sidx * k[u];
-                uint32_t byte[4];
-#pragma unroll
-                for (int e = 0; e < 4; ++e) {
-                    byte[e] = b0 + e < cp[u] ? src[u][sidx * n[u] + i] : 0u;
-                    if (++i == k[u]) {
-                        i = 0;
-                        ++sidx;
-                    }
+            for (int e = 0; e < 4; ++e) {
+                const int64_t pos = min<int64_t>(static_cast<int64_t>(sidx) * n[u] + i, wmax);
+                byte[u][e] = rx ? src[u][pos] : 0u;
+                if (++i == k[u]) {
+                    i = 0;
+                    ++sidx;
                 }
-                v = byte[0] | (byte[1] << 8) | (byte[2] << 16) | (byte[3] << 24);
             }
+        }
+#pragma unroll
+        for (int u = 0; u < kVrCopyU; ++u) {
+            const uint32_t f = g[u] >> 16 & 0xff;
+            if (f == 2) continue;
+            if (ww == w) {
+                const int hdr = static_cast<int>(h0[u] * 256 + h1[u]);
+                ln[u] = f == 1 ? ((g[u] >> 24) ? min(hdr, L) : hdr) : 0;
+                cp[u] = min(ln[u], L);
+            }
+            uint32_t v = 0;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) v |= (b0 + e < cp[u] ? byte[u][e] : 0u) << (8 * e);
+            uint8_t* o = a.out + x[u] * L;
             if (b0 + 4 <= L && (L & 3) == 0) {
                 *reinterpret_cast<uint32_t*>(o + b0) = v;
             } else {
                 for (int e = 0; e < 4 && b0 + e < L; ++e) o[b0 + e] = static_cast<uint8_t>(v >> (8 * e));
             }
+            if (ww == 0) a.out_len[x[u]] = ln[u];
         }
-        if (w == 0) a.out_len[x[u]] = ln[u];
     }
 }
 
@@ -364,7 +382,9 @@ int vr_launch_encode(const VrEncodeArgs& a, void* s) {
     if (a.nenc <= 0) return FEC_OK;
     const int wpb = std::min(4, 65536 / std::max(1, a.wave_bytes));
     if (wpb < 1) return FEC_ERR_ARG;
-    const int64_t waves = std::max<int64_t>(1, std::min<int64_t>((a.cum_host_total + 15) / 16, 16384));
+    // A wave walks its codewords one after another (a chain of dependent loads per codeword):
+    // as many waves as the chip holds before the walks get longer than 2 codewords.
+    const int64_t waves = std::max<int64_t>(1, std::min<int64_t>((a.cum_host_total + 1) / 2, 16384));
     const unsigned grid = static_cast<unsigned>((waves + wpb - 1) / wpb);
     hipLaunchKernelGGL(fec_vr_encode_kernel, dim3(grid), dim3(64 * wpb), static_cast<size_t>(wpb) * a.wave_bytes,
                        static_cast<hipStream_t>(s), a);
@@ -372,6 +392,8 @@ int vr_launch_encode(const VrEncodeArgs& a, void* s) {
 }
 int vr_launch_copy(const VrCopyArgs& a, void* s) {
     if (a.P <= 0) return FEC_OK;
+    hipLaunchKernelGGL(fec_vr_geo_kernel, dim3(static_cast<unsigned>((a.P + 255) / 256)), dim3(256), 0,
+                       static_cast<hipStream_t>(s), a);
     const int64_t per_wg = static_cast<int64_t>(kVrCopyU) * a.ppb;
     hipLaunchKernelGGL(fec_vr_copy_kernel, dim3(static_cast<unsigned>((a.P + per_wg - 1) / per_wg)), dim3(256), 0,
                        static_cast<hipStream_t>(s), a);
