@@ -10,6 +10,8 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <ctime>
+#include <sys/resource.h>
 #include <new>
 #include <mutex>
 #include <set>
@@ -382,12 +384,19 @@ struct VrPlan::FbCursor {
     size_t j = 0, e = 0;
     uint32_t cur = 0;
     size_t changes = 0;
+    int64_t done = 0;  // jobs known complete: the shared counter is read only past them
     explicit FbCursor(VrPlan& plan) : p(plan) {}
-    bool ready(size_t job) const {
-        return static_cast<int64_t>(job) < p.fb_done_.load(std::memory_order_acquire);
+    bool ready(size_t job) {
+        if (static_cast<int64_t>(job) < done) return true;
+        done = p.fb_done_.load(std::memory_order_acquire);
+        return static_cast<int64_t>(job) < done;
     }
-    void wait(size_t job) const {
+    double waited_ms = 0;  // FEC_VR_DEBUG: time the control loop spent waiting for the producer
+    void wait(size_t job) {
+        if (ready(job)) return;
+        const auto t0 = std::chrono::steady_clock::now();
         while (!ready(job)) std::this_thread::yield();
+        waited_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     }
     // skip to the next entry that changes the value; false at the end of the published jobs
     bool peek(int64_t* seq, bool block) {
@@ -537,7 +546,13 @@ void VrPlan::control(const uint8_t* pattern, int64_t n_pattern, int T, int B, in
             rate_runs.push_back(RateRun{count, rate});
     };
 
+    int64_t n_iter = 0, n_jump = 0;  // FEC_VR_DEBUG counters
+    timespec cpu0{};
+    clock_gettime(CLOCK_THREAD_CPUTIME_ID, &cpu0);
+    rusage ru0{};
+    getrusage(RUSAGE_THREAD, &ru0);
     for (int64_t seq = 0;; ++seq) {
+        ++n_iter;
         // ---- steady stretch: the same frame, every packet received, nothing switching ----
         // Every branch below is then fixed: the feedback repeats (no change in the feedback
         // stream), the encoder has no switch to make and no transition running, the decoder has
@@ -578,6 +593,7 @@ void VrPlan::control(const uint8_t* pattern, int64_t n_pattern, int T, int B, in
                     latest_seq = end;
                     sent = end;
                     steady_packets += end - seq;
+                    ++n_jump;
                     seq = end;
                 }
             }
@@ -711,9 +727,20 @@ void VrPlan::control(const uint8_t* pattern, int64_t n_pattern, int T, int B, in
     for (int64_t s : drops) erased[static_cast<size_t>(s)] = 1;
     if (std::getenv("FEC_VR_DEBUG")) {
         const auto tc2 = std::chrono::steady_clock::now();
-        std::fprintf(stderr, "vr control: drops %.3f ms, loop %.3f ms (%zu feedback changes)\n",
+        timespec cpu1{};
+        clock_gettime(CLOCK_THREAD_CPUTIME_ID, &cpu1);
+        rusage ru1{};
+        getrusage(RUSAGE_THREAD, &ru1);
+        std::fprintf(stderr, "vr control: loop thread cpu %.3f ms (user %.3f sys %.3f), %ld minor faults\n",
+                     (cpu1.tv_sec - cpu0.tv_sec) * 1e3 + (cpu1.tv_nsec - cpu0.tv_nsec) * 1e-6,
+                     (ru1.ru_utime.tv_sec - ru0.ru_utime.tv_sec) * 1e3 + (ru1.ru_utime.tv_usec - ru0.ru_utime.tv_usec) * 1e-3,
+                     (ru1.ru_stime.tv_sec - ru0.ru_stime.tv_sec) * 1e3 + (ru1.ru_stime.tv_usec - ru0.ru_stime.tv_usec) * 1e-3,
+                     ru1.ru_minflt - ru0.ru_minflt);
+        std::fprintf(stderr, "vr control: drops %.3f ms, loop %.3f ms (%zu feedback changes, %.3f ms waiting for "
+                     "them; %lld iterations, %lld steady stretches, %zu drops)\n",
                      std::chrono::duration<double, std::milli>(tc1 - tc0).count(),
-                     std::chrono::duration<double, std::milli>(tc2 - tc1).count(), fb.changes);
+                     std::chrono::duration<double, std::milli>(tc2 - tc1).count(), fb.changes, fb.waited_ms,
+                     static_cast<long long>(n_iter), static_cast<long long>(n_jump), drops.size());
     }
     // the last two decoder instances, then the coding-rate sum; no more jobs
     if (dold >= 0) done_with(dold);
