@@ -108,6 +108,7 @@ __device__ __forceinline__ void stage_to_lds_padded(uint8_t* lds, const uint8_t*
     auto grp = [&](int x) { return static_cast<int>((static_cast<float>(x) + 0.5f) * rG); };
     auto at = [&](int b) { return b + gp * grp(b - delta); };
     const int nchunks = (total + 15) >> 4;
+    const bool straddle = (delta & 15) != 0;  // boundaries are at delta + k G, G a multiple of 16
     for (int c0 = 0; c0 < nchunks; c0 += nthreads * BATCH) {
         uint4 v[BATCH];
 #pragma unroll
@@ -120,13 +121,21 @@ __device__ __forceinline__ void stage_to_lds_padded(uint8_t* lds, const uint8_t*
                 v[q] = full ? *reinterpret_cast<const uint4*>(gbase + lo) : make_uint4(0, 0, 0, 0);
             }
         }
+        if (!straddle) {
 #pragma unroll
-        for (int q = 0; q < BATCH; ++q) {
-            const int lo = (c0 + q * nthreads + tid) << 4;
-            if (lo >= delta && lo + 16 <= total) {
-                const int k1 = grp(lo - delta), k2 = grp(lo + 15 - delta);
-                *reinterpret_cast<uint4*>(lds + lo + gp * k1) = v[q];
-                if (k2 != k1) *reinterpret_cast<uint4*>(lds + lo + gp * k2) = v[q];
+            for (int q = 0; q < BATCH; ++q) {
+                const int lo = (c0 + q * nthreads + tid) << 4;
+                if (lo >= delta && lo + 16 <= total) *reinterpret_cast<uint4*>(lds + at(lo)) = v[q];
+            }
+        } else {
+#pragma unroll
+            for (int q = 0; q < BATCH; ++q) {
+                const int lo = (c0 + q * nthreads + tid) << 4;
+                if (lo >= delta && lo + 16 <= total) {
+                    const int k1 = grp(lo - delta), k2 = grp(lo + 15 - delta);
+                    *reinterpret_cast<uint4*>(lds + lo + gp * k1) = v[q];
+                    if (k2 != k1) *reinterpret_cast<uint4*>(lds + lo + gp * k2) = v[q];
+                }
             }
         }
     }
