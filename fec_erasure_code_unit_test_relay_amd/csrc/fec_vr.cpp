@@ -448,6 +448,7 @@ void VrPlan::control(const uint8_t* pattern, int64_t n_pattern, int T, int B, in
     slow.assign(static_cast<size_t>(P), 0);
     lost = switches = 0;
     steady_packets = 0;
+    transition_packets = 0;
     sum_coding_rate = 0;
     std::vector<std::vector<Reports>> reps;   // per decoder instance, in call order
     std::vector<const DecodeRules*> drules;   // per decoder instance
@@ -513,6 +514,11 @@ void VrPlan::control(const uint8_t* pattern, int64_t n_pattern, int T, int B, in
         if (seq != dec[id].end) throw std::logic_error("vr: decoder calls out of order");
         dec[id].end = seq + 1;
     };
+    auto call_range = [&](int id, int64_t lo, int64_t hi) {  // call(id, s) for s in [lo, hi)
+        if (lo != dec[id].end) throw std::logic_error("vr: decoder calls out of order");
+        dec[id].end = hi;
+    };
+    const bool fast_transitions = !std::getenv("FEC_VR_NO_FAST_TRANSITION");
     // onDecodedMessage (:2403-2436): packets seq - T >= seq_start are reported once.  Instance id
     // reports the seqs [lo, hi) (packets x = seq - dT in [seq_start, P)), extending its newest range.
     auto report_range = [&](int id, int64_t lo, int64_t hi) {
@@ -596,6 +602,89 @@ void VrPlan::control(const uint8_t* pattern, int64_t n_pattern, int T, int B, in
                     ++n_jump;
                     seq = end;
                 }
+            }
+        }
+        // ---- transition stretch: double coding after a switch, every packet received ----
+        // The encoder cannot switch again before its transition ends (transition_flag), so the
+        // feedback only moves the sender's next parameters; the frames differ only in their
+        // counter (and carry the old instance while double coding); the decoder, already on the new
+        // tuple, calls the old and the new instance up to sde, then the new one alone.  Packets
+        // [seq, end) are appended in one pass, up to the transition's last packet (counter == eT),
+        // the next drop and the last packet -- the same state as packet-by-packet below.
+        if (fast_transitions && cur >= 0 && transition_flag && counter_transition >= 1 && counter_transition <= eT &&
+            seq_start >= 0 && latest_seq == seq && sdc < seq && dT == eT && dB == eB && dN == eN &&
+            seq < P + T - 1) {
+            while (dri < drops.size() && drops[dri] < seq) ++dri;
+            const int64_t next_drop = dri < drops.size() ? drops[dri] : INT64_MAX;
+            const int64_t end = std::min({next_drop, seq + (eT - counter_transition + 1), P + T - 1});
+            if (end > seq) {
+                if (adaptive && udp[0] != 0) {  // the start of packet seq's iteration
+                    sT = udp[0];
+                    sB = udp[1];
+                    sN = udp[2];
+                    sT_ack = udp[3];
+                    sB_ack = udp[4];
+                    sN_ack = udp[5];
+                }
+                const float rate1 = static_cast<float>(eT - eN + 1) / (eT - eN + 1 + eB);
+                const float rate2 = static_cast<float>(eT - eN + 1) /
+                                    ((eT - eN + 1 + eB) + (eT - eN_old + 1) + (eT - eN_old + 1 + eB));
+                int64_t old_end = -1;
+                for (int64_t q = seq; q < end; ++q) {
+                    VrFrame fr;
+                    fr.T = eT;
+                    fr.B = eB;
+                    fr.N = eN;
+                    fr.enc_cur = cur;
+                    fr.counter = counter_transition;
+                    if (counter_transition == eT) double_coding_flag = false;
+                    ++counter_transition;
+                    if (old >= 0 && double_coding_flag) {
+                        fr.enc_old = old;
+                        old_end = q + 1;
+                    }
+                    put_rate(1, double_coding_flag ? rate2 : rate1);
+                    put_frame(q, fr);
+                }
+                enc[cur].end = end;
+                if (old_end >= 0) enc[old].end = old_end;
+                // decoder: [seq, split) double decoding (old and new instance), [split, end) the new one
+                const int64_t split = dcf ? std::min(end, sde + 1) : seq;
+                if (split > seq) {
+                    if (dold >= 0) {
+                        call_range(dold, seq, split);
+                        report_range(dold, seq, split);
+                    }
+                    call_range(dcur, seq, split);
+                }
+                if (end > split) {
+                    dcf = false;
+                    call_range(dcur, split, end);
+                    report_range(dcur, split, end);
+                }
+                latest_seq = end;
+                sent = end;
+                transition_packets += end - seq;
+                // the sender's parameters at the start of packet end-1's iteration, and the udp after it
+                if (end - seq >= 2) {
+                    const uint32_t v = fb.value(end - 2);
+                    if (adaptive && (v & 0xff) != 0) {
+                        sT = static_cast<int>(v & 0xff);
+                        sB = static_cast<int>(v >> 8 & 0xff);
+                        sN = static_cast<int>(v >> 16 & 0xff);
+                        sT_ack = eT;
+                        sB_ack = eB;
+                        sN_ack = eN;
+                    }
+                }
+                const uint32_t fbv = fb.value(end - 1);
+                udp[0] = static_cast<uint8_t>(fbv);
+                udp[1] = static_cast<uint8_t>(fbv >> 8);
+                udp[2] = static_cast<uint8_t>(fbv >> 16);
+                udp[3] = static_cast<uint8_t>(eT);
+                udp[4] = static_cast<uint8_t>(eB);
+                udp[5] = static_cast<uint8_t>(eN);
+                seq = end;
             }
         }
         // ---- Application_Layer_Sender::generate_message_and_encode ----

@@ -127,6 +127,7 @@ struct VrPlan {
     int64_t lost = 0, switches = 0;   // "Start double coding at the source" count
     float sum_coding_rate = 0;        // Variable_Rate_FEC_Encoder final_sum_coding_rate
     int64_t steady_packets = 0;       // packets the control loop appended as steady stretches
+    int64_t transition_packets = 0;   // ... and as transition stretches (double coding, no drop)
     double control_ms = 0, decoders_ms = 0;  // wall time of run()'s two phases
     double coding_rate() const { return sent ? sum_coding_rate / static_cast<float>(sent) : 0.0; }
 

@@ -110,6 +110,23 @@ def test_published_adaptive_mds_log_is_not_the_current_code():
     assert v.lost == 2478 and v.fate.min() >= 1
 
 
+@pytest.mark.parametrize("name,mds", [("bin_erasure", False), ("bin_erasure2", False), ("erasure50", True),
+                                      ("erasure90", False)])
+def test_control_loop_transition_stretches_equal_packet_by_packet(monkeypatch, name, mds):
+    """The control loop appends the double-coding stretch after a switch in one pass
+    (fec_vr.cpp, transition stretch); FEC_VR_NO_FAST_TRANSITION walks it packet by packet.  Both
+    give the same schedule: instances, every frame (counter, old instance), fates, reporting
+    decoders, coding rate."""
+    pat = load_pattern(name)
+    monkeypatch.setenv("FEC_VR_NO_FAST_TRANSITION", "1")
+    a = VrPlan(pat, 360000, adaptive_mode_MDS=mds)
+    monkeypatch.delenv("FEC_VR_NO_FAST_TRANSITION")
+    b = VrPlan(pat, 360000, adaptive_mode_MDS=mds)
+    for k in ("encoders", "decoders", "frames", "erased", "fate", "fate_decoder"):
+        assert np.array_equal(getattr(a, k), getattr(b, k)), k
+    assert (a.lost, a.switches, a.sent, a.coding_rate) == (b.lost, b.switches, b.sent, b.coding_rate)
+
+
 def test_schedule_structure(adaptive):
     v = adaptive
     enc, dec, fr = v.encoders, v.decoders, v.frames
