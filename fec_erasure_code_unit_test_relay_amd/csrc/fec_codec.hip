@@ -741,6 +741,9 @@ int guarded(F&& f) {
 struct ServerHost {
     fec::ServerBox* h_box = nullptr;  // pinned, coherent, mapped
     fec::ServerBox* m_box = nullptr;  // its device address
+    uint64_t* h_req = nullptr;        // sealed request block (fec_kernels.h), pinned, coherent, mapped
+    uint64_t* m_req = nullptr;
+    int nunits = 0;                   // its units (the decoder's: with the coefficient units)
     bool on = false;                  // this coder runs on a server (else one launch per call)
     bool live = false;                // a server launch may be running on the coder's stream
 };
@@ -803,7 +806,7 @@ fec_encoder::~fec_encoder() {
     if (s) (void)hipStreamDestroy(s);
     if (d_win) (void)hipFree(d_win);
     for (void* p : {static_cast<void*>(h_stage), static_cast<void*>(h_res), static_cast<void*>(h_done),
-                    static_cast<void*>(sv.h_box)})
+                    static_cast<void*>(sv.h_box), static_cast<void*>(sv.h_req)})
         if (p) (void)hipHostFree(p);
 }
 
@@ -813,7 +816,7 @@ fec_decoder::~fec_decoder() {
     for (void* p : {static_cast<void*>(d_ring), static_cast<void*>(d_coef)})
         if (p) (void)hipFree(p);
     for (void* p : {static_cast<void*>(h_cw), static_cast<void*>(h_coef), static_cast<void*>(h_res),
-                    static_cast<void*>(h_done), static_cast<void*>(sv.h_box)})
+                    static_cast<void*>(h_done), static_cast<void*>(sv.h_box), static_cast<void*>(sv.h_req)})
         if (p) (void)hipHostFree(p);
 }
 
@@ -1129,6 +1132,15 @@ hipError_t server_post(ServerHost& sv, uint32_t ticket, hipStream_t s,
     return hipSuccess;
 }
 
+// The request `words` (n dwords) into the sealed request block from unit `first` on, stamped with
+// `ticket`: one 8-byte store per unit, in decreasing order (the server takes a request when the
+// units of its head carry the ticket, fec_kernels.h; units written earlier are then visible too).
+void server_seal(ServerHost& sv, int first, const uint32_t* words, int n, uint32_t ticket) {
+    volatile uint64_t* u = sv.h_req + first;
+    const uint64_t tk = static_cast<uint64_t>(ticket) << 32;
+    for (int i = n - 1; i >= 0; --i) u[i] = tk | words[i];
+}
+
 // Wait for the server's done ticket (in host memory: no PCIe round trip per poll).  A launch that
 // failed, or a server that stopped (alive = 0) before finishing, is reported after the stream is
 // drained; ten seconds without an answer are reported as an error.
@@ -1176,9 +1188,13 @@ int fec_encoder_create(int max_payload, int T, int B, int N, fec_encoder** out) 
         const int W = std::max(1, g.n - 1), SK = g.S * g.k;
         e->sv.on = server_enabled() && g.CW <= 2048 && g.L <= 1500 && g.k * g.n <= 16 * 32 &&
                    static_cast<int64_t>(W) * SK <= 48 * 1024;
-        if (e->sv.on)
+        if (e->sv.on) {
             HIP_TRY(host_mapped(reinterpret_cast<uint8_t**>(&e->sv.h_box), reinterpret_cast<uint8_t**>(&e->sv.m_box),
                                 sizeof(fec::ServerBox)));
+            e->sv.nunits = fec::kEncReqFields + (g.L + 3) / 4;
+            HIP_TRY(host_mapped(reinterpret_cast<uint8_t**>(&e->sv.h_req), reinterpret_cast<uint8_t**>(&e->sv.m_req),
+                                sizeof(uint64_t) * e->sv.nunits));
+        }
         HIP_TRY(hipDeviceSynchronize());  // the window is zero before the first call's kernel
         *out = e.release();
         return FEC_OK;
@@ -1207,15 +1223,26 @@ int fec_encoder_transmit(fec_encoder* e, const uint8_t* data, int payload, int s
     fec::CodecView v;
     if (int st = fec::codec_view(e->codec.get(), &v)) return st;
     if (e->sv.on) {
-        // the resident server: payload and request into the mailbox, no launch (fec_server.hip)
-        if (payload > 0) std::memcpy(e->h_stage, data, payload);
-        volatile fec::ServerBox* b = e->sv.h_box;
-        b->len = payload;
-        b->seq = seq - e->origin;
+        // the resident server: the request, sealed with its ticket, into the mailbox; no launch
+        // (fec_server.hip)
         const uint32_t ticket = ++e->ticket;
+        {
+            uint32_t w[fec::kEncReqFields + 375];
+            const int64_t rel = seq - e->origin;
+            w[0] = static_cast<uint32_t>(payload);
+            w[1] = static_cast<uint32_t>(rel);
+            w[2] = static_cast<uint32_t>(rel >> 32);
+            const int nw = e->sv.nunits - fec::kEncReqFields;
+            w[fec::kEncReqFields + nw - 1] = 0;
+            if (payload > 0) std::memcpy(w + fec::kEncReqFields, data, payload);
+            std::memset(reinterpret_cast<uint8_t*>(w + fec::kEncReqFields) + payload, 0, 4 * nw - payload);
+            server_seal(e->sv, 0, w, e->sv.nunits, ticket);
+        }
         auto launch = [&](uint32_t last) -> hipError_t {
             fec::EncServerArgs a;
             a.box = e->sv.m_box;
+            a.req = e->sv.m_req;
+            a.nunits = e->sv.nunits;
             a.stage = e->m_stage;
             a.res = e->m_res;
             a.res_len_off = e->res_len_off;
@@ -1280,9 +1307,13 @@ int fec_decoder_create(int max_payload, int T, int B, int N, fec_decoder** out) 
         HIP_TRY(host_mapped(&d->h_done, &d->m_done, 4));
         d->sv.on = server_enabled() && g.k * g.n <= 16 * 32 && g.CW <= 4096 &&
                    static_cast<int64_t>(fec_decoder::RR) * g.CW <= 48 * 1024;
-        if (d->sv.on)
+        if (d->sv.on) {
             HIP_TRY(host_mapped(reinterpret_cast<uint8_t**>(&d->sv.h_box), reinterpret_cast<uint8_t**>(&d->sv.m_box),
                                 sizeof(fec::ServerBox)));
+            d->sv.nunits = fec::kDecReqFields + (g.CW + 3) / 4 + (g.k * g.n + 3) / 4;
+            HIP_TRY(host_mapped(reinterpret_cast<uint8_t**>(&d->sv.h_req), reinterpret_cast<uint8_t**>(&d->sv.m_req),
+                                sizeof(uint64_t) * d->sv.nunits));
+        }
         HIP_TRY(hipDeviceSynchronize());  // the ring is zero before the first call's kernel
         *out = d.release();
         return FEC_OK;
@@ -1323,26 +1354,40 @@ int fec_decoder_receive(fec_decoder* d, const uint8_t* cw, int cw_size, int seq,
         *payload = 0;
         if (er) return FEC_OK;  // nothing to keep, nothing to compute
     }
-    if (!er) {  // FEC_Decoder.cpp:55-63: keep a zero-padded copy of the wire codeword
-        const int sz = std::max(0, std::min(cw_size, g.CW));
-        std::memset(d->h_cw, 0, (g.CW + 3) & ~3);
-        if (sz) std::memcpy(d->h_cw, cw, sz);
-    }
     if (d->sv.on) {
-        // the resident server: codeword / coefficients and request into the mailbox, no launch
-        if (r.fate == fec::kRecovered) std::memcpy(d->h_coef, r.coef, g.k * g.n);
-        volatile fec::ServerBox* b = d->sv.h_box;
-        b->erased = er ? 1 : 0;
-        b->fate = r.fate;
-        b->clamp = r.slow ? 1 : 0;
-        b->seq = rel;
-        b->x = r.x;
+        // the resident server: the request (fields, the zero-padded codeword FEC_Decoder.cpp:55-63,
+        // the coefficients of a recovered packet), sealed with its ticket, into the mailbox; no launch
         fec::CodecView v;
         if (int e = fec::codec_view(d->codec.get(), &v)) return e;
         const uint32_t ticket = ++d->ticket;
+        {
+            const int ncw = (g.CW + 3) / 4, ncf = (g.k * g.n + 3) / 4;
+            uint32_t w[fec::kDecReqFields + 1024 + 128];
+            w[0] = er ? 1u : 0u;
+            w[1] = static_cast<uint32_t>(r.fate);
+            w[2] = r.slow ? 1u : 0u;
+            w[3] = static_cast<uint32_t>(rel);
+            w[4] = static_cast<uint32_t>(rel >> 32);
+            w[5] = static_cast<uint32_t>(r.x);
+            w[6] = static_cast<uint32_t>(static_cast<int64_t>(r.x) >> 32);
+            uint8_t* cwb = reinterpret_cast<uint8_t*>(w + fec::kDecReqFields);
+            const int sz = er ? 0 : std::max(0, std::min(cw_size, g.CW));
+            if (sz) std::memcpy(cwb, cw, sz);
+            std::memset(cwb + sz, 0, 4 * ncw - sz);
+            int nseal = fec::kDecReqFields + ncw;
+            if (r.fate == fec::kRecovered) {
+                uint8_t* cfb = reinterpret_cast<uint8_t*>(w + nseal);
+                std::memset(cfb, 0, 4 * ncf);
+                std::memcpy(cfb, r.coef, g.k * g.n);
+                nseal += ncf;
+            }
+            server_seal(d->sv, 0, w, nseal, ticket);
+        }
         auto launch = [&](uint32_t last) -> hipError_t {
             fec::DecServerArgs a;
             a.box = d->sv.m_box;
+            a.req = d->sv.m_req;
+            a.nunits_main = d->sv.nunits - (g.k * g.n + 3) / 4;
             a.stage = d->m_cw;
             a.coef = d->m_coef;
             a.res = d->m_res;
@@ -1364,6 +1409,11 @@ int fec_decoder_receive(fec_decoder* d, const uint8_t* cw, int cw_size, int seq,
         std::memcpy(payload_out, d->h_res, g.L);
         std::memcpy(payload, d->h_res + d->res_len_off, 4);
         return FEC_OK;
+    }
+    if (!er) {  // FEC_Decoder.cpp:55-63: keep a zero-padded copy of the wire codeword
+        const int sz = std::max(0, std::min(cw_size, g.CW));
+        std::memset(d->h_cw, 0, (g.CW + 3) & ~3);
+        if (sz) std::memcpy(d->h_cw, cw, sz);
     }
     const uint8_t* coef = nullptr;
     if (r.fate == fec::kRecovered) {

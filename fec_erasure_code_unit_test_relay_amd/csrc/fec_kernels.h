@@ -313,8 +313,20 @@ struct ServerBox {
 };
 static_assert(offsetof(ServerBox, len) == 16 && offsetof(ServerBox, x) == 40 && sizeof(ServerBox) == 48,
               "the server loads the 8 field dwords after the 4 control words");
+// A server's sealed request block (pinned, coherent, mapped): unit i = request dword i | ticket << 32,
+// each written by the host as one 8-byte store, the units in decreasing index order and the mailbox's
+// req word after them.  The server's poll reads the first kServerHeadUnits units and the stop word in
+// one round trip and takes the request when every unit it read carries the new ticket; the units past
+// the head were written before it and are read afterwards.  Encoder request: [len, seq lo, seq hi,
+// payload words]; decoder: [erased, fate, clamp, seq lo, seq hi, x lo, x hi, codeword words,
+// coefficient words] (the coefficients are read only for a recovered packet).
+constexpr int kServerHeadUnits = 192;
+constexpr int kEncReqFields = 3;
+constexpr int kDecReqFields = 7;
 struct EncServerArgs {
     ServerBox* box;
+    const uint64_t* req;        // sealed request block: kEncReqFields + ceil(L / 4) units
+    int nunits;
     const uint8_t* stage;       // mapped payload row (dword padded)
     uint8_t* res;               // mapped result row: codeword (dword padded) | trimmed size at res_len_off
     int res_len_off;
@@ -327,6 +339,8 @@ struct EncServerArgs {
 };
 struct DecServerArgs {
     ServerBox* box;
+    const uint64_t* req;        // sealed request block: kDecReqFields + ceil(CW / 4) + ceil(k n / 4) units
+    int nunits_main;            // without the coefficient units
     const uint8_t* stage;       // mapped codeword row (dword padded)
     const uint8_t* coef;        // mapped k x n coefficients (dword padded)
     uint8_t* res;               // mapped result row: payload (dword padded) | length at res_len_off

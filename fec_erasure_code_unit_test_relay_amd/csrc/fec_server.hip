@@ -6,8 +6,10 @@
 // FEC_Encoder.cpp:42-68; FEC_Decoder::onReceive, FEC_Decoder.cpp:49-72): the codeword (payload)
 // comes back from the call.  A launch per call costs more than the reference's whole CPU encode
 // (DESIGN.md §4), so the coder keeps a server workgroup polling its mailbox instead:
-//   host:   payload / codeword -> mapped staging row, request fields, then the request ticket;
-//   server: sees the ticket, does the packet's byte work against its state, which it keeps in LDS
+//   host:   the request (fields and payload / codeword) -> the sealed request block, every 8-byte
+//           unit stamped with the request's ticket (fec_kernels.h), then the request word;
+//   server: one poll reads the block's head and sees the whole request in it (the fields and the
+//           packet arrive with the ticket: no second round trip), does the packet's byte work against its state, which it keeps in LDS
 //           for its whole life (the encoder's n-1 windows, Encoder.cpp:73-95 / the decoder's ring of
 //           received codewords, FEC_Decoder.cpp:55-63), writes the result row, then the done ticket;
 //   host:   polls the done ticket in its own (coherent) memory.
@@ -31,6 +33,9 @@ namespace {
 __device__ __forceinline__ uint32_t sys_load(const uint32_t* p) {
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
+__device__ __forceinline__ uint64_t sys_load64(const uint64_t* p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
 __device__ __forceinline__ void sys_store(uint32_t* p, uint32_t v) {
     __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
@@ -40,49 +45,63 @@ __device__ __forceinline__ uint8_t sgmul(const uint8_t* gexp, const uint8_t* glo
 
 enum : uint32_t { kCmdIdle = 0, kCmdStop = 1, kCmdWork = 2 };
 
-// Thread 0 waits for the next request (a ticket other than `last`), the stop word or the idle limit;
-// the command lands in `cmd` for the whole workgroup.
-__device__ __forceinline__ uint32_t server_wait(ServerBox* box, uint32_t last, int64_t idle_ticks, uint32_t* cmd,
-                                                uint32_t* ticket) {
-    if (threadIdx.x == 0) {
-        uint32_t c = kCmdIdle, t = last;
+// Wave 0 waits for request last + 1: each poll reads the head of the sealed request block (lane l:
+// units l, l + 64, l + 128) and the stop word in one round trip, and takes the request when every
+// head unit carries the new ticket; the head's request dwords land in reqw (LDS).  On the stop word
+// or the idle limit it ends the launch (exit handshake: announce, then one more look at the request
+// word; a request posted meanwhile is served, its units complete since they were written first).
+__device__ __forceinline__ uint32_t server_wait(ServerBox* box, const uint64_t* req, int nhead, uint32_t last,
+                                                int64_t idle_ticks, uint32_t* reqw, uint32_t* cmd) {
+    if (threadIdx.x < 64) {
+        const int lane = threadIdx.x;
+        const uint32_t want = last + 1;
+        uint32_t c = kCmdIdle;
         const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
         for (;;) {
-            // both words in one round trip
+            uint64_t u[3];
+#pragma unroll
+            for (int q = 0; q < 3; ++q) {
+                const int i = lane + 64 * q;
+                u[q] = i < nhead ? sys_load64(req + i) : static_cast<uint64_t>(want) << 32;
+            }
             const uint32_t st = sys_load(&box->stop);
-            t = sys_load(&box->req);
+            bool ok = true;
+#pragma unroll
+            for (int q = 0; q < 3; ++q) ok = ok && static_cast<uint32_t>(u[q] >> 32) == want;
             if (st) {
                 c = kCmdStop;
                 break;
             }
-            if (t != last) {
+            if (__all(ok)) {
+#pragma unroll
+                for (int q = 0; q < 3; ++q) {
+                    const int i = lane + 64 * q;
+                    if (i < nhead) reqw[i] = static_cast<uint32_t>(u[q]);
+                }
                 c = kCmdWork;
                 break;
             }
             if (static_cast<int64_t>(__builtin_amdgcn_s_memrealtime() - t0) > idle_ticks) {
-                // exit handshake: announce, then one more look (a request posted meanwhile is served)
-                sys_store(&box->alive, 0u);
+                if (lane == 0) sys_store(&box->alive, 0u);
                 __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "");
-                t = sys_load(&box->req);
-                if (t != last && !sys_load(&box->stop)) {
-                    sys_store(&box->alive, 1u);
+                if (sys_load(&box->req) == want && !sys_load(&box->stop)) {
+                    if (lane == 0) sys_store(&box->alive, 1u);
+#pragma unroll
+                    for (int q = 0; q < 3; ++q) {
+                        const int i = lane + 64 * q;
+                        if (i < nhead) reqw[i] = static_cast<uint32_t>(sys_load64(req + i));
+                    }
                     c = kCmdWork;
                 }
                 break;
             }
             __builtin_amdgcn_s_sleep(2);
         }
-        if (c == kCmdWork) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // the request's fields and rows
-        *cmd = c;
-        *ticket = t;
+        if (c == kCmdWork) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // the units past the head
+        if (lane == 0) *cmd = c;
     }
     __syncthreads();
     return *cmd;
-}
-
-// The request's 8 field dwords (len, erased, fate, clamp, seq, x), one per thread 0..7.
-__device__ __forceinline__ void load_fields(const ServerBox* box, uint32_t* fld) {
-    if (threadIdx.x < 8) fld[threadIdx.x] = sys_load(reinterpret_cast<const uint32_t*>(&box->len) + threadIdx.x);
 }
 
 // After every thread's result stores: the done ticket, behind a system-scope release.
@@ -106,12 +125,11 @@ __global__ __launch_bounds__(256) void fec_encoder_server_kernel(EncServerArgs a
     __shared__ uint8_t gexp[512];
     __shared__ uint8_t glog[256];
     __shared__ uint8_t Gs[16 * 32];
-    __shared__ uint32_t prow[376];  // payload row (L <= 1500)
+    __shared__ uint32_t reqw[kEncReqFields + 375];  // the request: fields, payload words (L <= 1500)
     __shared__ uint32_t cwl[512];   // codeword (CW <= 2048)
     __shared__ int ro[32];          // window offset of packet seq - d (-1: before the coder's origin)
     __shared__ int last_nz;
-    __shared__ uint32_t cmd, ticket;
-    __shared__ uint32_t fld[8];
+    __shared__ uint32_t cmd;
     const int tid = threadIdx.x;
     const int L = a.L, k = a.k, n = a.n, CW = a.CW, SK = a.SK, W = a.W;
     for (int i = tid; i < 512; i += 256) gexp[i] = a.gf[i];
@@ -120,19 +138,17 @@ __global__ __launch_bounds__(256) void fec_encoder_server_kernel(EncServerArgs a
     for (int b = tid; b < W * SK; b += 256) win[b] = a.win_home[b];
     __syncthreads();
     uint32_t last = a.last;
-    while (server_wait(a.box, last, a.idle_ticks, &cmd, &ticket) == kCmdWork) {
-        const uint32_t tk = ticket;
-        // the request's fields (8 dwords after the control words) and the payload row, all loads
-        // in flight together: one PCIe round trip
-        load_fields(a.box, fld);
-        for (int w = tid; 4 * w < L; w += 256) prow[w] = sys_load(reinterpret_cast<const uint32_t*>(a.stage) + w);
+    const int nhead = min(a.nunits, kServerHeadUnits);
+    while (server_wait(a.box, a.req, nhead, last, a.idle_ticks, reqw, &cmd) == kCmdWork) {
+        const uint32_t tk = last + 1;
+        for (int i = nhead + tid; i < a.nunits; i += 256) reqw[i] = static_cast<uint32_t>(sys_load64(a.req + i));
         if (tid == 0) last_nz = -1;
         __syncthreads();
-        const int ln = min(max(static_cast<int>(fld[0]), 0), L);
-        const int64_t seq = static_cast<int64_t>(fld[4]) | (static_cast<int64_t>(fld[5]) << 32);
+        const int ln = min(max(static_cast<int>(reqw[0]), 0), L);
+        const int64_t seq = static_cast<int64_t>(reqw[1]) | (static_cast<int64_t>(reqw[2]) << 32);
         if (tid < 32) ro[tid] = (tid >= 1 && seq - tid >= 0) ? static_cast<int>((seq - tid) % W) * SK : -1;
         __syncthreads();
-        const uint8_t* pay = reinterpret_cast<const uint8_t*>(prow);
+        const uint8_t* pay = reinterpret_cast<const uint8_t*>(reqw + kEncReqFields);
         auto xbyte = [&](int b) -> uint8_t {  // [len_hi, len_lo, payload, zero pad] (Encoder.cpp:75-83)
             return b == 0 ? static_cast<uint8_t>(ln >> 8)
                           : b == 1 ? static_cast<uint8_t>(ln & 0xff) : (b - 2 < ln ? pay[b - 2] : 0);
@@ -177,8 +193,8 @@ __global__ __launch_bounds__(256) void fec_decoder_server_kernel(DecServerArgs a
     __shared__ uint8_t gexp[512];
     __shared__ uint8_t glog[256];
     __shared__ uint8_t coef[16 * 32];
-    __shared__ uint32_t cmd, ticket;
-    __shared__ uint32_t fld[8];
+    __shared__ uint32_t reqw[kDecReqFields + 1024];  // the request: fields, codeword words (CW <= 4096)
+    __shared__ uint32_t cmd;
     __shared__ int s_hdr;
     const int tid = threadIdx.x;
     const int L = a.L, k = a.k, n = a.n, CW = a.CW, RR = a.RR;
@@ -187,34 +203,23 @@ __global__ __launch_bounds__(256) void fec_decoder_server_kernel(DecServerArgs a
     for (int b = tid; b < RR * CW; b += 256) ring[b] = a.ring_home[b];
     __syncthreads();
     uint32_t last = a.last;
-    while (server_wait(a.box, last, a.idle_ticks, &cmd, &ticket) == kCmdWork) {
-        const uint32_t tk = ticket;
-        // the request's fields, the staged codeword and the coefficients, all loads in flight
-        // together (one PCIe round trip); the codeword and coefficients are used only when the
-        // fields say so
-        load_fields(a.box, fld);
-        uint32_t cwv[4];
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const int w = tid + 256 * q;
-            cwv[q] = 4 * w < CW ? sys_load(reinterpret_cast<const uint32_t*>(a.stage) + w) : 0u;
-        }
-        for (int w = tid; 4 * w < k * n; w += 256)
-            reinterpret_cast<uint32_t*>(coef)[w] = sys_load(reinterpret_cast<const uint32_t*>(a.coef) + w);
+    const int nhead = min(a.nunits_main, kServerHeadUnits);
+    while (server_wait(a.box, a.req, nhead, last, a.idle_ticks, reqw, &cmd) == kCmdWork) {
+        const uint32_t tk = last + 1;
+        // the units past the head (large codewords); the coefficients only for a recovered packet
+        for (int i = nhead + tid; i < a.nunits_main; i += 256) reqw[i] = static_cast<uint32_t>(sys_load64(a.req + i));
+        const int fate = static_cast<int>(reqw[1]);
+        if (fate == kRecovered)
+            for (int w = tid; 4 * w < k * n; w += 256)
+                reinterpret_cast<uint32_t*>(coef)[w] = static_cast<uint32_t>(sys_load64(a.req + a.nunits_main + w));
         __syncthreads();
-        const int64_t seq = static_cast<int64_t>(fld[4]) | (static_cast<int64_t>(fld[5]) << 32);
-        const int64_t x = static_cast<int64_t>(fld[6]) | (static_cast<int64_t>(fld[7]) << 32);
-        const int fate = static_cast<int>(fld[2]);
-        const int clamp = static_cast<int>(fld[3]);
-        if (!fld[1]) {  // the decoder keeps its own copy of the (zero-padded) codeword
+        const int64_t seq = static_cast<int64_t>(reqw[3]) | (static_cast<int64_t>(reqw[4]) << 32);
+        const int64_t x = static_cast<int64_t>(reqw[5]) | (static_cast<int64_t>(reqw[6]) << 32);
+        const int clamp = static_cast<int>(reqw[2]);
+        if (!reqw[0]) {  // the decoder keeps its own copy of the (zero-padded) codeword
             uint8_t* dst = ring + (seq % RR) * CW;
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                const int w = tid + 256 * q;
-#pragma unroll
-                for (int e = 0; e < 4; ++e)
-                    if (4 * w + e < CW) dst[4 * w + e] = static_cast<uint8_t>(cwv[q] >> (8 * e));
-            }
+            const uint8_t* src = reinterpret_cast<const uint8_t*>(reqw + kDecReqFields);
+            for (int b = tid; b < CW; b += 256) dst[b] = src[b];
         }
         __syncthreads();
         // symbol (s, q) of packet sp from the ring (sp < 0: a zero row, never with a non-zero coefficient)

@@ -351,6 +351,30 @@ def test_streaming_api_matches_oracle():
         assert p == op and (got == ogot).all(), t
 
 
+def test_streaming_api_across_server_idle_exits():
+    """The per-packet coders' resident servers exit after 50 ms without a request (state back to
+    HBM) and are relaunched by the next call (fec_server.hip, exit handshake): calls separated by
+    pauses longer than that give the oracle's outputs, recovered packets included."""
+    import time
+    T, B, N = 10, 3, 3
+    P = 120
+    pat = np.zeros(P + T, dtype=np.uint8)
+    pat[[20, 21, 22, 60, 61, 90]] = 1
+    enc, dec = fec.FEC_Encoder(L, T, B, N), fec.FEC_Decoder(L, T, B, N)
+    oe, od = oracle.Encoder(L, T, B, N), oracle.Decoder(L, T, B, N)
+    src = oracle.fill_payload(0, P + T, L, SEED)
+    for t in range(P + T):
+        if t in (5, 31, 70, 100):
+            time.sleep(0.12)
+        wire, size = enc.onTransmit(src[t], L, t)
+        ocw, osize = oe.onTransmit(src[t], L, t)
+        assert size == osize and (wire == ocw[:size]).all(), t
+        erased = bool(pat[t])
+        got, p = dec.onReceive(None if erased else wire, size, t, erased)
+        ogot, op = od.onReceive(None if erased else ocw, osize, t, erased)
+        assert p == op and (got == ogot).all(), t
+
+
 def test_cpp_dropin_program(tmp_path):
     """The reference-named C++ classes (include/fec_amd_dropin.h) in a host program."""
     src = os.path.join(ROOT, "tests", "cpp", "dropin_test.cpp")
