@@ -101,7 +101,7 @@ struct fec_codec {
     }
     int copy_lds(int tp) const { return round16(tp * g.CW) + 2 * ((g.L + 2 + 7) & ~7) + 4 * tp; }
     int ns4() const { return (g.S + 3) / 4; }
-    int copyf_raw(int tp) const { return round16(16 + tp * g.CW + fec::kCopyRowPadMax * ((tp + 15) / 16) + 4 * g.n + 16); }
+    int copyf_raw(int tp) const { return round16(16 + tp * g.CW + 4 * g.n + 16); }
     int copyf_lds(int tp) const { return copyf_raw(tp) + round16(tp * g.L) + 4 * tp + tp + g.T + 16; }
 
     int begin(int kernel, hipStream_t s, hipEvent_t* stop) {
@@ -523,8 +523,11 @@ int launch_copy(fec_codec* c, const uint8_t* d_cw, const uint8_t* d_er, int64_t 
         // (tools/step_ab.py, same process, profiles/r02/decode_diag/copy_nt_ab.txt)
         fa.nt = 1;
         if (const char* v = std::getenv("FEC_COPY_NT")) fa.nt = std::atoi(v) ? 1 : 0;
-        fa.row_pad = fec::copy_row_pad(g.CW);
-        if (const char* v = std::getenv("FEC_COPY_ROW_PAD")) fa.row_pad = std::max(0, std::min(fec::kCopyRowPadMax, std::atoi(v) & ~3));
+        // (Tried: 32 bytes of LDS padding after every 16 tile rows, which gives the 32 lanes of a
+        // ds_read_b32 group distinct banks -- conflict cycles 3.81 M -> 31 k per launch -- but the
+        // padded staging made the step 2.2 % slower in the same process, 0.3228 vs 0.3157 ms:
+        // profiles/r03/r03v_copy_row_pad_*.txt.  2-way conflicts cost one LDS cycle per 32-lane
+        // group; the copy is bound by its HBM traffic and load latency, not by the LDS.)
         const int64_t blocks = (Pout + fa.TP - 1) / fa.TP;
         // 256 threads (one per (packet, group) item of the tile rounded up to waves, 320 at (10,3,3),
         // measured slower in the step: 0.3402 vs 0.3235 ms, profiles/r03/r03y_copy_threads_ab.txt)

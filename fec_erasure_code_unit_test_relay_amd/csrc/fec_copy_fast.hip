@@ -29,13 +29,10 @@ __global__ __launch_bounds__(256) void fec_copy_fast_kernel(CopyFastArgs a) {
 
     const uint8_t* gA = a.cw + x0 * CW;
     const int delta = static_cast<int>(reinterpret_cast<uintptr_t>(gA) & 15);
-    // rows at stride CW = 418 put 2 lanes of 32 on a bank (ds_read_b32, (a/4) mod 32); 32 bytes
-    // of padding after every 16 rows give the lanes of rows t and t + 16 distinct banks
-    const int gp = (delta & 3) == 0 ? a.row_pad : 0, G = 16 * CW;
     if (a.nt)
-        stage_to_lds_padded<8, true>(raw, gA - delta, delta, delta + ntile * CW, tid, NT, G, gp);
+        stage_to_lds<8, true>(raw, gA - delta, delta, delta + ntile * CW, tid, NT);
     else
-        stage_to_lds_padded<8>(raw, gA - delta, delta, delta + ntile * CW, tid, NT, G, gp);
+        stage_to_lds<8>(raw, gA - delta, delta, delta + ntile * CW, tid, NT);
     for (int i = tid; i < ntile + T; i += NT) erw[i] = a.er[x0 + i];  // x0+ntile+T-1 < P
     __syncthreads();
     phase_stamp(a.stamps, blockIdx.x, 1);
@@ -43,7 +40,7 @@ __global__ __launch_bounds__(256) void fec_copy_fast_kernel(CopyFastArgs a) {
     for (int t = tid; t < ntile; t += NT) {
         int ln = 0, copy = 0;
         if (!erw[t]) {
-            const uint8_t* row = raw + delta + t * CW + gp * (t >> 4);
+            const uint8_t* row = raw + delta + t * CW;
             // header bytes h = 0, 1: sub-stream 0 position 0 and h=1 -> (1/k)*n + 1%k
             const int hdr = row[0] * 256 + row[(1 / K) * n + 1 % K];
             bool slow = false;
@@ -62,7 +59,7 @@ __global__ __launch_bounds__(256) void fec_copy_fast_kernel(CopyFastArgs a) {
         const int cl = clen[t];
         uint32_t W[K + 1];  // systematic bytes of the group: byte e*K+i = position i of sub-stream 4g+e
         if (cl > 0) {
-            const int off = delta + t * CW + gp * (t >> 4) + 4 * n * g;
+            const int off = delta + t * CW + 4 * n * g;
             const int a4 = off & ~3;
             uint32_t D[n + 1];
 #pragma unroll
@@ -132,21 +129,6 @@ __global__ __launch_bounds__(256) void fec_copy_fast_kernel(CopyFastArgs a) {
                 *reinterpret_cast<uint32_t*>(dst + o) = *reinterpret_cast<const uint32_t*>(xo + o);
     }
     phase_stamp(a.stamps, blockIdx.x, 3);
-}
-
-int copy_row_pad(int CW) {
-    int best = 0, best_extra = 1 << 30;
-    for (int gp = 0; gp <= kCopyRowPadMax; gp += 4) {
-        int cnt[32] = {};
-        for (int t = 0; t < 32; ++t) ++cnt[((t * CW + gp * (t >> 4)) >> 2) & 31];
-        int extra = 0;
-        for (int b = 0; b < 32; ++b) extra += cnt[b] > 1 ? cnt[b] - 1 : 0;
-        if (extra < best_extra) {
-            best_extra = extra;
-            best = gp;
-        }
-    }
-    return best;
 }
 
 #define FEC_COPY_FAST_LIST(X) \

@@ -92,67 +92,6 @@ __device__ __forceinline__ void stage_to_lds(uint8_t* lds, const uint8_t* gbase,
     }
 }
 
-// stage_to_lds with gp bytes of padding in LDS after every G bytes of the range (byte b >= delta
-// lands at b + gp * ((b - delta) / G)): rows at a stride that maps 2 lanes to a bank get distinct
-// banks when every 16 rows shift by gp.  With gp != 0, delta and G must be multiples of 4 (a dword
-// never straddles a boundary); a 16-byte chunk that straddles one is stored at both positions.
-template <int BATCH, bool NT = false>
-__device__ __forceinline__ void stage_to_lds_padded(uint8_t* lds, const uint8_t* gbase, int delta, int total,
-                                                    int tid, int nthreads, int G, int gp) {
-    if (gp == 0) {
-        stage_to_lds<BATCH, NT>(lds, gbase, delta, total, tid, nthreads);
-        return;
-    }
-    // (x + 0.5) / G is never within float rounding of an integer for x < 2^24: floor is exact
-    const float rG = 1.0f / static_cast<float>(G);
-    auto grp = [&](int x) { return static_cast<int>((static_cast<float>(x) + 0.5f) * rG); };
-    auto at = [&](int b) { return b + gp * grp(b - delta); };
-    const int nchunks = (total + 15) >> 4;
-    const bool straddle = (delta & 15) != 0;  // boundaries are at delta + k G, G a multiple of 16
-    for (int c0 = 0; c0 < nchunks; c0 += nthreads * BATCH) {
-        uint4 v[BATCH];
-#pragma unroll
-        for (int q = 0; q < BATCH; ++q) {
-            const int lo = (c0 + q * nthreads + tid) << 4;
-            const bool full = lo >= delta && lo + 16 <= total;
-            if constexpr (NT) {
-                v[q] = full ? nt_load16(gbase + lo) : make_uint4(0, 0, 0, 0);
-            } else {
-                v[q] = full ? *reinterpret_cast<const uint4*>(gbase + lo) : make_uint4(0, 0, 0, 0);
-            }
-        }
-        if (!straddle) {
-#pragma unroll
-            for (int q = 0; q < BATCH; ++q) {
-                const int lo = (c0 + q * nthreads + tid) << 4;
-                if (lo >= delta && lo + 16 <= total) *reinterpret_cast<uint4*>(lds + at(lo)) = v[q];
-            }
-        } else {
-#pragma unroll
-            for (int q = 0; q < BATCH; ++q) {
-                const int lo = (c0 + q * nthreads + tid) << 4;
-                if (lo >= delta && lo + 16 <= total) {
-                    const int k1 = grp(lo - delta), k2 = grp(lo + 15 - delta);
-                    *reinterpret_cast<uint4*>(lds + lo + gp * k1) = v[q];
-                    if (k2 != k1) *reinterpret_cast<uint4*>(lds + lo + gp * k2) = v[q];
-                }
-            }
-        }
-    }
-    if (tid == 0) {
-        for (int b = delta; b < total && (b & 3); ++b) lds[at(b)] = gbase[b];
-        for (int b = total & ~3; b < total && b >= ((delta + 3) & ~3); ++b) lds[at(b)] = gbase[b];
-    }
-    for (int o = tid * 4; o < 32; o += nthreads * 4) {
-        const int lo16 = delta & ~15, hi16 = total & ~15;
-        const int oa = lo16 + o, ob = hi16 + (o - 16);
-        if (o < 16 && oa >= delta && oa + 4 <= total && !(lo16 >= delta && lo16 + 16 <= total))
-            *reinterpret_cast<uint32_t*>(lds + at(oa)) = *reinterpret_cast<const uint32_t*>(gbase + oa);
-        if (o >= 16 && ob >= delta && ob + 4 <= total && hi16 != lo16)
-            *reinterpret_cast<uint32_t*>(lds + at(ob)) = *reinterpret_cast<const uint32_t*>(gbase + ob);
-    }
-}
-
 // Diagnostic phase stamp (s_memtime, shader clock) of workgroup `wg`, slot `k` of 8; only when a
 // stamp buffer is given.  Stamps never feed an output.
 __device__ __forceinline__ void phase_stamp(uint64_t* stamps, int wg, int k) {

@@ -133,7 +133,6 @@ const void* fec_encode_tile_kernel_for(int k, int np, int L);
 // fec_encode_tile_kernel<k, n-k, 0> with segment mode (EncTileArgs::seg) compiled in, else nullptr.
 const void* fec_encode_tile_seg_kernel_for(int k, int np);
 
-constexpr int kCopyRowPadMax = 124;  // fec_copy_fast_kernel: LDS bytes after every 16 tile rows, at most
 struct CopyFastArgs {
     const uint8_t* cw;
     const uint8_t* er;
@@ -146,11 +145,7 @@ struct CopyFastArgs {
     uint64_t* stamps;           // diagnostics: per-workgroup phase timestamps (null = off)
     int skip_erased;            // 1: leave erased packets' rows and lengths to fec_recover_kernel
     int nt;                     // 1: non-temporal codeword loads and payload stores
-    int row_pad;                // LDS bytes after every 16 tile rows (copy_row_pad(CW)), 0..kCopyRowPadMax
 };
-// The padding that spreads the copy's ds_read_b32 lanes (32 rows of one group at stride CW, lane
-// group of 32, bank (a/4) mod 32) over the most banks.
-int copy_row_pad(int CW);
 
 // fec_copy_fast_kernel<k, n-k> for the instantiated pairs (fec_copy_fast.hip), else nullptr.
 const void* fec_copy_fast_kernel_for(int k, int np);
