@@ -973,7 +973,7 @@ int fec_codec_info(const fec_codec* c, char* buf, size_t size) {
     char enc[64];
     const int np = c->g.n - c->g.k;
     if (c->tile_kernel && (c->encode_path == 0 || c->encode_path == 5))
-        std::snprintf(enc, sizeof(enc), "fec_encode_tile_kernel<%d, %d, %d>", c->g.k, np,
+        std::snprintf(enc, sizeof(enc), "fec_encode_tile_kernel<%d, %d, %d, false>", c->g.k, np,
                       c->tile_kernel == fec::fec_encode_tile_kernel_for(c->g.k, np, 0) ? 0 : c->g.L);
     else
         std::snprintf(enc, sizeof(enc), "fec_encode_kernel");

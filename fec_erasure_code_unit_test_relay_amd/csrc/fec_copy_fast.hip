@@ -12,6 +12,10 @@
 
 namespace fec {
 
+#ifndef FEC_COPY_STAGE_BATCH
+#define FEC_COPY_STAGE_BATCH 8  // 16-byte loads in flight per thread while staging the tile
+#endif
+
 template <int K, int NP>
 __global__ __launch_bounds__(256) void fec_copy_fast_kernel(CopyFastArgs a) {
     constexpr int n = K + NP;
@@ -30,9 +34,9 @@ __global__ __launch_bounds__(256) void fec_copy_fast_kernel(CopyFastArgs a) {
     const uint8_t* gA = a.cw + x0 * CW;
     const int delta = static_cast<int>(reinterpret_cast<uintptr_t>(gA) & 15);
     if (a.nt)
-        stage_to_lds<8, true>(raw, gA - delta, delta, delta + ntile * CW, tid, NT);
+        stage_to_lds<FEC_COPY_STAGE_BATCH, true>(raw, gA - delta, delta, delta + ntile * CW, tid, NT);
     else
-        stage_to_lds<8>(raw, gA - delta, delta, delta + ntile * CW, tid, NT);
+        stage_to_lds<FEC_COPY_STAGE_BATCH>(raw, gA - delta, delta, delta + ntile * CW, tid, NT);
     for (int i = tid; i < ntile + T; i += NT) erw[i] = a.er[x0 + i];  // x0+ntile+T-1 < P
     __syncthreads();
     phase_stamp(a.stamps, blockIdx.x, 1);
