@@ -21,6 +21,28 @@
 #include "fec_amd.h"
 #include "fec_kernels.h"
 
+// FEC_VR_PROFILE (diagnostic builds only): cycle counts of the control loop's parts --
+// 0 steady stretch check, 1 transition stretch, 2 sender + encoder, 3 feedback, 4 decoder, 5 loop top.
+#ifdef FEC_VR_PROFILE
+#include <x86intrin.h>
+#define FEC_VR_PROF_DECL uint64_t prof_c[6] = {}, prof_t = __rdtsc();
+#define FEC_VR_PROF(k)                 \
+    {                                  \
+        const uint64_t t_ = __rdtsc(); \
+        prof_c[k] += t_ - prof_t;      \
+        prof_t = t_;                   \
+    }
+#define FEC_VR_PROF_PRINT                                                                                  \
+    std::fprintf(stderr, "vr control Mcycles: steady %.3f transition %.3f sender %.3f feedback %.3f "      \
+                         "decoder %.3f top %.3f\n",                                                        \
+                 prof_c[0] * 1e-6, prof_c[1] * 1e-6, prof_c[2] * 1e-6, prof_c[3] * 1e-6, prof_c[4] * 1e-6, \
+                 prof_c[5] * 1e-6);
+#else
+#define FEC_VR_PROF_DECL
+#define FEC_VR_PROF(k)
+#define FEC_VR_PROF_PRINT
+#endif
+
 namespace fec {
 
 // ---- Parameter_Estimator::estimate (Parameter_Estimator.cpp:58-190) -------------------------
@@ -557,8 +579,10 @@ void VrPlan::control(const uint8_t* pattern, int64_t n_pattern, int T, int B, in
     clock_gettime(CLOCK_THREAD_CPUTIME_ID, &cpu0);
     rusage ru0{};
     getrusage(RUSAGE_THREAD, &ru0);
+    FEC_VR_PROF_DECL
     for (int64_t seq = 0;; ++seq) {
         ++n_iter;
+        FEC_VR_PROF(5)
         // ---- steady stretch: the same frame, every packet received, nothing switching ----
         // Every branch below is then fixed: the feedback repeats (no change in the feedback
         // stream), the encoder has no switch to make and no transition running, the decoder has
@@ -604,6 +628,7 @@ void VrPlan::control(const uint8_t* pattern, int64_t n_pattern, int T, int B, in
                 }
             }
         }
+        FEC_VR_PROF(0)
         // ---- transition stretch: double coding after a switch, every packet received ----
         // The encoder cannot switch again before its transition ends (transition_flag), so the
         // feedback only moves the sender's next parameters; the frames differ only in their
@@ -687,6 +712,7 @@ void VrPlan::control(const uint8_t* pattern, int64_t n_pattern, int T, int B, in
                 seq = end;
             }
         }
+        FEC_VR_PROF(1)
         // ---- Application_Layer_Sender::generate_message_and_encode ----
         if (adaptive && udp[0] != 0) {
             sT = udp[0];
@@ -751,8 +777,10 @@ void VrPlan::control(const uint8_t* pattern, int64_t n_pattern, int T, int B, in
         sent = seq + 1;
 
         // ---- Application_Layer_Receiver::receive_message_and_decode ----
+        FEC_VR_PROF(2)
         if (drop) continue;  // artificial erasure: returns -1, feedback unchanged
         const uint32_t fbv = fb.value(seq);  // the estimators' feedback after seq
+        FEC_VR_PROF(3)
         // ---- Variable_Rate_FEC_Decoder::decode ----
         if (seq_start == -1) {  // initialize_decoder (:2478-2494)
             seq_start = 0;
@@ -800,6 +828,7 @@ void VrPlan::control(const uint8_t* pattern, int64_t n_pattern, int T, int B, in
             }
             latest_seq = seq + 1;
         }
+        FEC_VR_PROF(4)
         udp[0] = static_cast<uint8_t>(fbv);
         udp[1] = static_cast<uint8_t>(fbv >> 8);
         udp[2] = static_cast<uint8_t>(fbv >> 16);
@@ -820,6 +849,7 @@ void VrPlan::control(const uint8_t* pattern, int64_t n_pattern, int T, int B, in
         clock_gettime(CLOCK_THREAD_CPUTIME_ID, &cpu1);
         rusage ru1{};
         getrusage(RUSAGE_THREAD, &ru1);
+        FEC_VR_PROF_PRINT
         std::fprintf(stderr, "vr control: loop thread cpu %.3f ms (user %.3f sys %.3f), %ld minor faults\n",
                      (cpu1.tv_sec - cpu0.tv_sec) * 1e3 + (cpu1.tv_nsec - cpu0.tv_nsec) * 1e-6,
                      (ru1.ru_utime.tv_sec - ru0.ru_utime.tv_sec) * 1e3 + (ru1.ru_utime.tv_usec - ru0.ru_utime.tv_usec) * 1e-3,
