@@ -541,6 +541,21 @@ void VrPlan::control(const uint8_t* pattern, int64_t n_pattern, int T, int B, in
         dec[id].end = hi;
     };
     const bool fast_transitions = !std::getenv("FEC_VR_NO_FAST_TRANSITION");
+    // Stretches run through dropped packets (FEC_VR_NO_DROP_STRETCH: they end before a drop): a drop
+    // changes nothing the loop tracks but the receiver's view -- the next received packet calls and
+    // reports the missing ones exactly as if they had arrived, and the feedback after it is bounded by
+    // the feedback stream's next change -- so a stretch only has to end on a received packet.
+    const bool drop_stretch = !std::getenv("FEC_VR_NO_DROP_STRETCH");
+    // one past the last received packet in [lo, hi), or lo if every one of them drops
+    auto received_end = [&](int64_t lo, int64_t hi) {
+        auto j = std::lower_bound(drops.begin(), drops.end(), hi);
+        int64_t e = hi;
+        while (e > lo && j != drops.begin() && *(j - 1) == e - 1) {
+            --j;
+            --e;
+        }
+        return e;
+    };
     // onDecodedMessage (:2403-2436): packets seq - T >= seq_start are reported once.  Instance id
     // reports the seqs [lo, hi) (packets x = seq - dT in [seq_start, P)), extending its newest range.
     auto report_range = [&](int id, int64_t lo, int64_t hi) {
@@ -599,7 +614,8 @@ void VrPlan::control(const uint8_t* pattern, int64_t n_pattern, int T, int B, in
                 while (dri < drops.size() && drops[dri] < seq) ++dri;
                 const int64_t next_drop = dri < drops.size() ? drops[dri] : INT64_MAX;
                 const int64_t next_fb = fb.next(seq);
-                const int64_t end = std::min({next_drop, next_fb, P + T - 1});
+                const int64_t end = drop_stretch ? received_end(seq, std::min(next_fb, P + T - 1))
+                                                 : std::min({next_drop, next_fb, P + T - 1});
                 if (end > seq) {
                     if (adaptive && udp[0] != 0) {
                         sT = udp[0];
@@ -641,7 +657,8 @@ void VrPlan::control(const uint8_t* pattern, int64_t n_pattern, int T, int B, in
             seq < P + T - 1) {
             while (dri < drops.size() && drops[dri] < seq) ++dri;
             const int64_t next_drop = dri < drops.size() ? drops[dri] : INT64_MAX;
-            const int64_t end = std::min({next_drop, seq + (eT - counter_transition + 1), P + T - 1});
+            const int64_t tend = std::min(seq + (eT - counter_transition + 1), P + T - 1);
+            const int64_t end = drop_stretch ? received_end(seq, tend) : std::min(next_drop, tend);
             if (end > seq) {
                 if (adaptive && udp[0] != 0) {  // the start of packet seq's iteration
                     sT = udp[0];
@@ -690,9 +707,10 @@ void VrPlan::control(const uint8_t* pattern, int64_t n_pattern, int T, int B, in
                 latest_seq = end;
                 sent = end;
                 transition_packets += end - seq;
-                // the sender's parameters at the start of packet end-1's iteration, and the udp after it
-                if (end - seq >= 2) {
-                    const uint32_t v = fb.value(end - 2);
+                // the sender's parameters at the start of packet end-1's iteration (the udp after the
+                // last packet received before it), and the udp after end-1 (received)
+                if (const int64_t r = received_end(seq, end - 1); r > seq) {
+                    const uint32_t v = fb.value(r - 1);
                     if (adaptive && (v & 0xff) != 0) {
                         sT = static_cast<int>(v & 0xff);
                         sB = static_cast<int>(v >> 8 & 0xff);

@@ -113,14 +113,16 @@ def test_published_adaptive_mds_log_is_not_the_current_code():
 @pytest.mark.parametrize("name,mds", [("bin_erasure", False), ("bin_erasure2", False), ("erasure50", True),
                                       ("erasure90", False)])
 def test_control_loop_transition_stretches_equal_packet_by_packet(monkeypatch, name, mds):
-    """The control loop appends the double-coding stretch after a switch in one pass
-    (fec_vr.cpp, transition stretch); FEC_VR_NO_FAST_TRANSITION walks it packet by packet.  Both
-    give the same schedule: instances, every frame (counter, old instance), fates, reporting
-    decoders, coding rate."""
+    """The control loop appends the double-coding stretch after a switch in one pass, and runs
+    steady and transition stretches through dropped packets (fec_vr.cpp); FEC_VR_NO_FAST_TRANSITION
+    and FEC_VR_NO_DROP_STRETCH walk those packets one by one.  Both give the same schedule:
+    instances, every frame (counter, old instance), fates, reporting decoders, coding rate."""
     pat = load_pattern(name)
     monkeypatch.setenv("FEC_VR_NO_FAST_TRANSITION", "1")
+    monkeypatch.setenv("FEC_VR_NO_DROP_STRETCH", "1")
     a = VrPlan(pat, 360000, adaptive_mode_MDS=mds)
     monkeypatch.delenv("FEC_VR_NO_FAST_TRANSITION")
+    monkeypatch.delenv("FEC_VR_NO_DROP_STRETCH")
     b = VrPlan(pat, 360000, adaptive_mode_MDS=mds)
     for k in ("encoders", "decoders", "frames", "erased", "fate", "fate_decoder"):
         assert np.array_equal(getattr(a, k), getattr(b, k)), k
