@@ -495,7 +495,12 @@ void VrPlan::control(const uint8_t* pattern, int64_t n_pattern, int T, int B, in
         drops.push_back(q++);
     }
     feedback_plan(P + T + 1);
-    std::thread fb_thread([this, T, mds] { feedback_run(T, mds); });
+    // FEC_VR_FB_SYNC (diagnostic): the feedback jobs run to the end on this thread first
+    const bool fb_sync = std::getenv("FEC_VR_FB_SYNC") != nullptr;
+    if (fb_sync) feedback_run(T, mds);
+    std::thread fb_thread([this, T, mds, fb_sync] {
+        if (!fb_sync) feedback_run(T, mds);
+    });
     struct Joiner {
         std::thread& t;
         ~Joiner() { t.join(); }
