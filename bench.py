@@ -33,14 +33,15 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak, /opt/skills/guides/MI355X_MICROARCH.
 
 
 def kernel_sources_digest():
-    """SHA-256 over the HIP/C++ sources of libfec_amd.so (csrc/*.hip, *.h, *.cpp): a PMC traffic
-    figure is only valid for the kernels it was measured on."""
+    """SHA-256 over the device sources of libfec_amd.so (csrc/*.hip: the kernels and their launch
+    code; *.h): a PMC traffic figure or a rocprof duration is only valid for the kernels it was
+    measured on.  The host-only C++ files (*.cpp: the variable-rate plan, the host planner's rule
+    tables, the drop-in classes, the erasure generators) launch none of the step's kernels."""
     import glob
     import hashlib
     h = hashlib.sha256()
     csrc = os.path.join(ROOT, "fec_erasure_code_unit_test_relay_amd", "csrc")
-    for path in sorted(glob.glob(os.path.join(csrc, "*.hip")) + glob.glob(os.path.join(csrc, "*.h")) +
-                       glob.glob(os.path.join(csrc, "*.cpp"))):
+    for path in sorted(glob.glob(os.path.join(csrc, "*.hip")) + glob.glob(os.path.join(csrc, "*.h"))):
         h.update(os.path.basename(path).encode())
         with open(path, "rb") as f:
             h.update(f.read())
