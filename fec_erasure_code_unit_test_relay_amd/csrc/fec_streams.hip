@@ -17,9 +17,17 @@
 #include <stdint.h>
 
 #include <algorithm>
+#include <atomic>
+#include <chrono>
+#include <condition_variable>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
+#include <functional>
 #include <memory>
+#include <mutex>
 #include <new>
+#include <thread>
 #include <vector>
 
 #include "fec_amd.h"
@@ -304,7 +312,74 @@ __device__ __forceinline__ void stream_output(const StreamsDecArgs& a, const Str
 }  // namespace
 }  // namespace fec
 
+namespace {
+// Fork-join pool for the decoders' symbolic steps of one call: the streams are independent, so the
+// call's items are cut into contiguous parts, one per thread (the calling thread takes part 0).  A
+// worker polls for the next job for a while (calls come back to back) before it sleeps: a sleeping
+// thread's wake-up costs tens of microseconds, as much as its share of the steps.
+class StepPool {
+public:
+    explicit StepPool(int threads) {
+        for (int i = 1; i < threads; ++i) th_.emplace_back([this, i] { loop(i); });
+    }
+    ~StepPool() {
+        {
+            std::lock_guard<std::mutex> lk(mu_);
+            stop_.store(true);
+        }
+        cv_.notify_all();
+        for (auto& t : th_) t.join();
+    }
+    int parts() const { return static_cast<int>(th_.size()) + 1; }
+    // f(part) for every part; returns after all of them
+    void run(const std::function<void(int)>& f) {
+        {
+            std::lock_guard<std::mutex> lk(mu_);
+            job_ = &f;
+            left_.store(static_cast<int>(th_.size()), std::memory_order_relaxed);
+            gen_.fetch_add(1, std::memory_order_release);
+        }
+        cv_.notify_all();
+        f(0);
+        while (left_.load(std::memory_order_acquire) > 0) __builtin_ia32_pause();
+    }
+
+private:
+    void loop(int i) {
+        uint64_t seen = 0;
+        for (;;) {
+            // poll up to ~0.2 ms for the next job, then sleep
+            const auto t0 = std::chrono::steady_clock::now();
+            for (int spin = 0; gen_.load(std::memory_order_acquire) == seen && !stop_.load(); ++spin) {
+                __builtin_ia32_pause();
+                if ((spin & 255) == 255 && std::chrono::steady_clock::now() - t0 > std::chrono::microseconds(200)) break;
+            }
+            const std::function<void(int)>* f;
+            {
+                std::unique_lock<std::mutex> lk(mu_);
+                cv_.wait(lk, [&] { return stop_.load() || gen_.load() != seen; });
+                if (stop_.load()) return;
+                seen = gen_.load();
+                f = job_;
+            }
+            (*f)(i);
+            left_.fetch_sub(1, std::memory_order_release);
+        }
+    }
+    std::vector<std::thread> th_;
+    std::mutex mu_;
+    std::condition_variable cv_;
+    const std::function<void(int)>* job_ = nullptr;
+    std::atomic<uint64_t> gen_{0};
+    std::atomic<bool> stop_{false};
+    std::atomic<int> left_{0};
+};
+}  // namespace
+
+constexpr int kPoolMinItems = 1024;  // items per part below which a call steps on one thread
+
 struct fec_streams {
+    std::unique_ptr<StepPool> pool;          // symbolic steps of large calls (FEC_STREAMS_THREADS)
     fec_codec* codec = nullptr;
     fec::Geometry g;
     int nstreams = 0, W = 1, SK = 0;
@@ -315,18 +390,27 @@ struct fec_streams {
     uint32_t stamp = 0;
     uint8_t* d_win = nullptr;                // encoder windows
     uint8_t* d_ring = nullptr;               // decoder rings
-    void* d_stage = nullptr;                 // per-call records (ids + seqs / items + coefs)
-    void* h_stage = nullptr;                 // pinned twin of d_stage
+    // Per-call records (ids + seqs / items + coefs) go through a ring of kStageBufs staging buffers,
+    // so the host prepares a call (the decoders' symbolic steps) while the GPU still runs the ones
+    // before it; a buffer is rewritten only after its upload has completed.
+    static constexpr int kStageBufs = 4;
+    void* d_stage[kStageBufs] = {};
+    void* h_stage[kStageBufs] = {};          // pinned twins of d_stage
+    hipEvent_t staged[kStageBufs] = {};      // the last upload from h_stage[b] (h_stage[b] reusable)
+    int buf = 0;                             // the next call's buffer
     size_t stage_bytes = 0;
-    hipEvent_t staged = nullptr;             // the last upload from h_stage (h_stage reusable)
-    hipEvent_t done = nullptr;               // the last call's kernel (d_stage, windows, rings free)
+    hipEvent_t done = nullptr;               // the last call's kernel (windows, rings, older d_stage free)
     bool poisoned = false;                   // a failed call left host and device state apart
     ~fec_streams() {
-        if (staged) (void)hipEventDestroy(staged);
+        for (hipEvent_t e : staged)
+            if (e) (void)hipEventDestroy(e);
         if (done) (void)hipEventDestroy(done);
-        for (void* p : {static_cast<void*>(d_win), static_cast<void*>(d_ring), d_stage})
+        for (void* p : {static_cast<void*>(d_win), static_cast<void*>(d_ring)})
             if (p) (void)hipFree(p);
-        if (h_stage) (void)hipHostFree(h_stage);
+        for (void* p : d_stage)
+            if (p) (void)hipFree(p);
+        for (void* p : h_stage)
+            if (p) (void)hipHostFree(p);
         if (codec) fec_codec_destroy(codec);
     }
 };
@@ -352,12 +436,14 @@ int check_ids(fec_streams* h, const int32_t* ids, int M) {
     return FEC_OK;
 }
 
-// The previous call's records have left the pinned staging buffer (host wait), and its kernel --
-// which reads d_stage and reads / writes the windows and rings -- comes before anything this call
-// enqueues on `s`, whichever stream the previous call used (device-side wait).
-int stage_free(fec_streams* h, hipStream_t s) {
+// This call's staging buffer: the records of the call that used it before have left it (host
+// wait on that upload only), and the previous call's kernel -- which read / wrote the windows and
+// rings, after every older kernel and so after the last reader of d_stage[b] -- comes before
+// anything this call enqueues on `s`, whichever stream the previous call used (device-side wait).
+int stage_free(fec_streams* h, hipStream_t s, int* b) {
     if (h->poisoned) return FEC_ERR_HIP;
-    FS_TRY(hipEventSynchronize(h->staged));
+    *b = h->buf;
+    FS_TRY(hipEventSynchronize(h->staged[*b]));
     FS_TRY(hipStreamWaitEvent(s, h->done, 0));
     return FEC_OK;
 }
@@ -438,6 +524,12 @@ int fec_streams_create(int max_payload, int T, int B, int N, int nstreams, fec_s
         h->rules = fec::shared_decode_rules(T, B, N);
         h->planners.resize(nstreams);
         for (auto& p : h->planners) p.reset(new fec::StreamPlanner(g, h->rules.get()));
+        {
+            const unsigned hw = std::thread::hardware_concurrency();
+            int nth = static_cast<int>(std::max(1u, std::min(hw > 1 ? hw - 1 : 1u, 8u)));
+            if (const char* e = std::getenv("FEC_STREAMS_THREADS")) nth = std::max(1, std::atoi(e));
+            if (nth > 1 && nstreams >= 2 * kPoolMinItems) h->pool.reset(new StepPool(nth));
+        }
         h->enc_seq.assign(nstreams, 0);
         h->dec_seq.assign(nstreams, 0);
         h->mark.assign(nstreams, 0);
@@ -448,10 +540,12 @@ int fec_streams_create(int max_payload, int T, int B, int N, int nstreams, fec_s
         FS_TRY(hipMalloc(&h->d_ring, rb));
         FS_TRY(hipMemset(h->d_ring, 0, rb));
         h->stage_bytes = static_cast<size_t>(nstreams) * (sizeof(fec::StreamItem) + g.k * g.n + 16) + 64;
-        FS_TRY(hipMalloc(&h->d_stage, h->stage_bytes));
-        FS_TRY(hipHostMalloc(&h->h_stage, h->stage_bytes));
-        FS_TRY(hipEventCreateWithFlags(&h->staged, hipEventDisableTiming));
-        FS_TRY(hipEventRecord(h->staged, nullptr));
+        for (int b = 0; b < fec_streams::kStageBufs; ++b) {
+            FS_TRY(hipMalloc(&h->d_stage[b], h->stage_bytes));
+            FS_TRY(hipHostMalloc(&h->h_stage[b], h->stage_bytes));
+            FS_TRY(hipEventCreateWithFlags(&h->staged[b], hipEventDisableTiming));
+            FS_TRY(hipEventRecord(h->staged[b], nullptr));
+        }
         FS_TRY(hipEventCreateWithFlags(&h->done, hipEventDisableTiming));
         FS_TRY(hipEventRecord(h->done, nullptr));
         *out = h.release();
@@ -476,23 +570,24 @@ int fec_streams_encode(fec_streams* h, const int32_t* ids, int M, const uint8_t*
     if (M == 0) return FEC_OK;
     if (int st = check_ids(h, ids, M)) return st;
     hipStream_t s = static_cast<hipStream_t>(stream);
-    if (int st = stage_free(h, s)) return st;
-    int64_t* hseq = static_cast<int64_t*>(h->h_stage);
+    int b = 0;
+    if (int st = stage_free(h, s, &b)) return st;
+    int64_t* hseq = static_cast<int64_t*>(h->h_stage[b]);
     int32_t* hid = reinterpret_cast<int32_t*>(hseq + M);
     for (int m = 0; m < M; ++m) {
         hseq[m] = h->enc_seq[ids[m]];  // committed below, once the launch is in
         hid[m] = ids[m];
     }
     const size_t bytes = static_cast<size_t>(M) * 12;
-    FS_TRY(hipMemcpyAsync(h->d_stage, h->h_stage, bytes, hipMemcpyHostToDevice, s));
-    FS_TRY(hipEventRecord(h->staged, s));
+    FS_TRY(hipMemcpyAsync(h->d_stage[b], h->h_stage[b], bytes, hipMemcpyHostToDevice, s));
+    FS_TRY(hipEventRecord(h->staged[b], s));
     fec::CodecView v;
     fec::codec_view(h->codec, &v);
     fec::StreamsEncArgs a;
     a.payload = d_payload;
     a.len = d_payload_len;
-    a.seq = static_cast<const int64_t*>(h->d_stage);
-    a.ids = reinterpret_cast<const int32_t*>(static_cast<const int64_t*>(h->d_stage) + M);
+    a.seq = static_cast<const int64_t*>(h->d_stage[b]);
+    a.ids = reinterpret_cast<const int32_t*>(static_cast<const int64_t*>(h->d_stage[b]) + M);
     a.win = h->d_win;
     a.cw = d_codeword;
     a.cw_len = d_codeword_len;
@@ -513,6 +608,7 @@ int fec_streams_encode(fec_streams* h, const int32_t* ids, int M, const uint8_t*
     hipLaunchKernelGGL(fec::fec_streams_encode_kernel, dim3((M + 3) / 4), dim3(256), 0, s, a);
     FS_TRY(hipGetLastError());
     FS_TRY(hipEventRecord(h->done, s));
+    h->buf = (b + 1) % fec_streams::kStageBufs;
     for (int m = 0; m < M; ++m) ++h->enc_seq[ids[m]];
     return FEC_OK;
 }
@@ -524,9 +620,14 @@ int fec_streams_decode(fec_streams* h, const int32_t* ids, int M, const uint8_t*
                                                      !d_payload_len)))
         return FEC_ERR_ARG;
     if (M == 0) return FEC_OK;
+    static const bool dbg = std::getenv("FEC_STREAMS_DEBUG") != nullptr;  // per-phase host times
+    const auto t0 = std::chrono::steady_clock::now();
     if (int st = check_ids(h, ids, M)) return st;
     hipStream_t s = static_cast<hipStream_t>(stream);
-    if (int st = stage_free(h, s)) return st;
+    int b = 0;
+    const auto t1 = std::chrono::steady_clock::now();
+    if (int st = stage_free(h, s, &b)) return st;
+    const auto t2 = std::chrono::steady_clock::now();
     const fec::Geometry& g = h->g;
     // The symbolic decoders advance below, before the upload and the launch; if either fails, the
     // host planners are ahead of the device rings and the group refuses every later call.
@@ -535,41 +636,57 @@ int fec_streams_decode(fec_streams* h, const int32_t* ids, int M, const uint8_t*
         bool armed = true;
         ~Poison() { if (armed) h->poisoned = true; }
     } poison{h};
-    fec::StreamItem* items = static_cast<fec::StreamItem*>(h->h_stage);
+    fec::StreamItem* items = static_cast<fec::StreamItem*>(h->h_stage[b]);
     uint8_t* coefs = reinterpret_cast<uint8_t*>(items + M);
     const int kn = g.k * g.n;
-    int ncoef = 0;
-    try {
-        for (int m = 0; m < M; ++m) {
-            const int id = ids[m];
-            const bool er = erasure[m] != 0;
-            const int64_t seq = h->dec_seq[id]++;
-            const fec::StepResult r = h->planners[id]->step(seq, er);
-            fec::StreamItem& it = items[m];
-            it.id = id;
-            it.fate = r.fate;
-            it.clamp = r.slow ? 1 : 0;
-            it.coef = 0;
-            it.seq = seq;
-            it.x = r.x;
-            it.erased = er ? 1 : 0;
-            it.pad = 0;
-            if (r.fate == fec::kRecovered) {
-                std::memcpy(coefs + static_cast<size_t>(ncoef) * kn, r.coef, kn);
-                it.coef = ncoef++;
+    std::atomic<int> ncoef_a{0};
+    std::atomic<bool> failed{false};
+    // one symbolic decoder step per item; the recovered packets' coefficient rows take slots in
+    // arrival order (an item carries its slot)
+    auto steps = [&](int m0, int m1) {
+        try {
+            for (int m = m0; m < m1; ++m) {
+                const int id = ids[m];
+                const bool er = erasure[m] != 0;
+                const int64_t seq = h->dec_seq[id]++;
+                const fec::StepResult r = h->planners[id]->step(seq, er);
+                fec::StreamItem& it = items[m];
+                it.id = id;
+                it.fate = r.fate;
+                it.clamp = r.slow ? 1 : 0;
+                it.coef = 0;
+                it.seq = seq;
+                it.x = r.x;
+                it.erased = er ? 1 : 0;
+                it.pad = 0;
+                if (r.fate == fec::kRecovered) {
+                    const int slot = ncoef_a.fetch_add(1, std::memory_order_relaxed);
+                    std::memcpy(coefs + static_cast<size_t>(slot) * kn, r.coef, kn);
+                    it.coef = slot;
+                }
             }
+        } catch (...) {
+            failed.store(true);
         }
-    } catch (...) {
-        return FEC_ERR_ARG;
+    };
+    if (h->pool && M >= 2 * kPoolMinItems) {
+        const int np = h->pool->parts();
+        h->pool->run([&](int p) { steps(static_cast<int>(static_cast<int64_t>(M) * p / np),
+                                        static_cast<int>(static_cast<int64_t>(M) * (p + 1) / np)); });
+    } else {
+        steps(0, M);
     }
+    if (failed.load()) return FEC_ERR_ARG;
+    const int ncoef = ncoef_a.load();
+    const auto t3 = std::chrono::steady_clock::now();
     const size_t bytes = static_cast<size_t>(M) * sizeof(fec::StreamItem) + static_cast<size_t>(ncoef) * kn;
-    FS_TRY(hipMemcpyAsync(h->d_stage, h->h_stage, bytes, hipMemcpyHostToDevice, s));
-    FS_TRY(hipEventRecord(h->staged, s));
+    FS_TRY(hipMemcpyAsync(h->d_stage[b], h->h_stage[b], bytes, hipMemcpyHostToDevice, s));
+    FS_TRY(hipEventRecord(h->staged[b], s));
     fec::CodecView v;
     fec::codec_view(h->codec, &v);
     fec::StreamsDecArgs a;
     a.cw_in = d_codeword;
-    a.items = static_cast<const fec::StreamItem*>(h->d_stage);
+    a.items = static_cast<const fec::StreamItem*>(h->d_stage[b]);
     a.coefs = reinterpret_cast<const uint8_t*>(a.items + M);
     a.ring = h->d_ring;
     a.gf = v.gf;
@@ -586,7 +703,14 @@ int fec_streams_decode(fec_streams* h, const int32_t* ids, int M, const uint8_t*
     hipLaunchKernelGGL(fec::fec_streams_decode_kernel, dim3((M + 3) / 4), dim3(256), 0, s, a);
     FS_TRY(hipGetLastError());
     FS_TRY(hipEventRecord(h->done, s));
+    h->buf = (b + 1) % fec_streams::kStageBufs;
     poison.armed = false;
+    if (dbg) {
+        const auto t4 = std::chrono::steady_clock::now();
+        auto us = [](auto a, auto z) { return std::chrono::duration<double, std::micro>(z - a).count(); };
+        std::fprintf(stderr, "streams decode: ids %.1f us, stage wait %.1f, steps %.1f, upload + launch %.1f\n",
+                     us(t0, t1), us(t1, t2), us(t2, t3), us(t3, t4));
+    }
     return FEC_OK;
 }
 
