@@ -11,6 +11,8 @@
 #include <cstdlib>
 #include <cstring>
 #include <ctime>
+#include <pthread.h>
+#include <sched.h>
 #include <sys/resource.h>
 #include <new>
 #include <mutex>
@@ -118,6 +120,28 @@ const DecodeRules& VrPlan::rules_for(int T, int B, int N) {
 namespace {
 
 constexpr int kTTot = 10;                 // T_TOT (FEC_Macro.h:32)
+
+// FEC_VR_PIN=1: the plan's own threads (feedback producer, decoder workers) on the 8 CPUs of the
+// calling thread's aligned group (within the process's allowed set), so that what the producer
+// writes and the control loop reads stays near.  The calling thread itself is left alone.
+thread_local int t_pin_home = -1;  // set by the control thread for the threads it starts
+int vr_pin_home() {
+    static const bool on = [] {
+        const char* v = std::getenv("FEC_VR_PIN");
+        return v && std::atoi(v) != 0;
+    }();
+    return on ? sched_getcpu() : -1;
+}
+void vr_pin_near(int home) {
+    if (home < 0) return;
+    cpu_set_t allowed, set;
+    CPU_ZERO(&set);
+    if (sched_getaffinity(0, sizeof(allowed), &allowed) != 0) return;
+    const int base = home & ~7;
+    for (int c = base; c < base + 8 && c < CPU_SETSIZE; ++c)
+        if (CPU_ISSET(c, &allowed)) CPU_SET(c, &set);
+    if (CPU_COUNT(&set) > 0) (void)pthread_setaffinity_np(pthread_self(), sizeof(set), &set);
+}
 constexpr int kEstimationCycle = 1000 / 10;  // ESTIMATION_WINDOW_SIZE / ..._REDUCTION_FACTOR (:54-55)
 
 struct Report {        // decoder instance `id` reports packet x at its call for seq
@@ -201,7 +225,8 @@ void VrPlan::start_workers() {
     for (auto& r : recs_) r.clear();
     pending_ = true;
     for (size_t w = 0; w < nth; ++w) {
-        workers_.emplace_back([this, w] {
+        workers_.emplace_back([this, w, home = t_pin_home] {
+            vr_pin_near(home);
             for (;;) {
                 DecJob j;
                 {
@@ -498,7 +523,9 @@ void VrPlan::control(const uint8_t* pattern, int64_t n_pattern, int T, int B, in
     // FEC_VR_FB_SYNC (diagnostic): the feedback jobs run to the end on this thread first
     const bool fb_sync = std::getenv("FEC_VR_FB_SYNC") != nullptr;
     if (fb_sync) feedback_run(T, mds);
-    std::thread fb_thread([this, T, mds, fb_sync] {
+    t_pin_home = vr_pin_home();
+    std::thread fb_thread([this, T, mds, fb_sync, home = t_pin_home] {
+        vr_pin_near(home);
         if (!fb_sync) feedback_run(T, mds);
     });
     struct Joiner {

@@ -14,6 +14,6 @@ cat /proc/self/status | grep -i cpus_allowed_list
 lscpu | grep -i "numa\|socket\|model name" | head -6
 for i in 1 2 3; do
   echo "default: $(timeout 60 /tmp/vr_plan_bench /tmp/bin_erasure.bin 40 | cut -c1-60)"
+  echo "FEC_VR_PIN=1: $(FEC_VR_PIN=1 timeout 60 /tmp/vr_plan_bench /tmp/bin_erasure.bin 40 | cut -c1-60)"
   echo "cpus 0-9: $(timeout 60 taskset -c 0-9 /tmp/vr_plan_bench /tmp/bin_erasure.bin 40 | cut -c1-60)"
-  echo "cpus 0-9 + 128-137: $(timeout 60 taskset -c 0-9,128-137 /tmp/vr_plan_bench /tmp/bin_erasure.bin 40 | cut -c1-60)"
 done | tee $OUT/aff.txt
