@@ -121,17 +121,22 @@ namespace {
 
 constexpr int kTTot = 10;                 // T_TOT (FEC_Macro.h:32)
 
-// FEC_VR_PIN=1: the plan's own threads (feedback producer, decoder workers) on the 8 CPUs of the
-// calling thread's aligned group (within the process's allowed set), so that what the producer
-// writes and the control loop reads stays near.  The calling thread itself is left alone.
+// The plan's own threads (feedback producer, decoder workers), and the calling thread for the
+// control loop, run on the 8 CPUs of the calling thread's aligned group (within the process's
+// allowed set), so that what the producer writes and the control loop reads stays near: on a
+// two-socket box the scheduler otherwise spreads them over both sockets (plan 2.5 - 2.7 ms
+// unplaced, 1.8 - 2.1 ms with the plan's threads placed, 1.6 - 1.9 ms with the caller held too,
+// profiles/r03/r03v_vr_affinity.txt).  The caller's own placement is restored when the control
+// loop ends.  FEC_VR_PIN=0: nothing placed; 1: the plan's threads only; 2 (default): both.
 thread_local int t_pin_home = -1;  // set by the control thread for the threads it starts
-int vr_pin_home() {
-    static const bool on = [] {
+int vr_pin_mode() {
+    static const int mode = [] {
         const char* v = std::getenv("FEC_VR_PIN");
-        return v && std::atoi(v) != 0;
+        return v ? std::atoi(v) : 2;
     }();
-    return on ? sched_getcpu() : -1;
+    return mode;
 }
+int vr_pin_home() { return vr_pin_mode() > 0 ? sched_getcpu() : -1; }
 void vr_pin_near(int home) {
     if (home < 0) return;
     cpu_set_t allowed, set;
@@ -524,6 +529,20 @@ void VrPlan::control(const uint8_t* pattern, int64_t n_pattern, int T, int B, in
     const bool fb_sync = std::getenv("FEC_VR_FB_SYNC") != nullptr;
     if (fb_sync) feedback_run(T, mds);
     t_pin_home = vr_pin_home();
+    // FEC_VR_PIN=2: the control loop itself on the group too, for the rest of this function
+    struct CallerPlacement {
+        cpu_set_t saved;
+        bool held = false;
+        explicit CallerPlacement(int home) {
+            if (home < 0 || vr_pin_mode() < 2) return;
+            if (pthread_getaffinity_np(pthread_self(), sizeof(saved), &saved) != 0) return;
+            held = true;
+            vr_pin_near(home);
+        }
+        ~CallerPlacement() {
+            if (held) (void)pthread_setaffinity_np(pthread_self(), sizeof(saved), &saved);
+        }
+    } caller_placement{t_pin_home};
     std::thread fb_thread([this, T, mds, fb_sync, home = t_pin_home] {
         vr_pin_near(home);
         if (!fb_sync) feedback_run(T, mds);

@@ -13,7 +13,9 @@ g++ -O2 -std=c++17 -pthread -I$C -Iinclude -I/opt/rocm/include -D__HIP_PLATFORM_
 cat /proc/self/status | grep -i cpus_allowed_list
 lscpu | grep -i "numa\|socket\|model name" | head -6
 for i in 1 2 3; do
-  echo "default: $(timeout 60 /tmp/vr_plan_bench /tmp/bin_erasure.bin 40 | cut -c1-60)"
-  echo "FEC_VR_PIN=1: $(FEC_VR_PIN=1 timeout 60 /tmp/vr_plan_bench /tmp/bin_erasure.bin 40 | cut -c1-60)"
-  echo "cpus 0-9: $(timeout 60 taskset -c 0-9 /tmp/vr_plan_bench /tmp/bin_erasure.bin 40 | cut -c1-60)"
+  for p in 0 1 2; do
+    echo "FEC_VR_PIN=$p: $(FEC_VR_PIN=$p timeout 60 /tmp/vr_plan_bench /tmp/bin_erasure.bin 40 | cut -c1-60)"
+  done
 done | tee $OUT/aff.txt
+timeout -k 10 200 python3 -u bench.py --no-cpu-baseline --no-host-inclusive --steps 20 > $OUT/bench.json 2> $OUT/bench.err || { tail -20 $OUT/bench.err; exit 1; }
+python3 -c "import json; d=json.loads(open('$OUT/bench.json').read().strip().splitlines()[-1]); print(d['value'], json.dumps(d['configs']['config4_adaptive'])[:260])"
