@@ -30,6 +30,9 @@
 #include <thread>
 #include <vector>
 
+#include <pthread.h>
+#include <sched.h>
+
 #include "fec_amd.h"
 #include "fec_host.h"
 #include "fec_kernels.h"
@@ -317,10 +320,29 @@ namespace {
 // call's items are cut into contiguous parts, one per thread (the calling thread takes part 0).  A
 // worker polls for the next job for a while (calls come back to back) before it sleeps: a sleeping
 // thread's wake-up costs tens of microseconds, as much as its share of the steps.
+// The workers run on the 8 CPUs of the creating thread's aligned group (within the allowed set):
+// on a two-socket box the scheduler otherwise spreads them over both sockets (FEC_STREAMS_PIN=0:
+// unplaced).
+void place_near(int home) {
+    if (home < 0) return;
+    cpu_set_t allowed, set;
+    CPU_ZERO(&set);
+    if (sched_getaffinity(0, sizeof(allowed), &allowed) != 0) return;
+    const int base = home & ~7;
+    for (int c = base; c < base + 8 && c < CPU_SETSIZE; ++c)
+        if (CPU_ISSET(c, &allowed)) CPU_SET(c, &set);
+    if (CPU_COUNT(&set) > 0) (void)pthread_setaffinity_np(pthread_self(), sizeof(set), &set);
+}
+
 class StepPool {
 public:
     explicit StepPool(int threads) {
-        for (int i = 1; i < threads; ++i) th_.emplace_back([this, i] { loop(i); });
+        const char* pin = std::getenv("FEC_STREAMS_PIN");
+        const int home = (pin && std::atoi(pin) == 0) ? -1 : sched_getcpu();
+        for (int i = 1; i < threads; ++i) th_.emplace_back([this, i, home] {
+            place_near(home);
+            loop(i);
+        });
     }
     ~StepPool() {
         {
