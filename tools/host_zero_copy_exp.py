@@ -21,6 +21,7 @@ from fec_erasure_code_unit_test_relay_amd._lib import lib  # noqa: E402
 ap = argparse.ArgumentParser()
 ap.add_argument("--packets", type=int, default=1_000_000)
 ap.add_argument("--reps", type=int, default=3)
+ap.add_argument("--no-pipe", action="store_true")
 args = ap.parse_args()
 torch.cuda.set_device(0)
 T = 10
@@ -125,7 +126,7 @@ def zero_copy_pipelined(NC):
     return n0
 
 
-for NC in (2, 4, 8, 16):
+for NC in (() if args.no_pipe else (2, 4, 8, 16)):
     h_out.zero_()
     h_ol.zero_()
     dt = timed(lambda: zero_copy_pipelined(NC), args.reps)
