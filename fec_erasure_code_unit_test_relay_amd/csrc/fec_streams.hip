@@ -416,9 +416,14 @@ struct fec_streams {
     // so the host prepares a call (the decoders' symbolic steps) while the GPU still runs the ones
     // before it; a buffer is rewritten only after its upload has completed.
     static constexpr int kStageBufs = 4;
+    // The kernels read the records straight from the pinned buffers (mapped: m_stage) -- an upload
+    // per call put an SDMA copy and its hand-off to the kernel on the GPU's path, twice per
+    // encode + decode pair (FEC_STREAMS_UPLOAD=1 keeps those uploads into d_stage).
     void* d_stage[kStageBufs] = {};
-    void* h_stage[kStageBufs] = {};          // pinned twins of d_stage
-    hipEvent_t staged[kStageBufs] = {};      // the last upload from h_stage[b] (h_stage[b] reusable)
+    void* h_stage[kStageBufs] = {};          // pinned records
+    void* m_stage[kStageBufs] = {};          // their device addresses
+    bool upload = false;
+    hipEvent_t staged[kStageBufs] = {};      // the last kernel (and upload) that read h_stage[b]
     int buf = 0;                             // the next call's buffer
     size_t stage_bytes = 0;
     hipEvent_t done = nullptr;               // the last call's kernel (windows, rings, older d_stage free)
@@ -458,8 +463,8 @@ int check_ids(fec_streams* h, const int32_t* ids, int M) {
     return FEC_OK;
 }
 
-// This call's staging buffer: the records of the call that used it before have left it (host
-// wait on that upload only), and the previous call's kernel -- which read / wrote the windows and
+// This call's staging buffer: the call that used it before has read it (host wait on that call's
+// kernel, kStageBufs calls back), and the previous call's kernel -- which read / wrote the windows and
 // rings, after every older kernel and so after the last reader of d_stage[b] -- comes before
 // anything this call enqueues on `s`, whichever stream the previous call used (device-side wait).
 int stage_free(fec_streams* h, hipStream_t s, int* b) {
@@ -562,9 +567,11 @@ int fec_streams_create(int max_payload, int T, int B, int N, int nstreams, fec_s
         FS_TRY(hipMalloc(&h->d_ring, rb));
         FS_TRY(hipMemset(h->d_ring, 0, rb));
         h->stage_bytes = static_cast<size_t>(nstreams) * (sizeof(fec::StreamItem) + g.k * g.n + 16) + 64;
+        if (const char* e = std::getenv("FEC_STREAMS_UPLOAD")) h->upload = std::atoi(e) != 0;
         for (int b = 0; b < fec_streams::kStageBufs; ++b) {
-            FS_TRY(hipMalloc(&h->d_stage[b], h->stage_bytes));
-            FS_TRY(hipHostMalloc(&h->h_stage[b], h->stage_bytes));
+            if (h->upload) FS_TRY(hipMalloc(&h->d_stage[b], h->stage_bytes));
+            FS_TRY(hipHostMalloc(&h->h_stage[b], h->stage_bytes, hipHostMallocMapped));
+            FS_TRY(hipHostGetDevicePointer(&h->m_stage[b], h->h_stage[b], 0));
             FS_TRY(hipEventCreateWithFlags(&h->staged[b], hipEventDisableTiming));
             FS_TRY(hipEventRecord(h->staged[b], nullptr));
         }
@@ -601,15 +608,15 @@ int fec_streams_encode(fec_streams* h, const int32_t* ids, int M, const uint8_t*
         hid[m] = ids[m];
     }
     const size_t bytes = static_cast<size_t>(M) * 12;
-    FS_TRY(hipMemcpyAsync(h->d_stage[b], h->h_stage[b], bytes, hipMemcpyHostToDevice, s));
-    FS_TRY(hipEventRecord(h->staged[b], s));
+    if (h->upload) FS_TRY(hipMemcpyAsync(h->d_stage[b], h->h_stage[b], bytes, hipMemcpyHostToDevice, s));
+    const void* rec = h->upload ? h->d_stage[b] : h->m_stage[b];
     fec::CodecView v;
     fec::codec_view(h->codec, &v);
     fec::StreamsEncArgs a;
     a.payload = d_payload;
     a.len = d_payload_len;
-    a.seq = static_cast<const int64_t*>(h->d_stage[b]);
-    a.ids = reinterpret_cast<const int32_t*>(static_cast<const int64_t*>(h->d_stage[b]) + M);
+    a.seq = static_cast<const int64_t*>(rec);
+    a.ids = reinterpret_cast<const int32_t*>(static_cast<const int64_t*>(rec) + M);
     a.win = h->d_win;
     a.cw = d_codeword;
     a.cw_len = d_codeword_len;
@@ -630,6 +637,7 @@ int fec_streams_encode(fec_streams* h, const int32_t* ids, int M, const uint8_t*
     hipLaunchKernelGGL(fec::fec_streams_encode_kernel, dim3((M + 3) / 4), dim3(256), 0, s, a);
     FS_TRY(hipGetLastError());
     FS_TRY(hipEventRecord(h->done, s));
+    FS_TRY(hipEventRecord(h->staged[b], s));
     h->buf = (b + 1) % fec_streams::kStageBufs;
     for (int m = 0; m < M; ++m) ++h->enc_seq[ids[m]];
     return FEC_OK;
@@ -702,13 +710,13 @@ int fec_streams_decode(fec_streams* h, const int32_t* ids, int M, const uint8_t*
     const int ncoef = ncoef_a.load();
     const auto t3 = std::chrono::steady_clock::now();
     const size_t bytes = static_cast<size_t>(M) * sizeof(fec::StreamItem) + static_cast<size_t>(ncoef) * kn;
-    FS_TRY(hipMemcpyAsync(h->d_stage[b], h->h_stage[b], bytes, hipMemcpyHostToDevice, s));
-    FS_TRY(hipEventRecord(h->staged[b], s));
+    if (h->upload) FS_TRY(hipMemcpyAsync(h->d_stage[b], h->h_stage[b], bytes, hipMemcpyHostToDevice, s));
+    const void* rec = h->upload ? h->d_stage[b] : h->m_stage[b];
     fec::CodecView v;
     fec::codec_view(h->codec, &v);
     fec::StreamsDecArgs a;
     a.cw_in = d_codeword;
-    a.items = static_cast<const fec::StreamItem*>(h->d_stage[b]);
+    a.items = static_cast<const fec::StreamItem*>(rec);
     a.coefs = reinterpret_cast<const uint8_t*>(a.items + M);
     a.ring = h->d_ring;
     a.gf = v.gf;
@@ -725,6 +733,7 @@ int fec_streams_decode(fec_streams* h, const int32_t* ids, int M, const uint8_t*
     hipLaunchKernelGGL(fec::fec_streams_decode_kernel, dim3((M + 3) / 4), dim3(256), 0, s, a);
     FS_TRY(hipGetLastError());
     FS_TRY(hipEventRecord(h->done, s));
+    FS_TRY(hipEventRecord(h->staged[b], s));
     h->buf = (b + 1) % fec_streams::kStageBufs;
     poison.armed = false;
     if (dbg) {
