@@ -1,0 +1,777 @@
+// fec_sdswdf.hip -- the relay's state-dependent symbol-wise decode-and-forward (SD-SWDF,
+// RELAYING_TYPE 3) and the destination's state-dependent decode, batched over many packets of
+// one relay stream.
+//
+// Reference: Decoder_Symbol_Wise::symbol_wise_encode_state_dependent (src/Decoder_Symbol_Wise.cpp
+// :178-432) at the relay, symbol_wise_decode_state_dependent (:487-546) + extract_data (:653-661)
+// at the destination, driven by Variable_Rate_FEC_Decoder with one relay frame per seq
+// (FLAG_FOR_CONSTANT_TRANS = 1): relay received packet :1458-1493, relay erased packet :636-675,
+// destination frame :1798-1815, destination missing frame :1703-1721.
+//
+// The relay keeps the last 3*T_TOT packets with their erasure flags and the headers it sent.  For
+// every index of its outgoing frame (symInd = k-1-index, from k-1 down to -(n2-k)) it looks at
+// one diagonal of the source code: a partial one (symInd >= n-k) whose received symbols it
+// forwards, or a complete one it decodes (decodeBlock, T = n-1) and re-encodes for the second hop
+// (encodeBlock, G2), forwarding a symbol the destination has not had yet.  The 11-byte header
+// tells the destination which symbol of its diagonal each frame symbol is.
+//
+// Every decision depends only on the erasure flags and the headers, never on payload bytes, and
+// every forwarded byte is a GF linear combination of at most n received symbols of one diagonal:
+// symbol (j, p) of source packet t-(n-1)+p+symInd at the relay, symbol (j, q) of frame
+// t2-k_shift-(n-1-q) at the destination.  So a host planner replays the reference's control flow
+// symbolically (coefficient vectors instead of bytes, the decode rules of fec_host.cpp instead of
+// the per-call RREF) and interns one record per distinct packet plan; the byte work is two
+// data-parallel kernels, one thread per (packet, code block), reading the plan of their packet.
+//
+// Reference behaviour kept (well-defined, restated in oracle/fec_oracle.c or_sdswdf_*): the burst
+// test as written (it only acts with FLAG_FOR_SDBO = 1, a run-time flag here), header rows shifted
+// 10 of their 11 ints (:133, :169; entry 10 of a row is never moved), decodeBlock clearing the flags
+// of what it recovers (so the "forward a received symbol" branch also forwards recovered data),
+// the block count ceil(max_payload/k)+1 on ints, the relay's flag never set.  Undefined behaviour
+// defined away: slots hold zero-padded packets, the erased-packet frame has its full
+// size, out-of-bounds stack writes (:309-312, :325) land nowhere, and stale temp_codeword bytes
+// (:248-250) are never forwarded (the oracle proves it by filling them with garbage).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstring>
+#include <memory>
+#include <new>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "fec_amd.h"
+#include "fec_host.h"
+#include "fec_kernels.h"
+
+namespace fec {
+namespace {
+
+constexpr int kTT = 10;             // T_TOT (FEC_Macro.h:32)
+constexpr int kSlots = 3 * kTT;     // codeword_vector_state_dependent rows
+constexpr int kHdr = kTT + 1;       // header entries per row (and frame header bytes)
+constexpr int kSdThreads = 256;
+
+// A symbolic symbol: its GF coefficients over the n positions of the diagonal being read.
+struct Vec {
+    uint8_t c[kMaxN];
+};
+
+void vec_zero(Vec& v, int n) { std::memset(v.c, 0, static_cast<size_t>(n)); }
+void vec_unit(Vec& v, int n, int p) {
+    vec_zero(v, n);
+    v.c[p] = 1;
+}
+void vec_axpy(Vec& y, uint8_t a, const Vec& x, int n) {  // y ^= a * x
+    if (!a) return;
+    const Field& f = field();
+    for (int i = 0; i < n; ++i) y.c[i] ^= f.mt[a][x.c[i]];
+}
+
+// decodeBlock(cw, G, cw, er, k, n, T = n-1, t = 0) on symbolic symbols (codingOperations.cpp
+// :149-232 through the window-n decode rule): recovered data symbols become combinations of the
+// symbols the rule names, and their erasure flags are cleared (:224-229).
+void sym_decode(const DecodeRules& rules, int k, int n, Vec* tc, uint8_t* er) {
+    uint32_t mask = 0;
+    for (int c = 0; c < n; ++c) mask |= (er[c] ? 1u : 0u) << c;
+    int cnt = __builtin_popcount(mask);
+    if (cnt == n) return;  // all erased (:181-182)
+    const uint8_t* e = rules.entry(n, mask);
+    Vec rec[kMaxK];
+    uint32_t done = 0;
+    for (int i = 0; i < k; ++i) {
+        if (!er[i] || e[i] == 0xFF) continue;
+        const uint8_t* col = e + k + i * n;
+        vec_zero(rec[i], n);
+        for (int c = 0; c < n; ++c) vec_axpy(rec[i], col[c], tc[c], n);
+        done |= 1u << i;
+    }
+    for (int i = 0; i < k; ++i)
+        if ((done >> i) & 1u) {
+            tc[i] = rec[i];
+            er[i] = 0;
+        }
+}
+
+// Distinct records, each stored once (plans repeat: an erasure-free stretch is one record).
+class RecordTable {
+public:
+    explicit RecordTable(int bytes) : bytes_(bytes) {}
+    int32_t intern(const uint8_t* rec) {
+        std::string key(reinterpret_cast<const char*>(rec), static_cast<size_t>(bytes_));
+        auto it = ids_.find(key);
+        if (it != ids_.end()) return it->second;
+        const int32_t id = static_cast<int32_t>(ids_.size());
+        ids_.emplace(std::move(key), id);
+        data_.insert(data_.end(), rec, rec + bytes_);
+        return id;
+    }
+    void clear() {
+        ids_.clear();
+        data_.clear();
+    }
+    const std::vector<uint8_t>& data() const { return data_; }
+    int64_t count() const { return static_cast<int64_t>(ids_.size()); }
+
+private:
+    int bytes_;
+    std::unordered_map<std::string, int32_t> ids_;
+    std::vector<uint8_t> data_;
+};
+
+// The relay: symbol_wise_encode_state_dependent per packet, symbolic.  Output record per packet:
+// header[n2-1][0..10] as bytes, then n2 rows of n coefficients (row index: frame symbol `index`
+// of every code block j = sum_p coef[p] * symbol (j, p) of source packet t-(n-1)+p+(k-1-index)).
+class SdRelayPlanner {
+public:
+    SdRelayPlanner(int k, int n, int n2, int sdbo, std::shared_ptr<const DecodeRules> rules,
+                   std::vector<uint8_t> G2)
+        : k_(k), n_(n), n2_(n2), sdbo_(sdbo), rules_(std::move(rules)), G2_(std::move(G2)),
+          records_(kHdr + n2 * n) {
+        rec_.resize(static_cast<size_t>(record_bytes()));
+        reset();
+    }
+    int record_bytes() const { return kHdr + n2_ * n_; }
+    const RecordTable& records() const { return records_; }
+    void reset() {
+        std::memset(er_, 0, sizeof(er_));
+        std::memset(valid_, 0, sizeof(valid_));
+        for (int i = 0; i < kSlots; ++i)
+            for (int jj = 0; jj < kHdr; ++jj) header_[i][jj] = jj + 1;  // :60-62
+        records_.clear();
+        memo_.clear();
+    }
+    // Packet t (t = 0, 1, ... in order), erased on hop 1: the id of its record.  The plan of a
+    // packet is a function of the flags of the slots its diagonals read and of the headers of
+    // the last n2-1 packets (rows n2-1 and up hold constants): repeated states are looked up.
+    int32_t step(bool erased) {
+        shift();
+        er_[2 * kTT] = erased ? 1 : 0;
+        valid_[2 * kTT] = erased ? 0 : 1;
+        const int lo = 2 * kTT - n_ + 1 - (n2_ - k_);
+        key_.clear();
+        for (int i = lo; i <= 2 * kTT; ++i) key_.push_back(static_cast<char>(er_[i] | (valid_[i] << 1)));
+        for (int r = 0; r < n2_ - 1; ++r)
+            for (int e = 0; e < n2_ - 1; ++e) key_.push_back(static_cast<char>(header_[r][e]));
+        auto it = memo_.find(key_);
+        if (it != memo_.end()) {
+            for (int i = 0; i < n2_; ++i) header_[n2_ - 1][i] = it->second.hdr[i];
+            return it->second.id;
+        }
+        encode(rec_.data());
+        Memo m;
+        m.id = records_.intern(rec_.data());
+        for (int i = 0; i < n2_; ++i) m.hdr[i] = static_cast<uint8_t>(header_[n2_ - 1][i]);
+        memo_.emplace(key_, m);
+        return m.id;
+    }
+
+private:
+    // push_current_codeword / rotate_pointers_and_insert_zero_word (:131-135, :167-171)
+    void shift() {
+        for (int i = 0; i < kSlots - 1; ++i) {
+            std::memcpy(header_[i], header_[i + 1], sizeof(int) * kTT);
+            er_[i] = er_[i + 1];
+            valid_[i] = valid_[i + 1];
+        }
+    }
+    void encode(uint8_t* rec) {
+        const int k = k_, n = n_, n2 = n2_, k2 = k_, TT = kTT;
+        uint8_t stam[2 * kMaxN + 2 * kHdr];
+        int tempHeader[kMaxN + kHdr];
+        // burst check (:198-231); the in_burst assignments make it "longest run, first end"
+        int longest = 0, end = 0, run = 0;
+        for (int aa = 0; aa < n; ++aa) {
+            if (er_[2 * TT - n + 1 + aa] == 1) {
+                ++run;
+            } else {
+                if (run > longest) {
+                    longest = run;
+                    end = aa - 1;
+                }
+                run = 0;
+            }
+        }
+        if (run > longest) {
+            longest = run;
+            end = n - 1;
+        }
+        const bool burst = sdbo_ == 1 && longest > n - k && end >= k - 1;
+        uint8_t* coef = rec + kHdr;
+        Vec tc[kMaxN], enc[kMaxN];
+        int index = -1;
+        for (int symInd = k - 1; symInd >= -(n2 - k2); --symInd) {
+            ++index;
+            // the diagonal: position p from slot p + symInd + 2T-n+1; a zero slot (erased, or
+            // before the first packet) is a zero symbol; positions past the current packet are
+            // not filled (stale in the reference, never forwarded)
+            const int filled = symInd >= 0 ? n - symInd : n;
+            for (int p = 0; p < n; ++p) {
+                const int slot = p + symInd + 2 * TT - n + 1;
+                if (p < filled && valid_[slot]) vec_unit(tc[p], n, p);
+                else vec_zero(tc[p], n);
+            }
+            const int symbolIndex = n - 1 - symInd;
+            const int prev = symbolIndex - (n - k);  // == index: header entries already sent
+            Vec out;
+            vec_zero(out, n);
+            int hdr = 0;
+            if (n - symInd <= k) {  // forward from a partial diagonal (:252-301)
+                for (int i = 0; i < n; ++i) tempHeader[i] = 0;
+                for (int s2 = 0; s2 < prev; ++s2) tempHeader[s2] = header_[n2 - (prev - s2) - 1][s2];
+                bool found = false;
+                if (burst && index <= k - 1) {
+                    hdr = index + 1;
+                    found = true;
+                } else {
+                    for (int kk = index; kk < n - symInd; ++kk) {
+                        if (er_[kk + symInd + 2 * TT - n + 1] != 0) continue;
+                        bool sent = false;
+                        for (int jj = 0; jj < kk; ++jj)
+                            if (tempHeader[jj] == kk + 1) sent = true;
+                        if (!sent) {
+                            out = tc[kk];
+                            hdr = kk + 1;
+                            found = true;
+                            break;
+                        }
+                    }
+                }
+                if (!found) {  // zero symbol, first header value not used yet (:285-301)
+                    int pot;
+                    for (pot = 1; pot < n; ++pot) {
+                        bool used = false;
+                        for (int aa = 0; aa < prev; ++aa)
+                            if (tempHeader[aa] == pot) {
+                                used = true;
+                                break;
+                            }
+                        if (!used) break;
+                    }
+                    hdr = pot;
+                }
+            } else if (burst && index <= k - 1) {  // (:303-305)
+                hdr = index + 1;
+            } else {  // decode the diagonal, re-encode, forward a symbol not sent yet (:306-393)
+                for (int aa = 0; aa < n2; ++aa) stam[aa] = 0;
+                for (int aa = 0; aa < n - symInd; ++aa) stam[aa] = er_[aa + symInd + 2 * TT - n + 1];
+                for (int aa = n - symInd; aa < n; ++aa) stam[aa] = 1;
+                int erasure_count = 0;
+                for (int aa = 0; aa < n; ++aa) erasure_count += stam[aa] == 1;
+                sym_decode(*rules_, k, n, tc, stam);
+                for (int i = 0; i < k2; ++i) enc[i] = tc[i];  // memcpy + encodeBlock(t = k2-1)
+                for (int i = k2; i < n2; ++i) {
+                    vec_zero(enc[i], n);
+                    for (int d = 0; d < k2; ++d) vec_axpy(enc[i], G2_[d * n2 + i], tc[d], n);
+                }
+                for (int i = 0; i < n2; ++i) tempHeader[i] = 0;
+                for (int s2 = 0; s2 < prev; ++s2) tempHeader[s2] = header_[n2 - (prev - s2) - 1][s2];
+                bool assigned = false;
+                for (int i = 0; i < n2; ++i) {
+                    bool sent = false;
+                    for (int kk = 0; kk < prev; ++kk)
+                        if (tempHeader[kk] == i + 1) {
+                            sent = true;
+                            break;
+                        }
+                    if (sent) continue;
+                    if (burst || erasure_count <= n - k) {
+                        out = enc[i];
+                        hdr = i + 1;
+                        assigned = true;
+                        break;
+                    } else if (stam[i] == 0) {  // not decodable: forward (:361-371)
+                        out = tc[i];
+                        hdr = i + 1;
+                        assigned = true;
+                        break;
+                    }
+                }
+                if (!assigned) {  // (:375-393)
+                    for (int i = 0; i < n2; ++i) {
+                        bool sent = false;
+                        for (int kk = 0; kk < index; ++kk)
+                            if (tempHeader[kk] == i + 1) {
+                                sent = true;
+                                break;
+                            }
+                        if (!sent) {
+                            hdr = i + 1;
+                            break;
+                        }
+                    }
+                    if (!hdr) hdr = header_[n2 - 1][index];  // unreachable: index < n2 values used
+                }
+            }
+            header_[n2 - 1][index] = hdr;
+            std::memcpy(coef + index * n, out.c, static_cast<size_t>(n));
+        }
+        for (int aa = 0; aa < kHdr; ++aa) rec[aa] = static_cast<uint8_t>(header_[n2 - 1][aa]);
+    }
+
+    struct Memo {
+        int32_t id;
+        uint8_t hdr[kHdr];
+    };
+    int k_, n_, n2_, sdbo_;
+    std::shared_ptr<const DecodeRules> rules_;
+    std::vector<uint8_t> G2_;
+    uint8_t er_[kSlots];
+    uint8_t valid_[kSlots];  // the slot holds a received packet (not erased, not before packet 0)
+    int header_[kSlots][kHdr];
+    RecordTable records_;
+    std::vector<uint8_t> rec_;
+    std::string key_;
+    std::unordered_map<std::string, Memo> memo_;
+};
+
+// The destination: symbol_wise_decode_state_dependent per frame, symbolic.  Output record: k
+// rows of n coefficients (row s = data symbol s of every code block j = sum_q coef[q] * frame
+// symbol (j, q) of frame t2-s-(n-1-q)); the flag is returned.
+class SdDestPlanner {
+public:
+    SdDestPlanner(int k, int n, std::shared_ptr<const DecodeRules> rules)
+        : k_(k), n_(n), rules_(std::move(rules)), records_(k * n) {
+        rec_.resize(static_cast<size_t>(record_bytes()));
+        reset();
+    }
+    int record_bytes() const { return k_ * n_; }
+    const RecordTable& records() const { return records_; }
+    void reset() {
+        std::memset(valid_, 0, sizeof(valid_));
+        for (int i = 0; i < kSlots; ++i)
+            for (int jj = 0; jj < kHdr; ++jj) header_[i][jj] = jj + 1;
+        records_.clear();
+        memo_.clear();
+    }
+    // Frame t2 (in order): its record id; *flag = the loss flag.  The plan is a function of the
+    // header rows and presence of the last k+n-1 frames: repeated states are looked up.
+    int32_t step(bool erased, const uint8_t* hdr, bool* flag) {
+        for (int i = 0; i < kSlots - 1; ++i) {
+            std::memcpy(header_[i], header_[i + 1], sizeof(int) * kTT);
+            valid_[i] = valid_[i + 1];
+        }
+        for (int i = 0; i < kHdr; ++i) header_[kSlots - 1][i] = erased ? 0 : hdr[i];  // :1709, :1803
+        valid_[kSlots - 1] = erased ? 0 : 1;
+        const int lo = kSlots - k_ - n_ + 1;
+        key_.clear();
+        for (int r = lo; r < kSlots; ++r) {
+            key_.push_back(static_cast<char>(valid_[r]));
+            for (int e = 0; e < n_; ++e) key_.push_back(static_cast<char>(header_[r][e]));
+        }
+        auto it = memo_.find(key_);
+        if (it != memo_.end()) {
+            *flag = it->second.flag;
+            return it->second.id;
+        }
+        Memo m;
+        m.flag = decode(rec_.data());
+        m.id = records_.intern(rec_.data());
+        memo_.emplace(key_, m);
+        *flag = m.flag;
+        return m.id;
+    }
+
+private:
+    bool decode(uint8_t* rec) {
+        const int k = k_, n = n_, TT = kTT;
+        bool flag = false;
+        Vec tt[kMaxN];
+        uint8_t stam[kMaxN];
+        int th[kMaxN];
+        for (int ks = 0; ks < k; ++ks) {
+            for (int c = 0; c < n; ++c) vec_zero(tt[c], n);
+            int cnt = 0;
+            for (int q = 0; q < n; ++q) {  // :501-508 (slot 3T-1-ks-(n-1-q))
+                const int row = 3 * TT - 1 - ks - (n - 1 - q);
+                th[q] = header_[row][q];
+                cnt += th[q] == 0;
+            }
+            for (int q = 0; q < n; ++q) {  // reorder by header (:510-518)
+                const int h = th[q];
+                if (h != 0 && h < n + 1) {
+                    const int row = 3 * TT - 1 - ks - (n - 1 - q);
+                    if (valid_[row]) vec_unit(tt[h - 1], n, q);
+                    else vec_zero(tt[h - 1], n);
+                }
+            }
+            if (cnt > 0 && cnt < n - k + 1) {  // :525-533
+                for (int c = 0; c < n; ++c) stam[c] = 1;
+                for (int q = 0; q < n; ++q)
+                    if (th[q] != 0 && th[q] < n + 1) stam[th[q] - 1] = 0;
+                sym_decode(*rules_, k, n, tt, stam);
+            } else if (cnt >= n - k + 1) {
+                flag = true;
+            }
+            std::memcpy(rec + ks * n, tt[ks].c, static_cast<size_t>(n));
+        }
+        return flag;
+    }
+
+    struct Memo {
+        int32_t id;
+        bool flag;
+    };
+    int k_, n_;
+    std::shared_ptr<const DecodeRules> rules_;
+    uint8_t valid_[kSlots];
+    int header_[kSlots][kHdr];
+    RecordTable records_;
+    std::vector<uint8_t> rec_;
+    std::string key_;
+    std::unordered_map<std::string, Memo> memo_;
+};
+
+struct SdRelayArgs {
+    const uint8_t* cw;      // source codewords, rows of cw_stride bytes
+    int64_t cw_stride;
+    const int32_t* plan;    // per packet: record id
+    const uint8_t* table;   // records of R bytes: header[11], coef[n2][n]
+    int R;
+    int64_t P;
+    int k, n, n2, S, blocks;
+    const uint8_t* gf;      // exp[512], log[256]
+    uint8_t* frames;        // rows of F bytes
+    int F;
+};
+
+struct SdDestArgs {
+    const uint8_t* frames;  // relay frames, rows of F bytes; frame symbol (j, q) at 15 + j*n + q
+    int F;
+    const int32_t* plan;    // per seq: record id
+    const uint8_t* table;   // records of k*n bytes
+    int64_t P;
+    int k, n, S, blocks;
+    const uint8_t* gf;
+    uint8_t* out;           // rows of S*k bytes
+};
+
+__global__ __launch_bounds__(kSdThreads) void fec_sdswdf_relay_kernel(SdRelayArgs a) {
+    __shared__ uint8_t gexp[512];
+    __shared__ uint8_t glog[256];
+    for (int i = threadIdx.x; i < 512; i += kSdThreads) gexp[i] = a.gf[i];
+    for (int i = threadIdx.x; i < 256; i += kSdThreads) glog[i] = a.gf[512 + i];
+    __syncthreads();
+    const int k = a.k, n = a.n, n2 = a.n2, S = a.S;
+    const int64_t total = a.P * S;
+    for (int64_t id = static_cast<int64_t>(blockIdx.x) * kSdThreads + threadIdx.x; id < total;
+         id += static_cast<int64_t>(gridDim.x) * kSdThreads) {
+        const int64_t t = id / S;
+        const int j = static_cast<int>(id - t * S);
+        uint8_t* f = a.frames + t * a.F;
+        const uint8_t* rec = a.table + static_cast<int64_t>(a.plan[t]) * a.R;
+        if (j == 0) {  // [size BE16][header 11][codeword_new_vector's two leading zero bytes]
+            const int size = (S + 1) * n2;
+            f[0] = static_cast<uint8_t>(size >> 8);
+            f[1] = static_cast<uint8_t>(size);
+            for (int i = 0; i < kHdr; ++i) f[2 + i] = rec[i];
+            f[2 + kHdr] = 0;
+            f[3 + kHdr] = 0;
+        }
+        if (j == S - 1)
+            for (int o = 4 + kHdr + S * n2; o < a.F; ++o) f[o] = 0;
+        uint8_t* blk = f + 4 + kHdr + j * n2;
+        if (j >= a.blocks) {  // not relayed (:184-185): stays zero
+            for (int i = 0; i < n2; ++i) blk[i] = 0;
+            continue;
+        }
+        const uint8_t* coef = rec + kHdr;
+        for (int index = 0; index < n2; ++index) {
+            const int64_t u0 = t - (n - 1) + (k - 1 - index);  // packet of diagonal position 0
+            uint8_t acc = 0;
+            for (int p = 0; p < n; ++p) {
+                const uint8_t c = coef[index * n + p];
+                const int64_t u = u0 + p;
+                if (!c || u < 0) continue;
+                const uint8_t v = a.cw[u * a.cw_stride + j * n + p];
+                if (v) acc ^= gexp[glog[c] + glog[v]];
+            }
+            blk[index] = acc;
+        }
+    }
+}
+
+__global__ __launch_bounds__(kSdThreads) void fec_sdswdf_dest_kernel(SdDestArgs a) {
+    __shared__ uint8_t gexp[512];
+    __shared__ uint8_t glog[256];
+    for (int i = threadIdx.x; i < 512; i += kSdThreads) gexp[i] = a.gf[i];
+    for (int i = threadIdx.x; i < 256; i += kSdThreads) glog[i] = a.gf[512 + i];
+    __syncthreads();
+    const int k = a.k, n = a.n, S = a.S;
+    const int64_t total = a.P * S;
+    for (int64_t id = static_cast<int64_t>(blockIdx.x) * kSdThreads + threadIdx.x; id < total;
+         id += static_cast<int64_t>(gridDim.x) * kSdThreads) {
+        const int64_t t = id / S;
+        const int j = static_cast<int>(id - t * S);
+        uint8_t* o = a.out + t * static_cast<int64_t>(S) * k + j * k;
+        if (j >= a.blocks) {
+            for (int s = 0; s < k; ++s) o[s] = 0;
+            continue;
+        }
+        const uint8_t* coef = a.table + static_cast<int64_t>(a.plan[t]) * (k * n);
+        for (int s = 0; s < k; ++s) {
+            uint8_t acc = 0;
+            for (int q = 0; q < n; ++q) {
+                const uint8_t c = coef[s * n + q];
+                const int64_t u = t - s - (n - 1 - q);
+                if (!c || u < 0) continue;
+                const uint8_t v = a.frames[u * a.F + 4 + kHdr + j * n + q];
+                if (v) acc ^= gexp[glog[c] + glog[v]];
+            }
+            o[s] = acc;
+        }
+    }
+}
+
+int grid_for(int64_t items) {
+    return static_cast<int>(std::min<int64_t>((items + kSdThreads - 1) / kSdThreads, 16384));
+}
+
+// A device buffer that only grows.
+struct DevBuf {
+    void* p = nullptr;
+    size_t bytes = 0;
+    ~DevBuf() {
+        if (p) (void)hipFree(p);
+    }
+    int reserve(size_t want) {
+        if (want <= bytes) return FEC_OK;
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        bytes = 0;
+        if (hipMalloc(&p, want) != hipSuccess) return FEC_ERR_NOMEM;
+        bytes = want;
+        return FEC_OK;
+    }
+};
+
+}  // namespace
+}  // namespace fec
+
+struct fec_sdswdf {
+    // hop 1: Decoder(n1-1, n1-k, n1-k), the relay's decoder_current; hop 2: Encoder(n2-1, n2-k,
+    // n2-k) / the destination's decoder_current.  The device constants (the GF tables the kernels
+    // stage) come with the hop codecs, created on the first batch call: the planners are host only.
+    fec::Geometry g1, g2;
+    int T1 = 0, N1 = 0, T2 = 0, N2 = 0;
+    fec_codec* hop1 = nullptr;
+    fec_codec* hop2 = nullptr;
+    fec::CodecView v1, v2;
+    int sdbo = 0, blocks = 0, F = 0;
+    std::unique_ptr<fec::SdRelayPlanner> relay;
+    std::unique_ptr<fec::SdDestPlanner> dest;
+    std::vector<int32_t> plan;
+    std::vector<uint8_t> hdrs;
+    fec::DevBuf d_plan, d_table;
+    ~fec_sdswdf() {
+        if (hop1) fec_codec_destroy(hop1);
+        if (hop2) fec_codec_destroy(hop2);
+    }
+};
+
+namespace {
+
+int ensure_device(fec_sdswdf* w) {
+    if (w->hop1) return FEC_OK;
+    if (int st = fec_codec_create(w->g1.L, w->T1, w->N1, w->N1, &w->hop1)) return st;
+    if (int st = fec_codec_create(w->g2.L, w->T2, w->N2, w->N2, &w->hop2)) return st;
+    fec::codec_view(w->hop1, &w->v1);
+    fec::codec_view(w->hop2, &w->v2);
+    return FEC_OK;
+}
+
+// The relay's host plan for seqs 0..P-1 of a fresh relay: record ids in w->plan, records in
+// w->relay->records().
+void plan_relay(fec_sdswdf* w, const uint8_t* h_erasure, int64_t P) {
+    w->relay->reset();
+    w->plan.resize(static_cast<size_t>(P));
+    for (int64_t t = 0; t < P; ++t) w->plan[static_cast<size_t>(t)] = w->relay->step(h_erasure[t] != 0);
+}
+
+// The destination's host plan for seqs 0..P-1 given the frames' header bytes (11 per seq).
+void plan_dest(fec_sdswdf* w, const uint8_t* h_erasure, const uint8_t* hdrs, int64_t P, uint8_t* h_flag) {
+    w->dest->reset();
+    w->plan.resize(static_cast<size_t>(P));
+    for (int64_t t = 0; t < P; ++t) {
+        bool fl = false;
+        w->plan[static_cast<size_t>(t)] = w->dest->step(h_erasure[t] != 0, hdrs + t * fec::kHdr, &fl);
+        if (h_flag) h_flag[t] = fl ? 1 : 0;
+    }
+}
+
+int upload_plan(fec_sdswdf* w, const fec::RecordTable& tab, int64_t P, hipStream_t s) {
+    const size_t pb = static_cast<size_t>(P) * sizeof(int32_t);
+    const size_t tb = std::max<size_t>(tab.data().size(), 1);
+    if (int st = w->d_plan.reserve(pb)) return st;
+    if (int st = w->d_table.reserve(tb)) return st;
+    if (hipMemcpyAsync(w->d_plan.p, w->plan.data(), pb, hipMemcpyHostToDevice, s) != hipSuccess) return FEC_ERR_HIP;
+    if (!tab.data().empty() &&
+        hipMemcpyAsync(w->d_table.p, tab.data().data(), tab.data().size(), hipMemcpyHostToDevice, s) != hipSuccess)
+        return FEC_ERR_HIP;
+    return FEC_OK;
+}
+
+template <class F>
+int guarded_sd(F&& f) {
+    try {
+        return f();
+    } catch (const std::bad_alloc&) {
+        return FEC_ERR_NOMEM;
+    } catch (...) {
+        return FEC_ERR_ARG;
+    }
+}
+
+}  // namespace
+
+extern "C" {
+
+int fec_sdswdf_create(int max_payload, int T1, int N1, int T2, int N2, int sdbo, fec_sdswdf** out) {
+    if (!out) return FEC_ERR_ARG;
+    *out = nullptr;
+    // k2 == k (the only case Decoder_Symbol_Wise handles, :185), n2 <= n1 (the selection reads
+    // temp_codeword[i] for i < n2, :367), T <= T_TOT (header rows hold T_TOT+1 entries)
+    if (T1 < 0 || N1 < 0 || T2 < 0 || N2 < 0 || T1 - N1 != T2 - N2 || T1 - N1 + 1 < 1 || T1 > fec::kTT ||
+        T2 > T1 || (sdbo != 0 && sdbo != 1))
+        return FEC_ERR_ARG;
+    return guarded_sd([&] {
+        std::unique_ptr<fec_sdswdf> w(new fec_sdswdf());
+        w->g1 = fec::Geometry::make(max_payload, T1, N1, N1);
+        w->g2 = fec::Geometry::make(max_payload, T2, N2, N2);
+        w->T1 = T1;
+        w->N1 = N1;
+        w->T2 = T2;
+        w->N2 = N2;
+        const int k = w->g1.k, n1 = w->g1.n, n2 = w->g2.n;
+        w->sdbo = sdbo;
+        w->blocks = max_payload / k + 1;  // ceil(max_payload / k) + 1 on ints (:184-185)
+        w->F = 2 + fec::kHdr + (w->g1.S + 1) * n2;
+        w->relay.reset(new fec::SdRelayPlanner(k, n1, n2, sdbo, fec::shared_decode_rules(T1, N1, N1),
+                                               fec::make_generator(T2, N2, N2)));
+        w->dest.reset(new fec::SdDestPlanner(k, n2, fec::shared_decode_rules(T2, N2, N2)));
+        *out = w.release();
+        return static_cast<int>(FEC_OK);
+    });
+}
+
+int fec_sdswdf_destroy(fec_sdswdf* w) {
+    delete w;
+    return FEC_OK;
+}
+
+int fec_sdswdf_geometry(const fec_sdswdf* w, int* k, int* n1, int* n2, int* S, int* blocks, int* frame_bytes,
+                        int* delay) {
+    if (!w) return FEC_ERR_ARG;
+    if (k) *k = w->g1.k;
+    if (n1) *n1 = w->g1.n;
+    if (n2) *n2 = w->g2.n;
+    if (S) *S = w->g1.S;
+    if (blocks) *blocks = w->blocks;
+    if (frame_bytes) *frame_bytes = w->F;
+    if (delay) *delay = w->g1.n + w->g2.n - w->g1.k - 1;
+    return FEC_OK;
+}
+
+int fec_sdswdf_relay_plan(fec_sdswdf* w, const uint8_t* h_erasure, int64_t P, int32_t* h_plan,
+                          uint8_t* h_records, int64_t records_cap, int64_t* n_records, int* record_bytes) {
+    if (!w || P < 0 || (P > 0 && !h_erasure)) return FEC_ERR_ARG;
+    return guarded_sd([&] {
+        plan_relay(w, h_erasure, P);
+        const auto& d = w->relay->records().data();
+        if (n_records) *n_records = w->relay->records().count();
+        if (record_bytes) *record_bytes = w->relay->record_bytes();
+        if (h_plan) std::memcpy(h_plan, w->plan.data(), static_cast<size_t>(P) * sizeof(int32_t));
+        if (h_records) {
+            if (records_cap < static_cast<int64_t>(d.size())) return static_cast<int>(FEC_ERR_WORKSPACE);
+            std::memcpy(h_records, d.data(), d.size());
+        }
+        return static_cast<int>(FEC_OK);
+    });
+}
+
+int fec_sdswdf_dest_plan(fec_sdswdf* w, const uint8_t* h_erasure, const uint8_t* h_headers, int64_t P,
+                         int32_t* h_plan, uint8_t* h_flag, uint8_t* h_records, int64_t records_cap,
+                         int64_t* n_records, int* record_bytes) {
+    if (!w || P < 0 || (P > 0 && (!h_erasure || !h_headers))) return FEC_ERR_ARG;
+    return guarded_sd([&] {
+        plan_dest(w, h_erasure, h_headers, P, h_flag);
+        const auto& d = w->dest->records().data();
+        if (n_records) *n_records = w->dest->records().count();
+        if (record_bytes) *record_bytes = w->dest->record_bytes();
+        if (h_plan) std::memcpy(h_plan, w->plan.data(), static_cast<size_t>(P) * sizeof(int32_t));
+        if (h_records) {
+            if (records_cap < static_cast<int64_t>(d.size())) return static_cast<int>(FEC_ERR_WORKSPACE);
+            std::memcpy(h_records, d.data(), d.size());
+        }
+        return static_cast<int>(FEC_OK);
+    });
+}
+
+int fec_sdswdf_relay_batch(fec_sdswdf* w, const uint8_t* d_cw, int64_t cw_stride, const uint8_t* h_erasure,
+                           int64_t P, uint8_t* d_frames, void* stream) {
+    if (!w || P < 0) return FEC_ERR_ARG;
+    if (P == 0) return FEC_OK;
+    if (!d_cw || !h_erasure || !d_frames || cw_stride < static_cast<int64_t>(w->g1.S) * w->g1.n) return FEC_ERR_ARG;
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    return guarded_sd([&] {
+        if (int st = ensure_device(w)) return st;
+        plan_relay(w, h_erasure, P);
+        if (int st = upload_plan(w, w->relay->records(), P, s)) return st;
+        fec::SdRelayArgs a;
+        a.cw = d_cw;
+        a.cw_stride = cw_stride;
+        a.plan = static_cast<const int32_t*>(w->d_plan.p);
+        a.table = static_cast<const uint8_t*>(w->d_table.p);
+        a.R = w->relay->record_bytes();
+        a.P = P;
+        a.k = w->v1.k;
+        a.n = w->v1.n;
+        a.n2 = w->v2.n;
+        a.S = w->v1.S;
+        a.blocks = w->blocks;
+        a.gf = w->v1.gf;
+        a.frames = d_frames;
+        a.F = w->F;
+        hipLaunchKernelGGL(fec::fec_sdswdf_relay_kernel, dim3(fec::grid_for(P * a.S)), dim3(fec::kSdThreads), 0, s, a);
+        if (hipGetLastError() != hipSuccess) return static_cast<int>(FEC_ERR_HIP);
+        // the host plan arrays are reused by the next call
+        return hipStreamSynchronize(s) == hipSuccess ? static_cast<int>(FEC_OK) : static_cast<int>(FEC_ERR_HIP);
+    });
+}
+
+int fec_sdswdf_destination_batch(fec_sdswdf* w, const uint8_t* d_frames, const uint8_t* h_erasure, int64_t P,
+                                 uint8_t* d_out, uint8_t* h_flag, void* stream) {
+    if (!w || P < 0) return FEC_ERR_ARG;
+    if (P == 0) return FEC_OK;
+    if (!d_frames || !h_erasure || !d_out) return FEC_ERR_ARG;
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    return guarded_sd([&] {
+        if (int st = ensure_device(w)) return st;
+        // the frames' 11-byte headers drive the destination's control flow (:1663-1664): fetch them
+        w->hdrs.resize(static_cast<size_t>(P) * fec::kHdr);
+        if (hipMemcpy2DAsync(w->hdrs.data(), fec::kHdr, d_frames + 2, w->F, fec::kHdr, static_cast<size_t>(P),
+                             hipMemcpyDeviceToHost, s) != hipSuccess ||
+            hipStreamSynchronize(s) != hipSuccess)
+            return static_cast<int>(FEC_ERR_HIP);
+        plan_dest(w, h_erasure, w->hdrs.data(), P, h_flag);
+        if (int st = upload_plan(w, w->dest->records(), P, s)) return st;
+        fec::SdDestArgs a;
+        a.frames = d_frames;
+        a.F = w->F;
+        a.plan = static_cast<const int32_t*>(w->d_plan.p);
+        a.table = static_cast<const uint8_t*>(w->d_table.p);
+        a.P = P;
+        a.k = w->v2.k;
+        a.n = w->v2.n;
+        a.S = w->v2.S;
+        a.blocks = w->blocks;
+        a.gf = w->v2.gf;
+        a.out = d_out;
+        hipLaunchKernelGGL(fec::fec_sdswdf_dest_kernel, dim3(fec::grid_for(P * a.S)), dim3(fec::kSdThreads), 0, s, a);
+        if (hipGetLastError() != hipSuccess) return static_cast<int>(FEC_ERR_HIP);
+        return hipStreamSynchronize(s) == hipSuccess ? static_cast<int>(FEC_OK) : static_cast<int>(FEC_ERR_HIP);
+    });
+}
+
+}  // extern "C"

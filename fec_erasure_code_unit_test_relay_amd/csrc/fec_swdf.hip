@@ -24,8 +24,9 @@
 // the codec's decode rule for (w = n, erasure mask) (fec_host.cpp DecodeRules).  So the byte work
 // is two data-parallel kernels: a diagonal decode (one thread per (packet, block)) used by both
 // the relay and the destination, and the relay's re-encode.  Undefined behaviour of the reference
-// defined away ("Relay"): n flags (not n-1 plus garbage) reach decodeBlock, the block count
-// is S = ceil((L+2)/k) (not max_payload/k + 1), slots hold zero-padded packets, k2 == k.
+// defined away ("Relay"): n flags (not n-1 plus garbage) reach decodeBlock, slots hold
+// zero-padded packets, k2 == k.  The block count is the reference's ceil(max_payload/k)+1 on ints
+// (:553, :632; at most S): the blocks past it are not relayed and stay zero, as in the reference.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -45,7 +46,7 @@ struct SwDecodeArgs {
     int in_off;
     const uint8_t* er;      // per row: 1 = erased
     int64_t P;
-    int k, n, S;
+    int k, n, S, blocks;
     const uint8_t* rules;   // window-n rule table (raw coefficients)
     int ES;
     const uint8_t* gf;      // exp[512], log[256]
@@ -57,7 +58,7 @@ struct SwDecodeArgs {
 struct SwEncodeArgs {
     const uint8_t* y;       // rows of S*k bytes
     int64_t P;
-    int k, n2, S;
+    int k, n2, S, blocks;
     const uint8_t* G2;      // k x n2
     const uint8_t* gf;
     uint8_t* frames;        // rows of F = 2 + (S+1)*n2 bytes
@@ -76,6 +77,11 @@ __global__ __launch_bounds__(kSwThreads) void fec_swdf_decode_kernel(SwDecodeArg
          id += static_cast<int64_t>(gridDim.x) * kSwThreads) {
         const int64_t t = id / S;
         const int j = static_cast<int>(id - t * S);
+        uint8_t* o = a.out + t * a.out_stride + j * k;
+        if (j >= a.blocks) {  // not relayed / decoded (:553, :632)
+            for (int i = 0; i < k; ++i) o[i] = 0;
+            continue;
+        }
         uint32_t mask = 0;
         uint8_t d[32];
         for (int m = 0; m < n; ++m) {
@@ -103,7 +109,6 @@ __global__ __launch_bounds__(kSwThreads) void fec_swdf_decode_kernel(SwDecodeArg
             for (int i = 0; i < k; ++i)
                 if ((done >> i) & 1u) d[i] = rec[i];
         }
-        uint8_t* o = a.out + t * a.out_stride + j * k;
         for (int i = 0; i < k; ++i) o[i] = d[k - 1 - i];
         if (a.flag && j == 0) a.flag[t] = cnt >= n - k + 1 ? 1 : 0;
     }
@@ -135,6 +140,10 @@ __global__ __launch_bounds__(kSwThreads) void fec_swdf_encode_kernel(SwEncodeArg
         if (j == S - 1)
             for (int o = 4 + S * n2; o < a.F; ++o) f[o] = 0;
         uint8_t* blk = f + 4 + j * n2;
+        if (j >= a.blocks) {
+            for (int p = 0; p < n2; ++p) blk[p] = 0;
+            continue;
+        }
         const uint8_t* yt = a.y + t * Sk + j * k;
         for (int p = 0; p < k; ++p) blk[p] = yt[p];
         for (int p = k; p < n2; ++p) {
@@ -158,6 +167,7 @@ struct fec_swdf {
     fec_codec* hop2 = nullptr;  // Encoder(n2-1, n2-k, n2-k) / the destination's decoder_current
     fec::CodecView v1, v2;
     int F = 0;
+    int blocks = 0;  // ceil(max_payload / k) + 1 on ints (Decoder_Symbol_Wise.cpp:553, :632)
     ~fec_swdf() {
         if (hop1) fec_codec_destroy(hop1);
         if (hop2) fec_codec_destroy(hop2);
@@ -170,7 +180,7 @@ int grid_for(int64_t items) {
     return static_cast<int>(std::min<int64_t>((items + fec::kSwThreads - 1) / fec::kSwThreads, 8192));
 }
 
-int launch_diag_decode(const fec::CodecView& v, const uint8_t* in, int64_t in_stride, int in_off,
+int launch_diag_decode(const fec::CodecView& v, int blocks, const uint8_t* in, int64_t in_stride, int in_off,
                        const uint8_t* er, int64_t P, uint8_t* out, int64_t out_stride, uint8_t* flag,
                        hipStream_t s) {
     fec::SwDecodeArgs a;
@@ -182,6 +192,7 @@ int launch_diag_decode(const fec::CodecView& v, const uint8_t* in, int64_t in_st
     a.k = v.k;
     a.n = v.n;
     a.S = v.S;
+    a.blocks = blocks;
     if (v.wbase_n < 0) return FEC_ERR_ARG;  // n > 17: no window-n rule table
     a.rules = v.rules + v.wbase_n;
     a.ES = v.ES;
@@ -211,6 +222,7 @@ int fec_swdf_create(int max_payload, int T1, int N1, int T2, int N2, fec_swdf** 
         fec::codec_view(w->hop2, &w->v2);
         if (w->v1.S != w->v2.S || w->v1.n > 32 || w->v2.n > 32) return FEC_ERR_ARG;
         w->F = 2 + (w->v1.S + 1) * w->v2.n;
+        w->blocks = max_payload / w->v1.k + 1;
         *out = w.release();
         return FEC_OK;
     } catch (const std::bad_alloc&) {
@@ -251,13 +263,14 @@ int fec_swdf_relay_batch(fec_swdf* w, const uint8_t* d_cw, int64_t cw_stride, co
     hipStream_t s = static_cast<hipStream_t>(stream);
     uint8_t* y = static_cast<uint8_t*>(d_work);
     const int Sk = w->v1.S * w->v1.k;
-    if (int st = launch_diag_decode(w->v1, d_cw, cw_stride, 0, d_erasure, P, y, Sk, d_flag, s)) return st;
+    if (int st = launch_diag_decode(w->v1, w->blocks, d_cw, cw_stride, 0, d_erasure, P, y, Sk, d_flag, s)) return st;
     fec::SwEncodeArgs a;
     a.y = y;
     a.P = P;
     a.k = w->v2.k;
     a.n2 = w->v2.n;
     a.S = w->v2.S;
+    a.blocks = w->blocks;
     a.G2 = w->v2.G;
     a.gf = w->v2.gf;
     a.frames = d_frames;
@@ -272,7 +285,7 @@ int fec_swdf_destination_batch(fec_swdf* w, const uint8_t* d_frames, const uint8
     if (P == 0) return FEC_OK;
     if (!d_frames || !d_erasure || !d_out) return FEC_ERR_ARG;
     // frame symbol (j, m) at byte 4 + j*n2 + m (size header + codeword_new_vector's offset 2)
-    return launch_diag_decode(w->v2, d_frames, w->F, 4, d_erasure, P, d_out, w->v2.S * w->v2.k, d_flag,
+    return launch_diag_decode(w->v2, w->blocks, d_frames, w->F, 4, d_erasure, P, d_out, w->v2.S * w->v2.k, d_flag,
                               static_cast<hipStream_t>(stream));
 }
 

@@ -82,3 +82,113 @@ class SymbolWiseRelay:
         check(lib().fec_swdf_destination_batch(self._h, _ptr(frames), _ptr(erasure), P, _ptr(out), _ptr(flag),
                                                stream), "fec_swdf_destination_batch")
         return out, flag
+
+
+class StateDependentRelay:
+    """Fixed-rate SD-SWDF chain (RELAYING_TYPE 3): source (T1, N1, N1) -> relay
+    (symbol_wise_encode_state_dependent, Decoder_Symbol_Wise.cpp:178-432) -> destination
+    (symbol_wise_decode_state_dependent + extract_data, :487-546, :653-661), with
+    k = T1-N1+1 = T2-N2+1 and T2 <= T1 <= T_TOT = 10.  The erasure flags of both hops are host
+    arrays: they drive the host planner (the reference's per-packet control flow); the bytes stay
+    on the GPU."""
+
+    RECORD_HDR = 11
+
+    def __init__(self, max_payload: int, T1: int, N1: int, T2: int, N2: int, sdbo: int = 0):
+        h = ctypes.c_void_p()
+        check(lib().fec_sdswdf_create(max_payload, T1, N1, T2, N2, sdbo, ctypes.byref(h)), "fec_sdswdf_create")
+        self._h = h
+        v = [ctypes.c_int() for _ in range(7)]
+        check(lib().fec_sdswdf_geometry(h, *[ctypes.byref(x) for x in v]), "fec_sdswdf_geometry")
+        self.k, self.n1, self.n2, self.S, self.blocks, self.frame_bytes, self.delay = (x.value for x in v)
+        self.L = max_payload
+
+    def __del__(self):
+        if getattr(self, "_h", None):
+            try:
+                lib().fec_sdswdf_destroy(self._h)
+            except Exception:
+                pass
+            self._h = None
+
+    @staticmethod
+    def _host_flags(erasure, P):
+        import numpy as np
+        e = np.ascontiguousarray(np.asarray(erasure)[:P], dtype=np.uint8)
+        assert e.size == P
+        return e
+
+    def relay(self, codewords, erasure, frames=None):
+        """seqs 0..P-1: source codewords [P, >= S*n1] uint8 on the GPU (zero-padded rows; erased
+        rows are never read), hop-1 flags [P] (host array) -> frames [P, frame_bytes]."""
+        import torch
+        assert codewords.dtype == torch.uint8 and codewords.is_cuda and codewords.is_contiguous()
+        assert codewords.dim() == 2 and codewords.shape[1] >= self.S * self.n1
+        P = codewords.shape[0]
+        e = self._host_flags(erasure, P)
+        if frames is None:
+            frames = torch.empty((P, self.frame_bytes), dtype=torch.uint8, device=codewords.device)
+        assert frames.shape == (P, self.frame_bytes) and frames.is_contiguous() and frames.dtype == torch.uint8
+        stream = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+        check(lib().fec_sdswdf_relay_batch(self._h, _ptr(codewords), codewords.shape[1],
+                                           e.ctypes.data_as(ctypes.c_void_p), P, _ptr(frames), stream),
+              "fec_sdswdf_relay_batch")
+        return frames
+
+    def destination(self, frames, erasure, out=None):
+        """seqs 0..P-1: relay frames [P, frame_bytes] on the GPU, hop-2 flags [P] (host array) ->
+        (data_with_header rows [P, S*k] on the GPU (row t = source packet t - delay), flags [P]
+        numpy uint8)."""
+        import numpy as np
+        import torch
+        assert frames.dtype == torch.uint8 and frames.is_cuda and frames.is_contiguous()
+        assert frames.dim() == 2 and frames.shape[1] == self.frame_bytes
+        P = frames.shape[0]
+        e = self._host_flags(erasure, P)
+        if out is None:
+            out = torch.empty((P, self.S * self.k), dtype=torch.uint8, device=frames.device)
+        assert out.shape == (P, self.S * self.k) and out.is_contiguous() and out.dtype == torch.uint8
+        flag = np.zeros(P, dtype=np.uint8)
+        stream = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+        check(lib().fec_sdswdf_destination_batch(self._h, _ptr(frames), e.ctypes.data_as(ctypes.c_void_p), P,
+                                                 _ptr(out), flag.ctypes.data_as(ctypes.c_void_p), stream),
+              "fec_sdswdf_destination_batch")
+        return out, flag
+
+    def relay_plan(self, erasure):
+        """The relay's host plan alone (no GPU): (record id per seq [P] int32, records [R, 11 +
+        n2*n1] uint8: header bytes, then n2 rows of n1 coefficients)."""
+        import numpy as np
+        e = self._host_flags(erasure, len(erasure))
+        P = e.size
+        ids = np.zeros(P, dtype=np.int32)
+        n = ctypes.c_int64()
+        rb = ctypes.c_int()
+        check(lib().fec_sdswdf_relay_plan(self._h, e.ctypes.data_as(ctypes.c_void_p), P,
+                                          ids.ctypes.data_as(ctypes.c_void_p), None, 0, ctypes.byref(n),
+                                          ctypes.byref(rb)), "fec_sdswdf_relay_plan")
+        rec = np.zeros((n.value, rb.value), dtype=np.uint8)
+        check(lib().fec_sdswdf_relay_plan(self._h, e.ctypes.data_as(ctypes.c_void_p), P,
+                                          ids.ctypes.data_as(ctypes.c_void_p), rec.ctypes.data_as(ctypes.c_void_p),
+                                          rec.size, ctypes.byref(n), ctypes.byref(rb)), "fec_sdswdf_relay_plan")
+        return ids, rec
+
+    def dest_plan(self, erasure, headers):
+        """The destination's host plan alone (no GPU): headers [P, 11] = bytes 2..12 of every
+        frame -> (record id per seq, records [R, k*n2], flags [P])."""
+        import numpy as np
+        e = self._host_flags(erasure, len(erasure))
+        P = e.size
+        hd = np.ascontiguousarray(headers[:P], dtype=np.uint8)
+        assert hd.shape == (P, 11)
+        ids = np.zeros(P, dtype=np.int32)
+        fl = np.zeros(P, dtype=np.uint8)
+        n = ctypes.c_int64()
+        rb = ctypes.c_int()
+        args = [self._h, e.ctypes.data_as(ctypes.c_void_p), hd.ctypes.data_as(ctypes.c_void_p), P,
+                ids.ctypes.data_as(ctypes.c_void_p), fl.ctypes.data_as(ctypes.c_void_p)]
+        check(lib().fec_sdswdf_dest_plan(*args, None, 0, ctypes.byref(n), ctypes.byref(rb)), "fec_sdswdf_dest_plan")
+        rec = np.zeros((n.value, rb.value), dtype=np.uint8)
+        check(lib().fec_sdswdf_dest_plan(*args, rec.ctypes.data_as(ctypes.c_void_p), rec.size, ctypes.byref(n),
+                                         ctypes.byref(rb)), "fec_sdswdf_dest_plan")
+        return ids, rec, fl

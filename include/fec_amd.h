@@ -313,6 +313,42 @@ int fec_swdf_relay_batch(fec_swdf *swdf, const uint8_t *d_cw, int64_t cw_stride,
 int fec_swdf_destination_batch(fec_swdf *swdf, const uint8_t *d_frames, const uint8_t *d_erasure, int64_t P,
                                uint8_t *d_out, uint8_t *d_flag, void *hip_stream);
 
+/* ---- relay: state-dependent symbol-wise decode-and-forward (SD-SWDF, RELAYING_TYPE 3) --------
+ * Decoder_Symbol_Wise::symbol_wise_encode_state_dependent (src/Decoder_Symbol_Wise.cpp:178-432) at
+ * the relay and symbol_wise_decode_state_dependent + extract_data (:487-546, :653-661) at the
+ * destination, as Variable_Rate_FEC_Decoder drives them with one relay frame per seq
+ * (src/Variable_Rate_FEC_Decoder.cpp:636-675, 1458-1493 relay; :1703-1721, 1798-1815 destination),
+ * fixed rate, k = T1-N1+1 = T2-N2+1, T2 <= T1 <= T_TOT = 10; sdbo = FLAG_FOR_SDBO (FEC_Macro.h:50
+ * ships 0).  The control flow depends only on erasure flags and headers: a host planner replays it
+ * per packet (serial, like the reference) and the GPU applies the per-packet plans to the bytes.
+ * A batch runs a fresh relay / destination over seqs 0..P-1; both calls return when done.
+ *   fec_sdswdf_relay_batch: d_cw P rows of cw_stride bytes (source codewords zero-padded to >= S*n1;
+ *     erased rows are never read), h_erasure P hop-1 flags (host) -> d_frames P rows of frame_bytes:
+ *     [size BE16][header 11 bytes][codeword_new_vector[n2-1][0..size)], size = (S+1)*n2.
+ *   fec_sdswdf_destination_batch: d_frames (rows of frame_bytes; the 11 header bytes of every
+ *     received frame steer the decode), h_erasure P hop-2 flags (host) -> d_out P rows of S*k
+ *     bytes: row t = data_with_header of source packet t - delay (blocks*k decoded, rest zero);
+ *     h_flag (host, may be NULL): 1 when a diagonal had too many erasures (the loss counter).
+ *   fec_sdswdf_relay_plan / fec_sdswdf_dest_plan: the host plans alone (tests): per seq a record id,
+ *     and the distinct records: relay = header[11] + n2 rows of n1 coefficients (frame symbol i of
+ *     block j = sum_p coef[i][p] * symbol (j, p) of source packet t-(n1-1)+p+(k-1-i)); destination
+ *     = k rows of n2 coefficients (data symbol s of block j = sum_q coef[s][q] * frame symbol
+ *     (j, q) of frame t-s-(n2-1-q)). */
+typedef struct fec_sdswdf fec_sdswdf;
+int fec_sdswdf_create(int max_payload, int T1, int N1, int T2, int N2, int sdbo, fec_sdswdf **out);
+int fec_sdswdf_destroy(fec_sdswdf *w);
+int fec_sdswdf_geometry(const fec_sdswdf *w, int *k, int *n1, int *n2, int *S, int *blocks,
+                        int *frame_bytes, int *delay);
+int fec_sdswdf_relay_batch(fec_sdswdf *w, const uint8_t *d_cw, int64_t cw_stride, const uint8_t *h_erasure,
+                           int64_t P, uint8_t *d_frames, void *hip_stream);
+int fec_sdswdf_destination_batch(fec_sdswdf *w, const uint8_t *d_frames, const uint8_t *h_erasure, int64_t P,
+                                 uint8_t *d_out, uint8_t *h_flag, void *hip_stream);
+int fec_sdswdf_relay_plan(fec_sdswdf *w, const uint8_t *h_erasure, int64_t P, int32_t *h_plan,
+                          uint8_t *h_records, int64_t records_cap, int64_t *n_records, int *record_bytes);
+int fec_sdswdf_dest_plan(fec_sdswdf *w, const uint8_t *h_erasure, const uint8_t *h_headers, int64_t P,
+                         int32_t *h_plan, uint8_t *h_flag, uint8_t *h_records, int64_t records_cap,
+                         int64_t *n_records, int *record_bytes);
+
 /* ---- erasure patterns (inputs of the decode path; host only, no device needed) ---------------
  * Byte-exact restatements of Erasure_File_Generator (src/Erasure_File_Generator.cpp:25-287): out[i]
  * = 1 if packet i is erased.  Same engine (mt19937), same draw order and the same libstdc++

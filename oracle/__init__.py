@@ -67,6 +67,10 @@ def lib() -> ctypes.CDLL:
         L.or_swdf_run.restype = ctypes.c_int
         L.or_swdf_run.argtypes = [ctypes.c_int] * 5 + [ctypes.c_int64, u8p, u8p, ctypes.c_uint64,
                                                         u8p, u8p, u8p, u8p]
+        L.or_sdswdf_run.restype = ctypes.c_int
+        L.or_sdswdf_run.argtypes = [ctypes.c_int] * 5 + [ctypes.c_int64, u8p, u8p, ctypes.c_uint64,
+                                                          ctypes.c_int, u8p, u8p, u8p]
+        L.or_sdswdf_set_garbage.argtypes = [ctypes.c_int]
         L.or_vr_run.restype = ctypes.c_int64
         i64p = ctypes.POINTER(ctypes.c_int64)
         L.or_vr_run.argtypes = [ctypes.c_int] * 5 + [u8p, ctypes.c_int64, ctypes.c_int64, ctypes.c_uint64, ip,
@@ -247,6 +251,31 @@ def swdf_run(max_payload: int, T1: int, N1: int, T2: int, N2: int, P: int, e1: n
     if st != 0:
         raise ValueError("unsupported SWDF configuration")
     return dict(frames=frames, relay_flag=rf, dest_out=out, dest_flag=df, delay=n1 + n2 - k - 1, S=S, k=k)
+
+
+def sdswdf_run(max_payload: int, T1: int, N1: int, T2: int, N2: int, P: int, e1: np.ndarray,
+               e2: np.ndarray, seed: int = 0x5EED, sdbo: int = 0, garbage: int = 0):
+    """The local simulation's state-dependent SWDF chain (RELAYING_TYPE 3, one relay frame per seq):
+    source FEC_Encoder -> hop 1 -> relay symbol_wise_encode_state_dependent -> hop 2 -> destination
+    symbol_wise_decode_state_dependent + extract_data.  Returns dict(frames [P, 2+11+(S+1)*n2],
+    dest_out [P, S*k] (data_with_header), dest_flag [P], delay = n1+n2-k-1).  `garbage` is the
+    relay's temp_codeword content at the start of each call (outputs must not depend on it)."""
+    k, n1, n2 = T1 - N1 + 1, T1 + 1, T2 + 1
+    S = -(-(max_payload + 2) // k)
+    F = 2 + 11 + (S + 1) * n2
+    a = np.ascontiguousarray(e1[:P], dtype=np.uint8)
+    b = np.ascontiguousarray(e2[:P], dtype=np.uint8)
+    assert a.size == P and b.size == P
+    frames = np.zeros((P, F), dtype=np.uint8)
+    out = np.zeros((P, S * k), dtype=np.uint8)
+    df = np.zeros(P, dtype=np.uint8)
+    lib().or_sdswdf_set_garbage(garbage)
+    st = lib().or_sdswdf_run(max_payload, T1, N1, T2, N2, P, _u8(a), _u8(b), seed, sdbo, _u8(frames),
+                             _u8(out), _u8(df))
+    lib().or_sdswdf_set_garbage(0)
+    if st != 0:
+        raise ValueError("unsupported SD-SWDF configuration")
+    return dict(frames=frames, dest_out=out, dest_flag=df, delay=n1 + n2 - k - 1, S=S, k=k)
 
 
 def vr_run(pattern: np.ndarray, P: int, max_payload: int = 300, T: int = 10, B: int = -1, N: int = -1,

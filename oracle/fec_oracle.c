@@ -562,9 +562,10 @@ int64_t or_encode_stream(int max_payload, int T, int B, int N, int64_t seq0, int
 /*   - the erasure vector handed to decodeBlock is malloc(T_TOT) (relay, :561) or                 */
 /*     malloc(T_INITIAL) = 5 bytes (destination, :633) with only n-1 entries written and n read   */
 /*     (:571-573, :641-643): here it holds all n window flags;                                    */
-/*   - the block count is `ceil(max_payload / k) + 1` in integer arithmetic (:553, :632), which    */
-/*     differs from the codeword's S = ceil((max_payload+2)/k) sub-streams for some k (k = 1, 7,   */
-/*     ...): here it is S;                                                                         */
+/*   (the block count is the reference's `ceil(max_payload / k) + 1` in integer arithmetic       */
+/*     (:553, :632): it is at most the codeword's S = ceil((max_payload+2)/k) sub-streams, so every */
+/*     read stays inside the codeword; for k = 1, 7 at L = 300 the last sub-stream is not relayed, */
+/*     as in the reference, and the destination's bytes of that block stay zero)                   */
 /*   - push_current_codeword copies GLOBAL_MAX_SIZE_OF_CODEWORD bytes to offset 2 of a buffer of   */
 /*     that size (:136) and reads past the received packet: here the slot holds the packet        */
 /*     zero-padded (a trimmed wire codeword re-padded, as FEC_Decoder does);                      */
@@ -574,7 +575,7 @@ int64_t or_encode_stream(int max_payload, int T, int B, int N, int64_t seq0, int
 #define OR_SW_SLOT 20000 /* GLOBAL_MAX_SIZE_OF_CODEWORD (FEC_Macro.h:49) */
 
 struct or_swdf {
-    int L, k, n, n2, S;
+    int L, k, n, n2, S, blocks;
     uint8_t *cv[OR_SW_WIN];  /* codeword_vector (received packet at offset 2) */
     uint8_t *cnv[OR_SW_WIN]; /* codeword_new_vector (relay output, symbols at offset 2) */
     uint8_t er[OR_SW_WIN];   /* temp_erasure_vector */
@@ -592,6 +593,7 @@ or_swdf *or_swdf_new(int max_payload, int k, int n, int n2) {
     s->n = n;
     s->n2 = n2;
     s->S = or_ceil_div(max_payload + 2, k);
+    s->blocks = max_payload / k + 1; /* ceil(max_payload / k) + 1 on ints: :553, :632 */
     for (int i = 0; i < OR_SW_WIN; i++) {
         s->cv[i] = (uint8_t *)calloc(OR_SW_SLOT, 1);
         s->cnv[i] = (uint8_t *)calloc(OR_SW_SLOT, 1);
@@ -644,7 +646,7 @@ int or_swdf_encode_1(or_swdf *s) {
     const int k = s->k, n = s->n, k2 = s->k, n2 = s->n2;
     int erasure_counter = 0;
     for (int i = 0; i < n; i++) erasure_counter += s->er[i] == 1;
-    const int blocks = s->S;
+    const int blocks = s->blocks;
     uint8_t temp_codeword[OR_MAXN], temp_encoded_codeword[OR_MAXN], stam[OR_MAXN];
     int flag = 0;
     for (int j = 0; j < blocks; j++) {
@@ -692,7 +694,7 @@ int or_swdf_decode_1(or_swdf *s, uint8_t *out) {
     uint8_t temp_codeword[OR_MAXN], stam[OR_MAXN];
     uint8_t *buffer = (uint8_t *)calloc((size_t)s->S * n, 1);
     int flag = 0;
-    for (int j = 0; j < s->S; j++) {
+    for (int j = 0; j < s->blocks; j++) {
         for (int i = 0; i < n; i++)
             temp_codeword[n - 1 - i] = s->cv[n - 1 - i][4 + (j + 1) * n - 1 - i]; /* :636-639 */
         if (erasure_counter > 0 && erasure_counter < n - k + 1) {
@@ -704,8 +706,9 @@ int or_swdf_decode_1(or_swdf *s, uint8_t *out) {
         for (int i = 0; i < n; i++) buffer[j * n + i] = temp_codeword[n - 1 - i]; /* :647-649 */
     }
     int ind = 0; /* extract_data, :653-661 */
-    for (int j = 0; j < s->S; j++)
+    for (int j = 0; j < s->blocks; j++)
         for (int i = 0; i < k; i++) out[ind++] = buffer[j * n + n - k + i];
+    while (ind < s->S * k) out[ind++] = 0; /* blocks < S: the unrelayed tail */
     free(buffer);
     return flag;
 }
@@ -760,6 +763,387 @@ int or_swdf_run(int max_payload, int T1, int N1, int T2, int N2, int64_t P, cons
     or_encoder_free(src);
     or_swdf_free(relay);
     or_swdf_free(dest);
+    return 0;
+}
+
+/* ------------------------------------------------------------------------------------------ */
+/* State-dependent symbol-wise decode-and-forward (SD-SWDF, RELAYING_TYPE 3):                   */
+/* Decoder_Symbol_Wise::symbol_wise_encode_state_dependent (Decoder_Symbol_Wise.cpp:178-432) at  */
+/* the relay and symbol_wise_decode_state_dependent (:487-546) + extract_data (:653-661) at the */
+/* destination, driven as Variable_Rate_FEC_Decoder does at a fixed rate with one relay frame   */
+/* per seq (FLAG_FOR_CONSTANT_TRANS = 1): relay received packet :1458-1493, relay erased packet */
+/* :636-675, destination received frame :1798-1815, destination missing frame :1703-1721.       */
+/* The relay keeps the last 3*T_TOT packets (codeword_vector_state_dependent, the current one   */
+/* in slot 2*T_TOT) with their erasure flags and the per-packet headers it sent (header[row][i] */
+/* = which symbol of the hop-2 diagonal codeword the frame's symbol i carries, 1-based; 0 =    */
+/* none).  Per index of the outgoing frame it forwards a received symbol of a partially         */
+/* received diagonal (symInd >= n-k), or decodes a complete diagonal and forwards a re-encoded  */
+/* symbol the destination has not had yet.                                                      */
+/* Reference behaviour kept as it is (all of it well-defined):                                  */
+/*   - the burst test's `if (in_burst=false)` / `if (in_burst=true)` assignments (:213, :216):   */
+/*     the longest erasure run and its end are found as written; the test only matters with     */
+/*     FLAG_FOR_SDBO = 1 (FEC_Macro.h:50 ships 0), a run-time flag here;                        */
+/*   - header rows are shifted 10 (T_TOT) ints of 11 (:133, :169): entry 10 of a row keeps      */
+/*     whatever was last written to that row, and the destination reads it (:507);             */
+/*   - decodeBlock clears the erasure flags of what it recovers (codingOperations.cpp:224-229), */
+/*     so the relay's "forward a received symbol" branch (:361) also forwards recovered data;  */
+/*   - the relay's flag is never set (:195), and the block count is ceil(max_payload/k)+1 on    */
+/*     ints (:184-185, :494, :655).                                                             */
+/* Defined away (undefined behaviour of the reference):                           */
+/*   - the received packet is copied with GLOBAL_MAX_SIZE_OF_CODEWORD bytes from the message    */
+/*     (Variable_Rate_FEC_Decoder.cpp:1461, :1804): here the slot holds the packet zero-padded; */
+/*   - stam_erasure_vector[T_TOT+1] is written up to index n-symInd-1 >= n (:309-312) and       */
+/*     temp_encoded_codeword[n2] receives n bytes (:325): both are large enough here (only the  */
+/*     first n / n2 entries are ever read back when n2 <= n, which is required);                */
+/*   - temp_codeword keeps stale values from the previous diagonal in the positions a partial  */
+/*     diagonal does not fill (:248-250): those are artificially erased parity positions that   */
+/*     decodeBlock and encodeBlock never read and the selection never forwards -- the oracle    */
+/*     fills temp_codeword with a settable garbage byte at every call to prove that;            */
+/*   - header[i] is malloc(sizeof(int)*T_TOT+1) = 41 bytes but entry 10 is used (:28, :60):    */
+/*     the row has 11 ints here (glibc's 41-byte chunk holds 56 bytes, so entry 10 works there  */
+/*     too);                                                                                     */
+/*   - the relay's erased-packet path stores the frame 11 bytes short (:665 overwrites :657):   */
+/*     the truncated tail would reach the destination as stale receive-buffer bytes; the frame */
+/*     here has the full size the relay reports (:655).                                         */
+/* ------------------------------------------------------------------------------------------ */
+#define OR_TTOT 10            /* T_TOT, FEC_Macro.h:32 */
+#define OR_SD_SLOTS (3 * OR_TTOT)
+#define OR_SD_HDR (OR_TTOT + 1)
+#define OR_SD_SLOT 8192       /* >= every codeword / frame here (GLOBAL_MAX_SIZE_OF_CODEWORD is 20000) */
+
+static int g_sd_garbage = 0; /* temp_codeword's content at the start of a call (see above) */
+void or_sdswdf_set_garbage(int v) { g_sd_garbage = v & 255; }
+
+struct or_sdswdf {
+    int L, k, n, n2, S, blocks;
+    uint8_t *sd[OR_SD_SLOTS];          /* codeword_vector_state_dependent (packet at offset 2) */
+    uint8_t er[OR_SD_SLOTS];           /* temp_erasure_vector_state_dependent */
+    int header[OR_SD_SLOTS][OR_SD_HDR];
+    uint8_t *cnv;                      /* codeword_new_vector[n2-1]: the only row the relay writes */
+                                       /* and sends; the shift (:124-129) never moves into it      */
+    uint8_t G1[OR_MAXK * OR_MAXN];     /* decoder_current->getG(): Decoder(n-1, n-k, n-k) */
+    uint8_t G2[OR_MAXK * OR_MAXN];     /* encoder_current->getG(): Encoder(n2-1, n2-k2, n2-k2) */
+    uint8_t tc[OR_MAXN];               /* temp_codeword (a stack array kept across iterations) */
+    uint8_t cnsw[30000];               /* codeword_new_symbol_wise */
+};
+
+/* Decoder_Symbol_Wise::Decoder_Symbol_Wise, :16-65 (state-dependent part). */
+or_sdswdf *or_sdswdf_new(int max_payload, int k, int n, int n2) {
+    or_gf_init();
+    if (k < 1 || n < k || n > OR_SD_HDR || n2 < 0 || n2 > n || (n2 > 0 && n2 < k)) return NULL;
+    or_sdswdf *s = (or_sdswdf *)calloc(1, sizeof(or_sdswdf));
+    s->L = max_payload;
+    s->k = k;
+    s->n = n;
+    s->n2 = n2;
+    s->S = or_ceil_div(max_payload + 2, k);
+    s->blocks = max_payload / k + 1;
+    for (int i = 0; i < OR_SD_SLOTS; i++) {
+        s->sd[i] = (uint8_t *)calloc(OR_SD_SLOT, 1);
+        for (int jj = 0; jj < OR_SD_HDR; jj++) s->header[i][jj] = jj + 1; /* :60-62 */
+    }
+    s->cnv = (uint8_t *)calloc(OR_SD_SLOT, 1);
+    or_gen_G(s->G1, n - 1, n - k, n - k, k, n);
+    if (n2 > 0) or_gen_G(s->G2, n2 - 1, n2 - k, n2 - k, k, n2);
+    return s;
+}
+
+void or_sdswdf_free(or_sdswdf *s) {
+    if (!s) return;
+    for (int i = 0; i < OR_SD_SLOTS; i++) free(s->sd[i]);
+    free(s->cnv);
+    free(s);
+}
+
+/* The state-dependent part of push_current_codeword / rotate_pointers_and_insert_zero_word
+ * (:131-135, :167-171): slots, flags and the first T_TOT ints of every header row move down. */
+static void or_sd_shift(or_sdswdf *s) {
+    uint8_t *first = s->sd[0];
+    for (int i = 0; i < OR_SD_SLOTS - 1; i++) {
+        s->sd[i] = s->sd[i + 1]; /* memcpy of the whole slot: same content */
+        memcpy(s->header[i], s->header[i + 1], sizeof(int) * OR_TTOT);
+        s->er[i] = s->er[i + 1];
+    }
+    memcpy(first, s->sd[OR_SD_SLOTS - 2], OR_SD_SLOT); /* the last slot keeps its own content */
+    s->sd[OR_SD_SLOTS - 1] = first;
+}
+
+/* Relay: a received packet goes to slot 2*T_TOT (Variable_Rate_FEC_Decoder.cpp:1459-1463), an
+ * erased one is a zero slot flagged erased (:638-643). */
+void or_sdswdf_relay_push(or_sdswdf *s, const uint8_t *cw, int size, int erased) {
+    or_sd_shift(s);
+    uint8_t *slot = s->sd[2 * OR_TTOT];
+    memset(slot, 0, OR_SD_SLOT);
+    if (!erased && cw && size > 0) memcpy(slot + 2, cw, (size_t)(size < OR_SD_SLOT - 2 ? size : OR_SD_SLOT - 2));
+    s->er[2 * OR_TTOT] = erased ? 1 : 0;
+}
+
+/* Destination: a received frame (its 11 header bytes and codeword) goes to slot 3*T_TOT-1 and
+ * header row 3*T_TOT-1 (:1799-1806); a missing one is a zero slot, a zero header row, flagged
+ * erased (:1705-1712). */
+void or_sdswdf_dest_push(or_sdswdf *s, const uint8_t *frame, int frame_bytes, int erased) {
+    or_sd_shift(s);
+    uint8_t *slot = s->sd[3 * OR_TTOT - 1];
+    memset(slot, 0, OR_SD_SLOT);
+    for (int i = 0; i < OR_SD_HDR; i++) s->header[3 * OR_TTOT - 1][i] = erased ? 0 : (int)frame[2 + i];
+    if (!erased) {
+        int size = frame_bytes - 2 - OR_SD_HDR;
+        if (size > OR_SD_SLOT - 2) size = OR_SD_SLOT - 2;
+        if (size > 0) memcpy(slot + 2, frame + 2 + OR_SD_HDR, (size_t)size);
+    }
+    s->er[3 * OR_TTOT - 1] = erased ? 1 : 0;
+}
+
+/* symbol_wise_encode_state_dependent, Decoder_Symbol_Wise.cpp:178-432 (k2 == k). */
+void or_sdswdf_encode(or_sdswdf *s, int sdbo) {
+    const int k = s->k, n = s->n, k2 = s->k, n2 = s->n2, TT = OR_TTOT;
+    const int blocks = s->blocks; /* :184-185 */
+    uint8_t *temp_codeword = s->tc;
+    uint8_t temp_encoded_codeword[OR_MAXN];
+    uint8_t stam[OR_MAXN];
+    int tempHeader[OR_MAXN];
+    memset(temp_codeword, g_sd_garbage, OR_MAXN);
+    /* burst check, :198-231 */
+    int is_burst_longer_than_N = 0;
+    for (int aa = 0; aa < n; aa++) stam[aa] = s->er[2 * TT - n + 1 + aa];
+    int longest_burst_length = 0, index_end_burst = 0, in_burst = 0, temp_burst_length = 0;
+    for (int aa = 0; aa < n; aa++) {
+        if (stam[aa] == 1) {
+            temp_burst_length++;
+            if ((in_burst = 0)) in_burst = 1; /* :213-214 as written */
+        } else {
+            if ((in_burst = 1)) {             /* :216, always taken */
+                in_burst = 0;
+                if (temp_burst_length > longest_burst_length) {
+                    longest_burst_length = temp_burst_length;
+                    index_end_burst = aa - 1;
+                }
+                temp_burst_length = 0;
+            }
+        }
+    }
+    if (temp_burst_length > longest_burst_length) {
+        longest_burst_length = temp_burst_length;
+        index_end_burst = n - 1;
+    }
+    if ((sdbo == 1) & (longest_burst_length > n - k) && index_end_burst >= k - 1) is_burst_longer_than_N = 1;
+    (void)in_burst;
+    for (int j = 0; j < blocks; j++) { /* :233 */
+        int index = -1;
+        for (int symInd = k - 1; symInd >= -(n2 - k2); symInd--) { /* :239 */
+            index++;
+            int symbolIndex = -1;
+            for (int i = symInd; i < n; i++) { /* :244-251 */
+                symbolIndex++;
+                if (i < (n < n + symInd ? n : n + symInd))
+                    temp_codeword[symbolIndex] = s->sd[i + 2 * TT - n + 1][2 + j * n + symbolIndex];
+            }
+            uint8_t *dst = &s->cnsw[2 + j * n2 + index];
+            if (n - symInd <= k) { /* forward a received symbol of a partial diagonal, :252-301 */
+                int notFoundSym = 1;
+                int symbolIndex2 = -1;
+                for (int i = 0; i < n; i++) tempHeader[i] = 0;
+                for (int i = symbolIndex - (n - k); i >= 1; i--) {
+                    symbolIndex2++;
+                    tempHeader[symbolIndex2] = s->header[n2 - i - 1][symbolIndex2];
+                }
+                if (is_burst_longer_than_N && index <= k - 1) {
+                    *dst = 0;
+                    s->header[n2 - 1][index] = index + 1;
+                    notFoundSym = 0;
+                } else {
+                    for (int kk = index; kk < n - symInd; kk++) {
+                        if (s->er[kk + symInd + 2 * TT - n + 1] == 0) {
+                            int notFoundFlag = 1; /* not sent before, :271-275 */
+                            for (int jj = 0; jj < kk; jj++)
+                                if (tempHeader[jj] == kk + 1) notFoundFlag = 0;
+                            if (notFoundFlag) {
+                                *dst = temp_codeword[kk];
+                                s->header[n2 - 1][index] = kk + 1;
+                                notFoundSym = 0;
+                                break;
+                            }
+                        }
+                    }
+                }
+                if (notFoundSym) { /* :285-301 */
+                    *dst = 0;
+                    int potIndex;
+                    for (potIndex = 1; potIndex < n; potIndex++) {
+                        int notFoundInd = 1;
+                        for (int aa = 0; aa <= symbolIndex2; aa++)
+                            if (tempHeader[aa] == potIndex) {
+                                notFoundInd = 0;
+                                break;
+                            }
+                        if (notFoundInd) break;
+                    }
+                    s->header[n2 - 1][index] = potIndex;
+                }
+            } else { /* decode the diagonal and send a symbol not sent yet, :302-395 */
+                if (is_burst_longer_than_N && index <= k - 1) {
+                    *dst = 0;
+                    s->header[n2 - 1][index] = index + 1;
+                } else {
+                    for (int aa = 0; aa < n2; aa++) stam[aa] = 0;
+                    for (int aa = 0; aa < n - symInd; aa++) stam[aa] = s->er[aa + symInd + 2 * TT - n + 1];
+                    for (int aa = n - symInd; aa < n; aa++) stam[aa] = 1;
+                    int erasure_count = 0;
+                    for (int aa = 0; aa < n; aa++) erasure_count += stam[aa] == 1;
+                    or_decode_block(temp_codeword, s->G1, temp_codeword, stam, k, n, n - 1, 0); /* :322-324 */
+                    memcpy(temp_encoded_codeword, temp_codeword, (size_t)n);
+                    or_encode_block(temp_codeword, s->G2, temp_encoded_codeword, k2, n2, k2 - 1); /* :327-328 */
+                    for (int i = 0; i < n2; i++) tempHeader[i] = 0;
+                    int symbolIndex2 = -1;
+                    for (int i = symbolIndex - (n - k); i >= 1; i--) {
+                        symbolIndex2++;
+                        tempHeader[symbolIndex2] = s->header[n2 - i - 1][symbolIndex2];
+                    }
+                    int not_assinged_val = 1;
+                    for (int i = 0; i < n2; i++) { /* :344-374 */
+                        int notFoundFlag = 1;
+                        for (int kk = 0; kk < symbolIndex - (n - k); kk++)
+                            if (tempHeader[kk] == i + 1) {
+                                notFoundFlag = 0;
+                                break;
+                            }
+                        if (notFoundFlag) {
+                            if (is_burst_longer_than_N || erasure_count <= n - k) {
+                                *dst = temp_encoded_codeword[i];
+                                s->header[n2 - 1][index] = i + 1;
+                                not_assinged_val = 0;
+                                break;
+                            } else if (stam[i] == 0) { /* didn't decode: forward, :361-371 */
+                                if (sdbo == 1 && is_burst_longer_than_N)
+                                    *dst = temp_encoded_codeword[i];
+                                else
+                                    *dst = temp_codeword[i];
+                                s->header[n2 - 1][index] = i + 1;
+                                not_assinged_val = 0;
+                                break;
+                            }
+                        }
+                    }
+                    if (not_assinged_val) { /* too many erasures, :375-393 */
+                        *dst = 0;
+                        for (int i = 0; i < n2; i++) {
+                            int notFoundFlag = 1;
+                            for (int kk = 0; kk < index; kk++)
+                                if (tempHeader[kk] == i + 1) {
+                                    notFoundFlag = 0;
+                                    break;
+                                }
+                            if (notFoundFlag) {
+                                s->header[n2 - 1][index] = i + 1;
+                                break;
+                            }
+                        }
+                    }
+                }
+            }
+        }
+    }
+    for (int j = 0; j < blocks; j++) /* :405-409 */
+        for (int i = 0; i < n2; i++) s->cnv[2 + j * n2 + i] = s->cnsw[2 + j * n2 + i];
+}
+
+/* The relay's frame (Variable_Rate_FEC_Decoder.cpp:1473-1489, :654-669): [codeword_r_d_size BE16]
+ * [header[n2-1][0..T_TOT] as bytes][codeword_new_vector[n2-1][0 .. codeword_r_d_size)] with
+ * codeword_r_d_size = (ceil((max_payload+2)/k2) + 1) * n2 (:998).  Returns the frame bytes. */
+int or_sdswdf_frame(const or_sdswdf *s, uint8_t *frame) {
+    const int size = (s->S + 1) * s->n2;
+    frame[0] = (uint8_t)(size / 256);
+    frame[1] = (uint8_t)size;
+    for (int aa = 0; aa < OR_SD_HDR; aa++) frame[2 + aa] = (uint8_t)s->header[s->n2 - 1][aa];
+    memcpy(frame + 2 + OR_SD_HDR, s->cnv, (size_t)size);
+    return 2 + OR_SD_HDR + size;
+}
+
+/* symbol_wise_decode_state_dependent (:487-546) followed by extract_data (:653-661): out
+ * receives S*k bytes (blocks*k decoded, the rest zero).  Returns the flag. */
+int or_sdswdf_decode(or_sdswdf *s, uint8_t *out) {
+    const int k = s->k, n = s->n, TT = OR_TTOT;
+    uint8_t temp_codeword[OR_MAXN], temp_temp_codeword[OR_MAXN], stam[OR_MAXN];
+    int tempHeader[OR_MAXN];
+    uint8_t *buffer = (uint8_t *)calloc((size_t)s->blocks * n, 1);
+    int flag = 0;
+    for (int j = 0; j < s->blocks; j++) {
+        for (int k_shift = 0; k_shift < k; k_shift++) {
+            for (int i = 0; i < n; i++) { /* :501-508 */
+                temp_codeword[n - 1 - i] = s->sd[3 * TT - k_shift - i - 1][4 + (j + 1) * n - 1 - i];
+                tempHeader[n - 1 - i] = s->header[3 * TT - k_shift - i - 1][n - 1 - i];
+            }
+            for (int i = 0; i < n; i++) temp_temp_codeword[i] = 0; /* reorder by header, :510-518 */
+            for (int i = 0; i < n; i++)
+                if (tempHeader[i] != 0 && tempHeader[i] < n + 1) temp_temp_codeword[tempHeader[i] - 1] = temp_codeword[i];
+            for (int i = 0; i < n; i++) temp_codeword[i] = temp_temp_codeword[i];
+            int erasure_counter = 0;
+            for (int i = 0; i < n; i++) erasure_counter += tempHeader[i] == 0;
+            if (erasure_counter > 0 && erasure_counter < n - k + 1) { /* :525-533 */
+                for (int aa = 0; aa < n; aa++) stam[aa] = 1;
+                for (int aa = 0; aa < n; aa++)
+                    if (tempHeader[aa] != 0 && tempHeader[aa] < n + 1) stam[tempHeader[aa] - 1] = 0;
+                or_decode_block(temp_codeword, s->G1, temp_codeword, stam, k, n, n - 1, 0);
+            } else if (erasure_counter >= n - k + 1) {
+                flag = 1;
+            }
+            buffer[j * n + n - k + k_shift] = temp_codeword[k_shift]; /* :537 */
+        }
+    }
+    int ind = 0; /* extract_data, :653-661 */
+    for (int j = 0; j < s->blocks; j++)
+        for (int i = 0; i < k; i++) out[ind++] = buffer[j * n + n - k + i];
+    while (ind < s->S * k) out[ind++] = 0;
+    free(buffer);
+    return flag;
+}
+
+/* The local simulation's SD-SWDF chain (application_local_simulation.cpp:505-587 with
+ * RELAYING_TYPE 3 and FLAG_FOR_CONSTANT_TRANS = 1): FEC_Encoder(L, T1, N1, N1) at the source,
+ * hop-1 erasures e1, the relay's state-dependent encode for n2 = T2+1 (k2 = T2-N2+1 = k), one
+ * frame per seq, hop-2 erasures e2, the destination's state-dependent decode.  Outputs per seq
+ * t < P: frames (P x (2 + 11 + (S+1)*n2)), dest_out (P x S*k data_with_header of source packet
+ * t - (n1+n2-k-1)), dest_flag.  Returns 0, or -1 for an unsupported configuration. */
+int or_sdswdf_run(int max_payload, int T1, int N1, int T2, int N2, int64_t P, const uint8_t *e1,
+                  const uint8_t *e2, uint64_t seed, int sdbo, uint8_t *frames, uint8_t *dest_out,
+                  uint8_t *dest_flag) {
+    const int k = T1 - N1 + 1, n1 = T1 + 1, n2 = T2 + 1;
+    if (T2 - N2 + 1 != k || T1 > OR_TTOT || T2 > OR_TTOT || n2 > n1) return -1;
+    or_encoder *src = or_encoder_new(max_payload, T1, N1, N1);
+    or_sdswdf *relay = or_sdswdf_new(max_payload, k, n1, n2);
+    or_sdswdf *dest = or_sdswdf_new(max_payload, k, n2, 0);
+    if (!src || !relay || !dest) {
+        or_encoder_free(src);
+        or_sdswdf_free(relay);
+        or_sdswdf_free(dest);
+        return -1;
+    }
+    int kk, nn, S, CW;
+    or_geometry(max_payload, T1, N1, N1, &kk, &nn, &S, &CW);
+    const int F = 2 + OR_SD_HDR + (S + 1) * n2;
+    uint8_t *payload = (uint8_t *)malloc((size_t)max_payload);
+    uint8_t *cw = (uint8_t *)malloc((size_t)CW);
+    uint8_t *frame = (uint8_t *)malloc((size_t)F);
+    uint8_t *tmp = (uint8_t *)malloc((size_t)S * k);
+    for (int64_t t = 0; t < P; t++) {
+        or_fill_payload(payload, t, 1, max_payload, seed);
+        or_encoder_transmit(src, payload, max_payload, (int)t, cw);
+        or_sdswdf_relay_push(relay, cw, CW, e1[t]);
+        or_sdswdf_encode(relay, sdbo);
+        or_sdswdf_frame(relay, frame);
+        if (frames) memcpy(frames + t * F, frame, (size_t)F);
+        or_sdswdf_dest_push(dest, frame, F, e2[t]);
+        uint8_t *o = dest_out ? dest_out + t * (int64_t)S * k : tmp;
+        const int df = or_sdswdf_decode(dest, o);
+        if (dest_flag) dest_flag[t] = (uint8_t)df;
+    }
+    free(payload);
+    free(cw);
+    free(frame);
+    free(tmp);
+    or_encoder_free(src);
+    or_sdswdf_free(relay);
+    or_sdswdf_free(dest);
     return 0;
 }
 

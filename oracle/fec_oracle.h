@@ -81,6 +81,21 @@ int or_swdf_run(int max_payload, int T1, int N1, int T2, int N2, int64_t P, cons
                 const uint8_t *e2, uint64_t seed, uint8_t *frames, uint8_t *relay_flag,
                 uint8_t *dest_out, uint8_t *dest_flag);
 
+/* Decoder_Symbol_Wise state-dependent relay (SD-SWDF, RELAYING_TYPE 3; Decoder_Symbol_Wise.cpp
+ * :178-546), reference-structured, and its fixed-rate chain (see fec_oracle.c). */
+typedef struct or_sdswdf or_sdswdf;
+or_sdswdf *or_sdswdf_new(int max_payload, int k, int n, int n2);
+void or_sdswdf_free(or_sdswdf *s);
+void or_sdswdf_set_garbage(int v);
+void or_sdswdf_relay_push(or_sdswdf *s, const uint8_t *cw, int size, int erased);
+void or_sdswdf_dest_push(or_sdswdf *s, const uint8_t *frame, int frame_bytes, int erased);
+void or_sdswdf_encode(or_sdswdf *s, int sdbo);
+int or_sdswdf_frame(const or_sdswdf *s, uint8_t *frame);
+int or_sdswdf_decode(or_sdswdf *s, uint8_t *out);
+int or_sdswdf_run(int max_payload, int T1, int N1, int T2, int N2, int64_t P, const uint8_t *e1,
+                  const uint8_t *e2, uint64_t seed, int sdbo, uint8_t *frames, uint8_t *dest_out,
+                  uint8_t *dest_flag);
+
 /* The adaptive P2P loop (BASELINE config 4), reference-structured on real bytes: returns the
  * packets lost among 0..P-1; out_len[P] (0 = lost), out_data (P*max_payload or NULL); packets
  * (packets_cap bytes, or NULL) receives the first max_sent P2P wire packets [seq BE32][T][B][N]

@@ -33,8 +33,10 @@ def test_oracle_swdf_clean_hops_deliver_every_packet(cfg):
     z = np.zeros(P, dtype=np.uint8)
     r = oracle.swdf_run(L, *cfg, P, z, z, seed=SEED)
     D, S, k = r["delay"], r["S"], r["k"]
+    nb = (L // k + 1) * k  # the relayed blocks: ceil(max_payload/k)+1 on ints (:553, :632)
     want = source_dwh(P, S, k)
-    assert (r["dest_out"][D:] == want[:P - D]).all()
+    assert (r["dest_out"][D:, :nb] == want[:P - D, :nb]).all()
+    assert (r["dest_out"][:, nb:] == 0).all()
     assert r["relay_flag"].sum() == 0 and r["dest_flag"].sum() == 0
 
 
