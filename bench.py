@@ -33,15 +33,17 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak, /opt/skills/guides/MI355X_MICROARCH.
 
 
 def kernel_sources_digest():
-    """SHA-256 over the device sources of libfec_amd.so (csrc/*.hip: the kernels and their launch
-    code; *.h): a PMC traffic figure or a rocprof duration is only valid for the kernels it was
-    measured on.  The host-only C++ files (*.cpp: the variable-rate plan, the host planner's rule
-    tables, the drop-in classes, the erasure generators) launch none of the step's kernels."""
+    """SHA-256 over every source of libfec_amd.so (csrc/*.hip, *.h, *.cpp and include/*.h): a PMC
+    traffic figure or a rocprof duration is only valid for the library it was measured on -- the
+    host files launch kernels too (fec_vr.cpp config 4's, fec_host.cpp builds the rule tables the
+    planner kernels read)."""
     import glob
     import hashlib
     h = hashlib.sha256()
     csrc = os.path.join(ROOT, "fec_erasure_code_unit_test_relay_amd", "csrc")
-    for path in sorted(glob.glob(os.path.join(csrc, "*.hip")) + glob.glob(os.path.join(csrc, "*.h"))):
+    paths = [p for ext in ("*.hip", "*.h", "*.cpp") for p in glob.glob(os.path.join(csrc, ext))]
+    paths += glob.glob(os.path.join(ROOT, "include", "*.h"))
+    for path in sorted(paths, key=os.path.basename):
         h.update(os.path.basename(path).encode())
         with open(path, "rb") as f:
             h.update(f.read())
@@ -531,6 +533,12 @@ def main():
                     help="CPU test of the --gpus launcher: ranks rendezvous over gloo, no GPU work")
     args = ap.parse_args()
     T, B, N = map(int, args.tbn.split(","))
+    # The library's run-time settings in effect are recorded in the line (`env`); a setting that
+    # skips work cannot produce a valid line (the product library compiles the encoder's ablation
+    # switch out, but a diagnostic build might be loaded).
+    fec_env = {k: v for k, v in sorted(os.environ.items()) if k.startswith("FEC_")}
+    if fec_env.get("FEC_TILE_DBG", "0") not in ("", "0"):
+        raise SystemExit("bench.py: FEC_TILE_DBG (work-skipping encoder ablation) is set; refusing to measure")
 
     if launch_mode(args.gpus, os.environ) == "spawn":
         sys.exit(spawn_ranks(args.gpus, sys.argv[1:]))
@@ -700,6 +708,7 @@ def main():
                        "codeword_bytes": codec.CW, "packets_per_gpu": P,
                        "parallelism": f"streams{world} (one independent stream per GPU)"},
             "verified": bool(verified_all == world),
+            "env": fec_env,
             "step_launch": "hipGraph replay" if args.graph else "eager launches",
             "device_warmup": {"seconds": args.warm_seconds, "untimed_steps": warm_steps,
                               "note": "untimed replays of the same step before the W warm-up steps "

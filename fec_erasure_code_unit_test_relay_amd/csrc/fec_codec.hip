@@ -9,6 +9,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <memory>
+#include <mutex>
 #include <new>
 #include <vector>
 
@@ -352,7 +353,11 @@ int launch_encode_tile(fec_codec* c, const uint8_t* d_payload, const int32_t* d_
     a.nso = c->tile_off[7];
     a.off_scratch = c->tile_off[8];
     a.dbg = 0;
+#ifdef FEC_ABLATION_BUILD
+    // timing ablations (work skipped, codewords wrong by design): only in a diagnostic build,
+    // `make EXTRA=-DFEC_ABLATION_BUILD OUT=... BUILD=...`; the product library ignores FEC_TILE_DBG
     if (const char* v = std::getenv("FEC_TILE_DBG")) a.dbg = std::atoi(v);
+#endif
     a.seg = nullptr;
     a.cur_rows = a.old_rows = nullptr;
     a.cur_len = a.old_len = nullptr;
@@ -749,11 +754,13 @@ struct ServerHost {
     int nunits = 0;                   // its units (the decoder's: with the coefficient units)
     bool on = false;                  // this coder runs on a server (else one launch per call)
     bool live = false;                // a server launch may be running on the coder's stream
+    bool slot = false;                // it holds one of the process's persistent-server slots
 };
 
 struct fec_encoder {
     std::unique_ptr<fec_codec> codec;
     ServerHost sv;
+    bool poisoned = false;         // a failed HIP call left host and device state apart
     int64_t origin = -1;           // seq of the first call (the encoder's creation point)
     int64_t next = 0;              // expected seq
     int res_len_off = 0;           // offset of the trimmed size in the result block (4-aligned)
@@ -770,9 +777,14 @@ struct fec_encoder {
 };
 
 struct fec_decoder {
-    static constexpr int RR = 64;  // device ring rows (>= T + k)
+    static constexpr int RR = 64;  // ring rows (>= T + k)
     std::unique_ptr<fec_codec> codec;
     ServerHost sv;
+    std::vector<uint8_t> h_ring;   // server mode: the received codewords, zero-padded (RR x CW; zero
+                                   // rows for missing packets) -- the decoder's own copies
+    std::vector<uint32_t> req;     // server mode: request words (fields, window rows, coefficients)
+    int win_units = 0;             // ceil((k+n-1) * CW / 4)
+    bool poisoned = false;         // a failed HIP call left host and device state apart
     std::unique_ptr<fec::StreamPlanner> planner;
     int64_t origin = -1;           // seq of the first call; the planner runs on seq - origin
     int64_t next = 0;
@@ -794,6 +806,7 @@ struct fec_decoder {
 
 namespace {
 // The server ends on its stop word; the stream then holds no running launch.
+void server_slot_give(ServerHost& sv);
 void server_stop(ServerHost& sv, hipStream_t s) {
     if (sv.live && sv.h_box && s) {
         reinterpret_cast<volatile fec::ServerBox*>(sv.h_box)->stop = 1;
@@ -801,6 +814,7 @@ void server_stop(ServerHost& sv, hipStream_t s) {
         (void)hipStreamSynchronize(s);
         sv.live = false;
     }
+    server_slot_give(sv);
 }
 }  // namespace
 
@@ -1107,30 +1121,119 @@ bool server_enabled() {
 }
 constexpr int64_t kServerIdleTicks = 5000000;  // 50 ms of the 100 MHz counter without a request
 
-// Post request `ticket` (its fields and rows are written) and make sure a server serves it.  A
-// server that announced its exit (alive = 0) is waited for; it is relaunched unless it served this
-// request on its way out (fec_server.hip: the exit handshake).
-hipError_t server_post(ServerHost& sv, uint32_t ticket, hipStream_t s,
-                       const std::function<hipError_t(uint32_t)>& launch) {
-    volatile fec::ServerBox* b = sv.h_box;
-    if (!sv.live) {
-        b->alive = 1;
-        std::atomic_thread_fence(std::memory_order_seq_cst);
-        if (hipError_t e = launch(ticket - 1)) return e;
-        sv.live = true;
+// Persistent servers per process.  A live server occupies its stream's hardware queue until it
+// idles out, and a process has few queues (GPU_MAX_HW_QUEUES, 4 by default): streams beyond that
+// share queues, and work queued behind a live server waits for it.  So at most FEC_SERVER_MAX
+// (default 2; 0 = none) coders keep a persistent server; the others serve each call with a one-shot
+// launch of the same kernel (idle limit 0: it serves the posted request and exits, and the call
+// waits for the launch to end), and before such a launch they stop the live persistent servers
+// (their stop word), since the one-shot's stream may share a queue with one of them.  A stopped
+// server's coder relaunches it at its next call.  A coder gives its slot back at its next call
+// after its server ended, or when it is destroyed.
+std::atomic<int> g_server_slots{0};
+std::mutex g_server_mu;
+std::vector<ServerHost*> g_server_live;  // persistent servers launched and not seen ended
+
+int server_slot_cap() {
+    static const int cap = [] {
+        const char* v = std::getenv("FEC_SERVER_MAX");
+        const int c = v ? std::atoi(v) : 2;
+        return c < 0 ? 0 : c;
+    }();
+    return cap;
+}
+bool server_slot_take(ServerHost& sv) {
+    if (sv.slot) return true;
+    int c = g_server_slots.load();
+    while (c < server_slot_cap())
+        if (g_server_slots.compare_exchange_weak(c, c + 1)) {
+            sv.slot = true;
+            return true;
+        }
+    return false;
+}
+void server_unregister(ServerHost& sv) {
+    std::lock_guard<std::mutex> lk(g_server_mu);
+    g_server_live.erase(std::remove(g_server_live.begin(), g_server_live.end(), &sv), g_server_live.end());
+}
+void server_slot_give(ServerHost& sv) {
+    server_unregister(sv);
+    if (sv.slot) {
+        g_server_slots.fetch_sub(1);
+        sv.slot = false;
     }
+}
+// At the start of a call: whether this call's server is (or becomes) persistent.
+bool server_persistent(ServerHost& sv) {
+    if (!sv.live) server_slot_give(sv);
+    return sv.live || server_slot_take(sv);
+}
+// Before a one-shot launch: every other coder's persistent server stops (it writes its state back
+// and ends; its coder sees exited = 1 and relaunches at its next call).
+void server_stop_others(const ServerHost& self) {
+    std::lock_guard<std::mutex> lk(g_server_mu);
+    for (ServerHost* o : g_server_live)
+        if (o != &self) reinterpret_cast<volatile fec::ServerBox*>(o->h_box)->stop = 1;
+    g_server_live.erase(std::remove_if(g_server_live.begin(), g_server_live.end(),
+                                       [&](ServerHost* o) { return o != &self; }),
+                        g_server_live.end());
+    std::atomic_thread_fence(std::memory_order_seq_cst);
+}
+
+using ServerLaunch = std::function<hipError_t(uint32_t last, int64_t idle_ticks)>;
+
+hipError_t server_start(ServerHost& sv, uint32_t last, bool persistent, const ServerLaunch& launch) {
+    volatile fec::ServerBox* b = sv.h_box;
+    if (!persistent) server_stop_others(sv);
+    b->stop = 0;
+    b->exited = 0;
+    b->alive = 1;
+    std::atomic_thread_fence(std::memory_order_seq_cst);
+    if (hipError_t e = launch(last, persistent ? kServerIdleTicks : 0)) return e;
+    sv.live = true;
+    if (persistent) {
+        std::lock_guard<std::mutex> lk(g_server_mu);
+        if (std::find(g_server_live.begin(), g_server_live.end(), &sv) == g_server_live.end())
+            g_server_live.push_back(&sv);
+    }
+    return hipSuccess;
+}
+
+// After reading alive = 0: the server is exiting.  Wait until it revived for this request
+// (alive = 1), answered it, or made its exit final (exited = 1: then the launch is drained).
+hipError_t server_settle(ServerHost& sv, uint32_t ticket, hipStream_t s, bool* ended) {
+    const volatile fec::ServerBox* b = sv.h_box;
+    *ended = false;
+    const auto t0 = std::chrono::steady_clock::now();
+    for (uint32_t i = 1;; ++i) {
+        if (b->exited) break;
+        if (b->alive || b->done == ticket) return hipSuccess;
+        if ((i & 4095) == 0) {
+            if (hipError_t e = hipStreamQuery(s); e != hipSuccess && e != hipErrorNotReady) return e;
+            if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(1)) break;
+        }
+        __builtin_ia32_pause();
+    }
+    const hipError_t e = hipStreamSynchronize(s);
+    sv.live = false;
+    server_unregister(sv);
+    *ended = true;
+    return e;
+}
+
+// Post request `ticket` (its sealed units are written) and make sure a server serves it.
+hipError_t server_post(ServerHost& sv, uint32_t ticket, hipStream_t s, bool persistent, const ServerLaunch& launch) {
+    volatile fec::ServerBox* b = sv.h_box;
+    if (!sv.live)
+        if (hipError_t e = server_start(sv, ticket - 1, persistent, launch)) return e;
     std::atomic_thread_fence(std::memory_order_release);
     b->req = ticket;
     std::atomic_thread_fence(std::memory_order_seq_cst);
     if (b->alive == 0) {
-        if (hipError_t e = hipStreamSynchronize(s)) return e;
-        sv.live = false;
-        if (b->done != ticket) {
-            b->alive = 1;
-            std::atomic_thread_fence(std::memory_order_seq_cst);
-            if (hipError_t e = launch(ticket - 1)) return e;
-            sv.live = true;
-        }
+        bool ended = false;
+        if (hipError_t e = server_settle(sv, ticket, s, &ended)) return e;
+        if (ended && b->done != ticket)
+            if (hipError_t e = server_start(sv, ticket - 1, persistent, launch)) return e;
     }
     return hipSuccess;
 }
@@ -1144,23 +1247,35 @@ void server_seal(ServerHost& sv, int first, const uint32_t* words, int n, uint32
     for (int i = n - 1; i >= 0; --i) u[i] = tk | words[i];
 }
 
-// Wait for the server's done ticket (in host memory: no PCIe round trip per poll).  A launch that
-// failed, or a server that stopped (alive = 0) before finishing, is reported after the stream is
-// drained; ten seconds without an answer are reported as an error.
-hipError_t server_wait(ServerHost& sv, uint32_t ticket, hipStream_t s) {
+// Wait for the server's done ticket (in host memory: no PCIe round trip per poll).  A server whose
+// exit became final before answering (stopped by another coder's one-shot, or idled out in the
+// exit race) is relaunched for the request, a few times at most; a failed launch is reported after
+// the stream is drained; ten seconds without an answer are reported as an error.  A one-shot launch
+// is drained after its answer.
+hipError_t server_wait(ServerHost& sv, uint32_t ticket, hipStream_t s, bool persistent, const ServerLaunch& launch) {
     const volatile fec::ServerBox* b = sv.h_box;
     const auto t0 = std::chrono::steady_clock::now();
+    int relaunches = 0;
     for (uint32_t i = 1;; ++i) {
         if (b->done == ticket) {
             std::atomic_thread_fence(std::memory_order_acquire);
-            return hipSuccess;
-        }
-        if ((i & 4095) == 0) {
-            if (b->alive == 0) {  // the server is gone without this request's answer
+            if (!persistent) {
                 const hipError_t e = hipStreamSynchronize(s);
                 sv.live = false;
-                if (b->done == ticket) return hipSuccess;
-                return e != hipSuccess ? e : hipErrorLaunchFailure;
+                return e;
+            }
+            return hipSuccess;
+        }
+        if ((i & 1023) == 0) {
+            if (b->exited) {  // the server is gone without this request's answer
+                const hipError_t e = hipStreamSynchronize(s);
+                sv.live = false;
+                server_unregister(sv);
+                if (b->done == ticket) continue;
+                if (e != hipSuccess) return e;
+                if (++relaunches > 8) return hipErrorLaunchFailure;
+                if (hipError_t e2 = server_start(sv, ticket - 1, persistent, launch)) return e2;
+                continue;
             }
             if (hipError_t e = hipStreamQuery(s); e != hipSuccess && e != hipErrorNotReady) return e;
             if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(10)) return hipErrorLaunchTimeOut;
@@ -1221,10 +1336,19 @@ int fec_encoder_transmit(fec_encoder* e, const uint8_t* data, int payload, int s
         e->next = seq;
     }
     if (seq != e->next) return FEC_ERR_SEQUENCE;
+    if (e->poisoned) return FEC_ERR_HIP;
     const Geometry& g = e->codec->g;
     if (payload > g.L) payload = g.L;
     fec::CodecView v;
     if (int st = fec::codec_view(e->codec.get(), &v)) return st;
+    // from here on a failed HIP call leaves the window ring (device) and e->next (host) apart
+    struct Poison {
+        bool& p;
+        bool ok = false;
+        ~Poison() {
+            if (!ok) p = true;
+        }
+    } poison{e->poisoned};
     if (e->sv.on) {
         // the resident server: the request, sealed with its ticket, into the mailbox; no launch
         // (fec_server.hip)
@@ -1241,7 +1365,8 @@ int fec_encoder_transmit(fec_encoder* e, const uint8_t* data, int payload, int s
             std::memset(reinterpret_cast<uint8_t*>(w + fec::kEncReqFields) + payload, 0, 4 * nw - payload);
             server_seal(e->sv, 0, w, e->sv.nunits, ticket);
         }
-        auto launch = [&](uint32_t last) -> hipError_t {
+        const bool persistent = server_persistent(e->sv);
+        auto launch = [&](uint32_t last, int64_t idle_ticks) -> hipError_t {
             fec::EncServerArgs a;
             a.box = e->sv.m_box;
             a.req = e->sv.m_req;
@@ -1260,14 +1385,15 @@ int fec_encoder_transmit(fec_encoder* e, const uint8_t* data, int payload, int s
             a.SK = g.S * g.k;
             a.W = std::max(1, g.n - 1);
             a.last = last;
-            a.idle_ticks = kServerIdleTicks;
+            a.idle_ticks = idle_ticks;
             return fec::server_encode_launch(a, e->s) == FEC_OK ? hipSuccess : hipErrorLaunchFailure;
         };
-        HIP_TRY(server_post(e->sv, ticket, e->s, launch));
-        HIP_TRY(server_wait(e->sv, ticket, e->s));
+        HIP_TRY(server_post(e->sv, ticket, e->s, persistent, launch));
+        HIP_TRY(server_wait(e->sv, ticket, e->s, persistent, launch));
         std::memcpy(cw_out, e->h_res, g.CW);
         std::memcpy(cw_size, e->h_res + e->res_len_off, 4);
         ++e->next;
+        poison.ok = true;
         return FEC_OK;
     }
     // one launch: the closed form over the device-resident window (fec_streams_encode_kernel reads
@@ -1284,6 +1410,7 @@ int fec_encoder_transmit(fec_encoder* e, const uint8_t* data, int payload, int s
     std::memcpy(cw_out, e->h_res, g.CW);
     std::memcpy(cw_size, e->h_res + e->res_len_off, 4);
     ++e->next;
+    poison.ok = true;
     return FEC_OK;
 }
 
@@ -1308,14 +1435,17 @@ int fec_decoder_create(int max_payload, int T, int B, int N, fec_decoder** out) 
         HIP_TRY(host_mapped(&d->h_coef, &d->m_coef, (g.k * g.n + 3) & ~3));
         HIP_TRY(host_mapped(&d->h_res, &d->m_res, d->res_len_off + 4));
         HIP_TRY(host_mapped(&d->h_done, &d->m_done, 4));
-        d->sv.on = server_enabled() && g.k * g.n <= 16 * 32 && g.CW <= 4096 &&
-                   static_cast<int64_t>(fec_decoder::RR) * g.CW <= 48 * 1024;
+        const int Wn = g.k + g.n - 1;
+        d->sv.on = server_enabled() && g.k * g.n <= 16 * 32 && static_cast<int64_t>(Wn) * g.CW <= 48 * 1024;
         if (d->sv.on) {
             HIP_TRY(host_mapped(reinterpret_cast<uint8_t**>(&d->sv.h_box), reinterpret_cast<uint8_t**>(&d->sv.m_box),
                                 sizeof(fec::ServerBox)));
-            d->sv.nunits = fec::kDecReqFields + (g.CW + 3) / 4 + (g.k * g.n + 3) / 4;
+            d->win_units = (Wn * g.CW + 3) / 4;
+            d->sv.nunits = fec::kDecReqFields + d->win_units + (g.k * g.n + 3) / 4;
             HIP_TRY(host_mapped(reinterpret_cast<uint8_t**>(&d->sv.h_req), reinterpret_cast<uint8_t**>(&d->sv.m_req),
                                 sizeof(uint64_t) * d->sv.nunits));
+            d->h_ring.assign(static_cast<size_t>(fec_decoder::RR) * g.CW, 0);
+            d->req.assign(static_cast<size_t>(d->sv.nunits), 0);
         }
         HIP_TRY(hipDeviceSynchronize());  // the ring is zero before the first call's kernel
         *out = d.release();
@@ -1328,6 +1458,32 @@ int fec_decoder_destroy(fec_decoder* d) {
     return FEC_OK;
 }
 
+namespace {
+// Server mode, packet x received (fate kCopy): its systematic bytes from the decoder's own copy of
+// its codeword -- the fast path's copy (Decoder.cpp:77-108) and the slow path's output for a
+// received packet (its sub-streams' data symbols; the length clamped, Decoder.cpp:148-149).  No GF
+// work: the same formula as the device copy kernels (fec_streams.hip stream_decode_one).
+void host_copy_out(const Geometry& g, const uint8_t* cwx, bool clamp, uint8_t* payload_out, int* payload) {
+    auto byte_at = [&](int h) -> uint8_t {
+        const int s = h / g.k, i = h - s * g.k;
+        return cwx[s * g.n + i];
+    };
+    const int hdr = byte_at(0) * 256 + byte_at(1);
+    const int ln = clamp ? std::min(hdr, g.L) : hdr;
+    const int cp = std::min(ln, g.L);
+    // data byte h = symbol (h / k, h % k): runs of up to k contiguous bytes per sub-stream
+    for (int b = 0, h = 2; b < cp;) {
+        const int s = h / g.k, i = h - s * g.k;
+        const int run = std::min(g.k - i, cp - b);
+        std::memcpy(payload_out + b, cwx + s * g.n + i, run);
+        b += run;
+        h += run;
+    }
+    std::memset(payload_out + cp, 0, g.L - cp);
+    *payload = ln;
+}
+}  // namespace
+
 int fec_decoder_receive(fec_decoder* d, const uint8_t* cw, int cw_size, int seq, int erasure,
                         uint8_t* payload_out, int* payload) {
     if (!d || !payload_out || !payload || seq < 0) return FEC_ERR_ARG;
@@ -1339,11 +1495,19 @@ int fec_decoder_receive(fec_decoder* d, const uint8_t* cw, int cw_size, int seq,
         d->next = seq;
     }
     if (seq != d->next) return FEC_ERR_SEQUENCE;
+    if (d->poisoned) return FEC_ERR_HIP;
     const int64_t rel = seq - d->origin;
     const Geometry& g = d->codec->g;
     const bool er = erasure != 0 || cw == nullptr;
-    // the previous call's kernel has read h_cw / h_coef (its completion word is set)
-    if (d->ticket) HIP_TRY(d->sv.on ? server_wait(d->sv, d->ticket, d->s) : wait_done(d->h_done, d->ticket, d->s));
+    // the previous call's kernel has read h_cw / h_coef (its completion word is set); server-mode
+    // calls are synchronous
+    if (d->ticket && !d->sv.on) HIP_TRY(wait_done(d->h_done, d->ticket, d->s));
+    if (d->sv.on) {  // FEC_Decoder.cpp:55-63: the decoder's zero-padded copy of the wire codeword
+        uint8_t* row = d->h_ring.data() + (rel % fec_decoder::RR) * g.CW;
+        const int sz = er ? 0 : std::max(0, std::min(cw_size, g.CW));
+        if (sz) std::memcpy(row, cw, sz);
+        std::memset(row + sz, 0, g.CW - sz);
+    }
     fec::StepResult r;
     int st = guarded([&] {
         r = d->planner->step(rel, er);
@@ -1351,66 +1515,78 @@ int fec_decoder_receive(fec_decoder* d, const uint8_t* cw, int cw_size, int seq,
     });
     if (st) return st;
     ++d->next;
+    // from here on a failed HIP call leaves the planner (host) ahead of the device ring
+    struct Poison {
+        bool& p;
+        bool ok = false;
+        ~Poison() {
+            if (!ok) p = true;
+        }
+    } poison{d->poisoned};
     const bool no_output = r.fate == fec::kNone || r.fate == fec::kLost;
     if (no_output) {
         std::memset(payload_out, 0, g.L);
         *payload = 0;
-        if (er) return FEC_OK;  // nothing to keep, nothing to compute
+        if (er || d->sv.on) {  // nothing to keep on the device, nothing to compute
+            poison.ok = true;
+            return FEC_OK;
+        }
     }
     if (d->sv.on) {
-        // the resident server: the request (fields, the zero-padded codeword FEC_Decoder.cpp:55-63,
-        // the coefficients of a recovered packet), sealed with its ticket, into the mailbox; no launch
+        const uint8_t* ring = d->h_ring.data();
+        if (r.fate == fec::kCopy) {
+            host_copy_out(g, ring + (r.x % fec_decoder::RR) * g.CW, r.slow, payload_out, payload);
+            poison.ok = true;
+            return FEC_OK;
+        }
+        // a recovered packet: the coefficients and the k+n-1 codewords they read (packets
+        // x-k+1 .. x+n-1, zero rows before the origin or not yet received), sealed into the
+        // mailbox of the resident server (fec_server.hip)
         fec::CodecView v;
         if (int e = fec::codec_view(d->codec.get(), &v)) return e;
         const uint32_t ticket = ++d->ticket;
-        {
-            const int ncw = (g.CW + 3) / 4, ncf = (g.k * g.n + 3) / 4;
-            uint32_t w[fec::kDecReqFields + 1024 + 128];
-            w[0] = er ? 1u : 0u;
-            w[1] = static_cast<uint32_t>(r.fate);
-            w[2] = r.slow ? 1u : 0u;
-            w[3] = static_cast<uint32_t>(rel);
-            w[4] = static_cast<uint32_t>(rel >> 32);
-            w[5] = static_cast<uint32_t>(r.x);
-            w[6] = static_cast<uint32_t>(static_cast<int64_t>(r.x) >> 32);
-            uint8_t* cwb = reinterpret_cast<uint8_t*>(w + fec::kDecReqFields);
-            const int sz = er ? 0 : std::max(0, std::min(cw_size, g.CW));
-            if (sz) std::memcpy(cwb, cw, sz);
-            std::memset(cwb + sz, 0, 4 * ncw - sz);
-            int nseal = fec::kDecReqFields + ncw;
-            if (r.fate == fec::kRecovered) {
-                uint8_t* cfb = reinterpret_cast<uint8_t*>(w + nseal);
-                std::memset(cfb, 0, 4 * ncf);
-                std::memcpy(cfb, r.coef, g.k * g.n);
-                nseal += ncf;
-            }
-            server_seal(d->sv, 0, w, nseal, ticket);
+        uint32_t* w = d->req.data();
+        std::fill(w, w + fec::kDecReqFields, 0u);
+        w[0] = static_cast<uint32_t>(r.fate);
+        w[1] = r.slow ? 1u : 0u;
+        uint8_t* wb = reinterpret_cast<uint8_t*>(w + fec::kDecReqFields);
+        const int Wn = g.k + g.n - 1;
+        for (int row = 0; row < Wn; ++row) {
+            const int64_t sp = r.x - (g.k - 1) + row;
+            uint8_t* dst = wb + static_cast<size_t>(row) * g.CW;
+            if (sp < 0 || sp > rel) std::memset(dst, 0, g.CW);
+            else std::memcpy(dst, ring + (sp % fec_decoder::RR) * g.CW, g.CW);
         }
-        auto launch = [&](uint32_t last) -> hipError_t {
+        std::memset(wb + static_cast<size_t>(Wn) * g.CW, 0, 4 * d->win_units - static_cast<size_t>(Wn) * g.CW);
+        uint8_t* cfb = reinterpret_cast<uint8_t*>(w + fec::kDecReqFields + d->win_units);
+        const int ncf = (g.k * g.n + 3) / 4;
+        std::memset(cfb, 0, 4 * ncf);
+        std::memcpy(cfb, r.coef, g.k * g.n);
+        server_seal(d->sv, 0, w, d->sv.nunits, ticket);
+        const bool persistent = server_persistent(d->sv);
+        auto launch = [&](uint32_t last, int64_t idle_ticks) -> hipError_t {
             fec::DecServerArgs a;
             a.box = d->sv.m_box;
             a.req = d->sv.m_req;
-            a.nunits_main = d->sv.nunits - (g.k * g.n + 3) / 4;
-            a.stage = d->m_cw;
-            a.coef = d->m_coef;
+            a.nunits = d->sv.nunits;
+            a.win_units = d->win_units;
             a.res = d->m_res;
             a.res_len_off = d->res_len_off;
-            a.ring_home = d->d_ring;
             a.gf = v.gf;
             a.L = g.L;
             a.k = g.k;
             a.n = g.n;
             a.CW = g.CW;
-            a.RR = fec_decoder::RR;
+            a.Wn = Wn;
             a.last = last;
-            a.idle_ticks = kServerIdleTicks;
+            a.idle_ticks = idle_ticks;
             return fec::server_decode_launch(a, d->s) == FEC_OK ? hipSuccess : hipErrorLaunchFailure;
         };
-        HIP_TRY(server_post(d->sv, ticket, d->s, launch));
-        if (no_output) return FEC_OK;  // the codeword is stored asynchronously; the next call waits for it
-        HIP_TRY(server_wait(d->sv, ticket, d->s));
+        HIP_TRY(server_post(d->sv, ticket, d->s, persistent, launch));
+        HIP_TRY(server_wait(d->sv, ticket, d->s, persistent, launch));
         std::memcpy(payload_out, d->h_res, g.L);
         std::memcpy(payload, d->h_res + d->res_len_off, 4);
+        poison.ok = true;
         return FEC_OK;
     }
     if (!er) {  // FEC_Decoder.cpp:55-63: keep a zero-padded copy of the wire codeword
@@ -1433,10 +1609,14 @@ int fec_decoder_receive(fec_decoder* d, const uint8_t* cw, int cw_size, int seq,
                                        r.x, coef, d->m_res, reinterpret_cast<int32_t*>(d->m_res + d->res_len_off),
                                        reinterpret_cast<uint32_t*>(d->m_done), ticket, d->s))
         return e;
-    if (no_output) return FEC_OK;  // the codeword is stored asynchronously; the next call waits for it
+    if (no_output) {  // the codeword is stored asynchronously; the next call waits for it
+        poison.ok = true;
+        return FEC_OK;
+    }
     HIP_TRY(wait_done(d->h_done, ticket, d->s));
     std::memcpy(payload_out, d->h_res, g.L);
     std::memcpy(payload, d->h_res + d->res_len_off, 4);
+    poison.ok = true;
     return FEC_OK;
 }
 

@@ -292,29 +292,27 @@ namespace fec {
 int codec_view(const ::fec_codec* c, CodecView* v);
 // ---- resident per-packet servers (fec_server.hip) ----------------------------------------
 // Mailbox shared by a per-packet coder (host) and its server workgroup (device), in pinned,
-// coherent, mapped host memory.  The host writes the request fields, then `req`; the server
-// writes the result row, then `done`; `stop` ends the server, `alive` is its exit handshake.
+// coherent, mapped host memory.  The host writes the sealed request, then `req`; the server writes
+// the result row, then `done`; `stop` ends the server; `alive` / `exited` are its exit handshake.
 struct ServerBox {
     uint32_t req;     // ticket of the latest request (host, written last)
     uint32_t stop;    // host: 1 = exit now
-    uint32_t alive;   // 1 while a server polls (host sets it before a launch; the server clears it on exit)
+    uint32_t alive;   // 1 while a server polls (host sets it before a launch; the server clears it
+                      // when it starts to exit, and sets it again if a request arrived meanwhile)
     uint32_t done;    // ticket of the latest finished request (server, written last)
-    int32_t len;      // encoder: payload size
-    int32_t erased;   // decoder: this call's packet is missing
-    int32_t fate;     // decoder: PacketFate of packet x
-    int32_t clamp;    // decoder: slow path (length clamped to max_payload, Decoder.cpp:148-149)
-    int64_t seq;      // seq relative to the coder's origin
-    int64_t x;        // decoder: packet output by this call (relative)
+    uint32_t exited;  // server: 1 once its exit is final (after its last look at req); host clears
+                      // it before a launch
+    uint32_t reserved[7];
 };
-static_assert(offsetof(ServerBox, len) == 16 && offsetof(ServerBox, x) == 40 && sizeof(ServerBox) == 48,
-              "the server loads the 8 field dwords after the 4 control words");
+static_assert(offsetof(ServerBox, exited) == 16 && sizeof(ServerBox) == 48, "mailbox layout");
 // A server's sealed request block (pinned, coherent, mapped): unit i = request dword i | ticket << 32,
 // each written by the host as one 8-byte store, the units in decreasing index order and the mailbox's
 // req word after them.  The server's poll reads the first kServerHeadUnits units and the stop word in
 // one round trip and takes the request when every unit it read carries the new ticket; the units past
 // the head were written before it and are read afterwards.  Encoder request: [len, seq lo, seq hi,
-// payload words]; decoder: [erased, fate, clamp, seq lo, seq hi, x lo, x hi, codeword words,
-// coefficient words] (the coefficients are read only for a recovered packet).
+// payload words]; decoder request (a recovered packet only; the host outputs the systematic copies,
+// DESIGN.md §4): [fate, clamp, 5 reserved, the k+n-1 zero-padded codewords of packets x-k+1 .. x+n-1
+// (zero rows for missing ones), the k x n coefficients].
 constexpr int kServerHeadUnits = 192;
 constexpr int kEncReqFields = 3;
 constexpr int kDecReqFields = 7;
@@ -334,15 +332,13 @@ struct EncServerArgs {
 };
 struct DecServerArgs {
     ServerBox* box;
-    const uint64_t* req;        // sealed request block: kDecReqFields + ceil(CW / 4) + ceil(k n / 4) units
-    int nunits_main;            // without the coefficient units
-    const uint8_t* stage;       // mapped codeword row (dword padded)
-    const uint8_t* coef;        // mapped k x n coefficients (dword padded)
+    const uint64_t* req;        // sealed request block: kDecReqFields + win_units + ceil(k n / 4) units
+    int nunits;
+    int win_units;              // ceil(Wn * CW / 4)
     uint8_t* res;               // mapped result row: payload (dword padded) | length at res_len_off
     int res_len_off;
-    uint8_t* ring_home;         // HBM home of the RR x CW ring between launches
     const uint8_t* gf;
-    int L, k, n, CW, RR;
+    int L, k, n, CW, Wn;        // Wn = k + n - 1 window rows
     uint32_t last;
     int64_t idle_ticks;
 };

@@ -9,17 +9,21 @@
 //   host:   the request (fields and payload / codeword) -> the sealed request block, every 8-byte
 //           unit stamped with the request's ticket (fec_kernels.h), then the request word;
 //   server: one poll reads the block's head and sees the whole request in it (the fields and the
-//           packet arrive with the ticket: no second round trip), does the packet's byte work against its state, which it keeps in LDS
-//           for its whole life (the encoder's n-1 windows, Encoder.cpp:73-95 / the decoder's ring of
-//           received codewords, FEC_Decoder.cpp:55-63), writes the result row, then the done ticket;
+//           packet arrive with the ticket: no second round trip), does the packet's byte work (the
+//           encoder against the n-1 windows it keeps in LDS for its whole life, Encoder.cpp:73-95;
+//           the decoder's recovery against the window of codewords the request carries), writes the
+//           result row, then the done ticket;
 //   host:   polls the done ticket in its own (coherent) memory.
 // Every poll also reads a stop word (set when the coder is destroyed), and a server that has seen
 // no request for `idle_ticks` of the 100 MHz real-time counter writes its state back to HBM and
 // exits; the next call launches a new one.  So every launch ends: on the stop word, on idle, or on
-// the process's exit.  The exit handshake (alive = 0, then one more look at the request word) and
-// the host's check of `alive` after posting are Dekker-ordered by sequentially consistent fences on
-// both sides; a host that sees alive = 0 waits for the launch to end before relaunching, so a
-// request is never served twice.
+// the process's exit.  The exit handshake (alive = 0, then one more look at the request word, then
+// exited = 1 if none) and the host's check of `alive` after posting are Dekker-ordered by
+// sequentially consistent fences on both sides; a host that sees alive = 0 waits for alive = 1
+// (revived for its request), its done ticket, or exited = 1 (then it waits for the launch to end and
+// relaunches), so a request is never served twice and a revived server is never waited out.
+// A server launched with idle_ticks = 0 serves the request already posted and exits (one-shot: the
+// host's fallback when the process's persistent-server slots are taken, fec_codec.hip).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -68,7 +72,11 @@ __device__ __forceinline__ uint32_t server_wait(ServerBox* box, const uint64_t* 
             bool ok = true;
 #pragma unroll
             for (int q = 0; q < 3; ++q) ok = ok && static_cast<uint32_t>(u[q] >> 32) == want;
-            if (st) {
+            if (st) {  // stopped (the coder's destruction, or another coder needs the queue)
+                if (lane == 0) {
+                    sys_store(&box->alive, 0u);
+                    sys_store(&box->exited, 1u);
+                }
                 c = kCmdStop;
                 break;
             }
@@ -92,6 +100,8 @@ __device__ __forceinline__ uint32_t server_wait(ServerBox* box, const uint64_t* 
                         if (i < nhead) reqw[i] = static_cast<uint32_t>(sys_load64(req + i));
                     }
                     c = kCmdWork;
+                } else if (lane == 0) {
+                    sys_store(&box->exited, 1u);  // final: no request will be served by this launch
                 }
                 break;
             }
@@ -184,60 +194,48 @@ __global__ __launch_bounds__(256) void fec_encoder_server_kernel(EncServerArgs a
     for (int b = tid; b < W * SK; b += 256) a.win_home[b] = win[b];
 }
 
-// Decoder server.  Per request (the host planner's step for seq: the packet's erasure, and the
-// fate of packet x = seq - T with its recovery coefficients): store the received codeword in the
-// LDS ring (FEC_Decoder.cpp:55-63), then output packet x -- the fast-path copy (Decoder.cpp:77-108)
-// or the recovery (codingOperations.cpp:149-232) -- into the result row.
+// Decoder server.  Per request (a packet x the host planner recovers): the k+n-1 received
+// codewords around x and the k x n coefficients arrive in the sealed request; the server applies
+// the coefficients (the byte half of decodeBlock, codingOperations.cpp:149-232) and writes the
+// payload of packet x into the result row.  It keeps no state: the systematic copies of the fast
+// path (Decoder.cpp:77-108) are done by the host, which holds the received codewords anyway
+// (FEC_Decoder.cpp:55-63).
 __global__ __launch_bounds__(256) void fec_decoder_server_kernel(DecServerArgs a) {
-    extern __shared__ __attribute__((aligned(16))) uint8_t ring[];  // RR x CW (slot seq % RR)
+    extern __shared__ __attribute__((aligned(16))) uint8_t win[];  // Wn x CW: packets x-k+1 .. x+n-1
     __shared__ uint8_t gexp[512];
     __shared__ uint8_t glog[256];
     __shared__ uint8_t coef[16 * 32];
-    __shared__ uint32_t reqw[kDecReqFields + 1024];  // the request: fields, codeword words (CW <= 4096)
+    __shared__ uint32_t reqw[kServerHeadUnits];
     __shared__ uint32_t cmd;
     __shared__ int s_hdr;
     const int tid = threadIdx.x;
-    const int L = a.L, k = a.k, n = a.n, CW = a.CW, RR = a.RR;
+    const int L = a.L, k = a.k, n = a.n, CW = a.CW;
     for (int i = tid; i < 512; i += 256) gexp[i] = a.gf[i];
     for (int i = tid; i < 256; i += 256) glog[i] = a.gf[512 + i];
-    for (int b = tid; b < RR * CW; b += 256) ring[b] = a.ring_home[b];
     __syncthreads();
     uint32_t last = a.last;
-    const int nhead = min(a.nunits_main, kServerHeadUnits);
+    const int nhead = min(a.nunits, kServerHeadUnits);
     while (server_wait(a.box, a.req, nhead, last, a.idle_ticks, reqw, &cmd) == kCmdWork) {
         const uint32_t tk = last + 1;
-        // the units past the head (large codewords); the coefficients only for a recovered packet
-        for (int i = nhead + tid; i < a.nunits_main; i += 256) reqw[i] = static_cast<uint32_t>(sys_load64(a.req + i));
-        const int fate = static_cast<int>(reqw[1]);
-        if (fate == kRecovered)
-            for (int w = tid; 4 * w < k * n; w += 256)
-                reinterpret_cast<uint32_t*>(coef)[w] = static_cast<uint32_t>(sys_load64(a.req + a.nunits_main + w));
+        auto unit = [&](int u) -> uint32_t { return u < nhead ? reqw[u] : static_cast<uint32_t>(sys_load64(a.req + u)); };
+        for (int w = tid; w < a.win_units; w += 256) reinterpret_cast<uint32_t*>(win)[w] = unit(kDecReqFields + w);
+        for (int w = tid; 4 * w < k * n; w += 256)
+            reinterpret_cast<uint32_t*>(coef)[w] = unit(kDecReqFields + a.win_units + w);
         __syncthreads();
-        const int64_t seq = static_cast<int64_t>(reqw[3]) | (static_cast<int64_t>(reqw[4]) << 32);
-        const int64_t x = static_cast<int64_t>(reqw[5]) | (static_cast<int64_t>(reqw[6]) << 32);
-        const int clamp = static_cast<int>(reqw[2]);
-        if (!reqw[0]) {  // the decoder keeps its own copy of the (zero-padded) codeword
-            uint8_t* dst = ring + (seq % RR) * CW;
-            const uint8_t* src = reinterpret_cast<const uint8_t*>(reqw + kDecReqFields);
-            for (int b = tid; b < CW; b += 256) dst[b] = src[b];
-        }
-        __syncthreads();
-        // symbol (s, q) of packet sp from the ring (sp < 0: a zero row, never with a non-zero coefficient)
-        auto sym = [&](int64_t sp, int o) -> uint8_t { return sp < 0 ? 0 : ring[(sp % RR) * CW + o]; };
+        const int clamp = static_cast<int>(reqw[1]);
+        // data byte h of packet x: sum_q coef[i][q] * symbol (s, q) of packet x-i+q (window row k-1-i+q)
         auto byte_at = [&](int h) -> uint8_t {
             const int s = h / k, i = h - s * k;
-            if (fate == kCopy) return sym(x, s * n + i);
             uint8_t acc = 0;
             for (int q = 0; q < n; ++q) {
                 const uint8_t c = coef[i * n + q];
-                if (c) acc ^= sgmul(gexp, glog, c, sym(x - i + q, s * n + q));
+                if (c) acc ^= sgmul(gexp, glog, c, win[(k - 1 - i + q) * CW + s * n + q]);
             }
             return acc;
         };
-        const bool out = fate == kCopy || fate == kRecovered;
-        if (tid == 0) s_hdr = out ? byte_at(0) * 256 + byte_at(1) : 0;
+        if (tid == 0) s_hdr = byte_at(0) * 256 + byte_at(1);
         __syncthreads();
-        const int ln = out ? (clamp ? min(s_hdr, L) : s_hdr) : 0;
+        const int ln = clamp ? min(s_hdr, L) : s_hdr;
         const int cp = min(ln, L);
         uint8_t* orow = a.res;
         for (int w = tid; 4 * w < L; w += 256) {
@@ -254,7 +252,6 @@ __global__ __launch_bounds__(256) void fec_decoder_server_kernel(DecServerArgs a
         last = tk;
         __syncthreads();
     }
-    for (int b = tid; b < RR * CW; b += 256) a.ring_home[b] = ring[b];
 }
 
 int server_encode_launch(const EncServerArgs& a, hipStream_t s) {
@@ -263,7 +260,7 @@ int server_encode_launch(const EncServerArgs& a, hipStream_t s) {
 }
 
 int server_decode_launch(const DecServerArgs& a, hipStream_t s) {
-    hipLaunchKernelGGL(fec_decoder_server_kernel, dim3(1), dim3(256), static_cast<size_t>(a.RR) * a.CW, s, a);
+    hipLaunchKernelGGL(fec_decoder_server_kernel, dim3(1), dim3(256), static_cast<size_t>(a.win_units) * 4, s, a);
     return hipGetLastError() == hipSuccess ? FEC_OK : FEC_ERR_HIP;
 }
 

@@ -7,6 +7,7 @@ the (oracle-validated) symbolic planner's, payload lengths.
 import hashlib
 import os
 import subprocess
+import sys
 
 import numpy as np
 import pytest
@@ -373,6 +374,59 @@ def test_streaming_api_across_server_idle_exits():
         got, p = dec.onReceive(None if erased else wire, size, t, erased)
         ogot, op = od.onReceive(None if erased else ocw, osize, t, erased)
         assert p == op and (got == ogot).all(), t
+
+
+def test_streaming_api_many_coders_interleaved():
+    """Six encoder/decoder pairs used in turn (12 coders, more than the process's persistent-server
+    slots, FEC_SERVER_MAX = 2, and more streams than hardware queues): every call equals the oracle,
+    recovered packets included, and no call waits out another coder's server (50 ms idle limit)."""
+    import time
+    T, B, N = 10, 3, 3
+    P = 150
+    pairs = []
+    for c in range(6):
+        pat = np.zeros(P + T, dtype=np.uint8)
+        pat[[10 + c, 11 + c, 12 + c, 60, 61 + c, 100 + 2 * c]] = 1
+        pairs.append((fec.FEC_Encoder(L, T, B, N), fec.FEC_Decoder(L, T, B, N),
+                      oracle.Encoder(L, T, B, N), oracle.Decoder(L, T, B, N), pat))
+    src = oracle.fill_payload(0, P + T, L, SEED)
+    worst = 0.0
+    for t in range(P + T):
+        for enc, dec, oe, od, pat in pairs:
+            t0 = time.perf_counter()
+            wire, size = enc.onTransmit(src[t], L, t)
+            erased = bool(pat[t])
+            got, p = dec.onReceive(None if erased else wire, size, t, erased)
+            worst = max(worst, time.perf_counter() - t0)
+            ocw, osize = oe.onTransmit(src[t], L, t)
+            ogot, op = od.onReceive(None if erased else ocw, osize, t, erased)
+            assert size == osize and (wire == ocw[:size]).all(), t
+            assert p == op and (got == ogot).all(), t
+    assert worst < 0.025, f"a call took {worst * 1e3:.1f} ms"
+
+
+def test_config5_bench_two_ranks_gloo():
+    """BASELINE config 5's partition (one independent stream per rank, no data-path collective):
+    bench.py --gpus 2 starts two rank processes itself; on a one-GPU box they share the card and
+    rendezvous over gloo (FEC_BENCH_BACKEND=gloo).  Both ranks verify their round trip and rank 0
+    reports the whole job."""
+    import json
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT", "MASTER_ADDR")}
+    env["FEC_BENCH_BACKEND"] = "gloo"
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "3",
+                        "--warmup", "1", "--warm-seconds", "0.2", "--packets", "200000", "--no-extra-configs",
+                        "--no-cpu-baseline", "--no-host-inclusive"], env=env, capture_output=True, text=True,
+                       timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["scaling"] == "weak"
+    assert d["verified"] is True  # every rank's round trip (bench.py reduces the flags over the ranks)
+    assert d["config"]["packets_per_gpu"] == 200000
+    dec = d["decode"]  # summed over the two ranks
+    assert dec["erased"] > 0 and dec["recovered"] + dec["lost"] == dec["erased"]
 
 
 def test_cpp_dropin_program(tmp_path):

@@ -1,0 +1,16 @@
+#!/bin/bash
+# Round-4 GPU check: the whole -m gpu suite, smoke(), then the per-packet latency probe.
+set -o pipefail
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+TAG=${1:-r04}
+OUT=$R/gpurun_out/$TAG
+mkdir -p $OUT
+cd $R
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > $OUT/pytest_gpu.log 2>&1 || { echo "pytest failed"; tail -40 $OUT/pytest_gpu.log; exit 1; }
+tail -2 $OUT/pytest_gpu.log
+timeout -k 10 120 python -u -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1 || { echo "smoke failed"; tail -20 $OUT/smoke.log; exit 1; }
+tail -1 $OUT/smoke.log
+g++ -O2 -std=c++17 -I include tools/stream_latency.cpp -L fec_erasure_code_unit_test_relay_amd -lfec_amd -Wl,-rpath,$R/fec_erasure_code_unit_test_relay_amd -o /tmp/stream_latency || exit 1
+timeout -k 10 120 /tmp/stream_latency 20000 > $OUT/stream_latency.txt 2>&1 || { cat $OUT/stream_latency.txt; exit 1; }
+timeout -k 10 120 /tmp/stream_latency 20000 >> $OUT/stream_latency.txt 2>&1 || { cat $OUT/stream_latency.txt; exit 1; }
+cat $OUT/stream_latency.txt
