@@ -116,7 +116,9 @@ def lib() -> ctypes.CDLL:
     L.fec_vr_encode_batch.argtypes = [vp, vp, vp, vp, vp, vp, vp, vp]
     L.fec_vr_decode_batch.argtypes = [vp, vp, vp, vp, vp, vp, vp]
     L.fec_vr_frames_batch.argtypes = [vp, vp, vp, vp, vp, vp, i64, vp, vp]
-    L.fec_vr_parse_batch.argtypes = [vp, i64, vp, i64, i32, vp, vp, vp, vp]
+    L.fec_vr_parse_batch.argtypes = [vp, vp, i64, vp, vp, vp, vp, vp]
+    L.fec_vr_plan_layout.argtypes = [vp, i64p, i64p]
+    L.fec_vr_plan_row_offsets.argtypes = [vp, vp, vp]
     L.fec_swdf_create.argtypes = [i32, i32, i32, i32, i32, ctypes.POINTER(vp)]
     L.fec_swdf_destroy.argtypes = [vp]
     L.fec_swdf_geometry.argtypes = [vp, ip, ip, ip, ip, ip, ip]
@@ -148,7 +150,8 @@ def lib() -> ctypes.CDLL:
                  "fec_erasure_three_sections_iid", "fec_erasure_ge", "fec_erasure_ge_varying",
                  "fec_erasure_fritchman_varying", "fec_erasure_periodic", "fec_vr_plan_create",
                  "fec_vr_plan_rerun", "fec_vr_plan_destroy", "fec_vr_plan_stats", "fec_vr_plan_timing", "fec_vr_plan_instances", "fec_vr_plan_packets",
-                 "fec_vr_encode_batch", "fec_vr_decode_batch", "fec_vr_frames_batch", "fec_vr_parse_batch", "fec_block_encode_batch",
+                 "fec_vr_encode_batch", "fec_vr_decode_batch", "fec_vr_frames_batch", "fec_vr_parse_batch",
+                 "fec_vr_plan_layout", "fec_vr_plan_row_offsets", "fec_block_encode_batch",
                  "fec_block_decode_batch"]:
         getattr(L, name).restype = i32
     _lib = L

@@ -207,19 +207,22 @@ __device__ __forceinline__ void tile_walk(const EncTileArgs& a, uint8_t* smem) {
     const int PPW = CL ? CG.PPW : a.PPW, R = 4 * PPW;
     // Segment mode (a.seg, the variable-rate schedule): this workgroup encodes tiles [t0, t0+cnt)
     // of one encoder instance -- a fresh encoder over the payload rows [sfirst, sfirst+P) -- and
-    // writes row t to the frames' array of its role (cur before the role switch, old after) at
-    // row sfirst+t, stride a.W.
+    // writes row t to the frames' array of its role (cur before the role switch, old after) in the
+    // compact layout (fec_vr.h): the instance's cur rows from byte scur, its old rows from sold,
+    // stride a.W (its CW rounded to 16).
     constexpr bool segm = SEG;
     int P = a.P;
-    int64_t sfirst = 0, ssw = 0;
+    int64_t sfirst = 0, ssw = 0, scur = 0, sold = 0;
     int seg_t0 = 0, seg_cnt = 0;
     if (segm) {
-        const int64_t* sg = a.seg + 4 * blockIdx.x;
+        const int64_t* sg = a.seg + 6 * blockIdx.x;
         sfirst = sg[0];
         ssw = sg[1];
         P = static_cast<int>(sg[2]);
         seg_t0 = static_cast<int>(sg[3] & 0xffffffff);
         seg_cnt = static_cast<int>(sg[3] >> 32);
+        scur = sg[4];
+        sold = sg[5];
     }
     const uint8_t* pay_base = segm ? a.payload_base + sfirst * (CL ? LC : a.L) : a.payload_base;
     const int pay_bytes = segm ? P * (CL ? LC : a.L) : a.payload_bytes;
@@ -270,14 +273,19 @@ __device__ __forceinline__ void tile_walk(const EncTileArgs& a, uint8_t* smem) {
     const int first = segm ? seg_t0 : static_cast<int>(blockIdx.x) * a.tiles_per_wg;
     const int cnt = segm ? seg_cnt : min(a.tiles_per_wg, a.ntiles - first);  // real tiles of this workgroup (>= 1)
     const int ngl = CL ? CG.ngl : a.ngl;                     // payload LDS-DMA instructions per wave per tile
-    const int nglt = ngl + (has_len ? 1 : 0);
     const int nso = CL ? CG.nso : a.nso;                     // 16-byte stores per thread per tile
-    // VMEM store instructions per wave per tile, the same in every wave (the vmcnt arithmetic of
-    // wait_vm below counts them): nso 16-byte stores + the trimmed-size store; in segment mode
-    // nit row-chunk iterations of two stores (cur and old resources) + two size stores
+    // segment mode's row-chunk iterations (two stores each: the cur and old resources)
     const int nch_seg = (CW + 15) >> 4;
     const int nit_seg = (R * nch_seg + kTileThreads - 1) / kTileThreads;
-    const int ns = segm ? 2 * nit_seg + 2 : nso + 1;
+    // VMEM bookkeeping instead of hand-counted waits: vm_issued counts the VMEM instructions this
+    // wave has issued (the same in every wave: each counted instruction sits in uniform control
+    // flow and is issued even when no lane's offset is in range), incremented right where they are
+    // issued; vm_mark[it & 1] is vm_issued just after tile it's LDS-DMA.  Waiting for that DMA is
+    // wait_vm(vm_issued - vm_mark[it & 1]): every instruction issued after it may stay in flight.
+    // Instructions left uncounted (the tail tile's extra dword/byte stores) only make a wait
+    // stricter, never weaker; moving a DMA or a store moves its count with it.
+    uint32_t vm_issued = 0;
+    uint32_t vm_mark[2] = {0u, 0u};
 
     // tile it (0 = the tile in front of the first one) -> LDS input buffer (it & 1)
     const tv4u rs4 = raw_rsrc(pay_base, pay_bytes);
@@ -309,13 +317,16 @@ __device__ __forceinline__ void tile_walk(const EncTileArgs& a, uint8_t* smem) {
                     dma16_nt(rs4, static_cast<uint32_t>(o < 0 ? 0x7fffffff : o), dst + (j * 4 + wv) * 1024);
                 else
                     dma16(rs4, static_cast<uint32_t>(o < 0 ? 0x7fffffff : o), dst + (j * 4 + wv) * 1024);
+                ++vm_issued;
             }
         }
         if (has_len) {
             const int r = row0 + a.history + lane;
             const bool ok = wv == 0 && lane < R && r >= 0;
             dma4(rl4, static_cast<uint32_t>(ok ? r * 4 : 0x7fffffff), lds_len + (it & 1) * 1024 + wv * 256);
+            ++vm_issued;
         }
+        vm_mark[it & 1] = vm_issued;
     };
 
     // parity rows start zeroed
@@ -327,11 +338,7 @@ __device__ __forceinline__ void tile_walk(const EncTileArgs& a, uint8_t* smem) {
     uint32_t H[K];
     for (int it = 0; it <= cnt; ++it) {
         // tile it's input: every VMEM instruction issued after it may still be in flight
-        {
-            const int s2 = it - 2 >= 1 ? ns : 0, s1 = it - 1 >= 1 ? ns : 0;
-            const int g1 = it + 1 <= cnt ? nglt : 0;
-            wait_vm(s2 + g1 + s1);
-        }
+        wait_vm(static_cast<int>(vm_issued - vm_mark[it & 1]));
         wait_lds_barrier();  // B1: the tile is in LDS everywhere; last tile's output stored
         const int row0 = (first - 1 + it) * R;
         const uint8_t* in = smem + off_in + (it & 1) * in_bytes;
@@ -346,7 +353,7 @@ __device__ __forceinline__ void tile_walk(const EncTileArgs& a, uint8_t* smem) {
                         reinterpret_cast<uint32_t*>(smem + off_in + (it & 1) * in_bytes)[(pl_last * RS + b) >> 2] =
                             __builtin_amdgcn_raw_buffer_load_b32(rs, (P - 1 + a.history) * L + b, 0, 0);
                 }
-                wait_vm(0);
+                wait_vm(0);  // (wave 0's loads only: not counted, drained here)
                 wait_lds_barrier();
             }
         }
@@ -508,15 +515,15 @@ __device__ __forceinline__ void tile_walk(const EncTileArgs& a, uint8_t* smem) {
         if (segm) {
             // row by row into the frames' arrays (stride W, a multiple of 16): chunk c of row p is
             // LDS bytes [p*CW + 16c, +16), the bytes past the codeword zeroed.  Every wave issues
-            // the same stores (ns above): one into the cur rows and one into the old rows per
+            // the same stores (counted in vm_issued): one into the cur rows and one into the old rows per
             // chunk, a lane's other one out of range (buffer stores drop it).
             typedef uint32_t v4u __attribute__((ext_vector_type(4)));
             const int64_t W64 = a.W;
+            const int nsw = static_cast<int>(min<int64_t>(ssw - sfirst, P));  // rows from nsw on go to old
             const __amdgpu_buffer_rsrc_t rcur =
-                __builtin_amdgcn_make_buffer_rsrc(a.cur_rows + sfirst * W64, 0, static_cast<int>(P * W64), 0x00020000);
+                __builtin_amdgcn_make_buffer_rsrc(a.cur_rows + scur, 0, static_cast<int>(nsw * W64), 0x00020000);
             const __amdgpu_buffer_rsrc_t rold =
-                __builtin_amdgcn_make_buffer_rsrc(a.old_rows + sfirst * W64, 0, static_cast<int>(P * W64), 0x00020000);
-            const int nsw = static_cast<int>(ssw - sfirst);  // rows from nsw on go to old
+                __builtin_amdgcn_make_buffer_rsrc(a.old_rows + sold, 0, static_cast<int>((P - nsw) * W64), 0x00020000);
             for (int j = 0; j < nit_seg; ++j) {
                 const int qq = tid + j * kTileThreads;
                 const int pq = qq / nch_seg, c = qq - pq * nch_seg;
@@ -533,8 +540,10 @@ __device__ __forceinline__ void tile_walk(const EncTileArgs& a, uint8_t* smem) {
 #pragma unroll
                 for (int m = 0; m < 4; ++m) vv[m] = __builtin_amdgcn_alignbyte(d5[m + 1], d5[m], sh) & keep_bytes(left - 4 * m);
                 const int off = t * static_cast<int>(W64) + 16 * c;
+                const int off_old = (t - nsw) * static_cast<int>(W64) + 16 * c;
                 __builtin_amdgcn_raw_buffer_store_b128(vv, rcur, ok && t < nsw ? off : 0x7ffffff0, 0, 0);
-                __builtin_amdgcn_raw_buffer_store_b128(vv, rold, ok && t >= nsw ? off : 0x7ffffff0, 0, 0);
+                __builtin_amdgcn_raw_buffer_store_b128(vv, rold, ok && t >= nsw ? off_old : 0x7ffffff0, 0, 0);
+                vm_issued += 2;
             }
             const bool own = tid < R && row0 + tid < P;
             const uint8_t* cwp = out + (own ? tid : 0) * CW;
@@ -554,6 +563,7 @@ __device__ __forceinline__ void tile_walk(const EncTileArgs& a, uint8_t* smem) {
             const int tl = row0 + tid;
             __builtin_amdgcn_raw_buffer_store_b32(static_cast<uint32_t>(sz), rlc, own && tl < nsw ? 4 * tl : 0x7ffffff0, 0, 0);
             __builtin_amdgcn_raw_buffer_store_b32(static_cast<uint32_t>(sz), rlo, own && tl >= nsw ? 4 * tl : 0x7ffffff0, 0, 0);
+            vm_issued += 2;
         } else {
             const int gbase = row0 * CW;  // 16-byte aligned
             const int lim = P * CW - gbase;
@@ -583,6 +593,7 @@ __device__ __forceinline__ void tile_walk(const EncTileArgs& a, uint8_t* smem) {
                     __builtin_amdgcn_raw_buffer_store_b128(vv, rc, so, 0, 2);  // nt
                 else
                     __builtin_amdgcn_raw_buffer_store_b128(vv, rc, so, 0, 0);
+                ++vm_issued;
             }
             // trimmed wire size of packet tid (FEC_Encoder.cpp:55-60): 1 + last non-zero byte
             const bool own = tid < R && row0 + tid < P;
@@ -601,6 +612,7 @@ __device__ __forceinline__ void tile_walk(const EncTileArgs& a, uint8_t* smem) {
             }
             __builtin_amdgcn_raw_buffer_store_b32(static_cast<uint32_t>(sz), rw, own ? 4 * (row0 + tid) : 0x7ffffff0,
                                                   0, 0);
+            ++vm_issued;
         }
     }
     wait_vm(0);

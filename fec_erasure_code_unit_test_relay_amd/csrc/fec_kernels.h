@@ -65,10 +65,12 @@ struct EncTileArgs {
     int dbg;                      // timing experiments only (FEC_TILE_DBG): 1 no parity products,
                                   // 2 no codeword words, 4 no output stores
     int nt;                       // 1: codeword stores non-temporal (FEC_TILE_NT)
-    // segment mode (variable-rate schedule, fec_vr.cpp): null for one stream.  Per workgroup 4
-    // int64: first seq of the encoder instance (its row 0), its role-switch seq, its rows P, and
-    // t0 | cnt << 32 (tiles [t0, t0+cnt) of the instance).  history = 0; rows go to cur_rows /
-    // old_rows (before / from the role switch) at row `seq`, stride W (a multiple of 16).
+    // segment mode (variable-rate schedule, fec_vr.cpp): null for one stream.  Per workgroup 6
+    // int64: first seq of the encoder instance (its row 0), its role-switch seq, its rows P,
+    // t0 | cnt << 32 (tiles [t0, t0+cnt) of the instance), and the byte offsets of the instance's
+    // first cur row and first old row in cur_rows / old_rows (the compact layout, fec_vr.h).
+    // history = 0; rows before / from the role switch go to cur_rows / old_rows at stride W (the
+    // instance's CW rounded to 16).
     const int64_t* seg;
     uint8_t* cur_rows;
     uint8_t* old_rows;

@@ -323,6 +323,8 @@ namespace {
 // The workers run on the 8 CPUs of the creating thread's aligned group (within the allowed set):
 // on a two-socket box the scheduler otherwise spreads them over both sockets (FEC_STREAMS_PIN=0:
 // unplaced).
+// A group with fewer than 4 allowed CPUs (a sparse cpuset: taskset, cgroup) is left alone: spin-
+// polling workers crowded on one or two CPUs stall each other for milliseconds.
 void place_near(int home) {
     if (home < 0) return;
     cpu_set_t allowed, set;
@@ -331,7 +333,13 @@ void place_near(int home) {
     const int base = home & ~7;
     for (int c = base; c < base + 8 && c < CPU_SETSIZE; ++c)
         if (CPU_ISSET(c, &allowed)) CPU_SET(c, &set);
-    if (CPU_COUNT(&set) > 0) (void)pthread_setaffinity_np(pthread_self(), sizeof(set), &set);
+    if (CPU_COUNT(&set) >= 4) (void)pthread_setaffinity_np(pthread_self(), sizeof(set), &set);
+}
+// CPUs this process may run on (its affinity mask), at least 1.
+int allowed_cpus() {
+    cpu_set_t allowed;
+    if (sched_getaffinity(0, sizeof(allowed), &allowed) != 0) return static_cast<int>(std::thread::hardware_concurrency());
+    return std::max(1, CPU_COUNT(&allowed));
 }
 
 class StepPool {
@@ -552,8 +560,8 @@ int fec_streams_create(int max_payload, int T, int B, int N, int nstreams, fec_s
         h->planners.resize(nstreams);
         for (auto& p : h->planners) p.reset(new fec::StreamPlanner(g, h->rules.get()));
         {
-            const unsigned hw = std::thread::hardware_concurrency();
-            int nth = static_cast<int>(std::max(1u, std::min(hw > 1 ? hw - 1 : 1u, 8u)));
+            const int hw = allowed_cpus();  // not hardware_concurrency: the process's cpuset may be smaller
+            int nth = std::max(1, std::min(hw > 1 ? hw - 1 : 1, 8));
             if (const char* e = std::getenv("FEC_STREAMS_THREADS")) nth = std::max(1, std::atoi(e));
             if (nth > 1 && nstreams >= 2 * kPoolMinItems) h->pool.reset(new StepPool(nth));
         }

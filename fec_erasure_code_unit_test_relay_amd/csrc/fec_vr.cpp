@@ -145,7 +145,15 @@ void vr_pin_near(int home) {
     const int base = home & ~7;
     for (int c = base; c < base + 8 && c < CPU_SETSIZE; ++c)
         if (CPU_ISSET(c, &allowed)) CPU_SET(c, &set);
-    if (CPU_COUNT(&set) > 0) (void)pthread_setaffinity_np(pthread_self(), sizeof(set), &set);
+    // a sparse group (fewer than 4 allowed CPUs: taskset, cgroup) is left alone: the plan's
+    // spin-polling threads crowded on one or two CPUs would stall each other
+    if (CPU_COUNT(&set) >= 4) (void)pthread_setaffinity_np(pthread_self(), sizeof(set), &set);
+}
+// CPUs this process may run on (its affinity mask), at least 1.
+int vr_allowed_cpus() {
+    cpu_set_t allowed;
+    if (sched_getaffinity(0, sizeof(allowed), &allowed) != 0) return static_cast<int>(std::thread::hardware_concurrency());
+    return std::max(1, CPU_COUNT(&allowed));
 }
 constexpr int kEstimationCycle = 1000 / 10;  // ESTIMATION_WINDOW_SIZE / ..._REDUCTION_FACTOR (:54-55)
 
@@ -217,8 +225,8 @@ void VrPlan::run(int max_payload, int T, int B, int N, bool mds, const uint8_t* 
 }
 
 void VrPlan::start_workers() {
-    const unsigned hw = std::thread::hardware_concurrency();
-    size_t nth = std::max<size_t>(1, std::min<size_t>(hw > 1 ? hw - 1 : 1u, 8u));
+    const int hw = vr_allowed_cpus();  // not hardware_concurrency: the process's cpuset may be smaller
+    size_t nth = static_cast<size_t>(std::max(1, std::min(hw > 1 ? hw - 1 : 1, 8)));
     if (const char* e = std::getenv("FEC_VR_THREADS")) nth = std::max(1, std::atoi(e));
     {
         std::lock_guard<std::mutex> lk(qmu_);
@@ -1082,11 +1090,35 @@ struct Fork {
         return FEC_OK;
     }
 };
+// Joins a begun fork on every exit path: work queued on the side streams is ordered before the
+// caller's later work even when a launch fails half way (the error is still returned).
+struct ForkScope {
+    Fork& f;
+    bool joined = false;
+    explicit ForkScope(Fork& fk) : f(fk) {}
+    ForkScope(const ForkScope&) = delete;
+    ForkScope& operator=(const ForkScope&) = delete;
+    int join() {
+        joined = true;
+        return f.join();
+    }
+    ~ForkScope() {
+        if (!joined) (void)f.join();
+    }
+};
 }  // namespace
 
 struct fec_vr_plan {
     fec::VrPlan plan;
     int cw_max = 0;
+    // ---- compact row layout (fec_vr.h), per run: per encoder instance first, cur end, end, CWp,
+    // base_cur, base_old; totals; the device per-row offsets ----
+    std::vector<int64_t> layout;
+    int64_t cur_bytes = 0, old_bytes = 0;
+    Upload off_up;
+    void* d_rowoff = nullptr;              // cur_off [sent+1] | old_off [sent+1]
+    size_t d_rowoff_cap = 0;
+    bool rowoff_ready = false;
     // ---- device tables, rebuilt per run ----
     Upload enc_up, dec_up, hdr_up;
     void* d_pk = nullptr;                  // per-packet decoder id, fate, slow flag [P] each
@@ -1113,6 +1145,8 @@ struct fec_vr_plan {
     const int32_t* d_lo_inst = nullptr;
     const int64_t* d_lo_span = nullptr;
     const int64_t* d_lo_cum = nullptr;
+    const int64_t* d_enc_base = nullptr;   // [nenc][2]: byte offsets of the first cur / old row
+    const int64_t* d_lo_base = nullptr;
     int n_lo = 0;
     int64_t lo_total = 0;
     // per tuple with a tile geometry: one launch of fec_encode_tile_kernel<k, n-k> in segment mode
@@ -1136,6 +1170,10 @@ struct fec_vr_plan {
         if (d_pk) {
             (void)hipEventSynchronize(dec_up.used);
             (void)hipFree(d_pk);
+        }
+        if (d_rowoff) {
+            (void)hipEventSynchronize(off_up.used);
+            (void)hipFree(d_rowoff);
         }
     }
     // (re)plans; the per-packet arrays are rewritten only once their last copy has left them
@@ -1165,7 +1203,7 @@ int prepare_encode(fec_vr_plan* v, hipStream_t s) {
     std::map<int, int> tix;   // tuple -> index in v->tiles (-1: no tile geometry)
     std::vector<uint32_t> gtab;
     std::vector<int32_t> inst, lo_inst;
-    std::vector<int64_t> span, cum{0}, lo_span, lo_cum{0};
+    std::vector<int64_t> span, cum{0}, lo_span, lo_cum{0}, base, lo_base;
     std::vector<std::vector<int64_t>> segs;
     inst.reserve(p.enc.size() * 4);
     span.reserve(p.enc.size() * 2);
@@ -1175,9 +1213,12 @@ int prepare_encode(fec_vr_plan* v, hipStream_t s) {
     if (const char* e = std::getenv("FEC_VR_TILE_UNIT")) unit = std::max(1, std::atoi(e));
     const bool tiles_on = !std::getenv("FEC_VR_NO_TILE");
     int tab = 32, out = 16, slot = 16, nmax = 1;
-    for (const auto& e : p.enc) {
+    for (size_t ei = 0; ei < p.enc.size(); ++ei) {
+        const auto& e = p.enc[ei];
         const fec::Geometry g = fec::Geometry::make(p.L, e.T, e.B, e.N);
         const int key = e.T * 1024 + e.B * 32 + e.N;
+        const int64_t b_cur = v->layout[6 * ei + 4], b_old = v->layout[6 * ei + 5];
+        const int64_t cwp = (g.CW + 15) & ~15;
         auto it = toff.find(key);
         if (it == toff.end()) {
             const std::vector<uint32_t> t = fec::parity_mul_tables(fec::make_generator(e.T, e.B, e.N), g.k, g.n);
@@ -1199,27 +1240,29 @@ int prepare_encode(fec_vr_plan* v, hipStream_t s) {
         nmax = std::max(nmax, g.n);
         inst.insert(inst.end(), {g.k, g.n, g.CW, it->second});
         span.insert(span.end(), {e.first, e.role_switch});
+        base.insert(base.end(), {b_cur, b_old});
         cum.push_back(cum.back() + (e.end - e.first));
         int ti = tix[key];
-        if (ti >= 0 && (e.end - e.first) * static_cast<int64_t>(v->cw_max) >= 0x7fff0000) ti = -1;  // 32-bit buffer offsets
+        if (ti >= 0 && (e.end - e.first) * cwp >= 0x7fff0000) ti = -1;  // 32-bit buffer offsets
         if (ti >= 0) {
             const int64_t rows = e.end - e.first, R = v->tiles[static_cast<size_t>(ti)].tg.R;
             const int64_t nt = (rows + R - 1) / R;
             for (int64_t t0 = 0; t0 < nt; t0 += unit) {
                 const int64_t c = std::min<int64_t>(unit, nt - t0);
                 segs[static_cast<size_t>(ti)].insert(segs[static_cast<size_t>(ti)].end(),
-                                                     {e.first, e.role_switch, rows, t0 | (c << 32)});
+                                                     {e.first, e.role_switch, rows, t0 | (c << 32), b_cur, b_old});
             }
         } else {
             lo_inst.insert(lo_inst.end(), {g.k, g.n, g.CW, it->second});
             lo_span.insert(lo_span.end(), {e.first, e.role_switch});
+            lo_base.insert(lo_base.end(), {b_cur, b_old});
             lo_cum.push_back(lo_cum.back() + (e.end - e.first));
         }
     }
     std::vector<int64_t> seg;
     for (size_t i = 0; i < v->tiles.size(); ++i) {
-        v->tiles[i].seg0 = seg.size() / 4;
-        v->tiles[i].nseg = static_cast<int>(segs[i].size() / 4);
+        v->tiles[i].seg0 = seg.size() / 6;
+        v->tiles[i].nseg = static_cast<int>(segs[i].size() / 6);
         seg.insert(seg.end(), segs[i].begin(), segs[i].end());
     }
     std::stable_sort(v->tiles.begin(), v->tiles.end(),
@@ -1233,6 +1276,8 @@ int prepare_encode(fec_vr_plan* v, hipStream_t s) {
     u.add(&v->d_lo_inst, lo_inst);
     u.add(&v->d_lo_span, lo_span);
     u.add(&v->d_lo_cum, lo_cum);
+    u.add(&v->d_enc_base, base);
+    u.add(&v->d_lo_base, lo_base);
     u.add(&v->d_seg, seg);
     if (int st = u.commit(s)) return st;
     v->enc_total = cum.back();
@@ -1292,12 +1337,12 @@ int launch_tile_tuple(const fec_vr_plan* v, const fec_vr_plan::TileTuple& tt, co
     a.off_scratch = tg.off_scratch;
     a.dbg = 0;
     a.nt = 0;
-    a.seg = v->d_seg + 4 * tt.seg0;
+    a.seg = v->d_seg + 6 * tt.seg0;
     a.cur_rows = d_cw_cur;
     a.old_rows = d_cw_old;
     a.cur_len = d_len_cur;
     a.old_len = d_len_old;
-    a.W = v->cw_max;
+    a.W = (tg.CW + 15) & ~15;  // the compact layout's row stride of this tuple
     void* args[] = {&a};
     if (hipLaunchKernel(tt.kfn, dim3(static_cast<unsigned>(tt.nseg)), dim3(256), args, d_len ? tg.lds_len : tg.lds, s) !=
         hipSuccess)
@@ -1366,9 +1411,52 @@ void fec_vr_plan::run(int max_payload, int T, int B, int N, bool mds, const uint
     cw_max = 0;
     for (const auto& e : plan.enc) cw_max = std::max(cw_max, cw_of(plan, e));
     for (const auto& d : plan.dec) cw_max = std::max(cw_max, cw_of(plan, d));
-    cw_max = (cw_max + 15) & ~15;  // row stride: rows start 16-byte aligned (the tile encoder's stores)
-    enc_ready = dec_ready = hdr_ready = false;
+    cw_max = (cw_max + 15) & ~15;  // the widest row (wire packets' stride)
+    // the compact layout: per encoder instance (creation order = seq order) its cur rows
+    // [first, role_switch) and old rows [role_switch, end), each CW rounded to 16 bytes
+    layout.assign(plan.enc.size() * 6, 0);
+    cur_bytes = old_bytes = 0;
+    for (size_t i = 0; i < plan.enc.size(); ++i) {
+        const auto& e = plan.enc[i];
+        const int64_t cwp = (cw_of(plan, e) + 15) & ~15;
+        const int64_t cend = std::min(e.role_switch < 0 ? e.end : e.role_switch, e.end);
+        if (i > 0 && e.first != std::min(plan.enc[i - 1].role_switch, plan.enc[i - 1].end))
+            throw std::logic_error("encoder instances do not tile the frames");
+        int64_t* l = &layout[6 * i];
+        l[0] = e.first;
+        l[1] = cend;
+        l[2] = e.end;
+        l[3] = cwp;
+        l[4] = cur_bytes;
+        l[5] = old_bytes;
+        cur_bytes += (cend - e.first) * cwp;
+        old_bytes += (e.end - cend) * cwp;
+    }
+    enc_ready = dec_ready = hdr_ready = rowoff_ready = false;
 }
+
+namespace {
+// The device per-row offsets of the compact layout (fec_vr_offsets_kernel), once per run.
+int ensure_rowoff(fec_vr_plan* v, hipStream_t s) {
+    if (v->rowoff_ready) return FEC_OK;
+    const int64_t rows = v->plan.sent;
+    Upload& u = v->off_up;
+    if (int st = u.begin()) return st;
+    const int64_t* d_inst = nullptr;
+    u.add(&d_inst, v->layout);
+    if (int st = u.commit(s)) return st;
+    if (int st = Upload::reserve(&v->d_rowoff, &v->d_rowoff_cap, 2 * sizeof(int64_t) * (rows + 1), u.used, s))
+        return st;
+    fec::VrOffsetsArgs a{d_inst, static_cast<int>(v->plan.enc.size()), rows, v->cur_bytes, v->old_bytes,
+                         static_cast<int64_t*>(v->d_rowoff), static_cast<int64_t*>(v->d_rowoff) + rows + 1};
+    if (int st = fec::vr_launch_offsets(a, s)) return st;
+    if (int st = u.done_reading(s)) return st;
+    v->rowoff_ready = true;
+    return FEC_OK;
+}
+const int64_t* cur_off(const fec_vr_plan* v) { return static_cast<const int64_t*>(v->d_rowoff); }
+const int64_t* old_off(const fec_vr_plan* v) { return static_cast<const int64_t*>(v->d_rowoff) + v->plan.sent + 1; }
+}  // namespace
 
 extern "C" {
 
@@ -1480,12 +1568,13 @@ int fec_vr_encode_batch(fec_vr_plan* v, const uint8_t* d_payload, const int32_t*
     if (int st = vr_guarded([&] { return prepare_encode(v, s); })) return st;
     // the tile encoder writes 16-byte chunks of rows at stride cw_max (a multiple of 16)
     auto al = [](const void* q, uintptr_t m) { return (reinterpret_cast<uintptr_t>(q) & m) == 0; };
-    const bool tiled = !v->tiles.empty() && v->cw_max % 16 == 0 && al(d_cw_cur, 15) && al(d_cw_old, 15) &&
+    const bool tiled = !v->tiles.empty() && al(d_cw_cur, 15) && al(d_cw_old, 15) &&
                        al(d_payload, 3) && al(d_len_cur, 3) && al(d_len_old, 3);
     // Independent launches on the caller's stream and the side streams: the generic encoder (a
     // latency-bound walk over the few tuples without a tile geometry) first, on a side stream, then
     // the tuples largest first, round robin.
     if (int st = v->fork.begin(s)) return st;
+    ForkScope scope(v->fork);
     hipStream_t sg = s;
     if (tiled && v->n_lo > 0)
         if (int st = v->fork.stream(1, &sg)) return st;
@@ -1493,8 +1582,8 @@ int fec_vr_encode_batch(fec_vr_plan* v, const uint8_t* d_payload, const int32_t*
                         tiled ? v->d_lo_inst : v->d_enc_inst, tiled ? v->d_lo_span : v->d_enc_span,
                         tiled ? v->d_lo_cum : v->d_enc_cum,
                         tiled ? v->n_lo : static_cast<int>(v->plan.enc.size()), tiled ? v->lo_total : v->enc_total,
-                        v->enc_tab, v->enc_out, v->enc_slot, v->enc_wave, v->d_gtab, v->cw_max, d_cw_cur, d_cw_old,
-                        d_len_cur, d_len_old};
+                        v->enc_tab, v->enc_out, v->enc_slot, v->enc_wave, v->d_gtab,
+                        tiled ? v->d_lo_base : v->d_enc_base, d_cw_cur, d_cw_old, d_len_cur, d_len_old};
     if (int st = fec::vr_launch_encode(a, sg)) return st;
     if (tiled) {
         int i = 0;  // the largest on the caller's stream, the rest round robin after the generic one
@@ -1507,7 +1596,7 @@ int fec_vr_encode_batch(fec_vr_plan* v, const uint8_t* d_payload, const int32_t*
                 return st;
         }
     }
-    if (int st = v->fork.join()) return st;
+    if (int st = scope.join()) return st;
     return v->enc_up.done_reading(s);
 }
 
@@ -1542,8 +1631,9 @@ int fec_vr_frames_batch(fec_vr_plan* v, const uint8_t* d_cw_cur, const int32_t* 
         if (st) return st;
         v->hdr_ready = true;
     }
-    fec::VrFrameArgs a{d_cw_cur, d_len_cur, d_cw_old, d_len_old, v->cw_max, v->d_hdr, p.sent, d_packets, stride,
-                       d_packet_len};
+    if (int st = ensure_rowoff(v, s)) return st;
+    fec::VrFrameArgs a{d_cw_cur, d_len_cur, d_cw_old, d_len_old, cur_off(v), old_off(v), v->d_hdr, p.sent,
+                       d_packets, stride, d_packet_len};
     if (int st = fec::vr_launch_frames(a, hip_stream)) return st;
     return v->hdr_up.done_reading(s);
 }
@@ -1563,26 +1653,55 @@ int fec_vr_decode_batch(fec_vr_plan* v, const uint8_t* d_cw_cur, const uint8_t* 
         }))
         return st;
     const auto& p = v->plan;
-    fec::VrCopyArgs ca{d_cw_cur, v->cw_max, v->d_pk_dec, v->d_inst, v->d_fate, v->d_slow, p.P, p.L, d_out, d_out_len,
-                       std::max(1, 256 / ((p.L + 3) / 4)), v->d_geo};
+    if (int st = ensure_rowoff(v, s)) return st;
+    fec::VrCopyArgs ca{d_cw_cur, cur_off(v), v->d_pk_dec, v->d_inst, v->d_fate, v->d_slow, p.P, p.L, d_out,
+                       d_out_len, v->d_geo};
     // the recovery writes only the rows (and lengths) the copy leaves alone: side by side
     if (int st = v->fork.begin(s)) return st;
+    ForkScope scope(v->fork);
     hipStream_t sr;
     if (int st = v->fork.stream(p.rec_x.empty() ? 0 : 1, &sr)) return st;
     if (int st = fec::vr_launch_copy(ca, hip_stream)) return st;
-    fec::VrRecArgs ra{d_cw_cur, d_cw_old, v->cw_max, p.sent, v->d_rec_x, v->d_rec_dec, v->d_rec_coef,
+    fec::VrRecArgs ra{d_cw_cur, d_cw_old, cur_off(v), old_off(v), p.sent, v->d_rec_x, v->d_rec_dec, v->d_rec_coef,
                       static_cast<int>(p.rec_x.size()), v->d_inst, v->d_inst_switch, v->d_gf, p.L, d_out, d_out_len};
     if (int st = fec::vr_launch_recover(ra, sr)) return st;
-    if (int st = v->fork.join()) return st;
+    if (int st = scope.join()) return st;
     return v->dec_up.done_reading(s);
 }
 
-int fec_vr_parse_batch(const uint8_t* d_packets, int64_t stride, const int32_t* d_packet_len, int64_t rows,
-                       int cw_max, uint8_t* d_cw_cur, uint8_t* d_cw_old, int32_t* d_header, void* hip_stream) {
-    if (rows < 0 || cw_max < 1 || (rows > 0 && (!d_packets || !d_packet_len || !d_cw_cur || !d_cw_old)))
-        return FEC_ERR_ARG;
-    fec::VrParseArgs a{d_packets, stride, d_packet_len, rows, cw_max, d_cw_cur, d_cw_old, d_header};
+int fec_vr_parse_batch(fec_vr_plan* v, const uint8_t* d_packets, int64_t stride, const int32_t* d_packet_len,
+                       uint8_t* d_cw_cur, uint8_t* d_cw_old, int32_t* d_header, void* hip_stream) {
+    if (!v || !d_packets || !d_packet_len || !d_cw_cur || !d_cw_old) return FEC_ERR_ARG;
+    hipStream_t s = static_cast<hipStream_t>(hip_stream);
+    if (int st = vr_guarded([&] { return ensure_rowoff(v, s); })) return st;
+    fec::VrParseArgs a{d_packets, stride, d_packet_len, v->plan.sent, cur_off(v), old_off(v), d_cw_cur, d_cw_old,
+                       d_header};
     return fec::vr_launch_parse(a, hip_stream);
+}
+
+int fec_vr_plan_layout(const fec_vr_plan* v, int64_t* cur_bytes, int64_t* old_bytes) {
+    if (!v) return FEC_ERR_ARG;
+    if (cur_bytes) *cur_bytes = v->cur_bytes;
+    if (old_bytes) *old_bytes = v->old_bytes;
+    return FEC_OK;
+}
+
+int fec_vr_plan_row_offsets(const fec_vr_plan* v, int64_t* cur_off, int64_t* old_off) {
+    if (!v) return FEC_ERR_ARG;
+    const auto& L = v->layout;
+    const int64_t rows = v->plan.sent;
+    const size_t ne = L.size() / 6;
+    size_t e = 0;
+    for (int64_t s = 0; s < rows; ++s) {  // as fec_vr_offsets_kernel
+        while (e + 1 < ne && L[6 * (e + 1)] <= s) ++e;
+        const int64_t* me = &L[6 * e];
+        if (cur_off) cur_off[s] = me[4] + (s - me[0]) * me[3];
+        const int64_t* pv = e > 0 ? me - 6 : nullptr;
+        if (old_off) old_off[s] = (pv && s >= pv[1] && s < pv[2]) ? pv[5] + (s - pv[1]) * pv[3] : me[5];
+    }
+    if (cur_off) cur_off[rows] = v->cur_bytes;
+    if (old_off) old_off[rows] = v->old_bytes;
+    return FEC_OK;
 }
 
 }  // extern "C"

@@ -190,6 +190,15 @@ private:
 };
 
 // Device side of the schedule (fec_vr_kernels.hip).  All launches go to `s`.
+//
+// Row layout of the frames' codeword arrays (compact): row s of `cur` holds the codeword of frame
+// s's current encoder instance, row s of `old` the old instance's during double coding (no row
+// otherwise).  Every row is its instance's CW rounded up to 16 bytes; the rows of one instance are
+// consecutive at that stride, and instances follow each other in seq order, so both arrays are
+// dense and a run of consecutive packets is one contiguous span.  Per instance e: cur rows
+// [first_e, role_switch_e) from byte base_cur_e, old rows [role_switch_e, end_e) from base_old_e;
+// per row: cur_off[s] / old_off[s] (sent + 1 entries each, prefix form: row s spans
+// [off[s], off[s+1]), empty for a frame without an old codeword).
 // Every encoder instance of the schedule in one launch (any mix of (T,B,N)): codeword c of the
 // list = instance e's call for seq = first_e + (c - cum[e]), written to cur[seq] before e's
 // role switch and to old[seq] after (Variable_Rate_FEC_Encoder.cpp:140-217).
@@ -207,7 +216,7 @@ struct VrEncodeArgs {
     int slot_bytes;           //   one ring slot (k planes of ceil(S/4) words, max over tuples)
     int wave_bytes;           //   tab + out + n_max * slot
     const uint32_t* gtab;     // per tuple [k][n-k][8]: gf_mul4 tables of G[i][k+jj] (+ non-zero flag)
-    int64_t W;                // row stride of cur / old
+    const int64_t* base;      // [nenc][2]: byte offsets of the instance's first cur row / first old row
     uint8_t* cur;
     uint8_t* old;
     int32_t* len_cur;
@@ -215,7 +224,7 @@ struct VrEncodeArgs {
 };
 struct VrCopyArgs {     // received packets: systematic bytes of cur[x] in its decoder's geometry
     const uint8_t* cur;
-    int64_t W;
+    const int64_t* cur_off;  // [sent+1]
     const int32_t* pk_dec;   // [P] reporting decoder
     const int32_t* inst;     // [ndec][4]: k, n, CW, 0
     const uint8_t* fate;     // [P]
@@ -224,13 +233,13 @@ struct VrCopyArgs {     // received packets: systematic bytes of cur[x] in its d
     int L;
     uint8_t* out;
     int32_t* out_len;
-    int ppb;                 // packets per 256-thread workgroup: max(1, 256 / ceil(L / 4))
     uint32_t* geo;           // [P] scratch: k | n << 8 | fate << 16 | slow << 24 (fec_vr_geo_kernel)
 };
 struct VrRecArgs {      // recovered packets: coefficient rows over the reporting decoder's inputs
     const uint8_t* cur;
     const uint8_t* old;
-    int64_t W;
+    const int64_t* cur_off;  // [sent+1]
+    const int64_t* old_off;  // [sent+1]
     int64_t rows;            // sent packets (valid rows of cur / old)
     const int64_t* rec_x;
     const int32_t* rec_dec;
@@ -250,7 +259,8 @@ struct VrFrameArgs {
     const int32_t* len_cur;
     const uint8_t* old;
     const int32_t* len_old;
-    int64_t W;               // row stride of cur / old
+    const int64_t* cur_off;  // [rows+1]
+    const int64_t* old_off;  // [rows+1]
     const int32_t* hdr;      // [rows][4]: T, B, N, counter
     int64_t rows;
     uint8_t* packets;
@@ -258,17 +268,30 @@ struct VrFrameArgs {
     int32_t* packet_len;
 };
 // The receiver's split of a wire packet (Application_Layer_Receiver.cpp:361-366,
-// Variable_Rate_FEC_Decoder.cpp:2156-2160): cur / old rows zero-padded to W, header fields out.
+// Variable_Rate_FEC_Decoder.cpp:2156-2160): cur / old rows zero-padded to their row size, header
+// fields out.
 struct VrParseArgs {
     const uint8_t* packets;
     int64_t stride;
     const int32_t* packet_len;
     int64_t rows;
-    int64_t W;
+    const int64_t* cur_off;  // [rows+1]
+    const int64_t* old_off;  // [rows+1]
     uint8_t* cur;
     uint8_t* old;
     int32_t* hdr;            // [rows][5]: seq, T, B, N, counter (may be null)
 };
+// The per-row offsets from the encoder instances (one thread per instance: its cur rows, and the
+// old rows of the instance before it, which are the same seqs).
+struct VrOffsetsArgs {
+    const int64_t* inst;     // [nenc][6]: first, role_switch (cur end), end, CW rounded to 16, base_cur, base_old
+    int nenc;
+    int64_t rows;            // sent
+    int64_t cur_total, old_total;
+    int64_t* cur_off;        // [rows+1]
+    int64_t* old_off;        // [rows+1]
+};
+int vr_launch_offsets(const VrOffsetsArgs& a, void* s);
 int vr_launch_frames(const VrFrameArgs& a, void* s);
 int vr_launch_parse(const VrParseArgs& a, void* s);
 int vr_launch_encode(const VrEncodeArgs& a, void* s);

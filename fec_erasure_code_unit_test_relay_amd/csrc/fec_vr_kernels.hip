@@ -20,8 +20,8 @@ __global__ __launch_bounds__(256) void fec_vr_frame_kernel(VrFrameArgs a) {
          r += static_cast<int64_t>(gridDim.x) * 4) {
         const int lc = a.len_cur[r], lo = a.len_old[r];
         uint8_t* o = a.packets + r * a.stride;
-        const uint8_t* c = a.cur + r * a.W;
-        const uint8_t* d = a.old + r * a.W;
+        const uint8_t* c = a.cur + a.cur_off[r];
+        const uint8_t* d = a.old + a.old_off[r];
         if (lane < 10) {
             const int32_t* h = a.hdr + 4 * r;
             uint8_t v;
@@ -50,12 +50,11 @@ __global__ __launch_bounds__(256) void fec_vr_parse_kernel(VrParseArgs a) {
         const int plen = a.packet_len[r];
         const int lc = plen >= 10 ? p[8] * 256 + p[9] : 0;
         const int64_t lo = plen - 10 - lc;
-        uint8_t* c = a.cur + r * a.W;
-        uint8_t* d = a.old + r * a.W;
-        for (int64_t b = lane; b < a.W; b += 64) {
-            c[b] = b < lc ? p[10 + b] : 0;
-            d[b] = b < lo ? p[10 + lc + b] : 0;
-        }
+        uint8_t* c = a.cur + a.cur_off[r];
+        uint8_t* d = a.old + a.old_off[r];
+        const int64_t wc = a.cur_off[r + 1] - a.cur_off[r], wo = a.old_off[r + 1] - a.old_off[r];
+        for (int64_t b = lane; b < wc; b += 64) c[b] = b < lc ? p[10 + b] : 0;
+        for (int64_t b = lane; b < wo; b += 64) d[b] = b < lo ? p[10 + lc + b] : 0;
         if (a.hdr && lane == 0) {
             int32_t* h = a.hdr + 5 * r;
             h[0] = (p[0] << 24) | (p[1] << 16) | (p[2] << 8) | p[3];
@@ -164,7 +163,8 @@ __global__ __launch_bounds__(256) void fec_vr_encode_kernel(VrEncodeArgs a) {
         }
         next_row = seq + 1;
         const bool to_old = seq >= sw;
-        uint8_t* row = (to_old ? a.old : a.cur) + seq * a.W;
+        const int64_t CWp = (CW + 15) & ~15;
+        uint8_t* row = to_old ? a.old + a.base[2 * e + 1] + (seq - sw) * CWp : a.cur + a.base[2 * e] + (seq - first) * CWp;
         const int head = static_cast<int>(reinterpret_cast<uintptr_t>(row) & 3);
         wave_sync();
         const int slot_seq = static_cast<int>(seq % n);
@@ -232,80 +232,120 @@ __global__ __launch_bounds__(256) void fec_vr_geo_kernel(VrCopyArgs a) {
     a.geo[x] = g;
 }
 
-// One thread per output dword of kVrCopyU packets: a workgroup covers kVrCopyU * a.ppb consecutive
-// packets, thread t takes word t % L4 of packets u * ppb + t / L4 (u < kVrCopyU).  Per packet: its
-// word (fec_vr_geo_kernel), then the header and the word's 4 bytes together (the byte positions
-// depend only on k and n; the bytes past the copied length are masked afterwards), then the store.
-// (The chain fate -> decoder -> geometry -> header -> bytes in this kernel: 220 us per 360 000
-// packets, r03z.)  Payload byte b is codeword byte (h / k) * n + h % k of the reporting decoder's
-// geometry, h = b + 2; the header is at symbols 0 and 1 of sub-stream 0 (k = 1: position 0 of
-// sub-streams 0 and 1), Decoder.cpp:89-96; the slow path clamps the length (:148-149).
-constexpr int kVrCopyU = 4;
+// The received packets' systematic copies, a tile of kVrCopyTP consecutive packets per workgroup:
+// their cur rows are one contiguous span of the compact layout, read with 16-byte loads into LDS
+// next to a per-packet record (row offset and width, geometry, copied length); then each thread
+// makes output dwords (payload byte b = codeword byte (h / k) * n + h % k of the reporting
+// decoder's geometry, fec_vr_geo_kernel's word, h = b + 2; the header at symbols 0 and 1 of
+// sub-stream 0, k = 1: position 0 of sub-streams 0 and 1, Decoder.cpp:89-96; the slow path clamps
+// the length, :148-149), and the tile's payload rows leave as one contiguous run.  A tile wider
+// than the stage (rows of k <= 3) gathers from HBM.  Lost packets get a zero row and length 0;
+// recovered ones are left to fec_vr_recover_kernel.  Bytes past a row read as zero.
+constexpr int kVrCopyTP = 16;
+constexpr int kVrCopyStage = 16384;
 __global__ __launch_bounds__(256) void fec_vr_copy_kernel(VrCopyArgs a) {
+    __shared__ __attribute__((aligned(16))) uint8_t stage[kVrCopyStage];
+    __shared__ int s_ro[kVrCopyTP], s_rw[kVrCopyTP], s_kn[kVrCopyTP], s_cp[kVrCopyTP];
+    __shared__ float s_rk[kVrCopyTP];
+    const int tid = threadIdx.x;
     const int L = a.L, L4 = (L + 3) >> 2;
-    const int pl = static_cast<int>(threadIdx.x) / L4;
-    const int w = static_cast<int>(threadIdx.x) - pl * L4;
-    if (pl >= a.ppb) return;
-    const int64_t wmax = a.W - 1;
-    int64_t x[kVrCopyU];
-    uint32_t g[kVrCopyU];
+    const float rl4 = 1.0f / static_cast<float>(L4);
+    const int64_t ntiles = (a.P + kVrCopyTP - 1) / kVrCopyTP;
+    for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+        const int64_t x0 = tile * kVrCopyTP;
+        const int np = static_cast<int>(min<int64_t>(kVrCopyTP, a.P - x0));
+        const int64_t o0 = a.cur_off[x0];
+        const int64_t span = a.cur_off[x0 + np] - o0;
+        const bool staged = span <= kVrCopyStage;  // uniform over the workgroup
+        if (staged) {
+            const uint4* src = reinterpret_cast<const uint4*>(a.cur + o0);
+            for (int c = tid; 16 * c < span; c += 256) reinterpret_cast<uint4*>(stage)[c] = src[c];
+        }
+        int ln = 0;
+        if (tid < np) {
+            const int64_t x = x0 + tid;
+            const uint32_t g = a.geo[x];
+            const int64_t ro = a.cur_off[x];
+            s_ro[tid] = static_cast<int>(ro - o0);
+            s_rw[tid] = static_cast<int>(a.cur_off[x + 1] - ro);
+            const int f = static_cast<int>(g >> 16 & 0xff);
+            const int k = f == 1 ? static_cast<int>(g & 0xff) : 1;
+            s_kn[tid] = f == 1 ? static_cast<int>(g & 0xffff) : (f == 2 ? -1 : 0);  // -1: recovered, 0: lost
+            s_rk[tid] = 1.0f / static_cast<float>(k);
+        }
+        __syncthreads();
+        if (tid < np) {  // the header of a received packet: its length, clamped on the slow path
+            const int64_t x = x0 + tid;
+            const int kn = s_kn[tid];
+            if (kn > 0) {
+                const int k = kn & 0xff, n = kn >> 8, rw = s_rw[tid];
+                const uint8_t* lrow = stage + s_ro[tid];
+                const uint8_t* grow = a.cur + o0 + s_ro[tid];
+                const int p1 = k > 1 ? 1 : n;
+                const int h0 = rw > 0 ? (staged ? lrow[0] : grow[0]) : 0;
+                const int h1 = p1 < rw ? (staged ? lrow[p1] : grow[p1]) : 0;
+                const int hdr = h0 * 256 + h1;
+                ln = (a.geo[x] >> 24) ? min(hdr, L) : hdr;
+            }
+            if (kn >= 0) a.out_len[x] = ln;
+            s_cp[tid] = min(ln, L);
+        }
+        __syncthreads();
+        for (int d = tid; d < np * L4; d += 256) {
+            const int p = static_cast<int>((static_cast<float>(d) + 0.5f) * rl4);
+            const int w = d - p * L4;
+            const int kn = s_kn[p];
+            if (kn < 0) continue;  // recovered: fec_vr_recover_kernel's row
+            const int cp = s_cp[p], b0 = 4 * w;
+            uint32_t val = 0;
+            if (b0 < cp) {
+                const int k = kn & 0xff, n = kn >> 8, rw = s_rw[p];
+                const uint8_t* lrow = stage + s_ro[p];
+                const uint8_t* grow = a.cur + o0 + s_ro[p];
+                const int h = b0 + 2;
+                int sidx = static_cast<int>((static_cast<float>(h) + 0.5f) * s_rk[p]);
+                int i = h - sidx * k;
 #pragma unroll
-    for (int u = 0; u < kVrCopyU; ++u) {
-        x[u] = (static_cast<int64_t>(blockIdx.x) * kVrCopyU + u) * a.ppb + pl;
-        g[u] = x[u] < a.P ? a.geo[x[u]] : 2u << 16;  // 2: recovered (fec_vr_recover_kernel) or none
-    }
-    int k[kVrCopyU], n[kVrCopyU], cp[kVrCopyU], ln[kVrCopyU];
-    const uint8_t* src[kVrCopyU];
-    uint32_t h0[kVrCopyU], h1[kVrCopyU];
-#pragma unroll
-    for (int u = 0; u < kVrCopyU; ++u) {
-        const bool rx = (g[u] >> 16 & 0xff) == 1;
-        k[u] = rx ? static_cast<int>(g[u] & 0xff) : 1;
-        n[u] = rx ? static_cast<int>(g[u] >> 8 & 0xff) : 1;
-        src[u] = a.cur + (rx ? x[u] : 0) * a.W;
-        h0[u] = rx ? src[u][0] : 0u;
-        h1[u] = rx ? src[u][k[u] > 1 ? 1 : n[u]] : 0u;
-    }
-    for (int ww = w; ww < L4; ww += 256) {  // one pass unless L > 1024 (then ppb = 1)
-        const int b0 = 4 * ww;
-        uint32_t byte[kVrCopyU][4];
-#pragma unroll
-        for (int u = 0; u < kVrCopyU; ++u) {
-            const bool rx = (g[u] >> 16 & 0xff) == 1;
-            const int h = b0 + 2;
-            int sidx = static_cast<int>((static_cast<float>(h) + 0.5f) / static_cast<float>(k[u]));
-            int i = h - sidx * k[u];
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-                const int64_t pos = min<int64_t>(static_cast<int64_t>(sidx) * n[u] + i, wmax);
-                byte[u][e] = rx ? src[u][pos] : 0u;
-                if (++i == k[u]) {
-                    i = 0;
-                    ++sidx;
+                for (int e = 0; e < 4; ++e) {
+                    const int pos = sidx * n + i;
+                    if (b0 + e < cp && pos < rw) val |= static_cast<uint32_t>(staged ? lrow[pos] : grow[pos]) << (8 * e);
+                    if (++i == k) {
+                        i = 0;
+                        ++sidx;
+                    }
                 }
             }
-        }
-#pragma unroll
-        for (int u = 0; u < kVrCopyU; ++u) {
-            const uint32_t f = g[u] >> 16 & 0xff;
-            if (f == 2) continue;
-            if (ww == w) {
-                const int hdr = static_cast<int>(h0[u] * 256 + h1[u]);
-                ln[u] = f == 1 ? ((g[u] >> 24) ? min(hdr, L) : hdr) : 0;
-                cp[u] = min(ln[u], L);
-            }
-            uint32_t v = 0;
-#pragma unroll
-            for (int e = 0; e < 4; ++e) v |= (b0 + e < cp[u] ? byte[u][e] : 0u) << (8 * e);
-            uint8_t* o = a.out + x[u] * L;
-            if (b0 + 4 <= L && (L & 3) == 0) {
-                *reinterpret_cast<uint32_t*>(o + b0) = v;
+            uint8_t* o = a.out + (x0 + p) * L;
+            if ((L & 3) == 0) {
+                *reinterpret_cast<uint32_t*>(o + b0) = val;
             } else {
-                for (int e = 0; e < 4 && b0 + e < L; ++e) o[b0 + e] = static_cast<uint8_t>(v >> (8 * e));
+                for (int e = 0; e < 4 && b0 + e < L; ++e) o[b0 + e] = static_cast<uint8_t>(val >> (8 * e));
             }
-            if (ww == 0) a.out_len[x[u]] = ln[u];
         }
+        __syncthreads();  // the stage and records are read before the next tile's
     }
+}
+
+// Per-row offsets of the compact layout, one thread per row s: e = the last instance with
+// first_e <= s (binary search); cur row at base_cur_e + (s - first_e) * CWp_e; the same seq's old
+// row belongs to instance e-1 while s < end_{e-1} (double coding), else it is empty (offset = where
+// e's old block begins, base_old_e).
+__global__ __launch_bounds__(256) void fec_vr_offsets_kernel(VrOffsetsArgs a) {
+    const int64_t s = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x;
+    if (s == 0) {
+        a.cur_off[a.rows] = a.cur_total;
+        a.old_off[a.rows] = a.old_total;
+    }
+    if (s >= a.rows) return;
+    int lo = 0, hi = a.nenc - 1;
+    while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (a.inst[6 * mid] <= s) lo = mid; else hi = mid - 1;
+    }
+    const int64_t* me = a.inst + 6 * lo;
+    a.cur_off[s] = me[4] + (s - me[0]) * me[3];
+    const int64_t* pv = lo > 0 ? me - 6 : nullptr;
+    a.old_off[s] = (pv && s >= pv[1] && s < pv[2]) ? pv[5] + (s - pv[1]) * pv[3] : me[5];
 }
 
 // One wave per recovered packet (as fec_recover_kernel): byte h = (sub-stream h/k, position i =
@@ -342,7 +382,7 @@ __global__ __launch_bounds__(256) void fec_vr_recover_kernel(VrRecArgs a) {
                     const int lq = lc[i * n + q];
                     const int64_t row = x - i + q;
                     if (lq == 255 || row < 0 || row >= a.rows) continue;
-                    const uint8_t v = (row < sw ? a.cur : a.old)[row * a.W + s * n + q];
+                    const uint8_t v = row < sw ? a.cur[a.cur_off[row] + s * n + q] : a.old[a.old_off[row] + s * n + q];
                     if (v) acc ^= gexp[lq + glog[v]];
                 }
             }
@@ -394,9 +434,14 @@ int vr_launch_copy(const VrCopyArgs& a, void* s) {
     if (a.P <= 0) return FEC_OK;
     hipLaunchKernelGGL(fec_vr_geo_kernel, dim3(static_cast<unsigned>((a.P + 255) / 256)), dim3(256), 0,
                        static_cast<hipStream_t>(s), a);
-    const int64_t per_wg = static_cast<int64_t>(kVrCopyU) * a.ppb;
-    hipLaunchKernelGGL(fec_vr_copy_kernel, dim3(static_cast<unsigned>((a.P + per_wg - 1) / per_wg)), dim3(256), 0,
+    const int64_t grid = (a.P + kVrCopyTP - 1) / kVrCopyTP;
+    hipLaunchKernelGGL(fec_vr_copy_kernel, dim3(static_cast<unsigned>(grid)), dim3(256), 0,
                        static_cast<hipStream_t>(s), a);
+    return hipGetLastError() == hipSuccess ? FEC_OK : FEC_ERR_HIP;
+}
+int vr_launch_offsets(const VrOffsetsArgs& a, void* s) {
+    hipLaunchKernelGGL(fec_vr_offsets_kernel, dim3(static_cast<unsigned>((std::max<int64_t>(1, a.rows) + 255) / 256)),
+                       dim3(256), 0, static_cast<hipStream_t>(s), a);
     return hipGetLastError() == hipSuccess ? FEC_OK : FEC_ERR_HIP;
 }
 int vr_launch_recover(const VrRecArgs& a, void* s) {

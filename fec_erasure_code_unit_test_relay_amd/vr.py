@@ -85,21 +85,45 @@ class VrPlan:
         return {tuple(int(v) for v in r[:3]) for r in self.encoders}
 
     # -- batched device-resident path -----------------------------------------------------------
+    def layout(self):
+        """(cur_bytes, old_bytes): sizes of the compact codeword arrays (fec_vr.h)."""
+        cb, ob = ctypes.c_int64(), ctypes.c_int64()
+        check(lib().fec_vr_plan_layout(self._h, ctypes.byref(cb), ctypes.byref(ob)), "fec_vr_plan_layout")
+        return cb.value, ob.value
+
+    def row_offsets(self):
+        """(cur_off, old_off) int64 [sent+1] each: row s of the cur / old array spans
+        [off[s], off[s+1]) (empty old rows for frames without double coding)."""
+        co = np.zeros(self.sent + 1, dtype=np.int64)
+        oo = np.zeros(self.sent + 1, dtype=np.int64)
+        check(lib().fec_vr_plan_row_offsets(self._h, co.ctypes.data_as(ctypes.c_void_p),
+                                            oo.ctypes.data_as(ctypes.c_void_p)), "fec_vr_plan_row_offsets")
+        return co, oo
+
+    @staticmethod
+    def rows(arr, off, first: int, end: int, width: int):
+        """Rows [first, end) of one encoder instance (consecutive at stride CW rounded to 16) of a
+        compact array as a [end-first, width] view."""
+        if end <= first:
+            return arr[:0].view(0, width)
+        o0 = int(off[first])
+        stride = int(off[first + 1] - off[first])
+        return arr[o0:o0 + (end - first) * stride].view(end - first, stride)[:, :width]
+
     def alloc_frames(self, device="cuda", zero=True):
-        """(cw_cur, len_cur, cw_old, len_old) buffers for encode().  Zeroed by default (rows read
-        beyond an encoder's CW only when a decoder's (T,B,N) differs from the frame's); the
-        decoders of this plan read each row within its own codeword, so `zero=False` is enough to
-        reproduce the receiver here."""
+        """(cw_cur, len_cur, cw_old, len_old) buffers for encode(): the two compact codeword arrays
+        (1-D, fec_vr_plan_layout's sizes) and the per-frame trimmed sizes."""
         import torch
         mk = torch.zeros if zero else torch.empty
-        return (mk((self.sent, self.cw_max), dtype=torch.uint8, device=device),
+        cb, ob = self.layout()
+        return (mk(max(cb, 16), dtype=torch.uint8, device=device),
                 torch.zeros(self.sent, dtype=torch.int32, device=device),
-                mk((self.sent, self.cw_max), dtype=torch.uint8, device=device),
+                mk(max(ob, 16), dtype=torch.uint8, device=device),
                 torch.zeros(self.sent, dtype=torch.int32, device=device))
 
     def encode(self, payload, lengths=None, frames=None):
-        """payload: [sent, L] uint8 on the GPU -> (cw_cur, len_cur, cw_old, len_old): row s = the
-        codewords frame s carries (stride cw_max), trimmed sizes (old: 0 if none)."""
+        """payload: [sent, L] uint8 on the GPU -> (cw_cur, len_cur, cw_old, len_old): the codewords
+        every frame carries in the compact arrays (row_offsets()), trimmed sizes (old: 0 if none)."""
         import torch
         assert payload.dtype == torch.uint8 and payload.is_cuda and tuple(payload.shape) == (self.sent, self.L)
         cw_cur, len_cur, cw_old, len_old = frames if frames is not None else self.alloc_frames(payload.device)
@@ -140,16 +164,18 @@ class VrPlan:
         return packets, packet_len
 
 
-def parse_packets(packets, packet_len, cw_max: int):
-    """The receiver's split of P2P wire packets (rows [R, stride] uint8 on the GPU) into the current
-    / old codewords (zero-padded to cw_max) and header fields [R, 5] (seq, T, B, N, counter)."""
+def parse_packets(plan: "VrPlan", packets, packet_len):
+    """The receiver's split of the plan's P2P wire packets (rows [sent, stride] uint8 on the GPU)
+    into the current / old codeword rows of the compact arrays (zero-padded to their row size) and
+    header fields [sent, 5] (seq, T, B, N, counter)."""
     import torch
     assert packets.dtype == torch.uint8 and packets.is_cuda and packets.is_contiguous() and packets.dim() == 2
     R = packets.shape[0]
-    assert packet_len.dtype == torch.int32 and packet_len.numel() >= R
-    cur = torch.empty((R, cw_max), dtype=torch.uint8, device=packets.device)
-    old = torch.empty((R, cw_max), dtype=torch.uint8, device=packets.device)
+    assert R == plan.sent and packet_len.dtype == torch.int32 and packet_len.numel() >= R
+    cb, ob = plan.layout()
+    cur = torch.empty(max(cb, 16), dtype=torch.uint8, device=packets.device)
+    old = torch.empty(max(ob, 16), dtype=torch.uint8, device=packets.device)
     hdr = torch.empty((R, 5), dtype=torch.int32, device=packets.device)
-    check(lib().fec_vr_parse_batch(_ptr(packets), packets.shape[1], _ptr(packet_len), R, cw_max, _ptr(cur), _ptr(old),
+    check(lib().fec_vr_parse_batch(plan._h, _ptr(packets), packets.shape[1], _ptr(packet_len), _ptr(cur), _ptr(old),
                                    _ptr(hdr), _stream_handle(torch)), "fec_vr_parse_batch")
     return cur, old, hdr

@@ -247,7 +247,7 @@ int fec_vr_plan_destroy(fec_vr_plan *plan);
 int fec_vr_plan_rerun(fec_vr_plan *plan, const uint8_t *erasure, int64_t n_erasure, int64_t P, int async);
 /* lost: packets among 0..P-1 the receiver outputs empty ("Final FEC loss rate" x P); switches:
  * "Start double coding at the source" count; coding_rate: Variable_Rate_FEC_Encoder's final rate;
- * sent: packets the sender produced; cw_max: row stride of the codeword arrays below. */
+ * sent: packets the sender produced; cw_max: the widest codeword row (16-byte multiple). */
 int fec_vr_plan_stats(const fec_vr_plan *plan, int64_t *lost, int64_t *switches, double *coding_rate,
                       int64_t *sent, int *n_encoders, int *n_decoders, int *cw_max);
 /* wall time of the plan's two phases: the serial control loop (sender, estimators, switches,
@@ -260,11 +260,17 @@ int fec_vr_plan_instances(const fec_vr_plan *plan, int64_t *encoders, int64_t *d
  * recovered, 3 lost) and the decoder instance that reported it.  NULL pointers are skipped. */
 int fec_vr_plan_packets(const fec_vr_plan *plan, int32_t *frames, uint8_t *erased, uint8_t *fate,
                         int32_t *fate_decoder);
-/* Device-resident execution (one fec_encode_batch / fec_decode_batch per instance role).  Encode:
- * d_payload (sent rows of max_payload bytes) -> row s of d_cw_cur / d_cw_old (stride cw_max, rows
- * zero beyond each codeword: clear them first) = the codewords frame s carries, trimmed sizes in
- * d_len_cur / d_len_old.  Decode: those arrays + d_erased (sent bytes) -> d_out (P rows of
- * max_payload) and d_out_len (P ints, 0 = lost), the receiver's reported outputs. */
+/* Device-resident execution.  The frames' codewords live in two compact arrays (no per-row padding
+ * beyond 16-byte alignment): row s of d_cw_cur = the codeword of frame s's current encoder, row s
+ * of d_cw_old = the old encoder's during double coding (empty otherwise); each row is its
+ * instance's CW rounded up to 16 bytes, rows in seq order.  fec_vr_plan_layout gives the two array
+ * sizes, fec_vr_plan_row_offsets the per-row byte offsets (sent + 1 each, prefix form).  Encode:
+ * d_payload (sent rows of max_payload bytes) -> d_cw_cur / d_cw_old rows, trimmed sizes in
+ * d_len_cur / d_len_old (sent each; 0 when no old codeword).  Decode: those arrays + d_erased
+ * (sent bytes) -> d_out (P rows of max_payload) and d_out_len (P ints, 0 = lost), the receiver's
+ * reported outputs. */
+int fec_vr_plan_layout(const fec_vr_plan *plan, int64_t *cur_bytes, int64_t *old_bytes);
+int fec_vr_plan_row_offsets(const fec_vr_plan *plan, int64_t *cur_off, int64_t *old_off);
 int fec_vr_encode_batch(fec_vr_plan *plan, const uint8_t *d_payload, const int32_t *d_payload_len,
                         uint8_t *d_cw_cur, int32_t *d_len_cur, uint8_t *d_cw_old, int32_t *d_len_old,
                         void *hip_stream);
@@ -274,16 +280,15 @@ int fec_vr_decode_batch(fec_vr_plan *plan, const uint8_t *d_cw_cur, const uint8_
  * packet Application_Layer_Sender sends (Application_Layer_Sender.cpp:259-269): [seq BE32][T][B][N]
  * [counter_for_start_and_end] + Variable_Rate_FEC_Encoder's frame (Variable_Rate_FEC_Encoder.cpp:
  * 194-217): [size_current BE16][codeword_current (trimmed)][codeword_old (trimmed)]; sizes in
- * d_packet_len.  Receiver (no plan needed): the split of rows packets into the current / old
- * codewords, zero-padded to cw_max bytes (Application_Layer_Receiver.cpp:361-366,
- * Variable_Rate_FEC_Decoder.cpp:2156-2160), header fields to d_header (rows x 5 int32: seq, T, B,
+ * d_packet_len.  Receiver: the split of the plan's sent packets into the current / old codeword
+ * rows of the compact arrays, zero-padded to their row size (Application_Layer_Receiver.cpp:361-366,
+ * Variable_Rate_FEC_Decoder.cpp:2156-2160), header fields to d_header (sent x 5 int32: seq, T, B,
  * N, counter; may be NULL). */
 int fec_vr_frames_batch(fec_vr_plan *plan, const uint8_t *d_cw_cur, const int32_t *d_len_cur,
                         const uint8_t *d_cw_old, const int32_t *d_len_old, uint8_t *d_packets,
                         int64_t stride, int32_t *d_packet_len, void *hip_stream);
-int fec_vr_parse_batch(const uint8_t *d_packets, int64_t stride, const int32_t *d_packet_len, int64_t rows,
-                       int cw_max, uint8_t *d_cw_cur, uint8_t *d_cw_old, int32_t *d_header,
-                       void *hip_stream);
+int fec_vr_parse_batch(fec_vr_plan *plan, const uint8_t *d_packets, int64_t stride, const int32_t *d_packet_len,
+                       uint8_t *d_cw_cur, uint8_t *d_cw_old, int32_t *d_header, void *hip_stream);
 
 /* ---- relay: symbol-wise decode-and-forward (SWDF, RELAYING_TYPE 2) ---------------------------
  * Decoder_Symbol_Wise (src/Decoder_Symbol_Wise.cpp) as the relay and the destination drive it

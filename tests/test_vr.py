@@ -166,6 +166,29 @@ def test_adaptive_mds_mode_and_iid():
     assert v.lost < 2982 and v.fate.min() >= 1
 
 
+def test_compact_row_layout(adaptive):
+    """The frames' codeword arrays are compact (fec_vr.h): every row is its encoder instance's CW
+    rounded to 16 bytes, rows in seq order with no gaps, an old row exactly for the frames that
+    carry an old codeword (Variable_Rate_FEC_Encoder.cpp:194-217), and the arrays are about the
+    codewords' own size instead of sent x cw_max."""
+    v = adaptive
+    co, oo = v.row_offsets()
+    cb, ob = v.layout()
+    assert co[0] == 0 and oo[0] == 0 and co[-1] == cb and oo[-1] == ob
+    cw = {}
+    for T, B, N, first, sw, end in v.encoders.tolist():
+        k = T - N + 1
+        n = k + B
+        c = -(-302 // k) * n
+        cwp = (c + 15) // 16 * 16
+        assert (np.diff(co[first:sw + 1]) == cwp).all()
+        assert (np.diff(oo[sw:end + 1]) == cwp).all()
+    has_old = v.frames[:, 5] >= 0
+    assert ((np.diff(oo) > 0) == has_old).all()
+    assert cb < 0.2 * v.sent * v.cw_max
+    assert (co % 16 == 0).all() and (oo % 16 == 0).all()
+
+
 @pytest.mark.gpu
 def test_gpu_adaptive_schedule_round_trip(adaptive):
     import torch
@@ -196,13 +219,19 @@ def test_gpu_adaptive_codewords_match_fixed_encoders(adaptive):
     v = adaptive
     payload = fill_payload(0, v.sent, 300, 0x5EED)
     cw_cur, len_cur, cw_old, len_old = v.encode(payload)
+    co, oo = v.row_offsets()
+    assert co[-1] <= cw_cur.numel() and oo[-1] <= cw_old.numel()
+    assert (np.diff(co) >= 0).all() and (np.diff(oo) >= 0).all() and (co % 16 == 0).all() and (oo % 16 == 0).all()
     for j in (0, 5, 100, len(v.encoders) - 1):
         T, B, N, first, sw, end = (int(x) for x in v.encoders[j])
         c = Codec(300, T, B, N)
         ref, ref_len = c.encode(payload[first:end].contiguous())
         n1 = sw - first
-        assert bool((cw_cur[first:sw, :c.CW] == ref[:n1]).all()) and bool((len_cur[first:sw] == ref_len[:n1]).all())
-        assert bool((cw_old[sw:end, :c.CW] == ref[n1:]).all()) and bool((len_old[sw:end] == ref_len[n1:]).all())
+        assert int(co[first + 1] - co[first]) == (c.CW + 15) // 16 * 16
+        assert bool((v.rows(cw_cur, co, first, sw, c.CW) == ref[:n1]).all())
+        assert bool((len_cur[first:sw] == ref_len[:n1]).all())
+        assert bool((v.rows(cw_old, oo, sw, end, c.CW) == ref[n1:]).all())
+        assert bool((len_old[sw:end] == ref_len[n1:]).all())
 
 
 @pytest.mark.gpu
@@ -246,7 +275,7 @@ def test_gpu_adaptive_wire_packets_and_outputs_equal_oracle(adaptive, c4):
     assert hashlib.sha256(pk[mask].tobytes()).hexdigest() == c4["wire_sha256"]
     for i, want in enumerate(c4["first_wire_packets"]):
         assert pk[i, :pl[i]].tolist() == want
-    cur, old, hdr = parse_packets(packets, plen, v.cw_max)
+    cur, old, hdr = parse_packets(v, packets, plen)
     assert bool((hdr[:, 0] == torch.arange(v.sent, device="cuda", dtype=torch.int32)).all())
     out, out_len = v.decode(cur, old)
     torch.cuda.synchronize()
