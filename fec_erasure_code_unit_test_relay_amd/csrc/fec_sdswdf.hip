@@ -35,9 +35,12 @@
 
 #include <algorithm>
 #include <cstring>
+#include <map>
 #include <memory>
+#include <mutex>
 #include <new>
 #include <string>
+#include <tuple>
 #include <unordered_map>
 #include <vector>
 
@@ -165,6 +168,20 @@ public:
         for (int i = 0; i < n2_; ++i) m.hdr[i] = static_cast<uint8_t>(header_[n2_ - 1][i]);
         memo_.emplace(key_, m);
         return m.id;
+    }
+
+    // One call of the reference method on caller-held state (the drop-in Decoder_Symbol_Wise,
+    // fec_sw_state_encode): the flags and header rows as the caller's arrays hold them; every slot
+    // counts as holding bytes (an erased slot holds zeros, Variable_Rate_FEC_Decoder.cpp:641-642).
+    // Writes the record and header[n2-1][0..n2) back.
+    void plan_state(const uint8_t* er, int* const* header, uint8_t* rec) {
+        for (int i = 0; i < kSlots; ++i) {
+            er_[i] = er[i] ? 1 : 0;
+            valid_[i] = 1;
+            std::memcpy(header_[i], header[i], sizeof(int) * kHdr);
+        }
+        encode(rec);
+        for (int i = 0; i < n2_; ++i) header[n2_ - 1][i] = header_[n2_ - 1][i];
     }
 
 private:
@@ -371,6 +388,16 @@ public:
         memo_.emplace(key_, m);
         *flag = m.flag;
         return m.id;
+    }
+
+    // One call on caller-held header rows (fec_sw_state_decode): every slot holds bytes (a missing
+    // frame's slot is zeroed by the caller, Variable_Rate_FEC_Decoder.cpp:1710-1711).
+    bool plan_state(int* const* header, uint8_t* rec) {
+        for (int i = 0; i < kSlots; ++i) {
+            valid_[i] = 1;
+            std::memcpy(header_[i], header[i], sizeof(int) * kHdr);
+        }
+        return decode(rec);
     }
 
 private:
@@ -625,7 +652,326 @@ int guarded_sd(F&& f) {
 
 }  // namespace
 
+// ---- per-call relay methods on caller-held state (the drop-in Decoder_Symbol_Wise) -----------
+namespace fec {
+namespace {
+
+constexpr int kSwMaxOut = 32;
+
+// out[o][j] = XOR_p coef[o][p] * src_o[(rbase_o + p) * row_bytes_o + j * bs_o + p] for j < blocks:
+// one GF dot product per output symbol over a diagonal of a packed window (rows = the caller's
+// slots, each packed from its first symbol's byte on).
+struct SwApplyArgs {
+    const uint8_t* win[2];   // packed windows (device view of pinned host memory)
+    int row_bytes[2];
+    int bs[2];               // bytes per code block in a row
+    int nout, nin, blocks;
+    int src[kSwMaxOut];
+    int rbase[kSwMaxOut];
+    const uint8_t* coef;     // [nout][nin]
+    const uint8_t* gf;
+    uint8_t* res;            // [nout][blocks]
+};
+
+__global__ __launch_bounds__(256) void fec_sw_apply_kernel(SwApplyArgs a) {
+    __shared__ uint8_t gexp[512];
+    __shared__ uint8_t glog[256];
+    for (int i = threadIdx.x; i < 512; i += 256) gexp[i] = a.gf[i];
+    for (int i = threadIdx.x; i < 256; i += 256) glog[i] = a.gf[512 + i];
+    __syncthreads();
+    const int total = a.nout * a.blocks;
+    for (int id = blockIdx.x * 256 + threadIdx.x; id < total; id += gridDim.x * 256) {
+        const int o = id / a.blocks, j = id - o * a.blocks;
+        const int sidx = a.src[o];
+        const uint8_t* w = a.win[sidx];
+        const int rb = a.row_bytes[sidx], bs = a.bs[sidx];
+        uint8_t acc = 0;
+        for (int p = 0; p < a.nin; ++p) {
+            const uint8_t c = a.coef[o * a.nin + p];
+            if (!c) continue;
+            const uint8_t v = w[(a.rbase[o] + p) * rb + j * bs + p];
+            if (v) acc ^= gexp[glog[c] + glog[v]];
+        }
+        a.res[id] = acc;
+    }
+}
+
+// Pinned, mapped staging for one call (windows, coefficients, results), GF tables on the device,
+// a stream; calls are serialised (the reference relay is single-threaded).
+struct SwCtx {
+    std::mutex mu;
+    uint8_t* h = nullptr;
+    uint8_t* d = nullptr;
+    size_t cap = 0;
+    uint8_t* d_gf = nullptr;
+    hipStream_t s = nullptr;
+    std::map<std::tuple<int, int, int, int, int>, std::unique_ptr<SdRelayPlanner>> relays;
+    std::map<std::pair<int, int>, std::unique_ptr<SdDestPlanner>> dests;
+    int ensure(size_t bytes) {
+        if (!s && hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) return FEC_ERR_HIP;
+        if (!d_gf) {
+            const Field& F = field();
+            std::vector<uint8_t> gf(F.exp, F.exp + 512);
+            gf.insert(gf.end(), F.log, F.log + 256);
+            if (hipMalloc(&d_gf, gf.size()) != hipSuccess) return FEC_ERR_NOMEM;
+            if (hipMemcpy(d_gf, gf.data(), gf.size(), hipMemcpyHostToDevice) != hipSuccess) return FEC_ERR_HIP;
+        }
+        if (bytes <= cap) return FEC_OK;
+        if (h) (void)hipHostFree(h);
+        h = d = nullptr;
+        cap = 0;
+        const size_t c = std::max<size_t>(bytes, 64 * 1024);
+        if (hipHostMalloc(reinterpret_cast<void**>(&h), c, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess)
+            return FEC_ERR_NOMEM;
+        if (hipHostGetDevicePointer(reinterpret_cast<void**>(&d), h, 0) != hipSuccess) return FEC_ERR_HIP;
+        cap = c;
+        return FEC_OK;
+    }
+};
+SwCtx& sw_ctx() {
+    static SwCtx* c = new SwCtx();  // process lifetime (no teardown order with the HIP runtime)
+    return *c;
+}
+
+// Pack rows [lo, lo+nrows) of `rows` (caller's slots), bytes [off, off + len) of each, into dst.
+void sw_pack(uint8_t* dst, int row_bytes, uint8_t* const* rows, int lo, int nrows, int off, int len) {
+    for (int r = 0; r < nrows; ++r) {
+        std::memcpy(dst + static_cast<size_t>(r) * row_bytes, rows[lo + r] + off, static_cast<size_t>(len));
+        std::memset(dst + static_cast<size_t>(r) * row_bytes + len, 0, static_cast<size_t>(row_bytes - len));
+    }
+}
+
+int sw_run(SwCtx& c, SwApplyArgs& a) {
+    const int total = a.nout * a.blocks;
+    hipLaunchKernelGGL(fec_sw_apply_kernel, dim3(static_cast<unsigned>((total + 255) / 256)), dim3(256), 0, c.s, a);
+    if (hipGetLastError() != hipSuccess) return FEC_ERR_HIP;
+    return hipStreamSynchronize(c.s) == hipSuccess ? FEC_OK : FEC_ERR_HIP;
+}
+
+// The decode rule of a full window (decodeBlock T = n-1, t = 0) on unit vectors, as coefficient rows:
+// position q's value after the decode = row q over the n positions.
+void sw_decode_rows(int k, int n, const uint8_t* er, uint8_t* rows /* n x n */) {
+    std::memset(rows, 0, static_cast<size_t>(n) * n);
+    for (int q = 0; q < n; ++q) rows[q * n + q] = 1;  // received (or erased: the slot holds zeros)
+    uint32_t mask = 0;
+    for (int c = 0; c < n; ++c) mask |= (er[c] ? 1u : 0u) << c;
+    if (__builtin_popcount(mask) == n) return;
+    const auto rules = shared_decode_rules(n - 1, n - k, n - k);
+    const uint8_t* e = rules->entry(n, mask);
+    for (int i = 0; i < k; ++i) {
+        if (!((mask >> i) & 1u) || e[i] == 0xFF) continue;
+        std::memcpy(rows + i * n, e + k + i * n, static_cast<size_t>(n));
+    }
+}
+
+}  // namespace
+}  // namespace fec
+
 extern "C" {
+
+int fec_sw_state_encode(int max_payload, int k, int n, int k2, int n2, int sdbo, uint8_t* const* slots,
+                        const uint8_t* er, int* const* header, uint8_t* cnv, uint8_t* cnsw) {
+    using namespace fec;
+    if (!slots || !er || !header || !cnv || !cnsw || k < 1 || n < k || n > kHdr || k2 != k || n2 < k || n2 > n ||
+        max_payload < 1 || (sdbo != 0 && sdbo != 1))
+        return FEC_ERR_ARG;
+    SwCtx& c = sw_ctx();
+    std::lock_guard<std::mutex> lk(c.mu);
+    return guarded_sd([&] {
+        auto& pl = c.relays[std::make_tuple(k, n, n2, sdbo, max_payload)];
+        if (!pl)
+            pl.reset(new SdRelayPlanner(k, n, n2, sdbo, shared_decode_rules(n - 1, n - k, n - k),
+                                        make_generator(n2 - 1, n2 - k2, n2 - k2)));
+        std::vector<uint8_t> rec(static_cast<size_t>(pl->record_bytes()));
+        pl->plan_state(er, header, rec.data());
+        const int blocks = max_payload / k + 1;  // :184-185
+        const int lo = 2 * kTT - n + 1 - (n2 - k), nrows = 2 * kTT - lo + 1;
+        const int rb = (blocks * n + 3) & ~3;
+        const size_t wbytes = static_cast<size_t>(nrows) * rb, cbytes = static_cast<size_t>(n2) * n;
+        if (int st = c.ensure(wbytes + cbytes + static_cast<size_t>(n2) * blocks + 64)) return st;
+        sw_pack(c.h, rb, slots, lo, nrows, 2, blocks * n);
+        std::memcpy(c.h + wbytes, rec.data() + kHdr, cbytes);
+        SwApplyArgs a{};
+        a.win[0] = a.win[1] = c.d;
+        a.row_bytes[0] = a.row_bytes[1] = rb;
+        a.bs[0] = a.bs[1] = n;
+        a.nout = n2;
+        a.nin = n;
+        a.blocks = blocks;
+        for (int o = 0; o < n2; ++o) {
+            a.src[o] = 0;
+            a.rbase[o] = (k - 1 - o) + 2 * kTT - n + 1 - lo;  // diagonal of symInd = k-1-o
+        }
+        a.coef = c.d + wbytes;
+        a.gf = c.d_gf;
+        a.res = c.d + wbytes + cbytes;
+        if (int st = sw_run(c, a)) return st;
+        const uint8_t* res = c.h + wbytes + cbytes;
+        for (int j = 0; j < blocks; ++j)
+            for (int i = 0; i < n2; ++i) {
+                cnsw[2 + j * n2 + i] = res[i * blocks + j];  // :277-393
+                cnv[2 + j * n2 + i] = res[i * blocks + j];   // :405-409
+            }
+        return static_cast<int>(FEC_OK);
+    });
+}
+
+int fec_sw_state_decode(int max_payload, int k, int n, uint8_t* const* slots, int* const* header, uint8_t* buffer,
+                        int* flag) {
+    using namespace fec;
+    if (!slots || !header || !buffer || k < 1 || n < k || n > kHdr || max_payload < 1) return FEC_ERR_ARG;
+    SwCtx& c = sw_ctx();
+    std::lock_guard<std::mutex> lk(c.mu);
+    return guarded_sd([&] {
+        auto& pl = c.dests[std::make_pair(k, n)];
+        if (!pl) pl.reset(new SdDestPlanner(k, n, shared_decode_rules(n - 1, n - k, n - k)));
+        std::vector<uint8_t> rec(static_cast<size_t>(pl->record_bytes()));
+        const bool fl = pl->plan_state(header, rec.data());
+        if (flag) *flag = fl ? 1 : 0;
+        const int blocks = max_payload / k + 1;  // :494
+        const int lo = 3 * kTT - 1 - (k - 1) - (n - 1), nrows = 3 * kTT - lo;
+        const int rb = (blocks * n + 3) & ~3;
+        const size_t wbytes = static_cast<size_t>(nrows) * rb, cbytes = static_cast<size_t>(k) * n;
+        if (int st = c.ensure(wbytes + cbytes + static_cast<size_t>(k) * blocks + 64)) return st;
+        sw_pack(c.h, rb, slots, lo, nrows, 4, blocks * n);  // symbol (j, q) at slot byte 4 + j*n + q (:504)
+        std::memcpy(c.h + wbytes, rec.data(), cbytes);
+        SwApplyArgs a{};
+        a.win[0] = a.win[1] = c.d;
+        a.row_bytes[0] = a.row_bytes[1] = rb;
+        a.bs[0] = a.bs[1] = n;
+        a.nout = k;
+        a.nin = n;
+        a.blocks = blocks;
+        for (int o = 0; o < k; ++o) {
+            a.src[o] = 0;
+            a.rbase[o] = 3 * kTT - 1 - o - (n - 1) - lo;  // frame t2-o-(n-1-q) for position q
+        }
+        a.coef = c.d + wbytes;
+        a.gf = c.d_gf;
+        a.res = c.d + wbytes + cbytes;
+        if (int st = sw_run(c, a)) return st;
+        const uint8_t* res = c.h + wbytes + cbytes;
+        for (int j = 0; j < blocks; ++j)
+            for (int ks = 0; ks < k; ++ks) buffer[j * n + n - k + ks] = res[ks * blocks + j];  // :537
+        return static_cast<int>(FEC_OK);
+    });
+}
+
+int fec_sw_encode_1(int max_payload, int k, int n, int k2, int n2, uint8_t* const* cv, const uint8_t* er,
+                    uint8_t* const* cnv, uint8_t* cnsw, int* flag) {
+    using namespace fec;
+    if (!cv || !er || !cnv || !cnsw || k < 1 || n < k || n > kMaxRuleN || k2 != k || n2 < k2 || n2 > kSwMaxOut ||
+        max_payload < 1)
+        return FEC_ERR_ARG;
+    SwCtx& c = sw_ctx();
+    std::lock_guard<std::mutex> lk(c.mu);
+    return guarded_sd([&] {
+        const int blocks = max_payload / k + 1;  // :553
+        int cnt = 0;
+        for (int i = 0; i < n; ++i) cnt += er[i] ? 1 : 0;
+        if (flag) *flag = cnt >= n - k + 1 ? 1 : 0;  // :574-576
+        // the decode (:570-573; the n flags of the window reach decodeBlock), then
+        // the k data symbols reversed (:577-578)
+        std::vector<uint8_t> rows(static_cast<size_t>(n) * n);
+        if (cnt > 0 && cnt < n - k + 1) {
+            sw_decode_rows(k, n, er, rows.data());
+        } else {
+            std::memset(rows.data(), 0, rows.size());
+            for (int q = 0; q < n; ++q) rows[q * n + q] = 1;
+        }
+        const int npar = n2 - k2;
+        const int nout = k + npar;
+        const int rbA = (blocks * n + 3) & ~3, rbB = (blocks * n2 + 3) & ~3;
+        const size_t wA = static_cast<size_t>(n) * rbA, wB = static_cast<size_t>(std::max(1, n2 - 1)) * rbB;
+        const int nin = std::max(n, k);
+        const size_t cbytes = static_cast<size_t>(nout) * nin;
+        if (int st = c.ensure(wA + wB + cbytes + static_cast<size_t>(nout) * blocks + 64)) return st;
+        sw_pack(c.h, rbA, cv, 0, n, 2, blocks * n);                     // diagonal d[i] = cv[i][2+j*n+i] (:567)
+        if (n2 > 1) sw_pack(c.h + wA, rbB, cnv, 0, n2 - 1, 2, blocks * n2);  // the relay's earlier frames
+        uint8_t* cf = c.h + wA + wB;
+        std::memset(cf, 0, cbytes);
+        SwApplyArgs a{};
+        a.win[0] = c.d;
+        a.win[1] = c.d + wA;
+        a.row_bytes[0] = rbA;
+        a.row_bytes[1] = rbB;
+        a.bs[0] = n;
+        a.bs[1] = n2;
+        a.nout = nout;
+        a.nin = nin;
+        a.blocks = blocks;
+        for (int i = 0; i < k; ++i) {  // output i: decoded position k-1-i
+            a.src[i] = 0;
+            a.rbase[i] = 0;
+            std::memcpy(cf + i * nin, rows.data() + (k - 1 - i) * n, static_cast<size_t>(n));
+        }
+        // parity position n2-1-delta (:601-613): XOR_m G2[m][n2-1-delta] * cnv[m+delta][2+j*n2+m]
+        const std::vector<uint8_t> G2 = make_generator(n2 - 1, n2 - k2, n2 - k2);
+        for (int delta = 0; delta < npar; ++delta) {
+            const int o = k + delta;
+            a.src[o] = 1;
+            a.rbase[o] = delta;
+            for (int m = 0; m < k; ++m) cf[o * nin + m] = G2[m * n2 + n2 - 1 - delta];
+        }
+        a.coef = c.d + wA + wB;
+        a.gf = c.d_gf;
+        a.res = c.d + wA + wB + cbytes;
+        if (int st = sw_run(c, a)) return st;
+        const uint8_t* res = c.h + wA + wB + cbytes;
+        for (int j = 0; j < blocks; ++j) {
+            for (int i = 0; i < k; ++i) {
+                cnsw[2 + j * n + i] = res[i * blocks + j];
+                cnv[n2 - 1][2 + j * n2 + i] = res[i * blocks + j];  // :593-597 (k_min = k, delta_k = 0)
+            }
+            for (int delta = 0; delta < npar; ++delta) cnv[n2 - 1][2 + j * n2 + n2 - 1 - delta] = res[(k + delta) * blocks + j];
+        }
+        return static_cast<int>(FEC_OK);
+    });
+}
+
+int fec_sw_decode_1(int max_payload, int k, int n, uint8_t* const* cv, const uint8_t* er, uint8_t* buffer, int* flag) {
+    using namespace fec;
+    if (!cv || !er || !buffer || k < 1 || n < k || n > kMaxRuleN || max_payload < 1) return FEC_ERR_ARG;
+    SwCtx& c = sw_ctx();
+    std::lock_guard<std::mutex> lk(c.mu);
+    return guarded_sd([&] {
+        const int blocks = max_payload / k + 1;  // :632
+        int cnt = 0;
+        for (int i = 0; i < n; ++i) cnt += er[i] ? 1 : 0;
+        if (flag) *flag = cnt >= n - k + 1 ? 1 : 0;  // :644-646
+        std::vector<uint8_t> rows(static_cast<size_t>(n) * n);
+        if (cnt > 0 && cnt < n - k + 1) {
+            sw_decode_rows(k, n, er, rows.data());
+        } else {
+            std::memset(rows.data(), 0, rows.size());
+            for (int q = 0; q < n; ++q) rows[q * n + q] = 1;
+        }
+        const int rb = (blocks * n + 3) & ~3;
+        const size_t wbytes = static_cast<size_t>(n) * rb, cbytes = static_cast<size_t>(n) * n;
+        if (int st = c.ensure(wbytes + cbytes + static_cast<size_t>(n) * blocks + 64)) return st;
+        sw_pack(c.h, rb, cv, 0, n, 4, blocks * n);  // position q = cv[q][4 + j*n + q] (:636-639)
+        std::memcpy(c.h + wbytes, rows.data(), cbytes);
+        SwApplyArgs a{};
+        a.win[0] = a.win[1] = c.d;
+        a.row_bytes[0] = a.row_bytes[1] = rb;
+        a.bs[0] = a.bs[1] = n;
+        a.nout = n;
+        a.nin = n;
+        a.blocks = blocks;
+        for (int o = 0; o < n; ++o) {
+            a.src[o] = 0;
+            a.rbase[o] = 0;
+        }
+        a.coef = c.d + wbytes;
+        a.gf = c.d_gf;
+        a.res = c.d + wbytes + cbytes;
+        if (int st = sw_run(c, a)) return st;
+        const uint8_t* res = c.h + wbytes + cbytes;
+        for (int j = 0; j < blocks; ++j)
+            for (int i = 0; i < n; ++i) buffer[j * n + i] = res[(n - 1 - i) * blocks + j];  // :647-649
+        return static_cast<int>(FEC_OK);
+    });
+}
 
 int fec_sdswdf_create(int max_payload, int T1, int N1, int T2, int N2, int sdbo, fec_sdswdf** out) {
     if (!out) return FEC_ERR_ARG;

@@ -354,6 +354,29 @@ int fec_sdswdf_dest_plan(fec_sdswdf *w, const uint8_t *h_erasure, const uint8_t 
                          int32_t *h_plan, uint8_t *h_flag, uint8_t *h_records, int64_t records_cap,
                          int64_t *n_records, int *record_bytes);
 
+/* ---- relay per call: the Decoder_Symbol_Wise methods on caller-held state ---------------------
+ * What siphon::Decoder_Symbol_Wise (fec_amd_dropin.h) calls: one reference method call each, on
+ * the arrays the reference's callers fill (Variable_Rate_FEC_Decoder.cpp:950-1879).  The control
+ * flow runs on the host over the flags and headers; the GF work of all the packet's code blocks is
+ * one GPU launch (its inputs packed into pinned staging, results back), then the call returns.
+ *   fec_sw_state_encode  = symbol_wise_encode_state_dependent (Decoder_Symbol_Wise.cpp:178-432):
+ *     slots = codeword_vector_state_dependent [30] (packet at offset 2), er = its flags [30],
+ *     header [30] rows of 11 ints (row n2-1 written), cnv = codeword_new_vector[n2-1], cnsw =
+ *     codeword_new_symbol_wise;
+ *   fec_sw_state_decode  = symbol_wise_decode_state_dependent (:487-546) into buffer, *flag;
+ *   fec_sw_encode_1      = symbol_wise_encode_1 (:547-619): cv = codeword_vector [T_TOT+1], er =
+ *     temp_erasure_vector, cnv = codeword_new_vector [T_TOT+1] (row n2-1 written);
+ *   fec_sw_decode_1      = symbol_wise_decode_1 (:621-651) into buffer, *flag.
+ * k2 == k; n <= 11 (types 3) / n <= 17 (type 2); sdbo = FLAG_FOR_SDBO. */
+int fec_sw_state_encode(int max_payload, int k, int n, int k2, int n2, int sdbo, uint8_t *const *slots,
+                        const uint8_t *er, int *const *header, uint8_t *cnv, uint8_t *cnsw);
+int fec_sw_state_decode(int max_payload, int k, int n, uint8_t *const *slots, int *const *header, uint8_t *buffer,
+                        int *flag);
+int fec_sw_encode_1(int max_payload, int k, int n, int k2, int n2, uint8_t *const *cv, const uint8_t *er,
+                    uint8_t *const *cnv, uint8_t *cnsw, int *flag);
+int fec_sw_decode_1(int max_payload, int k, int n, uint8_t *const *cv, const uint8_t *er, uint8_t *buffer,
+                    int *flag);
+
 /* ---- erasure patterns (inputs of the decode path; host only, no device needed) ---------------
  * Byte-exact restatements of Erasure_File_Generator (src/Erasure_File_Generator.cpp:25-287): out[i]
  * = 1 if packet i is erased.  Same engine (mt19937), same draw order and the same libstdc++

@@ -11,6 +11,8 @@
 //                                        |   onReceive(codeword,codeword_size,seq,&payload,erasure)
 //   include/Encoder.h / Decoder.h getG() | Encoder::getG(), Decoder::getG() (public members
 //                                        |   FEC_Encoder::encoder / FEC_Decoder::decoder)
+//   include/Decoder_Symbol_Wise.h:15-79  | siphon::Decoder_Symbol_Wise (the relay's symbol-wise
+//                                        |   decode-and-forward, types 2 and 3), GF work on the GPU
 //
 // Semantics kept: one call per seq in increasing order from 0; onTransmit returns a pointer into
 // the caller's Memory_Allocator ring (two allocations per call, like FEC_Encoder.cpp:48,62);
@@ -114,3 +116,67 @@ private:
     int k, n, T, B, N, max_payload, max_blocklength;
     unsigned char* data_with_header;
 };
+
+// ---- relay: Decoder_Symbol_Wise (include/Decoder_Symbol_Wise.h:15-79) --------------------------
+// The same public members (the relay and destination code of Variable_Rate_FEC_Decoder writes the
+// received packets, erasure flags and headers straight into them, Variable_Rate_FEC_Decoder.cpp
+// :1051-1103, :1458-1600, :1703-1870) and methods.  The control flow of every method runs on the
+// host over those members (it depends only on flags and headers); its GF work -- the diagonal
+// decodes (decodeBlock, T = n-1) and re-encodes (encodeBlock, t = k2-1) of all the packet's code
+// blocks -- is one GPU launch per call (fec_sw_* in fec_amd.h).  Differences from the reference,
+// all of them its undefined behaviour: the decodes of symbol_wise_encode_1 /
+// symbol_wise_decode_1 see the window's n erasure flags (not n-1 plus heap bytes), slots are
+// GLOBAL_MAX_SIZE_OF_CODEWORD + 16 bytes (the reference copies that many bytes to offset 2 of a
+// slot of that size), temp_codeword's stale bytes are never forwarded; k2 == k is required (as the
+// reference assumes, Decoder_Symbol_Wise.cpp:185); FLAG_FOR_SDBO is 0 (FEC_Macro.h:50).
+#ifdef T_TOT
+static_assert(T_TOT == 10, "the MI355X relay is built for T_TOT = 10 (FEC_Macro.h:32)");
+#endif
+namespace siphon {
+class Decoder_Symbol_Wise {
+public:
+    static constexpr int kTTot = 10;  // T_TOT
+    explicit Decoder_Symbol_Wise(int max_payload_value);
+    virtual ~Decoder_Symbol_Wise();
+
+    unsigned char* codeword;
+    unsigned char** codeword_vector;
+    unsigned char** codeword_new_vector;
+    unsigned char** codeword_vector_to_transmit;
+    unsigned char** codeword_vector_store_in_burst;
+    unsigned char** codeword_vector_to_trasnmit_store;
+
+    unsigned char** codeword_vector_state_dependent;
+    bool* temp_erasure_vector_state_dependent;
+    int** header;
+
+    unsigned char codeword_new_symbol_wise[30000];
+    bool* temp_erasure_vector;
+    int n2_vector[kTTot + 1];
+    int k2_vector[kTTot + 1];
+
+    Decoder* decoder_current;
+    Encoder* encoder_current;
+
+    void symbol_wise_encode_1(int k, int n, int k2, int n2, bool* flag);
+    void rotate_pointers_and_insert_zero_word(int n, int n2, int temp_size, int codeword_r_d_size_current,
+                                              bool flag_fot_rotate_burst);
+    void push_current_codeword(unsigned char* message, int n, int n2, int temp_size, int codeword_r_d_size_current);
+    void symbol_wise_decode_1(unsigned char* buffer, bool* flag, int k, int n);
+    void symbol_wise_encode_state_dependent(int k, int n, int k2, int n2, bool* flag);
+    void symbol_wise_decode_state_dependent(unsigned char* buffer, bool* flag, int k, int n);
+    void extract_data(unsigned char* buffer, int k, int n, int received_seq, unsigned char* temp_buffer);
+    void copy_elements(Decoder_Symbol_Wise* source, bool encode);
+
+    int max_payload;
+    int k, n;
+    int n2;
+    int codeword_size_vector[kTTot + 1];
+    int store_codeword_size_vector[kTTot + 1];
+    int burst_codeword_size_vector[kTTot + 1];
+
+private:
+    void shift(int n, int n2);
+};
+}  // namespace siphon
+

@@ -640,37 +640,50 @@ void or_swdf_rotate(or_swdf *s, int n, int n2) {
     s->er[n - 1] = 1;
 }
 
-/* symbol_wise_encode_1, Decoder_Symbol_Wise.cpp:547-619.  Returns the flag (too many erasures in
- * the window to decode). */
-int or_swdf_encode_1(or_swdf *s) {
-    const int k = s->k, n = s->n, k2 = s->k, n2 = s->n2;
+/* symbol_wise_encode_1, Decoder_Symbol_Wise.cpp:547-619, over the caller's arrays (the member
+ * layout of include/Decoder_Symbol_Wise.h): cv = codeword_vector (packet at offset 2), er =
+ * temp_erasure_vector, cnv = codeword_new_vector (row n2-1 written), cnsw = codeword_new_symbol_wise.
+ * *flag: too many erasures in the window to decode.  k2 == k (see above).  Returns 0 / -1. */
+int or_sw_encode_1(int max_payload, int k, int n, int k2, int n2, uint8_t *const *cv, const uint8_t *er,
+                   uint8_t *const *cnv, uint8_t *cnsw, int *flag) {
+    if (k < 1 || n < k || n >= OR_MAXN || k2 != k || n2 < k2 || n2 >= OR_MAXN) return -1;
+    uint8_t G1[OR_MAXK * OR_MAXN], G2[OR_MAXK * OR_MAXN];
+    or_gen_G(G1, n - 1, n - k, n - k, k, n);
+    or_gen_G(G2, n2 - 1, n2 - k2, n2 - k2, k2, n2);
     int erasure_counter = 0;
-    for (int i = 0; i < n; i++) erasure_counter += s->er[i] == 1;
-    const int blocks = s->blocks;
+    for (int i = 0; i < n; i++) erasure_counter += er[i] == 1;
+    const int blocks = max_payload / k + 1; /* :553 */
     uint8_t temp_codeword[OR_MAXN], temp_encoded_codeword[OR_MAXN], stam[OR_MAXN];
-    int flag = 0;
+    *flag = 0;
     for (int j = 0; j < blocks; j++) {
-        for (int i = 0; i < n; i++) temp_codeword[i] = s->cv[i][2 + j * n + i]; /* diagonal, :564-568 */
+        for (int i = 0; i < n; i++) temp_codeword[i] = cv[i][2 + j * n + i]; /* diagonal, :564-568 */
         if (erasure_counter > 0 && erasure_counter < n - k + 1) {           /* :570-573 */
-            for (int aa = 0; aa < n; aa++) stam[aa] = s->er[aa];
-            or_decode_block(temp_codeword, s->G1, temp_codeword, stam, k, n, n - 1, 0);
+            for (int aa = 0; aa < n; aa++) stam[aa] = er[aa];
+            or_decode_block(temp_codeword, G1, temp_codeword, stam, k, n, n - 1, 0);
         } else if (erasure_counter >= n - k + 1) {
-            flag = 1;
+            *flag = 1;
         }
-        for (int i = 0; i < k; i++) s->cnsw[2 + j * n + i] = temp_codeword[k - 1 - i]; /* :577-578 */
+        for (int i = 0; i < k; i++) cnsw[2 + j * n + i] = temp_codeword[k - 1 - i]; /* :577-578 */
     }
     /* encoding, :586-618 (k_min = k, delta_k = 0 since k2 == k) */
     for (int j = 0; j < blocks; j++)
-        for (int i = 0; i < k; i++) s->cnv[n2 - 1][2 + j * n2 + i] = s->cnsw[2 + j * n + i];
+        for (int i = 0; i < k; i++) cnv[n2 - 1][2 + j * n2 + i] = cnsw[2 + j * n + i];
     for (int j = 0; j < blocks; j++) {
         for (int delta = 0; delta < n2 - k2; delta++) {
             for (int i = delta; i < k + delta; i++)
-                temp_codeword[i - delta] = s->cnv[i][2 + j * n2 + i - delta]; /* :603-605 */
+                temp_codeword[i - delta] = cnv[i][2 + j * n2 + i - delta]; /* :603-605 */
             memcpy(temp_encoded_codeword, temp_codeword, (size_t)k);
-            or_encode_block(temp_codeword, s->G2, temp_encoded_codeword, k2, n2, k2 - 1);
-            s->cnv[n2 - 1][2 + j * n2 + n2 - 1 - delta] = temp_encoded_codeword[n2 - 1 - delta];
+            or_encode_block(temp_codeword, G2, temp_encoded_codeword, k2, n2, k2 - 1);
+            cnv[n2 - 1][2 + j * n2 + n2 - 1 - delta] = temp_encoded_codeword[n2 - 1 - delta];
         }
     }
+    return 0;
+}
+
+/* symbol_wise_encode_1 on the relay object.  Returns the flag. */
+int or_swdf_encode_1(or_swdf *s) {
+    int flag = 0;
+    or_sw_encode_1(s->L, s->k, s->n, s->k, s->n2, s->cv, s->er, s->cnv, s->cnsw, &flag);
     return flag;
 }
 
@@ -685,26 +698,40 @@ int or_swdf_frame(const or_swdf *s, uint8_t *frame) {
     return size + 2;
 }
 
-/* symbol_wise_decode_1 (Decoder_Symbol_Wise.cpp:621-651) followed by extract_data (:653-665):
- * out receives S*k bytes, the data_with_header the destination recovers.  Returns the flag. */
-int or_swdf_decode_1(or_swdf *s, uint8_t *out) {
-    const int k = s->k, n = s->n;
+/* symbol_wise_decode_1 (Decoder_Symbol_Wise.cpp:621-651) over the caller's arrays: buffer receives
+ * blocks*n bytes (buffer[j*n + i] = decoded position n-1-i).  Returns 0 / -1. */
+int or_sw_decode_1(int max_payload, int k, int n, uint8_t *const *cv, const uint8_t *er, uint8_t *buffer,
+                   int *flag) {
+    if (k < 1 || n < k || n >= OR_MAXN) return -1;
+    uint8_t G1[OR_MAXK * OR_MAXN];
+    or_gen_G(G1, n - 1, n - k, n - k, k, n);
     int erasure_counter = 0;
-    for (int i = 0; i < n; i++) erasure_counter += s->er[i] == 1;
+    for (int i = 0; i < n; i++) erasure_counter += er[i] == 1;
     uint8_t temp_codeword[OR_MAXN], stam[OR_MAXN];
-    uint8_t *buffer = (uint8_t *)calloc((size_t)s->S * n, 1);
-    int flag = 0;
-    for (int j = 0; j < s->blocks; j++) {
+    const int blocks = max_payload / k + 1; /* :632 */
+    *flag = 0;
+    for (int j = 0; j < blocks; j++) {
         for (int i = 0; i < n; i++)
-            temp_codeword[n - 1 - i] = s->cv[n - 1 - i][4 + (j + 1) * n - 1 - i]; /* :636-639 */
+            temp_codeword[n - 1 - i] = cv[n - 1 - i][4 + (j + 1) * n - 1 - i]; /* :636-639 */
         if (erasure_counter > 0 && erasure_counter < n - k + 1) {
-            for (int aa = 0; aa < n; aa++) stam[aa] = s->er[aa];
-            or_decode_block(temp_codeword, s->G1, temp_codeword, stam, k, n, n - 1, 0);
+            for (int aa = 0; aa < n; aa++) stam[aa] = er[aa];
+            or_decode_block(temp_codeword, G1, temp_codeword, stam, k, n, n - 1, 0);
         } else if (erasure_counter >= n - k + 1) {
-            flag = 1;
+            *flag = 1;
         }
         for (int i = 0; i < n; i++) buffer[j * n + i] = temp_codeword[n - 1 - i]; /* :647-649 */
     }
+    return 0;
+}
+
+/* symbol_wise_decode_1 followed by extract_data (:653-665) on the destination object: out receives
+ * S*k bytes, the data_with_header the destination recovers (blocks*k decoded, the rest zero).
+ * Returns the flag. */
+int or_swdf_decode_1(or_swdf *s, uint8_t *out) {
+    const int k = s->k, n = s->n;
+    uint8_t *buffer = (uint8_t *)calloc((size_t)s->S * n, 1);
+    int flag = 0;
+    or_sw_decode_1(s->L, k, n, s->cv, s->er, buffer, &flag);
     int ind = 0; /* extract_data, :653-661 */
     for (int j = 0; j < s->blocks; j++)
         for (int i = 0; i < k; i++) out[ind++] = buffer[j * n + n - k + i];
@@ -894,18 +921,26 @@ void or_sdswdf_dest_push(or_sdswdf *s, const uint8_t *frame, int frame_bytes, in
     s->er[3 * OR_TTOT - 1] = erased ? 1 : 0;
 }
 
-/* symbol_wise_encode_state_dependent, Decoder_Symbol_Wise.cpp:178-432 (k2 == k). */
-void or_sdswdf_encode(or_sdswdf *s, int sdbo) {
-    const int k = s->k, n = s->n, k2 = s->k, n2 = s->n2, TT = OR_TTOT;
-    const int blocks = s->blocks; /* :184-185 */
-    uint8_t *temp_codeword = s->tc;
+/* symbol_wise_encode_state_dependent, Decoder_Symbol_Wise.cpp:178-432 (k2 == k), over the caller's
+ * arrays (the member layout of include/Decoder_Symbol_Wise.h): slots = codeword_vector_state_
+ * dependent [30] (packet at offset 2), er = temp_erasure_vector_state_dependent, header [30] rows
+ * of T_TOT+1 ints, cnv = codeword_new_vector[n2-1], cnsw = codeword_new_symbol_wise.  Returns 0/-1. */
+int or_sw_state_encode(int max_payload, int k, int n, int k2, int n2, int sdbo, uint8_t *const *slots,
+                       const uint8_t *er, int *const *header, uint8_t *cnv, uint8_t *cnsw) {
+    if (k < 1 || n < k || n > OR_SD_HDR || k2 != k || n2 < k || n2 > n) return -1;
+    const int TT = OR_TTOT;
+    const int blocks = max_payload / k + 1; /* :184-185 */
+    uint8_t G1[OR_MAXK * OR_MAXN], G2[OR_MAXK * OR_MAXN];
+    or_gen_G(G1, n - 1, n - k, n - k, k, n);
+    or_gen_G(G2, n2 - 1, n2 - k2, n2 - k2, k2, n2);
+    uint8_t temp_codeword[OR_MAXN];
     uint8_t temp_encoded_codeword[OR_MAXN];
     uint8_t stam[OR_MAXN];
     int tempHeader[OR_MAXN];
     memset(temp_codeword, g_sd_garbage, OR_MAXN);
     /* burst check, :198-231 */
     int is_burst_longer_than_N = 0;
-    for (int aa = 0; aa < n; aa++) stam[aa] = s->er[2 * TT - n + 1 + aa];
+    for (int aa = 0; aa < n; aa++) stam[aa] = er[2 * TT - n + 1 + aa];
     int longest_burst_length = 0, index_end_burst = 0, in_burst = 0, temp_burst_length = 0;
     for (int aa = 0; aa < n; aa++) {
         if (stam[aa] == 1) {
@@ -936,30 +971,30 @@ void or_sdswdf_encode(or_sdswdf *s, int sdbo) {
             for (int i = symInd; i < n; i++) { /* :244-251 */
                 symbolIndex++;
                 if (i < (n < n + symInd ? n : n + symInd))
-                    temp_codeword[symbolIndex] = s->sd[i + 2 * TT - n + 1][2 + j * n + symbolIndex];
+                    temp_codeword[symbolIndex] = slots[i + 2 * TT - n + 1][2 + j * n + symbolIndex];
             }
-            uint8_t *dst = &s->cnsw[2 + j * n2 + index];
+            uint8_t *dst = &cnsw[2 + j * n2 + index];
             if (n - symInd <= k) { /* forward a received symbol of a partial diagonal, :252-301 */
                 int notFoundSym = 1;
                 int symbolIndex2 = -1;
                 for (int i = 0; i < n; i++) tempHeader[i] = 0;
                 for (int i = symbolIndex - (n - k); i >= 1; i--) {
                     symbolIndex2++;
-                    tempHeader[symbolIndex2] = s->header[n2 - i - 1][symbolIndex2];
+                    tempHeader[symbolIndex2] = header[n2 - i - 1][symbolIndex2];
                 }
                 if (is_burst_longer_than_N && index <= k - 1) {
                     *dst = 0;
-                    s->header[n2 - 1][index] = index + 1;
+                    header[n2 - 1][index] = index + 1;
                     notFoundSym = 0;
                 } else {
                     for (int kk = index; kk < n - symInd; kk++) {
-                        if (s->er[kk + symInd + 2 * TT - n + 1] == 0) {
+                        if (er[kk + symInd + 2 * TT - n + 1] == 0) {
                             int notFoundFlag = 1; /* not sent before, :271-275 */
                             for (int jj = 0; jj < kk; jj++)
                                 if (tempHeader[jj] == kk + 1) notFoundFlag = 0;
                             if (notFoundFlag) {
                                 *dst = temp_codeword[kk];
-                                s->header[n2 - 1][index] = kk + 1;
+                                header[n2 - 1][index] = kk + 1;
                                 notFoundSym = 0;
                                 break;
                             }
@@ -978,26 +1013,26 @@ void or_sdswdf_encode(or_sdswdf *s, int sdbo) {
                             }
                         if (notFoundInd) break;
                     }
-                    s->header[n2 - 1][index] = potIndex;
+                    header[n2 - 1][index] = potIndex;
                 }
             } else { /* decode the diagonal and send a symbol not sent yet, :302-395 */
                 if (is_burst_longer_than_N && index <= k - 1) {
                     *dst = 0;
-                    s->header[n2 - 1][index] = index + 1;
+                    header[n2 - 1][index] = index + 1;
                 } else {
                     for (int aa = 0; aa < n2; aa++) stam[aa] = 0;
-                    for (int aa = 0; aa < n - symInd; aa++) stam[aa] = s->er[aa + symInd + 2 * TT - n + 1];
+                    for (int aa = 0; aa < n - symInd; aa++) stam[aa] = er[aa + symInd + 2 * TT - n + 1];
                     for (int aa = n - symInd; aa < n; aa++) stam[aa] = 1;
                     int erasure_count = 0;
                     for (int aa = 0; aa < n; aa++) erasure_count += stam[aa] == 1;
-                    or_decode_block(temp_codeword, s->G1, temp_codeword, stam, k, n, n - 1, 0); /* :322-324 */
+                    or_decode_block(temp_codeword, G1, temp_codeword, stam, k, n, n - 1, 0); /* :322-324 */
                     memcpy(temp_encoded_codeword, temp_codeword, (size_t)n);
-                    or_encode_block(temp_codeword, s->G2, temp_encoded_codeword, k2, n2, k2 - 1); /* :327-328 */
+                    or_encode_block(temp_codeword, G2, temp_encoded_codeword, k2, n2, k2 - 1); /* :327-328 */
                     for (int i = 0; i < n2; i++) tempHeader[i] = 0;
                     int symbolIndex2 = -1;
                     for (int i = symbolIndex - (n - k); i >= 1; i--) {
                         symbolIndex2++;
-                        tempHeader[symbolIndex2] = s->header[n2 - i - 1][symbolIndex2];
+                        tempHeader[symbolIndex2] = header[n2 - i - 1][symbolIndex2];
                     }
                     int not_assinged_val = 1;
                     for (int i = 0; i < n2; i++) { /* :344-374 */
@@ -1010,7 +1045,7 @@ void or_sdswdf_encode(or_sdswdf *s, int sdbo) {
                         if (notFoundFlag) {
                             if (is_burst_longer_than_N || erasure_count <= n - k) {
                                 *dst = temp_encoded_codeword[i];
-                                s->header[n2 - 1][index] = i + 1;
+                                header[n2 - 1][index] = i + 1;
                                 not_assinged_val = 0;
                                 break;
                             } else if (stam[i] == 0) { /* didn't decode: forward, :361-371 */
@@ -1018,7 +1053,7 @@ void or_sdswdf_encode(or_sdswdf *s, int sdbo) {
                                     *dst = temp_encoded_codeword[i];
                                 else
                                     *dst = temp_codeword[i];
-                                s->header[n2 - 1][index] = i + 1;
+                                header[n2 - 1][index] = i + 1;
                                 not_assinged_val = 0;
                                 break;
                             }
@@ -1034,7 +1069,7 @@ void or_sdswdf_encode(or_sdswdf *s, int sdbo) {
                                     break;
                                 }
                             if (notFoundFlag) {
-                                s->header[n2 - 1][index] = i + 1;
+                                header[n2 - 1][index] = i + 1;
                                 break;
                             }
                         }
@@ -1044,7 +1079,14 @@ void or_sdswdf_encode(or_sdswdf *s, int sdbo) {
         }
     }
     for (int j = 0; j < blocks; j++) /* :405-409 */
-        for (int i = 0; i < n2; i++) s->cnv[2 + j * n2 + i] = s->cnsw[2 + j * n2 + i];
+        for (int i = 0; i < n2; i++) cnv[2 + j * n2 + i] = cnsw[2 + j * n2 + i];
+    return 0;
+}
+
+void or_sdswdf_encode(or_sdswdf *s, int sdbo) {
+    int *rows[OR_SD_SLOTS];
+    for (int i = 0; i < OR_SD_SLOTS; i++) rows[i] = s->header[i];
+    or_sw_state_encode(s->L, s->k, s->n, s->k, s->n2, sdbo, s->sd, s->er, rows, s->cnv, s->cnsw);
 }
 
 /* The relay's frame (Variable_Rate_FEC_Decoder.cpp:1473-1489, :654-669): [codeword_r_d_size BE16]
@@ -1059,19 +1101,23 @@ int or_sdswdf_frame(const or_sdswdf *s, uint8_t *frame) {
     return 2 + OR_SD_HDR + size;
 }
 
-/* symbol_wise_decode_state_dependent (:487-546) followed by extract_data (:653-661): out
- * receives S*k bytes (blocks*k decoded, the rest zero).  Returns the flag. */
-int or_sdswdf_decode(or_sdswdf *s, uint8_t *out) {
-    const int k = s->k, n = s->n, TT = OR_TTOT;
+/* symbol_wise_decode_state_dependent (:487-546) over the caller's arrays: buffer[j*n + n-k+ks]
+ * for j < blocks, ks < k; *flag.  Returns 0 / -1. */
+int or_sw_state_decode(int max_payload, int k, int n, uint8_t *const *slots, int *const *header, uint8_t *buffer,
+                       int *flag) {
+    if (k < 1 || n < k || n > OR_SD_HDR) return -1;
+    const int TT = OR_TTOT;
+    const int blocks = max_payload / k + 1; /* :494 */
+    uint8_t G1[OR_MAXK * OR_MAXN];
+    or_gen_G(G1, n - 1, n - k, n - k, k, n);
     uint8_t temp_codeword[OR_MAXN], temp_temp_codeword[OR_MAXN], stam[OR_MAXN];
     int tempHeader[OR_MAXN];
-    uint8_t *buffer = (uint8_t *)calloc((size_t)s->blocks * n, 1);
-    int flag = 0;
-    for (int j = 0; j < s->blocks; j++) {
+    *flag = 0;
+    for (int j = 0; j < blocks; j++) {
         for (int k_shift = 0; k_shift < k; k_shift++) {
             for (int i = 0; i < n; i++) { /* :501-508 */
-                temp_codeword[n - 1 - i] = s->sd[3 * TT - k_shift - i - 1][4 + (j + 1) * n - 1 - i];
-                tempHeader[n - 1 - i] = s->header[3 * TT - k_shift - i - 1][n - 1 - i];
+                temp_codeword[n - 1 - i] = slots[3 * TT - k_shift - i - 1][4 + (j + 1) * n - 1 - i];
+                tempHeader[n - 1 - i] = header[3 * TT - k_shift - i - 1][n - 1 - i];
             }
             for (int i = 0; i < n; i++) temp_temp_codeword[i] = 0; /* reorder by header, :510-518 */
             for (int i = 0; i < n; i++)
@@ -1083,13 +1129,25 @@ int or_sdswdf_decode(or_sdswdf *s, uint8_t *out) {
                 for (int aa = 0; aa < n; aa++) stam[aa] = 1;
                 for (int aa = 0; aa < n; aa++)
                     if (tempHeader[aa] != 0 && tempHeader[aa] < n + 1) stam[tempHeader[aa] - 1] = 0;
-                or_decode_block(temp_codeword, s->G1, temp_codeword, stam, k, n, n - 1, 0);
+                or_decode_block(temp_codeword, G1, temp_codeword, stam, k, n, n - 1, 0);
             } else if (erasure_counter >= n - k + 1) {
-                flag = 1;
+                *flag = 1;
             }
             buffer[j * n + n - k + k_shift] = temp_codeword[k_shift]; /* :537 */
         }
     }
+    return 0;
+}
+
+/* symbol_wise_decode_state_dependent followed by extract_data (:653-661) on the destination
+ * object: out receives S*k bytes (blocks*k decoded, the rest zero).  Returns the flag. */
+int or_sdswdf_decode(or_sdswdf *s, uint8_t *out) {
+    const int k = s->k, n = s->n;
+    int *rows[OR_SD_SLOTS];
+    for (int i = 0; i < OR_SD_SLOTS; i++) rows[i] = s->header[i];
+    uint8_t *buffer = (uint8_t *)calloc((size_t)s->blocks * n, 1);
+    int flag = 0;
+    or_sw_state_decode(s->L, k, n, s->sd, rows, buffer, &flag);
     int ind = 0; /* extract_data, :653-661 */
     for (int j = 0; j < s->blocks; j++)
         for (int i = 0; i < k; i++) out[ind++] = buffer[j * n + n - k + i];

@@ -96,6 +96,18 @@ int or_sdswdf_run(int max_payload, int T1, int N1, int T2, int N2, int64_t P, co
                   const uint8_t *e2, uint64_t seed, int sdbo, uint8_t *frames, uint8_t *dest_out,
                   uint8_t *dest_flag);
 
+/* The four Decoder_Symbol_Wise methods over the caller's arrays (the member layout of
+ * include/Decoder_Symbol_Wise.h), with the signatures of the product's per-call C ABI (fec_sw_* in
+ * include/fec_amd.h), so that a relay driver can run over either. */
+int or_sw_state_encode(int max_payload, int k, int n, int k2, int n2, int sdbo, uint8_t *const *slots,
+                       const uint8_t *er, int *const *header, uint8_t *cnv, uint8_t *cnsw);
+int or_sw_state_decode(int max_payload, int k, int n, uint8_t *const *slots, int *const *header, uint8_t *buffer,
+                       int *flag);
+int or_sw_encode_1(int max_payload, int k, int n, int k2, int n2, uint8_t *const *cv, const uint8_t *er,
+                   uint8_t *const *cnv, uint8_t *cnsw, int *flag);
+int or_sw_decode_1(int max_payload, int k, int n, uint8_t *const *cv, const uint8_t *er, uint8_t *buffer,
+                   int *flag);
+
 /* The adaptive P2P loop (BASELINE config 4), reference-structured on real bytes: returns the
  * packets lost among 0..P-1; out_len[P] (0 = lost), out_data (P*max_payload or NULL); packets
  * (packets_cap bytes, or NULL) receives the first max_sent P2P wire packets [seq BE32][T][B][N]

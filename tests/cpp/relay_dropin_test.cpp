@@ -1,0 +1,424 @@
+// Relay drop-in check: siphon::Decoder_Symbol_Wise (include/fec_amd_dropin.h: host control flow,
+// GF work on the GPU) driven the way Variable_Rate_FEC_Decoder drives the reference's relay and
+// destination (src/Variable_Rate_FEC_Decoder.cpp:950-1879, one relay frame per seq), for
+// RELAYING_TYPE 2 (symbol_wise_encode_1 / decode_1) and 3 (the state-dependent pair), against
+//   (1) the oracle's whole fixed-rate chains (or_swdf_run / or_sdswdf_run), and
+//   (2) the same driver over OracleSW: the reference's Decoder_Symbol_Wise restated over its member
+//       arrays with the oracle's methods (or_sw_*), including a double-coding stretch (two live
+//       objects per node, the frame [BE16 size][cur][old], copy_elements at its end,
+//       Variable_Rate_FEC_Decoder.cpp:1423-1600, :1772-1873).
+// Frames, destination outputs and loss flags must be equal per seq.
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <vector>
+
+#include "fec_amd_dropin.h"
+#include "../../oracle/fec_oracle.h"
+
+namespace {
+constexpr int TT = 10;            // T_TOT
+constexpr int GMAX = 20000;       // GLOBAL_MAX_SIZE_OF_CODEWORD
+constexpr int SLOT = GMAX + 16;
+constexpr int L = 300;
+
+// The reference object restated over its members with the oracle's methods (test side only).
+struct OracleSW {
+    int max_payload;
+    unsigned char** codeword_vector;
+    unsigned char** codeword_new_vector;
+    unsigned char** codeword_vector_to_transmit;
+    unsigned char** codeword_vector_state_dependent;
+    bool* temp_erasure_vector_state_dependent;
+    int** header;
+    unsigned char codeword_new_symbol_wise[30000];
+    bool* temp_erasure_vector;
+    Decoder* decoder_current = nullptr;
+    Encoder* encoder_current = nullptr;
+    static unsigned char** slots(int c) {
+        unsigned char** v = static_cast<unsigned char**>(std::calloc(c, sizeof(void*)));
+        for (int i = 0; i < c; ++i) v[i] = static_cast<unsigned char*>(std::calloc(SLOT, 1));
+        return v;
+    }
+    explicit OracleSW(int mp) : max_payload(mp) {
+        codeword_vector = slots(TT + 1);
+        codeword_new_vector = slots(TT + 1);
+        codeword_vector_to_transmit = slots(TT + 1);
+        codeword_vector_state_dependent = slots(3 * TT);
+        temp_erasure_vector = static_cast<bool*>(std::calloc(TT + 1, 1));
+        temp_erasure_vector_state_dependent = static_cast<bool*>(std::calloc(3 * TT, 1));
+        header = static_cast<int**>(std::calloc(3 * TT, sizeof(int*)));
+        for (int i = 0; i < 3 * TT; ++i) {
+            header[i] = static_cast<int*>(std::calloc(TT + 1, sizeof(int)));
+            for (int j = 0; j < TT + 1; ++j) header[i][j] = j + 1;
+        }
+        std::memset(codeword_new_symbol_wise, 0, sizeof(codeword_new_symbol_wise));
+    }
+    ~OracleSW() {
+        for (int i = 0; i < TT + 1; ++i) {
+            std::free(codeword_vector[i]);
+            std::free(codeword_new_vector[i]);
+            std::free(codeword_vector_to_transmit[i]);
+        }
+        for (int i = 0; i < 3 * TT; ++i) {
+            std::free(codeword_vector_state_dependent[i]);
+            std::free(header[i]);
+        }
+        std::free(codeword_vector);
+        std::free(codeword_new_vector);
+        std::free(codeword_vector_to_transmit);
+        std::free(codeword_vector_state_dependent);
+        std::free(header);
+        std::free(temp_erasure_vector);
+        std::free(temp_erasure_vector_state_dependent);
+        delete decoder_current;
+        delete encoder_current;
+    }
+    void shift(int n, int n2) {  // Decoder_Symbol_Wise.cpp:120-135
+        for (int i = 0; i < n - 1; ++i) {
+            std::memcpy(codeword_vector[i], codeword_vector[i + 1], GMAX);
+            temp_erasure_vector[i] = temp_erasure_vector[i + 1];
+        }
+        for (int i = 0; i < n2 - 1; ++i) {
+            std::memcpy(codeword_new_vector[i], codeword_new_vector[i + 1], GMAX);
+            std::memcpy(codeword_vector_to_transmit[i], codeword_vector_to_transmit[i + 1], GMAX);
+        }
+        for (int i = 0; i < 3 * TT - 1; ++i) {
+            std::memcpy(codeword_vector_state_dependent[i], codeword_vector_state_dependent[i + 1], GMAX);
+            std::memcpy(header[i], header[i + 1], sizeof(int) * TT);
+            temp_erasure_vector_state_dependent[i] = temp_erasure_vector_state_dependent[i + 1];
+        }
+    }
+    void push_current_codeword(unsigned char* m, int n, int n2, int, int) {
+        shift(n, n2);
+        std::memcpy(&codeword_vector[n - 1][2], m, GMAX);
+        temp_erasure_vector[n - 1] = false;
+    }
+    void rotate_pointers_and_insert_zero_word(int n, int n2, int, int, bool) {
+        shift(n, n2);
+        std::memset(codeword_vector[n - 1], 0, GMAX);
+        temp_erasure_vector[n - 1] = true;
+    }
+    void symbol_wise_encode_1(int k, int n, int k2, int n2, bool* flag) {
+        int f = 0;
+        or_sw_encode_1(max_payload, k, n, k2, n2, codeword_vector, reinterpret_cast<uint8_t*>(temp_erasure_vector),
+                       codeword_new_vector, codeword_new_symbol_wise, &f);
+        *flag = f != 0;
+    }
+    void symbol_wise_decode_1(unsigned char* buffer, bool* flag, int k, int n) {
+        int f = 0;
+        or_sw_decode_1(max_payload, k, n, codeword_vector, reinterpret_cast<uint8_t*>(temp_erasure_vector), buffer, &f);
+        *flag = f != 0;
+    }
+    void symbol_wise_encode_state_dependent(int k, int n, int k2, int n2, bool* flag) {
+        *flag = false;
+        or_sw_state_encode(max_payload, k, n, k2, n2, 0, codeword_vector_state_dependent,
+                           reinterpret_cast<uint8_t*>(temp_erasure_vector_state_dependent), header,
+                           codeword_new_vector[n2 - 1], codeword_new_symbol_wise);
+    }
+    void symbol_wise_decode_state_dependent(unsigned char* buffer, bool* flag, int k, int n) {
+        int f = 0;
+        or_sw_state_decode(max_payload, k, n, codeword_vector_state_dependent, header, buffer, &f);
+        *flag = f != 0;
+    }
+    void extract_data(unsigned char* buffer, int k, int n, int, unsigned char* temp_buffer) {
+        const int blocks = max_payload / k + 1;
+        int ind = 0;
+        for (int j = 0; j < blocks; ++j)
+            for (int i = 0; i < k; ++i) temp_buffer[ind++] = buffer[j * n + n - k + i];
+    }
+    void copy_elements(OracleSW* s, bool encode) {  // :88-117
+        for (int i = 0; i < TT + 1; ++i) {
+            std::memcpy(codeword_vector[i], s->codeword_vector[i], GMAX);
+            std::memcpy(codeword_new_vector[i], s->codeword_new_vector[i], GMAX);
+            std::memcpy(codeword_vector_to_transmit[i], s->codeword_vector_to_transmit[i], GMAX);
+            temp_erasure_vector[i] = s->temp_erasure_vector[i];
+        }
+        for (int i = 0; i < 3 * TT; ++i) {
+            std::memcpy(codeword_vector_state_dependent[i], s->codeword_vector_state_dependent[i], GMAX);
+            std::memcpy(header[i], s->header[i], sizeof(int) * (TT + 1));
+            temp_erasure_vector_state_dependent[i] = s->temp_erasure_vector_state_dependent[i];
+        }
+        delete decoder_current;
+        decoder_current = new Decoder(s->decoder_current->T, s->decoder_current->B, s->decoder_current->N, s->max_payload);
+        if (encode) {
+            delete encoder_current;
+            encoder_current = new Encoder(s->encoder_current->T, s->encoder_current->B, s->encoder_current->N,
+                                          s->max_payload);
+        }
+    }
+};
+
+// A relayed code: the source's (n, k) on hop 1, the relay's (n2, k) on hop 2 (T2 = n2 - 1 <= T).
+struct Code {
+    int k, n, n2, S, CW;
+};
+Code code(int T, int N, int T2 = -1) {
+    Code c{T - N + 1, T + 1, (T2 < 0 ? T : T2) + 1, 0, 0};
+    c.S = (L + 2 + c.k - 1) / c.k;
+    c.CW = c.S * c.n;
+    return c;
+}
+int rd_size(const Code& c) { return (c.S + 1) * c.n2; }  // codeword_r_d_size (:997-999), k2 == k
+
+// One node's relay step for one code (an object, a codeword or nullptr = erased): the object calls
+// of :1051-1062 / :1459-1467, then the code's part of the frame appended to `frame`.
+template <class SW>
+void relay_step(SW* w, int R, const Code& c, const unsigned char* cw, std::vector<unsigned char>& frame) {
+    static std::vector<unsigned char> buf(SLOT);
+    bool flag = false;
+    if (cw) {
+        std::memset(buf.data(), 0, SLOT);
+        std::memcpy(buf.data(), cw, c.CW);
+        w->push_current_codeword(buf.data(), c.n, c.n2, c.CW, rd_size(c));
+        if (R == 3) {
+            std::memcpy(&w->codeword_vector_state_dependent[2 * TT][2], buf.data(), GMAX);
+            w->temp_erasure_vector_state_dependent[2 * TT] = false;
+        }
+    } else {
+        w->rotate_pointers_and_insert_zero_word(c.n, c.n2, 0, 0, true);
+        if (R == 3) {
+            std::memset(w->codeword_vector_state_dependent[2 * TT], 0, GMAX);
+            w->temp_erasure_vector_state_dependent[2 * TT] = true;
+        }
+    }
+    if (R == 3) w->symbol_wise_encode_state_dependent(c.k, c.n, c.k, c.n2, &flag);
+    else w->symbol_wise_encode_1(c.k, c.n, c.k, c.n2, &flag);
+    if (R == 3)
+        for (int a = 0; a < TT + 1; ++a) frame.push_back(static_cast<unsigned char>(w->header[c.n2 - 1][a]));
+    const unsigned char* row = w->codeword_new_vector[c.n2 - 1];
+    frame.insert(frame.end(), row, row + rd_size(c));
+}
+
+// The destination's step for one code (:1703-1721 missing, :1798-1815 received): part = the
+// code's frame part ([header 11]? [codeword_new_vector row]) or nullptr; out = blocks*k bytes.
+template <class SW>
+int dest_step(SW* d, int R, const Code& c, const unsigned char* part, unsigned char* out) {
+    static std::vector<unsigned char> buf(SLOT), buffer(30000);
+    bool flag = false;
+    if (part) {
+        const unsigned char* cw = part + (R == 3 ? TT + 1 : 0);
+        std::memset(buf.data(), 0, SLOT);
+        std::memcpy(buf.data(), cw, rd_size(c));
+        d->push_current_codeword(buf.data(), c.n2, 0, rd_size(c), 0);
+        if (R == 3) {
+            for (int i = 0; i < TT + 1; ++i) d->header[3 * TT - 1][i] = part[i];
+            std::memcpy(&d->codeword_vector_state_dependent[3 * TT - 1][2], buf.data(), GMAX);
+            d->temp_erasure_vector_state_dependent[3 * TT - 1] = false;
+        }
+    } else {
+        d->rotate_pointers_and_insert_zero_word(c.n2, 0, 0, 0, false);
+        if (R == 3) {
+            for (int i = 0; i < TT + 1; ++i) d->header[3 * TT - 1][i] = 0;
+            std::memset(d->codeword_vector_state_dependent[3 * TT - 1], 0, GMAX);
+            d->temp_erasure_vector_state_dependent[3 * TT - 1] = true;
+        }
+    }
+    if (R == 3) d->symbol_wise_decode_state_dependent(buffer.data(), &flag, c.k, c.n2);
+    else d->symbol_wise_decode_1(buffer.data(), &flag, c.k, c.n2);
+    d->extract_data(buffer.data(), c.k, c.n2, 0, out);
+    return flag ? 1 : 0;
+}
+
+struct Trace {
+    std::vector<std::vector<unsigned char>> frames;
+    std::vector<std::vector<unsigned char>> outs;
+    std::vector<int> flags;
+};
+
+// The chain: source encoders (the old code (T1,N1) from seq 0, a new one (T2,N2) from seq s0 when
+// s0 >= 0: both run for T_TOT+1 packets, the relay double codes them, then the new one alone),
+// hop-1 erasures e1 (both codewords of a seq are lost together), the relay, hop-2 erasures e2,
+// the destination.  Relay frame = [size_cur BE16][cur part][old part] (:1530-1571).
+template <class SW>
+Trace chain(int R, int T1, int N1, int T2, int N2, int s0, int Th2, int P, const std::vector<unsigned char>& e1,
+            const std::vector<unsigned char>& e2) {
+    const Code c_old = code(T1, N1, Th2), c_new = code(T2, N2);
+    or_encoder* eo = or_encoder_new(L, T1, N1, N1);
+    or_encoder* en = s0 >= 0 ? or_encoder_new(L, T2, N2, N2) : nullptr;
+    SW* relay = new SW(L);
+    SW* relay_new = nullptr;
+    SW* dest = new SW(L);
+    SW* dest_new = nullptr;
+    relay->decoder_current = new Decoder(c_old.n - 1, c_old.n - c_old.k, c_old.n - c_old.k, L);
+    relay->encoder_current = new Encoder(c_old.n - 1, c_old.n - c_old.k, c_old.n - c_old.k, L);
+    dest->decoder_current = new Decoder(c_old.n - 1, c_old.n - c_old.k, c_old.n - c_old.k, L);
+    Code cur = c_old;
+    const int end_dc = s0 + TT;  // seq_end_double_coding = start + T_TOT + 1 - 1 (:1438)
+    std::vector<unsigned char> payload(L), cwo(8192), cwn(8192);
+    Trace tr;
+    for (int t = 0; t < P; ++t) {
+        or_fill_payload(payload.data(), t, 1, L, 0x5EED);
+        const bool dc = s0 >= 0 && t >= s0 && t <= end_dc;
+        const bool only_new = s0 >= 0 && t > end_dc;
+        if (!only_new) or_encoder_transmit(eo, payload.data(), L, t, cwo.data());
+        if (dc || only_new) or_encoder_transmit(en, payload.data(), L, t, cwn.data());
+        if (s0 >= 0 && t == s0) {  // a new relay object for the new code (:1437-1456)
+            relay_new = new SW(L);
+            relay_new->decoder_current = new Decoder(c_new.n - 1, c_new.n - c_new.k, c_new.n - c_new.k, L);
+            relay_new->encoder_current = new Encoder(c_new.n - 1, c_new.n - c_new.k, c_new.n - c_new.k, L);
+            dest_new = new SW(L);
+            dest_new->decoder_current = new Decoder(c_new.n - 1, c_new.n - c_new.k, c_new.n - c_new.k, L);
+        }
+        if (s0 >= 0 && t == end_dc + 1) {  // end of double coding: the new objects take over (:1423-1433)
+            relay->copy_elements(relay_new, true);
+            dest->copy_elements(dest_new, false);
+            delete relay_new;
+            delete dest_new;
+            relay_new = dest_new = nullptr;
+            cur = c_new;
+        }
+        const bool lost1 = e1[t] != 0;
+        std::vector<unsigned char> frame(2);
+        int size_cur;
+        if (dc) {  // :1502-1571: the old code's object gets the old codeword, the new one the new
+            std::vector<unsigned char> pn, po;
+            relay_step(relay_new, R, c_new, lost1 ? nullptr : cwn.data(), pn);
+            relay_step(relay, R, c_old, lost1 ? nullptr : cwo.data(), po);
+            size_cur = rd_size(c_new);
+            frame.insert(frame.end(), pn.begin(), pn.end());
+            frame.insert(frame.end(), po.begin(), po.end());
+        } else {
+            std::vector<unsigned char> pc;
+            relay_step(relay, R, cur, lost1 ? nullptr : (only_new ? cwn.data() : cwo.data()), pc);
+            size_cur = rd_size(cur);
+            frame.insert(frame.end(), pc.begin(), pc.end());
+        }
+        frame[0] = static_cast<unsigned char>(size_cur / 256);
+        frame[1] = static_cast<unsigned char>(size_cur % 256);
+        // destination: during double coding the old object decodes the old part and reports, the
+        // new one decodes the new part (:1823-1873)
+        const bool lost2 = e2[t] != 0;
+        const int hdr = R == 3 ? TT + 1 : 0;
+        std::vector<unsigned char> out(static_cast<size_t>(L + 32), 0);
+        int flag;
+        if (dc) {
+            const unsigned char* pn = lost2 ? nullptr : frame.data() + 2;
+            const unsigned char* po = lost2 ? nullptr : frame.data() + 2 + hdr + size_cur;
+            flag = dest_step(dest, R, c_old, po, out.data());
+            std::vector<unsigned char> tmp(static_cast<size_t>(L + 32), 0);
+            dest_step(dest_new, R, c_new, pn, tmp.data());
+        } else {
+            flag = dest_step(dest, R, cur, lost2 ? nullptr : frame.data() + 2, out.data());
+        }
+        tr.frames.push_back(frame);
+        tr.outs.push_back(out);
+        tr.flags.push_back(flag);
+    }
+    or_encoder_free(eo);
+    if (en) or_encoder_free(en);
+    delete relay;
+    delete relay_new;
+    delete dest;
+    delete dest_new;
+    return tr;
+}
+
+std::vector<unsigned char> pattern(int P, unsigned seed, int per_mille, int burst_every) {
+    std::vector<unsigned char> e(P, 0);
+    unsigned s = seed;
+    for (int t = 0; t < P; ++t) {
+        s = s * 1103515245u + 12345u;
+        if (static_cast<int>((s >> 16) % 1000) < per_mille) e[t] = 1;
+        if (burst_every && t % burst_every >= 40 && t % burst_every < 43) e[t] = 1;
+    }
+    return e;
+}
+
+int compare(const char* what, const Trace& a, const Trace& b, int P) {
+    for (int t = 0; t < P; ++t) {
+        if (a.frames[t] != b.frames[t]) {
+            std::printf("%s: frame %d differs (%zu vs %zu bytes)\n", what, t, a.frames[t].size(), b.frames[t].size());
+            return 1;
+        }
+        if (a.outs[t] != b.outs[t] || a.flags[t] != b.flags[t]) {
+            std::printf("%s: destination output %d differs (flag %d vs %d)\n", what, t, a.flags[t], b.flags[t]);
+            return 1;
+        }
+    }
+    return 0;
+}
+
+// (1) a fixed-rate chain over SW against the oracle's own chain functions
+template <class SW>
+int fixed_vs_oracle_run(int R, int T1, int N1, int T2, int N2, int P) {
+    const auto e1 = pattern(P, 7, 30, 173), e2 = pattern(P, 11, 25, 211);
+    const Trace d = chain<SW>(R, T1, N1, T1, N1, -1, T2, P, e1, e2);
+    const Code c = code(T1, N1, T2);
+    const int F = 2 + (R == 3 ? TT + 1 : 0) + rd_size(c);
+    std::vector<unsigned char> frames(static_cast<size_t>(P) * F), out(static_cast<size_t>(P) * c.S * c.k),
+        rf(P), df(P);
+    const int st = R == 3 ? or_sdswdf_run(L, T1, N1, T2, N2, P, e1.data(), e2.data(), 0x5EED, 0, frames.data(),
+                                          out.data(), df.data())
+                          : or_swdf_run(L, T1, N1, T2, N2, P, e1.data(), e2.data(), 0x5EED, frames.data(), rf.data(),
+                                        out.data(), df.data());
+    if (st) {
+        std::printf("oracle chain failed\n");
+        return 1;
+    }
+    const int blocks = L / c.k + 1;
+    for (int t = 0; t < P; ++t) {
+        if (d.frames[t].size() != static_cast<size_t>(F) || std::memcmp(d.frames[t].data(), &frames[size_t(t) * F], F)) {
+            std::printf("type %d (%d,%d): frame %d differs from the oracle chain\n", R, T1, N1, t);
+            return 1;
+        }
+        if (std::memcmp(d.outs[t].data(), &out[size_t(t) * c.S * c.k], blocks * c.k) || d.flags[t] != df[t]) {
+            std::printf("type %d (%d,%d): destination %d differs from the oracle chain\n", R, T1, N1, t);
+            return 1;
+        }
+    }
+    std::printf("type %d (%d,%d)->(%d,%d) fixed rate: %d seqs equal to the oracle chain\n", R, T1, N1, T2, N2, P);
+    return 0;
+}
+
+#ifndef RELAY_ORACLE_ONLY
+// (2) double coding: the same driver over the drop-in and over OracleSW
+int double_coding(int R, int T1, int N1, int T2, int N2, int s0, int P) {
+    const auto e1 = pattern(P, 5, 20, 149), e2 = pattern(P, 9, 20, 0);
+    const Trace d = chain<siphon::Decoder_Symbol_Wise>(R, T1, N1, T2, N2, s0, -1, P, e1, e2);
+    const Trace o = chain<OracleSW>(R, T1, N1, T2, N2, s0, -1, P, e1, e2);
+    char what[96];
+    std::snprintf(what, sizeof what, "type %d (%d,%d)=>(%d,%d) at %d", R, T1, N1, T2, N2, s0);
+    if (compare(what, d, o, P)) return 1;
+    int good = 0;
+    for (int t = 0; t < P; ++t) good += d.flags[t] == 0;
+    std::printf("%s: %d seqs equal (double coding %d..%d), %d unflagged\n", what, P, s0, s0 + TT, good);
+    return 0;
+}
+#endif
+}  // namespace
+
+#ifdef RELAY_ORACLE_ONLY
+// CPU build (tests/test_sdswdf.py): the driver over OracleSW against the oracle's chains, which
+// checks the driver and the or_sw_* methods without a GPU.
+int main() {
+    int rc = 0;
+    rc |= fixed_vs_oracle_run<OracleSW>(3, 10, 3, 10, 3, 600);
+    rc |= fixed_vs_oracle_run<OracleSW>(3, 10, 5, 8, 3, 400);
+    rc |= fixed_vs_oracle_run<OracleSW>(2, 10, 3, 10, 3, 600);
+    rc |= fixed_vs_oracle_run<OracleSW>(2, 10, 1, 10, 1, 400);
+    for (int R : {2, 3}) {  // the double-coding driver runs (memory-clean under -fsanitize) over OracleSW
+        const Trace o = chain<OracleSW>(R, 10, 3, 10, 5, 200, -1, 420, pattern(420, 5, 20, 149), pattern(420, 9, 20, 0));
+        int good = 0;
+        for (int f : o.flags) good += f == 0;
+        std::printf("type %d double coding over OracleSW: %d of 420 unflagged\n", R, good);
+        if (good < 300) rc = 1;
+    }
+    if (rc == 0) std::printf("RELAY ORACLE DRIVER OK\n");
+    return rc;
+}
+#else
+int main() {
+    using DSW = siphon::Decoder_Symbol_Wise;
+    int rc = 0;
+    rc |= fixed_vs_oracle_run<DSW>(3, 10, 3, 10, 3, 600);
+    rc |= fixed_vs_oracle_run<DSW>(3, 10, 5, 8, 3, 400);
+    rc |= fixed_vs_oracle_run<DSW>(2, 10, 3, 10, 3, 600);
+    rc |= fixed_vs_oracle_run<DSW>(2, 10, 1, 10, 1, 400);
+    rc |= double_coding(3, 10, 3, 10, 5, 200, 420);
+    rc |= double_coding(2, 10, 3, 10, 5, 200, 420);
+    rc |= double_coding(3, 10, 5, 10, 1, 150, 380);
+    if (rc == 0) std::printf("RELAY DROPIN OK\n");
+    return rc;
+}
+#endif

@@ -1,7 +1,9 @@
 """The header swap INTEGRATION.md §2 documents, checked against the reference's own callers.
 
-A maintainer replaces six reference headers (FEC_Encoder.h, FEC_Decoder.h, Memory_Allocator.h,
-FEC_Message.h, Encoder.h, Decoder.h) with one-line forwarders to include/fec_amd_dropin.h.  This test
+A maintainer replaces seven reference headers (FEC_Encoder.h, FEC_Decoder.h, Memory_Allocator.h,
+FEC_Message.h, Encoder.h, Decoder.h, Decoder_Symbol_Wise.h) with one-line forwarders to
+include/fec_amd_dropin.h (Decoder_Symbol_Wise.h keeps its FEC_Macro.h include), and drops
+src/Decoder_Symbol_Wise.cpp from the build (the drop-in library defines siphon::Decoder_Symbol_Wise).  This test
 does exactly that in a temporary copy of the reference's include/ (nothing of the reference is kept
 or committed), stubs only what the image lacks (Boost posix_time, Intel ISA-L's header), and runs
 `g++ -fsyntax-only` on the reference's callers of the coding path.  It is skipped where
@@ -17,9 +19,12 @@ from conftest import ROOT
 
 REF = "/root/reference"
 SWAPPED = ["FEC_Encoder.h", "FEC_Decoder.h", "Memory_Allocator.h", "FEC_Message.h", "Encoder.h",
-           "Decoder.h"]
-CALLERS = ["Variable_Rate_FEC_Encoder.cpp", "Variable_Rate_FEC_Decoder.cpp", "Decoder_Symbol_Wise.cpp",
-           "Application_Layer_Sender.cpp", "Application_Layer_Receiver.cpp"]
+           "Decoder.h", "Decoder_Symbol_Wise.h"]
+FORWARDER = {"Decoder_Symbol_Wise.h": '#pragma once\n#include "FEC_Macro.h"\n#include "fec_amd_dropin.h"\n'}
+CALLERS = ["Variable_Rate_FEC_Encoder.cpp", "Variable_Rate_FEC_Decoder.cpp", "Application_Layer_Sender.cpp",
+           "Application_Layer_Receiver.cpp"]
+# compiled only against the original headers (the swap removes it from the build)
+ORIGINAL_ONLY = ["Decoder_Symbol_Wise.cpp"]
 
 # Boost is absent from the image; the reference uses three posix_time names
 # (Variable_Rate_FEC_Decoder.h:19,174; Payload_Simulator.h:20,46).  Real Boost brings <string> and
@@ -61,7 +66,7 @@ def _overlay(tmp_path, swap: bool):
     shutil.copytree(os.path.join(REF, "include"), inc)
     if swap:
         for h in SWAPPED:
-            (inc / h).write_text('#pragma once\n#include "fec_amd_dropin.h"\n')
+            (inc / h).write_text(FORWARDER.get(h, '#pragma once\n#include "fec_amd_dropin.h"\n'))
     stub = tmp_path / "stubs"
     (stub / "boost" / "date_time" / "posix_time").mkdir(parents=True, exist_ok=True)
     (stub / "boost" / "date_time" / "posix_time" / "posix_time.hpp").write_text(BOOST_STUB)
@@ -84,6 +89,6 @@ def test_stubs_alone_compile_the_original_headers(tmp_path):
     """Control: the same stubs with the reference's original headers compile the same callers, so a
     failure above is the drop-in header's, not the stubs'."""
     flags = _overlay(tmp_path, swap=False)
-    for src in CALLERS:
+    for src in CALLERS + ORIGINAL_ONLY:
         r = _syntax(flags, src)
         assert r.returncode == 0, f"{src}:\n{r.stderr[-2000:]}"

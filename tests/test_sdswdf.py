@@ -271,3 +271,45 @@ def test_gpu_sdswdf_large_batch_round_trip():
     out, dflag = r.destination(frames, z)
     good = (out[D:, 2:2 + L] == payload[:P - D]).all(dim=1).cpu().numpy()
     assert good.mean() > 0.98
+
+
+def _build_relay_driver(tmp_path, oracle_only):
+    import os
+    import shutil
+    import subprocess
+    from conftest import ROOT
+    import fec_erasure_code_unit_test_relay_amd as fec
+    if shutil.which("g++") is None or not os.path.exists(fec.LIB_PATH):
+        pytest.skip("needs g++ and the built libfec_amd.so")
+    libdir = os.path.dirname(fec.LIB_PATH)
+    exe = str(tmp_path / ("relay_oracle" if oracle_only else "relay_dropin"))
+    cmd = ["g++", "-O2", "-std=c++17", "-x", "c++", os.path.join(ROOT, "tests", "cpp", "relay_dropin_test.cpp"),
+           "-x", "c", os.path.join(ROOT, "oracle", "fec_oracle.c"), "-x", "none",
+           "-I", os.path.join(ROOT, "include"), "-L", libdir, "-lfec_amd", f"-Wl,-rpath,{libdir}", "-o", exe]
+    if oracle_only:
+        cmd.insert(1, "-DRELAY_ORACLE_ONLY")
+    subprocess.run(cmd, check=True, timeout=300)
+    return exe
+
+
+def test_relay_driver_over_oracle_methods_equals_oracle_chains(tmp_path):
+    """tests/cpp/relay_dropin_test.cpp drives the reference's Decoder_Symbol_Wise member arrays the
+    way Variable_Rate_FEC_Decoder does (types 2 and 3); over the oracle's per-call methods (or_sw_*,
+    the signatures of the product's fec_sw_* C ABI) it reproduces the oracle's whole relay chains."""
+    import subprocess
+    exe = _build_relay_driver(tmp_path, oracle_only=True)
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "RELAY ORACLE DRIVER OK" in r.stdout
+
+
+@pytest.mark.gpu
+def test_gpu_relay_dropin_class_equals_oracle(tmp_path):
+    """siphon::Decoder_Symbol_Wise (include/fec_amd_dropin.h, GF work through fec_sw_* on the GPU)
+    under the same driver: frames, destination outputs and flags equal the oracle's chains at fixed
+    rate, and equal the oracle-method class through a double-coding transition (copy_elements)."""
+    import subprocess
+    exe = _build_relay_driver(tmp_path, oracle_only=False)
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "RELAY DROPIN OK" in r.stdout
