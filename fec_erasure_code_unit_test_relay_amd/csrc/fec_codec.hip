@@ -1139,13 +1139,14 @@ constexpr int64_t kServerIdleTicks = 5000000;  // 50 ms of the 100 MHz counter w
 
 // Persistent servers per process.  A live server occupies its stream's hardware queue until it
 // idles out, and a process has few queues (GPU_MAX_HW_QUEUES, 4 by default): streams beyond that
-// share queues, and work queued behind a live server waits for it.  So at most FEC_SERVER_MAX
-// (default 2; 0 = none) coders keep a persistent server; the others serve each call with a one-shot
-// launch of the same kernel (idle limit 0: it serves the posted request and exits, and the call
-// waits for the launch to end), and before such a launch they stop the live persistent servers
-// (their stop word), since the one-shot's stream may share a queue with one of them.  A stopped
-// server's coder relaunches it at its next call.  A coder gives its slot back at its next call
-// after its server ended, or when it is destroyed.
+// share queues, and work queued behind a live server waits for it.  Which streams share a queue is
+// the runtime's choice, so no two servers are ever live at once: every server launch first stops
+// the other live servers (their stop word; they write their state back and end).  At most
+// FEC_SERVER_MAX (default 1; 0 = none) coders keep a persistent server; the others serve each call
+// with a one-shot launch of the same kernel (idle limit 0: it serves the posted request and exits,
+// and the call waits for the launch to end).  A stopped server's coder relaunches it at its next
+// call.  A coder gives its slot back at its next call after its server ended, or when it is
+// destroyed.
 std::atomic<int> g_server_slots{0};
 std::mutex g_server_mu;
 std::vector<ServerHost*> g_server_live;  // persistent servers launched and not seen ended
@@ -1153,7 +1154,7 @@ std::vector<ServerHost*> g_server_live;  // persistent servers launched and not 
 int server_slot_cap() {
     static const int cap = [] {
         const char* v = std::getenv("FEC_SERVER_MAX");
-        const int c = v ? std::atoi(v) : 2;
+        const int c = v ? std::atoi(v) : 1;
         return c < 0 ? 0 : c;
     }();
     return cap;
@@ -1184,7 +1185,7 @@ bool server_persistent(ServerHost& sv) {
     if (!sv.live) server_slot_give(sv);
     return sv.live || server_slot_take(sv);
 }
-// Before a one-shot launch: every other coder's persistent server stops (it writes its state back
+// Before a server launch: every other coder's persistent server stops (it writes its state back
 // and ends; its coder sees exited = 1 and relaunches at its next call).
 void server_stop_others(const ServerHost& self) {
     std::lock_guard<std::mutex> lk(g_server_mu);
@@ -1200,7 +1201,7 @@ using ServerLaunch = std::function<hipError_t(uint32_t last, int64_t idle_ticks)
 
 hipError_t server_start(ServerHost& sv, uint32_t last, bool persistent, const ServerLaunch& launch) {
     volatile fec::ServerBox* b = sv.h_box;
-    if (!persistent) server_stop_others(sv);
+    server_stop_others(sv);
     b->stop = 0;
     b->exited = 0;
     b->alive = 1;

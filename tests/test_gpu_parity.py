@@ -378,7 +378,7 @@ def test_streaming_api_across_server_idle_exits():
 
 def test_streaming_api_many_coders_interleaved():
     """Six encoder/decoder pairs used in turn (12 coders, more than the process's persistent-server
-    slots, FEC_SERVER_MAX = 2, and more streams than hardware queues): every call equals the oracle,
+    slots, FEC_SERVER_MAX = 1, and more streams than hardware queues): every call equals the oracle,
     recovered packets included, and no call waits out another coder's server (50 ms idle limit)."""
     import time
     T, B, N = 10, 3, 3
