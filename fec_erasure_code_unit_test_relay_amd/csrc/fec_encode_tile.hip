@@ -332,11 +332,13 @@ __device__ __forceinline__ void tile_walk(const EncTileArgs& a, uint8_t* smem) {
     // parity rows start zeroed
     for (int x = tid; x < NPA * QJ; x += kTileThreads) q[x] = 0;
 
-    issue(0);
-    if (cnt >= 1) issue(1);
+    // tile 0 (in front of the first one) only feeds parity history: none to feed without parity
+    constexpr int it0 = NP > 0 ? 0 : 1;
+    issue(it0);
+    if (cnt >= it0 + 1) issue(it0 + 1);
 
     uint32_t H[K];
-    for (int it = 0; it <= cnt; ++it) {
+    for (int it = it0; it <= cnt; ++it) {
         // tile it's input: every VMEM instruction issued after it may still be in flight
         wait_vm(static_cast<int>(vm_issued - vm_mark[it & 1]));
         wait_lds_barrier();  // B1: the tile is in LDS everywhere; last tile's output stored
@@ -641,20 +643,27 @@ __global__ __launch_bounds__(kTileThreads, (tile_min_wg<K, NP>())) void fec_enco
 #ifdef FEC_WAVE_ONLY
 #define FEC_ENC_TILE_LIST(X) X(8, 3)
 #define FEC_ENC_TILE_L300_LIST(X) X(8, 3)
+#define FEC_ENC_TILE_SEG300_LIST(X) X(8, 3)
 #else
 #define FEC_ENC_TILE_LIST(X) \
     X(8, 3) X(9, 5) X(11, 0) X(10, 1) X(9, 2) X(7, 4) X(6, 5) X(5, 6) X(4, 7) X(3, 8) X(2, 9)  \
     X(10, 3) X(9, 3) X(10, 4) X(8, 4) X(10, 5) X(7, 5) X(3, 9)
 // L = 300 specialisations: the (T,B,N) of BASELINE configs 1-3 and 5
 #define FEC_ENC_TILE_L300_LIST(X) X(8, 3) X(9, 5)
+// segment mode at L = 300 (config 4's tuples): the list's entries with an L = 300 tile geometry
+#define FEC_ENC_TILE_SEG300_LIST(X) \
+    X(8, 3) X(9, 5) X(11, 0) X(10, 1) X(9, 2) X(7, 4) X(6, 5) X(5, 6) X(4, 7) X(10, 3) X(9, 3) X(10, 4) \
+    X(8, 4) X(10, 5) X(7, 5)
 #endif
 
 #define FEC_ENC_TILE_INST(K, NP) \
     template __global__ void fec_encode_tile_kernel<K, NP, 0, false>(EncTileArgs); \
     template __global__ void fec_encode_tile_kernel<K, NP, 0, true>(EncTileArgs);
 #define FEC_ENC_TILE_INST300(K, NP) template __global__ void fec_encode_tile_kernel<K, NP, 300, false>(EncTileArgs);
+#define FEC_ENC_TILE_SEG_INST300(K, NP) template __global__ void fec_encode_tile_kernel<K, NP, 300, true>(EncTileArgs);
 FEC_ENC_TILE_LIST(FEC_ENC_TILE_INST)
 FEC_ENC_TILE_L300_LIST(FEC_ENC_TILE_INST300)
+FEC_ENC_TILE_SEG300_LIST(FEC_ENC_TILE_SEG_INST300)
 
 const void* fec_encode_tile_kernel_for(int k, int np, int L) {
     if (!std::getenv("FEC_TILE_RUNTIME_L") && L == 300) {
@@ -670,8 +679,15 @@ const void* fec_encode_tile_kernel_for(int k, int np, int L) {
     return nullptr;
 }
 
-// The segment-mode instance (runtime L) for the variable-rate schedule, or nullptr.
-const void* fec_encode_tile_seg_kernel_for(int k, int np) {
+// The segment-mode instance for the variable-rate schedule (L = 300 fixed at compile time, else
+// from the arguments), or nullptr.
+const void* fec_encode_tile_seg_kernel_for(int k, int np, int L) {
+    if (L == 300) {
+#define FEC_ENC_TILE_SEG_CASE300(K, NP) \
+    if (k == K && np == NP) return reinterpret_cast<const void*>(&fec_encode_tile_kernel<K, NP, 300, true>);
+        FEC_ENC_TILE_SEG300_LIST(FEC_ENC_TILE_SEG_CASE300)
+#undef FEC_ENC_TILE_SEG_CASE300
+    }
 #define FEC_ENC_TILE_SEG_CASE(K, NP) \
     if (k == K && np == NP) return reinterpret_cast<const void*>(&fec_encode_tile_kernel<K, NP, 0, true>);
     FEC_ENC_TILE_LIST(FEC_ENC_TILE_SEG_CASE)

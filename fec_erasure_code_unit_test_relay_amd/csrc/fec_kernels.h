@@ -132,8 +132,8 @@ constexpr TileGeom tile_geometry(int k, int np, int L) {
 // fec_encode_tile_kernel<k, n-k, L> for L = 300 (the reference's payload size, L fixed at compile
 // time) or <k, n-k, 0> (L from the arguments) (fec_encode_tile.hip), else nullptr.  256 threads.
 const void* fec_encode_tile_kernel_for(int k, int np, int L);
-// fec_encode_tile_kernel<k, n-k, 0> with segment mode (EncTileArgs::seg) compiled in, else nullptr.
-const void* fec_encode_tile_seg_kernel_for(int k, int np);
+// fec_encode_tile_kernel<k, n-k, 300 or 0> with segment mode (EncTileArgs::seg) compiled in, else nullptr.
+const void* fec_encode_tile_seg_kernel_for(int k, int np, int L);
 
 struct CopyFastArgs {
     const uint8_t* cw;

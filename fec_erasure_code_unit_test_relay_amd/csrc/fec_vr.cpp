@@ -1226,7 +1226,7 @@ int prepare_encode(fec_vr_plan* v, hipStream_t s) {
             gtab.insert(gtab.end(), t.begin(), t.end());
             int ti = -1;
             const fec::TileGeom tg = fec::tile_geometry(g.k, g.n - g.k, p.L);
-            const void* kfn = fec::fec_encode_tile_seg_kernel_for(g.k, g.n - g.k);
+            const void* kfn = fec::fec_encode_tile_seg_kernel_for(g.k, g.n - g.k, p.L);
             if (tiles_on && tg.ok && kfn && (p.L & 3) == 0) {
                 ti = static_cast<int>(v->tiles.size());
                 v->tiles.push_back({kfn, tg, it->second, 0, 0});

@@ -111,27 +111,59 @@ __global__ __launch_bounds__(256) void fec_vr_encode_kernel(VrEncodeArgs a) {
         const int sidx = static_cast<int>((static_cast<float>(q) + 0.5f) * rk);
         slot[(q - sidx * k) * PL + sidx] = static_cast<uint8_t>(v);
     };
-    auto load_row = [&](int64_t r) {
-        uint8_t* slot = ring + static_cast<int>(((r % n) + n) % n) * SB;
-        for (int d = lane; d < k * NSG; d += 64) reinterpret_cast<uint32_t*>(slot)[d] = 0;
-        if (r < first) return;  // all-zero row before the instance's first call
-        int ln = a.len ? a.len[r] : L;
-        ln = ln < 0 ? 0 : (ln > L ? L : ln);
-        __builtin_amdgcn_wave_barrier();
-        if (lane == 0) {
+    // rows r0..r1 into their ring slots: zeroed, then the header and payload bytes of every row
+    // with its loads in flight together (a fresh instance needs n rows: one dependent HBM round
+    // trip for all of them, not one per row)
+    auto load_rows = [&](int64_t r0, int64_t r1) {
+        const int nr = static_cast<int>(r1 - r0 + 1);
+        const int sw_ = k * NSG;
+        for (int d = lane; d < nr * sw_; d += 64) {
+            const int rr = d / sw_;
+            reinterpret_cast<uint32_t*>(ring + static_cast<int>(((r0 + rr) % n + n) % n) * SB)[d - rr * sw_] = 0;
+        }
+        wave_sync();
+        auto row_len = [&](int64_t r) {
+            int ln = a.len ? a.len[r] : L;
+            return ln < 0 ? 0 : (ln > L ? L : ln);
+        };
+        for (int rr = lane; rr < nr; rr += 64) {
+            const int64_t r = r0 + rr;
+            if (r < first) continue;  // all-zero row before the instance's first call
+            const int ln = row_len(r);
+            uint8_t* slot = ring + static_cast<int>((r % n + n) % n) * SB;
             put(slot, 0, static_cast<uint32_t>(ln >> 8));
             put(slot, 1, static_cast<uint32_t>(ln & 0xff));
         }
-        const uint8_t* src = a.payload + r * L;
-        if (words) {
-            for (int w = lane; 4 * w < ln; w += 64) {
-                const uint32_t v = *reinterpret_cast<const uint32_t*>(src + 4 * w);
+        const int nw = words ? (L + 3) >> 2 : L;  // loads per row
+        constexpr int kU = 4;
+        for (int i0 = lane; i0 < nr * nw; i0 += 64 * kU) {
+            uint32_t v[kU];
+            int lim[kU], q0[kU];
+            uint8_t* sl[kU];
 #pragma unroll
-                for (int b = 0; b < 4; ++b)
-                    if (4 * w + b < ln) put(slot, 4 * w + b + 2, v >> (8 * b));
+            for (int u = 0; u < kU; ++u) {
+                const int idx = i0 + 64 * u;
+                const int rr = idx / nw, w = idx - rr * nw;
+                const int64_t r = r0 + rr;
+                lim[u] = 0;
+                v[u] = 0;
+                sl[u] = ring;
+                q0[u] = 0;
+                if (idx < nr * nw && r >= first) {
+                    const int ln = row_len(r);
+                    const int b0 = words ? 4 * w : w;
+                    if (b0 < ln) {
+                        const uint8_t* src = a.payload + r * L;
+                        v[u] = words ? *reinterpret_cast<const uint32_t*>(src + b0) : src[b0];
+                        lim[u] = min(words ? 4 : 1, ln - b0);
+                        q0[u] = b0 + 2;
+                        sl[u] = ring + static_cast<int>((r % n + n) % n) * SB;
+                    }
+                }
             }
-        } else {
-            for (int b = lane; b < ln; b += 64) put(slot, b + 2, src[b]);
+#pragma unroll
+            for (int u = 0; u < kU; ++u)
+                for (int b = 0; b < lim[u]; ++b) put(sl[u], q0[u] + b, v[u] >> (8 * b));
         }
     };
     for (int64_t c = c0; c < c1; ++c) {
@@ -157,9 +189,9 @@ __global__ __launch_bounds__(256) void fec_vr_encode_kernel(VrEncodeArgs a) {
         if (fresh) {
             const uint32_t* gt = a.gtab + a.inst[4 * e + 3];
             for (int i = lane; i < k * (n - k) * 8; i += 64) tabw[i] = gt[i];
-            for (int64_t r = seq - (n - 1); r <= seq; ++r) load_row(r);
+            load_rows(seq - (n - 1), seq);
         } else {
-            for (int64_t r = next_row; r <= seq; ++r) load_row(r);
+            load_rows(next_row, seq);
         }
         next_row = seq + 1;
         const bool to_old = seq >= sw;

@@ -9,7 +9,7 @@ cd $R
 export TMPDIR=/tmp
 timeout -k 10 300 python -u -m pytest tests/test_vr.py -m gpu -x -q --timeout 120 --timeout-method thread > $OUT/pytest.log 2>&1 || { echo "pytest failed"; tail -30 $OUT/pytest.log; exit 1; }
 tail -1 $OUT/pytest.log
-for u in 4 2 1 4 2 1; do
+for u in ${FEC_UNITS:-4 8 16 4 8 16}; do
     echo "unit $u"; FEC_VR_TILE_UNIT=$u timeout -k 10 120 python -u tools/vr_prof.py 20 2>&1 | grep -E "encode|decode" | tee -a $OUT/vr_unit.log || exit 1
 done
 timeout -k 10 180 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o run -- python3 tools/vr_prof.py 20 > $OUT/rocprof.log 2>&1 || { echo "rocprof failed"; tail -20 $OUT/rocprof.log; exit 1; }

@@ -71,5 +71,28 @@ int main() {
                     sum / (2 * (NS - 1)), 2 * (NS - 1));
         for (auto x : s) CHECK(hipStreamDestroy(x));
     }
+    // mode 3: one CU-masked "server" stream created first, then NS plain streams; the spinner runs
+    // on the masked stream: does any plain stream land on its queue?
+    {
+        hipStream_t srv;
+        CHECK(hipExtStreamCreateWithCUMask(&srv, static_cast<uint32_t>(mask.size()), mask.data()));
+        std::vector<hipStream_t> s(NS);
+        for (int i = 0; i < NS; ++i) CHECK(hipStreamCreateWithFlags(&s[i], hipStreamNonBlocking));
+        for (int i = 0; i < NS; ++i) hipLaunchKernelGGL(tiny, dim3(1), dim3(64), 0, s[i], d);
+        CHECK(hipDeviceSynchronize());
+        double worst = 0;
+        hipLaunchKernelGGL(spin, dim3(1), dim3(64), 0, srv, spin_ticks);
+        for (int i = 0; i < NS; ++i) {
+            const auto t0 = std::chrono::steady_clock::now();
+            hipLaunchKernelGGL(tiny, dim3(1), dim3(64), 0, s[i], d);
+            CHECK(hipStreamSynchronize(s[i]));
+            const double us = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
+            worst = us > worst ? us : worst;
+        }
+        CHECK(hipDeviceSynchronize());
+        std::printf("masked server first, then %d plain streams: worst %.1f us\n", NS, worst);
+        for (auto x : s) CHECK(hipStreamDestroy(x));
+        CHECK(hipStreamDestroy(srv));
+    }
     return 0;
 }
