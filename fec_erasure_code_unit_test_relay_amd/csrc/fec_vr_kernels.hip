@@ -264,7 +264,8 @@ __global__ __launch_bounds__(256) void fec_vr_geo_kernel(VrCopyArgs a) {
     a.geo[x] = g;
 }
 
-// The received packets' systematic copies, a tile of kVrCopyTP consecutive packets per workgroup:
+// The received packets' systematic copies for L % 4 != 0 (or rows too long for the output tile
+// below): a tile of kVrCopyTP consecutive packets per workgroup:
 // their cur rows are one contiguous span of the compact layout, read with 16-byte loads into LDS
 // next to a per-packet record (row offset and width, geometry, copied length); then each thread
 // makes output dwords (payload byte b = codeword byte (h / k) * n + h % k of the reporting
@@ -275,7 +276,7 @@ __global__ __launch_bounds__(256) void fec_vr_geo_kernel(VrCopyArgs a) {
 // recovered ones are left to fec_vr_recover_kernel.  Bytes past a row read as zero.
 constexpr int kVrCopyTP = 16;
 constexpr int kVrCopyStage = 16384;
-__global__ __launch_bounds__(256) void fec_vr_copy_kernel(VrCopyArgs a) {
+__global__ __launch_bounds__(256) void fec_vr_copy_gather_kernel(VrCopyArgs a) {
     __shared__ __attribute__((aligned(16))) uint8_t stage[kVrCopyStage];
     __shared__ int s_ro[kVrCopyTP], s_rw[kVrCopyTP], s_kn[kVrCopyTP], s_cp[kVrCopyTP];
     __shared__ float s_rk[kVrCopyTP];
@@ -358,6 +359,147 @@ __global__ __launch_bounds__(256) void fec_vr_copy_kernel(VrCopyArgs a) {
     }
 }
 
+// The received packets' systematic copies, a tile of kVrCopyTP consecutive packets per workgroup:
+// their cur rows are one contiguous span of the compact layout, read with 16-byte loads into LDS
+// next to a per-packet record (row offset and width, geometry, copied length).  Then a half-wave
+// per packet and a lane per sub-stream s: the sub-stream's k systematic bytes (row bytes
+// [s*n, s*n+k), three dword shifts) go to bytes [s*k, s*k+k) of the packet's [header, payload]
+// image in an LDS output tile, as 12 byte writes in reverse order -- the writes past k land in
+// the next sub-stream's bytes first and that lane's own writes come later, so no lane needs k at
+// compile time or a per-byte test (a thread per output dword instead spent a division and four
+// dependent byte positions per dword: 88.9 vs 81.4 us on the schedule of bin/erasure.bin,
+// tools/ubench/vr_copy_real.hip).  The header (symbols 0 and 1 of sub-stream 0, k = 1: position 0
+// of sub-streams 0 and 1, Decoder.cpp:89-96) gives the length, clamped on the slow path
+// (:148-149); the tile's payload rows leave as one contiguous run of 16-byte stores, bytes past a
+// packet's copied length zero.  A tile wider than the stage (rows of k <= 3) gathers from HBM into
+// the output tile.  Lost packets get a zero row and length 0; recovered ones are left to
+// fec_vr_recover_kernel.  Needs L % 4 == 0 (output dwords inside one row).
+constexpr int kVrCopyOrs = 32;  // output tile row = L + 32 bytes: [6 guard][header 2][payload][spill]
+__global__ __launch_bounds__(256) void fec_vr_copy_kernel(VrCopyArgs a) {
+    __shared__ __attribute__((aligned(16))) uint8_t stage[kVrCopyStage + 16];
+    extern __shared__ __attribute__((aligned(16))) uint8_t otile[];
+    __shared__ int s_ro[kVrCopyTP], s_rw[kVrCopyTP], s_kn[kVrCopyTP], s_cp[kVrCopyTP], s_S[kVrCopyTP];
+    const int tid = threadIdx.x, l32 = tid & 31, hw = tid >> 5;
+    const int L = a.L, ors = L + kVrCopyOrs;
+    const int64_t ntiles = (a.P + kVrCopyTP - 1) / kVrCopyTP;
+    for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+        const int64_t x0 = tile * kVrCopyTP;
+        const int np = static_cast<int>(min<int64_t>(kVrCopyTP, a.P - x0));
+        const int64_t o0 = a.cur_off[x0];
+        const int64_t span = a.cur_off[x0 + np] - o0;
+        const bool staged = span <= kVrCopyStage;  // uniform over the workgroup
+        if (staged) {
+            const uint4* src = reinterpret_cast<const uint4*>(a.cur + o0);
+            for (int c = tid; 16 * c < span; c += 256) reinterpret_cast<uint4*>(stage)[c] = src[c];
+        }
+        if (tid < np) {
+            const int64_t x = x0 + tid;
+            const uint32_t g = a.geo[x];
+            const int64_t ro = a.cur_off[x];
+            s_ro[tid] = static_cast<int>(ro - o0);
+            s_rw[tid] = static_cast<int>(a.cur_off[x + 1] - ro);
+            const int f = static_cast<int>(g >> 16 & 0xff);
+            const int k = f == 1 ? static_cast<int>(g & 0xff) : 1;
+            s_kn[tid] = f == 1 ? static_cast<int>(g & 0xffff) : (f == 2 ? -1 : 0);  // -1: recovered, 0: lost
+            s_S[tid] = (L + 2 + k - 1) / k;
+        }
+        __syncthreads();
+        if (tid < np) {  // the header of a received packet: its length, clamped on the slow path
+            const int64_t x = x0 + tid;
+            const int kn = s_kn[tid];
+            int ln = 0;
+            if (kn > 0) {
+                const int k = kn & 0xff, n = kn >> 8, rw = s_rw[tid];
+                const uint8_t* lrow = stage + s_ro[tid];
+                const uint8_t* grow = a.cur + o0 + s_ro[tid];
+                const int p1 = k > 1 ? 1 : n;
+                const int h0 = rw > 0 ? (staged ? lrow[0] : grow[0]) : 0;
+                const int h1 = p1 < rw ? (staged ? lrow[p1] : grow[p1]) : 0;
+                const int hdr = h0 * 256 + h1;
+                ln = (a.geo[x] >> 24) ? min(hdr, L) : hdr;
+            }
+            if (kn >= 0) a.out_len[x] = ln;
+            s_cp[tid] = min(ln, L);
+        }
+        if (staged) {
+            for (int pp = hw; pp < np; pp += 8) {
+                const int kn = s_kn[pp];
+                if (kn <= 0) continue;
+                const int k = kn & 0xff, n = kn >> 8, S = s_S[pp];
+                const int ro = s_ro[pp];
+                uint8_t* img = otile + pp * ors + 6;  // byte q of the packet's [header, payload]
+                for (int sb = l32; sb < S; sb += 32) {
+                    const int aa = ro + sb * n;  // rows start 16-byte aligned in the stage
+                    const uint32_t* src = reinterpret_cast<const uint32_t*>(stage + (aa & ~3));
+                    const uint32_t d0 = src[0], d1 = src[1], d2 = src[2], d3 = src[3];
+                    const int sh = aa & 3;
+                    const uint32_t w0 = __builtin_amdgcn_alignbyte(d1, d0, sh);
+                    const uint32_t w1 = __builtin_amdgcn_alignbyte(d2, d1, sh);
+                    const uint32_t w2 = __builtin_amdgcn_alignbyte(d3, d2, sh);
+                    uint8_t* dst = img + sb * k;
+                    dst[11] = static_cast<uint8_t>(w2 >> 24);
+                    dst[10] = static_cast<uint8_t>(w2 >> 16);
+                    dst[9] = static_cast<uint8_t>(w2 >> 8);
+                    dst[8] = static_cast<uint8_t>(w2);
+                    dst[7] = static_cast<uint8_t>(w1 >> 24);
+                    dst[6] = static_cast<uint8_t>(w1 >> 16);
+                    dst[5] = static_cast<uint8_t>(w1 >> 8);
+                    dst[4] = static_cast<uint8_t>(w1);
+                    dst[3] = static_cast<uint8_t>(w0 >> 24);
+                    dst[2] = static_cast<uint8_t>(w0 >> 16);
+                    dst[1] = static_cast<uint8_t>(w0 >> 8);
+                    dst[0] = static_cast<uint8_t>(w0);
+                }
+            }
+        } else {
+            const int L4 = L >> 2;
+            for (int d = tid; d < np * L4; d += 256) {
+                const int p = d / L4, w = d - p * L4;
+                const int kn = s_kn[p];
+                if (kn <= 0) continue;
+                const int k = kn & 0xff, n = kn >> 8, rw = s_rw[p];
+                const uint8_t* grow = a.cur + o0 + s_ro[p];
+                const int h = 4 * w + 2;
+                int sidx = h / k, i = h - sidx * k;
+                uint32_t val = 0;
+                for (int e = 0; e < 4; ++e) {
+                    const int pos = sidx * n + i;
+                    if (pos < rw) val |= static_cast<uint32_t>(grow[pos]) << (8 * e);
+                    if (++i == k) {
+                        i = 0;
+                        ++sidx;
+                    }
+                }
+                *reinterpret_cast<uint32_t*>(otile + p * ors + 8 + 4 * w) = val;
+            }
+        }
+        __syncthreads();
+        const int ob = np * L;
+        uint8_t* dst = a.out + x0 * L;
+        const bool al16 = ((reinterpret_cast<uintptr_t>(dst)) & 15) == 0;
+        for (int o = 16 * tid; o < ob; o += 16 * 256) {
+            uint32_t v[4];
+            bool skip[4], any_skip = false;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int oq = o + 4 * q;
+                const int p = oq / L, off = oq - p * L;
+                skip[q] = oq >= ob || s_kn[p < np ? p : 0] < 0;
+                any_skip |= skip[q];
+                v[q] = skip[q] ? 0u : *reinterpret_cast<const uint32_t*>(otile + p * ors + 8 + off) & keep_bytes(s_cp[p] - off);
+            }
+            if (!any_skip && al16) {
+                *reinterpret_cast<uint4*>(dst + o) = make_uint4(v[0], v[1], v[2], v[3]);
+            } else {
+#pragma unroll
+                for (int q = 0; q < 4; ++q)
+                    if (!skip[q]) *reinterpret_cast<uint32_t*>(dst + o + 4 * q) = v[q];
+            }
+        }
+        __syncthreads();  // the stage, records and output tile are read before the next tile's
+    }
+}
+
 // Per-row offsets of the compact layout, one thread per row s: e = the last instance with
 // first_e <= s (binary search); cur row at base_cur_e + (s - first_e) * CWp_e; the same seq's old
 // row belongs to instance e-1 while s < end_{e-1} (double coding), else it is empty (offset = where
@@ -382,10 +524,13 @@ __global__ __launch_bounds__(256) void fec_vr_offsets_kernel(VrOffsetsArgs a) {
 
 // One wave per recovered packet (as fec_recover_kernel): byte h = (sub-stream h/k, position i =
 // h%k) = XOR_q coef[i][q] * symbol q of packet x-i+q, read from the reporting decoder's input.
+// The k+n-1 input rows' addresses (cur before the decoder's role switch, old after; none outside
+// the frames) are resolved once per packet into LDS, so each symbol is one dependent load.
 __global__ __launch_bounds__(256) void fec_vr_recover_kernel(VrRecArgs a) {
     __shared__ uint8_t gexp[512];
     __shared__ uint8_t glog[256];
     __shared__ uint8_t lcf[4][kVrCoefStride];
+    __shared__ const uint8_t* rowp[4][kMaxK + kMaxRuleN];
     const int tid = threadIdx.x;
     for (int i = tid; i < 512; i += 256) gexp[i] = a.gf[i];
     for (int i = tid; i < 256; i += 256) glog[i] = a.gf[512 + i];
@@ -393,6 +538,7 @@ __global__ __launch_bounds__(256) void fec_vr_recover_kernel(VrRecArgs a) {
     const int lane = tid & 63, wl = tid >> 6;
     const int L = a.L;
     uint8_t* lc = lcf[wl];
+    const uint8_t** rp = rowp[wl];
     for (int r = blockIdx.x * 4 + wl; r < a.nrec; r += gridDim.x * 4) {
         const int64_t x = a.rec_x[r];
         const int j = a.rec_dec[r];
@@ -402,19 +548,27 @@ __global__ __launch_bounds__(256) void fec_vr_recover_kernel(VrRecArgs a) {
             const uint8_t c = a.rec_coef[static_cast<int64_t>(r) * kVrCoefStride + i];
             lc[i] = c ? glog[c] : 255;
         }
-        __builtin_amdgcn_wave_barrier();
+        if (lane < k + n - 1) {  // row x-k+1+lane
+            const int64_t row = x - k + 1 + lane;
+            rp[lane] = (row < 0 || row >= a.rows) ? nullptr
+                                                   : (row < sw ? a.cur + a.cur_off[row] : a.old + a.old_off[row]);
+        }
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         int ln = 0;
         for (int h0 = 0; h0 < L + 2; h0 += 64) {
             const int h = h0 + lane;
             uint8_t acc = 0;
             if (h < L + 2) {
                 const int s = h / k, i = h - s * k;
+                const uint8_t* const* rpi = rp + (k - 1 - i);  // row of symbol q: x-i+q
+                const uint8_t* lci = lc + i * n;
+#pragma unroll 4
                 for (int q = 0; q < n; ++q) {
-                    const int lq = lc[i * n + q];
-                    const int64_t row = x - i + q;
-                    if (lq == 255 || row < 0 || row >= a.rows) continue;
-                    const uint8_t v = row < sw ? a.cur[a.cur_off[row] + s * n + q] : a.old[a.old_off[row] + s * n + q];
+                    const int lq = lci[q];
+                    const uint8_t* row = rpi[q];
+                    const uint8_t v = (lq == 255 || !row) ? 0 : row[s * n + q];
                     if (v) acc ^= gexp[lq + glog[v]];
                 }
             }
@@ -427,7 +581,9 @@ __global__ __launch_bounds__(256) void fec_vr_recover_kernel(VrRecArgs a) {
             if (b >= 0 && b < L) a.out[x * L + b] = b < ln ? acc : 0;
         }
         if (lane == 0) a.out_len[x] = ln;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     }
 }
 
@@ -467,8 +623,13 @@ int vr_launch_copy(const VrCopyArgs& a, void* s) {
     hipLaunchKernelGGL(fec_vr_geo_kernel, dim3(static_cast<unsigned>((a.P + 255) / 256)), dim3(256), 0,
                        static_cast<hipStream_t>(s), a);
     const int64_t grid = (a.P + kVrCopyTP - 1) / kVrCopyTP;
-    hipLaunchKernelGGL(fec_vr_copy_kernel, dim3(static_cast<unsigned>(grid)), dim3(256), 0,
-                       static_cast<hipStream_t>(s), a);
+    const size_t otile = static_cast<size_t>(kVrCopyTP) * (a.L + kVrCopyOrs);
+    if ((a.L & 3) == 0 && otile <= 32768)
+        hipLaunchKernelGGL(fec_vr_copy_kernel, dim3(static_cast<unsigned>(grid)), dim3(256), otile,
+                           static_cast<hipStream_t>(s), a);
+    else
+        hipLaunchKernelGGL(fec_vr_copy_gather_kernel, dim3(static_cast<unsigned>(grid)), dim3(256), 0,
+                           static_cast<hipStream_t>(s), a);
     return hipGetLastError() == hipSuccess ? FEC_OK : FEC_ERR_HIP;
 }
 int vr_launch_offsets(const VrOffsetsArgs& a, void* s) {

@@ -1,0 +1,553 @@
+// vr_copy_real.hip -- config 4's decode copy on the real schedule (experiment, not product).
+//
+// Inputs from tools/vr_dump.py (bin/erasure.bin, 360 000 packets): per packet the copy's geometry
+// word (k | n << 8 | fate << 16) and the cur rows' offsets of the compact layout; the codeword bytes
+// are random.  Variants, each checked byte for byte (payload rows and lengths) against V0:
+//   V0  the r04 product kernel: a 16-packet tile staged in LDS, one thread per output dword that
+//       gathers its 4 bytes (a division and 4 dependent byte positions per dword);
+//   V1  the same staging; a half-wave per packet, a lane per sub-stream copies the sub-stream's k
+//       systematic bytes (3 aligned-dword shifts) into an LDS output tile with byte writes issued
+//       in reverse order (a lane's writes past its k bytes land first and are overwritten by the
+//       next sub-stream's), then the tile's payload rows leave in 16-byte stores.
+//   hipcc -O3 --offload-arch=gfx950 -o vr_copy_real vr_copy_real.hip && ./vr_copy_real [data_dir]
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#define CHECK(x)                                                                          \
+    do {                                                                                  \
+        hipError_t e = (x);                                                               \
+        if (e != hipSuccess) {                                                            \
+            std::fprintf(stderr, "%s:%d %s\n", __FILE__, __LINE__, hipGetErrorString(e)); \
+            std::exit(1);                                                                 \
+        }                                                                                 \
+    } while (0)
+
+struct Args {
+    const uint8_t* cur;
+    const int64_t* cur_off;
+    const uint32_t* geo;
+    int64_t P;
+    int L;
+    uint8_t* out;
+    int32_t* out_len;
+};
+
+constexpr int kTP = 16;
+constexpr int kStage = 16384;
+
+// ---- V0: the r04 product kernel (fec_vr_kernels.hip at cc91b30) ------------------------------
+__global__ __launch_bounds__(256) void copy_v0(Args a) {
+    __shared__ __attribute__((aligned(16))) uint8_t stage[kStage];
+    __shared__ int s_ro[kTP], s_rw[kTP], s_kn[kTP], s_cp[kTP];
+    __shared__ float s_rk[kTP];
+    const int tid = threadIdx.x;
+    const int L = a.L, L4 = (L + 3) >> 2;
+    const float rl4 = 1.0f / static_cast<float>(L4);
+    const int64_t ntiles = (a.P + kTP - 1) / kTP;
+    for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+        const int64_t x0 = tile * kTP;
+        const int np = static_cast<int>(min<int64_t>(kTP, a.P - x0));
+        const int64_t o0 = a.cur_off[x0];
+        const int64_t span = a.cur_off[x0 + np] - o0;
+        const bool staged = span <= kStage;
+        if (staged) {
+            const uint4* src = reinterpret_cast<const uint4*>(a.cur + o0);
+            for (int c = tid; 16 * c < span; c += 256) reinterpret_cast<uint4*>(stage)[c] = src[c];
+        }
+        int ln = 0;
+        if (tid < np) {
+            const int64_t x = x0 + tid;
+            const uint32_t g = a.geo[x];
+            const int64_t ro = a.cur_off[x];
+            s_ro[tid] = static_cast<int>(ro - o0);
+            s_rw[tid] = static_cast<int>(a.cur_off[x + 1] - ro);
+            const int f = static_cast<int>(g >> 16 & 0xff);
+            const int k = f == 1 ? static_cast<int>(g & 0xff) : 1;
+            s_kn[tid] = f == 1 ? static_cast<int>(g & 0xffff) : (f == 2 ? -1 : 0);
+            s_rk[tid] = 1.0f / static_cast<float>(k);
+        }
+        __syncthreads();
+        if (tid < np) {
+            const int64_t x = x0 + tid;
+            const int kn = s_kn[tid];
+            if (kn > 0) {
+                const int k = kn & 0xff, n = kn >> 8, rw = s_rw[tid];
+                const uint8_t* lrow = stage + s_ro[tid];
+                const uint8_t* grow = a.cur + o0 + s_ro[tid];
+                const int p1 = k > 1 ? 1 : n;
+                const int h0 = rw > 0 ? (staged ? lrow[0] : grow[0]) : 0;
+                const int h1 = p1 < rw ? (staged ? lrow[p1] : grow[p1]) : 0;
+                const int hdr = h0 * 256 + h1;
+                ln = (a.geo[x] >> 24) ? min(hdr, L) : hdr;
+            }
+            if (kn >= 0) a.out_len[x] = ln;
+            s_cp[tid] = min(ln, L);
+        }
+        __syncthreads();
+        for (int d = tid; d < np * L4; d += 256) {
+            const int p = static_cast<int>((static_cast<float>(d) + 0.5f) * rl4);
+            const int w = d - p * L4;
+            const int kn = s_kn[p];
+            if (kn < 0) continue;
+            const int cp = s_cp[p], b0 = 4 * w;
+            uint32_t val = 0;
+            if (b0 < cp) {
+                const int k = kn & 0xff, n = kn >> 8, rw = s_rw[p];
+                const uint8_t* lrow = stage + s_ro[p];
+                const uint8_t* grow = a.cur + o0 + s_ro[p];
+                const int h = b0 + 2;
+                int sidx = static_cast<int>((static_cast<float>(h) + 0.5f) * s_rk[p]);
+                int i = h - sidx * k;
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    const int pos = sidx * n + i;
+                    if (b0 + e < cp && pos < rw) val |= static_cast<uint32_t>(staged ? lrow[pos] : grow[pos]) << (8 * e);
+                    if (++i == k) {
+                        i = 0;
+                        ++sidx;
+                    }
+                }
+            }
+            uint8_t* o = a.out + (x0 + p) * L;
+            *reinterpret_cast<uint32_t*>(o + b0) = val;
+        }
+        __syncthreads();
+    }
+}
+
+// ---- V1 ----------------------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t keep_bytes(int nb) {
+    return nb >= 4 ? 0xffffffffu : (nb <= 0 ? 0u : (0xffffffffu >> (8 * (4 - nb))));
+}
+
+// LDS output tile: row p at p * ors + 8 (payload byte b at +b; b in [-2, L + 2k) is writable).
+template <int TP, int STG = kStage>
+__global__ __launch_bounds__(256) void copy_v1(Args a) {
+    __shared__ __attribute__((aligned(16))) uint8_t stage[STG + 16];
+    extern __shared__ __attribute__((aligned(16))) uint8_t otile[];
+    __shared__ int s_ro[TP], s_rw[TP], s_kn[TP], s_cp[TP], s_S[TP];
+    const int tid = threadIdx.x, l32 = tid & 31, hw = tid >> 5;
+    const int L = a.L, ors = L + 32;
+    const int64_t ntiles = (a.P + TP - 1) / TP;
+    for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+        const int64_t x0 = tile * TP;
+        const int np = static_cast<int>(min<int64_t>(TP, a.P - x0));
+        const int64_t o0 = a.cur_off[x0];
+        const int64_t span = a.cur_off[x0 + np] - o0;
+        const bool staged = span <= STG;
+        if (staged) {
+            const uint4* src = reinterpret_cast<const uint4*>(a.cur + o0);
+            for (int c = tid; 16 * c < span; c += 256) reinterpret_cast<uint4*>(stage)[c] = src[c];
+        }
+        if (tid < np) {
+            const int64_t x = x0 + tid;
+            const uint32_t g = a.geo[x];
+            const int64_t ro = a.cur_off[x];
+            s_ro[tid] = static_cast<int>(ro - o0);
+            s_rw[tid] = static_cast<int>(a.cur_off[x + 1] - ro);
+            const int f = static_cast<int>(g >> 16 & 0xff);
+            const int k = f == 1 ? static_cast<int>(g & 0xff) : 1;
+            s_kn[tid] = f == 1 ? static_cast<int>(g & 0xffff) : (f == 2 ? -1 : 0);
+            s_S[tid] = (L + 2 + k - 1) / k;
+        }
+        __syncthreads();
+        // lengths (one thread per packet) and the systematic bytes (a half-wave per packet)
+        if (tid < np) {
+            const int64_t x = x0 + tid;
+            const int kn = s_kn[tid];
+            int ln = 0;
+            if (kn > 0) {
+                const int k = kn & 0xff, n = kn >> 8, rw = s_rw[tid];
+                const uint8_t* lrow = stage + s_ro[tid];
+                const uint8_t* grow = a.cur + o0 + s_ro[tid];
+                const int p1 = k > 1 ? 1 : n;
+                const int h0 = rw > 0 ? (staged ? lrow[0] : grow[0]) : 0;
+                const int h1 = p1 < rw ? (staged ? lrow[p1] : grow[p1]) : 0;
+                const int hdr = h0 * 256 + h1;
+                ln = (a.geo[x] >> 24) ? min(hdr, L) : hdr;
+            }
+            if (kn >= 0) a.out_len[x] = ln;
+            s_cp[tid] = min(ln, L);
+        }
+        if (staged) {
+            for (int pp = hw; pp < np; pp += 8) {
+                const int kn = s_kn[pp];
+                if (kn <= 0) continue;
+                const int k = kn & 0xff, n = kn >> 8, S = s_S[pp];
+                const int ro = s_ro[pp];
+                uint8_t* orow = otile + pp * ors + 6;  // byte q of the packet's [header, payload]
+                for (int s = l32; s < S; s += 32) {
+                    const int aa = ro + s * n;
+                    const uint32_t* src = reinterpret_cast<const uint32_t*>(stage + (aa & ~3));
+                    const uint32_t d0 = src[0], d1 = src[1], d2 = src[2], d3 = src[3];
+                    const int sh = aa & 3;
+                    const uint32_t w0 = __builtin_amdgcn_alignbyte(d1, d0, sh);
+                    const uint32_t w1 = __builtin_amdgcn_alignbyte(d2, d1, sh);
+                    const uint32_t w2 = __builtin_amdgcn_alignbyte(d3, d2, sh);
+                    uint8_t* dst = orow + s * k;
+                    // reverse order: bytes past k (the next sub-stream's) are overwritten later
+                    dst[11] = static_cast<uint8_t>(w2 >> 24);
+                    dst[10] = static_cast<uint8_t>(w2 >> 16);
+                    dst[9] = static_cast<uint8_t>(w2 >> 8);
+                    dst[8] = static_cast<uint8_t>(w2);
+                    dst[7] = static_cast<uint8_t>(w1 >> 24);
+                    dst[6] = static_cast<uint8_t>(w1 >> 16);
+                    dst[5] = static_cast<uint8_t>(w1 >> 8);
+                    dst[4] = static_cast<uint8_t>(w1);
+                    dst[3] = static_cast<uint8_t>(w0 >> 24);
+                    dst[2] = static_cast<uint8_t>(w0 >> 16);
+                    dst[1] = static_cast<uint8_t>(w0 >> 8);
+                    dst[0] = static_cast<uint8_t>(w0);
+                }
+            }
+        } else {
+            // rows wider than the stage (k <= 3): byte gathers from HBM into the output tile
+            const int L4 = (L + 3) >> 2;
+            for (int d = tid; d < np * L4; d += 256) {
+                const int p = d / L4, w = d - p * L4;
+                const int kn = s_kn[p];
+                if (kn <= 0) continue;
+                const int k = kn & 0xff, n = kn >> 8, rw = s_rw[p];
+                const uint8_t* grow = a.cur + o0 + s_ro[p];
+                const int h = 4 * w + 2;
+                int sidx = h / k, i = h - sidx * k;
+                uint32_t val = 0;
+                for (int e = 0; e < 4; ++e) {
+                    const int pos = sidx * n + i;
+                    if (pos < rw) val |= static_cast<uint32_t>(grow[pos]) << (8 * e);
+                    if (++i == k) {
+                        i = 0;
+                        ++sidx;
+                    }
+                }
+                *reinterpret_cast<uint32_t*>(otile + p * ors + 8 + 4 * w) = val;
+            }
+        }
+        __syncthreads();
+        // the tile's payload rows, one contiguous run: bytes past a packet's copied length zero;
+        // recovered packets' rows are fec_vr_recover_kernel's
+        const int ob = np * L;
+        uint8_t* dst = a.out + x0 * L;
+        for (int o = 16 * tid; o < ob; o += 16 * 256) {
+            uint32_t v[4];
+            bool skip[4], any_skip = false;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int oq = o + 4 * q;
+                const int p = oq / L, off = oq - p * L;
+                const int kn = s_kn[p];
+                skip[q] = kn < 0;
+                any_skip |= skip[q];
+                v[q] = *reinterpret_cast<const uint32_t*>(otile + p * ors + 8 + off) & keep_bytes(s_cp[p] - off);
+            }
+            if (!any_skip) {
+                *reinterpret_cast<uint4*>(dst + o) = make_uint4(v[0], v[1], v[2], v[3]);
+            } else {
+#pragma unroll
+                for (int q = 0; q < 4; ++q)
+                    if (!skip[q]) *reinterpret_cast<uint32_t*>(dst + o + 4 * q) = v[q];
+            }
+        }
+        __syncthreads();
+    }
+}
+
+// ---- V2: V1 with persistent workgroups; the next tile's rows are loaded into registers while the
+// current one is worked on -------------------------------------------------------------------
+template <int TP, int STG>
+__global__ __launch_bounds__(256) void copy_v2(Args a) {
+    constexpr int NR = STG / 4096;  // 16-byte loads per thread for a full stage
+    __shared__ __attribute__((aligned(16))) uint8_t stage[STG + 16];
+    extern __shared__ __attribute__((aligned(16))) uint8_t otile[];
+    __shared__ int s_ro[TP], s_rw[TP], s_kn[TP], s_cp[TP], s_S[TP];
+    const int tid = threadIdx.x, l32 = tid & 31, hw = tid >> 5;
+    const int L = a.L, ors = L + 32;
+    const int64_t ntiles = (a.P + TP - 1) / TP;
+    int64_t tile = blockIdx.x;
+    if (tile >= ntiles) return;
+    uint4 rg[NR];
+    int64_t n_o0 = 0, n_span = 0;
+    auto prefetch = [&](int64_t t) {
+        const int64_t x0 = t * TP;
+        const int np = static_cast<int>(min<int64_t>(TP, a.P - x0));
+        n_o0 = a.cur_off[x0];
+        n_span = a.cur_off[x0 + np] - n_o0;
+        if (n_span <= STG) {
+            const uint4* src = reinterpret_cast<const uint4*>(a.cur + n_o0);
+#pragma unroll
+            for (int j = 0; j < NR; ++j) {
+                const int c = tid + 256 * j;
+                if (16 * c < n_span) rg[j] = src[c];
+            }
+        }
+    };
+    prefetch(tile);
+    for (; tile < ntiles; tile += gridDim.x) {
+        const int64_t x0 = tile * TP;
+        const int np = static_cast<int>(min<int64_t>(TP, a.P - x0));
+        const int64_t o0 = n_o0, span = n_span;
+        const bool staged = span <= STG;
+        if (staged) {
+#pragma unroll
+            for (int j = 0; j < NR; ++j) {
+                const int c = tid + 256 * j;
+                if (16 * c < span) reinterpret_cast<uint4*>(stage)[c] = rg[j];
+            }
+        }
+        if (tid < np) {
+            const int64_t x = x0 + tid;
+            const uint32_t g = a.geo[x];
+            const int64_t ro = a.cur_off[x];
+            s_ro[tid] = static_cast<int>(ro - o0);
+            s_rw[tid] = static_cast<int>(a.cur_off[x + 1] - ro);
+            const int f = static_cast<int>(g >> 16 & 0xff);
+            const int k = f == 1 ? static_cast<int>(g & 0xff) : 1;
+            s_kn[tid] = f == 1 ? static_cast<int>(g & 0xffff) : (f == 2 ? -1 : 0);
+            s_S[tid] = (L + 2 + k - 1) / k;
+        }
+        __syncthreads();
+        if (tile + gridDim.x < ntiles) prefetch(tile + gridDim.x);
+        if (tid < np) {
+            const int64_t x = x0 + tid;
+            const int kn = s_kn[tid];
+            int ln = 0;
+            if (kn > 0) {
+                const int k = kn & 0xff, n = kn >> 8, rw = s_rw[tid];
+                const uint8_t* lrow = stage + s_ro[tid];
+                const uint8_t* grow = a.cur + o0 + s_ro[tid];
+                const int p1 = k > 1 ? 1 : n;
+                const int h0 = rw > 0 ? (staged ? lrow[0] : grow[0]) : 0;
+                const int h1 = p1 < rw ? (staged ? lrow[p1] : grow[p1]) : 0;
+                const int hdr = h0 * 256 + h1;
+                ln = (a.geo[x] >> 24) ? min(hdr, L) : hdr;
+            }
+            if (kn >= 0) a.out_len[x] = ln;
+            s_cp[tid] = min(ln, L);
+        }
+        if (staged) {
+            for (int pp = hw; pp < np; pp += 8) {
+                const int kn = s_kn[pp];
+                if (kn <= 0) continue;
+                const int k = kn & 0xff, n = kn >> 8, S = s_S[pp];
+                const int ro = s_ro[pp];
+                uint8_t* orow = otile + pp * ors + 6;
+                for (int s = l32; s < S; s += 32) {
+                    const int aa = ro + s * n;
+                    const uint32_t* src = reinterpret_cast<const uint32_t*>(stage + (aa & ~3));
+                    const uint32_t d0 = src[0], d1 = src[1], d2 = src[2], d3 = src[3];
+                    const int sh = aa & 3;
+                    const uint32_t w0 = __builtin_amdgcn_alignbyte(d1, d0, sh);
+                    const uint32_t w1 = __builtin_amdgcn_alignbyte(d2, d1, sh);
+                    const uint32_t w2 = __builtin_amdgcn_alignbyte(d3, d2, sh);
+                    uint8_t* dst = orow + s * k;
+                    dst[11] = static_cast<uint8_t>(w2 >> 24);
+                    dst[10] = static_cast<uint8_t>(w2 >> 16);
+                    dst[9] = static_cast<uint8_t>(w2 >> 8);
+                    dst[8] = static_cast<uint8_t>(w2);
+                    dst[7] = static_cast<uint8_t>(w1 >> 24);
+                    dst[6] = static_cast<uint8_t>(w1 >> 16);
+                    dst[5] = static_cast<uint8_t>(w1 >> 8);
+                    dst[4] = static_cast<uint8_t>(w1);
+                    dst[3] = static_cast<uint8_t>(w0 >> 24);
+                    dst[2] = static_cast<uint8_t>(w0 >> 16);
+                    dst[1] = static_cast<uint8_t>(w0 >> 8);
+                    dst[0] = static_cast<uint8_t>(w0);
+                }
+            }
+        } else {
+            const int L4 = (L + 3) >> 2;
+            for (int d = tid; d < np * L4; d += 256) {
+                const int p = d / L4, w = d - p * L4;
+                const int kn = s_kn[p];
+                if (kn <= 0) continue;
+                const int k = kn & 0xff, n = kn >> 8, rw = s_rw[p];
+                const uint8_t* grow = a.cur + o0 + s_ro[p];
+                const int h = 4 * w + 2;
+                int sidx = h / k, i = h - sidx * k;
+                uint32_t val = 0;
+                for (int e = 0; e < 4; ++e) {
+                    const int pos = sidx * n + i;
+                    if (pos < rw) val |= static_cast<uint32_t>(grow[pos]) << (8 * e);
+                    if (++i == k) {
+                        i = 0;
+                        ++sidx;
+                    }
+                }
+                *reinterpret_cast<uint32_t*>(otile + p * ors + 8 + 4 * w) = val;
+            }
+        }
+        __syncthreads();
+        const int ob = np * L;
+        uint8_t* dst = a.out + x0 * L;
+        for (int o = 16 * tid; o < ob; o += 16 * 256) {
+            uint32_t v[4];
+            bool skip[4], any_skip = false;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int oq = o + 4 * q;
+                const int p = oq / L, off = oq - p * L;
+                skip[q] = s_kn[p] < 0;
+                any_skip |= skip[q];
+                v[q] = *reinterpret_cast<const uint32_t*>(otile + p * ors + 8 + off) & keep_bytes(s_cp[p] - off);
+            }
+            if (!any_skip) {
+                *reinterpret_cast<uint4*>(dst + o) = make_uint4(v[0], v[1], v[2], v[3]);
+            } else {
+#pragma unroll
+                for (int q = 0; q < 4; ++q)
+                    if (!skip[q]) *reinterpret_cast<uint32_t*>(dst + o + 4 * q) = v[q];
+            }
+        }
+        __syncthreads();
+    }
+}
+
+static std::vector<uint8_t> read_file(const std::string& path) {
+    FILE* f = std::fopen(path.c_str(), "rb");
+    if (!f) {
+        std::fprintf(stderr, "cannot open %s (run tools/vr_dump.py)\n", path.c_str());
+        std::exit(1);
+    }
+    std::fseek(f, 0, SEEK_END);
+    const long n = std::ftell(f);
+    std::fseek(f, 0, SEEK_SET);
+    std::vector<uint8_t> b(static_cast<size_t>(n));
+    if (std::fread(b.data(), 1, b.size(), f) != b.size()) std::exit(1);
+    std::fclose(f);
+    return b;
+}
+
+int main(int argc, char** argv) {
+    const std::string dir = argc > 1 ? argv[1] : "tools/ubench/data";
+    const auto geo_b = read_file(dir + "/vr_geo.bin");
+    const auto off_b = read_file(dir + "/vr_curoff.bin");
+    const int64_t P = static_cast<int64_t>(geo_b.size() / 4);
+    const int64_t rows = static_cast<int64_t>(off_b.size() / 8) - 1;
+    const int64_t* hoff = reinterpret_cast<const int64_t*>(off_b.data());
+    const int64_t cur_bytes = hoff[rows];
+    const int L = 300;
+    std::printf("P %ld, rows %ld, cur %ld bytes (%.1f per row)\n", static_cast<long>(P), static_cast<long>(rows),
+                static_cast<long>(cur_bytes), static_cast<double>(cur_bytes) / rows);
+    std::vector<uint8_t> hcur(static_cast<size_t>(cur_bytes));
+    uint64_t st = 0x12345;
+    for (auto& c : hcur) {
+        st = st * 6364136223846793005ull + 1442695040888963407ull;
+        c = static_cast<uint8_t>(st >> 56);
+    }
+    // plausible headers: every row's first two systematic bytes give a length <= L (as encoded)
+    uint8_t *cur, *out0, *out1;
+    int64_t* off;
+    uint32_t* geo;
+    int32_t *len0, *len1;
+    CHECK(hipMalloc(&cur, cur_bytes + 64));
+    CHECK(hipMalloc(&off, off_b.size()));
+    CHECK(hipMalloc(&geo, geo_b.size()));
+    CHECK(hipMalloc(&out0, P * L));
+    CHECK(hipMalloc(&out1, P * L));
+    CHECK(hipMalloc(&len0, P * 4));
+    CHECK(hipMalloc(&len1, P * 4));
+    CHECK(hipMemcpy(cur, hcur.data(), cur_bytes, hipMemcpyHostToDevice));
+    CHECK(hipMemcpy(off, off_b.data(), off_b.size(), hipMemcpyHostToDevice));
+    CHECK(hipMemcpy(geo, geo_b.data(), geo_b.size(), hipMemcpyHostToDevice));
+    CHECK(hipMemset(out0, 0x55, P * L));
+    CHECK(hipMemset(out1, 0x55, P * L));
+    CHECK(hipMemset(len0, 0, P * 4));
+    CHECK(hipMemset(len1, 0, P * 4));
+    hipEvent_t e0, e1;
+    CHECK(hipEventCreate(&e0));
+    CHECK(hipEventCreate(&e1));
+    const double bytes = static_cast<double>(cur_bytes) + P * (L + 4.0 + 4 + 8);
+    auto timeit = [&](const char* name, auto launch) {
+        float best = 1e9f, sum = 0;
+        for (int r = 0; r < 30; ++r) {
+            CHECK(hipEventRecord(e0));
+            launch();
+            CHECK(hipEventRecord(e1));
+            CHECK(hipEventSynchronize(e1));
+            float ms;
+            CHECK(hipEventElapsedTime(&ms, e0, e1));
+            if (r >= 5) {
+                best = ms < best ? ms : best;
+                sum += ms;
+            }
+        }
+        std::printf("%-34s best %7.1f us  mean %7.1f us  %5.2f TB/s\n", name, best * 1e3, sum / 25 * 1e3,
+                    bytes / (best * 1e-3) / 1e12);
+    };
+    Args a0{cur, off, geo, P, L, out0, len0};
+    Args a1{cur, off, geo, P, L, out1, len1};
+    const unsigned grid = static_cast<unsigned>((P + kTP - 1) / kTP);
+    timeit("V0 product (dword gathers)", [&] { hipLaunchKernelGGL(copy_v0, dim3(grid), dim3(256), 0, 0, a0); });
+    int64_t total_bad = 0;
+    auto check_v = [&](const char* name) {
+        std::vector<uint8_t> h0(P * L), h1(P * L);
+        std::vector<int32_t> l0(P), l1(P);
+        CHECK(hipMemcpy(h0.data(), out0, P * L, hipMemcpyDeviceToHost));
+        CHECK(hipMemcpy(h1.data(), out1, P * L, hipMemcpyDeviceToHost));
+        CHECK(hipMemcpy(l0.data(), len0, P * 4, hipMemcpyDeviceToHost));
+        CHECK(hipMemcpy(l1.data(), len1, P * 4, hipMemcpyDeviceToHost));
+        const uint32_t* hg = reinterpret_cast<const uint32_t*>(geo_b.data());
+        int64_t bad = 0;
+        for (int64_t x = 0; x < P; ++x) {
+            if (((hg[x] >> 16) & 0xff) == 2) continue;  // recovered rows: not the copy's
+            if (l0[x] != l1[x] || std::memcmp(&h0[x * L], &h1[x * L], L)) ++bad;
+        }
+        std::printf("    %s vs V0: %ld packets differ\n", name, static_cast<long>(bad));
+        total_bad += bad;
+        CHECK(hipMemset(out1, 0x55, P * L));
+        CHECK(hipMemset(len1, 0, P * 4));
+    };
+    const unsigned g32 = static_cast<unsigned>((P + 31) / 32);
+    timeit("V1 sub-stream lanes, TP 16", [&] {
+        hipLaunchKernelGGL((copy_v1<16, 16384>), dim3(grid), dim3(256), 16 * (L + 32), 0, a1);
+    });
+    check_v("V1/16");
+    timeit("V1 TP 32, 16 KB stage", [&] {
+        hipLaunchKernelGGL((copy_v1<32, 16384>), dim3(g32), dim3(256), 32 * (L + 32), 0, a1);
+    });
+    check_v("V1/32/16K");
+    timeit("V1 TP 32, 32 KB stage", [&] {
+        hipLaunchKernelGGL((copy_v1<32, 32768>), dim3(g32), dim3(256), 32 * (L + 32), 0, a1);
+    });
+    check_v("V1/32/32K");
+    for (int G : {1024, 1792, 2048, 3072}) {
+        char nm[64];
+        std::snprintf(nm, sizeof nm, "V2 persistent TP 16, grid %d", G);
+        timeit(nm, [&] {
+            hipLaunchKernelGGL((copy_v2<16, 16384>), dim3(G), dim3(256), 16 * (L + 32), 0, a1);
+        });
+        check_v(nm);
+    }
+    for (int G : {512, 768, 1024}) {
+        char nm[64];
+        std::snprintf(nm, sizeof nm, "V2 persistent TP 32 (16K), grid %d", G);
+        timeit(nm, [&] {
+            hipLaunchKernelGGL((copy_v2<32, 16384>), dim3(G), dim3(256), 32 * (L + 32), 0, a1);
+        });
+        check_v(nm);
+    }
+    return total_bad ? 1 : 0;
+    // compare
+    std::vector<uint8_t> h0(P * L), h1(P * L);
+    std::vector<int32_t> l0(P), l1(P);
+    CHECK(hipMemcpy(h0.data(), out0, P * L, hipMemcpyDeviceToHost));
+    CHECK(hipMemcpy(h1.data(), out1, P * L, hipMemcpyDeviceToHost));
+    CHECK(hipMemcpy(l0.data(), len0, P * 4, hipMemcpyDeviceToHost));
+    CHECK(hipMemcpy(l1.data(), len1, P * 4, hipMemcpyDeviceToHost));
+    const uint32_t* hg = reinterpret_cast<const uint32_t*>(geo_b.data());
+    int64_t bad = 0;
+    for (int64_t x = 0; x < P; ++x) {
+        if (((hg[x] >> 16) & 0xff) == 2) continue;  // recovered rows: not the copy's
+        if (l0[x] != l1[x] || std::memcmp(&h0[x * L], &h1[x * L], L)) {
+            if (bad < 5) std::printf("packet %ld differs (len %d vs %d, k %u)\n", static_cast<long>(x), l0[x], l1[x], hg[x] & 0xff);
+            ++bad;
+        }
+    }
+    std::printf("V1 vs V0: %ld packets differ\n", static_cast<long>(bad));
+    return bad ? 1 : 0;
+}

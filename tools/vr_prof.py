@@ -31,7 +31,17 @@ for name, f in [("encode", lambda: v.encode(pl, frames=frames)),
     for _ in range(reps):
         f()
     torch.cuda.synchronize()
-    print(f"{name}: {(time.perf_counter() - t0) / reps * 1e3:.3f} ms", flush=True)
+    t1 = time.perf_counter()
+    print(f"{name}: {(t1 - t0) / reps * 1e3:.3f} ms", flush=True)
+    # host side alone: the calls enqueued behind a 20 ms spin kernel, so that none of them starts
+    # meanwhile (a launch-bound call takes about this long per call whatever its kernels do)
+    torch.cuda._sleep(int(2e9 * 0.02))
+    t0 = time.perf_counter()
+    for _ in range(min(reps, 10)):
+        f()
+    t1 = time.perf_counter()
+    torch.cuda.synchronize()
+    print(f"{name} enqueue: {(t1 - t0) / min(reps, 10) * 1e3:.3f} ms per call", flush=True)
 t0 = time.perf_counter()
 for _ in range(reps):
     VrPlan(pat, P, light=True)
