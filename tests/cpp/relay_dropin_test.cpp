@@ -226,52 +226,69 @@ struct Trace {
     std::vector<int> flags;
 };
 
-// The chain: source encoders (the old code (T1,N1) from seq 0, a new one (T2,N2) from seq s0 when
-// s0 >= 0: both run for T_TOT+1 packets, the relay double codes them, then the new one alone),
-// hop-1 erasures e1 (both codewords of a seq are lost together), the relay, hop-2 erasures e2,
-// the destination.  Relay frame = [size_cur BE16][cur part][old part] (:1530-1571).
+// A code schedule: entry i's source code (T_i, N_i, N_i) starts at seq s_i (s_0 = 0, and
+// s_{i+1} >= s_i + T_TOT + 1: the encoder double codes the T_TOT + 1 packets from a switch,
+// Variable_Rate_FEC_Encoder.cpp:74-235, and cannot switch again before that ends).
+struct Switch {
+    int seq, T, N;
+};
+
+// The chain: per seq t the source encoder(s) of the schedule, hop-1 erasures e1 (both codewords of
+// a seq are lost together), the relay, hop-2 erasures e2, the destination.  During double coding
+// the relay runs two objects -- the old code's and a new one for the new code (:1437-1456) -- and
+// sends [BE16 size_cur][new code's part][old code's part] (:1502-1571); the destination's old
+// object reports, the new one decodes the new part (:1823-1873); at the end both nodes copy the
+// new object into the main one (copy_elements, :1423-1433).  Th2 >= 0: the hop-2 code of a
+// one-entry schedule (n2 = Th2 + 1 <= n).
 template <class SW>
-Trace chain(int R, int T1, int N1, int T2, int N2, int s0, int Th2, int P, const std::vector<unsigned char>& e1,
+Trace chain(int R, const std::vector<Switch>& sched, int Th2, int P, const std::vector<unsigned char>& e1,
             const std::vector<unsigned char>& e2) {
-    const Code c_old = code(T1, N1, Th2), c_new = code(T2, N2);
-    or_encoder* eo = or_encoder_new(L, T1, N1, N1);
-    or_encoder* en = s0 >= 0 ? or_encoder_new(L, T2, N2, N2) : nullptr;
-    SW* relay = new SW(L);
+    const int ns = static_cast<int>(sched.size());
+    std::vector<Code> codes;
+    for (int i = 0; i < ns; ++i) codes.push_back(code(sched[i].T, sched[i].N, ns == 1 ? Th2 : -1));
+    auto mk = [&](int i, bool with_encoder) {
+        SW* w = new SW(L);
+        const Code& c = codes[static_cast<size_t>(i)];
+        w->decoder_current = new Decoder(c.n - 1, c.n - c.k, c.n - c.k, L);
+        if (with_encoder) w->encoder_current = new Encoder(c.n - 1, c.n - c.k, c.n - c.k, L);
+        return w;
+    };
+    std::vector<or_encoder*> enc(static_cast<size_t>(ns), nullptr);
+    enc[0] = or_encoder_new(L, sched[0].T, sched[0].N, sched[0].N);
+    SW* relay = mk(0, true);
     SW* relay_new = nullptr;
-    SW* dest = new SW(L);
+    SW* dest = mk(0, false);
     SW* dest_new = nullptr;
-    relay->decoder_current = new Decoder(c_old.n - 1, c_old.n - c_old.k, c_old.n - c_old.k, L);
-    relay->encoder_current = new Encoder(c_old.n - 1, c_old.n - c_old.k, c_old.n - c_old.k, L);
-    dest->decoder_current = new Decoder(c_old.n - 1, c_old.n - c_old.k, c_old.n - c_old.k, L);
-    Code cur = c_old;
-    const int end_dc = s0 + TT;  // seq_end_double_coding = start + T_TOT + 1 - 1 (:1438)
+    int ci = 0;  // the schedule entry of the newest code
     std::vector<unsigned char> payload(L), cwo(8192), cwn(8192);
     Trace tr;
     for (int t = 0; t < P; ++t) {
-        or_fill_payload(payload.data(), t, 1, L, 0x5EED);
-        const bool dc = s0 >= 0 && t >= s0 && t <= end_dc;
-        const bool only_new = s0 >= 0 && t > end_dc;
-        if (!only_new) or_encoder_transmit(eo, payload.data(), L, t, cwo.data());
-        if (dc || only_new) or_encoder_transmit(en, payload.data(), L, t, cwn.data());
-        if (s0 >= 0 && t == s0) {  // a new relay object for the new code (:1437-1456)
-            relay_new = new SW(L);
-            relay_new->decoder_current = new Decoder(c_new.n - 1, c_new.n - c_new.k, c_new.n - c_new.k, L);
-            relay_new->encoder_current = new Encoder(c_new.n - 1, c_new.n - c_new.k, c_new.n - c_new.k, L);
-            dest_new = new SW(L);
-            dest_new->decoder_current = new Decoder(c_new.n - 1, c_new.n - c_new.k, c_new.n - c_new.k, L);
+        if (ci + 1 < ns && t == sched[static_cast<size_t>(ci) + 1].seq) {  // a switch: new objects
+            ++ci;
+            enc[static_cast<size_t>(ci)] = or_encoder_new(L, sched[ci].T, sched[ci].N, sched[ci].N);
+            relay_new = mk(ci, true);
+            dest_new = mk(ci, false);
         }
-        if (s0 >= 0 && t == end_dc + 1) {  // end of double coding: the new objects take over (:1423-1433)
+        const int s0 = sched[static_cast<size_t>(ci)].seq;
+        if (ci > 0 && t == s0 + TT + 1) {  // end of double coding: the new objects take over
             relay->copy_elements(relay_new, true);
             dest->copy_elements(dest_new, false);
             delete relay_new;
             delete dest_new;
             relay_new = dest_new = nullptr;
-            cur = c_new;
+            or_encoder_free(enc[static_cast<size_t>(ci) - 1]);
+            enc[static_cast<size_t>(ci) - 1] = nullptr;
         }
+        const bool dc = ci > 0 && t <= s0 + TT;  // seq_end_double_coding = start + T_TOT (:1438)
+        const Code& c_new = codes[static_cast<size_t>(ci)];
+        const Code& c_old = codes[static_cast<size_t>(dc ? ci - 1 : ci)];
+        or_fill_payload(payload.data(), t, 1, L, 0x5EED);
+        or_encoder_transmit(enc[static_cast<size_t>(ci)], payload.data(), L, t, cwn.data());
+        if (dc) or_encoder_transmit(enc[static_cast<size_t>(ci) - 1], payload.data(), L, t, cwo.data());
         const bool lost1 = e1[t] != 0;
         std::vector<unsigned char> frame(2);
         int size_cur;
-        if (dc) {  // :1502-1571: the old code's object gets the old codeword, the new one the new
+        if (dc) {  // the old code's object gets the old codeword, the new one the new
             std::vector<unsigned char> pn, po;
             relay_step(relay_new, R, c_new, lost1 ? nullptr : cwn.data(), pn);
             relay_step(relay, R, c_old, lost1 ? nullptr : cwo.data(), po);
@@ -280,14 +297,12 @@ Trace chain(int R, int T1, int N1, int T2, int N2, int s0, int Th2, int P, const
             frame.insert(frame.end(), po.begin(), po.end());
         } else {
             std::vector<unsigned char> pc;
-            relay_step(relay, R, cur, lost1 ? nullptr : (only_new ? cwn.data() : cwo.data()), pc);
-            size_cur = rd_size(cur);
+            relay_step(relay, R, c_new, lost1 ? nullptr : cwn.data(), pc);
+            size_cur = rd_size(c_new);
             frame.insert(frame.end(), pc.begin(), pc.end());
         }
         frame[0] = static_cast<unsigned char>(size_cur / 256);
         frame[1] = static_cast<unsigned char>(size_cur % 256);
-        // destination: during double coding the old object decodes the old part and reports, the
-        // new one decodes the new part (:1823-1873)
         const bool lost2 = e2[t] != 0;
         const int hdr = R == 3 ? TT + 1 : 0;
         std::vector<unsigned char> out(static_cast<size_t>(L + 32), 0);
@@ -299,14 +314,14 @@ Trace chain(int R, int T1, int N1, int T2, int N2, int s0, int Th2, int P, const
             std::vector<unsigned char> tmp(static_cast<size_t>(L + 32), 0);
             dest_step(dest_new, R, c_new, pn, tmp.data());
         } else {
-            flag = dest_step(dest, R, cur, lost2 ? nullptr : frame.data() + 2, out.data());
+            flag = dest_step(dest, R, c_new, lost2 ? nullptr : frame.data() + 2, out.data());
         }
         tr.frames.push_back(frame);
         tr.outs.push_back(out);
         tr.flags.push_back(flag);
     }
-    or_encoder_free(eo);
-    if (en) or_encoder_free(en);
+    for (auto* e : enc)
+        if (e) or_encoder_free(e);
     delete relay;
     delete relay_new;
     delete dest;
@@ -343,7 +358,7 @@ int compare(const char* what, const Trace& a, const Trace& b, int P) {
 template <class SW>
 int fixed_vs_oracle_run(int R, int T1, int N1, int T2, int N2, int P) {
     const auto e1 = pattern(P, 7, 30, 173), e2 = pattern(P, 11, 25, 211);
-    const Trace d = chain<SW>(R, T1, N1, T1, N1, -1, T2, P, e1, e2);
+    const Trace d = chain<SW>(R, {{0, T1, N1}}, T2, P, e1, e2);
     const Code c = code(T1, N1, T2);
     const int F = 2 + (R == 3 ? TT + 1 : 0) + rd_size(c);
     std::vector<unsigned char> frames(static_cast<size_t>(P) * F), out(static_cast<size_t>(P) * c.S * c.k),
@@ -375,8 +390,8 @@ int fixed_vs_oracle_run(int R, int T1, int N1, int T2, int N2, int P) {
 // (2) double coding: the same driver over the drop-in and over OracleSW
 int double_coding(int R, int T1, int N1, int T2, int N2, int s0, int P) {
     const auto e1 = pattern(P, 5, 20, 149), e2 = pattern(P, 9, 20, 0);
-    const Trace d = chain<siphon::Decoder_Symbol_Wise>(R, T1, N1, T2, N2, s0, -1, P, e1, e2);
-    const Trace o = chain<OracleSW>(R, T1, N1, T2, N2, s0, -1, P, e1, e2);
+    const Trace d = chain<siphon::Decoder_Symbol_Wise>(R, {{0, T1, N1}, {s0, T2, N2}}, -1, P, e1, e2);
+    const Trace o = chain<OracleSW>(R, {{0, T1, N1}, {s0, T2, N2}}, -1, P, e1, e2);
     char what[96];
     std::snprintf(what, sizeof what, "type %d (%d,%d)=>(%d,%d) at %d", R, T1, N1, T2, N2, s0);
     if (compare(what, d, o, P)) return 1;
@@ -388,17 +403,66 @@ int double_coding(int R, int T1, int N1, int T2, int N2, int s0, int P) {
 #endif
 }  // namespace
 
+// (3) a schedule from files: argv = --schedule <sched.txt> <e1.bin> <e2.bin>; sched.txt = "P" then
+// one "seq T N" line per switch (the first at seq 0); e1 / e2 = P hop erasure bytes.  Types 2 and
+// 3 over SW and over OracleSW (or over OracleSW alone, ref == nullptr: CPU build).
+std::vector<unsigned char> read_bytes(const char* path, int P) {
+    std::vector<unsigned char> v(static_cast<size_t>(P), 0);
+    FILE* f = std::fopen(path, "rb");
+    if (!f || std::fread(v.data(), 1, v.size(), f) != v.size()) {
+        std::printf("cannot read %d bytes from %s\n", P, path);
+        std::exit(2);
+    }
+    std::fclose(f);
+    return v;
+}
+template <class SW>
+int schedule_run(int argc, char** argv, bool compare_with_oracle) {
+    if (argc < 5) return 2;
+    FILE* f = std::fopen(argv[2], "r");
+    int P = 0;
+    if (!f || std::fscanf(f, "%d", &P) != 1) return 2;
+    std::vector<Switch> sched;
+    Switch w;
+    while (std::fscanf(f, "%d %d %d", &w.seq, &w.T, &w.N) == 3) sched.push_back(w);
+    std::fclose(f);
+    const auto e1 = read_bytes(argv[3], P), e2 = read_bytes(argv[4], P);
+    int rc = 0;
+    for (int R : {2, 3}) {
+        const Trace d = chain<SW>(R, sched, -1, P, e1, e2);
+        int good = 0;
+        for (int fl : d.flags) good += fl == 0;
+        if (compare_with_oracle) {
+            const Trace o = chain<OracleSW>(R, sched, -1, P, e1, e2);
+            char what[64];
+            std::snprintf(what, sizeof what, "type %d schedule", R);
+            if (compare(what, d, o, P)) {
+                rc = 1;
+                continue;
+            }
+        }
+        std::printf("type %d schedule: %zu codes, %d seqs%s, %d unflagged\n", R, sched.size(), P,
+                    compare_with_oracle ? " equal to the oracle methods" : "", good);
+    }
+    return rc;
+}
+
 #ifdef RELAY_ORACLE_ONLY
 // CPU build (tests/test_sdswdf.py): the driver over OracleSW against the oracle's chains, which
 // checks the driver and the or_sw_* methods without a GPU.
-int main() {
+int main(int argc, char** argv) {
+    if (argc > 1 && std::strcmp(argv[1], "--schedule") == 0) {
+        const int rc = schedule_run<OracleSW>(argc, argv, false);
+        if (rc == 0) std::printf("RELAY ORACLE DRIVER OK\n");
+        return rc;
+    }
     int rc = 0;
     rc |= fixed_vs_oracle_run<OracleSW>(3, 10, 3, 10, 3, 600);
     rc |= fixed_vs_oracle_run<OracleSW>(3, 10, 5, 8, 3, 400);
     rc |= fixed_vs_oracle_run<OracleSW>(2, 10, 3, 10, 3, 600);
     rc |= fixed_vs_oracle_run<OracleSW>(2, 10, 1, 10, 1, 400);
     for (int R : {2, 3}) {  // the double-coding driver runs (memory-clean under -fsanitize) over OracleSW
-        const Trace o = chain<OracleSW>(R, 10, 3, 10, 5, 200, -1, 420, pattern(420, 5, 20, 149), pattern(420, 9, 20, 0));
+        const Trace o = chain<OracleSW>(R, {{0, 10, 3}, {200, 10, 5}}, -1, 420, pattern(420, 5, 20, 149), pattern(420, 9, 20, 0));
         int good = 0;
         for (int f : o.flags) good += f == 0;
         std::printf("type %d double coding over OracleSW: %d of 420 unflagged\n", R, good);
@@ -408,8 +472,13 @@ int main() {
     return rc;
 }
 #else
-int main() {
+int main(int argc, char** argv) {
     using DSW = siphon::Decoder_Symbol_Wise;
+    if (argc > 1 && std::strcmp(argv[1], "--schedule") == 0) {
+        const int rc = schedule_run<DSW>(argc, argv, true);
+        if (rc == 0) std::printf("RELAY DROPIN OK\n");
+        return rc;
+    }
     int rc = 0;
     rc |= fixed_vs_oracle_run<DSW>(3, 10, 3, 10, 3, 600);
     rc |= fixed_vs_oracle_run<DSW>(3, 10, 5, 8, 3, 400);
