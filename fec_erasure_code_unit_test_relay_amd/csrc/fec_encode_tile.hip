@@ -679,6 +679,58 @@ const void* fec_encode_tile_kernel_for(int k, int np, int L) {
     return nullptr;
 }
 
+// Several tuples' segment walks in one launch (EncMultiArgs).  The register budget is that of 4
+// workgroups per CU (128 VGPRs), which every listed tuple's walk fits; LDS is the largest listed
+// tuple's (the launcher sizes it).
+#define FEC_ENC_TILE_MULTI_LIST(X) \
+    X(8, 3) X(11, 0) X(10, 1) X(9, 2) X(7, 4) X(6, 5) X(5, 6) X(4, 7) X(10, 3) X(9, 3) X(8, 4) X(7, 5)
+
+template <int K, int NP>
+__device__ __forceinline__ void tile_multi_case(const EncMultiArgs& m, int ti, uint8_t* smem) {
+    constexpr TileGeom CG = tile_geometry(K, NP, 300);
+    EncTileArgs a{};
+    a.payload_base = m.payload;
+    a.len_base = m.len;
+    a.ptab = m.gtab + m.toff[ti];
+    a.L = 300;
+    a.seg = m.seg;
+    a.cur_rows = m.cur_rows;
+    a.old_rows = m.old_rows;
+    a.cur_len = m.cur_len;
+    a.old_len = m.old_len;
+    a.W = (CG.CW + 15) & ~15;
+    switch (__builtin_amdgcn_readfirstlane(threadIdx.x >> 6)) {
+        case 0: tile_walk<K, NP, 0, 300, true>(a, smem); break;
+        case 1: tile_walk<K, NP, 1, 300, true>(a, smem); break;
+        case 2: tile_walk<K, NP, 2, 300, true>(a, smem); break;
+        default: tile_walk<K, NP, 3, 300, true>(a, smem); break;
+    }
+}
+
+__global__ __launch_bounds__(kTileThreads, 4) void fec_encode_tile_multi_kernel(EncMultiArgs m) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t tsmem[];
+    const int bid = static_cast<int>(blockIdx.x);
+    int ti = 0;
+    while (ti + 1 < m.ntuple && bid >= m.tfirst[ti + 1]) ++ti;
+    switch (m.tkey[ti]) {
+#define FEC_ENC_TILE_MULTI_CASE(K, NP) \
+    case K * 32 + NP: tile_multi_case<K, NP>(m, ti, tsmem); break;
+        FEC_ENC_TILE_MULTI_LIST(FEC_ENC_TILE_MULTI_CASE)
+#undef FEC_ENC_TILE_MULTI_CASE
+        default: break;
+    }
+}
+
+bool fec_encode_tile_multi_supports(int k, int np, int L) {
+    if (L != 300) return false;
+#define FEC_ENC_TILE_MULTI_HAS(K, NP) \
+    if (k == K && np == NP) return true;
+    FEC_ENC_TILE_MULTI_LIST(FEC_ENC_TILE_MULTI_HAS)
+#undef FEC_ENC_TILE_MULTI_HAS
+    return false;
+}
+const void* fec_encode_tile_multi_kernel_ptr() { return reinterpret_cast<const void*>(&fec_encode_tile_multi_kernel); }
+
 // The segment-mode instance for the variable-rate schedule (L = 300 fixed at compile time, else
 // from the arguments), or nullptr.
 const void* fec_encode_tile_seg_kernel_for(int k, int np, int L) {

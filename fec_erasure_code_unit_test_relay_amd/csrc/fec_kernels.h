@@ -135,6 +135,30 @@ const void* fec_encode_tile_kernel_for(int k, int np, int L);
 // fec_encode_tile_kernel<k, n-k, 300 or 0> with segment mode (EncTileArgs::seg) compiled in, else nullptr.
 const void* fec_encode_tile_seg_kernel_for(int k, int np, int L);
 
+// Segment mode for several (k, n-k) tuples in one launch (the variable-rate schedule at L = 300):
+// workgroup b serves segment b of the concatenated segment table; the segments of tuple t are
+// [tfirst[t], tfirst[t+1]) and it is encoded by fec_encode_tile_kernel<k_t, n_t-k_t, 300, true>'s
+// walk.  Only tuples for which fec_encode_tile_multi_supports() holds (their walk fits the shared
+// register budget of 4 workgroups per CU).
+constexpr int kEncMultiMax = 16;
+struct EncMultiArgs {
+    const uint8_t* payload;       // [sent][L] payload rows
+    const int32_t* len;           // lengths (null: all L)
+    const uint32_t* gtab;         // gf_mul4 tables of every tuple
+    const int64_t* seg;           // [nseg][6] segment table, grouped by tuple
+    uint8_t* cur_rows;
+    uint8_t* old_rows;
+    int32_t* cur_len;
+    int32_t* old_len;
+    int L;                        // 300
+    int ntuple;
+    int tkey[kEncMultiMax];       // k * 32 + (n - k)
+    int tfirst[kEncMultiMax + 1];
+    int toff[kEncMultiMax];       // dword offset of the tuple's tables in gtab
+};
+bool fec_encode_tile_multi_supports(int k, int np, int L);
+const void* fec_encode_tile_multi_kernel_ptr();
+
 struct CopyFastArgs {
     const uint8_t* cw;
     const uint8_t* er;

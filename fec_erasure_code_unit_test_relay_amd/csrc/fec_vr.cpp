@@ -1156,8 +1156,12 @@ struct fec_vr_plan {
         int toff;        // dword offset of its gf_mul4 tables in gtab
         size_t seg0;     // its first segment in d_seg
         int nseg;
+        int k, np;
+        bool multi;      // served by the one multi-tuple launch (fec_encode_tile_multi_kernel)
     };
-    std::vector<TileTuple> tiles;
+    std::vector<TileTuple> tiles;  // the multi-tuple launch's first (heaviest first), then the others
+    int n_multi = 0;               // tiles[0, n_multi): one launch, workgroup b = segment b of d_seg
+    int multi_lds = 0, multi_lds_len = 0;
     const int64_t* d_seg = nullptr;
     bool enc_ready = false, dec_ready = false, hdr_ready = false;
     Fork fork;  // side streams (declared after the uploads: destroyed, and drained, first)
@@ -1212,6 +1216,7 @@ int prepare_encode(fec_vr_plan* v, hipStream_t s) {
     int unit = 4;
     if (const char* e = std::getenv("FEC_VR_TILE_UNIT")) unit = std::max(1, std::atoi(e));
     const bool tiles_on = !std::getenv("FEC_VR_NO_TILE");
+    const bool multi_on = !std::getenv("FEC_VR_NO_MULTI");
     int tab = 32, out = 16, slot = 16, nmax = 1;
     for (size_t ei = 0; ei < p.enc.size(); ++ei) {
         const auto& e = p.enc[ei];
@@ -1229,7 +1234,7 @@ int prepare_encode(fec_vr_plan* v, hipStream_t s) {
             const void* kfn = fec::fec_encode_tile_seg_kernel_for(g.k, g.n - g.k, p.L);
             if (tiles_on && tg.ok && kfn && (p.L & 3) == 0) {
                 ti = static_cast<int>(v->tiles.size());
-                v->tiles.push_back({kfn, tg, it->second, 0, 0});
+                v->tiles.push_back({kfn, tg, it->second, 0, 0, g.k, g.n - g.k, false});
                 segs.emplace_back();
             }
             tix[key] = ti;
@@ -1259,14 +1264,38 @@ int prepare_encode(fec_vr_plan* v, hipStream_t s) {
             lo_cum.push_back(lo_cum.back() + (e.end - e.first));
         }
     }
-    std::vector<int64_t> seg;
+    // order: the tuples of the multi-tuple launch first, heaviest walk (k * (n-k)) first so that its
+    // workgroups start first; then the others by segment count, largest first
     for (size_t i = 0; i < v->tiles.size(); ++i) {
-        v->tiles[i].seg0 = seg.size() / 6;
-        v->tiles[i].nseg = static_cast<int>(segs[i].size() / 6);
-        seg.insert(seg.end(), segs[i].begin(), segs[i].end());
+        auto& t = v->tiles[i];
+        t.nseg = static_cast<int>(segs[i].size() / 6);
+        t.multi = multi_on && fec::fec_encode_tile_multi_supports(t.k, t.np, p.L);
     }
-    std::stable_sort(v->tiles.begin(), v->tiles.end(),
-                     [](const fec_vr_plan::TileTuple& x, const fec_vr_plan::TileTuple& y) { return x.nseg > y.nseg; });
+    std::vector<size_t> order(v->tiles.size());
+    for (size_t i = 0; i < order.size(); ++i) order[i] = i;
+    std::stable_sort(order.begin(), order.end(), [&](size_t x, size_t y) {
+        const auto &a = v->tiles[x], &b = v->tiles[y];
+        if (a.multi != b.multi) return a.multi;
+        return a.multi ? a.k * a.np > b.k * b.np : a.nseg > b.nseg;
+    });
+    std::vector<int64_t> seg;
+    std::vector<fec_vr_plan::TileTuple> sorted;
+    v->n_multi = 0;
+    v->multi_lds = v->multi_lds_len = 0;
+    for (size_t i : order) {
+        auto t = v->tiles[i];
+        t.seg0 = seg.size() / 6;
+        seg.insert(seg.end(), segs[i].begin(), segs[i].end());
+        if (t.multi && v->n_multi < fec::kEncMultiMax) {
+            ++v->n_multi;
+            v->multi_lds = std::max(v->multi_lds, t.tg.lds);
+            v->multi_lds_len = std::max(v->multi_lds_len, t.tg.lds_len);
+        } else {
+            t.multi = false;
+        }
+        sorted.push_back(t);
+    }
+    v->tiles.swap(sorted);
     Upload& u = v->enc_up;
     if (int st = u.begin()) return st;
     u.add(&v->d_enc_inst, inst);
@@ -1348,6 +1377,51 @@ int launch_tile_tuple(const fec_vr_plan* v, const fec_vr_plan::TileTuple& tt, co
         hipSuccess)
         return FEC_ERR_HIP;
     return FEC_OK;
+}
+
+// The tuples tiles[0, n_multi) in one launch of fec_encode_tile_multi_kernel: workgroup b serves
+// segment b of d_seg.
+int launch_tile_multi(const fec_vr_plan* v, const uint8_t* d_payload, const int32_t* d_len, uint8_t* d_cw_cur,
+                      int32_t* d_len_cur, uint8_t* d_cw_old, int32_t* d_len_old, hipStream_t s) {
+    const void* kfn = fec::fec_encode_tile_multi_kernel_ptr();
+    const int lds = d_len ? v->multi_lds_len : v->multi_lds;
+    {
+        static std::mutex mu;
+        static int raised = 0;
+        std::lock_guard<std::mutex> lk(mu);
+        if (lds > raised) {
+            if (hipFuncSetAttribute(kfn, hipFuncAttributeMaxDynamicSharedMemorySize, lds) != hipSuccess)
+                return FEC_ERR_HIP;
+            raised = lds;
+        }
+    }
+    fec::EncMultiArgs m{};
+    m.payload = d_payload;
+    m.len = d_len;
+    m.gtab = v->d_gtab;
+    m.seg = v->d_seg;
+    m.cur_rows = d_cw_cur;
+    m.old_rows = d_cw_old;
+    m.cur_len = d_len_cur;
+    m.old_len = d_len_old;
+    m.L = v->plan.L;
+    m.ntuple = v->n_multi;
+    int nwg = 0;
+    for (int i = 0; i < v->n_multi; ++i) {
+        const auto& t = v->tiles[static_cast<size_t>(i)];
+        if (static_cast<int>(t.seg0) != nwg) return FEC_ERR_ARG;  // segments in launch order
+        m.tkey[i] = t.k * 32 + t.np;
+        m.tfirst[i] = nwg;
+        m.toff[i] = t.toff;
+        nwg += t.nseg;
+    }
+    m.tfirst[v->n_multi] = nwg;
+    if (nwg <= 0) return FEC_OK;
+    void* args[] = {&m};
+    return hipLaunchKernel(kfn, dim3(static_cast<unsigned>(nwg)), dim3(256), args, static_cast<size_t>(lds), s) ==
+                   hipSuccess
+               ? FEC_OK
+               : FEC_ERR_HIP;
 }
 
 int prepare_decode(fec_vr_plan* v, hipStream_t s) {
@@ -1570,31 +1644,35 @@ int fec_vr_encode_batch(fec_vr_plan* v, const uint8_t* d_payload, const int32_t*
     auto al = [](const void* q, uintptr_t m) { return (reinterpret_cast<uintptr_t>(q) & m) == 0; };
     const bool tiled = !v->tiles.empty() && al(d_cw_cur, 15) && al(d_cw_old, 15) &&
                        al(d_payload, 3) && al(d_len_cur, 3) && al(d_len_old, 3);
-    // Independent launches on the caller's stream and the side streams: the generic encoder (a
-    // latency-bound walk over the few tuples without a tile geometry) first, on a side stream, then
-    // the tuples largest first, round robin.
+    // The tuples of the multi-tuple launch in one launch on the caller's stream; the generic encoder
+    // (a latency-bound walk over the few tuples without a tile geometry) and any other tuple on side
+    // streams, forked and joined with events (one stream with hipExtAnyOrderLaunch does not overlap
+    // launches on gfx950).
+    const int n_multi = tiled ? v->n_multi : 0;
+    const int n_side_tiles = tiled ? static_cast<int>(v->tiles.size()) - n_multi : 0;
+    const bool gen = !tiled || v->n_lo > 0;
     if (int st = v->fork.begin(s)) return st;
     ForkScope scope(v->fork);
-    hipStream_t sg = s;
-    if (tiled && v->n_lo > 0)
-        if (int st = v->fork.stream(1, &sg)) return st;
-    fec::VrEncodeArgs a{d_payload, d_payload_len, v->plan.L,
-                        tiled ? v->d_lo_inst : v->d_enc_inst, tiled ? v->d_lo_span : v->d_enc_span,
-                        tiled ? v->d_lo_cum : v->d_enc_cum,
-                        tiled ? v->n_lo : static_cast<int>(v->plan.enc.size()), tiled ? v->lo_total : v->enc_total,
-                        v->enc_tab, v->enc_out, v->enc_slot, v->enc_wave, v->d_gtab,
-                        tiled ? v->d_lo_base : v->d_enc_base, d_cw_cur, d_cw_old, d_len_cur, d_len_old};
-    if (int st = fec::vr_launch_encode(a, sg)) return st;
-    if (tiled) {
-        int i = 0;  // the largest on the caller's stream, the rest round robin after the generic one
-        for (const auto& tt : v->tiles) {  // prepare_encode sorted them by segments, descending
-            hipStream_t st_i;
-            if (int st = v->fork.stream(i == 0 || v->n_lo == 0 ? i : i + 1, &st_i)) return st;
-            ++i;
-            if (int st = launch_tile_tuple(v, tt, d_payload, d_payload_len, d_cw_cur, d_len_cur, d_cw_old, d_len_old,
-                                           st_i))
-                return st;
-        }
+    int next_side = n_multi > 0 ? 1 : 0;  // stream index 0 = the caller's
+    if (gen) {
+        hipStream_t sg;
+        if (int st = v->fork.stream(next_side++, &sg)) return st;
+        fec::VrEncodeArgs a{d_payload, d_payload_len, v->plan.L,
+                            tiled ? v->d_lo_inst : v->d_enc_inst, tiled ? v->d_lo_span : v->d_enc_span,
+                            tiled ? v->d_lo_cum : v->d_enc_cum,
+                            tiled ? v->n_lo : static_cast<int>(v->plan.enc.size()), tiled ? v->lo_total : v->enc_total,
+                            v->enc_tab, v->enc_out, v->enc_slot, v->enc_wave, v->d_gtab,
+                            tiled ? v->d_lo_base : v->d_enc_base, d_cw_cur, d_cw_old, d_len_cur, d_len_old};
+        if (int st = fec::vr_launch_encode(a, sg)) return st;
+    }
+    if (n_multi > 0)
+        if (int st = launch_tile_multi(v, d_payload, d_payload_len, d_cw_cur, d_len_cur, d_cw_old, d_len_old, s)) return st;
+    for (int i = 0; i < n_side_tiles; ++i) {
+        hipStream_t st_i;
+        if (int st = v->fork.stream(next_side++, &st_i)) return st;  // side streams round robin
+        if (int st = launch_tile_tuple(v, v->tiles[static_cast<size_t>(n_multi + i)], d_payload, d_payload_len,
+                                       d_cw_cur, d_len_cur, d_cw_old, d_len_old, st_i))
+            return st;
     }
     if (int st = scope.join()) return st;
     return v->enc_up.done_reading(s);
