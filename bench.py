@@ -377,6 +377,43 @@ def extra_configs(steps=5):
         "verified": bool(torch.equal(out4[ok4], pl[:P][ok4])) and v.lost == 2982 and
         int((ol4 == 0).sum()) == 2982 and w.lost == 2982}
     res["multistream_10k"] = multistream(steps)
+    res["relay_10_3"] = relay_chains(steps)
+    return res
+
+
+def relay_chains(steps):
+    """The Decoder_Symbol_Wise relay: source (10,3,3) codewords of 360 000 packets
+    -> relay -> destination, hop 1 erasures bin/erasure.bin, hop 2 bin/erasure2.bin, for
+    RELAYING_TYPE 2 (symbol_wise_encode_1 / decode_1) and 3 (state-dependent).  One step = relay +
+    destination of the whole batch; type 3's host planners (the reference's per-packet control
+    flow over flags and headers) are inside it.  verified: with clean hops every source packet
+    comes out of the destination at the chain's delay."""
+    import torch
+    from fec_erasure_code_unit_test_relay_amd import Codec, fill_payload
+    from fec_erasure_code_unit_test_relay_amd.relay import StateDependentRelay, SymbolWiseRelay
+    from fec_erasure_code_unit_test_relay_amd.streams import load_pattern
+    P = 360000
+    c = Codec(L, 10, 3, 3)
+    payload = fill_payload(0, P, L, 0x5EED)
+    cw, _ = c.encode(payload)
+    e1 = load_pattern("bin_erasure")[:P].astype(np.uint8)
+    e2 = load_pattern("bin_erasure2")[:P].astype(np.uint8)
+    z = np.zeros(P, dtype=np.uint8)
+    res = {"packets": P, "hops": "bin/erasure.bin, bin/erasure2.bin"}
+    r2 = SymbolWiseRelay(L, 10, 3, 10, 3)
+    e1d, e2d, zd = (torch.from_numpy(x.copy()).cuda() for x in (e1, e2, z))
+    o, df = r2.destination(r2.relay(cw, zd)[0], zd)
+    D = r2.delay
+    ok2 = bool(torch.equal(o[D:, 2:2 + L], payload[:P - D])) and int(df.sum()) == 0
+    dt2 = timed(lambda: r2.destination(r2.relay(cw, e1d)[0], e2d), steps)
+    res["type2"] = {"ms": round(dt2 * 1e3, 3), "GiB_s": round(P * L / dt2 / 2**30, 2), "verified": ok2}
+    r3 = StateDependentRelay(L, 10, 3, 10, 3)
+    o, df = r3.destination(r3.relay(cw, z), z)
+    D = r3.delay
+    ok3 = bool(torch.equal(o[D:, 2:2 + L], payload[:P - D])) and int(df.sum()) == 0
+    dt3 = timed(lambda: r3.destination(r3.relay(cw, e1), e2), max(1, min(steps, 2)))
+    res["type3"] = {"ms": round(dt3 * 1e3, 3), "GiB_s": round(P * L / dt3 / 2**30, 3), "verified": ok3,
+                    "note": "host planners included (relay and destination control flow per packet)"}
     return res
 
 

@@ -556,6 +556,16 @@ int grid_for(int64_t items) {
 }
 
 // A device buffer that only grows.
+// The frames' 11-byte headers gathered into contiguous rows [P][11] (one thread per header byte),
+// so that the destination planner's read-back is one linear copy.
+__global__ __launch_bounds__(256) void fec_sdswdf_hdr_gather_kernel(const uint8_t* frames, int64_t F, int64_t P,
+                                                                     uint8_t* hdrs) {
+    const int64_t i = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x;
+    if (i >= P * kHdr) return;
+    const int64_t r = i / kHdr;
+    hdrs[i] = frames[r * F + 2 + (i - r * kHdr)];
+}
+
 struct DevBuf {
     void* p = nullptr;
     size_t bytes = 0;
@@ -590,7 +600,7 @@ struct fec_sdswdf {
     std::unique_ptr<fec::SdDestPlanner> dest;
     std::vector<int32_t> plan;
     std::vector<uint8_t> hdrs;
-    fec::DevBuf d_plan, d_table;
+    fec::DevBuf d_plan, d_table, d_hdrs;
     ~fec_sdswdf() {
         if (hop1) fec_codec_destroy(hop1);
         if (hop2) fec_codec_destroy(hop2);
@@ -1095,9 +1105,13 @@ int fec_sdswdf_destination_batch(fec_sdswdf* w, const uint8_t* d_frames, const u
     return guarded_sd([&] {
         if (int st = ensure_device(w)) return st;
         // the frames' 11-byte headers drive the destination's control flow (:1663-1664): fetch them
-        w->hdrs.resize(static_cast<size_t>(P) * fec::kHdr);
-        if (hipMemcpy2DAsync(w->hdrs.data(), fec::kHdr, d_frames + 2, w->F, fec::kHdr, static_cast<size_t>(P),
-                             hipMemcpyDeviceToHost, s) != hipSuccess ||
+        const size_t hb = static_cast<size_t>(P) * fec::kHdr;
+        w->hdrs.resize(hb);
+        if (int st = w->d_hdrs.reserve(hb)) return st;
+        hipLaunchKernelGGL(fec::fec_sdswdf_hdr_gather_kernel, dim3(static_cast<unsigned>((hb + 255) / 256)), dim3(256),
+                           0, s, d_frames, static_cast<int64_t>(w->F), P, static_cast<uint8_t*>(w->d_hdrs.p));
+        if (hipGetLastError() != hipSuccess ||
+            hipMemcpyAsync(w->hdrs.data(), w->d_hdrs.p, hb, hipMemcpyDeviceToHost, s) != hipSuccess ||
             hipStreamSynchronize(s) != hipSuccess)
             return static_cast<int>(FEC_ERR_HIP);
         plan_dest(w, h_erasure, w->hdrs.data(), P, h_flag);
