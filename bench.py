@@ -378,6 +378,46 @@ def extra_configs(steps=5):
         int((ol4 == 0).sum()) == 2982 and w.lost == 2982}
     res["multistream_10k"] = multistream(steps)
     res["relay_10_3"] = relay_chains(steps)
+    res["per_packet_api"] = per_packet_api()
+    return res
+
+
+def per_packet_api(packets=20000):
+    """The reference's per-packet contract (FEC_Encoder::onTransmit / FEC_Decoder::onReceive, one
+    call per seq) from C: tools/stream_latency.cpp built against libfec_amd.so and run as a child
+    process, (10,3,3) with bursts of erasures; the reference's own figures are 14.37 us per
+    onTransmit and 0.48 us per fast-path onReceive on one core."""
+    import re
+    import shutil
+    import subprocess
+    import tempfile
+    from fec_erasure_code_unit_test_relay_amd import _lib
+    gxx = shutil.which("g++")
+    if gxx is None:
+        return {"skipped": "no g++"}
+    libdir = os.path.dirname(_lib.LIB_PATH)
+    with tempfile.TemporaryDirectory() as td:
+        exe = os.path.join(td, "stream_latency")
+        b = subprocess.run([gxx, "-O2", "-std=c++17", "-I", os.path.join(ROOT, "include"),
+                            os.path.join(ROOT, "tools", "stream_latency.cpp"), "-L", libdir, "-lfec_amd",
+                            f"-Wl,-rpath,{libdir}", "-o", exe], capture_output=True, text=True, timeout=120)
+        if b.returncode != 0:
+            return {"skipped": "build failed: " + b.stderr[-300:]}
+        r = subprocess.run([exe, str(packets)], capture_output=True, text=True, timeout=120)
+    out = r.stdout
+    m = re.search(r"fec_encoder_transmit ([\d.]+) us/call, fec_decoder_receive ([\d.]+) us/call "
+                  r"\((\d+) packets, (\d+) erased, (\d+) lost, (\d+) wrong\)", out)
+    if r.returncode != 0 or not m:
+        return {"skipped": "run failed: " + (r.stderr or out)[-300:]}
+    res = {"packets": int(m.group(3)), "erased": int(m.group(4)),
+           "onTransmit_us": float(m.group(1)), "onReceive_us": float(m.group(2)),
+           "reference_onTransmit_us": 14.37, "reference_onReceive_fast_path_us": 0.48,
+           "verified": int(m.group(6)) == 0}
+    for key, pat in (("onReceive_received_output", r"output received.*?mean ([\d.]+) p50 ([\d.]+) p99 ([\d.]+)"),
+                     ("onReceive_recovered_output", r"output erased.*?mean ([\d.]+) p50 ([\d.]+) p99 ([\d.]+)")):
+        q = re.search(pat, out)
+        if q:
+            res[key] = {"mean_us": float(q.group(1)), "p50_us": float(q.group(2)), "p99_us": float(q.group(3))}
     return res
 
 
