@@ -1277,9 +1277,19 @@ hipError_t server_wait(ServerHost& sv, uint32_t ticket, hipStream_t s, bool pers
         if (b->done == ticket) {
             std::atomic_thread_fence(std::memory_order_acquire);
             if (!persistent) {
-                const hipError_t e = hipStreamSynchronize(s);
+                // a one-shot launch answers, then makes its exit final (exited = 1) as its last
+                // write to the box; whatever it does after that (an encoder's state write-back)
+                // goes to its own device memory, ordered before the next launch on its stream.
+                // So the box is free once exited = 1: no stream synchronisation on the call path.
+                for (uint32_t j = 1; !b->exited; ++j) {
+                    if ((j & 4095) == 0) {
+                        if (hipError_t e = hipStreamQuery(s); e != hipSuccess && e != hipErrorNotReady) return e;
+                        if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(10))
+                            return hipErrorLaunchTimeOut;
+                    }
+                    __builtin_ia32_pause();
+                }
                 sv.live = false;
-                return e;
             }
             return hipSuccess;
         }
