@@ -1231,7 +1231,10 @@ hipError_t server_settle(ServerHost& sv, uint32_t ticket, hipStream_t s, bool* e
         }
         __builtin_ia32_pause();
     }
-    const hipError_t e = hipStreamSynchronize(s);
+    // exited = 1 is the launch's last write to the box (its state write-back, if any, goes to device
+    // memory and is ordered before the stream's next launch): the box is free without a stream
+    // synchronisation.  Only the time limit above falls back to one.
+    const hipError_t e = b->exited ? hipSuccess : hipStreamSynchronize(s);
     sv.live = false;
     server_unregister(sv);
     *ended = true;
@@ -1294,12 +1297,12 @@ hipError_t server_wait(ServerHost& sv, uint32_t ticket, hipStream_t s, bool pers
             return hipSuccess;
         }
         if ((i & 1023) == 0) {
-            if (b->exited) {  // the server is gone without this request's answer
-                const hipError_t e = hipStreamSynchronize(s);
+            if (b->exited) {  // the server is gone without this request's answer (exited = 1: its last box write)
+                std::atomic_thread_fence(std::memory_order_acquire);
                 sv.live = false;
                 server_unregister(sv);
                 if (b->done == ticket) continue;
-                if (e != hipSuccess) return e;
+                if (hipError_t e = hipStreamQuery(s); e != hipSuccess && e != hipErrorNotReady) return e;
                 if (++relaunches > 8) return hipErrorLaunchFailure;
                 if (hipError_t e2 = server_start(sv, ticket - 1, persistent, launch)) return e2;
                 continue;
