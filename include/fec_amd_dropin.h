@@ -48,6 +48,8 @@ class Memory_Allocator {
 public:
     explicit Memory_Allocator(int number_of_buffers);
     virtual ~Memory_Allocator();
+    Memory_Allocator(const Memory_Allocator&) = delete;  // owns its buffers / device coder
+    Memory_Allocator& operator=(const Memory_Allocator&) = delete;
     unsigned char* allocate_memory(int size);
 
 private:
@@ -93,6 +95,8 @@ class FEC_Encoder {
 public:
     FEC_Encoder(int max_payload_value, int T_value, int B_value, int N_value, Memory_Allocator* memory);
     virtual ~FEC_Encoder();
+    FEC_Encoder(const FEC_Encoder&) = delete;  // owns its buffers / device coder
+    FEC_Encoder& operator=(const FEC_Encoder&) = delete;
     unsigned char* onTransmit(unsigned char* data, int payload, int seq, int* codeword_size);
     Encoder* encoder;
 
@@ -106,6 +110,8 @@ class FEC_Decoder {
 public:
     FEC_Decoder(int max_payload_value, int T_value, int B_value, int N_value, Memory_Allocator* memory);
     virtual ~FEC_Decoder();
+    FEC_Decoder(const FEC_Decoder&) = delete;  // owns its buffers / device coder
+    FEC_Decoder& operator=(const FEC_Decoder&) = delete;
     unsigned char* onReceive(unsigned char* codeword_received, int codeword_size, int seq, int* payload,
                              bool erasure);
     Decoder* decoder;
@@ -138,6 +144,8 @@ public:
     static constexpr int kTTot = 10;  // T_TOT
     explicit Decoder_Symbol_Wise(int max_payload_value);
     virtual ~Decoder_Symbol_Wise();
+    Decoder_Symbol_Wise(const Decoder_Symbol_Wise&) = delete;  // owns its slot arrays
+    Decoder_Symbol_Wise& operator=(const Decoder_Symbol_Wise&) = delete;
 
     unsigned char* codeword;
     unsigned char** codeword_vector;
