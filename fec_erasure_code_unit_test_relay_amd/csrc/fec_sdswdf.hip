@@ -34,11 +34,13 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <array>
 #include <cstring>
 #include <map>
 #include <memory>
 #include <mutex>
 #include <new>
+#include <stdexcept>
 #include <string>
 #include <tuple>
 #include <unordered_map>
@@ -123,6 +125,43 @@ private:
     std::vector<uint8_t> data_;
 };
 
+// Header rows as small ids: entries 0..T_TOT-1 of a row (the part the reference's shifts move,
+// :133, :169; entry T_TOT stays with its slot) packed into two words.  The planners keep a window
+// of row ids instead of shifting 30 rows of ints per packet, and key their memo on it.
+class RowIds {
+public:
+    uint16_t intern(const int* e) {
+        uint64_t a = 0, b = 0;
+        for (int i = 0; i < 8; ++i) a |= static_cast<uint64_t>(static_cast<uint8_t>(e[i])) << (8 * i);
+        for (int i = 8; i < kTT; ++i) b |= static_cast<uint64_t>(static_cast<uint8_t>(e[i])) << (8 * (i - 8));
+        auto it = ids_.find(Key{a, b});
+        if (it != ids_.end()) return it->second;
+        if (rows_.size() >= 0xffff) throw std::length_error("sdswdf: header rows");
+        const uint16_t id = static_cast<uint16_t>(rows_.size());
+        std::array<int, kTT> r{};
+        for (int i = 0; i < kTT; ++i) r[i] = e[i];
+        rows_.push_back(r);
+        ids_.emplace(Key{a, b}, id);
+        return id;
+    }
+    const std::array<int, kTT>& row(uint16_t id) const { return rows_[id]; }
+    void clear() {
+        ids_.clear();
+        rows_.clear();
+    }
+
+private:
+    struct Key {
+        uint64_t a, b;
+        bool operator==(const Key& o) const { return a == o.a && b == o.b; }
+    };
+    struct KeyHash {
+        size_t operator()(const Key& k) const { return static_cast<size_t>((k.a ^ (k.b * 0x9E3779B97F4A7C15ull)) * 0xff51afd7ed558ccdull >> 17); }
+    };
+    std::unordered_map<Key, uint16_t, KeyHash> ids_;
+    std::vector<std::array<int, kTT>> rows_;
+};
+
 // The relay: symbol_wise_encode_state_dependent per packet, symbolic.  Output record per packet:
 // header[n2-1][0..10] as bytes, then n2 rows of n coefficients (row index: frame symbol `index`
 // of every code block j = sum_p coef[p] * symbol (j, p) of source packet t-(n-1)+p+(k-1-index)).
@@ -144,29 +183,61 @@ public:
             for (int jj = 0; jj < kHdr; ++jj) header_[i][jj] = jj + 1;  // :60-62
         records_.clear();
         memo_.clear();
+        rows_.clear();
+        er_bits_ = valid_bits_ = 0;
+        const uint16_t id0 = rows_.intern(header_[0]);
+        for (auto& w : win_) w = id0;
+        prev_e10_ = kHdr;
     }
     // Packet t (t = 0, 1, ... in order), erased on hop 1: the id of its record.  The plan of a
     // packet is a function of the flags of the slots its diagonals read and of the headers of
     // the last n2-1 packets (rows n2-1 and up hold constants): repeated states are looked up.
+    // Between packets the state is kept compact: the flags as bit masks (slot i = bit i) and the
+    // last n2-1 emitted header rows as ids (header row r < n2-1 = emission t-(n2-1)+r; entry T_TOT of
+    // those rows never moves from its initial value; row n2-1 keeps its own entry T_TOT); the
+    // reference-structured arrays are rebuilt from it only when a state is planned for the first
+    // time.
     int32_t step(bool erased) {
-        shift();
-        er_[2 * kTT] = erased ? 1 : 0;
-        valid_[2 * kTT] = erased ? 0 : 1;
+        // push_current_codeword / rotate_pointers_and_insert_zero_word: slot i <- slot i+1, the top
+        // slot keeps its flags; then slot 2T is the new packet
+        constexpr uint32_t top = 1u << (kSlots - 1), cur = 1u << (2 * kTT);
+        er_bits_ = ((er_bits_ >> 1) | (er_bits_ & top)) & ~cur;
+        valid_bits_ = ((valid_bits_ >> 1) | (valid_bits_ & top)) & ~cur;
+        if (erased) er_bits_ |= cur;
+        else valid_bits_ |= cur;
         const int lo = 2 * kTT - n_ + 1 - (n2_ - k_);
+        const uint32_t wmask = (2 * kTT - lo + 1) >= 32 ? ~0u : ((1u << (2 * kTT - lo + 1)) - 1u);
+        const uint32_t ew = (er_bits_ >> lo) & wmask, vw = (valid_bits_ >> lo) & wmask;
         key_.clear();
-        for (int i = lo; i <= 2 * kTT; ++i) key_.push_back(static_cast<char>(er_[i] | (valid_[i] << 1)));
-        for (int r = 0; r < n2_ - 1; ++r)
-            for (int e = 0; e < n2_ - 1; ++e) key_.push_back(static_cast<char>(header_[r][e]));
+        key_.append(reinterpret_cast<const char*>(&ew), sizeof ew);
+        key_.append(reinterpret_cast<const char*>(&vw), sizeof vw);
+        key_.append(reinterpret_cast<const char*>(win_), sizeof(uint16_t) * static_cast<size_t>(n2_ > 1 ? n2_ - 1 : 0));
+        key_.push_back(static_cast<char>(prev_e10_));
         auto it = memo_.find(key_);
-        if (it != memo_.end()) {
-            for (int i = 0; i < n2_; ++i) header_[n2_ - 1][i] = it->second.hdr[i];
-            return it->second.id;
+        if (it == memo_.end()) {
+            for (int i = 0; i < kSlots; ++i) {
+                er_[i] = static_cast<uint8_t>(er_bits_ >> i & 1u);
+                valid_[i] = static_cast<uint8_t>(valid_bits_ >> i & 1u);
+                for (int jj = 0; jj < kHdr; ++jj) header_[i][jj] = jj + 1;
+            }
+            for (int r = 0; r < n2_ - 1; ++r) {
+                const auto& row = rows_.row(win_[r]);
+                for (int e = 0; e < kTT; ++e) header_[r][e] = row[e];
+            }
+            header_[n2_ - 1][kTT] = prev_e10_;
+            encode(rec_.data());
+            Memo m;
+            m.id = records_.intern(rec_.data());
+            for (int i = 0; i < kHdr; ++i) m.hdr[i] = static_cast<uint8_t>(header_[n2_ - 1][i]);
+            m.row = rows_.intern(header_[n2_ - 1]);
+            it = memo_.emplace(key_, m).first;
         }
-        encode(rec_.data());
-        Memo m;
-        m.id = records_.intern(rec_.data());
-        for (int i = 0; i < n2_; ++i) m.hdr[i] = static_cast<uint8_t>(header_[n2_ - 1][i]);
-        memo_.emplace(key_, m);
+        const Memo& m = it->second;
+        if (n2_ > 1) {
+            for (int r = 0; r + 1 < n2_ - 1; ++r) win_[r] = win_[r + 1];
+            win_[n2_ - 2] = m.row;
+        }
+        prev_e10_ = m.hdr[kTT];
         return m.id;
     }
 
@@ -330,6 +401,7 @@ private:
     struct Memo {
         int32_t id;
         uint8_t hdr[kHdr];
+        uint16_t row;  // entries 0..T_TOT-1 of the emitted header row
     };
     int k_, n_, n2_, sdbo_;
     std::shared_ptr<const DecodeRules> rules_;
@@ -341,6 +413,10 @@ private:
     std::vector<uint8_t> rec_;
     std::string key_;
     std::unordered_map<std::string, Memo> memo_;
+    RowIds rows_;
+    uint32_t er_bits_ = 0, valid_bits_ = 0;
+    uint16_t win_[kMaxN] = {};
+    int prev_e10_ = kHdr;
 };
 
 // The destination: symbol_wise_decode_state_dependent per frame, symbolic.  Output record: k
@@ -361,26 +437,42 @@ public:
             for (int jj = 0; jj < kHdr; ++jj) header_[i][jj] = jj + 1;
         records_.clear();
         memo_.clear();
+        rows_.clear();
+        valid_bits_ = 0;
+        const uint16_t id0 = rows_.intern(header_[0]);
+        for (auto& w : ids_) w = id0;
+        top_e10_ = kHdr;
     }
     // Frame t2 (in order): its record id; *flag = the loss flag.  The plan is a function of the
-    // header rows and presence of the last k+n-1 frames: repeated states are looked up.
+    // header rows and presence of the last k+n-1 frames: repeated states are looked up.  Between
+    // frames the state is compact: presence as a bit mask, every header row as an id of its
+    // entries 0..T_TOT-1, and the top row's entry T_TOT (the rows below keep the initial one: the
+    // shifts never move it, :1663-1664); the arrays are rebuilt only for a state seen first.
     int32_t step(bool erased, const uint8_t* hdr, bool* flag) {
-        for (int i = 0; i < kSlots - 1; ++i) {
-            std::memcpy(header_[i], header_[i + 1], sizeof(int) * kTT);
-            valid_[i] = valid_[i + 1];
-        }
-        for (int i = 0; i < kHdr; ++i) header_[kSlots - 1][i] = erased ? 0 : hdr[i];  // :1709, :1803
-        valid_[kSlots - 1] = erased ? 0 : 1;
+        constexpr uint32_t top = 1u << (kSlots - 1);
+        valid_bits_ = (valid_bits_ >> 1) & ~top;
+        if (!erased) valid_bits_ |= top;
+        std::memmove(ids_, ids_ + 1, sizeof(uint16_t) * (kSlots - 1));
+        int row[kHdr];
+        for (int i = 0; i < kHdr; ++i) row[i] = erased ? 0 : hdr[i];  // :1709, :1803
+        ids_[kSlots - 1] = rows_.intern(row);
+        top_e10_ = row[kTT];
         const int lo = kSlots - k_ - n_ + 1;
+        const uint32_t vw = valid_bits_ >> lo;
         key_.clear();
-        for (int r = lo; r < kSlots; ++r) {
-            key_.push_back(static_cast<char>(valid_[r]));
-            for (int e = 0; e < n_; ++e) key_.push_back(static_cast<char>(header_[r][e]));
-        }
+        key_.append(reinterpret_cast<const char*>(&vw), sizeof vw);
+        key_.append(reinterpret_cast<const char*>(ids_ + lo), sizeof(uint16_t) * static_cast<size_t>(kSlots - lo));
+        key_.push_back(static_cast<char>(top_e10_));
         auto it = memo_.find(key_);
         if (it != memo_.end()) {
             *flag = it->second.flag;
             return it->second.id;
+        }
+        for (int r = 0; r < kSlots; ++r) {
+            valid_[r] = static_cast<uint8_t>(valid_bits_ >> r & 1u);
+            const auto& rw = rows_.row(ids_[r]);
+            for (int e = 0; e < kTT; ++e) header_[r][e] = rw[e];
+            header_[r][kTT] = r == kSlots - 1 ? top_e10_ : kHdr;
         }
         Memo m;
         m.flag = decode(rec_.data());
@@ -448,6 +540,10 @@ private:
     std::vector<uint8_t> rec_;
     std::string key_;
     std::unordered_map<std::string, Memo> memo_;
+    RowIds rows_;
+    uint32_t valid_bits_ = 0;
+    uint16_t ids_[kSlots] = {};
+    int top_e10_ = kHdr;
 };
 
 struct SdRelayArgs {
