@@ -287,10 +287,11 @@ def test_gpu_adaptive_wire_packets_and_outputs_equal_oracle(adaptive, c4):
 
 @pytest.mark.gpu
 def test_gpu_adaptive_tile_encode_equals_generic_kernel(monkeypatch):
-    """Config 4's encode through the tile encoder (one launch per (T,B,N) tuple, segment mode)
+    """Config 4's encode through the tile encoder (segment mode, every tuple in one launch)
     equals the generic variable-rate kernel (FEC_VR_NO_TILE, itself checked against the oracle's
-    wire packets above) row for row, over repeated launches: the tile path's hand-counted vmcnt
-    waits once let a tile's input be read before its LDS-DMA landed, 1 launch in 3."""
+    wire packets above) row for row, over repeated launches: round 3's hand-counted vmcnt waits
+    once let a tile's input be read before its LDS-DMA landed, 1 launch in 3 (the waits now come
+    from an issue ledger, fec_encode_tile.hip)."""
     import torch
     from fec_erasure_code_unit_test_relay_amd import fill_payload
     torch.cuda.set_device(0)
@@ -307,3 +308,34 @@ def test_gpu_adaptive_tile_encode_equals_generic_kernel(monkeypatch):
         torch.cuda.synchronize()
         for a, b in zip(got, ref):
             assert torch.equal(a, b)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("L,with_len", [(300, False), (300, True), (296, False)])
+def test_gpu_adaptive_encode_paths_agree(monkeypatch, L, with_len):
+    """Config 4's encode through its three paths gives the same frames and sizes: every tile tuple
+    in one launch (fec_encode_tile_multi_kernel, L = 300), one launch per tuple
+    (FEC_VR_NO_MULTI; also what L != 300 takes), and the generic kernel alone (FEC_VR_NO_TILE), with
+    full-length payloads and with a per-packet length array (0..L)."""
+    import torch
+    from fec_erasure_code_unit_test_relay_amd import fill_payload
+    torch.cuda.set_device(0)
+    pat = load_pattern("bin_erasure")
+    P = 60000
+    got = {}
+    for name, env in (("multi", {}), ("per_tuple", {"FEC_VR_NO_MULTI": "1"}), ("generic", {"FEC_VR_NO_TILE": "1"})):
+        for k in ("FEC_VR_NO_MULTI", "FEC_VR_NO_TILE"):
+            monkeypatch.delenv(k, raising=False)
+        for k, val in env.items():
+            monkeypatch.setenv(k, val)
+        v = VrPlan(pat, P, max_payload=L)
+        payload = fill_payload(0, v.sent, L, 0x5EED)
+        lengths = None
+        if with_len:
+            rng = np.random.default_rng(7)
+            lengths = torch.from_numpy(rng.integers(0, L + 1, v.sent).astype(np.int32)).cuda()
+        got[name] = [t.clone() for t in v.encode(payload, lengths=lengths)]
+        torch.cuda.synchronize()
+    for name in ("per_tuple", "generic"):
+        for a, b in zip(got["multi"], got[name]):
+            assert torch.equal(a, b), name
