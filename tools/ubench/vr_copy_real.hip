@@ -502,6 +502,14 @@ int main(int argc, char** argv) {
         CHECK(hipMemset(out1, 0x55, P * L));
         CHECK(hipMemset(len1, 0, P * 4));
     };
+    timeit("V1 sub-stream lanes, TP 16, 8 KB stage", [&] {
+        hipLaunchKernelGGL((copy_v1<16, 8192>), dim3(grid), dim3(256), 16 * (L + 32), 0, a1);
+    });
+    check_v("V1/16/8K");
+    timeit("V1 sub-stream lanes, TP 8, 8 KB stage", [&] {
+        hipLaunchKernelGGL((copy_v1<8, 8192>), dim3(static_cast<unsigned>((P + 7) / 8)), dim3(256), 8 * (L + 32), 0, a1);
+    });
+    check_v("V1/8/8K");
     const unsigned g32 = static_cast<unsigned>((P + 31) / 32);
     timeit("V1 sub-stream lanes, TP 16", [&] {
         hipLaunchKernelGGL((copy_v1<16, 16384>), dim3(grid), dim3(256), 16 * (L + 32), 0, a1);
