@@ -363,3 +363,35 @@ def test_gpu_relay_dropin_vr_schedule_equals_oracle_methods(tmp_path):
     r = subprocess.run([exe, "--schedule"] + files, capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "RELAY DROPIN OK" in r.stdout
+
+
+def test_relay_c_abi_rejects_bad_arguments_before_device_work():
+    """The drop-in relay's per-call methods (fec_sw_*, include/fec_amd.h) and fec_sdswdf_create
+    check their arguments before any HIP call (so this runs on the CPU): FEC_ERR_ARG for a missing
+    array, k2 != k (the reference always calls them with k2 = k, Variable_Rate_FEC_Decoder.cpp:998),
+    n2 < k, the state-dependent pair's n2 > n or n past T_TOT + 1, k < 1, max_payload < 1."""
+    import ctypes
+    from fec_erasure_code_unit_test_relay_amd._lib import lib
+    Lb = lib()
+    i, vp = ctypes.c_int, ctypes.c_void_p
+    Lb.fec_sw_state_encode.argtypes = [i] * 6 + [vp] * 5
+    Lb.fec_sw_state_decode.argtypes = [i] * 3 + [vp] * 4
+    Lb.fec_sw_encode_1.argtypes = [i] * 5 + [vp] * 5
+    Lb.fec_sw_decode_1.argtypes = [i] * 3 + [vp] * 4
+    Lb.fec_sdswdf_create.argtypes = [i] * 6 + [ctypes.POINTER(vp)]
+    buf = np.zeros(64, dtype=np.uint64)
+    p = buf.ctypes.data_as(vp)
+    ERR = -1
+    for args in [(300, 8, 11, 7, 11, 0), (300, 8, 11, 8, 12, 0), (300, 8, 12, 8, 12, 0), (300, 0, 11, 0, 11, 0)]:
+        assert Lb.fec_sw_state_encode(*args, p, p, p, p, p) == ERR, args  # n2 <= n <= T_TOT + 1
+    for args in [(300, 8, 11, 7, 11), (300, 8, 11, 8, 7), (300, 0, 11, 0, 11), (0, 8, 11, 8, 11)]:
+        assert Lb.fec_sw_encode_1(*args, p, p, p, p, p) == ERR, args  # n2 >= k2 = k
+    assert Lb.fec_sw_state_encode(300, 8, 11, 8, 11, 0, None, p, p, p, p) == ERR
+    assert Lb.fec_sw_encode_1(300, 8, 11, 8, 11, p, None, p, p, p) == ERR
+    assert Lb.fec_sw_state_decode(300, 8, 12, p, p, p, p) == ERR
+    assert Lb.fec_sw_state_decode(300, 8, 11, p, None, p, p) == ERR
+    assert Lb.fec_sw_decode_1(300, 0, 11, p, p, p, p) == ERR
+    assert Lb.fec_sw_decode_1(0, 8, 11, p, p, p, p) == ERR
+    h = vp()
+    assert Lb.fec_sdswdf_create(300, 10, 3, 10, 4, 0, ctypes.byref(h)) == ERR  # k2 != k
+    assert Lb.fec_sdswdf_create(300, 9, 3, 10, 4, 0, ctypes.byref(h)) == ERR   # T2 > T1
