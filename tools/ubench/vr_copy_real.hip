@@ -407,6 +407,149 @@ __global__ __launch_bounds__(256) void copy_v2(Args a) {
     }
 }
 
+// ---- V3: persistent workgroups that prefetch only the next tile's offsets and records (a few
+// registers), so each tile's stage loads issue at the top of its iteration with their addresses
+// known: one memory round trip per tile instead of two (offsets, then rows) --------------------
+template <int TP, int STG>
+__global__ __launch_bounds__(256) void copy_v3(Args a) {
+    __shared__ __attribute__((aligned(16))) uint8_t stage[STG + 16];
+    extern __shared__ __attribute__((aligned(16))) uint8_t otile[];
+    __shared__ int s_ro[TP], s_rw[TP], s_kn[TP], s_cp[TP], s_S[TP];
+    const int tid = threadIdx.x, l32 = tid & 31, hw = tid >> 5;
+    const int L = a.L, ors = L + 32;
+    const int64_t ntiles = (a.P + TP - 1) / TP;
+    int64_t tile = blockIdx.x;
+    if (tile >= ntiles) return;
+    int64_t n_o0 = 0, n_end = 0, n_ro = 0, n_ro1 = 0;
+    uint32_t n_g = 0;
+    auto prefetch = [&](int64_t t) {
+        const int64_t x0 = t * TP;
+        const int np = static_cast<int>(min<int64_t>(TP, a.P - x0));
+        n_o0 = a.cur_off[x0];
+        n_end = a.cur_off[x0 + np];
+        if (tid < np) {
+            n_g = a.geo[x0 + tid];
+            n_ro = a.cur_off[x0 + tid];
+            n_ro1 = a.cur_off[x0 + tid + 1];
+        }
+    };
+    prefetch(tile);
+    for (; tile < ntiles; tile += gridDim.x) {
+        const int64_t x0 = tile * TP;
+        const int np = static_cast<int>(min<int64_t>(TP, a.P - x0));
+        const int64_t o0 = n_o0, span = n_end - n_o0;
+        const bool staged = span <= STG;
+        if (staged) {
+            const uint4* src = reinterpret_cast<const uint4*>(a.cur + o0);
+            for (int c = tid; 16 * c < span; c += 256) reinterpret_cast<uint4*>(stage)[c] = src[c];
+        }
+        if (tid < np) {
+            const uint32_t g = n_g;
+            s_ro[tid] = static_cast<int>(n_ro - o0);
+            s_rw[tid] = static_cast<int>(n_ro1 - n_ro);
+            const int f = static_cast<int>(g >> 16 & 0xff);
+            const int k = f == 1 ? static_cast<int>(g & 0xff) : 1;
+            s_kn[tid] = f == 1 ? static_cast<int>(g & 0xffff) : (f == 2 ? -1 : 0);
+            s_S[tid] = (L + 2 + k - 1) / k;
+            s_cp[tid] = static_cast<int>(g >> 24);  // slow flag, until the length replaces it
+        }
+        __syncthreads();
+        if (tile + gridDim.x < ntiles) prefetch(tile + gridDim.x);
+        if (tid < np) {
+            const int64_t x = x0 + tid;
+            const int kn = s_kn[tid];
+            int ln = 0;
+            if (kn > 0) {
+                const int k = kn & 0xff, n = kn >> 8, rw = s_rw[tid];
+                const uint8_t* lrow = stage + s_ro[tid];
+                const uint8_t* grow = a.cur + o0 + s_ro[tid];
+                const int p1 = k > 1 ? 1 : n;
+                const int h0 = rw > 0 ? (staged ? lrow[0] : grow[0]) : 0;
+                const int h1 = p1 < rw ? (staged ? lrow[p1] : grow[p1]) : 0;
+                const int hdr = h0 * 256 + h1;
+                ln = s_cp[tid] ? min(hdr, L) : hdr;
+            }
+            if (kn >= 0) a.out_len[x] = ln;
+            s_cp[tid] = min(ln, L);
+        }
+        if (staged) {
+            for (int pp = hw; pp < np; pp += 8) {
+                const int kn = s_kn[pp];
+                if (kn <= 0) continue;
+                const int k = kn & 0xff, n = kn >> 8, S = s_S[pp];
+                const int ro = s_ro[pp];
+                uint8_t* orow = otile + pp * ors + 6;
+                for (int s = l32; s < S; s += 32) {
+                    const int aa = ro + s * n;
+                    const uint32_t* src = reinterpret_cast<const uint32_t*>(stage + (aa & ~3));
+                    const uint32_t d0 = src[0], d1 = src[1], d2 = src[2], d3 = src[3];
+                    const int sh = aa & 3;
+                    const uint32_t w0 = __builtin_amdgcn_alignbyte(d1, d0, sh);
+                    const uint32_t w1 = __builtin_amdgcn_alignbyte(d2, d1, sh);
+                    const uint32_t w2 = __builtin_amdgcn_alignbyte(d3, d2, sh);
+                    uint8_t* dst = orow + s * k;
+                    dst[11] = static_cast<uint8_t>(w2 >> 24);
+                    dst[10] = static_cast<uint8_t>(w2 >> 16);
+                    dst[9] = static_cast<uint8_t>(w2 >> 8);
+                    dst[8] = static_cast<uint8_t>(w2);
+                    dst[7] = static_cast<uint8_t>(w1 >> 24);
+                    dst[6] = static_cast<uint8_t>(w1 >> 16);
+                    dst[5] = static_cast<uint8_t>(w1 >> 8);
+                    dst[4] = static_cast<uint8_t>(w1);
+                    dst[3] = static_cast<uint8_t>(w0 >> 24);
+                    dst[2] = static_cast<uint8_t>(w0 >> 16);
+                    dst[1] = static_cast<uint8_t>(w0 >> 8);
+                    dst[0] = static_cast<uint8_t>(w0);
+                }
+            }
+        } else {
+            const int L4 = (L + 3) >> 2;
+            for (int d = tid; d < np * L4; d += 256) {
+                const int p = d / L4, w = d - p * L4;
+                const int kn = s_kn[p];
+                if (kn <= 0) continue;
+                const int k = kn & 0xff, n = kn >> 8, rw = s_rw[p];
+                const uint8_t* grow = a.cur + o0 + s_ro[p];
+                const int h = 4 * w + 2;
+                int sidx = h / k, i = h - sidx * k;
+                uint32_t val = 0;
+                for (int e = 0; e < 4; ++e) {
+                    const int pos = sidx * n + i;
+                    if (pos < rw) val |= static_cast<uint32_t>(grow[pos]) << (8 * e);
+                    if (++i == k) {
+                        i = 0;
+                        ++sidx;
+                    }
+                }
+                *reinterpret_cast<uint32_t*>(otile + p * ors + 8 + 4 * w) = val;
+            }
+        }
+        __syncthreads();
+        const int ob = np * L;
+        uint8_t* dst = a.out + x0 * L;
+        for (int o = 16 * tid; o < ob; o += 16 * 256) {
+            uint32_t v[4];
+            bool skip[4], any_skip = false;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int oq = o + 4 * q;
+                const int p = oq / L, off = oq - p * L;
+                skip[q] = s_kn[p] < 0;
+                any_skip |= skip[q];
+                v[q] = *reinterpret_cast<const uint32_t*>(otile + p * ors + 8 + off) & keep_bytes(s_cp[p] - off);
+            }
+            if (!any_skip) {
+                *reinterpret_cast<uint4*>(dst + o) = make_uint4(v[0], v[1], v[2], v[3]);
+            } else {
+#pragma unroll
+                for (int q = 0; q < 4; ++q)
+                    if (!skip[q]) *reinterpret_cast<uint32_t*>(dst + o + 4 * q) = v[q];
+            }
+        }
+        __syncthreads();
+    }
+}
+
 static std::vector<uint8_t> read_file(const std::string& path) {
     FILE* f = std::fopen(path.c_str(), "rb");
     if (!f) {
@@ -536,6 +679,26 @@ int main(int argc, char** argv) {
         std::snprintf(nm, sizeof nm, "V2 persistent TP 32 (16K), grid %d", G);
         timeit(nm, [&] {
             hipLaunchKernelGGL((copy_v2<32, 16384>), dim3(G), dim3(256), 32 * (L + 32), 0, a1);
+        });
+        check_v(nm);
+    }
+    int cus = 0;
+    CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0));
+    for (int per : {4, 6, 7, 8, 12}) {
+        char nm[64];
+        const int G = cus * per;
+        std::snprintf(nm, sizeof nm, "V3 persistent, offsets ahead, grid %d", G);
+        timeit(nm, [&] {
+            hipLaunchKernelGGL((copy_v3<16, 16384>), dim3(G), dim3(256), 16 * (L + 32), 0, a1);
+        });
+        check_v(nm);
+    }
+    for (int per : {6, 7}) {
+        char nm[64];
+        const int G = cus * per;
+        std::snprintf(nm, sizeof nm, "V3 persistent, 8 KB stage, grid %d", G);
+        timeit(nm, [&] {
+            hipLaunchKernelGGL((copy_v3<16, 8192>), dim3(G), dim3(256), 16 * (L + 32), 0, a1);
         });
         check_v(nm);
     }

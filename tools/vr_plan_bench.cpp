@@ -1,7 +1,8 @@
 // Host-only timing of the config 4 plan (fec::VrPlan::run): control loop and decoder phases.
-//   g++ -O2 -std=c++17 -pthread -I fec_erasure_code_unit_test_relay_amd/csrc -I include \
-//       tools/vr_plan_bench.cpp fec_erasure_code_unit_test_relay_amd/csrc/fec_vr_host.cpp ... (see tools/vr_plan_bench.sh)
-//   ./vr_plan_bench pattern.bin [reps]
+//   g++ -O2 -std=c++17 -pthread -I fec_erasure_code_unit_test_relay_amd/csrc -I include -I/opt/rocm/include \
+//       -D__HIP_PLATFORM_AMD__ tools/vr_plan_bench.cpp -o tools/ubench/vr_plan_bench \
+//       -L fec_erasure_code_unit_test_relay_amd -lfec_amd -Wl,-rpath,'$ORIGIN/../../fec_erasure_code_unit_test_relay_amd'
+//   ./tools/ubench/vr_plan_bench pattern.bin [reps]   (FEC_VR_DEBUG=1: phase split on stderr)
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
