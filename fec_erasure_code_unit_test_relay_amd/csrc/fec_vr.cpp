@@ -6,6 +6,7 @@
 
 #include <algorithm>
 #include <chrono>
+#include <cmath>
 #include <atomic>
 #include <cstdio>
 #include <cstdlib>
@@ -224,6 +225,45 @@ void VrPlan::run(int max_payload, int T, int B, int N, bool mds, const uint8_t* 
     if (!async) finish();
 }
 
+// s += r, `count` times, in float (round to nearest even), with the result of the sequential loop
+// (Variable_Rate_FEC_Encoder.cpp:176-190 adds one rate per packet): 360 000 dependent adds were
+// the last ~0.3 ms of the plan.  While s stays in one binade [2^(e-1), 2^e) its ulp u is fixed, so
+// each add gives s + d with d = r rounded to a multiple of u -- the same d every time unless r / u
+// is an odd multiple of 1/2 (a tie, whose rounding depends on s's last bit: stepped one by one).
+// The adds are taken in one multiplication up to the first one whose exact sum reaches 2^e (there
+// the ulp doubles), which is then stepped on its own.  Every intermediate value is a multiple of u
+// below 2^e, exact in double and in float.
+float float_add_repeated(float s, float r, int64_t count) {
+    while (count > 0) {
+        if (!(s > 0.0f) || !(r > 0.0f) || !std::isfinite(s) || !std::isfinite(r)) {
+            s += r;
+            --count;
+            continue;
+        }
+        int e = 0;
+        (void)std::frexp(s, &e);                  // s in [2^(e-1), 2^e)
+        const double hi = std::ldexp(1.0, e);
+        const double u = std::ldexp(1.0, e - 24);  // 24-bit significand
+        const double q = static_cast<double>(r) / u;
+        const float t = s + r;
+        if (q - std::floor(q) == 0.5 || static_cast<double>(s) + r >= hi) {  // a tie, or the binade's last add
+            s = t;
+            --count;
+            continue;
+        }
+        const double d = static_cast<double>(t) - static_cast<double>(s);
+        if (d == 0.0) return s;  // r below half an ulp: s stays
+        // m = the number of adds j = 0, 1, ... with s + j*d + r < hi (each of them adds exactly d)
+        int64_t m = static_cast<int64_t>(std::ceil((hi - r - static_cast<double>(s)) / d));
+        while (m > 0 && static_cast<double>(s) + static_cast<double>(m - 1) * d + r >= hi) --m;
+        while (static_cast<double>(s) + static_cast<double>(m) * d + r < hi) ++m;
+        m = std::min(m, count);
+        s = static_cast<float>(static_cast<double>(s) + static_cast<double>(m) * d);
+        count -= m;
+    }
+    return s;
+}
+
 void VrPlan::start_workers() {
     const int hw = vr_allowed_cpus();  // not hardware_concurrency: the process's cpuset may be smaller
     size_t nth = static_cast<size_t>(std::max(1, std::min(hw > 1 ? hw - 1 : 1, 8)));
@@ -251,8 +291,7 @@ void VrPlan::start_workers() {
                 }
                 if (j.id < 0) {  // final_sum_coding_rate, one float add per packet in sending order
                     float s = 0;
-                    for (const RateRun& r : rate_runs)
-                        for (int64_t i = 0; i < r.count; ++i) s += r.rate;
+                    for (const RateRun& r : rate_runs) s = float_add_repeated(s, r.rate, r.count);
                     sum_coding_rate = s;
                 } else {
                     decode_instance(j, recs_[w]);
@@ -317,6 +356,8 @@ void VrPlan::decode_instance(const DecJob& job, std::vector<RecEntry>& recs) {
     StreamPlanner pl(g, job.rules);
     const Reports* rp = job.reps.data();
     const Reports* rp_end = rp + job.reps.size();
+    for (const Reports* r = rp; r != rp_end; ++r)  // the packets this instance reports (report_range)
+        std::fill(fate_dec.begin() + (r->lo - r->xoff), fate_dec.begin() + (r->hi - r->xoff), job.id);
     size_t di = static_cast<size_t>(std::lower_bound(drops.begin(), drops.end(), d.first) - drops.begin());
     int64_t s = d.first;
     while (s < d.end) {
@@ -626,7 +667,8 @@ void VrPlan::control(const uint8_t* pattern, int64_t n_pattern, int T, int B, in
             rv.back().hi = hi;
         else
             rv.push_back(Reports{id, lo, hi, dT});
-        std::fill(fate_dec.begin() + (lo - dT), fate_dec.begin() + (hi - dT), id);
+        // fate_dec of [lo, hi) is written by the worker that replays instance id (decode_instance):
+        // off the control loop, whose steady stretches would otherwise fill 4 bytes per packet
     };
     auto report = [&](int id, int64_t seq) { report_range(id, seq, seq + 1); };
     auto update_decoder = [&](int T_, int B_, int N_, int64_t first) {  // (:2520-2536)

@@ -94,6 +94,9 @@ struct VrHostAlloc {
 template <typename T>
 using VrHostVec = std::vector<T, VrHostAlloc<T>>;
 
+// s += r, `count` times, in float: the sequential loop's result in O(binades) steps (fec_vr.cpp).
+float float_add_repeated(float s, float r, int64_t count);
+
 struct VrPlan {
     struct FrameRun {      // frames[first .. next run's first) are all `f`
         int64_t first;
