@@ -138,14 +138,18 @@ int vr_pin_mode() {
     return mode;
 }
 int vr_pin_home() { return vr_pin_mode() > 0 ? sched_getcpu() : -1; }
-void vr_pin_near(int home) {
-    if (home < 0) return;
+// The allowed CPUs of home's aligned group of 8 (empty when home < 0).
+cpu_set_t vr_group(int home) {
     cpu_set_t allowed, set;
     CPU_ZERO(&set);
-    if (sched_getaffinity(0, sizeof(allowed), &allowed) != 0) return;
+    if (home < 0 || sched_getaffinity(0, sizeof(allowed), &allowed) != 0) return set;
     const int base = home & ~7;
     for (int c = base; c < base + 8 && c < CPU_SETSIZE; ++c)
         if (CPU_ISSET(c, &allowed)) CPU_SET(c, &set);
+    return set;
+}
+void vr_pin_near(int home) {
+    cpu_set_t set = vr_group(home);
     // a sparse group (fewer than 4 allowed CPUs: taskset, cgroup) is left alone: the plan's
     // spin-polling threads crowded on one or two CPUs would stall each other
     if (CPU_COUNT(&set) >= 4) (void)pthread_setaffinity_np(pthread_self(), sizeof(set), &set);
@@ -267,6 +271,12 @@ float float_add_repeated(float s, float r, int64_t count) {
 void VrPlan::start_workers() {
     const int hw = vr_allowed_cpus();  // not hardware_concurrency: the process's cpuset may be smaller
     size_t nth = static_cast<size_t>(std::max(1, std::min(hw > 1 ? hw - 1 : 1, 8)));
+    // placed on a group: one CPU per thread -- the control loop and the feedback producer keep two
+    // of them (8 workers on top of those made the control loop 15 % slower: 1.30 vs 1.23 ms plan,
+    // profiles/r04/vr/r04zj_plan_threads_ab.txt)
+    const cpu_set_t grp = vr_group(t_pin_home);
+    if (const int g = CPU_COUNT(&grp); g >= 4)
+        nth = static_cast<size_t>(std::max(1, std::min<int>(static_cast<int>(nth), g - 2)));
     if (const char* e = std::getenv("FEC_VR_THREADS")) nth = std::max(1, std::atoi(e));
     {
         std::lock_guard<std::mutex> lk(qmu_);
