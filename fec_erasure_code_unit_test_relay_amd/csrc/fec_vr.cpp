@@ -192,10 +192,13 @@ void vr_host_free(void* q) {
         std::free(p);
 }
 
-const VrFrame& VrPlan::frame(int64_t s) const {
+VrFrame VrPlan::frame(int64_t s) const {
     auto it = std::upper_bound(frame_runs.begin(), frame_runs.end(), s,
                                [](int64_t v, const FrameRun& r) { return v < r.first; });
-    return std::prev(it)->f;
+    const FrameRun& r = *std::prev(it);
+    VrFrame f = r.f;
+    f.counter += r.cstep * static_cast<int>(s - r.first);
+    return f;
 }
 
 // Two parts that overlap.  (1) The control loop -- sender, estimator feedback, encoder switches,
@@ -282,6 +285,8 @@ void VrPlan::start_workers() {
         std::lock_guard<std::mutex> lk(qmu_);
         q_.clear();
         qclosed_ = false;
+        qsize_.store(0, std::memory_order_relaxed);
+        sleepers_.store(0, std::memory_order_relaxed);
     }
     batch_.clear();
     recs_.resize(nth);
@@ -292,12 +297,25 @@ void VrPlan::start_workers() {
             vr_pin_near(home);
             for (;;) {
                 DecJob j;
+                // poll the queue for a while (a job comes every ~0.5 us while the control loop
+                // runs), then sleep on the condition variable
+                for (int spin = 0; spin < 4096 && qsize_.load(std::memory_order_acquire) == 0; ++spin)
+                    __builtin_ia32_pause();
                 {
                     std::unique_lock<std::mutex> lk(qmu_);
-                    qcv_.wait(lk, [&] { return !q_.empty() || qclosed_; });
-                    if (q_.empty()) break;
+                    if (q_.empty() && !qclosed_) {
+                        sleepers_.fetch_add(1, std::memory_order_relaxed);
+                        qcv_.wait(lk, [&] { return !q_.empty() || qclosed_; });
+                        sleepers_.fetch_sub(1, std::memory_order_relaxed);
+                    }
+                    if (q_.empty()) {
+                        qsize_.store(-1, std::memory_order_release);  // closed: every worker leaves
+                        break;
+                    }
                     j = std::move(q_.front());
                     q_.pop_front();
+                    qsize_.store(q_.empty() && qclosed_ ? -1 : static_cast<int64_t>(q_.size()),
+                                 std::memory_order_release);
                 }
                 if (j.id < 0) {  // final_sum_coding_rate, one float add per packet in sending order
                     float s = 0;
@@ -315,19 +333,23 @@ void VrPlan::start_workers() {
 // would cost the control thread more than the job).
 void VrPlan::publish(DecJob&& j, bool flush) {
     batch_.push_back(std::move(j));
-    if (!flush && batch_.size() < 32) return;
+    if (!flush && batch_.size() < 8) return;
+    bool wake;
     {
         std::lock_guard<std::mutex> lk(qmu_);
         for (DecJob& b : batch_) q_.push_back(std::move(b));
+        qsize_.store(static_cast<int64_t>(q_.size()), std::memory_order_release);
+        wake = sleepers_.load(std::memory_order_relaxed) > 0;  // a sleeper registered under qmu_
     }
     batch_.clear();
-    qcv_.notify_all();
+    if (wake) qcv_.notify_all();
 }
 
 void VrPlan::close_jobs() {
     {
         std::lock_guard<std::mutex> lk(qmu_);
         qclosed_ = true;
+        qsize_.store(-1, std::memory_order_release);  // pollers stop polling and take the lock
     }
     qcv_.notify_all();
 }
@@ -690,8 +712,23 @@ void VrPlan::control(const uint8_t* pattern, int64_t n_pattern, int T, int B, in
         dcur = new_decoder(T_, B_, N_, first);
         dec[dold].role_switch = first;
     };
-    auto put_frame = [&](int64_t seq, const VrFrame& f) {
-        if (frame_runs.empty() || !(frame_runs.back().f == f)) frame_runs.push_back(FrameRun{seq, f});
+    // frames as runs: equal frames, or a transition's frames whose counter grows by one per packet
+    // (cstep 1; one run per transition instead of one per packet)
+    // (`n` packets from seq carry f; seq is the packet after the last run's last)
+    auto put_frame = [&](int64_t seq, const VrFrame& f, int64_t n = 1) {
+        if (!frame_runs.empty()) {
+            FrameRun& b = frame_runs.back();
+            if (b.f.same_but_counter(f)) {
+                const int64_t d = seq - b.first;
+                if (b.cstep == 0 && f.counter == b.f.counter) return;
+                if (n == 1 && b.cstep == 1 && f.counter == b.f.counter + d) return;
+                if (n == 1 && b.cstep == 0 && d == 1 && f.counter == b.f.counter + 1) {
+                    b.cstep = 1;
+                    return;
+                }
+            }
+        }
+        frame_runs.push_back(FrameRun{seq, f, 0});
     };
     auto put_rate = [&](int64_t count, float rate) {
         if (!rate_runs.empty() && rate_runs.back().rate == rate)
@@ -742,7 +779,7 @@ void VrPlan::control(const uint8_t* pattern, int64_t n_pattern, int T, int B, in
                     fr.N = eN;
                     fr.enc_cur = cur;
                     fr.counter = counter_transition;
-                    put_frame(seq, fr);
+                    put_frame(seq, fr, end - seq);
                     put_rate(end - seq, static_cast<float>(eT - eN + 1) / (eT - eN + 1 + eB));
                     report_range(dcur, seq, end);
                     enc[cur].end = end;
@@ -1665,12 +1702,13 @@ int fec_vr_plan_packets(const fec_vr_plan* vc, int32_t* frames, uint8_t* erased,
         for (size_t r = 0; r < p.frame_runs.size(); ++r) {
             const int64_t hi = r + 1 < p.frame_runs.size() ? p.frame_runs[r + 1].first : p.sent;
             const fec::VrFrame& f = p.frame_runs[r].f;
+            const int32_t cstep = p.frame_runs[r].cstep;
             for (int64_t s = p.frame_runs[r].first; s < hi; ++s) {
                 int32_t* o = frames + 6 * s;
                 o[0] = f.T;
                 o[1] = f.B;
                 o[2] = f.N;
-                o[3] = f.counter;
+                o[3] = f.counter + cstep * static_cast<int32_t>(s - p.frame_runs[r].first);
                 o[4] = f.enc_cur;
                 o[5] = f.enc_old;
             }
@@ -1746,11 +1784,12 @@ int fec_vr_frames_batch(fec_vr_plan* v, const uint8_t* d_cw_cur, const int32_t* 
             for (size_t r = 0; r < p.frame_runs.size(); ++r) {
                 const int64_t hi = r + 1 < p.frame_runs.size() ? p.frame_runs[r + 1].first : p.sent;
                 const fec::VrFrame& f = p.frame_runs[r].f;
+                const int32_t cstep = p.frame_runs[r].cstep;
                 for (int64_t q = p.frame_runs[r].first; q < hi; ++q) {
                     h[4 * q] = f.T;
                     h[4 * q + 1] = f.B;
                     h[4 * q + 2] = f.N;
-                    h[4 * q + 3] = f.counter;
+                    h[4 * q + 3] = f.counter + cstep * static_cast<int32_t>(q - p.frame_runs[r].first);
                 }
             }
             Upload& u = v->hdr_up;

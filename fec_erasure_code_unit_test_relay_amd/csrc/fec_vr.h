@@ -68,8 +68,9 @@ struct VrInstance {
 struct VrFrame {  // Application_Layer_Sender header (Application_Layer_Sender.cpp:259-269) + VR frame
     int T = 0, B = 0, N = 0, counter = 0;
     int enc_cur = -1, enc_old = -1;  // encoder instances whose codewords the frame carries
-    bool operator==(const VrFrame& o) const {
-        return T == o.T && B == o.B && N == o.N && counter == o.counter && enc_cur == o.enc_cur && enc_old == o.enc_old;
+    bool operator==(const VrFrame& o) const { return same_but_counter(o) && counter == o.counter; }
+    bool same_but_counter(const VrFrame& o) const {
+        return T == o.T && B == o.B && N == o.N && enc_cur == o.enc_cur && enc_old == o.enc_old;
     }
 };
 
@@ -98,9 +99,10 @@ using VrHostVec = std::vector<T, VrHostAlloc<T>>;
 float float_add_repeated(float s, float r, int64_t count);
 
 struct VrPlan {
-    struct FrameRun {      // frames[first .. next run's first) are all `f`
+    struct FrameRun {      // frames[first .. next run's first): `f`, the counter + cstep per packet
         int64_t first;
         VrFrame f;
+        int32_t cstep = 0;  // 1: a transition's frames, whose counter grows by one per packet
     };
     struct RateRun {       // `count` packets adding `rate` to final_sum_coding_rate, in order
         int64_t count;
@@ -147,7 +149,7 @@ struct VrPlan {
     void run(int max_payload, int T, int B, int N, bool mds, const uint8_t* pattern, int64_t n_pattern,
              int64_t P_value, bool async = false);
     void finish();  // waits for the decoder phase of an async run (no-op otherwise)
-    const VrFrame& frame(int64_t s) const;  // frame of sent packet s
+    VrFrame frame(int64_t s) const;  // frame of sent packet s
 
 private:
     struct DecJob {        // a decoder instance the control loop is done with (id < 0: the rate sum)
@@ -188,6 +190,10 @@ private:
     std::deque<DecJob> q_;
     std::vector<DecJob> batch_;  // jobs not yet handed to the workers
     bool qclosed_ = false;
+    // Workers poll these before sleeping on qcv_, and the control loop wakes the queue only when a
+    // worker sleeps: a futex wake per published batch cost the control loop ~0.7 ms of system time
+    std::atomic<int64_t> qsize_{0};  // q_.size() (written under qmu_) or -1 once closed and empty
+    std::atomic<int> sleepers_{0};   // workers waiting on qcv_ (changed under qmu_)
     std::chrono::steady_clock::time_point t_dec_;
     bool pending_ = false;
 };
