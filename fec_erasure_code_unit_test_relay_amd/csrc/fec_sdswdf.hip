@@ -99,6 +99,69 @@ void sym_decode(const DecodeRules& rules, int k, int n, Vec* tc, uint8_t* er) {
         }
 }
 
+// Open-addressing map from N-word keys (linear probing, power-of-two table, grown at half load):
+// the planners look up one state per packet; with a string key in std::unordered_map that lookup
+// was most of the planners' time.
+template <int N, class V>
+class FlatMap {
+public:
+    using Key = std::array<uint64_t, N>;
+    FlatMap() { clear(); }
+    void clear() {
+        keys_.assign(64, Key{});
+        used_.assign(64, 0);
+        vals_.assign(64, V{});
+        size_ = 0;
+    }
+    const V* find(const Key& k) const {
+        const size_t mask = keys_.size() - 1;
+        for (size_t i = hash(k) & mask;; i = (i + 1) & mask) {
+            if (!used_[i]) return nullptr;
+            if (keys_[i] == k) return &vals_[i];
+        }
+    }
+    const V* insert(const Key& k, const V& v) {  // k is not in the map
+        if (2 * (size_ + 1) > keys_.size()) grow();
+        const size_t mask = keys_.size() - 1;
+        size_t i = hash(k) & mask;
+        while (used_[i]) i = (i + 1) & mask;
+        used_[i] = 1;
+        keys_[i] = k;
+        vals_[i] = v;
+        ++size_;
+        return &vals_[i];
+    }
+    size_t size() const { return size_; }
+
+private:
+    static size_t hash(const Key& k) {
+        uint64_t h = 0x9E3779B97F4A7C15ull;
+        for (int i = 0; i < N; ++i) {
+            h = (h ^ k[i]) * 0xff51afd7ed558ccdull;
+            h ^= h >> 29;
+        }
+        return static_cast<size_t>(h ^ (h >> 32));
+    }
+    void grow() {
+        std::vector<Key> ok;
+        std::vector<uint8_t> ou;
+        std::vector<V> ov;
+        ok.swap(keys_);
+        ou.swap(used_);
+        ov.swap(vals_);
+        keys_.assign(ok.size() * 2, Key{});
+        used_.assign(ok.size() * 2, 0);
+        vals_.assign(ok.size() * 2, V{});
+        size_ = 0;
+        for (size_t i = 0; i < ok.size(); ++i)
+            if (ou[i]) insert(ok[i], ov[i]);
+    }
+    std::vector<Key> keys_;
+    std::vector<uint8_t> used_;
+    std::vector<V> vals_;
+    size_t size_ = 0;
+};
+
 // Distinct records, each stored once (plans repeat: an erasure-free stretch is one record).
 class RecordTable {
 public:
@@ -134,14 +197,14 @@ public:
         uint64_t a = 0, b = 0;
         for (int i = 0; i < 8; ++i) a |= static_cast<uint64_t>(static_cast<uint8_t>(e[i])) << (8 * i);
         for (int i = 8; i < kTT; ++i) b |= static_cast<uint64_t>(static_cast<uint8_t>(e[i])) << (8 * (i - 8));
-        auto it = ids_.find(Key{a, b});
-        if (it != ids_.end()) return it->second;
+        const FlatMap<2, uint16_t>::Key key{a, b};
+        if (const uint16_t* f = ids_.find(key)) return *f;
         if (rows_.size() >= 0xffff) throw std::length_error("sdswdf: header rows");
         const uint16_t id = static_cast<uint16_t>(rows_.size());
         std::array<int, kTT> r{};
         for (int i = 0; i < kTT; ++i) r[i] = e[i];
         rows_.push_back(r);
-        ids_.emplace(Key{a, b}, id);
+        ids_.insert(key, id);
         return id;
     }
     const std::array<int, kTT>& row(uint16_t id) const { return rows_[id]; }
@@ -151,14 +214,7 @@ public:
     }
 
 private:
-    struct Key {
-        uint64_t a, b;
-        bool operator==(const Key& o) const { return a == o.a && b == o.b; }
-    };
-    struct KeyHash {
-        size_t operator()(const Key& k) const { return static_cast<size_t>((k.a ^ (k.b * 0x9E3779B97F4A7C15ull)) * 0xff51afd7ed558ccdull >> 17); }
-    };
-    std::unordered_map<Key, uint16_t, KeyHash> ids_;
+    FlatMap<2, uint16_t> ids_;
     std::vector<std::array<int, kTT>> rows_;
 };
 
@@ -171,6 +227,7 @@ public:
                    std::vector<uint8_t> G2)
         : k_(k), n_(n), n2_(n2), sdbo_(sdbo), rules_(std::move(rules)), G2_(std::move(G2)),
           records_(kHdr + n2 * n) {
+        if (n2 - 1 > 11) throw std::invalid_argument("sdswdf: n2 > 12");  // RelayKey
         rec_.resize(static_cast<size_t>(record_bytes()));
         reset();
     }
@@ -208,13 +265,13 @@ public:
         const int lo = 2 * kTT - n_ + 1 - (n2_ - k_);
         const uint32_t wmask = (2 * kTT - lo + 1) >= 32 ? ~0u : ((1u << (2 * kTT - lo + 1)) - 1u);
         const uint32_t ew = (er_bits_ >> lo) & wmask, vw = (valid_bits_ >> lo) & wmask;
-        key_.clear();
-        key_.append(reinterpret_cast<const char*>(&ew), sizeof ew);
-        key_.append(reinterpret_cast<const char*>(&vw), sizeof vw);
-        key_.append(reinterpret_cast<const char*>(win_), sizeof(uint16_t) * static_cast<size_t>(n2_ > 1 ? n2_ - 1 : 0));
-        key_.push_back(static_cast<char>(prev_e10_));
-        auto it = memo_.find(key_);
-        if (it == memo_.end()) {
+        // key: the window's flags, the last n2-1 emitted rows' ids (words 1-3, 4 per word; the
+        // unused ones stay 0) and the previous row's entry T_TOT (word 3, top 16 bits)
+        RelayKey key{static_cast<uint64_t>(ew) | static_cast<uint64_t>(vw) << 32, 0, 0, 0};
+        for (int r = 0; r < n2_ - 1; ++r) key[1 + (r >> 2)] |= static_cast<uint64_t>(win_[r]) << (16 * (r & 3));
+        key[3] |= static_cast<uint64_t>(static_cast<uint16_t>(prev_e10_)) << 48;
+        const Memo* mp = memo_.find(key);
+        if (!mp) {
             for (int i = 0; i < kSlots; ++i) {
                 er_[i] = static_cast<uint8_t>(er_bits_ >> i & 1u);
                 valid_[i] = static_cast<uint8_t>(valid_bits_ >> i & 1u);
@@ -230,9 +287,9 @@ public:
             m.id = records_.intern(rec_.data());
             for (int i = 0; i < kHdr; ++i) m.hdr[i] = static_cast<uint8_t>(header_[n2_ - 1][i]);
             m.row = rows_.intern(header_[n2_ - 1]);
-            it = memo_.emplace(key_, m).first;
+            mp = memo_.insert(key, m);
         }
-        const Memo& m = it->second;
+        const Memo& m = *mp;
         if (n2_ > 1) {
             for (int r = 0; r + 1 < n2_ - 1; ++r) win_[r] = win_[r + 1];
             win_[n2_ - 2] = m.row;
@@ -403,6 +460,7 @@ private:
         uint8_t hdr[kHdr];
         uint16_t row;  // entries 0..T_TOT-1 of the emitted header row
     };
+    using RelayKey = FlatMap<4, Memo>::Key;  // n2 - 1 <= 10 row ids (n2 <= n1 <= T_TOT + 1)
     int k_, n_, n2_, sdbo_;
     std::shared_ptr<const DecodeRules> rules_;
     std::vector<uint8_t> G2_;
@@ -411,8 +469,7 @@ private:
     int header_[kSlots][kHdr];
     RecordTable records_;
     std::vector<uint8_t> rec_;
-    std::string key_;
-    std::unordered_map<std::string, Memo> memo_;
+    FlatMap<4, Memo> memo_;
     RowIds rows_;
     uint32_t er_bits_ = 0, valid_bits_ = 0;
     uint16_t win_[kMaxN] = {};
@@ -426,6 +483,7 @@ class SdDestPlanner {
 public:
     SdDestPlanner(int k, int n, std::shared_ptr<const DecodeRules> rules)
         : k_(k), n_(n), rules_(std::move(rules)), records_(k * n) {
+        if (k + n - 1 > 28) throw std::invalid_argument("sdswdf: k + n - 1 > 28");  // DestKey
         rec_.resize(static_cast<size_t>(record_bytes()));
         reset();
     }
@@ -439,6 +497,7 @@ public:
         memo_.clear();
         rows_.clear();
         valid_bits_ = 0;
+        last_ok_ = false;
         const uint16_t id0 = rows_.intern(header_[0]);
         for (auto& w : ids_) w = id0;
         top_e10_ = kHdr;
@@ -453,20 +512,28 @@ public:
         valid_bits_ = (valid_bits_ >> 1) & ~top;
         if (!erased) valid_bits_ |= top;
         std::memmove(ids_, ids_ + 1, sizeof(uint16_t) * (kSlots - 1));
-        int row[kHdr];
-        for (int i = 0; i < kHdr; ++i) row[i] = erased ? 0 : hdr[i];  // :1709, :1803
-        ids_[kSlots - 1] = rows_.intern(row);
-        top_e10_ = row[kTT];
+        // the row's id: consecutive frames mostly carry the same header (a steady stretch), and a
+        // missing frame's row is zeros (:1709, :1803)
+        uint8_t bytes[kHdr] = {};
+        if (!erased) std::memcpy(bytes, hdr, kHdr);
+        if (!last_ok_ || std::memcmp(bytes, last_hdr_, kHdr) != 0) {
+            int row[kHdr];
+            for (int i = 0; i < kHdr; ++i) row[i] = bytes[i];
+            last_id_ = rows_.intern(row);
+            std::memcpy(last_hdr_, bytes, kHdr);
+            last_ok_ = true;
+        }
+        ids_[kSlots - 1] = last_id_;
+        top_e10_ = bytes[kTT];
         const int lo = kSlots - k_ - n_ + 1;
         const uint32_t vw = valid_bits_ >> lo;
-        key_.clear();
-        key_.append(reinterpret_cast<const char*>(&vw), sizeof vw);
-        key_.append(reinterpret_cast<const char*>(ids_ + lo), sizeof(uint16_t) * static_cast<size_t>(kSlots - lo));
-        key_.push_back(static_cast<char>(top_e10_));
-        auto it = memo_.find(key_);
-        if (it != memo_.end()) {
-            *flag = it->second.flag;
-            return it->second.id;
+        // key: presence, the top row's entry T_TOT (word 0) and the k+n-1 rows' ids (4 per word)
+        DestKey key{};
+        key[0] = static_cast<uint64_t>(vw) | static_cast<uint64_t>(static_cast<uint16_t>(top_e10_)) << 32;
+        for (int r = lo; r < kSlots; ++r) key[1 + ((r - lo) >> 2)] |= static_cast<uint64_t>(ids_[r]) << (16 * ((r - lo) & 3));
+        if (const Memo* f = memo_.find(key)) {
+            *flag = f->flag;
+            return f->id;
         }
         for (int r = 0; r < kSlots; ++r) {
             valid_[r] = static_cast<uint8_t>(valid_bits_ >> r & 1u);
@@ -477,7 +544,7 @@ public:
         Memo m;
         m.flag = decode(rec_.data());
         m.id = records_.intern(rec_.data());
-        memo_.emplace(key_, m);
+        memo_.insert(key, m);
         *flag = m.flag;
         return m.id;
     }
@@ -532,18 +599,21 @@ private:
         int32_t id;
         bool flag;
     };
+    using DestKey = FlatMap<8, Memo>::Key;  // k + n - 1 <= 28 row ids (k, n <= T_TOT + 1)
     int k_, n_;
     std::shared_ptr<const DecodeRules> rules_;
     uint8_t valid_[kSlots];
     int header_[kSlots][kHdr];
     RecordTable records_;
     std::vector<uint8_t> rec_;
-    std::string key_;
-    std::unordered_map<std::string, Memo> memo_;
+    FlatMap<8, Memo> memo_;
     RowIds rows_;
     uint32_t valid_bits_ = 0;
     uint16_t ids_[kSlots] = {};
     int top_e10_ = kHdr;
+    uint8_t last_hdr_[kHdr] = {};  // the last frame's header bytes and their row id
+    uint16_t last_id_ = 0;
+    bool last_ok_ = false;
 };
 
 struct SdRelayArgs {
