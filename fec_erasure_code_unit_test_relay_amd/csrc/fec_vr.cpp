@@ -292,14 +292,17 @@ void VrPlan::start_workers() {
     recs_.resize(nth);
     for (auto& r : recs_) r.clear();
     pending_ = true;
+    // pause-loop iterations a worker polls the queue before sleeping (FEC_VR_SPIN; 0: sleep at once)
+    int spin_max = 4096;
+    if (const char* e = std::getenv("FEC_VR_SPIN")) spin_max = std::max(0, std::atoi(e));
     for (size_t w = 0; w < nth; ++w) {
-        workers_.emplace_back([this, w, home = t_pin_home] {
+        workers_.emplace_back([this, w, spin_max, home = t_pin_home] {
             vr_pin_near(home);
             for (;;) {
                 DecJob j;
                 // poll the queue for a while (a job comes every ~0.5 us while the control loop
                 // runs), then sleep on the condition variable
-                for (int spin = 0; spin < 4096 && qsize_.load(std::memory_order_acquire) == 0; ++spin)
+                for (int spin = 0; spin < spin_max && qsize_.load(std::memory_order_acquire) == 0; ++spin)
                     __builtin_ia32_pause();
                 {
                     std::unique_lock<std::mutex> lk(qmu_);
