@@ -242,6 +242,7 @@ public:
         memo_.clear();
         rows_.clear();
         er_bits_ = valid_bits_ = 0;
+        last_key_ok_ = false;
         const uint16_t id0 = rows_.intern(header_[0]);
         for (auto& w : win_) w = id0;
         prev_e10_ = kHdr;
@@ -270,7 +271,7 @@ public:
         RelayKey key{static_cast<uint64_t>(ew) | static_cast<uint64_t>(vw) << 32, 0, 0, 0};
         for (int r = 0; r < n2_ - 1; ++r) key[1 + (r >> 2)] |= static_cast<uint64_t>(win_[r]) << (16 * (r & 3));
         key[3] |= static_cast<uint64_t>(static_cast<uint16_t>(prev_e10_)) << 48;
-        const Memo* mp = memo_.find(key);
+        const Memo* mp = last_key_ok_ && key == last_key_ ? &last_m_ : memo_.find(key);
         if (!mp) {
             for (int i = 0; i < kSlots; ++i) {
                 er_[i] = static_cast<uint8_t>(er_bits_ >> i & 1u);
@@ -289,7 +290,12 @@ public:
             m.row = rows_.intern(header_[n2_ - 1]);
             mp = memo_.insert(key, m);
         }
-        const Memo& m = *mp;
+        if (mp != &last_m_) {
+            last_key_ = key;
+            last_m_ = *mp;
+            last_key_ok_ = true;
+        }
+        const Memo& m = last_m_;
         if (n2_ > 1) {
             for (int r = 0; r + 1 < n2_ - 1; ++r) win_[r] = win_[r + 1];
             win_[n2_ - 2] = m.row;
@@ -470,6 +476,9 @@ private:
     RecordTable records_;
     std::vector<uint8_t> rec_;
     FlatMap<4, Memo> memo_;
+    RelayKey last_key_{};  // the last state looked up and its memo entry
+    Memo last_m_{};
+    bool last_key_ok_ = false;
     RowIds rows_;
     uint32_t er_bits_ = 0, valid_bits_ = 0;
     uint16_t win_[kMaxN] = {};
@@ -498,6 +507,7 @@ public:
         rows_.clear();
         valid_bits_ = 0;
         last_ok_ = false;
+        last_key_ok_ = false;
         const uint16_t id0 = rows_.intern(header_[0]);
         for (auto& w : ids_) w = id0;
         top_e10_ = kHdr;
@@ -531,7 +541,14 @@ public:
         DestKey key{};
         key[0] = static_cast<uint64_t>(vw) | static_cast<uint64_t>(static_cast<uint16_t>(top_e10_)) << 32;
         for (int r = lo; r < kSlots; ++r) key[1 + ((r - lo) >> 2)] |= static_cast<uint64_t>(ids_[r]) << (16 * ((r - lo) & 3));
+        if (last_key_ok_ && key == last_key_) {  // a steady stretch repeats the state
+            *flag = last_m_.flag;
+            return last_m_.id;
+        }
         if (const Memo* f = memo_.find(key)) {
+            last_key_ = key;
+            last_m_ = *f;
+            last_key_ok_ = true;
             *flag = f->flag;
             return f->id;
         }
@@ -545,6 +562,9 @@ public:
         m.flag = decode(rec_.data());
         m.id = records_.intern(rec_.data());
         memo_.insert(key, m);
+        last_key_ = key;
+        last_m_ = m;
+        last_key_ok_ = true;
         *flag = m.flag;
         return m.id;
     }
@@ -614,6 +634,9 @@ private:
     uint8_t last_hdr_[kHdr] = {};  // the last frame's header bytes and their row id
     uint16_t last_id_ = 0;
     bool last_ok_ = false;
+    DestKey last_key_{};           // the last state looked up and its memo entry
+    Memo last_m_{};
+    bool last_key_ok_ = false;
 };
 
 struct SdRelayArgs {
