@@ -511,6 +511,9 @@ public:
         const uint16_t id0 = rows_.intern(header_[0]);
         for (auto& w : ids_) w = id0;
         top_e10_ = kHdr;
+        win_key_ = DestKey{};
+        const int lo = kSlots - k_ - n_ + 1;
+        for (int r = lo; r < kSlots; ++r) win_key_[1 + ((r - lo) >> 2)] |= static_cast<uint64_t>(ids_[r]) << (16 * ((r - lo) & 3));
     }
     // Frame t2 (in order): its record id; *flag = the loss flag.  The plan is a function of the
     // header rows and presence of the last k+n-1 frames: repeated states are looked up.  Between
@@ -537,10 +540,13 @@ public:
         top_e10_ = bytes[kTT];
         const int lo = kSlots - k_ - n_ + 1;
         const uint32_t vw = valid_bits_ >> lo;
-        // key: presence, the top row's entry T_TOT (word 0) and the k+n-1 rows' ids (4 per word)
-        DestKey key{};
-        key[0] = static_cast<uint64_t>(vw) | static_cast<uint64_t>(static_cast<uint16_t>(top_e10_)) << 32;
-        for (int r = lo; r < kSlots; ++r) key[1 + ((r - lo) >> 2)] |= static_cast<uint64_t>(ids_[r]) << (16 * ((r - lo) & 3));
+        // key: presence, the top row's entry T_TOT (word 0) and the k+n-1 rows' ids (4 per word,
+        // oldest first), slid by one id per frame
+        const int W = kSlots - lo, nw = (W + 3) >> 2;
+        for (int i = 1; i <= nw; ++i) win_key_[i] = (win_key_[i] >> 16) | (i < 7 ? win_key_[i + 1] << 48 : 0);
+        win_key_[1 + ((W - 1) >> 2)] |= static_cast<uint64_t>(last_id_) << (16 * ((W - 1) & 3));
+        win_key_[0] = static_cast<uint64_t>(vw) | static_cast<uint64_t>(static_cast<uint16_t>(top_e10_)) << 32;
+        const DestKey& key = win_key_;
         if (last_key_ok_ && key == last_key_) {  // a steady stretch repeats the state
             *flag = last_m_.flag;
             return last_m_.id;
@@ -634,6 +640,7 @@ private:
     uint8_t last_hdr_[kHdr] = {};  // the last frame's header bytes and their row id
     uint16_t last_id_ = 0;
     bool last_ok_ = false;
+    DestKey win_key_{};            // the current state's key (ids part kept up to date per frame)
     DestKey last_key_{};           // the last state looked up and its memo entry
     Memo last_m_{};
     bool last_key_ok_ = false;
