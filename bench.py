@@ -374,9 +374,13 @@ def extra_configs(steps=5):
     w = VrPlan(pat, P, light=True)
     # the caller on the host's least busy 8-CPU group for config 4 (the plan's threads follow it)
     group = quiet_cpu_group()
-    saved_aff = os.sched_getaffinity(0) if group else None
+    saved_aff = None
     if group:
-        os.sched_setaffinity(0, group)
+        try:
+            saved_aff = os.sched_getaffinity(0)
+            os.sched_setaffinity(0, group)
+        except OSError:
+            group, saved_aff = None, None
 
     def vr_step():
         w.rerun(pat, P, wait=False)
@@ -405,7 +409,10 @@ def extra_configs(steps=5):
         phases.append(w.rerun(pat, P, wait=True).plan_ms)
     plan_s = (time.perf_counter() - t0) / nst
     if saved_aff:
-        os.sched_setaffinity(0, saved_aff)
+        try:
+            os.sched_setaffinity(0, saved_aff)
+        except OSError:
+            pass
     dev_dt = timed(lambda: (v.encode(pl, frames=frames), v.decode(frames[0], frames[2], out=out4, out_len=ol4)), nst)
     fate = torch.from_numpy(v.fate).cuda()
     ok4 = fate != 3
