@@ -978,8 +978,8 @@ extern "C" {
 int fec_sw_state_encode(int max_payload, int k, int n, int k2, int n2, int sdbo, uint8_t* const* slots,
                         const uint8_t* er, int* const* header, uint8_t* cnv, uint8_t* cnsw) {
     using namespace fec;
-    if (!slots || !er || !header || !cnv || !cnsw || k < 1 || n < k || n > kHdr || k2 != k || n2 < k || n2 > n ||
-        max_payload < 1 || (sdbo != 0 && sdbo != 1))
+    if (!slots || !er || !header || !cnv || !cnsw || k < 1 || n < k || n > kHdr || k2 != k || n2 < k || n2 < 2 ||
+        n2 > n || max_payload < 1 || (sdbo != 0 && sdbo != 1))
         return FEC_ERR_ARG;
     SwCtx& c = sw_ctx();
     std::lock_guard<std::mutex> lk(c.mu);
@@ -1183,8 +1183,9 @@ int fec_sdswdf_create(int max_payload, int T1, int N1, int T2, int N2, int sdbo,
     if (!out) return FEC_ERR_ARG;
     *out = nullptr;
     // k2 == k (the only case Decoder_Symbol_Wise handles, :185), n2 <= n1 (the selection reads
-    // temp_codeword[i] for i < n2, :367), T <= T_TOT (header rows hold T_TOT+1 entries)
-    if (T1 < 0 || N1 < 0 || T2 < 0 || N2 < 0 || T1 - N1 != T2 - N2 || T1 - N1 + 1 < 1 || T1 > fec::kTT ||
+    // temp_codeword[i] for i < n2, :367), T <= T_TOT (header rows hold T_TOT+1 entries), n2 >= 2
+    // (a frame's (S+1)*n2 code bytes hold the 2 offset bytes and S blocks only when n2 >= 2)
+    if (T1 < 0 || N1 < 0 || T2 < 1 || N2 < 0 || T1 - N1 != T2 - N2 || T1 - N1 + 1 < 1 || T1 > fec::kTT ||
         T2 > T1 || (sdbo != 0 && sdbo != 1))
         return FEC_ERR_ARG;
     return guarded_sd([&] {

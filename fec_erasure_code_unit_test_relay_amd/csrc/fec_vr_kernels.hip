@@ -547,6 +547,7 @@ __global__ __launch_bounds__(256) void fec_vr_recover_kernel(VrRecArgs a) {
     __shared__ uint8_t glog[256];
     __shared__ uint8_t lcf[4][kVrCoefStride];
     __shared__ const uint8_t* rowp[4][kMaxK + kMaxRuleN];
+    __shared__ int32_t roww[4][kMaxK + kMaxRuleN];  // the row's width in the compact layout
     const int tid = threadIdx.x;
     for (int i = tid; i < 512; i += 256) gexp[i] = a.gf[i];
     for (int i = tid; i < 256; i += 256) glog[i] = a.gf[512 + i];
@@ -555,6 +556,7 @@ __global__ __launch_bounds__(256) void fec_vr_recover_kernel(VrRecArgs a) {
     const int L = a.L;
     uint8_t* lc = lcf[wl];
     const uint8_t** rp = rowp[wl];
+    int32_t* rw = roww[wl];
     for (int r = blockIdx.x * 4 + wl; r < a.nrec; r += gridDim.x * 4) {
         const int64_t x = a.rec_x[r];
         const int j = a.rec_dec[r];
@@ -566,8 +568,12 @@ __global__ __launch_bounds__(256) void fec_vr_recover_kernel(VrRecArgs a) {
         }
         if (lane < k + n - 1) {  // row x-k+1+lane
             const int64_t row = x - k + 1 + lane;
-            rp[lane] = (row < 0 || row >= a.rows) ? nullptr
-                                                   : (row < sw ? a.cur + a.cur_off[row] : a.old + a.old_off[row]);
+            // a row spans [off[row], off[row+1]) (offsets [rows+1]); an empty old row has width 0,
+            // and a symbol past a row's width reads 0 (as the zero-padded rows of the reference)
+            const bool in = row >= 0 && row < a.rows;
+            const int64_t* off = row < sw ? a.cur_off : a.old_off;
+            rp[lane] = !in ? nullptr : (row < sw ? a.cur : a.old) + off[row];
+            rw[lane] = !in ? 0 : static_cast<int32_t>(off[row + 1] - off[row]);
         }
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
@@ -579,6 +585,7 @@ __global__ __launch_bounds__(256) void fec_vr_recover_kernel(VrRecArgs a) {
             if (h < L + 2) {
                 const int s = h / k, i = h - s * k;
                 const uint8_t* const* rpi = rp + (k - 1 - i);  // row of symbol q: x-i+q
+                const int32_t* rwi = rw + (k - 1 - i);
                 const uint8_t* lci = lc + i * n;
                 // every symbol's load first (rows outside the frames read a harmless byte that is
                 // then dropped), so the n loads of a lane are in flight together
@@ -587,14 +594,14 @@ __global__ __launch_bounds__(256) void fec_vr_recover_kernel(VrRecArgs a) {
                 for (int q = 0; q < kMaxRuleN; ++q) {
                     if (q < n) {
                         const uint8_t* row = rpi[q];
-                        sym[q] = *(row ? row + s * n + q : a.cur);
+                        sym[q] = *(row && s * n + q < rwi[q] ? row + s * n + q : a.cur);
                     }
                 }
 #pragma unroll
                 for (int q = 0; q < kMaxRuleN; ++q) {
                     if (q < n) {
                         const int lq = lci[q];
-                        const uint8_t v = (lq == 255 || !rpi[q]) ? 0 : sym[q];
+                        const uint8_t v = (lq == 255 || !rpi[q] || s * n + q >= rwi[q]) ? 0 : sym[q];
                         if (v) acc ^= gexp[lq + glog[v]];
                     }
                 }

@@ -231,7 +231,8 @@ def test_host_plan_sdbo_equals_oracle():
 def test_sdswdf_rejects_unsupported_configurations():
     from fec_erasure_code_unit_test_relay_amd import FecError
     from fec_erasure_code_unit_test_relay_amd.relay import StateDependentRelay
-    for cfg in [(10, 3, 9, 3), (10, 3, 11, 4), (11, 3, 11, 3), (8, 2, 10, 4)]:
+    # ... and n2 = 1 (T2 = N2 = 0 with T1 = N1: k = 1), whose frame cannot hold its blocks
+    for cfg in [(10, 3, 9, 3), (10, 3, 11, 4), (11, 3, 11, 3), (8, 2, 10, 4), (3, 3, 0, 0)]:
         with pytest.raises(FecError):
             StateDependentRelay(L, *cfg)
 
@@ -403,7 +404,8 @@ def test_relay_c_abi_rejects_bad_arguments_before_device_work():
     buf = np.zeros(64, dtype=np.uint64)
     p = buf.ctypes.data_as(vp)
     ERR = -1
-    for args in [(300, 8, 11, 7, 11, 0), (300, 8, 11, 8, 12, 0), (300, 8, 12, 8, 12, 0), (300, 0, 11, 0, 11, 0)]:
+    for args in [(300, 8, 11, 7, 11, 0), (300, 8, 11, 8, 12, 0), (300, 8, 12, 8, 12, 0), (300, 0, 11, 0, 11, 0),
+                 (300, 1, 4, 1, 1, 0)]:
         assert Lb.fec_sw_state_encode(*args, p, p, p, p, p) == ERR, args  # n2 <= n <= T_TOT + 1
     for args in [(300, 8, 11, 7, 11), (300, 8, 11, 8, 7), (300, 0, 11, 0, 11), (0, 8, 11, 8, 11)]:
         assert Lb.fec_sw_encode_1(*args, p, p, p, p, p) == ERR, args  # n2 >= k2 = k
@@ -416,3 +418,6 @@ def test_relay_c_abi_rejects_bad_arguments_before_device_work():
     h = vp()
     assert Lb.fec_sdswdf_create(300, 10, 3, 10, 4, 0, ctypes.byref(h)) == ERR  # k2 != k
     assert Lb.fec_sdswdf_create(300, 9, 3, 10, 4, 0, ctypes.byref(h)) == ERR   # T2 > T1
+    assert Lb.fec_sdswdf_create(300, 3, 3, 0, 0, 0, ctypes.byref(h)) == ERR    # n2 = 1
+    Lb.fec_swdf_create.argtypes = [i] * 5 + [ctypes.POINTER(vp)]
+    assert Lb.fec_swdf_create(300, 3, 3, 0, 0, ctypes.byref(h)) == ERR         # n2 = 1
