@@ -652,6 +652,9 @@ def main():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--packets", type=int, default=1_000_000, help="decoded packets per GPU")
     ap.add_argument("--tbn", default="10,3,3")
+    ap.add_argument("--stream-id", type=int, default=None,
+                    help="payload seed and pattern phase of this stream (default: the rank); a single-rank "
+                         "run with --stream-id r reproduces rank r's stream of a multi-rank run")
     ap.add_argument("--cpu-packets", type=int, default=30000)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-host-inclusive", action="store_true")
@@ -715,8 +718,9 @@ def main():
     codec = Codec(L, T, B, N)
     if args.encode_path != "auto":
         codec.set_encode_path(args.encode_path)
-    seed = stream_seed(rank)
-    pat = stream_pattern(Pf, rank)
+    sid = rank if args.stream_id is None else args.stream_id + rank
+    seed = stream_seed(sid)
+    pat = stream_pattern(Pf, sid)
     payload = fill_payload(0, Pf, L, seed)
     er = torch.from_numpy(pat).cuda()
     cw = torch.empty((Pf, codec.CW), dtype=torch.uint8, device="cuda")
@@ -828,6 +832,18 @@ def main():
     # trivial counter reduction over RCCL
     rec_all, lost_all, erased_all, verified_all = reduce_counters(
         [rec, lost, int(pat[:P].sum()), int(verified)], dist, comm_dev)
+    # every rank's own counters and an output digest (the test compares them with single-rank runs
+    # of the same stream, --stream-id)
+    digest = int(torch.sum(ol.to(torch.int64) * torch.arange(1, P + 1, device=ol.device, dtype=torch.int64)).item())
+    mine = torch.tensor([sid, int(pat[:P].sum()), rec, lost, int(verified), digest], dtype=torch.int64,
+                        device=comm_dev)
+    if world > 1:
+        allr = [torch.zeros_like(mine) for _ in range(world)]
+        dist.all_gather(allr, mine)
+    else:
+        allr = [mine]
+    per_rank = [dict(zip(("stream", "erased", "recovered", "lost", "verified", "out_len_digest"),
+                         (int(x) for x in t.tolist()))) for t in allr]
 
     # per-kernel durations: HIP events on the launch stream, separate pass
     # (warm-up launches first, so the averages are the steady state the rocprofv3 trace sees)
@@ -900,6 +916,7 @@ def main():
                               "note": "untimed replays of the same step before the W warm-up steps "
                                       "(clock / first-touch settling); the timed K steps are unchanged"},
             "decode": {"erased": erased_all, "recovered": rec_all, "lost": lost_all},
+            "per_rank": per_rank,
             "algorithmic_bytes_per_packet": L + codec.CW + codec.CW + 1 + L,
             "algorithmic_GBps": round(world * P * (2 * L + 2 * codec.CW + 1) / (elapsed / args.steps) / 1e9, 1),
             "kernels_ms_per_launch": {k: round(v, 5) for k, v in per_launch.items()},

@@ -871,7 +871,7 @@ const char* fec_strerror(int status) {
     }
 }
 
-int fec_version(void) { return 1; }
+int fec_version(void) { return FEC_AMD_ABI_VERSION; }
 
 int fec_codec_create(int max_payload, int T, int B, int N, fec_codec** out) {
     if (!out) return FEC_ERR_ARG;
@@ -1147,6 +1147,24 @@ constexpr int64_t kServerIdleTicks = 5000000;  // 50 ms of the 100 MHz counter w
 // and the call waits for the launch to end).  A stopped server's coder relaunches it at its next
 // call.  A coder gives its slot back at its next call after its server ended, or when it is
 // destroyed.
+// The coders' streams (the servers and one-shot launches run there) are created with the greatest
+// stream priority: the runtime keeps high-priority streams on hardware queues of their own, apart
+// from the normal-priority streams of torch, the batched calls and the caller, so a live server never
+// holds a launch of those behind it (a plain stream shares one of GPU_MAX_HW_QUEUES queues with the
+// others: a 50 ms server held a launch on another stream for 49.9 ms; on a high-priority stream the
+// worst of 13 launches, the null stream's included, took 18-23 us, profiles/r05/r05q_queue_prio.txt).
+// FEC_CODER_PLAIN_STREAMS=1 (diagnostic) creates them plainly.
+hipError_t coder_stream_create(hipStream_t* s) {
+    static const bool plain = [] {
+        const char* v = std::getenv("FEC_CODER_PLAIN_STREAMS");
+        return v && v[0] == '1';
+    }();
+    if (plain) return hipStreamCreateWithFlags(s, hipStreamNonBlocking);
+    int least = 0, greatest = 0;
+    if (hipDeviceGetStreamPriorityRange(&least, &greatest) != hipSuccess) greatest = 0;
+    return hipStreamCreateWithPriority(s, hipStreamNonBlocking, greatest);
+}
+
 std::atomic<int> g_server_slots{0};
 std::mutex g_server_mu;
 std::vector<ServerHost*> g_server_live;  // persistent servers launched and not seen ended
@@ -1303,7 +1321,10 @@ hipError_t server_wait(ServerHost& sv, uint32_t ticket, hipStream_t s, bool pers
                 server_unregister(sv);
                 if (b->done == ticket) continue;
                 if (hipError_t e = hipStreamQuery(s); e != hipSuccess && e != hipErrorNotReady) return e;
-                if (++relaunches > 8) return hipErrorLaunchFailure;
+                // a server stopped by another coder's launch (its stop word) is contention, not a
+                // failure: relaunched without limit (the ten-second bound below still holds); only
+                // exits of its own (the idle exit race) count toward the limit
+                if (b->stop == 0 && ++relaunches > 8) return hipErrorLaunchFailure;
                 if (hipError_t e2 = server_start(sv, ticket - 1, persistent, launch)) return e2;
                 continue;
             }
@@ -1326,7 +1347,7 @@ int fec_encoder_create(int max_payload, int T, int B, int N, fec_encoder** out) 
         const Geometry& g = c->g;
         if (g.k > 16 || g.k * g.n > 16 * 32) return FEC_ERR_ARG;  // fec_streams_encode_kernel's bounds
         e->res_len_off = (g.CW + 3) & ~3;
-        HIP_TRY(hipStreamCreateWithFlags(&e->s, hipStreamNonBlocking));
+        HIP_TRY(coder_stream_create(&e->s));
         const size_t wb = static_cast<size_t>(std::max(1, g.n - 1)) * g.S * g.k;
         HIP_TRY(hipMalloc(&e->d_win, wb));
         HIP_TRY(hipMemset(e->d_win, 0, wb));
@@ -1457,7 +1478,7 @@ int fec_decoder_create(int max_payload, int T, int B, int N, fec_decoder** out) 
         if (g.T + g.k > fec_decoder::RR) return FEC_ERR_ARG;
         d->planner.reset(new fec::StreamPlanner(g, c->rules.get()));
         d->res_len_off = (g.L + 3) & ~3;
-        HIP_TRY(hipStreamCreateWithFlags(&d->s, hipStreamNonBlocking));
+        HIP_TRY(coder_stream_create(&d->s));
         HIP_TRY(hipMalloc(&d->d_ring, static_cast<size_t>(fec_decoder::RR) * g.CW));
         HIP_TRY(hipMemset(d->d_ring, 0, static_cast<size_t>(fec_decoder::RR) * g.CW));
         HIP_TRY(hipMalloc(&d->d_coef, g.k * g.n));

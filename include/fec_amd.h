@@ -38,6 +38,11 @@ typedef struct fec_codec fec_codec;        /* one (max_payload,T,B,N) configurat
 typedef struct fec_encoder fec_encoder;    /* one streaming encoder (per stream) */
 typedef struct fec_decoder fec_decoder;    /* one streaming decoder (per stream) */
 
+/* ABI version of this header, returned by fec_version().  2: fec_vr_parse_batch takes the plan
+ * first and writes the compact cur/old layout (the d_cw_cur / d_cw_old of the fec_vr_* calls are
+ * compact arrays since then, fec_vr.h); a caller built against version 1 must be rebuilt. */
+#define FEC_AMD_ABI_VERSION 2
+
 const char *fec_strerror(int status);
 int fec_version(void);
 

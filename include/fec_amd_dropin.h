@@ -135,6 +135,11 @@ private:
 // GLOBAL_MAX_SIZE_OF_CODEWORD + 16 bytes (the reference copies that many bytes to offset 2 of a
 // slot of that size), temp_codeword's stale bytes are never forwarded; k2 == k is required (as the
 // reference assumes, Decoder_Symbol_Wise.cpp:185); FLAG_FOR_SDBO is 0 (FEC_Macro.h:50).
+// Slot pointers are not stable: push_current_codeword and rotate_pointers_and_insert_zero_word
+// rotate the codeword_vector_state_dependent / header row pointers instead of copying 30 slots of
+// contents (Decoder_Symbol_Wise.cpp:131-135, :167-171), so a caller must re-read a slot through the
+// member arrays after those calls rather than keep a pointer to it across them (the reference's
+// own callers, Variable_Rate_FEC_Decoder.cpp:636-675 and :1458-1493, always index the arrays).
 #ifdef T_TOT
 static_assert(T_TOT == 10, "the MI355X relay is built for T_TOT = 10 (FEC_Macro.h:32)");
 #endif

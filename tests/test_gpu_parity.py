@@ -405,28 +405,89 @@ def test_streaming_api_many_coders_interleaved():
     assert worst < 0.025, f"a call took {worst * 1e3:.1f} ms"
 
 
-def test_config5_bench_two_ranks_gloo():
-    """BASELINE config 5's partition (one independent stream per rank, no data-path collective):
-    bench.py --gpus 2 starts two rank processes itself; on a one-GPU box they share the card and
-    rendezvous over gloo (FEC_BENCH_BACKEND=gloo).  Both ranks verify their round trip and rank 0
-    reports the whole job."""
+def test_live_server_holds_no_other_launch():
+    """A live per-packet server (FEC_Encoder's resident workgroup, polling for 50 ms after its last
+    call) must not hold work launched elsewhere in the process behind it: with the encoder's server
+    alive, torch kernels on six other streams and on the default stream, and a batched decode
+    (fec_decode_batch on torch's current stream), each finish within 5 ms of their launch.  The
+    coders' streams have the greatest priority, on hardware queues apart from normal streams
+    (fec_codec.hip coder_stream_create); the encoder's calls stay equal to the oracle."""
+    import time
+    torch = pytest.importorskip("torch")
+    T, B, N = 10, 3, 3
+    torch.cuda.set_device(0)
+    enc, oe = fec.FEC_Encoder(L, T, B, N), oracle.Encoder(L, T, B, N)
+    src = oracle.fill_payload(0, 400, L, SEED)
+    codec = fec.Codec(L, T, B, N)
+    Pb = 20000
+    cw, _ = codec.encode(fec.fill_payload(0, Pb, L, SEED))
+    er = torch.from_numpy(load_pattern("bin_erasure")[:Pb].copy()).cuda()
+    codec.workspace(Pb)
+    streams = [torch.cuda.Stream() for _ in range(6)]
+    xs = [torch.zeros(1 << 16, device="cuda") for _ in range(7)]
+    for i, st in enumerate(streams):  # first use of each stream (queue set-up) before the server starts
+        with torch.cuda.stream(st):
+            xs[i].add_(0.0)
+    codec.decode(cw, er)
+    torch.cuda.synchronize()
+    worst = {"stream": 0.0, "default": 0.0, "decode": 0.0}
+    for t in range(40):
+        wire, size = enc.onTransmit(src[t], L, t)  # the server is alive (50 ms idle limit)
+        ocw, osize = oe.onTransmit(src[t], L, t)
+        assert size == osize and (wire == ocw[:size]).all(), t
+        for i, st in enumerate(streams):
+            t0 = time.perf_counter()
+            with torch.cuda.stream(st):
+                xs[i].add_(1.0)
+            st.synchronize()
+            worst["stream"] = max(worst["stream"], time.perf_counter() - t0)
+        t0 = time.perf_counter()
+        xs[6].add_(1.0)  # default stream
+        torch.cuda.current_stream().synchronize()
+        worst["default"] = max(worst["default"], time.perf_counter() - t0)
+        t0 = time.perf_counter()
+        out, ln = codec.decode(cw, er)
+        torch.cuda.current_stream().synchronize()
+        worst["decode"] = max(worst["decode"], time.perf_counter() - t0)
+    for i in range(7):
+        assert float(xs[i][0]) == 40.0
+    assert max(worst.values()) < 0.005, {k: round(v * 1e3, 2) for k, v in worst.items()}
+
+
+def _bench_json(args, env):
     import json
-    env = {k: v for k, v in os.environ.items()
-           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT", "MASTER_ADDR")}
-    env["FEC_BENCH_BACKEND"] = "gloo"
-    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "3",
-                        "--warmup", "1", "--warm-seconds", "0.2", "--packets", "200000", "--no-extra-configs",
-                        "--no-cpu-baseline", "--no-host-inclusive"], env=env, capture_output=True, text=True,
-                       timeout=300)
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py")] + args, env=env, capture_output=True,
+                       text=True, timeout=300)
     assert r.returncode == 0, r.stderr[-3000:]
     lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
     assert len(lines) == 1, r.stdout[-2000:]
-    d = json.loads(lines[0])
+    return json.loads(lines[0])
+
+
+def test_config5_bench_two_ranks_gloo():
+    """BASELINE config 5's partition at its per-GPU size (one independent stream of 1M packets per
+    rank, no data-path collective): bench.py --gpus 2 starts two rank processes itself; on a one-GPU
+    box they share the card and rendezvous over gloo (FEC_BENCH_BACKEND=gloo).  Both ranks verify
+    their round trip, rank 0 reports the whole job, and each rank's counters and output digest equal
+    a single-rank run of the same stream (--stream-id: the same payload seed and pattern phase)."""
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT", "MASTER_ADDR")}
+    env["FEC_BENCH_BACKEND"] = "gloo"
+    common = ["--steps", "3", "--warmup", "1", "--warm-seconds", "0.2", "--packets", "1000000",
+              "--no-extra-configs", "--no-cpu-baseline", "--no-host-inclusive"]
+    d = _bench_json(["--gpus", "2"] + common, env)
     assert d["n_gpus"] == 2 and d["scaling"] == "weak"
     assert d["verified"] is True  # every rank's round trip (bench.py reduces the flags over the ranks)
-    assert d["config"]["packets_per_gpu"] == 200000
+    assert d["config"]["packets_per_gpu"] == 1000000
     dec = d["decode"]  # summed over the two ranks
     assert dec["erased"] > 0 and dec["recovered"] + dec["lost"] == dec["erased"]
+    ranks = d["per_rank"]
+    assert [x["stream"] for x in ranks] == [0, 1]
+    assert sum(x["erased"] for x in ranks) == dec["erased"] and sum(x["lost"] for x in ranks) == dec["lost"]
+    assert ranks[0]["erased"] != ranks[1]["erased"]  # different phases of the pattern
+    for sid in (0, 1):
+        single = _bench_json(["--gpus", "1", "--stream-id", str(sid)] + common, env)
+        assert single["per_rank"] == [ranks[sid]], (single["per_rank"], ranks[sid])
 
 
 def test_cpp_dropin_program(tmp_path):

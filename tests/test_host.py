@@ -28,7 +28,7 @@ def exported_symbols(path):
 
 def test_library_loads_and_exports_c_abi():
     assert os.path.exists(fec.LIB_PATH)
-    assert fec.lib().fec_version() == 1
+    assert fec.lib().fec_version() == 2
     syms = exported_symbols(fec.LIB_PATH)
     names = declared_functions(os.path.join(ROOT, "include", "fec_amd.h"))
     assert len(names) >= 20
