@@ -505,6 +505,38 @@ def relay_chains(steps):
     ok2 = bool(torch.equal(o[D:, 2:2 + L], payload[:P - D])) and int(df.sum()) == 0
     dt2 = timed(lambda: r2.destination(r2.relay(cw, e1d)[0], e2d), steps)
     res["type2"] = {"ms": round(dt2 * 1e3, 3), "GiB_s": round(P * L / dt2 / 2**30, 2), "verified": ok2}
+    # roofline of the two type-2 kernels (fec_sw_fast_relay_kernel / fec_sw_fast_dest_kernel): an event
+    # pair around each launch on its stream, outputs preallocated; algorithmic bytes per packet =
+    # relay: CW + 1 flag read, frame + 1 flag written; destination: frame + 1 flag read, S*k + 1 written
+    fr = torch.empty((P, r2.frame_bytes), dtype=torch.uint8, device="cuda")
+    rf = torch.empty(P, dtype=torch.uint8, device="cuda")
+    dout = torch.empty((P, r2.S * r2.k), dtype=torch.uint8, device="cuda")
+    dfl = torch.empty(P, dtype=torch.uint8, device="cuda")
+
+    def ev_ms(fn, n=20):
+        for _ in range(3):
+            fn()
+        tot = 0.0
+        for _ in range(n):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            fn()
+            e1.record()
+            e1.synchronize()
+            tot += e0.elapsed_time(e1)
+        return tot / n
+    ms_r = ev_ms(lambda: r2.relay(cw, e1d, fr, rf))
+    ms_d = ev_ms(lambda: r2.destination(fr, e2d, dout, dfl))
+    by_r = (c.CW + 1 + r2.frame_bytes + 1) * P
+    by_d = (r2.frame_bytes + 1 + r2.S * r2.k + 1) * P
+    res["type2"]["roofline"] = {
+        "bound": "hbm", "peak": 8000.0, "unit": "GB/s",
+        "relay": {"us": round(ms_r * 1e3, 1), "bytes": by_r, "achieved": round(by_r / ms_r / 1e6, 1),
+                  "frac": round(by_r / ms_r / 1e6 / 8000.0, 4)},
+        "destination": {"us": round(ms_d * 1e3, 1), "bytes": by_d, "achieved": round(by_d / ms_d / 1e6, 1),
+                        "frac": round(by_d / ms_d / 1e6 / 8000.0, 4)},
+        "note": "per kernel: algorithmic bytes / event-timed launch on its stream (an upper bound on the "
+                "kernel); relay CW+1 read + frame+1 written, destination frame+1 read + S*k+1 written per packet"}
     r3 = StateDependentRelay(L, 10, 3, 10, 3)
     o, df = r3.destination(r3.relay(cw, z), z)
     D = r3.delay
