@@ -376,16 +376,13 @@ __global__ __launch_bounds__(256) void fec_vr_copy_gather_kernel(VrCopyArgs a) {
 // the output tile.  Lost packets get a zero row and length 0; recovered ones are left to
 // fec_vr_recover_kernel.  Needs L % 4 == 0 (output dwords inside one row).
 constexpr int kVrCopyOrs = 32;  // output tile row = L + 32 bytes: [6 guard][header 2][payload][spill]
-__global__ __launch_bounds__(256) void fec_vr_copy_kernel(VrCopyArgs a) {
-    __shared__ __attribute__((aligned(16))) uint8_t stage[kVrCopyStage + 16];
-    extern __shared__ __attribute__((aligned(16))) uint8_t otile[];
+// One tile of at most kVrCopyTP packets from x0 (stage: kVrCopyStage + 16 bytes, otile: kVrCopyTP
+// rows of L + kVrCopyOrs bytes; every thread of the workgroup calls it).
+__device__ void vr_copy_tile_generic(const VrCopyArgs& a, int64_t x0, int np, uint8_t* stage, uint8_t* otile) {
     __shared__ int s_ro[kVrCopyTP], s_rw[kVrCopyTP], s_kn[kVrCopyTP], s_cp[kVrCopyTP], s_S[kVrCopyTP];
     const int tid = threadIdx.x, l32 = tid & 31, hw = tid >> 5;
     const int L = a.L, ors = L + kVrCopyOrs;
-    const int64_t ntiles = (a.P + kVrCopyTP - 1) / kVrCopyTP;
-    for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
-        const int64_t x0 = tile * kVrCopyTP;
-        const int np = static_cast<int>(min<int64_t>(kVrCopyTP, a.P - x0));
+    {
         const int64_t o0 = a.cur_off[x0];
         const int64_t span = a.cur_off[x0 + np] - o0;
         const bool staged = span <= kVrCopyStage;  // uniform over the workgroup
@@ -514,6 +511,140 @@ __global__ __launch_bounds__(256) void fec_vr_copy_kernel(VrCopyArgs a) {
         }
         __syncthreads();  // the stage, records and output tile are read before the next tile's
     }
+}
+
+__global__ __launch_bounds__(256) void fec_vr_copy_kernel(VrCopyArgs a) {
+    __shared__ __attribute__((aligned(16))) uint8_t stage[kVrCopyStage + 16];
+    extern __shared__ __attribute__((aligned(16))) uint8_t otile[];
+    const int64_t ntiles = (a.P + kVrCopyTP - 1) / kVrCopyTP;
+    for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+        const int64_t x0 = tile * kVrCopyTP;
+        vr_copy_tile_generic(a, x0, static_cast<int>(min<int64_t>(kVrCopyTP, a.P - x0)), stage, otile);
+    }
+}
+
+
+// The received packets' copies specialised on the reporting decoders' (k, n-k): a workgroup per tile
+// of kVrFastTP consecutive packets.  A tile whose packets are all received and reported in one
+// geometry with a specialisation below (the adaptive tuples (10, b, b) with k >= 4: their rows are
+// at most 848 bytes) is the headline copy (fec_copy_fast.hip) at the compact layout's row stride:
+// the rows (16-byte aligned, one contiguous span) staged with 16-byte loads, a lane per (packet,
+// group of 4 sub-streams) picking the 4k systematic bytes of the group's 4n with constant-selector
+// v_perm_b32 and writing them, shifted by the 2 header bytes, to the LDS output tile as dwords; the
+// tile's payload rows leave as 16-byte stores.  The length (header at symbols 0 and 1 of sub-stream
+// 0) is clamped on the slow path (Decoder.cpp:148-149).  Every other tile (a geometry change, lost
+// or recovered packets, k <= 3) takes the per-packet path above, as two tiles of kVrCopyTP.
+constexpr int kVrFastTP = 32;
+constexpr int kVrFastRow = 496;  // rows of k >= 7 (CW <= 484, CWp <= 496) as a whole tile; k = 4..6 in halves
+constexpr int kVrFastStage = kVrFastTP * kVrFastRow + 64;
+
+template <int K, int NP>
+__device__ void vr_copy_tile_fast(const VrCopyArgs& a, int64_t x0, int np, uint8_t* stage, uint8_t* xo, int* s_cp,
+                                  uint32_t gslow) {
+    constexpr int n = K + NP;
+    const int tid = threadIdx.x, L = a.L;
+    const int S = (L + 2 + K - 1) / K, NS4 = (S + 3) >> 2;
+    const int64_t o0 = a.cur_off[x0];
+    const int rw = static_cast<int>(a.cur_off[x0 + 1] - o0);  // CWp: rows at one stride in an instance
+    const int span = np * rw;
+    stage_to_lds<8, true>(stage, a.cur + o0, 0, span, tid, 256);
+    __syncthreads();
+    if (tid < np) {  // the header: the length, clamped on the slow path
+        const uint8_t* row = stage + tid * rw;
+        const int hdr = row[0] * 256 + row[(1 / K) * n + 1 % K];
+        const int ln = ((gslow >> tid) & 1u) ? min(hdr, L) : hdr;
+        a.out_len[x0 + tid] = ln;
+        s_cp[tid] = min(ln, L);
+    }
+    __syncthreads();
+    for (int it = tid; it < np * NS4; it += 256) {
+        const int g = it / np, t = it - g * np;
+        const int cl = s_cp[t];
+        uint32_t W[K + 1];
+        {
+            const uint32_t* src = reinterpret_cast<const uint32_t*>(stage + t * rw + 4 * n * g);
+            uint32_t D[n];
+#pragma unroll
+            for (int m = 0; m < n; ++m) D[m] = src[m];
+#pragma unroll
+            for (int m = 0; m < K; ++m) {
+                const int i0 = 4 * m, i1 = i0 + 1, i2 = i0 + 2, i3 = i0 + 3;
+                W[m] = gather4(D, (i0 / K) * n + i0 % K, (i1 / K) * n + i1 % K, (i2 / K) * n + i2 % K,
+                               (i3 / K) * n + i3 % K);
+            }
+        }
+        W[K] = 0;
+        uint8_t* orow = xo + t * L;  // payload bytes [4gK-2, 4gK+4K-2): head 2, K-1 dwords, tail 2
+        const int bh = 4 * g * K - 2;
+        if (bh >= 0 && bh < L) *reinterpret_cast<uint16_t*>(orow + bh) = static_cast<uint16_t>(W[0] & keep_bytes(cl - bh));
+#pragma unroll
+        for (int m = 0; m < K - 1; ++m) {
+            const int b = 4 * g * K + 4 * m;
+            if (b < L)
+                *reinterpret_cast<uint32_t*>(orow + b) = __builtin_amdgcn_alignbyte(W[m + 1], W[m], 2) & keep_bytes(cl - b);
+        }
+        const int bt = 4 * g * K + 4 * K - 4;
+        if (bt < L) *reinterpret_cast<uint16_t*>(orow + bt) = static_cast<uint16_t>((W[K - 1] >> 16) & keep_bytes(cl - bt));
+    }
+    __syncthreads();
+    const int ob = np * L;
+    uint8_t* dst = a.out + x0 * L;
+    if ((ob & 15) == 0 && (reinterpret_cast<uintptr_t>(dst) & 15) == 0) {
+        for (int o = 16 * tid; o < ob; o += 16 * 256) *reinterpret_cast<uint4*>(dst + o) = *reinterpret_cast<const uint4*>(xo + o);
+    } else {
+        for (int o = 4 * tid; o < ob; o += 4 * 256) *reinterpret_cast<uint32_t*>(dst + o) = *reinterpret_cast<const uint32_t*>(xo + o);
+    }
+}
+
+#define FEC_VR_FAST_LIST(X) X(11, 0) X(10, 1) X(9, 2) X(8, 3) X(7, 4) X(6, 5) X(5, 6) X(4, 7)
+
+__global__ __launch_bounds__(256) void fec_vr_copy_fast_kernel(VrCopyArgs a) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    __shared__ uint32_t s_geo[kVrFastTP];
+    __shared__ int s_cp[kVrFastTP];
+    __shared__ int s_uniform;
+    uint8_t* stage = smem;                    // kVrFastStage (the generic path: kVrCopyStage + 16)
+    uint8_t* xo = smem + kVrFastStage;        // output tile: kVrFastTP rows of L (generic: kVrCopyTP of L + 32)
+    const int tid = threadIdx.x;
+    const int64_t x0 = static_cast<int64_t>(blockIdx.x) * kVrFastTP;
+    const int np = static_cast<int>(min<int64_t>(kVrFastTP, a.P - x0));
+    if (tid < np) s_geo[tid] = a.geo[x0 + tid];
+    __syncthreads();
+    if (tid < 64) {  // wave 0: all received, one geometry
+        const uint32_t g0 = s_geo[0];
+        const bool same = tid >= np || (((s_geo[tid] >> 16) & 0xff) == 1 && (s_geo[tid] & 0xffff) == (g0 & 0xffff));
+        const uint64_t bad = __ballot(!same);
+        const uint64_t slow = __ballot(tid < np && (s_geo[tid] >> 24) != 0);
+        // ... and cur rows at one stride (the compact layout's CWp of that geometry) over the tile
+        const bool stride1 = a.cur_off[x0 + np] - a.cur_off[x0] == np * (a.cur_off[x0 + 1] - a.cur_off[x0]);
+        if (tid == 0)
+            s_uniform = (bad == 0 && ((g0 >> 16) & 0xff) == 1 && stride1) ? static_cast<int>(g0 & 0xffff) : 0;
+        if (tid == 0) s_geo[0] = static_cast<uint32_t>(slow);  // the slow flags of the tile (bit t)
+    }
+    __syncthreads();
+    const int kn = s_uniform;
+    const uint32_t gslow = s_geo[0];
+    __syncthreads();
+    switch (kn) {
+#define FEC_VR_FAST_CASE(K, NP)                                                                       \
+    case K | ((K + NP) << 8):                                                                         \
+        if (K >= 7) {                                                                                 \
+            vr_copy_tile_fast<K, NP>(a, x0, np, stage, xo, s_cp, gslow);                              \
+        } else {                                                                                      \
+            vr_copy_tile_fast<K, NP>(a, x0, min(np, kVrFastTP / 2), stage, xo, s_cp, gslow);          \
+            __syncthreads();                                                                          \
+            if (np > kVrFastTP / 2)                                                                   \
+                vr_copy_tile_fast<K, NP>(a, x0 + kVrFastTP / 2, np - kVrFastTP / 2, stage, xo, s_cp,  \
+                                         gslow >> (kVrFastTP / 2));                                   \
+        }                                                                                             \
+        return;
+        FEC_VR_FAST_LIST(FEC_VR_FAST_CASE)
+#undef FEC_VR_FAST_CASE
+        default:
+            break;
+    }
+    for (int h = 0; h < kVrFastTP && h < np; h += kVrCopyTP)
+        vr_copy_tile_generic(a, x0 + h, min(kVrCopyTP, np - h), stage, xo);
 }
 
 // Per-row offsets of the compact layout, one thread per row s: e = the last instance with
@@ -658,6 +789,17 @@ int vr_launch_copy(const VrCopyArgs& a, void* s) {
                        static_cast<hipStream_t>(s), a);
     const int64_t grid = (a.P + kVrCopyTP - 1) / kVrCopyTP;
     const size_t otile = static_cast<size_t>(kVrCopyTP) * (a.L + kVrCopyOrs);
+    static const bool fast_on = [] {
+        const char* v = std::getenv("FEC_VR_COPY_FAST");
+        return !(v && v[0] == '0');
+    }();
+    const size_t ofast = std::max(static_cast<size_t>(kVrFastTP) * a.L, otile);
+    if (fast_on && (a.L & 3) == 0 && ofast <= 32768) {  // the specialised tiles (the generic ones inside)
+        const int64_t g2 = (a.P + kVrFastTP - 1) / kVrFastTP;
+        hipLaunchKernelGGL(fec_vr_copy_fast_kernel, dim3(static_cast<unsigned>(g2)), dim3(256), kVrFastStage + ofast,
+                           static_cast<hipStream_t>(s), a);
+        return hipGetLastError() == hipSuccess ? FEC_OK : FEC_ERR_HIP;
+    }
     if ((a.L & 3) == 0 && otile <= 32768)
         hipLaunchKernelGGL(fec_vr_copy_kernel, dim3(static_cast<unsigned>(grid)), dim3(256), otile,
                            static_cast<hipStream_t>(s), a);
