@@ -251,18 +251,45 @@ __global__ __launch_bounds__(256) void fec_vr_encode_kernel(VrEncodeArgs a) {
 // The copy's per-packet word, one thread per packet: geo[x] = k | n << 8 | fate << 16 | slow << 24
 // in the reporting decoder's geometry (fate != 1: fate << 16 only).  Paying the chain fate ->
 // decoder -> geometry once here, with a thread per packet, leaves the copy one level of dependent
-// loads (its word) in front of the row bytes.
+// loads (its word) in front of the row bytes.  With a.tdesc, the first lane of each half-wave (a
+// tile of kVrFastTP = 32 packets) also writes the tile's descriptor for fec_vr_copy_fast_kernel:
+// its first cur row's offset, the geometry and row width shared by all its packets when every one
+// is received in one geometry at one row width (else 0), and its slow bits (ballots over the half).
+constexpr int kVrFastTP = 32;
+static_assert(256 % 64 == 0 && 2 * kVrFastTP == 64, "a tile descriptor is a half-wave's");
 __global__ __launch_bounds__(256) void fec_vr_geo_kernel(VrCopyArgs a) {
     const int64_t x = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x;
-    if (x >= a.P) return;
-    const uint32_t f = a.fate[x];
-    uint32_t g = f << 16;
-    if (f == 1) {
-        const int j = a.pk_dec[x];
-        g |= static_cast<uint32_t>(a.inst[4 * j]) | static_cast<uint32_t>(a.inst[4 * j + 1]) << 8 |
-             (a.slow[x] ? 1u << 24 : 0u);
+    const bool in = x < a.P;
+    uint32_t g = 0;
+    int rw = 0;
+    if (in) {
+        const uint32_t f = a.fate[x];
+        g = f << 16;
+        if (f == 1) {
+            const int j = a.pk_dec[x];
+            g |= static_cast<uint32_t>(a.inst[4 * j]) | static_cast<uint32_t>(a.inst[4 * j + 1]) << 8 |
+                 (a.slow[x] ? 1u << 24 : 0u);
+        }
+        a.geo[x] = g;
+        rw = static_cast<int>(a.cur_off[x + 1] - a.cur_off[x]);
     }
-    a.geo[x] = g;
+    if (a.tdesc == nullptr) return;  // uniform over the grid
+    const int lane = static_cast<int>(threadIdx.x & 63), h = lane & 32;
+    const uint32_t g0 = static_cast<uint32_t>(__shfl(static_cast<int>(g), h));
+    const int rw0 = __shfl(rw, h);
+    const bool ok = !in || (((g >> 16) & 0xff) == 1 && (g & 0xffff) == (g0 & 0xffff) && rw == rw0);
+    const uint64_t bad = __ballot(!ok), slow = __ballot(in && (g >> 24) != 0);
+    if ((lane & 31) == 0 && in) {
+        const uint32_t bad_h = static_cast<uint32_t>(bad >> h), slow_h = static_cast<uint32_t>(slow >> h);
+        const int64_t o0 = a.cur_off[x];
+        const bool uni = bad_h == 0 && ((g0 >> 16) & 0xff) == 1 && rw0 > 0 && rw0 < 65536;
+        uint4 d;
+        d.x = static_cast<uint32_t>(o0 & 0xffffffff);
+        d.y = static_cast<uint32_t>(o0 >> 32);
+        d.z = uni ? ((g0 & 0xffff) | static_cast<uint32_t>(rw0) << 16) : 0u;
+        d.w = slow_h;
+        reinterpret_cast<uint4*>(a.tdesc)[x / kVrFastTP] = d;
+    }
 }
 
 // The received packets' systematic copies for L % 4 != 0 (or rows too long for the output tile
@@ -534,19 +561,17 @@ __global__ __launch_bounds__(256) void fec_vr_copy_kernel(VrCopyArgs a) {
 // tile's payload rows leave as 16-byte stores.  The length (header at symbols 0 and 1 of sub-stream
 // 0) is clamped on the slow path (Decoder.cpp:148-149).  Every other tile (a geometry change, lost
 // or recovered packets, k <= 3) takes the per-packet path above, as two tiles of kVrCopyTP.
-constexpr int kVrFastTP = 32;
-constexpr int kVrFastRow = 496;  // rows of k >= 7 (CW <= 484, CWp <= 496) as a whole tile; k = 4..6 in halves
-constexpr int kVrFastStage = kVrFastTP * kVrFastRow + 64;
+constexpr int kVrFastRow = 496;  // the fast path stages at most kVrFastTP rows of 496 bytes (CWp of k >= 7 at L = 300)
+constexpr int kVrFastStage = kVrCopyStage + 16;  // >= kVrFastTP * kVrFastRow: the generic path's stage
+static_assert(kVrFastTP * kVrFastRow <= kVrFastStage, "fast stage");
 
 template <int K, int NP>
-__device__ void vr_copy_tile_fast(const VrCopyArgs& a, int64_t x0, int np, uint8_t* stage, uint8_t* xo, int* s_cp,
-                                  uint32_t gslow) {
+__device__ __forceinline__ void vr_copy_tile_fast(const VrCopyArgs& a, int64_t x0, int np, int64_t o0, int rw, uint8_t* stage,
+                                  uint8_t* xo, int* s_cp, uint32_t gslow) {
     constexpr int n = K + NP;
     const int tid = threadIdx.x, L = a.L;
     const int S = (L + 2 + K - 1) / K, NS4 = (S + 3) >> 2;
-    const int64_t o0 = a.cur_off[x0];
-    const int rw = static_cast<int>(a.cur_off[x0 + 1] - o0);  // CWp: rows at one stride in an instance
-    const int span = np * rw;
+    const int span = np * rw;  // rw = CWp: the tile's rows at one stride
     stage_to_lds<8, true>(stage, a.cur + o0, 0, span, tid, 256);
     __syncthreads();
     if (tid < np) {  // the header: the length, clamped on the slow path
@@ -590,7 +615,86 @@ __device__ void vr_copy_tile_fast(const VrCopyArgs& a, int64_t x0, int np, uint8
     const int ob = np * L;
     uint8_t* dst = a.out + x0 * L;
     if ((ob & 15) == 0 && (reinterpret_cast<uintptr_t>(dst) & 15) == 0) {
-        for (int o = 16 * tid; o < ob; o += 16 * 256) *reinterpret_cast<uint4*>(dst + o) = *reinterpret_cast<const uint4*>(xo + o);
+        for (int o = 16 * tid; o < ob; o += 16 * 256) nt_store16(dst + o, *reinterpret_cast<const uint4*>(xo + o));
+    } else {
+        for (int o = 4 * tid; o < ob; o += 4 * 256) *reinterpret_cast<uint32_t*>(dst + o) = *reinterpret_cast<const uint32_t*>(xo + o);
+    }
+}
+
+// The same tile without the stage: a lane per (packet, group of 4 sub-streams), 64 / NS4 packets
+// per wave, the group's 4n codeword bytes loaded straight into registers (buffer loads at dword
+// alignment; reads past cur return zero), the header from the packet's first lane by a lane
+// shuffle.  No LDS read of the rows: the staged version's dword reads run at the row stride (a
+// multiple of 16 bytes), 4- to 16-way bank conflicts.
+template <int NW>
+__device__ __forceinline__ void load_dwords(__amdgpu_buffer_rsrc_t r, int off, uint32_t (&D)[NW]) {
+    typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+    typedef uint32_t v2u __attribute__((ext_vector_type(2)));
+#pragma unroll
+    for (int c = 0; c + 4 <= NW; c += 4) {
+        const v4u v = __builtin_amdgcn_raw_buffer_load_b128(r, off + 4 * c, 0, 0);
+        D[c] = v.x;
+        D[c + 1] = v.y;
+        D[c + 2] = v.z;
+        D[c + 3] = v.w;
+    }
+    constexpr int c0 = NW & ~3, rem = NW & 3;
+    if constexpr (rem >= 2) {
+        const v2u v = __builtin_amdgcn_raw_buffer_load_b64(r, off + 4 * c0, 0, 0);
+        D[c0] = v.x;
+        D[c0 + 1] = v.y;
+    }
+    if constexpr (rem == 1 || rem == 3) D[NW - 1] = __builtin_amdgcn_raw_buffer_load_b32(r, off + 4 * (NW - 1), 0, 0);
+}
+
+template <int K, int NP>
+__device__ __forceinline__ void vr_copy_tile_direct(const VrCopyArgs& a, int64_t x0, int np, int64_t o0, int rw,
+                                                    uint8_t* xo, uint32_t gslow) {
+    constexpr int n = K + NP;
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, L = a.L;
+    const int S = (L + 2 + K - 1) / K, NS4 = (S + 3) >> 2;
+    const int ppw = 64 / NS4;  // NS4 <= 64 (launch condition)
+    const int pl = lane / NS4, g = lane - pl * NS4;
+    const int64_t left = a.cur_bytes - o0;
+    const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<uint8_t*>(a.cur + o0), 0, static_cast<int>(left < 0x7fffffff ? left : 0x7fffffff), 0x00020000);
+    for (int p0 = wv * ppw; p0 < np; p0 += 4 * ppw) {
+        const int t = p0 + pl;
+        const bool on = pl < ppw && t < np;
+        uint32_t D[n];
+        load_dwords<n>(r, on ? t * rw + 4 * n * g : 0x7ffffff0, D);
+        // header (symbols 0 and 1 of sub-stream 0: bytes 0 and 1 for k > 1) on the packet's first lane
+        const int hdr = static_cast<int>(((D[0] & 0xff) << 8) | ((D[0] >> 8) & 0xff));
+        const int ln0 = ((gslow >> (t & 31)) & 1u) ? min(hdr, L) : hdr;
+        const int ln = __shfl(ln0, pl * NS4);
+        if (on && g == 0) a.out_len[x0 + t] = ln;
+        const int cl = min(ln, L);
+        if (!on) continue;
+        uint32_t W[K + 1];
+#pragma unroll
+        for (int m = 0; m < K; ++m) {
+            const int i0 = 4 * m, i1 = i0 + 1, i2 = i0 + 2, i3 = i0 + 3;
+            W[m] = gather4(D, (i0 / K) * n + i0 % K, (i1 / K) * n + i1 % K, (i2 / K) * n + i2 % K,
+                           (i3 / K) * n + i3 % K);
+        }
+        W[K] = 0;
+        uint8_t* orow = xo + t * L;  // payload bytes [4gK-2, 4gK+4K-2): head 2, K-1 dwords, tail 2
+        const int bh = 4 * g * K - 2;
+        if (bh >= 0 && bh < L) *reinterpret_cast<uint16_t*>(orow + bh) = static_cast<uint16_t>(W[0] & keep_bytes(cl - bh));
+#pragma unroll
+        for (int m = 0; m < K - 1; ++m) {
+            const int b = 4 * g * K + 4 * m;
+            if (b < L)
+                *reinterpret_cast<uint32_t*>(orow + b) = __builtin_amdgcn_alignbyte(W[m + 1], W[m], 2) & keep_bytes(cl - b);
+        }
+        const int bt = 4 * g * K + 4 * K - 4;
+        if (bt < L) *reinterpret_cast<uint16_t*>(orow + bt) = static_cast<uint16_t>((W[K - 1] >> 16) & keep_bytes(cl - bt));
+    }
+    __syncthreads();
+    const int ob = np * L;
+    uint8_t* dst = a.out + x0 * L;
+    if ((ob & 15) == 0 && (reinterpret_cast<uintptr_t>(dst) & 15) == 0) {
+        for (int o = 16 * tid; o < ob; o += 16 * 256) nt_store16(dst + o, *reinterpret_cast<const uint4*>(xo + o));
     } else {
         for (int o = 4 * tid; o < ob; o += 4 * 256) *reinterpret_cast<uint32_t*>(dst + o) = *reinterpret_cast<const uint32_t*>(xo + o);
     }
@@ -598,53 +702,60 @@ __device__ void vr_copy_tile_fast(const VrCopyArgs& a, int64_t x0, int np, uint8
 
 #define FEC_VR_FAST_LIST(X) X(11, 0) X(10, 1) X(9, 2) X(8, 3) X(7, 4) X(6, 5) X(5, 6) X(4, 7)
 
-__global__ __launch_bounds__(256) void fec_vr_copy_fast_kernel(VrCopyArgs a) {
-    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-    __shared__ uint32_t s_geo[kVrFastTP];
-    __shared__ int s_cp[kVrFastTP];
-    __shared__ int s_uniform;
-    uint8_t* stage = smem;                    // kVrFastStage (the generic path: kVrCopyStage + 16)
-    uint8_t* xo = smem + kVrFastStage;        // output tile: kVrFastTP rows of L (generic: kVrCopyTP of L + 32)
-    const int tid = threadIdx.x;
-    const int64_t x0 = static_cast<int64_t>(blockIdx.x) * kVrFastTP;
+// One tile (descriptor d) of fec_vr_copy_fast_kernel.
+__device__ __forceinline__ void vr_copy_fast_tile(const VrCopyArgs& a, int64_t tile, uint4 d, uint8_t* stage, uint8_t* xo,
+                                                  int* s_cp) {
+    const int64_t x0 = tile * kVrFastTP;
     const int np = static_cast<int>(min<int64_t>(kVrFastTP, a.P - x0));
-    if (tid < np) s_geo[tid] = a.geo[x0 + tid];
-    __syncthreads();
-    if (tid < 64) {  // wave 0: all received, one geometry
-        const uint32_t g0 = s_geo[0];
-        const bool same = tid >= np || (((s_geo[tid] >> 16) & 0xff) == 1 && (s_geo[tid] & 0xffff) == (g0 & 0xffff));
-        const uint64_t bad = __ballot(!same);
-        const uint64_t slow = __ballot(tid < np && (s_geo[tid] >> 24) != 0);
-        // ... and cur rows at one stride (the compact layout's CWp of that geometry) over the tile
-        const bool stride1 = a.cur_off[x0 + np] - a.cur_off[x0] == np * (a.cur_off[x0 + 1] - a.cur_off[x0]);
-        if (tid == 0)
-            s_uniform = (bad == 0 && ((g0 >> 16) & 0xff) == 1 && stride1) ? static_cast<int>(g0 & 0xffff) : 0;
-        if (tid == 0) s_geo[0] = static_cast<uint32_t>(slow);  // the slow flags of the tile (bit t)
+    const int64_t o0 = static_cast<int64_t>(static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(d.x)))) |
+                       static_cast<int64_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(d.y))) << 32;
+    const uint32_t dz = static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(d.z)));
+    const uint32_t gslow = static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(d.w)));
+    const int kn = static_cast<int>(dz & 0xffff), rw = static_cast<int>(dz >> 16);
+    // the stage holds the whole tile's rows, or half of them (two passes), else the per-packet path
+    constexpr int cap = kVrFastTP * kVrFastRow;
+    const int step = np * rw <= cap ? np : ((kVrFastTP / 2) * rw <= cap ? kVrFastTP / 2 : 0);
+    if (a.direct) {  // whole tiles, rows read straight into registers
+        switch (kn) {
+#define FEC_VR_DIRECT_CASE(K, NP)                                                            \
+    case K | ((K + NP) << 8):                                                                \
+        if ((a.L + 2 + K - 1) / K <= 256) { /* NS4 <= 64: a packet's lanes in one wave */     \
+            vr_copy_tile_direct<K, NP>(a, x0, np, o0, rw, xo, gslow);                        \
+            return;                                                                          \
+        }                                                                                    \
+        break;
+            FEC_VR_FAST_LIST(FEC_VR_DIRECT_CASE)
+#undef FEC_VR_DIRECT_CASE
+            default: break;
+        }
     }
-    __syncthreads();
-    const int kn = s_uniform;
-    const uint32_t gslow = s_geo[0];
-    __syncthreads();
-    switch (kn) {
-#define FEC_VR_FAST_CASE(K, NP)                                                                       \
-    case K | ((K + NP) << 8):                                                                         \
-        if (K >= 7) {                                                                                 \
-            vr_copy_tile_fast<K, NP>(a, x0, np, stage, xo, s_cp, gslow);                              \
-        } else {                                                                                      \
-            vr_copy_tile_fast<K, NP>(a, x0, min(np, kVrFastTP / 2), stage, xo, s_cp, gslow);          \
-            __syncthreads();                                                                          \
-            if (np > kVrFastTP / 2)                                                                   \
-                vr_copy_tile_fast<K, NP>(a, x0 + kVrFastTP / 2, np - kVrFastTP / 2, stage, xo, s_cp,  \
-                                         gslow >> (kVrFastTP / 2));                                   \
-        }                                                                                             \
+    switch (step > 0 ? kn : 0) {
+#define FEC_VR_FAST_CASE(K, NP)                                                                              \
+    case K | ((K + NP) << 8):                                                                                \
+        for (int h = 0; h < np; h += step) {                                                                 \
+            if (h > 0) __syncthreads();                                                                      \
+            vr_copy_tile_fast<K, NP>(a, x0 + h, min(step, np - h), o0 + static_cast<int64_t>(h) * rw, rw, stage, \
+                                     xo, s_cp, gslow >> h);                                                  \
+        }                                                                                                    \
         return;
         FEC_VR_FAST_LIST(FEC_VR_FAST_CASE)
 #undef FEC_VR_FAST_CASE
-        default:
-            break;
+        default: break;
     }
     for (int h = 0; h < kVrFastTP && h < np; h += kVrCopyTP)
         vr_copy_tile_generic(a, x0 + h, min(kVrCopyTP, np - h), stage, xo);
+}
+
+// A workgroup per tile (resident workgroups walking several tiles, the next descriptor loaded
+// ahead, measured slower: 88.0 vs 83.7 us, and they held the recovery's waves off the CUs until
+// the copy's end, 90 vs 61 us; profiles/r05/vr/r05z_*).
+__global__ __launch_bounds__(256) void fec_vr_copy_fast_kernel(VrCopyArgs a) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    __shared__ int s_cp[kVrFastTP];
+    uint8_t* stage = smem;                    // kVrFastStage (the generic path: kVrCopyStage + 16)
+    uint8_t* xo = smem + kVrFastStage;        // output tile: kVrFastTP rows of L (generic: kVrCopyTP of L + 32)
+    const int64_t tile = blockIdx.x;
+    vr_copy_fast_tile(a, tile, reinterpret_cast<const uint4*>(a.tdesc)[tile], stage, xo, s_cp);
 }
 
 // Per-row offsets of the compact layout, one thread per row s: e = the last instance with
@@ -709,6 +820,9 @@ __global__ __launch_bounds__(256) void fec_vr_recover_kernel(VrRecArgs a) {
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        // (the symbol loads of all five 64-byte steps of a packet issued together -- one round trip
+        // instead of five -- measured slower beside the copy: 95 vs 61 us, 133 VGPRs,
+        // profiles/r05/vr/r05za_*)
         int ln = 0;
         for (int h0 = 0; h0 < L + 2; h0 += 64) {
             const int h = h0 + lane;
@@ -789,15 +903,16 @@ int vr_launch_copy(const VrCopyArgs& a, void* s) {
                        static_cast<hipStream_t>(s), a);
     const int64_t grid = (a.P + kVrCopyTP - 1) / kVrCopyTP;
     const size_t otile = static_cast<size_t>(kVrCopyTP) * (a.L + kVrCopyOrs);
-    static const bool fast_on = [] {
-        const char* v = std::getenv("FEC_VR_COPY_FAST");
-        return !(v && v[0] == '0');
-    }();
+    const char* fv = std::getenv("FEC_VR_COPY_FAST");  // (an A/B switch, read per launch: 0 off, s staged)
+    const bool fast_on = !(fv && fv[0] == '0');
+    VrCopyArgs b = a;
+    if (fv && fv[0] == 's') b.direct = 0;
     const size_t ofast = std::max(static_cast<size_t>(kVrFastTP) * a.L, otile);
-    if (fast_on && (a.L & 3) == 0 && ofast <= 32768) {  // the specialised tiles (the generic ones inside)
+    if (fast_on && a.tdesc && (a.L & 3) == 0 && ofast <= 32768) {  // the specialised tiles (the generic ones inside)
         const int64_t g2 = (a.P + kVrFastTP - 1) / kVrFastTP;
-        hipLaunchKernelGGL(fec_vr_copy_fast_kernel, dim3(static_cast<unsigned>(g2)), dim3(256), kVrFastStage + ofast,
-                           static_cast<hipStream_t>(s), a);
+        const size_t lds = kVrFastStage + ofast;
+        hipLaunchKernelGGL(fec_vr_copy_fast_kernel, dim3(static_cast<unsigned>(g2)), dim3(256), lds,
+                           static_cast<hipStream_t>(s), b);
         return hipGetLastError() == hipSuccess ? FEC_OK : FEC_ERR_HIP;
     }
     if ((a.L & 3) == 0 && otile <= 32768)

@@ -359,3 +359,33 @@ def test_gpu_adaptive_encode_paths_agree(monkeypatch, L, with_len):
     for name in ("per_tuple", "generic"):
         for a, b in zip(got["multi"], got[name]):
             assert torch.equal(a, b), name
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("L", [296, 600, 1000])
+def test_gpu_adaptive_decode_copy_paths_agree(monkeypatch, L):
+    """Config 4's decode at other payload sizes: the received packets' copy through the specialised
+    tiles (fec_vr_copy_fast_kernel: whole tiles at L <= 300ish, half tiles at L = 600, the per-packet
+    path inside it at L = 1000) equals the per-packet copy kernel alone (FEC_VR_COPY_FAST=0), with a
+    per-packet length array, and every reported packet comes back bit-exact."""
+    import torch
+    from fec_erasure_code_unit_test_relay_amd import fill_payload
+    torch.cuda.set_device(0)
+    pat = load_pattern("bin_erasure")
+    P = 40000
+    got = {}
+    for fast in ("1", "0"):
+        monkeypatch.setenv("FEC_VR_COPY_FAST", fast)
+        v = VrPlan(pat, P, max_payload=L)
+        payload = fill_payload(0, v.sent, L, 0x5EED)
+        lengths = torch.from_numpy(np.random.default_rng(11).integers(0, L + 1, v.sent).astype(np.int32)).cuda()
+        cw_cur, _, cw_old, _ = v.encode(payload, lengths=lengths)
+        out, out_len = v.decode(cw_cur, cw_old)
+        torch.cuda.synchronize()
+        got[fast] = (out.clone(), out_len.clone())
+        ok = torch.from_numpy(v.fate != 3).cuda()
+        ln = lengths[:P].long()
+        assert bool((out_len[ok] == ln[ok]).all())
+        keep = torch.arange(L, device="cuda")[None, :] < ln[:, None]
+        assert bool(((out == payload[:P] * keep)[ok]).all())
+    assert torch.equal(got["1"][0], got["0"][0]) and torch.equal(got["1"][1], got["0"][1])

@@ -1,16 +1,17 @@
 #!/bin/bash
 # Config 4 device work: VR GPU tests, then decode/encode timing with an env A/B (VAR=0 vs 1) and a
-# kernel trace of the default.   gpurun -- bash tools/gpu_vr_ab.sh <tag> <VAR>
+# kernel trace of the default.   gpurun -- bash tools/gpu_vr_ab.sh <tag> <VAR> ["v1 v2 ..."]
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 OUT=$R/gpurun_out/${1:-vrab}
 VAR=${2:-FEC_VR_COPY_FAST}
+VALS=${3:-0 1 0 1}
 mkdir -p $OUT
 cd $R
 export TMPDIR=/tmp
 timeout -k 10 300 python -u -m pytest tests/test_vr.py -m gpu -x -q --timeout 120 --timeout-method thread > $OUT/pytest.log 2>&1 || { echo "pytest failed"; tail -30 $OUT/pytest.log; exit 1; }
 tail -1 $OUT/pytest.log
-for v in 0 1 0 1; do
+for v in $VALS; do
     echo "$VAR=$v"; env $VAR=$v timeout -k 10 120 python -u tools/vr_prof.py 20 2>&1 | grep -E "^encode:|^decode:" | tee -a $OUT/ab.log || exit 1
 done
 timeout -k 10 180 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o run -- python3 tools/vr_prof.py 20 > $OUT/rocprof.log 2>&1 || { echo "rocprof failed"; tail -20 $OUT/rocprof.log; exit 1; }
