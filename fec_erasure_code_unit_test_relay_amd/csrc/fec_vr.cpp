@@ -1544,7 +1544,7 @@ int prepare_decode(fec_vr_plan* v, hipStream_t s) {
     const size_t o_fate = (P * 4 + 255) & ~size_t(255), o_slow = (o_fate + P + 255) & ~size_t(255);
     const size_t o_geo = (o_slow + P + 255) & ~size_t(255);  // device scratch of the copy
     const size_t o_desc = (o_geo + 4 * P + 255) & ~size_t(255);
-    if (int st = Upload::reserve(&v->d_pk, &v->d_pk_cap, o_desc + 16 * ((P + 31) / 32 + 1), u.used, s)) return st;
+    if (int st = Upload::reserve(&v->d_pk, &v->d_pk_cap, o_desc + 32 * ((P + 31) / 32 + 1), u.used, s)) return st;
     uint8_t* d = static_cast<uint8_t*>(v->d_pk);
     if (hipMemcpyAsync(d, p.fate_dec.data(), P * 4, hipMemcpyHostToDevice, s) != hipSuccess ||
         hipMemcpyAsync(d + o_fate, p.fate.data(), P, hipMemcpyHostToDevice, s) != hipSuccess ||
@@ -1830,7 +1830,7 @@ int fec_vr_decode_batch(fec_vr_plan* v, const uint8_t* d_cw_cur, const uint8_t* 
     const auto& p = v->plan;
     if (int st = ensure_rowoff(v, s)) return st;
     fec::VrCopyArgs ca{d_cw_cur, cur_off(v), v->d_pk_dec, v->d_inst, v->d_fate, v->d_slow, p.P, p.L, d_out,
-                       d_out_len, v->d_geo, v->d_tdesc, v->cur_bytes, 1};
+                       d_out_len, v->d_geo, v->d_tdesc, v->cur_bytes};
     // the recovery writes only the rows (and lengths) the copy leaves alone: side by side
     if (int st = v->fork.begin(s)) return st;
     ForkScope scope(v->fork);

@@ -243,11 +243,9 @@ struct VrCopyArgs {     // received packets: systematic bytes of cur[x] in its d
     uint8_t* out;
     int32_t* out_len;
     uint32_t* geo;           // [P] scratch: k | n << 8 | fate << 16 | slow << 24 (fec_vr_geo_kernel)
-    uint32_t* tdesc;         // [ceil(P/32)][4] scratch: per tile of 32 packets {cur_off lo, hi,
-                             //   k | n << 8 | row width << 16 if every packet is received in that
-                             //   geometry at one row width (else 0), slow bits} (fec_vr_geo_kernel)
+    uint32_t* tdesc;         // [ceil(P/32)] scratch: the copy's tile descriptors (fec_vr_geo_kernel,
+                             //   VrTileDesc in fec_vr_kernels.hip, 32 bytes each)
     int64_t cur_bytes;       // bytes of cur (reads past them return zero)
-    int direct;              // fec_vr_copy_fast_kernel: rows into registers (1) or staged in LDS (0)
 };
 struct VrRecArgs {      // recovered packets: coefficient rows over the reporting decoder's inputs
     const uint8_t* cur;

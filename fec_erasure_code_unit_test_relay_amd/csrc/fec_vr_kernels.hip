@@ -257,6 +257,14 @@ __global__ __launch_bounds__(256) void fec_vr_encode_kernel(VrEncodeArgs a) {
 // is received in one geometry at one row width (else 0), and its slow bits (ballots over the half).
 constexpr int kVrFastTP = 32;
 static_assert(256 % 64 == 0 && 2 * kVrFastTP == 64, "a tile descriptor is a half-wave's");
+struct VrTileDesc {  // fec_vr_copy_fast_kernel's tile of kVrFastTP packets
+    int64_t o0;      // byte offset of its first cur row
+    uint32_t g1, g2; // runs 1 and 2: k | n << 8 | row width << 16 (the received packets' geometry)
+    uint16_t split;  // run 2's first packet (>= the tile's packets: one run)
+    uint16_t ok;     // at most two runs, every received packet's row width < 64 KB, something received
+    uint32_t slow, recv, rec;  // bit t: packet t on the slow path / received (fate 1) / recovered (fate 2)
+};
+static_assert(sizeof(VrTileDesc) == 32, "descriptor size (fec_vr.cpp reserves 32 bytes per tile)");
 __global__ __launch_bounds__(256) void fec_vr_geo_kernel(VrCopyArgs a) {
     const int64_t x = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x;
     const bool in = x < a.P;
@@ -274,21 +282,38 @@ __global__ __launch_bounds__(256) void fec_vr_geo_kernel(VrCopyArgs a) {
         rw = static_cast<int>(a.cur_off[x + 1] - a.cur_off[x]);
     }
     if (a.tdesc == nullptr) return;  // uniform over the grid
-    const int lane = static_cast<int>(threadIdx.x & 63), h = lane & 32;
-    const uint32_t g0 = static_cast<uint32_t>(__shfl(static_cast<int>(g), h));
-    const int rw0 = __shfl(rw, h);
-    const bool ok = !in || (((g >> 16) & 0xff) == 1 && (g & 0xffff) == (g0 & 0xffff) && rw == rw0);
-    const uint64_t bad = __ballot(!ok), slow = __ballot(in && (g >> 24) != 0);
-    if ((lane & 31) == 0 && in) {
-        const uint32_t bad_h = static_cast<uint32_t>(bad >> h), slow_h = static_cast<uint32_t>(slow >> h);
-        const int64_t o0 = a.cur_off[x];
-        const bool uni = bad_h == 0 && ((g0 >> 16) & 0xff) == 1 && rw0 > 0 && rw0 < 65536;
-        uint4 d;
-        d.x = static_cast<uint32_t>(o0 & 0xffffffff);
-        d.y = static_cast<uint32_t>(o0 >> 32);
-        d.z = uni ? ((g0 & 0xffff) | static_cast<uint32_t>(rw0) << 16) : 0u;
-        d.w = slow_h;
-        reinterpret_cast<uint4*>(a.tdesc)[x / kVrFastTP] = d;
+    // the tile's runs: run 1 = packets [0, split), run 2 = [split, np), each one row width over all
+    // its packets and one geometry over its received ones (run 1's taken from the tile's first
+    // received packet; a run without one takes the other's, its rows being zero or the recovery's)
+    const int lane = static_cast<int>(threadIdx.x & 63), h = lane & 32, li = lane & 31;
+    const bool recv = in && ((g >> 16) & 0xff) == 1, rec = in && ((g >> 16) & 0xff) == 2;
+    const int kn = static_cast<int>(g & 0xffff);
+    const uint32_t recv_h = static_cast<uint32_t>(__ballot(recv) >> h);
+    const uint32_t rec_h = static_cast<uint32_t>(__ballot(rec) >> h);
+    const uint32_t slow_h = static_cast<uint32_t>(__ballot(in && (g >> 24) != 0) >> h);
+    const uint32_t wide_h = static_cast<uint32_t>(__ballot(in && rw > 0xffff) >> h);
+    const int rw1 = __shfl(rw, h);
+    const int kn_first = __shfl(kn, h + (recv_h ? __builtin_ctz(recv_h) : 0));
+    const uint32_t diff_h = static_cast<uint32_t>(__ballot(in && (rw != rw1 || (recv && kn != kn_first))) >> h);
+    const int split = diff_h ? __builtin_ctz(diff_h) : 32;
+    const uint32_t recv2 = split < 32 ? recv_h & (~0u << split) : 0u;
+    const int rw2 = __shfl(rw, h + (split < 32 ? split : 0));
+    const int kn2 = recv2 ? __shfl(kn, h + __builtin_ctz(recv2)) : kn_first;
+    const uint32_t bad_h =
+        static_cast<uint32_t>(__ballot(in && li >= split && (rw != rw2 || (recv && kn != kn2))) >> h);
+    const uint32_t key1 = static_cast<uint32_t>(kn_first) | static_cast<uint32_t>(rw1 & 0xffff) << 16;
+    const uint32_t key2 = static_cast<uint32_t>(kn2) | static_cast<uint32_t>(rw2 & 0xffff) << 16;
+    if (li == 0 && in) {
+        VrTileDesc d;
+        d.o0 = a.cur_off[x];
+        d.g1 = key1;
+        d.g2 = split < 32 ? key2 : 0u;
+        d.split = static_cast<uint16_t>(min<int64_t>(split, a.P - x));
+        d.ok = (recv_h != 0 && bad_h == 0 && wide_h == 0) ? 1 : 0;  // (rows at one stride per run)
+        d.slow = slow_h;
+        d.recv = recv_h;
+        d.rec = rec_h;
+        reinterpret_cast<VrTileDesc*>(a.tdesc)[x / kVrFastTP] = d;
     }
 }
 
@@ -552,80 +577,23 @@ __global__ __launch_bounds__(256) void fec_vr_copy_kernel(VrCopyArgs a) {
 
 
 // The received packets' copies specialised on the reporting decoders' (k, n-k): a workgroup per tile
-// of kVrFastTP consecutive packets.  A tile whose packets are all received and reported in one
-// geometry with a specialisation below (the adaptive tuples (10, b, b) with k >= 4: their rows are
-// at most 848 bytes) is the headline copy (fec_copy_fast.hip) at the compact layout's row stride:
-// the rows (16-byte aligned, one contiguous span) staged with 16-byte loads, a lane per (packet,
-// group of 4 sub-streams) picking the 4k systematic bytes of the group's 4n with constant-selector
-// v_perm_b32 and writing them, shifted by the 2 header bytes, to the LDS output tile as dwords; the
-// tile's payload rows leave as 16-byte stores.  The length (header at symbols 0 and 1 of sub-stream
-// 0) is clamped on the slow path (Decoder.cpp:148-149).  Every other tile (a geometry change, lost
-// or recovered packets, k <= 3) takes the per-packet path above, as two tiles of kVrCopyTP.
-constexpr int kVrFastRow = 496;  // the fast path stages at most kVrFastTP rows of 496 bytes (CWp of k >= 7 at L = 300)
-constexpr int kVrFastStage = kVrCopyStage + 16;  // >= kVrFastTP * kVrFastRow: the generic path's stage
-static_assert(kVrFastTP * kVrFastRow <= kVrFastStage, "fast stage");
+// of kVrFastTP consecutive packets, described by fec_vr_geo_kernel (VrTileDesc).  A tile whose
+// received packets form at most two runs of one geometry each (a decoder switch inside the tile)
+// with a specialisation below (the adaptive tuples (10, b, b) with k >= 4) is the headline copy
+// (fec_copy_fast.hip) at the compact layout's row stride, without a stage: a lane per (packet,
+// group of 4 sub-streams), 64 / NS4 packets per wave, the group's 4n codeword bytes loaded straight
+// into registers (buffer loads at dword alignment; reads past cur return zero), the 4k systematic
+// bytes picked with constant-selector v_perm_b32 and written, shifted by the 2 header bytes, to the
+// LDS output tile; the length (header at symbols 0 and 1 of sub-stream 0, from the packet's first
+// lane by a lane shuffle) clamped on the slow path (Decoder.cpp:148-149).  A lost packet gets a zero
+// row and length 0; a recovered one is left alone (fec_vr_recover_kernel writes it meanwhile: the
+// tile's rows leave as 16-byte stores, dword stores around such a row).  Every other tile (three
+// or more runs, k <= 3, nothing received) takes the per-packet path above, as two tiles of
+// kVrCopyTP.  (Staging the rows in LDS first, as the headline copy does, measured slower here:
+// 82.5 vs 65.4 us, profiles/r05/vr/r05zb_*: at the compact layout's 16-byte row stride the
+// gather's dword reads conflict 4- to 16-way.)
+constexpr int kVrFastStage = kVrCopyStage + 16;  // the per-packet path's stage
 
-template <int K, int NP>
-__device__ __forceinline__ void vr_copy_tile_fast(const VrCopyArgs& a, int64_t x0, int np, int64_t o0, int rw, uint8_t* stage,
-                                  uint8_t* xo, int* s_cp, uint32_t gslow) {
-    constexpr int n = K + NP;
-    const int tid = threadIdx.x, L = a.L;
-    const int S = (L + 2 + K - 1) / K, NS4 = (S + 3) >> 2;
-    const int span = np * rw;  // rw = CWp: the tile's rows at one stride
-    stage_to_lds<8, true>(stage, a.cur + o0, 0, span, tid, 256);
-    __syncthreads();
-    if (tid < np) {  // the header: the length, clamped on the slow path
-        const uint8_t* row = stage + tid * rw;
-        const int hdr = row[0] * 256 + row[(1 / K) * n + 1 % K];
-        const int ln = ((gslow >> tid) & 1u) ? min(hdr, L) : hdr;
-        a.out_len[x0 + tid] = ln;
-        s_cp[tid] = min(ln, L);
-    }
-    __syncthreads();
-    for (int it = tid; it < np * NS4; it += 256) {
-        const int g = it / np, t = it - g * np;
-        const int cl = s_cp[t];
-        uint32_t W[K + 1];
-        {
-            const uint32_t* src = reinterpret_cast<const uint32_t*>(stage + t * rw + 4 * n * g);
-            uint32_t D[n];
-#pragma unroll
-            for (int m = 0; m < n; ++m) D[m] = src[m];
-#pragma unroll
-            for (int m = 0; m < K; ++m) {
-                const int i0 = 4 * m, i1 = i0 + 1, i2 = i0 + 2, i3 = i0 + 3;
-                W[m] = gather4(D, (i0 / K) * n + i0 % K, (i1 / K) * n + i1 % K, (i2 / K) * n + i2 % K,
-                               (i3 / K) * n + i3 % K);
-            }
-        }
-        W[K] = 0;
-        uint8_t* orow = xo + t * L;  // payload bytes [4gK-2, 4gK+4K-2): head 2, K-1 dwords, tail 2
-        const int bh = 4 * g * K - 2;
-        if (bh >= 0 && bh < L) *reinterpret_cast<uint16_t*>(orow + bh) = static_cast<uint16_t>(W[0] & keep_bytes(cl - bh));
-#pragma unroll
-        for (int m = 0; m < K - 1; ++m) {
-            const int b = 4 * g * K + 4 * m;
-            if (b < L)
-                *reinterpret_cast<uint32_t*>(orow + b) = __builtin_amdgcn_alignbyte(W[m + 1], W[m], 2) & keep_bytes(cl - b);
-        }
-        const int bt = 4 * g * K + 4 * K - 4;
-        if (bt < L) *reinterpret_cast<uint16_t*>(orow + bt) = static_cast<uint16_t>((W[K - 1] >> 16) & keep_bytes(cl - bt));
-    }
-    __syncthreads();
-    const int ob = np * L;
-    uint8_t* dst = a.out + x0 * L;
-    if ((ob & 15) == 0 && (reinterpret_cast<uintptr_t>(dst) & 15) == 0) {
-        for (int o = 16 * tid; o < ob; o += 16 * 256) nt_store16(dst + o, *reinterpret_cast<const uint4*>(xo + o));
-    } else {
-        for (int o = 4 * tid; o < ob; o += 4 * 256) *reinterpret_cast<uint32_t*>(dst + o) = *reinterpret_cast<const uint32_t*>(xo + o);
-    }
-}
-
-// The same tile without the stage: a lane per (packet, group of 4 sub-streams), 64 / NS4 packets
-// per wave, the group's 4n codeword bytes loaded straight into registers (buffer loads at dword
-// alignment; reads past cur return zero), the header from the packet's first lane by a lane
-// shuffle.  No LDS read of the rows: the staged version's dword reads run at the row stride (a
-// multiple of 16 bytes), 4- to 16-way bank conflicts.
 template <int NW>
 __device__ __forceinline__ void load_dwords(__amdgpu_buffer_rsrc_t r, int off, uint32_t (&D)[NW]) {
     typedef uint32_t v4u __attribute__((ext_vector_type(4)));
@@ -647,29 +615,32 @@ __device__ __forceinline__ void load_dwords(__amdgpu_buffer_rsrc_t r, int off, u
     if constexpr (rem == 1 || rem == 3) D[NW - 1] = __builtin_amdgcn_raw_buffer_load_b32(r, off + 4 * (NW - 1), 0, 0);
 }
 
+// Packets [lo, hi) of the tile (one geometry, rows from byte ob of cur at stride rw) into the
+// output tile xo (row t at t * L) and their lengths.
 template <int K, int NP>
-__device__ __forceinline__ void vr_copy_tile_direct(const VrCopyArgs& a, int64_t x0, int np, int64_t o0, int rw,
-                                                    uint8_t* xo, uint32_t gslow) {
+__device__ __forceinline__ void vr_copy_run_direct(const VrCopyArgs& a, const VrTileDesc& d, int64_t x0, int lo, int hi,
+                                                   int64_t ob, int rw, uint8_t* xo) {
     constexpr int n = K + NP;
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, L = a.L;
     const int S = (L + 2 + K - 1) / K, NS4 = (S + 3) >> 2;
-    const int ppw = 64 / NS4;  // NS4 <= 64 (launch condition)
+    const int ppw = 64 / NS4;  // NS4 <= 64 (the caller's condition)
     const int pl = lane / NS4, g = lane - pl * NS4;
-    const int64_t left = a.cur_bytes - o0;
+    const int64_t left = a.cur_bytes - ob;
     const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(
-        const_cast<uint8_t*>(a.cur + o0), 0, static_cast<int>(left < 0x7fffffff ? left : 0x7fffffff), 0x00020000);
-    for (int p0 = wv * ppw; p0 < np; p0 += 4 * ppw) {
+        const_cast<uint8_t*>(a.cur + ob), 0, static_cast<int>(left < 0x7fffffff ? left : 0x7fffffff), 0x00020000);
+    for (int p0 = lo + wv * ppw; p0 < hi; p0 += 4 * ppw) {
         const int t = p0 + pl;
-        const bool on = pl < ppw && t < np;
+        const bool on = pl < ppw && t < hi;
+        const bool recv = on && ((d.recv >> t) & 1u), rec = on && ((d.rec >> t) & 1u);
         uint32_t D[n];
-        load_dwords<n>(r, on ? t * rw + 4 * n * g : 0x7ffffff0, D);
+        load_dwords<n>(r, recv ? (t - lo) * rw + 4 * n * g : 0x7ffffff0, D);
         // header (symbols 0 and 1 of sub-stream 0: bytes 0 and 1 for k > 1) on the packet's first lane
         const int hdr = static_cast<int>(((D[0] & 0xff) << 8) | ((D[0] >> 8) & 0xff));
-        const int ln0 = ((gslow >> (t & 31)) & 1u) ? min(hdr, L) : hdr;
+        const int ln0 = !recv ? 0 : (((d.slow >> t) & 1u) ? min(hdr, L) : hdr);
         const int ln = __shfl(ln0, pl * NS4);
-        if (on && g == 0) a.out_len[x0 + t] = ln;
+        if (on && !rec && g == 0) a.out_len[x0 + t] = ln;
         const int cl = min(ln, L);
-        if (!on) continue;
+        if (!on || rec) continue;
         uint32_t W[K + 1];
 #pragma unroll
         for (int m = 0; m < K; ++m) {
@@ -690,57 +661,65 @@ __device__ __forceinline__ void vr_copy_tile_direct(const VrCopyArgs& a, int64_t
         const int bt = 4 * g * K + 4 * K - 4;
         if (bt < L) *reinterpret_cast<uint16_t*>(orow + bt) = static_cast<uint16_t>((W[K - 1] >> 16) & keep_bytes(cl - bt));
     }
-    __syncthreads();
-    const int ob = np * L;
-    uint8_t* dst = a.out + x0 * L;
-    if ((ob & 15) == 0 && (reinterpret_cast<uintptr_t>(dst) & 15) == 0) {
-        for (int o = 16 * tid; o < ob; o += 16 * 256) nt_store16(dst + o, *reinterpret_cast<const uint4*>(xo + o));
-    } else {
-        for (int o = 4 * tid; o < ob; o += 4 * 256) *reinterpret_cast<uint32_t*>(dst + o) = *reinterpret_cast<const uint32_t*>(xo + o);
-    }
 }
 
 #define FEC_VR_FAST_LIST(X) X(11, 0) X(10, 1) X(9, 2) X(8, 3) X(7, 4) X(6, 5) X(5, 6) X(4, 7)
 
-// One tile (descriptor d) of fec_vr_copy_fast_kernel.
-__device__ __forceinline__ void vr_copy_fast_tile(const VrCopyArgs& a, int64_t tile, uint4 d, uint8_t* stage, uint8_t* xo,
-                                                  int* s_cp) {
+// Is (k | n << 8) one of the specialisations, with a packet's groups inside one wave (NS4 <= 64)?
+__device__ __forceinline__ bool vr_direct_ok(int kn, int L) {
+    switch (kn) {
+#define FEC_VR_DIRECT_OK(K, NP) \
+    case K | ((K + NP) << 8): return (L + 2 + K - 1) / K <= 256;
+        FEC_VR_FAST_LIST(FEC_VR_DIRECT_OK)
+#undef FEC_VR_DIRECT_OK
+        default: return false;
+    }
+}
+
+// One tile of fec_vr_copy_fast_kernel.
+__device__ __forceinline__ void vr_copy_fast_tile(const VrCopyArgs& a, int64_t tile, const VrTileDesc& d, uint8_t* stage,
+                                                  uint8_t* xo) {
     const int64_t x0 = tile * kVrFastTP;
     const int np = static_cast<int>(min<int64_t>(kVrFastTP, a.P - x0));
-    const int64_t o0 = static_cast<int64_t>(static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(d.x)))) |
-                       static_cast<int64_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(d.y))) << 32;
-    const uint32_t dz = static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(d.z)));
-    const uint32_t gslow = static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(d.w)));
-    const int kn = static_cast<int>(dz & 0xffff), rw = static_cast<int>(dz >> 16);
-    // the stage holds the whole tile's rows, or half of them (two passes), else the per-packet path
-    constexpr int cap = kVrFastTP * kVrFastRow;
-    const int step = np * rw <= cap ? np : ((kVrFastTP / 2) * rw <= cap ? kVrFastTP / 2 : 0);
-    if (a.direct) {  // whole tiles, rows read straight into registers
-        switch (kn) {
-#define FEC_VR_DIRECT_CASE(K, NP)                                                            \
-    case K | ((K + NP) << 8):                                                                \
-        if ((a.L + 2 + K - 1) / K <= 256) { /* NS4 <= 64: a packet's lanes in one wave */     \
-            vr_copy_tile_direct<K, NP>(a, x0, np, o0, rw, xo, gslow);                        \
-            return;                                                                          \
-        }                                                                                    \
-        break;
-            FEC_VR_FAST_LIST(FEC_VR_DIRECT_CASE)
+    const int L = a.L;
+    const int kn1 = static_cast<int>(d.g1 & 0xffff), rw1 = static_cast<int>(d.g1 >> 16);
+    const int kn2 = static_cast<int>(d.g2 & 0xffff), rw2 = static_cast<int>(d.g2 >> 16);
+    const int split = static_cast<int>(d.split);  // np: one run
+    if (d.ok && vr_direct_ok(kn1, L) && (split >= np || vr_direct_ok(kn2, L))) {
+        // the two runs as straight-line code (in a loop, the cases' loop invariants were hoisted
+        // in front of it all together: 145 VGPRs against 42 for one case)
+        auto run = [&](int lo, int hi, int kn, int rw, int64_t ob) __attribute__((always_inline)) {
+            switch (kn) {
+#define FEC_VR_DIRECT_CASE(K, NP) \
+    case K | ((K + NP) << 8): vr_copy_run_direct<K, NP>(a, d, x0, lo, hi, ob, rw, xo); break;
+                FEC_VR_FAST_LIST(FEC_VR_DIRECT_CASE)
 #undef FEC_VR_DIRECT_CASE
-            default: break;
+                default: break;
+            }
+        };
+        run(0, min(split, np), kn1, rw1, d.o0);
+        if (split < np) run(split, np, kn2, rw2, d.o0 + static_cast<int64_t>(split) * rw1);
+        __syncthreads();
+        const int tid = threadIdx.x;
+        const int ob = np * L;
+        uint8_t* dst = a.out + x0 * L;
+        if ((ob & 15) == 0 && (reinterpret_cast<uintptr_t>(dst) & 15) == 0) {
+            for (int o = 16 * tid; o < ob; o += 16 * 256) {
+                const uint4 v = *reinterpret_cast<const uint4*>(xo + o);
+                if (d.rec == 0) {
+                    nt_store16(dst + o, v);
+                } else {  // rows of recovered packets are the recovery's (L % 4 == 0: dwords in one row)
+                    const uint32_t w4[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+                    for (int q = 0; q < 4; ++q)
+                        if (!((d.rec >> ((o + 4 * q) / L)) & 1u)) *reinterpret_cast<uint32_t*>(dst + o + 4 * q) = w4[q];
+                }
+            }
+        } else {
+            for (int o = 4 * tid; o < ob; o += 4 * 256)
+                if (!((d.rec >> (o / L)) & 1u)) *reinterpret_cast<uint32_t*>(dst + o) = *reinterpret_cast<const uint32_t*>(xo + o);
         }
-    }
-    switch (step > 0 ? kn : 0) {
-#define FEC_VR_FAST_CASE(K, NP)                                                                              \
-    case K | ((K + NP) << 8):                                                                                \
-        for (int h = 0; h < np; h += step) {                                                                 \
-            if (h > 0) __syncthreads();                                                                      \
-            vr_copy_tile_fast<K, NP>(a, x0 + h, min(step, np - h), o0 + static_cast<int64_t>(h) * rw, rw, stage, \
-                                     xo, s_cp, gslow >> h);                                                  \
-        }                                                                                                    \
         return;
-        FEC_VR_FAST_LIST(FEC_VR_FAST_CASE)
-#undef FEC_VR_FAST_CASE
-        default: break;
     }
     for (int h = 0; h < kVrFastTP && h < np; h += kVrCopyTP)
         vr_copy_tile_generic(a, x0 + h, min(kVrCopyTP, np - h), stage, xo);
@@ -751,11 +730,21 @@ __device__ __forceinline__ void vr_copy_fast_tile(const VrCopyArgs& a, int64_t t
 // the copy's end, 90 vs 61 us; profiles/r05/vr/r05z_*).
 __global__ __launch_bounds__(256) void fec_vr_copy_fast_kernel(VrCopyArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-    __shared__ int s_cp[kVrFastTP];
-    uint8_t* stage = smem;                    // kVrFastStage (the generic path: kVrCopyStage + 16)
-    uint8_t* xo = smem + kVrFastStage;        // output tile: kVrFastTP rows of L (generic: kVrCopyTP of L + 32)
+    uint8_t* stage = smem;                    // kVrFastStage (the per-packet path)
+    uint8_t* xo = smem + kVrFastStage;        // output tile: kVrFastTP rows of L (per-packet path: kVrCopyTP of L + 32)
     const int64_t tile = blockIdx.x;
-    vr_copy_fast_tile(a, tile, reinterpret_cast<const uint4*>(a.tdesc)[tile], stage, xo, s_cp);
+    const VrTileDesc* dp = reinterpret_cast<const VrTileDesc*>(a.tdesc) + tile;
+    VrTileDesc d;  // one scalar load of the descriptor in front of the row bytes
+    d.o0 = static_cast<int64_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(dp->o0 & 0xffffffff)) & 0xffffffffu) |
+           static_cast<int64_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(dp->o0 >> 32))) << 32;
+    d.g1 = static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(dp->g1)));
+    d.g2 = static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(dp->g2)));
+    d.split = static_cast<uint16_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(dp->split)));
+    d.ok = static_cast<uint16_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(dp->ok)));
+    d.slow = static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(dp->slow)));
+    d.recv = static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(dp->recv)));
+    d.rec = static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(dp->rec)));
+    vr_copy_fast_tile(a, tile, d, stage, xo);
 }
 
 // Per-row offsets of the compact layout, one thread per row s: e = the last instance with
@@ -903,16 +892,14 @@ int vr_launch_copy(const VrCopyArgs& a, void* s) {
                        static_cast<hipStream_t>(s), a);
     const int64_t grid = (a.P + kVrCopyTP - 1) / kVrCopyTP;
     const size_t otile = static_cast<size_t>(kVrCopyTP) * (a.L + kVrCopyOrs);
-    const char* fv = std::getenv("FEC_VR_COPY_FAST");  // (an A/B switch, read per launch: 0 off, s staged)
+    const char* fv = std::getenv("FEC_VR_COPY_FAST");  // (an A/B switch, read per launch)
     const bool fast_on = !(fv && fv[0] == '0');
-    VrCopyArgs b = a;
-    if (fv && fv[0] == 's') b.direct = 0;
     const size_t ofast = std::max(static_cast<size_t>(kVrFastTP) * a.L, otile);
     if (fast_on && a.tdesc && (a.L & 3) == 0 && ofast <= 32768) {  // the specialised tiles (the generic ones inside)
         const int64_t g2 = (a.P + kVrFastTP - 1) / kVrFastTP;
         const size_t lds = kVrFastStage + ofast;
         hipLaunchKernelGGL(fec_vr_copy_fast_kernel, dim3(static_cast<unsigned>(g2)), dim3(256), lds,
-                           static_cast<hipStream_t>(s), b);
+                           static_cast<hipStream_t>(s), a);
         return hipGetLastError() == hipSuccess ? FEC_OK : FEC_ERR_HIP;
     }
     if ((a.L & 3) == 0 && otile <= 32768)
