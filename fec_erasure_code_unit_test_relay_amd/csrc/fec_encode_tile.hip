@@ -189,7 +189,7 @@ __device__ __forceinline__ uint32_t ttail_rem(const uint32_t (&X)[n]) {
 template <int K, int NP, int W, int LC, bool SEG>
 __device__ __forceinline__ void tile_walk(const EncTileArgs& a, uint8_t* smem) {
     constexpr int n = K + NP;
-    constexpr TileGeom CG = tile_geometry(K, NP, LC > 0 ? LC : 300);
+    constexpr TileGeom CG = tile_geometry(K, NP, LC > 0 ? LC : 300, SEG);
     constexpr bool CL = LC > 0;
     static_assert(!CL || CG.ok, "no tile geometry for this (k, n-k, L)");
     constexpr int NPA = NP > 0 ? NP : 1;
@@ -477,11 +477,23 @@ __device__ __forceinline__ void tile_walk(const EncTileArgs& a, uint8_t* smem) {
                 }
             }
             const int t = row0 + p;
+            uint32_t X[n];
+            tgroup_words<K, NP>(H, Qv, X);
+            if constexpr (SEG) {
+                // rows at the compact layout's stride W (16-byte aligned, dword-aligned groups): the
+                // group's n words in place; the last group's lane also zeroes the row's pad dwords past
+                // its words (its words past the codeword's end are zero: zero pad, zero parity)
+                const int Wb = CL ? ((CG.CW + 15) & ~15) : static_cast<int>(a.W);
+                const int d0 = (p * Wb + 4 * n * g) >> 2;
+                const int cntw = !(it > 0 && active && t < P) ? 0 : (is_last ? min(n + 3, (Wb >> 2) - n * g) : n);
+                uint32_t* outw = reinterpret_cast<uint32_t*>(out) + d0;
+                uint32_t* zdst = scratch + tid;
+#pragma unroll
+                for (int qq = 0; qq < n + 3; ++qq) *(qq < cntw ? outw + qq : zdst) = qq < n ? X[qq] : 0u;
+            } else {
             // the batch's last codeword may end inside a dword: the packet after it (not emitted)
             // still writes its first dword, which carries that codeword's last bytes
             const bool emit = it > 0 && active && (t < P || (t == P && g == 0));
-            uint32_t X[n];
-            tgroup_words<K, NP>(H, Qv, X);
             uint32_t tw = X[n - 1];
             if (is_last) {
                 switch (rem) {
@@ -509,6 +521,7 @@ __device__ __forceinline__ void tile_walk(const EncTileArgs& a, uint8_t* smem) {
                     *(qq < cntw ? outw + qq : zdst) = __builtin_amdgcn_perm(X[qq], lo, shsel);
                 }
             }
+            }
         }
         wait_lds_barrier();  // B3: output tile complete
         if (it == 0) continue;
@@ -531,16 +544,8 @@ __device__ __forceinline__ void tile_walk(const EncTileArgs& a, uint8_t* smem) {
                 const int pq = qq / nch_seg, c = qq - pq * nch_seg;
                 const int t = row0 + pq;
                 const bool ok = qq < R * nch_seg && t < P;
-                const int lb = ok ? pq * CW + 16 * c : 0;
-                const uint32_t* lw = reinterpret_cast<const uint32_t*>(out + (lb & ~3));
-                const int sh = lb & 3;
-                uint32_t d5[5];
-#pragma unroll
-                for (int m = 0; m < 5; ++m) d5[m] = lw[m];
-                const int left = CW - 16 * c;  // valid bytes of this chunk
-                v4u vv;
-#pragma unroll
-                for (int m = 0; m < 4; ++m) vv[m] = __builtin_amdgcn_alignbyte(d5[m + 1], d5[m], sh) & keep_bytes(left - 4 * m);
+                // row pq of the output tile at stride W (phase C wrote its pad dwords as zero)
+                const v4u vv = *reinterpret_cast<const v4u*>(out + (ok ? pq * static_cast<int>(W64) + 16 * c : 0));
                 const int off = t * static_cast<int>(W64) + 16 * c;
                 const int off_old = (t - nsw) * static_cast<int>(W64) + 16 * c;
                 __builtin_amdgcn_raw_buffer_store_b128(vv, rcur, ok && t < nsw ? off : 0x7ffffff0, 0, 0);
@@ -548,7 +553,7 @@ __device__ __forceinline__ void tile_walk(const EncTileArgs& a, uint8_t* smem) {
                 vm_issued += 2;
             }
             const bool own = tid < R && row0 + tid < P;
-            const uint8_t* cwp = out + (own ? tid : 0) * CW;
+            const uint8_t* cwp = out + (own ? tid : 0) * static_cast<int>(W64);
             int sz = CW;
             if (__builtin_amdgcn_ballot_w64(own && cwp[CW - 1] == 0)) {  // rare: a codeword ending in zero bytes
                 if (own && cwp[CW - 1] == 0) {
@@ -687,7 +692,7 @@ const void* fec_encode_tile_kernel_for(int k, int np, int L) {
 
 template <int K, int NP>
 __device__ __forceinline__ void tile_multi_case(const EncMultiArgs& m, int ti, uint8_t* smem) {
-    constexpr TileGeom CG = tile_geometry(K, NP, 300);
+    constexpr TileGeom CG = tile_geometry(K, NP, 300, true);
     EncTileArgs a{};
     a.payload_base = m.payload;
     a.len_base = m.len;

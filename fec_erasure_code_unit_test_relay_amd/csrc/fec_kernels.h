@@ -87,7 +87,9 @@ struct TileGeom {
     int off_in, in_bytes, off_pw, off_q, off_out, off_len, off_scratch;
     int lds, lds_len;  // dynamic LDS without / with the length rows
 };
-constexpr TileGeom tile_geometry(int k, int np, int L) {
+// seg: the segment-mode layout, whose output tile holds rows at the compact layout's stride W
+// (CW rounded to 16: rows leave as aligned 16-byte LDS reads) instead of packed at CW.
+constexpr TileGeom tile_geometry(int k, int np, int L, bool seg = false) {
     TileGeom t{};
     const int n = k + np;
     t.S = (L + 2 + k - 1) / k;
@@ -113,7 +115,7 @@ constexpr TileGeom tile_geometry(int k, int np, int L) {
     // after it) share one region
     t.off_pw = off;
     t.off_out = off;
-    const int pwb = 4 * t.R * t.NS4 * pws, outb = t.R * t.CW;
+    const int pwb = 4 * t.R * t.NS4 * pws, outb = t.R * (seg ? (t.CW + 15) & ~15 : t.CW);
     off = (off + (pwb > outb ? pwb : outb) + 15) & ~15;
     t.off_q = off;
     off = (off + 4 * npa * rows * t.NS4 + 15) & ~15;

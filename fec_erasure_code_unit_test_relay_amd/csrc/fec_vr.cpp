@@ -1234,6 +1234,7 @@ struct fec_vr_plan {
     const int32_t* d_hdr = nullptr;    // [sent][4]: frame header T, B, N, counter
     int64_t enc_total = 0;             // codewords of all encoder instances
     int enc_tab = 0, enc_out = 0, enc_slot = 0, enc_wave = 0;  // fec_vr_encode_kernel's LDS layout
+    int enc_nmax = 1;
     // the same instances without the ones the tile encoder takes (tuples with a tile geometry)
     const int32_t* d_lo_inst = nullptr;
     const int64_t* d_lo_span = nullptr;
@@ -1323,7 +1324,7 @@ int prepare_encode(fec_vr_plan* v, hipStream_t s) {
             it = toff.emplace(key, static_cast<int>(gtab.size())).first;
             gtab.insert(gtab.end(), t.begin(), t.end());
             int ti = -1;
-            const fec::TileGeom tg = fec::tile_geometry(g.k, g.n - g.k, p.L);
+            const fec::TileGeom tg = fec::tile_geometry(g.k, g.n - g.k, p.L, true);
             const void* kfn = fec::fec_encode_tile_seg_kernel_for(g.k, g.n - g.k, p.L);
             if (tiles_on && tg.ok && kfn && (p.L & 3) == 0) {
                 ti = static_cast<int>(v->tiles.size());
@@ -1409,6 +1410,7 @@ int prepare_encode(fec_vr_plan* v, hipStream_t s) {
     v->enc_out = out;
     v->enc_slot = slot;
     v->enc_wave = tab + out + nmax * slot;
+    v->enc_nmax = nmax;
     v->enc_ready = true;
     return FEC_OK;
 }
@@ -1758,8 +1760,12 @@ int fec_vr_encode_batch(fec_vr_plan* v, const uint8_t* d_payload, const int32_t*
                             tiled ? v->d_lo_cum : v->d_enc_cum,
                             tiled ? v->n_lo : static_cast<int>(v->plan.enc.size()), tiled ? v->lo_total : v->enc_total,
                             v->enc_tab, v->enc_out, v->enc_slot, v->enc_wave, v->d_gtab,
-                            tiled ? v->d_lo_base : v->d_enc_base, d_cw_cur, d_cw_old, d_len_cur, d_len_old};
-        if (int st = fec::vr_launch_encode(a, sg)) return st;
+                            tiled ? v->d_lo_base : v->d_enc_base, d_cw_cur, d_cw_old, d_len_cur, d_len_old,
+                            v->enc_nmax};
+        // the tile encoder's leftovers in closed form (FEC_VR_LO_CF=0: the ring walk)
+        const char* cf = std::getenv("FEC_VR_LO_CF");
+        const bool use_cf = tiled && !(cf && cf[0] == '0');
+        if (int st = use_cf ? fec::vr_launch_encode_cf(a, sg) : fec::vr_launch_encode(a, sg)) return st;
     }
     if (n_multi > 0)
         if (int st = launch_tile_multi(v, d_payload, d_payload_len, d_cw_cur, d_len_cur, d_cw_old, d_len_old, s)) return st;

@@ -230,6 +230,7 @@ struct VrEncodeArgs {
     uint8_t* old;
     int32_t* len_cur;
     int32_t* len_old;
+    int n_max;                //   widest n over the instances (fec_vr_encode_cf_kernel's LDS rows)
 };
 struct VrCopyArgs {     // received packets: systematic bytes of cur[x] in its decoder's geometry
     const uint8_t* cur;
@@ -307,6 +308,9 @@ int vr_launch_offsets(const VrOffsetsArgs& a, void* s);
 int vr_launch_frames(const VrFrameArgs& a, void* s);
 int vr_launch_parse(const VrParseArgs& a, void* s);
 int vr_launch_encode(const VrEncodeArgs& a, void* s);
+// The same in closed form, a workgroup per codeword (no LDS ring; the instance list's few codewords
+// beside the tile encoder)
+int vr_launch_encode_cf(const VrEncodeArgs& a, void* s);
 int vr_launch_copy(const VrCopyArgs& a, void* s);
 int vr_launch_recover(const VrRecArgs& a, void* s);
 
