@@ -133,8 +133,16 @@ def lib() -> ctypes.CDLL:
     L.fec_sdswdf_destination_batch.argtypes = [vp, vp, vp, i64, vp, vp, vp]
     L.fec_sdswdf_relay_plan.argtypes = [vp, vp, i64, vp, vp, i64, i64p, ip]
     L.fec_sdswdf_dest_plan.argtypes = [vp, vp, vp, i64, vp, vp, vp, i64, i64p, ip]
+    L.fec_sdswdf_relay_batch_starts.argtypes = [vp, vp, i64, vp, i64, vp, i32, vp, vp]
+    L.fec_sdswdf_destination_batch_starts.argtypes = [vp, vp, vp, i64, vp, i32, vp, vp, vp]
+    L.fec_relay_vr_create.argtypes = [i32, i32, vp, i32, i64, ctypes.POINTER(vp)]
+    L.fec_relay_vr_destroy.argtypes = [vp]
+    L.fec_relay_vr_geometry.argtypes = [vp, ip, ip, ip]
+    L.fec_relay_vr_run.argtypes = [vp, vp, vp, vp, vp, vp, vp, vp, vp]
     for name in ["fec_sdswdf_create", "fec_sdswdf_destroy", "fec_sdswdf_geometry", "fec_sdswdf_relay_batch",
                  "fec_sdswdf_destination_batch", "fec_sdswdf_relay_plan", "fec_sdswdf_dest_plan",
+                 "fec_sdswdf_relay_batch_starts", "fec_sdswdf_destination_batch_starts", "fec_relay_vr_create",
+                 "fec_relay_vr_destroy", "fec_relay_vr_geometry", "fec_relay_vr_run",
                  "fec_swdf_create", "fec_swdf_destroy", "fec_swdf_geometry", "fec_swdf_relay_batch",
                  "fec_swdf_destination_batch", "fec_codec_create", "fec_codec_destroy", "fec_codec_set_encode_path",
                  "fec_codec_set_copy_path", "fec_codec_set_plan_path", "fec_codec_info", "fec_codec_set_episode_dedup", "fec_debug_stamps", "fec_codec_geometry",

@@ -1,0 +1,391 @@
+// fec_relay_vr.hip -- the relay chain under variable rate, batched: RELAYING_TYPE 2 / 3 through
+// a schedule of code switches (fec_amd.h, fec_relay_vr_*).
+//
+// What the reference does (Variable_Rate_FEC_Decoder.cpp:600-740 at the relay, :1423-1600 and
+// :1772-1873 at the destination): at a switch to a new code (T, N) at seq s the relay and the
+// destination each create a fresh Decoder_Symbol_Wise for it; for the T_TOT + 1 double-coded seqs
+// s .. s + T_TOT the old object takes the old codeword and the new one the new codeword, the relay
+// sends [BE16 size_cur][new code's part][old code's part], the destination's old object reports
+// and the new one only decodes; at s + T_TOT + 1 both nodes copy the new object into the main one
+// (copy_elements, Decoder_Symbol_Wise.cpp:88-117) and go on with it.
+//
+// So every code instance i -- a fresh object at its start seq a_i that runs through b_i = the end
+// of the next switch's double coding -- is one fixed-rate relay chain over seqs [a_i, b_i] with its
+// own source encoder (also fresh at a_i, Variable_Rate_FEC_Encoder.cpp:74-235).  The batch lays
+// the instances of one code end to end in one stream of rows, each behind kGap rows of zero
+// codewords on received flags: a window reaching in front of an instance then sees exactly what a
+// fresh object holds (zero rows, received flags), so one fixed-rate batch per code (fec_swdf /
+// fec_sdswdf, the state-dependent planners reset at each instance's first row) runs all its
+// instances at once.  The gap rows' codewords and frames are zeroed between the stages; the relay
+// frames and the destination's reported rows are then gathered back into seq order, with the
+// double-coding layout.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstring>
+#include <map>
+#include <memory>
+#include <new>
+#include <vector>
+
+#include "fec_amd.h"
+
+namespace fec {
+namespace {
+
+constexpr int kTT = 10;         // T_TOT (FEC_Macro.h)
+constexpr int kGap = 3 * kTT + 3;  // zero rows in front of an instance (>= every window's reach)
+constexpr int kMaxCodes = 16;
+
+struct RvTupleDev {             // one code's batch buffers, for the gather kernel
+    const uint8_t* frames;      // rows of F bytes
+    const uint8_t* out;         // rows of ostride bytes
+    int F, part, hdr;           // frame row bytes, part bytes (from byte 2), of which header bytes (11 / 0)
+    int ostride, outb;          // out row bytes, bytes reported
+};
+struct RvGatherArgs {
+    RvTupleDev tup[kMaxCodes];
+    const int32_t* map;         // [P][6]: new (code, row), old (code, row) or -1, reporting (code, row)
+    int64_t P;
+    uint8_t* frames;            // [P][fstride]
+    int64_t fstride;
+    int32_t* frame_len;
+    uint8_t* out;               // [P][out_stride]
+    int64_t out_stride;
+};
+
+// A wave per seq: the frame [BE16 size of the new part's code bytes][new part][old part] and the
+// reporting destination's row (its blocks*k bytes, zero after).
+__global__ __launch_bounds__(256) void fec_relay_vr_gather_kernel(RvGatherArgs a) {
+    const int lane = threadIdx.x & 63;
+    for (int64_t t = static_cast<int64_t>(blockIdx.x) * 4 + (threadIdx.x >> 6); t < a.P;
+         t += static_cast<int64_t>(gridDim.x) * 4) {
+        const int32_t* m = a.map + 6 * t;
+        const RvTupleDev& tn = a.tup[m[0]];
+        uint8_t* fr = a.frames + t * a.fstride;
+        const uint8_t* pn = tn.frames + static_cast<int64_t>(m[1]) * tn.F + 2;
+        const int size_cur = tn.part - tn.hdr;  // the new code's codeword_r_d_size (:997-999, :1502-1571)
+        if (lane == 0) {
+            fr[0] = static_cast<uint8_t>(size_cur / 256);
+            fr[1] = static_cast<uint8_t>(size_cur % 256);
+        }
+        for (int b = lane; b < tn.part; b += 64) fr[2 + b] = pn[b];
+        int len = 2 + tn.part;
+        if (m[2] >= 0) {
+            const RvTupleDev& to = a.tup[m[2]];
+            const uint8_t* po = to.frames + static_cast<int64_t>(m[3]) * to.F + 2;
+            for (int b = lane; b < to.part; b += 64) fr[len + b] = po[b];
+            len += to.part;
+        }
+        if (lane == 0) a.frame_len[t] = len;
+        const RvTupleDev& tr = a.tup[m[4]];
+        const uint8_t* src = tr.out + static_cast<int64_t>(m[5]) * tr.ostride;
+        uint8_t* dst = a.out + t * a.out_stride;
+        for (int b = lane; b < a.out_stride; b += 64) dst[b] = b < tr.outb ? src[b] : 0;
+    }
+}
+
+// Payload rows into an instance-ordered stream (src[r] < 0: a gap row, zero with length 0).
+__global__ __launch_bounds__(256) void fec_relay_vr_payload_kernel(const uint8_t* payload, int L, const int64_t* src,
+                                                                   int64_t R, uint8_t* dst, int32_t* len) {
+    for (int64_t r = static_cast<int64_t>(blockIdx.x) * 4 + (threadIdx.x >> 6); r < R;
+         r += static_cast<int64_t>(gridDim.x) * 4) {
+        const int lane = threadIdx.x & 63;
+        const int64_t s = src[r];
+        for (int b = lane; b < L; b += 64) dst[r * L + b] = s < 0 ? 0 : payload[s * L + b];
+        if (lane == 0) len[r] = s < 0 ? 0 : L;
+    }
+}
+
+// Zero the gap rows (src[r] < 0) of rows of W bytes.
+__global__ __launch_bounds__(256) void fec_relay_vr_zero_kernel(const int64_t* src, int64_t R, uint8_t* rows, int W) {
+    for (int64_t r = static_cast<int64_t>(blockIdx.x) * 4 + (threadIdx.x >> 6); r < R;
+         r += static_cast<int64_t>(gridDim.x) * 4) {
+        if (src[r] >= 0) continue;
+        for (int b = threadIdx.x & 63; b < W; b += 64) rows[r * W + b] = 0;
+    }
+}
+
+unsigned grid_rows(int64_t R) { return static_cast<unsigned>(std::max<int64_t>(1, std::min<int64_t>((R + 3) / 4, 65536))); }
+
+struct DevBuf {
+    void* p = nullptr;
+    size_t cap = 0;
+    ~DevBuf() {
+        if (p) (void)hipFree(p);
+    }
+    int reserve(size_t n) {
+        if (n <= cap) return FEC_OK;
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        cap = 0;
+        if (hipMalloc(&p, std::max<size_t>(n, 16)) != hipSuccess) return FEC_ERR_NOMEM;
+        cap = n;
+        return FEC_OK;
+    }
+    template <class T>
+    T* as() const { return static_cast<T*>(p); }
+};
+
+struct Code {
+    int T = 0, N = 0, k = 0, n = 0, S = 0, CW = 0, rd = 0, part = 0, F = 0, ostride = 0, outb = 0;
+    std::vector<int64_t> src;     // per row: source seq, or -1 (gap)
+    std::vector<int64_t> starts;  // each instance's first row
+    int64_t R = 0;
+    fec_codec* codec = nullptr;
+    fec_swdf* sw = nullptr;
+    fec_sdswdf* sd = nullptr;
+    DevBuf d_src, d_pay, d_len, d_cw, d_cwlen, d_er1, d_er2, d_frames, d_out, d_flag, d_work;
+    std::vector<uint8_t> h_er1, h_er2, h_flag;
+    Code() = default;
+    Code(const Code&) = delete;
+    Code& operator=(const Code&) = delete;
+    ~Code() {
+        if (codec) fec_codec_destroy(codec);
+        if (sw) fec_swdf_destroy(sw);
+        if (sd) fec_sdswdf_destroy(sd);
+    }
+};
+
+}  // namespace
+}  // namespace fec
+
+struct fec_relay_vr {
+    int type = 2, L = 0;
+    int64_t P = 0;
+    std::vector<std::unique_ptr<fec::Code>> codes;
+    std::vector<int32_t> map;   // [P][6]
+    int fstride = 0, ostride = 0;
+    fec::DevBuf d_map;
+    bool map_up = false;
+};
+
+extern "C" {
+
+int fec_relay_vr_create(int type, int max_payload, const int32_t* sched, int nsw, int64_t P, fec_relay_vr** out) {
+    if (!out) return FEC_ERR_ARG;
+    *out = nullptr;
+    if ((type != 2 && type != 3) || max_payload < 1 || max_payload > 65535 || !sched || nsw < 1 || P < 1 ||
+        sched[0] != 0)
+        return FEC_ERR_ARG;
+    for (int i = 0; i < nsw; ++i) {
+        const int s = sched[3 * i], T = sched[3 * i + 1], N = sched[3 * i + 2];
+        if (T < 1 || T > fec::kTT || N < 0 || N > T || s < 0 || s >= P) return FEC_ERR_ARG;
+        if (i > 0 && s < sched[3 * (i - 1)] + fec::kTT + 1) return FEC_ERR_ARG;  // one transition at a time
+    }
+    try {
+        std::unique_ptr<fec_relay_vr> r(new fec_relay_vr());
+        r->type = type;
+        r->L = max_payload;
+        r->P = P;
+        std::map<int, int> code_of;  // T * 64 + N -> code index
+        struct Inst {
+            int64_t a, b, row0;
+            int c;
+        };
+        std::vector<Inst> inst;
+        for (int i = 0; i < nsw; ++i) {
+            const int T = sched[3 * i + 1], N = sched[3 * i + 2];
+            const int key = T * 64 + N;
+            auto it = code_of.find(key);
+            if (it == code_of.end()) {
+                if (static_cast<int>(r->codes.size()) >= fec::kMaxCodes) return FEC_ERR_ARG;
+                std::unique_ptr<fec::Code> c(new fec::Code());
+                c->T = T;
+                c->N = N;
+                int st;
+                if (type == 2) {
+                    st = fec_swdf_create(max_payload, T, N, T, N, &c->sw);
+                    int F = 0;
+                    if (!st) st = fec_swdf_geometry(c->sw, &c->k, &c->n, nullptr, &c->S, &F, nullptr);
+                    c->F = F;
+                    c->part = F - 2;
+                } else {
+                    st = fec_sdswdf_create(max_payload, T, N, T, N, 0, &c->sd);
+                    int F = 0;
+                    if (!st) st = fec_sdswdf_geometry(c->sd, &c->k, &c->n, nullptr, &c->S, nullptr, &F, nullptr);
+                    c->F = F;
+                    c->part = F - 2;
+                }
+                if (st) return st;
+                if ((st = fec_codec_create(max_payload, T, N, N, &c->codec))) return st;
+                c->CW = c->S * c->n;
+                c->ostride = c->S * c->k;
+                c->outb = (max_payload / c->k + 1) * c->k;  // extract_data's blocks * k (:653-661)
+                it = code_of.emplace(key, static_cast<int>(r->codes.size())).first;
+                r->codes.push_back(std::move(c));
+            }
+            const int64_t a = sched[3 * i];
+            const int64_t b = i + 1 < nsw ? std::min<int64_t>(sched[3 * (i + 1)] + fec::kTT, P - 1) : P - 1;
+            inst.push_back({a, b, 0, it->second});
+        }
+        for (auto& in : inst) {  // rows: per code, its instances in seq order, each behind kGap zero rows
+            fec::Code& c = *r->codes[static_cast<size_t>(in.c)];
+            for (int g = 0; g < fec::kGap; ++g) c.src.push_back(-1);
+            in.row0 = static_cast<int64_t>(c.src.size());
+            c.starts.push_back(in.row0);
+            for (int64_t t = in.a; t <= in.b; ++t) c.src.push_back(t);
+        }
+        int part_max = 0, ostride = max_payload + 32;
+        for (auto& c : r->codes) {
+            c->R = static_cast<int64_t>(c->src.size());
+            part_max = std::max(part_max, c->part);
+            ostride = std::max(ostride, c->outb);
+        }
+        r->fstride = (2 + 2 * part_max + 15) & ~15;
+        r->ostride = ostride;
+        // per seq: the newest instance, the old one during double coding, the reporting one
+        r->map.assign(static_cast<size_t>(P) * 6, -1);
+        for (size_t i = 0; i < inst.size(); ++i) {
+            const Inst& in = inst[i];
+            const bool has_next = i + 1 < inst.size();
+            const int64_t next = has_next ? inst[i + 1].a : P;
+            for (int64_t t = in.a; t <= in.b; ++t) {
+                int32_t* m = &r->map[static_cast<size_t>(t) * 6];
+                const int32_t row = static_cast<int32_t>(in.row0 + (t - in.a));
+                const bool dc_new = i > 0 && t <= in.a + fec::kTT;  // the new object of a transition
+                if (t < next) {  // newest instance at t
+                    m[0] = in.c;
+                    m[1] = row;
+                } else {  // the old object of the next switch's double coding
+                    m[2] = in.c;
+                    m[3] = row;
+                }
+                // reporting: the old object during the next switch's transition, else this one unless
+                // it is the new object of its own transition
+                if (t >= next || !dc_new) {
+                    m[4] = in.c;
+                    m[5] = row;
+                }
+            }
+        }
+        *out = r.release();
+        return FEC_OK;
+    } catch (const std::bad_alloc&) {
+        return FEC_ERR_NOMEM;
+    } catch (...) {
+        return FEC_ERR_ARG;
+    }
+}
+
+int fec_relay_vr_destroy(fec_relay_vr* r) {
+    if (r) (void)hipDeviceSynchronize();
+    delete r;
+    return FEC_OK;
+}
+
+int fec_relay_vr_geometry(const fec_relay_vr* r, int* frame_stride, int* out_stride, int* codes) {
+    if (!r) return FEC_ERR_ARG;
+    if (frame_stride) *frame_stride = r->fstride;
+    if (out_stride) *out_stride = r->ostride;
+    if (codes) *codes = static_cast<int>(r->codes.size());
+    return FEC_OK;
+}
+
+int fec_relay_vr_run(fec_relay_vr* r, const uint8_t* d_payload, const uint8_t* h_e1, const uint8_t* h_e2,
+                     uint8_t* d_frames, int32_t* d_frame_len, uint8_t* d_out, uint8_t* h_flag, void* hip_stream) {
+    if (!r || !d_payload || !h_e1 || !h_e2 || !d_frames || !d_frame_len || !d_out) return FEC_ERR_ARG;
+    hipStream_t s = static_cast<hipStream_t>(hip_stream);
+    try {
+        const int L = r->L;
+        for (auto& cp : r->codes) {
+            fec::Code& c = *cp;
+            const int64_t R = c.R;
+            c.h_er1.resize(static_cast<size_t>(R));
+            c.h_er2.resize(static_cast<size_t>(R));
+            for (int64_t q = 0; q < R; ++q) {
+                const int64_t t = c.src[static_cast<size_t>(q)];
+                c.h_er1[static_cast<size_t>(q)] = t < 0 ? 0 : (h_e1[t] ? 1 : 0);
+                c.h_er2[static_cast<size_t>(q)] = t < 0 ? 0 : (h_e2[t] ? 1 : 0);
+            }
+            if (int st = c.d_src.reserve(static_cast<size_t>(R) * 8)) return st;
+            if (int st = c.d_pay.reserve(static_cast<size_t>(R) * L)) return st;
+            if (int st = c.d_len.reserve(static_cast<size_t>(R) * 4)) return st;
+            if (int st = c.d_cw.reserve(static_cast<size_t>(R) * c.CW)) return st;
+            if (int st = c.d_cwlen.reserve(static_cast<size_t>(R) * 4)) return st;
+            if (int st = c.d_frames.reserve(static_cast<size_t>(R) * c.F)) return st;
+            if (int st = c.d_out.reserve(static_cast<size_t>(R) * c.ostride)) return st;
+            if (hipMemcpyAsync(c.d_src.p, c.src.data(), static_cast<size_t>(R) * 8, hipMemcpyHostToDevice, s) != hipSuccess)
+                return FEC_ERR_HIP;
+            hipLaunchKernelGGL(fec::fec_relay_vr_payload_kernel, dim3(fec::grid_rows(R)), dim3(256), 0, s, d_payload, L,
+                               c.d_src.as<const int64_t>(), R, c.d_pay.as<uint8_t>(), c.d_len.as<int32_t>());
+            if (hipGetLastError() != hipSuccess) return FEC_ERR_HIP;
+            // each instance a fresh source encoder: its rows behind kGap zero-length packets (>= n-1)
+            if (int st = fec_encode_batch(c.codec, c.d_pay.as<uint8_t>(), c.d_len.as<int32_t>(), 0, R, c.d_cw.as<uint8_t>(),
+                                          c.d_cwlen.as<int32_t>(), s))
+                return st;
+            hipLaunchKernelGGL(fec::fec_relay_vr_zero_kernel, dim3(fec::grid_rows(R)), dim3(256), 0, s,
+                               c.d_src.as<const int64_t>(), R, c.d_cw.as<uint8_t>(), c.CW);
+            if (hipGetLastError() != hipSuccess) return FEC_ERR_HIP;
+            if (r->type == 2) {
+                if (int st = c.d_er1.reserve(static_cast<size_t>(R))) return st;
+                if (int st = c.d_er2.reserve(static_cast<size_t>(R))) return st;
+                if (int st = c.d_flag.reserve(static_cast<size_t>(R))) return st;
+                const size_t wb = fec_swdf_workspace_bytes(c.sw, R);
+                if (int st = c.d_work.reserve(wb)) return st;
+                if (hipMemcpyAsync(c.d_er1.p, c.h_er1.data(), static_cast<size_t>(R), hipMemcpyHostToDevice, s) != hipSuccess ||
+                    hipMemcpyAsync(c.d_er2.p, c.h_er2.data(), static_cast<size_t>(R), hipMemcpyHostToDevice, s) != hipSuccess)
+                    return FEC_ERR_HIP;
+                if (int st = fec_swdf_relay_batch(c.sw, c.d_cw.as<uint8_t>(), c.CW, c.d_er1.as<uint8_t>(), R,
+                                                  c.d_frames.as<uint8_t>(), nullptr, c.d_work.p, wb, s))
+                    return st;
+                hipLaunchKernelGGL(fec::fec_relay_vr_zero_kernel, dim3(fec::grid_rows(R)), dim3(256), 0, s,
+                                   c.d_src.as<const int64_t>(), R, c.d_frames.as<uint8_t>(), c.F);
+                if (hipGetLastError() != hipSuccess) return FEC_ERR_HIP;
+                if (int st = fec_swdf_destination_batch(c.sw, c.d_frames.as<uint8_t>(), c.d_er2.as<uint8_t>(), R,
+                                                        c.d_out.as<uint8_t>(), c.d_flag.as<uint8_t>(), s))
+                    return st;
+                c.h_flag.resize(static_cast<size_t>(R));
+                if (hipMemcpyAsync(c.h_flag.data(), c.d_flag.p, static_cast<size_t>(R), hipMemcpyDeviceToHost, s) != hipSuccess)
+                    return FEC_ERR_HIP;
+            } else {
+                const int ns = static_cast<int>(c.starts.size());
+                if (int st = fec_sdswdf_relay_batch_starts(c.sd, c.d_cw.as<uint8_t>(), c.CW, c.h_er1.data(), R,
+                                                           c.starts.data(), ns, c.d_frames.as<uint8_t>(), s))
+                    return st;
+                hipLaunchKernelGGL(fec::fec_relay_vr_zero_kernel, dim3(fec::grid_rows(R)), dim3(256), 0, s,
+                                   c.d_src.as<const int64_t>(), R, c.d_frames.as<uint8_t>(), c.F);
+                if (hipGetLastError() != hipSuccess) return FEC_ERR_HIP;
+                c.h_flag.resize(static_cast<size_t>(R));
+                if (int st = fec_sdswdf_destination_batch_starts(c.sd, c.d_frames.as<uint8_t>(), c.h_er2.data(), R,
+                                                                 c.starts.data(), ns, c.d_out.as<uint8_t>(),
+                                                                 c.h_flag.data(), s))
+                    return st;
+            }
+        }
+        if (!r->map_up) {
+            if (int st = r->d_map.reserve(r->map.size() * 4)) return st;
+            if (hipMemcpyAsync(r->d_map.p, r->map.data(), r->map.size() * 4, hipMemcpyHostToDevice, s) != hipSuccess)
+                return FEC_ERR_HIP;
+            r->map_up = true;
+        }
+        fec::RvGatherArgs a{};
+        for (size_t i = 0; i < r->codes.size(); ++i) {
+            const fec::Code& c = *r->codes[i];
+            a.tup[i] = {c.d_frames.as<const uint8_t>(), c.d_out.as<const uint8_t>(), c.F, c.part,
+                        r->type == 3 ? 11 : 0, c.ostride, c.outb};
+        }
+        a.map = r->d_map.as<const int32_t>();
+        a.P = r->P;
+        a.frames = d_frames;
+        a.fstride = r->fstride;
+        a.frame_len = d_frame_len;
+        a.out = d_out;
+        a.out_stride = r->ostride;
+        hipLaunchKernelGGL(fec::fec_relay_vr_gather_kernel, dim3(fec::grid_rows(r->P)), dim3(256), 0, s, a);
+        if (hipGetLastError() != hipSuccess) return FEC_ERR_HIP;
+        if (hipStreamSynchronize(s) != hipSuccess) return FEC_ERR_HIP;
+        if (h_flag)
+            for (int64_t t = 0; t < r->P; ++t) {
+                const int32_t* m = &r->map[static_cast<size_t>(t) * 6];
+                h_flag[t] = r->codes[static_cast<size_t>(m[4])]->h_flag[static_cast<size_t>(m[5])];
+            }
+        return FEC_OK;
+    } catch (const std::bad_alloc&) {
+        return FEC_ERR_NOMEM;
+    } catch (...) {
+        return FEC_ERR_ARG;
+    }
+}
+
+}  // extern "C"

@@ -815,18 +815,30 @@ int ensure_device(fec_sdswdf* w) {
 }
 
 // The relay's host plan for seqs 0..P-1 of a fresh relay: record ids in w->plan, records in
-// w->relay->records().
-void plan_relay(fec_sdswdf* w, const uint8_t* h_erasure, int64_t P) {
+// w->relay->records().  starts (sorted, may be null): rows at which a fresh relay takes over (the
+// rows of several independent streams laid end to end, fec_relay_vr).
+void plan_relay(fec_sdswdf* w, const uint8_t* h_erasure, int64_t P, const int64_t* starts = nullptr, int nstarts = 0) {
     w->relay->reset();
     w->plan.resize(static_cast<size_t>(P));
-    for (int64_t t = 0; t < P; ++t) w->plan[static_cast<size_t>(t)] = w->relay->step(h_erasure[t] != 0);
+    int si = 0;
+    for (int64_t t = 0; t < P; ++t) {
+        while (si < nstarts && starts[si] <= t) {
+            if (starts[si++] == t) w->relay->reset();
+        }
+        w->plan[static_cast<size_t>(t)] = w->relay->step(h_erasure[t] != 0);
+    }
 }
 
 // The destination's host plan for seqs 0..P-1 given the frames' header bytes (11 per seq).
-void plan_dest(fec_sdswdf* w, const uint8_t* h_erasure, const uint8_t* hdrs, int64_t P, uint8_t* h_flag) {
+void plan_dest(fec_sdswdf* w, const uint8_t* h_erasure, const uint8_t* hdrs, int64_t P, uint8_t* h_flag,
+               const int64_t* starts = nullptr, int nstarts = 0) {
     w->dest->reset();
     w->plan.resize(static_cast<size_t>(P));
+    int si = 0;
     for (int64_t t = 0; t < P; ++t) {
+        while (si < nstarts && starts[si] <= t) {
+            if (starts[si++] == t) w->dest->reset();
+        }
         bool fl = false;
         w->plan[static_cast<size_t>(t)] = w->dest->step(h_erasure[t] != 0, hdrs + t * fec::kHdr, &fl);
         if (h_flag) h_flag[t] = fl ? 1 : 0;
@@ -1263,13 +1275,20 @@ int fec_sdswdf_dest_plan(fec_sdswdf* w, const uint8_t* h_erasure, const uint8_t*
 
 int fec_sdswdf_relay_batch(fec_sdswdf* w, const uint8_t* d_cw, int64_t cw_stride, const uint8_t* h_erasure,
                            int64_t P, uint8_t* d_frames, void* stream) {
-    if (!w || P < 0) return FEC_ERR_ARG;
+    return fec_sdswdf_relay_batch_starts(w, d_cw, cw_stride, h_erasure, P, nullptr, 0, d_frames, stream);
+}
+
+int fec_sdswdf_relay_batch_starts(fec_sdswdf* w, const uint8_t* d_cw, int64_t cw_stride, const uint8_t* h_erasure,
+                                  int64_t P, const int64_t* h_starts, int nstarts, uint8_t* d_frames, void* stream) {
+    if (!w || P < 0 || nstarts < 0 || (nstarts > 0 && !h_starts)) return FEC_ERR_ARG;
     if (P == 0) return FEC_OK;
     if (!d_cw || !h_erasure || !d_frames || cw_stride < static_cast<int64_t>(w->g1.S) * w->g1.n) return FEC_ERR_ARG;
+    for (int i = 1; i < nstarts; ++i)
+        if (h_starts[i] < h_starts[i - 1]) return FEC_ERR_ARG;
     hipStream_t s = static_cast<hipStream_t>(stream);
     return guarded_sd([&] {
         if (int st = ensure_device(w)) return st;
-        plan_relay(w, h_erasure, P);
+        plan_relay(w, h_erasure, P, h_starts, nstarts);
         if (int st = upload_plan(w, w->relay->records(), P, s)) return st;
         fec::SdRelayArgs a;
         a.cw = d_cw;
@@ -1295,9 +1314,17 @@ int fec_sdswdf_relay_batch(fec_sdswdf* w, const uint8_t* d_cw, int64_t cw_stride
 
 int fec_sdswdf_destination_batch(fec_sdswdf* w, const uint8_t* d_frames, const uint8_t* h_erasure, int64_t P,
                                  uint8_t* d_out, uint8_t* h_flag, void* stream) {
-    if (!w || P < 0) return FEC_ERR_ARG;
+    return fec_sdswdf_destination_batch_starts(w, d_frames, h_erasure, P, nullptr, 0, d_out, h_flag, stream);
+}
+
+int fec_sdswdf_destination_batch_starts(fec_sdswdf* w, const uint8_t* d_frames, const uint8_t* h_erasure, int64_t P,
+                                        const int64_t* h_starts, int nstarts, uint8_t* d_out, uint8_t* h_flag,
+                                        void* stream) {
+    if (!w || P < 0 || nstarts < 0 || (nstarts > 0 && !h_starts)) return FEC_ERR_ARG;
     if (P == 0) return FEC_OK;
     if (!d_frames || !h_erasure || !d_out) return FEC_ERR_ARG;
+    for (int i = 1; i < nstarts; ++i)
+        if (h_starts[i] < h_starts[i - 1]) return FEC_ERR_ARG;
     hipStream_t s = static_cast<hipStream_t>(stream);
     return guarded_sd([&] {
         if (int st = ensure_device(w)) return st;
@@ -1311,7 +1338,7 @@ int fec_sdswdf_destination_batch(fec_sdswdf* w, const uint8_t* d_frames, const u
             hipMemcpyAsync(w->hdrs.data(), w->d_hdrs.p, hb, hipMemcpyDeviceToHost, s) != hipSuccess ||
             hipStreamSynchronize(s) != hipSuccess)
             return static_cast<int>(FEC_ERR_HIP);
-        plan_dest(w, h_erasure, w->hdrs.data(), P, h_flag);
+        plan_dest(w, h_erasure, w->hdrs.data(), P, h_flag, h_starts, nstarts);
         if (int st = upload_plan(w, w->dest->records(), P, s)) return st;
         fec::SdDestArgs a;
         a.frames = d_frames;

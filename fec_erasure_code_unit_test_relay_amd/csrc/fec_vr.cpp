@@ -1257,6 +1257,8 @@ struct fec_vr_plan {
     int n_multi = 0;               // tiles[0, n_multi): one launch, workgroup b = segment b of d_seg
     int multi_lds = 0, multi_lds_len = 0;
     const int64_t* d_seg = nullptr;
+    const int64_t* d_np0 = nullptr;  // [n_np0][8]: segments of the instances of tuples with n = k
+    int n_np0 = 0;
     bool enc_ready = false, dec_ready = false, hdr_ready = false;
     Fork fork;  // side streams (declared after the uploads: destroyed, and drained, first)
 
@@ -1311,6 +1313,9 @@ int prepare_encode(fec_vr_plan* v, hipStream_t s) {
     if (const char* e = std::getenv("FEC_VR_TILE_UNIT")) unit = std::max(1, std::atoi(e));
     const bool tiles_on = !std::getenv("FEC_VR_NO_TILE");
     const bool multi_on = !std::getenv("FEC_VR_NO_MULTI");
+    const char* np0e = std::getenv("FEC_VR_NP0");
+    const bool np0_on = tiles_on && !(np0e && np0e[0] == '0');
+    std::vector<int64_t> np0;
     int tab = 32, out = 16, slot = 16, nmax = 1;
     for (size_t ei = 0; ei < p.enc.size(); ++ei) {
         const auto& e = p.enc[ei];
@@ -1343,7 +1348,15 @@ int prepare_encode(fec_vr_plan* v, hipStream_t s) {
         cum.push_back(cum.back() + (e.end - e.first));
         int ti = tix[key];
         if (ti >= 0 && (e.end - e.first) * cwp >= 0x7fff0000) ti = -1;  // 32-bit buffer offsets
-        if (ti >= 0) {
+        if (np0_on && g.n == g.k && (p.L & 3) == 0 && cwp <= 512) {
+            // no parity: fec_vr_encode_np0_kernel, segments of kVrNp0Rows rows
+            const int64_t rows = e.end - e.first;
+            for (int64_t t0 = 0; t0 < rows; t0 += fec::kVrNp0Rows) {
+                const int64_t c = std::min<int64_t>(fec::kVrNp0Rows, rows - t0);
+                np0.insert(np0.end(), {e.first, e.role_switch, rows, t0 | (c << 32), b_cur, b_old,
+                                       static_cast<int64_t>(g.CW) | (cwp << 32), 0});
+            }
+        } else if (ti >= 0) {
             const int64_t rows = e.end - e.first, R = v->tiles[static_cast<size_t>(ti)].tg.R;
             const int64_t nt = (rows + R - 1) / R;
             for (int64_t t0 = 0; t0 < nt; t0 += unit) {
@@ -1402,8 +1415,10 @@ int prepare_encode(fec_vr_plan* v, hipStream_t s) {
     u.add(&v->d_enc_base, base);
     u.add(&v->d_lo_base, lo_base);
     u.add(&v->d_seg, seg);
+    u.add(&v->d_np0, np0);
     if (int st = u.commit(s)) return st;
     v->enc_total = cum.back();
+    v->n_np0 = static_cast<int>(np0.size() / 8);
     v->n_lo = static_cast<int>(lo_span.size() / 2);
     v->lo_total = lo_cum.back();
     v->enc_tab = tab;
@@ -1766,6 +1781,12 @@ int fec_vr_encode_batch(fec_vr_plan* v, const uint8_t* d_payload, const int32_t*
         const char* cf = std::getenv("FEC_VR_LO_CF");
         const bool use_cf = tiled && !(cf && cf[0] == '0');
         if (int st = use_cf ? fec::vr_launch_encode_cf(a, sg) : fec::vr_launch_encode(a, sg)) return st;
+    }
+    if (tiled && v->n_np0 > 0) {
+        hipStream_t s0;
+        if (int st = v->fork.stream(next_side++, &s0)) return st;
+        fec::VrNp0Args a0{d_payload, d_payload_len, v->plan.L, v->d_np0, v->n_np0, d_cw_cur, d_cw_old, d_len_cur, d_len_old};
+        if (int st = fec::vr_launch_encode_np0(a0, s0)) return st;
     }
     if (n_multi > 0)
         if (int st = launch_tile_multi(v, d_payload, d_payload_len, d_cw_cur, d_len_cur, d_cw_old, d_len_old, s)) return st;

@@ -232,6 +232,23 @@ struct VrEncodeArgs {
     int32_t* len_old;
     int n_max;                //   widest n over the instances (fec_vr_encode_cf_kernel's LDS rows)
 };
+// Encoder instances of tuples with n = k (no parity: the codeword is X itself, [len BE16, payload,
+// zero pad] to S*k bytes): a workgroup per segment of at most kVrNp0Rows rows of one instance.
+constexpr int kVrNp0Rows = 32;
+struct VrNp0Args {
+    const uint8_t* payload;   // [sent][L]
+    const int32_t* len;       // may be null (all L)
+    int L;
+    const int64_t* seg;       // [nseg][8]: first seq, role switch, rows, t0 | cnt << 32, byte offsets of
+                              //   the first cur / old row, CW | W << 32 (W = CW rounded to 16, <= 512), 0
+    int nseg;
+    uint8_t* cur;
+    uint8_t* old;
+    int32_t* len_cur;
+    int32_t* len_old;
+};
+int vr_launch_encode_np0(const VrNp0Args& a, void* s);
+
 struct VrCopyArgs {     // received packets: systematic bytes of cur[x] in its decoder's geometry
     const uint8_t* cur;
     const int64_t* cur_off;  // [sent+1]

@@ -248,6 +248,57 @@ __global__ __launch_bounds__(256) void fec_vr_encode_kernel(VrEncodeArgs a) {
     }
 }
 
+// Instances of tuples with n = k (VrNp0Args): the codeword is X = [len BE16, payload, zero pad],
+// so a row is the payload shifted by the 2 header bytes.  Half a wave per row (lane c = 16-byte
+// chunk c of the row at stride W <= 512), 8 rows per pass: the chunk's payload dwords 4c-1 .. 4c+3
+// (one 16-byte and one 4-byte load; the header stands in for dword -1), shifted by 2 bytes, bytes
+// past the length zeroed, one 16-byte store; the trimmed size (FEC_Encoder.cpp:55-60) is the
+// half-wave's max of the last non-zero byte + 1.  In config 4 this is (10,0,0): 181 437 of the
+// 360 010 codewords, which the tile encoder walked with its parity machinery idle.
+__global__ __launch_bounds__(256) void fec_vr_encode_np0_kernel(VrNp0Args a) {
+    const int64_t* sg = a.seg + 8 * blockIdx.x;
+    const int64_t sfirst = sg[0], ssw = sg[1], P = sg[2];
+    const int t0 = static_cast<int>(sg[3] & 0xffffffff), cnt = static_cast<int>(sg[3] >> 32);
+    const int64_t scur = sg[4], sold = sg[5];
+    const int W = static_cast<int>(sg[6] >> 32);
+    const int64_t nsw = min(ssw - sfirst, P);  // rows from nsw on go to the old rows
+    const int tid = threadIdx.x, lane = tid & 63, c = lane & 31, L = a.L;
+    const bool on = 16 * c < W;
+    for (int rr = 2 * (tid >> 6) + (lane >> 5); rr < cnt; rr += 8) {
+        const int64_t t = t0 + rr, seq = sfirst + t;
+        int ln = a.len ? a.len[seq] : L;
+        ln = ln < 0 ? 0 : (ln > L ? L : ln);
+        const uint32_t* src = reinterpret_cast<const uint32_t*>(a.payload + seq * L);
+        uint32_t d[5];
+        if (on && 16 * c + 16 <= L) {
+            const uint4 v = *reinterpret_cast<const uint4*>(src + 4 * c);
+            d[1] = v.x;
+            d[2] = v.y;
+            d[3] = v.z;
+            d[4] = v.w;
+        } else {
+#pragma unroll
+            for (int m = 1; m < 5; ++m) d[m] = on && 4 * (4 * c + m - 1) < L ? src[4 * c + m - 1] : 0u;
+        }
+        d[0] = c == 0 ? (static_cast<uint32_t>((ln >> 8) & 0xff) << 16) | (static_cast<uint32_t>(ln & 0xff) << 24)
+                      : (on ? src[4 * c - 1] : 0u);
+        uint32_t o[4];
+        int last = -1;
+#pragma unroll
+        for (int m = 0; m < 4; ++m) {
+            const int q = 16 * c + 4 * m;  // X byte of o[m]'s byte 0
+            o[m] = __builtin_amdgcn_alignbyte(d[m + 1], d[m], 2) & keep_bytes(ln + 2 - q);
+            if (o[m]) last = q + 3 - (__builtin_clz(o[m]) >> 3);
+        }
+#pragma unroll
+        for (int off = 16; off > 0; off >>= 1) last = max(last, __shfl_xor(last, off));
+        const bool to_old = t >= nsw;
+        uint8_t* row = to_old ? a.old + sold + (t - nsw) * W : a.cur + scur + t * W;
+        if (on) *reinterpret_cast<uint4*>(row + 16 * c) = make_uint4(o[0], o[1], o[2], o[3]);
+        if (c == 0) (to_old ? a.len_old : a.len_cur)[seq] = last + 1;
+    }
+}
+
 // The same codewords in closed form, a workgroup per codeword and a thread per output dword: byte
 // q = (sub-stream s = q / n, position j = q % n) is X_seq[s][j] (j < k) or XOR_i G[i][j] *
 // X_{seq-(j-i)}[s][i] (rows before the instance's first call are zero).  The workgroup first brings
@@ -980,6 +1031,12 @@ int vr_launch_encode(const VrEncodeArgs& a, void* s) {
     const int64_t waves = std::max<int64_t>(1, std::min<int64_t>((a.cum_host_total + 1) / 2, 16384));
     const unsigned grid = static_cast<unsigned>((waves + wpb - 1) / wpb);
     hipLaunchKernelGGL(fec_vr_encode_kernel, dim3(grid), dim3(64 * wpb), static_cast<size_t>(wpb) * a.wave_bytes,
+                       static_cast<hipStream_t>(s), a);
+    return hipGetLastError() == hipSuccess ? FEC_OK : FEC_ERR_HIP;
+}
+int vr_launch_encode_np0(const VrNp0Args& a, void* s) {
+    if (a.nseg <= 0) return FEC_OK;
+    hipLaunchKernelGGL(fec_vr_encode_np0_kernel, dim3(static_cast<unsigned>(a.nseg)), dim3(256), 0,
                        static_cast<hipStream_t>(s), a);
     return hipGetLastError() == hipSuccess ? FEC_OK : FEC_ERR_HIP;
 }

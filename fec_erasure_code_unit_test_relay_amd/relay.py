@@ -192,3 +192,92 @@ class StateDependentRelay:
         check(lib().fec_sdswdf_dest_plan(*args, rec.ctypes.data_as(ctypes.c_void_p), rec.size, ctypes.byref(n),
                                          ctypes.byref(rb)), "fec_sdswdf_dest_plan")
         return ids, rec, fl
+
+
+T_TOT = 10  # FEC_Macro.h
+
+
+class AdaptiveRelay:
+    """The relay chain under variable rate (RELAYING_TYPE 2 or 3 through code switches,
+    Variable_Rate_FEC_Decoder.cpp:600-740 relay, :1423-1600 / :1772-1873 destination), batched:
+    ``schedule`` = [(seq, T, N), ...] source codes (T, N, N), the first at seq 0, each at least
+    T_TOT + 1 after the previous (the T_TOT + 1 double-coded seqs of a switch); hop 2 re-encodes
+    with the same (T, N).  ``run`` returns what the relay sends per seq ([BE16 size][new part]
+    [old part during double coding]) and what the reporting destination object outputs per seq
+    (fec_relay_vr_* in include/fec_amd.h)."""
+
+    def __init__(self, relay_type: int, max_payload: int, schedule, P: int):
+        import numpy as np
+        sched = np.ascontiguousarray(np.asarray(schedule, dtype=np.int32).reshape(-1, 3))
+        h = ctypes.c_void_p()
+        check(lib().fec_relay_vr_create(relay_type, max_payload, sched.ctypes.data_as(ctypes.c_void_p), sched.shape[0],
+                                        P, ctypes.byref(h)), "fec_relay_vr_create")
+        self._h = h
+        v = [ctypes.c_int() for _ in range(3)]
+        check(lib().fec_relay_vr_geometry(h, *[ctypes.byref(x) for x in v]), "fec_relay_vr_geometry")
+        self.frame_stride, self.out_stride, self.codes = (x.value for x in v)
+        self.type, self.L, self.P = relay_type, max_payload, P
+
+    def __del__(self):
+        if getattr(self, "_h", None):
+            try:
+                lib().fec_relay_vr_destroy(self._h)
+            except Exception:
+                pass
+            self._h = None
+
+    @staticmethod
+    def schedule_from_plan(plan, P: int):
+        """Switch points of a variable-rate plan's encoder instances (fec_vr.VrPlan.encoders:
+        (T, B, N, first, role switch, end), adaptive tuples B = N) that start at least T_TOT + 1
+        seqs after the previous kept one, as the relay's code schedule."""
+        sched = []
+        for T, B, N, first, _sw, _end in plan.encoders.tolist():
+            if first >= P:
+                break
+            if not sched or first >= sched[-1][0] + T_TOT + 1:
+                sched.append((int(first), int(T), int(N)))
+        return sched
+
+    def run(self, payload, e1, e2):
+        """payload [P, L] uint8 on the GPU (source packet t), hop erasure flags e1 / e2 (P host
+        bytes, numpy) -> (frames [P, frame_stride], frame_len [P] int32, out [P, out_stride], flags
+        [P] numpy uint8)."""
+        import numpy as np
+        import torch
+        assert payload.dtype == torch.uint8 and payload.is_cuda and payload.is_contiguous()
+        assert tuple(payload.shape) == (self.P, self.L)
+        e1 = np.ascontiguousarray(np.asarray(e1, dtype=np.uint8)[:self.P])
+        e2 = np.ascontiguousarray(np.asarray(e2, dtype=np.uint8)[:self.P])
+        assert e1.size == self.P and e2.size == self.P
+        dev = payload.device
+        frames = torch.empty((self.P, self.frame_stride), dtype=torch.uint8, device=dev)
+        flen = torch.empty(self.P, dtype=torch.int32, device=dev)
+        out = torch.empty((self.P, self.out_stride), dtype=torch.uint8, device=dev)
+        flags = np.zeros(self.P, dtype=np.uint8)
+        stream = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+        check(lib().fec_relay_vr_run(self._h, _ptr(payload), e1.ctypes.data_as(ctypes.c_void_p),
+                                     e2.ctypes.data_as(ctypes.c_void_p), _ptr(frames), _ptr(flen), _ptr(out),
+                                     flags.ctypes.data_as(ctypes.c_void_p), stream), "fec_relay_vr_run")
+        return frames, flen, out, flags
+
+
+def relay_digest(frames, frame_len, out, flags, block: int = 100):
+    """Per block of ``block`` seqs the CRC-32 of every seq's [frame_len LE32][frame][out][flag]
+    (as tests/cpp/relay_dropin_test.cpp --digest writes for the reference-structured driver)."""
+    import zlib
+    import numpy as np
+    fr = frames.cpu().numpy()
+    fl = frame_len.cpu().numpy().astype(np.int64)
+    ou = out.cpu().numpy()
+    P = fr.shape[0]
+    res = []
+    for b0 in range(0, P, block):
+        c = 0
+        for t in range(b0, min(P, b0 + block)):
+            c = zlib.crc32(int(fl[t]).to_bytes(4, "little"), c)
+            c = zlib.crc32(fr[t, :fl[t]].tobytes(), c)
+            c = zlib.crc32(ou[t].tobytes(), c)
+            c = zlib.crc32(bytes([int(flags[t])]), c)
+        res.append(c)
+    return res

@@ -353,11 +353,44 @@ int fec_sdswdf_relay_batch(fec_sdswdf *w, const uint8_t *d_cw, int64_t cw_stride
                            int64_t P, uint8_t *d_frames, void *hip_stream);
 int fec_sdswdf_destination_batch(fec_sdswdf *w, const uint8_t *d_frames, const uint8_t *h_erasure, int64_t P,
                                  uint8_t *d_out, uint8_t *h_flag, void *hip_stream);
+/* The same over several independent streams laid end to end (fec_relay_vr): a fresh relay /
+ * destination takes over at each row of h_starts (sorted); the rows in front of a start that its
+ * plans reach must be zero codewords / frames on received (0) flags, as before a stream's seq 0. */
+int fec_sdswdf_relay_batch_starts(fec_sdswdf *w, const uint8_t *d_cw, int64_t cw_stride, const uint8_t *h_erasure,
+                                  int64_t P, const int64_t *h_starts, int nstarts, uint8_t *d_frames,
+                                  void *hip_stream);
+int fec_sdswdf_destination_batch_starts(fec_sdswdf *w, const uint8_t *d_frames, const uint8_t *h_erasure,
+                                        int64_t P, const int64_t *h_starts, int nstarts, uint8_t *d_out,
+                                        uint8_t *h_flag, void *hip_stream);
 int fec_sdswdf_relay_plan(fec_sdswdf *w, const uint8_t *h_erasure, int64_t P, int32_t *h_plan,
                           uint8_t *h_records, int64_t records_cap, int64_t *n_records, int *record_bytes);
 int fec_sdswdf_dest_plan(fec_sdswdf *w, const uint8_t *h_erasure, const uint8_t *h_headers, int64_t P,
                          int32_t *h_plan, uint8_t *h_flag, uint8_t *h_records, int64_t records_cap,
                          int64_t *n_records, int *record_bytes);
+
+/* ---- relay under variable rate: RELAYING_TYPE 2 / 3 through code switches ---------------------
+ * The relay chain of Variable_Rate_FEC_Decoder under a schedule of source codes (:600-740 relay,
+ * :1423-1600 and :1772-1873 destination): at a switch to (T, N) at seq s the relay and the
+ * destination create fresh Decoder_Symbol_Wise objects for it; for the T_TOT + 1 double-coded seqs
+ * s .. s + T_TOT (Variable_Rate_FEC_Encoder.cpp:74-235) the old objects take the old code's
+ * codewords and the new ones the new code's, the relay sends [BE16 size_cur][new part][old part]
+ * (part = [header 11 bytes, type 3][codeword_new_vector row of size = (S+1)*n2 bytes]), the
+ * destination's old object reports; at s + T_TOT + 1 the new objects take over (copy_elements).
+ * Hop 1 carries FEC_Encoder(max_payload, T, N, N) codewords, hop 2 the relay's (T, N) re-encoding
+ * (T2 = T: the relay-mode estimator fixes T = T_TOT, Parameter_Estimator.cpp:72-75).
+ *   fec_relay_vr_create: type 2 or 3; sched = nsw entries (seq, T, N), the first at seq 0, each at
+ *     least T_TOT + 1 = 11 after the previous, 1 <= T <= 10, N <= T; P seqs.
+ *   fec_relay_vr_run: d_payload P rows of max_payload bytes (source packet t), h_e1 / h_e2 P hop-1 /
+ *     hop-2 erasure flags (host) -> d_frames P rows of frame_stride bytes and d_frame_len P sizes
+ *     (the relay's frame per seq), d_out P rows of out_stride bytes (what the reporting destination
+ *     object's extract_data wrote at seq t: blocks*k bytes of its code, zero after), h_flag P (host,
+ *     may be NULL): the reporting object's loss flag.  Returns when done. */
+typedef struct fec_relay_vr fec_relay_vr;
+int fec_relay_vr_create(int type, int max_payload, const int32_t *sched, int nsw, int64_t P, fec_relay_vr **out);
+int fec_relay_vr_destroy(fec_relay_vr *r);
+int fec_relay_vr_geometry(const fec_relay_vr *r, int *frame_stride, int *out_stride, int *codes);
+int fec_relay_vr_run(fec_relay_vr *r, const uint8_t *d_payload, const uint8_t *h_e1, const uint8_t *h_e2,
+                     uint8_t *d_frames, int32_t *d_frame_len, uint8_t *d_out, uint8_t *h_flag, void *hip_stream);
 
 /* ---- relay per call: the Decoder_Symbol_Wise methods on caller-held state ---------------------
  * What siphon::Decoder_Symbol_Wise (fec_amd_dropin.h) calls: one reference method call each, on

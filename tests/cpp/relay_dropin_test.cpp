@@ -8,6 +8,8 @@
 //       objects per node, the frame [BE16 size][cur][old], copy_elements at its end,
 //       Variable_Rate_FEC_Decoder.cpp:1423-1600, :1772-1873).
 // Frames, destination outputs and loss flags must be equal per seq.
+#include <algorithm>
+#include <cstdint>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -74,18 +76,23 @@ struct OracleSW {
         delete decoder_current;
         delete encoder_current;
     }
+    // rows [0, m-1) take the contents of rows [1, m), row m-1 keeps its own: as the reference's
+    // memcpy loop, by moving the row pointers and copying only the last row's GMAX bytes once
+    static void shift_rows(unsigned char** v, int m) {
+        if (m < 2) return;
+        unsigned char* p0 = v[0];
+        for (int i = 0; i < m - 1; ++i) v[i] = v[i + 1];
+        std::memcpy(p0, v[m - 1], GMAX);
+        v[m - 1] = p0;
+    }
     void shift(int n, int n2) {  // Decoder_Symbol_Wise.cpp:120-135
-        for (int i = 0; i < n - 1; ++i) {
-            std::memcpy(codeword_vector[i], codeword_vector[i + 1], GMAX);
-            temp_erasure_vector[i] = temp_erasure_vector[i + 1];
-        }
-        for (int i = 0; i < n2 - 1; ++i) {
-            std::memcpy(codeword_new_vector[i], codeword_new_vector[i + 1], GMAX);
-            std::memcpy(codeword_vector_to_transmit[i], codeword_vector_to_transmit[i + 1], GMAX);
-        }
+        shift_rows(codeword_vector, n);
+        for (int i = 0; i < n - 1; ++i) temp_erasure_vector[i] = temp_erasure_vector[i + 1];
+        shift_rows(codeword_new_vector, n2);
+        shift_rows(codeword_vector_to_transmit, n2);
+        shift_rows(codeword_vector_state_dependent, 3 * TT);
         for (int i = 0; i < 3 * TT - 1; ++i) {
-            std::memcpy(codeword_vector_state_dependent[i], codeword_vector_state_dependent[i + 1], GMAX);
-            std::memcpy(header[i], header[i + 1], sizeof(int) * TT);
+            std::memcpy(header[i], header[i + 1], sizeof(int) * TT);  // (entry TT stays with its row)
             temp_erasure_vector_state_dependent[i] = temp_erasure_vector_state_dependent[i + 1];
         }
     }
@@ -416,9 +423,49 @@ std::vector<unsigned char> read_bytes(const char* path, int P) {
     std::fclose(f);
     return v;
 }
+// CRC-32 (IEEE, zlib's) of the seqs' [frame_len LE32][frame][out][flag], per block of kDigestBlock
+// seqs: the digest a product run (fec_relay_vr) is compared with (tests/golden/relay_vr_360k.json).
+constexpr int kDigestBlock = 100;
+uint32_t crc32_update(uint32_t c, const unsigned char* p, size_t n) {
+    static uint32_t tab[256];
+    static bool init = false;
+    if (!init) {
+        for (uint32_t i = 0; i < 256; ++i) {
+            uint32_t x = i;
+            for (int b = 0; b < 8; ++b) x = (x & 1) ? 0xEDB88320u ^ (x >> 1) : x >> 1;
+            tab[i] = x;
+        }
+        init = true;
+    }
+    c = ~c;
+    for (size_t i = 0; i < n; ++i) c = tab[(c ^ p[i]) & 0xff] ^ (c >> 8);
+    return ~c;
+}
+void write_digest(FILE* f, int R, const Trace& d, int P) {
+    int good = 0;
+    for (int fl : d.flags) good += fl == 0;
+    std::fprintf(f, "type %d P %d unflagged %d\n", R, P, good);
+    for (int b0 = 0; b0 < P; b0 += kDigestBlock) {
+        uint32_t c = 0;
+        for (int t = b0; t < std::min(P, b0 + kDigestBlock); ++t) {
+            const uint32_t fl = static_cast<uint32_t>(d.frames[t].size());
+            const unsigned char le[4] = {static_cast<unsigned char>(fl), static_cast<unsigned char>(fl >> 8),
+                                         static_cast<unsigned char>(fl >> 16), static_cast<unsigned char>(fl >> 24)};
+            c = crc32_update(c, le, 4);
+            c = crc32_update(c, d.frames[t].data(), d.frames[t].size());
+            c = crc32_update(c, d.outs[t].data(), d.outs[t].size());
+            const unsigned char f1 = static_cast<unsigned char>(d.flags[t]);
+            c = crc32_update(c, &f1, 1);
+        }
+        std::fprintf(f, "%08x\n", c);
+    }
+}
+
 template <class SW>
 int schedule_run(int argc, char** argv, bool compare_with_oracle) {
     if (argc < 5) return 2;
+    FILE* dig = nullptr;  // --schedule s e1 e2 --digest out.txt: per-block digests of each type's trace
+    if (argc >= 7 && std::strcmp(argv[5], "--digest") == 0) dig = std::fopen(argv[6], "w");
     FILE* f = std::fopen(argv[2], "r");
     int P = 0;
     if (!f || std::fscanf(f, "%d", &P) != 1) return 2;
@@ -432,6 +479,7 @@ int schedule_run(int argc, char** argv, bool compare_with_oracle) {
         const Trace d = chain<SW>(R, sched, -1, P, e1, e2);
         int good = 0;
         for (int fl : d.flags) good += fl == 0;
+        if (dig) write_digest(dig, R, d, P);
         if (compare_with_oracle) {
             const Trace o = chain<OracleSW>(R, sched, -1, P, e1, e2);
             char what[64];
@@ -444,6 +492,7 @@ int schedule_run(int argc, char** argv, bool compare_with_oracle) {
         std::printf("type %d schedule: %zu codes, %d seqs%s, %d unflagged\n", R, sched.size(), P,
                     compare_with_oracle ? " equal to the oracle methods" : "", good);
     }
+    if (dig) std::fclose(dig);
     return rc;
 }
 

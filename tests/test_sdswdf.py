@@ -421,3 +421,79 @@ def test_relay_c_abi_rejects_bad_arguments_before_device_work():
     assert Lb.fec_sdswdf_create(300, 3, 3, 0, 0, 0, ctypes.byref(h)) == ERR    # n2 = 1
     Lb.fec_swdf_create.argtypes = [i] * 5 + [ctypes.POINTER(vp)]
     assert Lb.fec_swdf_create(300, 3, 3, 0, 0, ctypes.byref(h)) == ERR         # n2 = 1
+
+
+def _relay_vr_golden():
+    import json
+    import os
+    from conftest import ROOT
+    with open(os.path.join(ROOT, "tests", "golden", "relay_vr_360k.json")) as f:
+        return json.load(f)
+
+
+def test_relay_vr_golden_prefix_from_driver(tmp_path):
+    """tests/golden/relay_vr_360k.json (made by tests/golden/make_relay_vr_golden.py from the
+    reference-structured driver over the oracle's methods, all 360 000 seqs): the same driver on
+    the first 3 000 seqs of its schedule reproduces its first 30 block digests (the chain is
+    causal: a shorter run is a prefix)."""
+    import subprocess
+    import numpy as np
+    g = _relay_vr_golden()
+    exe = _build_relay_driver(tmp_path, oracle_only=True)
+    P = 3000
+    sched = [s for s in g["schedule"] if s[0] < P]
+    f = tmp_path / "sched.txt"
+    f.write_text(f"{P}\n" + "".join(f"{s} {T} {N}\n" for s, T, N in sched))
+    e1, e2, dig = tmp_path / "e1.bin", tmp_path / "e2.bin", tmp_path / "dig.txt"
+    np.ascontiguousarray(load_pattern("bin_erasure")[:P], dtype=np.uint8).tofile(e1)
+    np.ascontiguousarray(load_pattern("bin_erasure2")[:P], dtype=np.uint8).tofile(e2)
+    r = subprocess.run([exe, "--schedule", str(f), str(e1), str(e2), "--digest", str(dig)], capture_output=True,
+                       text=True, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    lines = dig.read_text().split("\n")
+    for t in ("2", "3"):
+        i = next(j for j, ln in enumerate(lines) if ln.startswith(f"type {t} "))
+        blocks = [ln.strip() for ln in lines[i + 1:i + 1 + P // 100]]
+        assert blocks == g[f"type{t}"]["blocks"][:P // 100], t
+
+
+def test_relay_vr_create_rejects_bad_schedules():
+    """fec_relay_vr_create checks its schedule before any device work: relay type 2 or 3, the
+    first switch at seq 0, switches at least T_TOT + 1 apart (one double-coding transition at a
+    time, Variable_Rate_FEC_Encoder.cpp:74-235), 1 <= T <= T_TOT, 0 <= N <= T, seqs inside [0, P)."""
+    import ctypes
+    import numpy as np
+    from fec_erasure_code_unit_test_relay_amd._lib import lib
+    L = lib()
+    h = ctypes.c_void_p()
+    for typ, sched, P in [(1, [(0, 10, 3)], 100), (2, [(1, 10, 3)], 100), (3, [(0, 10, 3), (10, 10, 5)], 100),
+                          (2, [(0, 11, 3)], 100), (2, [(0, 10, 11)], 100), (2, [(0, 0, 0)], 100),
+                          (3, [(0, 10, 3), (100, 10, 5)], 100), (2, [(0, 10, 3)], 0)]:
+        a = np.ascontiguousarray(np.asarray(sched, dtype=np.int32))
+        st = L.fec_relay_vr_create(typ, 300, a.ctypes.data_as(ctypes.c_void_p), a.shape[0], P, ctypes.byref(h))
+        assert st == -1, (typ, sched, P)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("relay_type", [2, 3])
+def test_gpu_relay_vr_full_schedule_equals_driver(relay_type):
+    """The batched relay chain under variable rate (fec_relay_vr: every code instance of config 4's
+    schedule on bin/erasure.bin, hop 2 on bin/erasure2.bin, one fixed-rate batch per code with
+    the instances end to end) equals, seq by seq, the reference-structured driver over the oracle's
+    Decoder_Symbol_Wise methods for all 360 000 seqs: every frame (double-coding layout), every
+    destination output and loss flag, by the golden file's per-100-seq CRC-32 digests."""
+    import torch
+    from fec_erasure_code_unit_test_relay_amd import fill_payload
+    from fec_erasure_code_unit_test_relay_amd.relay import AdaptiveRelay, relay_digest
+    torch.cuda.set_device(0)
+    g = _relay_vr_golden()
+    P = g["P"]
+    r = AdaptiveRelay(relay_type, 300, g["schedule"], P)
+    payload = fill_payload(0, P, 300, 0x5EED)
+    frames, flen, out, flags = r.run(payload, load_pattern("bin_erasure"), load_pattern("bin_erasure2"))
+    torch.cuda.synchronize()
+    want = g[f"type{relay_type}"]
+    assert int((flags == 0).sum()) == want["unflagged"]
+    got = [f"{c:08x}" for c in relay_digest(frames, flen, out, flags)]
+    bad = [i for i, (a, b) in enumerate(zip(got, want["blocks"])) if a != b]
+    assert len(got) == len(want["blocks"]) and not bad, f"first differing block {bad[:5]} of {len(got)}"
