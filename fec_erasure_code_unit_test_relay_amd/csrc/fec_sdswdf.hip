@@ -234,13 +234,18 @@ public:
     int record_bytes() const { return kHdr + n2_ * n_; }
     const RecordTable& records() const { return records_; }
     void reset() {
+        records_.clear();
+        memo_.clear();
+        rows_.clear();
+        restart();
+    }
+    // A fresh relay's state, keeping the records, the memo and the interned header rows (their
+    // meaning does not depend on the state): the plans of several streams in one table.
+    void restart() {
         std::memset(er_, 0, sizeof(er_));
         std::memset(valid_, 0, sizeof(valid_));
         for (int i = 0; i < kSlots; ++i)
             for (int jj = 0; jj < kHdr; ++jj) header_[i][jj] = jj + 1;  // :60-62
-        records_.clear();
-        memo_.clear();
-        rows_.clear();
         er_bits_ = valid_bits_ = 0;
         last_key_ok_ = false;
         const uint16_t id0 = rows_.intern(header_[0]);
@@ -499,12 +504,16 @@ public:
     int record_bytes() const { return k_ * n_; }
     const RecordTable& records() const { return records_; }
     void reset() {
-        std::memset(valid_, 0, sizeof(valid_));
-        for (int i = 0; i < kSlots; ++i)
-            for (int jj = 0; jj < kHdr; ++jj) header_[i][jj] = jj + 1;
         records_.clear();
         memo_.clear();
         rows_.clear();
+        restart();
+    }
+    // A fresh destination's state, keeping the records, the memo and the interned header rows.
+    void restart() {
+        std::memset(valid_, 0, sizeof(valid_));
+        for (int i = 0; i < kSlots; ++i)
+            for (int jj = 0; jj < kHdr; ++jj) header_[i][jj] = jj + 1;
         valid_bits_ = 0;
         last_ok_ = false;
         last_key_ok_ = false;
@@ -823,7 +832,7 @@ void plan_relay(fec_sdswdf* w, const uint8_t* h_erasure, int64_t P, const int64_
     int si = 0;
     for (int64_t t = 0; t < P; ++t) {
         while (si < nstarts && starts[si] <= t) {
-            if (starts[si++] == t) w->relay->reset();
+            if (starts[si++] == t) w->relay->restart();
         }
         w->plan[static_cast<size_t>(t)] = w->relay->step(h_erasure[t] != 0);
     }
@@ -837,7 +846,7 @@ void plan_dest(fec_sdswdf* w, const uint8_t* h_erasure, const uint8_t* hdrs, int
     int si = 0;
     for (int64_t t = 0; t < P; ++t) {
         while (si < nstarts && starts[si] <= t) {
-            if (starts[si++] == t) w->dest->reset();
+            if (starts[si++] == t) w->dest->restart();
         }
         bool fl = false;
         w->plan[static_cast<size_t>(t)] = w->dest->step(h_erasure[t] != 0, hdrs + t * fec::kHdr, &fl);

@@ -1313,8 +1313,11 @@ int prepare_encode(fec_vr_plan* v, hipStream_t s) {
     if (const char* e = std::getenv("FEC_VR_TILE_UNIT")) unit = std::max(1, std::atoi(e));
     const bool tiles_on = !std::getenv("FEC_VR_NO_TILE");
     const bool multi_on = !std::getenv("FEC_VR_NO_MULTI");
+    // (10,0,0)'s rows through fec_vr_encode_np0_kernel beside the multi-tuple launch: opt-in
+    // (FEC_VR_NP0=1) -- the multi-tuple launch did not get shorter without them (109 vs 105 us)
+    // and the two together took longer (encode 0.144 vs 0.125 ms, profiles/r05/vr/r05zh_*)
     const char* np0e = std::getenv("FEC_VR_NP0");
-    const bool np0_on = tiles_on && !(np0e && np0e[0] == '0');
+    const bool np0_on = tiles_on && np0e && np0e[0] == '1';
     std::vector<int64_t> np0;
     int tab = 32, out = 16, slot = 16, nmax = 1;
     for (size_t ei = 0; ei < p.enc.size(); ++ei) {
