@@ -1313,11 +1313,13 @@ int prepare_encode(fec_vr_plan* v, hipStream_t s) {
     if (const char* e = std::getenv("FEC_VR_TILE_UNIT")) unit = std::max(1, std::atoi(e));
     const bool tiles_on = !std::getenv("FEC_VR_NO_TILE");
     const bool multi_on = !std::getenv("FEC_VR_NO_MULTI");
-    // (10,0,0)'s rows through fec_vr_encode_np0_kernel beside the multi-tuple launch: opt-in
-    // (FEC_VR_NP0=1) -- the multi-tuple launch did not get shorter without them (109 vs 105 us)
-    // and the two together took longer (encode 0.144 vs 0.125 ms, profiles/r05/vr/r05zh_*)
+    // (10,0,0)'s rows through fec_vr_encode_np0_kernel: opt-in.  Beside the multi-tuple launch
+    // (FEC_VR_NP0=1) the two took longer (encode 0.144 vs 0.125 ms; the multi-tuple launch 109 vs
+    // 105 us, profiles/r05/vr/r05zh_*); in front of it on the caller's stream (FEC_VR_NP0=2) the
+    // multi-tuple launch shrinks to 70 us but np0 takes 27 - 37 us: encode 0.126 - 0.128 vs
+    // 0.126 - 0.129 ms (r05zn), no gain.
     const char* np0e = std::getenv("FEC_VR_NP0");
-    const bool np0_on = tiles_on && np0e && np0e[0] == '1';
+    const bool np0_on = tiles_on && np0e && (np0e[0] == '1' || np0e[0] == '2');
     std::vector<int64_t> np0;
     int tab = 32, out = 16, slot = 16, nmax = 1;
     for (size_t ei = 0; ei < p.enc.size(); ++ei) {
@@ -1786,8 +1788,10 @@ int fec_vr_encode_batch(fec_vr_plan* v, const uint8_t* d_payload, const int32_t*
         if (int st = use_cf ? fec::vr_launch_encode_cf(a, sg) : fec::vr_launch_encode(a, sg)) return st;
     }
     if (tiled && v->n_np0 > 0) {
-        hipStream_t s0;
-        if (int st = v->fork.stream(next_side++, &s0)) return st;
+        hipStream_t s0 = s;  // FEC_VR_NP0=2: in front of the multi-tuple launch on the caller's stream
+        const char* np0e = std::getenv("FEC_VR_NP0");
+        if (!(np0e && np0e[0] == '2'))
+            if (int st = v->fork.stream(next_side++, &s0)) return st;
         fec::VrNp0Args a0{d_payload, d_payload_len, v->plan.L, v->d_np0, v->n_np0, d_cw_cur, d_cw_old, d_len_cur, d_len_old};
         if (int st = fec::vr_launch_encode_np0(a0, s0)) return st;
     }

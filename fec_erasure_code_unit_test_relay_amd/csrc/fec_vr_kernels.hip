@@ -249,28 +249,32 @@ __global__ __launch_bounds__(256) void fec_vr_encode_kernel(VrEncodeArgs a) {
 }
 
 // Instances of tuples with n = k (VrNp0Args): the codeword is X = [len BE16, payload, zero pad],
-// so a row is the payload shifted by the 2 header bytes.  Half a wave per row (lane c = 16-byte
-// chunk c of the row at stride W <= 512), 8 rows per pass: the chunk's payload dwords 4c-1 .. 4c+3
-// (one 16-byte and one 4-byte load; the header stands in for dword -1), shifted by 2 bytes, bytes
-// past the length zeroed, one 16-byte store; the trimmed size (FEC_Encoder.cpp:55-60) is the
-// half-wave's max of the last non-zero byte + 1.  In config 4 this is (10,0,0): 181 437 of the
+// so a row is the payload shifted by the 2 header bytes.  A thread per 16-byte chunk c of a row at
+// stride W (the segment's rows x chunks flattened over the workgroup, every lane busy): the chunk's
+// payload dwords 4c-1 .. 4c+3 (the header stands in for dword -1), shifted by 2 bytes, bytes past
+// the length zeroed, one 16-byte store; the trimmed size (FEC_Encoder.cpp:55-60) is each row's max
+// of the last non-zero byte + 1 (an LDS max per row).  In config 4 this is (10,0,0): 181 437 of the
 // 360 010 codewords, which the tile encoder walked with its parity machinery idle.
 __global__ __launch_bounds__(256) void fec_vr_encode_np0_kernel(VrNp0Args a) {
+    __shared__ int s_last[kVrNp0Rows];
     const int64_t* sg = a.seg + 8 * blockIdx.x;
     const int64_t sfirst = sg[0], ssw = sg[1], P = sg[2];
     const int t0 = static_cast<int>(sg[3] & 0xffffffff), cnt = static_cast<int>(sg[3] >> 32);
     const int64_t scur = sg[4], sold = sg[5];
-    const int W = static_cast<int>(sg[6] >> 32);
+    const int W = static_cast<int>(sg[6] >> 32), NCH = W >> 4;
     const int64_t nsw = min(ssw - sfirst, P);  // rows from nsw on go to the old rows
-    const int tid = threadIdx.x, lane = tid & 63, c = lane & 31, L = a.L;
-    const bool on = 16 * c < W;
-    for (int rr = 2 * (tid >> 6) + (lane >> 5); rr < cnt; rr += 8) {
+    const int tid = threadIdx.x, L = a.L;
+    if (tid < kVrNp0Rows) s_last[tid] = -1;
+    __syncthreads();
+    const float rch = 1.0f / static_cast<float>(NCH);
+    for (int i = tid; i < cnt * NCH; i += 256) {
+        const int rr = static_cast<int>((static_cast<float>(i) + 0.5f) * rch), c = i - rr * NCH;
         const int64_t t = t0 + rr, seq = sfirst + t;
         int ln = a.len ? a.len[seq] : L;
         ln = ln < 0 ? 0 : (ln > L ? L : ln);
         const uint32_t* src = reinterpret_cast<const uint32_t*>(a.payload + seq * L);
         uint32_t d[5];
-        if (on && 16 * c + 16 <= L) {
+        if (16 * c + 16 <= L) {
             const uint4 v = *reinterpret_cast<const uint4*>(src + 4 * c);
             d[1] = v.x;
             d[2] = v.y;
@@ -278,10 +282,10 @@ __global__ __launch_bounds__(256) void fec_vr_encode_np0_kernel(VrNp0Args a) {
             d[4] = v.w;
         } else {
 #pragma unroll
-            for (int m = 1; m < 5; ++m) d[m] = on && 4 * (4 * c + m - 1) < L ? src[4 * c + m - 1] : 0u;
+            for (int m = 1; m < 5; ++m) d[m] = 4 * (4 * c + m - 1) < L ? src[4 * c + m - 1] : 0u;
         }
         d[0] = c == 0 ? (static_cast<uint32_t>((ln >> 8) & 0xff) << 16) | (static_cast<uint32_t>(ln & 0xff) << 24)
-                      : (on ? src[4 * c - 1] : 0u);
+                      : src[4 * c - 1];
         uint32_t o[4];
         int last = -1;
 #pragma unroll
@@ -290,12 +294,15 @@ __global__ __launch_bounds__(256) void fec_vr_encode_np0_kernel(VrNp0Args a) {
             o[m] = __builtin_amdgcn_alignbyte(d[m + 1], d[m], 2) & keep_bytes(ln + 2 - q);
             if (o[m]) last = q + 3 - (__builtin_clz(o[m]) >> 3);
         }
-#pragma unroll
-        for (int off = 16; off > 0; off >>= 1) last = max(last, __shfl_xor(last, off));
+        if (last >= 0) atomicMax(&s_last[rr], last);
         const bool to_old = t >= nsw;
         uint8_t* row = to_old ? a.old + sold + (t - nsw) * W : a.cur + scur + t * W;
-        if (on) *reinterpret_cast<uint4*>(row + 16 * c) = make_uint4(o[0], o[1], o[2], o[3]);
-        if (c == 0) (to_old ? a.len_old : a.len_cur)[seq] = last + 1;
+        *reinterpret_cast<uint4*>(row + 16 * c) = make_uint4(o[0], o[1], o[2], o[3]);
+    }
+    __syncthreads();
+    if (tid < cnt) {
+        const int64_t t = t0 + tid;
+        (t >= nsw ? a.len_old : a.len_cur)[sfirst + t] = s_last[tid] + 1;
     }
 }
 
