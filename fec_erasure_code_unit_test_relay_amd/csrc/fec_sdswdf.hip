@@ -34,6 +34,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <array>
 #include <cstring>
 #include <map>
@@ -756,6 +757,199 @@ __global__ __launch_bounds__(kSdThreads) void fec_sdswdf_dest_kernel(SdDestArgs 
     }
 }
 
+// ---- tile kernels (round 5) ------------------------------------------------------------------
+// The same byte work by tiles: a workgroup per TP = 4 * (64 / NS4) consecutive packets, a lane per
+// (packet, group of 4 code blocks).  The rows the tile's plans read (one contiguous span) are
+// staged in LDS with 16-byte loads; each record's non-zero coefficients come as a compact list
+// per output row (SdEntries: per row [beg, end) into entries of p | log2(c) << 8, built on the
+// host from the interned records; there were 133 records for 360 000 packets of bin/erasure.bin,
+// 31 of 121 coefficients non-zero per packet, 72 % of the rows a single 1); a product is four
+// branch-free log/exp lookups (log[0] = 512 past the exp table's zeros), a coefficient 1 a copy.
+// The lane's 4 blocks of every output row land in an LDS output tile placed at the global rows'
+// 16-byte phase, which leaves as 16-byte stores (byte stores at the tile's two ends).
+struct SdTileArgs {
+    const uint8_t* in;        // rows of stride bytes (source codewords / relay frames)
+    int64_t stride, in_bytes; // row pitch; bytes of in (reads past them return zero)
+    int in_off;               // byte of symbol (j, 0) in a row (0 / 4 + kHdr)
+    const int32_t* plan;      // per packet: record id
+    const uint8_t* rec;       // records (relay: header bytes at rec*R)
+    int R;
+    const uint32_t* ent_off;  // per record: offset of its entry block in ent (uint16 units)
+    const uint16_t* ent;      // entry blocks: beg[ROWS + 1], then entries p | logc << 8
+    int64_t P;
+    int S, blocks;
+    const uint8_t* gf;        // exp[512], log[256]
+    uint8_t* out;             // relay: frames of F bytes; destination: rows of S*k bytes
+    int F;
+};
+
+#ifndef FEC_SD_PASS
+#define FEC_SD_PASS 1
+#endif
+// packets per lane and tile (halo rows staged once per tile).  2 measured slower: relay 268 vs
+// 246 us, destination 129 vs 121 us per 360 000 packets (profiles/r05/relay/r05zp_*).
+constexpr int kSdPass = FEC_SD_PASS;
+// shift = the row offset of an output row's diagonal: relay row index reads source packet
+// t - (N-1) + (K-1-index) + p; destination row s reads frame t - s - (N2-1-q).
+template <int K, int N, int ROWS, bool RELAY>
+__global__ __launch_bounds__(256) void fec_sd_tile_kernel(SdTileArgs a) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    uint8_t* gexp = smem;                                          // 1040: exp[0..509], zeros after
+    uint16_t* glog = reinterpret_cast<uint16_t*>(smem + 1040);    // 512: log, log[0] = 512
+    int32_t* srec = reinterpret_cast<int32_t*>(smem + 1552);       // TP record ids (<= 64)
+    uint8_t* raw = smem + 1552 + 256;                             // staged rows, then the output tile
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    for (int i = tid; i < 1040; i += 256) gexp[i] = i < 510 ? a.gf[i] : 0;
+    for (int i = tid; i < 256; i += 256) glog[i] = i ? a.gf[512 + i] : 512;
+    const int S = a.S, NS4 = (S + 3) >> 2, ppw = 64 / NS4, TP = kSdPass * 4 * ppw;
+    const int64_t t0 = static_cast<int64_t>(blockIdx.x) * TP;
+    const int nt = static_cast<int>(min<int64_t>(TP, a.P - t0));
+    // rows read: relay [t0 - (N-1) - (ROWS-1) + (K-1), t0+nt); destination [t0 - (K-1) - (N-1), t0+nt)
+    constexpr int BACK = RELAY ? (N - 1) + (ROWS - 1) - (K - 1) : (ROWS - 1) + (N - 1);
+    const int64_t r0 = t0 - BACK;
+    const int nrows = nt + BACK;
+    const int64_t g0 = r0 * a.stride;
+    const int64_t A = g0 >= 0 ? (g0 & ~int64_t(15)) : -((-g0 + 15) & ~int64_t(15));
+    const int dlt = static_cast<int>(g0 - A);
+    const int span = dlt + nrows * static_cast<int>(a.stride);
+    {
+        const int64_t base = A > 0 ? A : 0, lim = a.in_bytes - base;
+        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+            const_cast<uint8_t*>(a.in + base), 0, static_cast<int>(lim < 0x7fffffff ? lim : 0x7fffffff), 0x00020000);
+        typedef uint32_t v4 __attribute__((ext_vector_type(4)));
+        for (int c = tid; 16 * c < span; c += 256) {
+            const int64_t o = A + 16 * c;  // bytes before the array read as zero (rows before seq 0)
+            const v4 v = o < 0 ? v4{0, 0, 0, 0}
+                               : __builtin_amdgcn_raw_buffer_load_b128(rs, static_cast<int>(o - base), 0, 0);
+            *reinterpret_cast<v4*>(raw + 16 * c) = v;
+        }
+    }
+    if (tid < nt) srec[tid] = a.plan[t0 + tid];
+    __syncthreads();
+    const int pl = lane / NS4, g = lane - pl * NS4;
+    uint32_t A4[kSdPass][ROWS];
+#pragma unroll
+    for (int ps = 0; ps < kSdPass; ++ps) {
+    const int tl = (ps * 4 + wv) * ppw + pl;  // the lane's packet in the tile
+    const bool on = pl < ppw && tl < nt;
+#pragma unroll
+    for (int r = 0; r < ROWS; ++r) A4[ps][r] = 0;
+    if (on) {
+        const int rid = srec[tl];
+        const uint16_t* eb = a.ent + a.ent_off[rid];
+        const uint8_t* rowbase = raw + dlt + a.in_off + 4 * g * N;
+#pragma unroll
+        for (int r = 0; r < ROWS; ++r) {
+            // row of the diagonal's symbol p, relative to r0
+            const int lr0 = RELAY ? tl + (ROWS - 1) - r : tl + (K - 1) - r;  // + p (relay) / + q (destination)
+            uint32_t acc = 0;
+            for (int e = eb[r]; e < eb[r + 1]; ++e) {
+                const uint32_t en = eb[ROWS + 1 + e];
+                const int p = static_cast<int>(en & 0xff), lc = static_cast<int>(en >> 8);
+                const uint8_t* sp = rowbase + (lr0 + p) * static_cast<int>(a.stride) + p;
+                uint32_t w = 0;
+                if (lc == 0) {
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) w |= static_cast<uint32_t>(sp[q * N]) << (8 * q);
+                } else {
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) w |= static_cast<uint32_t>(gexp[lc + glog[sp[q * N]]]) << (8 * q);
+                }
+                acc ^= w;
+            }
+            A4[ps][r] = acc;
+        }
+    }
+    }
+    __syncthreads();  // the staged rows are read: the output tile takes their place
+    const int OB = RELAY ? a.F : S * K;                 // output row bytes
+    const int64_t ob0 = t0 * OB;
+    const int odl = static_cast<int>(ob0 & 15);
+    uint8_t* ot = raw + odl;                            // output byte b of row tl at ot[tl * OB + b]
+#pragma unroll
+    for (int ps = 0; ps < kSdPass; ++ps) {
+    const int tl = (ps * 4 + wv) * ppw + pl;
+    const bool on = pl < ppw && tl < nt;
+    if (on) {
+        uint8_t* orow = ot + tl * OB;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int j = 4 * g + q;
+            if (j >= S) break;
+            const bool keep = j < a.blocks;  // blocks past ceil(max_payload/k)+1 stay zero (:184-185)
+            uint8_t* d = orow + (RELAY ? 4 + kHdr + j * ROWS : j * K);
+#pragma unroll
+            for (int r = 0; r < ROWS; ++r) d[r] = keep ? static_cast<uint8_t>(A4[ps][r] >> (8 * q)) : 0;
+        }
+        if (RELAY && g == 0) {  // [size BE16][header 11][2 zero bytes] ... [zero tail]
+            const int size = (S + 1) * ROWS;
+            orow[0] = static_cast<uint8_t>(size >> 8);
+            orow[1] = static_cast<uint8_t>(size);
+            const uint8_t* h = a.rec + static_cast<int64_t>(srec[tl]) * a.R;
+            for (int i = 0; i < kHdr; ++i) orow[2 + i] = h[i];
+            orow[2 + kHdr] = 0;
+            orow[3 + kHdr] = 0;
+            for (int o = 4 + kHdr + S * ROWS; o < OB; ++o) orow[o] = 0;
+        }
+    }
+    }
+    __syncthreads();
+    const int obytes = nt * OB;
+    uint8_t* dst = a.out + ob0 - odl;  // 16-byte aligned when out is
+    for (int c = tid; 16 * c < odl + obytes; c += 256) {
+        const int lo = 16 * c;
+        if (lo >= odl && lo + 16 <= odl + obytes && (reinterpret_cast<uintptr_t>(dst) & 15) == 0) {
+            *reinterpret_cast<uint4*>(dst + lo) = *reinterpret_cast<const uint4*>(raw + lo);
+        } else {
+            for (int b = max(lo, odl); b < min(lo + 16, odl + obytes); ++b) dst[b] = raw[b];
+        }
+    }
+}
+
+#define FEC_SD_TILE_LIST(X) \
+    X(11, 11, 11) X(10, 11, 11) X(9, 11, 11) X(8, 11, 11) X(7, 11, 11) X(6, 11, 11) X(5, 11, 11) X(4, 11, 11) \
+    X(6, 11, 9) X(8, 11, 9)
+#define FEC_SD_TILE_INST(K, N, N2) \
+    template __global__ void fec_sd_tile_kernel<K, N, N2, true>(SdTileArgs); \
+    template __global__ void fec_sd_tile_kernel<K, N2, K, false>(SdTileArgs);
+FEC_SD_TILE_LIST(FEC_SD_TILE_INST)
+
+// The tile kernel for the relay (k, n1, n2) / the destination (k, n2), or nullptr.
+const void* sd_tile_kernel_for(bool relay, int k, int n1, int n2) {
+#define FEC_SD_TILE_CASE(K, N, N2)                                                                        \
+    if (k == K && n2 == N2 && (!relay || n1 == N))                                                     \
+        return relay ? reinterpret_cast<const void*>(&fec_sd_tile_kernel<K, N, N2, true>)               \
+                     : reinterpret_cast<const void*>(&fec_sd_tile_kernel<K, N2, K, false>);
+    FEC_SD_TILE_LIST(FEC_SD_TILE_CASE)
+#undef FEC_SD_TILE_CASE
+    return nullptr;
+}
+
+// Entry blocks of a record table: per record, for each of its `rows` output rows of `cols`
+// coefficients (starting at byte `first` of the record), the non-zero ones as p | log2(c) << 8.
+void build_entries(const std::vector<uint8_t>& recs, int R, int first, int rows, int cols, std::vector<uint32_t>& off,
+                   std::vector<uint16_t>& ent) {
+    const Field& F = field();
+    const size_t nrec = R > 0 ? recs.size() / static_cast<size_t>(R) : 0;
+    off.assign(std::max<size_t>(nrec, 1), 0);
+    ent.clear();
+    for (size_t r = 0; r < nrec; ++r) {
+        off[r] = static_cast<uint32_t>(ent.size());
+        const uint8_t* c = recs.data() + r * static_cast<size_t>(R) + first;
+        const size_t b0 = ent.size();
+        ent.resize(b0 + static_cast<size_t>(rows) + 1, 0);
+        std::vector<uint16_t> list;
+        for (int i = 0; i < rows; ++i) {
+            ent[b0 + static_cast<size_t>(i)] = static_cast<uint16_t>(list.size());
+            for (int p = 0; p < cols; ++p)
+                if (uint8_t v = c[i * cols + p]) list.push_back(static_cast<uint16_t>(p | (F.log[v] << 8)));
+        }
+        ent[b0 + static_cast<size_t>(rows)] = static_cast<uint16_t>(list.size());
+        ent.insert(ent.end(), list.begin(), list.end());
+    }
+    if (ent.empty()) ent.push_back(0);
+}
+
 int grid_for(int64_t items) {
     return static_cast<int>(std::min<int64_t>((items + kSdThreads - 1) / kSdThreads, 16384));
 }
@@ -805,7 +999,9 @@ struct fec_sdswdf {
     std::unique_ptr<fec::SdDestPlanner> dest;
     std::vector<int32_t> plan;
     std::vector<uint8_t> hdrs;
-    fec::DevBuf d_plan, d_table, d_hdrs;
+    fec::DevBuf d_plan, d_table, d_hdrs, d_eoff, d_ent;
+    std::vector<uint32_t> eoff;
+    std::vector<uint16_t> ent;
     ~fec_sdswdf() {
         if (hop1) fec_codec_destroy(hop1);
         if (hop2) fec_codec_destroy(hop2);
@@ -863,6 +1059,52 @@ int upload_plan(fec_sdswdf* w, const fec::RecordTable& tab, int64_t P, hipStream
     if (!tab.data().empty() &&
         hipMemcpyAsync(w->d_table.p, tab.data().data(), tab.data().size(), hipMemcpyHostToDevice, s) != hipSuccess)
         return FEC_ERR_HIP;
+    return FEC_OK;
+}
+
+// The tile kernels (fec_sd_tile_kernel): the records' entry blocks up, then one launch; returns
+// 1 when the tile kernel does not apply (the caller launches the per-(packet, block) kernel).
+int launch_tile(fec_sdswdf* w, bool relay, const fec::RecordTable& tab, const uint8_t* d_in, int64_t stride,
+                int64_t P, uint8_t* d_out, hipStream_t s) {
+    const char* e = std::getenv("FEC_SD_TILE");
+    if (e && e[0] == '0') return 1;
+    const int k = w->g1.k, n1 = w->g1.n, n2 = w->g2.n, S = w->g1.S;
+    const void* kern = fec::sd_tile_kernel_for(relay, k, n1, n2);
+    const int NS4 = (S + 3) / 4;
+    if (!kern || NS4 > 64) return 1;
+    const int TP = fec::kSdPass * 4 * (64 / NS4);
+    const int N = relay ? n1 : n2, ROWS = relay ? n2 : k;
+    const int back = relay ? (N - 1) + (ROWS - 1) - (k - 1) : (ROWS - 1) + (N - 1);
+    const int OB = relay ? w->F : S * k;
+    const int64_t stage = 16 + static_cast<int64_t>(TP + back) * stride + 16, otile = 16 + static_cast<int64_t>(TP) * OB + 16;
+    const int64_t lds = 1552 + 256 + ((std::max(stage, otile) + 15) & ~int64_t(15));
+    if (lds > 65536) return 1;
+    const int R = relay ? fec::kHdr + n2 * n1 : k * n2;
+    fec::build_entries(tab.data(), R, relay ? fec::kHdr : 0, ROWS, N, w->eoff, w->ent);
+    if (int st = w->d_eoff.reserve(w->eoff.size() * 4)) return st;
+    if (int st = w->d_ent.reserve(w->ent.size() * 2)) return st;
+    if (hipMemcpyAsync(w->d_eoff.p, w->eoff.data(), w->eoff.size() * 4, hipMemcpyHostToDevice, s) != hipSuccess ||
+        hipMemcpyAsync(w->d_ent.p, w->ent.data(), w->ent.size() * 2, hipMemcpyHostToDevice, s) != hipSuccess)
+        return FEC_ERR_HIP;
+    fec::SdTileArgs a;
+    a.in = d_in;
+    a.stride = stride;
+    a.in_bytes = P * stride;
+    a.in_off = relay ? 0 : 4 + fec::kHdr;
+    a.plan = static_cast<const int32_t*>(w->d_plan.p);
+    a.rec = static_cast<const uint8_t*>(w->d_table.p);
+    a.R = R;
+    a.ent_off = static_cast<const uint32_t*>(w->d_eoff.p);
+    a.ent = static_cast<const uint16_t*>(w->d_ent.p);
+    a.P = P;
+    a.S = S;
+    a.blocks = w->blocks;
+    a.gf = relay ? w->v1.gf : w->v2.gf;
+    a.out = d_out;
+    a.F = w->F;
+    void* args[] = {&a};
+    const unsigned grid = static_cast<unsigned>((P + TP - 1) / TP);
+    if (hipLaunchKernel(kern, dim3(grid), dim3(256), args, static_cast<size_t>(lds), s) != hipSuccess) return FEC_ERR_HIP;
     return FEC_OK;
 }
 
@@ -1299,6 +1541,10 @@ int fec_sdswdf_relay_batch_starts(fec_sdswdf* w, const uint8_t* d_cw, int64_t cw
         if (int st = ensure_device(w)) return st;
         plan_relay(w, h_erasure, P, h_starts, nstarts);
         if (int st = upload_plan(w, w->relay->records(), P, s)) return st;
+        const int tl = launch_tile(w, true, w->relay->records(), d_cw, cw_stride, P, d_frames, s);
+        if (tl < 0) return tl;
+        if (tl == 0)
+            return hipStreamSynchronize(s) == hipSuccess ? static_cast<int>(FEC_OK) : static_cast<int>(FEC_ERR_HIP);
         fec::SdRelayArgs a;
         a.cw = d_cw;
         a.cw_stride = cw_stride;
@@ -1349,6 +1595,10 @@ int fec_sdswdf_destination_batch_starts(fec_sdswdf* w, const uint8_t* d_frames, 
             return static_cast<int>(FEC_ERR_HIP);
         plan_dest(w, h_erasure, w->hdrs.data(), P, h_flag, h_starts, nstarts);
         if (int st = upload_plan(w, w->dest->records(), P, s)) return st;
+        const int tl = launch_tile(w, false, w->dest->records(), d_frames, w->F, P, d_out, s);
+        if (tl < 0) return tl;
+        if (tl == 0)
+            return hipStreamSynchronize(s) == hipSuccess ? static_cast<int>(FEC_OK) : static_cast<int>(FEC_ERR_HIP);
         fec::SdDestArgs a;
         a.frames = d_frames;
         a.F = w->F;
