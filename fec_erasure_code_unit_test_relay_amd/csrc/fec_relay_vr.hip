@@ -335,9 +335,6 @@ int fec_relay_vr_run(fec_relay_vr* r, const uint8_t* d_payload, const uint8_t* h
                 if (int st = fec_swdf_destination_batch(c.sw, c.d_frames.as<uint8_t>(), c.d_er2.as<uint8_t>(), R,
                                                         c.d_out.as<uint8_t>(), c.d_flag.as<uint8_t>(), s))
                     return st;
-                c.h_flag.resize(static_cast<size_t>(R));
-                if (hipMemcpyAsync(c.h_flag.data(), c.d_flag.p, static_cast<size_t>(R), hipMemcpyDeviceToHost, s) != hipSuccess)
-                    return FEC_ERR_HIP;
             } else {
                 const int ns = static_cast<int>(c.starts.size());
                 if (int st = fec_sdswdf_relay_batch_starts(c.sd, c.d_cw.as<uint8_t>(), c.CW, c.h_er1.data(), R,
@@ -374,6 +371,15 @@ int fec_relay_vr_run(fec_relay_vr* r, const uint8_t* d_payload, const uint8_t* h
         a.out_stride = r->ostride;
         hipLaunchKernelGGL(fec::fec_relay_vr_gather_kernel, dim3(fec::grid_rows(r->P)), dim3(256), 0, s, a);
         if (hipGetLastError() != hipSuccess) return FEC_ERR_HIP;
+        if (r->type == 2)  // the destinations' flags, after every code's launches (a copy to pageable
+                           // memory returns only when the stream has reached it)
+            for (auto& cp : r->codes) {
+                fec::Code& c = *cp;
+                c.h_flag.resize(static_cast<size_t>(c.R));
+                if (hipMemcpyAsync(c.h_flag.data(), c.d_flag.p, static_cast<size_t>(c.R), hipMemcpyDeviceToHost, s) !=
+                    hipSuccess)
+                    return FEC_ERR_HIP;
+            }
         if (hipStreamSynchronize(s) != hipSuccess) return FEC_ERR_HIP;
         if (h_flag)
             for (int64_t t = 0; t < r->P; ++t) {
