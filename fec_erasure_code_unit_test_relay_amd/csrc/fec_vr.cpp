@@ -1260,9 +1260,15 @@ struct fec_vr_plan {
     const int64_t* d_np0 = nullptr;  // [n_np0][8]: segments of the instances of tuples with n = k
     int n_np0 = 0;
     bool enc_ready = false, dec_ready = false, hdr_ready = false;
+    bool geo_ready = false;  // d_geo / d_tdesc written for this plan (they depend on the plan alone)
+    hipEvent_t geo_done = nullptr;  // after that launch: every later copy's stream waits on it
     Fork fork;  // side streams (declared after the uploads: destroyed, and drained, first)
 
     ~fec_vr_plan() {
+        if (geo_done) {
+            (void)hipEventSynchronize(geo_done);
+            (void)hipEventDestroy(geo_done);
+        }
         if (pk_sent) {
             (void)hipEventSynchronize(pk_sent);
             (void)hipEventDestroy(pk_sent);
@@ -1623,7 +1629,7 @@ void fec_vr_plan::run(int max_payload, int T, int B, int N, bool mds, const uint
         cur_bytes += (cend - e.first) * cwp;
         old_bytes += (e.end - cend) * cwp;
     }
-    enc_ready = dec_ready = hdr_ready = rowoff_ready = false;
+    enc_ready = dec_ready = hdr_ready = rowoff_ready = geo_ready = false;
 }
 
 namespace {
@@ -1870,6 +1876,14 @@ int fec_vr_decode_batch(fec_vr_plan* v, const uint8_t* d_cw_cur, const uint8_t* 
     ForkScope scope(v->fork);
     hipStream_t sr;
     if (int st = v->fork.stream(p.rec_x.empty() ? 0 : 1, &sr)) return st;
+    if (!v->geo_ready) {
+        if (!v->geo_done && hipEventCreateWithFlags(&v->geo_done, hipEventDisableTiming) != hipSuccess) return FEC_ERR_HIP;
+        if (int st = fec::vr_launch_geo(ca, hip_stream)) return st;
+        if (hipEventRecord(v->geo_done, s) != hipSuccess) return FEC_ERR_HIP;
+        v->geo_ready = true;
+    } else if (hipStreamWaitEvent(s, v->geo_done, 0) != hipSuccess) {  // a decode on another stream
+        return FEC_ERR_HIP;
+    }
     if (int st = fec::vr_launch_copy(ca, hip_stream)) return st;
     fec::VrRecArgs ra{d_cw_cur, d_cw_old, cur_off(v), old_off(v), p.sent, v->d_rec_x, v->d_rec_dec, v->d_rec_coef,
                       static_cast<int>(p.rec_x.size()), v->d_inst, v->d_inst_switch, v->d_gf, p.L, d_out, d_out_len};

@@ -328,6 +328,9 @@ int vr_launch_encode(const VrEncodeArgs& a, void* s);
 // The same in closed form, a workgroup per codeword (no LDS ring; the instance list's few codewords
 // beside the tile encoder)
 int vr_launch_encode_cf(const VrEncodeArgs& a, void* s);
+// The per-packet geometry words and tile descriptors of a plan (fec_vr_geo_kernel): once per plan,
+// in front of its first copy.
+int vr_launch_geo(const VrCopyArgs& a, void* s);
 int vr_launch_copy(const VrCopyArgs& a, void* s);
 int vr_launch_recover(const VrRecArgs& a, void* s);
 

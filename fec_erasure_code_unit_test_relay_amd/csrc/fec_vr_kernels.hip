@@ -1055,10 +1055,14 @@ int vr_launch_encode_cf(const VrEncodeArgs& a, void* s) {
     hipLaunchKernelGGL(fec_vr_encode_cf_kernel, dim3(grid), dim3(256), lds, static_cast<hipStream_t>(s), a);
     return hipGetLastError() == hipSuccess ? FEC_OK : FEC_ERR_HIP;
 }
-int vr_launch_copy(const VrCopyArgs& a, void* s) {
+int vr_launch_geo(const VrCopyArgs& a, void* s) {
     if (a.P <= 0) return FEC_OK;
     hipLaunchKernelGGL(fec_vr_geo_kernel, dim3(static_cast<unsigned>((a.P + 255) / 256)), dim3(256), 0,
                        static_cast<hipStream_t>(s), a);
+    return hipGetLastError() == hipSuccess ? FEC_OK : FEC_ERR_HIP;
+}
+int vr_launch_copy(const VrCopyArgs& a, void* s) {
+    if (a.P <= 0) return FEC_OK;
     const int64_t grid = (a.P + kVrCopyTP - 1) / kVrCopyTP;
     const size_t otile = static_cast<size_t>(kVrCopyTP) * (a.L + kVrCopyOrs);
     const char* fv = std::getenv("FEC_VR_COPY_FAST");  // (an A/B switch, read per launch)
