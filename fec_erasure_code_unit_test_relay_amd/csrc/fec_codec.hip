@@ -547,14 +547,23 @@ int launch_copy(fec_codec* c, const uint8_t* d_cw, const uint8_t* d_er, int64_t 
         // padded staging made the step 2.2 % slower in the same process, 0.3228 vs 0.3157 ms:
         // profiles/r03/r03v_copy_row_pad_*.txt.  2-way conflicts cost one LDS cycle per 32-lane
         // group; the copy is bound by its HBM traffic and load latency, not by the LDS.)
-        const int64_t blocks = (Pout + fa.TP - 1) / fa.TP;
+        // two tiles per workgroup (FEC_COPY_PAIR=1): the stage of one tile must fit the registers
+        // two tiles per workgroup, the second one's loads in flight while the first is converted:
+        // 0.3055 vs 0.3126 ms per step, copy 143.6 vs 151.5 us in the step
+        // (profiles/r05/headline/r05zu_copy_pair_ab.txt); FEC_COPY_PAIR=0: one tile per workgroup
+        const char* pv = std::getenv("FEC_COPY_PAIR");
+        const bool pair = !(pv && pv[0] == '0');
+        const void* pk = (pair && fa.nt && 16 + fa.TP * g.CW + 16 <= 6 * 16 * 256)
+                             ? fec::fec_copy_pair_kernel_for(g.k, g.n - g.k) : nullptr;
+        const int64_t tiles = (Pout + fa.TP - 1) / fa.TP;
+        const int64_t blocks = pk ? (tiles + 1) / 2 : tiles;
         // 256 threads (one per (packet, group) item of the tile rounded up to waves, 320 at (10,3,3),
         // measured slower in the step: 0.3402 vs 0.3235 ms, profiles/r03/r03y_copy_threads_ab.txt)
         const int nthr = 256;
         hipEvent_t stop;
         if (int st = c->begin(FEC_KERNEL_DEC_COPY, s, &stop)) return st;
         void* args[] = {&fa};
-        HIP_TRY(hipLaunchKernel(c->copy_fast, dim3(static_cast<unsigned>(blocks)), dim3(nthr), args,
+        HIP_TRY(hipLaunchKernel(pk ? pk : c->copy_fast, dim3(static_cast<unsigned>(blocks)), dim3(nthr), args,
                                 c->copyf_lds(fa.TP), s));
         return c->end(stop, s);
     }

@@ -177,6 +177,9 @@ struct CopyFastArgs {
 
 // fec_copy_fast_kernel<k, n-k> for the instantiated pairs (fec_copy_fast.hip), else nullptr.
 const void* fec_copy_fast_kernel_for(int k, int np);
+// Two consecutive tiles per workgroup, the second one's loads in flight while the first is
+// converted (same arguments and LDS as fec_copy_fast_kernel; stage <= kPairQ * 4 KB), or nullptr.
+const void* fec_copy_pair_kernel_for(int k, int np);
 // Specialised planner for (k, n-k), or nullptr (then fec_plan_kernel runs); its rule table is
 // the log-form copy (coefficient bytes log2, 0 -> 0xff).
 const void* fec_plan_fast_kernel_for(int k, int np);

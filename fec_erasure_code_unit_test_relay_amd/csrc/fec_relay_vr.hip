@@ -137,6 +137,7 @@ struct Code {
     fec_sdswdf* sd = nullptr;
     DevBuf d_src, d_pay, d_len, d_cw, d_cwlen, d_er1, d_er2, d_frames, d_out, d_flag, d_work;
     std::vector<uint8_t> h_er1, h_er2, h_flag;
+    bool src_up = false;
     Code() = default;
     Code(const Code&) = delete;
     Code& operator=(const Code&) = delete;
@@ -305,8 +306,12 @@ int fec_relay_vr_run(fec_relay_vr* r, const uint8_t* d_payload, const uint8_t* h
             if (int st = c.d_cwlen.reserve(static_cast<size_t>(R) * 4)) return st;
             if (int st = c.d_frames.reserve(static_cast<size_t>(R) * c.F)) return st;
             if (int st = c.d_out.reserve(static_cast<size_t>(R) * c.ostride)) return st;
-            if (hipMemcpyAsync(c.d_src.p, c.src.data(), static_cast<size_t>(R) * 8, hipMemcpyHostToDevice, s) != hipSuccess)
-                return FEC_ERR_HIP;
+            if (!c.src_up) {  // the row map depends on the schedule alone: uploaded once
+                if (hipMemcpyAsync(c.d_src.p, c.src.data(), static_cast<size_t>(R) * 8, hipMemcpyHostToDevice, s) !=
+                    hipSuccess)
+                    return FEC_ERR_HIP;
+                c.src_up = true;
+            }
             hipLaunchKernelGGL(fec::fec_relay_vr_payload_kernel, dim3(fec::grid_rows(R)), dim3(256), 0, s, d_payload, L,
                                c.d_src.as<const int64_t>(), R, c.d_pay.as<uint8_t>(), c.d_len.as<int32_t>());
             if (hipGetLastError() != hipSuccess) return FEC_ERR_HIP;
