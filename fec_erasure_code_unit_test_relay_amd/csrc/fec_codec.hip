@@ -363,7 +363,11 @@ int launch_encode_tile(fec_codec* c, const uint8_t* d_payload, const int32_t* d_
     a.cur_rows = a.old_rows = nullptr;
     a.cur_len = a.old_len = nullptr;
     a.W = 0;
-    a.nt = 0;  // bit 0: non-temporal codeword stores, bit 1: non-temporal payload loads
+    // bit 0: non-temporal codeword stores, bit 1: non-temporal payload loads.  Default 2: the
+    // payload rows are read once; 0.2983 - 0.3015 vs 0.3058 - 0.3088 ms per step, encoder 141 - 143
+    // vs 145 us (three alternations in one process, profiles/r05/headline/r05zz_tile_nt_ab.txt);
+    // non-temporal codeword stores (bit 0) slow the encoder to 170 - 177 us (the copy reads them next)
+    a.nt = 2;
     if (const char* v = std::getenv("FEC_TILE_NT")) a.nt = std::atoi(v) & 3;
     const int64_t blocks = (ntiles + tpw - 1) / tpw;
     hipEvent_t stop;

@@ -704,6 +704,7 @@ __device__ __forceinline__ void tile_multi_case(const EncMultiArgs& m, int ti, u
     a.cur_len = m.cur_len;
     a.old_len = m.old_len;
     a.W = (CG.CW + 15) & ~15;
+    a.nt = m.nt;
     switch (__builtin_amdgcn_readfirstlane(threadIdx.x >> 6)) {
         case 0: tile_walk<K, NP, 0, 300, true>(a, smem); break;
         case 1: tile_walk<K, NP, 1, 300, true>(a, smem); break;

@@ -157,6 +157,7 @@ struct EncMultiArgs {
     int tkey[kEncMultiMax];       // k * 32 + (n - k)
     int tfirst[kEncMultiMax + 1];
     int toff[kEncMultiMax];       // dword offset of the tuple's tables in gtab
+    int nt;                       // EncTileArgs::nt for every walk (bit 1: non-temporal payload loads)
 };
 bool fec_encode_tile_multi_supports(int k, int np, int L);
 const void* fec_encode_tile_multi_kernel_ptr();

@@ -1527,6 +1527,8 @@ int launch_tile_multi(const fec_vr_plan* v, const uint8_t* d_payload, const int3
     m.old_len = d_len_old;
     m.L = v->plan.L;
     m.ntuple = v->n_multi;
+    m.nt = 0;  // (A/B switch FEC_VR_TILE_NT, as the one-stream encoder's FEC_TILE_NT)
+    if (const char* e = std::getenv("FEC_VR_TILE_NT")) m.nt = std::atoi(e) & 2;
     int nwg = 0;
     for (int i = 0; i < v->n_multi; ++i) {
         const auto& t = v->tiles[static_cast<size_t>(i)];
