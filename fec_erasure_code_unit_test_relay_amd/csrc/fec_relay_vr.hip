@@ -152,8 +152,21 @@ struct Code {
 }  // namespace fec
 
 struct fec_relay_vr {
+    static constexpr int kStreams = 4;  // the codes' chains run side by side, round robin
     int type = 2, L = 0;
     int64_t P = 0;
+    hipStream_t st[kStreams] = {};
+    hipEvent_t ev_fork = nullptr, ev_join[kStreams] = {};
+    ~fec_relay_vr() {
+        for (int i = 0; i < kStreams; ++i) {
+            if (st[i]) {
+                (void)hipStreamSynchronize(st[i]);
+                (void)hipStreamDestroy(st[i]);
+            }
+            if (ev_join[i]) (void)hipEventDestroy(ev_join[i]);
+        }
+        if (ev_fork) (void)hipEventDestroy(ev_fork);
+    }
     std::vector<std::unique_ptr<fec::Code>> codes;
     std::vector<int32_t> map;   // [P][6]
     int fstride = 0, ostride = 0;
@@ -286,11 +299,23 @@ int fec_relay_vr_geometry(const fec_relay_vr* r, int* frame_stride, int* out_str
 int fec_relay_vr_run(fec_relay_vr* r, const uint8_t* d_payload, const uint8_t* h_e1, const uint8_t* h_e2,
                      uint8_t* d_frames, int32_t* d_frame_len, uint8_t* d_out, uint8_t* h_flag, void* hip_stream) {
     if (!r || !d_payload || !h_e1 || !h_e2 || !d_frames || !d_frame_len || !d_out) return FEC_ERR_ARG;
-    hipStream_t s = static_cast<hipStream_t>(hip_stream);
+    hipStream_t caller = static_cast<hipStream_t>(hip_stream);
     try {
         const int L = r->L;
-        for (auto& cp : r->codes) {
-            fec::Code& c = *cp;
+        if (!r->ev_fork) {
+            if (hipEventCreateWithFlags(&r->ev_fork, hipEventDisableTiming) != hipSuccess) return FEC_ERR_HIP;
+            for (int i = 0; i < fec_relay_vr::kStreams; ++i)
+                if (hipStreamCreateWithFlags(&r->st[i], hipStreamNonBlocking) != hipSuccess ||
+                    hipEventCreateWithFlags(&r->ev_join[i], hipEventDisableTiming) != hipSuccess)
+                    return FEC_ERR_HIP;
+        }
+        if (hipEventRecord(r->ev_fork, caller) != hipSuccess) return FEC_ERR_HIP;
+        const int nst = std::min<int>(fec_relay_vr::kStreams, static_cast<int>(r->codes.size()));
+        for (int i = 0; i < nst; ++i)
+            if (hipStreamWaitEvent(r->st[i], r->ev_fork, 0) != hipSuccess) return FEC_ERR_HIP;
+        for (size_t ci = 0; ci < r->codes.size(); ++ci) {
+            fec::Code& c = *r->codes[ci];
+            hipStream_t s = r->st[ci % fec_relay_vr::kStreams];
             const int64_t R = c.R;
             c.h_er1.resize(static_cast<size_t>(R));
             c.h_er2.resize(static_cast<size_t>(R));
@@ -355,6 +380,10 @@ int fec_relay_vr_run(fec_relay_vr* r, const uint8_t* d_payload, const uint8_t* h
                     return st;
             }
         }
+        hipStream_t s = caller;
+        for (int i = 0; i < nst; ++i)
+            if (hipEventRecord(r->ev_join[i], r->st[i]) != hipSuccess || hipStreamWaitEvent(s, r->ev_join[i], 0) != hipSuccess)
+                return FEC_ERR_HIP;
         if (!r->map_up) {
             if (int st = r->d_map.reserve(r->map.size() * 4)) return st;
             if (hipMemcpyAsync(r->d_map.p, r->map.data(), r->map.size() * 4, hipMemcpyHostToDevice, s) != hipSuccess)
