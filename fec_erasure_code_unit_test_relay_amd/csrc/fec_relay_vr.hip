@@ -26,6 +26,7 @@
 #include <map>
 #include <memory>
 #include <new>
+#include <thread>
 #include <vector>
 
 #include "fec_amd.h"
@@ -152,7 +153,7 @@ struct Code {
 }  // namespace fec
 
 struct fec_relay_vr {
-    static constexpr int kStreams = 4;  // the codes' chains run side by side, round robin
+    static constexpr int kStreams = fec::kMaxCodes;  // a stream per code: the codes' chains run side by side
     int type = 2, L = 0;
     int64_t P = 0;
     hipStream_t st[kStreams] = {};
@@ -313,9 +314,11 @@ int fec_relay_vr_run(fec_relay_vr* r, const uint8_t* d_payload, const uint8_t* h
         const int nst = std::min<int>(fec_relay_vr::kStreams, static_cast<int>(r->codes.size()));
         for (int i = 0; i < nst; ++i)
             if (hipStreamWaitEvent(r->st[i], r->ev_fork, 0) != hipSuccess) return FEC_ERR_HIP;
-        for (size_t ci = 0; ci < r->codes.size(); ++ci) {
+        // one code's chain on its own stream; type 3's host planners make its batches synchronous,
+        // so its codes run on threads of their own (each code has its own planner objects)
+        auto run_code = [&](size_t ci) -> int {
             fec::Code& c = *r->codes[ci];
-            hipStream_t s = r->st[ci % fec_relay_vr::kStreams];
+            hipStream_t s = r->st[ci];
             const int64_t R = c.R;
             c.h_er1.resize(static_cast<size_t>(R));
             c.h_er2.resize(static_cast<size_t>(R));
@@ -379,6 +382,27 @@ int fec_relay_vr_run(fec_relay_vr* r, const uint8_t* d_payload, const uint8_t* h
                                                                  c.h_flag.data(), s))
                     return st;
             }
+            return static_cast<int>(FEC_OK);
+        };
+        if (r->type == 2) {
+            for (size_t ci = 0; ci < r->codes.size(); ++ci)
+                if (int st = run_code(ci)) return st;
+        } else {
+            std::vector<int> status(r->codes.size(), FEC_OK);
+            std::vector<std::thread> th;
+            for (size_t ci = 0; ci < r->codes.size(); ++ci)
+                th.emplace_back([&, ci] {
+                    try {
+                        status[ci] = run_code(ci);
+                    } catch (const std::bad_alloc&) {
+                        status[ci] = FEC_ERR_NOMEM;
+                    } catch (...) {
+                        status[ci] = FEC_ERR_ARG;
+                    }
+                });
+            for (auto& t : th) t.join();
+            for (int st : status)
+                if (st) return st;
         }
         hipStream_t s = caller;
         for (int i = 0; i < nst; ++i)
