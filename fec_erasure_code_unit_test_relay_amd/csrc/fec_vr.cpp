@@ -1780,7 +1780,12 @@ int fec_vr_encode_batch(fec_vr_plan* v, const uint8_t* d_payload, const int32_t*
     if (int st = v->fork.begin(s)) return st;
     ForkScope scope(v->fork);
     int next_side = n_multi > 0 ? 1 : 0;  // stream index 0 = the caller's
-    if (gen) {
+    // the closed-form leftovers after the multi-tuple launch on the caller's stream (beside it on a
+    // side stream they took its CUs: encode 0.128 - 0.129 vs 0.126 ms, profiles/r05/vr/r05zzc_*;
+    // FEC_VR_GEN_AFTER=0 puts them beside it)
+    const char* ga = std::getenv("FEC_VR_GEN_AFTER");
+    const bool gen_after = gen && tiled && n_multi > 0 && !(ga && ga[0] == '0');
+    if (gen && !gen_after) {
         hipStream_t sg;
         if (int st = v->fork.stream(next_side++, &sg)) return st;
         fec::VrEncodeArgs a{d_payload, d_payload_len, v->plan.L,
@@ -1805,6 +1810,12 @@ int fec_vr_encode_batch(fec_vr_plan* v, const uint8_t* d_payload, const int32_t*
     }
     if (n_multi > 0)
         if (int st = launch_tile_multi(v, d_payload, d_payload_len, d_cw_cur, d_len_cur, d_cw_old, d_len_old, s)) return st;
+    if (gen_after) {
+        fec::VrEncodeArgs a{d_payload, d_payload_len, v->plan.L, v->d_lo_inst, v->d_lo_span, v->d_lo_cum, v->n_lo,
+                            v->lo_total, v->enc_tab, v->enc_out, v->enc_slot, v->enc_wave, v->d_gtab, v->d_lo_base,
+                            d_cw_cur, d_cw_old, d_len_cur, d_len_old, v->enc_nmax};
+        if (int st = fec::vr_launch_encode_cf(a, s)) return st;
+    }
     for (int i = 0; i < n_side_tiles; ++i) {
         hipStream_t st_i;
         if (int st = v->fork.stream(next_side++, &st_i)) return st;  // side streams round robin
