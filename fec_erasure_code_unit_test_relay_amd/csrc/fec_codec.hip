@@ -1021,7 +1021,13 @@ int fec_codec_info(const fec_codec* c, char* buf, size_t size) {
     else
         std::snprintf(enc, sizeof(enc), "fec_encode_kernel");
     char cpy[64];
-    if (c->copy_fast && c->copy_path != 1)
+    const char* pv = std::getenv("FEC_COPY_PAIR");
+    const char* ntv = std::getenv("FEC_COPY_NT");
+    const bool pair = !(pv && pv[0] == '0') && !(ntv && !std::atoi(ntv)) &&
+                      16 + c->copyf_tp * c->g.CW + 16 <= 6 * 16 * 256 && fec::fec_copy_pair_kernel_for(c->g.k, np);
+    if (c->copy_fast && c->copy_path != 1 && pair)
+        std::snprintf(cpy, sizeof(cpy), "fec_copy_pair_kernel<%d, %d>", c->g.k, np);
+    else if (c->copy_fast && c->copy_path != 1)
         std::snprintf(cpy, sizeof(cpy), "fec_copy_fast_kernel<%d, %d>", c->g.k, np);
     else
         std::snprintf(cpy, sizeof(cpy), "fec_copy_kernel");

@@ -583,7 +583,14 @@ struct FastGeo {
     static constexpr int LDS = OFF_RAW + RAWB;
     static constexpr uint32_t MDIV = static_cast<uint32_t>((uint64_t(1) << 32) / OUT_ROW + 1);
     static constexpr uint32_t MSTRIDE = static_cast<uint32_t>((uint64_t(1) << 32) / STRIDE + 1);
+    // the H rows in front of a tile that is not a workgroup's first are the last H rows of the tile
+    // before: the slab's first NH 16-byte chunks (its rows start at byte DLT of chunk 0, and row H
+    // at a chunk boundary: t0 * STRIDE is a multiple of 16) are carried over in registers
+    static constexpr int DLT = (16 - (H * STRIDE) % 16) % 16;
+    static constexpr int NH = (DLT + H * STRIDE) / 16;
+    static constexpr int HQ = (NH + kFT - 1) / kFT;
     static_assert(H <= 64 && D0 + kFR <= kFR + 64, "rows in front of a tile");
+    static_assert((DLT + H * STRIDE) % 16 == 0, "carried rows");
 };
 
 struct SwFastArgs {
@@ -598,6 +605,7 @@ struct SwFastArgs {
     int64_t ntiles;
     int tiles_per_wg;
     uint64_t* stamps;       // diagnostics (FEC_SWDF_STAMPS): per workgroup, cycles per phase summed over tiles
+    int carry;              // carry the rows in front of a tile over from the tile before (FEC_SWDF_CARRY=0: reload)
 };
 
 // Phase clock for the diagnostics: cycles between consecutive marks, summed over the tiles.
@@ -636,7 +644,10 @@ struct FastTile {
     uint16_t* glog16;
     uint32_t* pmask;
     uint16_t* rl;
+    static constexpr int NH = GM::NH, HQ = GM::HQ;
     uint4 v[QCH];
+    uint4 hc[HQ];                   // the next tile's first NH chunks (keep())
+    bool carry = false, carry_next = false;
     uint32_t f0 = 0, f1 = 0;        // flags of local rows lane and 64 + lane (next tile)
     uint64_t fb0 = 0, fb1 = 0;      // flags of local rows 0..63, 64..127 (this tile)
     int dlt = 0, dlt_next = 0;      // LDS byte of local row 0 = raw + dlt
@@ -654,8 +665,10 @@ struct FastTile {
         for (int i = tid; i < 1040; i += kFT) gexp[i] = i < 510 ? a.gf[i] : 0;
         for (int i = tid; i < 256; i += kFT) glog16[i] = i ? a.gf[512 + i] : 512;
     }
-    // the slab of rows [r0, t0+nt) (r0 = t0 - H) and the tile's flags, into registers
-    __device__ void issue(int64_t tile) {
+    // the slab of rows [r0, t0+nt) (r0 = t0 - H) and the tile's flags, into registers; with cont
+    // (the tile follows this workgroup's previous one) its first NH chunks come from keep() instead
+    __device__ void issue(int64_t tile, bool cont) {
+        carry_next = cont;
         const int64_t t0 = tile * kFR, r0 = t0 - H;
         const int nt = static_cast<int>(min<int64_t>(kFR, a.P - t0));
         const int64_t g0 = r0 * STRIDE;                         // may be negative
@@ -669,7 +682,7 @@ struct FastTile {
         for (int q = 0; q < QCH; ++q) {
             const int c = tid + q * kFT;
             const int64_t o = A - base + 16 * static_cast<int64_t>(c);  // < 0: a row before packet 0
-            const uint32_t off = (c < nch && o >= 0) ? static_cast<uint32_t>(o) : 0x7ffffff0u;
+            const uint32_t off = (c < nch && o >= 0 && !(cont && c < NH)) ? static_cast<uint32_t>(o) : 0x7ffffff0u;
             const auto x = __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0);
             v[q] = make_uint4(x[0], x[1], x[2], x[3]);
         }
@@ -680,6 +693,16 @@ struct FastTile {
         f1 = __builtin_amdgcn_raw_buffer_load_b8(re, (64 + lane < ROWS && rb >= 0) ? static_cast<uint32_t>(rb) : 0x7ffffff0u, 0, 0);
         dlt_next = static_cast<int>(g0 - A);
     }
+    // after the decode (the rows are final): the last H rows of this (full) tile, which the next
+    // tile of the workgroup starts with, into registers -- chunk c of the next slab is chunk
+    // kFR * STRIDE / 16 + c of this one
+    __device__ void keep() {
+#pragma unroll
+        for (int q = 0; q < HQ; ++q) {
+            const int c = tid + q * kFT;
+            if (c < NH) hc[q] = *reinterpret_cast<const uint4*>(smem + GM::OFF_RAW + kFR * STRIDE + 16 * c);
+        }
+    }
     __device__ uint32_t rowb(int l) const { return static_cast<uint32_t>(GM::OFF_RAW + dlt + l * STRIDE); }
     __device__ bool erased(int l) const { return ((l < 64 ? fb0 >> l : fb1 >> (l - 64)) & 1u) != 0; }
     // the slab into LDS, the bytes of erased rows zeroed
@@ -687,12 +710,14 @@ struct FastTile {
         fb0 = __ballot(f0 != 0);
         fb1 = __ballot(f1 != 0);
         dlt = dlt_next;
+        carry = carry_next;
         const bool any = (fb0 | fb1) != 0;
 #pragma unroll
         for (int q = 0; q < QCH; ++q) {
             const int c = tid + q * kFT;
             if (16 * c >= 16 + ROWS * STRIDE) continue;
             uint4 x = v[q];
+            if (q < HQ && carry && c < NH) x = hc[q < HQ ? q : 0];  // (masking them again is harmless)
             if (any) {
                 // chunk bytes [16c, 16c+16) = row bytes from (16c - dlt); at most two rows
                 const int o = 16 * c - dlt;
@@ -812,18 +837,19 @@ __global__ __launch_bounds__(kFT) void fec_sw_fast_dest_kernel(SwFastArgs a) {
     const int64_t tile0 = static_cast<int64_t>(blockIdx.x) * a.tiles_per_wg;
     const int64_t tile1 = min(tile0 + a.tiles_per_wg, a.ntiles);
     PhaseClock clk(a.stamps != nullptr);
-    if (tile0 < tile1) T.issue(tile0);
+    if (tile0 < tile1) T.issue(tile0, false);
     for (int64_t tile = tile0; tile < tile1; ++tile) {
         const int64_t t0 = tile * kFR;
         const int nt = static_cast<int>(min<int64_t>(kFR, a.P - t0));
         clk.mark(0);
         T.land();
         T.masks(t0, nt);
-        if (tile + 1 < tile1) T.issue(tile + 1);
+        if (tile + 1 < tile1) T.issue(tile + 1, a.carry != 0);
         __syncthreads();
         clk.mark(1);
         T.decode();
         __syncthreads();
+        if (a.carry && tile + 1 < tile1) T.keep();
         clk.mark(2);
         // output bytes of the tile's rows, 16 per lane: byte b -> row t = b / SK, o = b - t*SK,
         // j = o / K, i = o % K; LDS byte = row (t + K-1-i) of the slab, 4 + j*N + K-1-i.  A fixed
@@ -887,18 +913,19 @@ __global__ __launch_bounds__(kFT, 4) void fec_sw_fast_relay_kernel(SwFastArgs a)
     const int64_t tile0 = static_cast<int64_t>(blockIdx.x) * a.tiles_per_wg;
     const int64_t tile1 = min(tile0 + a.tiles_per_wg, a.ntiles);
     PhaseClock clk(a.stamps != nullptr);
-    if (tile0 < tile1) T.issue(tile0);
+    if (tile0 < tile1) T.issue(tile0, false);
     for (int64_t tile = tile0; tile < tile1; ++tile) {
         const int64_t t0 = tile * kFR;
         const int nt = static_cast<int>(min<int64_t>(kFR, a.P - t0));
         clk.mark(0);
         T.land();
         T.masks(t0, nt);
-        if (tile + 1 < tile1) T.issue(tile + 1);
+        if (tile + 1 < tile1) T.issue(tile + 1, a.carry != 0);
         __syncthreads();
         clk.mark(1);
         T.decode();
         __syncthreads();
+        if (a.carry && tile + 1 < tile1) T.keep();
         clk.mark(2);
         // CT[l][m][g] from the (decoded) rows: a lane per (row, group of 4 blocks); only the rows
         // a frame of the tile reads (local rows >= k-1)
@@ -1216,6 +1243,16 @@ bool fast_enabled() {
     return on;
 }
 
+// the specialised kernels carry a tile's front rows over from the workgroup's previous tile
+// (FEC_SWDF_CARRY=0: every tile reloads them from HBM)
+bool carry_enabled() {
+    static const bool on = [] {
+        const char* v = std::getenv("FEC_SWDF_CARRY");
+        return !(v && v[0] == '0');
+    }();
+    return on;
+}
+
 bool tiles_enabled() {
     static const bool on = [] {
         const char* v = std::getenv("FEC_SWDF_TILE");
@@ -1326,6 +1363,7 @@ int fec_swdf_relay_batch(fec_swdf* w, const uint8_t* d_cw, int64_t cw_stride, co
             if (hipMemcpy(w->d_tab, tab.data(), tab.size() * 4, hipMemcpyHostToDevice) != hipSuccess) return FEC_ERR_HIP;
         }
         fec::SwFastArgs a{};
+        a.carry = carry_enabled() ? 1 : 0;
         a.in = d_cw;
         a.er = d_erasure;
         a.P = P;
@@ -1392,6 +1430,7 @@ int fec_swdf_destination_batch(fec_swdf* w, const uint8_t* d_frames, const uint8
     // frame symbol (j, m) at byte 4 + j*n2 + m (size header + codeword_new_vector's offset 2)
     if (fast_enabled() && w->v2.wbase_n >= 0) {
         fec::SwFastArgs a{};
+        a.carry = carry_enabled() ? 1 : 0;
         a.in = d_frames;
         a.er = d_erasure;
         a.P = P;

@@ -9,6 +9,7 @@
 //       Variable_Rate_FEC_Decoder.cpp:1423-1600, :1772-1873).
 // Frames, destination outputs and loss flags must be equal per seq.
 #include <algorithm>
+#include <chrono>
 #include <cstdint>
 #include <cstdio>
 #include <cstdlib>
@@ -156,6 +157,16 @@ struct OracleSW {
     }
 };
 
+// --time mode: wall time per seq of each node's object calls, split into the slot shifts of
+// push_current_codeword / rotate_pointers_and_insert_zero_word and the GF call of the type
+struct CallClock {
+    double relay_shift = 0, relay_gf = 0, dest_shift = 0, dest_gf = 0;
+};
+CallClock g_clock;
+double now_us() {
+    return std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
 // A relayed code: the source's (n, k) on hop 1, the relay's (n2, k) on hop 2 (T2 = n2 - 1 <= T).
 struct Code {
     int k, n, n2, S, CW;
@@ -174,6 +185,7 @@ template <class SW>
 void relay_step(SW* w, int R, const Code& c, const unsigned char* cw, std::vector<unsigned char>& frame) {
     static std::vector<unsigned char> buf(SLOT);
     bool flag = false;
+    const double t0 = now_us();
     if (cw) {
         std::memset(buf.data(), 0, SLOT);
         std::memcpy(buf.data(), cw, c.CW);
@@ -189,8 +201,12 @@ void relay_step(SW* w, int R, const Code& c, const unsigned char* cw, std::vecto
             w->temp_erasure_vector_state_dependent[2 * TT] = true;
         }
     }
+    const double t1 = now_us();
     if (R == 3) w->symbol_wise_encode_state_dependent(c.k, c.n, c.k, c.n2, &flag);
     else w->symbol_wise_encode_1(c.k, c.n, c.k, c.n2, &flag);
+    const double t2 = now_us();
+    g_clock.relay_shift += t1 - t0;
+    g_clock.relay_gf += t2 - t1;
     if (R == 3)
         for (int a = 0; a < TT + 1; ++a) frame.push_back(static_cast<unsigned char>(w->header[c.n2 - 1][a]));
     const unsigned char* row = w->codeword_new_vector[c.n2 - 1];
@@ -203,6 +219,7 @@ template <class SW>
 int dest_step(SW* d, int R, const Code& c, const unsigned char* part, unsigned char* out) {
     static std::vector<unsigned char> buf(SLOT), buffer(30000);
     bool flag = false;
+    const double t0 = now_us();
     if (part) {
         const unsigned char* cw = part + (R == 3 ? TT + 1 : 0);
         std::memset(buf.data(), 0, SLOT);
@@ -221,8 +238,12 @@ int dest_step(SW* d, int R, const Code& c, const unsigned char* part, unsigned c
             d->temp_erasure_vector_state_dependent[3 * TT - 1] = true;
         }
     }
+    const double t1 = now_us();
     if (R == 3) d->symbol_wise_decode_state_dependent(buffer.data(), &flag, c.k, c.n2);
     else d->symbol_wise_decode_1(buffer.data(), &flag, c.k, c.n2);
+    const double t2 = now_us();
+    g_clock.dest_shift += t1 - t0;
+    g_clock.dest_gf += t2 - t1;
     d->extract_data(buffer.data(), c.k, c.n2, 0, out);
     return flag ? 1 : 0;
 }
@@ -496,10 +517,32 @@ int schedule_run(int argc, char** argv, bool compare_with_oracle) {
     return rc;
 }
 
+// --time P: the fixed-rate (10,3) chain over SW for P seqs, per type; prints microseconds per seq
+// of the relay's and the destination's object calls (slot shifts, GF call)
+template <class SW>
+void time_run(const char* what, int P) {
+    const auto e1 = pattern(P, 7, 30, 173), e2 = pattern(P, 11, 25, 211);
+    for (int R : {2, 3}) {
+        chain<SW>(R, {{0, 10, 3}}, -1, 64, e1, e2);  // warm-up: contexts, planners, device buffers
+        g_clock = CallClock{};
+        const double t0 = now_us();
+        chain<SW>(R, {{0, 10, 3}}, -1, P, e1, e2);
+        const double total = now_us() - t0;
+        std::printf("{\"class\": \"%s\", \"type\": %d, \"seqs\": %d, \"us_per_seq\": {\"relay_shift\": %.2f, "
+                    "\"relay_gf\": %.2f, \"dest_shift\": %.2f, \"dest_gf\": %.2f, \"chain\": %.2f}}\n",
+                    what, R, P, g_clock.relay_shift / P, g_clock.relay_gf / P, g_clock.dest_shift / P,
+                    g_clock.dest_gf / P, total / P);
+    }
+}
+
 #ifdef RELAY_ORACLE_ONLY
 // CPU build (tests/test_sdswdf.py): the driver over OracleSW against the oracle's chains, which
 // checks the driver and the or_sw_* methods without a GPU.
 int main(int argc, char** argv) {
+    if (argc > 2 && std::strcmp(argv[1], "--time") == 0) {
+        time_run<OracleSW>("oracle", std::atoi(argv[2]));
+        return 0;
+    }
     if (argc > 1 && std::strcmp(argv[1], "--schedule") == 0) {
         const int rc = schedule_run<OracleSW>(argc, argv, false);
         if (rc == 0) std::printf("RELAY ORACLE DRIVER OK\n");
@@ -523,6 +566,11 @@ int main(int argc, char** argv) {
 #else
 int main(int argc, char** argv) {
     using DSW = siphon::Decoder_Symbol_Wise;
+    if (argc > 2 && std::strcmp(argv[1], "--time") == 0) {
+        time_run<DSW>("dropin", std::atoi(argv[2]));
+        time_run<OracleSW>("oracle", std::atoi(argv[2]));
+        return 0;
+    }
     if (argc > 1 && std::strcmp(argv[1], "--schedule") == 0) {
         const int rc = schedule_run<DSW>(argc, argv, true);
         if (rc == 0) std::printf("RELAY DROPIN OK\n");

@@ -337,6 +337,38 @@ def test_gpu_relay_dropin_class_equals_oracle(tmp_path):
     assert "RELAY DROPIN OK" in r.stdout
 
 
+def _time_lines(out):
+    import json
+    rows = [json.loads(x) for x in out.splitlines() if x.startswith("{")]
+    for r in rows:
+        assert r["us_per_seq"]["chain"] > 0 and r["us_per_seq"]["relay_gf"] > 0, r
+    return rows
+
+
+def test_relay_driver_time_mode_over_oracle_methods(tmp_path):
+    """relay_dropin_test.cpp --time P (the per-call cost of the relay class: slot shifts and GF calls
+    per seq at the relay and the destination) runs over the oracle-method class on the CPU."""
+    import subprocess
+    exe = _build_relay_driver(tmp_path, oracle_only=True)
+    r = subprocess.run([exe, "--time", "300"], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert [(x["class"], x["type"]) for x in _time_lines(r.stdout)] == [("oracle", 2), ("oracle", 3)]
+
+
+@pytest.mark.gpu
+def test_gpu_relay_dropin_per_call_cost(tmp_path):
+    """The per-call cost of siphon::Decoder_Symbol_Wise (every GF call a device round trip) beside
+    the oracle-method class, per seq of a (10,3) relay chain; the lines are printed for the record
+    (profiles/r05/relay/r05_per_call_relay.txt)."""
+    import subprocess
+    exe = _build_relay_driver(tmp_path, oracle_only=False)
+    r = subprocess.run([exe, "--time", "3000"], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    rows = _time_lines(r.stdout)
+    assert [(x["class"], x["type"]) for x in rows] == [("dropin", 2), ("dropin", 3), ("oracle", 2), ("oracle", 3)]
+    print(r.stdout)
+
+
 def _vr_relay_schedule(tmp_path, P):
     """Switch points and codes of config 4's schedule on bin/erasure.bin (the plan's encoder
     instances: each starts at its first seq), hop-1 erasures from bin/erasure.bin and hop-2 ones
