@@ -332,8 +332,10 @@ __device__ __forceinline__ void tile_walk(const EncTileArgs& a, uint8_t* smem) {
     // parity rows start zeroed
     for (int x = tid; x < NPA * QJ; x += kTileThreads) q[x] = 0;
 
-    // tile 0 (in front of the first one) only feeds parity history: none to feed without parity
-    constexpr int it0 = NP > 0 ? 0 : 1;
+    // tile 0 (in front of the first one) only feeds parity history: none to feed without parity,
+    // nor in front of an instance's first tile (its rows read as zero: the parity rows' zeros)
+    // (a.nt bit 2, FEC_VR_HIST0=1: computed anyway, as before)
+    const int it0 = (NP == 0 || (SEG && seg_t0 == 0 && !(a.nt & 4))) ? 1 : 0;
     issue(it0);
     if (cnt >= it0 + 1) issue(it0 + 1);
 

@@ -64,7 +64,8 @@ struct EncTileArgs {
     int off_scratch;              // 1 KB: a dword per thread for writes that must land nowhere
     int dbg;                      // timing experiments only (FEC_TILE_DBG): 1 no parity products,
                                   // 2 no codeword words, 4 no output stores
-    int nt;                       // 1: codeword stores non-temporal (FEC_TILE_NT)
+    int nt;                       // 1: codeword stores non-temporal (FEC_TILE_NT); 2: payload loads non-temporal;
+                                  // 4: segment mode computes the zero history tile of an instance start
     // segment mode (variable-rate schedule, fec_vr.cpp): null for one stream.  Per workgroup 6
     // int64: first seq of the encoder instance (its row 0), its role-switch seq, its rows P,
     // t0 | cnt << 32 (tiles [t0, t0+cnt) of the instance), and the byte offsets of the instance's

@@ -1131,6 +1131,7 @@ struct Fork {
     hipStream_t st[kSide] = {};
     hipEvent_t ev_fork = nullptr, ev_join[kSide] = {};
     bool forked[kSide] = {};
+    bool marked = false;  // ev_fork recorded on the caller's stream for this batch
     hipStream_t caller = nullptr;
 
     Fork() = default;
@@ -1156,7 +1157,16 @@ struct Fork {
         }
         caller = s;
         for (bool& f : forked) f = false;
-        return hipEventRecord(ev_fork, s) == hipSuccess ? FEC_OK : FEC_ERR_HIP;
+        marked = false;
+        return FEC_OK;
+    }
+    // the fork point: recorded on the caller's stream at the first side stream's use (a batch
+    // without side work records nothing), or here, ahead of later caller-stream launches the side
+    // work must not wait for
+    int mark() {
+        if (marked) return FEC_OK;
+        marked = true;
+        return hipEventRecord(ev_fork, caller) == hipSuccess ? FEC_OK : FEC_ERR_HIP;
     }
     // launch slot i: 0 = the caller's stream, i > 0 = side stream (i - 1) % kSide
     int stream(int i, hipStream_t* out) {
@@ -1165,6 +1175,7 @@ struct Fork {
             return FEC_OK;
         }
         const int j = (i - 1) % kSide;
+        if (int st = mark()) return st;
         if (!forked[j]) {
             if (hipStreamWaitEvent(st[j], ev_fork, 0) != hipSuccess) return FEC_ERR_HIP;
             forked[j] = true;
@@ -1262,6 +1273,7 @@ struct fec_vr_plan {
     bool enc_ready = false, dec_ready = false, hdr_ready = false;
     bool geo_ready = false;  // d_geo / d_tdesc written for this plan (they depend on the plan alone)
     hipEvent_t geo_done = nullptr;  // after that launch: every later copy's stream waits on it
+    hipStream_t geo_stream = nullptr;  // the stream it ran on (its later copies need no wait)
     Fork fork;  // side streams (declared after the uploads: destroyed, and drained, first)
 
     ~fec_vr_plan() {
@@ -1529,6 +1541,8 @@ int launch_tile_multi(const fec_vr_plan* v, const uint8_t* d_payload, const int3
     m.ntuple = v->n_multi;
     m.nt = 0;  // (A/B switch FEC_VR_TILE_NT, as the one-stream encoder's FEC_TILE_NT)
     if (const char* e = std::getenv("FEC_VR_TILE_NT")) m.nt = std::atoi(e) & 2;
+    // an instance's first tile without the zero history tile in front of it (FEC_VR_HIST0=1: with)
+    if (const char* e = std::getenv("FEC_VR_HIST0")) m.nt |= std::atoi(e) ? 4 : 0;
     int nwg = 0;
     for (int i = 0; i < v->n_multi; ++i) {
         const auto& t = v->tiles[static_cast<size_t>(i)];
@@ -1779,6 +1793,8 @@ int fec_vr_encode_batch(fec_vr_plan* v, const uint8_t* d_payload, const int32_t*
     const bool gen = !tiled || v->n_lo > 0;
     if (int st = v->fork.begin(s)) return st;
     ForkScope scope(v->fork);
+    if (n_side_tiles > 0)  // (their launches follow the multi-tuple launch on the caller's stream)
+        if (int st = v->fork.mark()) return st;
     int next_side = n_multi > 0 ? 1 : 0;  // stream index 0 = the caller's
     // the closed-form leftovers after the multi-tuple launch on the caller's stream (beside it on a
     // side stream they took its CUs: encode 0.128 - 0.129 vs 0.126 ms, profiles/r05/vr/r05zzc_*;
@@ -1884,22 +1900,30 @@ int fec_vr_decode_batch(fec_vr_plan* v, const uint8_t* d_cw_cur, const uint8_t* 
     if (int st = ensure_rowoff(v, s)) return st;
     fec::VrCopyArgs ca{d_cw_cur, cur_off(v), v->d_pk_dec, v->d_inst, v->d_fate, v->d_slow, p.P, p.L, d_out,
                        d_out_len, v->d_geo, v->d_tdesc, v->cur_bytes};
-    // the recovery writes only the rows (and lengths) the copy leaves alone: side by side
-    if (int st = v->fork.begin(s)) return st;
-    ForkScope scope(v->fork);
-    hipStream_t sr;
-    if (int st = v->fork.stream(p.rec_x.empty() ? 0 : 1, &sr)) return st;
+    fec::VrRecArgs ra{d_cw_cur, d_cw_old, cur_off(v), old_off(v), p.sent, v->d_rec_x, v->d_rec_dec, v->d_rec_coef,
+                      static_cast<int>(p.rec_x.size()), v->d_inst, v->d_inst_switch, v->d_gf, p.L, d_out, d_out_len};
+    // the recovery writes only the rows (and lengths) the copy leaves alone: one launch holding both
+    // (FEC_VR_FUSED=0: the copy on the caller's stream, the recovery beside it on a side stream)
     if (!v->geo_ready) {
         if (!v->geo_done && hipEventCreateWithFlags(&v->geo_done, hipEventDisableTiming) != hipSuccess) return FEC_ERR_HIP;
         if (int st = fec::vr_launch_geo(ca, hip_stream)) return st;
         if (hipEventRecord(v->geo_done, s) != hipSuccess) return FEC_ERR_HIP;
         v->geo_ready = true;
-    } else if (hipStreamWaitEvent(s, v->geo_done, 0) != hipSuccess) {  // a decode on another stream
+        v->geo_stream = s;
+    } else if (s != v->geo_stream && hipStreamWaitEvent(s, v->geo_done, 0) != hipSuccess) {  // a decode on another stream
         return FEC_ERR_HIP;
     }
+    const char* fu = std::getenv("FEC_VR_FUSED");
+    if (!(fu && fu[0] == '0')) {
+        const int st = fec::vr_launch_decode(ca, ra, hip_stream);
+        if (st == FEC_OK) return v->dec_up.done_reading(s);
+        if (st != 1) return st;
+    }
+    if (int st = v->fork.begin(s)) return st;
+    ForkScope scope(v->fork);
+    hipStream_t sr;
+    if (int st = v->fork.stream(p.rec_x.empty() ? 0 : 1, &sr)) return st;
     if (int st = fec::vr_launch_copy(ca, hip_stream)) return st;
-    fec::VrRecArgs ra{d_cw_cur, d_cw_old, cur_off(v), old_off(v), p.sent, v->d_rec_x, v->d_rec_dec, v->d_rec_coef,
-                      static_cast<int>(p.rec_x.size()), v->d_inst, v->d_inst_switch, v->d_gf, p.L, d_out, d_out_len};
     if (int st = fec::vr_launch_recover(ra, sr)) return st;
     if (int st = scope.join()) return st;
     return v->dec_up.done_reading(s);

@@ -333,5 +333,8 @@ int vr_launch_encode_cf(const VrEncodeArgs& a, void* s);
 int vr_launch_geo(const VrCopyArgs& a, void* s);
 int vr_launch_copy(const VrCopyArgs& a, void* s);
 int vr_launch_recover(const VrRecArgs& a, void* s);
+// copy and recovery in one launch (fec_vr_decode_kernel); 1 = not applicable (no fast copy tiles,
+// or nothing to recover): launch the two instead
+int vr_launch_decode(const VrCopyArgs& a, const VrRecArgs& ra, void* s);
 
 }  // namespace fec

@@ -928,7 +928,7 @@ __global__ __launch_bounds__(256) void fec_vr_offsets_kernel(VrOffsetsArgs a) {
 // h%k) = XOR_q coef[i][q] * symbol q of packet x-i+q, read from the reporting decoder's input.
 // The k+n-1 input rows' addresses (cur before the decoder's role switch, old after; none outside
 // the frames) are resolved once per packet into LDS, so each symbol is one dependent load.
-__global__ __launch_bounds__(256) void fec_vr_recover_kernel(VrRecArgs a) {
+__device__ __forceinline__ void vr_recover_body(const VrRecArgs& a, int bid, int nblk) {
     __shared__ uint8_t gexp[512];
     __shared__ uint8_t glog[256];
     __shared__ uint8_t lcf[4][kVrCoefStride];
@@ -943,7 +943,7 @@ __global__ __launch_bounds__(256) void fec_vr_recover_kernel(VrRecArgs a) {
     uint8_t* lc = lcf[wl];
     const uint8_t** rp = rowp[wl];
     int32_t* rw = roww[wl];
-    for (int r = blockIdx.x * 4 + wl; r < a.nrec; r += gridDim.x * 4) {
+    for (int r = bid * 4 + wl; r < a.nrec; r += nblk * 4) {
         const int64_t x = a.rec_x[r];
         const int j = a.rec_dec[r];
         const int k = a.inst[4 * j], n = a.inst[4 * j + 1];
@@ -1008,6 +1008,37 @@ __global__ __launch_bounds__(256) void fec_vr_recover_kernel(VrRecArgs a) {
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     }
+}
+
+__global__ __launch_bounds__(256) void fec_vr_recover_kernel(VrRecArgs a) {
+    vr_recover_body(a, static_cast<int>(blockIdx.x), static_cast<int>(gridDim.x));
+}
+
+// The decode in one launch: workgroups [0, nrb) are the recovery's (fec_vr_recover_kernel's grid,
+// dispatched first so that its latency-bound waves start beside the copy), the others one copy
+// tile each (fec_vr_copy_fast_kernel).  The two write disjoint rows, so no order between them is
+// needed; one launch instead of a fork to a side stream and a join back saves their event waits.
+__global__ __launch_bounds__(256) void fec_vr_decode_kernel(VrCopyArgs a, VrRecArgs ra, int nrb) {
+    if (static_cast<int>(blockIdx.x) < nrb) {
+        vr_recover_body(ra, static_cast<int>(blockIdx.x), nrb);
+        return;
+    }
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    uint8_t* stage = smem;
+    uint8_t* xo = smem + kVrFastStage;
+    const int64_t tile = static_cast<int64_t>(blockIdx.x) - nrb;
+    const VrTileDesc* dp = reinterpret_cast<const VrTileDesc*>(a.tdesc) + tile;
+    VrTileDesc d;
+    d.o0 = static_cast<int64_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(dp->o0 & 0xffffffff)) & 0xffffffffu) |
+           static_cast<int64_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(dp->o0 >> 32))) << 32;
+    d.g1 = static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(dp->g1)));
+    d.g2 = static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(dp->g2)));
+    d.split = static_cast<uint16_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(dp->split)));
+    d.ok = static_cast<uint16_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(dp->ok)));
+    d.slow = static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(dp->slow)));
+    d.recv = static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(dp->recv)));
+    d.rec = static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(dp->rec)));
+    vr_copy_fast_tile(a, tile, d, stage, xo);
 }
 
 
@@ -1081,6 +1112,19 @@ int vr_launch_copy(const VrCopyArgs& a, void* s) {
     else
         hipLaunchKernelGGL(fec_vr_copy_gather_kernel, dim3(static_cast<unsigned>(grid)), dim3(256), 0,
                            static_cast<hipStream_t>(s), a);
+    return hipGetLastError() == hipSuccess ? FEC_OK : FEC_ERR_HIP;
+}
+int vr_launch_decode(const VrCopyArgs& a, const VrRecArgs& ra, void* s) {
+    const size_t otile = static_cast<size_t>(kVrCopyTP) * (a.L + kVrCopyOrs);
+    const size_t ofast = std::max(static_cast<size_t>(kVrFastTP) * a.L, otile);
+    const char* fv = std::getenv("FEC_VR_COPY_FAST");
+    if ((fv && fv[0] == '0') || !a.tdesc || (a.L & 3) != 0 || ofast > 32768 || a.P <= 0 || ra.nrec <= 0)
+        return 1;  // not this form: vr_launch_copy + vr_launch_recover
+    int nrb = 1024;  // the recovery's grid (as vr_launch_recover)
+    if (const char* e = std::getenv("FEC_VR_REC_BLOCKS")) nrb = std::max(1, std::atoi(e));
+    const int64_t g2 = (a.P + kVrFastTP - 1) / kVrFastTP;
+    hipLaunchKernelGGL(fec_vr_decode_kernel, dim3(static_cast<unsigned>(nrb + g2)), dim3(256), kVrFastStage + ofast,
+                       static_cast<hipStream_t>(s), a, ra, nrb);
     return hipGetLastError() == hipSuccess ? FEC_OK : FEC_ERR_HIP;
 }
 int vr_launch_offsets(const VrOffsetsArgs& a, void* s) {
