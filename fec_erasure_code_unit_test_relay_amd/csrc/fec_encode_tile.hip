@@ -32,6 +32,7 @@
 // workgroups per CU overlap one another's phases.
 #include "fec_device.h"
 #include "fec_kernels.h"
+#include "fec_vr_cf.h"
 
 #include <cstdlib>
 #include <utility>
@@ -700,7 +701,9 @@ __device__ __forceinline__ void tile_multi_case(const EncMultiArgs& m, int ti, u
     a.len_base = m.len;
     a.ptab = m.gtab + m.toff[ti];
     a.L = 300;
-    a.seg = m.seg;
+    // the walk reads segment blockIdx.x: with the leftovers' workgroups first, that is m.ncf past
+    // its segment in m.seg
+    a.seg = m.cf_first ? m.seg - 6 * static_cast<int64_t>(m.ncf) : m.seg;
     a.cur_rows = m.cur_rows;
     a.old_rows = m.old_rows;
     a.cur_len = m.cur_len;
@@ -715,9 +718,21 @@ __device__ __forceinline__ void tile_multi_case(const EncMultiArgs& m, int ti, u
     }
 }
 
-__global__ __launch_bounds__(kTileThreads, 4) void fec_encode_tile_multi_kernel(EncMultiArgs m) {
+// Workgroups past the segments' (m.ncf of them) encode the schedule's leftover codewords in closed
+// form (fec_vr_cf.h): they start as the segment walks drain and fill the launch's tail.
+__global__ __launch_bounds__(kTileThreads, 4) void fec_encode_tile_multi_kernel(EncMultiArgs m, VrEncodeArgs cf) {
     extern __shared__ __attribute__((aligned(16))) uint8_t tsmem[];
-    const int bid = static_cast<int>(blockIdx.x);
+    int bid = static_cast<int>(blockIdx.x);
+    if (m.cf_first) {  // (the leftovers' workgroups first instead)
+        if (bid < m.ncf) {
+            vr_encode_cf_body(cf, tsmem, bid, m.ncf);
+            return;
+        }
+        bid -= m.ncf;
+    } else if (bid >= m.tfirst[m.ntuple]) {
+        vr_encode_cf_body(cf, tsmem, bid - m.tfirst[m.ntuple], m.ncf);
+        return;
+    }
     int ti = 0;
     while (ti + 1 < m.ntuple && bid >= m.tfirst[ti + 1]) ++ti;
     switch (m.tkey[ti]) {

@@ -159,6 +159,9 @@ struct EncMultiArgs {
     int tfirst[kEncMultiMax + 1];
     int toff[kEncMultiMax];       // dword offset of the tuple's tables in gtab
     int nt;                       // EncTileArgs::nt for every walk (bit 1: non-temporal payload loads)
+    int ncf;                      // workgroups after the segments' running the closed-form leftovers
+                                  // (the kernel's second argument, VrEncodeArgs; 0: none)
+    int cf_first;                 // 1: those workgroups come first (FEC_VR_CF_FIRST=1)
 };
 bool fec_encode_tile_multi_supports(int k, int np, int L);
 const void* fec_encode_tile_multi_kernel_ptr();

@@ -1515,9 +1515,11 @@ int launch_tile_tuple(const fec_vr_plan* v, const fec_vr_plan::TileTuple& tt, co
 // The tuples tiles[0, n_multi) in one launch of fec_encode_tile_multi_kernel: workgroup b serves
 // segment b of d_seg.
 int launch_tile_multi(const fec_vr_plan* v, const uint8_t* d_payload, const int32_t* d_len, uint8_t* d_cw_cur,
-                      int32_t* d_len_cur, uint8_t* d_cw_old, int32_t* d_len_old, hipStream_t s) {
+                      int32_t* d_len_cur, uint8_t* d_cw_old, int32_t* d_len_old, const fec::VrEncodeArgs* cf,
+                      hipStream_t s) {
     const void* kfn = fec::fec_encode_tile_multi_kernel_ptr();
-    const int lds = d_len ? v->multi_lds_len : v->multi_lds;
+    int lds = d_len ? v->multi_lds_len : v->multi_lds;
+    if (cf) lds = std::max(lds, static_cast<int>(fec::vr_encode_cf_lds(*cf)));
     {
         static std::mutex mu;
         static int raised = 0;
@@ -1553,9 +1555,16 @@ int launch_tile_multi(const fec_vr_plan* v, const uint8_t* d_payload, const int3
         nwg += t.nseg;
     }
     m.tfirst[v->n_multi] = nwg;
-    if (nwg <= 0) return FEC_OK;
-    void* args[] = {&m};
-    return hipLaunchKernel(kfn, dim3(static_cast<unsigned>(nwg)), dim3(256), args, static_cast<size_t>(lds), s) ==
+    fec::VrEncodeArgs cfa{};
+    if (cf) {
+        cfa = *cf;
+        m.ncf = static_cast<int>(std::min<int64_t>(cf->cum_host_total, 16384));
+        const char* e = std::getenv("FEC_VR_CF_FIRST");
+        m.cf_first = e && e[0] == '1';
+    }
+    if (nwg + m.ncf <= 0) return FEC_OK;
+    void* args[] = {&m, &cfa};
+    return hipLaunchKernel(kfn, dim3(static_cast<unsigned>(nwg + m.ncf)), dim3(256), args, static_cast<size_t>(lds), s) ==
                    hipSuccess
                ? FEC_OK
                : FEC_ERR_HIP;
@@ -1824,14 +1833,20 @@ int fec_vr_encode_batch(fec_vr_plan* v, const uint8_t* d_payload, const int32_t*
         fec::VrNp0Args a0{d_payload, d_payload_len, v->plan.L, v->d_np0, v->n_np0, d_cw_cur, d_cw_old, d_len_cur, d_len_old};
         if (int st = fec::vr_launch_encode_np0(a0, s0)) return st;
     }
+    fec::VrEncodeArgs lo{d_payload, d_payload_len, v->plan.L, v->d_lo_inst, v->d_lo_span, v->d_lo_cum, v->n_lo,
+                         v->lo_total, v->enc_tab, v->enc_out, v->enc_slot, v->enc_wave, v->d_gtab, v->d_lo_base,
+                         d_cw_cur, d_cw_old, d_len_cur, d_len_old, v->enc_nmax};
+    // the closed-form leftovers inside the multi-tuple launch, in the workgroups after its segments'
+    // (FEC_VR_CF_FUSE=0: their own launch after it on the caller's stream)
+    const char* cfu = std::getenv("FEC_VR_CF_FUSE");
+    const bool cf_fuse = gen_after && !(cfu && cfu[0] == '0') && v->n_lo > 0 && v->lo_total > 0 &&
+                         fec::vr_encode_cf_lds(lo) <= 65536;
     if (n_multi > 0)
-        if (int st = launch_tile_multi(v, d_payload, d_payload_len, d_cw_cur, d_len_cur, d_cw_old, d_len_old, s)) return st;
-    if (gen_after) {
-        fec::VrEncodeArgs a{d_payload, d_payload_len, v->plan.L, v->d_lo_inst, v->d_lo_span, v->d_lo_cum, v->n_lo,
-                            v->lo_total, v->enc_tab, v->enc_out, v->enc_slot, v->enc_wave, v->d_gtab, v->d_lo_base,
-                            d_cw_cur, d_cw_old, d_len_cur, d_len_old, v->enc_nmax};
-        if (int st = fec::vr_launch_encode_cf(a, s)) return st;
-    }
+        if (int st = launch_tile_multi(v, d_payload, d_payload_len, d_cw_cur, d_len_cur, d_cw_old, d_len_old,
+                                       cf_fuse ? &lo : nullptr, s))
+            return st;
+    if (gen_after && !cf_fuse)
+        if (int st = fec::vr_launch_encode_cf(lo, s)) return st;
     for (int i = 0; i < n_side_tiles; ++i) {
         hipStream_t st_i;
         if (int st = v->fork.stream(next_side++, &st_i)) return st;  // side streams round robin

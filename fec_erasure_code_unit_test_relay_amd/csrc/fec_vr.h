@@ -336,5 +336,7 @@ int vr_launch_recover(const VrRecArgs& a, void* s);
 // copy and recovery in one launch (fec_vr_decode_kernel); 1 = not applicable (no fast copy tiles,
 // or nothing to recover): launch the two instead
 int vr_launch_decode(const VrCopyArgs& a, const VrRecArgs& ra, void* s);
+// dynamic LDS of the closed-form leftovers' workgroup (fec_vr_encode_cf_kernel, fec_vr_cf.h)
+size_t vr_encode_cf_lds(const VrEncodeArgs& a);
 
 }  // namespace fec
