@@ -430,8 +430,9 @@ def extra_configs(steps=5):
                 "feedback and the symbolic decoder instances on host threads) + its table "
                 "uploads + the device work (one encode launch over every encoder instance of "
                 "every (T,B,N), launched after the control loop so that it overlaps the symbolic "
-                "decoders; decode = one copy launch + one recovery launch over the plan's "
-                "coefficient rows); host_plan_ms = the plan alone, both phases waited for",
+                "decoders; decode = one launch holding the copy tiles and the recovery over the plan's "
+                "coefficient rows); host_plan_ms = the plan alone, both phases waited for; "
+                "device_only = encode + decode back to back, no plan",
         "verified": bool(torch.equal(out4[ok4], pl[:P][ok4])) and v.lost == 2982 and
         int((ol4 == 0).sum()) == 2982 and w.lost == 2982}
     res["multistream_10k"] = multistream(steps)
