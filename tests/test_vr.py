@@ -389,3 +389,43 @@ def test_gpu_adaptive_decode_copy_paths_agree(monkeypatch, L):
         keep = torch.arange(L, device="cuda")[None, :] < ln[:, None]
         assert bool(((out == payload[:P] * keep)[ok]).all())
     assert torch.equal(got["1"][0], got["0"][0]) and torch.equal(got["1"][1], got["0"][1])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("with_len", [False, True])
+def test_gpu_adaptive_launch_forms_agree(monkeypatch, with_len):
+    """Config 4's device work in its round-5 launch forms and their A/B switches gives identical
+    bytes: the closed-form leftovers inside the multi-tuple launch (last or first workgroups) or in
+    their own launch (FEC_VR_CF_FUSE=0), the history iteration at an instance's first tile skipped or
+    computed (FEC_VR_HIST0=1), and copy + recovery in one decode launch or forked (FEC_VR_FUSED=0):
+    the compact frame arrays, trimmed sizes and decoded outputs are equal to the defaults'."""
+    import torch
+    from fec_erasure_code_unit_test_relay_amd import fill_payload
+    torch.cuda.set_device(0)
+    pat = load_pattern("bin_erasure")
+    P = 60000
+    forms = [{}, {"FEC_VR_CF_FUSE": "0"}, {"FEC_VR_CF_FIRST": "1"}, {"FEC_VR_HIST0": "1"},
+             {"FEC_VR_FUSED": "0"}, {"FEC_VR_CF_FUSE": "0", "FEC_VR_FUSED": "0", "FEC_VR_HIST0": "1"}]
+    got = []
+    for env in forms:
+        for k in ("FEC_VR_CF_FUSE", "FEC_VR_CF_FIRST", "FEC_VR_HIST0", "FEC_VR_FUSED"):
+            monkeypatch.delenv(k, raising=False)
+        for k, val in env.items():
+            monkeypatch.setenv(k, val)
+        v = VrPlan(pat, P)
+        payload = fill_payload(0, v.sent, 300, 0x5EED)
+        lengths = None
+        if with_len:
+            lengths = torch.from_numpy(np.random.default_rng(5).integers(0, 301, v.sent).astype(np.int32)).cuda()
+        frames = v.alloc_frames(zero=True)
+        cw_cur, len_cur, cw_old, len_old = v.encode(payload, lengths=lengths, frames=frames)
+        out, out_len = v.decode(cw_cur, cw_old)
+        torch.cuda.synchronize()
+        got.append(tuple(t.clone() for t in (cw_cur, len_cur, cw_old, len_old, out, out_len)))
+        ok = torch.from_numpy(v.fate != 3).cuda()
+        ln = lengths[:P].long() if with_len else torch.full((P,), 300, device="cuda")
+        keep = torch.arange(300, device="cuda")[None, :] < ln[:, None]
+        assert bool(((out == payload[:P] * keep)[ok]).all()), env
+    for env, g in zip(forms[1:], got[1:]):
+        for a, b in zip(got[0], g):
+            assert torch.equal(a, b), env
