@@ -34,6 +34,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <memory>
+#include <utility>
 #include <vector>
 #include <new>
 
@@ -626,6 +627,15 @@ struct PhaseClock {
     }
 };
 
+template <typename F, int... Is>
+__device__ __forceinline__ void tfor_sw_impl(F&& f, std::integer_sequence<int, Is...>) {
+    (f(std::integral_constant<int, Is>{}), ...);
+}
+template <int N, typename F>
+__device__ __forceinline__ void tfor_sw(F&& f) {  // f(integral_constant<0..N-1>), unrolled
+    tfor_sw_impl(f, std::make_integer_sequence<int, N>{});
+}
+
 template <int NW>
 __device__ __forceinline__ void align_words(uint32_t (&d)[NW], int s) {  // d <- bytes from offset s
 #pragma unroll
@@ -863,7 +873,23 @@ __global__ __launch_bounds__(kFT) void fec_sw_fast_dest_kernel(SwFastArgs a) {
             const int c = T.tid + q * kFT;
             const uint32_t b = 16 * c;
             uint32_t val[4] = {0, 0, 0, 0};
-            if (static_cast<int>(b) < obytes) {
+            if constexpr (SK % 16 == 0 && 16 % K == 0) {
+                // a row's output is whole chunks and a chunk whole blocks (k = 8: two): byte (jb, i)
+                // of the chunk is at a compile-time offset from one address, (K-1-i) rows and jb
+                // blocks on -- 16 byte reads with immediate offsets, no per-byte index arithmetic
+                if (static_cast<int>(b) < obytes) {
+                    constexpr int CPR = SK / 16, BPC = 16 / K;
+                    const int t = static_cast<int>(b) / (16 * CPR);
+                    const int j0 = (static_cast<int>(b) / 16 - t * CPR) * BPC;
+                    const uint8_t* base = smem + T.rowb(t) + 4 + j0 * N;
+                    tfor_sw<16>([&](auto xc) __attribute__((always_inline)) {
+                        constexpr int x = decltype(xc)::value;
+                        constexpr int jb = x / K, i = x % K;
+                        const uint32_t byte = base[(K - 1 - i) * GM::STRIDE + jb * N + K - 1 - i];
+                        val[x >> 2] |= byte << (8 * (x & 3));
+                    });
+                }
+            } else if (static_cast<int>(b) < obytes) {
                 int t = static_cast<int>(b / SK);
                 const int o = static_cast<int>(b) - t * SK;
                 int j = o / K, i = o - j * K;
