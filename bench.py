@@ -887,6 +887,7 @@ def main():
     t0 = time.perf_counter()
     for _ in range(args.steps):
         run()
+    t_submit = time.perf_counter() - t0  # host time to enqueue the K steps (diagnostic)
     torch.cuda.synchronize()
     barrier()
     torch.cuda.synchronize()
@@ -980,6 +981,7 @@ def main():
                        "parallelism": f"streams{world} (one independent stream per GPU)"},
             "verified": bool(verified_all == world),
             "env": fec_env,
+            "host_submit_ms_per_step": round(t_submit / args.steps * 1e3, 4),
             "step_launch": ("hipGraph replay" if args.graph else "eager launches") +
                            ("; batch i's recovery beside batch i+1's encode (--pipeline)" if args.pipeline else ""),
             "device_warmup": {"seconds": args.warm_seconds, "untimed_steps": warm_steps,
