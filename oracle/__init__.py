@@ -76,8 +76,26 @@ def lib() -> ctypes.CDLL:
         L.or_vr_run.argtypes = [ctypes.c_int] * 5 + [u8p, ctypes.c_int64, ctypes.c_int64, ctypes.c_uint64, ip,
                                                       u8p, u8p, ctypes.c_int64, i64p, ctypes.c_int64,
                                                       i64p, ctypes.POINTER(ctypes.c_double)]
+        L.or_relay_session_run.restype = ctypes.c_int
+        L.or_relay_session_run.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int64, u8p, ctypes.c_int64, u8p,
+                                           ctypes.c_int64, ctypes.c_uint64, ctypes.POINTER(SessionOut)]
         _lib = L
     return _lib
+
+
+SESSION_DW = 320      # OR_SESSION_DW
+SESSION_BLOCK = 100   # OR_SESSION_BLOCK
+
+
+class SessionOut(ctypes.Structure):
+    """or_session_out (oracle/fec_oracle.h)."""
+    _fields_ = [("Q", ctypes.c_int64)] + [(f, ctypes.c_void_p) for f in (
+        "hop1_len", "hop1_hdr", "relay_len", "relay_hdr", "dest_proc", "dest_flag", "dest_lost", "dest_out",
+        "crc", "crc2", "hop1_pkts", "relay_pkts")] + [
+        ("hop1_stride", ctypes.c_int64), ("relay_stride", ctypes.c_int64)] + [(f, ctypes.c_int64) for f in (
+            "lost", "src_switches", "relay_switches", "dest_switches", "relay_flags", "dest_flags",
+            "status_seq")] + [(f, ctypes.c_float) for f in ("rate1", "rate2", "min_rate")] + [
+        (f, ctypes.c_int64) for f in ("rate1_n", "rate2_n", "min_rate_n")]
 
 
 def _u8(a: np.ndarray):
@@ -302,3 +320,37 @@ def vr_run(pattern: np.ndarray, P: int, max_payload: int = 300, T: int = 10, B: 
         assert packet_off[-1] <= packets_cap, "packets_cap too small"
         res["packets"] = packets[: packet_off[-1]]
     return res
+
+
+def relay_session_run(relay_type: int, Q: int, e1: np.ndarray, e2: np.ndarray, max_payload: int = 300,
+                      seed: int = 0x5EED, want_out: bool = False, hop1_stride: int = 0, relay_stride: int = 0):
+    """The two-hop adaptive relay session (RELAYING_TYPE 2 / 3, application_local_simulation.cpp:71-593
+    with constant transmission) for Q seqs over hop patterns e1 / e2: the reference-structured
+    oracle loop (or_relay_session_run).  Returns dict(lost, switches (source, relay, destination),
+    rates, hop1_len / relay_len [Q], hop1_hdr [Q,16], relay_hdr [Q,8], crc / crc2 per block of
+    SESSION_BLOCK seqs, and with want_out dest_proc / dest_flag / dest_lost [Q], dest_out [Q,
+    SESSION_DW]; hop1_pkts / relay_pkts [Q, stride] when a stride is given)."""
+    a = np.ascontiguousarray(e1, dtype=np.uint8)
+    b = np.ascontiguousarray(e2, dtype=np.uint8)
+    nb = (Q + SESSION_BLOCK - 1) // SESSION_BLOCK
+    r = dict(hop1_len=np.zeros(Q, np.int32), hop1_hdr=np.zeros((Q, 16), np.uint8), relay_len=np.zeros(Q, np.int32),
+             relay_hdr=np.zeros((Q, 8), np.uint8), crc=np.zeros(nb, np.uint32))
+    if want_out:
+        r.update(dest_proc=np.zeros(Q, np.uint8), dest_flag=np.zeros(Q, np.uint8), dest_lost=np.zeros(Q, np.uint8),
+                 dest_out=np.zeros((Q, SESSION_DW), np.uint8), crc2=np.zeros(nb, np.uint32))
+    if hop1_stride:
+        r["hop1_pkts"] = np.zeros((Q, hop1_stride), np.uint8)
+    if relay_stride:
+        r["relay_pkts"] = np.zeros((Q, relay_stride), np.uint8)
+    o = SessionOut()
+    o.hop1_stride, o.relay_stride = hop1_stride, relay_stride
+    for f, v in r.items():
+        setattr(o, f, v.ctypes.data)
+    rc = lib().or_relay_session_run(relay_type, max_payload, Q, _u8(a), a.size, _u8(b), b.size, seed, ctypes.byref(o))
+    if rc != 0:
+        raise ValueError(f"or_relay_session_run: {rc} at seq {o.status_seq}")
+    r.update(lost=o.lost, src_switches=o.src_switches, relay_switches=o.relay_switches,
+             dest_switches=o.dest_switches, relay_flags=o.relay_flags, dest_flags=o.dest_flags,
+             rate1=o.rate1, rate1_n=o.rate1_n, rate2=o.rate2, rate2_n=o.rate2_n, min_rate=o.min_rate,
+             min_rate_n=o.min_rate_n)
+    return r

@@ -822,6 +822,11 @@ int or_swdf_run(int max_payload, int T1, int N1, int T2, int N2, int64_t P, cons
 /*   - stam_erasure_vector[T_TOT+1] is written up to index n-symInd-1 >= n (:309-312) and       */
 /*     temp_encoded_codeword[n2] receives n bytes (:325): both are large enough here (only the  */
 /*     first n / n2 entries are ever read back when n2 <= n, which is required);                */
+/*   - n2 > n (the two-hop session, when hop 2 is the noisier one): the selection reads        */
+/*     temp_codeword[i] for n <= i < n2 (:367) past the reference's VLA of n bytes: here those     */
+/*     entries hold the settable garbage byte (0 unless or_sdswdf_set_garbage says otherwise);    */
+/*     stam_erasure_vector's writes up to index n - symInd - 1 <= T_TOT stay in its T_TOT + 1     */
+/*     entries whenever n - k + n2 - 1 <= T_TOT, as the session's split guarantees;               */
 /*   - temp_codeword keeps stale values from the previous diagonal in the positions a partial  */
 /*     diagonal does not fill (:248-250): those are artificially erased parity positions that   */
 /*     decodeBlock and encodeBlock never read and the selection never forwards -- the oracle    */
@@ -927,7 +932,7 @@ void or_sdswdf_dest_push(or_sdswdf *s, const uint8_t *frame, int frame_bytes, in
  * of T_TOT+1 ints, cnv = codeword_new_vector[n2-1], cnsw = codeword_new_symbol_wise.  Returns 0/-1. */
 int or_sw_state_encode(int max_payload, int k, int n, int k2, int n2, int sdbo, uint8_t *const *slots,
                        const uint8_t *er, int *const *header, uint8_t *cnv, uint8_t *cnsw) {
-    if (k < 1 || n < k || n > OR_SD_HDR || k2 != k || n2 < k || n2 > n) return -1;
+    if (k < 1 || n < k || n > OR_SD_HDR || k2 != k || n2 < k || n2 > OR_SD_HDR) return -1;
     const int TT = OR_TTOT;
     const int blocks = max_payload / k + 1; /* :184-185 */
     uint8_t G1[OR_MAXK * OR_MAXN], G2[OR_MAXK * OR_MAXN];
@@ -1240,13 +1245,15 @@ static void or_est_mds(or_estimator *e) {
     }
 }
 
-/* estimate, :58-186 (RELAYING_TYPE 0: T comes from the first message) */
-static void or_est_estimate(or_estimator *e, int64_t seq, int msg_T) {
+/* estimate, :58-186 (RELAYING_TYPE 0: T comes from the first message; RELAYING_TYPE 2 / 3,
+ * relay != 0: T = T_TOT at every call, :72-75) */
+static void or_est_estimate_mode(or_estimator *e, int64_t seq, int msg_T, int relay) {
     if (e->T == 0) return;
     if (e->previous_win_end == -2) {
         e->T = msg_T;
         e->previous_win_end = seq - 1;
     }
+    if (relay) e->T = OR_T_TOT;
     const int64_t current_win_end = seq;
     if (current_win_end - e->previous_win_end < 1) return;
     const int T = e->T;
@@ -1300,6 +1307,7 @@ static void or_est_estimate(or_estimator *e, int64_t seq, int msg_T) {
     }
     if (e->mds) or_est_mds(e);
 }
+static void or_est_estimate(or_estimator *e, int64_t seq, int msg_T) { or_est_estimate_mode(e, seq, msg_T, 0); }
 
 typedef struct { /* Variable_Rate_FEC_Encoder, Variable_Rate_FEC_Encoder.cpp:25-72 */
     int L;
@@ -1561,4 +1569,865 @@ int64_t or_vr_run(int max_payload, int T, int B, int N, int mds, const uint8_t *
     free(pkt);
     free(dec.buf);
     return dec.lost;
+}
+
+/* ------------------------------------------------------------------------------------------ */
+/* The two-hop adaptive relay session (RELAYING_TYPE 2 / 3, N_INITIAL = N_INITIAL_2 = -1):       */
+/* application_local_simulation.cpp:71-593 with FLAG_FOR_CONSTANT_TRANS = 1 (FEC_Macro.h:30),    */
+/* DOUBLE_ERAUSRE_NUM = 1, MIN_T2 = MIN_N2 = SPLIT_PROP = 0 (FEC_Macro.h:38-41).  Per seq i:      */
+/*   source  Application_Layer_Sender::generate_message_and_encode (Application_Layer_Sender.cpp:  */
+/*           64-282): the relay's 12-byte feedback, the T / T2 split of T_TOT, the relay-mode       */
+/*           Variable_Rate_FEC_Encoder (Variable_Rate_FEC_Encoder.cpp:74-235: T2 = T_TOT - N at a  */
+/*           switch, T_TOT + 1 double-coded packets) and the 16-byte header;                        */
+/*   relay   Application_Layer_Receiver::receive_message_and_symbol_wise_encode (Application_Layer_  */
+/*           Receiver.cpp:56-204): hop-1 erasure -> the erased-packet path (Variable_Rate_FEC_      */
+/*           Decoder.cpp:542-948), else the relay-mode estimator pair, the hop-2 code taken from   */
+/*           the header when (T1, N1) changes, Variable_Rate_FEC_Decoder::receive_message_and_      */
+/*           symbol_wise_encode (:950-1601) and the 12-byte response [its estimate, the ack, the   */
+/*           destination's 6 bytes];                                                               */
+/*   relay   Application_Layer_Sender::send_sym_wise_message (:284-346): [seq][n2-1][n2-k2]x2      */
+/*   sender  [counter] + the stored word;                                                          */
+/*   dest.   Application_Layer_Receiver::receive_message_and_symbol_wise_decode (:206-319): hop-2   */
+/*           erasure -> nothing; else the estimator pair, Variable_Rate_FEC_Decoder::receive_       */
+/*           message_and_symbol_wise_decode (:1603-1879, with its loop over the missing seqs) and  */
+/*           the 6-byte feedback; calc_missed_chars (:2698-2792) decides the dropped packets.       */
+/* Every Decoder_Symbol_Wise call goes through the or_sw_* methods above.                          */
+/* Defined away (undefined or ill-formed in the reference; the product does the same):            */
+/*   - a slot receives the rest of the received packet from the pointer on, zero beyond the packet */
+/*     (the reference copies GLOBAL_MAX_SIZE_OF_CODEWORD bytes from it, :1459 / Decoder_Symbol_   */
+/*     Wise.cpp:136, past the receive buffer); a slot holds OS_SLOT bytes (every read is below     */
+/*     2 + blocks * n <= 3314 here);                                                              */
+/*   - the GF methods use the generator of the call's own (k, n) / (k2, n2) (the reference uses    */
+/*     the object's decoder_current / encoder_current, which differ only after a relay missed a   */
+/*     switch packet; it then reads the old generator with the new dimensions, past its end when   */
+/*     the new code is larger);                                                                    */
+/*   - the relay's erased-packet word has the full size it reports (:665 overwrites :657 for       */
+/*     type 3, as in or_sdswdf_run);                                                               */
+/*   - the source header's T_old / N_old / T2_old / N2_old bytes before the first switch are 0     */
+/*     (uninitialised members of Variable_Rate_FEC_Encoder; no receiver reads them);               */
+/*   - the sender's T2_ack / B2_ack / N2_ack locals (uninitialised when the feedback is empty) are */
+/*     not kept (no reader);                                                                       */
+/*   - the driver's loop runs Q seqs, all inside FLAG_FOR_CONSTANT_TRANS's range (the reference's */
+/*     last NUMBER_OF_ITERATIONS + T_TOT + T2 - 1 - (NUMBER_OF_ITERATIONS + T_INITIAL) seqs drop   */
+/*     hop-1 erasures into its burst path); patterns count as received past their end; the first  */
+/*     hop-1 packet must arrive (an erased seq 0 reaches uninitialised members, :544-563).          */
+/* ------------------------------------------------------------------------------------------ */
+#define OS_TT 10
+#define OS_SLOT 4096
+#define OS_SD (3 * OS_TT)
+#define OS_HDR (OS_TT + 1)
+#define OS_PKT 16384
+
+typedef struct { /* Decoder_Symbol_Wise's members (include/Decoder_Symbol_Wise.h) */
+    uint8_t *cv[OS_TT + 1];  /* codeword_vector */
+    uint8_t er[OS_TT + 1];   /* temp_erasure_vector */
+    uint8_t *cnv[OS_TT + 1]; /* codeword_new_vector */
+    uint8_t *sd[OS_SD];      /* codeword_vector_state_dependent */
+    uint8_t sder[OS_SD];     /* temp_erasure_vector_state_dependent */
+    int header[OS_SD][OS_HDR];
+    int *hrows[OS_SD];
+    uint8_t cnsw[30000];     /* codeword_new_symbol_wise */
+} os_dsw;
+
+static os_dsw *os_dsw_new(void) { /* Decoder_Symbol_Wise.cpp:16-65 */
+    os_dsw *d = (os_dsw *)calloc(1, sizeof(os_dsw));
+    for (int i = 0; i < OS_TT + 1; i++) {
+        d->cv[i] = (uint8_t *)calloc(OS_SLOT, 1);
+        d->cnv[i] = (uint8_t *)calloc(OS_SLOT, 1);
+    }
+    for (int i = 0; i < OS_SD; i++) {
+        d->sd[i] = (uint8_t *)calloc(OS_SLOT, 1);
+        for (int j = 0; j < OS_HDR; j++) d->header[i][j] = j + 1;
+        d->hrows[i] = d->header[i];
+    }
+    return d;
+}
+static void os_dsw_free(os_dsw *d) {
+    if (!d) return;
+    for (int i = 0; i < OS_TT + 1; i++) {
+        free(d->cv[i]);
+        free(d->cnv[i]);
+    }
+    for (int i = 0; i < OS_SD; i++) free(d->sd[i]);
+    free(d);
+}
+/* copy_elements, :88-117 (the codes of decoder_current / encoder_current do not matter here) */
+static void os_dsw_copy(os_dsw *d, const os_dsw *s) {
+    for (int i = 0; i < OS_TT + 1; i++) {
+        memcpy(d->cv[i], s->cv[i], OS_SLOT);
+        memcpy(d->cnv[i], s->cnv[i], OS_SLOT);
+        d->er[i] = s->er[i];
+    }
+    for (int i = 0; i < OS_SD; i++) {
+        memcpy(d->sd[i], s->sd[i], OS_SLOT);
+        memcpy(d->header[i], s->header[i], sizeof(int) * OS_HDR);
+        d->sder[i] = s->sder[i];
+    }
+}
+/* rows [0, m-1) take the contents of rows [1, m); row m-1 keeps its own (the memcpy loops) */
+static void os_shift_rows(uint8_t **v, int m) {
+    if (m < 2) return;
+    uint8_t *p0 = v[0];
+    for (int i = 0; i < m - 1; i++) v[i] = v[i + 1];
+    memcpy(p0, v[m - 2], OS_SLOT);
+    v[m - 1] = p0;
+}
+static void os_dsw_shift(os_dsw *d, int n, int n2) { /* :120-135 / :144-171 */
+    os_shift_rows(d->cv, n);
+    for (int i = 0; i < n - 1; i++) d->er[i] = d->er[i + 1];
+    os_shift_rows(d->cnv, n2);
+    os_shift_rows(d->sd, OS_SD);
+    for (int i = 0; i < OS_SD - 1; i++) {
+        memcpy(d->header[i], d->header[i + 1], sizeof(int) * OS_TT); /* entry T_TOT stays */
+        d->sder[i] = d->sder[i + 1];
+    }
+}
+/* the rest of a received packet from `msg` on (`avail` bytes) at offset `off` of a zeroed slot */
+static void os_fill(uint8_t *slot, int off, const uint8_t *msg, int avail) {
+    memset(slot, 0, OS_SLOT);
+    if (avail > OS_SLOT - off) avail = OS_SLOT - off;
+    if (msg && avail > 0) memcpy(slot + off, msg, (size_t)avail);
+}
+static void os_push(os_dsw *d, const uint8_t *msg, int avail, int n, int n2) { /* :119-140 */
+    os_dsw_shift(d, n, n2);
+    os_fill(d->cv[n - 1], 2, msg, avail);
+    d->er[n - 1] = 0;
+}
+static void os_rotate(os_dsw *d, int n, int n2) { /* :142-176 */
+    os_dsw_shift(d, n, n2);
+    memset(d->cv[n - 1], 0, OS_SLOT);
+    d->er[n - 1] = 1;
+}
+static int os_rd_size(int L, int k2, int n2) { /* (ceil(float(max_payload + 2) / k2) + 1) * n2, :997-999 */
+    return ((L + 2 + k2 - 1) / k2 + 1) * n2;
+}
+
+typedef struct { /* Variable_Rate_FEC_Encoder in relay mode */
+    int L;
+    or_encoder *cur, *old;
+    int T, B, N, T_old, B_old, N_old, T2, B2, N2, T2_old, B2_old, N2_old;
+    int counter_transition, transition_flag, double_coding_flag;
+    int64_t switches;
+    float rate1; /* debug_rate_first_hop (onReceivedMessage, :362-385) */
+    int64_t rate1_n;
+    float rate1_curr;
+} os_vre;
+
+/* encode, :74-235 with RELAYING_TYPE 2 / 3: the frame [size_cur BE16][cw_cur][cw_old] into `frame`,
+ * the message's (T, B, N) and counter out.  Returns the frame bytes. */
+static int os_vre_encode(os_vre *v, int *mT, int *mB, int *mN, const uint8_t *data, int size, int seq, int T_ack,
+                         int B_ack, uint8_t *frame, int *counter, uint8_t *tmp_cur, uint8_t *tmp_old) {
+    if (v->cur == NULL) {
+        v->T = *mT;
+        v->B = *mB;
+        v->N = *mN;
+        v->cur = or_encoder_new(v->L, v->T, v->B, v->N);
+        v->transition_flag = 1;
+        v->double_coding_flag = 0;
+    } else if ((*mT != v->T || *mB != v->B || *mN != v->N) && v->transition_flag == 0 && T_ack == v->T &&
+               B_ack == v->B) { /* :92-127 */
+        v->switches++;
+        v->T_old = v->T;
+        v->B_old = v->B;
+        v->N_old = v->N;
+        v->T = *mT;
+        v->B = *mB;
+        v->N = *mN;
+        v->T2_old = v->T2; /* :107-115 */
+        v->B2_old = v->B2;
+        v->N2_old = v->N2;
+        v->T2 = OS_TT - v->N;
+        v->transition_flag = 1;
+        v->double_coding_flag = 1;
+        v->counter_transition = 0;
+        if (v->old) or_encoder_free(v->old);
+        v->old = v->cur;
+        v->cur = or_encoder_new(v->L, v->T, v->B, v->N);
+    } else {
+        *mT = v->T;
+        *mB = v->B;
+        *mN = v->N;
+    }
+    v->rate1_n++; /* onReceivedMessage, :368-374 */
+    v->rate1_curr = (float)(*mT - *mN + 1) / (*mT + 1);
+    v->rate1 += (float)(*mT - *mN + 1) / (*mT + 1);
+    const int size_cur = or_encoder_transmit(v->cur, data, size, seq, tmp_cur);
+    int size_old = 0;
+    *counter = v->counter_transition;
+    if (v->counter_transition <= OS_TT + 1) { /* :149-168 */
+        if (v->counter_transition == OS_TT + 1) v->double_coding_flag = 0;
+        v->counter_transition++;
+        if (v->old != NULL && v->double_coding_flag == 1)
+            size_old = or_encoder_transmit(v->old, data, size, seq, tmp_old);
+    } else {
+        v->transition_flag = 0;
+        v->counter_transition++;
+    }
+    frame[0] = (uint8_t)((size_cur - size_cur % 256) / 256); /* :194-214 */
+    frame[1] = (uint8_t)(size_cur % 256);
+    memcpy(frame + 2, tmp_cur, (size_t)size_cur);
+    if (size_old) memcpy(frame + 2 + size_cur, tmp_old, (size_t)size_old);
+    return 2 + size_cur + size_old;
+}
+
+typedef struct { /* Variable_Rate_FEC_Decoder's relay / destination members */
+    int64_t seq_start, latest_seq, sdc, sde;
+    int T, B, N, dcf;
+    int k_old, n_old, k2_old, n2_old, k_last, n_last, k2_last, n2_last;
+    os_dsw *main, *nw;
+    int64_t switches, flags;
+} os_vrd;
+
+static void os_vrd_init(os_vrd *d) {
+    memset(d, 0, sizeof(*d));
+    d->seq_start = d->latest_seq = d->sdc = d->sde = -1;
+    d->main = os_dsw_new();
+}
+
+/* one Decoder_Symbol_Wise relay call (symbol_wise_encode_1 / _state_dependent) after its slot push */
+static int os_relay_call(int R, int L, os_dsw *o, int k, int n, int k2, int n2, int *flag) {
+    *flag = 0;
+    if (R == 3) return or_sw_state_encode(L, k, n, k2, n2, 0, o->sd, o->sder, o->hrows, o->cnv[n2 - 1], o->cnsw);
+    return or_sw_encode_1(L, k, n, k2, n2, o->cv, o->er, o->cnv, o->cnsw, flag);
+}
+/* append a code's part of the relay word: [header[n2-1] as bytes (type 3)][cnv[n2-1][0 .. size)] */
+static int os_word_part(int R, const os_dsw *o, int n2, int size, uint8_t *w) {
+    int p = 0;
+    if (R == 3)
+        for (int aa = 0; aa < OS_HDR; aa++) w[p++] = (uint8_t)o->header[n2 - 1][aa];
+    memcpy(w + p, o->cnv[n2 - 1], (size_t)size);
+    return p + size;
+}
+
+/* Variable_Rate_FEC_Decoder::receive_message_and_symbol_wise_encode_erased_packet_for_constnat_trans
+ * (:542-948): the relay's word for an erased hop-1 seq.  Returns its bytes, or -1. */
+static int os_relay_erased(int R, int L, os_vrd *d, int64_t seq, uint8_t *word) {
+    const int n = d->n_last, k = d->k_last, n2 = d->n2_last, k2 = d->k2_last; /* :544-547 */
+    if (d->seq_start == -1) return -1; /* seq 0 erased: uninitialised members (see above) */
+    int flag = 0;
+    if (seq > d->sde && d->dcf == 1) { /* :605-616 */
+        d->dcf = 0;
+        os_dsw_copy(d->main, d->nw);
+        d->n2_old = d->n2_last;
+        d->k2_old = d->k2_last;
+    }
+    if (seq == d->sdc) { /* :619-633 (never met with constant transmission; kept as written) */
+        d->sde = d->sdc + OS_TT + 1 - 1;
+        os_dsw_free(d->nw);
+        d->k_old = d->T - d->N + 1;
+        d->n_old = d->T + 1;
+        d->T = d->B = d->N = 0; /* the erased message's (T, B, N), Application_Layer_Receiver.cpp:78 */
+        d->nw = os_dsw_new();
+        d->dcf = 1;
+        d->switches++;
+    }
+    int p = 2, size_first;
+    if (d->dcf == 0) { /* :636-684 */
+        os_rotate(d->main, n, n2);
+        if (R == 3) {
+            memset(d->main->sd[2 * OS_TT], 0, OS_SLOT);
+            d->main->sder[2 * OS_TT] = 1;
+        }
+        if (os_relay_call(R, L, d->main, k, n, k2, n2, &flag)) return -1;
+        d->flags += flag;
+        size_first = os_rd_size(L, k2, n2);
+        p += os_word_part(R, d->main, n2, size_first, word + p);
+    } else { /* :685-761 */
+        os_rotate(d->main, d->n_old, d->n2_old);
+        if (R == 3) {
+            memset(d->main->sd[2 * OS_TT], 0, OS_SLOT);
+            d->main->sder[2 * OS_TT] = 1;
+        }
+        if (os_relay_call(R, L, d->main, d->k_old, d->n_old, d->k2_old, d->n2_old, &flag)) return -1;
+        d->flags += flag;
+        os_rotate(d->nw, n, n2);
+        if (R == 3) {
+            memset(d->main->sd[2 * OS_TT], 0, OS_SLOT); /* :702-704: the main object's slot, as written */
+            d->nw->sder[2 * OS_TT] = 1;
+        }
+        int f2;
+        if (os_relay_call(R, L, d->nw, k, n, k2, n2, &f2)) return -1;
+        size_first = os_rd_size(L, k2, n2);
+        p += os_word_part(R, d->nw, n2, size_first, word + p);
+        p += os_word_part(R, d->main, d->n2_old, os_rd_size(L, d->k2_old, d->n2_old), word + p);
+    }
+    word[0] = (uint8_t)(size_first / 256);
+    word[1] = (uint8_t)(size_first % 256);
+    d->latest_seq = seq + 1; /* :942, then the caller's latest_seq = temp + 1 (Application_Layer_Receiver.cpp:82) */
+    return p;
+}
+
+/* Variable_Rate_FEC_Decoder::receive_message_and_symbol_wise_encode (:950-1601) for a received
+ * hop-1 packet in sequence (no gap: constant transmission).  frame = the VR frame ([size BE16][cur]
+ * [old]), fbytes its size.  Returns the word's bytes, or -1. */
+static int os_relay_received(int R, int L, os_vrd *d, int64_t seq, int mT, int mB, int mN, int counter, int n,
+                             int k, int n2, int k2, const uint8_t *frame, int fbytes, uint8_t *word) {
+    if (d->seq_start == -1) { /* :952-967 */
+        d->T = mT;
+        d->B = mB;
+        d->N = mN;
+        d->seq_start = 0;
+        d->latest_seq = 0;
+        d->n_old = n;
+        d->k2_old = k2;
+        d->n2_old = n2;
+        d->k2_last = k2;
+        d->n2_last = n2;
+    }
+    if (seq < d->latest_seq) return -1;
+    if (seq != d->latest_seq) return -1; /* a gap: not with constant transmission */
+    if (d->T != mT || d->B != mB || d->N != mN) d->sdc = seq - counter; /* :975-978 */
+    const uint8_t *cwr = frame + 2;
+    const int size_received = frame[0] * 256 + frame[1];
+    const uint8_t *cwt = cwr + size_received;
+    const int avail = fbytes - 2, avail_t = fbytes - 2 - size_received;
+    int flag = 0;
+    if (seq > d->sde && d->dcf == 1) { /* :1423-1434 */
+        d->dcf = 0;
+        os_dsw_copy(d->main, d->nw);
+        d->n_old = n;
+        d->n2_old = n2;
+        d->k2_old = k2;
+    }
+    if (seq == d->sdc) { /* :1437-1456 */
+        d->sde = d->sdc + OS_TT + 1 - 1;
+        os_dsw_free(d->nw);
+        d->k_old = d->T - d->N + 1;
+        d->n_old = d->T + 1;
+        if (d->k2_old != d->k_old) { /* :1443-1447 */
+            d->n2_old = OS_TT - d->N + 1;
+            d->k2_old = d->T - d->N + 1;
+        }
+        d->T = mT;
+        d->B = mB;
+        d->N = mN;
+        d->nw = os_dsw_new();
+        d->dcf = 1;
+        d->switches++;
+    }
+    const int size_cur = os_rd_size(L, k2, n2);
+    int p = 2;
+    if (d->dcf == 0) { /* :1458-1501 */
+        os_push(d->main, cwr, avail, n, n2);
+        if (R == 3) {
+            os_fill(d->main->sd[2 * OS_TT], 2, cwr, avail);
+            d->main->sder[2 * OS_TT] = 0;
+        }
+        if (os_relay_call(R, L, d->main, k, n, k2, n2, &flag)) return -1;
+        d->flags += flag;
+        p += os_word_part(R, d->main, n2, size_cur, word + p);
+    } else { /* :1502-1588 */
+        os_push(d->main, cwt, avail_t, d->n_old, d->n2_old);
+        if (R == 3) {
+            os_fill(d->main->sd[2 * OS_TT], 2, cwt, avail_t);
+            d->main->sder[2 * OS_TT] = 0;
+        }
+        if (os_relay_call(R, L, d->main, d->k_old, d->n_old, d->k2_old, d->n2_old, &flag)) return -1;
+        d->flags += flag;
+        os_push(d->nw, cwr, avail, n, n2);
+        if (R == 3) {
+            os_fill(d->nw->sd[2 * OS_TT], 2, cwr, avail);
+            d->nw->sder[2 * OS_TT] = 0;
+        }
+        int f2;
+        if (os_relay_call(R, L, d->nw, k, n, k2, n2, &f2)) return -1;
+        p += os_word_part(R, d->nw, n2, size_cur, word + p);
+        p += os_word_part(R, d->main, d->n2_old, os_rd_size(L, d->k2_old, d->n2_old), word + p);
+    }
+    word[0] = (uint8_t)(size_cur / 256);
+    word[1] = (uint8_t)(size_cur % 256);
+    d->latest_seq = seq + 1; /* :1595-1599 */
+    d->k_last = k;
+    d->n_last = n;
+    d->k2_last = k2;
+    d->n2_last = n2;
+    return p;
+}
+
+typedef struct { /* the destination's outputs of one processed seq */
+    uint8_t *buffer, *temp; /* Decoder_Symbol_Wise output buffer, extract_data's temp_buffer */
+    int nbytes;             /* blocks * k bytes extracted by the last reporting call */
+    float rate2, rate2_curr;
+    int64_t rate2_n;
+} os_destio;
+
+/* the destination's decode of one seq by `o` with (k, n) + extract_data (:653-661) into io->temp */
+static int os_dest_call(int R, int L, os_dsw *o, int k, int n, os_destio *io, int extract) {
+    int flag = 0;
+    if (R == 3) {
+        if (or_sw_state_decode(L, k, n, o->sd, o->hrows, io->buffer, &flag)) return -1;
+    } else {
+        if (or_sw_decode_1(L, k, n, o->cv, o->er, io->buffer, &flag)) return -1;
+    }
+    if (extract) {
+        const int blocks = L / k + 1;
+        int ind = 0;
+        for (int j = 0; j < blocks; j++)
+            for (int i = 0; i < k; i++) io->temp[ind++] = io->buffer[j * n + n - k + i];
+        io->nbytes = ind;
+        io->rate2_curr = (float)k / n; /* :1722-1724 */
+        io->rate2 += (float)k / n;
+        io->rate2_n++;
+    }
+    return flag;
+}
+
+/* the destination's slot update for one seq: a received part (`part` with `avail` bytes, its 11
+ * header ints for type 3) or a missing one */
+static void os_dest_slot(int R, os_dsw *o, int n, const uint8_t *part, int avail, const int *hdr,
+                         os_dsw *memset_this) {
+    if (part) {
+        os_push(o, part, avail, n, 0);
+        if (R == 3) {
+            for (int i = 0; i < OS_HDR; i++) o->header[3 * OS_TT - 1][i] = hdr[i];
+            os_fill(o->sd[3 * OS_TT - 1], 2, part, avail);
+            o->sder[3 * OS_TT - 1] = 0;
+        }
+    } else {
+        os_rotate(o, n, 0);
+        if (R == 3) {
+            for (int i = 0; i < OS_HDR; i++) o->header[3 * OS_TT - 1][i] = 0;
+            memset(memset_this->sd[3 * OS_TT - 1], 0, OS_SLOT); /* :1759 zeroes the main object's */
+            o->sder[3 * OS_TT - 1] = 1;
+        }
+    }
+}
+
+/* Variable_Rate_FEC_Decoder::receive_message_and_symbol_wise_decode (:1603-1879) for a received
+ * relay packet (word = the stored word after the 8-byte header).  on_output(seq) is called for
+ * every seq whose output the main object extracts (gap seqs and the received one). */
+typedef struct {
+    int R, L;
+    os_vrd d;
+    os_destio io;
+    /* per processed seq: */
+    void (*emit)(void *ctx, int64_t seq, int flag);
+    void *ctx;
+} os_dest;
+
+static int os_dest_received(os_dest *D, int64_t seq, int mT, int mB, int mN, int counter, int n, int k,
+                            const uint8_t *word, int wbytes) {
+    const int R = D->R, L = D->L;
+    os_vrd *d = &D->d;
+    if (d->seq_start == -1) { /* :1607-1621 */
+        d->T = mT;
+        d->B = mB;
+        d->N = mN;
+        d->seq_start = 0;
+        d->latest_seq = 0;
+        d->k_old = k;
+        d->n_old = n;
+        d->k_last = k;
+        d->n_last = n;
+    }
+    if (seq < d->latest_seq) return 0;
+    int transition_flag = 0;
+    if (d->T != mT || d->B != mB || d->N != mN) { /* :1629-1636 */
+        d->sdc = counter > 128 ? seq - (counter - 255) : seq - counter;
+        transition_flag = 1;
+    }
+    const int hb = R == 3 ? OS_HDR : 0;
+    const int size_received = word[0] * 256 + word[1];
+    const uint8_t *cwr = word + 2 + hb;
+    const uint8_t *cwt = cwr + size_received + hb;
+    const int avail = wbytes - 2 - hb, avail_t = wbytes - 2 - hb - size_received - hb;
+    int new_header[OS_HDR], new_header_trans[OS_HDR];
+    for (int i = 0; i < OS_HDR; i++) {
+        new_header[i] = word[2 + i]; /* :1663-1664 */
+        const int q = 2 + OS_HDR + size_received + i; /* :1653-1654 (zero past the word) */
+        new_header_trans[i] = q < wbytes ? word[q] : 0;
+    }
+    for (int64_t s = d->latest_seq; s < seq; s++) { /* :1671-1769 */
+        if (s > d->sde && d->dcf == 1) {
+            d->dcf = 0;
+            os_dsw_copy(d->main, d->nw);
+            d->n_last = n;
+            d->k_last = k;
+        }
+        if (s == d->sdc) {
+            d->sde = d->sdc + OS_TT + 1 - 1;
+            os_dsw_free(d->nw);
+            d->k_old = d->T - d->N + 1;
+            d->n_old = d->T + 1;
+            d->T = mT;
+            d->B = mB;
+            d->N = mN;
+            transition_flag = 0;
+            d->nw = os_dsw_new();
+            d->dcf = 1;
+            d->switches++;
+        }
+        int fl;
+        if (d->dcf == 0) {
+            os_dest_slot(R, d->main, d->n_last, NULL, 0, NULL, d->main);
+            if ((fl = os_dest_call(R, L, d->main, d->k_last, d->n_last, &D->io, 1)) < 0) return -1;
+        } else {
+            os_dest_slot(R, d->main, d->n_old, NULL, 0, NULL, d->main);
+            if ((fl = os_dest_call(R, L, d->main, d->k_old, d->n_old, &D->io, 1)) < 0) return -1;
+            os_dest_slot(R, d->nw, n, NULL, 0, NULL, d->main);
+            if (os_dest_call(R, L, d->nw, k, n, &D->io, 0) < 0) return -1;
+        }
+        d->flags += fl;
+        D->emit(D->ctx, s, fl);
+    }
+    if (seq > d->sde && d->dcf == 1) { /* :1772-1781 */
+        d->dcf = 0;
+        os_dsw_copy(d->main, d->nw);
+        d->n_last = n;
+        d->k_last = k;
+    }
+    if (seq == d->sdc || (seq >= d->sdc && transition_flag == 1)) { /* :1783-1796 */
+        d->sde = d->sdc + OS_TT + 1 - 1;
+        os_dsw_free(d->nw);
+        d->k_old = d->T - d->N + 1;
+        d->n_old = d->T + 1;
+        d->T = mT;
+        d->B = mB;
+        d->N = mN;
+        d->nw = os_dsw_new();
+        d->dcf = 1;
+        d->switches++;
+    }
+    int fl;
+    if (d->dcf == 0) { /* :1798-1822 */
+        os_dest_slot(R, d->main, d->n_last, cwr, avail, new_header, d->main);
+        if ((fl = os_dest_call(R, L, d->main, d->k_last, d->n_last, &D->io, 1)) < 0) return -1;
+    } else { /* :1823-1873 */
+        os_dest_slot(R, d->main, d->n_old, cwt, avail_t, new_header_trans, d->main);
+        if ((fl = os_dest_call(R, L, d->main, d->k_old, d->n_old, &D->io, 1)) < 0) return -1;
+        os_dest_slot(R, d->nw, n, cwr, avail, new_header, d->main);
+        if (os_dest_call(R, L, d->nw, k, n, &D->io, 0) < 0) return -1;
+    }
+    d->flags += fl;
+    D->emit(D->ctx, seq, fl);
+    d->latest_seq = seq + 1;
+    return 0;
+}
+
+static uint32_t os_crc32(uint32_t c, const uint8_t *p, size_t n) { /* IEEE, as zlib.crc32 */
+    static uint32_t tab[256];
+    static int init = 0;
+    if (!init) {
+        for (uint32_t i = 0; i < 256; i++) {
+            uint32_t x = i;
+            for (int b = 0; b < 8; b++) x = (x & 1) ? 0xEDB88320u ^ (x >> 1) : x >> 1;
+            tab[i] = x;
+        }
+        init = 1;
+    }
+    c = ~c;
+    for (size_t i = 0; i < n; i++) c = tab[(c ^ p[i]) & 0xff] ^ (c >> 8);
+    return ~c;
+}
+
+typedef struct {
+    or_session_out *o;
+    int L;
+    uint64_t seed;
+    os_destio *io;
+    uint8_t *payload;
+} os_emit_ctx;
+
+/* calc_missed_chars (:2698-2792) and the per-seq outputs of a processed destination seq */
+static void os_emit(void *vctx, int64_t seq, int flag) {
+    os_emit_ctx *c = (os_emit_ctx *)vctx;
+    or_session_out *o = c->o;
+    if (seq < 0 || seq >= o->Q) return;
+    int lost = 0;
+    if (seq >= OS_TT) {
+        or_fill_payload(c->payload, seq - OS_TT, 1, c->L, c->seed);
+        for (int kk = 0; kk < 250 && kk < c->L; kk++)
+            if (c->io->temp[kk + 2] != c->payload[kk]) {
+                lost = 1;
+                break;
+            }
+    }
+    o->lost += lost;
+    if (o->dest_proc) o->dest_proc[seq] = 1;
+    if (o->dest_flag) o->dest_flag[seq] = (uint8_t)flag;
+    if (o->dest_lost) o->dest_lost[seq] = (uint8_t)lost;
+    if (o->dest_out) {
+        uint8_t *dst = o->dest_out + seq * (int64_t)OR_SESSION_DW;
+        const int nb = c->io->nbytes < OR_SESSION_DW ? c->io->nbytes : OR_SESSION_DW;
+        memcpy(dst, c->io->temp, (size_t)nb); /* blocks * k bytes, the rest zero */
+        memset(dst + nb, 0, (size_t)(OR_SESSION_DW - nb));
+    }
+}
+
+int or_relay_session_run(int relay_type, int max_payload, int64_t Q, const uint8_t *e1, int64_t n_e1,
+                         const uint8_t *e2, int64_t n_e2, uint64_t seed, or_session_out *o) {
+    const int R = relay_type, L = max_payload;
+    if ((R != 2 && R != 3) || L < 1 || L + 32 > OR_SESSION_DW + 32 || Q < 1 || !o) return -1;
+    if (n_e1 > 0 && e1[0]) return -2; /* see above */
+    or_gf_init();
+    o->Q = Q;
+    o->lost = o->src_switches = o->relay_switches = o->dest_switches = o->relay_flags = o->dest_flags = 0;
+    o->rate1 = o->rate2 = o->min_rate = 0;
+    o->rate1_n = o->rate2_n = o->min_rate_n = 0;
+    o->status_seq = -1;
+    if (o->dest_proc) memset(o->dest_proc, 0, (size_t)Q);
+    if (o->dest_flag) memset(o->dest_flag, 0, (size_t)Q);
+    if (o->dest_lost) memset(o->dest_lost, 0, (size_t)Q);
+    if (o->dest_out) memset(o->dest_out, 0, (size_t)Q * OR_SESSION_DW);
+    /* source: Application_Layer_Sender(.., T = T_TOT, B = N = -1, flag 0) (:9-53), its VR encoder
+     * with T2 = T_TOT, N2 = B2 = 0 (application_local_simulation.cpp:136-143) */
+    int sT = OS_TT, sB = 0, sN = 0, sT_ack = OS_TT, sB_ack = 0, sN_ack = 0, sT2 = 0, sN2 = 0;
+    os_vre venc;
+    memset(&venc, 0, sizeof(venc));
+    venc.L = L;
+    venc.transition_flag = 1;
+    venc.double_coding_flag = 1;
+    venc.T2 = OS_TT;
+    uint8_t *payload = (uint8_t *)malloc((size_t)L);
+    uint8_t *pkt = (uint8_t *)calloc(OS_PKT, 1);     /* hop-1 packet: 16-byte header + VR frame */
+    uint8_t *word = (uint8_t *)calloc(OS_PKT, 1);    /* the relay's stored word */
+    uint8_t *rpkt = (uint8_t *)calloc(OS_PKT, 1);    /* hop-2 packet: 8-byte header + word */
+    uint8_t *tmp_cur = (uint8_t *)calloc(OS_PKT, 1), *tmp_old = (uint8_t *)calloc(OS_PKT, 1);
+    uint8_t udp[12] = {0}, udp2[6] = {0};
+    /* relay receiver (Application_Layer_Receiver.cpp:10-39, index 0) */
+    or_estimator *est = (or_estimator *)malloc(sizeof(or_estimator));
+    or_estimator *bg = (or_estimator *)malloc(sizeof(or_estimator));
+    or_est_init(est, OR_T_TOT, 0);
+    or_est_init(bg, OR_T_TOT, 0);
+    int64_t cycle = 1, last_received = -1;
+    int first_call = 1, T_s_r = 0, N_s_r = 0, stale_counter = 0;
+    int n2_new = OS_TT + 1, k2_new = OS_TT + 1; /* application_local_simulation.cpp:316-324 */
+    os_vrd relay;
+    os_vrd_init(&relay);
+    /* destination receiver (index 1) */
+    or_estimator *dest = (or_estimator *)malloc(sizeof(or_estimator));
+    or_estimator *dbg = (or_estimator *)malloc(sizeof(or_estimator));
+    or_est_init(dest, OR_T_TOT, 0);
+    or_est_init(dbg, OR_T_TOT, 0);
+    int64_t dcycle = 1;
+    os_dest D;
+    memset(&D, 0, sizeof(D));
+    D.R = R;
+    D.L = L;
+    os_vrd_init(&D.d);
+    D.io.buffer = (uint8_t *)calloc(30000, 1);
+    D.io.temp = (uint8_t *)calloc(30000, 1);
+    os_emit_ctx ectx = {o, L, seed, &D.io, (uint8_t *)malloc((size_t)L)};
+    D.emit = os_emit;
+    D.ctx = &ectx;
+    int rc = 0;
+    uint32_t crc = 0;
+    for (int64_t i = 0; i < Q; i++) {
+        /* ---- source, Application_Layer_Sender.cpp:64-282 ---- */
+        or_fill_payload(payload, i, 1, L, seed);
+        if (udp[0] != 0) { /* :79-95 (adaptive) */
+            sT = udp[0];
+            sB = udp[1];
+            sN = udp[2];
+            sT_ack = udp[3];
+            sB_ack = udp[4];
+            sN_ack = udp[5];
+            sT2 = udp[6];
+            sN2 = udp[8];
+        }
+        if (i > 0) { /* :109-198 */
+            sN = sN < OS_TT ? sN : OS_TT; /* min(T_TOT, floor(DOUBLE_ERAUSRE_NUM * N)) */
+            sN2 = sN2 < OS_TT ? sN2 : OS_TT;
+            if (sN + sN2 <= OS_TT) {
+                sT = OS_TT - sN2;
+                sT2 = OS_TT - sN;
+                if (sT >= 1) { /* MIN_T2 = 0, MIN_N2 = 0 */
+                    venc.N2 = sN2;
+                    venc.B2 = sN2;
+                } else {
+                    sT = 1;
+                    sN2 = OS_TT - sT;
+                    sN = sN < sT ? sN : sT;
+                    sT2 = OS_TT - sN;
+                    venc.N2 = sN2;
+                    venc.B2 = sN2;
+                }
+            } else { /* SPLIT_PROP = 0: stay */
+                sN = sN_ack;
+                sT = sT_ack;
+            }
+        }
+        (void)sT2;
+        (void)sB;
+        int mT = sT, mB = sN, mN = sN, counter = 0; /* set_parameters(seq, T, N, N, ..) :200-201 */
+        const int fbytes = os_vre_encode(&venc, &mT, &mB, &mN, payload, L, (int)i, sT_ack, sB_ack, pkt + 16, &counter,
+                                         tmp_cur, tmp_old);
+        pkt[15] = (uint8_t)venc.N2_old; /* :222-244 */
+        pkt[14] = (uint8_t)venc.T2_old;
+        pkt[13] = (uint8_t)venc.N_old;
+        pkt[12] = (uint8_t)venc.T_old;
+        pkt[11] = (uint8_t)counter;
+        pkt[10] = (uint8_t)venc.N2;
+        pkt[9] = (uint8_t)venc.B2;
+        pkt[8] = (uint8_t)venc.T2;
+        pkt[7] = (uint8_t)counter;
+        pkt[6] = (uint8_t)mN;
+        pkt[5] = (uint8_t)mB;
+        pkt[4] = (uint8_t)mT;
+        pkt[3] = (uint8_t)(i % 256);
+        pkt[2] = (uint8_t)((i / 256) % 256);
+        pkt[1] = (uint8_t)((i / 256 / 256) % 256);
+        pkt[0] = (uint8_t)((i / 256 / 256 / 256) % 256);
+        const int psize = 16 + fbytes;
+        if (o->hop1_len) o->hop1_len[i] = psize;
+        if (o->hop1_hdr) memcpy(o->hop1_hdr + 16 * i, pkt, 16);
+        if (o->hop1_pkts && psize <= o->hop1_stride) {
+            memcpy(o->hop1_pkts + i * o->hop1_stride, pkt, (size_t)psize);
+            memset(o->hop1_pkts + i * o->hop1_stride + psize, 0, (size_t)(o->hop1_stride - psize));
+        }
+        uint8_t le[4] = {(uint8_t)psize, (uint8_t)(psize >> 8), (uint8_t)(psize >> 16), (uint8_t)(psize >> 24)};
+        crc = os_crc32(crc, le, 4);
+        crc = os_crc32(crc, pkt, (size_t)psize);
+        /* ---- relay receiver, Application_Layer_Receiver.cpp:56-204 ---- */
+        if (first_call) { /* :69-72 */
+            T_s_r = pkt[4];
+            N_s_r = pkt[6];
+            first_call = 0;
+        }
+        int wbytes;
+        int64_t tseq;
+        const int lost1 = i < n_e1 && e1[i];
+        if (lost1) { /* :76-85 */
+            tseq = last_received + 1;
+            wbytes = os_relay_erased(R, L, &relay, tseq, word);
+            last_received = tseq;
+        } else {
+            tseq = i;
+            const int hT = pkt[4], hB = pkt[5], hN = pkt[6], hc = pkt[7];
+            stale_counter = hc;
+            or_est_estimate_mode(est, tseq, hT, 1);
+            or_est_estimate_mode(bg, tseq, hT, 1);
+            if (tseq + 1 > cycle * OR_EST_CYCLE) { /* :104-113 */
+                free(est);
+                est = bg;
+                bg = (or_estimator *)malloc(sizeof(or_estimator));
+                or_est_init(bg, OR_T_TOT, 0);
+                cycle++;
+            }
+            const int k = hT - hN + 1, n = hT + 1;
+            if (T_s_r != hT || N_s_r != hN) { /* :142-150 */
+                T_s_r = hT;
+                N_s_r = hN;
+                k2_new = pkt[8] - pkt[10] + 1;
+                n2_new = pkt[8] + 1;
+            }
+            wbytes = os_relay_received(R, L, &relay, tseq, hT, hB, hN, hc, n, k, n2_new, k2_new, pkt + 16, fbytes,
+                                       word);
+            udp[0] = (uint8_t)est->T; /* :176-201 */
+            udp[1] = (uint8_t)est->B_current;
+            udp[2] = (uint8_t)est->N_current;
+            udp[3] = (uint8_t)hT;
+            udp[4] = (uint8_t)hB;
+            udp[5] = (uint8_t)hN;
+            for (int q = 6; q < 12; q++) udp[q] = udp2[q - 6];
+            last_received = tseq;
+        }
+        if (wbytes < 0) {
+            rc = -3;
+            o->status_seq = i;
+            break;
+        }
+        /* ---- relay sender, Application_Layer_Sender.cpp:284-346 (start_index = the last word,
+         * application_local_simulation.cpp:558-587) ---- */
+        int rcount = lost1 ? stale_counter : pkt[7]; /* the erased path keeps the message's counter */
+        memcpy(rpkt + 8, word, (size_t)wbytes);
+        rpkt[7] = (uint8_t)rcount;
+        rpkt[6] = (uint8_t)(n2_new - k2_new);
+        rpkt[5] = (uint8_t)(n2_new - k2_new);
+        rpkt[4] = (uint8_t)(n2_new - 1);
+        rpkt[3] = (uint8_t)(tseq % 256);
+        rpkt[2] = (uint8_t)((tseq / 256) % 256);
+        rpkt[1] = (uint8_t)((tseq / 256 / 256) % 256);
+        rpkt[0] = (uint8_t)((tseq / 256 / 256 / 256) % 256);
+        const int rsize = 8 + wbytes;
+        if (o->relay_len) o->relay_len[i] = rsize;
+        if (o->relay_hdr) memcpy(o->relay_hdr + 8 * i, rpkt, 8);
+        if (o->relay_pkts && rsize <= o->relay_stride) {
+            memcpy(o->relay_pkts + i * o->relay_stride, rpkt, (size_t)rsize);
+            memset(o->relay_pkts + i * o->relay_stride + rsize, 0, (size_t)(o->relay_stride - rsize));
+        }
+        le[0] = (uint8_t)rsize;
+        le[1] = (uint8_t)(rsize >> 8);
+        le[2] = (uint8_t)(rsize >> 16);
+        le[3] = (uint8_t)(rsize >> 24);
+        crc = os_crc32(crc, le, 4);
+        crc = os_crc32(crc, rpkt, (size_t)rsize);
+        /* ---- destination, Application_Layer_Receiver.cpp:206-319 ---- */
+        const int lost2 = tseq < n_e2 && e2[tseq];
+        if (!lost2) {
+            const int hT = rpkt[4], hB = rpkt[5], hN = rpkt[6], hc = rpkt[7];
+            or_est_estimate_mode(dest, tseq, hT, 1);
+            or_est_estimate_mode(dbg, tseq, hT, 1);
+            if (tseq + 1 > dcycle * OR_EST_CYCLE) { /* :251-260 */
+                free(dest);
+                dest = dbg;
+                dbg = (or_estimator *)malloc(sizeof(or_estimator));
+                or_est_init(dbg, OR_T_TOT, 0);
+                dcycle++;
+            }
+            const int k = hT - hN + 1, n = hT + 1;
+            memset(rpkt + rsize, 0, 64); /* zero past the word (new_Header_trans of a single word) */
+            if (os_dest_received(&D, tseq, hT, hB, hN, hc, n, k, rpkt + 8, wbytes) < 0) {
+                rc = -4;
+                o->status_seq = i;
+                break;
+            }
+            udp2[0] = (uint8_t)dest->T; /* :302-309 */
+            udp2[1] = (uint8_t)dest->B_current;
+            udp2[2] = (uint8_t)dest->N_current;
+            udp2[3] = (uint8_t)hT;
+            udp2[4] = (uint8_t)hB;
+            udp2[5] = (uint8_t)hN;
+        }
+        /* application_local_simulation.cpp:589-592 */
+        o->min_rate += venc.rate1_curr < D.io.rate2_curr ? venc.rate1_curr : D.io.rate2_curr;
+        o->min_rate_n++;
+        if ((i + 1) % OR_SESSION_BLOCK == 0 || i + 1 == Q) {
+            if (o->crc) o->crc[i / OR_SESSION_BLOCK] = crc;
+            crc = 0;
+        }
+    }
+    /* the destination outputs enter the digest per block (after the loop: a seq's output can be
+     * emitted one or more seqs after it was sent) */
+    if (rc == 0 && o->crc2 && o->dest_out && o->dest_proc) {
+        for (int64_t b0 = 0; b0 < Q; b0 += OR_SESSION_BLOCK) {
+            uint32_t c = 0;
+            for (int64_t t = b0; t < Q && t < b0 + OR_SESSION_BLOCK; t++) {
+                const uint8_t fl[3] = {o->dest_proc[t], o->dest_flag ? o->dest_flag[t] : 0,
+                                       o->dest_lost ? o->dest_lost[t] : 0};
+                c = os_crc32(c, fl, 3);
+                c = os_crc32(c, o->dest_out + t * (int64_t)OR_SESSION_DW, OR_SESSION_DW);
+            }
+            o->crc2[b0 / OR_SESSION_BLOCK] = c;
+        }
+    }
+    o->src_switches = venc.switches;
+    o->relay_switches = relay.switches;
+    o->dest_switches = D.d.switches;
+    o->relay_flags = relay.flags;
+    o->dest_flags = D.d.flags;
+    o->rate1 = venc.rate1;
+    o->rate1_n = venc.rate1_n;
+    o->rate2 = D.io.rate2;
+    o->rate2_n = D.io.rate2_n;
+    or_encoder_free(venc.cur);
+    or_encoder_free(venc.old);
+    os_dsw_free(relay.main);
+    os_dsw_free(relay.nw);
+    os_dsw_free(D.d.main);
+    os_dsw_free(D.d.nw);
+    free(D.io.buffer);
+    free(D.io.temp);
+    free(ectx.payload);
+    free(est);
+    free(bg);
+    free(dest);
+    free(dbg);
+    free(payload);
+    free(pkt);
+    free(word);
+    free(rpkt);
+    free(tmp_cur);
+    free(tmp_old);
+    return rc;
 }

@@ -117,6 +117,37 @@ int64_t or_vr_run(int max_payload, int T, int B, int N, int mds, const uint8_t *
                   int64_t P, uint64_t seed, int *out_len, uint8_t *out_data, uint8_t *packets,
                   int64_t packets_cap, int64_t *packet_off, int64_t max_sent, int64_t *stats, double *coding_rate);
 
+/* The two-hop adaptive relay session (RELAYING_TYPE 2 / 3, application_local_simulation.cpp:71-593
+ * with FLAG_FOR_CONSTANT_TRANS = 1): Q seqs, hop erasure patterns e1 / e2 (received past their
+ * end), payloads or_fill_payload(seed).  Per-seq outputs (each array optional, Q entries):
+ * hop1_len / hop1_hdr[16] = the source's packet (16-byte header + VR frame); relay_len /
+ * relay_hdr[8] = the relay's packet to the destination (8-byte header + stored word);
+ * dest_proc = 1 when the destination's main object extracted an output at seq t (a received
+ * frame, or a missing seq before one), dest_flag its decode flag, dest_lost = calc_missed_chars'
+ * verdict on packet t - T_TOT, dest_out [Q][OR_SESSION_DW] = the extracted blocks*k bytes (zero
+ * beyond).  crc[ceil(Q/OR_SESSION_BLOCK)]: per block of seqs the CRC-32 of every seq's [hop-1
+ * len LE32][hop-1 packet][relay len LE32][relay packet]; crc2 (needs dest_out, dest_proc): of
+ * [proc][flag][lost][dest_out row].  Returns 0, -2 when hop-1 seq 0 is erased, -3 / -4 when a
+ * relay / destination call has no restatement (status_seq = the loop index). */
+#define OR_SESSION_DW 320
+#define OR_SESSION_BLOCK 100
+typedef struct {
+    int64_t Q;
+    int32_t *hop1_len;
+    uint8_t *hop1_hdr;
+    int32_t *relay_len;
+    uint8_t *relay_hdr;
+    uint8_t *dest_proc, *dest_flag, *dest_lost, *dest_out;
+    uint32_t *crc, *crc2;
+    uint8_t *hop1_pkts, *relay_pkts; /* optional: every packet at these strides (bytes past it zero) */
+    int64_t hop1_stride, relay_stride;
+    int64_t lost, src_switches, relay_switches, dest_switches, relay_flags, dest_flags, status_seq;
+    float rate1, rate2, min_rate;
+    int64_t rate1_n, rate2_n, min_rate_n;
+} or_session_out;
+int or_relay_session_run(int relay_type, int max_payload, int64_t Q, const uint8_t *e1, int64_t n_e1,
+                         const uint8_t *e2, int64_t n_e2, uint64_t seed, or_session_out *o);
+
 #ifdef __cplusplus
 }
 #endif
