@@ -67,19 +67,41 @@ def pmc_traffic(kernel_symbol):
     return best
 
 
-def rocprof_kernel_time(kernel_symbol):
-    """Average duration (ns) of `kernel_symbol` per launch from the newest committed rocprofv3
-    --kernel-trace --stats summary of the bench command (profiles/*/*_kernel_time.json, made by
-    tools/kernel_time.py).  Returns (avg_ns, source, fresh) like pmc_traffic, or None."""
+def rocprof_child(argv, symbols, keep_dir=None, timeout=300):
+    """This bench's own step, re-run as a child process under `rocprofv3 --kernel-trace --stats`
+    (--rocprof-child: warm-up and timed steps only, no other legs): the average duration of each
+    kernel in `symbols` as the profiler sees it on this box, in this invocation -- the roofline's
+    kernel time.  Returns ({symbol: {"avg_us", "calls", "min_us", "max_us"}}, info) or (None, reason)."""
+    import csv
     import glob
-    best = None
-    digest = kernel_sources_digest()
-    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*", "*_kernel_time.json"))):
-        with open(path) as f:
-            entry = json.load(f).get(kernel_symbol)
-        if entry:
-            best = (entry["avg_ns"], os.path.relpath(path, ROOT), entry.get("sources_sha256") == digest)
-    return best
+    import shutil
+    import subprocess
+    import tempfile
+    prof = shutil.which("rocprofv3") or "/opt/rocm/bin/rocprofv3"
+    if not os.path.exists(prof):
+        return None, "rocprofv3 not found"
+    out = keep_dir or tempfile.mkdtemp(prefix="bench_rocprof_", dir="/tmp")
+    os.makedirs(out, exist_ok=True)
+    env = dict(os.environ, TMPDIR="/tmp")
+    cmd = [prof, "--kernel-trace", "--stats", "--output-format", "csv", "-d", out, "-o", "bench", "--",
+           sys.executable, os.path.abspath(__file__)] + argv + ["--rocprof-child"]
+    try:
+        r = subprocess.run(cmd, cwd="/tmp", env=env, capture_output=True, text=True, timeout=timeout)
+    except subprocess.TimeoutExpired:
+        return None, f"rocprofv3 child timed out after {timeout} s"
+    stats = sorted(glob.glob(os.path.join(out, "**", "*kernel_stats.csv"), recursive=True))
+    if r.returncode != 0 or not stats:
+        return None, f"rocprofv3 child exit {r.returncode}: {(r.stderr or r.stdout)[-400:]}"
+    res = {}
+    for row in csv.DictReader(open(stats[-1])):
+        name = row["Name"].split("(")[0].replace("void ", "").replace("fec::", "").strip()
+        for sym in symbols:
+            if sym and name == sym:
+                res[sym] = {"avg_us": float(row["AverageNs"]) / 1e3, "calls": int(row["Calls"]),
+                            "min_us": float(row["MinNs"]) / 1e3, "max_us": float(row["MaxNs"]) / 1e3}
+    if not keep_dir:
+        shutil.rmtree(out, ignore_errors=True)
+    return res, os.path.relpath(stats[-1], ROOT) if keep_dir else "temporary"
 
 
 def cpu_baseline(T, B, N, packets, rank_pattern, threads=None):
@@ -743,6 +765,12 @@ def main():
                          "disjoint output rows)")
     ap.add_argument("--launch-selftest", action="store_true",
                     help="CPU test of the --gpus launcher: ranks rendezvous over gloo, no GPU work")
+    ap.add_argument("--rocprof-child", action="store_true",
+                    help="(internal) the step alone under rocprofv3, started by this bench for its roofline")
+    ap.add_argument("--no-rocprof", action="store_true",
+                    help="take the roofline's kernel time from HIP events only (no rocprofv3 child run)")
+    ap.add_argument("--rocprof-keep", default=None,
+                    help="keep the rocprofv3 child's output (kernel_stats.csv) in this directory")
     args = ap.parse_args()
     T, B, N = map(int, args.tbn.split(","))
     # The library's run-time settings in effect are recorded in the line (`env`); a setting that
@@ -893,6 +921,9 @@ def main():
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     elapsed = max_over_ranks(elapsed, dist, comm_dev)
+    if args.rocprof_child:  # the profiled child: the step's kernels only
+        print(json.dumps({"rocprof_child": True, "ms_per_step": elapsed / args.steps * 1e3}), flush=True)
+        return
 
     # correctness of the timed work (outside the timed region): round trip + planner agreement
     eps, rec, lost = codec.counters()
@@ -948,11 +979,10 @@ def main():
     b2b = {"fec_encode_kernel": back_to_back(lambda: codec.encode(payload, out=cw, out_len=wl)),
            "fec_copy_kernel": back_to_back(lambda: codec.copy(cw, er, out=out, out_len=ol))}
     algo = {"fec_encode_kernel": (L + codec.CW) * Pf, "fec_copy_kernel": (codec.CW + 1 + L) * P}
-    # The roofline's duration is the in-step one (the event pair around each launch of the timed
-    # step's kernels, above): the kernel in the context it is timed in.  It still includes the
-    # event packets (an upper bound on the kernel: rocprofv3's in-step average is ~10 % lower); the
-    # kernel alone back to back is slower than in the step (the copy's non-temporal traffic leaves
-    # the caches to the encoder there).
+    # The event figure's duration is the in-step one (the event pair bound to each launch of the
+    # step's kernels, above): the kernel in the context it is timed in; the kernel alone back to
+    # back is slower than in the step (the copy's non-temporal traffic leaves the caches to the
+    # encoder there).
     dominant = max(algo, key=lambda k: per_launch[k])
     achieved = algo[dominant] / (per_launch[dominant] * 1e-3) / 1e9
 
@@ -999,31 +1029,36 @@ def main():
         }
         info = codec.info()
         symbol = info["encode_kernel"] if dominant == "fec_encode_kernel" else info.get("copy_kernel")
-        tr = pmc_traffic(symbol) if symbol and P == 1_000_000 else None
-        result["roofline"].update(algorithmic_bytes=algo[dominant], traffic_kernel=symbol)
-        if tr and tr[2]:
-            result["roofline"].update(traffic=tr[0], traffic_unit="bytes per launch",
-                                      traffic_source=tr[1])
-        elif tr:
-            result["roofline"].update(traffic_stale=f"{tr[1]} was measured on other kernel sources")
-        # the same kernel's average duration under rocprofv3 (the bench command itself, committed
-        # summary): the kernel without the event packets around each launch
-        kt = rocprof_kernel_time(symbol) if symbol and P == 1_000_000 else None
-        # primary achieved / frac: the committed rocprofv3 summary of this bench command when it was
-        # measured on the current kernel sources (the kernel alone, as profiles/ shows it); else the
-        # event timing above (which includes the event packets around each launch)
+        result["roofline"].update(algorithmic_bytes=algo[dominant])
+        # The kernel time of the roofline: this invocation's own rocprofv3 trace of the same step
+        # (a child process of this bench, on this box, on these sources), dominant kernel = the
+        # slower of the two byte kernels by it; the HIP-event figure (events bound to each launch,
+        # hipExtLaunchKernel) is reported beside it.  --no-rocprof: the event figure alone.
         rf = result["roofline"]
-        rf.update(achieved_event=rf["achieved"], frac_event=rf["frac"])
-        if kt and kt[2]:
-            a_rp = algo[dominant] / (kt[0] * 1e-9) / 1e9
-            rf.update(rocprof_avg_us=round(kt[0] / 1e3, 2), achieved_rocprof=round(a_rp, 1),
-                      frac_rocprof=round(a_rp / HBM_PEAK_GBS, 4), rocprof_source=kt[1],
-                      achieved=round(a_rp, 1), frac=round(a_rp / HBM_PEAK_GBS, 4),
-                      frac_source=f"rocprofv3 kernel average ({kt[1]})")
+        rf.update(achieved_event=rf["achieved"], frac_event=rf["frac"], kernel_event=dominant)
+        sym = {"fec_encode_kernel": info["encode_kernel"], "fec_copy_kernel": info.get("copy_kernel")}
+        kt, kinfo = (None, "--no-rocprof") if args.no_rocprof or P != 1_000_000 else rocprof_child(
+            [a for a in sys.argv[1:] if a not in ("--rocprof-child",)], list(sym.values()), args.rocprof_keep)
+        if kt and all(v in kt for v in sym.values() if v):
+            dom = max((k for k in sym if sym[k]), key=lambda k: kt[sym[k]]["avg_us"])
+            a_rp = algo[dom] / (kt[sym[dom]]["avg_us"] * 1e-6) / 1e9
+            rf.update(kernel=dom, achieved=round(a_rp, 1), frac=round(a_rp / HBM_PEAK_GBS, 4),
+                      algorithmic_bytes=algo[dom], rocprof_avg_us=round(kt[sym[dom]]["avg_us"], 2),
+                      frac_source="rocprofv3 --kernel-trace --stats of this bench's step, run by this "
+                                  "invocation as a child process (" + kinfo + ")",
+                      rocprof_kernels_us={k: round(kt[v]["avg_us"], 2) for k, v in sym.items() if v},
+                      rocprof_calls={k: kt[v]["calls"] for k, v in sym.items() if v})
+            symbol = sym[dom]
         else:
-            rf.update(frac_source="event timing (no rocprofv3 summary of the current kernel sources)")
-            if kt:
-                rf.update(rocprof_stale=f"{kt[1]} was measured on other kernel sources")
+            rf.update(frac_source="HIP events bound to each launch (rocprofv3 child: " + str(kinfo) + ")")
+        # HBM traffic per launch from the committed FETCH_SIZE / WRITE_SIZE passes of this command,
+        # only when they were measured on the current sources
+        tr = pmc_traffic(symbol) if symbol and P == 1_000_000 else None
+        rf.update(traffic=None, traffic_kernel=symbol)
+        if tr and tr[2]:
+            rf.update(traffic=tr[0], traffic_unit="bytes per launch", traffic_source=tr[1])
+        elif tr:
+            rf.update(traffic_stale=f"{tr[1]} was measured on other kernel sources")
     if not args.no_host_inclusive:
         hi = host_inclusive(codec, payload, pat, er, cw, wl, out, ol, P, Pf, world, barrier,
                             lambda x: max_over_ranks(x, dist, comm_dev),

@@ -139,7 +139,17 @@ def lib() -> ctypes.CDLL:
     L.fec_relay_vr_destroy.argtypes = [vp]
     L.fec_relay_vr_geometry.argtypes = [vp, ip, ip, ip]
     L.fec_relay_vr_run.argtypes = [vp, vp, vp, vp, vp, vp, vp, vp, vp]
-    for name in ["fec_sdswdf_create", "fec_sdswdf_destroy", "fec_sdswdf_geometry", "fec_sdswdf_relay_batch",
+    L.fec_relay_session_create.argtypes = [i32, i32, i64, vp, i64, vp, i64, ctypes.POINTER(vp)]
+    L.fec_relay_session_destroy.argtypes = [vp]
+    L.fec_relay_session_info.argtypes = [vp, vp, vp]
+    L.fec_relay_session_relay_offsets.argtypes = [vp, vp]
+    L.fec_relay_session_hop1_headers.argtypes = [vp, vp]
+    L.fec_relay_session_dest_meta.argtypes = [vp, vp, vp]
+    L.fec_relay_session_run.argtypes = [vp, vp, vp, vp, vp, vp, vp]
+    L.fec_relay_session_hop1.argtypes = [vp, vp, i64, vp, vp]
+    for name in ["fec_relay_session_create", "fec_relay_session_destroy", "fec_relay_session_info",
+                 "fec_relay_session_relay_offsets", "fec_relay_session_hop1_headers", "fec_relay_session_dest_meta",
+                 "fec_relay_session_run", "fec_relay_session_hop1", "fec_sdswdf_create", "fec_sdswdf_destroy", "fec_sdswdf_geometry", "fec_sdswdf_relay_batch",
                  "fec_sdswdf_destination_batch", "fec_sdswdf_relay_plan", "fec_sdswdf_dest_plan",
                  "fec_sdswdf_relay_batch_starts", "fec_sdswdf_destination_batch_starts", "fec_relay_vr_create",
                  "fec_relay_vr_destroy", "fec_relay_vr_geometry", "fec_relay_vr_run",

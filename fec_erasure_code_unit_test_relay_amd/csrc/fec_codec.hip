@@ -1,5 +1,6 @@
 // fec_codec.hip -- codec objects, launchers and the C ABI declared in include/fec_amd.h.
 #include <hip/hip_runtime.h>
+#include <hip/hip_ext.h>
 
 #include <algorithm>
 #include <atomic>
@@ -119,6 +120,21 @@ struct fec_codec {
     }
     int end(hipEvent_t stop, hipStream_t s) {
         if (stop) HIP_TRY(hipEventRecord(stop, s));
+        return FEC_OK;
+    }
+    // A launch whose timing events (when on) are bound to the dispatch itself (hipExtLaunchKernel's
+    // start / stop events) rather than recorded around it as separate stream packets: the pair then
+    // brackets the kernel, not the queue's gap in front of it (tools/ubench/event_timing.hip).
+    int launch(int kernel, const void* fn, dim3 grid, dim3 block, void** args, size_t lds, hipStream_t s) {
+        if (!timing) {
+            HIP_TRY(hipLaunchKernel(fn, grid, block, args, lds, s));
+            return FEC_OK;
+        }
+        EventPair e{kernel, nullptr, nullptr};
+        HIP_TRY(hipEventCreate(&e.a));
+        HIP_TRY(hipEventCreate(&e.b));
+        events.push_back(e);
+        HIP_TRY(hipExtLaunchKernel(fn, grid, block, args, lds, s, e.a, e.b, 0));
         return FEC_OK;
     }
 };
@@ -370,12 +386,9 @@ int launch_encode_tile(fec_codec* c, const uint8_t* d_payload, const int32_t* d_
     a.nt = 2;
     if (const char* v = std::getenv("FEC_TILE_NT")) a.nt = std::atoi(v) & 3;
     const int64_t blocks = (ntiles + tpw - 1) / tpw;
-    hipEvent_t stop;
-    if (int st = c->begin(FEC_KERNEL_ENCODE, s, &stop)) return st;
     void* args[] = {&a};
-    HIP_TRY(hipLaunchKernel(c->tile_kernel, dim3(static_cast<unsigned>(blocks)), dim3(256), args,
-                            d_len ? c->tile_lds_len : c->tile_lds, s));
-    return c->end(stop, s);
+    return c->launch(FEC_KERNEL_ENCODE, c->tile_kernel, dim3(static_cast<unsigned>(blocks)), dim3(256), args,
+                     d_len ? c->tile_lds_len : c->tile_lds, s);
 }
 
 int launch_encode(fec_codec* c, const uint8_t* d_payload, const int32_t* d_len, int64_t history,
@@ -517,6 +530,15 @@ int launch_plan(fec_codec* c, const uint8_t* d_er, int64_t P, void* d_ws, size_t
     return c->end(stop, s);
 }
 
+// The two-tiles-per-workgroup copy for this codec, or null: the one test launch_copy and
+// fec_codec_info both use (nt = the copy's non-temporal loads, which the paired kernel needs).
+const void* copy_pair_kernel(const fec_codec* c, bool nt) {
+    const char* pv = std::getenv("FEC_COPY_PAIR");
+    if ((pv && pv[0] == '0') || !nt || !c->copy_fast) return nullptr;
+    if (16 + c->copyf_tp * c->g.CW + 16 > 6 * 16 * 256) return nullptr;  // the stage of one tile in registers
+    return fec::fec_copy_pair_kernel_for(c->g.k, c->g.n - c->g.k);
+}
+
 int launch_copy(fec_codec* c, const uint8_t* d_cw, const uint8_t* d_er, int64_t P, uint8_t* d_out,
                 int32_t* d_outlen, hipStream_t s, bool skip_erased = false) {
     const Geometry& g = c->g;
@@ -551,25 +573,19 @@ int launch_copy(fec_codec* c, const uint8_t* d_cw, const uint8_t* d_er, int64_t 
         // padded staging made the step 2.2 % slower in the same process, 0.3228 vs 0.3157 ms:
         // profiles/r03/r03v_copy_row_pad_*.txt.  2-way conflicts cost one LDS cycle per 32-lane
         // group; the copy is bound by its HBM traffic and load latency, not by the LDS.)
-        // two tiles per workgroup (FEC_COPY_PAIR=1): the stage of one tile must fit the registers
-        // two tiles per workgroup, the second one's loads in flight while the first is converted:
-        // 0.3055 vs 0.3126 ms per step, copy 143.6 vs 151.5 us in the step
-        // (profiles/r05/headline/r05zu_copy_pair_ab.txt); FEC_COPY_PAIR=0: one tile per workgroup
-        const char* pv = std::getenv("FEC_COPY_PAIR");
-        const bool pair = !(pv && pv[0] == '0');
-        const void* pk = (pair && fa.nt && 16 + fa.TP * g.CW + 16 <= 6 * 16 * 256)
-                             ? fec::fec_copy_pair_kernel_for(g.k, g.n - g.k) : nullptr;
+        // two tiles per workgroup, the second one's loads in flight while the first is converted
+        // (copy_pair_kernel: when the stage of one tile fits the registers): 0.3055 vs 0.3126 ms per
+        // step, copy 143.6 vs 151.5 us in the step (profiles/r05/headline/r05zu_copy_pair_ab.txt);
+        // FEC_COPY_PAIR=0: one tile per workgroup
+        const void* pk = copy_pair_kernel(c, fa.nt != 0);
         const int64_t tiles = (Pout + fa.TP - 1) / fa.TP;
         const int64_t blocks = pk ? (tiles + 1) / 2 : tiles;
         // 256 threads (one per (packet, group) item of the tile rounded up to waves, 320 at (10,3,3),
         // measured slower in the step: 0.3402 vs 0.3235 ms, profiles/r03/r03y_copy_threads_ab.txt)
         const int nthr = 256;
-        hipEvent_t stop;
-        if (int st = c->begin(FEC_KERNEL_DEC_COPY, s, &stop)) return st;
         void* args[] = {&fa};
-        HIP_TRY(hipLaunchKernel(pk ? pk : c->copy_fast, dim3(static_cast<unsigned>(blocks)), dim3(nthr), args,
-                                c->copyf_lds(fa.TP), s));
-        return c->end(stop, s);
+        return c->launch(FEC_KERNEL_DEC_COPY, pk ? pk : c->copy_fast, dim3(static_cast<unsigned>(blocks)), dim3(nthr),
+                         args, c->copyf_lds(fa.TP), s);
     }
     fec::CopyArgs ca;
     ca.cw = d_cw;
@@ -1021,10 +1037,8 @@ int fec_codec_info(const fec_codec* c, char* buf, size_t size) {
     else
         std::snprintf(enc, sizeof(enc), "fec_encode_kernel");
     char cpy[64];
-    const char* pv = std::getenv("FEC_COPY_PAIR");
     const char* ntv = std::getenv("FEC_COPY_NT");
-    const bool pair = !(pv && pv[0] == '0') && !(ntv && !std::atoi(ntv)) &&
-                      16 + c->copyf_tp * c->g.CW + 16 <= 6 * 16 * 256 && fec::fec_copy_pair_kernel_for(c->g.k, np);
+    const bool pair = copy_pair_kernel(c, !(ntv && !std::atoi(ntv))) != nullptr;
     if (c->copy_fast && c->copy_path != 1 && pair)
         std::snprintf(cpy, sizeof(cpy), "fec_copy_pair_kernel<%d, %d>", c->g.k, np);
     else if (c->copy_fast && c->copy_path != 1)

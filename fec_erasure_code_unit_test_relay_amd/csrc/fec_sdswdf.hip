@@ -364,6 +364,9 @@ private:
             // before the first packet) is a zero symbol; positions past the current packet are
             // not filled (stale in the reference, never forwarded)
             const int filled = symInd >= 0 ? n - symInd : n;
+            // n2 > n (the two-hop session): the selection may read temp_codeword[i] for n <= i < n2,
+            // past the reference's VLA (:367): a zero symbol here, as in the oracle
+            for (int p = n; p < n2; ++p) vec_zero(tc[p], n);
             for (int p = 0; p < n; ++p) {
                 const int slot = p + symInd + 2 * TT - n + 1;
                 if (p < filled && valid_[slot]) vec_unit(tc[p], n, p);
@@ -983,6 +986,32 @@ struct DevBuf {
 };
 
 }  // namespace
+
+// Per-call planning on explicit state for the two-hop session (fec_session.hip): one planner per
+// geometry, kept for the process (the drop-in methods keep theirs in SwCtx).
+int sd_relay_plan_state(int k, int n, int n2, int sdbo, const uint8_t* er, int* const* header, uint8_t* rec) {
+    static std::mutex mu;
+    static std::map<std::tuple<int, int, int, int>, std::unique_ptr<SdRelayPlanner>> pls;
+    if (k < 1 || n < k || n > kHdr || n2 < k || n2 > kHdr || (sdbo != 0 && sdbo != 1)) return FEC_ERR_ARG;
+    std::lock_guard<std::mutex> lk(mu);
+    auto& pl = pls[std::make_tuple(k, n, n2, sdbo)];
+    if (!pl)
+        pl.reset(new SdRelayPlanner(k, n, n2, sdbo, shared_decode_rules(n - 1, n - k, n - k),
+                                    make_generator(n2 - 1, n2 - k, n2 - k)));
+    pl->plan_state(er, header, rec);
+    return FEC_OK;
+}
+int sd_relay_record_bytes(int n, int n2) { return kHdr + n2 * n; }
+int sd_dest_plan_state(int k, int n, int* const* header, uint8_t* rec, bool* flag) {
+    static std::mutex mu;
+    static std::map<std::pair<int, int>, std::unique_ptr<SdDestPlanner>> pls;
+    if (k < 1 || n < k || n > kHdr) return FEC_ERR_ARG;
+    std::lock_guard<std::mutex> lk(mu);
+    auto& pl = pls[std::make_pair(k, n)];
+    if (!pl) pl.reset(new SdDestPlanner(k, n, shared_decode_rules(n - 1, n - k, n - k)));
+    *flag = pl->plan_state(header, rec);
+    return FEC_OK;
+}
 }  // namespace fec
 
 struct fec_sdswdf {

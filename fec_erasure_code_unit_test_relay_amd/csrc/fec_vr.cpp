@@ -1297,6 +1297,7 @@ struct fec_vr_plan {
     // (re)plans; the per-packet arrays are rewritten only once their last copy has left them
     void run(int max_payload, int T, int B, int N, bool mds, const uint8_t* erasure, int64_t n_erasure, int64_t P,
              bool async);
+    void set_layout();  // the compact row layout of plan.enc (after run, or for a schedule set from outside)
 };
 
 namespace {
@@ -1630,6 +1631,10 @@ void fec_vr_plan::run(int max_payload, int T, int B, int N, bool mds, const uint
                       int64_t P, bool async) {
     if (pk_sent) (void)hipEventSynchronize(pk_sent);
     plan.run(max_payload, T, B, N, mds, erasure, n_erasure, P, async);
+    set_layout();
+}
+
+void fec_vr_plan::set_layout() {
     cw_max = 0;
     for (const auto& e : plan.enc) cw_max = std::max(cw_max, cw_of(plan, e));
     for (const auto& d : plan.dec) cw_max = std::max(cw_max, cw_of(plan, d));
@@ -1679,6 +1684,33 @@ int ensure_rowoff(fec_vr_plan* v, hipStream_t s) {
 const int64_t* cur_off(const fec_vr_plan* v) { return static_cast<const int64_t*>(v->d_rowoff); }
 const int64_t* old_off(const fec_vr_plan* v) { return static_cast<const int64_t*>(v->d_rowoff) + v->plan.sent + 1; }
 }  // namespace
+
+namespace fec {
+// An encoder schedule built outside VrPlan's P2P loop (the two-hop session, fec_session.hip): its
+// instances go through the same batched encoder and compact layout.
+int vr_plan_from_instances(int max_payload, const std::vector<VrInstance>& enc, int64_t sent, fec_vr_plan** out) {
+    if (!out || enc.empty() || sent < 1) return FEC_ERR_ARG;
+    *out = nullptr;
+    return vr_guarded([&] {
+        std::unique_ptr<fec_vr_plan> v(new fec_vr_plan());
+        v->plan.L = max_payload;
+        v->plan.enc = enc;
+        v->plan.sent = sent;
+        v->plan.P = sent;
+        v->set_layout();
+        *out = v.release();
+        return FEC_OK;
+    });
+}
+// The device per-row offsets of the compact layout ([sent+1] each), built on first use on `s`.
+int vr_plan_device_offsets(fec_vr_plan* v, void* s, const int64_t** cur_offs, const int64_t** old_offs) {
+    if (!v) return FEC_ERR_ARG;
+    if (int st = vr_guarded([&] { return ensure_rowoff(v, static_cast<hipStream_t>(s)); })) return st;
+    *cur_offs = cur_off(v);
+    *old_offs = old_off(v);
+    return FEC_OK;
+}
+}  // namespace fec
 
 extern "C" {
 

@@ -32,6 +32,8 @@
 
 #include "fec_host.h"
 
+struct fec_vr_plan;  // the C ABI's plan handle (fec_vr.cpp)
+
 namespace fec {
 
 // Parameter_Estimator (src/Parameter_Estimator.cpp:21-223), RELAYING_TYPE 0.
@@ -338,5 +340,10 @@ int vr_launch_recover(const VrRecArgs& a, void* s);
 int vr_launch_decode(const VrCopyArgs& a, const VrRecArgs& ra, void* s);
 // dynamic LDS of the closed-form leftovers' workgroup (fec_vr_encode_cf_kernel, fec_vr_cf.h)
 size_t vr_encode_cf_lds(const VrEncodeArgs& a);
+
+// A schedule of encoder instances from outside the P2P loop (fec_session.hip) as a plan handle of
+// the C ABI (fec_vr_encode_batch, fec_vr_plan_layout, fec_vr_plan_destroy); its device row offsets.
+int vr_plan_from_instances(int max_payload, const std::vector<VrInstance>& enc, int64_t sent, fec_vr_plan** out);
+int vr_plan_device_offsets(fec_vr_plan* v, void* s, const int64_t** cur_off, const int64_t** old_off);
 
 }  // namespace fec

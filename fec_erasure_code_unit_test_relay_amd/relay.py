@@ -262,6 +262,86 @@ class AdaptiveRelay:
         return frames, flen, out, flags
 
 
+class RelaySession:
+    """The two-hop adaptive relay session (RELAYING_TYPE 2 / 3 with N_INITIAL = N_INITIAL_2 = -1,
+    application_local_simulation.cpp:71-593): source (Application_Layer_Sender with the relay's
+    12-byte feedback, the relay-mode Variable_Rate_FEC_Encoder) -> hop 1 -> relay
+    (receive_message_and_symbol_wise_encode + send_sym_wise_message) -> hop 2 -> destination
+    (receive_message_and_symbol_wise_decode), for Q seqs over the hop patterns e1 / e2
+    (fec_relay_session_* in include/fec_amd.h).  The control plane runs at construction (host, on
+    the patterns alone); run() does the session's byte work on the GPU."""
+
+    DW = 320  # destination output row
+
+    def __init__(self, relay_type: int, Q: int, e1, e2, max_payload: int = 300):
+        import numpy as np
+        a = np.ascontiguousarray(np.asarray(e1, dtype=np.uint8))
+        b = np.ascontiguousarray(np.asarray(e2, dtype=np.uint8))
+        h = ctypes.c_void_p()
+        check(lib().fec_relay_session_create(relay_type, max_payload, Q, a.ctypes.data_as(ctypes.c_void_p), a.size,
+                                             b.ctypes.data_as(ctypes.c_void_p), b.size, ctypes.byref(h)),
+              "fec_relay_session_create")
+        self._h = h
+        self.type, self.Q, self.L = relay_type, Q, max_payload
+        st = np.zeros(16, np.int64)
+        rt = np.zeros(4, np.float64)
+        check(lib().fec_relay_session_info(h, st.ctypes.data_as(ctypes.c_void_p), rt.ctypes.data_as(ctypes.c_void_p)),
+              "fec_relay_session_info")
+        keys = ("Q", "relay_bytes", "src_switches", "relay_switches", "dest_switches", "dest_flags", "relay_calls",
+                "lineages", "dest_outputs", "processed", "symbol_bytes", "encoder_instances", "longest_lineage",
+                "relay_flags", "rate1_n", "rate2_n")
+        self.stats = {k: int(v) for k, v in zip(keys, st)}
+        self.stats.update(rate1=float(rt[0]), rate2=float(rt[1]), min_rate=float(rt[2]), control_ms=float(rt[3]))
+        self.relay_off = np.zeros(Q + 1, np.int64)
+        check(lib().fec_relay_session_relay_offsets(h, self.relay_off.ctypes.data_as(ctypes.c_void_p)),
+              "fec_relay_session_relay_offsets")
+        self.hop1_hdr = np.zeros((Q, 16), np.uint8)
+        check(lib().fec_relay_session_hop1_headers(h, self.hop1_hdr.ctypes.data_as(ctypes.c_void_p)),
+              "fec_relay_session_hop1_headers")
+        self.proc = np.zeros(Q, np.uint8)
+        self.flag = np.zeros(Q, np.uint8)
+        check(lib().fec_relay_session_dest_meta(h, self.proc.ctypes.data_as(ctypes.c_void_p),
+                                                self.flag.ctypes.data_as(ctypes.c_void_p)), "fec_relay_session_dest_meta")
+
+    def __del__(self):
+        if getattr(self, "_h", None):
+            try:
+                lib().fec_relay_session_destroy(self._h)
+            except Exception:
+                pass
+            self._h = None
+
+    def run(self, payload, relay=None, out=None, lost=None, count=None):
+        """payload [Q, L] uint8 on the GPU -> (relay packets [relay_bytes] (packet t at
+        relay_off[t]..relay_off[t+1]), destination outputs [Q, 320], lost flags [Q], lost count [1])."""
+        import torch
+        assert payload.dtype == torch.uint8 and payload.is_cuda and payload.is_contiguous()
+        assert tuple(payload.shape) == (self.Q, self.L)
+        dev = payload.device
+        if relay is None:
+            relay = torch.empty(int(self.relay_off[-1]), dtype=torch.uint8, device=dev)
+        if out is None:
+            out = torch.empty((self.Q, self.DW), dtype=torch.uint8, device=dev)
+        if lost is None:
+            lost = torch.empty(self.Q, dtype=torch.uint8, device=dev)
+        if count is None:
+            count = torch.empty(1, dtype=torch.int64, device=dev)
+        stream = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+        check(lib().fec_relay_session_run(self._h, _ptr(payload), _ptr(relay), _ptr(out), _ptr(lost), _ptr(count),
+                                          stream), "fec_relay_session_run")
+        return relay, out, lost, count
+
+    def hop1_packets(self, stride: int):
+        """After run(): the source's wire packets [Q, stride] (16-byte header + VR frame, zero padded)
+        and their sizes [Q]."""
+        import torch
+        pk = torch.empty((self.Q, stride), dtype=torch.uint8, device="cuda")
+        ln = torch.empty(self.Q, dtype=torch.int32, device="cuda")
+        stream = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+        check(lib().fec_relay_session_hop1(self._h, _ptr(pk), stride, _ptr(ln), stream), "fec_relay_session_hop1")
+        return pk, ln
+
+
 def relay_digest(frames, frame_len, out, flags, block: int = 100):
     """Per block of ``block`` seqs the CRC-32 of every seq's [frame_len LE32][frame][out][flag]
     (as tests/cpp/relay_dropin_test.cpp --digest writes for the reference-structured driver)."""

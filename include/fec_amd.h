@@ -392,6 +392,48 @@ int fec_relay_vr_geometry(const fec_relay_vr *r, int *frame_stride, int *out_str
 int fec_relay_vr_run(fec_relay_vr *r, const uint8_t *d_payload, const uint8_t *h_e1, const uint8_t *h_e2,
                      uint8_t *d_frames, int32_t *d_frame_len, uint8_t *d_out, uint8_t *h_flag, void *hip_stream);
 
+/* ---- the two-hop adaptive relay session (RELAYING_TYPE 2 / 3, N_INITIAL = N_INITIAL_2 = -1) -------
+ * application_local_simulation.cpp:71-593 with FLAG_FOR_CONSTANT_TRANS = 1, replacing the loop of
+ * Application_Layer_Sender::generate_message_and_encode (:64-282: the 12-byte feedback, the split
+ * T = T_TOT - N2, T2 = T_TOT - N), Variable_Rate_FEC_Encoder::encode in relay mode
+ * (Variable_Rate_FEC_Encoder.cpp:74-235), Application_Layer_Receiver::receive_message_and_symbol_
+ * wise_encode / _decode (Application_Layer_Receiver.cpp:56-319, the relay-mode estimators,
+ * Parameter_Estimator.cpp:72-75), Variable_Rate_FEC_Decoder's relay and destination paths
+ * (Variable_Rate_FEC_Decoder.cpp:542-1879) and send_sym_wise_message (Application_Layer_Sender.cpp:
+ * 284-346).  The control flow runs on the host at create (it depends on the hop erasure patterns
+ * only); run does the byte work of the whole session on the GPU.
+ *   fec_relay_session_create: relay_type 2 or 3, Q seqs (the reference's loop runs to seq
+ *     NUMBER_OF_ITERATIONS + T_TOT + T2 - 1), hop patterns e1 / e2 (received past their end; e1[0]
+ *     must be 0).
+ *   fec_relay_session_info: stats[16] = {Q, relay_bytes, source switches, relay switches,
+ *     destination switches, destination flags, relay calls, lineages, destination outputs,
+ *     processed seqs, symbol bytes, encoder instances, longest lineage, relay flags, rate1 count,
+ *     rate2 count}; rates[4] = {sum of first-hop rates, of second-hop rates, of min rates, control
+ *     plane ms} (the reference's float sums, in its order).
+ *   fec_relay_session_relay_offsets: off[Q+1], relay packet t at d_relay[off[t], off[t+1]).
+ *   fec_relay_session_hop1_headers: hdr[Q][16], the source's packet headers (:222-244).
+ *   fec_relay_session_dest_meta: proc[Q] (1 = the destination's main object extracted an output at
+ *     seq t), flag[Q] (its decode flag).
+ *   fec_relay_session_run: d_payload Q rows of max_payload bytes (source packet t) -> d_relay
+ *     (relay_bytes: every relay packet, 8-byte header + word), d_dest_out Q rows of 320 bytes (the
+ *     extracted data_with_header of packet t - T_TOT, zero where not processed), d_dest_lost Q
+ *     (calc_missed_chars, Variable_Rate_FEC_Decoder.cpp:2698-2792), *d_lost their count; async on
+ *     the stream.
+ *   fec_relay_session_hop1: after a run, the source's wire packets (16-byte header + VR frame) at
+ *     `stride`, zero padded, sizes in d_len. */
+typedef struct fec_relay_session fec_relay_session;
+int fec_relay_session_create(int relay_type, int max_payload, int64_t Q, const uint8_t *e1, int64_t n_e1,
+                             const uint8_t *e2, int64_t n_e2, fec_relay_session **out);
+int fec_relay_session_destroy(fec_relay_session *h);
+int fec_relay_session_info(const fec_relay_session *h, int64_t *stats, double *rates);
+int fec_relay_session_relay_offsets(const fec_relay_session *h, int64_t *off);
+int fec_relay_session_hop1_headers(const fec_relay_session *h, uint8_t *hdr);
+int fec_relay_session_dest_meta(const fec_relay_session *h, uint8_t *proc, uint8_t *flag);
+int fec_relay_session_run(fec_relay_session *h, const uint8_t *d_payload, uint8_t *d_relay, uint8_t *d_dest_out,
+                          uint8_t *d_dest_lost, int64_t *d_lost, void *hip_stream);
+int fec_relay_session_hop1(fec_relay_session *h, uint8_t *d_packets, int64_t stride, int32_t *d_len,
+                           void *hip_stream);
+
 /* ---- relay per call: the Decoder_Symbol_Wise methods on caller-held state ---------------------
  * What siphon::Decoder_Symbol_Wise (fec_amd_dropin.h) calls: one reference method call each, on
  * the arrays the reference's callers fill (Variable_Rate_FEC_Decoder.cpp:950-1879).  The control
