@@ -80,7 +80,7 @@ def rocprof_child(argv, symbols, keep_dir=None, timeout=300):
     prof = shutil.which("rocprofv3") or "/opt/rocm/bin/rocprofv3"
     if not os.path.exists(prof):
         return None, "rocprofv3 not found"
-    out = keep_dir or tempfile.mkdtemp(prefix="bench_rocprof_", dir="/tmp")
+    out = os.path.abspath(keep_dir) if keep_dir else tempfile.mkdtemp(prefix="bench_rocprof_", dir="/tmp")
     os.makedirs(out, exist_ok=True)
     env = dict(os.environ, TMPDIR="/tmp")
     cmd = [prof, "--kernel-trace", "--stats", "--output-format", "csv", "-d", out, "-o", "bench", "--",
@@ -464,6 +464,7 @@ def extra_configs(steps=5):
     res["multistream_10k"] = multistream(steps)
     res["relay_10_3"] = relay_chains(steps)
     res["relay_adaptive"] = relay_adaptive(steps)
+    res["relay_session"] = relay_session(steps)
     res["per_packet_api"] = per_packet_api()
     return res
 
@@ -604,6 +605,48 @@ def relay_adaptive(steps):
                            "unflagged": int((flags == 0).sum()), "verified": bool(ok)}
     res["note"] = ("one fixed-rate batch per code over its instances laid end to end (each behind zero rows), "
                    "planners reset per instance; host work (erasure gathers, type 3's planners) inside")
+    return res
+
+
+def relay_session(steps):
+    """The two-hop adaptive relay session (RELAYING_TYPE 2 and 3 with N_INITIAL = N_INITIAL_2 = -1,
+    application_local_simulation.cpp:71-593): the source splits T_TOT over the hops from the relay's
+    12-byte feedback, the relay re-encodes symbol-wise, the destination decodes; hop 1
+    bin/erasure.bin, hop 2 bin/erasure2.bin, Q = 360 020 seqs (the reference's loop to seq
+    NUMBER_OF_ITERATIONS + T + T2 - 1).  control_ms: the host control plane from scratch (the
+    session's every decision, symbolic); ms: one run of the session's byte work on the GPU (the
+    source's encoder instances, every relay call's symbols, the relay lineages, the destination's
+    outputs and loss check).  verified: the lost count and the control plane's totals equal the
+    oracle's committed run (tests/golden/relay_session_360k.json)."""
+    import json
+    import torch
+    from fec_erasure_code_unit_test_relay_amd import fill_payload
+    from fec_erasure_code_unit_test_relay_amd.relay import RelaySession
+    from fec_erasure_code_unit_test_relay_amd.streams import load_pattern
+    g = json.load(open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "tests", "golden",
+                                    "relay_session_360k.json")))
+    Q = g["Q"]
+    e1, e2 = load_pattern("bin_erasure"), load_pattern("bin_erasure2")
+    payload = fill_payload(0, Q, L, 0x5EED)
+    res = {"seqs": Q, "hops": "bin/erasure.bin, bin/erasure2.bin"}
+    for t in (2, 3):
+        t0 = time.perf_counter()
+        s = RelaySession(t, Q, e1, e2)
+        ctl = time.perf_counter() - t0
+        relay, out, lost, count = s.run(payload)
+        torch.cuda.synchronize()
+        dt = timed(lambda: s.run(payload, relay, out, lost, count), max(3, min(steps, 10)))
+        ref = g["types"][str(t)]
+        st = s.stats
+        ok = int(count.item()) == ref["lost"] and st["relay_bytes"] == ref["relay_bytes"] and \
+            st["src_switches"] == ref["src_switches"] and st["rate2"] == ref["rate2_sum"]
+        res[f"type{t}"] = {"ms": round(dt * 1e3, 3), "GiB_s": round(Q * L / dt / 2**30, 3),
+                           "control_ms": round(ctl * 1e3, 1), "lost": int(count.item()),
+                           "switches": st["src_switches"], "relay_calls": st["relay_calls"],
+                           "lineages": st["lineages"], "longest_lineage": st["longest_lineage"],
+                           "rate_first_hop": round(st["rate1"] / st["rate1_n"], 4),
+                           "rate_second_hop": round(st["rate2"] / st["rate2_n"], 4),
+                           "oracle_seconds_1_core": ref["oracle_seconds"], "verified": bool(ok)}
     return res
 
 

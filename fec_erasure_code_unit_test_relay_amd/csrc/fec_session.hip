@@ -40,6 +40,7 @@
 #include <memory>
 #include <stdexcept>
 #include <string>
+#include <unordered_map>
 #include <vector>
 
 #include "fec_amd.h"
@@ -240,6 +241,41 @@ struct SessionPlan {
 
 private:
     int32_t next_lineage = 0;
+    // memos of the per-call planning: a type-2 window's decode rows (by k, n, erasure mask), the
+    // type-2 parity coefficients (by k, n2), a state-dependent call's record (by geometry, flags and
+    // the header entries the selection reads)
+    std::unordered_map<uint64_t, std::pair<int32_t, bool>> rows_memo_;
+    std::unordered_map<uint32_t, int32_t> g2_memo_;
+    std::unordered_map<std::string, std::pair<int32_t, std::vector<uint8_t>>> sd_memo_;
+    std::string key_;
+    std::vector<uint8_t> rec_;
+    int32_t rows_coef(int k, int n, const uint8_t* er, bool* flag) {
+        uint64_t mask = 0;
+        for (int i = 0; i < n; ++i) mask |= static_cast<uint64_t>(er[i] ? 1 : 0) << i;
+        const uint64_t key = static_cast<uint64_t>(k) | static_cast<uint64_t>(n) << 8 | mask << 16;
+        auto it = rows_memo_.find(key);
+        if (it == rows_memo_.end()) {
+            uint8_t rows[kSMaxN * kSMaxN];
+            bool f;
+            decode_rows(k, n, er, rows, &f);
+            it = rows_memo_.emplace(key, std::make_pair(intern(rows, static_cast<size_t>(k) * n), f)).first;
+        }
+        *flag = it->second.second;
+        return it->second.first;
+    }
+    int32_t g2_coef(int k, int n2) {
+        const uint32_t key = static_cast<uint32_t>(k) | static_cast<uint32_t>(n2) << 8;
+        auto it = g2_memo_.find(key);
+        if (it != g2_memo_.end()) return it->second;
+        // parity position n2-1-delta = XOR_m G2[m][n2-1-delta] * row m+delta (:601-613)
+        const std::vector<uint8_t> G2 = make_generator(n2 - 1, n2 - k, n2 - k);
+        uint8_t g[kSMaxN * kSMaxN] = {};
+        for (int delta = 0; delta < n2 - k; ++delta)
+            for (int m = 0; m < k; ++m) g[delta * k + m] = G2[m * n2 + n2 - 1 - delta];
+        const int32_t at = intern(g, static_cast<size_t>(std::max(1, (n2 - k) * k)));
+        g2_memo_.emplace(key, at);
+        return at;
+    }
     std::unique_ptr<SymDsw> fresh() {
         std::unique_ptr<SymDsw> d(new SymDsw());
         d->lineage = next_lineage++;
@@ -297,37 +333,46 @@ int SessionPlan::relay_call(SymDsw& o, int k, int n, int k2, int n2, int64_t out
     c.type = static_cast<uint8_t>(R);
     c.blocks = blocks;
     if (R == 2) {
-        uint8_t rows[kSMaxN * kSMaxN];
-        decode_rows(k, n, o.er, rows, flag);
         for (int m = 0; m < n; ++m) rrefs.push_back(o.cv[m]);
         j.nout = static_cast<uint8_t>(k);
         j.nin = static_cast<uint8_t>(n);
         j.ostride = static_cast<uint8_t>(k);
-        j.coef = intern(rows, static_cast<size_t>(k) * n);
-        // parity position n2-1-delta = XOR_m G2[m][n2-1-delta] * row m+delta (:601-613)
-        const std::vector<uint8_t> G2 = make_generator(n2 - 1, n2 - k2, n2 - k2);
-        uint8_t g[kSMaxN * kSMaxN] = {};
-        for (int delta = 0; delta < n2 - k; ++delta)
-            for (int m = 0; m < k; ++m) g[delta * k + m] = G2[m * n2 + n2 - 1 - delta];
-        c.g2 = intern(g, static_cast<size_t>(std::max(1, (n2 - k) * k)));
+        j.coef = rows_coef(k, n, o.er, flag);
+        c.g2 = g2_coef(k, n2);
         d_bytes += static_cast<int64_t>(blocks) * k;
     } else {
         *flag = false;  // the relay's flag is never set (:195)
-        int* rows[kSSd];
-        for (int i = 0; i < kSSd; ++i) rows[i] = o.header[i];
-        std::vector<uint8_t> rec(static_cast<size_t>(kSHdr + n2 * n));
-        if (int st = sd_relay_plan_state(k, n, n2, 0, o.sder, rows, rec.data())) return st;
-        std::memcpy(hdr, rec.data(), kSHdr);
+        // the selection reads the window's flags (slots lo..2T) and header rows 0..n2-1 (rows
+        // 0..n2-2: entries < n2-1, row n2-1: rewritten entries < n2, the rest carried into the record)
+        const int lo = 2 * kST - n + 1 - (n2 - k);
+        key_.assign(1, static_cast<char>(k));
+        key_.push_back(static_cast<char>(n));
+        key_.push_back(static_cast<char>(n2));
+        for (int r = lo; r <= 2 * kST; ++r) key_.push_back(static_cast<char>(o.sder[r]));
+        for (int r = 0; r < n2; ++r)
+            for (int e = 0; e < kSHdr; ++e) key_.push_back(static_cast<char>(o.header[r][e]));
+        auto it = sd_memo_.find(key_);
+        if (it == sd_memo_.end()) {
+            int* rows[kSSd];
+            for (int i = 0; i < kSSd; ++i) rows[i] = o.header[i];
+            rec_.assign(static_cast<size_t>(kSHdr + n2 * n), 0);
+            if (int st = sd_relay_plan_state(k, n, n2, 0, o.sder, rows, rec_.data())) return st;
+            const int32_t at = intern(rec_.data() + kSHdr, static_cast<size_t>(n2) * n);
+            it = sd_memo_.emplace(key_, std::make_pair(at, std::vector<uint8_t>(rec_.begin(), rec_.begin() + kSHdr)))
+                     .first;
+        }
+        const std::vector<uint8_t>& hrow = it->second.second;
+        for (int i = 0; i < n2; ++i) o.header[n2 - 1][i] = hrow[static_cast<size_t>(i)];  // (the planner's write-back)
+        std::memcpy(hdr, hrow.data(), kSHdr);
         // window rows: output o, position p reads slot lo + (n2-1-o) + p (p < n - symInd; the
         // coefficients past the partial diagonal are zero, so rows past slot 2*T_TOT are never read)
-        const int lo = 2 * kST - n + 1 - (n2 - k);
         for (int r = lo; r < lo + n2 + n - 1; ++r) rrefs.push_back(r <= 2 * kST ? o.sd[r] : -1);
         j.nout = static_cast<uint8_t>(n2);
         j.nin = static_cast<uint8_t>(n);
         j.ostride = static_cast<uint8_t>(n2);
         j.rb0 = static_cast<int8_t>(n2 - 1);  // output o: the diagonal of symInd = k-1-o
         j.rstep = 1;
-        j.coef = intern(rec.data() + kSHdr, static_cast<size_t>(n2) * n);
+        j.coef = it->second.first;
         c.g2 = 0;
         d_bytes += static_cast<int64_t>(blocks) * n2;
     }
@@ -518,20 +563,29 @@ int SessionPlan::emit(SymDsw& o, int k, int n, int64_t seq) {
     j.ref0 = static_cast<int32_t>(djr.size());
     bool flag = false;
     if (R == 2) {
-        uint8_t rows[kSMaxN * kSMaxN];
-        decode_rows(k, n, o.er, rows, &flag);
         for (int m = 0; m < n; ++m) djr.push_back(static_cast<int32_t>(o.cv[m]));
-        j.coef = intern(rows, static_cast<size_t>(k) * n);
+        j.coef = rows_coef(k, n, o.er, &flag);
     } else {
-        int* rows[kSSd];
-        for (int i = 0; i < kSSd; ++i) rows[i] = o.header[i];
-        std::vector<uint8_t> rec(static_cast<size_t>(k) * n);
-        if (int st = sd_dest_plan_state(k, n, rows, rec.data(), &flag)) return st;
+        // the decode reads header entries < n of rows lo..3T-1 (:501-508)
         const int lo = kSSd - 1 - (k - 1) - (n - 1);
+        key_.assign(1, static_cast<char>(k | 0x40));
+        key_.push_back(static_cast<char>(n));
+        for (int r = lo; r < kSSd; ++r)
+            for (int e = 0; e < n; ++e) key_.push_back(static_cast<char>(o.header[r][e]));
+        auto it = sd_memo_.find(key_);
+        if (it == sd_memo_.end()) {
+            int* rows[kSSd];
+            for (int i = 0; i < kSSd; ++i) rows[i] = o.header[i];
+            rec_.assign(static_cast<size_t>(k) * n, 0);
+            if (int st = sd_dest_plan_state(k, n, rows, rec_.data(), &flag)) return st;
+            it = sd_memo_.emplace(key_, std::make_pair(intern(rec_.data(), rec_.size()),
+                                                       std::vector<uint8_t>(1, flag ? 1 : 0))).first;
+        }
+        flag = it->second.second[0] != 0;
         for (int r = lo; r < kSSd; ++r) djr.push_back(static_cast<int32_t>(o.sd[r]));
         j.rb0 = static_cast<int8_t>(k - 1);  // output ks: frames t2-ks-(n-1-q) (:501-508)
         j.rstep = 1;
-        j.coef = intern(rec.data(), rec.size());
+        j.coef = it->second.first;
     }
     djobs.push_back(j);
     proc[static_cast<size_t>(seq)] = 1;

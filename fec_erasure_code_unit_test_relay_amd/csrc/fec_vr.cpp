@@ -320,7 +320,9 @@ void VrPlan::start_workers() {
                     qsize_.store(q_.empty() && qclosed_ ? -1 : static_cast<int64_t>(q_.size()),
                                  std::memory_order_release);
                 }
-                if (j.id < 0) {  // final_sum_coding_rate, one float add per packet in sending order
+                if (j.id <= -2) {  // feedback job -2 - id
+                    feedback_job(-2 - static_cast<int64_t>(j.id), fb_T_, fb_mds_);
+                } else if (j.id < 0) {  // final_sum_coding_rate, one float add per packet in sending order
                     float s = 0;
                     for (const RateRun& r : rate_runs) s = float_add_repeated(s, r.rate, r.count);
                     sum_coding_rate = s;
@@ -474,12 +476,19 @@ void VrPlan::feedback_plan(int64_t end) {
         b.to = j == 0 ? swap_at(2) : swap_at(c + 1);
         b.changes.clear();
     }
-    fb_done_.store(0, std::memory_order_relaxed);
+    fb_ready_.reset(new std::atomic<uint8_t>[static_cast<size_t>(njobs) + 1]);
+    for (int64_t j = 0; j <= njobs; ++j) fb_ready_[static_cast<size_t>(j)].store(0, std::memory_order_relaxed);
 }
 
 void VrPlan::feedback_run(int T, bool mds) {
     const int64_t njobs = static_cast<int64_t>(fb_jobs_.size());
-    for (int64_t j = 0; j < njobs; ++j) {
+    for (int64_t j = 0; j < njobs; ++j) feedback_job(j, T, mds);
+}
+
+// One feedback job (one estimator's stretch), then its ready flag.  The jobs are independent: the
+// workers run them in parallel, ahead of every decoder job (start_workers' queue is FIFO).
+void VrPlan::feedback_job(int64_t j, int T, bool mds) {
+    {
         FbJob& b = fb_jobs_[static_cast<size_t>(j)];
         ParameterEstimator e(kTTot, j == 0 ? mds : false);
         uint32_t last = 0xffffffffu;
@@ -508,7 +517,7 @@ void VrPlan::feedback_run(int T, bool mds) {
             if (s >= b.rec) put(s);
             ++s;
         }
-        fb_done_.store(j + 1, std::memory_order_release);
+        fb_ready_[static_cast<size_t>(j)].store(1, std::memory_order_release);
     }
 }
 
@@ -522,9 +531,10 @@ struct VrPlan::FbCursor {
     size_t changes = 0;
     int64_t done = 0;  // jobs known complete: the shared counter is read only past them
     explicit FbCursor(VrPlan& plan) : p(plan) {}
-    bool ready(size_t job) {
+    bool ready(size_t job) {  // jobs complete in any order; the cursor reads them in order
         if (static_cast<int64_t>(job) < done) return true;
-        done = p.fb_done_.load(std::memory_order_acquire);
+        const int64_t n = static_cast<int64_t>(p.fb_jobs_.size());
+        while (done < n && p.fb_ready_[static_cast<size_t>(done)].load(std::memory_order_acquire)) ++done;
         return static_cast<int64_t>(job) < done;
     }
     double waited_ms = 0;  // FEC_VR_DEBUG: time the control loop spent waiting for the producer
@@ -627,9 +637,14 @@ void VrPlan::control(const uint8_t* pattern, int64_t n_pattern, int T, int B, in
             if (held) (void)pthread_setaffinity_np(pthread_self(), sizeof(saved), &saved);
         }
     } caller_placement{t_pin_home};
-    std::thread fb_thread([this, T, mds, fb_sync, home = t_pin_home] {
+    // The feedback jobs: on the worker pool, ahead of the decoder jobs (round 5 ran them in order on
+    // one producer thread while the control loop waited for them; FEC_VR_FB_THREAD=1 restores that)
+    const bool fb_thread_on = !fb_sync && std::getenv("FEC_VR_FB_THREAD") != nullptr;
+    fb_T_ = T;
+    fb_mds_ = mds;
+    std::thread fb_thread([this, T, mds, fb_thread_on, home = t_pin_home] {
         vr_pin_near(home);
-        if (!fb_sync) feedback_run(T, mds);
+        if (fb_thread_on) feedback_run(T, mds);
     });
     struct Joiner {
         std::thread& t;
@@ -638,6 +653,16 @@ void VrPlan::control(const uint8_t* pattern, int64_t n_pattern, int T, int B, in
     FbCursor fb(*this);
     const auto tc1 = std::chrono::steady_clock::now();
     start_workers();
+    if (!fb_sync && !fb_thread_on) {
+        std::lock_guard<std::mutex> lk(qmu_);
+        for (size_t jf = 0; jf < fb_jobs_.size(); ++jf) {
+            DecJob fj;
+            fj.id = -2 - static_cast<int>(jf);
+            q_.push_back(std::move(fj));
+        }
+        qsize_.store(static_cast<int64_t>(q_.size()), std::memory_order_release);
+    }
+    qcv_.notify_all();
     size_t dri = 0;       // next drop
     uint8_t udp[12] = {};
     // ---- Variable_Rate_FEC_Decoder (Variable_Rate_FEC_Decoder.cpp:25-80, 2133-2400, 2440-2514) ----
@@ -1030,6 +1055,7 @@ void VrPlan::control(const uint8_t* pattern, int64_t n_pattern, int T, int B, in
                      std::chrono::duration<double, std::milli>(tc2 - tc1).count(), fb.changes, fb.waited_ms,
                      static_cast<long long>(n_iter), static_cast<long long>(n_jump), drops.size());
     }
+    fb_wait_ms = fb.waited_ms;
     // the last two decoder instances, then the coding-rate sum; no more jobs
     if (dold >= 0) done_with(dold);
     if (dcur >= 0) done_with(dcur);
@@ -1761,6 +1787,12 @@ int fec_vr_plan_timing(const fec_vr_plan* vc, double* control_ms, double* decode
     v->plan.finish();
     if (control_ms) *control_ms = v->plan.control_ms;
     if (decoders_ms) *decoders_ms = v->plan.decoders_ms;
+    return FEC_OK;
+}
+
+int fec_vr_plan_feedback_wait(const fec_vr_plan* v, double* waited_ms) {
+    if (!v || !waited_ms) return FEC_ERR_ARG;
+    *waited_ms = v->plan.fb_wait_ms;
     return FEC_OK;
 }
 

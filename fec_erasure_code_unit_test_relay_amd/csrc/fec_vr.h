@@ -136,6 +136,7 @@ struct VrPlan {
     int64_t steady_packets = 0;       // packets the control loop appended as steady stretches
     int64_t transition_packets = 0;   // ... and as transition stretches (double coding, no drop)
     double control_ms = 0, decoders_ms = 0;  // wall time of run()'s two phases
+    double fb_wait_ms = 0;            // the control loop's time waiting for feedback jobs
     double coding_rate() const { return sent ? sum_coding_rate / static_cast<float>(sent) : 0.0; }
 
     VrPlan() = default;
@@ -154,7 +155,7 @@ struct VrPlan {
     VrFrame frame(int64_t s) const;  // frame of sent packet s
 
 private:
-    struct DecJob {        // a decoder instance the control loop is done with (id < 0: the rate sum)
+    struct DecJob {        // a decoder instance the control loop is done with (id -1: the rate sum, <= -2: feedback job -2-id)
         int id = -1;
         VrInstance d;
         const DecodeRules* rules = nullptr;
@@ -176,9 +177,12 @@ private:
     struct FbCursor;
     void feedback_plan(int64_t end);
     void feedback_run(int T, bool mds);
+    void feedback_job(int64_t j, int T, bool mds);
     std::vector<int64_t> fb_swaps_;
     std::vector<FbJob> fb_jobs_;
-    std::atomic<int64_t> fb_done_{0};   // jobs published by the producer thread
+    std::unique_ptr<std::atomic<uint8_t>[]> fb_ready_;  // per job: complete (any order)
+    int fb_T_ = 0;
+    bool fb_mds_ = false;
     void start_workers();
     void publish(DecJob&& j, bool flush = false);
     void close_jobs();

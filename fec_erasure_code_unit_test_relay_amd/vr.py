@@ -60,7 +60,10 @@ class VrPlan:
         self.sent, self.cw_max = sent.value, cwm.value
         c_ms, d_ms = ctypes.c_double(), ctypes.c_double()
         check(lib().fec_vr_plan_timing(h, ctypes.byref(c_ms), ctypes.byref(d_ms)), "fec_vr_plan_timing")
-        self.plan_ms = {"control_loop": c_ms.value, "decoder_instances": d_ms.value}
+        fw = ctypes.c_double()
+        lib().fec_vr_plan_feedback_wait.restype = ctypes.c_int
+        check(lib().fec_vr_plan_feedback_wait(h, ctypes.byref(fw)), "fec_vr_plan_feedback_wait")
+        self.plan_ms = {"control_loop": c_ms.value, "decoder_instances": d_ms.value, "feedback_wait": fw.value}
         if light:
             return
         self.encoders = np.zeros((ne.value, 6), dtype=np.int64)

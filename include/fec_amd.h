@@ -258,6 +258,9 @@ int fec_vr_plan_stats(const fec_vr_plan *plan, int64_t *lost, int64_t *switches,
 /* wall time of the plan's two phases: the serial control loop (sender, estimators, switches,
  * decoder swaps) and the parallel symbolic decoder instances, in ms */
 int fec_vr_plan_timing(const fec_vr_plan *plan, double *control_ms, double *decoders_ms);
+/* the control loop's time waiting for the estimator feedback jobs (which run on the plan's worker
+ * threads, ahead of its decoder jobs) in the last run */
+int fec_vr_plan_feedback_wait(const fec_vr_plan *plan, double *waited_ms);
 /* instances, 6 int64 each: T, B, N, first seq, seq from which it is the old one, end seq */
 int fec_vr_plan_instances(const fec_vr_plan *plan, int64_t *encoders, int64_t *decoders);
 /* per sent packet: frames (6 int32: header T, B, N, counter_for_start_and_end, current encoder,
