@@ -6,6 +6,11 @@
 
 namespace fec {
 
+// Buffer resources' num_records cap: the kernels read "zero" through the out-of-range offset
+// 0x7ffffff0 (a 16-byte load), which must lie wholly past the range even when the buffer is 2 GiB
+// or more (num_records 0x7fffffff would leave its first 15 bytes in range).
+constexpr int64_t kRsrcMax = 0x7fffffe0;
+
 // GF(2^8) product of four packed bytes by one constant c (c*x is XOR-linear: three register
 // tables indexed per byte by v_perm_b32).  tab[0..1] = c*{0..7}, tab[2..3] = c*({0..7}<<3),
 // tab[4] = c*({0..3}<<6).

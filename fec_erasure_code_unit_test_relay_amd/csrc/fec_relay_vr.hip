@@ -312,6 +312,18 @@ int fec_relay_vr_run(fec_relay_vr* r, const uint8_t* d_payload, const uint8_t* h
         }
         if (hipEventRecord(r->ev_fork, caller) != hipSuccess) return FEC_ERR_HIP;
         const int nst = std::min<int>(fec_relay_vr::kStreams, static_cast<int>(r->codes.size()));
+        // any return before the join below (an error) drains the side streams first: otherwise the
+        // caller's stream is not ordered after their work and the next run could rewrite buffers
+        // those kernels still read
+        struct SideDrain {
+            fec_relay_vr* r;
+            int n;
+            bool armed = true;
+            ~SideDrain() {
+                if (armed)
+                    for (int i = 0; i < n; ++i) (void)hipStreamSynchronize(r->st[i]);
+            }
+        } drain{r, nst};
         for (int i = 0; i < nst; ++i)
             if (hipStreamWaitEvent(r->st[i], r->ev_fork, 0) != hipSuccess) return FEC_ERR_HIP;
         // one code's chain on its own stream; type 3's host planners make its batches synchronous,
@@ -408,6 +420,7 @@ int fec_relay_vr_run(fec_relay_vr* r, const uint8_t* d_payload, const uint8_t* h
         for (int i = 0; i < nst; ++i)
             if (hipEventRecord(r->ev_join[i], r->st[i]) != hipSuccess || hipStreamWaitEvent(s, r->ev_join[i], 0) != hipSuccess)
                 return FEC_ERR_HIP;
+        drain.armed = false;  // the caller's stream now waits for every side stream
         if (!r->map_up) {
             if (int st = r->d_map.reserve(r->map.size() * 4)) return st;
             if (hipMemcpyAsync(r->d_map.p, r->map.data(), r->map.size() * 4, hipMemcpyHostToDevice, s) != hipSuccess)

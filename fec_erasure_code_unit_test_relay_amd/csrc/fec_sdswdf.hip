@@ -50,6 +50,7 @@
 #include "fec_amd.h"
 #include "fec_host.h"
 #include "fec_kernels.h"
+#include "fec_device.h"
 
 namespace fec {
 namespace {
@@ -818,7 +819,7 @@ __global__ __launch_bounds__(256) void fec_sd_tile_kernel(SdTileArgs a) {
     {
         const int64_t base = A > 0 ? A : 0, lim = a.in_bytes - base;
         const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-            const_cast<uint8_t*>(a.in + base), 0, static_cast<int>(lim < 0x7fffffff ? lim : 0x7fffffff), 0x00020000);
+            const_cast<uint8_t*>(a.in + base), 0, static_cast<int>(lim < fec::kRsrcMax ? lim : fec::kRsrcMax), 0x00020000);
         typedef uint32_t v4 __attribute__((ext_vector_type(4)));
         for (int c = tid; 16 * c < span; c += 256) {
             const int64_t o = A + 16 * c;  // bytes before the array read as zero (rows before seq 0)

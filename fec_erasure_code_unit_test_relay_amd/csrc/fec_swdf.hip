@@ -279,7 +279,7 @@ __global__ __launch_bounds__(kTThreads) void fec_sw_tile_kernel(SwTileArgs a) {
     const int64_t tile1 = min(tile0 + a.tiles_per_wg, a.ntiles);
     const uint8_t* in_end = a.in + a.P * a.in_stride;
     const __amdgpu_buffer_rsrc_t rer =
-        __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(a.er), 0, static_cast<int>(min<int64_t>(a.P, 0x7fffffff)), 0x00020000);
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(a.er), 0, static_cast<int>(min<int64_t>(a.P, fec::kRsrcMax)), 0x00020000);
 
     // Loads of a tile's rows slab (16-byte chunks of the aligned span, through a buffer resource:
     // past the input's end they read zero) and flags, into registers.
@@ -295,7 +295,7 @@ __global__ __launch_bounds__(kTThreads) void fec_sw_tile_kernel(SwTileArgs a) {
         const int nch = (dl + static_cast<int>((t0 + nt - rs) * a.in_stride) + 15) >> 4;
         const int64_t span = in_end - ga;
         const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
-            const_cast<uint8_t*>(ga), 0, static_cast<int>(min<int64_t>(span, 0x7fffffff)), 0x00020000);
+            const_cast<uint8_t*>(ga), 0, static_cast<int>(min<int64_t>(span, fec::kRsrcMax)), 0x00020000);
 #pragma unroll
         for (int q = 0; q < kTQ; ++q) {
             const int c = tid + q * kTThreads;
@@ -687,7 +687,7 @@ struct FastTile {
         const int nch = static_cast<int>((g0 - A + static_cast<int64_t>(H + nt) * STRIDE + 15) >> 4);
         const int64_t span = a.P * STRIDE - base;
         const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-            const_cast<uint8_t*>(a.in + base), 0, static_cast<int>(span < 0x7fffffff ? span : 0x7fffffff), 0x00020000);
+            const_cast<uint8_t*>(a.in + base), 0, static_cast<int>(span < fec::kRsrcMax ? span : fec::kRsrcMax), 0x00020000);
 #pragma unroll
         for (int q = 0; q < QCH; ++q) {
             const int c = tid + q * kFT;
@@ -697,7 +697,7 @@ struct FastTile {
             v[q] = make_uint4(x[0], x[1], x[2], x[3]);
         }
         const __amdgpu_buffer_rsrc_t re = __builtin_amdgcn_make_buffer_rsrc(
-            const_cast<uint8_t*>(a.er), 0, static_cast<int>(a.P < 0x7fffffff ? a.P : 0x7fffffff), 0x00020000);
+            const_cast<uint8_t*>(a.er), 0, static_cast<int>(a.P < fec::kRsrcMax ? a.P : fec::kRsrcMax), 0x00020000);
         const int64_t ra = r0 + lane, rb = r0 + 64 + lane;
         f0 = __builtin_amdgcn_raw_buffer_load_b8(re, (lane < ROWS && ra >= 0) ? static_cast<uint32_t>(ra) : 0x7ffffff0u, 0, 0);
         f1 = __builtin_amdgcn_raw_buffer_load_b8(re, (64 + lane < ROWS && rb >= 0) ? static_cast<uint32_t>(rb) : 0x7ffffff0u, 0, 0);

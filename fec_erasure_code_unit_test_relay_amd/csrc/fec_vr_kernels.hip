@@ -692,7 +692,7 @@ __device__ __forceinline__ void vr_copy_run_direct(const VrCopyArgs& a, const Vr
     const int pl = lane / NS4, g = lane - pl * NS4;
     const int64_t left = a.cur_bytes - ob;
     const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(
-        const_cast<uint8_t*>(a.cur + ob), 0, static_cast<int>(left < 0x7fffffff ? left : 0x7fffffff), 0x00020000);
+        const_cast<uint8_t*>(a.cur + ob), 0, static_cast<int>(left < fec::kRsrcMax ? left : fec::kRsrcMax), 0x00020000);
     for (int p0 = lo + wv * ppw; p0 < hi; p0 += 4 * ppw) {
         const int t = p0 + pl;
         const bool on = pl < ppw && t < hi;

@@ -57,6 +57,22 @@ def test_hop1_burst_then_adaptation(R):
     # double coding: T_TOT + 1 packets carry two codewords
     L1 = r["hop1_len"]
     assert (L1[s:s + 11] > L1[s + 11:s + 20].max()).all()
+    # hand-traced relay word layout through the switch (Variable_Rate_FEC_Decoder.cpp:1458-1588,
+    # send_sym_wise_message :317-330): [8-byte header][size_cur BE16][new part][old part] during the
+    # relay's double coding (seqs s .. s + T_TOT), one part before and after; a part is
+    # codeword_r_d_size = (ceil(302 / k2) + 1) * n2 bytes (:997-999), plus its 11-byte header row
+    # for type 3; the 8-byte header carries the new hop-2 code (n2 - 1, n2 - k2, n2 - k2)
+    def rd(k2, n2):
+        return (-(-302 // k2) + 1) * n2
+    hb = 11 if R == 3 else 0
+    k_old, n2_old = h[s - 1, 8] - h[s - 1, 10] + 1, h[s - 1, 8] + 1   # (11, 11) before the switch
+    k_new, n2_new = h[s, 8] - h[s, 10] + 1, h[s, 8] + 1
+    RL, RH = r["relay_len"], r["relay_hdr"].astype(int)
+    assert RL[s - 1] == 8 + 2 + hb + rd(k_old, n2_old)
+    for t in range(s, s + 11):
+        assert RL[t] == 8 + 2 + hb + rd(k_new, n2_new) + hb + rd(k_old, n2_old)
+        assert RH[t, 4] == n2_new - 1 and RH[t, 6] == n2_new - k_new
+    assert RL[s + 11] == 8 + 2 + hb + rd(k_new, n2_new)
 
 
 @pytest.mark.parametrize("R", [2, 3])
