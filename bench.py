@@ -95,10 +95,12 @@ def rocprof_child(argv, symbols, keep_dir=None, timeout=300):
     res = {}
     for row in csv.DictReader(open(stats[-1])):
         name = row["Name"].split("(")[0].replace("void ", "").replace("fec::", "").strip()
+        st = {"avg_us": float(row["AverageNs"]) / 1e3, "calls": int(row["Calls"]),
+              "min_us": float(row["MinNs"]) / 1e3, "max_us": float(row["MaxNs"]) / 1e3}
+        res.setdefault("__all__", {})[name] = st  # every kernel (the relay legs' lookups)
         for sym in symbols:
             if sym and name == sym:
-                res[sym] = {"avg_us": float(row["AverageNs"]) / 1e3, "calls": int(row["Calls"]),
-                            "min_us": float(row["MinNs"]) / 1e3, "max_us": float(row["MaxNs"]) / 1e3}
+                res[sym] = st
     if not keep_dir:
         shutil.rmtree(out, ignore_errors=True)
     return res, os.path.relpath(stats[-1], ROOT) if keep_dir else "temporary"
@@ -353,7 +355,7 @@ def quiet_cpu_group(sample_s=0.2):
     return best[1] if best else None
 
 
-def extra_configs(steps=5):
+def extra_configs(steps=5, kprof=None):
     """BASELINE configs 3 and 4 (parity cases, reported beside the headline, never as `value`):
     device-resident decode at (10,5,2) on bin/erasure.bin (P = 360000, the reference's pattern
     replayed from packet 0) and the adaptive variable-rate loop's schedule (encode + decode of
@@ -462,7 +464,7 @@ def extra_configs(steps=5):
         "verified": bool(torch.equal(out4[ok4], pl[:P][ok4])) and v.lost == 2982 and
         int((ol4 == 0).sum()) == 2982 and w.lost == 2982}
     res["multistream_10k"] = multistream(steps)
-    res["relay_10_3"] = relay_chains(steps)
+    res["relay_10_3"] = relay_chains(steps, kprof)
     res["relay_adaptive"] = relay_adaptive(steps)
     res["relay_session"] = relay_session(steps)
     res["per_packet_api"] = per_packet_api()
@@ -508,7 +510,38 @@ def per_packet_api(packets=20000):
     return res
 
 
-def relay_chains(steps):
+def relay_type2_setup():
+    """The type-2 relay chain's inputs (360 000 source (10,3,3) codewords, hop erasures
+    bin/erasure.bin / bin/erasure2.bin) and preallocated outputs."""
+    import torch
+    from fec_erasure_code_unit_test_relay_amd import Codec, fill_payload
+    from fec_erasure_code_unit_test_relay_amd.relay import SymbolWiseRelay
+    from fec_erasure_code_unit_test_relay_amd.streams import load_pattern
+    P = 360000
+    c = Codec(L, 10, 3, 3)
+    payload = fill_payload(0, P, L, 0x5EED)
+    cw, _ = c.encode(payload)
+    e1 = torch.from_numpy(load_pattern("bin_erasure")[:P].astype(np.uint8).copy()).cuda()
+    e2 = torch.from_numpy(load_pattern("bin_erasure2")[:P].astype(np.uint8).copy()).cuda()
+    r2 = SymbolWiseRelay(L, 10, 3, 10, 3)
+    bufs = (torch.empty((P, r2.frame_bytes), dtype=torch.uint8, device="cuda"),
+            torch.empty(P, dtype=torch.uint8, device="cuda"),
+            torch.empty((P, r2.S * r2.k), dtype=torch.uint8, device="cuda"),
+            torch.empty(P, dtype=torch.uint8, device="cuda"))
+    return P, c, payload, cw, e1, e2, r2, bufs
+
+
+def relay_chain_launches(n):
+    """rocprofv3 child leg: the type-2 relay and destination kernels, n launches each (after 3)."""
+    import torch
+    P, c, payload, cw, e1, e2, r2, (fr, rf, dout, dfl) = relay_type2_setup()
+    for _ in range(3 + n):
+        r2.relay(cw, e1, fr, rf)
+        r2.destination(fr, e2, dout, dfl)
+    torch.cuda.synchronize()
+
+
+def relay_chains(steps, kprof=None):
     """The Decoder_Symbol_Wise relay: source (10,3,3) codewords of 360 000 packets
     -> relay -> destination, hop 1 erasures bin/erasure.bin, hop 2 bin/erasure2.bin, for
     RELAYING_TYPE 2 (symbol_wise_encode_1 / decode_1) and 3 (state-dependent).  One step = relay +
@@ -564,8 +597,27 @@ def relay_chains(steps):
                   "frac": round(by_r / ms_r / 1e6 / 8000.0, 4)},
         "destination": {"us": round(ms_d * 1e3, 1), "bytes": by_d, "achieved": round(by_d / ms_d / 1e6, 1),
                         "frac": round(by_d / ms_d / 1e6 / 8000.0, 4)},
-        "note": "per kernel: algorithmic bytes / event-timed launch on its stream (an upper bound on the "
-                "kernel); relay CW+1 read + frame+1 written, destination frame+1 read + S*k+1 written per packet"}
+        "note": "per kernel: algorithmic bytes / kernel time; relay CW+1 read + frame+1 written, destination "
+                "frame+1 read + S*k+1 written per packet.  us / frac: this invocation's rocprofv3 child "
+                "(the relay and destination launched 20 times after the headline step) when it ran, else the "
+                "event pair around each launch on its stream (us_event / frac_event beside it); traffic: the "
+                "committed FETCH_SIZE (x2, gfx950) + WRITE_SIZE passes of tools/swdf_bench.py when they were "
+                "made on these kernel sources"}
+    for leg, prefix in (("relay", "fec_sw_fast_relay"), ("destination", "fec_sw_fast_dest")):
+        d = res["type2"]["roofline"][leg]
+        d.update(us_event=d["us"], frac_event=d["frac"])
+        names = [k for k in ((kprof or {}).get("__all__") or {}) if k.startswith(prefix)]
+        if names:
+            k = max(names, key=lambda n: kprof["__all__"][n]["calls"])
+            us = kprof["__all__"][k]["avg_us"]
+            d.update(kernel=k, us=round(us, 1), achieved=round(d["bytes"] / us / 1e3, 1),
+                     frac=round(d["bytes"] / us / 1e3 / 8000.0, 4), us_source="rocprofv3 child of this bench",
+                     rocprof_calls=kprof["__all__"][k]["calls"])
+            tr = pmc_traffic(k)
+            if tr and tr[2]:
+                d.update(traffic=tr[0], traffic_ratio=round(tr[0] / d["bytes"], 3), traffic_source=tr[1])
+            elif tr:
+                d.update(traffic=None, traffic_stale=f"{tr[1]} was measured on other kernel sources")
     r3 = StateDependentRelay(L, 10, 3, 10, 3)
     o, df = r3.destination(r3.relay(cw, z), z)
     D = r3.delay
@@ -604,7 +656,9 @@ def relay_adaptive(steps):
         res[f"type{t}"] = {"ms": round(dt * 1e3, 3), "GiB_s": round(P * L / dt / 2**30, 3),
                            "unflagged": int((flags == 0).sum()), "verified": bool(ok)}
     res["note"] = ("one fixed-rate batch per code over its instances laid end to end (each behind zero rows), "
-                   "planners reset per instance; host work (erasure gathers, type 3's planners) inside")
+                   "planners reset per instance; host work (erasure gathers, type 3's planners) inside; "
+                   "verified = equal to tests/golden/relay_vr_360k.json, made by this repo's reference-structured "
+                   "driver over the oracle's methods (the reference ships no relay output: parity unpinned)")
     return res
 
 
@@ -964,8 +1018,10 @@ def main():
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     elapsed = max_over_ranks(elapsed, dist, comm_dev)
-    if args.rocprof_child:  # the profiled child: the step's kernels only
+    if args.rocprof_child:  # the profiled child: the step's kernels, then the type-2 relay chain's
         print(json.dumps({"rocprof_child": True, "ms_per_step": elapsed / args.steps * 1e3}), flush=True)
+        if world == 1 and not args.no_extra_configs:
+            relay_chain_launches(20)
         return
 
     # correctness of the timed work (outside the timed region): round trip + planner agreement
@@ -1030,6 +1086,7 @@ def main():
     achieved = algo[dominant] / (per_launch[dominant] * 1e-3) / 1e9
 
     result = None
+    kt_all = None
     if rank == 0:
         ms_per_step = elapsed / args.steps * 1e3
         value = world * P * L / (elapsed / args.steps) / 2**30
@@ -1082,6 +1139,7 @@ def main():
         sym = {"fec_encode_kernel": info["encode_kernel"], "fec_copy_kernel": info.get("copy_kernel")}
         kt, kinfo = (None, "--no-rocprof") if args.no_rocprof or P != 1_000_000 else rocprof_child(
             [a for a in sys.argv[1:] if a not in ("--rocprof-child",)], list(sym.values()), args.rocprof_keep)
+        kt_all = kt
         if kt and all(v in kt for v in sym.values() if v):
             dom = max((k for k in sym if sym[k]), key=lambda k: kt[sym[k]]["avg_us"])
             a_rp = algo[dom] / (kt[sym[dom]]["avg_us"] * 1e-6) / 1e9
@@ -1109,7 +1167,7 @@ def main():
         if rank == 0:
             result["host_inclusive"] = hi
     if rank == 0 and world == 1 and not args.no_extra_configs:
-        result["configs"] = extra_configs()
+        result["configs"] = extra_configs(kprof=kt_all)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline(T, B, N, args.cpu_packets, pat)
     if rank == 0:

@@ -28,6 +28,10 @@ KERNEL_NAMES = ["fec_encode_kernel", "fec_scan_kernel", "fec_plan_kernel", "fec_
 class FecError(RuntimeError):
     def __init__(self, status: int, what: str = ""):
         msg = lib().fec_strerror(status).decode() if _lib is not None else str(status)
+        if status == FEC_ERR_HIP and _lib is not None:  # which HIP call failed, and where
+            buf = ctypes.create_string_buffer(512)
+            if _lib.fec_last_error(buf, len(buf)) > 0:
+                msg += f" [{buf.value.decode(errors='replace')}]"
         super().__init__(f"{what}: {msg} (status {status})")
         self.status = status
 
@@ -57,6 +61,8 @@ def lib() -> ctypes.CDLL:
     i64p = ctypes.POINTER(ctypes.c_int64)
     L.fec_strerror.restype = ctypes.c_char_p
     L.fec_strerror.argtypes = [i32]
+    L.fec_last_error.restype = i32
+    L.fec_last_error.argtypes = [ctypes.c_char_p, ctypes.c_size_t]
     L.fec_version.restype = i32
     L.fec_codec_create.argtypes = [i32, i32, i32, i32, ctypes.POINTER(vp)]
     L.fec_codec_destroy.argtypes = [vp]

@@ -17,6 +17,7 @@
 #include "fec_amd.h"
 #include "fec_host.h"
 #include "fec_kernels.h"
+#include "fec_status.h"
 
 using fec::Geometry;
 
@@ -882,10 +883,29 @@ fec_decoder::~fec_decoder() {
         if (p) (void)hipHostFree(p);
 }
 
+namespace fec {
+namespace {
+std::mutex g_err_mu;
+char g_err[512] = "";
+}  // namespace
+int hip_failed(hipError_t e, const char* site) {
+    std::lock_guard<std::mutex> lk(g_err_mu);
+    std::snprintf(g_err, sizeof(g_err), "%s (%d) at %s", hipGetErrorName(e), static_cast<int>(e), site);
+    return FEC_ERR_HIP;
+}
+}  // namespace fec
+
 // ------------------------------------------------------------------------------------------
 // C ABI
 // ------------------------------------------------------------------------------------------
 extern "C" {
+
+int fec_last_error(char* buf, size_t size) {
+    std::lock_guard<std::mutex> lk(fec::g_err_mu);
+    const int n = static_cast<int>(std::strlen(fec::g_err));
+    if (buf && size) std::snprintf(buf, size, "%s", fec::g_err);
+    return n;
+}
 
 const char* fec_strerror(int status) {
     switch (status) {

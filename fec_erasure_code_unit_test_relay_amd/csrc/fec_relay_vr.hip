@@ -30,6 +30,7 @@
 #include <vector>
 
 #include "fec_amd.h"
+#include "fec_status.h"
 
 namespace fec {
 namespace {
@@ -304,13 +305,13 @@ int fec_relay_vr_run(fec_relay_vr* r, const uint8_t* d_payload, const uint8_t* h
     try {
         const int L = r->L;
         if (!r->ev_fork) {
-            if (hipEventCreateWithFlags(&r->ev_fork, hipEventDisableTiming) != hipSuccess) return FEC_ERR_HIP;
-            for (int i = 0; i < fec_relay_vr::kStreams; ++i)
-                if (hipStreamCreateWithFlags(&r->st[i], hipStreamNonBlocking) != hipSuccess ||
-                    hipEventCreateWithFlags(&r->ev_join[i], hipEventDisableTiming) != hipSuccess)
-                    return FEC_ERR_HIP;
+            FEC_HIP(hipEventCreateWithFlags(&r->ev_fork, hipEventDisableTiming));
+            for (int i = 0; i < fec_relay_vr::kStreams; ++i) {
+                FEC_HIP(hipStreamCreateWithFlags(&r->st[i], hipStreamNonBlocking));
+                FEC_HIP(hipEventCreateWithFlags(&r->ev_join[i], hipEventDisableTiming));
+            }
         }
-        if (hipEventRecord(r->ev_fork, caller) != hipSuccess) return FEC_ERR_HIP;
+        FEC_HIP(hipEventRecord(r->ev_fork, caller));
         const int nst = std::min<int>(fec_relay_vr::kStreams, static_cast<int>(r->codes.size()));
         // any return before the join below (an error) drains the side streams first: otherwise the
         // caller's stream is not ordered after their work and the next run could rewrite buffers
@@ -325,7 +326,7 @@ int fec_relay_vr_run(fec_relay_vr* r, const uint8_t* d_payload, const uint8_t* h
             }
         } drain{r, nst};
         for (int i = 0; i < nst; ++i)
-            if (hipStreamWaitEvent(r->st[i], r->ev_fork, 0) != hipSuccess) return FEC_ERR_HIP;
+            FEC_HIP(hipStreamWaitEvent(r->st[i], r->ev_fork, 0));
         // one code's chain on its own stream; type 3's host planners make its batches synchronous,
         // so its codes run on threads of their own (each code has its own planner objects)
         auto run_code = [&](size_t ci) -> int {
@@ -347,36 +348,33 @@ int fec_relay_vr_run(fec_relay_vr* r, const uint8_t* d_payload, const uint8_t* h
             if (int st = c.d_frames.reserve(static_cast<size_t>(R) * c.F)) return st;
             if (int st = c.d_out.reserve(static_cast<size_t>(R) * c.ostride)) return st;
             if (!c.src_up) {  // the row map depends on the schedule alone: uploaded once
-                if (hipMemcpyAsync(c.d_src.p, c.src.data(), static_cast<size_t>(R) * 8, hipMemcpyHostToDevice, s) !=
-                    hipSuccess)
-                    return FEC_ERR_HIP;
+                FEC_HIP(hipMemcpyAsync(c.d_src.p, c.src.data(), static_cast<size_t>(R) * 8, hipMemcpyHostToDevice, s));
                 c.src_up = true;
             }
             hipLaunchKernelGGL(fec::fec_relay_vr_payload_kernel, dim3(fec::grid_rows(R)), dim3(256), 0, s, d_payload, L,
                                c.d_src.as<const int64_t>(), R, c.d_pay.as<uint8_t>(), c.d_len.as<int32_t>());
-            if (hipGetLastError() != hipSuccess) return FEC_ERR_HIP;
+            FEC_HIP(hipGetLastError());
             // each instance a fresh source encoder: its rows behind kGap zero-length packets (>= n-1)
             if (int st = fec_encode_batch(c.codec, c.d_pay.as<uint8_t>(), c.d_len.as<int32_t>(), 0, R, c.d_cw.as<uint8_t>(),
                                           c.d_cwlen.as<int32_t>(), s))
                 return st;
             hipLaunchKernelGGL(fec::fec_relay_vr_zero_kernel, dim3(fec::grid_rows(R)), dim3(256), 0, s,
                                c.d_src.as<const int64_t>(), R, c.d_cw.as<uint8_t>(), c.CW);
-            if (hipGetLastError() != hipSuccess) return FEC_ERR_HIP;
+            FEC_HIP(hipGetLastError());
             if (r->type == 2) {
                 if (int st = c.d_er1.reserve(static_cast<size_t>(R))) return st;
                 if (int st = c.d_er2.reserve(static_cast<size_t>(R))) return st;
                 if (int st = c.d_flag.reserve(static_cast<size_t>(R))) return st;
                 const size_t wb = fec_swdf_workspace_bytes(c.sw, R);
                 if (int st = c.d_work.reserve(wb)) return st;
-                if (hipMemcpyAsync(c.d_er1.p, c.h_er1.data(), static_cast<size_t>(R), hipMemcpyHostToDevice, s) != hipSuccess ||
-                    hipMemcpyAsync(c.d_er2.p, c.h_er2.data(), static_cast<size_t>(R), hipMemcpyHostToDevice, s) != hipSuccess)
-                    return FEC_ERR_HIP;
+                FEC_HIP(hipMemcpyAsync(c.d_er1.p, c.h_er1.data(), static_cast<size_t>(R), hipMemcpyHostToDevice, s));
+                FEC_HIP(hipMemcpyAsync(c.d_er2.p, c.h_er2.data(), static_cast<size_t>(R), hipMemcpyHostToDevice, s));
                 if (int st = fec_swdf_relay_batch(c.sw, c.d_cw.as<uint8_t>(), c.CW, c.d_er1.as<uint8_t>(), R,
                                                   c.d_frames.as<uint8_t>(), nullptr, c.d_work.p, wb, s))
                     return st;
                 hipLaunchKernelGGL(fec::fec_relay_vr_zero_kernel, dim3(fec::grid_rows(R)), dim3(256), 0, s,
                                    c.d_src.as<const int64_t>(), R, c.d_frames.as<uint8_t>(), c.F);
-                if (hipGetLastError() != hipSuccess) return FEC_ERR_HIP;
+                FEC_HIP(hipGetLastError());
                 if (int st = fec_swdf_destination_batch(c.sw, c.d_frames.as<uint8_t>(), c.d_er2.as<uint8_t>(), R,
                                                         c.d_out.as<uint8_t>(), c.d_flag.as<uint8_t>(), s))
                     return st;
@@ -387,7 +385,7 @@ int fec_relay_vr_run(fec_relay_vr* r, const uint8_t* d_payload, const uint8_t* h
                     return st;
                 hipLaunchKernelGGL(fec::fec_relay_vr_zero_kernel, dim3(fec::grid_rows(R)), dim3(256), 0, s,
                                    c.d_src.as<const int64_t>(), R, c.d_frames.as<uint8_t>(), c.F);
-                if (hipGetLastError() != hipSuccess) return FEC_ERR_HIP;
+                FEC_HIP(hipGetLastError());
                 c.h_flag.resize(static_cast<size_t>(R));
                 if (int st = fec_sdswdf_destination_batch_starts(c.sd, c.d_frames.as<uint8_t>(), c.h_er2.data(), R,
                                                                  c.starts.data(), ns, c.d_out.as<uint8_t>(),
@@ -417,14 +415,14 @@ int fec_relay_vr_run(fec_relay_vr* r, const uint8_t* d_payload, const uint8_t* h
                 if (st) return st;
         }
         hipStream_t s = caller;
-        for (int i = 0; i < nst; ++i)
-            if (hipEventRecord(r->ev_join[i], r->st[i]) != hipSuccess || hipStreamWaitEvent(s, r->ev_join[i], 0) != hipSuccess)
-                return FEC_ERR_HIP;
+        for (int i = 0; i < nst; ++i) {
+            FEC_HIP(hipEventRecord(r->ev_join[i], r->st[i]));
+            FEC_HIP(hipStreamWaitEvent(s, r->ev_join[i], 0));
+        }
         drain.armed = false;  // the caller's stream now waits for every side stream
         if (!r->map_up) {
             if (int st = r->d_map.reserve(r->map.size() * 4)) return st;
-            if (hipMemcpyAsync(r->d_map.p, r->map.data(), r->map.size() * 4, hipMemcpyHostToDevice, s) != hipSuccess)
-                return FEC_ERR_HIP;
+            FEC_HIP(hipMemcpyAsync(r->d_map.p, r->map.data(), r->map.size() * 4, hipMemcpyHostToDevice, s));
             r->map_up = true;
         }
         fec::RvGatherArgs a{};
@@ -441,17 +439,15 @@ int fec_relay_vr_run(fec_relay_vr* r, const uint8_t* d_payload, const uint8_t* h
         a.out = d_out;
         a.out_stride = r->ostride;
         hipLaunchKernelGGL(fec::fec_relay_vr_gather_kernel, dim3(fec::grid_rows(r->P)), dim3(256), 0, s, a);
-        if (hipGetLastError() != hipSuccess) return FEC_ERR_HIP;
+        FEC_HIP(hipGetLastError());
         if (r->type == 2)  // the destinations' flags, after every code's launches (a copy to pageable
                            // memory returns only when the stream has reached it)
             for (auto& cp : r->codes) {
                 fec::Code& c = *cp;
                 c.h_flag.resize(static_cast<size_t>(c.R));
-                if (hipMemcpyAsync(c.h_flag.data(), c.d_flag.p, static_cast<size_t>(c.R), hipMemcpyDeviceToHost, s) !=
-                    hipSuccess)
-                    return FEC_ERR_HIP;
+                FEC_HIP(hipMemcpyAsync(c.h_flag.data(), c.d_flag.p, static_cast<size_t>(c.R), hipMemcpyDeviceToHost, s));
             }
-        if (hipStreamSynchronize(s) != hipSuccess) return FEC_ERR_HIP;
+        FEC_HIP(hipStreamSynchronize(s));
         if (h_flag)
             for (int64_t t = 0; t < r->P; ++t) {
                 const int32_t* m = &r->map[static_cast<size_t>(t) * 6];

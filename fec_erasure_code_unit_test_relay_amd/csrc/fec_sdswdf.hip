@@ -51,6 +51,7 @@
 #include "fec_host.h"
 #include "fec_kernels.h"
 #include "fec_device.h"
+#include "fec_status.h"
 
 namespace fec {
 namespace {
@@ -1085,10 +1086,9 @@ int upload_plan(fec_sdswdf* w, const fec::RecordTable& tab, int64_t P, hipStream
     const size_t tb = std::max<size_t>(tab.data().size(), 1);
     if (int st = w->d_plan.reserve(pb)) return st;
     if (int st = w->d_table.reserve(tb)) return st;
-    if (hipMemcpyAsync(w->d_plan.p, w->plan.data(), pb, hipMemcpyHostToDevice, s) != hipSuccess) return FEC_ERR_HIP;
-    if (!tab.data().empty() &&
-        hipMemcpyAsync(w->d_table.p, tab.data().data(), tab.data().size(), hipMemcpyHostToDevice, s) != hipSuccess)
-        return FEC_ERR_HIP;
+    FEC_HIP(hipMemcpyAsync(w->d_plan.p, w->plan.data(), pb, hipMemcpyHostToDevice, s));
+    if (!tab.data().empty())
+        FEC_HIP(hipMemcpyAsync(w->d_table.p, tab.data().data(), tab.data().size(), hipMemcpyHostToDevice, s));
     return FEC_OK;
 }
 
@@ -1113,9 +1113,8 @@ int launch_tile(fec_sdswdf* w, bool relay, const fec::RecordTable& tab, const ui
     fec::build_entries(tab.data(), R, relay ? fec::kHdr : 0, ROWS, N, w->eoff, w->ent);
     if (int st = w->d_eoff.reserve(w->eoff.size() * 4)) return st;
     if (int st = w->d_ent.reserve(w->ent.size() * 2)) return st;
-    if (hipMemcpyAsync(w->d_eoff.p, w->eoff.data(), w->eoff.size() * 4, hipMemcpyHostToDevice, s) != hipSuccess ||
-        hipMemcpyAsync(w->d_ent.p, w->ent.data(), w->ent.size() * 2, hipMemcpyHostToDevice, s) != hipSuccess)
-        return FEC_ERR_HIP;
+    FEC_HIP(hipMemcpyAsync(w->d_eoff.p, w->eoff.data(), w->eoff.size() * 4, hipMemcpyHostToDevice, s));
+    FEC_HIP(hipMemcpyAsync(w->d_ent.p, w->ent.data(), w->ent.size() * 2, hipMemcpyHostToDevice, s));
     fec::SdTileArgs a;
     a.in = d_in;
     a.stride = stride;
@@ -1134,7 +1133,7 @@ int launch_tile(fec_sdswdf* w, bool relay, const fec::RecordTable& tab, const ui
     a.F = w->F;
     void* args[] = {&a};
     const unsigned grid = static_cast<unsigned>((P + TP - 1) / TP);
-    if (hipLaunchKernel(kern, dim3(grid), dim3(256), args, static_cast<size_t>(lds), s) != hipSuccess) return FEC_ERR_HIP;
+    FEC_HIP(hipLaunchKernel(kern, dim3(grid), dim3(256), args, static_cast<size_t>(lds), s));
     return FEC_OK;
 }
 
@@ -1207,13 +1206,13 @@ struct SwCtx {
     std::map<std::tuple<int, int, int, int, int>, std::unique_ptr<SdRelayPlanner>> relays;
     std::map<std::pair<int, int>, std::unique_ptr<SdDestPlanner>> dests;
     int ensure(size_t bytes) {
-        if (!s && hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) return FEC_ERR_HIP;
+        if (!s) FEC_HIP(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
         if (!d_gf) {
             const Field& F = field();
             std::vector<uint8_t> gf(F.exp, F.exp + 512);
             gf.insert(gf.end(), F.log, F.log + 256);
             if (hipMalloc(&d_gf, gf.size()) != hipSuccess) return FEC_ERR_NOMEM;
-            if (hipMemcpy(d_gf, gf.data(), gf.size(), hipMemcpyHostToDevice) != hipSuccess) return FEC_ERR_HIP;
+            FEC_HIP(hipMemcpy(d_gf, gf.data(), gf.size(), hipMemcpyHostToDevice));
         }
         if (bytes <= cap) return FEC_OK;
         if (h) (void)hipHostFree(h);
@@ -1222,7 +1221,7 @@ struct SwCtx {
         const size_t c = std::max<size_t>(bytes, 64 * 1024);
         if (hipHostMalloc(reinterpret_cast<void**>(&h), c, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess)
             return FEC_ERR_NOMEM;
-        if (hipHostGetDevicePointer(reinterpret_cast<void**>(&d), h, 0) != hipSuccess) return FEC_ERR_HIP;
+        FEC_HIP(hipHostGetDevicePointer(reinterpret_cast<void**>(&d), h, 0));
         cap = c;
         return FEC_OK;
     }
@@ -1243,8 +1242,9 @@ void sw_pack(uint8_t* dst, int row_bytes, uint8_t* const* rows, int lo, int nrow
 int sw_run(SwCtx& c, SwApplyArgs& a) {
     const int total = a.nout * a.blocks;
     hipLaunchKernelGGL(fec_sw_apply_kernel, dim3(static_cast<unsigned>((total + 255) / 256)), dim3(256), 0, c.s, a);
-    if (hipGetLastError() != hipSuccess) return FEC_ERR_HIP;
-    return hipStreamSynchronize(c.s) == hipSuccess ? FEC_OK : FEC_ERR_HIP;
+    FEC_HIP(hipGetLastError());
+    FEC_HIP(hipStreamSynchronize(c.s));
+    return FEC_OK;
 }
 
 // The decode rule of a full window (decodeBlock T = n-1, t = 0) on unit vectors, as coefficient rows:
@@ -1573,8 +1573,10 @@ int fec_sdswdf_relay_batch_starts(fec_sdswdf* w, const uint8_t* d_cw, int64_t cw
         if (int st = upload_plan(w, w->relay->records(), P, s)) return st;
         const int tl = launch_tile(w, true, w->relay->records(), d_cw, cw_stride, P, d_frames, s);
         if (tl < 0) return tl;
-        if (tl == 0)
-            return hipStreamSynchronize(s) == hipSuccess ? static_cast<int>(FEC_OK) : static_cast<int>(FEC_ERR_HIP);
+        if (tl == 0) {
+            FEC_HIP(hipStreamSynchronize(s));
+            return static_cast<int>(FEC_OK);
+        }
         fec::SdRelayArgs a;
         a.cw = d_cw;
         a.cw_stride = cw_stride;
@@ -1591,9 +1593,10 @@ int fec_sdswdf_relay_batch_starts(fec_sdswdf* w, const uint8_t* d_cw, int64_t cw
         a.frames = d_frames;
         a.F = w->F;
         hipLaunchKernelGGL(fec::fec_sdswdf_relay_kernel, dim3(fec::grid_for(P * a.S)), dim3(fec::kSdThreads), 0, s, a);
-        if (hipGetLastError() != hipSuccess) return static_cast<int>(FEC_ERR_HIP);
+        FEC_HIP(hipGetLastError());
         // the host plan arrays are reused by the next call
-        return hipStreamSynchronize(s) == hipSuccess ? static_cast<int>(FEC_OK) : static_cast<int>(FEC_ERR_HIP);
+        FEC_HIP(hipStreamSynchronize(s));
+        return static_cast<int>(FEC_OK);
     });
 }
 
@@ -1619,16 +1622,17 @@ int fec_sdswdf_destination_batch_starts(fec_sdswdf* w, const uint8_t* d_frames, 
         if (int st = w->d_hdrs.reserve(hb)) return st;
         hipLaunchKernelGGL(fec::fec_sdswdf_hdr_gather_kernel, dim3(static_cast<unsigned>((hb + 255) / 256)), dim3(256),
                            0, s, d_frames, static_cast<int64_t>(w->F), P, static_cast<uint8_t*>(w->d_hdrs.p));
-        if (hipGetLastError() != hipSuccess ||
-            hipMemcpyAsync(w->hdrs.data(), w->d_hdrs.p, hb, hipMemcpyDeviceToHost, s) != hipSuccess ||
-            hipStreamSynchronize(s) != hipSuccess)
-            return static_cast<int>(FEC_ERR_HIP);
+        FEC_HIP(hipGetLastError());
+        FEC_HIP(hipMemcpyAsync(w->hdrs.data(), w->d_hdrs.p, hb, hipMemcpyDeviceToHost, s));
+        FEC_HIP(hipStreamSynchronize(s));
         plan_dest(w, h_erasure, w->hdrs.data(), P, h_flag, h_starts, nstarts);
         if (int st = upload_plan(w, w->dest->records(), P, s)) return st;
         const int tl = launch_tile(w, false, w->dest->records(), d_frames, w->F, P, d_out, s);
         if (tl < 0) return tl;
-        if (tl == 0)
-            return hipStreamSynchronize(s) == hipSuccess ? static_cast<int>(FEC_OK) : static_cast<int>(FEC_ERR_HIP);
+        if (tl == 0) {
+            FEC_HIP(hipStreamSynchronize(s));
+            return static_cast<int>(FEC_OK);
+        }
         fec::SdDestArgs a;
         a.frames = d_frames;
         a.F = w->F;
@@ -1642,8 +1646,9 @@ int fec_sdswdf_destination_batch_starts(fec_sdswdf* w, const uint8_t* d_frames, 
         a.gf = w->v2.gf;
         a.out = d_out;
         hipLaunchKernelGGL(fec::fec_sdswdf_dest_kernel, dim3(fec::grid_for(P * a.S)), dim3(fec::kSdThreads), 0, s, a);
-        if (hipGetLastError() != hipSuccess) return static_cast<int>(FEC_ERR_HIP);
-        return hipStreamSynchronize(s) == hipSuccess ? static_cast<int>(FEC_OK) : static_cast<int>(FEC_ERR_HIP);
+        FEC_HIP(hipGetLastError());
+        FEC_HIP(hipStreamSynchronize(s));
+        return static_cast<int>(FEC_OK);
     });
 }
 

@@ -46,6 +46,7 @@
 #include "fec_amd.h"
 #include "fec_host.h"
 #include "fec_vr.h"
+#include "fec_status.h"
 
 namespace fec {
 int sd_relay_plan_state(int k, int n, int n2, int sdbo, const uint8_t* er, int* const* header, uint8_t* rec);
@@ -1302,7 +1303,7 @@ int fec_relay_session_run(fec_relay_session* h, const uint8_t* d_payload, uint8_
     const auto& p = h->plan;
     if (int st = ses_guarded([&] { return ses_upload(h, s); })) return st;
     // the source: every encoder instance of the schedule (the batched variable-rate encoder)
-    if (hipMemsetAsync(h->len_old.p, 0, static_cast<size_t>(p.Q) * 4, s) != hipSuccess) return FEC_ERR_HIP;
+    FEC_HIP(hipMemsetAsync(h->len_old.p, 0, static_cast<size_t>(p.Q) * 4, s));
     if (int st = fec_vr_encode_batch(h->vp, d_payload, nullptr, static_cast<uint8_t*>(h->cur.p),
                                      static_cast<int32_t*>(h->len_cur.p), static_cast<uint8_t*>(h->old.p),
                                      static_cast<int32_t*>(h->len_old.p), s))
@@ -1314,7 +1315,7 @@ int fec_relay_session_run(fec_relay_session* h, const uint8_t* d_payload, uint8_
         hipLaunchKernelGGL(fec::ses_apply_kernel<true>, dim3(grid), dim3(256), 0, s, d,
                            static_cast<const fec::SesJob*>(h->rjobs.p), static_cast<int64_t>(p.rjobs.size()),
                            h->rrefs.p, static_cast<uint8_t*>(h->sym.p));
-        if (hipGetLastError() != hipSuccess) return FEC_ERR_HIP;
+        FEC_HIP(hipGetLastError());
     }
     const int64_t nlin = static_cast<int64_t>(p.lin.size()) - 1;
     if (nlin > 0) {
@@ -1322,20 +1323,20 @@ int fec_relay_session_run(fec_relay_session* h, const uint8_t* d_payload, uint8_
         hipLaunchKernelGGL(fec::ses_lineage_kernel, dim3(static_cast<unsigned>(std::min<int64_t>(nlin, 65536))),
                            dim3(256), lds, s, d, static_cast<const fec::SesCall*>(h->calls.p),
                            static_cast<const int64_t*>(h->lin.p), nlin, static_cast<const uint8_t*>(h->sym.p));
-        if (hipGetLastError() != hipSuccess) return FEC_ERR_HIP;
+        FEC_HIP(hipGetLastError());
     }
     hipLaunchKernelGGL(fec::ses_prefix_kernel, dim3(static_cast<unsigned>((p.Q + 255) / 256)), dim3(256), 0, s, d,
                        static_cast<const fec::SesPrefix*>(h->prefix.p), p.Q);
-    if (hipGetLastError() != hipSuccess) return FEC_ERR_HIP;
+    FEC_HIP(hipGetLastError());
     // the destination's outputs and the loss check
-    if (hipMemsetAsync(d_dest_out, 0, static_cast<size_t>(p.Q) * 320, s) != hipSuccess) return FEC_ERR_HIP;
-    if (hipMemsetAsync(d_lost, 0, sizeof(int64_t), s) != hipSuccess) return FEC_ERR_HIP;
+    FEC_HIP(hipMemsetAsync(d_dest_out, 0, static_cast<size_t>(p.Q) * 320, s));
+    FEC_HIP(hipMemsetAsync(d_lost, 0, sizeof(int64_t), s));
     if (!p.djobs.empty()) {
         const unsigned grid = static_cast<unsigned>(std::min<int64_t>(static_cast<int64_t>(p.djobs.size()), 65536));
         hipLaunchKernelGGL(fec::ses_apply_kernel<false>, dim3(grid), dim3(256), 0, s, d,
                            static_cast<const fec::SesJob*>(h->djobs.p), static_cast<int64_t>(p.djobs.size()),
                            h->djr.p, d_dest_out);
-        if (hipGetLastError() != hipSuccess) return FEC_ERR_HIP;
+        FEC_HIP(hipGetLastError());
     }
     hipLaunchKernelGGL(fec::ses_loss_kernel, dim3(static_cast<unsigned>((p.Q + 3) / 4)), dim3(256), 0, s, d_dest_out,
                        static_cast<const uint8_t*>(h->proc.p), d_payload, p.L, p.Q, d_dest_lost, d_lost);

@@ -36,6 +36,7 @@
 #include "fec_amd.h"
 #include "fec_host.h"
 #include "fec_kernels.h"
+#include "fec_status.h"
 
 namespace fec {
 namespace {
@@ -454,7 +455,7 @@ namespace {
 
 #define FS_TRY(expr)                              \
     do {                                          \
-        if ((expr) != hipSuccess) return FEC_ERR_HIP; \
+        FEC_HIP((expr)); \
     } while (0)
 
 // ids distinct and in range

@@ -42,6 +42,7 @@
 #include "fec_device.h"
 #include "fec_host.h"
 #include "fec_kernels.h"
+#include "fec_status.h"
 
 namespace fec {
 
@@ -554,10 +555,13 @@ constexpr int cmax(int x, int y) { return x > y ? x : y; }
 
 // The whole geometry at compile time (k, n1, n2 and the payload size L): every division,
 // bound and LDS offset below is a constant.
-template <int K_, int N1_, int N2_, int L_, bool RELAY_>
+template <int K_, int N1_, int N2_, int L_, bool RELAY_, int TR_ = kFR, bool V2_ = false>
 struct FastGeo {
     static constexpr int K = K_, N1 = N1_, N2 = N2_, L = L_;
     static constexpr bool RELAY = RELAY_;
+    static constexpr int TR = TR_;                        // packets per tile
+    static constexpr bool V2 = RELAY_ && V2_;             // relay: the row-scatter kernel (no CT / parity tiles)
+    static constexpr bool CT3 = RELAY && !V2;             // relay: the three-tile (CT, parity, words) kernel
     static constexpr int S = (L + 2 + K - 1) / K;        // code blocks (= sub-streams)
     static constexpr int S4 = (S + 3) & ~3, G = S4 / 4;  // CT words per position
     static constexpr int N = RELAY ? N1 : N2;            // code length of the rows read
@@ -566,22 +570,25 @@ struct FastGeo {
     static constexpr int STRIDE = RELAY ? S * N1 : F;    // input row bytes
     static constexpr int H = RELAY ? N1 + N2 - 2 : N2 - 1;  // rows staged in front of a tile
     static constexpr int D0 = RELAY ? N2 - 1 : 0;        // packets decoded in front of a tile
-    static constexpr int ROWS = kFR + H;
+    static constexpr int ROWS = TR + H;
     static constexpr int OUT_ROW = RELAY ? F : S * K;
     static constexpr int F4 = (F + 3) & ~3;              // LDS frame pitch
     static constexpr int ES = (K * (1 + N) + 3) & ~3;    // rule entry bytes (fec_host.h DecodeRules)
     static constexpr int CTROW = K * S4;
     static constexpr int QCH = (16 + ROWS * STRIDE + 16 * kFT - 1) / (16 * kFT);  // slab chunks per thread
-    static constexpr int SCH = (kFR * OUT_ROW + 16 * kFT - 1) / (16 * kFT);      // output chunks per thread
+    static constexpr int SCH = (TR * OUT_ROW + 16 * kFT - 1) / (16 * kFT);      // output chunks per thread
     static constexpr int OFF_PMASK = 1552;
-    static constexpr int OFF_RULE = OFF_PMASK + 4 * (kFR + 64);
+    static constexpr int OFF_RULE = OFF_PMASK + 4 * (TR + 64);
     static constexpr int RULE_U16 = K + K * N + 4;      // per wave
     static constexpr int OFF_TB = al16(OFF_RULE + kFW * 2 * RULE_U16);
-    static constexpr int OFF_CT = al16(OFF_TB + (RELAY ? (N2 - K) * K * 20 : 0));
-    static constexpr int OFF_OW = al16(OFF_CT + (RELAY ? ROWS * CTROW : 0));
-    static constexpr int OFF_RAW = al16(OFF_OW + (RELAY ? (N2 - K) * kFR * S4 : 0));
-    static constexpr int RAWB = al16(cmax(16 + ROWS * STRIDE + 4 * N + 32, RELAY ? (kFR + 1) * F4 : 0));
-    static constexpr int LDS = OFF_RAW + RAWB;
+    static constexpr int OFF_CT = al16(OFF_TB + (CT3 ? (N2 - K) * K * 20 : 0));
+    static constexpr int OFF_OW = al16(OFF_CT + (CT3 ? ROWS * CTROW : 0));
+    static constexpr int OFF_RAW = al16(OFF_OW + (CT3 ? (N2 - K) * TR * S4 : 0));
+    static constexpr int RAWB = al16(cmax(16 + ROWS * STRIDE + 4 * N + 32, CT3 ? (TR + 1) * F4 : 0));
+    static constexpr int OFF_FR = OFF_RAW + RAWB;         // V2: the tile's frames at their own stride F
+    static constexpr int LDS = OFF_FR + (V2 ? al16(TR * F) : 0);
+    // waves per SIMD (the register budget of __launch_bounds__: 128 VGPRs, two workgroups per CU)
+    static constexpr int WPE = 4;
     static constexpr uint32_t MDIV = static_cast<uint32_t>((uint64_t(1) << 32) / OUT_ROW + 1);
     static constexpr uint32_t MSTRIDE = static_cast<uint32_t>((uint64_t(1) << 32) / STRIDE + 1);
     // the H rows in front of a tile that is not a workgroup's first are the last H rows of the tile
@@ -590,7 +597,8 @@ struct FastGeo {
     static constexpr int DLT = (16 - (H * STRIDE) % 16) % 16;
     static constexpr int NH = (DLT + H * STRIDE) / 16;
     static constexpr int HQ = (NH + kFT - 1) / kFT;
-    static_assert(H <= 64 && D0 + kFR <= kFR + 64, "rows in front of a tile");
+    static_assert(H <= 64 && D0 + TR <= TR + 64 && D0 + TR <= kFT, "rows in front of a tile");
+    static_assert(TR % 16 == 0 && TR <= 64, "tile rows: t0 * STRIDE and t0 * F multiples of 16");
     static_assert((DLT + H * STRIDE) % 16 == 0, "carried rows");
 };
 
@@ -679,8 +687,8 @@ struct FastTile {
     // (the tile follows this workgroup's previous one) its first NH chunks come from keep() instead
     __device__ void issue(int64_t tile, bool cont) {
         carry_next = cont;
-        const int64_t t0 = tile * kFR, r0 = t0 - H;
-        const int nt = static_cast<int>(min<int64_t>(kFR, a.P - t0));
+        const int64_t t0 = tile * GM::TR, r0 = t0 - H;
+        const int nt = static_cast<int>(min<int64_t>(GM::TR, a.P - t0));
         const int64_t g0 = r0 * STRIDE;                         // may be negative
         const int64_t A = g0 >= 0 ? (g0 & ~int64_t(15)) : -((-g0 + 15) & ~int64_t(15));
         const int64_t base = A > 0 ? A : 0;
@@ -705,12 +713,12 @@ struct FastTile {
     }
     // after the decode (the rows are final): the last H rows of this (full) tile, which the next
     // tile of the workgroup starts with, into registers -- chunk c of the next slab is chunk
-    // kFR * STRIDE / 16 + c of this one
+    // TR * STRIDE / 16 + c of this one
     __device__ void keep() {
 #pragma unroll
         for (int q = 0; q < HQ; ++q) {
             const int c = tid + q * kFT;
-            if (c < NH) hc[q] = *reinterpret_cast<const uint4*>(smem + GM::OFF_RAW + kFR * STRIDE + 16 * c);
+            if (c < NH) hc[q] = *reinterpret_cast<const uint4*>(smem + GM::OFF_RAW + GM::TR * STRIDE + 16 * c);
         }
     }
     __device__ uint32_t rowb(int l) const { return static_cast<uint32_t>(GM::OFF_RAW + dlt + l * STRIDE); }
@@ -849,8 +857,8 @@ __global__ __launch_bounds__(kFT) void fec_sw_fast_dest_kernel(SwFastArgs a) {
     PhaseClock clk(a.stamps != nullptr);
     if (tile0 < tile1) T.issue(tile0, false);
     for (int64_t tile = tile0; tile < tile1; ++tile) {
-        const int64_t t0 = tile * kFR;
-        const int nt = static_cast<int>(min<int64_t>(kFR, a.P - t0));
+        const int64_t t0 = tile * GM::TR;
+        const int nt = static_cast<int>(min<int64_t>(GM::TR, a.P - t0));
         clk.mark(0);
         T.land();
         T.masks(t0, nt);
@@ -941,8 +949,8 @@ __global__ __launch_bounds__(kFT, 4) void fec_sw_fast_relay_kernel(SwFastArgs a)
     PhaseClock clk(a.stamps != nullptr);
     if (tile0 < tile1) T.issue(tile0, false);
     for (int64_t tile = tile0; tile < tile1; ++tile) {
-        const int64_t t0 = tile * kFR;
-        const int nt = static_cast<int>(min<int64_t>(kFR, a.P - t0));
+        const int64_t t0 = tile * GM::TR;
+        const int nt = static_cast<int>(min<int64_t>(GM::TR, a.P - t0));
         clk.mark(0);
         T.land();
         T.masks(t0, nt);
@@ -1080,6 +1088,147 @@ __global__ __launch_bounds__(kFT, 4) void fec_sw_fast_relay_kernel(SwFastArgs a)
     clk.flush(a.stamps);
 }
 
+// Relay, row scatter: frame t block j position p depends on one (decoded) row only, row
+// t - p - n1 + k: its data symbols m of block j (p < k: symbol k-1-p; p >= k: XOR_m G2[k-1-m][p] *
+// symbol m).  A lane per (row, group of 4 blocks) reads the row's 4*n1-byte span once (n1+1 dword
+// reads + v_alignbyte), forms the k symbol words by v_perm, the n2-k parity words with the G2
+// tables in scalar registers, and writes each position's 4 bytes straight into the frames of the
+// tile, laid out in LDS at their own stride F (one base address, every byte at a compile-time
+// offset); the frames then go out as 16-byte chunks.  Three barriers per tile.
+template <class GM>
+__global__ __launch_bounds__(kFT, GM::WPE) void fec_sw_fast_relay2_kernel(SwFastArgs a) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    constexpr int K = GM::K, N1 = GM::N1, N2 = GM::N2, S = GM::S, G = GM::G, F = GM::F, TR = GM::TR;
+    constexpr int size = (S + 1) * N2;
+    constexpr int TAIL = F - 4 - S * N2;  // zero bytes after the blocks
+    static_assert(GM::OFF_FR >= (N2 - 1) * F, "frame base addresses stay non-negative");
+    FastTile<GM> T(smem, a);
+    // the G2 tables are read with uniform, compile-time indices: scalar loads into SGPRs
+    const auto* tab = (const __attribute__((address_space(4))) uint32_t*)(a.tab);
+    __syncthreads();
+    const int64_t tile0 = static_cast<int64_t>(blockIdx.x) * a.tiles_per_wg;
+    const int64_t tile1 = min(tile0 + a.tiles_per_wg, a.ntiles);
+    PhaseClock clk(a.stamps != nullptr);
+    if (tile0 < tile1) T.issue(tile0, false);
+    for (int64_t tile = tile0; tile < tile1; ++tile) {
+        const int64_t t0 = tile * TR;
+        const int nt = static_cast<int>(min<int64_t>(TR, a.P - t0));
+        clk.mark(0);
+        T.land();
+        T.masks(t0, nt);
+        if (tile + 1 < tile1) T.issue(tile + 1, a.carry != 0);
+        __syncthreads();
+        clk.mark(1);
+        T.decode();
+        __syncthreads();
+        if (a.carry && tile + 1 < tile1) T.keep();
+        clk.mark(2);
+        // rows k-1 .. k-1 + nt+n2-2 feed the tile's frames: row k-1+r, position p -> frame r-(n2-1)+p.
+        // Interior rows (r in [n2-1, nt)) reach a frame of the tile at every position; with a full
+        // group of 4 blocks their lanes write every byte without a test.  The other items -- the
+        // n2-1 rows at each end of the span and the partial last group -- test each position.
+        auto scatter = [&](int r, int g, auto checked) __attribute__((always_inline)) {
+            constexpr bool CHK = decltype(checked)::value;
+            const uint32_t sb = T.rowb(K - 1 + r) + 4 * g * N1;
+            const uint32_t ab = sb & 0x1fffcu;
+            uint32_t d[N1 + 1];
+#pragma unroll
+            for (int q = 0; q <= N1; ++q) d[q] = *reinterpret_cast<const uint32_t*>(smem + ab + 4 * q);
+            align_words(d, static_cast<int>(sb & 3));
+            uint32_t x[K], n0[K], n1[K], n2[K];  // symbol words and their 3-3-2 bit groups (gf_mul4x)
+#pragma unroll
+            for (int m = 0; m < K; ++m) {
+                x[m] = gather4(d, m, N1 + m, 2 * N1 + m, 3 * N1 + m);
+                n0[m] = x[m] & 0x07070707u;
+                n1[m] = (x[m] >> 3) & 0x07070707u;
+                n2[m] = (x[m] >> 6) & 0x03030303u;
+            }
+            const int tf = r - (N2 - 1);  // frame of position 0
+            const uint32_t fb = static_cast<uint32_t>(GM::OFF_FR + tf * F + 4 + 4 * g * N2) & 0x1ffffu;
+            const int nb = CHK ? min(4, S - 4 * g) : 4;
+            tfor_sw<N2>([&](auto pc) __attribute__((always_inline)) {
+                constexpr int p = decltype(pc)::value;
+                const int t = tf + p;
+                if (!CHK || (t >= 0 && t < nt)) {
+                    uint32_t w;
+                    if constexpr (p < K) {
+                        w = x[K - 1 - p];
+                    } else {
+                        w = 0;
+#pragma unroll
+                        for (int m = 0; m < K; ++m) {
+                            const int e = (p * K + m) * 5;
+                            w ^= __builtin_amdgcn_perm(tab[e + 1], tab[e], n0[m]) ^
+                                 __builtin_amdgcn_perm(tab[e + 3], tab[e + 2], n1[m]) ^
+                                 __builtin_amdgcn_perm(tab[e + 4], tab[e + 4], n2[m]);
+                        }
+                    }
+                    uint8_t* dst = smem + fb + p * (F + 1);
+                    dst[0] = static_cast<uint8_t>(w);
+                    if (!CHK || nb > 1) dst[N2] = static_cast<uint8_t>(w >> 8);
+                    if (!CHK || nb > 2) dst[2 * N2] = static_cast<uint8_t>(w >> 16);
+                    if (!CHK || nb > 3) dst[3 * N2] = static_cast<uint8_t>(w >> 24);
+                }
+            });
+        };
+        {
+            constexpr int GF = S / 4;                      // full groups
+            constexpr int GP = G - GF;                     // 0 or 1 partial group
+            const int nint = max(0, nt - (N2 - 1));        // interior rows
+            const int back0 = max(N2 - 1, nt);             // first row of the back end
+            const int nback = nt + N2 - 1 - back0;
+            const int n_int = nint * GF;
+            const int n_all = n_int + (N2 - 1 + nback) * G + nint * GP;
+            for (int it = T.tid; it < n_all; it += kFT) {
+                if (it < n_int) {
+                    const int r = N2 - 1 + it / GF, g = it - (it / GF) * GF;
+                    scatter(r, g, std::false_type{});
+                } else {
+                    int i = it - n_int, r, g;
+                    if (i < (N2 - 1) * G) {
+                        r = i / G;
+                        g = i - r * G;
+                    } else if ((i -= (N2 - 1) * G) < nback * G) {
+                        r = back0 + i / G;
+                        g = i - (i / G) * G;
+                    } else {
+                        r = N2 - 1 + (i - nback * G);
+                        g = GF;
+                    }
+                    scatter(r, g, std::true_type{});
+                }
+            }
+        }
+        // each frame's 4 header bytes (BE16 size, two zeros) and its zero tail
+        for (int it = T.tid; it < nt * (4 + TAIL); it += kFT) {
+            const int t = it / (4 + TAIL), b = it - t * (4 + TAIL);
+            const uint8_t v = b == 0 ? uint8_t(size >> 8) : b == 1 ? uint8_t(size & 255) : uint8_t(0);
+            smem[GM::OFF_FR + t * F + (b < 4 ? b : S * N2 + b)] = v;
+        }
+        __syncthreads();
+        clk.mark(3);
+        // the frames out, 16 bytes per lane (t0*F is a multiple of 16)
+        const int obytes = nt * F;
+        uint8_t* gout = a.out + t0 * F;
+        const __amdgpu_buffer_rsrc_t ro = __builtin_amdgcn_make_buffer_rsrc(gout, 0, obytes & ~15, 0x00020000);
+#pragma unroll
+        for (int qq = 0; qq < GM::SCH; ++qq) {
+            const int c = T.tid + qq * kFT;
+            const uint32_t b = 16 * c;
+            if (static_cast<int>(b) >= obytes) break;
+            const uint4 v = *reinterpret_cast<const uint4*>(smem + GM::OFF_FR + b);
+            if (static_cast<int>(b) + 16 <= obytes) {
+                __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(fec_v4u32, v), ro, b, 0, 0);
+            } else {  // the output's ragged end
+                const uint32_t vv[4] = {v.x, v.y, v.z, v.w};
+                for (int x = 0; static_cast<int>(b) + x < obytes; ++x) gout[b + x] = uint8_t(vv[x >> 2] >> (8 * (x & 3)));
+            }
+        }
+        clk.mark(4);
+    }
+    clk.flush(a.stamps);
+}
+
 }  // namespace fec
 
 struct fec_swdf {
@@ -1193,10 +1342,11 @@ constexpr int kFastN = 11, kFastL = 300;
 
 template <class GM>
 bool launch_fast_geo(fec::SwFastArgs a, hipStream_t s, hipError_t* err) {
-    using fec::kFR;
     using fec::kFT;
+    constexpr int kFR = GM::TR;
     auto kern = [] {
-        if constexpr (GM::RELAY) return fec::fec_sw_fast_relay_kernel<GM>;
+        if constexpr (GM::V2) return fec::fec_sw_fast_relay2_kernel<GM>;
+        else if constexpr (GM::RELAY) return fec::fec_sw_fast_relay_kernel<GM>;
         else return fec::fec_sw_fast_dest_kernel<GM>;
     }();
     constexpr int lds = GM::LDS;
@@ -1237,10 +1387,25 @@ bool launch_fast_geo(fec::SwFastArgs a, hipStream_t s, hipError_t* err) {
                      "FEC_SWDF_STAMPS fast %s K=%d grid=%u tiles/wg=%d lds=%d: cycles per tile of %d: %s %.0f %.0f %.0f "
                      "%.0f %.0f %.0f\n",
                      GM::RELAY ? "relay" : "dest", GM::K, g, a.tiles_per_wg, lds, kFR,
-                     GM::RELAY ? "land+masks/decode/CT/parity/words/store" : "land+masks/decode/out", sum[0] / tl,
+                     GM::V2 ? "land+masks/decode/scatter/store" : GM::RELAY ? "land+masks/decode/CT/parity/words/store"
+                                                                       : "land+masks/decode/out",
+                     sum[0] / tl,
                      sum[1] / tl, sum[2] / tl, sum[3] / tl, sum[4] / tl, sum[5] / tl);
     }
     return true;
+}
+
+// The relay's kernel: the row scatter (default) with tiles of FEC_SWDF_TR = 64 / 48 / 32 packets,
+// or FEC_SWDF_RELAY=3 the three-tile kernel of round 5 (kept for A/B).
+int relay_variant() {
+    static const int v = [] {
+        const char* r = std::getenv("FEC_SWDF_RELAY");
+        if (r && r[0] == '3') return 0;
+        const char* t = std::getenv("FEC_SWDF_TR");
+        const int tr = t ? std::atoi(t) : 64;
+        return tr == 32 ? 32 : tr == 48 ? 48 : 64;
+    }();
+    return v;
 }
 
 template <bool RELAY>
@@ -1248,10 +1413,16 @@ bool launch_fast(int K, fec::SwFastArgs a, int L, int n1, int n2, int blocks, in
                  hipError_t* err) {
     if (L != kFastL || n2 != kFastN || (RELAY && n1 != kFastN) || blocks != S) return false;
     if ((reinterpret_cast<uintptr_t>(a.in) & 15) || (reinterpret_cast<uintptr_t>(a.out) & 3)) return false;
+    const int rv = RELAY ? relay_variant() : 0;
 #define FEC_SW_FAST_CASE(KK)                                                        \
     case KK: {                                                                      \
         using GM = fec::FastGeo<KK, kFastN, kFastN, kFastL, RELAY>;                  \
         if (stride != GM::STRIDE) return false;                                     \
+        if constexpr (RELAY) {                                                      \
+            if (rv == 64) return launch_fast_geo<fec::FastGeo<KK, kFastN, kFastN, kFastL, true, 64, true>>(a, s, err); \
+            if (rv == 48) return launch_fast_geo<fec::FastGeo<KK, kFastN, kFastN, kFastL, true, 48, true>>(a, s, err); \
+            if (rv == 32) return launch_fast_geo<fec::FastGeo<KK, kFastN, kFastN, kFastL, true, 32, true>>(a, s, err); \
+        }                                                                           \
         return launch_fast_geo<GM>(a, s, err);                                      \
     }
     switch (K) {
@@ -1386,7 +1557,7 @@ int fec_swdf_relay_batch(fec_swdf* w, const uint8_t* d_cw, int64_t cw_stride, co
                     for (int x = 0; x < 4; ++x) t[4] |= uint32_t(f.mt[c][x << 6]) << (8 * x);
                 }
             if (hipMalloc(&w->d_tab, tab.size() * 4) != hipSuccess) return FEC_ERR_NOMEM;
-            if (hipMemcpy(w->d_tab, tab.data(), tab.size() * 4, hipMemcpyHostToDevice) != hipSuccess) return FEC_ERR_HIP;
+            FEC_HIP(hipMemcpy(w->d_tab, tab.data(), tab.size() * 4, hipMemcpyHostToDevice));
         }
         fec::SwFastArgs a{};
         a.carry = carry_enabled() ? 1 : 0;

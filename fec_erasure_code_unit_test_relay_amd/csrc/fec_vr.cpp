@@ -23,12 +23,14 @@
 
 #include "fec_amd.h"
 #include "fec_kernels.h"
+#include "fec_status.h"
 
 // FEC_VR_PROFILE (diagnostic builds only): cycle counts of the control loop's parts --
 // 0 steady stretch check, 1 transition stretch, 2 sender + encoder, 3 feedback, 4 decoder, 5 loop top.
 #ifdef FEC_VR_PROFILE
 #include <x86intrin.h>
-#define FEC_VR_PROF_DECL uint64_t prof_c[6] = {}, prof_t = __rdtsc();
+#include <map>
+#define FEC_VR_PROF_DECL uint64_t prof_c[6] = {}, prof_t = __rdtsc(); int64_t prof_cls[64] = {}; std::map<int, int64_t> prof_why_h;
 #define FEC_VR_PROF(k)                 \
     {                                  \
         const uint64_t t_ = __rdtsc(); \
@@ -39,7 +41,10 @@
     std::fprintf(stderr, "vr control Mcycles: steady %.3f transition %.3f sender %.3f feedback %.3f "      \
                          "decoder %.3f top %.3f\n",                                                        \
                  prof_c[0] * 1e-6, prof_c[1] * 1e-6, prof_c[2] * 1e-6, prof_c[3] * 1e-6, prof_c[4] * 1e-6, \
-                 prof_c[5] * 1e-6);
+                 prof_c[5] * 1e-6);                                                                    \
+    for (int c_ = 0; c_ < 64; ++c_)                                                                        \
+        if (prof_cls[c_]) std::fprintf(stderr, "vr iteration class %2d: %lld\n", c_, (long long)prof_cls[c_]); \
+    for (auto& w_ : prof_why_h) std::fprintf(stderr, "vr class-0 why %#x: %lld\n", w_.first, (long long)w_.second);
 #else
 #define FEC_VR_PROF_DECL
 #define FEC_VR_PROF(k)
@@ -320,8 +325,10 @@ void VrPlan::start_workers() {
                     qsize_.store(q_.empty() && qclosed_ ? -1 : static_cast<int64_t>(q_.size()),
                                  std::memory_order_release);
                 }
-                if (j.id <= -2) {  // feedback job -2 - id
-                    feedback_job(-2 - static_cast<int64_t>(j.id), fb_T_, fb_mds_);
+                if (j.id <= -2) {  // feedback jobs of run -2 - id, in order
+                    const int64_t c = -2 - static_cast<int64_t>(j.id), nj = static_cast<int64_t>(fb_jobs_.size());
+                    const int64_t ch = static_cast<int64_t>(fb_chunk_);
+                    for (int64_t jf = c * ch; jf < std::min(nj, (c + 1) * ch); ++jf) feedback_job(jf, fb_T_, fb_mds_);
                 } else if (j.id < 0) {  // final_sum_coding_rate, one float add per packet in sending order
                     float s = 0;
                     for (const RateRun& r : rate_runs) s = float_add_repeated(s, r.rate, r.count);
@@ -612,11 +619,18 @@ void VrPlan::control(const uint8_t* pattern, int64_t n_pattern, int T, int B, in
     // dropped packets (ERASURE_TYPE 5: pattern byte 1 for seq < P+T), then the feedback stream
     const auto tc0 = std::chrono::steady_clock::now();
     const int64_t n_drop = std::min<int64_t>(P + T, n_pattern);  // packets the pattern can drop
-    for (int64_t q = 0; q < n_drop;) {
-        const void* hit = std::memchr(pattern + q, 1, static_cast<size_t>(n_drop - q));
-        if (!hit) break;
-        q = static_cast<const uint8_t*>(hit) - pattern;
-        drops.push_back(q++);
+    // eight pattern bytes per test (a memchr call per drop cost ~20 ns each, 5 543 drops)
+    {
+        int64_t q = 0;
+        for (; q + 8 <= n_drop; q += 8) {
+            uint64_t w;
+            std::memcpy(&w, pattern + q, 8);
+            if (w == 0) continue;
+            for (int b = 0; b < 8; ++b)
+                if (pattern[q + b] == 1) drops.push_back(q + b);
+        }
+        for (; q < n_drop; ++q)
+            if (pattern[q] == 1) drops.push_back(q);
     }
     feedback_plan(P + T + 1);
     // FEC_VR_FB_SYNC (diagnostic): the feedback jobs run to the end on this thread first
@@ -654,10 +668,17 @@ void VrPlan::control(const uint8_t* pattern, int64_t n_pattern, int T, int B, in
     const auto tc1 = std::chrono::steady_clock::now();
     start_workers();
     if (!fb_sync && !fb_thread_on) {
+        // a few contiguous runs of jobs, one per worker (a queue entry per job -- thousands of
+        // them -- kept the workers on the queue's lock while the control loop published)
+        const size_t nj = fb_jobs_.size();
+        size_t nchunk = std::max<size_t>(1, workers_.size());
+        if (const char* e = std::getenv("FEC_VR_FB_CHUNKS")) nchunk = static_cast<size_t>(std::max(1, std::atoi(e)));
+        nchunk = std::min(nchunk, std::max<size_t>(1, nj));
+        fb_chunk_ = (nj + nchunk - 1) / nchunk;
         std::lock_guard<std::mutex> lk(qmu_);
-        for (size_t jf = 0; jf < fb_jobs_.size(); ++jf) {
+        for (size_t c = 0; c * fb_chunk_ < nj; ++c) {
             DecJob fj;
-            fj.id = -2 - static_cast<int>(jf);
+            fj.id = -2 - static_cast<int>(c);
             q_.push_back(std::move(fj));
         }
         qsize_.store(static_cast<int64_t>(q_.size()), std::memory_order_release);
@@ -706,6 +727,8 @@ void VrPlan::control(const uint8_t* pattern, int64_t n_pattern, int T, int B, in
     // reports the missing ones exactly as if they had arrived, and the feedback after it is bounded by
     // the feedback stream's next change -- so a stretch only has to end on a received packet.
     const bool drop_stretch = !std::getenv("FEC_VR_NO_DROP_STRETCH");
+    // FEC_VR_FB_STOP (A/B): steady stretches end before the feedback change's packet (round 5)
+    const bool fb_through = !std::getenv("FEC_VR_FB_STOP");
     // one past the last received packet in [lo, hi), or lo if every one of them drops
     auto received_end = [&](int64_t lo, int64_t hi) {
         auto j = std::lower_bound(drops.begin(), drops.end(), hi);
@@ -774,24 +797,45 @@ void VrPlan::control(const uint8_t* pattern, int64_t n_pattern, int T, int B, in
     for (int64_t seq = 0;; ++seq) {
         ++n_iter;
         FEC_VR_PROF(5)
+#ifdef FEC_VR_PROFILE
+        int prof_why = (cur < 0 ? 1 : 0) | (transition_flag ? 2 : 0) | (double_coding_flag ? 4 : 0) |
+                       (counter_transition <= eT ? 8 : 0) | (latest_seq != seq ? 16 : 0) | (dcf ? 32 : 0) |
+                       (sdc >= seq ? 64 : 0) | (dT != eT || dB != eB || dN != eN ? 128 : 0) |
+                       (udp[3] != eT || udp[4] != eB || udp[5] != eN ? 256 : 0) | (fb.next(seq) <= seq ? 512 : 0);
+#endif
         // ---- steady stretch: the same frame, every packet received, nothing switching ----
         // Every branch below is then fixed: the feedback repeats (no change in the feedback
         // stream), the encoder has no switch to make and no transition running, the decoder has
         // no gap, no parameter change and no double decoding.  Such packets are appended in one
-        // step (frames, coding-rate terms and reports as runs); the stretch ends before the next
-        // drop, the next feedback change and the last packet.
-        if (cur >= 0 && !transition_flag && !double_coding_flag && counter_transition > eT && seq_start >= 0 &&
-            latest_seq == seq && !dcf && sdc < seq && dT == eT && dB == eB && dN == eN && seq < P + T - 1) {
+        // step (frames, coding-rate terms and reports as runs).  The stretch runs through the next
+        // feedback change's packet (its own frame, rate and decoder call are a steady packet's; only
+        // the udp after it differs, set at the end) and ends before the last packet.  It may start
+        // at the packet that ends a transition (counter T+1: the encoder cannot switch there and
+        // clears transition_flag, which is all that differs from a steady packet).
+        const bool flip = fast_transitions && transition_flag && counter_transition == eT + 1;
+        if (cur >= 0 && (!transition_flag || flip) && !double_coding_flag && counter_transition > eT &&
+            seq_start >= 0 && latest_seq == seq && !dcf && sdc < seq && dT == eT && dB == eB && dN == eN &&
+            seq < P + T - 1) {
             const int fT = adaptive && udp[0] != 0 ? udp[0] : sT, fB = adaptive && udp[0] != 0 ? udp[1] : sB,
                       fN = adaptive && udp[0] != 0 ? udp[2] : sN;
             const int aT = adaptive && udp[0] != 0 ? udp[3] : sT_ack, aB = adaptive && udp[0] != 0 ? udp[4] : sB_ack;
             const bool would_switch = (fT != eT || fB != eB || fN != eN) && aT == eT && aB == eB;
+#ifdef FEC_VR_PROFILE
+            prof_why |= (would_switch ? 1024 : 0) | (seq >= P + T - 1 ? 2048 : 0);
+#endif
             if (!would_switch && udp[3] == eT && udp[4] == eB && udp[5] == eN) {
                 while (dri < drops.size() && drops[dri] < seq) ++dri;
                 const int64_t next_drop = dri < drops.size() ? drops[dri] : INT64_MAX;
                 const int64_t next_fb = fb.next(seq);
-                const int64_t end = drop_stretch ? received_end(seq, std::min(next_fb, P + T - 1))
+                // through the feedback change's packet (a received one) when it comes before the last
+                const bool fb_step = drop_stretch && fb_through && next_fb < P + T - 1 &&
+                                     !(next_fb < n_pattern && pattern[next_fb] == 1);
+                const int64_t end = fb_step ? next_fb + 1
+                                  : drop_stretch ? received_end(seq, std::min(next_fb, P + T - 1))
                                                  : std::min({next_drop, next_fb, P + T - 1});
+#ifdef FEC_VR_PROFILE
+                prof_why |= end > seq ? 0 : 4096;
+#endif
                 if (end > seq) {
                     if (adaptive && udp[0] != 0) {
                         sT = udp[0];
@@ -801,6 +845,7 @@ void VrPlan::control(const uint8_t* pattern, int64_t n_pattern, int T, int B, in
                         sB_ack = udp[4];
                         sN_ack = udp[5];
                     }
+                    if (flip) transition_flag = false;
                     VrFrame fr;
                     fr.T = eT;
                     fr.B = eB;
@@ -816,6 +861,12 @@ void VrPlan::control(const uint8_t* pattern, int64_t n_pattern, int T, int B, in
                     sent = end;
                     steady_packets += end - seq;
                     ++n_jump;
+                    if (fb_step) {  // the udp after the stretch's last packet (T, B, N: the frame's)
+                        const uint32_t v = fb.value(end - 1);
+                        udp[0] = static_cast<uint8_t>(v);
+                        udp[1] = static_cast<uint8_t>(v >> 8);
+                        udp[2] = static_cast<uint8_t>(v >> 16);
+                    }
                     seq = end;
                 }
             }
@@ -847,25 +898,38 @@ void VrPlan::control(const uint8_t* pattern, int64_t n_pattern, int T, int B, in
                 const float rate1 = static_cast<float>(eT - eN + 1) / (eT - eN + 1 + eB);
                 const float rate2 = static_cast<float>(eT - eN + 1) /
                                     ((eT - eN + 1 + eB) + (eT - eN_old + 1) + (eT - eN_old + 1 + eB));
-                int64_t old_end = -1;
-                for (int64_t q = seq; q < end; ++q) {
-                    VrFrame fr;
-                    fr.T = eT;
-                    fr.B = eB;
-                    fr.N = eN;
-                    fr.enc_cur = cur;
-                    fr.counter = counter_transition;
-                    if (counter_transition == eT) double_coding_flag = false;
-                    ++counter_transition;
-                    if (old >= 0 && double_coding_flag) {
-                        fr.enc_old = old;
-                        old_end = q + 1;
+                // per packet q (counter c = c0 + q - seq): the packet with c == eT ends double coding
+                // before its rate is added, so packets c < eT carry the old codeword and rate2, the
+                // rest rate1 -- in closed form: n2 double-coded packets, then n - n2
+                const int64_t n = end - seq;
+                const int c0 = counter_transition;
+                const int64_t n2 = double_coding_flag ? std::min<int64_t>(n, eT - c0) : 0;
+                auto frames = [&](int64_t q0, int64_t cnt, bool with_old) {
+                    // the first packets per packet (they settle the run's counter step), the rest
+                    // extend that run
+                    for (int64_t q = q0; q < q0 + std::min<int64_t>(cnt, 3); ++q) {
+                        VrFrame fr;
+                        fr.T = eT;
+                        fr.B = eB;
+                        fr.N = eN;
+                        fr.enc_cur = cur;
+                        fr.counter = c0 + static_cast<int>(q - seq);
+                        if (with_old) fr.enc_old = old;
+                        put_frame(q, fr);
                     }
-                    put_rate(1, double_coding_flag ? rate2 : rate1);
-                    put_frame(q, fr);
+                };
+                if (n2 > 0) {
+                    put_rate(n2, rate2);
+                    frames(seq, n2, old >= 0);
+                    if (old >= 0) enc[old].end = seq + n2;
                 }
+                if (n > n2) {
+                    put_rate(n - n2, rate1);
+                    frames(seq + n2, n - n2, false);
+                }
+                if (double_coding_flag && c0 + n - 1 >= eT) double_coding_flag = false;
+                counter_transition = c0 + static_cast<int>(n);
                 enc[cur].end = end;
-                if (old_end >= 0) enc[old].end = old_end;
                 // decoder: [seq, split) double decoding (old and new instance), [split, end) the new one
                 const int64_t split = dcf ? std::min(end, sde + 1) : seq;
                 if (split > seq) {
@@ -903,7 +967,9 @@ void VrPlan::control(const uint8_t* pattern, int64_t n_pattern, int T, int B, in
                 udp[3] = static_cast<uint8_t>(eT);
                 udp[4] = static_cast<uint8_t>(eB);
                 udp[5] = static_cast<uint8_t>(eN);
-                seq = end;
+                // packet `end` from the top: a steady stretch may start at it (the transition's end)
+                seq = end - 1;
+                continue;
             }
         }
         FEC_VR_PROF(1)
@@ -972,6 +1038,11 @@ void VrPlan::control(const uint8_t* pattern, int64_t n_pattern, int T, int B, in
 
         // ---- Application_Layer_Receiver::receive_message_and_decode ----
         FEC_VR_PROF(2)
+#ifdef FEC_VR_PROFILE
+        if (!drop && !transition_flag && latest_seq == seq) ++prof_why_h[prof_why];
+        ++prof_cls[(drop ? 1 : 0) | (transition_flag ? 2 : 0) | (double_coding_flag ? 4 : 0) |
+                   (latest_seq != seq ? 8 : 0) | (fr.counter == 0 ? 16 : 0) | (seq_start < 0 ? 32 : 0)];
+#endif
         if (drop) continue;  // artificial erasure: returns -1, feedback unchanged
         const uint32_t fbv = fb.value(seq);  // the estimators' feedback after seq
         FEC_VR_PROF(3)
@@ -1097,9 +1168,9 @@ struct Upload {
         if (used) (void)hipEventDestroy(used);
     }
     int begin() {
-        if (!sent && hipEventCreateWithFlags(&sent, hipEventDisableTiming) != hipSuccess) return FEC_ERR_HIP;
-        if (!used && hipEventCreateWithFlags(&used, hipEventDisableTiming) != hipSuccess) return FEC_ERR_HIP;
-        if (hipEventSynchronize(sent) != hipSuccess) return FEC_ERR_HIP;
+        if (!sent) FEC_HIP(hipEventCreateWithFlags(&sent, hipEventDisableTiming));
+        if (!used) FEC_HIP(hipEventCreateWithFlags(&used, hipEventDisableTiming));
+        FEC_HIP(hipEventSynchronize(sent));
         size = 0;
         fix.clear();
         return FEC_OK;
@@ -1124,10 +1195,10 @@ struct Upload {
     void add(const T** dptr, const std::vector<T, A>& v) { add(dptr, v.data(), v.size()); }
     // device buffer of at least `bytes`, free of earlier readers on stream s
     static int reserve(void** dp, size_t* cap, size_t bytes, hipEvent_t used, hipStream_t s) {
-        if (hipStreamWaitEvent(s, used, 0) != hipSuccess) return FEC_ERR_HIP;
+        FEC_HIP(hipStreamWaitEvent(s, used, 0));
         if (bytes <= *cap) return FEC_OK;
         if (*dp) {
-            if (hipEventSynchronize(used) != hipSuccess) return FEC_ERR_HIP;
+            FEC_HIP(hipEventSynchronize(used));
             (void)hipFree(*dp);
             *dp = nullptr;
             *cap = 0;
@@ -1139,8 +1210,8 @@ struct Upload {
     }
     int commit(hipStream_t s) {
         if (int st = reserve(&d, &dcap, std::max<size_t>(16, size), used, s)) return st;
-        if (hipMemcpyAsync(d, h, size, hipMemcpyHostToDevice, s) != hipSuccess) return FEC_ERR_HIP;
-        if (hipEventRecord(sent, s) != hipSuccess) return FEC_ERR_HIP;
+        FEC_HIP(hipMemcpyAsync(d, h, size, hipMemcpyHostToDevice, s));
+        FEC_HIP(hipEventRecord(sent, s));
         for (auto& f : fix) *f.first = static_cast<const uint8_t*>(d) + f.second;
         return FEC_OK;
     }
@@ -1175,7 +1246,7 @@ struct Fork {
     }
     int begin(hipStream_t s) {
         if (!ev_fork) {
-            if (hipEventCreateWithFlags(&ev_fork, hipEventDisableTiming) != hipSuccess) return FEC_ERR_HIP;
+            FEC_HIP(hipEventCreateWithFlags(&ev_fork, hipEventDisableTiming));
             for (int i = 0; i < kSide; ++i)
                 if (hipStreamCreateWithFlags(&st[i], hipStreamNonBlocking) != hipSuccess ||
                     hipEventCreateWithFlags(&ev_join[i], hipEventDisableTiming) != hipSuccess)
@@ -1203,7 +1274,7 @@ struct Fork {
         const int j = (i - 1) % kSide;
         if (int st = mark()) return st;
         if (!forked[j]) {
-            if (hipStreamWaitEvent(st[j], ev_fork, 0) != hipSuccess) return FEC_ERR_HIP;
+            FEC_HIP(hipStreamWaitEvent(st[j], ev_fork, 0));
             forked[j] = true;
         }
         *out = st[j];
@@ -1630,8 +1701,8 @@ int prepare_decode(fec_vr_plan* v, hipStream_t s) {
         hipMemcpyAsync(d + o_fate, p.fate.data(), P, hipMemcpyHostToDevice, s) != hipSuccess ||
         hipMemcpyAsync(d + o_slow, p.slow.data(), P, hipMemcpyHostToDevice, s) != hipSuccess)
         return FEC_ERR_HIP;
-    if (!v->pk_sent && hipEventCreateWithFlags(&v->pk_sent, hipEventDisableTiming) != hipSuccess) return FEC_ERR_HIP;
-    if (hipEventRecord(v->pk_sent, s) != hipSuccess) return FEC_ERR_HIP;
+    if (!v->pk_sent) FEC_HIP(hipEventCreateWithFlags(&v->pk_sent, hipEventDisableTiming));
+    FEC_HIP(hipEventRecord(v->pk_sent, s));
     v->d_pk_dec = reinterpret_cast<const int32_t*>(d);
     v->d_fate = d + o_fate;
     v->d_slow = d + o_slow;
@@ -1984,9 +2055,9 @@ int fec_vr_decode_batch(fec_vr_plan* v, const uint8_t* d_cw_cur, const uint8_t* 
     // the recovery writes only the rows (and lengths) the copy leaves alone: one launch holding both
     // (FEC_VR_FUSED=0: the copy on the caller's stream, the recovery beside it on a side stream)
     if (!v->geo_ready) {
-        if (!v->geo_done && hipEventCreateWithFlags(&v->geo_done, hipEventDisableTiming) != hipSuccess) return FEC_ERR_HIP;
+        if (!v->geo_done) FEC_HIP(hipEventCreateWithFlags(&v->geo_done, hipEventDisableTiming));
         if (int st = fec::vr_launch_geo(ca, hip_stream)) return st;
-        if (hipEventRecord(v->geo_done, s) != hipSuccess) return FEC_ERR_HIP;
+        FEC_HIP(hipEventRecord(v->geo_done, s));
         v->geo_ready = true;
         v->geo_stream = s;
     } else if (s != v->geo_stream && hipStreamWaitEvent(s, v->geo_done, 0) != hipSuccess) {  // a decode on another stream

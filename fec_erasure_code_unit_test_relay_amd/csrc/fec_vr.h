@@ -183,6 +183,7 @@ private:
     std::unique_ptr<std::atomic<uint8_t>[]> fb_ready_;  // per job: complete (any order)
     int fb_T_ = 0;
     bool fb_mds_ = false;
+    size_t fb_chunk_ = 1;  // feedback jobs per worker-pool run
     void start_workers();
     void publish(DecJob&& j, bool flush = false);
     void close_jobs();

@@ -44,6 +44,9 @@ typedef struct fec_decoder fec_decoder;    /* one streaming decoder (per stream)
 #define FEC_AMD_ABI_VERSION 2
 
 const char *fec_strerror(int status);
+/* The last failed HIP runtime call behind an FEC_ERR_HIP (its error name and source line), as a
+ * NUL-terminated string written to buf (truncated to size); returns its length, 0 when none. */
+int fec_last_error(char *buf, size_t size);
 int fec_version(void);
 
 /* ---- configuration -------------------------------------------------------------------------

@@ -513,7 +513,10 @@ def test_gpu_relay_vr_full_schedule_equals_driver(relay_type):
     schedule on bin/erasure.bin, hop 2 on bin/erasure2.bin, one fixed-rate batch per code with
     the instances end to end) equals, seq by seq, the reference-structured driver over the oracle's
     Decoder_Symbol_Wise methods for all 360 000 seqs: every frame (double-coding layout), every
-    destination output and loss flag, by the golden file's per-100-seq CRC-32 digests."""
+    destination output and loss flag, by the golden file's per-100-seq CRC-32 digests.  The golden
+    file (tests/golden/relay_vr_360k.json, make_relay_vr_golden.py) comes from this repo's oracle
+    driver, not from reference output (the reference ships none): parity unpinned.  The frame
+    layout through a switch is hand-traced in test_session.py::test_hop1_burst_then_adaptation."""
     import torch
     from fec_erasure_code_unit_test_relay_amd import fill_payload
     from fec_erasure_code_unit_test_relay_amd.relay import AdaptiveRelay, relay_digest

@@ -133,20 +133,27 @@ def test_published_adaptive_mds_log_is_not_the_current_code():
 @pytest.mark.parametrize("name,mds", [("bin_erasure", False), ("bin_erasure2", False), ("erasure50", True),
                                       ("erasure90", False)])
 def test_control_loop_transition_stretches_equal_packet_by_packet(monkeypatch, name, mds):
-    """The control loop appends the double-coding stretch after a switch in one pass, and runs
-    steady and transition stretches through dropped packets (fec_vr.cpp); FEC_VR_NO_FAST_TRANSITION
-    and FEC_VR_NO_DROP_STRETCH walk those packets one by one.  Both give the same schedule:
-    instances, every frame (counter, old instance), fates, reporting decoders, coding rate."""
+    """The control loop appends the double-coding stretch after a switch in one pass (and the
+    packet that ends it with the steady stretch after it), runs steady and transition stretches
+    through dropped packets and steady stretches through the feedback change's packet (fec_vr.cpp);
+    FEC_VR_NO_FAST_TRANSITION, FEC_VR_NO_DROP_STRETCH and FEC_VR_FB_STOP walk those packets one by
+    one.  All give the same schedule: instances, every frame (counter, old instance), fates,
+    reporting decoders, coding rate."""
     pat = load_pattern(name)
-    monkeypatch.setenv("FEC_VR_NO_FAST_TRANSITION", "1")
-    monkeypatch.setenv("FEC_VR_NO_DROP_STRETCH", "1")
+    off = ("FEC_VR_NO_FAST_TRANSITION", "FEC_VR_NO_DROP_STRETCH", "FEC_VR_FB_STOP")
+    for e in off:
+        monkeypatch.setenv(e, "1")
     a = VrPlan(pat, 360000, adaptive_mode_MDS=mds)
-    monkeypatch.delenv("FEC_VR_NO_FAST_TRANSITION")
-    monkeypatch.delenv("FEC_VR_NO_DROP_STRETCH")
+    for e in off:
+        monkeypatch.delenv(e)
     b = VrPlan(pat, 360000, adaptive_mode_MDS=mds)
+    monkeypatch.setenv("FEC_VR_FB_STOP", "1")   # round 5's stretches
+    c = VrPlan(pat, 360000, adaptive_mode_MDS=mds)
     for k in ("encoders", "decoders", "frames", "erased", "fate", "fate_decoder"):
         assert np.array_equal(getattr(a, k), getattr(b, k)), k
+        assert np.array_equal(getattr(a, k), getattr(c, k)), k
     assert (a.lost, a.switches, a.sent, a.coding_rate) == (b.lost, b.switches, b.sent, b.coding_rate)
+    assert (a.lost, a.switches, a.sent, a.coding_rate) == (c.lost, c.switches, c.sent, c.coding_rate)
 
 
 def test_schedule_structure(adaptive):
