@@ -10,7 +10,8 @@ import ctypes
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libfec_amd.so")
+# FEC_AMD_LIB: an A/B build of the same sources (csrc/Makefile OUT=..., e.g. another -D variant)
+LIB_PATH = os.environ.get("FEC_AMD_LIB") or os.path.join(_HERE, "libfec_amd.so")
 HEADER_PATHS = [os.path.join(_HERE, "..", "include", "fec_amd.h")]
 
 FEC_OK = 0
@@ -135,6 +136,7 @@ def lib() -> ctypes.CDLL:
     L.fec_sdswdf_create.argtypes = [i32, i32, i32, i32, i32, i32, ctypes.POINTER(vp)]
     L.fec_sdswdf_destroy.argtypes = [vp]
     L.fec_sdswdf_geometry.argtypes = [vp, ip, ip, ip, ip, ip, ip, ip]
+    L.fec_sdswdf_tile_geometry.argtypes = [i32, i32, i32, i32, i32, i32, i64, ip, ip]
     L.fec_sdswdf_relay_batch.argtypes = [vp, vp, i64, vp, i64, vp, vp]
     L.fec_sdswdf_destination_batch.argtypes = [vp, vp, vp, i64, vp, vp, vp]
     L.fec_sdswdf_relay_plan.argtypes = [vp, vp, i64, vp, vp, i64, i64p, ip]
@@ -155,7 +157,7 @@ def lib() -> ctypes.CDLL:
     L.fec_relay_session_hop1.argtypes = [vp, vp, i64, vp, vp]
     for name in ["fec_relay_session_create", "fec_relay_session_destroy", "fec_relay_session_info",
                  "fec_relay_session_relay_offsets", "fec_relay_session_hop1_headers", "fec_relay_session_dest_meta",
-                 "fec_relay_session_run", "fec_relay_session_hop1", "fec_sdswdf_create", "fec_sdswdf_destroy", "fec_sdswdf_geometry", "fec_sdswdf_relay_batch",
+                 "fec_relay_session_run", "fec_relay_session_hop1", "fec_sdswdf_create", "fec_sdswdf_destroy", "fec_sdswdf_geometry", "fec_sdswdf_tile_geometry", "fec_sdswdf_relay_batch",
                  "fec_sdswdf_destination_batch", "fec_sdswdf_relay_plan", "fec_sdswdf_dest_plan",
                  "fec_sdswdf_relay_batch_starts", "fec_sdswdf_destination_batch_starts", "fec_relay_vr_create",
                  "fec_relay_vr_destroy", "fec_relay_vr_geometry", "fec_relay_vr_run",

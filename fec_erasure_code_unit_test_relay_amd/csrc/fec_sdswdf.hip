@@ -794,6 +794,7 @@ struct SdTileArgs {
 // packets per lane and tile (halo rows staged once per tile).  2 measured slower: relay 268 vs
 // 246 us, destination 129 vs 121 us per 360 000 packets (profiles/r05/relay/r05zp_*).
 constexpr int kSdPass = FEC_SD_PASS;
+constexpr int kSdMaxTile = 64;  // packets per tile the record-id slots hold
 // shift = the row offset of an output row's diagonal: relay row index reads source packet
 // t - (N-1) + (K-1-index) + p; destination row s reads frame t - s - (N2-1-q).
 template <int K, int N, int ROWS, bool RELAY>
@@ -801,12 +802,13 @@ __global__ __launch_bounds__(256) void fec_sd_tile_kernel(SdTileArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     uint8_t* gexp = smem;                                          // 1040: exp[0..509], zeros after
     uint16_t* glog = reinterpret_cast<uint16_t*>(smem + 1040);    // 512: log, log[0] = 512
-    int32_t* srec = reinterpret_cast<int32_t*>(smem + 1552);       // TP record ids (<= 64)
-    uint8_t* raw = smem + 1552 + 256;                             // staged rows, then the output tile
+    int32_t* srec = reinterpret_cast<int32_t*>(smem + 1552);       // TP record ids (TP <= kSdMaxTile)
+    uint8_t* raw = smem + 1552 + 4 * kSdMaxTile;                  // staged rows, then the output tile
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     for (int i = tid; i < 1040; i += 256) gexp[i] = i < 510 ? a.gf[i] : 0;
     for (int i = tid; i < 256; i += 256) glog[i] = i ? a.gf[512 + i] : 512;
     const int S = a.S, NS4 = (S + 3) >> 2, ppw = 64 / NS4, TP = kSdPass * 4 * ppw;
+    if (TP > kSdMaxTile) return;  // never launched so (sd_tile_fit): the record ids would overrun their slots
     const int64_t t0 = static_cast<int64_t>(blockIdx.x) * TP;
     const int nt = static_cast<int>(min<int64_t>(TP, a.P - t0));
     // rows read: relay [t0 - (N-1) - (ROWS-1) + (K-1), t0+nt); destination [t0 - (K-1) - (N-1), t0+nt)
@@ -1092,6 +1094,33 @@ int upload_plan(fec_sdswdf* w, const fec::RecordTable& tab, int64_t P, hipStream
     return FEC_OK;
 }
 
+}  // namespace
+
+namespace fec {
+// Whether the tile kernel (fec_sd_tile_kernel) takes a batch of this geometry, its tile (TP
+// packets) and its dynamic LDS: it needs an instantiation for (k, n1, n2), at most 64 lanes of 4
+// code blocks per packet, at most 64 packets per tile (the kernel's record-id slots: 256 bytes of
+// LDS in front of the staged rows -- a larger tile wrote its ids over the rows and read garbage
+// record ids back, the memory fault behind r05zp's HIP error) and 64 KB of LDS.
+bool sd_tile_fit(bool relay, int k, int n1, int n2, int S, int F, int64_t stride, int* TP_out, int64_t* lds_out) {
+    const int NS4 = (S + 3) / 4;
+    if (!sd_tile_kernel_for(relay, k, n1, n2) || NS4 > 64) return false;
+    const int TP = kSdPass * 4 * (64 / NS4);
+    if (TP > kSdMaxTile) return false;
+    const int N = relay ? n1 : n2, ROWS = relay ? n2 : k;
+    const int back = relay ? (N - 1) + (ROWS - 1) - (k - 1) : (ROWS - 1) + (N - 1);
+    const int OB = relay ? F : S * k;
+    const int64_t stage = 16 + static_cast<int64_t>(TP + back) * stride + 16, otile = 16 + static_cast<int64_t>(TP) * OB + 16;
+    const int64_t lds = 1552 + 4 * kSdMaxTile + ((std::max(stage, otile) + 15) & ~int64_t(15));
+    if (lds > 65536) return false;
+    if (TP_out) *TP_out = TP;
+    if (lds_out) *lds_out = lds;
+    return true;
+}
+}  // namespace fec
+
+namespace {
+
 // The tile kernels (fec_sd_tile_kernel): the records' entry blocks up, then one launch; returns
 // 1 when the tile kernel does not apply (the caller launches the per-(packet, block) kernel).
 int launch_tile(fec_sdswdf* w, bool relay, const fec::RecordTable& tab, const uint8_t* d_in, int64_t stride,
@@ -1100,15 +1129,10 @@ int launch_tile(fec_sdswdf* w, bool relay, const fec::RecordTable& tab, const ui
     if (e && e[0] == '0') return 1;
     const int k = w->g1.k, n1 = w->g1.n, n2 = w->g2.n, S = w->g1.S;
     const void* kern = fec::sd_tile_kernel_for(relay, k, n1, n2);
-    const int NS4 = (S + 3) / 4;
-    if (!kern || NS4 > 64) return 1;
-    const int TP = fec::kSdPass * 4 * (64 / NS4);
+    int TP = 0;
+    int64_t lds = 0;
+    if (!fec::sd_tile_fit(relay, k, n1, n2, S, w->F, stride, &TP, &lds)) return 1;
     const int N = relay ? n1 : n2, ROWS = relay ? n2 : k;
-    const int back = relay ? (N - 1) + (ROWS - 1) - (k - 1) : (ROWS - 1) + (N - 1);
-    const int OB = relay ? w->F : S * k;
-    const int64_t stage = 16 + static_cast<int64_t>(TP + back) * stride + 16, otile = 16 + static_cast<int64_t>(TP) * OB + 16;
-    const int64_t lds = 1552 + 256 + ((std::max(stage, otile) + 15) & ~int64_t(15));
-    if (lds > 65536) return 1;
     const int R = relay ? fec::kHdr + n2 * n1 : k * n2;
     fec::build_entries(tab.data(), R, relay ? fec::kHdr : 0, ROWS, N, w->eoff, w->ent);
     if (int st = w->d_eoff.reserve(w->eoff.size() * 4)) return st;
@@ -1504,6 +1528,20 @@ int fec_sdswdf_create(int max_payload, int T1, int N1, int T2, int N2, int sdbo,
 int fec_sdswdf_destroy(fec_sdswdf* w) {
     delete w;
     return FEC_OK;
+}
+
+int fec_sdswdf_tile_geometry(int relay, int max_payload, int T1, int N1, int T2, int N2, int64_t stride,
+                             int* tile_packets, int* lds_bytes) {
+    if (max_payload < 0 || T1 < 0 || N1 < 0 || N1 > T1 || T2 < 1 || N2 < 0 || T1 - N1 != T2 - N2) return FEC_ERR_ARG;
+    const int k = T1 - N1 + 1, n1 = T1 + 1, n2 = T2 + 1, S = (max_payload + 2 + k - 1) / k;
+    const int F = 2 + fec::kHdr + (S + 1) * n2;
+    if (stride <= 0) stride = relay ? static_cast<int64_t>(S) * n1 : F;
+    int TP = 0;
+    int64_t lds = 0;
+    const bool fit = fec::sd_tile_fit(relay != 0, k, n1, n2, S, F, stride, &TP, &lds);
+    if (tile_packets) *tile_packets = fit ? TP : 0;
+    if (lds_bytes) *lds_bytes = fit ? static_cast<int>(lds) : 0;
+    return fit ? 1 : 0;
 }
 
 int fec_sdswdf_geometry(const fec_sdswdf* w, int* k, int* n1, int* n2, int* S, int* blocks, int* frame_bytes,

@@ -30,7 +30,13 @@
 #ifdef FEC_VR_PROFILE
 #include <x86intrin.h>
 #include <map>
-#define FEC_VR_PROF_DECL uint64_t prof_c[6] = {}, prof_t = __rdtsc(); int64_t prof_cls[64] = {}; std::map<int, int64_t> prof_why_h;
+#define FEC_VR_PROF_DECL uint64_t prof_c[8] = {}, prof_t = __rdtsc(); int64_t prof_cls[64] = {}; std::map<int, int64_t> prof_why_h;
+#define FEC_VR_SUB(k, stmt)                            \
+    {                                                  \
+        const uint64_t s_ = __rdtsc();                 \
+        stmt;                                          \
+        prof_c[k] += __rdtsc() - s_;                   \
+    }
 #define FEC_VR_PROF(k)                 \
     {                                  \
         const uint64_t t_ = __rdtsc(); \
@@ -42,11 +48,13 @@
                          "decoder %.3f top %.3f\n",                                                        \
                  prof_c[0] * 1e-6, prof_c[1] * 1e-6, prof_c[2] * 1e-6, prof_c[3] * 1e-6, prof_c[4] * 1e-6, \
                  prof_c[5] * 1e-6);                                                                    \
+    std::fprintf(stderr, "vr control Mcycles inside decoder: done_with %.3f new_decoder %.3f\n", prof_c[6] * 1e-6, prof_c[7] * 1e-6); \
     for (int c_ = 0; c_ < 64; ++c_)                                                                        \
         if (prof_cls[c_]) std::fprintf(stderr, "vr iteration class %2d: %lld\n", c_, (long long)prof_cls[c_]); \
     for (auto& w_ : prof_why_h) std::fprintf(stderr, "vr class-0 why %#x: %lld\n", w_.first, (long long)w_.second);
 #else
 #define FEC_VR_PROF_DECL
+#define FEC_VR_SUB(k, stmt) stmt;
 #define FEC_VR_PROF(k)
 #define FEC_VR_PROF_PRINT
 #endif
@@ -685,6 +693,7 @@ void VrPlan::control(const uint8_t* pattern, int64_t n_pattern, int T, int B, in
     }
     qcv_.notify_all();
     size_t dri = 0;       // next drop
+    FEC_VR_PROF_DECL
     uint8_t udp[12] = {};
     // ---- Variable_Rate_FEC_Decoder (Variable_Rate_FEC_Decoder.cpp:25-80, 2133-2400, 2440-2514) ----
     int64_t seq_start = -1, latest_seq = -1, sdc = -1, sde = -1;
@@ -755,12 +764,12 @@ void VrPlan::control(const uint8_t* pattern, int64_t n_pattern, int T, int B, in
     };
     auto report = [&](int id, int64_t seq) { report_range(id, seq, seq + 1); };
     auto update_decoder = [&](int T_, int B_, int N_, int64_t first) {  // (:2520-2536)
-        if (dold >= 0) done_with(dold);
+        if (dold >= 0) FEC_VR_SUB(6, done_with(dold))
         dold = dcur;
         dT = T_;
         dB = B_;
         dN = N_;
-        dcur = new_decoder(T_, B_, N_, first);
+        FEC_VR_SUB(7, dcur = new_decoder(T_, B_, N_, first))
         dec[dold].role_switch = first;
     };
     // frames as runs: equal frames, or a transition's frames whose counter grows by one per packet
@@ -793,7 +802,6 @@ void VrPlan::control(const uint8_t* pattern, int64_t n_pattern, int T, int B, in
     clock_gettime(CLOCK_THREAD_CPUTIME_ID, &cpu0);
     rusage ru0{};
     getrusage(RUSAGE_THREAD, &ru0);
-    FEC_VR_PROF_DECL
     for (int64_t seq = 0;; ++seq) {
         ++n_iter;
         FEC_VR_PROF(5)
@@ -969,6 +977,7 @@ void VrPlan::control(const uint8_t* pattern, int64_t n_pattern, int T, int B, in
                 udp[5] = static_cast<uint8_t>(eN);
                 // packet `end` from the top: a steady stretch may start at it (the transition's end)
                 seq = end - 1;
+                FEC_VR_PROF(1)
                 continue;
             }
         }

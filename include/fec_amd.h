@@ -353,6 +353,11 @@ int fec_swdf_destination_batch(fec_swdf *swdf, const uint8_t *d_frames, const ui
 typedef struct fec_sdswdf fec_sdswdf;
 int fec_sdswdf_create(int max_payload, int T1, int N1, int T2, int N2, int sdbo, fec_sdswdf **out);
 int fec_sdswdf_destroy(fec_sdswdf *w);
+/* Host-only (no device call): whether a type-3 batch of this geometry runs on the tile kernel
+ * (1) or the per-(packet, block) kernel (0), the tile's packets and its dynamic LDS bytes; stride <=
+ * 0 = the default row pitch (relay: S*n1, destination: the frame bytes). */
+int fec_sdswdf_tile_geometry(int relay, int max_payload, int T1, int N1, int T2, int N2, int64_t stride,
+                             int *tile_packets, int *lds_bytes);
 int fec_sdswdf_geometry(const fec_sdswdf *w, int *k, int *n1, int *n2, int *S, int *blocks,
                         int *frame_bytes, int *delay);
 int fec_sdswdf_relay_batch(fec_sdswdf *w, const uint8_t *d_cw, int64_t cw_stride, const uint8_t *h_erasure,

@@ -237,6 +237,27 @@ def test_sdswdf_rejects_unsupported_configurations():
             StateDependentRelay(L, *cfg)
 
 
+def test_sd_tile_kernel_fallback_geometry():
+    """CPU (host geometry only): which type-3 batches take the tile kernel.  A tile holds at most 64
+    packets (the kernel's record-id slots in LDS); round 5's two-packets-per-lane build
+    (FEC_SD_PASS=2) made k = 11 tiles of 72 packets at L = 300 that overran them, so a garbage
+    record id faulted the GPU -- the HIP error of r05zp, reproduced with that build in r06g
+    (DESIGN §5).  The fallback is chosen for any tile over 64 packets, e.g. k = 11 at a 40-byte
+    payload (S = 4: one lane per packet, 256 packets per tile)."""
+    import ctypes
+    from fec_erasure_code_unit_test_relay_amd._lib import lib
+    tp, lds = ctypes.c_int(), ctypes.c_int()
+    for relay in (1, 0):
+        for N in range(0, 8):  # config 4's codes at L = 300: (10, N) -> (10, N), k = 11 - N
+            assert lib().fec_sdswdf_tile_geometry(relay, L, 10, N, 10, N, 0, ctypes.byref(tp), ctypes.byref(lds)) == 1
+            assert 0 < tp.value <= 64 and lds.value <= 65536, (relay, N, tp.value, lds.value)
+        assert lib().fec_sdswdf_tile_geometry(relay, 40, 10, 0, 10, 0, 0, ctypes.byref(tp), ctypes.byref(lds)) == 0
+        assert tp.value == 0
+        # no tile kernel instantiated for (k, n1, n2) = (1, 11, 11): the per-(packet, block) kernel
+        assert lib().fec_sdswdf_tile_geometry(relay, L, 10, 10, 10, 10, 0, ctypes.byref(tp), ctypes.byref(lds)) == 0
+    assert lib().fec_sdswdf_tile_geometry(1, L, 10, 3, 9, 3, 0, ctypes.byref(tp), ctypes.byref(lds)) < 0
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("pi", range(len(PATTERNS)))
 @pytest.mark.parametrize("cfg", SD_CASES)
