@@ -555,11 +555,12 @@ constexpr int cmax(int x, int y) { return x > y ? x : y; }
 
 // The whole geometry at compile time (k, n1, n2 and the payload size L): every division,
 // bound and LDS offset below is a constant.
-template <int K_, int N1_, int N2_, int L_, bool RELAY_, int TR_ = kFR, bool V2_ = false>
+template <int K_, int N1_, int N2_, int L_, bool RELAY_, int TR_ = kFR, bool V2_ = false, int NT_ = kFT>
 struct FastGeo {
     static constexpr int K = K_, N1 = N1_, N2 = N2_, L = L_;
     static constexpr bool RELAY = RELAY_;
     static constexpr int TR = TR_;                        // packets per tile
+    static constexpr int NT = NT_, NW = NT_ / 64;         // threads, waves per workgroup
     static constexpr bool V2 = RELAY_ && V2_;             // relay: the row-scatter kernel (no CT / parity tiles)
     static constexpr bool CT3 = RELAY && !V2;             // relay: the three-tile (CT, parity, words) kernel
     static constexpr int S = (L + 2 + K - 1) / K;        // code blocks (= sub-streams)
@@ -575,12 +576,12 @@ struct FastGeo {
     static constexpr int F4 = (F + 3) & ~3;              // LDS frame pitch
     static constexpr int ES = (K * (1 + N) + 3) & ~3;    // rule entry bytes (fec_host.h DecodeRules)
     static constexpr int CTROW = K * S4;
-    static constexpr int QCH = (16 + ROWS * STRIDE + 16 * kFT - 1) / (16 * kFT);  // slab chunks per thread
-    static constexpr int SCH = (TR * OUT_ROW + 16 * kFT - 1) / (16 * kFT);      // output chunks per thread
+    static constexpr int QCH = (16 + ROWS * STRIDE + 16 * NT - 1) / (16 * NT);  // slab chunks per thread
+    static constexpr int SCH = (TR * OUT_ROW + 16 * NT - 1) / (16 * NT);      // output chunks per thread
     static constexpr int OFF_PMASK = 1552;
     static constexpr int OFF_RULE = OFF_PMASK + 4 * (TR + 64);
     static constexpr int RULE_U16 = K + K * N + 4;      // per wave
-    static constexpr int OFF_TB = al16(OFF_RULE + kFW * 2 * RULE_U16);
+    static constexpr int OFF_TB = al16(OFF_RULE + NW * 2 * RULE_U16);
     static constexpr int OFF_CT = al16(OFF_TB + (CT3 ? (N2 - K) * K * 20 : 0));
     static constexpr int OFF_OW = al16(OFF_CT + (CT3 ? ROWS * CTROW : 0));
     static constexpr int OFF_RAW = al16(OFF_OW + (CT3 ? (N2 - K) * TR * S4 : 0));
@@ -596,8 +597,8 @@ struct FastGeo {
     // at a chunk boundary: t0 * STRIDE is a multiple of 16) are carried over in registers
     static constexpr int DLT = (16 - (H * STRIDE) % 16) % 16;
     static constexpr int NH = (DLT + H * STRIDE) / 16;
-    static constexpr int HQ = (NH + kFT - 1) / kFT;
-    static_assert(H <= 64 && D0 + TR <= TR + 64 && D0 + TR <= kFT, "rows in front of a tile");
+    static constexpr int HQ = (NH + NT - 1) / NT;
+    static_assert(H <= 64 && D0 + TR <= TR + 64 && D0 + TR <= NT, "rows in front of a tile");
     static_assert(TR % 16 == 0 && TR <= 64, "tile rows: t0 * STRIDE and t0 * F multiples of 16");
     static_assert((DLT + H * STRIDE) % 16 == 0, "carried rows");
 };
@@ -669,7 +670,7 @@ struct FastTile {
     uint32_t f0 = 0, f1 = 0;        // flags of local rows lane and 64 + lane (next tile)
     uint64_t fb0 = 0, fb1 = 0;      // flags of local rows 0..63, 64..127 (this tile)
     int dlt = 0, dlt_next = 0;      // LDS byte of local row 0 = raw + dlt
-    uint32_t dec = 0;               // this wave's decoded packets (bit i: d = wave + kFW*i)
+    uint32_t dec = 0;               // this wave's decoded packets (bit i: d = wave + GM::NW*i)
     uint32_t pre[2][2];
 
     __device__ FastTile(uint8_t* s, const SwFastArgs& args) : smem(s), a(args) {
@@ -680,8 +681,8 @@ struct FastTile {
         glog16 = reinterpret_cast<uint16_t*>(smem + 1040);
         pmask = reinterpret_cast<uint32_t*>(smem + GM::OFF_PMASK);
         rl = reinterpret_cast<uint16_t*>(smem + GM::OFF_RULE) + wave * GM::RULE_U16;
-        for (int i = tid; i < 1040; i += kFT) gexp[i] = i < 510 ? a.gf[i] : 0;
-        for (int i = tid; i < 256; i += kFT) glog16[i] = i ? a.gf[512 + i] : 512;
+        for (int i = tid; i < 1040; i += GM::NT) gexp[i] = i < 510 ? a.gf[i] : 0;
+        for (int i = tid; i < 256; i += GM::NT) glog16[i] = i ? a.gf[512 + i] : 512;
     }
     // the slab of rows [r0, t0+nt) (r0 = t0 - H) and the tile's flags, into registers; with cont
     // (the tile follows this workgroup's previous one) its first NH chunks come from keep() instead
@@ -698,7 +699,7 @@ struct FastTile {
             const_cast<uint8_t*>(a.in + base), 0, static_cast<int>(span < fec::kRsrcMax ? span : fec::kRsrcMax), 0x00020000);
 #pragma unroll
         for (int q = 0; q < QCH; ++q) {
-            const int c = tid + q * kFT;
+            const int c = tid + q * GM::NT;
             const int64_t o = A - base + 16 * static_cast<int64_t>(c);  // < 0: a row before packet 0
             const uint32_t off = (c < nch && o >= 0 && !(cont && c < NH)) ? static_cast<uint32_t>(o) : 0x7ffffff0u;
             const auto x = __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0);
@@ -717,7 +718,7 @@ struct FastTile {
     __device__ void keep() {
 #pragma unroll
         for (int q = 0; q < HQ; ++q) {
-            const int c = tid + q * kFT;
+            const int c = tid + q * GM::NT;
             if (c < NH) hc[q] = *reinterpret_cast<const uint4*>(smem + GM::OFF_RAW + GM::TR * STRIDE + 16 * c);
         }
     }
@@ -732,7 +733,7 @@ struct FastTile {
         const bool any = (fb0 | fb1) != 0;
 #pragma unroll
         for (int q = 0; q < QCH; ++q) {
-            const int c = tid + q * kFT;
+            const int c = tid + q * GM::NT;
             if (16 * c >= 16 + ROWS * STRIDE) continue;
             uint4 x = v[q];
             if (q < HQ && carry && c < NH) x = hc[q < HQ ? q : 0];  // (masking them again is harmless)
@@ -760,11 +761,11 @@ struct FastTile {
             *reinterpret_cast<uint4*>(smem + GM::OFF_RAW + 16 * c) = x;
         }
     }
-    // masks of this wave's packets (d = wave + kFW*lane), flags out, the first two rules of this
+    // masks of this wave's packets (d = wave + GM::NW*lane), flags out, the first two rules of this
     // wave into registers
     __device__ void masks(int64_t t0, int nt) {
         const int nd = D0 + nt;
-        const int d = wave + kFW * lane;
+        const int d = wave + GM::NW * lane;
         uint32_t m = 0;
         if (d < nd) {
             const int lo = H - D0 + d - N + 1;
@@ -797,7 +798,7 @@ struct FastTile {
         for (int jj = 0; dd; ++jj) {
             const int i = __builtin_ctz(dd);
             dd &= dd - 1;
-            const int d = wave + kFW * i;
+            const int d = wave + GM::NW * i;
             const uint32_t mask = pmask[d];
             const int lb = H - D0 + d - N + 1;  // local row of diagonal position 0
             uint32_t w0, w1;
@@ -1096,7 +1097,7 @@ __global__ __launch_bounds__(kFT, 4) void fec_sw_fast_relay_kernel(SwFastArgs a)
 // tile, laid out in LDS at their own stride F (one base address, every byte at a compile-time
 // offset); the frames then go out as 16-byte chunks.  Three barriers per tile.
 template <class GM>
-__global__ __launch_bounds__(kFT, GM::WPE) void fec_sw_fast_relay2_kernel(SwFastArgs a) {
+__global__ __launch_bounds__(GM::NT, GM::WPE) void fec_sw_fast_relay2_kernel(SwFastArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     constexpr int K = GM::K, N1 = GM::N1, N2 = GM::N2, S = GM::S, G = GM::G, F = GM::F, TR = GM::TR;
     constexpr int size = (S + 1) * N2;
@@ -1179,7 +1180,7 @@ __global__ __launch_bounds__(kFT, GM::WPE) void fec_sw_fast_relay2_kernel(SwFast
             const int nback = nt + N2 - 1 - back0;
             const int n_int = nint * GF;
             const int n_all = n_int + (N2 - 1 + nback) * G + nint * GP;
-            for (int it = T.tid; it < n_all; it += kFT) {
+            for (int it = T.tid; it < n_all; it += GM::NT) {
                 if (it < n_int) {
                     const int r = N2 - 1 + it / GF, g = it - (it / GF) * GF;
                     scatter(r, g, std::false_type{});
@@ -1200,7 +1201,7 @@ __global__ __launch_bounds__(kFT, GM::WPE) void fec_sw_fast_relay2_kernel(SwFast
             }
         }
         // each frame's 4 header bytes (BE16 size, two zeros) and its zero tail
-        for (int it = T.tid; it < nt * (4 + TAIL); it += kFT) {
+        for (int it = T.tid; it < nt * (4 + TAIL); it += GM::NT) {
             const int t = it / (4 + TAIL), b = it - t * (4 + TAIL);
             const uint8_t v = b == 0 ? uint8_t(size >> 8) : b == 1 ? uint8_t(size & 255) : uint8_t(0);
             smem[GM::OFF_FR + t * F + (b < 4 ? b : S * N2 + b)] = v;
@@ -1213,7 +1214,7 @@ __global__ __launch_bounds__(kFT, GM::WPE) void fec_sw_fast_relay2_kernel(SwFast
         const __amdgpu_buffer_rsrc_t ro = __builtin_amdgcn_make_buffer_rsrc(gout, 0, obytes & ~15, 0x00020000);
 #pragma unroll
         for (int qq = 0; qq < GM::SCH; ++qq) {
-            const int c = T.tid + qq * kFT;
+            const int c = T.tid + qq * GM::NT;
             const uint32_t b = 16 * c;
             if (static_cast<int>(b) >= obytes) break;
             const uint4 v = *reinterpret_cast<const uint4*>(smem + GM::OFF_FR + b);
@@ -1342,7 +1343,7 @@ constexpr int kFastN = 11, kFastL = 300;
 
 template <class GM>
 bool launch_fast_geo(fec::SwFastArgs a, hipStream_t s, hipError_t* err) {
-    using fec::kFT;
+    constexpr int kFT = GM::NT;
     constexpr int kFR = GM::TR;
     auto kern = [] {
         if constexpr (GM::V2) return fec::fec_sw_fast_relay2_kernel<GM>;
@@ -1395,8 +1396,9 @@ bool launch_fast_geo(fec::SwFastArgs a, hipStream_t s, hipError_t* err) {
     return true;
 }
 
-// The relay's kernel: the row scatter (default) with tiles of FEC_SWDF_TR = 64 / 48 / 32 packets,
-// or FEC_SWDF_RELAY=3 the three-tile kernel of round 5 (kept for A/B).
+// The relay's kernel: the row scatter (default) with tiles of FEC_SWDF_TR = 64 / 48 packets
+// (512 threads) or 32 packets (256 threads, four workgroups per CU), or FEC_SWDF_RELAY=3 the
+// three-tile kernel of round 5 (kept for A/B).
 int relay_variant() {
     static const int v = [] {
         const char* r = std::getenv("FEC_SWDF_RELAY");
@@ -1421,7 +1423,7 @@ bool launch_fast(int K, fec::SwFastArgs a, int L, int n1, int n2, int blocks, in
         if constexpr (RELAY) {                                                      \
             if (rv == 64) return launch_fast_geo<fec::FastGeo<KK, kFastN, kFastN, kFastL, true, 64, true>>(a, s, err); \
             if (rv == 48) return launch_fast_geo<fec::FastGeo<KK, kFastN, kFastN, kFastL, true, 48, true>>(a, s, err); \
-            if (rv == 32) return launch_fast_geo<fec::FastGeo<KK, kFastN, kFastN, kFastL, true, 32, true>>(a, s, err); \
+            if (rv == 32) return launch_fast_geo<fec::FastGeo<KK, kFastN, kFastN, kFastL, true, 32, true, 256>>(a, s, err); \
         }                                                                           \
         return launch_fast_geo<GM>(a, s, err);                                      \
     }

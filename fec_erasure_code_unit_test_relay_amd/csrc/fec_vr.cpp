@@ -298,52 +298,78 @@ void VrPlan::start_workers() {
         std::lock_guard<std::mutex> lk(qmu_);
         q_.clear();
         qclosed_ = false;
+        qclosed_flag_.store(false, std::memory_order_relaxed);
         qsize_.store(0, std::memory_order_relaxed);
         sleepers_.store(0, std::memory_order_relaxed);
     }
     batch_.clear();
+    // decoder-job slots for every instance this run can make (one per switch at most), allocated
+    // by the control loop as it fills them; the chunk pointers never move while workers read them
+    const size_t nchunks = static_cast<size_t>((P + 64 + kJobChunk) / kJobChunk) + 1;
+    if (djobs_.size() < nchunks) djobs_.resize(nchunks);
+    dpub_.store(0, std::memory_order_relaxed);
+    dtake_.store(0, std::memory_order_relaxed);
+    dfill_ = 0;
     recs_.resize(nth);
     for (auto& r : recs_) r.clear();
     pending_ = true;
-    // pause-loop iterations a worker polls the queue before sleeping (FEC_VR_SPIN; 0: sleep at once)
+    // pause-loop iterations a worker polls for work before sleeping (FEC_VR_SPIN; 0: sleep at once)
     int spin_max = 4096;
     if (const char* e = std::getenv("FEC_VR_SPIN")) spin_max = std::max(0, std::atoi(e));
     for (size_t w = 0; w < nth; ++w) {
         workers_.emplace_back([this, w, spin_max, home = t_pin_home] {
             vr_pin_near(home);
+            auto decoder_ready = [&] { return dtake_.load(std::memory_order_relaxed) < dpub_.load(std::memory_order_acquire); };
             for (;;) {
-                DecJob j;
-                // poll the queue for a while (a job comes every ~0.5 us while the control loop
-                // runs), then sleep on the condition variable
-                for (int spin = 0; spin < spin_max && qsize_.load(std::memory_order_acquire) == 0; ++spin)
-                    __builtin_ia32_pause();
-                {
-                    std::unique_lock<std::mutex> lk(qmu_);
-                    if (q_.empty() && !qclosed_) {
-                        sleepers_.fetch_add(1, std::memory_order_relaxed);
-                        qcv_.wait(lk, [&] { return !q_.empty() || qclosed_; });
-                        sleepers_.fetch_sub(1, std::memory_order_relaxed);
+                // the mutex queue first: feedback runs (queued before any decoder job) and the rate sum
+                if (qsize_.load(std::memory_order_acquire) > 0) {
+                    DecJob j;
+                    bool got = false;
+                    {
+                        std::lock_guard<std::mutex> lk(qmu_);
+                        if (!q_.empty()) {
+                            j = std::move(q_.front());
+                            q_.pop_front();
+                            qsize_.store(static_cast<int64_t>(q_.size()), std::memory_order_release);
+                            got = true;
+                        }
                     }
-                    if (q_.empty()) {
-                        qsize_.store(-1, std::memory_order_release);  // closed: every worker leaves
-                        break;
+                    if (got) {
+                        if (j.id <= -2) {  // feedback jobs of run -2 - id, in order
+                            const int64_t c = -2 - static_cast<int64_t>(j.id), nj = static_cast<int64_t>(fb_jobs_.size());
+                            const int64_t ch = static_cast<int64_t>(fb_chunk_);
+                            for (int64_t jf = c * ch; jf < std::min(nj, (c + 1) * ch); ++jf) feedback_job(jf, fb_T_, fb_mds_);
+                        } else {  // final_sum_coding_rate, one float add per packet in sending order
+                            float sum = 0;
+                            for (const RateRun& r : rate_runs) sum = float_add_repeated(sum, r.rate, r.count);
+                            sum_coding_rate = sum;
+                        }
+                        continue;
                     }
-                    j = std::move(q_.front());
-                    q_.pop_front();
-                    qsize_.store(q_.empty() && qclosed_ ? -1 : static_cast<int64_t>(q_.size()),
-                                 std::memory_order_release);
                 }
-                if (j.id <= -2) {  // feedback jobs of run -2 - id, in order
-                    const int64_t c = -2 - static_cast<int64_t>(j.id), nj = static_cast<int64_t>(fb_jobs_.size());
-                    const int64_t ch = static_cast<int64_t>(fb_chunk_);
-                    for (int64_t jf = c * ch; jf < std::min(nj, (c + 1) * ch); ++jf) feedback_job(jf, fb_T_, fb_mds_);
-                } else if (j.id < 0) {  // final_sum_coding_rate, one float add per packet in sending order
-                    float s = 0;
-                    for (const RateRun& r : rate_runs) s = float_add_repeated(s, r.rate, r.count);
-                    sum_coding_rate = s;
-                } else {
-                    decode_instance(j, recs_[w]);
+                // a decoder instance, claimed lock-free
+                int64_t t = dtake_.load(std::memory_order_relaxed);
+                if (t < dpub_.load(std::memory_order_acquire)) {
+                    if (dtake_.compare_exchange_weak(t, t + 1, std::memory_order_acq_rel, std::memory_order_relaxed))
+                        decode_instance(dslot(t), recs_[w]);
+                    continue;
                 }
+                // nothing: poll for a while (a job comes every ~0.5 us while the control loop runs),
+                // then sleep on the condition variable
+                bool any = false;
+                for (int spin = 0; spin < spin_max && !any; ++spin) {
+                    any = qsize_.load(std::memory_order_acquire) > 0 || decoder_ready() ||
+                          qclosed_flag_.load(std::memory_order_acquire);
+                    if (!any) __builtin_ia32_pause();
+                }
+                std::unique_lock<std::mutex> lk(qmu_);
+                auto ready = [&] { return !q_.empty() || qclosed_ || decoder_ready(); };
+                if (!ready()) {
+                    sleepers_.fetch_add(1, std::memory_order_seq_cst);
+                    qcv_.wait(lk, ready);
+                    sleepers_.fetch_sub(1, std::memory_order_relaxed);
+                }
+                if (q_.empty() && qclosed_ && !decoder_ready()) break;  // closed: every job published is taken
             }
         });
     }
@@ -365,11 +391,34 @@ void VrPlan::publish(DecJob&& j, bool flush) {
     if (wake) qcv_.notify_all();
 }
 
+void VrPlan::publish_decoder(int id, const VrInstance& d, const DecodeRules* rules, std::vector<Reports>& reps,
+                             bool flush) {
+    if (id >= 0) {
+        const int64_t n = dfill_++;
+        auto& chunk = djobs_[static_cast<size_t>(n / kJobChunk)];
+        if (!chunk) chunk.reset(new DecJob[kJobChunk]);
+        DecJob& j = chunk[n % kJobChunk];
+        j.id = id;
+        j.d = d;
+        j.rules = rules;
+        j.reps.swap(reps);  // (the slot's old list goes back to the finished instance, unused)
+    }
+    // release the filled slots four at a time (each store takes the line the polling workers
+    // share); a worker about to sleep either sees them or is counted in sleepers_ (both
+    // sequentially consistent), and is then woken
+    if (dfill_ == dpub_.load(std::memory_order_relaxed) || (!flush && dfill_ % 4 != 0)) return;
+    dpub_.store(dfill_, std::memory_order_seq_cst);
+    if (sleepers_.load(std::memory_order_seq_cst) > 0) {
+        { std::lock_guard<std::mutex> lk(qmu_); }
+        qcv_.notify_all();
+    }
+}
+
 void VrPlan::close_jobs() {
     {
         std::lock_guard<std::mutex> lk(qmu_);
         qclosed_ = true;
-        qsize_.store(-1, std::memory_order_release);  // pollers stop polling and take the lock
+        qclosed_flag_.store(true, std::memory_order_release);  // pollers stop polling and take the lock
     }
     qcv_.notify_all();
 }
@@ -715,12 +764,7 @@ void VrPlan::control(const uint8_t* pattern, int64_t n_pattern, int T, int B, in
     };
     // an instance the control loop is done with (neither the current nor the old decoder)
     auto done_with = [&](int id) {
-        DecJob j;
-        j.id = id;
-        j.d = dec[static_cast<size_t>(id)];
-        j.rules = drules[static_cast<size_t>(id)];
-        j.reps.swap(reps[static_cast<size_t>(id)]);
-        publish(std::move(j));
+        publish_decoder(id, dec[static_cast<size_t>(id)], drules[static_cast<size_t>(id)], reps[static_cast<size_t>(id)]);
     };
     auto call = [&](int id, int64_t seq) {
         if (seq != dec[id].end) throw std::logic_error("vr: decoder calls out of order");
@@ -738,11 +782,15 @@ void VrPlan::control(const uint8_t* pattern, int64_t n_pattern, int T, int B, in
     const bool drop_stretch = !std::getenv("FEC_VR_NO_DROP_STRETCH");
     // FEC_VR_FB_STOP (A/B): steady stretches end before the feedback change's packet (round 5)
     const bool fb_through = !std::getenv("FEC_VR_FB_STOP");
-    // one past the last received packet in [lo, hi), or lo if every one of them drops
+    // one past the last received packet in [lo, hi), or lo if every one of them drops.  The drop
+    // cursor dri is at lo (drops[dri] is the first drop >= lo): the drops in [lo, hi) are scanned
+    // from it (a stretch holds a few at most; a binary search over all of them per call was ~200
+    // cycles of the control loop's transitions)
     auto received_end = [&](int64_t lo, int64_t hi) {
-        auto j = std::lower_bound(drops.begin(), drops.end(), hi);
+        size_t j = dri;
+        while (j < drops.size() && drops[j] < hi) ++j;
         int64_t e = hi;
-        while (e > lo && j != drops.begin() && *(j - 1) == e - 1) {
+        while (e > lo && j > dri && drops[j - 1] == e - 1) {
             --j;
             --e;
         }
@@ -1139,6 +1187,8 @@ void VrPlan::control(const uint8_t* pattern, int64_t n_pattern, int T, int B, in
     // the last two decoder instances, then the coding-rate sum; no more jobs
     if (dold >= 0) done_with(dold);
     if (dcur >= 0) done_with(dcur);
+    std::vector<Reports> none;
+    publish_decoder(-1, VrInstance{}, nullptr, none, true);  // the slots not yet released
     DecJob rate;
     rate.id = -1;
     publish(std::move(rate), true);

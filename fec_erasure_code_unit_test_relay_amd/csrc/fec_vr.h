@@ -186,6 +186,16 @@ private:
     size_t fb_chunk_ = 1;  // feedback jobs per worker-pool run
     void start_workers();
     void publish(DecJob&& j, bool flush = false);
+    // Decoder-instance jobs go to the workers without a lock: the control loop fills slot dpub_ of
+    // a chunked array (slots never move) and releases it; a worker claims slot dtake_ by
+    // compare-and-swap.  The mutex queue keeps the few other jobs (feedback runs, the rate sum).
+    static constexpr int64_t kJobChunk = 256;
+    std::vector<std::unique_ptr<DecJob[]>> djobs_;
+    std::atomic<int64_t> dpub_{0}, dtake_{0};
+    int64_t dfill_ = 0;  // slots filled by the control loop (released up to dpub_)
+    DecJob& dslot(int64_t i) { return djobs_[static_cast<size_t>(i / kJobChunk)][i % kJobChunk]; }
+    void publish_decoder(int id, const VrInstance& d, const DecodeRules* rules, std::vector<Reports>& reps,
+                         bool flush = false);
     void close_jobs();
     void decode_instance(const DecJob& job, std::vector<RecEntry>& recs);
     std::map<int, std::shared_ptr<const DecodeRules>> rules_;  // key T*1024 + B*32 + N
@@ -199,7 +209,8 @@ private:
     bool qclosed_ = false;
     // Workers poll these before sleeping on qcv_, and the control loop wakes the queue only when a
     // worker sleeps: a futex wake per published batch cost the control loop ~0.7 ms of system time
-    std::atomic<int64_t> qsize_{0};  // q_.size() (written under qmu_) or -1 once closed and empty
+    std::atomic<int64_t> qsize_{0};  // q_.size() (written under qmu_)
+    std::atomic<bool> qclosed_flag_{false};  // qclosed_, for the pollers
     std::atomic<int> sleepers_{0};   // workers waiting on qcv_ (changed under qmu_)
     std::chrono::steady_clock::time_point t_dec_;
     bool pending_ = false;
