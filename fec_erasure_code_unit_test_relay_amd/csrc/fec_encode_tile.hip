@@ -690,8 +690,12 @@ const void* fec_encode_tile_kernel_for(int k, int np, int L) {
 // Several tuples' segment walks in one launch (EncMultiArgs).  The register budget is that of 4
 // workgroups per CU (128 VGPRs), which every listed tuple's walk fits; LDS is the largest listed
 // tuple's (the launcher sizes it).
+// (the second line: the hop-1 tuples of the two-hop relay session, whose sender splits T_TOT --
+// T = T_TOT - N2 -- so T < 10 codes with B = N appear: (9,0,0), (9,1,1), (5,0,0), (8,0,0), (9,2,2),
+// (8,1,1), (4,0,0) are 48 % of its packets on bin/erasure.bin)
 #define FEC_ENC_TILE_MULTI_LIST(X) \
-    X(8, 3) X(11, 0) X(10, 1) X(9, 2) X(7, 4) X(6, 5) X(5, 6) X(4, 7) X(10, 3) X(9, 3) X(8, 4) X(7, 5)
+    X(8, 3) X(11, 0) X(10, 1) X(9, 2) X(7, 4) X(6, 5) X(5, 6) X(4, 7) X(10, 3) X(9, 3) X(8, 4) X(7, 5) \
+    X(10, 0) X(9, 1) X(6, 0) X(9, 0) X(8, 2) X(8, 1) X(5, 0)
 
 template <int K, int NP>
 __device__ __forceinline__ void tile_multi_case(const EncMultiArgs& m, int ti, uint8_t* smem) {

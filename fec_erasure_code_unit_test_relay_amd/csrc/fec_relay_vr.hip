@@ -42,6 +42,7 @@ constexpr int kMaxCodes = 16;
 struct RvTupleDev {             // one code's batch buffers, for the gather kernel
     const uint8_t* frames;      // rows of F bytes
     const uint8_t* out;         // rows of ostride bytes
+    const uint8_t* flag;        // per row: the destination's loss flag (type 2; null for type 3)
     int F, part, hdr;           // frame row bytes, part bytes (from byte 2), of which header bytes (11 / 0)
     int ostride, outb;          // out row bytes, bytes reported
 };
@@ -54,10 +55,54 @@ struct RvGatherArgs {
     int32_t* frame_len;
     uint8_t* out;               // [P][out_stride]
     int64_t out_stride;
+    uint8_t* flag;              // [P]: the reporting object's flag (type 2), or null
 };
 
+// Bytes [0, n) of src to dst + doff (doff in 0..3, dst 4-byte aligned), a lane per destination
+// dword, four dwords per lane per round with every load issued before the round's stores (a seq's
+// copies are short: their load latency, not bandwidth, is the cost): two source dword loads (the
+// source's own alignment) and v_alignbyte for an interior dword, byte loads at the run's two ends
+// (the neighbouring bytes belong to other fields).
+__device__ __forceinline__ void copy_run(uint8_t* dst, int doff, const uint8_t* src, int n, int lane) {
+    const int nd = (doff + n + 3) >> 2;  // destination dwords touched
+    const uintptr_t sa = reinterpret_cast<uintptr_t>(src);
+    for (int w0 = 0; w0 < nd; w0 += 256) {
+        uint32_t v[4];
+        bool whole[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int w = w0 + lane + 64 * i;
+            const int b0 = 4 * w - doff;  // source byte of the dword's first byte
+            const uint32_t sh = static_cast<uint32_t>((sa + b0) & 3);
+            // both aligned source dwords inside the run (no read past its last byte)
+            whole[i] = w < nd && b0 >= 0 && b0 + 4 <= n && (sh == 0 || b0 - static_cast<int>(sh) + 8 <= n);
+            v[i] = 0;
+            if (whole[i]) {
+                const uint32_t* p = reinterpret_cast<const uint32_t*>((sa + b0) & ~uintptr_t(3));
+                const uint32_t lo = p[0], hi = sh ? p[1] : 0u;
+                v[i] = sh ? __builtin_amdgcn_alignbyte(hi, lo, sh) : lo;
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int w = w0 + lane + 64 * i;
+            if (whole[i]) {
+                *reinterpret_cast<uint32_t*>(dst + 4 * w) = v[i];
+            } else if (w < nd) {
+                const int b0 = 4 * w - doff;
+                for (int x = 0; x < 4; ++x) {
+                    const int bb = b0 + x;
+                    if (bb >= 0 && bb < n) dst[4 * w + x] = src[bb];
+                }
+            }
+        }
+    }
+}
+
 // A wave per seq: the frame [BE16 size of the new part's code bytes][new part][old part] and the
-// reporting destination's row (its blocks*k bytes, zero after).
+// reporting destination's row (its blocks*k bytes, zero after), copied a dword per lane (frame rows
+// and output rows are 4-byte aligned; the parts' sources are at any byte).  (Eight seqs per wave,
+// their map entries loaded at once, was slower: 489 vs 403 us, profiles/r06.)
 __global__ __launch_bounds__(256) void fec_relay_vr_gather_kernel(RvGatherArgs a) {
     const int lane = threadIdx.x & 63;
     for (int64_t t = static_cast<int64_t>(blockIdx.x) * 4 + (threadIdx.x >> 6); t < a.P;
@@ -71,31 +116,69 @@ __global__ __launch_bounds__(256) void fec_relay_vr_gather_kernel(RvGatherArgs a
             fr[0] = static_cast<uint8_t>(size_cur / 256);
             fr[1] = static_cast<uint8_t>(size_cur % 256);
         }
-        for (int b = lane; b < tn.part; b += 64) fr[2 + b] = pn[b];
+        copy_run(fr, 2, pn, tn.part, lane);
         int len = 2 + tn.part;
         if (m[2] >= 0) {
             const RvTupleDev& to = a.tup[m[2]];
             const uint8_t* po = to.frames + static_cast<int64_t>(m[3]) * to.F + 2;
-            for (int b = lane; b < to.part; b += 64) fr[len + b] = po[b];
+            copy_run(fr + (len & ~3), len & 3, po, to.part, lane);
             len += to.part;
         }
         if (lane == 0) a.frame_len[t] = len;
         const RvTupleDev& tr = a.tup[m[4]];
         const uint8_t* src = tr.out + static_cast<int64_t>(m[5]) * tr.ostride;
         uint8_t* dst = a.out + t * a.out_stride;
-        for (int b = lane; b < a.out_stride; b += 64) dst[b] = b < tr.outb ? src[b] : 0;
+        copy_run(dst, 0, src, tr.outb, lane);
+        for (int b = tr.outb + lane; b < a.out_stride; b += 64) dst[b] = 0;
+        if (a.flag && lane == 0) a.flag[t] = tr.flag[m[5]];
     }
 }
 
-// Payload rows into an instance-ordered stream (src[r] < 0: a gap row, zero with length 0).
+// Payload rows into an instance-ordered stream (src[r] < 0: a gap row, zero with length 0), and
+// (er1 non-null) the rows' hop erasure flags from the seq-ordered patterns (gap rows received).
+// A wave per 4 rows: with L a multiple of 4 and at most 512 bytes, every row's dwords are loaded
+// before any is stored (the copy is latency-bound at one row per wave); bytes otherwise.
 __global__ __launch_bounds__(256) void fec_relay_vr_payload_kernel(const uint8_t* payload, int L, const int64_t* src,
-                                                                   int64_t R, uint8_t* dst, int32_t* len) {
-    for (int64_t r = static_cast<int64_t>(blockIdx.x) * 4 + (threadIdx.x >> 6); r < R;
-         r += static_cast<int64_t>(gridDim.x) * 4) {
-        const int lane = threadIdx.x & 63;
-        const int64_t s = src[r];
-        for (int b = lane; b < L; b += 64) dst[r * L + b] = s < 0 ? 0 : payload[s * L + b];
-        if (lane == 0) len[r] = s < 0 ? 0 : L;
+                                                                   int64_t R, uint8_t* dst, int32_t* len,
+                                                                   const uint8_t* e1, const uint8_t* e2, uint8_t* er1,
+                                                                   uint8_t* er2) {
+    const int lane = threadIdx.x & 63;
+    const int64_t nw = static_cast<int64_t>(gridDim.x) * 4;
+    for (int64_t r0 = (static_cast<int64_t>(blockIdx.x) * 4 + (threadIdx.x >> 6)) * 4; r0 < R; r0 += nw * 4) {
+        int64_t sv[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) sv[i] = r0 + i < R ? src[r0 + i] : -2;
+        if ((L & 3) == 0 && L <= 512) {
+            uint32_t v[4][2];
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+                for (int j = 0; j < 2; ++j) {
+                    const int w = lane + 64 * j;
+                    v[i][j] = (sv[i] >= 0 && w < L / 4) ? reinterpret_cast<const uint32_t*>(payload + sv[i] * L)[w] : 0u;
+                }
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+                for (int j = 0; j < 2; ++j) {
+                    const int w = lane + 64 * j;
+                    if (sv[i] > -2 && w < L / 4) reinterpret_cast<uint32_t*>(dst + (r0 + i) * L)[w] = v[i][j];
+                }
+        } else {
+            for (int i = 0; i < 4; ++i) {
+                if (sv[i] == -2) break;
+                const int64_t r = r0 + i;
+                for (int b = lane; b < L; b += 64) dst[r * L + b] = sv[i] < 0 ? 0 : payload[sv[i] * L + b];
+            }
+        }
+        if (lane < 4 && sv[lane] > -2) {
+            const int64_t r = r0 + lane, s = sv[lane];
+            len[r] = s < 0 ? 0 : L;
+            if (er1) {
+                er1[r] = s < 0 ? 0 : (e1[s] ? 1 : 0);
+                er2[r] = s < 0 ? 0 : (e2[s] ? 1 : 0);
+            }
+        }
     }
 }
 
@@ -168,11 +251,13 @@ struct fec_relay_vr {
             if (ev_join[i]) (void)hipEventDestroy(ev_join[i]);
         }
         if (ev_fork) (void)hipEventDestroy(ev_fork);
+        if (h_pin) (void)hipHostFree(h_pin);
     }
     std::vector<std::unique_ptr<fec::Code>> codes;
     std::vector<int32_t> map;   // [P][6]
     int fstride = 0, ostride = 0;
-    fec::DevBuf d_map;
+    fec::DevBuf d_map, d_e1, d_e2, d_flag;  // the hop patterns (seq order) and, type 2, the flags out
+    uint8_t* h_pin = nullptr;  // page-locked staging: e1, e2 up and the flags down (3 x P bytes)
     bool map_up = false;
 };
 
@@ -249,7 +334,7 @@ int fec_relay_vr_create(int type, int max_payload, const int32_t* sched, int nsw
             ostride = std::max(ostride, c->outb);
         }
         r->fstride = (2 + 2 * part_max + 15) & ~15;
-        r->ostride = ostride;
+        r->ostride = (ostride + 3) & ~3;  // output rows 4-byte aligned (the gather's dword stores)
         // per seq: the newest instance, the old one during double coding, the reporting one
         r->map.assign(static_cast<size_t>(P) * 6, -1);
         for (size_t i = 0; i < inst.size(); ++i) {
@@ -311,6 +396,17 @@ int fec_relay_vr_run(fec_relay_vr* r, const uint8_t* d_payload, const uint8_t* h
                 FEC_HIP(hipEventCreateWithFlags(&r->ev_join[i], hipEventDisableTiming));
             }
         }
+        if (r->type == 2) {  // the hop patterns, for the device-side row gathers (type 3's planners read them on the host)
+            if (int st = r->d_e1.reserve(static_cast<size_t>(r->P))) return st;
+            if (int st = r->d_e2.reserve(static_cast<size_t>(r->P))) return st;
+            if (int st = r->d_flag.reserve(static_cast<size_t>(r->P))) return st;
+            const size_t P = static_cast<size_t>(r->P);
+            if (!r->h_pin) FEC_HIP(hipHostMalloc(reinterpret_cast<void**>(&r->h_pin), 3 * P, hipHostMallocDefault));
+            std::memcpy(r->h_pin, h_e1, P);  // (the previous run's copies are done: it ended synchronised)
+            std::memcpy(r->h_pin + P, h_e2, P);
+            FEC_HIP(hipMemcpyAsync(r->d_e1.p, r->h_pin, P, hipMemcpyHostToDevice, caller));
+            FEC_HIP(hipMemcpyAsync(r->d_e2.p, r->h_pin + P, P, hipMemcpyHostToDevice, caller));
+        }
         FEC_HIP(hipEventRecord(r->ev_fork, caller));
         const int nst = std::min<int>(fec_relay_vr::kStreams, static_cast<int>(r->codes.size()));
         // any return before the join below (an error) drains the side streams first: otherwise the
@@ -333,12 +429,17 @@ int fec_relay_vr_run(fec_relay_vr* r, const uint8_t* d_payload, const uint8_t* h
             fec::Code& c = *r->codes[ci];
             hipStream_t s = r->st[ci];
             const int64_t R = c.R;
-            c.h_er1.resize(static_cast<size_t>(R));
-            c.h_er2.resize(static_cast<size_t>(R));
-            for (int64_t q = 0; q < R; ++q) {
-                const int64_t t = c.src[static_cast<size_t>(q)];
-                c.h_er1[static_cast<size_t>(q)] = t < 0 ? 0 : (h_e1[t] ? 1 : 0);
-                c.h_er2[static_cast<size_t>(q)] = t < 0 ? 0 : (h_e2[t] ? 1 : 0);
+            if (r->type == 3) {  // the planners' erasure rows, on the host
+                c.h_er1.resize(static_cast<size_t>(R));
+                c.h_er2.resize(static_cast<size_t>(R));
+                for (int64_t q = 0; q < R; ++q) {
+                    const int64_t t = c.src[static_cast<size_t>(q)];
+                    c.h_er1[static_cast<size_t>(q)] = t < 0 ? 0 : (h_e1[t] ? 1 : 0);
+                    c.h_er2[static_cast<size_t>(q)] = t < 0 ? 0 : (h_e2[t] ? 1 : 0);
+                }
+            } else {
+                if (int st = c.d_er1.reserve(static_cast<size_t>(R))) return st;
+                if (int st = c.d_er2.reserve(static_cast<size_t>(R))) return st;
             }
             if (int st = c.d_src.reserve(static_cast<size_t>(R) * 8)) return st;
             if (int st = c.d_pay.reserve(static_cast<size_t>(R) * L)) return st;
@@ -351,8 +452,11 @@ int fec_relay_vr_run(fec_relay_vr* r, const uint8_t* d_payload, const uint8_t* h
                 FEC_HIP(hipMemcpyAsync(c.d_src.p, c.src.data(), static_cast<size_t>(R) * 8, hipMemcpyHostToDevice, s));
                 c.src_up = true;
             }
-            hipLaunchKernelGGL(fec::fec_relay_vr_payload_kernel, dim3(fec::grid_rows(R)), dim3(256), 0, s, d_payload, L,
-                               c.d_src.as<const int64_t>(), R, c.d_pay.as<uint8_t>(), c.d_len.as<int32_t>());
+            const bool t2 = r->type == 2;
+            hipLaunchKernelGGL(fec::fec_relay_vr_payload_kernel, dim3(fec::grid_rows((R + 3) / 4)), dim3(256), 0, s, d_payload, L,
+                               c.d_src.as<const int64_t>(), R, c.d_pay.as<uint8_t>(), c.d_len.as<int32_t>(),
+                               t2 ? r->d_e1.as<const uint8_t>() : nullptr, t2 ? r->d_e2.as<const uint8_t>() : nullptr,
+                               t2 ? c.d_er1.as<uint8_t>() : nullptr, t2 ? c.d_er2.as<uint8_t>() : nullptr);
             FEC_HIP(hipGetLastError());
             // each instance a fresh source encoder: its rows behind kGap zero-length packets (>= n-1)
             if (int st = fec_encode_batch(c.codec, c.d_pay.as<uint8_t>(), c.d_len.as<int32_t>(), 0, R, c.d_cw.as<uint8_t>(),
@@ -362,13 +466,9 @@ int fec_relay_vr_run(fec_relay_vr* r, const uint8_t* d_payload, const uint8_t* h
                                c.d_src.as<const int64_t>(), R, c.d_cw.as<uint8_t>(), c.CW);
             FEC_HIP(hipGetLastError());
             if (r->type == 2) {
-                if (int st = c.d_er1.reserve(static_cast<size_t>(R))) return st;
-                if (int st = c.d_er2.reserve(static_cast<size_t>(R))) return st;
                 if (int st = c.d_flag.reserve(static_cast<size_t>(R))) return st;
                 const size_t wb = fec_swdf_workspace_bytes(c.sw, R);
                 if (int st = c.d_work.reserve(wb)) return st;
-                FEC_HIP(hipMemcpyAsync(c.d_er1.p, c.h_er1.data(), static_cast<size_t>(R), hipMemcpyHostToDevice, s));
-                FEC_HIP(hipMemcpyAsync(c.d_er2.p, c.h_er2.data(), static_cast<size_t>(R), hipMemcpyHostToDevice, s));
                 if (int st = fec_swdf_relay_batch(c.sw, c.d_cw.as<uint8_t>(), c.CW, c.d_er1.as<uint8_t>(), R,
                                                   c.d_frames.as<uint8_t>(), nullptr, c.d_work.p, wb, s))
                     return st;
@@ -428,8 +528,9 @@ int fec_relay_vr_run(fec_relay_vr* r, const uint8_t* d_payload, const uint8_t* h
         fec::RvGatherArgs a{};
         for (size_t i = 0; i < r->codes.size(); ++i) {
             const fec::Code& c = *r->codes[i];
-            a.tup[i] = {c.d_frames.as<const uint8_t>(), c.d_out.as<const uint8_t>(), c.F, c.part,
-                        r->type == 3 ? 11 : 0, c.ostride, c.outb};
+            a.tup[i] = {c.d_frames.as<const uint8_t>(), c.d_out.as<const uint8_t>(),
+                        r->type == 2 ? c.d_flag.as<const uint8_t>() : nullptr, c.F, c.part, r->type == 3 ? 11 : 0,
+                        c.ostride, c.outb};
         }
         a.map = r->d_map.as<const int32_t>();
         a.P = r->P;
@@ -438,17 +539,14 @@ int fec_relay_vr_run(fec_relay_vr* r, const uint8_t* d_payload, const uint8_t* h
         a.frame_len = d_frame_len;
         a.out = d_out;
         a.out_stride = r->ostride;
+        a.flag = r->type == 2 ? r->d_flag.as<uint8_t>() : nullptr;
         hipLaunchKernelGGL(fec::fec_relay_vr_gather_kernel, dim3(fec::grid_rows(r->P)), dim3(256), 0, s, a);
         FEC_HIP(hipGetLastError());
-        if (r->type == 2)  // the destinations' flags, after every code's launches (a copy to pageable
-                           // memory returns only when the stream has reached it)
-            for (auto& cp : r->codes) {
-                fec::Code& c = *cp;
-                c.h_flag.resize(static_cast<size_t>(c.R));
-                FEC_HIP(hipMemcpyAsync(c.h_flag.data(), c.d_flag.p, static_cast<size_t>(c.R), hipMemcpyDeviceToHost, s));
-            }
+        if (r->type == 2 && h_flag)  // the reporting objects' flags, gathered by the kernel in seq order
+            FEC_HIP(hipMemcpyAsync(r->h_pin + 2 * r->P, r->d_flag.p, static_cast<size_t>(r->P), hipMemcpyDeviceToHost, s));
         FEC_HIP(hipStreamSynchronize(s));
-        if (h_flag)
+        if (r->type == 2 && h_flag) std::memcpy(h_flag, r->h_pin + 2 * r->P, static_cast<size_t>(r->P));
+        if (r->type == 3 && h_flag)
             for (int64_t t = 0; t < r->P; ++t) {
                 const int32_t* m = &r->map[static_cast<size_t>(t) * 6];
                 h_flag[t] = r->codes[static_cast<size_t>(m[4])]->h_flag[static_cast<size_t>(m[5])];

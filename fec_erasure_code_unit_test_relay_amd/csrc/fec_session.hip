@@ -35,6 +35,7 @@
 #include <algorithm>
 #include <chrono>
 #include <cstdint>
+#include <cstdio>
 #include <cstring>
 #include <map>
 #include <memory>
@@ -929,28 +930,34 @@ __device__ __forceinline__ uint8_t gf_mul_t(const uint8_t* gexp, const uint8_t* 
     return (a && b) ? gexp[glog[a] + glog[b]] : 0;
 }
 
-// Every job's outputs: a workgroup per job (its window rows resolved once into LDS), a thread per
-// output symbol (block j, output o).  HOP1: window rows are hop-1 references (seq*2 + part; the
-// current part is followed by the old part, as in the received packet); else part indices into
-// the relay buffer.
+// Every job's outputs: a wave per job (its window rows resolved once into the wave's LDS slots, four
+// jobs per workgroup, no workgroup barrier), a lane per output symbol (block j, output o).  HOP1:
+// window rows are hop-1 references (seq*2 + part; the current part is followed by the old part, as
+// in the received packet); else part indices into the relay buffer.
 template <bool HOP1>
 __global__ __launch_bounds__(256) void ses_apply_kernel(SesDev d, const SesJob* jobs, int64_t njobs, const void* refs,
                                                         uint8_t* out) {
     __shared__ uint8_t gexp[512];
     __shared__ uint8_t glog[256];
-    __shared__ const uint8_t* rp_a[kApplyRows];  // first segment (current part, or the relay part)
-    __shared__ const uint8_t* rp_b[kApplyRows];  // second segment (the old part after the current one)
-    __shared__ int32_t rl_a[kApplyRows], rl_b[kApplyRows];
+    __shared__ const uint8_t* rp_a_s[4][kApplyRows];  // first segment (current part, or the relay part)
+    __shared__ const uint8_t* rp_b_s[4][kApplyRows];  // second segment (the old part after the current one)
+    __shared__ int32_t rl_a_s[4][kApplyRows], rl_b_s[4][kApplyRows];
     for (int i = threadIdx.x; i < 512; i += 256) gexp[i] = d.gf[i];
     glog[threadIdx.x] = d.gf[512 + threadIdx.x];
-    for (int64_t jb = blockIdx.x; jb < njobs; jb += gridDim.x) {
+    __syncthreads();
+    const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const uint8_t** rp_a = rp_a_s[wv];
+    const uint8_t** rp_b = rp_b_s[wv];
+    int32_t* rl_a = rl_a_s[wv];
+    int32_t* rl_b = rl_b_s[wv];
+    for (int64_t jb = static_cast<int64_t>(blockIdx.x) * 4 + wv; jb < njobs; jb += static_cast<int64_t>(gridDim.x) * 4) {
         const SesJob J = jobs[jb];
         const int nrows = J.rb0 + J.nin;
-        __syncthreads();  // (the previous job's rows are no longer read)
-        if (threadIdx.x < nrows) {
-            const int r = threadIdx.x;
-            const uint8_t* a = nullptr;
-            const uint8_t* b = nullptr;
+        __builtin_amdgcn_wave_barrier();  // (the previous job's rows are no longer read)
+        if (lane < nrows) {
+            const int r = lane;
+            const uint8_t* pa = nullptr;
+            const uint8_t* pb = nullptr;
             int la = 0, lb = 0;
             if (HOP1) {
                 const int64_t ref = static_cast<const int64_t*>(refs)[J.ref0 + r];
@@ -958,29 +965,31 @@ __global__ __launch_bounds__(256) void ses_apply_kernel(SesDev d, const SesJob* 
                     const int64_t seq = ref >> 1;
                     const int lc = d.len_cur[seq], lo = d.len_old[seq];
                     if ((ref & 1) == 0) {
-                        a = d.cur + d.cur_off[seq];
+                        pa = d.cur + d.cur_off[seq];
                         la = lc;
                     }
-                    b = d.old + d.old_off[seq];
+                    pb = d.old + d.old_off[seq];
                     lb = lo;
                 }
             } else {
                 const int32_t pi = static_cast<const int32_t*>(refs)[J.ref0 + r];
                 if (pi >= 0) {
-                    const int64_t p = d.parts[2 * pi], e = d.parts[2 * pi + 1];
-                    a = d.rpk + p;
-                    la = p < e ? static_cast<int32_t>(e - p) : 0;
+                    const int64_t pp = d.parts[2 * pi], e = d.parts[2 * pi + 1];
+                    pa = d.rpk + pp;
+                    la = pp < e ? static_cast<int32_t>(e - pp) : 0;
                 }
             }
-            rp_a[r] = a;
-            rp_b[r] = b;
+            rp_a[r] = pa;
+            rp_b[r] = pb;
             rl_a[r] = la;
             rl_b[r] = lb;
         }
-        __syncthreads();
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         const int total = J.nout * J.blocks;
         const uint8_t* cf = d.coef + J.coef;
-        for (int id = threadIdx.x; id < total; id += 256) {
+        for (int id = lane; id < total; id += 64) {
             const int o = id / J.blocks, j = id - o * J.blocks;
             const int rbase = J.rb0 - J.rstep * o;
             const int x0 = J.base - 2 + j * J.bs;  // the part's byte of the window's position 0
@@ -996,6 +1005,9 @@ __global__ __launch_bounds__(256) void ses_apply_kernel(SesDev d, const SesJob* 
             }
             out[J.out + static_cast<int64_t>(j) * J.ostride + o] = acc;
         }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     }
 }
 
@@ -1003,8 +1015,8 @@ __global__ __launch_bounds__(256) void ses_apply_kernel(SesDev d, const SesJob* 
 // per call in order: the shift of :124-129 (rows 0..n2-2 take rows 1..n2-1, row n2-1 keeps its
 // bytes), the call's symbols into row n2-1 (type 2: data at 2 + j*n2 + i; type 3: every position),
 // type 2's parity from rows 0..n2-2 (:601-613), then row n2-1's first `size` bytes to the packet.
-__global__ __launch_bounds__(256) void ses_lineage_kernel(SesDev d, const SesCall* calls, const int64_t* lin,
-                                                          int64_t nlin, const uint8_t* sym) {
+__global__ __launch_bounds__(256) void ses_lineage_map_kernel(SesDev d, const SesCall* calls, const int64_t* lin,
+                                                              int64_t nlin, const uint8_t* sym) {
     extern __shared__ uint8_t rows[];  // kSMaxN x kSRow
     __shared__ uint8_t gexp[512];
     __shared__ uint8_t glog[256];
@@ -1060,6 +1072,94 @@ __global__ __launch_bounds__(256) void ses_lineage_kernel(SesDev d, const SesCal
             __syncthreads();
             uint8_t* o = d.rpk + c.out;
             for (int x = threadIdx.x; x < c.size; x += 256) o[x] = top[x];
+        }
+    }
+}
+
+// The same walk with the map in registers: logical row i at physical row (map >> 4i) & 15, the
+// shift of :124-129 a rotation of the low n2 nibbles, computed by every thread alike (no map in
+// LDS, no barrier for it; a lineage's n2 can change where copy_elements hands a new code's object
+// to the main one); the new top row keeps the old one's bytes only where the call does not write
+// them ([0, 2) and [2 + blocks*n2, hwm): every byte at or past hwm is still zero in every row); one
+// barrier a call, between its writes and the store of its part; the next call's descriptor and the
+// first 1 024 of its symbols are loaded while the current call computes (a lineage is a chain of up
+// to ~600 calls, so the walk is bound by each call's latency).
+__global__ __launch_bounds__(256) void ses_lineage_kernel(SesDev d, const SesCall* calls, const int64_t* lin,
+                                                          int64_t nlin, const uint8_t* sym) {
+    extern __shared__ uint8_t rows[];  // kSMaxN x kSRow
+    __shared__ uint8_t gexp[512];
+    __shared__ uint8_t glog[256];
+    constexpr int NI = 4;  // prefetched symbol bytes per thread
+    for (int i = threadIdx.x; i < 512; i += 256) gexp[i] = d.gf[i];
+    glog[threadIdx.x] = d.gf[512 + threadIdx.x];
+    const int tid = threadIdx.x;
+    for (int64_t l = blockIdx.x; l < nlin; l += gridDim.x) {
+        __syncthreads();
+        for (int i = tid; i < kSMaxN * kSRow / 16; i += 256) reinterpret_cast<uint4*>(rows)[i] = make_uint4(0, 0, 0, 0);
+        __syncthreads();
+        const int64_t c0 = lin[l], c1 = lin[l + 1];
+        uint64_t map = 0;
+        for (int i = 0; i < kSMaxN; ++i) map |= static_cast<uint64_t>(i) << (4 * i);
+        int hwm = 2;
+        SesCall nc{};
+        uint8_t pre[NI];
+        auto nsym = [](const SesCall& c) { return c.type == 3 ? c.blocks * c.n2 : c.blocks * c.k; };
+        auto prefetch = [&](const SesCall& c) __attribute__((always_inline)) {
+            const uint8_t* s = sym + c.d;
+            const int ns = nsym(c);
+#pragma unroll
+            for (int q = 0; q < NI; ++q) {
+                const int id = tid + 256 * q;
+                pre[q] = id < ns ? s[id] : 0;
+            }
+        };
+        if (c0 < c1) {
+            nc = calls[c0];
+            prefetch(nc);
+        }
+        for (int64_t ci = c0; ci < c1; ++ci) {
+            const SesCall c = nc;
+            uint8_t cur[NI];
+#pragma unroll
+            for (int q = 0; q < NI; ++q) cur[q] = pre[q];
+            if (ci + 1 < c1) nc = calls[ci + 1];
+            const int n2 = c.n2, k = c.k, blocks = c.blocks;
+            const int end = 2 + blocks * n2;
+            const int old_top = static_cast<int>((map >> (4 * (n2 - 1))) & 15), top_row = static_cast<int>(map & 15);
+            {
+                const uint64_t mask = (uint64_t(1) << (4 * n2)) - 1, lo = map & mask;
+                map = (map & ~mask) | (lo >> 4) | ((lo & 15) << (4 * (n2 - 1)));
+            }
+            uint8_t* top = rows + top_row * kSRow;
+            const uint8_t* ot = rows + old_top * kSRow;
+            if (tid < 2) top[tid] = ot[tid];
+            for (int x = end + tid; x < hwm; x += 256) top[x] = ot[x];
+            hwm = max(hwm, end);
+            const uint8_t* s = sym + c.d;
+            const int ns = nsym(c);
+            const int per = c.type == 3 ? n2 : k;  // symbols per block
+            for (int id = tid, q = 0; id < ns; id += 256, ++q) {
+                const int j = id / per, i = id - j * per;
+                top[2 + j * n2 + i] = q < NI ? cur[q < NI ? q : 0] : s[id];
+            }
+            if (c.type != 3) {
+                const int np = n2 - k;
+                const uint8_t* g = d.coef + c.g2;
+                for (int id = tid; id < blocks * np; id += 256) {
+                    const int j = id / np, delta = id - j * np;
+                    uint8_t acc = 0;
+                    for (int m = 0; m < k; ++m) {
+                        const int pr = static_cast<int>((map >> (4 * (m + delta))) & 15);  // logical row m + delta
+                        acc ^= gf_mul_t(gexp, glog, g[delta * k + m], rows[pr * kSRow + 2 + j * n2 + m]);
+                    }
+                    top[2 + j * n2 + n2 - 1 - delta] = acc;
+                }
+            }
+            if (ci + 1 < c1) prefetch(nc);
+            __syncthreads();
+            uint8_t* o = d.rpk + c.out;
+            for (int x = tid; x < c.size; x += 256) o[x] = top[x];
+            if (n2 == 1) __syncthreads();  // one row: the next call may write the row this store reads
         }
     }
 }
@@ -1311,7 +1411,7 @@ int fec_relay_session_run(fec_relay_session* h, const uint8_t* d_payload, uint8_
     const fec::SesDev d = dev_view(h, d_relay);
     // the relay: every call's symbols, then the lineages in order, then the fixed bytes
     if (!p.rjobs.empty()) {
-        const unsigned grid = static_cast<unsigned>(std::min<int64_t>(static_cast<int64_t>(p.rjobs.size()), 65536));
+        const unsigned grid = static_cast<unsigned>(std::min<int64_t>((static_cast<int64_t>(p.rjobs.size()) + 3) / 4, 65536));
         hipLaunchKernelGGL(fec::ses_apply_kernel<true>, dim3(grid), dim3(256), 0, s, d,
                            static_cast<const fec::SesJob*>(h->rjobs.p), static_cast<int64_t>(p.rjobs.size()),
                            h->rrefs.p, static_cast<uint8_t*>(h->sym.p));
@@ -1320,9 +1420,10 @@ int fec_relay_session_run(fec_relay_session* h, const uint8_t* d_payload, uint8_
     const int64_t nlin = static_cast<int64_t>(p.lin.size()) - 1;
     if (nlin > 0) {
         const size_t lds = static_cast<size_t>(fec::kSMaxN) * fec::kSRow;
-        hipLaunchKernelGGL(fec::ses_lineage_kernel, dim3(static_cast<unsigned>(std::min<int64_t>(nlin, 65536))),
-                           dim3(256), lds, s, d, static_cast<const fec::SesCall*>(h->calls.p),
-                           static_cast<const int64_t*>(h->lin.p), nlin, static_cast<const uint8_t*>(h->sym.p));
+        hipLaunchKernelGGL(!std::getenv("FEC_SES_LIN_MAP") ? fec::ses_lineage_kernel : fec::ses_lineage_map_kernel,
+                           dim3(static_cast<unsigned>(std::min<int64_t>(nlin, 65536))), dim3(256), lds, s, d,
+                           static_cast<const fec::SesCall*>(h->calls.p), static_cast<const int64_t*>(h->lin.p), nlin,
+                           static_cast<const uint8_t*>(h->sym.p));
         FEC_HIP(hipGetLastError());
     }
     hipLaunchKernelGGL(fec::ses_prefix_kernel, dim3(static_cast<unsigned>((p.Q + 255) / 256)), dim3(256), 0, s, d,
@@ -1332,7 +1433,7 @@ int fec_relay_session_run(fec_relay_session* h, const uint8_t* d_payload, uint8_
     FEC_HIP(hipMemsetAsync(d_dest_out, 0, static_cast<size_t>(p.Q) * 320, s));
     FEC_HIP(hipMemsetAsync(d_lost, 0, sizeof(int64_t), s));
     if (!p.djobs.empty()) {
-        const unsigned grid = static_cast<unsigned>(std::min<int64_t>(static_cast<int64_t>(p.djobs.size()), 65536));
+        const unsigned grid = static_cast<unsigned>(std::min<int64_t>((static_cast<int64_t>(p.djobs.size()) + 3) / 4, 65536));
         hipLaunchKernelGGL(fec::ses_apply_kernel<false>, dim3(grid), dim3(256), 0, s, d,
                            static_cast<const fec::SesJob*>(h->djobs.p), static_cast<int64_t>(p.djobs.size()),
                            h->djr.p, d_dest_out);

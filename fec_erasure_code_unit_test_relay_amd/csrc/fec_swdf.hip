@@ -1396,16 +1396,13 @@ bool launch_fast_geo(fec::SwFastArgs a, hipStream_t s, hipError_t* err) {
     return true;
 }
 
-// The relay's kernel: the row scatter (default) with tiles of FEC_SWDF_TR = 64 / 48 packets
-// (512 threads) or 32 packets (256 threads, four workgroups per CU), or FEC_SWDF_RELAY=3 the
-// three-tile kernel of round 5 (kept for A/B).
+// The relay's kernel: the row scatter (default; tiles of 64 packets for k >= 7, of 32 / 16 for the
+// longer rows of k = 5..6 / 4, 512 threads), or FEC_SWDF_RELAY=3 round 5's three-tile kernel (k >= 7,
+// kept for A/B).
 int relay_variant() {
     static const int v = [] {
         const char* r = std::getenv("FEC_SWDF_RELAY");
-        if (r && r[0] == '3') return 0;
-        const char* t = std::getenv("FEC_SWDF_TR");
-        const int tr = t ? std::atoi(t) : 64;
-        return tr == 32 ? 32 : tr == 48 ? 48 : 64;
+        return (r && r[0] == '3') ? 0 : 1;
     }();
     return v;
 }
@@ -1416,18 +1413,20 @@ bool launch_fast(int K, fec::SwFastArgs a, int L, int n1, int n2, int blocks, in
     if (L != kFastL || n2 != kFastN || (RELAY && n1 != kFastN) || blocks != S) return false;
     if ((reinterpret_cast<uintptr_t>(a.in) & 15) || (reinterpret_cast<uintptr_t>(a.out) & 3)) return false;
     const int rv = RELAY ? relay_variant() : 0;
-#define FEC_SW_FAST_CASE(KK)                                                        \
-    case KK: {                                                                      \
-        using GM = fec::FastGeo<KK, kFastN, kFastN, kFastL, RELAY>;                  \
-        if (stride != GM::STRIDE) return false;                                     \
-        if constexpr (RELAY) {                                                      \
-            if (rv == 64) return launch_fast_geo<fec::FastGeo<KK, kFastN, kFastN, kFastL, true, 64, true>>(a, s, err); \
-            if (rv == 48) return launch_fast_geo<fec::FastGeo<KK, kFastN, kFastN, kFastL, true, 48, true>>(a, s, err); \
-            if (rv == 32) return launch_fast_geo<fec::FastGeo<KK, kFastN, kFastN, kFastL, true, 32, true, 256>>(a, s, err); \
-        }                                                                           \
-        return launch_fast_geo<GM>(a, s, err);                                      \
+#define FEC_SW_FAST_CASE(KK)                                                                      \
+    case KK: {                                                                                    \
+        using GM = fec::FastGeo<KK, kFastN, kFastN, kFastL, RELAY>;                                \
+        if (stride != GM::STRIDE) return false;                                                   \
+        if constexpr (RELAY) {                                                                    \
+            if (rv) return launch_fast_geo<fec::FastGeo<KK, kFastN, kFastN, kFastL, true, (KK >= 7 ? 64 : KK >= 5 ? 32 : 16), true>>(a, s, err); \
+            if constexpr (KK < 7) return false;                                                   \
+            else return launch_fast_geo<GM>(a, s, err);                                           \
+        } else {                                                                                  \
+            return launch_fast_geo<GM>(a, s, err);                                                \
+        }                                                                                         \
     }
     switch (K) {
+        FEC_SW_FAST_CASE(4) FEC_SW_FAST_CASE(5) FEC_SW_FAST_CASE(6)
         FEC_SW_FAST_CASE(7) FEC_SW_FAST_CASE(8) FEC_SW_FAST_CASE(9) FEC_SW_FAST_CASE(10) FEC_SW_FAST_CASE(11)
         default: return false;
     }

@@ -126,9 +126,15 @@ void ParameterEstimator::make_MDS_estimates() {
 
 const DecodeRules& VrPlan::rules_for(int T, int B, int N) {
     const int key = T * 1024 + B * 32 + N;
+    if (key >= 0 && static_cast<size_t>(key) < rules_fast_.size() && rules_fast_[static_cast<size_t>(key)])
+        return *rules_fast_[static_cast<size_t>(key)];
     auto it = rules_.find(key);
-    if (it != rules_.end()) return *it->second;
-    return *rules_.emplace(key, shared_decode_rules(T, B, N)).first->second;
+    if (it == rules_.end()) it = rules_.emplace(key, shared_decode_rules(T, B, N)).first;
+    if (key >= 0 && key < kRulesKeys) {  // a direct table beside the map (one lookup per switch)
+        if (rules_fast_.empty()) rules_fast_.assign(kRulesKeys, nullptr);
+        rules_fast_[static_cast<size_t>(key)] = it->second.get();
+    }
+    return *it->second;
 }
 
 namespace {
@@ -660,8 +666,11 @@ void VrPlan::control(const uint8_t* pattern, int64_t n_pattern, int T, int B, in
     steady_packets = 0;
     transition_packets = 0;
     sum_coding_rate = 0;
-    std::vector<std::vector<Reports>> reps;   // per decoder instance, in call order
-    std::vector<const DecodeRules*> drules;   // per decoder instance
+    // per decoder instance: its report ranges (kept across runs with their capacity: a run's
+    // instance i reuses the list of the previous run's, no allocation once warm) and its rules
+    std::vector<std::vector<Reports>>& reps = reps_;
+    std::vector<const DecodeRules*>& drules = drules_;
+    drules.clear();
 
     // ---- sender (Application_Layer_Sender.cpp:9-31, 64-93, 221-224) ----
     const bool adaptive = B == -1 || N == -1;
@@ -758,7 +767,11 @@ void VrPlan::control(const uint8_t* pattern, int64_t n_pattern, int T, int B, in
         v.first = v.end = first;
         v.role_switch = -1;  // set when it becomes the old decoder
         dec.push_back(v);
-        reps.emplace_back();
+        const size_t id = dec.size() - 1;
+        if (id < reps.size())
+            reps[id].clear();
+        else
+            reps.emplace_back();
         drules.push_back(&rules_for(T_, B_, N_));
         return static_cast<int>(dec.size()) - 1;
     };

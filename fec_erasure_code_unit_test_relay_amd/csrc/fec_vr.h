@@ -199,7 +199,11 @@ private:
     void close_jobs();
     void decode_instance(const DecJob& job, std::vector<RecEntry>& recs);
     std::map<int, std::shared_ptr<const DecodeRules>> rules_;  // key T*1024 + B*32 + N
+    static constexpr int kRulesKeys = 64 * 1024;
+    std::vector<const DecodeRules*> rules_fast_;               // the same, by key (filled on use)
     const DecodeRules& rules_for(int T, int B, int N);
+    std::vector<std::vector<Reports>> reps_;                   // the control loop's per-instance lists
+    std::vector<const DecodeRules*> drules_;
     std::vector<std::thread> workers_;
     std::vector<std::vector<RecEntry>> recs_;  // per worker
     std::mutex qmu_;
