@@ -661,7 +661,7 @@ __global__ __launch_bounds__(kTileThreads, (tile_min_wg<K, NP>())) void fec_enco
 // segment mode at L = 300 (config 4's tuples): the list's entries with an L = 300 tile geometry
 #define FEC_ENC_TILE_SEG300_LIST(X) \
     X(8, 3) X(9, 5) X(11, 0) X(10, 1) X(9, 2) X(7, 4) X(6, 5) X(5, 6) X(4, 7) X(10, 3) X(9, 3) X(10, 4) \
-    X(8, 4) X(10, 5) X(7, 5)
+    X(8, 4) X(10, 5) X(7, 5) X(10, 0) X(9, 1) X(6, 0) X(9, 0) X(8, 2) X(8, 1) X(5, 0)
 #endif
 
 #define FEC_ENC_TILE_INST(K, NP) \

@@ -143,7 +143,7 @@ const void* fec_encode_tile_seg_kernel_for(int k, int np, int L);
 // [tfirst[t], tfirst[t+1]) and it is encoded by fec_encode_tile_kernel<k_t, n_t-k_t, 300, true>'s
 // walk.  Only tuples for which fec_encode_tile_multi_supports() holds (their walk fits the shared
 // register budget of 4 workgroups per CU).
-constexpr int kEncMultiMax = 16;
+constexpr int kEncMultiMax = 24;
 struct EncMultiArgs {
     const uint8_t* payload;       // [sent][L] payload rows
     const int32_t* len;           // lengths (null: all L)

@@ -1165,10 +1165,14 @@ __global__ __launch_bounds__(GM::NT, GM::WPE) void fec_sw_fast_relay2_kernel(SwF
                         }
                     }
                     uint8_t* dst = smem + fb + p * (F + 1);
+#ifdef FEC_RELAY2_ABLATE_WRITES  // diagnostic build only (wrong output): one byte write per position
+                    dst[0] = static_cast<uint8_t>(w ^ (w >> 8) ^ (w >> 16) ^ (w >> 24));
+#else
                     dst[0] = static_cast<uint8_t>(w);
                     if (!CHK || nb > 1) dst[N2] = static_cast<uint8_t>(w >> 8);
                     if (!CHK || nb > 2) dst[2 * N2] = static_cast<uint8_t>(w >> 16);
                     if (!CHK || nb > 3) dst[3 * N2] = static_cast<uint8_t>(w >> 24);
+#endif
                 }
             });
         };
