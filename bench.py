@@ -656,7 +656,8 @@ def relay_adaptive(steps):
         res[f"type{t}"] = {"ms": round(dt * 1e3, 3), "GiB_s": round(P * L / dt / 2**30, 3),
                            "unflagged": int((flags == 0).sum()), "verified": bool(ok)}
     res["note"] = ("one fixed-rate batch per code over its instances laid end to end (each behind zero rows), "
-                   "planners reset per instance; host work (erasure gathers, type 3's planners) inside; "
+                   "planners reset per instance; type 2's erasure rows and flags gathered on the device, type 3's "
+                   "host planners (and their erasure rows) inside; "
                    "verified = equal to tests/golden/relay_vr_360k.json, made by this repo's reference-structured "
                    "driver over the oracle's methods (the reference ships no relay output: parity unpinned)")
     return res
