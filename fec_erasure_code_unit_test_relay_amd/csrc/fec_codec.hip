@@ -485,7 +485,7 @@ int launch_plan(fec_codec* c, const uint8_t* d_er, int64_t P, void* d_ws, size_t
     ea.keys = w.keys;
     ea.reps_tr = w.reps_tr;
     ea.stamps = (c->stamp_kernel == FEC_KERNEL_DEC_SCAN) ? c->d_stamps : nullptr;
-    const int64_t sblocks = std::min<int64_t>((P + 4095) / 4096, 8192);
+    const int64_t sblocks = std::min<int64_t>((P + 1023) / 1024, 32768);  // a wave per 1024 packets (fec_shapes.hip)
     hipLaunchKernelGGL(fec::fec_episode_kernel, dim3(static_cast<unsigned>(sblocks)), dim3(64), 0, s, ea);
     HIP_TRY(hipGetLastError());
     if (int st = c->end(stop, s)) return st;

@@ -22,6 +22,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <memory>
@@ -102,7 +103,8 @@ __device__ __forceinline__ void copy_run(uint8_t* dst, int doff, const uint8_t* 
 // A wave per seq: the frame [BE16 size of the new part's code bytes][new part][old part] and the
 // reporting destination's row (its blocks*k bytes, zero after), copied a dword per lane (frame rows
 // and output rows are 4-byte aligned; the parts' sources are at any byte).  (Eight seqs per wave,
-// their map entries loaded at once, was slower: 489 vs 403 us, profiles/r06.)
+// their map entries loaded at once, was slower: 489 vs 403 us; a wave per (seq, row) -- the frame
+// and the reported row on two waves -- too: 518 vs 476 us, profiles/r06/r06s.)
 __global__ __launch_bounds__(256) void fec_relay_vr_gather_kernel(RvGatherArgs a) {
     const int lane = threadIdx.x & 63;
     for (int64_t t = static_cast<int64_t>(blockIdx.x) * 4 + (threadIdx.x >> 6); t < a.P;
@@ -182,13 +184,18 @@ __global__ __launch_bounds__(256) void fec_relay_vr_payload_kernel(const uint8_t
     }
 }
 
-// Zero the gap rows (src[r] < 0) of rows of W bytes.
-__global__ __launch_bounds__(256) void fec_relay_vr_zero_kernel(const int64_t* src, int64_t R, uint8_t* rows, int W) {
-    for (int64_t r = static_cast<int64_t>(blockIdx.x) * 4 + (threadIdx.x >> 6); r < R;
-         r += static_cast<int64_t>(gridDim.x) * 4) {
-        if (src[r] >= 0) continue;
-        for (int b = threadIdx.x & 63; b < W; b += 64) rows[r * W + b] = 0;
-    }
+// Zero the gap rows of rows of W bytes: the kGap rows in front of instance b's first row
+// starts[b] are one contiguous run of kGap * W bytes, a workgroup per instance, dword stores
+// inside the run and byte stores at its two unaligned ends.  (A wave per row over all R rows,
+// reading the row map to find the gap rows, took 20 - 38 us for the large codes.)
+__global__ __launch_bounds__(256) void fec_relay_vr_zero_kernel(const int64_t* starts, int ninst, uint8_t* rows, int W) {
+    if (static_cast<int>(blockIdx.x) >= ninst) return;
+    const int64_t b0 = (starts[blockIdx.x] - kGap) * static_cast<int64_t>(W), b1 = b0 + static_cast<int64_t>(kGap) * W;
+    const int64_t a0 = (b0 + 3) & ~int64_t(3), a1 = b1 & ~int64_t(3);
+    const int tid = threadIdx.x;
+    for (int64_t o = a0 + 4 * tid; o < a1; o += 4 * 256) *reinterpret_cast<uint32_t*>(rows + o) = 0u;
+    if (tid < a0 - b0) rows[b0 + tid] = 0;
+    if (tid < b1 - a1) rows[a1 + tid] = 0;
 }
 
 unsigned grid_rows(int64_t R) { return static_cast<unsigned>(std::max<int64_t>(1, std::min<int64_t>((R + 3) / 4, 65536))); }
@@ -220,7 +227,7 @@ struct Code {
     fec_codec* codec = nullptr;
     fec_swdf* sw = nullptr;
     fec_sdswdf* sd = nullptr;
-    DevBuf d_src, d_pay, d_len, d_cw, d_cwlen, d_er1, d_er2, d_frames, d_out, d_flag, d_work;
+    DevBuf d_src, d_starts, d_pay, d_len, d_cw, d_cwlen, d_er1, d_er2, d_frames, d_out, d_flag, d_work;
     std::vector<uint8_t> h_er1, h_er2, h_flag;
     bool src_up = false;
     Code() = default;
@@ -237,7 +244,8 @@ struct Code {
 }  // namespace fec
 
 struct fec_relay_vr {
-    static constexpr int kStreams = fec::kMaxCodes;  // a stream per code: the codes' chains run side by side
+    static constexpr int kStreams = fec::kMaxCodes;  // type 3: a stream per code (its chains run side by side)
+    static constexpr int kQueues = 4;                // type 2: the chains on this many streams
     int type = 2, L = 0;
     int64_t P = 0;
     hipStream_t st[kStreams] = {};
@@ -425,9 +433,8 @@ int fec_relay_vr_run(fec_relay_vr* r, const uint8_t* d_payload, const uint8_t* h
             FEC_HIP(hipStreamWaitEvent(r->st[i], r->ev_fork, 0));
         // one code's chain on its own stream; type 3's host planners make its batches synchronous,
         // so its codes run on threads of their own (each code has its own planner objects)
-        auto run_code = [&](size_t ci) -> int {
+        auto run_code = [&](size_t ci, hipStream_t s) -> int {
             fec::Code& c = *r->codes[ci];
-            hipStream_t s = r->st[ci];
             const int64_t R = c.R;
             if (r->type == 3) {  // the planners' erasure rows, on the host
                 c.h_er1.resize(static_cast<size_t>(R));
@@ -442,6 +449,7 @@ int fec_relay_vr_run(fec_relay_vr* r, const uint8_t* d_payload, const uint8_t* h
                 if (int st = c.d_er2.reserve(static_cast<size_t>(R))) return st;
             }
             if (int st = c.d_src.reserve(static_cast<size_t>(R) * 8)) return st;
+            if (int st = c.d_starts.reserve(c.starts.size() * 8)) return st;
             if (int st = c.d_pay.reserve(static_cast<size_t>(R) * L)) return st;
             if (int st = c.d_len.reserve(static_cast<size_t>(R) * 4)) return st;
             if (int st = c.d_cw.reserve(static_cast<size_t>(R) * c.CW)) return st;
@@ -450,6 +458,7 @@ int fec_relay_vr_run(fec_relay_vr* r, const uint8_t* d_payload, const uint8_t* h
             if (int st = c.d_out.reserve(static_cast<size_t>(R) * c.ostride)) return st;
             if (!c.src_up) {  // the row map depends on the schedule alone: uploaded once
                 FEC_HIP(hipMemcpyAsync(c.d_src.p, c.src.data(), static_cast<size_t>(R) * 8, hipMemcpyHostToDevice, s));
+                FEC_HIP(hipMemcpyAsync(c.d_starts.p, c.starts.data(), c.starts.size() * 8, hipMemcpyHostToDevice, s));
                 c.src_up = true;
             }
             const bool t2 = r->type == 2;
@@ -462,8 +471,10 @@ int fec_relay_vr_run(fec_relay_vr* r, const uint8_t* d_payload, const uint8_t* h
             if (int st = fec_encode_batch(c.codec, c.d_pay.as<uint8_t>(), c.d_len.as<int32_t>(), 0, R, c.d_cw.as<uint8_t>(),
                                           c.d_cwlen.as<int32_t>(), s))
                 return st;
-            hipLaunchKernelGGL(fec::fec_relay_vr_zero_kernel, dim3(fec::grid_rows(R)), dim3(256), 0, s,
-                               c.d_src.as<const int64_t>(), R, c.d_cw.as<uint8_t>(), c.CW);
+            const int ninst = static_cast<int>(c.starts.size());
+            const dim3 zgrid(static_cast<unsigned>(std::max(1, ninst)));
+            hipLaunchKernelGGL(fec::fec_relay_vr_zero_kernel, zgrid, dim3(256), 0, s, c.d_starts.as<const int64_t>(), ninst,
+                               c.d_cw.as<uint8_t>(), c.CW);
             FEC_HIP(hipGetLastError());
             if (r->type == 2) {
                 if (int st = c.d_flag.reserve(static_cast<size_t>(R))) return st;
@@ -472,8 +483,8 @@ int fec_relay_vr_run(fec_relay_vr* r, const uint8_t* d_payload, const uint8_t* h
                 if (int st = fec_swdf_relay_batch(c.sw, c.d_cw.as<uint8_t>(), c.CW, c.d_er1.as<uint8_t>(), R,
                                                   c.d_frames.as<uint8_t>(), nullptr, c.d_work.p, wb, s))
                     return st;
-                hipLaunchKernelGGL(fec::fec_relay_vr_zero_kernel, dim3(fec::grid_rows(R)), dim3(256), 0, s,
-                                   c.d_src.as<const int64_t>(), R, c.d_frames.as<uint8_t>(), c.F);
+                hipLaunchKernelGGL(fec::fec_relay_vr_zero_kernel, zgrid, dim3(256), 0, s, c.d_starts.as<const int64_t>(),
+                                   ninst, c.d_frames.as<uint8_t>(), c.F);
                 FEC_HIP(hipGetLastError());
                 if (int st = fec_swdf_destination_batch(c.sw, c.d_frames.as<uint8_t>(), c.d_er2.as<uint8_t>(), R,
                                                         c.d_out.as<uint8_t>(), c.d_flag.as<uint8_t>(), s))
@@ -483,8 +494,8 @@ int fec_relay_vr_run(fec_relay_vr* r, const uint8_t* d_payload, const uint8_t* h
                 if (int st = fec_sdswdf_relay_batch_starts(c.sd, c.d_cw.as<uint8_t>(), c.CW, c.h_er1.data(), R,
                                                            c.starts.data(), ns, c.d_frames.as<uint8_t>(), s))
                     return st;
-                hipLaunchKernelGGL(fec::fec_relay_vr_zero_kernel, dim3(fec::grid_rows(R)), dim3(256), 0, s,
-                                   c.d_src.as<const int64_t>(), R, c.d_frames.as<uint8_t>(), c.F);
+                hipLaunchKernelGGL(fec::fec_relay_vr_zero_kernel, zgrid, dim3(256), 0, s, c.d_starts.as<const int64_t>(),
+                                   ninst, c.d_frames.as<uint8_t>(), c.F);
                 FEC_HIP(hipGetLastError());
                 c.h_flag.resize(static_cast<size_t>(R));
                 if (int st = fec_sdswdf_destination_batch_starts(c.sd, c.d_frames.as<uint8_t>(), c.h_er2.data(), R,
@@ -495,15 +506,39 @@ int fec_relay_vr_run(fec_relay_vr* r, const uint8_t* d_payload, const uint8_t* h
             return static_cast<int>(FEC_OK);
         };
         if (r->type == 2) {
-            for (size_t ci = 0; ci < r->codes.size(); ++ci)
-                if (int st = run_code(ci)) return st;
+            // the codes' chains on kQueues streams (the device's hardware queues: more streams
+            // share them, and a chain queued behind another on one waits for it), longest first,
+            // each on the least loaded stream.  A chain's cost in microseconds (profiles/r06/r06q):
+            // about 60 for its six launches plus 2 per 1000 rows with the specialised relay kernels;
+            // about 250 whatever its rows without them (k < 4: the generic encoder and decoder, a
+            // few hundred rows on bin/erasure.bin).
+            std::vector<size_t> order(r->codes.size());
+            for (size_t i = 0; i < order.size(); ++i) order[i] = i;
+            auto cost = [&](size_t i) {
+                const fec::Code& c = *r->codes[i];
+                return c.k >= 4 ? 60 + c.R / 500 : 250 + c.R / 500;
+            };
+            std::stable_sort(order.begin(), order.end(), [&](size_t x, size_t y) { return cost(x) > cost(y); });
+            int64_t load[fec_relay_vr::kQueues] = {};
+            const bool per_code = std::getenv("FEC_RELAY_VR_PER_CODE") != nullptr;  // A/B: a stream per code
+            for (size_t ci : order) {
+                if (per_code) {
+                    if (int st = run_code(ci, r->st[ci])) return st;
+                    continue;
+                }
+                int q = 0;
+                for (int j = 1; j < std::min(nst, fec_relay_vr::kQueues); ++j)
+                    if (load[j] < load[q]) q = j;
+                load[q] += cost(ci);
+                if (int st = run_code(ci, r->st[q])) return st;
+            }
         } else {
             std::vector<int> status(r->codes.size(), FEC_OK);
             std::vector<std::thread> th;
             for (size_t ci = 0; ci < r->codes.size(); ++ci)
                 th.emplace_back([&, ci] {
                     try {
-                        status[ci] = run_code(ci);
+                        status[ci] = run_code(ci, r->st[ci]);
                     } catch (const std::bad_alloc&) {
                         status[ci] = FEC_ERR_NOMEM;
                     } catch (...) {

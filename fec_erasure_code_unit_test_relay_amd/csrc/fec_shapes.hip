@@ -12,7 +12,7 @@
 // results depend on x - tr, not on tr.  Two episodes with the same erasure shape (bit j = packet
 // tr+j erased) therefore have identical results at equal offsets.
 //
-// fec_episode_kernel (64 packets per lane, 4096 per wave):
+// fec_episode_kernel (16 packets per lane, 1024 per wave):
 //   * erased output packets -> `erased` (one atomic per wave), src_d[x] = 0;
 //   * each resync point tr found by a thread: the thread walks the episode (flags in 64-packet
 //     windows) to its shape and last erasure, and inserts keyable shapes (tr >= T, span < 64, not
@@ -88,7 +88,10 @@ __device__ __forceinline__ int wave_reserve(int n, int32_t* counter) {
 
 }  // namespace
 
-// One wave per workgroup, 64 packets per lane, 4096 per wave and pass.  Device-scope atomics are
+// One wave per workgroup, kLanePk = 16 packets per lane, 1024 per wave and pass: a wave's episode
+// rounds (one per resync point of its busiest lane, each a walk, a table probe and an append) are
+// at most 16 / (T + 2) + 1 instead of 64 / (T + 2) + 1, and the launch has four times the waves
+// (config 3, 360 000 packets: 88 waves of 4096 took 26 us).  Device-scope atomics are
 // performed beyond the XCDs' L2s and serialise per address, so a wave issues few of them: one for
 // its erased outputs, one 64-bit one per round for its replay and duplicate entries; the shape
 // table is probed with plain loads (a key never changes once set, so a stale line can only read
@@ -98,32 +101,28 @@ __global__ __launch_bounds__(64) void fec_episode_kernel(EpisodeArgs a) {
     const int lane = threadIdx.x;
     const int T = a.T;  // < 64 (host check): the look-back of a resync test fits one word
     const int64_t TS = int64_t(1) << a.tbits;
-    constexpr int64_t kPerWave = 64 * 64;
+    constexpr int kLanePk = 16;
+    constexpr int64_t kPerWave = 64 * kLanePk;
     unsigned long long* wd = reinterpret_cast<unsigned long long*>(a.counters + 6);  // (replayed, dups)
     phase_stamp(a.stamps, blockIdx.x, 0);
     for (int64_t w0 = static_cast<int64_t>(blockIdx.x) * kPerWave; w0 < a.P;
          w0 += static_cast<int64_t>(gridDim.x) * kPerWave) {
-        const int64_t t0 = w0 + lane * 64;
-        uint64_t m64 = 0;  // bit e: packet t0+e erased
-        if (t0 + 63 < a.P && (reinterpret_cast<uintptr_t>(a.er + t0) & 15) == 0) {
-            const uint4* p = reinterpret_cast<const uint4*>(a.er + t0);
-            uint4 v[4];
-#pragma unroll
-            for (int j = 0; j < 4; ++j) v[j] = p[j];
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                const uint64_t m16 = nz_bytes_mask(v[j].x) | (nz_bytes_mask(v[j].y) << 4) |
-                                     (nz_bytes_mask(v[j].z) << 8) | (nz_bytes_mask(v[j].w) << 12);
-                m64 |= m16 << (16 * j);
-            }
-        } else {
-            m64 = erasure_bits64(a.er, a.P, t0);
+        const int64_t t0 = w0 + lane * kLanePk;
+        uint64_t m64 = 0;  // bit e: packet t0+e erased (e < kLanePk)
+        if (t0 + kLanePk - 1 < a.P && (reinterpret_cast<uintptr_t>(a.er + t0) & 15) == 0) {
+            const uint4 v = *reinterpret_cast<const uint4*>(a.er + t0);
+            m64 = nz_bytes_mask(v.x) | (nz_bytes_mask(v.y) << 4) | (nz_bytes_mask(v.z) << 8) | (nz_bytes_mask(v.w) << 12);
+        } else if (t0 < a.P) {
+            m64 = erasure_bits64(a.er, a.P, t0) & ((uint64_t(1) << kLanePk) - 1u);
         }
         // resync points: erased t with no erasure in [t-T-1, t-1] (Decoder.cpp:80-83, 109-133)
         uint64_t resm = 0;
+        // packets t0-64 .. t0-1: the four lanes below (shuffled with every lane active) and, for
+        // lanes 0..3, the word in front of them
+        const uint64_t b1 = __shfl_up(m64, 1), b2 = __shfl_up(m64, 2), b3 = __shfl_up(m64, 3), b4 = __shfl_up(m64, 4);
         if (m64) {
-            const uint64_t before = __shfl_up(m64, 1);  // packets t0-64 .. t0-1 (lane 0: below)
-            const uint64_t bw = lane == 0 ? erasure_bits64(a.er, a.P, t0 - 64) : before;
+            const uint64_t bw = lane < 4 ? erasure_bits64(a.er, a.P, t0 - 64)
+                                         : (b4 | (b3 << 16) | (b2 << 32) | (b1 << 48));
             for (uint64_t rest = m64; rest; rest &= rest - 1) {
                 const int e = __builtin_ctzll(rest);
                 const int lo = e - T - 1;
@@ -136,7 +135,7 @@ __global__ __launch_bounds__(64) void fec_episode_kernel(EpisodeArgs a) {
         phase_stamp(a.stamps, blockIdx.x, 1);
         // erased outputs (src_d: own plan rows until the plan says otherwise)
         uint64_t outm = m64;
-        if (t0 + 64 > a.Pout) outm &= (t0 >= a.Pout) ? 0u : ((uint64_t(1) << (a.Pout - t0)) - 1u);
+        if (t0 + kLanePk > a.Pout) outm &= (t0 >= a.Pout) ? 0u : ((uint64_t(1) << (a.Pout - t0)) - 1u);
         int so = wave_reserve(__builtin_popcountll(outm), &a.counters[1]);
         for (uint64_t rest = outm; rest; rest &= rest - 1) {
             const int64_t x = t0 + __builtin_ctzll(rest);
