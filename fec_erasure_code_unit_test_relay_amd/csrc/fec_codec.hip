@@ -485,7 +485,12 @@ int launch_plan(fec_codec* c, const uint8_t* d_er, int64_t P, void* d_ws, size_t
     ea.keys = w.keys;
     ea.reps_tr = w.reps_tr;
     ea.stamps = (c->stamp_kernel == FEC_KERNEL_DEC_SCAN) ? c->d_stamps : nullptr;
-    const int64_t sblocks = std::min<int64_t>((P + 1023) / 1024, 32768);  // a wave per 1024 packets (fec_shapes.hip)
+    // a wave per 1024 packets (fec_shapes.hip), at most FEC_EPISODE_GRID waves (A/B switch)
+    // one wave per CU: beside the headline copy, 977 waves at 1 M packets took its CUs (0.3224 vs
+    // 0.3066 ms per step with 245; 384: 0.3000 - 0.3015 vs 0.2987 - 0.2992, profiles/r06/r06u, r06w)
+    int64_t egrid = 256;
+    if (const char* v = std::getenv("FEC_EPISODE_GRID")) egrid = std::max(1, std::atoi(v));
+    const int64_t sblocks = std::min<int64_t>((P + 1023) / 1024, egrid);
     hipLaunchKernelGGL(fec::fec_episode_kernel, dim3(static_cast<unsigned>(sblocks)), dim3(64), 0, s, ea);
     HIP_TRY(hipGetLastError());
     if (int st = c->end(stop, s)) return st;
@@ -692,6 +697,18 @@ int launch_recover(fec_codec* c, const uint8_t* d_cw, int64_t P, uint8_t* d_out,
 
 // Full decode on `s`: the erasure-only plan runs on the codec's side stream concurrently with the
 // systematic copy, joined before the recovery pass (fork/join through events, capturable).
+// FEC_RECOVER_BESIDE=1 (A/B switch, off by default): the recovery on the side stream behind the
+// planner chain, beside a copy that leaves the erased rows alone (the compaction zeroes the lost
+// ones).  Slower wherever it was measured: the headline step 0.3157 - 0.3163 vs 0.3103 - 0.3114 ms,
+// config 3 (360 000 packets, whose 56 us copy is shorter than the ~100 us chain) 0.1253 vs 0.1235 ms
+// per decode (profiles/r06/r06v, r06w; round 3: profiles/r03/r03y_recover_beside_ab.txt).
+bool recover_beside(const fec_codec* c, const uint8_t* d_out) {
+    // only the specialised copies leave erased rows alone (fec_copy_fast.hip, skip_erased)
+    if (!c->copy_fast || c->copy_path == 1 || (reinterpret_cast<uintptr_t>(d_out) & 3) != 0) return false;
+    const char* v = std::getenv("FEC_RECOVER_BESIDE");
+    return v && v[0] == '1';
+}
+
 int launch_decode(fec_codec* c, const uint8_t* d_cw, const uint8_t* d_er, int64_t P, uint8_t* d_out,
                   int32_t* d_outlen, void* d_ws, size_t ws_bytes, hipStream_t s) {
     if (P - c->g.T <= 0) return FEC_OK;
@@ -699,6 +716,14 @@ int launch_decode(fec_codec* c, const uint8_t* d_cw, const uint8_t* d_er, int64_
     HIP_TRY(hipEventRecord(c->ev_fork, s));
     HIP_TRY(hipStreamWaitEvent(c->side, c->ev_fork, 0));
     if (int st = launch_plan(c, d_er, P, d_ws, ws_bytes, c->side)) return st;
+    if (recover_beside(c, d_out)) {
+        if (int st = launch_compact(c, P, d_out, d_outlen, d_ws, ws_bytes, c->side, 0, true)) return st;
+        if (int st = launch_recover(c, d_cw, P, d_out, d_outlen, d_ws, ws_bytes, c->side, 0, true)) return st;
+        HIP_TRY(hipEventRecord(c->ev_join, c->side));
+        if (int st = launch_copy(c, d_cw, d_er, P, d_out, d_outlen, s, true)) return st;
+        HIP_TRY(hipStreamWaitEvent(s, c->ev_join, 0));
+        return FEC_OK;
+    }
     if (int st = launch_compact(c, P, d_out, d_outlen, d_ws, ws_bytes, c->side)) return st;
     HIP_TRY(hipEventRecord(c->ev_join, c->side));
     // The copy writes every row (erased ones as zero rows, length 0); the recovery overwrites the

@@ -316,68 +316,122 @@ void VrPlan::start_workers() {
     dpub_.store(0, std::memory_order_relaxed);
     dtake_.store(0, std::memory_order_relaxed);
     dfill_ = 0;
+    if (workers_.size() != nth) stop_pool();  // (first run, or another thread count)
     recs_.resize(nth);
     for (auto& r : recs_) r.clear();
     pending_ = true;
-    // pause-loop iterations a worker polls for work before sleeping (FEC_VR_SPIN; 0: sleep at once)
-    int spin_max = 4096;
-    if (const char* e = std::getenv("FEC_VR_SPIN")) spin_max = std::max(0, std::atoi(e));
-    for (size_t w = 0; w < nth; ++w) {
-        workers_.emplace_back([this, w, spin_max, home = t_pin_home] {
-            vr_pin_near(home);
-            auto decoder_ready = [&] { return dtake_.load(std::memory_order_relaxed) < dpub_.load(std::memory_order_acquire); };
-            for (;;) {
-                // the mutex queue first: feedback runs (queued before any decoder job) and the rate sum
-                if (qsize_.load(std::memory_order_acquire) > 0) {
-                    DecJob j;
-                    bool got = false;
+    {
+        std::lock_guard<std::mutex> lk(pmu_);
+        pool_quit_ = false;
+        pool_set_ = grp;
+        pool_active_ = static_cast<int>(nth);
+        ++pool_epoch_;
+    }
+    if (workers_.empty()) {
+        for (size_t w = 0; w < nth; ++w)
+            workers_.emplace_back([this, w] {
+                uint64_t seen = 0;
+                cpu_set_t pinned;
+                CPU_ZERO(&pinned);
+                for (;;) {
+                    cpu_set_t set;
                     {
-                        std::lock_guard<std::mutex> lk(qmu_);
-                        if (!q_.empty()) {
-                            j = std::move(q_.front());
-                            q_.pop_front();
-                            qsize_.store(static_cast<int64_t>(q_.size()), std::memory_order_release);
-                            got = true;
-                        }
+                        std::unique_lock<std::mutex> lk(pmu_);
+                        pcv_.wait(lk, [&] { return pool_quit_ || pool_epoch_ != seen; });
+                        if (pool_quit_) return;
+                        seen = pool_epoch_;
+                        set = pool_set_;
                     }
-                    if (got) {
-                        if (j.id <= -2) {  // feedback jobs of run -2 - id, in order
-                            const int64_t c = -2 - static_cast<int64_t>(j.id), nj = static_cast<int64_t>(fb_jobs_.size());
-                            const int64_t ch = static_cast<int64_t>(fb_chunk_);
-                            for (int64_t jf = c * ch; jf < std::min(nj, (c + 1) * ch); ++jf) feedback_job(jf, fb_T_, fb_mds_);
-                        } else {  // final_sum_coding_rate, one float add per packet in sending order
-                            float sum = 0;
-                            for (const RateRun& r : rate_runs) sum = float_add_repeated(sum, r.rate, r.count);
-                            sum_coding_rate = sum;
-                        }
-                        continue;
+                    // on the control loop's group (a sparse one -- fewer than 4 CPUs: taskset,
+                    // cgroup -- is left alone, as vr_pin_near does)
+                    if (!CPU_EQUAL(&set, &pinned) && CPU_COUNT(&set) >= 4) {
+                        (void)pthread_setaffinity_np(pthread_self(), sizeof(set), &set);
+                        pinned = set;
                     }
+                    worker_run(w);
+                    std::lock_guard<std::mutex> lk(pmu_);
+                    if (--pool_active_ == 0) pdone_.notify_all();
                 }
-                // a decoder instance, claimed lock-free
-                int64_t t = dtake_.load(std::memory_order_relaxed);
-                if (t < dpub_.load(std::memory_order_acquire)) {
-                    if (dtake_.compare_exchange_weak(t, t + 1, std::memory_order_acq_rel, std::memory_order_relaxed))
-                        decode_instance(dslot(t), recs_[w]);
-                    continue;
+            });
+    } else {
+        pcv_.notify_all();
+    }
+}
+
+void VrPlan::stop_pool() {
+    {
+        std::lock_guard<std::mutex> lk(pmu_);
+        pool_quit_ = true;
+    }
+    pcv_.notify_all();
+    for (auto& th : workers_) th.join();
+    workers_.clear();
+}
+
+VrPlan::~VrPlan() {
+    finish();
+    stop_pool();
+}
+
+// One run's jobs on worker w: feedback runs and the rate sum from the mutex queue, decoder
+// instances claimed lock-free, until the control loop has closed the queue and every job is taken.
+void VrPlan::worker_run(size_t w) {
+    // pause-loop iterations a worker polls for work before sleeping (FEC_VR_SPIN; 0: sleep at once)
+    static const int spin_max = [] {
+        const char* e = std::getenv("FEC_VR_SPIN");
+        return e ? std::max(0, std::atoi(e)) : 4096;
+    }();
+    auto decoder_ready = [&] { return dtake_.load(std::memory_order_relaxed) < dpub_.load(std::memory_order_acquire); };
+    for (;;) {
+        // the mutex queue first: feedback runs (queued before any decoder job) and the rate sum
+        if (qsize_.load(std::memory_order_acquire) > 0) {
+            DecJob j;
+            bool got = false;
+            {
+                std::lock_guard<std::mutex> lk(qmu_);
+                if (!q_.empty()) {
+                    j = std::move(q_.front());
+                    q_.pop_front();
+                    qsize_.store(static_cast<int64_t>(q_.size()), std::memory_order_release);
+                    got = true;
                 }
-                // nothing: poll for a while (a job comes every ~0.5 us while the control loop runs),
-                // then sleep on the condition variable
-                bool any = false;
-                for (int spin = 0; spin < spin_max && !any; ++spin) {
-                    any = qsize_.load(std::memory_order_acquire) > 0 || decoder_ready() ||
-                          qclosed_flag_.load(std::memory_order_acquire);
-                    if (!any) __builtin_ia32_pause();
-                }
-                std::unique_lock<std::mutex> lk(qmu_);
-                auto ready = [&] { return !q_.empty() || qclosed_ || decoder_ready(); };
-                if (!ready()) {
-                    sleepers_.fetch_add(1, std::memory_order_seq_cst);
-                    qcv_.wait(lk, ready);
-                    sleepers_.fetch_sub(1, std::memory_order_relaxed);
-                }
-                if (q_.empty() && qclosed_ && !decoder_ready()) break;  // closed: every job published is taken
             }
-        });
+            if (got) {
+                if (j.id <= -2) {  // feedback jobs of run -2 - id, in order
+                    const int64_t c = -2 - static_cast<int64_t>(j.id), nj = static_cast<int64_t>(fb_jobs_.size());
+                    const int64_t ch = static_cast<int64_t>(fb_chunk_);
+                    for (int64_t jf = c * ch; jf < std::min(nj, (c + 1) * ch); ++jf) feedback_job(jf, fb_T_, fb_mds_);
+                } else {  // final_sum_coding_rate, one float add per packet in sending order
+                    float sum = 0;
+                    for (const RateRun& r : rate_runs) sum = float_add_repeated(sum, r.rate, r.count);
+                    sum_coding_rate = sum;
+                }
+                continue;
+            }
+        }
+        // a decoder instance, claimed lock-free
+        int64_t t = dtake_.load(std::memory_order_relaxed);
+        if (t < dpub_.load(std::memory_order_acquire)) {
+            if (dtake_.compare_exchange_weak(t, t + 1, std::memory_order_acq_rel, std::memory_order_relaxed))
+                decode_instance(dslot(t), recs_[w]);
+            continue;
+        }
+        // nothing: poll for a while (a job comes every ~0.5 us while the control loop runs),
+        // then sleep on the condition variable
+        bool any = false;
+        for (int spin = 0; spin < spin_max && !any; ++spin) {
+            any = qsize_.load(std::memory_order_acquire) > 0 || decoder_ready() ||
+                  qclosed_flag_.load(std::memory_order_acquire);
+            if (!any) __builtin_ia32_pause();
+        }
+        std::unique_lock<std::mutex> lk(qmu_);
+        auto ready = [&] { return !q_.empty() || qclosed_ || decoder_ready(); };
+        if (!ready()) {
+            sleepers_.fetch_add(1, std::memory_order_seq_cst);
+            qcv_.wait(lk, ready);
+            sleepers_.fetch_sub(1, std::memory_order_relaxed);
+        }
+        if (q_.empty() && qclosed_ && !decoder_ready()) return;  // closed: every job published is taken
     }
 }
 
@@ -432,8 +486,10 @@ void VrPlan::close_jobs() {
 void VrPlan::finish() {
     if (!pending_) return;
     close_jobs();
-    for (auto& th : workers_) th.join();
-    workers_.clear();
+    {
+        std::unique_lock<std::mutex> lk(pmu_);
+        pdone_.wait(lk, [&] { return pool_active_ == 0; });
+    }
     pending_ = false;
     lost = std::count(fate.begin(), fate.end(), static_cast<uint8_t>(kLost));
     // recovered packets in x order (each worker's list is in its own job order)
@@ -722,13 +778,17 @@ void VrPlan::control(const uint8_t* pattern, int64_t n_pattern, int T, int B, in
     const bool fb_thread_on = !fb_sync && std::getenv("FEC_VR_FB_THREAD") != nullptr;
     fb_T_ = T;
     fb_mds_ = mds;
-    std::thread fb_thread([this, T, mds, fb_thread_on, home = t_pin_home] {
-        vr_pin_near(home);
-        if (fb_thread_on) feedback_run(T, mds);
-    });
+    std::thread fb_thread;  // (only for FEC_VR_FB_THREAD=1)
+    if (fb_thread_on)
+        fb_thread = std::thread([this, T, mds, home = t_pin_home] {
+            vr_pin_near(home);
+            feedback_run(T, mds);
+        });
     struct Joiner {
         std::thread& t;
-        ~Joiner() { t.join(); }
+        ~Joiner() {
+            if (t.joinable()) t.join();
+        }
     } fb_join{fb_thread};
     FbCursor fb(*this);
     const auto tc1 = std::chrono::steady_clock::now();

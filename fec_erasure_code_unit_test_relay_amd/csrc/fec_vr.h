@@ -26,6 +26,7 @@
 #include <map>
 #include <memory>
 #include <mutex>
+#include <sched.h>
 #include <thread>
 #include <utility>
 #include <vector>
@@ -142,7 +143,7 @@ struct VrPlan {
     VrPlan() = default;
     VrPlan(const VrPlan&) = delete;
     VrPlan& operator=(const VrPlan&) = delete;
-    ~VrPlan() { finish(); }
+    ~VrPlan();
 
     // Runs the loop until the receiver has processed seq P+T-1 (application_local_simulation.cpp:813).
     // B_init = N_init = -1: adaptive (the sender starts at (T, 0, 0)).  Re-running one plan reuses
@@ -204,7 +205,20 @@ private:
     const DecodeRules& rules_for(int T, int B, int N);
     std::vector<std::vector<Reports>> reps_;                   // the control loop's per-instance lists
     std::vector<const DecodeRules*> drules_;
+    // The worker pool lives as long as the plan: a run hands it a new epoch (one wake-up per
+    // worker) instead of creating and joining threads (~0.1 ms per run on the control loop and as
+    // much again at finish()); pool_active_ counts the workers still inside the current run.
     std::vector<std::thread> workers_;
+    std::mutex pmu_;
+    std::condition_variable pcv_, pdone_;
+    uint64_t pool_epoch_ = 0;      // (pmu_) bumped by each run's start_workers
+    int pool_active_ = 0;          // (pmu_) workers not yet done with the current epoch
+    cpu_set_t pool_set_;           // (pmu_) the CPUs the workers of this epoch run on (the control
+                                   // loop's group, taken in its context: a worker's own affinity is
+                                   // the previous run's group)
+    bool pool_quit_ = false;       // (pmu_) the destructor's
+    void worker_run(size_t w);     // one epoch's jobs (until the queue is closed and drained)
+    void stop_pool();
     std::vector<std::vector<RecEntry>> recs_;  // per worker
     std::mutex qmu_;
     std::condition_variable qcv_;

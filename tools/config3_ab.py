@@ -1,6 +1,6 @@
 """In-process A/B of BASELINE config 3's decode (device-resident, (10,5,2), 360 000 packets of
 bin/erasure.bin) over environment switches the library reads per launch, alternating variants:
-    python tools/config3_ab.py FEC_PLAN_GRID=1024 FEC_PLAN_GRID=4096 [rounds]"""
+    python tools/config3_ab.py FEC_PLAN_GRID=1024 FEC_PLAN_GRID=4096,FEC_X=1 [rounds]"""
 import os
 import statistics
 import sys
@@ -28,8 +28,9 @@ c.workspace(P + 10)
 res = {a: [] for a in args}
 for _ in range(rounds):
     for a in args:
-        k, v = a.split("=", 1)
-        os.environ[k] = v
+        for kv in a.split(","):  # K=V[,K2=V2]: every variant names all its switches
+            k, v = kv.split("=", 1)
+            os.environ[k] = v
         for _ in range(3):
             c.decode(cw, er, out=out, out_len=ol)
         torch.cuda.synchronize()
