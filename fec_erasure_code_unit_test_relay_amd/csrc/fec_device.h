@@ -38,6 +38,30 @@ __device__ __forceinline__ uint32_t gather4(const uint32_t (&src)[NW], int i0, i
     return lo | hi;
 }
 
+// 1 + the index of the last non-zero byte of row[0, n) (0 if all are zero), row anywhere in LDS or
+// memory with row - 16 readable: 16 bytes per step from the end as four aligned dwords, bytes
+// outside the row masked off (a byte loop took CW dependent reads per all-zero row: the adaptive
+// relay's zero-length gap rows made its encoders 2.3 - 3.6x slower, profiles/r06/enc_rl_probe.txt).
+__device__ __forceinline__ int last_nonzero_end(const uint8_t* row, int n) {
+    const uintptr_t s0 = reinterpret_cast<uintptr_t>(row), s1 = s0 + static_cast<uintptr_t>(n);
+    uintptr_t a = (s1 + 3) & ~uintptr_t(3);  // one past the last dword touching the row
+    while (a > s0) {
+        uint32_t w[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) w[q] = *reinterpret_cast<const uint32_t*>(a - 4 * (q + 1));
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const uintptr_t d = a - 4 * (q + 1);  // the dword's first byte
+            uint32_t v = w[q];
+            if (d + 4 > s1) v &= 0xffffffffu >> (8 * static_cast<int>(d + 4 - s1));  // bytes past the row
+            if (d < s0) v = d + 4 <= s0 ? 0u : v & ~((1u << (8 * static_cast<int>(s0 - d))) - 1u);  // before it
+            if (v) return static_cast<int>(static_cast<intptr_t>(d - s0)) + (31 - __builtin_clz(v)) / 8 + 1;
+        }
+        a -= 16;
+    }
+    return 0;
+}
+
 __device__ __forceinline__ uint32_t keep_bytes(int c) {  // mask of the low c bytes (c clamped)
     return c <= 0 ? 0u : (c >= 4 ? 0xffffffffu : ((1u << (8 * c)) - 1u));
 }

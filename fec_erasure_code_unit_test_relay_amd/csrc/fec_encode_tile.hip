@@ -610,14 +610,22 @@ __device__ __forceinline__ void tile_walk(const EncTileArgs& a, uint8_t* smem) {
             const uint8_t* cwp = out + (own ? tid : 0) * CW;
             const bool zlast = cwp[CW - 1] == 0;
             int sz = CW;
-            if (__builtin_amdgcn_ballot_w64(own && zlast)) {  // rare: a codeword ending in zero bytes
+            if (__builtin_amdgcn_ballot_w64(own && zlast)) {  // a codeword ending in zero bytes
                 if (own && zlast) {
-                    sz = 0;
-                    for (int b = CW - 2; b >= 0; --b)
-                        if (cwp[b] != 0) {
-                            sz = b + 1;
-                            break;
-                        }
+                    if constexpr (LC == 0) {
+                        // the runtime-L kernels (the adaptive relay's codes, whose zero-length gap
+                        // rows are all-zero codewords): 16 bytes a step
+                        sz = last_nonzero_end(cwp, CW - 1);
+                    } else {
+                        // byte by byte: the scan above inlined here made the L = 300 headline
+                        // kernel 137 -> 230 us (registers; profiles/r06/r06z_encoder_scan.txt)
+                        sz = 0;
+                        for (int b = CW - 2; b >= 0; --b)
+                            if (cwp[b] != 0) {
+                                sz = b + 1;
+                                break;
+                            }
+                    }
                 }
             }
             __builtin_amdgcn_raw_buffer_store_b32(static_cast<uint32_t>(sz), rw, own ? 4 * (row0 + tid) : 0x7ffffff0,

@@ -138,9 +138,7 @@ __global__ __launch_bounds__(256) void fec_encode_kernel(EncArgs a) {
     }
     for (int tl = tid; tl < ntile; tl += 256) {
         const uint8_t* row = xout + tl * a.CW;
-        int z = a.CW - 1;
-        while (z >= 0 && row[z] == 0) --z;
-        a.cw_len[t0 + tl] = z + 1;
+        a.cw_len[t0 + tl] = row[a.CW - 1] ? a.CW : last_nonzero_end(row, a.CW - 1);
     }
 }
 
