@@ -46,6 +46,8 @@ struct RvTupleDev {             // one code's batch buffers, for the gather kern
     const uint8_t* flag;        // per row: the destination's loss flag (type 2; null for type 3)
     int F, part, hdr;           // frame row bytes, part bytes (from byte 2), of which header bytes (11 / 0)
     int ostride, outb;          // out row bytes, bytes reported
+    const uint8_t* frames_end;  // one past the frames buffer (R rows of F bytes)
+    const uint8_t* out_end;     // one past the out buffer (R rows of ostride bytes)
 };
 struct RvGatherArgs {
     RvTupleDev tup[kMaxCodes];
@@ -100,6 +102,66 @@ __device__ __forceinline__ void copy_run(uint8_t* dst, int doff, const uint8_t* 
     }
 }
 
+// A frame without an old part is its code's frame row verbatim but for the BE16 size in front
+// (Variable_Rate_FEC_Decoder.cpp:1502-1571): F bytes from any byte of the code's rows to a 16-byte
+// aligned row, a lane per 16-byte chunk -- the two aligned source chunks that cover it, shifted --
+// where copy_run takes two dword loads and a store per dword.  A lane whose second source chunk would
+// pass the buffer's end reads bytes.  Bytes past F in the last chunk (the next row's) land in the
+// destination row's padding, past frame_len.
+__device__ __forceinline__ uint32_t keep_low(int c) { return c >= 4 ? 0xffffffffu : (1u << (8 * c)) - 1u; }
+
+// The 16 bytes at s0 (any alignment): the two aligned chunks that cover them, shifted; bytes where
+// the second chunk would pass src_end one by one.
+__device__ __forceinline__ void load16_any(const uint8_t* s0, const uint8_t* src_end, uint32_t (&o)[4]) {
+    const uintptr_t A = reinterpret_cast<uintptr_t>(s0) & ~uintptr_t(15);
+    const int sh = static_cast<int>(reinterpret_cast<uintptr_t>(s0) - A);
+    if (reinterpret_cast<const uint8_t*>(A) + 32 <= src_end) {
+        const uint4 lo = *reinterpret_cast<const uint4*>(A), hi = *reinterpret_cast<const uint4*>(A + 16);
+        const uint32_t w[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
+        const int q = sh >> 2;
+        const uint32_t r = static_cast<uint32_t>(sh & 3);
+        uint32_t x[5];
+#pragma unroll
+        for (int k = 0; k < 5; ++k) x[k] = q == 0 ? w[k] : q == 1 ? w[k + 1] : q == 2 ? w[k + 2] : w[k + 3];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) o[j] = r ? __builtin_amdgcn_alignbyte(x[j + 1], x[j], r) : x[j];
+    } else {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            o[j] = 0;
+            for (int e = 0; e < 4; ++e)
+                if (s0 + 4 * j + e < src_end) o[j] |= static_cast<uint32_t>(s0[4 * j + e]) << (8 * e);
+        }
+    }
+}
+
+__device__ __forceinline__ void copy_row16(uint8_t* dst, const uint8_t* src, int n, const uint8_t* src_end,
+                                           int size, int lane) {
+    for (int c = lane; 16 * c < n; c += 64) {
+        uint32_t o[4];
+        load16_any(src + 16 * c, src_end, o);
+        if (c == 0) o[0] = (o[0] & 0xffff0000u) | static_cast<uint32_t>(size / 256) | (static_cast<uint32_t>(size % 256) << 8);
+        *reinterpret_cast<uint4*>(dst + 16 * c) = make_uint4(o[0], o[1], o[2], o[3]);
+    }
+}
+
+// The reported row: bytes [0, n) of src, zero up to `stride` (a multiple of 4, dst 4-byte aligned),
+// a lane per 16 bytes read as two aligned chunks, written as dwords.
+__device__ __forceinline__ void copy_out16(uint8_t* dst, const uint8_t* src, int n, int stride, const uint8_t* src_end,
+                                           int lane) {
+    for (int c = lane; 16 * c < stride; c += 64) {
+        uint32_t o[4] = {0u, 0u, 0u, 0u};
+        if (16 * c < n) load16_any(src + 16 * c, src_end, o);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int b = 16 * c + 4 * j;
+            if (b >= stride) break;
+            const uint32_t v = b + 4 <= n ? o[j] : (b >= n ? 0u : o[j] & keep_low(n - b));
+            *reinterpret_cast<uint32_t*>(dst + b) = v;
+        }
+    }
+}
+
 // A wave per seq: the frame [BE16 size of the new part's code bytes][new part][old part] and the
 // reporting destination's row (its blocks*k bytes, zero after), copied a dword per lane (frame rows
 // and output rows are 4-byte aligned; the parts' sources are at any byte).  (Eight seqs per wave,
@@ -114,13 +176,15 @@ __global__ __launch_bounds__(256) void fec_relay_vr_gather_kernel(RvGatherArgs a
         uint8_t* fr = a.frames + t * a.fstride;
         const uint8_t* pn = tn.frames + static_cast<int64_t>(m[1]) * tn.F + 2;
         const int size_cur = tn.part - tn.hdr;  // the new code's codeword_r_d_size (:997-999, :1502-1571)
-        if (lane == 0) {
-            fr[0] = static_cast<uint8_t>(size_cur / 256);
-            fr[1] = static_cast<uint8_t>(size_cur % 256);
-        }
-        copy_run(fr, 2, pn, tn.part, lane);
         int len = 2 + tn.part;
-        if (m[2] >= 0) {
+        if (m[2] < 0) {  // no old part: the row as it is, its size in front
+            copy_row16(fr, pn - 2, len, tn.frames_end, size_cur, lane);
+        } else {
+            if (lane == 0) {
+                fr[0] = static_cast<uint8_t>(size_cur / 256);
+                fr[1] = static_cast<uint8_t>(size_cur % 256);
+            }
+            copy_run(fr, 2, pn, tn.part, lane);
             const RvTupleDev& to = a.tup[m[2]];
             const uint8_t* po = to.frames + static_cast<int64_t>(m[3]) * to.F + 2;
             copy_run(fr + (len & ~3), len & 3, po, to.part, lane);
@@ -130,8 +194,7 @@ __global__ __launch_bounds__(256) void fec_relay_vr_gather_kernel(RvGatherArgs a
         const RvTupleDev& tr = a.tup[m[4]];
         const uint8_t* src = tr.out + static_cast<int64_t>(m[5]) * tr.ostride;
         uint8_t* dst = a.out + t * a.out_stride;
-        copy_run(dst, 0, src, tr.outb, lane);
-        for (int b = tr.outb + lane; b < a.out_stride; b += 64) dst[b] = 0;
+        copy_out16(dst, src, tr.outb, static_cast<int>(a.out_stride), tr.out_end, lane);
         if (a.flag && lane == 0) a.flag[t] = tr.flag[m[5]];
     }
 }
@@ -565,7 +628,8 @@ int fec_relay_vr_run(fec_relay_vr* r, const uint8_t* d_payload, const uint8_t* h
             const fec::Code& c = *r->codes[i];
             a.tup[i] = {c.d_frames.as<const uint8_t>(), c.d_out.as<const uint8_t>(),
                         r->type == 2 ? c.d_flag.as<const uint8_t>() : nullptr, c.F, c.part, r->type == 3 ? 11 : 0,
-                        c.ostride, c.outb};
+                        c.ostride, c.outb, c.d_frames.as<const uint8_t>() + c.R * static_cast<int64_t>(c.F),
+                        c.d_out.as<const uint8_t>() + c.R * static_cast<int64_t>(c.ostride)};
         }
         a.map = r->d_map.as<const int32_t>();
         a.P = r->P;
