@@ -479,7 +479,12 @@ int fec_relay_vr_run(fec_relay_vr* r, const uint8_t* d_payload, const uint8_t* h
             FEC_HIP(hipMemcpyAsync(r->d_e2.p, r->h_pin + P, P, hipMemcpyHostToDevice, caller));
         }
         FEC_HIP(hipEventRecord(r->ev_fork, caller));
-        const int nst = std::min<int>(fec_relay_vr::kStreams, static_cast<int>(r->codes.size()));
+        // the streams this run uses: type 2's chains go to kQueues of them, type 3's codes one each (the
+        // fork, the join and the drain touch only these: joining idle streams too cost the gather's
+        // start ~60 us behind the last chain, profiles/r06/r06zd_*)
+        const bool per_code = r->type == 3 || std::getenv("FEC_RELAY_VR_PER_CODE") != nullptr;  // (A/B for type 2)
+        const int nst = std::min<int>(per_code ? fec_relay_vr::kStreams : fec_relay_vr::kQueues,
+                                      static_cast<int>(r->codes.size()));
         // any return before the join below (an error) drains the side streams first: otherwise the
         // caller's stream is not ordered after their work and the next run could rewrite buffers
         // those kernels still read
@@ -583,14 +588,13 @@ int fec_relay_vr_run(fec_relay_vr* r, const uint8_t* d_payload, const uint8_t* h
             };
             std::stable_sort(order.begin(), order.end(), [&](size_t x, size_t y) { return cost(x) > cost(y); });
             int64_t load[fec_relay_vr::kQueues] = {};
-            const bool per_code = std::getenv("FEC_RELAY_VR_PER_CODE") != nullptr;  // A/B: a stream per code
             for (size_t ci : order) {
                 if (per_code) {
                     if (int st = run_code(ci, r->st[ci])) return st;
                     continue;
                 }
                 int q = 0;
-                for (int j = 1; j < std::min(nst, fec_relay_vr::kQueues); ++j)
+                for (int j = 1; j < nst; ++j)
                     if (load[j] < load[q]) q = j;
                 load[q] += cost(ci);
                 if (int st = run_code(ci, r->st[q])) return st;
