@@ -39,6 +39,7 @@ namespace {
 constexpr int kTT = 10;         // T_TOT (FEC_Macro.h)
 constexpr int kGap = 3 * kTT + 3;  // zero rows in front of an instance (>= every window's reach)
 constexpr int kMaxCodes = 16;
+constexpr int kGatherLanes = 32;  // lanes per seq in the gather (64: 340 us, 32: 207 us, 16: 210 us; r06ze, r06zf)
 
 struct RvTupleDev {             // one code's batch buffers, for the gather kernel
     const uint8_t* frames;      // rows of F bytes
@@ -66,15 +67,16 @@ struct RvGatherArgs {
 // copies are short: their load latency, not bandwidth, is the cost): two source dword loads (the
 // source's own alignment) and v_alignbyte for an interior dword, byte loads at the run's two ends
 // (the neighbouring bytes belong to other fields).
+template <int NL>  // lanes per run
 __device__ __forceinline__ void copy_run(uint8_t* dst, int doff, const uint8_t* src, int n, int lane) {
     const int nd = (doff + n + 3) >> 2;  // destination dwords touched
     const uintptr_t sa = reinterpret_cast<uintptr_t>(src);
-    for (int w0 = 0; w0 < nd; w0 += 256) {
+    for (int w0 = 0; w0 < nd; w0 += 4 * NL) {
         uint32_t v[4];
         bool whole[4];
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-            const int w = w0 + lane + 64 * i;
+            const int w = w0 + lane + NL * i;
             const int b0 = 4 * w - doff;  // source byte of the dword's first byte
             const uint32_t sh = static_cast<uint32_t>((sa + b0) & 3);
             // both aligned source dwords inside the run (no read past its last byte)
@@ -88,7 +90,7 @@ __device__ __forceinline__ void copy_run(uint8_t* dst, int doff, const uint8_t* 
         }
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-            const int w = w0 + lane + 64 * i;
+            const int w = w0 + lane + NL * i;
             if (whole[i]) {
                 *reinterpret_cast<uint32_t*>(dst + 4 * w) = v[i];
             } else if (w < nd) {
@@ -135,9 +137,10 @@ __device__ __forceinline__ void load16_any(const uint8_t* s0, const uint8_t* src
     }
 }
 
+template <int NL>
 __device__ __forceinline__ void copy_row16(uint8_t* dst, const uint8_t* src, int n, const uint8_t* src_end,
                                            int size, int lane) {
-    for (int c = lane; 16 * c < n; c += 64) {
+    for (int c = lane; 16 * c < n; c += NL) {
         uint32_t o[4];
         load16_any(src + 16 * c, src_end, o);
         if (c == 0) o[0] = (o[0] & 0xffff0000u) | static_cast<uint32_t>(size / 256) | (static_cast<uint32_t>(size % 256) << 8);
@@ -147,9 +150,10 @@ __device__ __forceinline__ void copy_row16(uint8_t* dst, const uint8_t* src, int
 
 // The reported row: bytes [0, n) of src, zero up to `stride` (a multiple of 4, dst 4-byte aligned),
 // a lane per 16 bytes read as two aligned chunks, written as dwords.
+template <int NL>
 __device__ __forceinline__ void copy_out16(uint8_t* dst, const uint8_t* src, int n, int stride, const uint8_t* src_end,
                                            int lane) {
-    for (int c = lane; 16 * c < stride; c += 64) {
+    for (int c = lane; 16 * c < stride; c += NL) {
         uint32_t o[4] = {0u, 0u, 0u, 0u};
         if (16 * c < n) load16_any(src + 16 * c, src_end, o);
 #pragma unroll
@@ -162,40 +166,49 @@ __device__ __forceinline__ void copy_out16(uint8_t* dst, const uint8_t* src, int
     }
 }
 
-// A wave per seq: the frame [BE16 size of the new part's code bytes][new part][old part] and the
-// reporting destination's row (its blocks*k bytes, zero after), copied a dword per lane (frame rows
-// and output rows are 4-byte aligned; the parts' sources are at any byte).  (Eight seqs per wave,
-// their map entries loaded at once, was slower: 489 vs 403 us; a wave per (seq, row) -- the frame
-// and the reported row on two waves -- too: 518 vs 476 us, profiles/r06/r06s.)
+// Half a wave (kGatherLanes) per seq: the frame [BE16 size of the new part's code bytes][new part][old part] and
+// the reporting destination's row (its blocks*k bytes, zero after).  Frame rows and output rows are
+// 4-byte aligned, the parts' sources at any byte; a frame without an old part (97 % of the seqs) is
+// its code's row verbatim but for the size in front, copied 16 bytes a lane (copy_row16), the
+// reported row likewise (copy_out16), and a double-coded frame a dword a lane (copy_run).  A frame
+// of the fast codes is 27 - 54 such chunks and a reported row 21: a whole wave per seq left most of
+// its lanes idle (207 vs 340 us per 360 000 seqs, profiles/r06/r06ze).  (Before: eight seqs per wave
+// with their map entries loaded at once was slower, 489 vs 403 us; a wave per (seq, row) too, 518 vs
+// 476 us, r06s; every load of a seq's three runs before their stores too, 620 vs 476 us, r06za.)
 __global__ __launch_bounds__(256) void fec_relay_vr_gather_kernel(RvGatherArgs a) {
-    const int lane = threadIdx.x & 63;
-    for (int64_t t = static_cast<int64_t>(blockIdx.x) * 4 + (threadIdx.x >> 6); t < a.P;
-         t += static_cast<int64_t>(gridDim.x) * 4) {
+    __shared__ RvTupleDev stup[kMaxCodes];  // per-lane indices into the tuples: from LDS
+    if (threadIdx.x < kMaxCodes) stup[threadIdx.x] = a.tup[threadIdx.x];
+    __syncthreads();
+    constexpr int NL = kGatherLanes, SPB = 256 / NL;  // lanes per seq, seqs per workgroup and pass
+    const int lane = threadIdx.x & (NL - 1);
+    const int64_t slot = static_cast<int64_t>(blockIdx.x) * SPB + threadIdx.x / NL;
+    for (int64_t t = slot; t < a.P; t += static_cast<int64_t>(gridDim.x) * SPB) {
         const int32_t* m = a.map + 6 * t;
-        const RvTupleDev& tn = a.tup[m[0]];
+        const int m0 = m[0], m1 = m[1], m2 = m[2], m3 = m[3], m4 = m[4], m5 = m[5];
+        const RvTupleDev& tn = stup[m0];
         uint8_t* fr = a.frames + t * a.fstride;
-        const uint8_t* pn = tn.frames + static_cast<int64_t>(m[1]) * tn.F + 2;
+        const uint8_t* pn = tn.frames + static_cast<int64_t>(m1) * tn.F + 2;
         const int size_cur = tn.part - tn.hdr;  // the new code's codeword_r_d_size (:997-999, :1502-1571)
         int len = 2 + tn.part;
-        if (m[2] < 0) {  // no old part: the row as it is, its size in front
-            copy_row16(fr, pn - 2, len, tn.frames_end, size_cur, lane);
+        if (m2 < 0) {  // no old part: the row as it is, its size in front
+            copy_row16<NL>(fr, pn - 2, len, tn.frames_end, size_cur, lane);
         } else {
             if (lane == 0) {
                 fr[0] = static_cast<uint8_t>(size_cur / 256);
                 fr[1] = static_cast<uint8_t>(size_cur % 256);
             }
-            copy_run(fr, 2, pn, tn.part, lane);
-            const RvTupleDev& to = a.tup[m[2]];
-            const uint8_t* po = to.frames + static_cast<int64_t>(m[3]) * to.F + 2;
-            copy_run(fr + (len & ~3), len & 3, po, to.part, lane);
+            copy_run<NL>(fr, 2, pn, tn.part, lane);
+            const RvTupleDev& to = stup[m2];
+            const uint8_t* po = to.frames + static_cast<int64_t>(m3) * to.F + 2;
+            copy_run<NL>(fr + (len & ~3), len & 3, po, to.part, lane);
             len += to.part;
         }
         if (lane == 0) a.frame_len[t] = len;
-        const RvTupleDev& tr = a.tup[m[4]];
-        const uint8_t* src = tr.out + static_cast<int64_t>(m[5]) * tr.ostride;
+        const RvTupleDev& tr = stup[m4];
+        const uint8_t* src = tr.out + static_cast<int64_t>(m5) * tr.ostride;
         uint8_t* dst = a.out + t * a.out_stride;
-        copy_out16(dst, src, tr.outb, static_cast<int>(a.out_stride), tr.out_end, lane);
-        if (a.flag && lane == 0) a.flag[t] = tr.flag[m[5]];
+        copy_out16<NL>(dst, src, tr.outb, static_cast<int>(a.out_stride), tr.out_end, lane);
+        if (a.flag && lane == 0) a.flag[t] = tr.flag[m5];
     }
 }
 
@@ -643,7 +656,7 @@ int fec_relay_vr_run(fec_relay_vr* r, const uint8_t* d_payload, const uint8_t* h
         a.out = d_out;
         a.out_stride = r->ostride;
         a.flag = r->type == 2 ? r->d_flag.as<uint8_t>() : nullptr;
-        hipLaunchKernelGGL(fec::fec_relay_vr_gather_kernel, dim3(fec::grid_rows(r->P)), dim3(256), 0, s, a);
+        hipLaunchKernelGGL(fec::fec_relay_vr_gather_kernel, dim3(fec::grid_rows((r->P * fec::kGatherLanes + 63) / 64)), dim3(256), 0, s, a);
         FEC_HIP(hipGetLastError());
         if (r->type == 2 && h_flag)  // the reporting objects' flags, gathered by the kernel in seq order
             FEC_HIP(hipMemcpyAsync(r->h_pin + 2 * r->P, r->d_flag.p, static_cast<size_t>(r->P), hipMemcpyDeviceToHost, s));
