@@ -331,7 +331,7 @@ int launch_encode_tile(fec_codec* c, const uint8_t* d_payload, const int32_t* d_
         for (int64_t r = 0; r < P; r += chunk) {
             const int64_t h = std::min<int64_t>(history + r, g.n - 1);
             if (int st = launch_encode_tile(c, d_payload + r * g.L, d_len ? d_len + r : nullptr, h,
-                                            std::min(chunk, P - r), d_cw + r * g.CW, d_cwlen + r, s))
+                                            std::min(chunk, P - r), d_cw + r * g.CW, d_cwlen ? d_cwlen + r : nullptr, s))
                 return st;
         }
         return FEC_OK;
@@ -923,6 +923,18 @@ int hip_failed(hipError_t e, const char* site) {
 // ------------------------------------------------------------------------------------------
 // C ABI
 // ------------------------------------------------------------------------------------------
+// The batch encode without the trimmed wire sizes where the kernel can skip them (the runtime-L
+// tile kernels and the generic one: fec_relay_vr's batches, whose zero-length gap rows made that
+// scan most of their encode); the L-specialised kernels write them to d_cwlen_fallback.
+namespace fec {
+int encode_batch_nolen(fec_codec* c, const uint8_t* d_payload, const int32_t* d_len, int64_t history, int64_t P,
+                       uint8_t* d_cw, int32_t* d_cwlen_fallback, hipStream_t s) {
+    if (!c || P < 0 || (P > 0 && (!d_payload || !d_cw || !d_cwlen_fallback))) return FEC_ERR_ARG;
+    const bool skip = !c->tile_kernel || c->tile_kernel == fec_encode_tile_kernel_for(c->g.k, c->g.n - c->g.k, 0);
+    return launch_encode(c, d_payload, d_len, history, P, d_cw, skip ? nullptr : d_cwlen_fallback, s);
+}
+}  // namespace fec
+
 extern "C" {
 
 int fec_last_error(char* buf, size_t size) {

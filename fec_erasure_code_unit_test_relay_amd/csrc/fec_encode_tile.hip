@@ -605,7 +605,9 @@ __device__ __forceinline__ void tile_walk(const EncTileArgs& a, uint8_t* smem) {
                     __builtin_amdgcn_raw_buffer_store_b128(vv, rc, so, 0, 0);
                 ++vm_issued;
             }
-            // trimmed wire size of packet tid (FEC_Encoder.cpp:55-60): 1 + last non-zero byte
+            // trimmed wire size of packet tid (FEC_Encoder.cpp:55-60): 1 + last non-zero byte; a
+            // runtime-L kernel's caller may not want them (cw_len null: the adaptive relay's batches)
+            if (LC == 0 && a.cw_len == nullptr) continue;
             const bool own = tid < R && row0 + tid < P;
             const uint8_t* cwp = out + (own ? tid : 0) * CW;
             const bool zlast = cwp[CW - 1] == 0;

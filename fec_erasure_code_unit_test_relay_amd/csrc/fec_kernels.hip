@@ -137,6 +137,7 @@ __global__ __launch_bounds__(256) void fec_encode_kernel(EncArgs a) {
         for (int o = tid; o < bytes; o += 256) dst[o] = xout[o];
     }
     for (int tl = tid; tl < ntile; tl += 256) {
+        if (!a.cw_len) break;  // (the caller does not want them: fec::encode_batch_nolen)
         const uint8_t* row = xout + tl * a.CW;
         a.cw_len[t0 + tl] = row[a.CW - 1] ? a.CW : last_nonzero_end(row, a.CW - 1);
     }

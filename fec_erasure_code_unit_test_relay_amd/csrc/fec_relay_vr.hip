@@ -34,6 +34,8 @@
 #include "fec_status.h"
 
 namespace fec {
+int encode_batch_nolen(fec_codec* c, const uint8_t* d_payload, const int32_t* d_len, int64_t history, int64_t P,
+                       uint8_t* d_cw, int32_t* d_cwlen_fallback, hipStream_t s);  // fec_codec.hip
 namespace {
 
 constexpr int kTT = 10;         // T_TOT (FEC_Macro.h)
@@ -549,8 +551,9 @@ int fec_relay_vr_run(fec_relay_vr* r, const uint8_t* d_payload, const uint8_t* h
                                t2 ? c.d_er1.as<uint8_t>() : nullptr, t2 ? c.d_er2.as<uint8_t>() : nullptr);
             FEC_HIP(hipGetLastError());
             // each instance a fresh source encoder: its rows behind kGap zero-length packets (>= n-1)
-            if (int st = fec_encode_batch(c.codec, c.d_pay.as<uint8_t>(), c.d_len.as<int32_t>(), 0, R, c.d_cw.as<uint8_t>(),
-                                          c.d_cwlen.as<int32_t>(), s))
+            // (without the trimmed wire sizes: nothing here reads them)
+            if (int st = fec::encode_batch_nolen(c.codec, c.d_pay.as<uint8_t>(), c.d_len.as<int32_t>(), 0, R,
+                                                 c.d_cw.as<uint8_t>(), c.d_cwlen.as<int32_t>(), s))
                 return st;
             const int ninst = static_cast<int>(c.starts.size());
             const dim3 zgrid(static_cast<unsigned>(std::max(1, ninst)));
